@@ -1,0 +1,749 @@
+// capi.hip — implementation of the C ABI declared in include/pq_gpu.h.
+//
+// Host side of the boundary: the page walk runs on the CPU (pqfmt), page
+// bytes are uploaded to HBM once per chunk, and the decode is a short,
+// allocation-free sequence of launches on the context's stream.  No C++
+// exception crosses an extern "C" function.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "host/format.hpp"
+#include "kernels/kernels.hpp"
+#include "pq_gpu.h"
+#include "regex/regex.hpp"
+
+using pqk::DevDict;
+using pqk::DevErr;
+using pqk::DevPage;
+using pqk::DevTile;
+
+struct PendingTimer {
+    std::string name;
+    hipEvent_t a, b;
+};
+
+struct pq_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool timing = false;
+    std::vector<PendingTimer> pending;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
+    std::map<std::string, std::pair<double, int64_t>> timers;
+};
+
+struct pq_chunk {
+    int32_t type = 0;
+    int16_t max_def = 0, max_rep = 0;
+    int32_t width = 0, plain_width = 0;
+    int64_t nrows = 0;
+    int64_t payload_bytes = 0;
+    std::vector<pq_page_desc> walked;   // every walked page, all chunks, global rows
+    std::vector<int64_t> page_seq;      // walk sequence of each device data page
+    std::vector<int64_t> dict_seq;      // walk sequence of each device dict page
+    std::vector<int64_t> data_walk_idx; // index into `walked` of each device data page
+    int walk_error = 0;
+    std::string walk_message;
+    int64_t walk_error_seq = 0;
+    int first_error = 0;                // error detected at upload time
+    // device
+    uint8_t* d_bytes = nullptr;
+    size_t nbytes = 0;
+    DevPage* d_pages = nullptr;
+    int npages = 0;
+    DevDict* d_dicts = nullptr;
+    int ndicts = 0;
+    DevTile* d_tiles = nullptr;
+    int ntiles = 0;
+    int32_t* d_page_tile0 = nullptr;
+    uint64_t* d_entries = nullptr;
+    int64_t nentries = 0;
+    int32_t* d_dict_count = nullptr;
+    DevErr* d_page_err = nullptr;
+    DevErr* d_dict_err = nullptr;
+    int32_t* d_flags = nullptr;  // [0] err_any, [1] overflow
+    uint64_t* d_row_codes = nullptr;
+    int64_t* d_tile_chars = nullptr;
+    int64_t* d_tile_base = nullptr;
+    int64_t* d_total = nullptr;
+    int64_t* d_scan_scratch = nullptr;
+    int64_t char_estimate = 0;
+    // regex
+    uint8_t* d_page_flags = nullptr;
+    uint8_t* d_dict_match = nullptr;
+    int64_t dict_match_cap = 0;
+    pqre::DeviceProgram* d_prog = nullptr;
+};
+
+namespace {
+
+template <class T>
+int dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)) == hipSuccess ? 0 : PQ_ERR_HIP;
+}
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+int set_err(pq_ctx* ctx, int code, const std::string& m) {
+    if (ctx) ctx->err = m;
+    return code;
+}
+
+int hip_check(pq_ctx* ctx, hipError_t e, const char* what) {
+    if (e == hipSuccess) return 0;
+    return set_err(ctx, PQ_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int plain_width_of(int32_t type) {
+    switch (type) {
+        case PQ_BOOLEAN: return 1;
+        case PQ_INT32: case PQ_FLOAT: return 4;
+        case PQ_INT64: case PQ_DOUBLE: return 8;
+        case PQ_INT96: return 12;
+        default: return 0;
+    }
+}
+
+// Launch bracket for per-kernel HIP-event timing on the context stream.
+struct Timed {
+    pq_ctx* ctx;
+    PendingTimer t{};
+    bool on;
+    Timed(pq_ctx* c, const char* name) : ctx(c), on(c->timing) {
+        if (!on) return;
+        t.name = name;
+        if (!ctx->free_events.empty()) {
+            t.a = ctx->free_events.back().first;
+            t.b = ctx->free_events.back().second;
+            ctx->free_events.pop_back();
+        } else {
+            (void)hipEventCreate(&t.a);
+            (void)hipEventCreate(&t.b);
+        }
+        (void)hipEventRecord(t.a, ctx->stream);
+    }
+    ~Timed() {
+        if (!on) return;
+        (void)hipEventRecord(t.b, ctx->stream);
+        ctx->pending.push_back(t);
+    }
+};
+
+void resolve_timers(pq_ctx* ctx) {
+    if (ctx->pending.empty()) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& p : ctx->pending) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, p.a, p.b);
+        auto& e = ctx->timers[p.name];
+        e.first += ms;
+        e.second += 1;
+        ctx->free_events.push_back({p.a, p.b});
+    }
+    ctx->pending.clear();
+}
+
+std::string format_error(const DevErr& e) {
+    switch (e.code) {
+        case PQ_ERR_BUFFER:
+            return "ByteBuffer: read beyond end (pos=" + std::to_string(static_cast<uint32_t>(e.pos)) +
+                   " need=" + std::to_string(static_cast<uint32_t>(e.need)) +
+                   " size=" + std::to_string(static_cast<uint32_t>(e.size)) + ")";
+        case PQ_ERR_FLBA: return "FIXED_LEN_BYTE_ARRAY not supported without type_length";
+        case PQ_ERR_UNSUPPORTED: return "page encoding outside the supported parity scope";
+        default: return "decode error " + std::to_string(e.code);
+    }
+}
+
+void free_chunk_device(pq_chunk* c) {
+    dfree(c->d_bytes);
+    dfree(c->d_pages);
+    dfree(c->d_dicts);
+    dfree(c->d_tiles);
+    dfree(c->d_page_tile0);
+    dfree(c->d_entries);
+    dfree(c->d_dict_count);
+    dfree(c->d_page_err);
+    dfree(c->d_dict_err);
+    dfree(c->d_flags);
+    dfree(c->d_row_codes);
+    dfree(c->d_tile_chars);
+    dfree(c->d_tile_base);
+    dfree(c->d_total);
+    dfree(c->d_scan_scratch);
+    dfree(c->d_page_flags);
+    dfree(c->d_dict_match);
+    if (c->d_prog) { pqre::free_device_program(c->d_prog); c->d_prog = nullptr; }
+}
+
+}  // namespace
+
+extern "C" {
+
+pq_ctx* pq_ctx_create(int device) {
+    try {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return nullptr;
+        if (hipSetDevice(device) != hipSuccess) return nullptr;
+        auto* c = new pq_ctx();
+        c->device = device;
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete c;
+            return nullptr;
+        }
+        return c;
+    } catch (...) {
+        return nullptr;
+    }
+}
+
+void pq_ctx_destroy(pq_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& p : ctx->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto& p : ctx->free_events) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* pq_last_error(const pq_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+void* pq_ctx_stream(pq_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+int pq_ctx_sync(pq_ctx* ctx) {
+    if (!ctx) return PQ_ERR_ARG;
+    return hip_check(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+}
+
+int pq_build_page_table(const uint8_t* file, size_t file_len, const pq_chunk_desc* chunk,
+                        pq_page_desc* pages, int64_t cap, int64_t* npages, char* err,
+                        size_t errlen) {
+    if (!file || !chunk || !npages) return PQ_ERR_ARG;
+    try {
+        pqfmt::WalkResult w = pqfmt::walk_chunk(file, file_len, *chunk);
+        *npages = static_cast<int64_t>(w.pages.size());
+        for (int64_t i = 0; i < cap && i < *npages; i++) pages[i] = w.pages[i];
+        if (err && errlen) {
+            std::strncpy(err, w.message.c_str(), errlen - 1);
+            err[errlen - 1] = 0;
+        }
+        return w.error;
+    } catch (...) {
+        return PQ_ERR_ALLOC;
+    }
+}
+
+int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc* chunks,
+                    int nchunks, pq_chunk** out) {
+    if (!ctx || !file || !chunks || nchunks <= 0 || !out) return PQ_ERR_ARG;
+    *out = nullptr;
+    try {
+        (void)hipSetDevice(ctx->device);
+        auto c = std::make_unique<pq_chunk>();
+        c->type = chunks[0].type;
+        c->max_def = chunks[0].max_def_level;
+        c->max_rep = chunks[0].max_rep_level;
+        c->plain_width = plain_width_of(c->type);
+        c->width = c->plain_width;
+
+        // 1) host walks; lay out every chunk's payload span in one image
+        struct Span { int64_t file_lo, file_hi, img; };
+        std::vector<Span> spans;
+        std::vector<DevPage> hpages;
+        std::vector<DevDict> hdicts;
+        std::vector<int64_t> dict_walk_to_dev;
+        int64_t seq = 0, row_base = 0, img = 0;
+        for (int k = 0; k < nchunks; k++) {
+            pqfmt::WalkResult w = pqfmt::walk_chunk(file, file_len, chunks[k]);
+            int64_t lo = INT64_MAX, hi = 0;
+            for (const auto& p : w.pages) {
+                if (p.page_type != PQ_DATA_PAGE && p.page_type != PQ_DICTIONARY_PAGE) continue;
+                lo = std::min(lo, p.payload_offset);
+                hi = std::max(hi, p.payload_offset + static_cast<int64_t>(p.payload_size));
+            }
+            if (lo == INT64_MAX) { lo = 0; hi = 0; }
+            Span sp{lo, hi, img};
+            spans.push_back(sp);
+            int64_t base_walk = static_cast<int64_t>(c->walked.size());
+            std::vector<int32_t> dict_of_walk(w.pages.size(), -1);
+            for (size_t i = 0; i < w.pages.size(); i++) {
+                pq_page_desc p = w.pages[i];
+                int64_t s = seq + static_cast<int64_t>(i);
+                if (p.page_type == PQ_DICTIONARY_PAGE) {
+                    DevDict d{};
+                    d.off = static_cast<uint64_t>(img + (p.payload_offset - lo));
+                    d.size = p.payload_size;
+                    d.nvals = p.num_values;
+                    d.entry_base = static_cast<int32_t>(c->nentries);
+                    int64_t cap = c->type == PQ_BYTE_ARRAY
+                                      ? std::min<int64_t>(p.num_values, p.payload_size / 4 + 1)
+                                      : 0;
+                    c->nentries += std::max<int64_t>(cap, 0);
+                    dict_of_walk[i] = static_cast<int32_t>(hdicts.size());
+                    hdicts.push_back(d);
+                    c->dict_seq.push_back(s);
+                    c->payload_bytes += p.payload_size;
+                } else if (p.page_type == PQ_DATA_PAGE) {
+                    DevPage d{};
+                    d.off = static_cast<uint64_t>(img + (p.payload_offset - lo));
+                    d.size = p.payload_size;
+                    d.nvals = p.num_values;
+                    d.first_row = row_base + p.first_row;
+                    int dict_dev = p.dict_page >= 0 ? dict_of_walk[p.dict_page] : -1;
+                    bool enc_dict = p.encoding == 2 || p.encoding == 8;
+                    d.mode = (enc_dict && dict_dev >= 0) ? pqk::MODE_DICT
+                             : (c->type == PQ_BOOLEAN ? pqk::MODE_BOOL : pqk::MODE_PLAIN);
+                    d.dict = d.mode == pqk::MODE_DICT ? dict_dev : -1;
+                    hpages.push_back(d);
+                    c->page_seq.push_back(s);
+                    c->data_walk_idx.push_back(base_walk + static_cast<int64_t>(i));
+                    c->payload_bytes += p.payload_size;
+                }
+                p.first_row += row_base;
+                c->walked.push_back(p);
+            }
+            int64_t rows = 0;
+            for (const auto& p : w.pages)
+                if (p.page_type == PQ_DATA_PAGE) rows += p.num_values;
+            row_base += rows;
+            img += (hi - lo + 15) / 16 * 16;
+            seq += static_cast<int64_t>(w.pages.size());
+            if (w.error) {  // later chunks are never reached by the reference
+                c->walk_error = w.error;
+                c->walk_message = w.message;
+                c->walk_error_seq = seq;
+                break;
+            }
+        }
+        c->nrows = row_base;
+        c->nbytes = static_cast<size_t>(img) + 64;
+        c->npages = static_cast<int>(hpages.size());
+        c->ndicts = static_cast<int>(hdicts.size());
+
+        // tiles
+        std::vector<DevTile> htiles;
+        std::vector<int32_t> tile0(hpages.size());
+        for (size_t p = 0; p < hpages.size(); p++) {
+            tile0[p] = static_cast<int32_t>(htiles.size());
+            for (int32_t r = 0; r < hpages[p].nvals; r += pqk::kTileRows)
+                htiles.push_back(DevTile{static_cast<int32_t>(p), r,
+                                         std::min(pqk::kTileRows, hpages[p].nvals - r), 0});
+        }
+        c->ntiles = static_cast<int>(htiles.size());
+
+        // 2) device allocations + one upload
+        int rc = 0;
+        rc |= dalloc(&c->d_bytes, c->nbytes);
+        rc |= dalloc(&c->d_pages, hpages.size());
+        rc |= dalloc(&c->d_dicts, hdicts.size());
+        rc |= dalloc(&c->d_tiles, htiles.size());
+        rc |= dalloc(&c->d_page_tile0, tile0.size());
+        rc |= dalloc(&c->d_entries, static_cast<size_t>(c->nentries));
+        rc |= dalloc(&c->d_dict_count, hdicts.size());
+        rc |= dalloc(&c->d_page_err, hpages.size());
+        rc |= dalloc(&c->d_dict_err, hdicts.size());
+        rc |= dalloc(&c->d_flags, 4);
+        rc |= dalloc(&c->d_tile_chars, htiles.size());
+        rc |= dalloc(&c->d_tile_base, htiles.size());
+        rc |= dalloc(&c->d_total, 1);
+        rc |= dalloc(&c->d_scan_scratch, htiles.size() / 8192 + 16);
+        if (c->type == PQ_BYTE_ARRAY) rc |= dalloc(&c->d_row_codes, static_cast<size_t>(c->nrows));
+        if (rc) {
+            free_chunk_device(c.get());
+            return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (chunk upload)");
+        }
+        std::vector<uint8_t> image(c->nbytes, 0);
+        for (const auto& sp : spans) {
+            if (sp.file_hi <= sp.file_lo) continue;
+            int64_t lo = sp.file_lo, hi = std::min<int64_t>(sp.file_hi, static_cast<int64_t>(file_len));
+            if (hi > lo) std::memcpy(image.data() + sp.img, file + lo, static_cast<size_t>(hi - lo));
+        }
+        hipStream_t s = ctx->stream;
+        rc = hip_check(ctx, hipMemcpyAsync(c->d_bytes, image.data(), c->nbytes, hipMemcpyHostToDevice, s), "upload");
+        if (!rc && !hpages.empty())
+            rc = hip_check(ctx, hipMemcpyAsync(c->d_pages, hpages.data(), hpages.size() * sizeof(DevPage), hipMemcpyHostToDevice, s), "upload");
+        if (!rc && !hdicts.empty())
+            rc = hip_check(ctx, hipMemcpyAsync(c->d_dicts, hdicts.data(), hdicts.size() * sizeof(DevDict), hipMemcpyHostToDevice, s), "upload");
+        if (!rc && !htiles.empty())
+            rc = hip_check(ctx, hipMemcpyAsync(c->d_tiles, htiles.data(), htiles.size() * sizeof(DevTile), hipMemcpyHostToDevice, s), "upload");
+        if (!rc && !tile0.empty())
+            rc = hip_check(ctx, hipMemcpyAsync(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
+        if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
+        if (rc) {
+            free_chunk_device(c.get());
+            return rc;
+        }
+        // output size estimate for BYTE_ARRAY chars: plain pages are bounded
+        // by their payload; dictionary pages by rows x mean entry length.
+        int64_t est = 0;
+        for (const auto& p : hpages) {
+            if (p.mode == pqk::MODE_DICT) {
+                const DevDict& d = hdicts[p.dict];
+                int64_t mean = d.nvals > 0 ? (d.size / d.nvals) + 1 : 1;
+                est += static_cast<int64_t>(p.nvals) * mean;
+            } else {
+                est += p.size;
+            }
+        }
+        c->char_estimate = est + est / 8 + 64;
+        *out = c.release();
+        return 0;
+    } catch (const pqfmt::Error& e) {
+        return set_err(ctx, e.code, e.what());
+    } catch (const std::exception& e) {
+        return set_err(ctx, PQ_ERR_ALLOC, e.what());
+    }
+}
+
+void pq_chunk_free(pq_ctx* ctx, pq_chunk* c) {
+    if (!c) return;
+    if (ctx) (void)hipStreamSynchronize(ctx->stream);
+    free_chunk_device(c);
+    delete c;
+}
+
+int64_t pq_chunk_num_rows(const pq_chunk* c) { return c ? c->nrows : 0; }
+int64_t pq_chunk_num_pages(const pq_chunk* c) { return c ? c->npages : 0; }
+int64_t pq_chunk_payload_bytes(const pq_chunk* c) { return c ? c->payload_bytes : 0; }
+int pq_chunk_pages(const pq_chunk* c, pq_page_desc* pages, int64_t cap, int64_t* npages) {
+    if (!c || !npages) return PQ_ERR_ARG;
+    *npages = static_cast<int64_t>(c->walked.size());
+    for (int64_t i = 0; i < cap && i < *npages; i++) pages[i] = c->walked[i];
+    return 0;
+}
+
+static int ensure_output(pq_ctx* ctx, pq_chunk* c, pq_column* out, int64_t char_cap) {
+    int64_t rows_needed = c->nrows;
+    int64_t bytes_needed = c->type == PQ_BYTE_ARRAY ? char_cap : c->nrows * c->width;
+    if (out->capacity_rows < rows_needed + 1 || out->d_validity == nullptr) {
+        dfree(out->d_validity);
+        dfree(out->d_offsets);
+        int64_t cap = rows_needed + 1;
+        if (dalloc(&out->d_validity, static_cast<size_t>(cap / 32 + 4)))
+            return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (validity)");
+        if (c->type == PQ_BYTE_ARRAY && dalloc(&out->d_offsets, static_cast<size_t>(cap)))
+            return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (offsets)");
+        out->capacity_rows = cap;
+    }
+    if (c->type == PQ_BYTE_ARRAY && out->d_offsets == nullptr) {
+        if (dalloc(&out->d_offsets, static_cast<size_t>(out->capacity_rows)))
+            return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (offsets)");
+    }
+    if (out->capacity_bytes < bytes_needed || out->d_values == nullptr) {
+        dfree(out->d_values);
+        if (dalloc(&out->d_values, static_cast<size_t>(bytes_needed + 64)))
+            return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (values)");
+        out->capacity_bytes = bytes_needed;
+    }
+    out->num_rows = c->nrows;
+    out->type = c->type;
+    out->value_width = c->type == PQ_BYTE_ARRAY ? 0 : c->width;
+    return 0;
+}
+
+static void launch_gather(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
+    Timed t(ctx, "ba_gather");
+    pqk::launch_ba_gather(ctx->stream, c->d_bytes, c->d_pages, c->d_tiles, c->ntiles, c->d_dicts,
+                          c->d_entries, c->d_row_codes, c->d_tile_base, c->nrows, c->d_total,
+                          out->capacity_bytes, c->d_flags + 1, out->d_validity, out->d_offsets,
+                          out->d_values);
+}
+
+int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
+    if (!ctx || !c || !out) return PQ_ERR_ARG;
+    if (c->type == PQ_BYTE_ARRAY) {
+        int64_t cap = std::max<int64_t>(out->capacity_bytes, c->char_estimate);
+        if (int rc = ensure_output(ctx, c, out, cap)) return rc;
+    } else {
+        if (int rc = ensure_output(ctx, c, out, 0)) return rc;
+    }
+    hipStream_t s = ctx->stream;
+    pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
+    (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), s);
+    (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
+    if (c->ndicts) {
+        Timed t(ctx, "dict_entries");
+        pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
+                                 c->d_dict_err, c->d_flags, c->type, c->plain_width);
+    }
+    if (c->type == PQ_BYTE_ARRAY) {
+        {
+            Timed t(ctx, "ba_rows");
+            pqk::launch_ba_rows(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_entries,
+                                c->d_dict_count, cp, c->d_row_codes, c->d_tile_chars,
+                                c->d_page_tile0, c->d_page_err, c->d_flags);
+        }
+        {
+            Timed t(ctx, "scan");
+            pqk::launch_scan_i64(s, c->d_tile_chars, c->d_tile_base, c->ntiles, c->d_total,
+                                 c->d_scan_scratch);
+        }
+        if (c->ntiles == 0) {
+            (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
+        }
+        launch_gather(ctx, c, out);
+    } else {
+        Timed t(ctx, "fixed");
+        pqk::launch_fixed(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_dict_count, cp,
+                          out->d_validity, out->d_values, c->d_page_err, c->d_flags);
+    }
+    hipError_t e = hipGetLastError();
+    return hip_check(ctx, e, "kernel launch");
+}
+
+// Synchronise and turn device error records into the reference's first error.
+static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
+    int32_t flags[4] = {0, 0, 0, 0};
+    if (int rc = hip_check(ctx, hipMemcpyAsync(flags, c->d_flags, sizeof flags, hipMemcpyDeviceToHost, ctx->stream), "flags"))
+        return rc;
+    if (int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync")) return rc;
+    int64_t best_seq = c->walk_error ? c->walk_error_seq : INT64_MAX;
+    int best_code = c->walk_error;
+    std::string best_msg = c->walk_message;
+    if (flags[0]) {
+        std::vector<DevErr> pe(c->npages), de(c->ndicts);
+        if (c->npages) (void)hipMemcpy(pe.data(), c->d_page_err, pe.size() * sizeof(DevErr), hipMemcpyDeviceToHost);
+        if (c->ndicts) (void)hipMemcpy(de.data(), c->d_dict_err, de.size() * sizeof(DevErr), hipMemcpyDeviceToHost);
+        for (int i = 0; i < c->npages; i++)
+            if (pe[i].code && c->page_seq[i] < best_seq) {
+                best_seq = c->page_seq[i];
+                best_code = pe[i].code;
+                best_msg = format_error(pe[i]);
+            }
+        for (int i = 0; i < c->ndicts; i++)
+            if (de[i].code && c->dict_seq[i] < best_seq) {
+                best_seq = c->dict_seq[i];
+                best_code = de[i].code;
+                best_msg = format_error(de[i]);
+            }
+        // clear records for the next call
+        if (c->npages) (void)hipMemsetAsync(c->d_page_err, 0, c->npages * sizeof(DevErr), ctx->stream);
+        if (c->ndicts) (void)hipMemsetAsync(c->d_dict_err, 0, c->ndicts * sizeof(DevErr), ctx->stream);
+    }
+    if (best_code) return set_err(ctx, best_code, best_msg);
+    if (c->type == PQ_BYTE_ARRAY && out) {
+        int64_t total = 0;
+        (void)hipMemcpy(&total, c->d_total, sizeof total, hipMemcpyDeviceToHost);
+        out->num_bytes = total;
+        if (flags[1]) {  // chars overflowed the estimate: grow and gather again
+            dfree(out->d_values);
+            if (dalloc(&out->d_values, static_cast<size_t>(total + 64)))
+                return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (chars)");
+            out->capacity_bytes = total;
+            (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), ctx->stream);
+            (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, ctx->stream);
+            launch_gather(ctx, c, out);
+            return hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync");
+        }
+    } else if (out) {
+        out->num_bytes = c->nrows * c->width;
+    }
+    return 0;
+}
+
+int pq_decode_check(pq_ctx* ctx, pq_chunk* c) { return (!ctx || !c) ? PQ_ERR_ARG : collect(ctx, c, nullptr); }
+
+int pq_decode(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
+    if (int rc = pq_decode_async(ctx, c, out)) return rc;
+    return collect(ctx, c, out);
+}
+
+int pq_column_copy_out(pq_ctx* ctx, const pq_column* col, uint32_t* validity, uint8_t* values,
+                       int64_t* offsets) {
+    if (!ctx || !col) return PQ_ERR_ARG;
+    hipStream_t s = ctx->stream;
+    int rc = 0;
+    if (validity && col->num_rows)
+        rc |= hip_check(ctx, hipMemcpyAsync(validity, col->d_validity, static_cast<size_t>((col->num_rows + 31) / 32) * 4, hipMemcpyDeviceToHost, s), "copy validity");
+    if (values && col->num_bytes)
+        rc |= hip_check(ctx, hipMemcpyAsync(values, col->d_values, static_cast<size_t>(col->num_bytes), hipMemcpyDeviceToHost, s), "copy values");
+    if (offsets && col->d_offsets)
+        rc |= hip_check(ctx, hipMemcpyAsync(offsets, col->d_offsets, static_cast<size_t>(col->num_rows + 1) * 8, hipMemcpyDeviceToHost, s), "copy offsets");
+    rc |= hip_check(ctx, hipStreamSynchronize(s), "copy sync");
+    return rc ? PQ_ERR_HIP : 0;
+}
+
+void pq_column_free(pq_ctx* ctx, pq_column* col) {
+    if (!col) return;
+    if (ctx) (void)hipStreamSynchronize(ctx->stream);
+    dfree(col->d_validity);
+    dfree(col->d_values);
+    dfree(col->d_offsets);
+    std::memset(col, 0, sizeof *col);
+}
+
+void pq_timing_enable(pq_ctx* ctx, int enable) { if (ctx) ctx->timing = enable != 0; }
+void pq_timing_reset(pq_ctx* ctx) {
+    if (!ctx) return;
+    resolve_timers(ctx);
+    ctx->timers.clear();
+}
+int pq_timing_get(pq_ctx* ctx, const char* name, double* total_ms, int64_t* launches) {
+    if (!ctx || !name) return 0;
+    resolve_timers(ctx);
+    auto it = ctx->timers.find(name);
+    if (it == ctx->timers.end()) return 0;
+    if (total_ms) *total_ms = it->second.first;
+    if (launches) *launches = it->second.second;
+    return 1;
+}
+
+// ── regex page filter ───────────────────────────────────────────────────────
+int pq_regex_compile_check(const char* pattern, char* err, size_t errlen) {
+    std::string msg;
+    int rc = pqre::check(pattern ? pattern : "", &msg);
+    if (err && errlen) {
+        std::strncpy(err, msg.c_str(), errlen - 1);
+        err[errlen - 1] = 0;
+    }
+    return rc;
+}
+
+int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg) {
+    if (!ctx || !c || !pattern) return PQ_ERR_ARG;
+    if (c->type != PQ_BYTE_ARRAY) return set_err(ctx, PQ_ERR_ARG, "regex page filter needs a BYTE_ARRAY column");
+    try {
+        std::string msg;
+        pqre::Program prog;
+        int rc = pqre::compile(pattern, &prog, &msg);
+        if (rc) return set_err(ctx, PQ_ERR_REGEX, msg);
+        if (!c->d_page_flags && dalloc(&c->d_page_flags, static_cast<size_t>(c->npages)))
+            return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (page flags)");
+        int64_t dict_cap = std::max<int64_t>(c->nentries, 1);
+        if (c->dict_match_cap < dict_cap) {
+            dfree(c->d_dict_match);
+            if (dalloc(&c->d_dict_match, static_cast<size_t>(dict_cap)))
+                return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (dict match)");
+            c->dict_match_cap = dict_cap;
+        }
+        if (c->d_prog) pqre::free_device_program(c->d_prog);
+        c->d_prog = pqre::upload_program(prog, ctx->stream);
+        if (!c->d_prog) return set_err(ctx, PQ_ERR_HIP, "regex program upload failed");
+        hipStream_t s = ctx->stream;
+        pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
+        (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), s);
+        if (c->ndicts) {
+            {
+                Timed t(ctx, "dict_entries");
+                pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
+                                         c->d_dict_count, c->d_dict_err, c->d_flags, c->type,
+                                         c->plain_width);
+            }
+            Timed t(ctx, "regex_dict");
+            pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
+                                    c->d_dict_count, c->d_dict_match);
+        }
+        {
+            Timed t(ctx, "regex_pages");
+            pqre::launch_regex_pages(s, c->d_prog, c->d_bytes, c->d_pages, c->npages, c->d_dicts,
+                                     c->d_entries, c->d_dict_count, c->d_dict_match, cp, neg,
+                                     c->d_page_flags, c->d_page_err, c->d_flags);
+        }
+        return hip_check(ctx, hipGetLastError(), "regex launch");
+    } catch (const std::exception& e) {
+        return set_err(ctx, PQ_ERR_ALLOC, e.what());
+    }
+}
+
+int pq_regex_pages_result(pq_ctx* ctx, pq_chunk* c, uint8_t* page_flags) {
+    if (!ctx || !c) return PQ_ERR_ARG;
+    if (int rc = collect(ctx, c, nullptr)) return rc;
+    if (page_flags && c->npages)
+        return hip_check(ctx, hipMemcpy(page_flags, c->d_page_flags, static_cast<size_t>(c->npages), hipMemcpyDeviceToHost), "copy page flags");
+    return 0;
+}
+
+int pq_regex_pages(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg, uint8_t* page_flags) {
+    if (int rc = pq_regex_pages_async(ctx, c, pattern, neg)) return rc;
+    return pq_regex_pages_result(ctx, c, page_flags);
+}
+
+// ── file helpers ────────────────────────────────────────────────────────────
+}  // extern "C"
+
+struct pq_file {
+    pqfmt::FileMeta meta;
+    std::vector<pqfmt::LeafColumn> cols;
+    std::vector<std::array<int64_t, 4>> pidx;
+};
+
+extern "C" {
+
+int pq_file_open(const uint8_t* file, size_t file_len, pq_file** out, char* err, size_t errlen) {
+    if (!file || !out) return PQ_ERR_ARG;
+    *out = nullptr;
+    try {
+        auto f = std::make_unique<pq_file>();
+        f->meta = pqfmt::parse_footer(file, file_len);
+        f->cols = pqfmt::leaf_columns(f->meta);
+        f->pidx = pqfmt::page_index(file, file_len, f->meta);
+        *out = f.release();
+        return 0;
+    } catch (const pqfmt::Error& e) {
+        if (err && errlen) { std::strncpy(err, e.what(), errlen - 1); err[errlen - 1] = 0; }
+        return e.code;
+    } catch (const std::exception& e) {
+        if (err && errlen) { std::strncpy(err, e.what(), errlen - 1); err[errlen - 1] = 0; }
+        return PQ_ERR_ALLOC;
+    }
+}
+void pq_file_close(pq_file* f) { delete f; }
+int64_t pq_file_num_rows(const pq_file* f) { return f ? f->meta.num_rows : 0; }
+int pq_file_num_row_groups(const pq_file* f) { return f ? static_cast<int>(f->meta.row_groups.size()) : 0; }
+int pq_file_num_columns(const pq_file* f) { return f ? static_cast<int>(f->cols.size()) : 0; }
+int pq_file_column_name(const pq_file* f, int col, char* buf, size_t buflen) {
+    if (!f || col < 0 || col >= static_cast<int>(f->cols.size()) || !buf || !buflen) return PQ_ERR_ARG;
+    std::strncpy(buf, f->cols[col].name.c_str(), buflen - 1);
+    buf[buflen - 1] = 0;
+    return 0;
+}
+int pq_file_find_column(const pq_file* f, const char* name) {  // last match wins (build_column_index)
+    if (!f || !name) return -1;
+    int found = -1;
+    for (size_t i = 0; i < f->cols.size(); i++)
+        if (f->cols[i].name == name) found = static_cast<int>(i);
+    return found;
+}
+int pq_file_chunk(const pq_file* f, int rg, int col, pq_chunk_desc* out) {
+    if (!f || !out || rg < 0 || rg >= static_cast<int>(f->meta.row_groups.size()) || col < 0 ||
+        col >= static_cast<int>(f->cols.size()))
+        return PQ_ERR_ARG;
+    const auto& lc = f->cols[col];
+    const auto& r = f->meta.row_groups[rg];
+    if (lc.column_index >= static_cast<int>(r.columns.size())) return PQ_ERR_ARG;
+    const auto& cc = r.columns[lc.column_index];
+    if (!cc.meta) return PQ_ERR_OPTIONAL;  // "ColumnChunk has no metadata"
+    std::memset(out, 0, sizeof *out);
+    out->num_values = cc.meta->num_values;
+    out->data_page_offset = cc.meta->data_page_offset;
+    out->has_dictionary_page_offset = cc.meta->dictionary_page_offset.has_value();
+    out->dictionary_page_offset = cc.meta->dictionary_page_offset.value_or(0);
+    out->codec = cc.meta->codec;
+    out->type = lc.type;
+    out->max_def_level = lc.max_def;
+    out->max_rep_level = lc.max_rep;
+    return 0;
+}
+int64_t pq_file_row_group_rows(const pq_file* f, int rg) {
+    if (!f || rg < 0 || rg >= static_cast<int>(f->meta.row_groups.size())) return 0;
+    return f->meta.row_groups[rg].num_rows;
+}
+int64_t pq_file_num_pages(const pq_file* f) { return f ? static_cast<int64_t>(f->pidx.size()) : 0; }
+int pq_file_page_index(const pq_file* f, int64_t* entries, int64_t cap) {
+    if (!f || !entries) return PQ_ERR_ARG;
+    for (int64_t i = 0; i < cap && i < static_cast<int64_t>(f->pidx.size()); i++)
+        for (int k = 0; k < 4; k++) entries[4 * i + k] = f->pidx[i][k];
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,368 @@
+// format.cpp — see format.hpp for the reference behaviour each part follows.
+#include "format.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace pqfmt {
+
+// common.hpp:136-147 semantics: 7-bit groups, "varint too long" past 63 bits.
+uint64_t Cursor::varint() {
+    uint64_t r = 0;
+    int shift = 0;
+    for (;;) {
+        uint8_t b = byte();
+        r |= static_cast<uint64_t>(b & 0x7F) << shift;
+        if ((b & 0x80) == 0) break;
+        shift += 7;
+        if (shift > 63) throw Error(PQ_ERR_THRIFT, "varint too long");
+    }
+    return r;
+}
+
+bool Thrift::field(int16_t& id, uint8_t& type) {  // thrift.cpp:6-21
+    uint8_t b = c_.byte();
+    if (b == 0) { id = 0; type = 0; return false; }
+    type = b & 0x0F;
+    int16_t delta = (b >> 4) & 0x0F;
+    id = delta ? static_cast<int16_t>(last_ + delta) : static_cast<int16_t>(c_.zigzag());
+    last_ = id;
+    return true;
+}
+
+std::string Thrift::str() {  // thrift.cpp:35-39
+    uint32_t n = static_cast<uint32_t>(c_.varint());
+    const uint8_t* p = c_.bytes(n);
+    return std::string(reinterpret_cast<const char*>(p), n);
+}
+
+void Thrift::list(uint8_t& et, int32_t& n) {  // thrift.cpp:44-55
+    uint8_t b = c_.byte();
+    et = b & 0x0F;
+    n = ((b >> 4) & 0x0F) == 0x0F ? static_cast<int32_t>(c_.varint()) : (b >> 4) & 0x0F;
+}
+
+void Thrift::skip(uint8_t type) {  // thrift.cpp:67-119
+    switch (type) {
+        case 1: case 2: return;
+        case 3: c_.byte(); return;
+        case 4: case 5: case 6: c_.varint(); return;
+        case 7: c_.bytes(8); return;
+        case 8: str(); return;
+        case 9: case 10: {
+            uint8_t et; int32_t n;
+            list(et, n);
+            for (int32_t i = 0; i < n; i++) skip(et);
+            return;
+        }
+        case 11: {
+            int32_t n = static_cast<int32_t>(c_.varint());
+            if (n > 0) {
+                uint8_t kv = c_.byte();
+                for (int32_t i = 0; i < n; i++) { skip((kv >> 4) & 0x0F); skip(kv & 0x0F); }
+            }
+            return;
+        }
+        case 12: {
+            push();
+            int16_t id; uint8_t t;
+            while (field(id, t)) skip(t);
+            pop();
+            return;
+        }
+        default:
+            throw Error(PQ_ERR_THRIFT, "ThriftReader::skip: unknown type " + std::to_string(type));
+    }
+}
+
+namespace {
+
+SchemaElement read_schema(Thrift& t) {  // metadata.cpp:5-22
+    SchemaElement s;
+    int16_t id; uint8_t ty;
+    while (t.field(id, ty)) {
+        switch (id) {
+            case 1: s.type = t.i32(); break;
+            case 2: s.type_length = t.i32(); break;
+            case 3: s.repetition = t.i32(); break;
+            case 4: s.name = t.str(); break;
+            case 5: s.num_children = t.i32(); break;
+            case 6: s.converted_type = t.i32(); break;
+            case 7: s.scale = t.i32(); break;
+            case 8: s.precision = t.i32(); break;
+            case 9: s.field_id = t.i32(); break;
+            default: t.skip(ty);
+        }
+    }
+    return s;
+}
+
+ColumnMeta read_column_meta(Thrift& t) {  // metadata.cpp:36-64
+    ColumnMeta m;
+    int16_t id; uint8_t ty;
+    while (t.field(id, ty)) {
+        switch (id) {
+            case 1: m.type = t.i32(); break;
+            case 2: { uint8_t et; int32_t n; t.list(et, n); for (int32_t i = 0; i < n; i++) m.encodings.push_back(t.i32()); break; }
+            case 3: { uint8_t et; int32_t n; t.list(et, n); for (int32_t i = 0; i < n; i++) m.path.push_back(t.str()); break; }
+            case 4: m.codec = t.i32(); break;
+            case 5: m.num_values = t.i64(); break;
+            case 6: m.total_uncompressed = t.i64(); break;
+            case 7: m.total_compressed = t.i64(); break;
+            case 9: m.data_page_offset = t.i64(); break;
+            case 10: m.index_page_offset = t.i64(); break;
+            case 11: m.dictionary_page_offset = t.i64(); break;
+            default: t.skip(ty);
+        }
+    }
+    return m;
+}
+
+ColumnChunkMeta read_chunk(Thrift& t) {  // metadata.cpp:68-86
+    ColumnChunkMeta c;
+    int16_t id; uint8_t ty;
+    while (t.field(id, ty)) {
+        switch (id) {
+            case 1: c.file_path = t.str(); break;
+            case 2: c.file_offset = t.i64(); break;
+            case 3: t.push(); c.meta = read_column_meta(t); t.pop(); break;
+            default: t.skip(ty);
+        }
+    }
+    return c;
+}
+
+RowGroupMeta read_row_group(Thrift& t) {  // metadata.cpp:159-180
+    RowGroupMeta r;
+    int16_t id; uint8_t ty;
+    while (t.field(id, ty)) {
+        switch (id) {
+            case 1: {
+                uint8_t et; int32_t n;
+                t.list(et, n);
+                for (int32_t i = 0; i < n; i++) { t.push(); r.columns.push_back(read_chunk(t)); t.pop(); }
+                break;
+            }
+            case 2: r.total_byte_size = t.i64(); break;
+            case 3: r.num_rows = t.i64(); break;
+            default: t.skip(ty);
+        }
+    }
+    return r;
+}
+
+void skip_key_value(Thrift& t) {  // metadata.cpp:184-194
+    int16_t id; uint8_t ty;
+    while (t.field(id, ty)) {
+        if (id == 1 || id == 2) t.str();
+        else t.skip(ty);
+    }
+}
+
+int skip_subtree(const FileMeta& fm, int idx) {  // parquet_reader.cpp:545-557
+    int children = fm.schema[idx].num_children.value_or(0);
+    idx++;
+    for (int i = 0; i < children; i++) {
+        if (fm.schema[idx].num_children.value_or(0) > 0) idx = skip_subtree(fm, idx);
+        else idx++;
+    }
+    return idx;
+}
+
+void build_leaves(const FileMeta& fm, int idx, int end, int16_t def, int16_t rep, int& col,
+                  std::vector<LeafColumn>& out) {  // parquet_reader.cpp:495-543
+    while (idx < end) {
+        const SchemaElement& e = fm.schema[idx];
+        int16_t d = def, r = rep;
+        if (e.repetition) {
+            if (*e.repetition == 1) d++;
+            else if (*e.repetition == 2) { d++; r++; }
+        }
+        if (e.num_children.value_or(0) > 0) {
+            int children = *e.num_children;
+            idx++;
+            int i = idx, remaining = children;
+            while (remaining > 0 && i < end) {
+                remaining--;
+                if (fm.schema[i].num_children.value_or(0) > 0) i = skip_subtree(fm, i);
+                else i++;
+            }
+            build_leaves(fm, idx, i, d, r, col, out);
+            idx = i;
+        } else {
+            LeafColumn lc;
+            lc.name = e.name;
+            lc.type = e.type.value_or(PQ_BYTE_ARRAY);
+            lc.column_index = col++;
+            lc.max_def = d;
+            lc.max_rep = r;
+            lc.repetition = e.repetition;
+            lc.converted_type = e.converted_type;
+            out.push_back(lc);
+            idx++;
+        }
+    }
+}
+
+}  // namespace
+
+FileMeta parse_footer(const uint8_t* file, size_t len) {  // parquet_reader.cpp:14-61
+    if (len < 12) throw Error(PQ_ERR_ARG, "file too small to be a Parquet file");
+    if (std::memcmp(file, "PAR1", 4) != 0) throw Error(PQ_ERR_ARG, "missing PAR1 magic at start");
+    if (std::memcmp(file + len - 4, "PAR1", 4) != 0) throw Error(PQ_ERR_ARG, "missing PAR1 magic at end");
+    uint32_t flen;
+    std::memcpy(&flen, file + len - 8, 4);
+    if (static_cast<uint64_t>(flen) + 8 > len) throw Error(PQ_ERR_ARG, "invalid footer length");
+    Thrift t(file + len - 8 - flen, flen);
+    FileMeta fm;
+    int16_t id; uint8_t ty;
+    while (t.field(id, ty)) {  // metadata.cpp:198-242
+        switch (id) {
+            case 1: fm.version = t.i32(); break;
+            case 2: { uint8_t et; int32_t n; t.list(et, n); for (int32_t i = 0; i < n; i++) { t.push(); fm.schema.push_back(read_schema(t)); t.pop(); } break; }
+            case 3: fm.num_rows = t.i64(); break;
+            case 4: { uint8_t et; int32_t n; t.list(et, n); for (int32_t i = 0; i < n; i++) { t.push(); fm.row_groups.push_back(read_row_group(t)); t.pop(); } break; }
+            case 5: { uint8_t et; int32_t n; t.list(et, n); for (int32_t i = 0; i < n; i++) { t.push(); skip_key_value(t); t.pop(); } break; }
+            case 6: fm.created_by = t.str(); break;
+            default: t.skip(ty);
+        }
+    }
+    return fm;
+}
+
+std::vector<LeafColumn> leaf_columns(const FileMeta& fm) {
+    std::vector<LeafColumn> out;
+    if (fm.schema.empty()) return out;
+    int col = 0;
+    build_leaves(fm, 1, static_cast<int>(fm.schema.size()), 0, 0, col, out);
+    return out;
+}
+
+PageHeader read_page_header(const uint8_t* file, size_t len, size_t off) {  // metadata.cpp:121-155
+    uint8_t win[256] = {0};  // column_reader.cpp:34-38: fixed window, zeros past EOF
+    if (off < len) std::memcpy(win, file + off, std::min<size_t>(256, len - off));
+    Thrift t(win, sizeof win);
+    PageHeader h;
+    int16_t id; uint8_t ty;
+    while (t.field(id, ty)) {
+        switch (id) {
+            case 1: h.type = t.i32(); break;
+            case 2: h.uncompressed = t.i32(); break;
+            case 3: h.compressed = t.i32(); break;
+            case 4: t.i32(); break;
+            case 5: {  // DataPageHeader, metadata.cpp:90-102
+                t.push();
+                h.has_data = true;
+                h.data_num_values = 0;
+                h.data_encoding = 0;
+                int16_t i2; uint8_t t2;
+                while (t.field(i2, t2)) {
+                    if (i2 == 1) h.data_num_values = t.i32();
+                    else if (i2 == 2) h.data_encoding = t.i32();
+                    else if (i2 == 3 || i2 == 4) t.i32();
+                    else t.skip(t2);
+                }
+                t.pop();
+                break;
+            }
+            case 7: {  // DictionaryPageHeader, metadata.cpp:106-117
+                t.push();
+                h.has_dict = true;
+                h.dict_num_values = 0;
+                int16_t i2; uint8_t t2;
+                while (t.field(i2, t2)) {
+                    if (i2 == 1) h.dict_num_values = t.i32();
+                    else if (i2 == 2) t.i32();
+                    else if (i2 == 3) { /* read_bool: no bytes */ }
+                    else t.skip(t2);
+                }
+                t.pop();
+                break;
+            }
+            default: t.skip(ty);
+        }
+    }
+    h.header_size = t.pos();
+    return h;
+}
+
+WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c) {
+    WalkResult w;
+    try {
+        if (c.codec != 0) throw Error(PQ_ERR_CODEC, "Only uncompressed parquet files are supported");
+        int64_t off = c.data_page_offset;
+        if (c.has_dictionary_page_offset) off = std::min(off, c.dictionary_page_offset);
+        size_t cur = static_cast<size_t>(off);
+        int64_t values_read = 0, row = 0;
+        int32_t page_num = 0, dict_page = -1;
+        while (values_read < c.num_values) {  // column_reader.cpp:31-68
+            PageHeader h = read_page_header(file, len, cur);
+            pq_page_desc p{};
+            p.header_offset = static_cast<int64_t>(cur);
+            cur += h.header_size;
+            p.payload_offset = static_cast<int64_t>(cur);
+            p.payload_size = h.compressed;
+            p.page_type = h.type;
+            p.dict_page = dict_page;
+            p.first_row = row;
+            p.page_num = -1;
+            if (h.compressed < 0)
+                throw Error(PQ_ERR_ALLOC, "cannot create std::vector larger than max_size()");
+            if (h.type == PQ_DICTIONARY_PAGE) {
+                if (!h.has_dict) throw Error(PQ_ERR_OPTIONAL, "bad optional access");
+                if (h.dict_num_values < 0) throw Error(PQ_ERR_ALLOC, "vector::reserve");
+                p.num_values = h.dict_num_values;
+                p.page_num = page_num++;
+                dict_page = static_cast<int32_t>(w.pages.size());
+                p.dict_page = dict_page;
+            } else if (h.type == PQ_DATA_PAGE) {
+                if (!h.has_data) throw Error(PQ_ERR_OPTIONAL, "bad optional access");
+                if (h.data_num_values < 0)
+                    throw Error(PQ_ERR_ALLOC, "cannot create std::vector larger than max_size()");
+                p.num_values = h.data_num_values;
+                p.encoding = h.data_encoding;
+                p.page_num = page_num++;
+                values_read += h.data_num_values;
+                if (h.data_num_values > 0) row += h.data_num_values;
+            } else {
+                page_num++;  // read_pages counts skipped pages (column_reader.cpp:122)
+            }
+            w.pages.push_back(p);
+            cur += static_cast<size_t>(h.compressed);
+        }
+    } catch (const Error& e) {
+        w.error = e.code;
+        w.message = e.what();
+    }
+    return w;
+}
+
+std::vector<std::array<int64_t, 4>> page_index(const uint8_t* file, size_t len, const FileMeta& fm) {
+    std::vector<std::array<int64_t, 4>> out;  // parquet_reader.cpp:559-605
+    for (size_t rg = 0; rg < fm.row_groups.size(); rg++) {
+        const auto& r = fm.row_groups[rg];
+        for (size_t col = 0; col < r.columns.size(); col++) {
+            if (!r.columns[col].meta) continue;
+            const ColumnMeta& m = *r.columns[col].meta;
+            int64_t off = m.data_page_offset;
+            if (m.dictionary_page_offset) off = std::min(off, *m.dictionary_page_offset);
+            size_t cur = static_cast<size_t>(off);
+            int64_t values_read = 0;
+            while (values_read < m.num_values) {
+                if (cur > len + 256)  // corrupt chunk: the reference would loop forever here
+                    throw Error(PQ_ERR_UNSUPPORTED, "page walk ran past end of file");
+                PageHeader h = read_page_header(file, len, cur);
+                cur += h.header_size;
+                if (h.type == PQ_DATA_PAGE || h.type == PQ_DATA_PAGE_V2) {
+                    out.push_back({static_cast<int64_t>(cur), static_cast<int64_t>(static_cast<size_t>(h.compressed)),
+                                   static_cast<int64_t>(rg), static_cast<int64_t>(col)});
+                    if (h.type == PQ_DATA_PAGE && h.has_data) values_read += h.data_num_values;
+                }
+                cur += static_cast<size_t>(h.compressed);
+            }
+        }
+    }
+    return out;
+}
+
+}  // namespace pqfmt

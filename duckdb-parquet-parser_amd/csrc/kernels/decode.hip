@@ -1,0 +1,691 @@
+// decode.hip — gfx950 kernels for ColumnReader::read_all's value decode.
+//
+// Reference behaviour restated here (file:line in the reference):
+//   hybrid RLE/bit-packed decode   include/reader/rle_decoder.hpp:17-95
+//   def/rep level sections         src/reader/column_reader.cpp:146-170
+//   dictionary expansion           src/reader/column_reader.cpp:174-196
+//   BOOLEAN bit unpack             src/reader/column_reader.cpp:197-212
+//   PLAIN values                   src/reader/column_reader.cpp:213-268
+//   dictionary page                src/reader/column_reader.cpp:128-138
+//
+// Work decomposition: one wavefront per page (or per dictionary
+// page) for the serial stream parts, page bytes staged in LDS; the hybrid
+// stream's run headers are walked wave-uniformly and each run is expanded
+// 64 values per step across the lanes.  BYTE_ARRAY output is produced in two
+// kernels: k_ba_rows resolves every row to (source offset, length) and sums
+// per-tile bytes, a scan turns tile sums into output offsets, and
+// k_ba_gather writes offsets, validity and characters with 16-byte aligned,
+// coalesced stores.
+#include "kernels.hpp"
+
+#include "kernels/device_common.hpp"
+#include "pq_gpu.h"
+
+namespace pqk {
+namespace {
+
+using namespace dev;
+
+constexpr int kWavesPerBlock = 4;
+constexpr uint32_t kStageWords = 1024;  // 4 KiB of page bytes staged per wave
+
+// Page prologue shared by every data-page kernel: def-level stream, rep skip.
+struct PagePrologue {
+    uint32_t pos;       // ByteBuffer position after the level sections
+    Rle def;
+    int has_def;
+};
+
+__device__ int page_prologue(const Src& s, const ColumnParams& cp, PagePrologue& pp, DevErr* err,
+                             int32_t* any) {
+    uint32_t pos = 0;
+    pp.has_def = cp.max_def > 0;
+    if (pp.has_def) {  // 146-154
+        if (pos + 4 > s.size) { set_err(err, any, PQ_ERR_BUFFER, pos, 4, s.size); return 1; }
+        uint32_t def_len = src_u32(s, pos);
+        pos += 4;
+        if (static_cast<uint64_t>(pos) + def_len > s.size) {
+            set_err(err, any, PQ_ERR_BUFFER, pos, def_len, s.size);
+            return 1;
+        }
+        rle_init(pp.def, pos, def_len, level_bw(cp.max_def));
+        pos += def_len;
+    }
+    if (cp.max_rep > 0) {  // 156-164: decoded then unused by flat output
+        if (pos + 4 > s.size) { set_err(err, any, PQ_ERR_BUFFER, pos, 4, s.size); return 1; }
+        uint32_t rep_len = src_u32(s, pos);
+        pos += 4;
+        if (static_cast<uint64_t>(pos) + rep_len > s.size) {
+            set_err(err, any, PQ_ERR_BUFFER, pos, rep_len, s.size);
+            return 1;
+        }
+        pos += rep_len;
+    }
+    pp.pos = pos;
+    return 0;
+}
+
+// Inclusive wave prefix sum of a u32.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, kWave);
+        if (lane() >= static_cast<uint32_t>(d)) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t bcast_last(uint32_t v) { return __shfl(v, kWave - 1, kWave); }
+__device__ __forceinline__ uint32_t popc_below(uint64_t m) {
+    return __popcll(m & ((1ull << lane()) - 1ull));
+}
+
+// ── dictionary pages (column_reader.cpp:128-138) ───────────────────────────
+// BYTE_ARRAY entries are a serial u32-length chain: one wave per dictionary
+// page walks it in LDS; entries[] = (len << 32) | chars offset in the page.
+__global__ void __launch_bounds__(64) k_dict_entries(const uint8_t* __restrict__ bytes,
+                                                     const DevDict* __restrict__ dicts,
+                                                     uint64_t* __restrict__ entries,
+                                                     int32_t* __restrict__ dict_count,
+                                                     DevErr* __restrict__ dict_err,
+                                                     int32_t* __restrict__ err_any, int32_t type,
+                                                     int32_t plain_width) {
+    __shared__ uint32_t stage[8192];  // 32 KiB
+    const DevDict d = dicts[blockIdx.x];
+    const uint8_t* g = bytes + d.off;
+    uint32_t size = static_cast<uint32_t>(d.size);
+    DevErr* err = dict_err + blockIdx.x;
+    if (type != PQ_BYTE_ARRAY) {
+        // fixed width: entry k at k * plain_width; no walk needed
+        int32_t n = d.nvals;
+        if (n > 0 && type == PQ_FIXED_LEN_BYTE_ARRAY) {
+            set_err(err, err_any, PQ_ERR_FLBA, 0, 0, size);
+            if (lane() == 0) dict_count[blockIdx.x] = 0;
+            return;
+        }
+        if (n > 0 && plain_width <= 0) {
+            set_err(err, err_any, PQ_ERR_TYPE, 0, 0, size);
+            if (lane() == 0) dict_count[blockIdx.x] = 0;
+            return;
+        }
+        int32_t fit = plain_width > 0 ? static_cast<int32_t>(size / plain_width) : 0;
+        if (n > fit) {
+            set_err(err, err_any, PQ_ERR_BUFFER, fit * plain_width, plain_width, size);
+            n = fit;
+        }
+        if (lane() == 0) dict_count[blockIdx.x] = n < 0 ? 0 : n;
+        return;
+    }
+    Src s{nullptr, g, size};
+    if (size <= sizeof(stage)) {
+        stage_page(stage, g, size);
+        s.lds = stage;
+    }
+    if (lane() == 0) {
+        uint32_t pos = 0;
+        int32_t k = 0;
+        for (; k < d.nvals; k++) {
+            if (pos + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); break; }
+            uint32_t len = src_u32(s, pos);
+            pos += 4;
+            if (static_cast<uint64_t>(pos) + len > size) {
+                set_err(err, err_any, PQ_ERR_BUFFER, pos, len, size);
+                break;
+            }
+            entries[d.entry_base + k] = (static_cast<uint64_t>(len) << 32) | pos;
+            pos += len;
+        }
+        dict_count[blockIdx.x] = k;
+    }
+}
+
+// ── BYTE_ARRAY rows: every row -> (len << 32 | source offset) or NULL ──────
+struct RowsLds {
+    uint32_t stage[kStageWords];
+    uint32_t lv[kTileRows];   // def levels of the current tile
+    uint32_t a[kTileRows];    // dict index / plain chars offset per non-null rank
+    uint32_t b[kTileRows];    // plain length per non-null rank
+};
+
+__global__ void __launch_bounds__(256) k_ba_rows(const uint8_t* __restrict__ bytes,
+                                                 const DevPage* __restrict__ pages, int npages,
+                                                 const DevDict* __restrict__ dicts,
+                                                 const uint64_t* __restrict__ entries,
+                                                 const int32_t* __restrict__ dict_count,
+                                                 ColumnParams cp, uint64_t* __restrict__ row_codes,
+                                                 int64_t* __restrict__ tile_chars,
+                                                 const int32_t* __restrict__ page_tile0,
+                                                 DevErr* __restrict__ page_err,
+                                                 int32_t* __restrict__ err_any) {
+    __shared__ RowsLds lds_all[kWavesPerBlock];
+    const int wv = threadIdx.x / kWave;
+    const int p = blockIdx.x * kWavesPerBlock + wv;
+    if (p >= npages) return;
+    RowsLds& L = lds_all[wv];
+    const DevPage pg = pages[p];
+    DevErr* err = page_err + p;
+    const uint8_t* g = bytes + pg.off;
+    const uint32_t size = static_cast<uint32_t>(pg.size);
+    Src s{nullptr, g, size};
+    if (size <= kStageWords * 4) {
+        stage_page(L.stage, g, size);
+        s.lds = L.stage;
+    }
+    const int32_t tile0 = page_tile0[p];
+    const int32_t nv = pg.nvals;
+
+    PagePrologue pp;
+    if (page_prologue(s, cp, pp, err, err_any)) {
+        for (int32_t t = 0; t * kTileRows < nv; t++)
+            if (lane() == 0) tile_chars[tile0 + t] = 0;
+        return;
+    }
+    uint32_t pos = pp.pos;
+    const bool dict = pg.mode == MODE_DICT;
+    Rle ix;
+    uint32_t dict_n = 0;
+    uint32_t entry_base = 0;
+    if (dict) {  // 179-182: one bit-width byte, then the rest of the page
+        if (pos + 1 > size) {
+            set_err(err, err_any, PQ_ERR_BUFFER, pos, 1, size);
+            for (int32_t t = 0; t * kTileRows < nv; t++)
+                if (lane() == 0) tile_chars[tile0 + t] = 0;
+            return;
+        }
+        uint32_t bw = src_byte(s, pos);
+        pos += 1;
+        rle_init(ix, pos, size - pos, bw);
+        dict_n = static_cast<uint32_t>(dict_count[pg.dict]);
+        entry_base = static_cast<uint32_t>(dicts[pg.dict].entry_base);
+    }
+    int failed = 0;
+    for (int32_t r0 = 0, t = 0; r0 < nv; r0 += kTileRows, t++) {
+        const uint32_t m = min(static_cast<uint32_t>(nv - r0), static_cast<uint32_t>(kTileRows));
+        uint32_t* lv = L.lv;
+        int rc = 0;
+        if (pp.has_def) {
+            rc = rle_decode(pp.def, s, m, [&](uint32_t j, uint32_t v) { lv[j] = v & 0xFFFFu; });
+        } else {
+            for (uint32_t j = lane(); j < m; j += kWave) lv[j] = static_cast<uint32_t>(cp.max_def);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // non-null count of this tile (def as int16, column_reader.cpp:166-170)
+        uint32_t nn = 0, above = 0;
+        for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
+            uint32_t j = j0 + lane();
+            int32_t d = j < m ? static_cast<int16_t>(lv[j]) : -32768;
+            bool isnn = dict ? d == cp.max_def : d >= cp.max_def;
+            nn += __popcll(__ballot(isnn));
+            above |= __ballot(d > cp.max_def) != 0;
+        }
+        if (rc == 0 && dict && above) rc = PQ_ERR_UNSUPPORTED;
+        if (rc) { set_err(err, err_any, rc, 0, 0, size); failed = 1; }
+        if (!failed && dict) {
+            rc = rle_decode(ix, s, nn, [&](uint32_t j, uint32_t v) { L.a[j] = v; });
+            if (rc) { set_err(err, err_any, rc, 0, 0, size); failed = 1; }
+        } else if (!failed) {
+            // PLAIN BYTE_ARRAY chain (249-253): serial by lane 0
+            if (lane() == 0) {
+                for (uint32_t k = 0; k < nn; k++) {
+                    if (static_cast<uint64_t>(pos) + 4 > size) {
+                        set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size);
+                        failed = 1;
+                        break;
+                    }
+                    uint32_t len = src_u32(s, pos);
+                    pos += 4;
+                    if (static_cast<uint64_t>(pos) + len > size) {
+                        set_err(err, err_any, PQ_ERR_BUFFER, pos, len, size);
+                        failed = 1;
+                        break;
+                    }
+                    L.a[k] = pos;
+                    L.b[k] = len;
+                    pos += len;
+                }
+            }
+            failed = __shfl(failed, 0, kWave);
+            pos = __shfl(pos, 0, kWave);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        uint64_t tile_sum = 0;
+        uint32_t rank = 0;
+        for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
+            uint32_t j = j0 + lane();
+            bool in = j < m;
+            int32_t d = in ? static_cast<int16_t>(lv[j]) : -32768;
+            bool isnn = in && (dict ? d == cp.max_def : d >= cp.max_def);
+            uint64_t mask = __ballot(isnn);
+            uint32_t k = rank + popc_below(mask);
+            rank += __popcll(mask);
+            uint64_t code = 0xFFFFFFFFFFFFFFFFull;
+            if (isnn && !failed) {
+                if (dict) {
+                    uint32_t idx = L.a[k];
+                    if (static_cast<int32_t>(idx) >= 0 && idx < dict_n) code = entries[entry_base + idx];
+                } else {
+                    code = (static_cast<uint64_t>(L.b[k]) << 32) | L.a[k];
+                }
+            }
+            if (in) row_codes[pg.first_row + r0 + j] = code;
+            uint32_t len = code == 0xFFFFFFFFFFFFFFFFull ? 0u : static_cast<uint32_t>(code >> 32);
+            // 64-bit wave sum
+            uint64_t v = len;
+#pragma unroll
+            for (int dd = 32; dd >= 1; dd >>= 1) v += __shfl_xor(v, dd, kWave);
+            tile_sum += v;
+        }
+        if (lane() == 0) tile_chars[tile0 + t] = failed ? 0 : static_cast<int64_t>(tile_sum);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ── exclusive scan of int64 (3 phases) ─────────────────────────────────────
+constexpr int kScanBlock = 1024;
+constexpr int kScanItems = 8;  // per thread
+
+__device__ int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t* total) {
+    // sh: kScanBlock/64 slots
+    int64_t x = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        int64_t t = __shfl_up(x, d, kWave);
+        if (lane() >= static_cast<uint32_t>(d)) x += t;
+    }
+    const int w = threadIdx.x / kWave;
+    if (lane() == kWave - 1) sh[w] = x;
+    __syncthreads();
+    if (w == 0) {
+        int64_t y = lane() < blockDim.x / kWave ? sh[lane()] : 0;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            int64_t t = __shfl_up(y, d, kWave);
+            if (lane() >= static_cast<uint32_t>(d)) y += t;
+        }
+        if (lane() < blockDim.x / kWave) sh[lane()] = y;
+    }
+    __syncthreads();
+    int64_t base = w ? sh[w - 1] : 0;
+    *total = sh[blockDim.x / kWave - 1];
+    __syncthreads();
+    return base + x - v;
+}
+
+__global__ void __launch_bounds__(kScanBlock) k_scan_reduce(const int64_t* __restrict__ in, int64_t n,
+                                                            int64_t* __restrict__ block_sums) {
+    __shared__ int64_t sh[kScanBlock / kWave];
+    int64_t base = static_cast<int64_t>(blockIdx.x) * kScanBlock * kScanItems;
+    int64_t acc = 0;
+    for (int i = 0; i < kScanItems; i++) {
+        int64_t idx = base + static_cast<int64_t>(i) * kScanBlock + threadIdx.x;
+        if (idx < n) acc += in[idx];
+    }
+    int64_t tot;
+    block_excl_scan(acc, sh, &tot);
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kScanBlock) k_scan_blocks(int64_t* __restrict__ sums, int64_t nb,
+                                                            int64_t* __restrict__ total) {
+    __shared__ int64_t sh[kScanBlock / kWave];
+    int64_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += kScanBlock) {
+        int64_t idx = b0 + threadIdx.x;
+        int64_t v = idx < nb ? sums[idx] : 0;
+        int64_t tot;
+        int64_t ex = block_excl_scan(v, sh, &tot);
+        if (idx < nb) sums[idx] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ void __launch_bounds__(kScanBlock) k_scan_apply(const int64_t* __restrict__ in, int64_t n,
+                                                           const int64_t* __restrict__ block_off,
+                                                           int64_t* __restrict__ out) {
+    __shared__ int64_t sh[kScanBlock / kWave];
+    // each thread owns kScanItems consecutive elements
+    int64_t base = static_cast<int64_t>(blockIdx.x) * kScanBlock * kScanItems +
+                   static_cast<int64_t>(threadIdx.x) * kScanItems;
+    int64_t v[kScanItems];
+    int64_t acc = 0;
+    for (int i = 0; i < kScanItems; i++) {
+        v[i] = base + i < n ? in[base + i] : 0;
+        acc += v[i];
+    }
+    int64_t tot;
+    int64_t ex = block_excl_scan(acc, sh, &tot) + block_off[blockIdx.x];
+    for (int i = 0; i < kScanItems; i++) {
+        if (base + i < n) out[base + i] = ex;
+        ex += v[i];
+    }
+}
+
+// ── BYTE_ARRAY gather: offsets, validity, chars ────────────────────────────
+constexpr int kGatherWindow = 2048;  // 16-byte output blocks per window (32 KiB)
+struct GatherLds {
+    uint32_t loff[kTileRows + 1];
+    uint32_t src[kTileRows];
+    uint16_t blockrow[kGatherWindow];
+};
+
+__global__ void __launch_bounds__(256) k_ba_gather(const uint8_t* __restrict__ bytes,
+                                                   const DevPage* __restrict__ pages,
+                                                   const DevTile* __restrict__ tiles, int ntiles,
+                                                   const DevDict* __restrict__ dicts,
+                                                   const uint64_t* __restrict__ row_codes,
+                                                   const int64_t* __restrict__ tile_base,
+                                                   int64_t nrows_total,
+                                                   const int64_t* __restrict__ total_ptr,
+                                                   int64_t capacity, int32_t* __restrict__ overflow,
+                                                   uint32_t* __restrict__ validity,
+                                                   int64_t* __restrict__ offsets,
+                                                   uint8_t* __restrict__ chars) {
+    __shared__ GatherLds lds_all[kWavesPerBlock];
+    const int wv = threadIdx.x / kWave;
+    const int t = blockIdx.x * kWavesPerBlock + wv;
+    if (t >= ntiles) return;
+    GatherLds& L = lds_all[wv];
+    const DevTile tl = tiles[t];
+    const DevPage pg = pages[tl.page];
+    const uint8_t* srcbase = bytes + (pg.mode == MODE_DICT ? dicts[pg.dict].off : pg.off);
+    const int64_t R0 = pg.first_row + tl.row0;
+    const uint32_t n = static_cast<uint32_t>(tl.nrows);
+    const int64_t G0 = tile_base[t];
+
+    // lengths -> local offsets, validity bits, global offsets
+    uint32_t run = 0;
+    for (uint32_t j0 = 0; j0 < n; j0 += kWave) {
+        uint32_t j = j0 + lane();
+        bool in = j < n;
+        uint64_t code = in ? row_codes[R0 + j] : 0xFFFFFFFFFFFFFFFFull;
+        bool valid = code != 0xFFFFFFFFFFFFFFFFull;
+        uint32_t len = valid ? static_cast<uint32_t>(code >> 32) : 0u;
+        uint32_t inc = wave_incl_scan(len);
+        uint32_t ex = run + inc - len;
+        if (in) {
+            L.loff[j] = ex;
+            L.src[j] = valid ? static_cast<uint32_t>(code) : 0u;
+            offsets[R0 + j] = G0 + ex;
+        }
+        run += bcast_last(inc);
+        uint64_t vm = __ballot(valid);
+        int64_t R = R0 + j0;
+        uint32_t w = static_cast<uint32_t>(R >> 5), sh = static_cast<uint32_t>(R & 31);
+        // bits [R, R+64) -> up to three 32-bit words
+        if (lane() < 3) {
+            uint32_t part;
+            if (lane() == 0) part = static_cast<uint32_t>(vm << sh);
+            else if (lane() == 1) part = static_cast<uint32_t>((sh ? (vm >> (32 - sh)) : (vm >> 32)));
+            else part = sh ? static_cast<uint32_t>(vm >> (64 - sh)) : 0u;
+            if (part) atomicOr(&validity[w + lane()], part);
+        }
+    }
+    if (lane() == 0) L.loff[n] = run;
+    if (R0 + n == nrows_total && lane() == 0) offsets[nrows_total] = *total_ptr;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+    const uint32_t total = run;
+    if (total == 0) return;
+    if (G0 + total > capacity) {  // output buffer too small: host grows it and re-runs
+        if (lane() == 0) atomicOr(overflow, 1);
+        return;
+    }
+    const int64_t G1 = G0 + total;
+    const int64_t B0 = G0 >> 4;
+    const int64_t nb = ((G1 - 1) >> 4) - B0 + 1;
+    for (int64_t w0 = 0; w0 < nb; w0 += kGatherWindow) {
+        const int64_t w1 = min(nb, w0 + static_cast<int64_t>(kGatherWindow));
+        // scatter: row r owns the blocks whose first in-tile byte lies in it
+        for (uint32_t r = lane(); r < n; r += kWave) {
+            uint32_t s = L.loff[r], e = L.loff[r + 1];
+            if (e <= s) continue;
+            int64_t blo = s == 0 ? 0 : ((s + G0 + 15) >> 4) - B0;
+            int64_t bhi = ((e + G0 + 15) >> 4) - B0 - 1;
+            blo = max(blo, w0);
+            bhi = min(bhi, w1 - 1);
+            for (int64_t b = blo; b <= bhi; b++) L.blockrow[b - w0] = static_cast<uint16_t>(r);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (int64_t b = w0 + lane(); b < w1; b += kWave) {
+            const int64_t blk = (B0 + b) << 4;
+            const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
+            uint32_t r = L.blockrow[b - w0];
+            uint32_t q = static_cast<uint32_t>(gs - G0);
+            uint32_t p = q - L.loff[r];
+            uint32_t outw[4] = {0, 0, 0, 0};
+            const uint32_t cnt = static_cast<uint32_t>(ge - gs);
+            const uint32_t first = static_cast<uint32_t>(gs - blk);
+            for (uint32_t k = 0; k < cnt; k++) {
+                while (p >= L.loff[r + 1] - L.loff[r]) { r++; p = 0; }
+                uint32_t byte = srcbase[L.src[r] + p];
+                p++;
+                uint32_t at = first + k;
+                outw[at >> 2] |= byte << (8 * (at & 3));
+            }
+            if (cnt == 16) {
+                *reinterpret_cast<uint4*>(chars + blk) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+            } else {
+                for (uint32_t k = 0; k < cnt; k++) {
+                    uint32_t at = first + k;
+                    chars[blk + at] = static_cast<uint8_t>(outw[at >> 2] >> (8 * (at & 3)));
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+}
+
+// ── fixed-width values (INT32/INT64/FLOAT/DOUBLE/INT96/BOOLEAN) ─────────────
+struct FixedLds {
+    uint32_t stage[kStageWords];
+    uint32_t lv[kTileRows];
+    uint32_t a[kTileRows];
+};
+
+__global__ void __launch_bounds__(256) k_fixed(const uint8_t* __restrict__ bytes,
+                                               const DevPage* __restrict__ pages, int npages,
+                                               const DevDict* __restrict__ dicts,
+                                               const int32_t* __restrict__ dict_count,
+                                               ColumnParams cp, uint32_t* __restrict__ validity,
+                                               uint8_t* __restrict__ values,
+                                               DevErr* __restrict__ page_err,
+                                               int32_t* __restrict__ err_any) {
+    __shared__ FixedLds lds_all[kWavesPerBlock];
+    const int wv = threadIdx.x / kWave;
+    const int p = blockIdx.x * kWavesPerBlock + wv;
+    if (p >= npages) return;
+    FixedLds& L = lds_all[wv];
+    const DevPage pg = pages[p];
+    DevErr* err = page_err + p;
+    const uint8_t* g = bytes + pg.off;
+    const uint32_t size = static_cast<uint32_t>(pg.size);
+    Src s{nullptr, g, size};
+    if (size <= kStageWords * 4) {
+        stage_page(L.stage, g, size);
+        s.lds = L.stage;
+    }
+    const int32_t nv = pg.nvals;
+    const uint32_t W = static_cast<uint32_t>(cp.width);
+    const uint32_t PW = static_cast<uint32_t>(cp.plain_width);
+    PagePrologue pp;
+    if (page_prologue(s, cp, pp, err, err_any)) return;
+    uint32_t pos = pp.pos;
+    const int mode = pg.mode;
+    Rle ix;
+    uint32_t dict_n = 0;
+    Src ds{nullptr, nullptr, 0};
+    if (mode == MODE_DICT) {
+        if (pos + 1 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 1, size); return; }
+        uint32_t bw = src_byte(s, pos);
+        pos += 1;
+        rle_init(ix, pos, size - pos, bw);
+        dict_n = static_cast<uint32_t>(dict_count[pg.dict]);
+        const DevDict dd = dicts[pg.dict];
+        ds = Src{nullptr, bytes + dd.off, static_cast<uint32_t>(dd.size)};
+    }
+    uint32_t rank_base = 0;  // non-null values before this tile (PLAIN / BOOLEAN)
+    for (int32_t r0 = 0; r0 < nv; r0 += kTileRows) {
+        const uint32_t m = min(static_cast<uint32_t>(nv - r0), static_cast<uint32_t>(kTileRows));
+        int rc = 0;
+        if (pp.has_def) {
+            rc = rle_decode(pp.def, s, m, [&](uint32_t j, uint32_t v) { L.lv[j] = v & 0xFFFFu; });
+        } else {
+            for (uint32_t j = lane(); j < m; j += kWave) L.lv[j] = static_cast<uint32_t>(cp.max_def);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        uint32_t nn = 0, above = 0;
+        const bool dict = mode == MODE_DICT;
+        for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
+            uint32_t j = j0 + lane();
+            int32_t d = j < m ? static_cast<int16_t>(L.lv[j]) : -32768;
+            bool isnn = dict ? d == cp.max_def : d >= cp.max_def;
+            nn += __popcll(__ballot(isnn));
+            above |= __ballot(d > cp.max_def) != 0;
+        }
+        if (rc == 0 && dict && above) rc = PQ_ERR_UNSUPPORTED;
+        if (rc) { set_err(err, err_any, rc, 0, 0, size); return; }
+        if (dict) {
+            rc = rle_decode(ix, s, nn, [&](uint32_t j, uint32_t v) { L.a[j] = v; });
+            if (rc) { set_err(err, err_any, rc, 0, 0, size); return; }
+        } else if (nn > 0) {
+            // PLAIN bounds: the first rank whose read overruns (ByteBuffer::check)
+            if (cp.type == PQ_FIXED_LEN_BYTE_ARRAY) { set_err(err, err_any, PQ_ERR_FLBA, 0, 0, size); return; }
+            if (PW == 0 && mode != MODE_BOOL) { set_err(err, err_any, PQ_ERR_TYPE, 0, 0, size); return; }
+            if (mode == MODE_BOOL) {
+                uint64_t last = rank_base + nn - 1;  // bytes needed: floor(last/8)+1
+                uint64_t need_end = pos + last / 8 + 1;
+                if (need_end > size) {
+                    uint64_t k = static_cast<uint64_t>(size - pos) * 8;  // first rank without a byte
+                    set_err(err, err_any, PQ_ERR_BUFFER, static_cast<uint32_t>(pos + k / 8), 1, size);
+                    return;
+                }
+            } else {
+                uint64_t need_end = pos + static_cast<uint64_t>(rank_base + nn) * PW;
+                if (need_end > size) {
+                    uint64_t k = (size - pos) / PW;
+                    set_err(err, err_any, PQ_ERR_BUFFER, static_cast<uint32_t>(pos + k * PW), PW, size);
+                    return;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        uint32_t rank = 0;
+        for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
+            uint32_t j = j0 + lane();
+            bool in = j < m;
+            int32_t d = in ? static_cast<int16_t>(L.lv[j]) : -32768;
+            bool isnn = in && (dict ? d == cp.max_def : d >= cp.max_def);
+            uint64_t mask = __ballot(isnn);
+            uint32_t k = rank + popc_below(mask);
+            rank += __popcll(mask);
+            bool valid = isnn;
+            uint32_t w[3] = {0, 0, 0};
+            if (isnn) {
+                if (dict) {
+                    uint32_t idx = L.a[k];
+                    valid = static_cast<int32_t>(idx) >= 0 && idx < dict_n;
+                    if (valid) {
+                        uint32_t at = idx * PW;
+                        if (cp.type == PQ_BOOLEAN) w[0] = src_byte(ds, at) != 0;
+                        else for (uint32_t q = 0; q < (W + 3) / 4; q++) w[q] = src_u32(ds, at + 4 * q);
+                    }
+                } else if (mode == MODE_BOOL) {
+                    uint32_t kk = rank_base + k;
+                    w[0] = (src_byte(s, pos + kk / 8) >> (kk % 8)) & 1u;
+                } else {
+                    uint32_t at = pos + (rank_base + k) * PW;
+                    if (cp.type == PQ_BOOLEAN) w[0] = src_byte(s, at) != 0;
+                    else for (uint32_t q = 0; q < (W + 3) / 4; q++) w[q] = src_u32(s, at + 4 * q);
+                }
+            }
+            const int64_t R = pg.first_row + r0 + j;
+            if (in) {
+                uint8_t* o = values + R * W;
+                if (W == 4) *reinterpret_cast<uint32_t*>(o) = w[0];
+                else if (W == 8) *reinterpret_cast<uint2*>(o) = make_uint2(w[0], w[1]);
+                else if (W == 1) *o = static_cast<uint8_t>(w[0]);
+                else for (uint32_t q = 0; q < W / 4; q++) reinterpret_cast<uint32_t*>(o)[q] = w[q];
+            }
+            uint64_t vm = __ballot(valid && in);
+            const int64_t RB = pg.first_row + r0 + j0;
+            uint32_t wi = static_cast<uint32_t>(RB >> 5), sh = static_cast<uint32_t>(RB & 31);
+            if (lane() < 3) {
+                uint32_t part;
+                if (lane() == 0) part = static_cast<uint32_t>(vm << sh);
+                else if (lane() == 1) part = static_cast<uint32_t>(sh ? (vm >> (32 - sh)) : (vm >> 32));
+                else part = sh ? static_cast<uint32_t>(vm >> (64 - sh)) : 0u;
+                if (part) atomicOr(&validity[wi + lane()], part);
+            }
+        }
+        if (!dict) rank_base += nn;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+}  // namespace
+
+void launch_dict_entries(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
+                         uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any,
+                         int32_t type, int32_t plain_width) {
+    if (ndicts <= 0) return;
+    hipLaunchKernelGGL(k_dict_entries, dim3(ndicts), dim3(64), 0, s, bytes, dicts, entries,
+                       dict_count, dict_err, err_any, type, plain_width);
+}
+
+void launch_ba_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
+                    const DevDict* dicts, const uint64_t* entries, const int32_t* dict_count,
+                    ColumnParams cp, uint64_t* row_codes, int64_t* tile_chars,
+                    const int32_t* page_tile0, DevErr* page_err, int32_t* err_any) {
+    if (npages <= 0) return;
+    int blocks = (npages + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(k_ba_rows, dim3(blocks), dim3(256), 0, s, bytes, pages, npages, dicts,
+                       entries, dict_count, cp, row_codes, tile_chars, page_tile0, page_err,
+                       err_any);
+}
+
+void launch_scan_i64(hipStream_t s, const int64_t* in, int64_t* out_excl, int64_t n,
+                     int64_t* total, int64_t* scratch) {
+    if (n <= 0) {
+        (void)hipMemsetAsync(total, 0, sizeof(int64_t), s);
+        return;
+    }
+    const int64_t per = static_cast<int64_t>(kScanBlock) * kScanItems;
+    int64_t nb = (n + per - 1) / per;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(static_cast<uint32_t>(nb)), dim3(kScanBlock), 0, s, in,
+                       n, scratch);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanBlock), 0, s, scratch, nb, total);
+    hipLaunchKernelGGL(k_scan_apply, dim3(static_cast<uint32_t>(nb)), dim3(kScanBlock), 0, s, in,
+                       n, scratch, out_excl);
+}
+
+void launch_ba_gather(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
+                      const DevTile* tiles, int ntiles, const DevDict* dicts,
+                      const uint64_t* entries, const uint64_t* row_codes,
+                      const int64_t* tile_base, int64_t nrows_total, const int64_t* total,
+                      int64_t capacity, int32_t* overflow, uint32_t* validity, int64_t* offsets,
+                      uint8_t* chars) {
+    (void)entries;
+    if (ntiles <= 0) return;
+    int blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(k_ba_gather, dim3(blocks), dim3(256), 0, s, bytes, pages, tiles, ntiles,
+                       dicts, row_codes, tile_base, nrows_total, total, capacity, overflow,
+                       validity, offsets, chars);
+}
+
+void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
+                  const DevDict* dicts, const int32_t* dict_count, ColumnParams cp,
+                  uint32_t* validity, uint8_t* values, DevErr* page_err, int32_t* err_any) {
+    if (npages <= 0) return;
+    int blocks = (npages + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL(k_fixed, dim3(blocks), dim3(256), 0, s, bytes, pages, npages, dicts,
+                       dict_count, cp, validity, values, page_err, err_any);
+}
+
+}  // namespace pqk

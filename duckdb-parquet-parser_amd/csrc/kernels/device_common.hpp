@@ -1,0 +1,161 @@
+// device_common.hpp — device helpers shared by the decode and regex kernels:
+// the page byte source (LDS-staged words or the HBM image, zero past the page
+// end) and the hybrid RLE/bit-packed stream state machine, a restatement of
+// the reference's RleDecoder (include/reader/rle_decoder.hpp:6-108).
+#pragma once
+#include "kernels/kernels.hpp"
+#include "pq_gpu.h"
+
+namespace pqk {
+namespace dev {
+
+__device__ __forceinline__ uint32_t lane() { return __lane_id(); }
+
+// ── page byte source: LDS-staged words, or the HBM image (zero past end) ──
+struct Src {
+    const uint32_t* lds;  // staged payload words, or nullptr
+    const uint8_t* g;     // payload start in the device byte image
+    uint32_t size;        // payload bytes
+};
+
+__device__ __forceinline__ uint32_t gword(const uint8_t* g, uint64_t b) {
+    uintptr_t a = reinterpret_cast<uintptr_t>(g) + b;
+    const uint32_t* ap = reinterpret_cast<const uint32_t*>(a & ~static_cast<uintptr_t>(3));
+    return __builtin_amdgcn_alignbyte(ap[1], ap[0], static_cast<uint32_t>(a & 3));
+}
+
+__device__ __forceinline__ uint32_t src_word(const Src& s, uint64_t wi) {
+    uint64_t b = wi * 4;
+    if (b >= s.size) return 0u;
+    uint32_t w = s.lds ? s.lds[wi] : gword(s.g, b);
+    uint64_t rem = s.size - b;
+    if (rem < 4) w &= (1u << (8 * rem)) - 1u;
+    return w;
+}
+__device__ __forceinline__ uint32_t src_byte(const Src& s, uint32_t p) {
+    return (src_word(s, p >> 2) >> ((p & 3) * 8)) & 0xFFu;
+}
+__device__ __forceinline__ uint32_t src_u32(const Src& s, uint32_t p) {
+    uint32_t lo = src_word(s, p >> 2), hi = src_word(s, (p >> 2) + 1);
+    return __builtin_amdgcn_alignbyte(hi, lo, p & 3);
+}
+// low min(bw, 32) bits of the bit field starting at page bit `b`
+__device__ __forceinline__ uint32_t src_bits(const Src& s, uint64_t b, uint32_t bw) {
+    uint64_t wi = b >> 5;
+    uint64_t v = (static_cast<uint64_t>(src_word(s, wi + 1)) << 32) | src_word(s, wi);
+    uint32_t x = static_cast<uint32_t>(v >> (b & 31));
+    return bw >= 32 ? x : (x & ((1u << bw) - 1u));
+}
+
+// Stage a page's payload into this wave's LDS words (zero-filled tail word).
+__device__ inline void stage_page(uint32_t* lds, const uint8_t* g, uint32_t size) {
+    uint32_t nw = (size + 3) / 4;
+    for (uint32_t i = lane(); i < nw; i += kWave) {
+        uint32_t w = gword(g, static_cast<uint64_t>(i) * 4);
+        uint32_t rem = size - i * 4;
+        if (rem < 4) w &= (1u << (8 * rem)) - 1u;
+        lds[i] = w;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+}
+
+// ── hybrid RLE / bit-packed decoder: rle_decoder.hpp state machine ─────────
+struct Rle {
+    uint32_t base;      // stream start (page byte offset)
+    uint32_t size;      // size_
+    uint32_t pos;       // pos_
+    uint32_t bw;        // bit_width_
+    uint32_t repeat;    // repeat_count_
+    uint32_t literal;   // literal_count_ (u32 wrap kept)
+    uint32_t value;     // low 32 bits of current_value_
+    uint32_t lit_start; // literal_pos_ - data_
+    uint32_t lit_bit;   // literal_bit_offset_
+    uint32_t lit_valid; // literal_pos_ != nullptr
+};
+
+__device__ __forceinline__ void rle_init(Rle& r, uint32_t base, uint32_t size, uint32_t bw) {
+    r.base = base; r.size = size; r.pos = 0; r.bw = bw; r.repeat = 0; r.literal = 0;
+    r.value = 0; r.lit_start = 0; r.lit_bit = 0; r.lit_valid = 0;
+}
+
+// Produce the next n values of the stream; out(j, v) for j in [0, n) spread
+// over the lanes.  Wave-uniform control flow.
+template <class F>
+__device__ int rle_decode(Rle& r, const Src& s, uint32_t n, F&& out) {
+    uint32_t done = 0;
+    while (done < n) {
+        if (r.repeat == 0 && r.literal == 0) {
+            if (r.pos >= r.size) {  // exhausted: zero-fill (rle_decoder.hpp:20-23)
+                for (uint32_t j = done + lane(); j < n; j += kWave) out(j, 0u);
+                return 0;
+            }
+            uint32_t ind = 0, shift = 0;  // read_varint32 (76-86)
+            while (r.pos < r.size) {
+                uint32_t b = src_byte(s, r.base + r.pos);
+                r.pos++;
+                if (shift < 32) ind |= (b & 0x7Fu) << shift;
+                if (!(b & 0x80u)) break;
+                shift += 7;
+            }
+            if (ind & 1u) {  // literal run (41-46)
+                r.literal = (ind >> 1) * 8u;
+                r.lit_start = r.pos;
+                r.lit_valid = 1;
+                r.lit_bit = 0;
+            } else {  // repeated run (48-50, read_fixed_width_value 88-95)
+                r.repeat = ind >> 1;
+                uint32_t nb = (r.bw + 7) / 8, v = 0;
+                for (uint32_t i = 0; i < nb && r.pos < r.size; i++) {
+                    uint32_t b = src_byte(s, r.base + r.pos);
+                    r.pos++;
+                    if (i < 4) v |= b << (8 * i);
+                }
+                r.value = v;
+            }
+        }
+        if (r.bw > 64) return PQ_ERR_UNSUPPORTED;
+        if (r.repeat > 0) {
+            uint32_t k = min(r.repeat, n - done);
+            for (uint32_t j = lane(); j < k; j += kWave) out(done + j, r.value);
+            r.repeat -= k;
+            done += k;
+        } else {
+            // literal_count_ == 0 here means a zero-count run: the reference's
+            // counter wraps and every later value is read from the literal cursor.
+            if (r.bw > 0 && !r.lit_valid) return PQ_ERR_UNSUPPORTED;
+            bool wrapped = r.literal == 0;
+            uint32_t k = wrapped ? n - done : min(r.literal, n - done);
+            uint64_t bit0 = static_cast<uint64_t>(r.base + r.lit_start) * 8u + r.lit_bit;
+            for (uint32_t j = lane(); j < k; j += kWave)
+                out(done + j, r.bw ? src_bits(s, bit0 + static_cast<uint64_t>(j) * r.bw, r.bw) : 0u);
+            bool finishes = !wrapped && k == r.literal;
+            r.lit_bit += k * r.bw;
+            r.literal -= k;
+            if (finishes && r.bw > 0) r.pos = r.lit_start + (r.lit_bit + 7) / 8;  // 66-72
+            done += k;
+        }
+    }
+    return 0;
+}
+
+__device__ __forceinline__ uint32_t level_bw(int32_t m) {  // column_reader.cpp:270-276
+    uint32_t bw = 0;
+    while (m > 0) { bw++; m >>= 1; }
+    return bw;
+}
+
+__device__ __forceinline__ void set_err(DevErr* e, int32_t* any, int code, uint32_t pos, uint32_t need,
+                                        uint32_t size) {
+    if (lane() == 0) {
+        e->code = code;
+        e->pos = static_cast<int32_t>(pos);
+        e->need = static_cast<int32_t>(need);
+        e->size = static_cast<int32_t>(size);
+        atomicOr(any, 1);
+    }
+}
+
+
+}  // namespace dev
+}  // namespace pqk

@@ -1,0 +1,84 @@
+// kernels.hpp — device-side data layout shared by the HIP kernels and the
+// C-ABI host code (capi.hip).  See DESIGN.md "Data layout in HBM".
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace pqk {
+
+constexpr int kWave = 64;
+constexpr int kTileRows = 512;        // rows per decode tile (ref-layout page = 1 tile)
+constexpr uint32_t kNullCode = 0xFFFFFFFFu;
+
+enum PageMode : int32_t { MODE_DICT = 0, MODE_PLAIN = 1, MODE_BOOL = 2 };
+
+// One data page, as the kernels see it (32 B, HBM-resident).
+struct DevPage {
+    uint64_t off;       // payload offset in the device byte image
+    int32_t size;       // payload bytes (compressed_page_size)
+    int32_t nvals;      // DataPageHeader.num_values (= rows produced)
+    int64_t first_row;  // output row of the first value
+    int32_t mode;       // PageMode
+    int32_t dict;       // DevDict index or -1
+};
+
+// One dictionary page (column_reader.cpp:128-138).
+struct DevDict {
+    uint64_t off;        // payload offset in the device byte image
+    int32_t size;        // payload bytes
+    int32_t nvals;       // entries declared by the header
+    int32_t entry_base;  // first slot in the entry table
+    int32_t pad;
+};
+
+// A tile = up to kTileRows consecutive rows of one page.
+struct DevTile {
+    int32_t page;
+    int32_t row0;    // first row within the page
+    int32_t nrows;
+    int32_t pad;
+};
+
+// Error record: code 0 = ok; BUFFER errors carry (pos, need, size) so the host
+// can rebuild the reference message "ByteBuffer: read beyond end (...)".
+struct DevErr {
+    int32_t code;
+    int32_t pos;
+    int32_t need;
+    int32_t size;
+};
+
+struct ColumnParams {
+    int32_t type;
+    int16_t max_def;
+    int16_t max_rep;
+    int32_t width;      // fixed-width output bytes (BOOLEAN 1, INT96 12)
+    int32_t plain_width;// bytes per PLAIN value in the page
+};
+
+// ── launch wrappers (decode.hip) ────────────────────────────────────────────
+void launch_dict_entries(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
+                         uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any,
+                         int32_t type, int32_t plain_width);
+
+void launch_ba_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
+                    const DevDict* dicts, const uint64_t* entries, const int32_t* dict_count,
+                    ColumnParams cp, uint64_t* row_codes, int64_t* tile_chars,
+                    const int32_t* page_tile0, DevErr* page_err, int32_t* err_any);
+
+void launch_scan_i64(hipStream_t s, const int64_t* in, int64_t* out_excl, int64_t n,
+                     int64_t* total, int64_t* scratch);
+
+void launch_ba_gather(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
+                      const DevTile* tiles, int ntiles, const DevDict* dicts,
+                      const uint64_t* entries, const uint64_t* row_codes,
+                      const int64_t* tile_base, int64_t nrows_total, const int64_t* total,
+                      int64_t capacity, int32_t* overflow, uint32_t* validity, int64_t* offsets,
+                      uint8_t* chars);
+
+void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
+                  const DevDict* dicts, const int32_t* dict_count, ColumnParams cp,
+                  uint32_t* validity, uint8_t* values, DevErr* page_err, int32_t* err_any);
+
+}  // namespace pqk

@@ -1,0 +1,180 @@
+/*
+ * pq_gpu.h — C ABI of the MI355X Parquet page-decode / regex page-scan path.
+ *
+ * This is the drop-in boundary behind the reference's C++ API
+ * (sputnik89/duckdb-parquet-parser).  Plain C: pointers, sizes, status codes,
+ * no C++ or torch types, and no exception ever crosses it.  Each entry point
+ * names the reference interface it replaces:
+ *
+ *   pq_build_page_table  ColumnReader::read_all's page walk
+ *                        (src/reader/column_reader.cpp:18-71, the header loop
+ *                        and PageHeader::deserialize, src/reader/metadata.cpp:121-155)
+ *   pq_chunk_upload      the ReadRangeFunc byte supply
+ *                        (include/reader/column_reader.hpp:10; parquet_reader.cpp:173-178)
+ *   pq_decode            ColumnReader::read_all / read_pages value decode
+ *                        (column_reader.cpp:128-268, rle_decoder.hpp:6-108)
+ *   pq_regex_pages       the README's --regex-column page filter (README.md:54-64;
+ *                        no source in the reference — contract in SURVEY §8a R-REGEX)
+ *   pq_file_*            ParquetReader::open footer/schema/page index
+ *                        (parquet_reader.cpp:14-61, 495-605)
+ *
+ * Ownership: a context owns device memory it hands out; every pq_*_free
+ * releases it.  A context is used from one host thread at a time (the
+ * reference's ParquetReader is not thread-safe either, parquet_reader.cpp:189).
+ * Status: 0 = OK, negative = error class below; pq_last_error() has the text,
+ * which reproduces the reference's exception message where one exists.
+ */
+#ifndef PQ_GPU_H
+#define PQ_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    PQ_OK = 0,
+    PQ_ERR_CODEC = -1,        /* "Only uncompressed parquet files are supported" (column_reader.cpp:13-15) */
+    PQ_ERR_BUFFER = -2,       /* "ByteBuffer: read beyond end (pos=P need=N size=S)" (common.hpp:162-168) */
+    PQ_ERR_OPTIONAL = -3,     /* std::bad_optional_access (column_reader.cpp:50,57)                       */
+    PQ_ERR_FLBA = -4,         /* "FIXED_LEN_BYTE_ARRAY not supported without type_length" (254-256)      */
+    PQ_ERR_TYPE = -5,         /* "Unsupported type: N" (column_reader.cpp:265-266)                        */
+    PQ_ERR_THRIFT = -6,       /* ThriftReader::skip unknown type / "varint too long"                      */
+    PQ_ERR_ALLOC = -7,        /* negative sizes (std::vector length_error / bad_alloc)                    */
+    PQ_ERR_UNSUPPORTED = -8,  /* input outside the parity scope (reference behaviour undefined)          */
+    PQ_ERR_ARG = -20,         /* bad argument to this API                                                 */
+    PQ_ERR_HIP = -21,         /* HIP runtime failure / no device                                          */
+    PQ_ERR_REGEX = -22        /* pattern outside the supported RE2/Python-re subset                       */
+};
+
+enum { PQ_BOOLEAN = 0, PQ_INT32, PQ_INT64, PQ_INT96, PQ_FLOAT, PQ_DOUBLE, PQ_BYTE_ARRAY,
+       PQ_FIXED_LEN_BYTE_ARRAY };
+enum { PQ_DATA_PAGE = 0, PQ_INDEX_PAGE = 1, PQ_DICTIONARY_PAGE = 2, PQ_DATA_PAGE_V2 = 3 };
+
+typedef struct pq_ctx pq_ctx;
+typedef struct pq_chunk pq_chunk; /* device-resident column chunk(s) of one leaf column */
+
+/* ColumnChunk.meta_data + ColumnInfo fields the decode needs
+ * (include/reader/metadata.hpp:17-28, include/reader/column_info.hpp:6-20). */
+typedef struct {
+    int64_t num_values;
+    int64_t data_page_offset;
+    int64_t dictionary_page_offset;
+    int32_t has_dictionary_page_offset;
+    int32_t codec;
+    int32_t type;           /* ParquetType of the leaf column */
+    int16_t max_def_level;
+    int16_t max_rep_level;
+} pq_chunk_desc;
+
+/* One page of the walk (dictionary, data and skipped pages alike). */
+typedef struct {
+    int64_t header_offset;   /* file offset of the Thrift page header              */
+    int64_t payload_offset;  /* file offset of the payload (after the header)      */
+    int32_t payload_size;    /* compressed_page_size                               */
+    int32_t page_type;       /* PageType                                           */
+    int32_t num_values;      /* data: DataPageHeader.num_values; dict: entries     */
+    int32_t encoding;        /* data: DataPageHeader.encoding                      */
+    int32_t page_num;        /* ColumnReader::read_pages page_num                  */
+    int32_t dict_page;       /* index of the dictionary page in force, or -1       */
+    int64_t first_row;       /* data pages: first output row                       */
+} pq_page_desc;
+
+/* Device-resident columnar result (SURVEY §8b "pq_column_out"):
+ *   validity  LSB-first bitmap, bit i = row i non-null; ceil(n/32) words
+ *   values    fixed-width types: n * value_width bytes (NULL rows zeroed);
+ *             BYTE_ARRAY: the concatenated chars
+ *   offsets   BYTE_ARRAY: n + 1 int64 offsets into values
+ * INT96 is returned raw (12 bytes); the C++ adapter renders the reference's
+ * "INT96(hi:lo)" string (column_reader.cpp:257-264). BOOLEAN is 1 byte 0/1. */
+typedef struct {
+    int64_t num_rows;
+    int32_t type;
+    int32_t value_width;     /* 0 for BYTE_ARRAY */
+    uint32_t* d_validity;
+    uint8_t* d_values;
+    int64_t* d_offsets;
+    int64_t num_bytes;       /* bytes in d_values */
+    int64_t capacity_rows;   /* allocation bookkeeping (reuse across calls) */
+    int64_t capacity_bytes;
+} pq_column;
+
+/* ── context ─────────────────────────────────────────────────────────────── */
+pq_ctx* pq_ctx_create(int device);
+void pq_ctx_destroy(pq_ctx* ctx);
+const char* pq_last_error(const pq_ctx* ctx);
+void* pq_ctx_stream(pq_ctx* ctx);              /* the hipStream_t kernels run on */
+int pq_ctx_sync(pq_ctx* ctx);
+
+/* ── host page walk (R-WALK / R-HDR) ────────────────────────────────────── */
+/* Walks one chunk exactly like ColumnReader::read_all (256-byte header window,
+ * zero padding past EOF).  Writes up to `cap` pages; *npages = pages walked.
+ * Returns 0, or the error met by the walk after *npages good pages (the
+ * message in err). */
+int pq_build_page_table(const uint8_t* file, size_t file_len, const pq_chunk_desc* chunk,
+                        pq_page_desc* pages, int64_t cap, int64_t* npages, char* err,
+                        size_t errlen);
+
+/* ── device chunks ───────────────────────────────────────────────────────── */
+/* Upload `nchunks` column chunks of ONE leaf column (e.g. every row group's
+ * chunk of that column) from a host file image; the walk runs on the host,
+ * the page bytes go to HBM once.  Rows of chunk k follow chunk k-1
+ * (ParquetReader::read_column concatenation, parquet_reader.cpp:133-144). */
+int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc* chunks,
+                    int nchunks, pq_chunk** out);
+void pq_chunk_free(pq_ctx* ctx, pq_chunk* chunk);
+int64_t pq_chunk_num_rows(const pq_chunk* chunk);
+int64_t pq_chunk_num_pages(const pq_chunk* chunk);       /* data pages */
+int64_t pq_chunk_payload_bytes(const pq_chunk* chunk);   /* Σ data + dictionary payload bytes */
+int pq_chunk_pages(const pq_chunk* chunk, pq_page_desc* pages, int64_t cap, int64_t* npages);
+
+/* ── decode (ColumnReader::read_all on the GPU) ─────────────────────────── */
+/* Decodes every data page of `chunk` into `out` (device memory; buffers are
+ * reused when out->capacity_* suffice, so a caller can loop without
+ * allocation).  Synchronous by default; pq_decode_async leaves the work on
+ * the context stream. */
+int pq_decode(pq_ctx* ctx, pq_chunk* chunk, pq_column* out);
+int pq_decode_async(pq_ctx* ctx, pq_chunk* chunk, pq_column* out);
+int pq_decode_check(pq_ctx* ctx, pq_chunk* chunk); /* sync + error collection after _async */
+int pq_column_copy_out(pq_ctx* ctx, const pq_column* col, uint32_t* validity, uint8_t* values,
+                       int64_t* offsets);
+void pq_column_free(pq_ctx* ctx, pq_column* col);
+
+/* ── regex page filter (README.md:54-64, SURVEY §8a R-REGEX) ───────────── */
+/* page_flags[i] = 1 iff data page i of the chunk is REPORTED: no non-null
+ * value matches (neg = 0) / no non-null value fails to match (neg = 1). */
+int pq_regex_compile_check(const char* pattern, char* err, size_t errlen);
+int pq_regex_pages(pq_ctx* ctx, pq_chunk* chunk, const char* pattern, int neg,
+                   uint8_t* page_flags);
+int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* chunk, const char* pattern, int neg);
+int pq_regex_pages_result(pq_ctx* ctx, pq_chunk* chunk, uint8_t* page_flags);
+
+/* ── kernel timing (HIP events on the context stream) ───────────────────── */
+void pq_timing_enable(pq_ctx* ctx, int enable);
+void pq_timing_reset(pq_ctx* ctx);
+/* total milliseconds and launch count of kernel `name` since the last reset
+ * (names: see DESIGN.md).  Returns 0 if unknown. */
+int pq_timing_get(pq_ctx* ctx, const char* name, double* total_ms, int64_t* launches);
+
+/* ── file-level helpers (ParquetReader::open) ───────────────────────────── */
+typedef struct pq_file pq_file;
+int pq_file_open(const uint8_t* file, size_t file_len, pq_file** out, char* err, size_t errlen);
+void pq_file_close(pq_file* f);
+int64_t pq_file_num_rows(const pq_file* f);
+int pq_file_num_row_groups(const pq_file* f);
+int pq_file_num_columns(const pq_file* f);
+int pq_file_column_name(const pq_file* f, int col, char* buf, size_t buflen);
+int pq_file_find_column(const pq_file* f, const char* name);
+int pq_file_chunk(const pq_file* f, int row_group, int col, pq_chunk_desc* out);
+int64_t pq_file_row_group_rows(const pq_file* f, int row_group);
+/* build_page_index (parquet_reader.cpp:559-605): global data-page ids,
+ * rg-major then column then page order; 4 int64 per page:
+ * data_offset, data_size, row_group_idx, column_idx. */
+int64_t pq_file_num_pages(const pq_file* f);
+int pq_file_page_index(const pq_file* f, int64_t* entries, int64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,68 @@
+"""GPU parity for the --regex-column page filter (SURVEY §8a R-REGEX).
+
+Golden: for every data page (global page order of the column), decode its
+values with the oracle and ask Python `re.search(p, value, re.ASCII)`; the
+page is reported iff no non-null value satisfies the predicate (match, or
+non-match with --neg-regex).  NULLs never satisfy either.
+"""
+import re
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pqgpu import capi, gen
+from util import file_chunks, to_oracle_chunk
+
+pytestmark = pytest.mark.gpu
+
+PATTERNS = ["special.*requests", "^(carefully|quickly) ", "[0-9]", "e", "^$", "s$",
+            "(ironic|bold) (foxes|ideas)", "a.{3}e", "[^a-z ]", r"\bx" if False else "ly\\s",
+            "qu?i(ck|et)ly", "^[a-z]{1,4} "]
+
+
+def golden_pages(f: bytes, chunks, pattern: str, neg: bool) -> np.ndarray:
+    rx = re.compile(pattern, re.ASCII)
+    flags = []
+    for ch in chunks:
+        rc, msg, col = O.read_all(f, to_oracle_chunk(ch))
+        assert rc == 0, msg
+        for (_, ptype, _, first, nrows) in col.pages:
+            if ptype != 0:
+                continue
+            sat = False
+            for r in range(first, first + nrows):
+                if not col.valid[r]:
+                    continue
+                s = bytes(col.data[col.offsets[r]:col.offsets[r + 1]]).decode("utf-8")
+                m = rx.search(s) is not None
+                if m != neg:
+                    sat = True
+                    break
+            flags.append(0 if sat else 1)
+    return np.array(flags, dtype=np.uint8)
+
+
+CASES = [
+    ("c3_ref", gen.c3_cols(), 4000, gen.REF_LAYOUT),
+    ("c3_arrow", gen.c3_cols(), 9000, gen.ARROW_LAYOUT),
+    ("c2_dict", gen.c2_cols(), 20000, gen.REF_LAYOUT),
+    ("c2_dict_arrow", gen.c2_cols(), 20000, gen.ARROW_LAYOUT),
+    ("c3_optional", [gen.Col("c", gen.COMMENT, gen.BYTE_ARRAY, optional=True, null_frac=0.3,
+                             len_min=3, len_max=20)], 5000, gen.REF_LAYOUT),
+]
+
+
+@pytest.mark.parametrize("neg", [False, True], ids=["like", "notlike"])
+@pytest.mark.parametrize("name,cols,n,layout", CASES, ids=[c[0] for c in CASES])
+def test_regex_pages(ctx, name, cols, n, layout, neg):
+    f = gen.build(cols, n, 2, seed=7, layout=layout, rows_per_page=700)
+    chunks = file_chunks(f, 0)
+    dc = ctx.upload(f, chunks)
+    for p in PATTERNS:
+        exp = golden_pages(f, chunks, p, neg)
+        got = dc.regex_pages(p, neg)
+        assert len(got) == len(exp)
+        bad = np.nonzero(got != exp)[0]
+        assert len(bad) == 0, (p, neg, bad[:10])
+    dc.free()
