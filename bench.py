@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded values/s (RLE + dictionary BYTE_ARRAY) and regex pages/s.
+
+Workload (BASELINE.json configs[1] = SURVEY §8d C2): one BYTE_ARRAY UTF8
+OPTIONAL column, 10M rows in one row group, 1000-entry dictionary, runs of
+1+U[0,16) rows, 5% NULL, reference-writer page layout (512 rows/page,
+bit width 10), synthetic data from the deterministic generator.  One step =
+one full ColumnReader::read_all-equivalent decode of the chunk on the GPU
+(validity bitmap + int64 offsets + chars, all kernels), inputs resident in
+HBM.  With --gpus N each rank decodes its own 10M-row row group (C5-style
+page-range sharding, weak scaling, no collective on the data path).
+
+The regex leg (configs[2] = C3) times the --regex-column page filter over a
+10M-row PLAIN UTF-8 column (~293k pages) and reports pages/s.
+
+Rank 0 prints ONE JSON line (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "duckdb-parquet-parser_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+ROWS = 10_000_000
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rows", type=int, default=ROWS)
+    ap.add_argument("--layout", choices=["ref", "arrow"], default="ref")
+    ap.add_argument("--no-regex", action="store_true")
+    ap.add_argument("--regex-rows", type=int, default=ROWS)
+    ap.add_argument("--pattern", default="special.*requests")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    return ap.parse_args()
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
+    summary (profiles/pmc_*.json), corrected per the microarch guide
+    (FETCH_SIZE x2 for wide coalesced reads on gfx950)."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    k = d.get("kernels", {}).get(kernel)
+    return k.get("hbm_bytes_per_launch") if k else None
+
+
+def cpu_baseline(file: bytes, chunk, seconds: float):
+    """The reference's own ColumnReader::read_all (oracle/_ref, compiled from
+    the reference sources) on this host, 1 thread, bounded sample."""
+    from oracle import oracle as O
+    ch = O.Chunk(chunk.num_values, chunk.data_page_offset,
+                 chunk.dictionary_page_offset if chunk.has_dictionary_page_offset else None,
+                 chunk.codec, chunk.type, chunk.max_def_level, chunk.max_rep_level)
+    if O.have_ref():
+        s, nv = O.ref_time_read_all(file, ch, reps=1, threads=1)
+        reps = max(1, int(seconds / max(s, 1e-3)))
+        s, nv = O.ref_time_read_all(file, ch, reps=reps, threads=1)
+        return {"value": nv / s, "unit": "values/s", "cores": 1, "kind": "reference",
+                "sample": f"{reps} x ColumnReader::read_all of a {ch.num_values}-row C2 chunk "
+                          f"(in-memory ReadRangeFunc, -O2), {s:.1f} s"}
+    t0 = time.perf_counter()
+    reps = 0
+    nv = 0
+    while time.perf_counter() - t0 < seconds:
+        rc, msg, col = O.read_all(file, ch)
+        nv += len(col.valid)
+        reps += 1
+    s = time.perf_counter() - t0
+    return {"value": nv / s, "unit": "values/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} x oracle read_all of a {ch.num_values}-row C2 chunk, {s:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from pqgpu import capi, gen
+    from pqgpu.shard import rank_row_groups
+
+    # ── decode leg: each rank its own C2-shaped row group ────────────────
+    layout = gen.REF_LAYOUT if args.layout == "ref" else gen.ARROW_LAYOUT
+    my_rgs = rank_row_groups(world, rank, world)  # one 10M-row row group per rank
+    file = gen.build(gen.c2_cols(), args.rows, len(my_rgs), seed=gen.CONFIG_SEEDS["C2"],
+                     layout=layout, first_rg=my_rgs[0])
+    F = capi.File(file)
+    chunks = [F.chunk(rg, 0) for rg in range(F.num_row_groups)]
+    ctx = capi.Context(local)
+    dc = ctx.upload(file, chunks)
+    dc.decode()  # allocate outputs + error check
+    nrows = dc.num_rows
+    total_chars = dc.out.num_bytes
+    host = dc.to_host()
+    nonnull = int(host.validity.sum())
+    del host
+    for _ in range(args.warmup):
+        dc.decode_async()
+    ctx.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ctx.sync()
+
+    ctx.timing(True)
+    ctx.timing_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dc.decode_async()
+    ctx.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    ctx.timing(False)
+    dc.decode_check()
+    elapsed = t1 - t0
+    kern = {}
+    for name in ("dict_entries", "ba_rows", "scan", "ba_gather"):
+        ms, n = ctx.timing_get(name)
+        if n:
+            kern[name] = ms / n
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        rows_t = torch.tensor([nrows * args.steps], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(rows_t, op=dist.ReduceOp.SUM)
+        total_values = float(rows_t.item())
+    else:
+        total_values = float(nrows * args.steps)
+    value = total_values / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    payload = dc.payload_bytes
+    out_bytes = 8 * (nrows + 1) + total_chars + (nrows + 7) // 8
+    b_alg = payload + out_bytes  # SURVEY §8d C2 algorithmic bytes per decode
+    dom = max(kern, key=kern.get) if kern else "ba_gather"
+    dom_ms = kern.get(dom, ms_per_step)
+    dom_bytes = out_bytes if dom == "ba_gather" else payload
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    step_kernel_ms = sum(kern.values())
+
+    result = {
+        "metric": "decoded values/sec (RLE+dict BYTE_ARRAY) and regex pages/sec at 1/2/4/8 GPUs",
+        "value": value,
+        "unit": "values/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (deterministic splitmix64 generator, SURVEY §8d C2 shape)",
+        "config": {"workload": f"C2: dict BYTE_ARRAY OPTIONAL, {args.rows} rows/GPU, 1 row group/GPU, "
+                               f"{args.layout}-layout, 1000-entry dict, 5% NULL",
+                   "rows_per_gpu": nrows, "pages_per_gpu": dc.num_pages,
+                   "parallelism": f"page-range shards x{world} (no collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(dom),
+                     "kernel": dom, "kernel_ms": dom_ms, "algorithmic_bytes": dom_bytes},
+        "pipeline": {"kernel_ms": kern, "sum_kernel_ms": step_kernel_ms,
+                     "b_alg_bytes": b_alg, "b_alg_GBs_per_step": b_alg / (ms_per_step * 1e-3) / 1e9,
+                     "b_alg_frac_of_peak": b_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "nonnull": nonnull, "chars": total_chars},
+    }
+    dc.free()
+    del file
+
+    # ── regex leg (C3) ─────────────────────────────────────────────────────
+    if not args.no_regex:
+        rfile = gen.build(gen.c3_cols(), args.regex_rows, 1, seed=gen.CONFIG_SEEDS["C3"],
+                          first_rg=my_rgs[0])
+        RF = capi.File(rfile)
+        rdc = ctx.upload(rfile, [RF.chunk(0, 0)])
+        flags = rdc.regex_pages(args.pattern)
+        for _ in range(max(1, args.warmup // 2)):
+            rdc.regex_pages_async(args.pattern)
+        ctx.sync()
+        rsteps = max(3, args.steps // 2)
+        ctx.timing(True)
+        ctx.timing_reset()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(rsteps):
+            rdc.regex_pages_async(args.pattern)
+        ctx.sync()
+        t1 = time.perf_counter()
+        barrier()
+        ctx.timing(False)
+        rdc.regex_pages_result()
+        rel = t1 - t0
+        if dist is not None:
+            t = torch.tensor([rel], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            rel = float(t.item())
+        npages = rdc.num_pages
+        rms, rn = ctx.timing_get("regex_pages")
+        result["regex"] = {"pages_per_s": npages * rsteps * world / rel, "pages_per_gpu": npages,
+                           "ms_per_scan": rel / rsteps * 1e3, "pattern": args.pattern,
+                           "reported_pages": int(flags.sum()),
+                           "kernel_ms": rms / rn if rn else None,
+                           "payload_GBs": rdc.payload_bytes / (rms / rn * 1e-3) / 1e9 if rn else None}
+        rdc.free()
+
+    # ── CPU baseline beside it (rank 0, N=1 only) ──────────────────────────
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sample = gen.build(gen.c2_cols(), 1_000_000, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
+        SF = capi.File(sample)
+        result["cpu_baseline"] = cpu_baseline(sample, SF.chunk(0, 0), args.cpu_seconds)
+        result["cpu_baseline"]["host_cpu"] = _cpu_model()
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

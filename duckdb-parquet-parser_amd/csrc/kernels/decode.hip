@@ -460,7 +460,7 @@ __global__ void __launch_bounds__(256) k_ba_gather(const uint8_t* __restrict__ b
             const uint32_t cnt = static_cast<uint32_t>(ge - gs);
             const uint32_t first = static_cast<uint32_t>(gs - blk);
             for (uint32_t k = 0; k < cnt; k++) {
-                while (p >= L.loff[r + 1] - L.loff[r]) { r++; p = 0; }
+                while (r + 1 < n && p >= L.loff[r + 1] - L.loff[r]) { r++; p = 0; }
                 uint32_t byte = srcbase[L.src[r] + p];
                 p++;
                 uint32_t at = first + k;

@@ -1,0 +1,109 @@
+"""Regenerate the committed golden fixtures (run in the build container only).
+
+The reference ships no tests or fixtures, so the goldens are
+produced by the reference itself: oracle/_ref/libpqref.so, compiled from the
+unmodified reference sources by oracle/Makefile.  For each fixture file this
+writes
+  <name>.parquet          the input (generator or hand-built pages)
+  manifest.json           per column: ColumnReader::read_all result
+                          (rc, message, sha256 + length of the canonical
+                          dump), read_pages page records, the page index
+                          of ParquetReader::open
+  <name>.c<k>.dump        the canonical dump itself when it is small
+Nothing from the reference's source is stored; only inputs and outputs.
+
+    python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (ROOT, os.path.join(ROOT, "duckdb-parquet-parser_amd"), os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+
+from oracle import oracle as O  # noqa: E402
+from pqgpu import gen  # noqa: E402
+
+import pqbuild as B  # noqa: E402
+from test_gpu_decode import CRAFTED, ERRORS  # noqa: E402
+
+DUMP_LIMIT = 64 * 1024
+
+
+def generated():
+    yield "c1_int32_ref", gen.build(gen.c1_cols(), 10000, 1, seed=1)  # BASELINE config #1
+    yield "c2_dict_ref", gen.build(gen.c2_cols(), 20000, 1, seed=2)
+    yield "c2_dict_arrow", gen.build(gen.c2_cols(), 20000, 1, seed=2, layout=gen.ARROW_LAYOUT,
+                                     rows_per_page=5000)
+    yield "c3_plain_ref", gen.build(gen.c3_cols(), 3000, 1, seed=3)
+    yield "c4_mixed_arrow", gen.build(gen.c4_cols(), 2000, 2, seed=4, layout=gen.ARROW_LAYOUT,
+                                      rows_per_page=600)
+    yield "bool_dict_ref", gen.build([gen.Col("b", gen.UNIFORM, gen.BOOLEAN, optional=True,
+                                              null_frac=0.3)], 500, 1, seed=9)
+    yield "float_ref", gen.build([gen.Col("f", gen.DOUBLE_RANGE, gen.FLOAT, optional=True,
+                                          null_frac=0.1)], 800, 1, seed=9)
+    yield "int64_small_dict_arrow", gen.build([gen.Col("i", gen.SMALL_INT, gen.INT64, optional=True,
+                                                       null_frac=0.2, dict_size=7)], 3000, 1, seed=9,
+                                              layout=gen.ARROW_LAYOUT, rows_per_page=1000)
+
+
+def main():
+    if not O.have_ref():
+        sys.exit("oracle/_ref/libpqref.so missing: run `make -C oracle ref` first")
+    manifest = {}
+    items = list(generated())
+    for name, fn in sorted(CRAFTED.items()) + sorted(ERRORS.items()):
+        if name == "zero_count_no_literal":  # the reference dereferences NULL here
+            continue
+        f, ch = fn()
+        items.append(("crafted_" + name, (f, ch)))
+    for name, item in items:
+        path = os.path.join(HERE, name + ".parquet")
+        if isinstance(item, tuple):
+            data, ch = item
+            chunks = [[O.Chunk(ch["num_values"], ch["data_page_offset"], ch["dictionary_page_offset"],
+                               ch["codec"], ch["type"], ch["max_def"], ch["max_rep"])]]
+        else:
+            data = item
+        with open(path, "wb") as fh:
+            fh.write(data)
+        if not isinstance(item, tuple):
+            chunks, _, pidx = O.ref_open(path)
+        else:
+            try:
+                _, _, pidx = O.ref_open(path)
+            except RuntimeError:
+                pidx = None
+        entry = {"columns": [], "page_index": pidx.tolist() if pidx is not None else None}
+        for ci in range(len(chunks[0])):
+            col = []
+            for rg in range(len(chunks)):
+                ch = chunks[rg][ci]
+                rc, msg, dump = O.ref_read_all(data, ch)
+                prc, pmsg, pdump, pages = O.ref_read_pages(data, ch)
+                rec = {"chunk": [ch.num_values, ch.data_page_offset, ch.dictionary_page_offset,
+                                 ch.codec, ch.type, ch.max_def, ch.max_rep],
+                       "rc": rc, "msg": msg}
+                if rc == 0:
+                    rec["sha256"] = hashlib.sha256(dump).hexdigest()
+                    rec["len"] = len(dump)
+                    rec["pages"] = [list(p) for p in pages]
+                    assert pdump == dump
+                    if len(dump) <= DUMP_LIMIT:
+                        dname = f"{name}.rg{rg}.c{ci}.dump"
+                        with open(os.path.join(HERE, dname), "wb") as fh:
+                            fh.write(dump)
+                        rec["dump"] = dname
+                col.append(rec)
+            entry["columns"].append(col)
+        manifest[name] = entry
+    with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+        json.dump(manifest, fh, indent=1, sort_keys=True)
+    print("wrote", len(manifest), "fixtures")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,91 @@
+"""CPU: pin the oracle (and the host format layer) to the reference's outputs.
+
+tests/golden/manifest.json holds what the compiled reference returned for
+every fixture (tests/golden/make_golden.py).  The oracle must reproduce the
+dump bytes, the read_pages page records and the error text; the product's
+host layer must reproduce ParquetReader's page index and chunk metadata.
+"""
+import hashlib
+import json
+import os
+
+import pytest
+
+from oracle import oracle as O
+from pqgpu import capi
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+with open(os.path.join(HERE, "manifest.json")) as fh:
+    MANIFEST = json.load(fh)
+
+
+def _load(name):
+    with open(os.path.join(HERE, name + ".parquet"), "rb") as fh:
+        return fh.read()
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_oracle_matches_reference_outputs(name):
+    data = _load(name)
+    for col in MANIFEST[name]["columns"]:
+        for rec in col:
+            ch = O.Chunk(*rec["chunk"])
+            rc, msg, out = O.read_all(data, ch)
+            if rec["rc"] != 0:
+                assert rc != 0, "reference failed, oracle did not"
+                if rec["msg"].startswith("ByteBuffer") or "FIXED_LEN" in rec["msg"]:
+                    assert msg == rec["msg"]
+                continue
+            assert rc == 0, msg
+            dump = O.dump_column(out)
+            assert len(dump) == rec["len"]
+            assert hashlib.sha256(dump).hexdigest() == rec["sha256"]
+            if "dump" in rec:
+                with open(os.path.join(HERE, rec["dump"]), "rb") as fh:
+                    assert dump == fh.read()
+            got_pages = [[p[0], p[1], p[2], p[4]] for p in out.pages]
+            assert got_pages == rec["pages"]
+
+
+@pytest.mark.parametrize("name", sorted(n for n in MANIFEST if MANIFEST[n]["page_index"] is not None))
+def test_host_page_index_and_metadata(name):
+    data = _load(name)
+    F = capi.File(data)
+    assert F.page_index().tolist() == MANIFEST[name]["page_index"]
+    cols = MANIFEST[name]["columns"]
+    assert F.num_columns == len(cols)
+    for ci, col in enumerate(cols):
+        for rg, rec in enumerate(col):
+            d = F.chunk(rg, ci)
+            dict_off = d.dictionary_page_offset if d.has_dictionary_page_offset else None
+            assert [d.num_values, d.data_page_offset, dict_off, d.codec, d.type, d.max_def_level,
+                    d.max_rep_level] == rec["chunk"]
+
+
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_host_page_walk_matches_read_pages(name):
+    """pq_build_page_table (R-WALK) yields the reference's read_pages records."""
+    data = _load(name)
+    for col in MANIFEST[name]["columns"]:
+        for rec in col:
+            if rec["rc"] != 0:
+                continue
+            ch = O.Chunk(*rec["chunk"])
+            from util import to_desc
+            rc, msg, pages = capi.build_page_table(data, to_desc(ch))
+            assert rc == 0, msg
+            got = [[p.page_num, p.page_type, p.num_values] for p in pages if p.page_type in (0, 2)]
+            assert got == [r[:3] for r in rec["pages"]]
+
+
+@pytest.mark.skipif(not O.have_ref(), reason="reference harness not built")
+@pytest.mark.parametrize("name", sorted(MANIFEST))
+def test_reference_harness_reproduces_manifest(name):
+    """The live reference (oracle/_ref) still gives the recorded outputs."""
+    data = _load(name)
+    for col in MANIFEST[name]["columns"]:
+        for rec in col:
+            rc, msg, dump = O.ref_read_all(data, O.Chunk(*rec["chunk"]))
+            assert (rc, msg) == (rec["rc"], rec["msg"])
+            if rc == 0:
+                assert hashlib.sha256(dump).hexdigest() == rec["sha256"]

@@ -15,6 +15,8 @@ def to_oracle_chunk(d) -> O.Chunk:
 
 
 def to_desc(c) -> capi.ChunkDesc:
+    if isinstance(c, capi.ChunkDesc):
+        return c
     if isinstance(c, dict):
         c = to_oracle_chunk(c)
     d = capi.ChunkDesc()
