@@ -36,6 +36,7 @@ struct pq_ctx {
     std::vector<PendingTimer> pending;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
     std::map<std::string, std::pair<double, int64_t>> timers;
+    bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
 };
 
 struct pq_chunk {
@@ -74,6 +75,17 @@ struct pq_chunk {
     int64_t* d_total = nullptr;
     int64_t* d_scan_scratch = nullptr;
     int64_t char_estimate = 0;
+    // fused BYTE_ARRAY path (dict_fused.hip): one launch per input chunk
+    struct Range {
+        int32_t p0 = 0, np = 0, dict_id = -1;
+        uint32_t rows_cap = 0, stage_bytes = 0, wave_bytes = 0, dict_bytes = 0, dict_chars_bytes = 0;
+        int waves = 0, grid = 0;
+    };
+    std::vector<Range> ranges;
+    bool fused = false;
+    uint64_t* d_status = nullptr;
+    int32_t* d_tickets = nullptr;
+    int64_t* d_bases = nullptr;
     // regex
     uint8_t* d_page_flags = nullptr;
     uint8_t* d_dict_match = nullptr;
@@ -184,7 +196,59 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_scan_scratch);
     dfree(c->d_page_flags);
     dfree(c->d_dict_match);
+    dfree(c->d_status);
+    dfree(c->d_tickets);
+    dfree(c->d_bases);
     if (c->d_prog) { pqre::free_device_program(c->d_prog); c->d_prog = nullptr; }
+}
+
+// Decide whether every chunk of the column can take the fused BYTE_ARRAY
+// path (dict_fused.hip) and size its LDS carve-up; otherwise the generic
+// rows -> scan -> gather path runs.
+void plan_fused(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages,
+                const std::vector<DevDict>& dicts) {
+    c->fused = false;
+    if (!ctx->opt_fused || c->type != PQ_BYTE_ARRAY || c->max_def > 255 || c->max_def < 0 || c->ranges.empty()) return;
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+    const uint32_t kLds = 160 * 1024;
+    for (auto& r : c->ranges) {
+        int32_t dict_id = -1;
+        uint32_t maxn = 0, maxs = 0;
+        for (int p = r.p0; p < r.p0 + r.np; p++) {
+            const DevPage& pg = pages[p];
+            if (pg.mode == pqk::MODE_DICT) {
+                if (dict_id >= 0 && pg.dict != dict_id) return;  // several dictionaries in force
+                dict_id = pg.dict;
+            }
+            maxn = std::max(maxn, static_cast<uint32_t>(std::max(pg.nvals, 0)));
+            maxs = std::max(maxs, static_cast<uint32_t>(std::max(pg.size, 0)));
+        }
+        if (maxn > 4096 || maxs > 16384) return;
+        r.dict_id = dict_id;
+        r.rows_cap = (std::max(maxn, 64u) + 63) / 64 * 64;
+        r.stage_bytes = (maxs + 15) / 16 * 16 + 16;
+        r.wave_bytes = pqk::fused_wave_bytes(r.rows_cap, r.stage_bytes);
+        r.dict_chars_bytes = r.dict_bytes = 0;
+        if (dict_id >= 0) {
+            const DevDict& d = dicts[dict_id];
+            if (d.size > 65536 - 64 || d.nvals < 0 || d.nvals > 65535) return;
+            int64_t ecap = std::min<int64_t>(d.nvals, d.size / 4 + 1);
+            r.dict_chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
+            r.dict_bytes = r.dict_chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
+        }
+        if (r.dict_bytes + r.wave_bytes > kLds) return;
+        int W = static_cast<int>(std::min<uint32_t>(16, (kLds - r.dict_bytes) / r.wave_bytes));
+        if (W >= 2) W &= ~1;
+        r.waves = W;
+        uint32_t lds = r.dict_bytes + static_cast<uint32_t>(W) * r.wave_bytes;
+        int per_cu = pqk::fused_occupancy_waves(lds, W);
+        if (per_cu < 1) per_cu = 1;
+        int need = (r.np + W - 1) / W;
+        r.grid = std::max(1, std::min(per_cu * cus, need));
+    }
+    c->fused = true;
 }
 
 }  // namespace
@@ -216,6 +280,12 @@ void pq_ctx_destroy(pq_ctx* ctx) {
     for (auto& p : ctx->free_events) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
+    if (!ctx || !key) return PQ_ERR_ARG;
+    if (std::strcmp(key, "fused_ba") == 0) { ctx->opt_fused = value != 0; return 0; }
+    return set_err(ctx, PQ_ERR_ARG, std::string("unknown option ") + key);
 }
 
 const char* pq_last_error(const pq_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
@@ -256,32 +326,31 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         c->plain_width = plain_width_of(c->type);
         c->width = c->plain_width;
 
-        // 1) host walks; lay out every chunk's payload span in one image
-        struct Span { int64_t file_lo, file_hi, img; };
-        std::vector<Span> spans;
+        // 1) host walks; every payload gets a 16-byte aligned slot in one image
         std::vector<DevPage> hpages;
         std::vector<DevDict> hdicts;
-        std::vector<int64_t> dict_walk_to_dev;
+        std::vector<std::pair<int64_t, int64_t>> copies;  // (file offset, image offset) per payload
+        std::vector<int32_t> copy_size;
         int64_t seq = 0, row_base = 0, img = 0;
+        auto slot = [&](int64_t file_off, int32_t size) {
+            int64_t at = img;
+            copies.push_back({file_off, at});
+            copy_size.push_back(size);
+            img += (static_cast<int64_t>(size) + 15) / 16 * 16 + 16;
+            return at;
+        };
         for (int k = 0; k < nchunks; k++) {
             pqfmt::WalkResult w = pqfmt::walk_chunk(file, file_len, chunks[k]);
-            int64_t lo = INT64_MAX, hi = 0;
-            for (const auto& p : w.pages) {
-                if (p.page_type != PQ_DATA_PAGE && p.page_type != PQ_DICTIONARY_PAGE) continue;
-                lo = std::min(lo, p.payload_offset);
-                hi = std::max(hi, p.payload_offset + static_cast<int64_t>(p.payload_size));
-            }
-            if (lo == INT64_MAX) { lo = 0; hi = 0; }
-            Span sp{lo, hi, img};
-            spans.push_back(sp);
             int64_t base_walk = static_cast<int64_t>(c->walked.size());
             std::vector<int32_t> dict_of_walk(w.pages.size(), -1);
+            pq_chunk::Range rg;
+            rg.p0 = static_cast<int32_t>(hpages.size());
             for (size_t i = 0; i < w.pages.size(); i++) {
                 pq_page_desc p = w.pages[i];
-                int64_t s = seq + static_cast<int64_t>(i);
+                int64_t sq = seq + static_cast<int64_t>(i);
                 if (p.page_type == PQ_DICTIONARY_PAGE) {
                     DevDict d{};
-                    d.off = static_cast<uint64_t>(img + (p.payload_offset - lo));
+                    d.off = static_cast<uint64_t>(slot(p.payload_offset, p.payload_size));
                     d.size = p.payload_size;
                     d.nvals = p.num_values;
                     d.entry_base = static_cast<int32_t>(c->nentries);
@@ -291,11 +360,11 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
                     c->nentries += std::max<int64_t>(cap, 0);
                     dict_of_walk[i] = static_cast<int32_t>(hdicts.size());
                     hdicts.push_back(d);
-                    c->dict_seq.push_back(s);
+                    c->dict_seq.push_back(sq);
                     c->payload_bytes += p.payload_size;
                 } else if (p.page_type == PQ_DATA_PAGE) {
                     DevPage d{};
-                    d.off = static_cast<uint64_t>(img + (p.payload_offset - lo));
+                    d.off = static_cast<uint64_t>(slot(p.payload_offset, p.payload_size));
                     d.size = p.payload_size;
                     d.nvals = p.num_values;
                     d.first_row = row_base + p.first_row;
@@ -305,18 +374,19 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
                              : (c->type == PQ_BOOLEAN ? pqk::MODE_BOOL : pqk::MODE_PLAIN);
                     d.dict = d.mode == pqk::MODE_DICT ? dict_dev : -1;
                     hpages.push_back(d);
-                    c->page_seq.push_back(s);
+                    c->page_seq.push_back(sq);
                     c->data_walk_idx.push_back(base_walk + static_cast<int64_t>(i));
                     c->payload_bytes += p.payload_size;
                 }
                 p.first_row += row_base;
                 c->walked.push_back(p);
             }
+            rg.np = static_cast<int32_t>(hpages.size()) - rg.p0;
+            c->ranges.push_back(rg);
             int64_t rows = 0;
             for (const auto& p : w.pages)
                 if (p.page_type == PQ_DATA_PAGE) rows += p.num_values;
             row_base += rows;
-            img += (hi - lo + 15) / 16 * 16;
             seq += static_cast<int64_t>(w.pages.size());
             if (w.error) {  // later chunks are never reached by the reference
                 c->walk_error = w.error;
@@ -327,6 +397,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         }
         c->nrows = row_base;
         c->nbytes = static_cast<size_t>(img) + 64;
+        plan_fused(ctx, c.get(), hpages, hdicts);
         c->npages = static_cast<int>(hpages.size());
         c->ndicts = static_cast<int>(hdicts.size());
 
@@ -357,16 +428,21 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         rc |= dalloc(&c->d_tile_base, htiles.size());
         rc |= dalloc(&c->d_total, 1);
         rc |= dalloc(&c->d_scan_scratch, htiles.size() / 8192 + 16);
-        if (c->type == PQ_BYTE_ARRAY) rc |= dalloc(&c->d_row_codes, static_cast<size_t>(c->nrows));
+        if (c->type == PQ_BYTE_ARRAY && !c->fused) rc |= dalloc(&c->d_row_codes, static_cast<size_t>(c->nrows));
+        if (c->fused) {
+            rc |= dalloc(&c->d_status, hpages.size());
+            rc |= dalloc(&c->d_tickets, c->ranges.size());
+            rc |= dalloc(&c->d_bases, c->ranges.size() + 1);
+        }
         if (rc) {
             free_chunk_device(c.get());
             return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (chunk upload)");
         }
         std::vector<uint8_t> image(c->nbytes, 0);
-        for (const auto& sp : spans) {
-            if (sp.file_hi <= sp.file_lo) continue;
-            int64_t lo = sp.file_lo, hi = std::min<int64_t>(sp.file_hi, static_cast<int64_t>(file_len));
-            if (hi > lo) std::memcpy(image.data() + sp.img, file + lo, static_cast<size_t>(hi - lo));
+        for (size_t i = 0; i < copies.size(); i++) {  // zero padding past EOF
+            int64_t lo = copies[i].first, n = copy_size[i];
+            int64_t hi = std::min<int64_t>(lo + n, static_cast<int64_t>(file_len));
+            if (hi > lo) std::memcpy(image.data() + copies[i].second, file + lo, static_cast<size_t>(hi - lo));
         }
         hipStream_t s = ctx->stream;
         rc = hip_check(ctx, hipMemcpyAsync(c->d_bytes, image.data(), c->nbytes, hipMemcpyHostToDevice, s), "upload");
@@ -471,12 +547,43 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
     (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), s);
     (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
-    if (c->ndicts) {
+    if (c->ndicts && c->type == PQ_BYTE_ARRAY) {
+        Timed t(ctx, "dict_index");
+        pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
+                               c->d_dict_err, c->d_flags);
+    } else if (c->ndicts) {
         Timed t(ctx, "dict_entries");
         pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
                                  c->d_dict_err, c->d_flags, c->type, c->plain_width);
     }
-    if (c->type == PQ_BYTE_ARRAY) {
+    if (c->fused) {
+        const size_t nr = c->ranges.size();
+        (void)hipMemsetAsync(c->d_status, 0, std::max<size_t>(c->npages, 1) * sizeof(uint64_t), s);
+        (void)hipMemsetAsync(c->d_tickets, 0, nr * sizeof(int32_t), s);
+        (void)hipMemsetAsync(c->d_bases, 0, (nr + 1) * sizeof(int64_t), s);
+        for (size_t k = 0; k < nr; k++) {
+            const auto& r = c->ranges[k];
+            if (r.np == 0) {
+                (void)hipMemcpyAsync(c->d_bases + k + 1, c->d_bases + k, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+                continue;
+            }
+            pqk::FusedLaunch L{};
+            L.bytes = c->d_bytes; L.pages = c->d_pages; L.p0 = r.p0; L.np = r.np;
+            L.dicts = c->d_dicts; L.dict_id = r.dict_id; L.entries = c->d_entries;
+            L.dict_count = c->d_dict_count; L.max_def = c->max_def; L.max_rep = c->max_rep;
+            L.rows_cap = r.rows_cap; L.stage_bytes = r.stage_bytes; L.wave_bytes = r.wave_bytes;
+            L.dict_bytes = r.dict_bytes; L.dict_chars_bytes = r.dict_chars_bytes;
+            L.status = c->d_status + r.p0; L.ticket = c->d_tickets + k;
+            L.base_in = c->d_bases + k; L.base_out = c->d_bases + k + 1; L.nrows_total = c->nrows;
+            L.validity = out->d_validity; L.offsets = out->d_offsets; L.chars = out->d_values;
+            L.capacity = out->capacity_bytes; L.overflow = c->d_flags + 1;
+            L.page_err = c->d_page_err; L.err_any = c->d_flags; L.grid = r.grid; L.waves_per_block = r.waves;
+            Timed t(ctx, "ba_fused");
+            pqk::launch_ba_fused(s, L);
+        }
+        (void)hipMemcpyAsync(c->d_total, c->d_bases + nr, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+        (void)hipMemcpyAsync(out->d_offsets + c->nrows, c->d_bases + nr, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+    } else if (c->type == PQ_BYTE_ARRAY) {
         {
             Timed t(ctx, "ba_rows");
             pqk::launch_ba_rows(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_entries,
@@ -535,14 +642,18 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         int64_t total = 0;
         (void)hipMemcpy(&total, c->d_total, sizeof total, hipMemcpyDeviceToHost);
         out->num_bytes = total;
-        if (flags[1]) {  // chars overflowed the estimate: grow and gather again
+        if (flags[1]) {  // chars overflowed the estimate: grow and run again
             dfree(out->d_values);
             if (dalloc(&out->d_values, static_cast<size_t>(total + 64)))
                 return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (chars)");
             out->capacity_bytes = total;
-            (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), ctx->stream);
-            (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, ctx->stream);
-            launch_gather(ctx, c, out);
+            if (c->fused) {
+                if (int rc = pq_decode_async(ctx, c, out)) return rc;
+            } else {
+                (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), ctx->stream);
+                (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, ctx->stream);
+                launch_gather(ctx, c, out);
+            }
             return hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync");
         }
     } else if (out) {
@@ -634,10 +745,9 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
         (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), s);
         if (c->ndicts) {
             {
-                Timed t(ctx, "dict_entries");
-                pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
-                                         c->d_dict_count, c->d_dict_err, c->d_flags, c->type,
-                                         c->plain_width);
+                Timed t(ctx, "dict_index");
+                pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
+                                       c->d_dict_count, c->d_dict_err, c->d_flags);
             }
             Timed t(ctx, "regex_dict");
             pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,

@@ -65,20 +65,6 @@ __device__ int page_prologue(const Src& s, const ColumnParams& cp, PagePrologue&
     return 0;
 }
 
-// Inclusive wave prefix sum of a u32.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, kWave);
-        if (lane() >= static_cast<uint32_t>(d)) v += t;
-    }
-    return v;
-}
-__device__ __forceinline__ uint32_t bcast_last(uint32_t v) { return __shfl(v, kWave - 1, kWave); }
-__device__ __forceinline__ uint32_t popc_below(uint64_t m) {
-    return __popcll(m & ((1ull << lane()) - 1ull));
-}
-
 // ── dictionary pages (column_reader.cpp:128-138) ───────────────────────────
 // BYTE_ARRAY entries are a serial u32-length chain: one wave per dictionary
 // page walks it in LDS; entries[] = (len << 32) | chars offset in the page.

@@ -81,4 +81,37 @@ void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int
                   const DevDict* dicts, const int32_t* dict_count, ColumnParams cp,
                   uint32_t* validity, uint8_t* values, DevErr* page_err, int32_t* err_any);
 
+// ── fused BYTE_ARRAY path (dict_fused.hip) ─────────────────────────────────
+struct FusedLaunch {
+    const uint8_t* bytes;
+    const DevPage* pages;
+    int32_t p0, np;
+    const DevDict* dicts;
+    int32_t dict_id;
+    const uint64_t* entries;
+    const int32_t* dict_count;
+    int32_t max_def, max_rep;
+    uint32_t rows_cap, stage_bytes, wave_bytes, dict_bytes, dict_chars_bytes;
+    uint64_t* status;
+    int32_t* ticket;
+    const int64_t* base_in;
+    int64_t* base_out;
+    int64_t nrows_total;
+    uint32_t* validity;
+    int64_t* offsets;
+    uint8_t* chars;
+    int64_t capacity;
+    int32_t* overflow;
+    DevErr* page_err;
+    int32_t* err_any;
+    int grid;
+    int waves_per_block;
+};
+
+void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
+                       uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any);
+void launch_ba_fused(hipStream_t s, const FusedLaunch& L);
+uint32_t fused_wave_bytes(uint32_t rows_cap, uint32_t stage_bytes);
+int fused_occupancy_waves(uint32_t lds_bytes_per_block, int waves_per_block);
+
 }  // namespace pqk

@@ -84,6 +84,7 @@ def lib():
             "pq_last_error": ([vp], C.c_char_p),
             "pq_ctx_stream": ([vp], vp),
             "pq_ctx_sync": ([vp], C.c_int),
+            "pq_ctx_set_option": ([vp, C.c_char_p, C.c_int64], C.c_int),
             "pq_build_page_table": ([u8p, C.c_size_t, C.POINTER(ChunkDesc), C.POINTER(PageDesc),
                                      C.c_int64, C.POINTER(C.c_int64), C.c_char_p, C.c_size_t], C.c_int),
             "pq_chunk_upload": ([vp, u8p, C.c_size_t, C.POINTER(ChunkDesc), C.c_int,
@@ -228,6 +229,9 @@ class Context:
 
     def __del__(self):
         self.close()
+
+    def set_option(self, key: str, value: int):
+        self.check(lib().pq_ctx_set_option(self.h, key.encode(), int(value)))
 
     def error(self) -> str:
         return lib().pq_last_error(self.h).decode(errors="replace")

@@ -106,6 +106,10 @@ void pq_ctx_destroy(pq_ctx* ctx);
 const char* pq_last_error(const pq_ctx* ctx);
 void* pq_ctx_stream(pq_ctx* ctx);              /* the hipStream_t kernels run on */
 int pq_ctx_sync(pq_ctx* ctx);
+/* Tuning switches: "fused_ba" (default 1) = fused BYTE_ARRAY decode kernel
+ * when every chunk qualifies; 0 forces the generic rows/scan/gather kernels.
+ * Applies to chunks uploaded afterwards. */
+int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value);
 
 /* ── host page walk (R-WALK / R-HDR) ────────────────────────────────────── */
 /* Walks one chunk exactly like ColumnReader::read_all (256-byte header window,

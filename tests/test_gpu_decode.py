@@ -35,9 +35,17 @@ SMALL = [
 ]
 
 
+@pytest.fixture(params=[1, 0], ids=["fused", "generic"])
+def path(request, ctx):
+    """Both BYTE_ARRAY kernel paths: fused (dict_fused.hip) and generic."""
+    ctx.set_option("fused_ba", request.param)
+    yield request.param
+    ctx.set_option("fused_ba", 1)
+
+
 @pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT], ids=["ref", "arrow"])
 @pytest.mark.parametrize("name,cols,n", SMALL, ids=[s[0] for s in SMALL])
-def test_generated_columns(ctx, name, cols, n, layout):
+def test_generated_columns(ctx, path, name, cols, n, layout):
     f = gen.build(cols, n, 2, seed=11, layout=layout, rows_per_page=3000)
     for ci in range(len(cols)):
         chunks = file_chunks(f, ci)
@@ -141,7 +149,7 @@ ERRORS = {
 
 
 @pytest.mark.parametrize("case", sorted(CRAFTED), ids=sorted(CRAFTED))
-def test_crafted_pages(ctx, case):
+def test_crafted_pages(ctx, path, case):
     f, chunk = CRAFTED[case]()
     rc_o, msg_o, d_o = oracle_read_column(f, [chunk])
     assert rc_o == 0, msg_o
@@ -151,7 +159,7 @@ def test_crafted_pages(ctx, case):
 
 
 @pytest.mark.parametrize("case", sorted(ERRORS), ids=sorted(ERRORS))
-def test_error_pages(ctx, case):
+def test_error_pages(ctx, path, case):
     f, chunk = ERRORS[case]()
     rc_o, msg_o, _ = oracle_read_column(f, [chunk])
     assert rc_o != 0
