@@ -824,6 +824,18 @@ int pq_file_find_column(const pq_file* f, const char* name) {  // last match win
         if (f->cols[i].name == name) found = static_cast<int>(i);
     return found;
 }
+int pq_file_column_info(const pq_file* f, int col, int32_t* type, int16_t* max_def,
+                        int16_t* max_rep, int32_t* repetition, int32_t* converted_type) {
+    if (!f || col < 0 || col >= static_cast<int>(f->cols.size())) return PQ_ERR_ARG;
+    const auto& c = f->cols[col];
+    if (type) *type = c.type;
+    if (max_def) *max_def = c.max_def;
+    if (max_rep) *max_rep = c.max_rep;
+    if (repetition) *repetition = c.repetition.value_or(-1);
+    if (converted_type) *converted_type = c.converted_type.value_or(-1);
+    return 0;
+}
+
 int pq_file_chunk(const pq_file* f, int rg, int col, pq_chunk_desc* out) {
     if (!f || !out || rg < 0 || rg >= static_cast<int>(f->meta.row_groups.size()) || col < 0 ||
         col >= static_cast<int>(f->cols.size()))

@@ -1,0 +1,443 @@
+// reader.cpp — the C++ reader API (include/pqgpu/reader.hpp) over the C ABI.
+#include "pqgpu/reader.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+
+#include "host/format.hpp"
+#include "pq_gpu.h"
+
+namespace pqgpu {
+
+namespace {
+
+[[noreturn]] void raise(int code, const std::string& msg) {
+    if (code == PQ_ERR_OPTIONAL) throw std::bad_optional_access();
+    throw std::runtime_error(msg);
+}
+
+const char* type_name(ParquetType t) {  // common.hpp:205-217
+    switch (t) {
+        case ParquetType::BOOLEAN: return "BOOLEAN";
+        case ParquetType::INT32: return "INT32";
+        case ParquetType::INT64: return "INT64";
+        case ParquetType::INT96: return "INT96";
+        case ParquetType::FLOAT: return "FLOAT";
+        case ParquetType::DOUBLE: return "DOUBLE";
+        case ParquetType::BYTE_ARRAY: return "BYTE_ARRAY";
+        case ParquetType::FIXED_LEN_BYTE_ARRAY: return "FIXED_LEN_BYTE_ARRAY";
+        default: return "UNKNOWN";
+    }
+}
+
+// Decode `descs` (chunks of one column) on `dev`; returns host arrays and
+// optionally the walked page list.
+HostColumn decode_chunks(Device& dev, const uint8_t* file, size_t len, const std::vector<pq_chunk_desc>& descs,
+                         std::vector<pq_page_desc>* walked) {
+    pq_ctx* ctx = dev.ctx();
+    pq_chunk* ch = nullptr;
+    int rc = pq_chunk_upload(ctx, file, len, descs.data(), static_cast<int>(descs.size()), &ch);
+    if (rc) raise(rc, pq_last_error(ctx));
+    pq_column out{};
+    rc = pq_decode(ctx, ch, &out);
+    if (rc) {
+        std::string msg = pq_last_error(ctx);
+        pq_column_free(ctx, &out);
+        pq_chunk_free(ctx, ch);
+        raise(rc, msg);
+    }
+    HostColumn h;
+    h.type = static_cast<ParquetType>(out.type);
+    h.num_rows = out.num_rows;
+    h.validity.assign(static_cast<size_t>((out.num_rows + 31) / 32) + 1, 0);
+    h.values.assign(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)), 0);
+    if (out.type == PQ_BYTE_ARRAY) h.offsets.assign(static_cast<size_t>(out.num_rows + 1), 0);
+    rc = pq_column_copy_out(ctx, &out, h.validity.data(), h.values.data(),
+                            h.offsets.empty() ? nullptr : h.offsets.data());
+    h.values.resize(static_cast<size_t>(out.num_bytes));
+    if (walked) {
+        int64_t n = 0;
+        pq_chunk_pages(ch, nullptr, 0, &n);
+        walked->resize(static_cast<size_t>(n));
+        pq_chunk_pages(ch, walked->data(), n, &n);
+    }
+    pq_column_free(ctx, &out);
+    pq_chunk_free(ctx, ch);
+    if (rc) raise(rc, "device copy failed");
+    return h;
+}
+
+}  // namespace
+
+std::string Value::to_string() const {  // common.hpp:189-200
+    if (is_null) return "NULL";
+    return std::visit(
+        [](auto&& a) -> std::string {
+            using T = std::decay_t<decltype(a)>;
+            if constexpr (std::is_same_v<T, bool>) return a ? "true" : "false";
+            else if constexpr (std::is_same_v<T, std::string>) return a;
+            else return std::to_string(a);
+        },
+        data);
+}
+
+Value HostColumn::value(int64_t i) const {
+    if (!valid(i)) return Value::null();
+    switch (type) {
+        case ParquetType::BOOLEAN: return Value::from_bool(values[i] != 0);
+        case ParquetType::INT32: { int32_t v; std::memcpy(&v, &values[4 * i], 4); return Value::from_i32(v); }
+        case ParquetType::INT64: { int64_t v; std::memcpy(&v, &values[8 * i], 8); return Value::from_i64(v); }
+        case ParquetType::FLOAT: { float v; std::memcpy(&v, &values[4 * i], 4); return Value::from_float(v); }
+        case ParquetType::DOUBLE: { double v; std::memcpy(&v, &values[8 * i], 8); return Value::from_double(v); }
+        case ParquetType::INT96: {  // column_reader.cpp:257-264
+            int64_t lo;
+            int32_t hi;
+            std::memcpy(&lo, &values[12 * i], 8);
+            std::memcpy(&hi, &values[12 * i + 8], 4);
+            return Value::from_string("INT96(" + std::to_string(hi) + ":" + std::to_string(lo) + ")");
+        }
+        case ParquetType::BYTE_ARRAY:
+            return Value::from_string(std::string(reinterpret_cast<const char*>(values.data()) + offsets[i],
+                                                  static_cast<size_t>(offsets[i + 1] - offsets[i])));
+        default: return Value::null();
+    }
+}
+
+// ── Device ─────────────────────────────────────────────────────────────────
+Device::Device(int device) : ctx_(pq_ctx_create(device)) {
+    if (!ctx_) throw std::runtime_error("pqgpu: no HIP device " + std::to_string(device));
+}
+Device::~Device() { pq_ctx_destroy(ctx_); }
+Device& Device::default_device() {
+    static Device d(0);
+    return d;
+}
+
+// ── ColumnReader ───────────────────────────────────────────────────────────
+ColumnReader::ColumnReader(ReadRangeFunc read_range, const ColumnChunk& chunk, ParquetType type,
+                           int16_t max_def_level, int16_t max_rep_level, Device& dev)
+    : read_range_(std::move(read_range)), type_(type), max_def_level_(max_def_level),
+      max_rep_level_(max_rep_level), dev_(dev) {
+    if (!chunk.meta_data) throw std::runtime_error("ColumnChunk has no metadata");  // column_reader.cpp:9-11
+    meta_ = &*chunk.meta_data;
+    if (meta_->codec != CompressionCodec::UNCOMPRESSED)
+        throw std::runtime_error("Only uncompressed parquet files are supported");
+}
+
+HostColumn ColumnReader::read_columnar() {
+    // Fetch exactly the bytes the reference's walk touches (256-byte header
+    // windows + payloads) through the caller's ReadRangeFunc, then hand one
+    // contiguous image to the GPU path.
+    int64_t start = meta_->data_page_offset;
+    if (meta_->dictionary_page_offset) start = std::min(start, *meta_->dictionary_page_offset);
+    size_t cur = static_cast<size_t>(start), end = cur;
+    int64_t values_read = 0;
+    while (values_read < meta_->num_values) {
+        std::vector<uint8_t> hdr = read_range_(cur, 256);
+        hdr.resize(256, 0);
+        pqfmt::PageHeader h;
+        try {
+            h = pqfmt::read_page_header(hdr.data(), hdr.size(), 0);
+        } catch (const pqfmt::Error&) {
+            end = std::max(end, cur + 256);
+            break;  // the GPU-side walk reports it at the same place
+        }
+        end = std::max(end, cur + 256);
+        cur += h.header_size;
+        if (h.compressed < 0) break;
+        end = std::max(end, cur + static_cast<size_t>(h.compressed));
+        if (h.type == 0 && h.has_data) values_read += h.data_num_values;
+        else if (h.type == 0 || (h.type == 2 && !h.has_dict)) break;
+        cur += static_cast<size_t>(h.compressed);
+    }
+    std::vector<uint8_t> image = read_range_(static_cast<size_t>(start), end - static_cast<size_t>(start));
+    pq_chunk_desc d{};
+    d.num_values = meta_->num_values;
+    d.data_page_offset = meta_->data_page_offset - start;
+    d.has_dictionary_page_offset = meta_->dictionary_page_offset.has_value();
+    d.dictionary_page_offset = meta_->dictionary_page_offset.value_or(start) - start;
+    d.codec = static_cast<int32_t>(meta_->codec);
+    d.type = static_cast<int32_t>(type_);
+    d.max_def_level = max_def_level_;
+    d.max_rep_level = max_rep_level_;
+    return decode_chunks(dev_, image.data(), image.size(), {d}, nullptr);
+}
+
+std::vector<Value> ColumnReader::read_all() {
+    HostColumn h = read_columnar();
+    std::vector<Value> out;
+    out.reserve(static_cast<size_t>(h.num_rows));
+    for (int64_t i = 0; i < h.num_rows; i++) out.push_back(h.value(i));
+    return out;
+}
+
+std::vector<PageResult> ColumnReader::read_pages() {
+    int64_t start = meta_->data_page_offset;
+    if (meta_->dictionary_page_offset) start = std::min(start, *meta_->dictionary_page_offset);
+    HostColumn h = read_columnar();
+    // re-walk on the host for the page records (same walk as the device upload)
+    std::vector<uint8_t> img;
+    std::vector<PageResult> pages;
+    size_t cur = static_cast<size_t>(start);
+    int64_t values_read = 0, row = 0;
+    int page_num = 0;
+    while (values_read < meta_->num_values) {
+        std::vector<uint8_t> hdr = read_range_(cur, 256);
+        hdr.resize(256, 0);
+        pqfmt::PageHeader ph = pqfmt::read_page_header(hdr.data(), hdr.size(), 0);
+        cur += ph.header_size;
+        if (ph.type == 2) {
+            pages.push_back({page_num++, PageType::DICTIONARY_PAGE, ph.dict_num_values, {}});
+        } else if (ph.type == 0) {
+            PageResult pr{page_num++, PageType::DATA_PAGE, ph.data_num_values, {}};
+            for (int32_t k = 0; k < ph.data_num_values; k++) pr.values.push_back(h.value(row + k));
+            row += ph.data_num_values;
+            values_read += ph.data_num_values;
+            pages.push_back(std::move(pr));
+        } else {
+            page_num++;
+        }
+        cur += static_cast<size_t>(ph.compressed);
+    }
+    return pages;
+}
+
+// ── PageIterator / StringColumnIterator ────────────────────────────────────
+PageIterator::PageIterator(ParquetReader& r, size_t s, size_t e) : reader_(r), start_(s), end_(e), current_(s) {}
+bool PageIterator::has_next() const { return current_ < end_; }
+RawPage PageIterator::next() {  // parquet_reader.cpp:247-259
+    if (!has_next()) throw std::runtime_error("PageIterator: no more pages");
+    const auto& e = reader_.page_index_entry(current_);
+    RawPage p{current_, e.row_group_idx, e.column_idx, reader_.read_page_data(current_)};
+    current_++;
+    return p;
+}
+void PageIterator::reset() { current_ = start_; }
+
+StringColumnIterator::StringColumnIterator(HostColumn col) : col_(std::move(col)) { skip_nulls(); }
+void StringColumnIterator::skip_nulls() {
+    while (row_ < col_.num_rows && !col_.valid(row_)) row_++;
+}
+bool StringColumnIterator::has_next() const { return row_ < col_.num_rows; }
+std::tuple<size_t, size_t, const char*> StringColumnIterator::next() {
+    if (!has_next()) throw std::runtime_error("StringColumnIterator: no more strings");
+    int64_t i = row_++;
+    skip_nulls();
+    return {static_cast<size_t>(i), static_cast<size_t>(col_.offsets[i + 1] - col_.offsets[i]),
+            reinterpret_cast<const char*>(col_.values.data()) + col_.offsets[i]};
+}
+
+// ── ParquetReader ──────────────────────────────────────────────────────────
+ParquetReader::ParquetReader(Device& dev) : dev_(dev) {}
+ParquetReader::~ParquetReader() { pq_file_close(file_); }
+
+bool ParquetReader::open(const std::string& filename) {  // parquet_reader.cpp:14-61
+    std::ifstream f(filename, std::ios::binary | std::ios::ate);
+    if (!f.is_open()) {
+        std::cerr << "Error: cannot open file " << filename << std::endl;
+        return false;
+    }
+    std::vector<uint8_t> bytes(static_cast<size_t>(f.tellg()));
+    f.seekg(0);
+    f.read(reinterpret_cast<char*>(bytes.data()), static_cast<std::streamsize>(bytes.size()));
+    return open_buffer(std::move(bytes));
+}
+
+bool ParquetReader::open_buffer(std::vector<uint8_t> bytes) {
+    data_ = std::move(bytes);
+    char err[512] = {0};
+    pq_file_close(file_);
+    file_ = nullptr;
+    int rc = pq_file_open(data_.data(), data_.size(), &file_, err, sizeof err);
+    if (rc == PQ_ERR_ARG) {
+        std::cerr << "Error: " << err << std::endl;
+        return false;
+    }
+    if (rc) raise(rc, err);
+    columns_.clear();
+    for (int c = 0; c < pq_file_num_columns(file_); c++) {
+        char name[1024];
+        pq_file_column_name(file_, c, name, sizeof name);
+        int32_t type, rep, conv;
+        int16_t md, mr;
+        pq_file_column_info(file_, c, &type, &md, &mr, &rep, &conv);
+        ColumnInfo ci{name, static_cast<ParquetType>(type), c, md, mr, std::nullopt, std::nullopt};
+        if (rep >= 0) ci.repetition = static_cast<FieldRepetitionType>(rep);
+        if (conv >= 0) ci.converted_type = conv;
+        columns_.push_back(ci);
+    }
+    int64_t np = pq_file_num_pages(file_);
+    std::vector<int64_t> e(static_cast<size_t>(4 * np));
+    pq_file_page_index(file_, e.data(), np);
+    page_index_.clear();
+    for (int64_t i = 0; i < np; i++)
+        page_index_.push_back({static_cast<size_t>(e[4 * i]), static_cast<size_t>(e[4 * i + 1]),
+                               static_cast<size_t>(e[4 * i + 2]), static_cast<size_t>(e[4 * i + 3])});
+    return true;
+}
+
+size_t ParquetReader::num_columns() const { return columns_.size(); }
+int64_t ParquetReader::num_rows() const { return pq_file_num_rows(file_); }
+size_t ParquetReader::num_row_groups() const { return static_cast<size_t>(pq_file_num_row_groups(file_)); }
+std::vector<std::string> ParquetReader::column_names() const {
+    std::vector<std::string> n;
+    for (const auto& c : columns_) n.push_back(c.name);
+    return n;
+}
+const ColumnInfo& ParquetReader::column(size_t i) const {
+    if (i >= columns_.size()) throw std::runtime_error("Column index " + std::to_string(i) + " out of range");
+    return columns_[i];
+}
+const ColumnInfo& ParquetReader::column(const std::string& name) const {
+    int i = find_column(name);
+    if (i < 0) throw std::runtime_error("Column not found: " + name);
+    return columns_[static_cast<size_t>(i)];
+}
+int ParquetReader::find_column(const std::string& name) const { return pq_file_find_column(file_, name.c_str()); }
+
+std::string ParquetReader::schema_string() const {  // parquet_reader.cpp:99-121
+    std::ostringstream ss;
+    ss << "Schema:\n";
+    for (size_t i = 0; i < columns_.size(); i++) {
+        const auto& c = columns_[i];
+        ss << "  " << i << ": " << c.name << " (" << type_name(c.type);
+        if (c.repetition) {
+            switch (*c.repetition) {
+                case FieldRepetitionType::REQUIRED: ss << ", REQUIRED"; break;
+                case FieldRepetitionType::OPTIONAL: ss << ", OPTIONAL"; break;
+                case FieldRepetitionType::REPEATED: ss << ", REPEATED"; break;
+            }
+        }
+        ss << ")\n";
+    }
+    ss << "Rows: " << num_rows() << "\n";
+    ss << "Row groups: " << num_row_groups() << "\n";
+    return ss.str();
+}
+
+HostColumn ParquetReader::decode_column(int col_idx, int rg_first, int rg_count) {
+    std::vector<pq_chunk_desc> descs;
+    for (int rg = rg_first; rg < rg_first + rg_count; rg++) {
+        pq_chunk_desc d{};
+        int rc = pq_file_chunk(file_, rg, col_idx, &d);
+        if (rc) raise(rc == PQ_ERR_OPTIONAL ? 0 : rc, "ColumnChunk has no metadata");
+        if (d.codec != 0) throw std::runtime_error("Only uncompressed parquet files are supported");
+        descs.push_back(d);
+    }
+    return decode_chunks(dev_, data_.data(), data_.size(), descs, nullptr);
+}
+
+std::vector<Value> ParquetReader::read_column_by_idx(int rg, int col) {  // parquet_reader.cpp:146-165
+    if (rg < 0 || rg >= static_cast<int>(num_row_groups())) throw std::runtime_error("Invalid row group index");
+    if (col < 0 || col >= static_cast<int>(columns_.size())) throw std::runtime_error("Invalid column index");
+    HostColumn h = decode_column(col, rg, 1);
+    std::vector<Value> v;
+    v.reserve(static_cast<size_t>(h.num_rows));
+    for (int64_t i = 0; i < h.num_rows; i++) v.push_back(h.value(i));
+    return v;
+}
+std::vector<Value> ParquetReader::read_column(const std::string& name, size_t rg) {
+    int c = find_column(name);
+    if (c < 0) throw std::runtime_error("Column not found: " + name);
+    return read_column_by_idx(static_cast<int>(rg), c);
+}
+HostColumn ParquetReader::read_column_columnar(const std::string& name) {
+    int c = find_column(name);
+    if (c < 0) throw std::runtime_error("Column not found: " + name);
+    return decode_column(c, 0, static_cast<int>(num_row_groups()));
+}
+std::vector<Value> ParquetReader::read_column(const std::string& name) {  // parquet_reader.cpp:125-144
+    HostColumn h = read_column_columnar(name);
+    std::vector<Value> v;
+    v.reserve(static_cast<size_t>(h.num_rows));
+    for (int64_t i = 0; i < h.num_rows; i++) v.push_back(h.value(i));
+    return v;
+}
+
+StringColumnIterator ParquetReader::column_iterator(const std::string& name) {  // parquet_reader.cpp:282-295
+    int c = find_column(name);
+    if (c < 0) throw std::runtime_error("Column not found: " + name);
+    if (columns_[c].type != ParquetType::BYTE_ARRAY)
+        throw std::runtime_error("Column '" + name + "' is not BYTE_ARRAY (type: " + type_name(columns_[c].type) + ")");
+    return StringColumnIterator(decode_column(c, 0, static_cast<int>(num_row_groups())));
+}
+
+size_t ParquetReader::num_pages() const { return page_index_.size(); }
+std::vector<uint8_t> ParquetReader::read_range(size_t off, size_t len) {
+    std::vector<uint8_t> b(len, 0);
+    if (off < data_.size()) std::memcpy(b.data(), data_.data() + off, std::min(len, data_.size() - off));
+    return b;
+}
+const PageIndexEntry& ParquetReader::page_index_entry(size_t id) const {
+    if (id >= page_index_.size()) throw std::runtime_error("Global page ID " + std::to_string(id) + " out of range");
+    return page_index_[id];
+}
+std::vector<uint8_t> ParquetReader::read_page_data(size_t id) const {
+    const auto& e = page_index_entry(id);
+    return const_cast<ParquetReader*>(this)->read_range(e.data_offset, e.data_size);
+}
+std::vector<uint8_t> ParquetReader::read_pages_chunk(size_t s, size_t e, size_t max_bytes) const {  // 194-231
+    if (s >= page_index_.size()) throw std::runtime_error("Start page ID " + std::to_string(s) + " out of range");
+    if (e >= page_index_.size()) throw std::runtime_error("End page ID " + std::to_string(e) + " out of range");
+    if (s > e) throw std::runtime_error("Start page ID must be <= end page ID");
+    std::vector<uint8_t> out;
+    for (size_t i = s; i <= e; i++) {
+        size_t rem = max_bytes - out.size();
+        if (rem == 0) break;
+        const auto& en = page_index_[i];
+        auto d = const_cast<ParquetReader*>(this)->read_range(en.data_offset, std::min(en.data_size, rem));
+        out.insert(out.end(), d.begin(), d.end());
+    }
+    return out;
+}
+PageIterator ParquetReader::page_iterator() { return PageIterator(*this, 0, page_index_.size()); }
+PageIterator ParquetReader::page_iterator(size_t s, size_t e) {  // 261-278
+    if (s > page_index_.size()) throw std::runtime_error("start_page_id out of range");
+    if (e > page_index_.size()) throw std::runtime_error("end_page_id out of range");
+    if (s > e) throw std::runtime_error("start_page_id must be <= end_page_id");
+    return PageIterator(*this, s, e);
+}
+
+std::vector<size_t> ParquetReader::regex_pages(const std::string& name, const std::string& pattern, bool neg) {
+    int c = find_column(name);
+    if (c < 0) throw std::runtime_error("Column not found: " + name);
+    std::vector<pq_chunk_desc> descs;
+    for (int rg = 0; rg < static_cast<int>(num_row_groups()); rg++) {
+        pq_chunk_desc d{};
+        if (int rc = pq_file_chunk(file_, rg, c, &d)) raise(rc, "ColumnChunk has no metadata");
+        descs.push_back(d);
+    }
+    pq_ctx* ctx = dev_.ctx();
+    pq_chunk* ch = nullptr;
+    if (int rc = pq_chunk_upload(ctx, data_.data(), data_.size(), descs.data(), static_cast<int>(descs.size()), &ch))
+        raise(rc, pq_last_error(ctx));
+    std::vector<uint8_t> flags(static_cast<size_t>(std::max<int64_t>(pq_chunk_num_pages(ch), 1)));
+    int rc = pq_regex_pages(ctx, ch, pattern.c_str(), neg ? 1 : 0, flags.data());
+    std::string msg = rc ? pq_last_error(ctx) : "";
+    int64_t nw = 0;
+    pq_chunk_pages(ch, nullptr, 0, &nw);
+    std::vector<pq_page_desc> walked(static_cast<size_t>(nw));
+    pq_chunk_pages(ch, walked.data(), nw, &nw);
+    pq_chunk_free(ctx, ch);
+    if (rc) raise(rc, msg);
+    // device data page k <-> the k-th DATA_PAGE of the walk <-> its global id
+    std::vector<size_t> out;
+    size_t k = 0, gid = 0;
+    const int chunk_col = columns_[c].column_index;
+    std::vector<size_t> ids;
+    for (size_t i = 0; i < page_index_.size(); i++)
+        if (static_cast<int>(page_index_[i].column_idx) == chunk_col) ids.push_back(i);
+    for (const auto& p : walked) {
+        if (p.page_type != PQ_DATA_PAGE) continue;
+        while (gid < ids.size() && page_index_[ids[gid]].data_offset != static_cast<size_t>(p.payload_offset)) gid++;
+        if (gid < ids.size() && flags[k]) out.push_back(ids[gid]);
+        k++;
+        gid++;
+    }
+    return out;
+}
+
+}  // namespace pqgpu

@@ -57,12 +57,13 @@ __device__ __forceinline__ void win_slide(Win& w) {
     w.n3 = wload(w.src, w.nwords, i + 192);
 }
 
-// Make dwords [d, d + 4] addressable (d uniform, absolute dword index).
+// Make dwords [d, d + 4] addressable (d uniform, absolute dword index):
+// afterwards wbase <= d < wbase + 256, so d + 4 < wbase + 512.
 __device__ __forceinline__ void win_ensure(Win& w, uint32_t d) {
-    if (d < w.wbase || d + 4 >= w.wbase + 512) {
+    if (d < w.wbase || d >= w.wbase + 512) {
         win_fill(w, d);
-    } else {
-        while (d + 4 >= w.wbase + 256) win_slide(w);
+    } else if (d >= w.wbase + 256) {
+        win_slide(w);
     }
 }
 

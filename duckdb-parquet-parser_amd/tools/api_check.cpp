@@ -1,0 +1,94 @@
+// api_check — drives the C++ reader API (include/pqgpu/reader.hpp) exactly
+// as a user of the reference would, and writes canonical dumps (SURVEY §8:
+// u8 is_null + value bytes, strings as u32 length + bytes) for the tests.
+//
+//   api_check <file> read_column <name>            ParquetReader::read_column
+//   api_check <file> column_reader <rg> <col>      ColumnReader(read_range,...).read_all
+//   api_check <file> read_pages <rg> <col>         ColumnReader::read_pages (page records on stderr)
+//   api_check <file> iterator <name>               StringColumnIterator (pos, len, bytes)
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "pq_gpu.h"
+#include "pqgpu/reader.hpp"
+
+static void dump(const pqgpu::Value& v, std::vector<uint8_t>& out) {
+    out.push_back(v.is_null ? 1 : 0);
+    if (v.is_null) return;
+    std::visit([&](auto&& a) {
+        using T = std::decay_t<decltype(a)>;
+        if constexpr (std::is_same_v<T, std::string>) {
+            uint32_t n = static_cast<uint32_t>(a.size());
+            out.insert(out.end(), reinterpret_cast<uint8_t*>(&n), reinterpret_cast<uint8_t*>(&n) + 4);
+            out.insert(out.end(), a.begin(), a.end());
+        } else if constexpr (std::is_same_v<T, bool>) {
+            out.push_back(a ? 1 : 0);
+        } else {
+            const uint8_t* p = reinterpret_cast<const uint8_t*>(&a);
+            out.insert(out.end(), p, p + sizeof(T));
+        }
+    }, v.data);
+}
+
+int main(int argc, char** argv) {
+    if (argc < 4) return 2;
+    try {
+        pqgpu::ParquetReader r;
+        if (!r.open(argv[1])) return 1;
+        std::string mode = argv[2];
+        std::vector<uint8_t> out;
+        if (mode == "read_column") {
+            for (const auto& v : r.read_column(argv[3])) dump(v, out);
+        } else if (mode == "iterator") {
+            auto it = r.column_iterator(argv[3]);
+            while (it.has_next()) {
+                auto [pos, len, ptr] = it.next();
+                uint64_t p = pos;
+                uint32_t l = static_cast<uint32_t>(len);
+                out.insert(out.end(), reinterpret_cast<uint8_t*>(&p), reinterpret_cast<uint8_t*>(&p) + 8);
+                out.insert(out.end(), reinterpret_cast<uint8_t*>(&l), reinterpret_cast<uint8_t*>(&l) + 4);
+                out.insert(out.end(), ptr, ptr + len);
+            }
+        } else {
+            int rg = std::atoi(argv[3]), col = std::atoi(argv[4]);
+            const auto& ci = r.column(static_cast<size_t>(col));
+            pqgpu::ColumnChunk cc;
+            // metadata through the public file helpers of the C ABI is what
+            // ParquetReader uses; rebuild a ColumnChunk the way a caller would
+            pqgpu::ColumnMetaData md;
+            std::vector<uint8_t> all = r.read_range(0, r.file_size());
+            pq_file* f = nullptr;
+            pq_file_open(all.data(), all.size(), &f, nullptr, 0);
+            pq_chunk_desc d{};
+            pq_file_chunk(f, rg, col, &d);
+            pq_file_close(f);
+            md.type = static_cast<pqgpu::ParquetType>(d.type);
+            md.num_values = d.num_values;
+            md.data_page_offset = d.data_page_offset;
+            if (d.has_dictionary_page_offset) md.dictionary_page_offset = d.dictionary_page_offset;
+            cc.meta_data = md;
+            pqgpu::ColumnReader cr([&](size_t off, size_t len) { return r.read_range(off, len); }, cc,
+                                   ci.type, ci.max_def_level, ci.max_rep_level);
+            if (mode == "column_reader") {
+                for (const auto& v : cr.read_all()) dump(v, out);
+            } else {
+                for (const auto& pr : cr.read_pages()) {
+                    std::fprintf(stderr, "%d %d %d %zu\n", pr.page_num, static_cast<int>(pr.type),
+                                 pr.num_values, pr.values.size());
+                    for (const auto& v : pr.values) dump(v, out);
+                }
+            }
+        }
+        std::fwrite(out.data(), 1, out.size(), stdout);
+        return 0;
+    } catch (const std::bad_optional_access& e) {
+        std::cerr << "bad optional access\n";
+        return 3;
+    } catch (const std::exception& e) {
+        std::cerr << e.what() << "\n";
+        return 1;
+    }
+}

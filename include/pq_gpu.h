@@ -170,6 +170,10 @@ int pq_file_num_row_groups(const pq_file* f);
 int pq_file_num_columns(const pq_file* f);
 int pq_file_column_name(const pq_file* f, int col, char* buf, size_t buflen);
 int pq_file_find_column(const pq_file* f, const char* name);
+/* ColumnInfo (column_info.hpp:6-20): physical type, max levels, repetition
+ * and converted type (-1 when the schema element has none). */
+int pq_file_column_info(const pq_file* f, int col, int32_t* type, int16_t* max_def,
+                        int16_t* max_rep, int32_t* repetition, int32_t* converted_type);
 int pq_file_chunk(const pq_file* f, int row_group, int col, pq_chunk_desc* out);
 int64_t pq_file_row_group_rows(const pq_file* f, int row_group);
 /* build_page_index (parquet_reader.cpp:559-605): global data-page ids,
