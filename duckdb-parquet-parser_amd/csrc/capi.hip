@@ -37,6 +37,8 @@ struct pq_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
     std::map<std::string, std::pair<double, int64_t>> timers;
     bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
+    int opt_debug = 0;      // "fused_debug": ablation switches for timing studies
+    int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
 };
 
 struct pq_chunk {
@@ -241,6 +243,7 @@ void plan_fused(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages,
         if (r.dict_bytes + r.wave_bytes > kLds) return;
         int W = static_cast<int>(std::min<uint32_t>(16, (kLds - r.dict_bytes) / r.wave_bytes));
         if (W >= 2) W &= ~1;
+        if (ctx->opt_waves > 0) W = std::min(W, ctx->opt_waves);
         r.waves = W;
         uint32_t lds = r.dict_bytes + static_cast<uint32_t>(W) * r.wave_bytes;
         int per_cu = pqk::fused_occupancy_waves(lds, W);
@@ -285,6 +288,8 @@ void pq_ctx_destroy(pq_ctx* ctx) {
 int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (!ctx || !key) return PQ_ERR_ARG;
     if (std::strcmp(key, "fused_ba") == 0) { ctx->opt_fused = value != 0; return 0; }
+    if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
+    if (std::strcmp(key, "fused_waves") == 0) { ctx->opt_waves = static_cast<int>(value); return 0; }
     return set_err(ctx, PQ_ERR_ARG, std::string("unknown option ") + key);
 }
 
@@ -578,6 +583,7 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             L.validity = out->d_validity; L.offsets = out->d_offsets; L.chars = out->d_values;
             L.capacity = out->capacity_bytes; L.overflow = c->d_flags + 1;
             L.page_err = c->d_page_err; L.err_any = c->d_flags; L.grid = r.grid; L.waves_per_block = r.waves;
+            L.debug = ctx->opt_debug;
             Timed t(ctx, "ba_fused");
             pqk::launch_ba_fused(s, L);
         }

@@ -33,20 +33,33 @@ constexpr uint64_t kValMask = (1ull << 62) - 1;
 constexpr uint32_t kGatherWin = 512;  // 16-byte blocks per gather window
 
 // ── dictionary entry table ─────────────────────────────────────────────────
+// The serial walk keeps its results in LDS and flushes them once: a global
+// store inside the loop would make every later window read wait for the
+// store to retire (loads and stores share vmcnt).
+constexpr int kDictBatch = 4096;  // entries buffered in LDS between flushes
+
 __global__ void __launch_bounds__(64) k_dict_index(const uint8_t* __restrict__ bytes,
                                                    const DevDict* __restrict__ dicts,
                                                    uint64_t* __restrict__ entries,
                                                    int32_t* __restrict__ dict_count,
                                                    DevErr* __restrict__ dict_err,
                                                    int32_t* __restrict__ err_any) {
+    __shared__ uint64_t buf[kDictBatch];
     const DevDict d = dicts[blockIdx.x];
     const uint32_t size = static_cast<uint32_t>(d.size);
     DevErr* err = dict_err + blockIdx.x;
     Win w;
     win_init(w, reinterpret_cast<const uint32_t*>(bytes + d.off), (size + 3) / 4);
     uint32_t pos = 0;
-    int32_t k = 0;
+    int32_t k = 0, flushed = 0;
     const int32_t n = d.nvals;
+    auto flush = [&]() {
+        __builtin_amdgcn_wave_barrier();
+        for (int32_t i = flushed + static_cast<int32_t>(lane()); i < k; i += kWave)
+            entries[d.entry_base + i] = buf[i - flushed];
+        __builtin_amdgcn_wave_barrier();
+        flushed = k;
+    };
     for (; k < n; k++) {
         if (pos + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); break; }
         uint32_t len = uni(win_u32(w, pos));
@@ -55,9 +68,11 @@ __global__ void __launch_bounds__(64) k_dict_index(const uint8_t* __restrict__ b
             set_err(err, err_any, PQ_ERR_BUFFER, pos, len, size);
             break;
         }
-        if (lane() == 0) entries[d.entry_base + k] = (static_cast<uint64_t>(len) << 32) | pos;
+        if (lane() == 0) buf[k - flushed] = (static_cast<uint64_t>(len) << 32) | pos;
         pos += len;
+        if (k + 1 - flushed == kDictBatch) { k++; flush(); k--; }
     }
+    flush();
     if (lane() == 0) dict_count[blockIdx.x] = k;
 }
 
@@ -153,6 +168,7 @@ struct FusedArgs {
     int32_t* overflow;
     DevErr* page_err;
     int32_t* err_any;
+    int32_t debug;               // ablation switches (timing only; output invalid)
 };
 
 struct WaveMem {
@@ -403,15 +419,17 @@ __global__ void __launch_bounds__(1024) k_ba_fused(FusedArgs a) {
         }
         __builtin_amdgcn_wave_barrier();
         // 4. page start in the output
-        const int64_t G0 = *a.base_in + static_cast<int64_t>(look_back(a.status, t, total));
+        const int64_t G0 = (a.debug & 1) ? static_cast<int64_t>(t) * 24 * n
+                                         : *a.base_in + static_cast<int64_t>(look_back(a.status, t, total));
         if (t == a.np - 1 && lane() == 0) {
             *a.base_out = G0 + static_cast<int64_t>(total);
             if (pg.first_row + n == a.nrows_total) a.offsets[a.nrows_total] = G0 + total;
         }
         if (code) continue;
         // 5a. offsets
-        for (uint32_t j = lane(); j < n; j += kWave) a.offsets[pg.first_row + j] = G0 + M.off[j];
-        if (total == 0) continue;
+        if (!(a.debug & 4))
+            for (uint32_t j = lane(); j < n; j += kWave) a.offsets[pg.first_row + j] = G0 + M.off[j];
+        if (total == 0 || (a.debug & 2)) continue;
         const int64_t G1 = G0 + static_cast<int64_t>(total);
         if (G1 > a.capacity) {
             if (lane() == 0) atomicOr(a.overflow, 1);
@@ -504,7 +522,7 @@ void launch_ba_fused(hipStream_t s, const FusedLaunch& L) {
     a.dict_chars_bytes = L.dict_chars_bytes; a.status = L.status; a.ticket = L.ticket;
     a.base_in = L.base_in; a.base_out = L.base_out; a.nrows_total = L.nrows_total;
     a.validity = L.validity; a.offsets = L.offsets; a.chars = L.chars; a.capacity = L.capacity;
-    a.overflow = L.overflow; a.page_err = L.page_err; a.err_any = L.err_any;
+    a.overflow = L.overflow; a.page_err = L.page_err; a.err_any = L.err_any; a.debug = L.debug;
     const uint32_t lds = L.dict_bytes + L.waves_per_block * L.wave_bytes;
     static bool attr = false;
     if (!attr) {

@@ -106,6 +106,7 @@ struct FusedLaunch {
     int32_t* err_any;
     int grid;
     int waves_per_block;
+    int debug;
 };
 
 void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
