@@ -39,6 +39,7 @@ struct pq_ctx {
     bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
     int opt_debug = 0;      // "fused_debug": ablation switches for timing studies
     int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
+    uint64_t* d_prof = nullptr;  // "fused_prof": per-phase cycle sums of k_ba_fused
 };
 
 struct pq_chunk {
@@ -67,6 +68,7 @@ struct pq_chunk {
     int32_t* d_page_tile0 = nullptr;
     uint64_t* d_entries = nullptr;
     int64_t nentries = 0;
+    uint32_t max_dict_bytes = 0;        // largest dictionary payload
     int32_t* d_dict_count = nullptr;
     DevErr* d_page_err = nullptr;
     DevErr* d_dict_err = nullptr;
@@ -241,14 +243,15 @@ void plan_fused(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages,
             r.dict_bytes = r.dict_chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
         }
         if (r.dict_bytes + r.wave_bytes > kLds) return;
-        int W = static_cast<int>(std::min<uint32_t>(16, (kLds - r.dict_bytes) / r.wave_bytes));
-        if (W >= 2) W &= ~1;
-        if (ctx->opt_waves > 0) W = std::min(W, ctx->opt_waves);
+        // producer/writer pairs per workgroup (dict_fused.hip)
+        int pairs = static_cast<int>(std::min<uint32_t>(8, (kLds - r.dict_bytes) / r.wave_bytes));
+        if (ctx->opt_waves > 0) pairs = std::max(1, std::min(pairs, ctx->opt_waves / 2));
+        const int W = 2 * pairs;
         r.waves = W;
-        uint32_t lds = r.dict_bytes + static_cast<uint32_t>(W) * r.wave_bytes;
+        uint32_t lds = r.dict_bytes + static_cast<uint32_t>(pairs) * r.wave_bytes;
         int per_cu = pqk::fused_occupancy_waves(lds, W);
         if (per_cu < 1) per_cu = 1;
-        int need = (r.np + W - 1) / W;
+        int need = (r.np + pairs - 1) / pairs;
         r.grid = std::max(1, std::min(per_cu * cus, need));
     }
     c->fused = true;
@@ -281,6 +284,7 @@ void pq_ctx_destroy(pq_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& p : ctx->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto& p : ctx->free_events) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+    if (ctx->d_prof) (void)hipFree(ctx->d_prof);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -290,6 +294,17 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "fused_ba") == 0) { ctx->opt_fused = value != 0; return 0; }
     if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "fused_waves") == 0) { ctx->opt_waves = static_cast<int>(value); return 0; }
+    if (std::strcmp(key, "fused_prof") == 0) {
+        if (value && !ctx->d_prof) {
+            if (hipMalloc(reinterpret_cast<void**>(&ctx->d_prof), 64 * sizeof(uint64_t)) != hipSuccess)
+                return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (prof)");
+            (void)hipMemset(ctx->d_prof, 0, 64 * sizeof(uint64_t));
+        } else if (!value && ctx->d_prof) {
+            (void)hipFree(ctx->d_prof);
+            ctx->d_prof = nullptr;
+        }
+        return 0;
+    }
     return set_err(ctx, PQ_ERR_ARG, std::string("unknown option ") + key);
 }
 
@@ -359,6 +374,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
                     d.size = p.payload_size;
                     d.nvals = p.num_values;
                     d.entry_base = static_cast<int32_t>(c->nentries);
+                    c->max_dict_bytes = std::max<uint32_t>(c->max_dict_bytes, static_cast<uint32_t>(std::max(p.payload_size, 0)));
                     int64_t cap = c->type == PQ_BYTE_ARRAY
                                       ? std::min<int64_t>(p.num_values, p.payload_size / 4 + 1)
                                       : 0;
@@ -555,7 +571,7 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (c->ndicts && c->type == PQ_BYTE_ARRAY) {
         Timed t(ctx, "dict_index");
         pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
-                               c->d_dict_err, c->d_flags);
+                               c->d_dict_err, c->d_flags, c->max_dict_bytes);
     } else if (c->ndicts) {
         Timed t(ctx, "dict_entries");
         pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
@@ -584,6 +600,7 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             L.capacity = out->capacity_bytes; L.overflow = c->d_flags + 1;
             L.page_err = c->d_page_err; L.err_any = c->d_flags; L.grid = r.grid; L.waves_per_block = r.waves;
             L.debug = ctx->opt_debug;
+            L.prof = ctx->d_prof;
             Timed t(ctx, "ba_fused");
             pqk::launch_ba_fused(s, L);
         }
@@ -715,6 +732,17 @@ int pq_timing_get(pq_ctx* ctx, const char* name, double* total_ms, int64_t* laun
     return 1;
 }
 
+int pq_fused_prof_read(pq_ctx* ctx, uint64_t* out, int n) {
+    if (!ctx || !ctx->d_prof) return 0;
+    const int k = pqk::fused_prof_slots();
+    std::vector<uint64_t> h(static_cast<size_t>(k));
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
+    if (hipMemcpy(h.data(), ctx->d_prof, k * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    (void)hipMemset(ctx->d_prof, 0, k * sizeof(uint64_t));
+    for (int i = 0; i < std::min(n, k); i++) out[i] = h[static_cast<size_t>(i)];
+    return k;
+}
+
 // ── regex page filter ───────────────────────────────────────────────────────
 int pq_regex_compile_check(const char* pattern, char* err, size_t errlen) {
     std::string msg;
@@ -753,7 +781,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             {
                 Timed t(ctx, "dict_index");
                 pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
-                                       c->d_dict_count, c->d_dict_err, c->d_flags);
+                                       c->d_dict_count, c->d_dict_err, c->d_flags, c->max_dict_bytes);
             }
             Timed t(ctx, "regex_dict");
             pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,

@@ -47,6 +47,23 @@ __device__ __forceinline__ uint32_t src_bits(const Src& s, uint64_t b, uint32_t 
     return bw >= 32 ? x : (x & ((1u << bw) - 1u));
 }
 
+// LDS-only readers (no generic-pointer branch, so they always lower to DS ops).
+// `words` holds `size` bytes of a page; bytes past `size` read as zero.
+__device__ __forceinline__ uint32_t lds_word(const uint32_t* words, uint32_t size, uint64_t wi) {
+    uint64_t b = wi * 4;
+    if (b >= size) return 0u;
+    uint32_t w = words[wi];
+    uint64_t rem = size - b;
+    if (rem < 4) w &= (1u << (8 * rem)) - 1u;
+    return w;
+}
+__device__ __forceinline__ uint32_t lds_bits(const uint32_t* words, uint32_t size, uint64_t b, uint32_t bw) {
+    uint64_t wi = b >> 5;
+    uint64_t v = (static_cast<uint64_t>(lds_word(words, size, wi + 1)) << 32) | lds_word(words, size, wi);
+    uint32_t x = static_cast<uint32_t>(v >> (b & 31));
+    return bw >= 32 ? x : (x & ((1u << bw) - 1u));
+}
+
 // Stage a page's payload into this wave's LDS words (zero-filled tail word).
 __device__ inline void stage_page(uint32_t* lds, const uint8_t* g, uint32_t size) {
     uint32_t nw = (size + 3) / 4;

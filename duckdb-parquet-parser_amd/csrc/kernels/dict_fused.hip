@@ -1,15 +1,24 @@
 // dict_fused.hip — fast path for BYTE_ARRAY column chunks (SURVEY §8a
-// R-DICT-EXPAND / R-PLAIN / R-LEVELS / R-RLE) on gfx950.
+// R-DICT-PAGE / R-DICT-EXPAND / R-PLAIN / R-LEVELS / R-RLE) on gfx950.
 //
 // k_dict_index   dictionary page -> entry table (column_reader.cpp:128-138,
-//                249-253): one wavefront walks the u32 length chain with a
-//                register window (window.hpp), ~1 readlane chain per entry.
+//                249-253).  The u32 length chain is serial, so one workgroup
+//                walks it speculatively: the page sits in LDS, each of 16
+//                waves owns a 1/16 slice and each of its lanes walks the chain
+//                from one of the slice's first 64 byte offsets.  One thread
+//                then links the slices (the true chain enters slice w at the
+//                exit of slice w-1: pick that lane's result), and the chosen
+//                lanes re-walk to write (len << 32 | pos) per entry.  Slices
+//                whose entry point is not covered (an entry longer than 64
+//                bytes, a malformed chain) fall back to a serial walk, which
+//                also produces the exact reference error text.
 // k_ba_fused     one launch per column chunk; persistent workgroups, one page
 //                per wavefront at a time (ticket queue, pages in file order):
-//                  1 page payload -> LDS (16-byte loads)
-//                  2 def-level and index streams decoded (rle_decoder.hpp
-//                    state machine; run headers via register window, runs
-//                    expanded 64 values per step)
+//                  1 page payload -> LDS (16-byte loads, issued first and
+//                    landed after the level walk)
+//                  2 def-level and index streams: run headers on the scalar
+//                    unit (stream.hpp, SMEM), RLE runs expanded at once,
+//                    bit-packed runs expanded lane-parallel from LDS
 //                  3 per-row (source, length) + page-local prefix sum
 //                  4 decoupled look-back over page totals -> the page's
 //                    first output byte (no separate scan pass)
@@ -19,7 +28,8 @@
 // The chunk's dictionary sits in LDS once per workgroup.
 #include "kernels/device_common.hpp"
 #include "kernels/kernels.hpp"
-#include "kernels/window.hpp"
+#include "kernels/hybrid.hpp"
+#include "kernels/stream.hpp"
 #include "pq_gpu.h"
 
 namespace pqk {
@@ -31,117 +41,142 @@ constexpr uint64_t kAgg = 1ull << 62;
 constexpr uint64_t kInc = 2ull << 62;
 constexpr uint64_t kValMask = (1ull << 62) - 1;
 constexpr uint32_t kGatherWin = 512;  // 16-byte blocks per gather window
+constexpr uint32_t kLitCap = 16;      // recorded bit-packed runs per wave between expansions (serial walk)
 
 // ── dictionary entry table ─────────────────────────────────────────────────
-// The serial walk keeps its results in LDS and flushes them once: a global
-// store inside the loop would make every later window read wait for the
-// store to retire (loads and stores share vmcnt).
-constexpr int kDictBatch = 4096;  // entries buffered in LDS between flushes
+constexpr int kDictWaves = 16;
+constexpr uint32_t kBad = 0xFFFFFFFFu;
 
-__global__ void __launch_bounds__(64) k_dict_index(const uint8_t* __restrict__ bytes,
-                                                   const DevDict* __restrict__ dicts,
-                                                   uint64_t* __restrict__ entries,
-                                                   int32_t* __restrict__ dict_count,
-                                                   DevErr* __restrict__ dict_err,
-                                                   int32_t* __restrict__ err_any) {
-    __shared__ uint64_t buf[kDictBatch];
-    const DevDict d = dicts[blockIdx.x];
-    const uint32_t size = static_cast<uint32_t>(d.size);
-    DevErr* err = dict_err + blockIdx.x;
-    Win w;
-    win_init(w, reinterpret_cast<const uint32_t*>(bytes + d.off), (size + 3) / 4);
-    uint32_t pos = 0;
-    int32_t k = 0, flushed = 0;
-    const int32_t n = d.nvals;
-    auto flush = [&]() {
-        __builtin_amdgcn_wave_barrier();
-        for (int32_t i = flushed + static_cast<int32_t>(lane()); i < k; i += kWave)
-            entries[d.entry_base + i] = buf[i - flushed];
-        __builtin_amdgcn_wave_barrier();
-        flushed = k;
-    };
-    for (; k < n; k++) {
-        if (pos + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); break; }
-        uint32_t len = uni(win_u32(w, pos));
-        pos += 4;
-        if (static_cast<uint64_t>(pos) + len > size) {
-            set_err(err, err_any, PQ_ERR_BUFFER, pos, len, size);
-            break;
-        }
-        if (lane() == 0) buf[k - flushed] = (static_cast<uint64_t>(len) << 32) | pos;
-        pos += len;
-        if (k + 1 - flushed == kDictBatch) { k++; flush(); k--; }
-    }
-    flush();
-    if (lane() == 0) dict_count[blockIdx.x] = k;
+// Unaligned dword at LDS byte address a.
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t* words, uint32_t a) {
+    uint32_t w0 = words[a >> 2], w1 = words[(a >> 2) + 1];
+    return __builtin_amdgcn_alignbyte(w1, w0, a & 3);
+}
+__device__ __forceinline__ uint32_t lds_u8(const uint32_t* words, uint32_t a) {
+    return (words[a >> 2] >> (8 * (a & 3))) & 0xFFu;
 }
 
-// ── hybrid stream decode: headers from the register window, literals from LDS
-template <class F>
-__device__ int rlew_decode(Rle& r, Win& w, const Src& s, uint32_t n, F&& out) {
-    uint32_t done = 0;
-    while (done < n) {
-        if (r.repeat == 0 && r.literal == 0) {
-            if (r.pos >= r.size) {  // exhausted: zero-fill (rle_decoder.hpp:20-23)
-                for (uint32_t j = done + lane(); j < n; j += kWave) out(j, 0u);
-                return 0;
-            }
-            // varint header (76-86), bounded by the stream size
-            uint32_t ind = 0, shift = 0;
-            for (;;) {
-                uint64_t x = win_u64(w, r.base + r.pos);
-                uint32_t avail = min(8u, r.size - r.pos);
-                uint32_t i = 0;
-                bool end = false;
-                for (; i < avail; i++) {
-                    uint32_t b = static_cast<uint32_t>(x >> (8 * i)) & 0xFFu;
-                    if (shift < 32) ind |= (b & 0x7Fu) << shift;
-                    if (!(b & 0x80u)) { end = true; i++; break; }
-                    shift += 7;
-                }
-                r.pos += i;
-                if (end || r.pos >= r.size) break;
-            }
-            ind = uni(ind);
-            if (ind & 1u) {
-                r.literal = (ind >> 1) * 8u;
-                r.lit_start = r.pos;
-                r.lit_valid = 1;
-                r.lit_bit = 0;
-            } else {
-                r.repeat = ind >> 1;
-                uint32_t nb = min((r.bw + 7) / 8, r.size - r.pos);
-                uint64_t x = win_u64(w, r.base + r.pos);
-                uint32_t keep = min(nb, 4u);
-                r.value = uni(keep == 0 ? 0u : keep >= 4 ? static_cast<uint32_t>(x)
-                                                         : static_cast<uint32_t>(x) & ((1u << (8 * keep)) - 1u));
-                r.pos += nb;
-            }
+__device__ __forceinline__ uint64_t entry_code(uint32_t len, uint32_t pos) {
+    return (static_cast<uint64_t>(len) << 32) | pos;
+}
+
+__global__ void __launch_bounds__(kDictWaves * 64) k_dict_index(const uint8_t* __restrict__ bytes,
+                                                                const DevDict* __restrict__ dicts,
+                                                                uint64_t* __restrict__ entries,
+                                                                int32_t* __restrict__ dict_count,
+                                                                DevErr* __restrict__ dict_err,
+                                                                int32_t* __restrict__ err_any,
+                                                                uint32_t lds_cap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t words[];
+    __shared__ uint32_t ex[kDictWaves * kWave];  // chain exit per candidate (kBad: overran the page)
+    __shared__ uint32_t ec[kDictWaves * kWave];  // entries walked per candidate
+    __shared__ int32_t seg_lane[kDictWaves];
+    __shared__ uint32_t seg_base[kDictWaves], seg_n[kDictWaves];
+
+    const DevDict d = dicts[blockIdx.x];
+    const uint32_t size = static_cast<uint32_t>(max(d.size, 0));
+    const uint32_t n = static_cast<uint32_t>(max(d.nvals, 0));
+    DevErr* err = dict_err + blockIdx.x;
+    uint64_t* out = entries + d.entry_base;
+    const uint8_t* page = bytes + d.off;
+
+    if (size + 32 > lds_cap) {  // too large for LDS: serial scalar walk by wave 0
+        if (threadIdx.x >= kWave) return;
+        uint32_t pos = 0, k = 0;
+        for (; k < n; k++) {
+            if (static_cast<uint64_t>(pos) + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); break; }
+            uint32_t len = suni(sload_u32(page, pos));
+            pos += 4;
+            if (static_cast<uint64_t>(pos) + len > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, len, size); break; }
+            if (lane() == 0) out[k] = entry_code(len, pos);
+            pos += len;
         }
-        if (r.bw > 64) return PQ_ERR_UNSUPPORTED;
-        if (r.repeat > 0) {
-            uint32_t k = min(r.repeat, n - done);
-            for (uint32_t j = lane(); j < k; j += kWave) out(done + j, r.value);
-            r.repeat -= k;
-            done += k;
-        } else {
-            if (r.bw > 0 && !r.lit_valid) return PQ_ERR_UNSUPPORTED;
-            bool wrapped = r.literal == 0;
-            uint32_t k = wrapped ? n - done : min(r.literal, n - done);
-            uint64_t bit0 = static_cast<uint64_t>(r.base + r.lit_start) * 8u + r.lit_bit;
-            for (uint32_t j = lane(); j < k; j += kWave)
-                out(done + j, r.bw ? src_bits(s, bit0 + static_cast<uint64_t>(j) * r.bw, r.bw) : 0u);
-            bool finishes = !wrapped && k == r.literal;
-            r.lit_bit += k * r.bw;
-            r.literal -= k;
-            if (finishes && r.bw > 0) r.pos = r.lit_start + (r.lit_bit + 7) / 8;
-            done += k;
+        if (lane() == 0) dict_count[blockIdx.x] = static_cast<int32_t>(k);
+        return;
+    }
+    {  // payload (+ one block of the image's zero padding) -> LDS
+        const uint4* src = reinterpret_cast<const uint4*>(page);
+        uint4* dst = reinterpret_cast<uint4*>(words);
+        const uint32_t n16 = (size + 15) / 16 + 1;
+        for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    const uint32_t w = threadIdx.x / kWave, l = lane();
+    const uint32_t S = (size + kDictWaves - 1) / kDictWaves;
+    const uint32_t s0 = min(size, w * S), s1 = min(size, s0 + S);
+    {
+        uint32_t p = s0 + l, cnt = 0;
+        bool bad = p >= s1;
+        while (!bad && p < s1) {
+            if (p + 4 > size) { bad = true; break; }
+            uint32_t len = lds_u32(words, p);
+            if (static_cast<uint64_t>(p) + 4 + len > size) { bad = true; break; }
+            p += 4 + len;
+            cnt++;
+        }
+        ex[threadIdx.x] = bad ? kBad : p;
+        ec[threadIdx.x] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0, run = 0;
+        bool stop = n == 0;
+        for (uint32_t v = 0; v < kDictWaves; v++) {
+            seg_lane[v] = -1;
+            seg_base[v] = run;
+            seg_n[v] = 0;
+            const uint32_t a0 = min(size, v * S), a1 = min(size, a0 + S);
+            if (stop || t >= a1) continue;
+            const uint32_t c = t - a0;
+            if (c < kWave && ex[v * kWave + c] != kBad) {
+                uint32_t m = min(ec[v * kWave + c], n - run);
+                seg_lane[v] = static_cast<int32_t>(c);
+                seg_n[v] = m;
+                run += m;
+                t = ex[v * kWave + c];
+                if (run == n) stop = true;
+                continue;
+            }
+            while (t < a1 && run < n) {  // uncovered entry point: serial walk
+                if (t + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, t, 4, size); stop = true; break; }
+                uint32_t len = lds_u32(words, t);
+                if (static_cast<uint64_t>(t) + 4 + len > size) {
+                    set_err(err, err_any, PQ_ERR_BUFFER, t + 4, len, size);
+                    stop = true;
+                    break;
+                }
+                out[run++] = entry_code(len, t + 4);
+                t += 4 + len;
+            }
+            if (run == n) stop = true;
+        }
+        // chain reached the page end with entries still declared (t == size)
+        if (!stop && run < n) set_err(err, err_any, PQ_ERR_BUFFER, t, 4, size);
+        dict_count[blockIdx.x] = static_cast<int32_t>(run);
+    }
+    __syncthreads();
+    if (seg_lane[w] == static_cast<int32_t>(l)) {
+        uint32_t p = s0 + l;
+        uint64_t* o = out + seg_base[w];
+        for (uint32_t k = 0; k < seg_n[w]; k++) {
+            uint32_t len = lds_u32(words, p);
+            o[k] = entry_code(len, p + 4);
+            p += 4 + len;
         }
     }
-    return 0;
 }
 
 // ── fused page decode + gather ──────────────────────────────────────────────
+//
+// On gfx9 vector loads and stores share one counter (vmcnt), so a wave that
+// both loads and stores waits for its own earlier stores whenever it needs a
+// load result.  A workgroup is therefore split into producer/writer pairs:
+//   producer  tickets, page payload -> LDS, level/index decode, per-row
+//             (source, length) and page-local offsets, look-back.  Its only
+//             global stores are the look-back status words.
+//   writer    int64 offsets, validity words and characters: LDS -> HBM
+//             stores only; it never waits on memory.
+// Each producer hands pages to its writer through two LDS slots.
 struct FusedArgs {
     const uint8_t* bytes;
     const DevPage* pages;
@@ -152,8 +187,8 @@ struct FusedArgs {
     const int32_t* dict_count;
     int32_t max_def, max_rep;
     uint32_t rows_cap;           // max rows of a page (multiple of 64)
-    uint32_t stage_bytes;        // max payload bytes (multiple of 16)
-    uint32_t wave_bytes;         // LDS bytes per wavefront
+    uint32_t stage_bytes;        // max payload bytes (multiple of 16, + 16)
+    uint32_t pair_bytes;         // LDS bytes per producer/writer pair
     uint32_t dict_bytes;         // LDS bytes of the dictionary region
     uint32_t dict_chars_bytes;   // payload bytes region (multiple of 16)
     uint64_t* status;            // np look-back words (zeroed)
@@ -169,29 +204,84 @@ struct FusedArgs {
     DevErr* page_err;
     int32_t* err_any;
     int32_t debug;               // ablation switches (timing only; output invalid)
+    uint64_t* prof;              // per-phase cycle sums (kProfSlots), or null
 };
 
-struct WaveMem {
-    uint32_t* stage;    // stage_bytes
-    uint8_t* lv;        // rows_cap
-    uint16_t* ix;       // rows_cap: dict index / plain chars position per rank
-    uint16_t* il;       // rows_cap: plain length per rank
-    uint16_t* rsrc;     // rows_cap: source position per row
-    uint32_t* off;      // rows_cap + 1: page-local char offsets per row
-    uint16_t* brow;     // kGatherWin: first row of each 16-byte block
+enum {
+    PH_STAGE = 0, PH_DEF, PH_LEVELS, PH_VALUES, PH_ROWS, PH_LOOKBACK, PH_SLOTWAIT, PH_PAGES,
+    PH_W_WAIT, PH_W_OFFSETS, PH_W_GATHER, PH_W_PAGES, kProfSlots
 };
 
-__device__ __forceinline__ WaveMem carve(uint8_t* base, const FusedArgs& a) {
-    WaveMem m;
-    uint8_t* p = base;
-    m.stage = reinterpret_cast<uint32_t*>(p); p += a.stage_bytes;
-    m.off = reinterpret_cast<uint32_t*>(p); p += 4 * (a.rows_cap + 16);
-    m.lv = p; p += a.rows_cap;
-    m.ix = reinterpret_cast<uint16_t*>(p); p += 2 * a.rows_cap;
-    m.il = reinterpret_cast<uint16_t*>(p); p += 2 * a.rows_cap;
-    m.rsrc = reinterpret_cast<uint16_t*>(p); p += 2 * a.rows_cap;
-    m.brow = reinterpret_cast<uint16_t*>(p);
-    return m;
+enum : uint32_t { SLOT_FREE = 0, SLOT_FULL = 1, SLOT_DONE = 2 };
+
+struct SlotMeta {
+    int64_t G0;        // first output byte of the page
+    int64_t first_row;
+    uint32_t n;        // rows
+    uint32_t total;    // characters
+    uint32_t dict;     // characters come from the dictionary (else the page)
+    uint32_t state;    // SLOT_*
+};
+
+struct Slot {
+    SlotMeta* meta;
+    uint32_t* stage;   // page payload
+    uint32_t* off;     // rows_cap + 1: page-local char offsets
+    uint16_t* rsrc;    // rows_cap: source byte of each row
+    uint64_t* vm;      // rows_cap / 64: validity ballots
+};
+
+struct ProdMem {
+    uint8_t* lv;       // rows_cap: def levels
+    uint16_t* ix;      // rows_cap: dict index / plain chars position per rank
+    LitRun* lits;      // kLitCap (serial walk)
+    HybScratch hyb;    // decode scratch ...
+    uint16_t* il;      // ... reused: rows_cap plain lengths per rank
+};
+
+// LDS layout of one producer/writer pair (shared by kernel and host).
+struct PairLayout {
+    uint32_t hyb_pos, hyb_runs;
+    uint32_t p_lv, p_ix, p_lits, p_union, p_il, prod;          // producer scratch
+    uint32_t s_meta, s_stage, s_off, s_rsrc, s_vm, slot;       // one slot
+    uint32_t w_brow, writer;                                   // writer scratch
+    uint32_t bytes;
+};
+__host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
+__host__ __device__ inline PairLayout pair_layout(uint32_t rows_cap, uint32_t stage_bytes) {
+    PairLayout L;
+    L.hyb_pos = stage_bytes < kHybMaxPos ? stage_bytes : kHybMaxPos;
+    L.hyb_runs = L.hyb_pos < rows_cap ? L.hyb_pos : rows_cap;
+    uint32_t o = 0;
+    L.p_lv = o; o += al16(rows_cap);
+    L.p_ix = o; o += al16(2 * rows_cap);
+    L.p_lits = o; o += al16(static_cast<uint32_t>(sizeof(LitRun)) * kLitCap);
+    L.p_union = o;
+    L.p_il = o;
+    const uint32_t h = hyb_scratch_bytes(L.hyb_pos, L.hyb_runs), il = 2 * rows_cap;
+    o += al16(h > il ? h : il);
+    L.prod = o;
+    o = 0;
+    L.s_meta = o; o += al16(static_cast<uint32_t>(sizeof(SlotMeta)));
+    L.s_stage = o; o += al16(stage_bytes);
+    L.s_off = o; o += al16(4 * (rows_cap + 1));
+    L.s_rsrc = o; o += al16(2 * rows_cap);
+    L.s_vm = o; o += al16(8 * (rows_cap / 64 + 1));
+    L.slot = o;
+    L.w_brow = 0;
+    L.writer = al16(2 * kGatherWin);
+    L.bytes = L.prod + 2 * L.slot + L.writer;
+    return L;
+}
+
+__device__ __forceinline__ Slot slot_at(uint8_t* base, const PairLayout& L) {
+    Slot s;
+    s.meta = reinterpret_cast<SlotMeta*>(base + L.s_meta);
+    s.stage = reinterpret_cast<uint32_t*>(base + L.s_stage);
+    s.off = reinterpret_cast<uint32_t*>(base + L.s_off);
+    s.rsrc = reinterpret_cast<uint16_t*>(base + L.s_rsrc);
+    s.vm = reinterpret_cast<uint64_t*>(base + L.s_vm);
+    return s;
 }
 
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
@@ -209,6 +299,7 @@ __device__ uint64_t look_back(uint64_t* status, int32_t t, uint64_t total) {
     if (lane() == 0) __hip_atomic_store(&status[t], kAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t prefix = 0;
     int32_t q = t - 1;
+    uint32_t nap = 1;
     for (;;) {
         int32_t i = q - static_cast<int32_t>(lane());
         uint64_t s = i >= 0 ? __hip_atomic_load(&status[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kInc;
@@ -217,7 +308,8 @@ __device__ uint64_t look_back(uint64_t* status, int32_t t, uint64_t total) {
         uint32_t first_inc = incm ? static_cast<uint32_t>(__builtin_ctzll(incm)) : 64u;
         uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1ull);
         if (notready & upto) {
-            __builtin_amdgcn_s_sleep(1);
+            for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(8);
+            nap = nap < 8 ? 2 * nap : 8;
             continue;
         }
         uint64_t c = lane() <= first_inc ? (s & kValMask) : 0ull;
@@ -230,93 +322,149 @@ __device__ uint64_t look_back(uint64_t* status, int32_t t, uint64_t total) {
     return prefix;
 }
 
-// Unaligned dword at LDS byte address a (zero-extended reads stay in bounds).
-__device__ __forceinline__ uint32_t lds_u32(const uint32_t* words, uint32_t a) {
-    uint32_t w0 = words[a >> 2], w1 = words[(a >> 2) + 1];
-    return __builtin_amdgcn_alignbyte(w1, w0, a & 3);
+__device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
+
+// LDS hand-off flag.  A wave's LDS operations execute in issue order, so a
+// flag written after the data is seen after the data; the asm barriers keep
+// the compiler from moving LDS accesses across the flag.
+__device__ __forceinline__ uint32_t flag_get(const SlotMeta* m) {
+    __asm__ __volatile__("" ::: "memory");
+    uint32_t v = __hip_atomic_load(&m->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __asm__ __volatile__("" ::: "memory");
+    return __builtin_amdgcn_readfirstlane(v);
 }
-__device__ __forceinline__ uint32_t lds_u8(const uint32_t* words, uint32_t a) {
-    return (words[a >> 2] >> (8 * (a & 3))) & 0xFFu;
+__device__ __forceinline__ void flag_set(SlotMeta* m, uint32_t v) {
+    __asm__ __volatile__("" ::: "memory");
+    if (lane() == 0) __hip_atomic_store(&m->state, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __asm__ __volatile__("" ::: "memory");
+}
+__device__ __forceinline__ void flag_wait(const SlotMeta* m, bool want_free) {
+    for (;;) {
+        const uint32_t v = flag_get(m);
+        if (want_free ? v == SLOT_FREE : v != SLOT_FREE) return;
+        __builtin_amdgcn_s_sleep(2);
+    }
 }
 
-__global__ void __launch_bounds__(1024) k_ba_fused(FusedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t wv = threadIdx.x / kWave;
-
-    // dictionary -> LDS: raw payload words, then (pos | len << 16) per entry
-    uint32_t* dwords = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* dtab = reinterpret_cast<uint32_t*>(smem + a.dict_chars_bytes);
-    uint32_t dict_n = 0;
-    if (a.dict_id >= 0) {
-        const DevDict d = a.dicts[a.dict_id];
-        dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
-        uint4* dst = reinterpret_cast<uint4*>(dwords);
-        for (uint32_t i = threadIdx.x; i < a.dict_chars_bytes / 16; i += blockDim.x) dst[i] = src[i];
-        for (uint32_t k = threadIdx.x; k < dict_n; k += blockDim.x) {
-            uint64_t e = a.entries[d.entry_base + k];
-            dtab[k] = static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
+template <bool kProf>
+struct Prof {
+    uint64_t ph[kProfSlots];
+    uint64_t tk;
+    __device__ void start() {
+        if (kProf) {
+            for (int i = 0; i < kProfSlots; i++) ph[i] = 0;
+            tk = clk();
         }
     }
-    __syncthreads();
-    WaveMem M = carve(smem + a.dict_bytes + wv * a.wave_bytes, a);
-    const uint32_t bw_def = level_bw(a.max_def);
+    __device__ void mark(int slot) {
+        if (kProf) {
+            uint64_t now = clk();
+            ph[slot] += now - tk;
+            tk = now;
+        }
+    }
+    __device__ void count(int slot) {
+        if (kProf) ph[slot]++;
+    }
+    __device__ void flush(uint64_t* out) {
+        if (kProf && lane() == 0)
+            for (int i = 0; i < kProfSlots; i++)
+                if (ph[i]) atomicAdd(reinterpret_cast<unsigned long long*>(&out[i]), ph[i]);
+    }
+};
 
+// ── producer: one page per iteration ────────────────────────────────────────
+template <bool kProf>
+__device__ void produce(const FusedArgs& a, const PairLayout& L, uint8_t* pair, const uint32_t* dtab,
+                        uint32_t dict_n) {
+    ProdMem M;
+    M.lv = pair + L.p_lv;
+    M.ix = reinterpret_cast<uint16_t*>(pair + L.p_ix);
+    M.lits = reinterpret_cast<LitRun*>(pair + L.p_lits);
+    M.hyb = hyb_carve(pair + L.p_union, L.hyb_pos, L.hyb_runs);
+    M.il = reinterpret_cast<uint16_t*>(pair + L.p_il);
+    uint8_t* slots = pair + L.prod;
+    const uint32_t bw_def = level_bw(a.max_def);
+    Prof<kProf> P;
+    P.start();
+    uint32_t si = 0;
     for (;;) {
         int32_t t = 0;
         if (lane() == 0) t = atomicAdd(a.ticket, 1);
-        t = __shfl(t, 0, kWave);
-        if (t >= a.np) break;
+        t = static_cast<int32_t>(suni(static_cast<uint32_t>(__shfl(t, 0, kWave))));
+        Slot S = slot_at(slots + si * L.slot, L);
+        flag_wait(S.meta, true);
+        P.mark(PH_SLOTWAIT);
+        if (t >= a.np) {
+            flag_set(S.meta, SLOT_DONE);
+            break;
+        }
+        P.count(PH_PAGES);
         const int32_t p = a.p0 + t;
         const DevPage pg = a.pages[p];
-        DevErr* err = a.page_err + p;
+        const uint8_t* page = a.bytes + pg.off;
         const uint32_t size = static_cast<uint32_t>(pg.size);
         const uint32_t n = static_cast<uint32_t>(pg.nvals);
-        // 1. payload -> LDS (16-byte aligned in the device image)
+        // 1. payload -> LDS (slots are 16-byte aligned with >= 16 bytes of
+        //    zero padding, so the extra block stays inside the image)
         {
-            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + pg.off);
-            uint4* dst = reinterpret_cast<uint4*>(M.stage);
-            const uint32_t n16 = (size + 15) / 16;
-            for (uint32_t i = lane(); i < n16; i += kWave) dst[i] = src[i];
+            const uint4* gsrc = reinterpret_cast<const uint4*>(page);
+            uint4* sdst = reinterpret_cast<uint4*>(S.stage);
+            const uint32_t n16 = (size + 15) / 16 + 1;
+            for (uint32_t i = lane(); i < n16; i += kWave) sdst[i] = gsrc[i];
         }
         __builtin_amdgcn_wave_barrier();
-        const Src s{M.stage, nullptr, size};
-        Win w;
-        win_init(w, M.stage, (size + 3) / 4);
+        P.mark(PH_STAGE);
+        const uint32_t* pw = S.stage;
         int code = 0;
-        uint32_t epos = 0, eneed = 0;
+        uint32_t epos = 0, eneed = 0, nl = 0;
         // 2. levels (column_reader.cpp:146-170)
-        uint32_t pos = 0;
-        Rle def, ix;
+        uint32_t pos = 0, def_base = 0, dl = 0;
         if (a.max_def > 0) {
             if (pos + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
             else {
-                uint32_t dl = uni(win_u32(w, pos));
+                dl = suni(lds_u32(pw, pos));
                 pos += 4;
                 if (static_cast<uint64_t>(pos) + dl > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = dl; }
-                else { rle_init(def, pos, dl, bw_def); pos += dl; }
+                else { def_base = pos; pos += dl; }
             }
         }
         if (!code && a.max_rep > 0) {
             if (pos + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
             else {
-                uint32_t rl2 = uni(win_u32(w, pos));
+                uint32_t rl2 = suni(lds_u32(pw, pos));
                 pos += 4;
                 if (static_cast<uint64_t>(pos) + rl2 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = rl2; }
                 else pos += rl2;
             }
         }
-        if (!code) {
-            if (a.max_def > 0) {
-                code = rlew_decode(def, w, s, n, [&](uint32_t j, uint32_t v) { M.lv[j] = static_cast<uint8_t>(v > 255 ? 255 : v); });
-            } else {
-                for (uint32_t j = lane(); j < n; j += kWave) M.lv[j] = 0;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
+        // def levels (stream 0), then dictionary indices (stream 1): one loop
+        // so the decoder is instantiated once
         const bool dict = pg.mode == MODE_DICT;
         uint32_t nn = 0;
-        if (!code) {
+        uint32_t sbase = def_base, slen = dl, sbw = bw_def, scount = n;
+        bool run_stream = !code && a.max_def > 0;
+        if (!code && a.max_def == 0)
+            for (uint32_t j = lane(); j < n; j += kWave) M.lv[j] = 0;
+#pragma nounroll
+        for (uint32_t st = 0; st < 2; st++) {
+            if (run_stream) {
+                auto put = [&](uint32_t j, uint32_t v) {
+                    if (st == 0) M.lv[j] = static_cast<uint8_t>(v > 255 ? 255 : v);
+                    else M.ix[j] = static_cast<uint16_t>(static_cast<int32_t>(v) >= 0 && v < dict_n ? v : 0xFFFFu);
+                };
+                if (hyb_decode(pw, size, sbase, slen, sbw, scount, M.hyb, L.hyb_runs, M.ix, put)) {
+                    SRle r;
+                    srle_init(r, sbase, slen, sbw);
+                    code = srle_walk(r, page, scount, put, M.lits, nl, kLitCap,
+                                     [&]() { expand_lits(M.lits, nl, pw, size, sbw, put); });
+                    if (!code) expand_lits(M.lits, nl, pw, size, sbw, put);
+                    nl = 0;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (st == 1 || code) break;
+            P.mark(PH_DEF);
             uint32_t above = 0;
             for (uint32_t j0 = 0; j0 < n; j0 += kWave) {
                 uint32_t j = j0 + lane();
@@ -326,22 +474,24 @@ __global__ void __launch_bounds__(1024) k_ba_fused(FusedArgs a) {
                 above |= __ballot(j < n && d > static_cast<uint32_t>(a.max_def)) != 0;
             }
             if (dict && above) code = PQ_ERR_UNSUPPORTED;
-        }
-        // values: dictionary indices or the PLAIN length chain
-        if (!code && dict) {
-            if (pos + 1 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 1; }
-            else {
-                uint32_t bw = uni(win_u32(w, pos) & 0xFFu);
-                pos += 1;
-                rle_init(ix, pos, size - pos, bw);
-                code = rlew_decode(ix, w, s, nn, [&](uint32_t j, uint32_t v) {
-                    M.ix[j] = static_cast<uint16_t>(static_cast<int32_t>(v) >= 0 && v < dict_n ? v : 0xFFFFu);
-                });
+            P.mark(PH_LEVELS);
+            run_stream = false;
+            if (!code && dict) {  // column_reader.cpp:196-214
+                if (pos + 1 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 1; }
+                else {
+                    sbw = suni(lds_u32(pw, pos) & 0xFFu);
+                    pos += 1;
+                    sbase = pos;
+                    slen = size - pos;
+                    scount = nn;
+                    run_stream = true;
+                }
             }
-        } else if (!code) {
+        }
+        if (!code && !dict) {
             for (uint32_t k = 0; k < nn; k++) {  // column_reader.cpp:249-253
                 if (static_cast<uint64_t>(pos) + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; break; }
-                uint32_t len = uni(win_u32(w, pos));
+                uint32_t len = suni(lds_u32(pw, pos));
                 pos += 4;
                 if (static_cast<uint64_t>(pos) + len > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = len; break; }
                 if (lane() == 0) { M.ix[k] = static_cast<uint16_t>(pos); M.il[k] = static_cast<uint16_t>(len); }
@@ -349,7 +499,8 @@ __global__ void __launch_bounds__(1024) k_ba_fused(FusedArgs a) {
             }
         }
         __builtin_amdgcn_wave_barrier();
-        // 3. per-row source/length, page-local offsets
+        P.mark(PH_VALUES);
+        // 3. per-row source/length, page-local offsets, validity ballots
         uint64_t total = 0;
         if (!code) {
             uint32_t rank = 0, run = 0;
@@ -380,44 +531,27 @@ __global__ void __launch_bounds__(1024) k_ba_fused(FusedArgs a) {
                 }
                 uint32_t inc = wave_incl_scan(len);
                 if (in) {
-                    M.off[j] = run + inc - len;
-                    M.rsrc[j] = static_cast<uint16_t>(src);
+                    S.off[j] = run + inc - len;
+                    S.rsrc[j] = static_cast<uint16_t>(src);
                 }
                 run += bcast_last(inc);
-                // validity bits of rows [first_row + j0, +64)
-                uint64_t vm = __ballot(valid);
-                const int64_t R = pg.first_row + j0;
-                const uint32_t wi = static_cast<uint32_t>(R >> 5), sh = static_cast<uint32_t>(R & 31);
-                const uint32_t cnt = min(64u, n - j0);
-                if (lane() < 3) {
-                    uint32_t part = lane() == 0 ? static_cast<uint32_t>(vm << sh)
-                                  : lane() == 1 ? static_cast<uint32_t>(sh ? (vm >> (32 - sh)) : (vm >> 32))
-                                                : (sh ? static_cast<uint32_t>(vm >> (64 - sh)) : 0u);
-                    // bit range of this word covered by the page's rows
-                    int64_t wlo = static_cast<int64_t>(wi + lane()) * 32;
-                    int64_t rlo = R, rhi = R + cnt;
-                    bool full = wlo >= pg.first_row && wlo + 32 <= pg.first_row + static_cast<int64_t>(n) &&
-                                wlo >= rlo && wlo + 32 <= rhi;
-                    if (wlo < rhi && wlo + 32 > rlo) {
-                        if (full) a.validity[wi + lane()] = part;
-                        else if (part) atomicOr(&a.validity[wi + lane()], part);
-                    }
-                }
+                const uint64_t vm = __ballot(valid);
+                if (lane() == 0) S.vm[j0 / kWave] = vm;
             }
-            if (lane() == 0) M.off[n] = run;
+            if (lane() == 0) S.off[n] = run;
             total = run;
-        }
-        if (code) {
+        } else {
             if (lane() == 0) {
+                DevErr* err = a.page_err + p;
                 err->code = code;
                 err->pos = static_cast<int32_t>(epos);
                 err->need = static_cast<int32_t>(eneed);
                 err->size = static_cast<int32_t>(size);
                 atomicOr(a.err_any, 1);
             }
-            total = 0;
         }
         __builtin_amdgcn_wave_barrier();
+        P.mark(PH_ROWS);
         // 4. page start in the output
         const int64_t G0 = (a.debug & 1) ? static_cast<int64_t>(t) * 24 * n
                                          : *a.base_in + static_cast<int64_t>(look_back(a.status, t, total));
@@ -425,89 +559,213 @@ __global__ void __launch_bounds__(1024) k_ba_fused(FusedArgs a) {
             *a.base_out = G0 + static_cast<int64_t>(total);
             if (pg.first_row + n == a.nrows_total) a.offsets[a.nrows_total] = G0 + total;
         }
-        if (code) continue;
-        // 5a. offsets
-        if (!(a.debug & 4))
-            for (uint32_t j = lane(); j < n; j += kWave) a.offsets[pg.first_row + j] = G0 + M.off[j];
-        if (total == 0 || (a.debug & 2)) continue;
-        const int64_t G1 = G0 + static_cast<int64_t>(total);
-        if (G1 > a.capacity) {
-            if (lane() == 0) atomicOr(a.overflow, 1);
-            continue;
+        P.mark(PH_LOOKBACK);
+        if (lane() == 0) {
+            S.meta->G0 = G0;
+            S.meta->first_row = pg.first_row;
+            S.meta->n = code ? 0u : n;
+            S.meta->total = static_cast<uint32_t>(total);
+            S.meta->dict = dict;
         }
-        // 5b. characters: 16-byte blocks of the global char stream
-        const uint32_t* srcw = dict ? dwords : M.stage;
-        const int64_t B0 = G0 >> 4;
-        const int64_t nb = ((G1 - 1) >> 4) - B0 + 1;
-        for (int64_t w0 = 0; w0 < nb; w0 += kGatherWin) {
-            const int64_t w1 = min(nb, w0 + static_cast<int64_t>(kGatherWin));
-            for (uint32_t r = lane(); r < n; r += kWave) {
-                uint32_t s0 = M.off[r], e0 = M.off[r + 1];
-                if (e0 <= s0) continue;
-                int64_t blo = s0 == 0 ? 0 : ((s0 + G0 + 15) >> 4) - B0;
-                int64_t bhi = ((e0 + G0 + 15) >> 4) - B0 - 1;
-                blo = max(blo, w0);
-                bhi = min(bhi, w1 - 1);
-                for (int64_t b = blo; b <= bhi; b++) M.brow[b - w0] = static_cast<uint16_t>(r);
-            }
-            __builtin_amdgcn_wave_barrier();
-            for (int64_t b = w0 + lane(); b < w1; b += kWave) {
-                const int64_t blk = (B0 + b) << 4;
-                const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
-                uint32_t r = M.brow[b - w0];
-                uint32_t q = static_cast<uint32_t>(gs - G0);  // page-local output byte
-                uint32_t o = static_cast<uint32_t>(gs - blk);
-                const uint32_t oe = static_cast<uint32_t>(ge - blk);
-                uint32_t rend = M.off[r + 1];
-                uint32_t out[4] = {0, 0, 0, 0};
-                // output dword k covers block bytes [4k, 4k+4)
-#pragma unroll
-                for (uint32_t k = 0; k < 4; k++) {
-                    uint32_t lo = max(4 * k, o), hi = min(4 * k + 4, oe);
-                    if (lo >= hi) continue;
-                    uint32_t ql = q + (lo - o);  // page-local byte of block byte lo
-                    while (ql >= rend && r + 1 < n) { r++; rend = M.off[r + 1]; }
-                    if (ql + (hi - lo) <= rend) {
-                        // whole piece from one row: one unaligned dword read
-                        uint32_t sa = M.rsrc[r] + (ql - M.off[r]);
-                        uint32_t x = lds_u32(srcw, sa - (lo - 4 * k));
-                        uint32_t m = (hi - lo == 4) ? 0xFFFFFFFFu : (((1u << (8 * (hi - lo))) - 1u) << (8 * (lo - 4 * k)));
-                        out[k] |= x & m;
+        flag_set(S.meta, SLOT_FULL);
+        si ^= 1;
+    }
+    P.flush(a.prof);
+}
+
+// ── writer: offsets, validity and characters of the pages handed over ──────
+template <bool kProf>
+__device__ void write_pages(const FusedArgs& a, const PairLayout& L, uint8_t* pair, const uint32_t* dwords) {
+    uint8_t* slots = pair + L.prod;
+    uint16_t* brow = reinterpret_cast<uint16_t*>(pair + L.prod + 2 * L.slot + L.w_brow);
+    Prof<kProf> P;
+    P.start();
+    uint32_t si = 0;
+    for (;;) {
+        Slot S = slot_at(slots + si * L.slot, L);
+        flag_wait(S.meta, false);
+        P.mark(PH_W_WAIT);
+        if (flag_get(S.meta) == SLOT_DONE) break;
+        P.count(PH_W_PAGES);
+        const int64_t G0 = S.meta->G0;
+        const int64_t first_row = S.meta->first_row;
+        const uint32_t n = __builtin_amdgcn_readfirstlane(S.meta->n);
+        const uint32_t total = __builtin_amdgcn_readfirstlane(S.meta->total);
+        const bool dict = __builtin_amdgcn_readfirstlane(S.meta->dict) != 0;
+        // offsets (two rows per lane and store)
+        if (!(a.debug & 4)) {
+            for (uint32_t j = 2 * lane(); j < n; j += 2 * kWave) {
+                const int64_t o0 = G0 + S.off[j];
+                if (j + 1 < n) {
+                    const int64_t o1 = G0 + S.off[j + 1];
+                    int64_t* dst = a.offsets + first_row + j;
+                    if (((first_row + j) & 1) == 0) {
+                        *reinterpret_cast<longlong2*>(dst) = make_longlong2(o0, o1);
                     } else {
-                        for (uint32_t bb = lo; bb < hi; bb++) {
-                            uint32_t qb = q + (bb - o);
-                            while (qb >= rend && r + 1 < n) { r++; rend = M.off[r + 1]; }
-                            uint32_t sa = M.rsrc[r] + (qb - M.off[r]);
-                            out[k] |= lds_u8(srcw, sa) << (8 * (bb & 3));
+                        dst[0] = o0;
+                        dst[1] = o1;
+                    }
+                } else {
+                    a.offsets[first_row + j] = o0;
+                }
+            }
+        }
+        // validity words covering rows [first_row, first_row + n)
+        if (n) {
+            const int64_t w0 = first_row >> 5, w1 = (first_row + n - 1) >> 5;
+            for (int64_t w = w0 + lane(); w <= w1; w += kWave) {
+                const int64_t wr = w * 32;  // first row of this word
+                uint32_t bits = 0;
+                // rows [max(wr, first_row), min(wr + 32, first_row + n))
+                const int64_t lo = max(wr, first_row), hi = min(wr + 32, first_row + static_cast<int64_t>(n));
+                const uint32_t r0 = static_cast<uint32_t>(lo - first_row);
+                const uint32_t cnt = static_cast<uint32_t>(hi - lo);
+                const uint64_t m0 = S.vm[r0 >> 6];
+                const uint64_t m1 = ((r0 >> 6) + 1) * kWave < n ? S.vm[(r0 >> 6) + 1] : 0ull;
+                const uint32_t sh = r0 & 63;
+                uint64_t x = sh ? ((m0 >> sh) | (m1 << (64 - sh))) : m0;
+                x &= cnt >= 32 ? 0xFFFFFFFFull : ((1ull << cnt) - 1ull);
+                bits = static_cast<uint32_t>(x) << static_cast<uint32_t>(lo - wr);
+                if (cnt == 32) a.validity[w] = bits;
+                else if (bits) atomicOr(&a.validity[w], bits);
+            }
+        }
+        P.mark(PH_W_OFFSETS);
+        const int64_t G1 = G0 + static_cast<int64_t>(total);
+        if (total && !(a.debug & 2) && G1 > a.capacity) {
+            if (lane() == 0) atomicOr(a.overflow, 1);
+        } else if (total && !(a.debug & 2)) {
+            // characters: 16-byte blocks of the global char stream
+            const uint32_t* srcw = dict ? dwords : S.stage;
+            const int64_t B0 = G0 >> 4;
+            const int64_t nb = ((G1 - 1) >> 4) - B0 + 1;
+            for (int64_t w0 = 0; w0 < nb; w0 += kGatherWin) {
+                const int64_t w1 = min(nb, w0 + static_cast<int64_t>(kGatherWin));
+                for (uint32_t r = lane(); r < n && !(a.debug & 32); r += kWave) {
+                    uint32_t s0 = S.off[r], e0 = S.off[r + 1];
+                    if (e0 <= s0) continue;
+                    int64_t blo = s0 == 0 ? 0 : ((s0 + G0 + 15) >> 4) - B0;
+                    int64_t bhi = ((e0 + G0 + 15) >> 4) - B0 - 1;
+                    blo = max(blo, w0);
+                    bhi = min(bhi, w1 - 1);
+                    for (int64_t b = blo; b <= bhi; b++) brow[b - w0] = static_cast<uint16_t>(r);
+                }
+                __builtin_amdgcn_wave_barrier();
+                for (int64_t b = w0 + lane(); b < w1; b += kWave) {
+                    const int64_t blk = (B0 + b) << 4;
+                    const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
+                    uint32_t r = (a.debug & 32) ? 0u : brow[b - w0];
+                    uint32_t q = static_cast<uint32_t>(gs - G0);  // page-local output byte
+                    uint32_t o = static_cast<uint32_t>(gs - blk);
+                    const uint32_t oe = static_cast<uint32_t>(ge - blk);
+                    uint32_t rend = S.off[r + 1];
+                    uint32_t out[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; k++) {
+                        uint32_t lo = max(4 * k, o), hi = min(4 * k + 4, oe);
+                        if (lo >= hi || (a.debug & 8)) continue;
+                        uint32_t ql = q + (lo - o);
+                        while (ql >= rend && r + 1 < n) { r++; rend = S.off[r + 1]; }
+                        if (ql + (hi - lo) <= rend) {
+                            uint32_t sa = S.rsrc[r] + (ql - S.off[r]);
+                            uint32_t x = lds_u32(srcw, sa - (lo - 4 * k));
+                            uint32_t m = (hi - lo == 4) ? 0xFFFFFFFFu : (((1u << (8 * (hi - lo))) - 1u) << (8 * (lo - 4 * k)));
+                            out[k] |= x & m;
+                        } else {
+                            for (uint32_t bb = lo; bb < hi; bb++) {
+                                uint32_t qb = q + (bb - o);
+                                while (qb >= rend && r + 1 < n) { r++; rend = S.off[r + 1]; }
+                                uint32_t sa = S.rsrc[r] + (qb - S.off[r]);
+                                out[k] |= lds_u8(srcw, sa) << (8 * (bb & 3));
+                            }
                         }
                     }
+                    if (a.debug & 16) {
+                        if ((out[0] ^ out[1] ^ out[2] ^ out[3]) == 0x9e3779b9u) atomicOr(a.overflow, 2);
+                    } else if (o == 0 && oe == 16) {
+                        *reinterpret_cast<uint4*>(a.chars + blk) = make_uint4(out[0], out[1], out[2], out[3]);
+                    } else {
+                        for (uint32_t bb = o; bb < oe; bb++)
+                            a.chars[blk + bb] = static_cast<uint8_t>(out[bb >> 2] >> (8 * (bb & 3)));
+                    }
                 }
-                if (o == 0 && oe == 16) {
-                    *reinterpret_cast<uint4*>(a.chars + blk) = make_uint4(out[0], out[1], out[2], out[3]);
-                } else {
-                    for (uint32_t bb = o; bb < oe; bb++)
-                        a.chars[blk + bb] = static_cast<uint8_t>(out[bb >> 2] >> (8 * (bb & 3)));
-                }
+                __builtin_amdgcn_wave_barrier();
             }
-            __builtin_amdgcn_wave_barrier();
+        }
+        P.mark(PH_W_GATHER);
+        flag_set(S.meta, SLOT_FREE);
+        si ^= 1;
+    }
+    P.flush(a.prof);
+}
+
+template <bool kProf>
+__global__ void __launch_bounds__(1024) k_ba_fused(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wv = threadIdx.x / kWave;
+    const uint32_t npairs = blockDim.x / (2 * kWave);
+    const PairLayout L = pair_layout(a.rows_cap, a.stage_bytes);
+
+    // dictionary -> LDS: raw payload words, then (pos | len << 16) per entry
+    uint32_t* dwords = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* dtab = reinterpret_cast<uint32_t*>(smem + a.dict_chars_bytes);
+    uint32_t dict_n = 0;
+    if (a.dict_id >= 0) {
+        const DevDict d = a.dicts[a.dict_id];
+        dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
+        uint4* dst = reinterpret_cast<uint4*>(dwords);
+        for (uint32_t i = threadIdx.x; i < a.dict_chars_bytes / 16; i += blockDim.x) dst[i] = src[i];
+        for (uint32_t k = threadIdx.x; k < dict_n; k += blockDim.x) {
+            uint64_t e = a.entries[d.entry_base + k];
+            dtab[k] = static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
         }
     }
+    const uint32_t pi = wv < npairs ? wv : wv - npairs;
+    uint8_t* pair = smem + a.dict_bytes + pi * a.pair_bytes;
+    if (wv < npairs && lane() == 0) {
+        slot_at(pair + L.prod, L).meta->state = SLOT_FREE;
+        slot_at(pair + L.prod + L.slot, L).meta->state = SLOT_FREE;
+    }
+    __syncthreads();
+    if (wv < npairs) produce<kProf>(a, L, pair, dtab, dict_n);
+    else write_pages<kProf>(a, L, pair, dwords);
 }
 
 }  // namespace
 
 void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
-                       uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any) {
+                       uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any,
+                       uint32_t max_dict_bytes) {
     if (ndicts <= 0) return;
-    hipLaunchKernelGGL(k_dict_index, dim3(ndicts), dim3(64), 0, s, bytes, dicts, entries, dict_count,
-                       dict_err, err_any);
+    constexpr uint32_t kCap = 128 * 1024;  // + 8.2 KiB static tables < 160 KiB
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_dict_index),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kCap);
+        attr = true;
+    }
+    uint32_t lds = std::min<uint32_t>(kCap, (max_dict_bytes + 15) / 16 * 16 + 32);
+    hipLaunchKernelGGL(k_dict_index, dim3(ndicts), dim3(kDictWaves * kWave), lds, s, bytes, dicts, entries,
+                       dict_count, dict_err, err_any, lds);
 }
+
+namespace {
+void set_fused_attrs() {
+    static bool attr = false;
+    if (attr) return;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ba_fused<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ba_fused<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+}
+}  // namespace
 
 int fused_occupancy_waves(uint32_t lds_bytes_per_block, int waves_per_block) {
     int blocks = 0;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ba_fused),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_ba_fused, waves_per_block * kWave,
+    set_fused_attrs();
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_ba_fused<false>, waves_per_block * kWave,
                                                      lds_bytes_per_block) != hipSuccess)
         return 0;
     return blocks;
@@ -518,24 +776,25 @@ void launch_ba_fused(hipStream_t s, const FusedLaunch& L) {
     a.bytes = L.bytes; a.pages = L.pages; a.p0 = L.p0; a.np = L.np; a.dicts = L.dicts;
     a.dict_id = L.dict_id; a.entries = L.entries; a.dict_count = L.dict_count;
     a.max_def = L.max_def; a.max_rep = L.max_rep; a.rows_cap = L.rows_cap;
-    a.stage_bytes = L.stage_bytes; a.wave_bytes = L.wave_bytes; a.dict_bytes = L.dict_bytes;
+    a.stage_bytes = L.stage_bytes; a.pair_bytes = L.wave_bytes; a.dict_bytes = L.dict_bytes;
     a.dict_chars_bytes = L.dict_chars_bytes; a.status = L.status; a.ticket = L.ticket;
     a.base_in = L.base_in; a.base_out = L.base_out; a.nrows_total = L.nrows_total;
     a.validity = L.validity; a.offsets = L.offsets; a.chars = L.chars; a.capacity = L.capacity;
     a.overflow = L.overflow; a.page_err = L.page_err; a.err_any = L.err_any; a.debug = L.debug;
-    const uint32_t lds = L.dict_bytes + L.waves_per_block * L.wave_bytes;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ba_fused),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
-    hipLaunchKernelGGL(k_ba_fused, dim3(L.grid), dim3(L.waves_per_block * kWave), lds, s, a);
+    a.prof = L.prof;
+    const uint32_t lds = L.dict_bytes + (L.waves_per_block / 2) * L.wave_bytes;
+    set_fused_attrs();
+    if (a.prof)
+        hipLaunchKernelGGL(k_ba_fused<true>, dim3(L.grid), dim3(L.waves_per_block * kWave), lds, s, a);
+    else
+        hipLaunchKernelGGL(k_ba_fused<false>, dim3(L.grid), dim3(L.waves_per_block * kWave), lds, s, a);
 }
 
+// LDS bytes of one producer/writer pair (FusedLaunch::wave_bytes).
 uint32_t fused_wave_bytes(uint32_t rows_cap, uint32_t stage_bytes) {
-    uint32_t b = stage_bytes + 4 * (rows_cap + 16) + rows_cap + 2 * rows_cap * 3 + 2 * kGatherWin;
-    return (b + 15) / 16 * 16;
+    return pair_layout(rows_cap, stage_bytes).bytes;
 }
+
+int fused_prof_slots() { return kProfSlots; }
 
 }  // namespace pqk

@@ -1,0 +1,205 @@
+// hybrid.hpp — lane-parallel decode of one hybrid RLE/bit-packed stream
+// (rle_decoder.hpp:6-108) held in LDS, for one wavefront.
+//
+// The run headers form a chain: header -> payload -> next header.  Walking it
+// on the scalar unit costs ~100 SALU per run and the scalar unit is shared by
+// every wave of a CU, so for run-dense streams (short RLE runs, 8-value
+// bit-packed groups) the decode is bound by SALU issue.  Here every byte
+// position of the stream is parsed as if a header started there (one lane per
+// position), giving a successor function next(p).  The positions on the true
+// chain — the set reachable from position 0 — come from pointer doubling:
+//   S_0 = {0},  S_{k+1} = S_k ∪ J_k(S_k),  J_{k+1} = J_k ∘ J_k
+// which needs ceil(log2(runs)) rounds of LDS gathers.  A prefix sum of the run
+// lengths over chain positions (chain order = byte order) gives each run's
+// first output slot; a max-scan of run ids scattered at those slots gives the
+// run of every output, which is then expanded from the run's value (RLE) or
+// from its bit-packed payload in the staged page.
+//
+// Streams with anything unusual on the chain before the last needed value —
+// a zero-length run (the reference's literal_count_ wrap), a varint that
+// runs past the stream or over five bytes, bw > 32, a header too wide for
+// the 8-byte window — report "serial" and the caller runs the scalar walk
+// (stream.hpp), which restates the reference state machine exactly.
+#pragma once
+#include "kernels/device_common.hpp"
+
+namespace pqk {
+namespace dev {
+
+constexpr uint32_t kHybMaxPos = 1024;  // stream bytes decoded in parallel (else: serial walk)
+
+// Per-wave LDS scratch for hyb_decode, sized for `maxpos` stream bytes and
+// `maxruns` runs (see hyb_scratch_bytes).
+struct HybScratch {
+    uint16_t* nx0;    // maxpos + 1: successor (ping)
+    uint16_t* nx1;    // maxpos + 1: successor (pong)
+    uint16_t* cnt;    // maxpos: run length (saturated at 65535)
+    uint32_t* aux;    // maxpos: RLE value, or payload byte offset in the page
+    uint8_t* on;      // maxpos + 1: position is on the chain
+    uint8_t* meta;    // maxpos: bit0 literal, bit1 serial-only
+    uint16_t* rpos;   // maxruns: position of run r
+    uint16_t* rstart; // maxruns: first output slot of run r
+};
+
+__host__ __device__ constexpr uint32_t hyb_align4(uint32_t x) { return (x + 3u) & ~3u; }
+
+__host__ __device__ inline uint32_t hyb_scratch_bytes(uint32_t maxpos, uint32_t maxruns) {
+    return 2 * hyb_align4(2 * (maxpos + 1)) + hyb_align4(2 * maxpos) + 4 * maxpos +
+           hyb_align4(maxpos + 1) + hyb_align4(maxpos) + 2 * hyb_align4(2 * maxruns);
+}
+
+__device__ inline HybScratch hyb_carve(uint8_t* p, uint32_t maxpos, uint32_t maxruns) {
+    HybScratch s;
+    s.aux = reinterpret_cast<uint32_t*>(p); p += 4 * maxpos;
+    s.nx0 = reinterpret_cast<uint16_t*>(p); p += hyb_align4(2 * (maxpos + 1));
+    s.nx1 = reinterpret_cast<uint16_t*>(p); p += hyb_align4(2 * (maxpos + 1));
+    s.cnt = reinterpret_cast<uint16_t*>(p); p += hyb_align4(2 * maxpos);
+    s.rpos = reinterpret_cast<uint16_t*>(p); p += hyb_align4(2 * maxruns);
+    s.rstart = reinterpret_cast<uint16_t*>(p); p += hyb_align4(2 * maxruns);
+    s.on = p; p += hyb_align4(maxpos + 1);
+    s.meta = p;
+    return s;
+}
+
+// 8 bytes at LDS byte address a (the staged page has >= 16 readable bytes
+// past its end).
+__device__ __forceinline__ uint64_t lds_u64(const uint32_t* w, uint32_t a) {
+    const uint32_t i = a >> 2, sh = a & 3;
+    const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2];
+    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, kWave);
+        if (lane() >= static_cast<uint32_t>(d)) v = max(v, t);
+    }
+    return v;
+}
+
+// Decode the first n values of the stream at page bytes [base, base + S)
+// (page words `pw`, page size `psize`) with bit width bw.  out(j, v) for
+// j < n.  R: n u16 slots of LDS scratch (may alias the output array when
+// out writes slot j only after reading R[j] in the same lane).  Returns 0,
+// or 1 if the stream needs the serial walk (nothing was written then).
+template <class Out>
+__device__ int hyb_decode(const uint32_t* pw, uint32_t psize, uint32_t base, uint32_t S, uint32_t bw,
+                          uint32_t n, const HybScratch& sc, uint32_t maxruns, uint16_t* R, Out&& out) {
+    if (n == 0) return 0;
+    if (S > kHybMaxPos || bw > 32) return 1;
+    const uint32_t nb = (bw + 7) / 8;
+    // A. parse a header at every position
+    bool serial = false;
+    for (uint32_t p = lane(); p < S; p += kWave) {
+        const uint32_t rem = S - p;
+        uint64_t x = lds_u64(pw, base + p);
+        if (rem < 8) x &= (1ull << (8 * rem)) - 1ull;
+        const uint32_t vb = min(rem, 5u);  // varint bytes available
+        const uint64_t stops = ~x & 0x8080808080ull & ((1ull << (8 * vb)) - 1ull);
+        uint32_t meta = 0, next = S, count = 0, aux = 0;
+        if (stops == 0) {
+            meta = 2;
+        } else {
+            const uint32_t hl = (static_cast<uint32_t>(__builtin_ctzll(stops)) >> 3) + 1;
+            uint64_t v = (x & 0x7full) | ((x >> 1) & 0x3f80ull) | ((x >> 2) & 0x1fc000ull) |
+                         ((x >> 3) & 0xfe00000ull) | ((x >> 4) & 0x7f0000000ull);
+            v &= (1ull << (7 * hl)) - 1ull;
+            const uint32_t ind = static_cast<uint32_t>(v);
+            if (ind & 1u) {
+                count = (ind >> 1) * 8u;
+                const uint64_t end = static_cast<uint64_t>(p) + hl + (static_cast<uint64_t>(count) * bw + 7) / 8;
+                next = end >= S ? S : static_cast<uint32_t>(end);
+                aux = base + p + hl;
+                meta = 1;
+            } else {
+                count = ind >> 1;
+                const uint32_t take = min(nb, rem - hl);
+                if (hl + take > 8) meta = 2;
+                aux = take ? static_cast<uint32_t>((x >> (8 * hl)) & ((take >= 4) ? 0xFFFFFFFFull
+                                                                                  : ((1ull << (8 * take)) - 1ull)))
+                           : 0u;
+                next = min(S, p + hl + take);
+            }
+            if (count == 0) meta = 2;
+        }
+        sc.nx0[p] = static_cast<uint16_t>(next);
+        sc.cnt[p] = static_cast<uint16_t>(min(count, 65535u));
+        sc.aux[p] = aux;
+        sc.meta[p] = static_cast<uint8_t>(meta);
+        sc.on[p] = p == 0;
+    }
+    if (lane() == 0) { sc.nx0[S] = static_cast<uint16_t>(S); sc.nx1[S] = static_cast<uint16_t>(S); sc.on[S] = 0; }
+    __builtin_amdgcn_wave_barrier();
+    // B. chain membership by pointer doubling
+    uint16_t* J = sc.nx0;
+    uint16_t* K = sc.nx1;
+    for (;;) {
+        const uint32_t j0 = __builtin_amdgcn_readfirstlane(J[0]);
+        if (j0 >= S) break;
+        for (uint32_t p = lane(); p < S; p += kWave)
+            if (sc.on[p]) sc.on[J[p]] = 1;
+        for (uint32_t p = lane(); p < S; p += kWave) K[p] = J[J[p]];
+        __builtin_amdgcn_wave_barrier();
+        uint16_t* t = J; J = K; K = t;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // C. run starts (prefix of lengths in byte order), run list, serial check
+    for (uint32_t j = lane(); j < n; j += kWave) R[j] = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t csum = 0, rsum = 0;
+    for (uint32_t p0 = 0; p0 < S; p0 += kWave) {
+        const uint32_t p = p0 + lane();
+        const bool o = p < S && sc.on[p];
+        const uint32_t c = o ? sc.cnt[p] : 0u;
+        const uint32_t ci = wave_incl_scan(c);
+        const uint64_t om = __ballot(o);
+        const uint32_t st = csum + ci - c;
+        const uint32_t ri = rsum + popc_below(om);
+        if (o && st < n) {
+            serial |= (sc.meta[p] & 2u) != 0;
+            if (ri < maxruns) {
+                sc.rpos[ri] = static_cast<uint16_t>(p);
+                sc.rstart[ri] = static_cast<uint16_t>(st);
+                R[st] = static_cast<uint16_t>(ri);
+            } else {
+                serial = true;
+            }
+        }
+        csum += bcast_last(ci);
+        rsum += __popcll(om);
+        if (csum >= n) break;
+    }
+    if (__ballot(serial)) return 1;
+    __builtin_amdgcn_wave_barrier();
+    // D. run of every output (max-scan) and expansion
+    const uint32_t total = csum;
+    uint32_t carry = 0;
+    for (uint32_t j0 = 0; j0 < n; j0 += kWave) {
+        const uint32_t j = j0 + lane();
+        const uint32_t r0 = j < n ? R[j] : 0u;
+        const uint32_t r = max(wave_incl_max(r0), carry);
+        carry = bcast_last(r);
+        if (j < n) {
+            uint32_t v = 0;
+            if (j < total) {
+                const uint32_t p = sc.rpos[r];
+                const uint32_t a = sc.aux[p];
+                if (sc.meta[p] & 1u) {
+                    const uint64_t bit = static_cast<uint64_t>(a) * 8u + static_cast<uint64_t>(j - sc.rstart[r]) * bw;
+                    v = bw ? lds_bits(pw, psize, bit, bw) : 0u;
+                } else {
+                    v = a;
+                }
+            }
+            out(j, v);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return 0;
+}
+
+}  // namespace dev
+}  // namespace pqk

@@ -107,12 +107,15 @@ struct FusedLaunch {
     int grid;
     int waves_per_block;
     int debug;
+    uint64_t* prof;  // per-phase cycle sums (fused_prof_slots()), or null
 };
 
 void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
-                       uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any);
+                       uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any,
+                       uint32_t max_dict_bytes);
 void launch_ba_fused(hipStream_t s, const FusedLaunch& L);
 uint32_t fused_wave_bytes(uint32_t rows_cap, uint32_t stage_bytes);
 int fused_occupancy_waves(uint32_t lds_bytes_per_block, int waves_per_block);
+int fused_prof_slots();
 
 }  // namespace pqk

@@ -107,6 +107,7 @@ def lib():
             "pq_timing_enable": ([vp, C.c_int], None),
             "pq_timing_reset": ([vp], None),
             "pq_timing_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)], C.c_int),
+            "pq_fused_prof_read": ([vp, C.POINTER(C.c_uint64), C.c_int], C.c_int),
             "pq_file_open": ([u8p, C.c_size_t, C.POINTER(vp), C.c_char_p, C.c_size_t], C.c_int),
             "pq_file_close": ([vp], None),
             "pq_file_num_rows": ([vp], C.c_int64),
@@ -262,6 +263,16 @@ class Context:
 
     def sync(self):
         self.check(lib().pq_ctx_sync(self.h))
+
+    PROF_PHASES = ("stage", "def", "levels", "values", "rows", "lookback", "slotwait", "pages",
+                   "w_wait", "w_offsets", "w_gather", "w_pages")
+
+    def fused_prof_read(self) -> dict:
+        """Per-phase shader-clock sums of k_ba_fused since the last read
+        (option "fused_prof" must be 1)."""
+        buf = (C.c_uint64 * 16)()
+        k = lib().pq_fused_prof_read(self.h, buf, 16)
+        return {self.PROF_PHASES[i] if i < len(self.PROF_PHASES) else str(i): int(buf[i]) for i in range(k)}
 
 
 class DeviceChunk:

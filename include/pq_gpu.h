@@ -160,6 +160,10 @@ void pq_timing_reset(pq_ctx* ctx);
 /* total milliseconds and launch count of kernel `name` since the last reset
  * (names: see DESIGN.md).  Returns 0 if unknown. */
 int pq_timing_get(pq_ctx* ctx, const char* name, double* total_ms, int64_t* launches);
+/* Per-phase shader-clock sums of the fused BYTE_ARRAY kernel, collected while
+ * option "fused_prof" is 1 (diagnostics).  Copies up to n
+ * counters into out, zeroes them, returns the number of counters. */
+int pq_fused_prof_read(pq_ctx* ctx, uint64_t* out, int n);
 
 /* ── file-level helpers (ParquetReader::open) ───────────────────────────── */
 typedef struct pq_file pq_file;

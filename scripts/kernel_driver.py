@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""Run the C2 decode (or the C3 regex scan) a few times — a small target for
+rocprofv3 PMC passes.  usage: kernel_driver.py [decode|regex] [rows] [reps] [fused_debug]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "duckdb-parquet-parser_amd")]
+from pqgpu import capi, gen  # noqa: E402
+
+what = sys.argv[1] if len(sys.argv) > 1 else "decode"
+rows = int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+dbg = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+ctx = capi.Context(0)
+ctx.set_option("fused_debug", dbg)
+if what == "decode":
+    f = gen.build(gen.c2_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C2"])
+    F = capi.File(f)
+    dc = ctx.upload(f, [F.chunk(0, 0)])
+    for _ in range(reps):
+        dc.decode_async()
+    ctx.sync()
+else:
+    f = gen.build(gen.c3_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C3"])
+    F = capi.File(f)
+    dc = ctx.upload(f, [F.chunk(0, 0)])
+    for _ in range(reps):
+        dc.regex_pages("special.*requests", False)
+    ctx.sync()
+print("done", what, rows, reps)
