@@ -30,6 +30,8 @@ for _p in (ROOT, PKG):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+# kernel timers (HIP events on the decode stream, capi.hip Timed)
+KERNELS = ("dict_index", "dict_entries", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather")
 ROWS = 10_000_000
 
 
@@ -50,8 +52,9 @@ def parse():
 
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
-    summary (profiles/pmc_*.json), corrected per the microarch guide
-    (FETCH_SIZE x2 for wide coalesced reads on gfx950)."""
+    summary (profiles/pmc_latest.json, written by scripts/pmc_summary.py from
+    separate FETCH_SIZE and WRITE_SIZE passes of this same command; FETCH_SIZE
+    doubled for 16-B-per-lane reads on gfx950 as the microarch guide says)."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if not os.path.exists(path):
         return None
@@ -141,7 +144,7 @@ def main():
     dc.decode_check()
     elapsed = t1 - t0
     kern = {}
-    for name in ("dict_entries", "ba_rows", "scan", "ba_gather"):
+    for name in KERNELS:
         ms, n = ctx.timing_get(name)
         if n:
             kern[name] = ms / n
@@ -160,9 +163,14 @@ def main():
     payload = dc.payload_bytes
     out_bytes = 8 * (nrows + 1) + total_chars + (nrows + 7) // 8
     b_alg = payload + out_bytes  # SURVEY §8d C2 algorithmic bytes per decode
-    dom = max(kern, key=kern.get) if kern else "ba_gather"
+    dom = max(kern, key=kern.get) if kern else "ba_fused"
     dom_ms = kern.get(dom, ms_per_step)
-    dom_bytes = out_bytes if dom == "ba_gather" else payload
+    # algorithmic bytes of one launch of the dominant kernel:
+    # the fused/batched kernels read every page payload once and write the
+    # whole column (offsets, characters, validity); the generic pipeline's
+    # stages split that between them.
+    dom_bytes = {"ba_fused": b_alg, "ba_batch": b_alg, "ba_gather": out_bytes,
+                 "ba_rows": payload + 8 * nrows}.get(dom, payload)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     step_kernel_ms = sum(kern.values())
 

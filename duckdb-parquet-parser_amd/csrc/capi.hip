@@ -39,7 +39,9 @@ struct pq_ctx {
     bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
     int opt_debug = 0;      // "fused_debug": ablation switches for timing studies
     int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
-    uint64_t* d_prof = nullptr;  // "fused_prof": per-phase cycle sums of k_ba_fused
+    uint64_t* d_prof = nullptr;  // "fused_prof": per-phase cycle sums of k_ba_fused / k_ba_batch
+    bool opt_batch = false;      // "batch": batched dictionary path (dict_batch.hip)
+    int opt_batch_bytes = 12288; // "batch_bytes": payload bytes per batch buffer
 };
 
 struct pq_chunk {
@@ -84,7 +86,15 @@ struct pq_chunk {
         int32_t p0 = 0, np = 0, dict_id = -1;
         uint32_t rows_cap = 0, stage_bytes = 0, wave_bytes = 0, dict_bytes = 0, dict_chars_bytes = 0;
         int waves = 0, grid = 0;
+        // batched dictionary path (dict_batch.hip)
+        bool batch = false;
+        int32_t batch0 = 0, nbatches = 0;
+        uint32_t batch_bytes = 0, max_slot = 0, blds = 0;
+        int bwriters = 0, bgrid = 0;
     };
+    std::vector<pqk::DevBatch> hbatches;
+    pqk::DevBatch* d_batches = nullptr;
+    uint64_t* d_bstatus = nullptr;
     std::vector<Range> ranges;
     bool fused = false;
     uint64_t* d_status = nullptr;
@@ -203,6 +213,8 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_status);
     dfree(c->d_tickets);
     dfree(c->d_bases);
+    dfree(c->d_batches);
+    dfree(c->d_bstatus);
     if (c->d_prog) { pqre::free_device_program(c->d_prog); c->d_prog = nullptr; }
 }
 
@@ -241,6 +253,50 @@ void plan_fused(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages,
             int64_t ecap = std::min<int64_t>(d.nvals, d.size / 4 + 1);
             r.dict_chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
             r.dict_bytes = r.dict_chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
+        }
+        // batched path: every page dictionary-encoded, small pages and rows
+        r.batch = false;
+        if (ctx->opt_batch && dict_id >= 0 && r.rows_cap <= 1024) {
+            bool all_dict = true;
+            uint32_t max_slot = 0;
+            for (int p = r.p0; p < r.p0 + r.np; p++) {
+                all_dict &= pages[p].mode == pqk::MODE_DICT;
+                max_slot = std::max(max_slot, (static_cast<uint32_t>(std::max(pages[p].size, 0)) + 15) / 16 * 16 + 16);
+            }
+            const uint32_t pb = std::max<uint32_t>(static_cast<uint32_t>(ctx->opt_batch_bytes), max_slot);
+            const pqk::BatchPlan bp = pqk::plan_batch_lds(r.rows_cap, pb, max_slot, r.dict_bytes);
+            if (all_dict && max_slot <= 32768 && bp.writers >= 2) {
+                r.batch = true;
+                r.batch_bytes = pb;
+                r.max_slot = max_slot;
+                r.bwriters = bp.writers;
+                r.blds = bp.lds;
+                r.batch0 = static_cast<int32_t>(c->hbatches.size());
+                int p = r.p0;
+                const int pend = r.p0 + r.np;
+                while (p < pend) {
+                    pqk::DevBatch b{};
+                    b.p0 = p;
+                    b.img_lo = pages[p].off;
+                    uint64_t hi = b.img_lo;
+                    int q = p;
+                    while (q < pend && q - p < 64) {
+                        const uint64_t e = pages[q].off + (static_cast<uint64_t>(std::max(pages[q].size, 0)) + 15) / 16 * 16 + 16;
+                        if (e - b.img_lo > pb) break;
+                        hi = e;
+                        q++;
+                    }
+                    b.np = q - p;
+                    b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
+                    c->hbatches.push_back(b);
+                    p = q;
+                }
+                r.nbatches = static_cast<int32_t>(c->hbatches.size()) - r.batch0;
+                int per_cu = pqk::batch_occupancy(r.blds, 1 + r.bwriters);
+                if (per_cu < 1) per_cu = 1;
+                r.bgrid = std::max(1, std::min(per_cu * cus, r.nbatches));
+                continue;
+            }
         }
         if (r.dict_bytes + r.wave_bytes > kLds) return;
         // producer/writer pairs per workgroup (dict_fused.hip)
@@ -294,6 +350,12 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "fused_ba") == 0) { ctx->opt_fused = value != 0; return 0; }
     if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "fused_waves") == 0) { ctx->opt_waves = static_cast<int>(value); return 0; }
+    if (std::strcmp(key, "batch") == 0) { ctx->opt_batch = value != 0; return 0; }
+    if (std::strcmp(key, "batch_bytes") == 0) {
+        if (value < 1024 || value > 65536 || value % 16) return set_err(ctx, PQ_ERR_ARG, "batch_bytes: 1024..65536, multiple of 16");
+        ctx->opt_batch_bytes = static_cast<int>(value);
+        return 0;
+    }
     if (std::strcmp(key, "fused_prof") == 0) {
         if (value && !ctx->d_prof) {
             if (hipMalloc(reinterpret_cast<void**>(&ctx->d_prof), 64 * sizeof(uint64_t)) != hipSuccess)
@@ -450,6 +512,10 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         rc |= dalloc(&c->d_total, 1);
         rc |= dalloc(&c->d_scan_scratch, htiles.size() / 8192 + 16);
         if (c->type == PQ_BYTE_ARRAY && !c->fused) rc |= dalloc(&c->d_row_codes, static_cast<size_t>(c->nrows));
+        if (c->fused && !c->hbatches.empty()) {
+            rc |= dalloc(&c->d_batches, c->hbatches.size());
+            rc |= dalloc(&c->d_bstatus, c->hbatches.size());
+        }
         if (c->fused) {
             rc |= dalloc(&c->d_status, hpages.size());
             rc |= dalloc(&c->d_tickets, c->ranges.size());
@@ -475,6 +541,8 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc = hip_check(ctx, hipMemcpyAsync(c->d_tiles, htiles.data(), htiles.size() * sizeof(DevTile), hipMemcpyHostToDevice, s), "upload");
         if (!rc && !tile0.empty())
             rc = hip_check(ctx, hipMemcpyAsync(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
+        if (!rc && c->d_batches)
+            rc = hip_check(ctx, hipMemcpyAsync(c->d_batches, c->hbatches.data(), c->hbatches.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice, s), "upload");
         if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
         if (rc) {
             free_chunk_device(c.get());
@@ -582,10 +650,28 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         (void)hipMemsetAsync(c->d_status, 0, std::max<size_t>(c->npages, 1) * sizeof(uint64_t), s);
         (void)hipMemsetAsync(c->d_tickets, 0, nr * sizeof(int32_t), s);
         (void)hipMemsetAsync(c->d_bases, 0, (nr + 1) * sizeof(int64_t), s);
+        if (c->d_bstatus) (void)hipMemsetAsync(c->d_bstatus, 0, c->hbatches.size() * sizeof(uint64_t), s);
         for (size_t k = 0; k < nr; k++) {
             const auto& r = c->ranges[k];
             if (r.np == 0) {
                 (void)hipMemcpyAsync(c->d_bases + k + 1, c->d_bases + k, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+                continue;
+            }
+            if (r.batch) {
+                pqk::BatchLaunch B{};
+                B.bytes = c->d_bytes; B.pages = c->d_pages; B.batches = c->d_batches + r.batch0;
+                B.nbatches = r.nbatches; B.last_page = r.p0 + r.np - 1;
+                B.dicts = c->d_dicts; B.dict_id = r.dict_id; B.entries = c->d_entries; B.dict_count = c->d_dict_count;
+                B.max_def = c->max_def; B.max_rep = c->max_rep; B.rows_cap = r.rows_cap;
+                B.batch_bytes = r.batch_bytes; B.max_slot = r.max_slot; B.dict_bytes = r.dict_bytes;
+                B.dict_chars_bytes = r.dict_chars_bytes; B.status = c->d_bstatus + r.batch0;
+                B.ticket = c->d_tickets + k; B.base_in = c->d_bases + k; B.base_out = c->d_bases + k + 1;
+                B.nrows_total = c->nrows; B.validity = out->d_validity; B.offsets = out->d_offsets;
+                B.chars = out->d_values; B.capacity = out->capacity_bytes; B.overflow = c->d_flags + 1;
+                B.page_err = c->d_page_err; B.err_any = c->d_flags; B.debug = ctx->opt_debug; B.prof = ctx->d_prof;
+                B.grid = r.bgrid; B.writers = r.bwriters; B.lds = r.blds;
+                Timed t(ctx, "ba_batch");
+                pqk::launch_ba_batch(s, B);
                 continue;
             }
             pqk::FusedLaunch L{};
@@ -734,7 +820,7 @@ int pq_timing_get(pq_ctx* ctx, const char* name, double* total_ms, int64_t* laun
 
 int pq_fused_prof_read(pq_ctx* ctx, uint64_t* out, int n) {
     if (!ctx || !ctx->d_prof) return 0;
-    const int k = pqk::fused_prof_slots();
+    const int k = std::max(pqk::fused_prof_slots(), pqk::batch_prof_slots());
     std::vector<uint64_t> h(static_cast<size_t>(k));
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
     if (hipMemcpy(h.data(), ctx->d_prof, k * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return 0;

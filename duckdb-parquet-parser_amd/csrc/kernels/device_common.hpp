@@ -174,18 +174,37 @@ __device__ __forceinline__ void set_err(DevErr* e, int32_t* any, int code, uint3
 }
 
 
-// Inclusive wave prefix sum of a u32.
+// ── wave primitives on DPP (no LDS round trip; gfx9 row_bcast15/31) ───────
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), kCtrl, kRowMask, 0xf, true));
+}
+
+// Inclusive wave prefix sum / max of a u32 (all 64 lanes active).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, kWave);
-        if (lane() >= static_cast<uint32_t>(d)) v += t;
-    }
+    v += dpp0<0x111>(v);        // row_shr:1
+    v += dpp0<0x112>(v);        // row_shr:2
+    v += dpp0<0x114>(v);        // row_shr:4
+    v += dpp0<0x118>(v);        // row_shr:8
+    v += dpp0<0x142, 0xa>(v);   // row_bcast:15 -> rows 1, 3
+    v += dpp0<0x143, 0xc>(v);   // row_bcast:31 -> rows 2, 3
     return v;
 }
-__device__ __forceinline__ uint32_t bcast_last(uint32_t v) { return __shfl(v, kWave - 1, kWave); }
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, dpp0<0x111>(v));
+    v = max(v, dpp0<0x112>(v));
+    v = max(v, dpp0<0x114>(v));
+    v = max(v, dpp0<0x118>(v));
+    v = max(v, dpp0<0x142, 0xa>(v));
+    v = max(v, dpp0<0x143, 0xc>(v));
+    return v;
+}
+__device__ __forceinline__ uint32_t bcast_last(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), kWave - 1));
+}
 __device__ __forceinline__ uint32_t popc_below(uint64_t m) {
-    return __popcll(m & ((1ull << lane()) - 1ull));
+    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
 }
 
 }  // namespace dev

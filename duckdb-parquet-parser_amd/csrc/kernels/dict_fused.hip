@@ -42,6 +42,8 @@ constexpr uint64_t kInc = 2ull << 62;
 constexpr uint64_t kValMask = (1ull << 62) - 1;
 constexpr uint32_t kGatherWin = 512;  // 16-byte blocks per gather window
 constexpr uint32_t kLitCap = 16;      // recorded bit-packed runs per wave between expansions (serial walk)
+constexpr uint32_t kRingBytes = 2048;  // writer's character ring (power of two, >= 2 * kGatherWin)
+constexpr uint32_t kRingMaxRow = kRingBytes / 2 - 32;  // longer rows take the gather fallback
 
 // ── dictionary entry table ─────────────────────────────────────────────────
 constexpr int kDictWaves = 16;
@@ -220,7 +222,9 @@ struct SlotMeta {
     uint32_t n;        // rows
     uint32_t total;    // characters
     uint32_t dict;     // characters come from the dictionary (else the page)
+    uint32_t maxlen;   // longest row
     uint32_t state;    // SLOT_*
+    uint32_t pad;
 };
 
 struct Slot {
@@ -268,8 +272,8 @@ __host__ __device__ inline PairLayout pair_layout(uint32_t rows_cap, uint32_t st
     L.s_rsrc = o; o += al16(2 * rows_cap);
     L.s_vm = o; o += al16(8 * (rows_cap / 64 + 1));
     L.slot = o;
-    L.w_brow = 0;
-    L.writer = al16(2 * kGatherWin);
+    L.w_brow = 0;  // gather fallback: block -> row map, aliases the ring
+    L.writer = kRingBytes > 2 * kGatherWin ? kRingBytes : 2 * kGatherWin;
     L.bytes = L.prod + 2 * L.slot + L.writer;
     return L;
 }
@@ -391,7 +395,7 @@ __device__ void produce(const FusedArgs& a, const PairLayout& L, uint8_t* pair, 
     for (;;) {
         int32_t t = 0;
         if (lane() == 0) t = atomicAdd(a.ticket, 1);
-        t = static_cast<int32_t>(suni(static_cast<uint32_t>(__shfl(t, 0, kWave))));
+        t = static_cast<int32_t>(suni(static_cast<uint32_t>(t)));
         Slot S = slot_at(slots + si * L.slot, L);
         flag_wait(S.meta, true);
         P.mark(PH_SLOTWAIT);
@@ -502,6 +506,7 @@ __device__ void produce(const FusedArgs& a, const PairLayout& L, uint8_t* pair, 
         P.mark(PH_VALUES);
         // 3. per-row source/length, page-local offsets, validity ballots
         uint64_t total = 0;
+        uint32_t maxlen = 0;
         if (!code) {
             uint32_t rank = 0, run = 0;
             for (uint32_t j0 = 0; j0 < n; j0 += kWave) {
@@ -530,6 +535,7 @@ __device__ void produce(const FusedArgs& a, const PairLayout& L, uint8_t* pair, 
                     }
                 }
                 uint32_t inc = wave_incl_scan(len);
+                maxlen = max(maxlen, len);
                 if (in) {
                     S.off[j] = run + inc - len;
                     S.rsrc[j] = static_cast<uint16_t>(src);
@@ -567,17 +573,135 @@ __device__ void produce(const FusedArgs& a, const PairLayout& L, uint8_t* pair, 
             S.meta->total = static_cast<uint32_t>(total);
             S.meta->dict = dict;
         }
+        {
+            const uint32_t ml = wave_incl_max(maxlen);
+            if (lane() == kWave - 1) S.meta->maxlen = ml;
+        }
         flag_set(S.meta, SLOT_FULL);
         si ^= 1;
     }
     P.flush(a.prof);
 }
 
+// Store the bytes [lo, hi) of one 16-byte block (global byte blk) held in
+// `v`: a whole block as one 16-byte store, a partial one byte by byte (the
+// rest of that block belongs to the neighbouring page).
+__device__ __forceinline__ void store_block(uint8_t* chars, int64_t blk, uint32_t lo, uint32_t hi, uint4 v) {
+    if (lo == 0 && hi == 16) {
+        *reinterpret_cast<uint4*>(chars + blk) = v;
+    } else {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (uint32_t bb = lo; bb < hi; bb++) chars[blk + bb] = static_cast<uint8_t>(w[bb >> 2] >> (8 * (bb & 3)));
+    }
+}
+
+// Characters of one page, input-driven: one row per lane copies its bytes
+// into an LDS ring indexed by global byte address (so ring blocks line up
+// with 16-byte output blocks); completed blocks are streamed out and zeroed.
+__device__ void copy_chars(const FusedArgs& a, const Slot& S, uint32_t* ring, const uint32_t* srcw, uint32_t n,
+                           int64_t G0, int64_t G1) {
+    constexpr uint32_t kRingMask = kRingBytes / 4 - 1;  // in words
+    int64_t fb = G0 >> 4;  // first block not yet stored
+    uint32_t r0 = 0;
+    while (r0 < n) {
+        // rows [r0, r1): at most one per lane, ending within the ring's reach
+        const uint32_t r = r0 + lane();
+        const uint32_t e = r < n ? S.off[r + 1] : 0xFFFFFFFFu;
+        const int64_t limit = fb * 16 + kRingBytes - 16;
+        const uint64_t fit = __ballot(r < n && G0 + static_cast<int64_t>(e) <= limit);
+        const uint32_t k = fit == ~0ull ? kWave : static_cast<uint32_t>(__builtin_ctzll(~fit));
+        const uint32_t cnt = k ? k : 1u;  // a row longer than the ring never reaches here
+        if (lane() < cnt) {
+            const uint32_t s0 = S.off[r];
+            const uint32_t L = e - s0;
+            const uint32_t src = S.rsrc[r];
+            int64_t d = G0 + s0;
+            uint32_t q = 0;
+            while (q < L) {
+                const uint32_t lo = static_cast<uint32_t>(d & 3);
+                const uint32_t take = min(4u - lo, L - q);
+                const uint32_t x = lds_u32(srcw, src + q);
+                const uint32_t m = take == 4 ? 0xFFFFFFFFu : ((1u << (8 * take)) - 1u);
+                const uint32_t v = (x & m) << (8 * lo);
+                const uint32_t wi = static_cast<uint32_t>(d >> 2) & kRingMask;
+                if (take == 4) ring[wi] = v;
+                else atomicOr(&ring[wi], v);
+                q += take;
+                d += take;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t r1 = r0 + cnt;
+        const int64_t end = G0 + static_cast<int64_t>(S.off[r1]);
+        const int64_t lb = r1 >= n ? ((end + 15) >> 4) : (end >> 4);  // blocks [fb, lb) are complete
+        for (int64_t b = fb + lane(); b < lb; b += kWave) {
+            uint4* rb = reinterpret_cast<uint4*>(ring + ((static_cast<uint32_t>(b) * 4) & kRingMask));
+            const uint4 v = *rb;
+            *rb = make_uint4(0, 0, 0, 0);
+            const int64_t blk = b << 4;
+            const uint32_t lo = blk < G0 ? static_cast<uint32_t>(G0 - blk) : 0u;
+            const uint32_t hi = blk + 16 > G1 ? static_cast<uint32_t>(G1 - blk) : 16u;
+            if (!(a.debug & 16)) store_block(a.chars, blk, lo, hi, v);
+        }
+        __builtin_amdgcn_wave_barrier();
+        fb = lb;
+        r0 = r1;
+    }
+}
+
+// Output-driven fallback for pages with rows longer than the ring allows:
+// each lane assembles one 16-byte block from the rows that cover it.
+__device__ void gather_chars(const FusedArgs& a, const Slot& S, uint32_t* ringw, const uint32_t* srcw, uint32_t n,
+                             int64_t G0, int64_t G1) {
+    uint16_t* brow = reinterpret_cast<uint16_t*>(ringw);
+    const int64_t B0 = G0 >> 4;
+    const int64_t nb = ((G1 - 1) >> 4) - B0 + 1;
+    for (int64_t w0 = 0; w0 < nb; w0 += kGatherWin) {
+        const int64_t w1 = min(nb, w0 + static_cast<int64_t>(kGatherWin));
+        for (uint32_t r = lane(); r < n; r += kWave) {
+            uint32_t s0 = S.off[r], e0 = S.off[r + 1];
+            if (e0 <= s0) continue;
+            int64_t blo = s0 == 0 ? 0 : ((s0 + G0 + 15) >> 4) - B0;
+            int64_t bhi = ((e0 + G0 + 15) >> 4) - B0 - 1;
+            blo = max(blo, w0);
+            bhi = min(bhi, w1 - 1);
+            for (int64_t b = blo; b <= bhi; b++) brow[b - w0] = static_cast<uint16_t>(r);
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int64_t b = w0 + lane(); b < w1; b += kWave) {
+            const int64_t blk = (B0 + b) << 4;
+            const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
+            uint32_t r = brow[b - w0];
+            uint32_t q = static_cast<uint32_t>(gs - G0);  // page-local output byte
+            uint32_t o = static_cast<uint32_t>(gs - blk);
+            const uint32_t oe = static_cast<uint32_t>(ge - blk);
+            uint32_t rend = S.off[r + 1];
+            uint32_t out[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                uint32_t lo = max(4 * k, o), hi = min(4 * k + 4, oe);
+                if (lo >= hi) continue;
+                for (uint32_t bb = lo; bb < hi; bb++) {
+                    uint32_t qb = q + (bb - o);
+                    while (qb >= rend && r + 1 < n) { r++; rend = S.off[r + 1]; }
+                    uint32_t sa = S.rsrc[r] + (qb - S.off[r]);
+                    out[k] |= lds_u8(srcw, sa) << (8 * (bb & 3));
+                }
+            }
+            store_block(a.chars, blk, o, oe, make_uint4(out[0], out[1], out[2], out[3]));
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // ── writer: offsets, validity and characters of the pages handed over ──────
 template <bool kProf>
 __device__ void write_pages(const FusedArgs& a, const PairLayout& L, uint8_t* pair, const uint32_t* dwords) {
     uint8_t* slots = pair + L.prod;
-    uint16_t* brow = reinterpret_cast<uint16_t*>(pair + L.prod + 2 * L.slot + L.w_brow);
+    uint32_t* ring = reinterpret_cast<uint32_t*>(pair + L.prod + 2 * L.slot + L.w_brow);
+    for (uint32_t i = lane(); i < kRingBytes / 16; i += kWave)
+        reinterpret_cast<uint4*>(ring)[i] = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
     Prof<kProf> P;
     P.start();
     uint32_t si = 0;
@@ -632,65 +756,16 @@ __device__ void write_pages(const FusedArgs& a, const PairLayout& L, uint8_t* pa
         }
         P.mark(PH_W_OFFSETS);
         const int64_t G1 = G0 + static_cast<int64_t>(total);
+        const uint32_t* srcw = dict ? dwords : S.stage;
         if (total && !(a.debug & 2) && G1 > a.capacity) {
             if (lane() == 0) atomicOr(a.overflow, 1);
+        } else if (total && !(a.debug & 2) && __builtin_amdgcn_readfirstlane(S.meta->maxlen) <= kRingMaxRow) {
+            copy_chars(a, S, ring, srcw, n, G0, G1);
         } else if (total && !(a.debug & 2)) {
-            // characters: 16-byte blocks of the global char stream
-            const uint32_t* srcw = dict ? dwords : S.stage;
-            const int64_t B0 = G0 >> 4;
-            const int64_t nb = ((G1 - 1) >> 4) - B0 + 1;
-            for (int64_t w0 = 0; w0 < nb; w0 += kGatherWin) {
-                const int64_t w1 = min(nb, w0 + static_cast<int64_t>(kGatherWin));
-                for (uint32_t r = lane(); r < n && !(a.debug & 32); r += kWave) {
-                    uint32_t s0 = S.off[r], e0 = S.off[r + 1];
-                    if (e0 <= s0) continue;
-                    int64_t blo = s0 == 0 ? 0 : ((s0 + G0 + 15) >> 4) - B0;
-                    int64_t bhi = ((e0 + G0 + 15) >> 4) - B0 - 1;
-                    blo = max(blo, w0);
-                    bhi = min(bhi, w1 - 1);
-                    for (int64_t b = blo; b <= bhi; b++) brow[b - w0] = static_cast<uint16_t>(r);
-                }
-                __builtin_amdgcn_wave_barrier();
-                for (int64_t b = w0 + lane(); b < w1; b += kWave) {
-                    const int64_t blk = (B0 + b) << 4;
-                    const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
-                    uint32_t r = (a.debug & 32) ? 0u : brow[b - w0];
-                    uint32_t q = static_cast<uint32_t>(gs - G0);  // page-local output byte
-                    uint32_t o = static_cast<uint32_t>(gs - blk);
-                    const uint32_t oe = static_cast<uint32_t>(ge - blk);
-                    uint32_t rend = S.off[r + 1];
-                    uint32_t out[4] = {0, 0, 0, 0};
-#pragma unroll
-                    for (uint32_t k = 0; k < 4; k++) {
-                        uint32_t lo = max(4 * k, o), hi = min(4 * k + 4, oe);
-                        if (lo >= hi || (a.debug & 8)) continue;
-                        uint32_t ql = q + (lo - o);
-                        while (ql >= rend && r + 1 < n) { r++; rend = S.off[r + 1]; }
-                        if (ql + (hi - lo) <= rend) {
-                            uint32_t sa = S.rsrc[r] + (ql - S.off[r]);
-                            uint32_t x = lds_u32(srcw, sa - (lo - 4 * k));
-                            uint32_t m = (hi - lo == 4) ? 0xFFFFFFFFu : (((1u << (8 * (hi - lo))) - 1u) << (8 * (lo - 4 * k)));
-                            out[k] |= x & m;
-                        } else {
-                            for (uint32_t bb = lo; bb < hi; bb++) {
-                                uint32_t qb = q + (bb - o);
-                                while (qb >= rend && r + 1 < n) { r++; rend = S.off[r + 1]; }
-                                uint32_t sa = S.rsrc[r] + (qb - S.off[r]);
-                                out[k] |= lds_u8(srcw, sa) << (8 * (bb & 3));
-                            }
-                        }
-                    }
-                    if (a.debug & 16) {
-                        if ((out[0] ^ out[1] ^ out[2] ^ out[3]) == 0x9e3779b9u) atomicOr(a.overflow, 2);
-                    } else if (o == 0 && oe == 16) {
-                        *reinterpret_cast<uint4*>(a.chars + blk) = make_uint4(out[0], out[1], out[2], out[3]);
-                    } else {
-                        for (uint32_t bb = o; bb < oe; bb++)
-                            a.chars[blk + bb] = static_cast<uint8_t>(out[bb >> 2] >> (8 * (bb & 3)));
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
+            gather_chars(a, S, ring, srcw, n, G0, G1);
+            for (uint32_t i = lane(); i < kRingBytes / 16; i += kWave)
+                reinterpret_cast<uint4*>(ring)[i] = make_uint4(0, 0, 0, 0);
+            __builtin_amdgcn_wave_barrier();
         }
         P.mark(PH_W_GATHER);
         flag_set(S.meta, SLOT_FREE);

@@ -71,15 +71,6 @@ __device__ __forceinline__ uint64_t lds_u64(const uint32_t* w, uint32_t a) {
     return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, kWave);
-        if (lane() >= static_cast<uint32_t>(d)) v = max(v, t);
-    }
-    return v;
-}
-
 // Decode the first n values of the stream at page bytes [base, base + S)
 // (page words `pw`, page size `psize`) with bit width bw.  out(j, v) for
 // j < n.  R: n u16 slots of LDS scratch (may alias the output array when
@@ -88,60 +79,85 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
 template <class Out>
 __device__ int hyb_decode(const uint32_t* pw, uint32_t psize, uint32_t base, uint32_t S, uint32_t bw,
                           uint32_t n, const HybScratch& sc, uint32_t maxruns, uint16_t* R, Out&& out) {
+    constexpr uint32_t U = 4;  // positions / outputs per lane per batch (loads issued together)
     if (n == 0) return 0;
     if (S > kHybMaxPos || bw > 32) return 1;
     const uint32_t nb = (bw + 7) / 8;
     // A. parse a header at every position
-    bool serial = false;
-    for (uint32_t p = lane(); p < S; p += kWave) {
-        const uint32_t rem = S - p;
-        uint64_t x = lds_u64(pw, base + p);
-        if (rem < 8) x &= (1ull << (8 * rem)) - 1ull;
-        const uint32_t vb = min(rem, 5u);  // varint bytes available
-        const uint64_t stops = ~x & 0x8080808080ull & ((1ull << (8 * vb)) - 1ull);
-        uint32_t meta = 0, next = S, count = 0, aux = 0;
-        if (stops == 0) {
-            meta = 2;
-        } else {
-            const uint32_t hl = (static_cast<uint32_t>(__builtin_ctzll(stops)) >> 3) + 1;
-            uint64_t v = (x & 0x7full) | ((x >> 1) & 0x3f80ull) | ((x >> 2) & 0x1fc000ull) |
-                         ((x >> 3) & 0xfe00000ull) | ((x >> 4) & 0x7f0000000ull);
-            v &= (1ull << (7 * hl)) - 1ull;
-            const uint32_t ind = static_cast<uint32_t>(v);
-            if (ind & 1u) {
-                count = (ind >> 1) * 8u;
-                const uint64_t end = static_cast<uint64_t>(p) + hl + (static_cast<uint64_t>(count) * bw + 7) / 8;
-                next = end >= S ? S : static_cast<uint32_t>(end);
-                aux = base + p + hl;
-                meta = 1;
-            } else {
-                count = ind >> 1;
-                const uint32_t take = min(nb, rem - hl);
-                if (hl + take > 8) meta = 2;
-                aux = take ? static_cast<uint32_t>((x >> (8 * hl)) & ((take >= 4) ? 0xFFFFFFFFull
-                                                                                  : ((1ull << (8 * take)) - 1ull)))
-                           : 0u;
-                next = min(S, p + hl + take);
-            }
-            if (count == 0) meta = 2;
+    for (uint32_t p0 = 0; p0 < S; p0 += U * kWave) {
+        uint64_t xs[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t p = p0 + u * kWave + lane();
+            xs[u] = p < S ? lds_u64(pw, base + p) : 0ull;
         }
-        sc.nx0[p] = static_cast<uint16_t>(next);
-        sc.cnt[p] = static_cast<uint16_t>(min(count, 65535u));
-        sc.aux[p] = aux;
-        sc.meta[p] = static_cast<uint8_t>(meta);
-        sc.on[p] = p == 0;
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t p = p0 + u * kWave + lane();
+            if (p >= S) continue;
+            const uint32_t rem = S - p;
+            uint64_t x = xs[u];
+            if (rem < 8) x &= (1ull << (8 * rem)) - 1ull;
+            const uint32_t vb = min(rem, 5u);  // varint bytes available
+            const uint64_t stops = ~x & 0x8080808080ull & ((1ull << (8 * vb)) - 1ull);
+            uint32_t meta = 0, next = S, count = 0, aux = 0;
+            if (stops == 0) {
+                meta = 2;
+            } else {
+                const uint32_t hl = (static_cast<uint32_t>(__builtin_ctzll(stops)) >> 3) + 1;
+                uint64_t v = (x & 0x7full) | ((x >> 1) & 0x3f80ull) | ((x >> 2) & 0x1fc000ull) |
+                             ((x >> 3) & 0xfe00000ull) | ((x >> 4) & 0x7f0000000ull);
+                v &= (1ull << (7 * hl)) - 1ull;
+                const uint32_t ind = static_cast<uint32_t>(v);
+                if (ind & 1u) {
+                    count = (ind >> 1) * 8u;
+                    const uint64_t end = static_cast<uint64_t>(p) + hl + (static_cast<uint64_t>(count) * bw + 7) / 8;
+                    next = end >= S ? S : static_cast<uint32_t>(end);
+                    aux = base + p + hl;
+                    meta = 1;
+                } else {
+                    count = ind >> 1;
+                    const uint32_t take = min(nb, rem - hl);
+                    if (hl + take > 8) meta = 2;
+                    aux = take ? static_cast<uint32_t>((x >> (8 * hl)) &
+                                                       ((take >= 4) ? 0xFFFFFFFFull : ((1ull << (8 * take)) - 1ull)))
+                               : 0u;
+                    next = min(S, p + hl + take);
+                }
+                if (count == 0) meta = 2;
+            }
+            sc.nx0[p] = static_cast<uint16_t>(next);
+            sc.cnt[p] = static_cast<uint16_t>(min(count, 65535u));
+            sc.aux[p] = aux;
+            sc.meta[p] = static_cast<uint8_t>(meta);
+            sc.on[p] = p == 0;
+        }
     }
     if (lane() == 0) { sc.nx0[S] = static_cast<uint16_t>(S); sc.nx1[S] = static_cast<uint16_t>(S); sc.on[S] = 0; }
     __builtin_amdgcn_wave_barrier();
-    // B. chain membership by pointer doubling
+    // B. chain membership by pointer doubling: on |= J(on), J = J o J
     uint16_t* J = sc.nx0;
     uint16_t* K = sc.nx1;
     for (;;) {
         const uint32_t j0 = __builtin_amdgcn_readfirstlane(J[0]);
         if (j0 >= S) break;
-        for (uint32_t p = lane(); p < S; p += kWave)
-            if (sc.on[p]) sc.on[J[p]] = 1;
-        for (uint32_t p = lane(); p < S; p += kWave) K[p] = J[J[p]];
+        for (uint32_t p0 = 0; p0 < S; p0 += U * kWave) {
+            uint32_t jp[U], o[U], jj[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t p = p0 + u * kWave + lane();
+                jp[u] = p < S ? J[p] : S;
+                o[u] = p < S ? sc.on[p] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) jj[u] = J[jp[u]];
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t p = p0 + u * kWave + lane();
+                if (p < S) K[p] = static_cast<uint16_t>(jj[u]);
+                if (o[u]) sc.on[jp[u]] = 1;
+            }
+        }
         __builtin_amdgcn_wave_barrier();
         uint16_t* t = J; J = K; K = t;
     }
@@ -149,52 +165,74 @@ __device__ int hyb_decode(const uint32_t* pw, uint32_t psize, uint32_t base, uin
     // C. run starts (prefix of lengths in byte order), run list, serial check
     for (uint32_t j = lane(); j < n; j += kWave) R[j] = 0;
     __builtin_amdgcn_wave_barrier();
+    bool serial = false;
     uint32_t csum = 0, rsum = 0;
-    for (uint32_t p0 = 0; p0 < S; p0 += kWave) {
-        const uint32_t p = p0 + lane();
-        const bool o = p < S && sc.on[p];
-        const uint32_t c = o ? sc.cnt[p] : 0u;
-        const uint32_t ci = wave_incl_scan(c);
-        const uint64_t om = __ballot(o);
-        const uint32_t st = csum + ci - c;
-        const uint32_t ri = rsum + popc_below(om);
-        if (o && st < n) {
-            serial |= (sc.meta[p] & 2u) != 0;
-            if (ri < maxruns) {
-                sc.rpos[ri] = static_cast<uint16_t>(p);
-                sc.rstart[ri] = static_cast<uint16_t>(st);
-                R[st] = static_cast<uint16_t>(ri);
-            } else {
-                serial = true;
-            }
+    for (uint32_t p0 = 0; p0 < S && csum < n; p0 += U * kWave) {
+        uint32_t o[U], c[U], m[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t p = p0 + u * kWave + lane();
+            o[u] = p < S ? sc.on[p] : 0u;
+            c[u] = p < S ? sc.cnt[p] : 0u;
+            m[u] = p < S ? sc.meta[p] : 0u;
         }
-        csum += bcast_last(ci);
-        rsum += __popcll(om);
-        if (csum >= n) break;
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t p = p0 + u * kWave + lane();
+            const bool on = o[u] != 0;
+            const uint32_t cc = on ? c[u] : 0u;
+            const uint32_t ci = wave_incl_scan(cc);
+            const uint64_t om = __ballot(on);
+            const uint32_t st = csum + ci - cc;
+            const uint32_t ri = rsum + popc_below(om);
+            if (on && st < n) {
+                serial |= (m[u] & 2u) != 0;
+                if (ri < maxruns) {
+                    sc.rpos[ri] = static_cast<uint16_t>(p);
+                    sc.rstart[ri] = static_cast<uint16_t>(st);
+                    R[st] = static_cast<uint16_t>(ri);
+                } else {
+                    serial = true;
+                }
+            }
+            csum += bcast_last(ci);
+            rsum += __popcll(om);
+        }
     }
     if (__ballot(serial)) return 1;
     __builtin_amdgcn_wave_barrier();
     // D. run of every output (max-scan) and expansion
     const uint32_t total = csum;
     uint32_t carry = 0;
-    for (uint32_t j0 = 0; j0 < n; j0 += kWave) {
-        const uint32_t j = j0 + lane();
-        const uint32_t r0 = j < n ? R[j] : 0u;
-        const uint32_t r = max(wave_incl_max(r0), carry);
-        carry = bcast_last(r);
-        if (j < n) {
-            uint32_t v = 0;
-            if (j < total) {
-                const uint32_t p = sc.rpos[r];
-                const uint32_t a = sc.aux[p];
-                if (sc.meta[p] & 1u) {
-                    const uint64_t bit = static_cast<uint64_t>(a) * 8u + static_cast<uint64_t>(j - sc.rstart[r]) * bw;
-                    v = bw ? lds_bits(pw, psize, bit, bw) : 0u;
-                } else {
-                    v = a;
-                }
-            }
-            out(j, v);
+    for (uint32_t j0 = 0; j0 < n; j0 += U * kWave) {
+        uint32_t r[U], rp[U], rs[U], av[U], me[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t j = j0 + u * kWave + lane();
+            r[u] = j < n ? R[j] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            r[u] = max(wave_incl_max(r[u]), carry);
+            carry = bcast_last(r[u]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            rp[u] = sc.rpos[r[u]];
+            rs[u] = sc.rstart[r[u]];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            av[u] = sc.aux[rp[u]];
+            me[u] = sc.meta[rp[u]];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t j = j0 + u * kWave + lane();
+            // literal: bits of value (j - start); RLE: the run value
+            const uint64_t bit = static_cast<uint64_t>(av[u]) * 8u + static_cast<uint64_t>(j - rs[u]) * bw;
+            const uint32_t lit = (me[u] & 1u) && bw && j < total ? lds_bits(pw, psize, bit, bw) : 0u;
+            if (j < n) out(j, j >= total ? 0u : ((me[u] & 1u) ? lit : av[u]));
         }
     }
     __builtin_amdgcn_wave_barrier();

@@ -110,6 +110,54 @@ struct FusedLaunch {
     uint64_t* prof;  // per-phase cycle sums (fused_prof_slots()), or null
 };
 
+// ── batched dictionary BYTE_ARRAY path (dict_batch.hip) ────────────────────
+// A run of consecutive data pages whose payload slots form one contiguous
+// image range [img_lo, img_lo + img_bytes).
+struct DevBatch {
+    int32_t p0, np;
+    uint64_t img_lo;
+    uint32_t img_bytes;
+    uint32_t pad;
+};
+
+struct BatchLaunch {
+    const uint8_t* bytes;
+    const DevPage* pages;
+    const DevBatch* batches;
+    int32_t nbatches, last_page;
+    const DevDict* dicts;
+    int32_t dict_id;
+    const uint64_t* entries;
+    const int32_t* dict_count;
+    int32_t max_def, max_rep;
+    uint32_t rows_cap, batch_bytes, max_slot, dict_bytes, dict_chars_bytes;
+    uint64_t* status;
+    int32_t* ticket;
+    const int64_t* base_in;
+    int64_t* base_out;
+    int64_t nrows_total;
+    uint32_t* validity;
+    int64_t* offsets;
+    uint8_t* chars;
+    int64_t capacity;
+    int32_t* overflow;
+    DevErr* page_err;
+    int32_t* err_any;
+    int debug;
+    uint64_t* prof;
+    int grid, writers;
+    uint32_t lds;
+};
+
+struct BatchPlan {
+    int writers;   // writer waves per workgroup (0: does not fit)
+    uint32_t lds;  // dynamic LDS bytes per workgroup
+};
+BatchPlan plan_batch_lds(uint32_t rows_cap, uint32_t batch_bytes, uint32_t max_slot, uint32_t dict_bytes);
+int batch_occupancy(uint32_t lds_bytes, int waves);
+void launch_ba_batch(hipStream_t s, const BatchLaunch& B);
+int batch_prof_slots();
+
 void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
                        uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any,
                        uint32_t max_dict_bytes);

@@ -267,11 +267,13 @@ class Context:
     PROF_PHASES = ("stage", "def", "levels", "values", "rows", "lookback", "slotwait", "pages",
                    "w_wait", "w_offsets", "w_gather", "w_pages")
 
-    def fused_prof_read(self) -> dict:
-        """Per-phase shader-clock sums of k_ba_fused since the last read
-        (option "fused_prof" must be 1)."""
+    def fused_prof_read(self, raw: bool = False):
+        """Per-phase shader-clock sums of k_ba_fused / k_ba_batch since the
+        last read (option "fused_prof" must be 1)."""
         buf = (C.c_uint64 * 16)()
         k = lib().pq_fused_prof_read(self.h, buf, 16)
+        if raw:
+            return [int(buf[i]) for i in range(k)]
         return {self.PROF_PHASES[i] if i < len(self.PROF_PHASES) else str(i): int(buf[i]) for i in range(k)}
 
 

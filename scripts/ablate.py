@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
-"""Ablation timings of the fused BYTE_ARRAY kernel (C2 shape) on one GPU.
+"""Ablation timings of the BYTE_ARRAY dictionary kernels (C2 shape) on one GPU.
 
+Paths: batch (dict_batch.hip), fused (dict_fused.hip), generic (decode.hip).
 fused_debug bits (timing only; the output is not valid with bits set):
   1 = skip the decoupled look-back (fake page bases)
-  2 = skip the character gather
+  2 = skip the characters
   4 = skip the offsets stores
-  8 = writer: skip assembling the character blocks (stores zeros)
- 16 = writer: assemble the character blocks but do not store them
- 32 = writer: skip the block -> row map (wrong rows, same work otherwise)
-Prints one JSON line per variant with per-kernel average milliseconds.
+  8/16/32 = dict_fused.hip writer internals (see the kernel)
+Prints one JSON line per variant with per-kernel average milliseconds, then
+per-phase shader-clock cycles (option fused_prof) for the batch and fused
+kernels.
 """
 import json
 import os
@@ -18,41 +19,50 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "duckdb-parquet-parser_amd")]
 from pqgpu import capi, gen  # noqa: E402
 
-rows = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+KERNELS = ("dict_index", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather")
+BATCH_PHASES = ("p_waitbuf", "p_stage", "p_walk", "p_lookback", "batches",
+                "w_wait", "w_runs", "w_rows", "w_chars", "pages", "p_defwalk")
+
+rows = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 10_000_000
 layout = gen.ARROW_LAYOUT if "arrow" in sys.argv else gen.REF_LAYOUT
-f = gen.build(gen.c2_cols(), rows, 1, seed=2, layout=layout)
+f = gen.build(gen.c2_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
 F = capi.File(f)
 chunks = [F.chunk(0, 0)]
 ctx = capi.Context(0)
-variants = [(0, 0), (1, 0), (2, 0), (3, 0), (8, 0), (16, 0), (32, 0), (24, 0), (0, 8), (0, 4)]
-for fused in (1, 0):
-    for dbg, waves in (variants if fused else [(0, 0)]):
-        ctx.set_option("fused_ba", fused)
-        ctx.set_option("fused_debug", dbg)
-        ctx.set_option("fused_waves", waves)
-        dc = ctx.upload(f, chunks)
-        dc.decode_async()
-        ctx.sync()
-        ctx.timing(True)
-        ctx.timing_reset()
-        for _ in range(10):
-            dc.decode_async()
-        ctx.sync()
-        res = {}
-        for k in ("dict_index", "dict_entries", "ba_fused", "ba_rows", "scan", "ba_gather"):
-            ms, n = ctx.timing_get(k)
-            if n:
-                res[k] = round(ms / n, 4)
-        ctx.timing(False)
-        print(json.dumps({"fused": fused, "debug": dbg, "waves": waves, "ms": res}), flush=True)
-        dc.free()
-ctx.set_option("fused_debug", 0)
-ctx.set_option("fused_waves", 0)
-# per-phase shader clocks of the fused kernel (cycles per page, summed over waves)
-ctx.set_option("fused_ba", 1)
-ctx.set_option("fused_prof", 1)
-for dbg in (0, 1, 16):
+
+
+def setp(path, dbg=0, waves=0, bbytes=12288):
+    ctx.set_option("fused_ba", int(path != "generic"))
+    ctx.set_option("batch", int(path == "batch"))
     ctx.set_option("fused_debug", dbg)
+    ctx.set_option("fused_waves", waves)
+    ctx.set_option("batch_bytes", bbytes)
+
+
+variants = [("batch", 0, 0, 12288), ("batch", 1, 0, 12288), ("batch", 3, 0, 12288),
+            ("batch", 0, 0, 16384), ("fused", 0, 0, 12288)]
+for path, dbg, waves, bb in variants:
+    setp(path, dbg, waves, bb)
+    dc = ctx.upload(f, chunks)
+    dc.decode_async()
+    ctx.sync()
+    ctx.timing(True)
+    ctx.timing_reset()
+    for _ in range(10):
+        dc.decode_async()
+    ctx.sync()
+    res = {}
+    for k in KERNELS:
+        ms, n = ctx.timing_get(k)
+        if n:
+            res[k] = round(ms / n, 4)
+    ctx.timing(False)
+    print(json.dumps({"path": path, "debug": dbg, "waves": waves, "batch_bytes": bb, "ms": res}), flush=True)
+    dc.free()
+
+ctx.set_option("fused_prof", 1)
+for path in ("batch", "fused"):
+    setp(path)
     dc = ctx.upload(f, chunks)
     dc.decode_async()
     ctx.sync()
@@ -60,11 +70,19 @@ for dbg in (0, 1, 16):
     for _ in range(5):
         dc.decode_async()
     ctx.sync()
-    pr = ctx.fused_prof_read()
-    pages = max(pr.get("pages", 1), 1)
-    print(json.dumps({"debug": dbg, "prof_cycles_per_page": {k: round(v / pages, 1) for k, v in pr.items()
-                                                             if k not in ("pages", "w_pages")},
-                      "pages": pages, "w_pages": pr.get("w_pages")}), flush=True)
+    raw = ctx.fused_prof_read(raw=True)
+    if path == "batch":
+        pr = dict(zip(BATCH_PHASES, raw))
+        nb, npg = max(pr["batches"], 1), max(pr["pages"], 1)
+        out = {k: round(v / nb) for k, v in pr.items() if k.startswith("p_")}
+        out.update({k: round(v / npg) for k, v in pr.items() if k.startswith("w_")})
+        print(json.dumps({"path": path, "cycles (producer per batch, writer per page)": out,
+                          "batches": nb, "pages": npg}), flush=True)
+    else:
+        pr = dict(zip(capi.Context.PROF_PHASES, raw))
+        npg = max(pr.get("pages", 1), 1)
+        print(json.dumps({"path": path, "cycles_per_page": {k: round(v / npg) for k, v in pr.items()
+                                                           if k not in ("pages", "w_pages")}}), flush=True)
     dc.free()
-ctx.set_option("fused_debug", 0)
 ctx.set_option("fused_prof", 0)
+setp("batch")

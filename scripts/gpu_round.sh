@@ -29,5 +29,6 @@ rc=$?; [ $rc -eq 0 ] || { echo "FETCH rc=$rc"; tail -20 "$OUT/prof_fetch.log"; e
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -T -d "$OUT/prof_write" -o write --output-format csv -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu "$@" > "$OUT/prof_write.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || { echo "WRITE rc=$rc"; tail -20 "$OUT/prof_write.log"; exit $rc; }
-find "$OUT" -name "*.csv" | head -20
+python3 scripts/pmc_summary.py "$OUT" "$OUT/pmc_summary.json" > /dev/null
+cp "$OUT"/prof_kt/*kernel_stats.csv "$OUT/kernel_stats.csv"
 echo ROUND_OK

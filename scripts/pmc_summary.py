@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Summarise one scripts/gpu_round.sh run: per-kernel average duration
+(rocprofv3 --kernel-trace --stats) and HBM bytes per launch from the
+FETCH_SIZE / WRITE_SIZE PMC passes, corrected as
+/opt/skills/guides/MI355X_MICROARCH.md §HBM prescribes: the counters are in
+KiB; on gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane coalesced
+reads (x2); WRITE_SIZE is exact for 16-B-per-lane stores.
+
+usage: pmc_summary.py gpurun_out/TAG [out.json]
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+
+NAME = re.compile(r"\bk_([A-Za-z0-9_]+)")
+
+
+def short(kname: str) -> str:
+    m = NAME.search(kname)
+    return m.group(1) if m else kname.split("(")[0]
+
+
+def counters(pattern):
+    acc = {}
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                k = short(r["Kernel_Name"])
+                d = acc.setdefault(k, {"dispatches": set(), "value": 0.0})
+                d["dispatches"].add(r["Dispatch_Id"])
+                d["value"] += float(r["Counter_Value"])
+    return {k: (v["value"], len(v["dispatches"])) for k, v in acc.items()}
+
+
+def main():
+    d = sys.argv[1]
+    out = sys.argv[2] if len(sys.argv) > 2 else None
+    res = {"source": os.path.basename(os.path.normpath(d)), "kernels": {},
+           "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 wide-read halving); WRITE_SIZE KiB x1024"}
+    stats = glob.glob(os.path.join(d, "prof_kt", "*kernel_stats.csv"))
+    if stats:
+        with open(stats[0]) as fh:
+            for r in csv.DictReader(fh):
+                k = short(r["Name"])
+                res["kernels"].setdefault(k, {}).update(
+                    {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                     "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])})
+    fetch = counters(os.path.join(d, "prof_fetch", "**", "*counter_collection.csv"))
+    write = counters(os.path.join(d, "prof_write", "**", "*counter_collection.csv"))
+    for k in set(fetch) | set(write):
+        e = res["kernels"].setdefault(k, {})
+        if k in fetch:
+            v, n = fetch[k]
+            e["fetch_kib_raw_per_launch"] = v / n
+            e["fetch_bytes_per_launch"] = v / n * 1024 * 2
+        if k in write:
+            v, n = write[k]
+            e["write_bytes_per_launch"] = v / n * 1024
+        if "fetch_bytes_per_launch" in e and "write_bytes_per_launch" in e:
+            e["hbm_bytes_per_launch"] = e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"]
+    s = json.dumps(res, indent=1, sort_keys=True)
+    if out:
+        with open(out, "w") as fh:
+            fh.write(s + "\n")
+    print(s)
+
+
+if __name__ == "__main__":
+    main()

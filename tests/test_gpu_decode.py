@@ -35,12 +35,15 @@ SMALL = [
 ]
 
 
-@pytest.fixture(params=[1, 0], ids=["fused", "generic"])
+@pytest.fixture(params=["batch", "fused", "generic"])
 def path(request, ctx):
-    """Both BYTE_ARRAY kernel paths: fused (dict_fused.hip) and generic."""
-    ctx.set_option("fused_ba", request.param)
+    """Every BYTE_ARRAY kernel path: batched dictionary (dict_batch.hip),
+    per-page fused (dict_fused.hip) and generic (decode.hip)."""
+    ctx.set_option("fused_ba", int(request.param != "generic"))
+    ctx.set_option("batch", int(request.param == "batch"))
     yield request.param
     ctx.set_option("fused_ba", 1)
+    ctx.set_option("batch", 0)
 
 
 @pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT], ids=["ref", "arrow"])
@@ -53,6 +56,21 @@ def test_generated_columns(ctx, path, name, cols, n, layout):
         rc_g, msg_g, d_g = gpu_read_column(ctx, f, chunks)
         assert (rc_g, msg_g) == (rc_o, msg_o), (name, ci)
         assert d_g == d_o, (name, ci, len(d_g or b""), len(d_o or b""))
+
+
+@pytest.mark.parametrize("name,cols,n", [s for s in SMALL if s[0] in
+                                         ("c2_dict", "c4_mixed", "all_null", "long_strings", "wide_dict")],
+                         ids=lambda v: v if isinstance(v, str) else "")
+def test_small_arrow_pages(ctx, path, name, cols, n):
+    """Arrow-style pages small enough for the batched path: bit-packed
+    def-level runs, RLE runs >= 8, many pages per batch."""
+    f = gen.build(cols, n, 2, seed=12, layout=gen.ARROW_LAYOUT, rows_per_page=700)
+    for ci in range(len(cols)):
+        chunks = file_chunks(f, ci)
+        rc_o, msg_o, d_o = oracle_read_column(f, chunks)
+        rc_g, msg_g, d_g = gpu_read_column(ctx, f, chunks)
+        assert (rc_g, msg_g) == (rc_o, msg_o), (name, ci)
+        assert d_g == d_o, (name, ci)
 
 
 def test_repeat_decode_reuses_buffers(ctx):
@@ -94,6 +112,8 @@ CRAFTED = {
     "zero_group_bp": lambda: _dict_ba_file(bytes([2]) + B.rle(2, 1, 2) + B.varint(1) + bytes([0b11100100, 0x1b, 0xff]), 12, DICT),
     # zero-count RLE after a literal run: stale literal cursor
     "zero_count_rle_after_lit": lambda: _dict_ba_file(bytes([2]) + B.bitpack([1, 2, 3, 0, 1, 2, 3, 0], 2) + B.rle(0, 3, 2) + bytes([0x1b, 0xe4]), 16, DICT),
+    # more runs than the batched path's run list holds for this page size
+    "many_tiny_runs": lambda: _dict_ba_file(bytes([2]) + b"".join(B.rle(1, i % 4, 2) for i in range(40)), 40, DICT),
     # multi-byte varint run header (count 300)
     "long_rle_run": lambda: _dict_ba_file(bytes([2]) + B.rle(300, 2, 2), 300, DICT),
     # def levels + nulls, RLE and bit-packed level runs
