@@ -106,9 +106,15 @@ void pq_ctx_destroy(pq_ctx* ctx);
 const char* pq_last_error(const pq_ctx* ctx);
 void* pq_ctx_stream(pq_ctx* ctx);              /* the hipStream_t kernels run on */
 int pq_ctx_sync(pq_ctx* ctx);
-/* Tuning switches: "fused_ba" (default 1) = fused BYTE_ARRAY decode kernel
- * when every chunk qualifies; 0 forces the generic rows/scan/gather kernels.
- * Applies to chunks uploaded afterwards. */
+/* Tuning switches (apply to chunks uploaded afterwards):
+ *   "fused_ba"    1 (default): per-page fused BYTE_ARRAY kernel when every
+ *                 chunk qualifies; 0 forces the generic rows/scan/gather kernels
+ *   "batch"       1: batched dictionary kernel (dict_batch.hip) for chunks of
+ *                 dictionary pages; 0 (default)
+ *   "batch_bytes" payload bytes per batch buffer of the batched kernel
+ *   "fused_waves" waves per workgroup cap (0 = automatic)
+ * Diagnostics (timing studies only; outputs are not valid with bits set):
+ *   "fused_debug" ablation bits, "fused_prof" per-phase clocks. */
 int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value);
 
 /* ── host page walk (R-WALK / R-HDR) ────────────────────────────────────── */
