@@ -230,11 +230,16 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             rel = float(t.item())
         npages = rdc.num_pages
-        rms, rn = ctx.timing_get("regex_pages")
+        rms, rn, rkern = 0.0, 0, None
+        for rk in ("regex_plain", "regex_lanes", "regex_pages"):
+            rms, rn = ctx.timing_get(rk)
+            if rn:
+                rkern = rk
+                break
         result["regex"] = {"pages_per_s": npages * rsteps * world / rel, "pages_per_gpu": npages,
                            "ms_per_scan": rel / rsteps * 1e3, "pattern": args.pattern,
                            "reported_pages": int(flags.sum()),
-                           "kernel_ms": rms / rn if rn else None,
+                           "kernel": rkern, "kernel_ms": rms / rn if rn else None,
                            "payload_GBs": rdc.payload_bytes / (rms / rn * 1e-3) / 1e9 if rn else None}
         rdc.free()
 

@@ -42,6 +42,9 @@ struct pq_ctx {
     uint64_t* d_prof = nullptr;  // "fused_prof": per-phase cycle sums of k_ba_fused / k_ba_batch
     bool opt_batch = false;      // "batch": batched dictionary path (dict_batch.hip)
     int opt_batch_bytes = 12288; // "batch_bytes": payload bytes per batch buffer
+    bool opt_regex_dfa = true;   // "regex_dfa": DFA kernels (else the NFA kernel)
+    bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
+    int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
 };
 
 struct pq_chunk {
@@ -103,6 +106,14 @@ struct pq_chunk {
     // regex
     uint8_t* d_page_flags = nullptr;
     uint8_t* d_dict_match = nullptr;
+    uint8_t* d_dfa = nullptr;           // regex DFA image (regex.hpp DevDfa)
+    std::vector<pqk::DevBatch> hrwins;  // windowed PLAIN regex scan: page windows
+    pqk::DevBatch* d_rwins = nullptr;
+    int32_t* d_rwin_ticket = nullptr;
+    uint32_t rwin_bytes = 0, rwin_for_dfa = 0;
+    int rwin_grid = 0;
+    uint32_t dfa_bytes = 0;
+    std::string prog_pattern;           // pattern of d_prog / d_dfa
     int64_t dict_match_cap = 0;
     pqre::DeviceProgram* d_prog = nullptr;
 };
@@ -210,6 +221,7 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_scan_scratch);
     dfree(c->d_page_flags);
     dfree(c->d_dict_match);
+    dfree(c->d_dfa);
     dfree(c->d_status);
     dfree(c->d_tickets);
     dfree(c->d_bases);
@@ -351,6 +363,13 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "fused_waves") == 0) { ctx->opt_waves = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "batch") == 0) { ctx->opt_batch = value != 0; return 0; }
+    if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
+    if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
+    if (std::strcmp(key, "regex_win") == 0) {
+        if (value < 1024 || value > 32768 || value % 16) return set_err(ctx, PQ_ERR_ARG, "regex_win: 1024..32768, multiple of 16");
+        ctx->opt_regex_win = static_cast<int>(value);
+        return 0;
+    }
     if (std::strcmp(key, "batch_bytes") == 0) {
         if (value < 1024 || value > 65536 || value % 16) return set_err(ctx, PQ_ERR_ARG, "batch_bytes: 1024..65536, multiple of 16");
         ctx->opt_batch_bytes = static_cast<int>(value);
@@ -840,6 +859,55 @@ int pq_regex_compile_check(const char* pattern, char* err, size_t errlen) {
     return rc;
 }
 
+// Windows of consecutive pages for the windowed PLAIN regex kernel (regex.hip
+// k_regex_plain): <= 64 pages and <= win bytes of image each.  False when a
+// page does not fit (the lane-per-page kernel runs then).
+bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
+    if (c->d_rwins && c->rwin_for_dfa == c->dfa_bytes) return true;
+    std::vector<DevPage> hp(static_cast<size_t>(c->npages));
+    if (c->npages && hipMemcpy(hp.data(), c->d_pages, hp.size() * sizeof(DevPage), hipMemcpyDeviceToHost) != hipSuccess)
+        return false;
+    uint32_t maxslot = 0;
+    for (const auto& p : hp) maxslot = std::max(maxslot, (static_cast<uint32_t>(std::max(p.size, 0)) + 15) / 16 * 16 + 16);
+    const uint32_t win = std::max<uint32_t>(static_cast<uint32_t>(ctx->opt_regex_win), maxslot);
+    const uint32_t lds = pqre::regex_plain_lds(c->dfa_bytes, win);
+    if (lds > 160 * 1024) return false;
+    c->hrwins.clear();
+    size_t p = 0;
+    while (p < hp.size()) {
+        pqk::DevBatch b{};
+        b.p0 = static_cast<int32_t>(p);
+        b.img_lo = hp[p].off;
+        uint64_t hi = b.img_lo;
+        size_t q = p;
+        while (q < hp.size() && q - p < 64) {
+            const uint64_t e = hp[q].off + (static_cast<uint64_t>(std::max(hp[q].size, 0)) + 15) / 16 * 16 + 16;
+            if (e - b.img_lo > win) break;
+            hi = e;
+            q++;
+        }
+        b.np = static_cast<int32_t>(q - p);
+        b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
+        c->hrwins.push_back(b);
+        p = q;
+    }
+    dfree(c->d_rwins);
+    if (!c->d_rwin_ticket && dalloc(&c->d_rwin_ticket, 1)) return false;
+    if (dalloc(&c->d_rwins, std::max<size_t>(c->hrwins.size(), 1))) return false;
+    if (!c->hrwins.empty() &&
+        hipMemcpy(c->d_rwins, c->hrwins.data(), c->hrwins.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice) != hipSuccess)
+        return false;
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+    const int per_cu = std::max(1, pqre::regex_plain_occupancy(lds));
+    c->rwin_bytes = win;
+    c->rwin_for_dfa = c->dfa_bytes;
+    c->rwin_grid = std::max(1, std::min<int>(per_cu * cus, static_cast<int>((c->hrwins.size() + 7) / 8)));
+    (void)cus;
+    return true;
+}
+
 int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg) {
     if (!ctx || !c || !pattern) return PQ_ERR_ARG;
     if (c->type != PQ_BYTE_ARRAY) return set_err(ctx, PQ_ERR_ARG, "regex page filter needs a BYTE_ARRAY column");
@@ -853,13 +921,29 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
         int64_t dict_cap = std::max<int64_t>(c->nentries, 1);
         if (c->dict_match_cap < dict_cap) {
             dfree(c->d_dict_match);
+    dfree(c->d_dfa);
             if (dalloc(&c->d_dict_match, static_cast<size_t>(dict_cap)))
                 return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (dict match)");
             c->dict_match_cap = dict_cap;
         }
-        if (c->d_prog) pqre::free_device_program(c->d_prog);
-        c->d_prog = pqre::upload_program(prog, ctx->stream);
-        if (!c->d_prog) return set_err(ctx, PQ_ERR_HIP, "regex program upload failed");
+        // compiled programs are cached per chunk by pattern (the bench and the
+        // CLI rescan with one pattern)
+        const std::string key = std::string(pattern) + (ctx->opt_regex_dfa ? "|dfa" : "|nfa");
+        if (!c->d_prog || c->prog_pattern != key) {
+            if (c->d_prog) pqre::free_device_program(c->d_prog);
+            c->d_prog = pqre::upload_program(prog, ctx->stream);
+            if (!c->d_prog) return set_err(ctx, PQ_ERR_HIP, "regex program upload failed");
+            std::vector<uint8_t> img;
+            dfree(c->d_dfa);
+            c->dfa_bytes = 0;
+            if (ctx->opt_regex_dfa && pqre::build_dfa(prog, &img)) {
+                if (dalloc(&c->d_dfa, img.size())) return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (dfa)");
+                if (int rc2 = hip_check(ctx, hipMemcpy(c->d_dfa, img.data(), img.size(), hipMemcpyHostToDevice), "dfa upload"))
+                    return rc2;
+                c->dfa_bytes = static_cast<uint32_t>(img.size());
+            }
+            c->prog_pattern = key;
+        }
         hipStream_t s = ctx->stream;
         pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
         (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), s);
@@ -873,7 +957,18 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
                                     c->d_dict_count, c->d_dict_match);
         }
-        {
+        if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {
+            (void)hipMemsetAsync(c->d_rwin_ticket, 0, sizeof(int32_t), s);
+            Timed t(ctx, "regex_plain");
+            pqre::launch_regex_plain(s, c->d_dfa, c->dfa_bytes, c->rwin_bytes, c->d_bytes, c->d_pages, c->d_rwins,
+                                     static_cast<int>(c->hrwins.size()), c->d_rwin_ticket, c->rwin_grid, cp, neg,
+                                     c->d_page_flags, c->d_page_err, c->d_flags);
+        } else if (c->d_dfa) {
+            Timed t(ctx, "regex_lanes");
+            pqre::launch_regex_lanes(s, c->d_dfa, c->dfa_bytes, c->d_bytes, c->d_pages, c->npages, c->d_dicts,
+                                     c->d_dict_count, c->d_dict_match, cp, neg, c->d_page_flags,
+                                     c->d_page_err, c->d_flags);
+        } else {
             Timed t(ctx, "regex_pages");
             pqre::launch_regex_pages(s, c->d_prog, c->d_bytes, c->d_pages, c->npages, c->d_dicts,
                                      c->d_entries, c->d_dict_count, c->d_dict_match, cp, neg,

@@ -64,6 +64,16 @@ __device__ __forceinline__ uint32_t lds_bits(const uint32_t* words, uint32_t siz
     return bw >= 32 ? x : (x & ((1u << bw) - 1u));
 }
 
+// 8 bytes at LDS byte address a (the staged page has >= 16 readable bytes
+// past its end).
+__device__ __forceinline__ uint64_t lds_u64(const uint32_t* w, uint32_t a) {
+    const uint32_t i = a >> 2, sh = a & 3;
+    const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2];
+    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
 // Stage a page's payload into this wave's LDS words (zero-filled tail word).
 __device__ inline void stage_page(uint32_t* lds, const uint8_t* g, uint32_t size) {
     uint32_t nw = (size + 3) / 4;

@@ -27,6 +27,7 @@
 #include "kernels/device_common.hpp"
 #include "kernels/hybrid.hpp"
 #include "kernels/kernels.hpp"
+#include "kernels/lane_walk.hpp"
 #include "kernels/stream.hpp"
 #include "pq_gpu.h"
 
@@ -146,76 +147,6 @@ __host__ __device__ inline BLayout batch_layout(uint32_t rows_cap, uint32_t batc
 __device__ __forceinline__ uint32_t lds_u32a(const uint32_t* words, uint32_t a) {
     uint32_t w0 = words[a >> 2], w1 = words[(a >> 2) + 1];
     return __builtin_amdgcn_alignbyte(w1, w0, a & 3);
-}
-
-// ── per-lane scalar hybrid decoder (rle_decoder.hpp state machine) ──────────
-// Stream at page bytes [base, base + size) of the page copy `pw`.  Produces
-// `need` values as segments emit(kind, count, arg): kind 0 = `count` copies
-// of value `arg`; kind 1 = `count` bit-packed values from page bit `arg`.
-struct LRle {
-    uint32_t base, size, pos, bw, repeat, literal, value, lit_start, lit_bit, lit_valid;
-};
-
-template <class F>
-__device__ int lane_rle(LRle& r, const uint32_t* pw, uint32_t need, F&& emit) {
-    uint32_t done = 0;
-    while (done < need) {
-        if (r.repeat == 0 && r.literal == 0) {
-            if (r.pos >= r.size) {  // exhausted: zeros (rle_decoder.hpp:20-23)
-                emit(0u, need - done, 0u);
-                return 0;
-            }
-            uint32_t ind = 0, shift = 0;  // read_varint32 (76-86), bounded by the stream
-            for (;;) {
-                const uint64_t x = lds_u64(pw, r.base + r.pos);
-                const uint32_t avail = min(8u, r.size - r.pos);
-                uint32_t i = 0;
-                bool end = false;
-                for (; i < avail; i++) {
-                    const uint32_t b = static_cast<uint32_t>(x >> (8 * i)) & 0xFFu;
-                    if (shift < 32) ind |= (b & 0x7Fu) << shift;
-                    shift += 7;
-                    if (!(b & 0x80u)) { end = true; i++; break; }
-                }
-                r.pos += i;
-                if (end || r.pos >= r.size) break;
-            }
-            if (ind & 1u) {  // literal run (41-46)
-                r.literal = (ind >> 1) * 8u;
-                r.lit_start = r.pos;
-                r.lit_valid = 1;
-                r.lit_bit = 0;
-            } else {  // repeated run (48-50, 88-95)
-                r.repeat = ind >> 1;
-                const uint32_t nb = min((r.bw + 7) / 8, r.size - r.pos);
-                uint32_t v = nb ? static_cast<uint32_t>(lds_u64(pw, r.base + r.pos)) : 0u;
-                if (nb < 4) v &= (1u << (8 * nb)) - 1u;
-                r.value = v;
-                r.pos += nb;
-            }
-        }
-        if (r.bw > 64) return PQ_ERR_UNSUPPORTED;
-        if (r.repeat > 0) {
-            const uint32_t k = min(r.repeat, need - done);
-            emit(0u, k, r.value);
-            r.repeat -= k;
-            done += k;
-        } else {
-            // literal_count_ == 0: a zero-count run; the reference's counter
-            // wraps and every later value comes from the literal cursor
-            if (r.bw > 0 && !r.lit_valid) return PQ_ERR_UNSUPPORTED;
-            const bool wrapped = r.literal == 0;
-            const uint32_t k = wrapped ? need - done : min(r.literal, need - done);
-            if (r.bw == 0) emit(0u, k, 0u);
-            else emit(1u, k, (r.base + r.lit_start) * 8u + r.lit_bit);
-            const bool finishes = !wrapped && k == r.literal;
-            r.lit_bit += k * r.bw;
-            r.literal -= k;
-            if (finishes && r.bw > 0) r.pos = r.lit_start + (r.lit_bit + 7) / 8;  // 66-72
-            done += k;
-        }
-    }
-    return 0;
 }
 
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
@@ -343,6 +274,7 @@ __device__ void batch_produce(const BArgs& a, const BLayout& L, uint8_t* base, C
         uint32_t* mask = reinterpret_cast<uint32_t*>(buf + L.b_mask) + lane();  // word w at mask[64 * w]
         uint32_t* runs = reinterpret_cast<uint32_t*>(buf + L.b_runs + pay);
         const uint32_t run_cap = (static_cast<uint32_t>(pg.size) + 15) / 16 * 4 + 4;  // slot bytes / 4
+        auto rd8 = [&](uint32_t a) { return lds_u64(pw, a); };
         int code = 0;
         uint32_t epos = 0, eneed = 0;
         uint32_t nn = 0, nruns = 0, flags = 0, ipos = 0, ibw = 0;
@@ -379,7 +311,7 @@ __device__ void batch_produce(const BArgs& a, const BLayout& L, uint8_t* base, C
                     uint32_t row = 0;
                     bool above = false;
                     const uint32_t md = static_cast<uint32_t>(a.max_def);
-                    code = lane_rle(r, pw, n, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                    code = lane_rle(r, rd8, n, [&](uint32_t kind, uint32_t k, uint32_t arg) {
                         if (kind == 0) {
                             if (arg > md) above = true;
                             if (arg == md && k) {
@@ -419,7 +351,7 @@ __device__ void batch_produce(const BArgs& a, const BLayout& L, uint8_t* base, C
                     pos += 1;
                     ipos = pos;
                     LRle r{pos, size - pos, 0, ibw, 0, 0, 0, 0, 0, 0};
-                    code = lane_rle(r, pw, nn, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                    code = lane_rle(r, rd8, nn, [&](uint32_t kind, uint32_t k, uint32_t arg) {
                         if (kind == 0) {
                             const uint32_t idx = static_cast<int32_t>(arg) >= 0 && arg < dict_n ? arg : 0xFFFFu;
                             if (idx != 0xFFFFu) total += static_cast<uint64_t>(k) * (dtab[idx] >> 16);

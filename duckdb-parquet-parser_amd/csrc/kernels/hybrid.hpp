@@ -61,16 +61,6 @@ __device__ inline HybScratch hyb_carve(uint8_t* p, uint32_t maxpos, uint32_t max
     return s;
 }
 
-// 8 bytes at LDS byte address a (the staged page has >= 16 readable bytes
-// past its end).
-__device__ __forceinline__ uint64_t lds_u64(const uint32_t* w, uint32_t a) {
-    const uint32_t i = a >> 2, sh = a & 3;
-    const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2];
-    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
-    const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
-    return (static_cast<uint64_t>(hi) << 32) | lo;
-}
-
 // Decode the first n values of the stream at page bytes [base, base + S)
 // (page words `pw`, page size `psize`) with bit width bw.  out(j, v) for
 // j < n.  R: n u16 slots of LDS scratch (may alias the output array when

@@ -13,6 +13,7 @@
 
 #include "kernels/device_common.hpp"
 #include "kernels/kernels.hpp"
+#include "kernels/lane_walk.hpp"
 #include "pq_gpu.h"
 #include "regex/regex.hpp"
 
@@ -204,6 +205,411 @@ __global__ void __launch_bounds__(256) k_regex_pages(const DevProg* __restrict__
     if (lane() == 0) page_flags[p] = any ? 0 : 1;
 }
 
+
+// ── lane-per-page DFA scan ──────────────────────────────────────────────────
+// One lane per data page (a wavefront scans 64 pages at once): def levels
+// and dictionary indices with the reference's RLE state machine
+// (lane_walk.hpp), PLAIN strings streamed through a 16-byte register window
+// into the DFA (one LDS lookup per byte).  A lane stops as soon as its page
+// has a satisfying value.
+__device__ __forceinline__ uint32_t dfa_step_full(const uint16_t* T, uint32_t e, uint32_t b) {
+    return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(T) + (e & 0x7FFFu) + 2 * b);
+}
+
+__device__ __forceinline__ uint32_t win_byte(const uint4& w, uint32_t i) {
+    const uint32_t d = (i & 8) ? ((i & 4) ? w.w : w.z) : ((i & 4) ? w.y : w.x);
+    return (d >> (8 * (i & 3))) & 0xFFu;
+}
+
+__device__ __forceinline__ void lane_err(DevErr* e, int32_t* any, int code, uint32_t pos, uint32_t need,
+                                         uint32_t size) {
+    e->code = code;
+    e->pos = static_cast<int32_t>(pos);
+    e->need = static_cast<int32_t>(need);
+    e->size = static_cast<int32_t>(size);
+    atomicOr(any, 1);
+}
+
+__global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__ dfa_img, uint32_t dfa_bytes,
+                                                     const uint8_t* __restrict__ bytes,
+                                                     const DevPage* __restrict__ pages, int npages,
+                                                     const DevDict* __restrict__ dicts,
+                                                     const int32_t* __restrict__ dict_count,
+                                                     const uint8_t* __restrict__ dict_match,
+                                                     ColumnParams cp, int neg,
+                                                     uint8_t* __restrict__ page_flags,
+                                                     DevErr* __restrict__ page_err,
+                                                     int32_t* __restrict__ err_any) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(dfa_img);
+        uint4* dst = reinterpret_cast<uint4*>(dsm);
+        for (uint32_t i = threadIdx.x; i < dfa_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    const DevDfa* D = reinterpret_cast<const DevDfa*>(dsm);
+    const uint16_t* T = reinterpret_cast<const uint16_t*>(dsm + sizeof(DevDfa));
+    const uint32_t nc = D->nclasses;
+    const bool empty_ok = D->empty_string != 0;
+    const bool trivial = D->nonempty_trivial != 0;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npages) return;
+    const DevPage pg = pages[p];
+    const uint8_t* page = bytes + pg.off;
+    const uint32_t size = static_cast<uint32_t>(pg.size);
+    const uint32_t nv = static_cast<uint32_t>(max(pg.nvals, 0));
+    DevErr* err = page_err + p;
+    auto rd8 = [&](uint32_t a) { return gld8(page, a); };
+    const bool dict = pg.mode == pqk::MODE_DICT;
+    const uint32_t md = static_cast<uint32_t>(cp.max_def);
+    uint32_t pos = 0, nn = nv;
+    // def levels (column_reader.cpp:146-170)
+    if (cp.max_def > 0) {
+        if (pos + 4 > size) { lane_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); return; }
+        const uint32_t dl = static_cast<uint32_t>(gld8(page, pos));
+        pos += 4;
+        if (static_cast<uint64_t>(pos) + dl > size) { lane_err(err, err_any, PQ_ERR_BUFFER, pos, dl, size); return; }
+        LRle r = lrle(pos, dl, level_bw(cp.max_def));
+        const uint32_t bwd = r.bw;
+        nn = 0;
+        bool above = false;
+        const int rc = lane_rle(r, rd8, nv, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+            if (kind == 0) {
+                if (dict ? arg == md : arg >= md) nn += k;
+                above |= arg > md;
+            } else {
+                for (uint32_t i = 0; i < k; i++) {
+                    const uint32_t v = gbits(page, size, static_cast<uint64_t>(arg) + i * bwd, bwd);
+                    if (dict ? v == md : v >= md) nn++;
+                    above |= v > md;
+                }
+            }
+        });
+        if (rc) { lane_err(err, err_any, rc, 0, 0, size); return; }
+        if (dict && above) { lane_err(err, err_any, PQ_ERR_UNSUPPORTED, 0, 0, size); return; }
+        pos += dl;
+    }
+    if (cp.max_rep > 0) {
+        if (pos + 4 > size) { lane_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); return; }
+        const uint32_t rl = static_cast<uint32_t>(gld8(page, pos));
+        pos += 4;
+        if (static_cast<uint64_t>(pos) + rl > size) { lane_err(err, err_any, PQ_ERR_BUFFER, pos, rl, size); return; }
+        pos += rl;
+    }
+    bool any = false;
+    if (dict) {  // indices -> dictionary match bits (column_reader.cpp:174-196)
+        if (pos + 1 > size) { lane_err(err, err_any, PQ_ERR_BUFFER, pos, 1, size); return; }
+        const uint32_t bw = static_cast<uint32_t>(gld8(page, pos)) & 0xFFu;
+        pos += 1;
+        const uint32_t dict_n = static_cast<uint32_t>(dict_count[pg.dict]);
+        const uint8_t* mt = dict_match + dicts[pg.dict].entry_base;
+        auto sat = [&](uint32_t v) {
+            return static_cast<int32_t>(v) >= 0 && v < dict_n && ((mt[v] != 0) != (neg != 0));
+        };
+        LRle r = lrle(pos, size - pos, bw);
+        const int rc = lane_rle(r, rd8, nn, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+            if (any || k == 0) return;
+            if (kind == 0) {
+                any = sat(arg);
+            } else {
+                for (uint32_t i = 0; i < k && !any; i++)
+                    any = sat(gbits(page, size, static_cast<uint64_t>(arg) + static_cast<uint64_t>(i) * bw, bw));
+            }
+        });
+        if (rc) { lane_err(err, err_any, rc, 0, 0, size); return; }
+    } else if (nn) {  // PLAIN: u32 length + bytes per value (column_reader.cpp:249-253)
+        const uint32_t slot_end = (size + 15) / 16 * 16 + 16;  // readable bytes of the slot
+        auto win = [&](uint32_t at) {
+            const bool ok = at + 16 <= slot_end;
+            const uint4 v = *reinterpret_cast<const uint4*>(page + (ok ? at : 0u));
+            return ok ? v : make_uint4(0, 0, 0, 0);
+        };
+        const bool full = D->full != 0;
+        const uint32_t negv = neg != 0;
+        uint32_t k = 0, cur = pos;
+        int ecode = 0;
+        uint32_t epos = 0, eneed = 0;
+        while (__ballot(k < nn && !ecode && !any)) {
+            // 1. the next kCollect strings' (offset, length): length chain
+            //    (ByteBuffer reads, column_reader.cpp:249-253) and its errors
+            constexpr uint32_t kCollect = 8;
+            uint32_t soff[kCollect], slen[kCollect];
+            uint32_t cnt = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < kCollect; c++) {
+                soff[c] = 0;
+                slen[c] = 0;
+                if (k < nn && !ecode) {
+                    if (static_cast<uint64_t>(cur) + 4 > size) {
+                        ecode = PQ_ERR_BUFFER; epos = cur; eneed = 4;
+                    } else {
+                        const uint32_t len = static_cast<uint32_t>(gld8(page, cur));
+                        cur += 4;
+                        if (static_cast<uint64_t>(cur) + len > size) {
+                            ecode = PQ_ERR_BUFFER; epos = cur; eneed = len;
+                        } else {
+                            soff[c] = cur;
+                            slen[c] = len;
+                            cur += len;
+                            k++;
+                            cnt = c + 1;
+                        }
+                    }
+                }
+            }
+            // 2. match them, one string per lane at a time, 16-byte blocks
+            uint4 N0 = win(soff[0] & ~15u), N1 = win((soff[0] & ~15u) + 16);
+#pragma unroll
+            for (uint32_t c = 0; c < kCollect; c++) {
+                if (!__ballot(c < cnt)) break;
+                const bool act = c < cnt && !any && !ecode;
+                const uint32_t off = soff[c], len = act ? slen[c] : 0u;
+                const uint32_t o = off & 15u, sh = o & 3, q = o >> 2;
+                uint32_t wb = off - o;
+                uint4 W0 = N0, W1 = N1, W2 = win(wb + 32);
+                if (c + 1 < kCollect) {  // prefetch the next string's first blocks
+                    const uint32_t nb = soff[c + 1] & ~15u;
+                    N0 = win(nb);
+                    N1 = win(nb + 16);
+                }
+                uint32_t e = full ? (DFA_START * kDfaRowBytes) : DFA_START;
+                // (ballots only: lanes of other branches are inactive here)
+                for (uint32_t b0 = 0; __ballot(len > b0); b0 += 16) {
+                    const uint32_t w[8] = {W0.x, W0.y, W0.z, W0.w, W1.x, W1.y, W1.z, W1.w};
+                    uint32_t A[4];
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++) {
+                        uint32_t lo = w[j], hi = w[j + 1];
+                        lo = q == 1 ? w[j + 1] : lo; hi = q == 1 ? w[j + 2] : hi;
+                        lo = q == 2 ? w[j + 2] : lo; hi = q == 2 ? w[j + 3] : hi;
+                        lo = q == 3 ? w[j + 3] : lo; hi = q == 3 ? w[j + 4] : hi;
+                        A[j] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+                    }
+                    const uint32_t rem = len > b0 ? len - b0 : 0u;
+                    if (full) {
+#pragma unroll
+                        for (uint32_t i = 0; i < 16; i++) {
+                            const uint32_t t = dfa_step_full(T, e, (A[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+                            e = i < rem ? t : e;
+                        }
+                    } else {
+#pragma unroll
+                        for (uint32_t i = 0; i < 16; i++) {
+                            const uint32_t bt = (A[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                            const uint32_t t = T[(e & 0x7FFFu) * nc + D->cls_of[bt]];
+                            e = i < rem ? t : e;
+                        }
+                    }
+                    wb += 16;
+                    W0 = W1;
+                    W1 = W2;
+                    W2 = win(wb + 32);
+                }
+                const uint32_t st = full ? (e & 0x7FFFu) / kDfaRowBytes : (e & 0x7FFFu);
+                const bool m = len == 0 ? empty_ok : (trivial || st == DFA_ACCEPT || (e >> 15) != 0);
+                if (act) any = (static_cast<uint32_t>(m) != negv);
+            }
+        }
+        if (ecode) {
+            lane_err(err, err_any, ecode, epos, eneed, size);
+            return;
+        }
+    }
+    page_flags[p] = any ? 0 : 1;
+}
+
+// ── windowed PLAIN scan ─────────────────────────────────────────────────────
+// Chunks without dictionary pages: each wave takes windows of consecutive
+// pages (one contiguous image range, <= win_bytes) in ticket order, copies
+// the window into LDS with coalesced 16-byte loads, walks each page's u32
+// length chain with one lane per page (LDS latency, not HBM), and lists the
+// strings; then all 64 lanes match the listed strings, two per lane, so two
+// DFA chains (one LDS lookup per byte each) are in flight per lane.
+constexpr uint32_t kPlainWaves = 8;
+
+
+__global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
+                                                                  uint32_t dfa_bytes, uint32_t win_bytes,
+                                                                  const uint8_t* __restrict__ bytes,
+                                                                  const DevPage* __restrict__ pages,
+                                                                  const pqk::DevBatch* __restrict__ wins,
+                                                                  int nwins, int32_t* __restrict__ ticket,
+                                                                  ColumnParams cp, int neg,
+                                                                  uint8_t* __restrict__ page_flags,
+                                                                  DevErr* __restrict__ page_err,
+                                                                  int32_t* __restrict__ err_any) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(dfa_img);
+        uint4* dst = reinterpret_cast<uint4*>(dsm);
+        for (uint32_t i = threadIdx.x; i < dfa_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    const DevDfa* D = reinterpret_cast<const DevDfa*>(dsm);
+    const uint16_t* T = reinterpret_cast<const uint16_t*>(dsm + sizeof(DevDfa));
+    const uint32_t nc = D->nclasses;
+    const bool full = D->full != 0;
+    const bool empty_ok = D->empty_string != 0;
+    const bool trivial = D->nonempty_trivial != 0;
+    const uint32_t negv = neg != 0;
+    const uint32_t wv = threadIdx.x / kWave;
+    // per wave: window bytes (+16 zero), string list (u32 per 4 window
+    // bytes), per-page inclusive string counts and list bases, hit mask
+    uint8_t* wbase = dsm + dfa_bytes + wv * (2 * win_bytes + 16 + 2 * 64 * 4 + 16);
+    uint32_t* stage = reinterpret_cast<uint32_t*>(wbase);
+    uint32_t* list = reinterpret_cast<uint32_t*>(wbase + win_bytes + 16);
+    uint32_t* pref = reinterpret_cast<uint32_t*>(wbase + 2 * win_bytes + 16);
+    uint32_t* lbase = pref + 64;
+    uint32_t* hit = lbase + 64;  // [0..1]: satisfied-page mask of the window
+    const uint32_t md = static_cast<uint32_t>(cp.max_def);
+    // windows are independent (no ordering): static grid-stride assignment
+    (void)ticket;
+    const int32_t nw_total = static_cast<int32_t>(gridDim.x * (blockDim.x / kWave));
+    for (int32_t w = static_cast<int32_t>(blockIdx.x * (blockDim.x / kWave) + wv); w < nwins; w += nw_total) {
+        const pqk::DevBatch B = wins[w];
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(bytes + B.img_lo);
+            uint4* dst = reinterpret_cast<uint4*>(stage);
+            for (uint32_t i = lane(); i < B.img_bytes / 16; i += kWave) dst[i] = src[i];
+            if (lane() == 0) { dst[B.img_bytes / 16] = make_uint4(0, 0, 0, 0); hit[0] = 0; hit[1] = 0; }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // lane-per-page: levels, then the length chain into the list
+        const bool act = lane() < static_cast<uint32_t>(B.np);
+        const int32_t pidx = B.p0 + static_cast<int32_t>(lane());
+        DevPage pg{};
+        if (act) pg = pages[pidx];
+        const uint32_t pay = static_cast<uint32_t>(pg.off - B.img_lo);
+        const uint32_t* pw = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(stage) + pay);
+        const uint32_t size = static_cast<uint32_t>(pg.size);
+        uint32_t cnt = 0;
+        if (act) {
+            auto rd8 = [&](uint32_t a) { return lds_u64(pw, a); };
+            DevErr* err = page_err + pidx;
+            uint32_t pos = 0, nn = static_cast<uint32_t>(max(pg.nvals, 0));
+            int code = 0;
+            uint32_t epos = 0, eneed = 0;
+            if (cp.max_def > 0) {
+                if (pos + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
+                else {
+                    const uint32_t dl = static_cast<uint32_t>(rd8(pos));
+                    pos += 4;
+                    if (static_cast<uint64_t>(pos) + dl > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = dl; }
+                    else {
+                        LRle r = lrle(pos, dl, level_bw(cp.max_def));
+                        const uint32_t bwd = r.bw;
+                        const uint32_t nv = nn;
+                        nn = 0;
+                        code = lane_rle(r, rd8, nv, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                            if (kind == 0) {
+                                if (arg >= md) nn += k;
+                            } else {
+                                for (uint32_t i = 0; i < k; i++)
+                                    if (lds_bits(pw, size, static_cast<uint64_t>(arg) + i * bwd, bwd) >= md) nn++;
+                            }
+                        });
+                        pos += dl;
+                    }
+                }
+            }
+            if (!code && cp.max_rep > 0) {
+                if (pos + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
+                else {
+                    const uint32_t rl = static_cast<uint32_t>(rd8(pos));
+                    pos += 4;
+                    if (static_cast<uint64_t>(pos) + rl > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = rl; }
+                    else pos += rl;
+                }
+            }
+            uint32_t* lst = list + pay / 4;  // this page's list region (<= slot / 4 entries)
+            for (uint32_t k = 0; k < nn && !code; k++) {  // column_reader.cpp:249-253
+                if (static_cast<uint64_t>(pos) + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; break; }
+                const uint32_t len = static_cast<uint32_t>(rd8(pos));
+                pos += 4;
+                if (static_cast<uint64_t>(pos) + len > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = len; break; }
+                lst[cnt++] = (pay + pos) | (min(len, 0xFFFFu) << 16);  // window offset | length
+                pos += len;
+            }
+            if (code) {
+                lane_err(err, err_any, code, epos, eneed, size);
+                cnt = 0;
+            }
+        }
+        // flatten: string g of the window -> (page lane, k)
+        const uint32_t inc = wave_incl_scan(cnt);
+        pref[lane()] = inc;
+        lbase[lane()] = pay / 4;
+        const uint32_t total = bcast_last(inc);
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t g0 = 0; g0 < total; g0 += 2 * kWave) {
+            uint32_t e2[2], off2[2], len2[2], pg2[2];
+            bool ok2[2];
+#pragma unroll
+            for (uint32_t h = 0; h < 2; h++) {
+                const uint32_t g = g0 + h * kWave + lane();
+                ok2[h] = g < total;
+                // first page lane whose inclusive count exceeds g
+                uint32_t lo = 0;
+#pragma unroll
+                for (uint32_t stp = 32; stp >= 1; stp >>= 1)
+                    if (pref[lo + stp - 1] <= g) lo += stp;
+                const uint32_t gl = ok2[h] ? lo : 0u;
+                const uint32_t before = gl ? pref[gl - 1] : 0u;
+                const uint32_t ent = ok2[h] ? list[lbase[gl] + (g - before)] : 0u;
+                off2[h] = ent & 0xFFFFu;
+                len2[h] = ok2[h] ? (ent >> 16) : 0u;
+                pg2[h] = gl;
+                e2[h] = full ? (DFA_START * kDfaRowBytes) : DFA_START;
+            }
+            const uint32_t maxl = max(len2[0], len2[1]);
+            for (uint32_t b0 = 0; __ballot(maxl > b0); b0 += 16) {
+#pragma unroll
+                for (uint32_t h = 0; h < 2; h++) {
+                    const uint32_t a = off2[h] + b0;
+                    const uint32_t i0 = a >> 2, sh = a & 3;
+                    uint32_t d[5];
+#pragma unroll
+                    for (uint32_t j = 0; j < 5; j++) d[j] = stage[i0 + j];
+                    uint32_t A[4];
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++) A[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+                    const uint32_t rem = len2[h] > b0 ? len2[h] - b0 : 0u;
+                    uint32_t e = e2[h];
+                    if (full) {
+#pragma unroll
+                        for (uint32_t i = 0; i < 16; i++) {
+                            const uint32_t t = dfa_step_full(T, e, (A[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+                            e = i < rem ? t : e;
+                        }
+                    } else {
+#pragma unroll
+                        for (uint32_t i = 0; i < 16; i++) {
+                            const uint32_t bt = (A[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                            const uint32_t t = T[(e & 0x7FFFu) * nc + D->cls_of[bt]];
+                            e = i < rem ? t : e;
+                        }
+                    }
+                    e2[h] = e;
+                }
+            }
+#pragma unroll
+            for (uint32_t h = 0; h < 2; h++) {
+                const uint32_t e = e2[h];
+                const uint32_t st = full ? (e & 0x7FFFu) / kDfaRowBytes : (e & 0x7FFFu);
+                const bool m = len2[h] == 0 ? empty_ok : (trivial || st == DFA_ACCEPT || (e >> 15) != 0);
+                const bool sat = ok2[h] && (static_cast<uint32_t>(m) != negv);
+                if (sat) atomicOr(&hit[pg2[h] >> 5], 1u << (pg2[h] & 31));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (act) {
+            const bool any = (hit[lane() >> 5] >> (lane() & 31)) & 1u;
+            page_flags[pidx] = any ? 0 : 1;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 }  // namespace
 
 DeviceProgram* upload_program(const Program& p, hipStream_t s) {
@@ -235,6 +641,51 @@ void launch_regex_dict(hipStream_t s, const DeviceProgram* prog, const uint8_t* 
     if (ndicts <= 0) return;
     hipLaunchKernelGGL(k_regex_dict, dim3(ndicts), dim3(256), 0, s, prog->d, bytes, dicts, entries,
                        dict_count, dict_match);
+}
+
+void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, const uint8_t* bytes,
+                        const DevPage* pages, int npages, const DevDict* dicts, const int32_t* dict_count,
+                        const uint8_t* dict_match, ColumnParams cp, int neg, uint8_t* page_flags,
+                        DevErr* page_err, int32_t* err_any) {
+    if (npages <= 0) return;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_regex_lanes),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDfaMaxBytes);
+        attr = true;
+    }
+    const int blocks = (npages + 255) / 256;
+    hipLaunchKernelGGL(k_regex_lanes, dim3(blocks), dim3(256), dfa_bytes, s, dfa, dfa_bytes, bytes, pages, npages,
+                       dicts, dict_count, dict_match, cp, neg, page_flags, page_err, err_any);
+}
+
+uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes) {
+    return dfa_bytes + kPlainWaves * (2 * win_bytes + 16 + 2 * 64 * 4 + 16);
+}
+
+void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
+                        const uint8_t* bytes, const DevPage* pages, const pqk::DevBatch* wins, int nwins,
+                        int32_t* ticket, int grid, ColumnParams cp, int neg, uint8_t* page_flags,
+                        DevErr* page_err, int32_t* err_any) {
+    if (nwins <= 0) return;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_regex_plain),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_regex_plain, dim3(grid), dim3(kPlainWaves * kWave), regex_plain_lds(dfa_bytes, win_bytes),
+                       s, dfa, dfa_bytes, win_bytes, bytes, pages, wins, nwins, ticket, cp, neg, page_flags,
+                       page_err, err_any);
+}
+
+int regex_plain_occupancy(uint32_t lds) {
+    int blocks = 0;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_regex_plain),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_regex_plain, kPlainWaves * kWave, lds) != hipSuccess)
+        return 0;
+    return blocks;
 }
 
 void launch_regex_pages(hipStream_t s, const DeviceProgram* prog, const uint8_t* bytes,

@@ -14,6 +14,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "kernels/kernels.hpp"
 
@@ -47,6 +48,43 @@ struct DevProg {
 struct DeviceProgram {
     DevProg* d;
 };
+
+// The same automaton as a DFA over the Glushkov position sets (subset
+// construction on the host, regex_host.cpp build_dfa).  Layout in device
+// memory: this header, then u16 trans[nstates * nclasses]; an entry is the
+// next state id with bit 15 set when that state accepts at the string end
+// ($).  State ids: 0 DEAD (absorbing reject), 1 ACCEPT (absorbing match),
+// 2 START (before the first byte), 3.. position sets.
+constexpr uint32_t kDfaMaxBytes = 32768;
+constexpr uint32_t kDfaRowBytes = 516;  // full-table row stride (129 dwords)
+struct DevDfa {
+    uint32_t nstates, nclasses;
+    uint32_t empty_string;      // "" matches
+    uint32_t nonempty_trivial;  // every non-empty string matches
+    uint32_t bytes;             // header + table, multiple of 16
+    uint32_t full;              // 1: one column per byte value, entries = next row's byte
+                                // offset (rows kDfaRowBytes apart) | accept-at-end << 15
+    uint32_t pad[2];
+    uint8_t cls_of[256];        // byte -> class
+};
+enum : uint32_t { DFA_DEAD = 0, DFA_ACCEPT = 1, DFA_START = 2 };
+
+// Builds the DFA image; false if it would exceed kDfaMaxBytes (the NFA
+// kernel is used then).
+bool build_dfa(const Program& p, std::vector<uint8_t>* image);
+
+// Windowed PLAIN scan (chunks without dictionary pages).
+uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes);
+int regex_plain_occupancy(uint32_t lds);
+void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
+                        const uint8_t* bytes, const pqk::DevPage* pages, const pqk::DevBatch* wins, int nwins,
+                        int32_t* ticket, int grid, pqk::ColumnParams cp, int neg, uint8_t* page_flags,
+                        pqk::DevErr* page_err, int32_t* err_any);
+
+void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, const uint8_t* bytes,
+                        const pqk::DevPage* pages, int npages, const pqk::DevDict* dicts,
+                        const int32_t* dict_count, const uint8_t* dict_match, pqk::ColumnParams cp, int neg,
+                        uint8_t* page_flags, pqk::DevErr* page_err, int32_t* err_any);
 
 int check(const std::string& pattern, std::string* msg);
 int compile(const std::string& pattern, Program* out, std::string* msg);

@@ -508,7 +508,143 @@ void build_dev(const Program& p, DevProg* d) {
     d->empty_string = p.empty_string;
 }
 
+bool build_dfa(const Program& p, std::vector<uint8_t>* image) {
+    // byte classes: bytes with the same position mask behave alike
+    std::vector<uint64_t> cmask;
+    uint8_t cls_of[256];
+    for (int b = 0; b < 256; b++) {
+        size_t c = 0;
+        while (c < cmask.size() && cmask[c] != p.cls[b]) c++;
+        if (c == cmask.size()) cmask.push_back(p.cls[b]);
+        cls_of[b] = static_cast<uint8_t>(c);
+    }
+    uint32_t nc = static_cast<uint32_t>(cmask.size());
+    const size_t max_states = (kDfaMaxBytes - sizeof(DevDfa)) / (2 * nc);
+    auto follow = [&](uint64_t D) {
+        uint64_t f = 0;
+        for (int b = 0; b < p.npos; b++)
+            if (D >> b & 1) f |= p.follow[b];
+        return f;
+    };
+    std::vector<uint64_t> sets = {0, 0, 0};  // DEAD, ACCEPT, START (sets unused)
+    std::vector<uint16_t> trans;
+    std::vector<std::pair<uint64_t, uint32_t>> index;  // set -> id (linear; state counts are small)
+    auto id_of = [&](uint64_t D, bool& overflow) -> uint32_t {
+        if (D & p.last) return DFA_ACCEPT;
+        if (D == 0 && p.first_mid == 0) return DFA_DEAD;
+        for (auto& e : index)
+            if (e.first == D) return e.second;
+        if (sets.size() >= max_states || sets.size() >= 0x7FFF) { overflow = true; return DFA_DEAD; }
+        const uint32_t id = static_cast<uint32_t>(sets.size());
+        sets.push_back(D);
+        index.push_back({D, id});
+        return id;
+    };
+    auto entry = [&](uint32_t id) -> uint16_t {
+        const bool acc = id == DFA_ACCEPT || (id >= 3 && (sets[id] & p.accept_end) != 0);
+        return static_cast<uint16_t>(id | (acc ? 0x8000u : 0u));
+    };
+    bool overflow = false;
+    trans.assign(3 * nc, 0);
+    for (uint32_t c = 0; c < nc; c++) {
+        trans[DFA_DEAD * nc + c] = entry(DFA_DEAD);
+        trans[DFA_ACCEPT * nc + c] = entry(DFA_ACCEPT);
+    }
+    for (uint32_t c = 0; c < nc; c++) {
+        const uint32_t id = id_of(p.first_at0 & cmask[c], overflow);
+        trans[DFA_START * nc + c] = static_cast<uint16_t>(id);  // flags patched below
+    }
+    for (size_t s = 3; s < sets.size() && !overflow; s++) {
+        trans.resize((s + 1) * nc);
+        const uint64_t f = p.first_mid | follow(sets[s]);
+        for (uint32_t c = 0; c < nc; c++) trans[s * nc + c] = static_cast<uint16_t>(id_of(f & cmask[c], overflow));
+    }
+    if (overflow) return false;
+    trans.resize(sets.size() * nc);
+    for (auto& t : trans) t = entry(t & 0x7FFFu);
+    bool is_full = false;
+    // few states: expand to one column per byte value (no class lookup on
+    // the device's dependent chain)
+    if (sets.size() * kDfaRowBytes < 0x8000u && sizeof(DevDfa) + sets.size() * kDfaRowBytes <= kDfaMaxBytes) {
+        std::vector<uint16_t> full(sets.size() * 256);
+        for (size_t st = 0; st < sets.size(); st++)
+            for (int b = 0; b < 256; b++) full[st * 256 + b] = trans[st * nc + cls_of[b]];
+        // entries hold the next state's row byte offset, so the device forms
+        // the next address with one mask and one add.  Rows are 516 bytes
+        // apart (129 dwords): the LDS bank of an entry is (state + byte/2) mod
+        // 32, so lanes in different states spread over the banks.
+        std::vector<uint16_t> pad(sets.size() * (kDfaRowBytes / 2), 0);
+        for (size_t st = 0; st < sets.size(); st++)
+            for (int b = 0; b < 256; b++) {
+                const uint32_t t = full[st * 256 + b];
+                pad[st * (kDfaRowBytes / 2) + b] = static_cast<uint16_t>((t & 0x7FFFu) * kDfaRowBytes | (t & 0x8000u));
+            }
+        full.swap(pad);
+        trans.swap(full);
+        nc = 256;
+        for (int b = 0; b < 256; b++) cls_of[b] = static_cast<uint8_t>(b);
+        is_full = true;
+    }
+    DevDfa h{};
+    h.nstates = static_cast<uint32_t>(sets.size());
+    h.nclasses = nc;
+    h.empty_string = p.empty_string;
+    h.nonempty_trivial = p.nonempty_trivial;
+    h.full = is_full;
+    h.bytes = static_cast<uint32_t>((sizeof(DevDfa) + 2 * trans.size() + 15) / 16 * 16);
+    std::memcpy(h.cls_of, cls_of, 256);
+    image->assign(h.bytes, 0);
+    std::memcpy(image->data(), &h, sizeof h);
+    std::memcpy(image->data() + sizeof h, trans.data(), 2 * trans.size());
+    return true;
+}
+
 }  // namespace pqre
+
+// DFA form of the same match (test hook: the kernel's automaton on the host).
+// Returns 1/0, PQ_ERR_REGEX for a bad pattern, or PQ_ERR_UNSUPPORTED when the
+// DFA exceeds its size cap.
+extern "C" int pq_regex_match_host_dfa(const char* pattern, const uint8_t* s, size_t n) {
+    pqre::Program p;
+    std::string msg;
+    if (pqre::compile(pattern ? pattern : "", &p, &msg)) return PQ_ERR_REGEX;
+    std::vector<uint8_t> img;
+    if (!pqre::build_dfa(p, &img)) return PQ_ERR_UNSUPPORTED;
+    pqre::DevDfa h;
+    std::memcpy(&h, img.data(), sizeof h);
+    const uint16_t* t = reinterpret_cast<const uint16_t*>(img.data() + sizeof h);
+    if (n == 0) return h.empty_string ? 1 : 0;
+    if (h.nonempty_trivial) return 1;
+    if (h.full) {
+        const uint8_t* tb = reinterpret_cast<const uint8_t*>(t);
+        uint32_t e = pqre::DFA_START * pqre::kDfaRowBytes;
+        for (size_t i = 0; i < n; i++) {
+            uint16_t v;
+            std::memcpy(&v, tb + (e & 0x7FFFu) + 2 * s[i], 2);
+            e = v;
+        }
+        return ((e & 0x7FFFu) == pqre::DFA_ACCEPT * pqre::kDfaRowBytes || (e >> 15)) ? 1 : 0;
+    }
+    uint32_t e = pqre::DFA_START;
+    for (size_t i = 0; i < n; i++) e = t[(e & 0x7FFFu) * h.nclasses + h.cls_of[s[i]]];
+    return ((e & 0x7FFFu) == pqre::DFA_ACCEPT || (e >> 15)) ? 1 : 0;
+}
+
+// DFA statistics of a pattern (diagnostics): states, byte classes, full table.
+extern "C" int pq_regex_dfa_info(const char* pattern, int* nstates, int* nclasses, int* full, int* bytes) {
+    pqre::Program p;
+    std::string msg;
+    if (pqre::compile(pattern ? pattern : "", &p, &msg)) return PQ_ERR_REGEX;
+    std::vector<uint8_t> img;
+    if (!pqre::build_dfa(p, &img)) return PQ_ERR_UNSUPPORTED;
+    pqre::DevDfa h;
+    std::memcpy(&h, img.data(), sizeof h);
+    if (nstates) *nstates = static_cast<int>(h.nstates);
+    if (nclasses) *nclasses = static_cast<int>(h.nclasses);
+    if (full) *full = static_cast<int>(h.full);
+    if (bytes) *bytes = static_cast<int>(h.bytes);
+    return 0;
+}
 
 extern "C" int pq_regex_match_host(const char* pattern, const uint8_t* s, size_t n) {
     pqre::Program p;

@@ -104,6 +104,7 @@ def lib():
             "pq_regex_pages_async": ([vp, vp, C.c_char_p, C.c_int], C.c_int),
             "pq_regex_pages_result": ([vp, vp, vp], C.c_int),
             "pq_regex_match_host": ([C.c_char_p, u8p, C.c_size_t], C.c_int),
+            "pq_regex_match_host_dfa": ([C.c_char_p, u8p, C.c_size_t], C.c_int),
             "pq_timing_enable": ([vp, C.c_int], None),
             "pq_timing_reset": ([vp], None),
             "pq_timing_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)], C.c_int),
@@ -359,6 +360,11 @@ def regex_check(pattern: str):
 
 def regex_match_host(pattern: str, s: bytes) -> int:
     return lib().pq_regex_match_host(pattern.encode(), _buf(s), len(s))
+
+
+def regex_match_host_dfa(pattern: str, s: bytes) -> int:
+    """The GPU kernel's DFA run on the host (-8: DFA over its size cap)."""
+    return lib().pq_regex_match_host_dfa(pattern.encode(), _buf(s), len(s))
 
 
 def canonical_dump(col: HostColumn) -> bytes:

@@ -12,7 +12,7 @@ import pytest
 
 from oracle import oracle as O
 from pqgpu import capi, gen
-from util import file_chunks, to_oracle_chunk
+from util import file_chunks, to_desc, to_oracle_chunk
 
 pytestmark = pytest.mark.gpu
 
@@ -53,9 +53,20 @@ CASES = [
 ]
 
 
+@pytest.fixture(params=["window", "lanes", "nfa"])
+def kernel(request, ctx):
+    """Every page kernel: windowed DFA (default for chunks without dictionary
+    pages), lane-per-page DFA (dictionary chunks) and wave-per-page NFA."""
+    ctx.set_option("regex_dfa", int(request.param != "nfa"))
+    ctx.set_option("regex_plain", int(request.param == "window"))
+    yield request.param
+    ctx.set_option("regex_dfa", 1)
+    ctx.set_option("regex_plain", 1)
+
+
 @pytest.mark.parametrize("neg", [False, True], ids=["like", "notlike"])
 @pytest.mark.parametrize("name,cols,n,layout", CASES, ids=[c[0] for c in CASES])
-def test_regex_pages(ctx, name, cols, n, layout, neg):
+def test_regex_pages(ctx, kernel, name, cols, n, layout, neg):
     f = gen.build(cols, n, 2, seed=7, layout=layout, rows_per_page=700)
     chunks = file_chunks(f, 0)
     dc = ctx.upload(f, chunks)
@@ -65,4 +76,20 @@ def test_regex_pages(ctx, name, cols, n, layout, neg):
         assert len(got) == len(exp)
         bad = np.nonzero(got != exp)[0]
         assert len(bad) == 0, (p, neg, bad[:10])
+    dc.free()
+
+
+def test_regex_reports_decode_errors(ctx, kernel):
+    """A page whose values cannot be decoded fails the scan with the decode's
+    own error text, even when an earlier value already matched."""
+    import struct
+    import pqbuild as B
+    pay = struct.pack("<I", 7) + b"special" + struct.pack("<I", 50) + b"xy"
+    f, ch = B.build_file([B.data_header(len(pay), 2, 0) + pay], gen.BYTE_ARRAY, False, 2)
+    rc_o, msg_o, _ = O.read_all(f, to_oracle_chunk(ch))
+    assert rc_o != 0
+    dc = ctx.upload(f, [to_desc(ch)])
+    with pytest.raises(capi.PqError) as ei:
+        dc.regex_pages("special", False)
+    assert ei.value.code == rc_o and ei.value.msg == msg_o
     dc.free()
