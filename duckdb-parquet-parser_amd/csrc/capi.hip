@@ -41,6 +41,7 @@ struct pq_ctx {
     int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
     uint64_t* d_prof = nullptr;  // "fused_prof": per-phase cycle sums of k_ba_fused / k_ba_batch
     bool opt_batch = false;      // "batch": batched dictionary path (dict_batch.hip)
+    int opt_claim = 1;           // "fused_claim": pages claimed per ticket by k_ba_fused producers (>1 serialises the look-back; diagnostics)
     int opt_batch_bytes = 12288; // "batch_bytes": payload bytes per batch buffer
     bool opt_regex_dfa = true;   // "regex_dfa": DFA kernels (else the NFA kernel)
     bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
@@ -363,6 +364,11 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "fused_waves") == 0) { ctx->opt_waves = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "batch") == 0) { ctx->opt_batch = value != 0; return 0; }
+    if (std::strcmp(key, "fused_claim") == 0) {
+        if (value < 1 || value > 64) return set_err(ctx, PQ_ERR_ARG, "fused_claim: 1..64");
+        ctx->opt_claim = static_cast<int>(value);
+        return 0;
+    }
     if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_win") == 0) {
@@ -706,6 +712,7 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             L.page_err = c->d_page_err; L.err_any = c->d_flags; L.grid = r.grid; L.waves_per_block = r.waves;
             L.debug = ctx->opt_debug;
             L.prof = ctx->d_prof;
+            L.claim = ctx->opt_claim;
             Timed t(ctx, "ba_fused");
             pqk::launch_ba_fused(s, L);
         }

@@ -233,6 +233,148 @@ struct BProf {
     }
 };
 
+
+// ── lean per-lane walks (the common case) ───────────────────────────────────
+// One run header per step: an 8-byte window read, a branch-free varint parse
+// and a few selects.  Mask bits are accumulated in registers and written a
+// word at a time; index runs are only recorded (their character totals are
+// summed afterwards, off the header chain).  Anything unusual — a zero-count
+// run, a varint longer than 4 bytes or cut by the stream end, an RLE value cut
+// by the stream end, bit width > 32 — returns false and the exact state
+// machine (lane_walk.hpp) redoes the stream.
+struct Hdr {
+    uint32_t lit, count, hl, ok;
+};
+__device__ __forceinline__ Hdr parse_hdr(uint64_t x, uint32_t avail) {
+    Hdr h;
+    const uint64_t am = avail >= 8 ? ~0ull : ((1ull << (8 * avail)) - 1ull);
+    const uint32_t stops = static_cast<uint32_t>(~x & 0x80808080ull & am);
+    h.hl = stops ? (static_cast<uint32_t>(__builtin_ctz(stops)) >> 3) + 1 : 0u;
+    uint32_t v = static_cast<uint32_t>((x & 0x7full) | ((x >> 1) & 0x3f80ull) | ((x >> 2) & 0x1fc000ull) |
+                                       ((x >> 3) & 0xfe00000ull));
+    v &= h.hl >= 4 ? 0x0FFFFFFFu : ((1u << (7 * h.hl)) - 1u);
+    h.lit = v & 1u;
+    h.count = h.lit ? (v >> 1) * 8u : (v >> 1);
+    h.ok = stops != 0 && (v >> 1) != 0;
+    return h;
+}
+
+// def levels, bit width <= 8: validity mask (word w of this lane's page at
+// mask[64 w]) and the non-null count.  Returns false: use the exact walk.
+__device__ bool fast_def(const uint32_t* pw, uint32_t psize, uint32_t base, uint32_t size, uint32_t bw,
+                         uint32_t md, uint32_t n, uint32_t* mask, uint32_t& nn, bool& above) {
+    uint32_t pos = 0, row = 0, acc = 0, fill = 0, wi = 0;
+    nn = 0;
+    above = false;
+    bool ok = true;
+    while (row < n) {
+        if (pos >= size) break;  // exhausted: remaining levels are 0 (NULL)
+        const uint64_t x = lds_u64(pw, base + pos);
+        const Hdr h = parse_hdr(x, size - pos);
+        if (!h.ok || h.count == 0) { ok = false; break; }
+        const uint32_t k = min(h.count, n - row);
+        uint32_t bits, nbits = k;
+        uint32_t lbit = 0;
+        if (!h.lit) {
+            if (h.hl >= size - pos) { ok = false; break; }  // value byte cut by the stream end
+            const uint32_t v = static_cast<uint32_t>(x >> (8 * h.hl)) & 0xFFu & ((1u << (8 * ((bw + 7) / 8))) - 1u);
+            above |= v > md;
+            bits = v == md ? 0xFFFFFFFFu : 0u;
+            pos += h.hl + (bw + 7) / 8;
+        } else {
+            if (bw != 1 || md != 1) { ok = false; break; }  // general widths: exact walk
+            lbit = (base + pos + h.hl) * 8u;
+            bits = 0;
+            pos += h.hl + (h.count * bw + 7) / 8;
+        }
+        // append nbits bits (RLE: repeated pattern; literal: the level bits)
+        uint32_t done = 0;
+        while (done < nbits) {
+            const uint32_t take = min(32u - fill, nbits - done);
+            uint32_t chunk = h.lit ? lds_bits(pw, psize, static_cast<uint64_t>(lbit) + done, take) : bits;
+            chunk &= take == 32 ? 0xFFFFFFFFu : ((1u << take) - 1u);
+            nn += __popc(chunk);
+            acc |= chunk << fill;
+            fill += take;
+            done += take;
+            if (fill == 32) {
+                mask[64 * wi] = acc;
+                wi++;
+                acc = 0;
+                fill = 0;
+            }
+        }
+        row += k;
+    }
+    if (fill) mask[64 * wi] = acc;
+    return ok;
+}
+
+// dictionary index stream, bit width <= 32: run records (count | literal |
+// index or bit offset).  Returns false: use the exact walk.
+__device__ bool fast_idx(const uint32_t* pw, uint32_t base, uint32_t size, uint32_t bw, uint32_t need,
+                         uint32_t dict_n, uint32_t* runs, uint32_t run_cap, uint32_t& nruns) {
+    if (bw > 32) return false;
+    const uint32_t nb = (bw + 7) / 8;
+    uint32_t pos = 0, done = 0;
+    nruns = 0;
+    while (done < need) {
+        if (pos >= size) {  // exhausted: zeros
+            if (nruns < run_cap) runs[nruns] = run_rec(need - done, 0u, 0u < dict_n ? 0u : 0xFFFFu);
+            nruns++;
+            break;
+        }
+        const uint64_t x = lds_u64(pw, base + pos);
+        const Hdr h = parse_hdr(x, size - pos);
+        if (!h.ok || h.count == 0) return false;
+        const uint32_t k = min(h.count, need - done);
+        uint32_t rec;
+        if (!h.lit) {
+            if (h.hl + nb > size - pos || h.hl + nb > 8) return false;  // value cut by the stream end
+            const uint32_t v = nb ? static_cast<uint32_t>(x >> (8 * h.hl)) & (nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u))
+                                  : 0u;
+            rec = run_rec(k, 0u, static_cast<int32_t>(v) >= 0 && v < dict_n ? v : 0xFFFFu);
+            pos += h.hl + nb;
+        } else {
+            rec = run_rec(k, 1u, (base + pos + h.hl) * 8u);
+            pos += h.hl + (h.count * bw + 7) / 8;
+        }
+        if (nruns < run_cap) runs[nruns] = rec;
+        nruns++;
+        done += k;
+    }
+    return true;
+}
+
+// character total of a page from its run list (dictionary lengths)
+__device__ uint64_t runs_total(const uint32_t* pw, uint32_t psize, const uint32_t* runs, uint32_t nruns, uint32_t bw,
+                               uint32_t dict_n, const uint32_t* dtab) {
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < nruns; r++) {
+        const uint32_t rec = runs[r];
+        const uint32_t k = run_count(rec), pl = run_payload(rec);
+        if (!run_lit(rec)) {
+            if (pl != 0xFFFFu) total += static_cast<uint64_t>(k) * (dtab[pl] >> 16);
+        } else {
+            uint32_t i = 0;
+            for (; i + 4 <= k; i += 4) {
+                uint32_t v[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++)
+                    v[u] = lds_bits(pw, psize, static_cast<uint64_t>(pl) + static_cast<uint64_t>(i + u) * bw, bw);
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++)
+                    if (static_cast<int32_t>(v[u]) >= 0 && v[u] < dict_n) total += dtab[v[u]] >> 16;
+            }
+            for (; i < k; i++) {
+                const uint32_t v = lds_bits(pw, psize, static_cast<uint64_t>(pl) + static_cast<uint64_t>(i) * bw, bw);
+                if (static_cast<int32_t>(v) >= 0 && v < dict_n) total += dtab[v] >> 16;
+            }
+        }
+    }
+    return total;
+}
+
 // ── producer ────────────────────────────────────────────────────────────────
 template <bool kProf>
 __device__ void batch_produce(const BArgs& a, const BLayout& L, uint8_t* base, Ctrl* ctrl, const uint32_t* dtab,
@@ -307,37 +449,42 @@ __device__ void batch_produce(const BArgs& a, const BLayout& L, uint8_t* base, C
                     nn = n;
                 } else {
                     // def levels: rows with level == max_def are non-null
-                    LRle r{def_base, dl, 0, bw_def, 0, 0, 0, 0, 0, 0};
-                    uint32_t row = 0;
-                    bool above = false;
                     const uint32_t md = static_cast<uint32_t>(a.max_def);
-                    code = lane_rle(r, rd8, n, [&](uint32_t kind, uint32_t k, uint32_t arg) {
-                        if (kind == 0) {
-                            if (arg > md) above = true;
-                            if (arg == md && k) {
-                                nn += k;
-                                uint32_t r0 = row;
-                                const uint32_t r1 = row + k;
-                                while (r0 < r1) {
-                                    const uint32_t w = r0 >> 5, b = r0 & 31;
-                                    const uint32_t cnt = min(32u - b, r1 - r0);
-                                    const uint32_t m = cnt == 32 ? 0xFFFFFFFFu : (((1u << cnt) - 1u) << b);
-                                    mask[64 * w] |= m;
-                                    r0 += cnt;
+                    bool above = false;
+                    if (!fast_def(pw, size, def_base, dl, bw_def, md, n, mask, nn, above)) {
+                        for (uint32_t w = 0; w < L.mask_words; w++) mask[64 * w] = 0u;
+                        nn = 0;
+                        above = false;
+                        LRle r{def_base, dl, 0, bw_def, 0, 0, 0, 0, 0, 0};
+                        uint32_t row = 0;
+                        code = lane_rle(r, rd8, n, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                            if (kind == 0) {
+                                if (arg > md) above = true;
+                                if (arg == md && k) {
+                                    nn += k;
+                                    uint32_t r0 = row;
+                                    const uint32_t r1 = row + k;
+                                    while (r0 < r1) {
+                                        const uint32_t w = r0 >> 5, b = r0 & 31;
+                                        const uint32_t cnt = min(32u - b, r1 - r0);
+                                        const uint32_t m = cnt == 32 ? 0xFFFFFFFFu : (((1u << cnt) - 1u) << b);
+                                        mask[64 * w] |= m;
+                                        r0 += cnt;
+                                    }
+                                }
+                            } else {
+                                for (uint32_t i = 0; i < k; i++) {
+                                    const uint32_t v = lds_bits(pw, size, static_cast<uint64_t>(arg) + i * bw_def, bw_def);
+                                    if (v > md) above = true;
+                                    if (v == md) {
+                                        nn++;
+                                        mask[64 * ((row + i) >> 5)] |= 1u << ((row + i) & 31);
+                                    }
                                 }
                             }
-                        } else {
-                            for (uint32_t i = 0; i < k; i++) {
-                                const uint32_t v = lds_bits(pw, size, static_cast<uint64_t>(arg) + i * bw_def, bw_def);
-                                if (v > md) above = true;
-                                if (v == md) {
-                                    nn++;
-                                    mask[64 * ((row + i) >> 5)] |= 1u << ((row + i) & 31);
-                                }
-                            }
-                        }
-                        row += k;
-                    });
+                            row += k;
+                        });
+                    }
                     if (!code && above) code = PQ_ERR_UNSUPPORTED;
                 }
             }
@@ -350,21 +497,34 @@ __device__ void batch_produce(const BArgs& a, const BLayout& L, uint8_t* base, C
                     ibw = lds_u32a(pw, pos) & 0xFFu;
                     pos += 1;
                     ipos = pos;
-                    LRle r{pos, size - pos, 0, ibw, 0, 0, 0, 0, 0, 0};
-                    code = lane_rle(r, rd8, nn, [&](uint32_t kind, uint32_t k, uint32_t arg) {
-                        if (kind == 0) {
-                            const uint32_t idx = static_cast<int32_t>(arg) >= 0 && arg < dict_n ? arg : 0xFFFFu;
-                            if (idx != 0xFFFFu) total += static_cast<uint64_t>(k) * (dtab[idx] >> 16);
-                            if (nruns < run_cap) runs[nruns] = run_rec(k, 0u, idx);
-                        } else {
-                            for (uint32_t i = 0; i < k; i++) {
-                                const uint32_t v = lds_bits(pw, size, static_cast<uint64_t>(arg) + i * ibw, ibw);
-                                if (static_cast<int32_t>(v) >= 0 && v < dict_n) total += dtab[v] >> 16;
+                    if (!fast_idx(pw, pos, size - pos, ibw, nn, dict_n, runs, run_cap, nruns)) {
+                        nruns = 0;
+                        LRle r{pos, size - pos, 0, ibw, 0, 0, 0, 0, 0, 0};
+                        code = lane_rle(r, rd8, nn, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                            if (kind == 0) {
+                                const uint32_t idx = static_cast<int32_t>(arg) >= 0 && arg < dict_n ? arg : 0xFFFFu;
+                                if (nruns < run_cap) runs[nruns] = run_rec(k, 0u, idx);
+                            } else {
+                                if (nruns < run_cap) runs[nruns] = run_rec(k, 1u, arg);
                             }
-                            if (nruns < run_cap) runs[nruns] = run_rec(k, 1u, arg);
-                        }
-                        nruns++;
-                    });
+                            nruns++;
+                        });
+                    }
+                    if (!code && nruns <= run_cap) total = runs_total(pw, size, runs, nruns, ibw, dict_n, dtab);
+                    if (!code && nruns > run_cap) {  // total from the exact walk, values not kept
+                        LRle r{pos, size - pos, 0, ibw, 0, 0, 0, 0, 0, 0};
+                        total = 0;
+                        (void)lane_rle(r, rd8, nn, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                            if (kind == 0) {
+                                if (static_cast<int32_t>(arg) >= 0 && arg < dict_n) total += static_cast<uint64_t>(k) * (dtab[arg] >> 16);
+                            } else {
+                                for (uint32_t i = 0; i < k; i++) {
+                                    const uint32_t v = lds_bits(pw, size, static_cast<uint64_t>(arg) + i * ibw, ibw);
+                                    if (static_cast<int32_t>(v) >= 0 && v < dict_n) total += dtab[v] >> 16;
+                                }
+                            }
+                        });
+                    }
                     if (nruns > run_cap) flags |= REC_SERIAL;
                 }
             }
@@ -438,7 +598,7 @@ __device__ __forceinline__ void store_block(uint8_t* chars, int64_t blk, uint32_
 
 // Characters of one page through the LDS ring (see dict_fused.hip).
 __device__ void ring_copy(const BArgs& a, const uint32_t* off, const uint16_t* rsrc, uint32_t* ring,
-                          const uint32_t* srcw, uint32_t n, int64_t G0, int64_t G1) {
+                          const uint32_t* srcw, uint32_t srcw_last, uint32_t n, int64_t G0, int64_t G1) {
     constexpr uint32_t kRingMask = kRingBytes / 4 - 1;
     int64_t fb = G0 >> 4;
     uint32_t r0 = 0;
@@ -450,22 +610,30 @@ __device__ void ring_copy(const BArgs& a, const uint32_t* off, const uint16_t* r
         const uint32_t k = fit == ~0ull ? kWave : static_cast<uint32_t>(__builtin_ctzll(~fit));
         const uint32_t cnt = k ? k : 1u;
         if (lane() < cnt) {
+            // all source dwords of a 64-byte segment are read before any
+            // destination dword is written (one LDS round trip per segment)
             const uint32_t s0 = off[r];
             const uint32_t len = e - s0;
             const uint32_t src = rsrc[r];
-            int64_t d = G0 + s0;
-            uint32_t q = 0;
-            while (q < len) {
-                const uint32_t lo = static_cast<uint32_t>(d & 3);
-                const uint32_t take = min(4u - lo, len - q);
-                const uint32_t x = lds_u32a(srcw, src + q);
-                const uint32_t m = take == 4 ? 0xFFFFFFFFu : ((1u << (8 * take)) - 1u);
-                const uint32_t v = (x & m) << (8 * lo);
-                const uint32_t wi = static_cast<uint32_t>(d >> 2) & kRingMask;
-                if (take == 4) ring[wi] = v;
-                else atomicOr(&ring[wi], v);
-                q += take;
-                d += take;
+            const int64_t d = G0 + s0;
+            const uint32_t lo0 = static_cast<uint32_t>(d & 3);
+            const uint32_t nd = (lo0 + len + 3) >> 2;
+            const uint32_t a0 = src - lo0;  // >= 1: every value follows a 4-byte length prefix
+            const uint32_t sh = a0 & 3, i0 = a0 >> 2;
+            const uint32_t lastb = (lo0 + len - 1) & 3;
+            const uint32_t dw0 = static_cast<uint32_t>(d >> 2);
+            for (uint32_t j0 = 0; j0 < nd && len; j0 += 16) {
+                uint32_t x[17];
+#pragma unroll
+                for (uint32_t k = 0; k < 17; k++) x[k] = srcw[min(i0 + j0 + k, srcw_last)];
+#pragma unroll
+                for (uint32_t k = 0; k < 16; k++) {
+                    const uint32_t j = j0 + k;
+                    uint32_t v = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+                    if (j == 0) v &= 0xFFFFFFFFu << (8 * lo0);
+                    if (j == nd - 1) v &= 0xFFFFFFFFu >> (8 * (3 - lastb));
+                    if (j < nd) atomicOr(&ring[(dw0 + j) & kRingMask], v);
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -665,7 +833,7 @@ __device__ void batch_write(const BArgs& a, const BLayout& L, uint8_t* base, Ctr
                 if (G1 > a.capacity) {
                     if (lane() == 0) atomicOr(a.overflow, 1);
                 } else if (bcast_last(wave_incl_max(maxlen)) <= kRingMaxRow) {
-                    ring_copy(a, off, rsrc, ring, dwords, n, G0, G1);
+                    ring_copy(a, off, rsrc, ring, dwords, a.dict_chars_bytes / 4 - 1, n, G0, G1);
                 } else {
                     slow_copy(a, off, rsrc, dwords, n, G0);
                 }

@@ -207,11 +207,12 @@ struct FusedArgs {
     int32_t* err_any;
     int32_t debug;               // ablation switches (timing only; output invalid)
     uint64_t* prof;              // per-phase cycle sums (kProfSlots), or null
+    int32_t claim;               // pages claimed per ticket (one atomic per claim)
 };
 
 enum {
     PH_STAGE = 0, PH_DEF, PH_LEVELS, PH_VALUES, PH_ROWS, PH_LOOKBACK, PH_SLOTWAIT, PH_PAGES,
-    PH_W_WAIT, PH_W_OFFSETS, PH_W_GATHER, PH_W_PAGES, kProfSlots
+    PH_W_WAIT, PH_W_OFFSETS, PH_W_GATHER, PH_W_PAGES, PH_HA, PH_HB, PH_HC, PH_HD, kProfSlots
 };
 
 enum : uint32_t { SLOT_FREE = 0, SLOT_FULL = 1, SLOT_DONE = 2 };
@@ -392,10 +393,27 @@ __device__ void produce(const FusedArgs& a, const PairLayout& L, uint8_t* pair, 
     Prof<kProf> P;
     P.start();
     uint32_t si = 0;
+    // Same-address atomics serialise chip-wide, so a producer claims `claim`
+    // consecutive pages per ticket; it still processes pages in ticket order,
+    // which keeps the look-back deadlock-free.
+    int32_t tnext = 0, tend = 0;
+    // debug bit 64 (with bit 1, no look-back): static page assignment, to
+    // time the ticket atomics
+    const bool stat = (a.debug & 65) == 65;
+    const int32_t nprod = static_cast<int32_t>(gridDim.x * (blockDim.x / (2 * kWave)));
+    int32_t sp = static_cast<int32_t>(blockIdx.x * (blockDim.x / (2 * kWave)) + threadIdx.x / kWave);
     for (;;) {
-        int32_t t = 0;
-        if (lane() == 0) t = atomicAdd(a.ticket, 1);
-        t = static_cast<int32_t>(suni(static_cast<uint32_t>(t)));
+        if (stat) {
+            tnext = sp;
+            tend = sp + 1;
+            sp += nprod;
+        } else if (tnext == tend) {
+            int32_t c = 0;
+            if (lane() == 0) c = atomicAdd(a.ticket, a.claim);
+            tnext = static_cast<int32_t>(suni(static_cast<uint32_t>(c)));
+            tend = tnext + a.claim;
+        }
+        const int32_t t = tnext++;
         Slot S = slot_at(slots + si * L.slot, L);
         flag_wait(S.meta, true);
         P.mark(PH_SLOTWAIT);
@@ -457,7 +475,8 @@ __device__ void produce(const FusedArgs& a, const PairLayout& L, uint8_t* pair, 
                     if (st == 0) M.lv[j] = static_cast<uint8_t>(v > 255 ? 255 : v);
                     else M.ix[j] = static_cast<uint16_t>(static_cast<int32_t>(v) >= 0 && v < dict_n ? v : 0xFFFFu);
                 };
-                if (hyb_decode(pw, size, sbase, slen, sbw, scount, M.hyb, L.hyb_runs, M.ix, put)) {
+                auto hm = [&](int ph) { P.mark(PH_HA + ph); };
+                if (hyb_decode(pw, size, sbase, slen, sbw, scount, M.hyb, L.hyb_runs, M.ix, put, hm)) {
                     SRle r;
                     srle_init(r, sbase, slen, sbw);
                     code = srle_walk(r, page, scount, put, M.lits, nl, kLitCap,
@@ -598,8 +617,8 @@ __device__ __forceinline__ void store_block(uint8_t* chars, int64_t blk, uint32_
 // Characters of one page, input-driven: one row per lane copies its bytes
 // into an LDS ring indexed by global byte address (so ring blocks line up
 // with 16-byte output blocks); completed blocks are streamed out and zeroed.
-__device__ void copy_chars(const FusedArgs& a, const Slot& S, uint32_t* ring, const uint32_t* srcw, uint32_t n,
-                           int64_t G0, int64_t G1) {
+__device__ void copy_chars(const FusedArgs& a, const Slot& S, uint32_t* ring, const uint32_t* srcw,
+                           uint32_t srcw_last, uint32_t n, int64_t G0, int64_t G1) {
     constexpr uint32_t kRingMask = kRingBytes / 4 - 1;  // in words
     int64_t fb = G0 >> 4;  // first block not yet stored
     uint32_t r0 = 0;
@@ -612,22 +631,31 @@ __device__ void copy_chars(const FusedArgs& a, const Slot& S, uint32_t* ring, co
         const uint32_t k = fit == ~0ull ? kWave : static_cast<uint32_t>(__builtin_ctzll(~fit));
         const uint32_t cnt = k ? k : 1u;  // a row longer than the ring never reaches here
         if (lane() < cnt) {
+            // destination dwords [d >> 2, (d + L - 1) >> 2]; all source dwords
+            // of a 64-byte segment are read before any is written, so a row
+            // costs one LDS round trip per segment
             const uint32_t s0 = S.off[r];
             const uint32_t L = e - s0;
             const uint32_t src = S.rsrc[r];
-            int64_t d = G0 + s0;
-            uint32_t q = 0;
-            while (q < L) {
-                const uint32_t lo = static_cast<uint32_t>(d & 3);
-                const uint32_t take = min(4u - lo, L - q);
-                const uint32_t x = lds_u32(srcw, src + q);
-                const uint32_t m = take == 4 ? 0xFFFFFFFFu : ((1u << (8 * take)) - 1u);
-                const uint32_t v = (x & m) << (8 * lo);
-                const uint32_t wi = static_cast<uint32_t>(d >> 2) & kRingMask;
-                if (take == 4) ring[wi] = v;
-                else atomicOr(&ring[wi], v);
-                q += take;
-                d += take;
+            const int64_t d = G0 + s0;
+            const uint32_t lo0 = static_cast<uint32_t>(d & 3);
+            const uint32_t nd = (lo0 + L + 3) >> 2;
+            const uint32_t a0 = src - lo0;  // >= 1: every value follows a 4-byte length prefix
+            const uint32_t sh = a0 & 3, i0 = a0 >> 2;
+            const uint32_t lastb = (lo0 + L - 1) & 3;
+            const uint32_t dw0 = static_cast<uint32_t>(d >> 2);
+            for (uint32_t j0 = 0; j0 < nd && L; j0 += 16) {
+                uint32_t x[17];
+#pragma unroll
+                for (uint32_t k = 0; k < 17; k++) x[k] = srcw[min(i0 + j0 + k, srcw_last)];
+#pragma unroll
+                for (uint32_t k = 0; k < 16; k++) {
+                    const uint32_t j = j0 + k;
+                    uint32_t v = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+                    if (j == 0) v &= 0xFFFFFFFFu << (8 * lo0);
+                    if (j == nd - 1) v &= 0xFFFFFFFFu >> (8 * (3 - lastb));
+                    if (j < nd) atomicOr(&ring[(dw0 + j) & kRingMask], v);
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -760,7 +788,7 @@ __device__ void write_pages(const FusedArgs& a, const PairLayout& L, uint8_t* pa
         if (total && !(a.debug & 2) && G1 > a.capacity) {
             if (lane() == 0) atomicOr(a.overflow, 1);
         } else if (total && !(a.debug & 2) && __builtin_amdgcn_readfirstlane(S.meta->maxlen) <= kRingMaxRow) {
-            copy_chars(a, S, ring, srcw, n, G0, G1);
+            copy_chars(a, S, ring, srcw, (dict ? a.dict_chars_bytes : a.stage_bytes) / 4 - 1, n, G0, G1);
         } else if (total && !(a.debug & 2)) {
             gather_chars(a, S, ring, srcw, n, G0, G1);
             for (uint32_t i = lane(); i < kRingBytes / 16; i += kWave)
@@ -857,6 +885,7 @@ void launch_ba_fused(hipStream_t s, const FusedLaunch& L) {
     a.validity = L.validity; a.offsets = L.offsets; a.chars = L.chars; a.capacity = L.capacity;
     a.overflow = L.overflow; a.page_err = L.page_err; a.err_any = L.err_any; a.debug = L.debug;
     a.prof = L.prof;
+    a.claim = L.claim > 0 ? L.claim : 1;
     const uint32_t lds = L.dict_bytes + (L.waves_per_block / 2) * L.wave_bytes;
     set_fused_attrs();
     if (a.prof)

@@ -66,9 +66,15 @@ __device__ inline HybScratch hyb_carve(uint8_t* p, uint32_t maxpos, uint32_t max
 // j < n.  R: n u16 slots of LDS scratch (may alias the output array when
 // out writes slot j only after reading R[j] in the same lane).  Returns 0,
 // or 1 if the stream needs the serial walk (nothing was written then).
-template <class Out>
+struct NoMark {
+    __device__ void operator()(int) const {}
+};
+
+// mark(phase) is called after each of the phases A..D (0..3), for profiling.
+template <class Out, class Mark = NoMark>
 __device__ int hyb_decode(const uint32_t* pw, uint32_t psize, uint32_t base, uint32_t S, uint32_t bw,
-                          uint32_t n, const HybScratch& sc, uint32_t maxruns, uint16_t* R, Out&& out) {
+                          uint32_t n, const HybScratch& sc, uint32_t maxruns, uint16_t* R, Out&& out,
+                          Mark&& mark = Mark()) {
     constexpr uint32_t U = 4;  // positions / outputs per lane per batch (loads issued together)
     if (n == 0) return 0;
     if (S > kHybMaxPos || bw > 32) return 1;
@@ -125,12 +131,14 @@ __device__ int hyb_decode(const uint32_t* pw, uint32_t psize, uint32_t base, uin
     }
     if (lane() == 0) { sc.nx0[S] = static_cast<uint16_t>(S); sc.nx1[S] = static_cast<uint16_t>(S); sc.on[S] = 0; }
     __builtin_amdgcn_wave_barrier();
+    mark(0);
     // B. chain membership by pointer doubling: on |= J(on), J = J o J
     uint16_t* J = sc.nx0;
     uint16_t* K = sc.nx1;
+    // J[0] of the round is read by lane 0 in the round's first batch, so the
+    // termination test costs no extra LDS round trip
     for (;;) {
-        const uint32_t j0 = __builtin_amdgcn_readfirstlane(J[0]);
-        if (j0 >= S) break;
+        uint32_t j0 = S;
         for (uint32_t p0 = 0; p0 < S; p0 += U * kWave) {
             uint32_t jp[U], o[U], jj[U];
 #pragma unroll
@@ -138,6 +146,10 @@ __device__ int hyb_decode(const uint32_t* pw, uint32_t psize, uint32_t base, uin
                 const uint32_t p = p0 + u * kWave + lane();
                 jp[u] = p < S ? J[p] : S;
                 o[u] = p < S ? sc.on[p] : 0u;
+            }
+            if (p0 == 0) {
+                j0 = __builtin_amdgcn_readfirstlane(jp[0]);
+                if (j0 >= S) break;  // chain fully marked: nothing written this round
             }
 #pragma unroll
             for (uint32_t u = 0; u < U; u++) jj[u] = J[jp[u]];
@@ -148,10 +160,12 @@ __device__ int hyb_decode(const uint32_t* pw, uint32_t psize, uint32_t base, uin
                 if (o[u]) sc.on[jp[u]] = 1;
             }
         }
+        if (j0 >= S) break;
         __builtin_amdgcn_wave_barrier();
         uint16_t* t = J; J = K; K = t;
     }
     __builtin_amdgcn_wave_barrier();
+    mark(1);
     // C. run starts (prefix of lengths in byte order), run list, serial check
     for (uint32_t j = lane(); j < n; j += kWave) R[j] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -191,6 +205,7 @@ __device__ int hyb_decode(const uint32_t* pw, uint32_t psize, uint32_t base, uin
     }
     if (__ballot(serial)) return 1;
     __builtin_amdgcn_wave_barrier();
+    mark(2);
     // D. run of every output (max-scan) and expansion
     const uint32_t total = csum;
     uint32_t carry = 0;
@@ -226,6 +241,7 @@ __device__ int hyb_decode(const uint32_t* pw, uint32_t psize, uint32_t base, uin
         }
     }
     __builtin_amdgcn_wave_barrier();
+    mark(3);
     return 0;
 }
 

@@ -108,6 +108,7 @@ struct FusedLaunch {
     int waves_per_block;
     int debug;
     uint64_t* prof;  // per-phase cycle sums (fused_prof_slots()), or null
+    int claim;       // pages per ticket
 };
 
 // ── batched dictionary BYTE_ARRAY path (dict_batch.hip) ────────────────────

@@ -266,7 +266,7 @@ class Context:
         self.check(lib().pq_ctx_sync(self.h))
 
     PROF_PHASES = ("stage", "def", "levels", "values", "rows", "lookback", "slotwait", "pages",
-                   "w_wait", "w_offsets", "w_gather", "w_pages")
+                   "w_wait", "w_offsets", "w_gather", "w_pages", "hyb_A", "hyb_B", "hyb_C", "hyb_D")
 
     def fused_prof_read(self, raw: bool = False):
         """Per-phase shader-clock sums of k_ba_fused / k_ba_batch since the

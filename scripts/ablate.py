@@ -31,7 +31,8 @@ chunks = [F.chunk(0, 0)]
 ctx = capi.Context(0)
 
 
-def setp(path, dbg=0, waves=0, bbytes=12288):
+def setp(path, dbg=0, waves=0, bbytes=12288, claim=1):
+    ctx.set_option("fused_claim", claim)
     ctx.set_option("fused_ba", int(path != "generic"))
     ctx.set_option("batch", int(path == "batch"))
     ctx.set_option("fused_debug", dbg)
@@ -39,10 +40,10 @@ def setp(path, dbg=0, waves=0, bbytes=12288):
     ctx.set_option("batch_bytes", bbytes)
 
 
-variants = [("batch", 0, 0, 12288), ("batch", 1, 0, 12288), ("batch", 3, 0, 12288),
-            ("batch", 0, 0, 16384), ("fused", 0, 0, 12288)]
-for path, dbg, waves, bb in variants:
-    setp(path, dbg, waves, bb)
+variants = [("fused", 0, 0, 12288, 1), ("batch", 0, 0, 12288, 1), ("batch", 1, 0, 12288, 1),
+            ("batch", 3, 0, 12288, 1), ("batch", 0, 0, 16384, 1), ("batch", 0, 0, 8192, 1)]
+for path, dbg, waves, bb, claim in variants:
+    setp(path, dbg, waves, bb, claim)
     dc = ctx.upload(f, chunks)
     dc.decode_async()
     ctx.sync()
@@ -57,7 +58,8 @@ for path, dbg, waves, bb in variants:
         if n:
             res[k] = round(ms / n, 4)
     ctx.timing(False)
-    print(json.dumps({"path": path, "debug": dbg, "waves": waves, "batch_bytes": bb, "ms": res}), flush=True)
+    print(json.dumps({"path": path, "debug": dbg, "waves": waves, "batch_bytes": bb, "claim": claim, "ms": res}),
+          flush=True)
     dc.free()
 
 ctx.set_option("fused_prof", 1)
