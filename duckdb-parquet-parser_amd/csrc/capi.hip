@@ -46,6 +46,7 @@ struct pq_ctx {
     bool opt_regex_dfa = true;   // "regex_dfa": DFA kernels (else the NFA kernel)
     bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
+    bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
 };
 
 struct pq_chunk {
@@ -81,6 +82,10 @@ struct pq_chunk {
     int32_t* d_flags = nullptr;  // [0] err_any, [1] overflow
     uint64_t* d_row_codes = nullptr;
     int64_t* d_tile_chars = nullptr;
+    // tile-parallel PLAIN fixed-width decode (fixed_fast.hip)
+    bool fixed_plain = false;
+    int32_t* d_tile_rank = nullptr;
+    int32_t* d_page_pos = nullptr;
     int64_t* d_tile_base = nullptr;
     int64_t* d_total = nullptr;
     int64_t* d_scan_scratch = nullptr;
@@ -217,6 +222,8 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_flags);
     dfree(c->d_row_codes);
     dfree(c->d_tile_chars);
+    dfree(c->d_tile_rank);
+    dfree(c->d_page_pos);
     dfree(c->d_tile_base);
     dfree(c->d_total);
     dfree(c->d_scan_scratch);
@@ -371,6 +378,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     }
     if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
+    if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_win") == 0) {
         if (value < 1024 || value > 32768 || value % 16) return set_err(ctx, PQ_ERR_ARG, "regex_win: 1024..32768, multiple of 16");
         ctx->opt_regex_win = static_cast<int>(value);
@@ -519,6 +527,11 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
                                          std::min(pqk::kTileRows, hpages[p].nvals - r), 0});
         }
         c->ntiles = static_cast<int>(htiles.size());
+        // every data page PLAIN, a fixed-width type whose bytes are copied as is
+        c->fixed_plain = (c->type == PQ_INT32 || c->type == PQ_INT64 || c->type == PQ_FLOAT ||
+                          c->type == PQ_DOUBLE || c->type == PQ_INT96) &&
+                         c->width == c->plain_width && c->max_def >= 0 && c->max_rep >= 0;
+        for (const auto& pg : hpages) c->fixed_plain &= pg.mode == pqk::MODE_PLAIN;
 
         // 2) device allocations + one upload
         int rc = 0;
@@ -533,6 +546,10 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         rc |= dalloc(&c->d_dict_err, hdicts.size());
         rc |= dalloc(&c->d_flags, 4);
         rc |= dalloc(&c->d_tile_chars, htiles.size());
+        if (c->fixed_plain) {
+            rc |= dalloc(&c->d_tile_rank, htiles.size());
+            rc |= dalloc(&c->d_page_pos, hpages.size());
+        }
         rc |= dalloc(&c->d_tile_base, htiles.size());
         rc |= dalloc(&c->d_total, 1);
         rc |= dalloc(&c->d_scan_scratch, htiles.size() / 8192 + 16);
@@ -566,6 +583,8 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc = hip_check(ctx, hipMemcpyAsync(c->d_tiles, htiles.data(), htiles.size() * sizeof(DevTile), hipMemcpyHostToDevice, s), "upload");
         if (!rc && !tile0.empty())
             rc = hip_check(ctx, hipMemcpyAsync(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
+        if (!rc) (void)hipMemsetAsync(c->d_page_err, 0, std::max<size_t>(hpages.size(), 1) * sizeof(DevErr), s);
+        if (!rc) (void)hipMemsetAsync(c->d_dict_err, 0, std::max<size_t>(hdicts.size(), 1) * sizeof(DevErr), s);
         if (!rc && c->d_batches)
             rc = hip_check(ctx, hipMemcpyAsync(c->d_batches, c->hbatches.data(), c->hbatches.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice, s), "upload");
         if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
@@ -734,6 +753,11 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
         }
         launch_gather(ctx, c, out);
+    } else if (c->fixed_plain && ctx->opt_fixed_plain) {
+        Timed t(ctx, "fixed_plain");
+        pqk::launch_fixed_plain(s, c->d_bytes, c->d_pages, c->npages, c->d_tiles, c->ntiles, c->d_page_tile0, cp,
+                                out->d_validity, out->d_values, c->d_tile_rank, c->d_page_pos, c->d_page_err,
+                                c->d_flags);
     } else {
         Timed t(ctx, "fixed");
         pqk::launch_fixed(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_dict_count, cp,

@@ -1,0 +1,247 @@
+// fixed_fast.hip — tile-parallel PLAIN fixed-width decode (SURVEY §8a R-PLAIN,
+// R-LEVELS) for INT32 / INT64 / FLOAT / DOUBLE / INT96 chunks whose data
+// pages are all PLAIN.
+//
+// decode.hip's k_fixed gives each page one wavefront that walks its 512-row
+// tiles in order; arrow-layout pages hold 20k rows, so a 10M-row chunk is
+// only 500 wavefronts.  Here the work is split by tile:
+//   k_fixed_req      REQUIRED columns: every tile copies its rows' bytes
+//                    straight from the page (column_reader.cpp:241-248 is a
+//                    memcpy per value) with 16-byte loads/stores, and sets its
+//                    validity bits.
+//   k_fixed_levels   OPTIONAL columns, one wavefront per page: the def-level
+//                    stream (exact scalar walk, stream.hpp) -> validity bits
+//                    of the page's rows, per-tile ranks of the first non-null
+//                    row, and the PLAIN bounds check (ByteBuffer::check on the
+//                    first rank whose read overruns, after all levels, as the
+//                    reference orders it).
+//   k_fixed_scatter  OPTIONAL columns, one wavefront per tile: row -> rank by
+//                    a popcount prefix of the validity bits, value bytes from
+//                    pos + rank * width; NULL rows are zero.
+#include "kernels/device_common.hpp"
+#include "kernels/kernels.hpp"
+#include "kernels/lane_walk.hpp"
+#include "kernels/stream.hpp"
+#include "pq_gpu.h"
+
+namespace pqk {
+namespace {
+
+using namespace dev;
+
+constexpr int kTilesPerBlock = 4;
+constexpr uint32_t kLitCapF = 16;
+
+// Validity bits of rows [R, R + cnt) (cnt <= 64) from a 64-bit lane ballot
+// `vm` (bit j = row R + j); words fully inside [lo_row, hi_row) are stored,
+// others ORed (a neighbouring page or tile owns their other bits).
+__device__ __forceinline__ void put_valid64(uint32_t* validity, int64_t R, uint32_t cnt, uint64_t vm,
+                                            int64_t lo_row, int64_t hi_row) {
+    const uint32_t wi = static_cast<uint32_t>(R >> 5), sh = static_cast<uint32_t>(R & 31);
+    if (lane() < 3) {
+        const uint32_t part = lane() == 0 ? static_cast<uint32_t>(vm << sh)
+                            : lane() == 1 ? static_cast<uint32_t>(sh ? (vm >> (32 - sh)) : (vm >> 32))
+                                          : (sh ? static_cast<uint32_t>(vm >> (64 - sh)) : 0u);
+        const int64_t wlo = static_cast<int64_t>(wi + lane()) * 32;
+        const int64_t rhi = R + cnt;
+        const bool full = wlo >= lo_row && wlo + 32 <= hi_row && wlo >= R && wlo + 32 <= rhi;
+        if (wlo < rhi && wlo + 32 > R) {
+            if (full) validity[wi + lane()] = part;
+            else if (part) atomicOr(&validity[wi + lane()], part);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_fixed_req(const uint8_t* __restrict__ bytes, const DevPage* __restrict__ pages,
+                                                   const DevTile* __restrict__ tiles, int ntiles, uint32_t pw,
+                                                   uint32_t* __restrict__ validity, uint8_t* __restrict__ values,
+                                                   DevErr* __restrict__ page_err, int32_t* __restrict__ err_any) {
+    const int t = blockIdx.x * kTilesPerBlock + static_cast<int>(threadIdx.x / kWave);
+    if (t >= ntiles) return;
+    const DevTile T = tiles[t];
+    const DevPage pg = pages[T.page];
+    const uint32_t size = static_cast<uint32_t>(pg.size);
+    const uint32_t r0 = static_cast<uint32_t>(T.row0), m = static_cast<uint32_t>(T.nrows);
+    // ByteBuffer::check (common.hpp:162-168): the first rank whose read
+    // overruns the page; its tile reports it, no tile copies past it
+    const uint64_t need = static_cast<uint64_t>(max(pg.nvals, 0)) * pw;
+    uint32_t mc = m;
+    if (need > size) {
+        const uint32_t k = size / pw;
+        if (k >= r0 && k < r0 + m) set_err(page_err + T.page, err_any, PQ_ERR_BUFFER, k * pw, pw, size);
+        mc = k > r0 ? min(m, k - r0) : 0u;
+    }
+    const int64_t R0 = pg.first_row + r0;
+    const uint8_t* src = bytes + pg.off + static_cast<uint64_t>(r0) * pw;
+    uint8_t* dst = values + static_cast<uint64_t>(R0) * pw;
+    const uint32_t nbytes = mc * pw;
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        const uint32_t n16 = nbytes / 16;
+        for (uint32_t i = lane(); i < n16; i += kWave) d4[i] = s4[i];
+        for (uint32_t i = n16 * 4 + lane(); i < nbytes / 4; i += kWave)
+            reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
+    } else {
+        for (uint32_t i = lane(); i < nbytes / 4; i += kWave)
+            reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
+    }
+    for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
+        const uint32_t cnt = min(64u, m - j0);
+        put_valid64(validity, R0 + j0, cnt, __ballot(lane() < cnt), R0, R0 + m);
+    }
+}
+
+// One wavefront per page.  tile_rank[t] = non-null rows of the page before
+// tile t; page_pos[p] = the byte where the page's values start.
+__global__ void __launch_bounds__(256) k_fixed_levels(const uint8_t* __restrict__ bytes,
+                                                      const DevPage* __restrict__ pages, int npages,
+                                                      const int32_t* __restrict__ page_tile0, ColumnParams cp,
+                                                      uint32_t* __restrict__ validity,
+                                                      int32_t* __restrict__ tile_rank,
+                                                      int32_t* __restrict__ page_pos,
+                                                      DevErr* __restrict__ page_err,
+                                                      int32_t* __restrict__ err_any) {
+    __shared__ LitRun lits_all[kTilesPerBlock][kLitCapF];
+    __shared__ uint32_t bits_all[kTilesPerBlock][kTileRows / 32];
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    const int p = blockIdx.x * kTilesPerBlock + wv;
+    if (p >= npages) return;
+    LitRun* lits = lits_all[wv];
+    uint32_t* bits = bits_all[wv];
+    const DevPage pg = pages[p];
+    const uint8_t* page = bytes + pg.off;
+    const uint32_t size = static_cast<uint32_t>(pg.size);
+    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    DevErr* err = page_err + p;
+    const uint32_t md = static_cast<uint32_t>(cp.max_def);
+    uint32_t pos = 0;
+    // levels (column_reader.cpp:146-170)
+    const bool has_def = cp.max_def > 0;
+    SRle def;
+    srle_init(def, 0, 0, 0);
+    if (has_def) {
+        if (pos + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); return; }
+        const uint32_t dl = suni(sload_u32(page, pos));
+        pos += 4;
+        if (static_cast<uint64_t>(pos) + dl > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, dl, size); return; }
+        srle_init(def, pos, dl, level_bw(cp.max_def));
+        pos += dl;
+    }
+    if (cp.max_rep > 0) {
+        if (pos + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); return; }
+        const uint32_t rl = suni(sload_u32(page, pos));
+        pos += 4;
+        if (static_cast<uint64_t>(pos) + rl > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, rl, size); return; }
+        pos += rl;
+    }
+    // def levels, one 512-row tile at a time (the walk state carries over)
+    const int32_t t0 = page_tile0[p];
+    uint32_t nn = 0;
+    for (uint32_t r0 = 0; r0 < n; r0 += kTileRows) {
+        const uint32_t m = min(n - r0, static_cast<uint32_t>(kTileRows));
+        for (uint32_t w = lane(); w < kTileRows / 32; w += kWave) bits[w] = has_def ? 0u : ~0u;
+        __builtin_amdgcn_wave_barrier();
+        auto put = [&](uint32_t j, uint32_t v) {
+            if (v >= md) atomicOr(&bits[j >> 5], 1u << (j & 31));
+        };
+        uint32_t nl = 0;
+        const int rc = !has_def ? 0 : srle_walk(def, page, m, put, lits, nl, kLitCapF, [&]() {
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t r = 0; r < nl; r++) {
+                const LitRun L = lits[r];
+                const uint64_t b0 = (static_cast<uint64_t>(L.bit0_hi) << 32) | L.bit0_lo;
+                for (uint32_t j = lane(); j < L.count; j += kWave) put(L.start + j, gbits(page, size, b0 + static_cast<uint64_t>(j) * def.bw, def.bw));
+            }
+            __builtin_amdgcn_wave_barrier();
+        });
+        if (rc) { set_err(err, err_any, rc, 0, 0, size); return; }
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t r = 0; r < nl; r++) {
+            const LitRun L = lits[r];
+            const uint64_t b0 = (static_cast<uint64_t>(L.bit0_hi) << 32) | L.bit0_lo;
+            for (uint32_t j = lane(); j < L.count; j += kWave) put(L.start + j, gbits(page, size, b0 + static_cast<uint64_t>(j) * def.bw, def.bw));
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane() == 0) tile_rank[t0 + static_cast<int32_t>(r0 / kTileRows)] = static_cast<int32_t>(nn);
+        const int64_t R0 = pg.first_row + r0;
+        for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
+            const uint32_t j = j0 + lane();
+            const bool v = j < m && ((bits[j >> 5] >> (j & 31)) & 1u);
+            const uint64_t vm = __ballot(v);
+            nn += __popcll(vm);
+            put_valid64(validity, R0 + j0, min(64u, m - j0), vm, pg.first_row, pg.first_row + n);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    // values: ByteBuffer::check on the first overrunning rank
+    const uint32_t w = static_cast<uint32_t>(cp.plain_width);
+    if (static_cast<uint64_t>(pos) + static_cast<uint64_t>(nn) * w > size) {
+        const uint32_t k = (size - pos) / w;
+        set_err(err, err_any, PQ_ERR_BUFFER, pos + k * w, w, size);
+    }
+    if (lane() == 0) page_pos[p] = static_cast<int32_t>(pos);
+}
+
+__global__ void __launch_bounds__(256) k_fixed_scatter(const uint8_t* __restrict__ bytes,
+                                                       const DevPage* __restrict__ pages,
+                                                       const DevTile* __restrict__ tiles, int ntiles,
+                                                       uint32_t pw, const uint32_t* __restrict__ validity_in,
+                                                       const int32_t* __restrict__ tile_rank,
+                                                       const int32_t* __restrict__ page_pos,
+                                                       const DevErr* __restrict__ page_err,
+                                                       uint8_t* __restrict__ values) {
+    const int t = blockIdx.x * kTilesPerBlock + static_cast<int>(threadIdx.x / kWave);
+    if (t >= ntiles) return;
+    const DevTile T = tiles[t];
+    if (page_err[T.page].code) return;  // the decode fails; nothing may be read past the page
+    const DevPage pg = pages[T.page];
+    const uint8_t* src = bytes + pg.off + static_cast<uint32_t>(page_pos[T.page]);
+    const uint32_t m = static_cast<uint32_t>(T.nrows);
+    const int64_t R0 = pg.first_row + T.row0;
+    uint32_t rank = static_cast<uint32_t>(tile_rank[t]);
+    for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
+        const uint32_t j = j0 + lane();
+        const int64_t R = R0 + j;
+        const bool v = j < m && ((validity_in[R >> 5] >> (R & 31)) & 1u);
+        const uint64_t vm = __ballot(v);
+        const uint32_t k = rank + popc_below(vm);
+        rank += __popcll(vm);
+        if (j < m) {
+            uint8_t* o = values + static_cast<uint64_t>(R) * pw;
+            const uint8_t* s = src + static_cast<uint64_t>(k) * pw;
+            if (pw == 8) {
+                const uint2 x = v ? *reinterpret_cast<const uint2*>(s) : make_uint2(0, 0);
+                *reinterpret_cast<uint2*>(o) = x;
+            } else if (pw == 4) {
+                *reinterpret_cast<uint32_t*>(o) = v ? *reinterpret_cast<const uint32_t*>(s) : 0u;
+            } else {
+                for (uint32_t q = 0; q < pw / 4; q++)
+                    reinterpret_cast<uint32_t*>(o)[q] = v ? reinterpret_cast<const uint32_t*>(s)[q] : 0u;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,
+                        int ntiles, const int32_t* page_tile0, ColumnParams cp, uint32_t* validity,
+                        uint8_t* values, int32_t* tile_rank, int32_t* page_pos, DevErr* page_err,
+                        int32_t* err_any) {
+    if (ntiles <= 0) return;
+    const uint32_t pw = static_cast<uint32_t>(cp.plain_width);
+    const int tb = (ntiles + kTilesPerBlock - 1) / kTilesPerBlock;
+    if (cp.max_def == 0 && cp.max_rep == 0) {
+        hipLaunchKernelGGL(k_fixed_req, dim3(tb), dim3(kTilesPerBlock * kWave), 0, s, bytes, pages, tiles, ntiles, pw,
+                           validity, values, page_err, err_any);
+        return;
+    }
+    const int pb = (npages + kTilesPerBlock - 1) / kTilesPerBlock;
+    hipLaunchKernelGGL(k_fixed_levels, dim3(pb), dim3(kTilesPerBlock * kWave), 0, s, bytes, pages, npages, page_tile0,
+                       cp, validity, tile_rank, page_pos, page_err, err_any);
+    hipLaunchKernelGGL(k_fixed_scatter, dim3(tb), dim3(kTilesPerBlock * kWave), 0, s, bytes, pages, tiles, ntiles, pw,
+                       validity, tile_rank, page_pos, page_err, values);
+}
+
+}  // namespace pqk

@@ -81,6 +81,12 @@ void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int
                   const DevDict* dicts, const int32_t* dict_count, ColumnParams cp,
                   uint32_t* validity, uint8_t* values, DevErr* page_err, int32_t* err_any);
 
+// ── tile-parallel PLAIN fixed-width path (fixed_fast.hip) ──────────────────
+void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,
+                        int ntiles, const int32_t* page_tile0, ColumnParams cp, uint32_t* validity,
+                        uint8_t* values, int32_t* tile_rank, int32_t* page_pos, DevErr* page_err,
+                        int32_t* err_any);
+
 // ── fused BYTE_ARRAY path (dict_fused.hip) ─────────────────────────────────
 struct FusedLaunch {
     const uint8_t* bytes;

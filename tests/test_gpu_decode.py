@@ -37,13 +37,17 @@ SMALL = [
 
 @pytest.fixture(params=["batch", "fused", "generic"])
 def path(request, ctx):
-    """Every BYTE_ARRAY kernel path: batched dictionary (dict_batch.hip),
-    per-page fused (dict_fused.hip) and generic (decode.hip)."""
+    """Every kernel path: BYTE_ARRAY batched dictionary (dict_batch.hip),
+    per-page fused (dict_fused.hip) and generic (decode.hip); fixed-width
+    PLAIN tile-parallel (fixed_fast.hip) except under "generic", which runs
+    decode.hip's per-page k_fixed."""
     ctx.set_option("fused_ba", int(request.param != "generic"))
     ctx.set_option("batch", int(request.param == "batch"))
+    ctx.set_option("fixed_plain", int(request.param != "generic"))
     yield request.param
     ctx.set_option("fused_ba", 1)
     ctx.set_option("batch", 0)
+    ctx.set_option("fixed_plain", 1)
 
 
 @pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT], ids=["ref", "arrow"])
@@ -101,6 +105,28 @@ def _dict_ba_file(idx_stream: bytes, nvals: int, dict_vals, def_stream: bytes | 
 
 DICT = [b"alpha", b"", b"gamma-gamma", b"d"]
 
+
+def _opt_fixed_file(ptype, fmt, nvals, seed, rle_levels=False, drop=0):
+    """One OPTIONAL PLAIN fixed-width page; `drop` trailing values removed
+    from the payload (the read overruns on the last non-null rows)."""
+    rng = np.random.default_rng(seed)
+    if rle_levels:
+        k = nvals * 2 // 3
+        defs = [1] * k + [0] * (nvals - k)
+        stream = B.rle(k, 1, 1) + B.rle(nvals - k, 0, 1)
+    else:
+        defs = [int(x) for x in rng.random(nvals) < 0.7]
+        head = (nvals // 2) // 8 * 8
+        stream = B.bitpack(defs[:head], 1) + B.rle(nvals - head, 1, 1)
+        defs = defs[:head] + [1] * (nvals - head)
+    nn = sum(defs) - drop
+    vals = b"".join(struct.pack(fmt, *([int(rng.integers(-1 << 40, 1 << 40))] if fmt in ("<q",) else
+                                       [float(rng.standard_normal())] if fmt in ("<d", "<f") else
+                                       [int(rng.integers(-1 << 60, 1 << 60)), int(rng.integers(-1 << 30, 1 << 30))]))
+                    for _ in range(nn))
+    pay = B.levels_section(stream) + vals
+    return B.build_file([B.data_header(len(pay), nvals, 0) + pay], ptype, True, nvals)
+
 CRAFTED = {
     # bit width 0: every index is 0
     "bw0_rle": lambda: _dict_ba_file(bytes([0]) + B.rle(10, 0, 0), 10, DICT),
@@ -135,6 +161,15 @@ CRAFTED = {
     "bool_bits": lambda: B.build_file([B.data_header(len(B.levels_section(B.bitpack([1, 0, 1, 1, 1, 0, 1, 1], 1))) + 1, 8, 0)
                                        + B.levels_section(B.bitpack([1, 0, 1, 1, 1, 0, 1, 1], 1)) + bytes([0b101101])],
                                       gen.BOOLEAN, True, 8),
+    # OPTIONAL INT64 over several 512-row tiles: bit-packed and RLE level runs
+    "opt_int64_tiles": lambda: _opt_fixed_file(gen.INT64, "<q", 1700, seed=5),
+    # OPTIONAL DOUBLE, one long all-valid RLE level run then nulls
+    "opt_double_rle_levels": lambda: _opt_fixed_file(gen.DOUBLE, "<d", 1300, seed=6, rle_levels=True),
+    # OPTIONAL INT96
+    "opt_int96": lambda: _opt_fixed_file(gen.INT96, "<qi", 600, seed=7),
+    # REQUIRED INT32 over several tiles, pages of different sizes
+    "req_int32_tiles": lambda: B.build_file([B.data_header(4 * n, n, 0) + struct.pack(f"<{n}i", *range(-n, 0))
+                                             for n in (1500, 1, 513)], gen.INT32, False, 2014),
     # empty chunk
     "empty": lambda: B.build_file([], gen.INT64, False, 0),
     # multiple dictionary pages: the latest one is in force
@@ -157,6 +192,11 @@ ERRORS = {
     "no_dph": lambda: B.build_file([B.data_header(4, 1, 0, with_dph=False) + b"abcd"], gen.INT32, False, 1),
     # PLAIN INT64 page too short
     "short_int64": lambda: B.build_file([B.data_header(12, 2, 0) + struct.pack("<q", 5) + b"abcd"], gen.INT64, False, 2),
+    # REQUIRED INT32, three tiles, values run out inside the second tile
+    "req_int32_short_tile2": lambda: B.build_file([B.data_header(4 * 700, 1500, 0) + bytes(4 * 700)],
+                                                  gen.INT32, False, 1500),
+    # OPTIONAL FLOAT, values run out after a later null-only stretch
+    "opt_float_short": lambda: _opt_fixed_file(gen.FLOAT, "<f", 1200, seed=8, drop=3),
     # FLBA with a non-null value
     "flba": lambda: B.build_file([B.data_header(4, 1, 0) + b"abcd"], gen.FLBA, False, 1),
     # dictionary page truncated
