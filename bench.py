@@ -31,7 +31,8 @@ for _p in (ROOT, PKG):
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel timers (HIP events on the decode stream, capi.hip Timed)
-KERNELS = ("dict_index", "dict_entries", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather")
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_count", "pipe_codes", "pipe_write", "ba_batch",
+           "ba_fused", "ba_rows", "scan", "ba_gather")
 ROWS = 10_000_000
 
 
@@ -167,10 +168,11 @@ def main():
     dom_ms = kern.get(dom, ms_per_step)
     # algorithmic bytes of one launch of the dominant kernel:
     # the fused/batched kernels read every page payload once and write the
-    # whole column (offsets, characters, validity); the generic pipeline's
-    # stages split that between them.
+    # whole column (offsets, characters, validity); the pipelines' stages
+    # split that between them (pipe_write: u16 codes in, the column out).
     dom_bytes = {"ba_fused": b_alg, "ba_batch": b_alg, "ba_gather": out_bytes,
-                 "ba_rows": payload + 8 * nrows}.get(dom, payload)
+                 "ba_rows": payload + 8 * nrows, "pipe_write": out_bytes + 2 * nrows,
+                 "pipe_codes": payload + 2 * nrows}.get(dom, payload)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     step_kernel_ms = sum(kern.values())
 

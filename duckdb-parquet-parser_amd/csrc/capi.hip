@@ -47,6 +47,7 @@ struct pq_ctx {
     bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
+    bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
 };
 
 struct pq_chunk {
@@ -82,6 +83,15 @@ struct pq_chunk {
     int32_t* d_flags = nullptr;  // [0] err_any, [1] overflow
     uint64_t* d_row_codes = nullptr;
     int64_t* d_tile_chars = nullptr;
+    // three-pass dictionary BYTE_ARRAY decode (dict_pipe.hip)
+    bool pipe = false, pipe_count = false;
+    int32_t pipe_dict = -1;
+    uint32_t pipe_dict_chars_bytes = 0, pipe_dict_bytes = 0, pipe_lds = 0;
+    int pipe_grid = 0;
+    uint2* d_runs = nullptr;
+    uint32_t* d_info = nullptr;
+    uint16_t* d_codes = nullptr;
+    int32_t* d_tile_nn = nullptr;
     // tile-parallel PLAIN fixed-width decode (fixed_fast.hip)
     bool fixed_plain = false;
     int32_t* d_tile_rank = nullptr;
@@ -223,6 +233,10 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_row_codes);
     dfree(c->d_tile_chars);
     dfree(c->d_tile_rank);
+    dfree(c->d_runs);
+    dfree(c->d_info);
+    dfree(c->d_codes);
+    dfree(c->d_tile_nn);
     dfree(c->d_page_pos);
     dfree(c->d_tile_base);
     dfree(c->d_total);
@@ -236,6 +250,40 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_batches);
     dfree(c->d_bstatus);
     if (c->d_prog) { pqre::free_device_program(c->d_prog); c->d_prog = nullptr; }
+}
+
+// The three-pass dictionary path (dict_pipe.hip) takes a BYTE_ARRAY chunk
+// whose data pages all use one dictionary page that fits in LDS.
+void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, const std::vector<DevDict>& dicts) {
+    c->pipe = false;
+    c->pipe_count = false;
+    if (c->type != PQ_BYTE_ARRAY || c->max_def > 254 || c->max_def < 0 || c->max_rep < 0 || pages.empty()) return;
+    int32_t dict_id = -1;
+    bool multi = false;
+    for (const auto& pg : pages) {
+        // pages of up to 2048 rows (the run table holds kPipeRunCap runs per stream)
+        if (pg.mode != pqk::MODE_DICT || pg.nvals > 2048 || pg.size > (1 << 27)) return;
+        if (dict_id >= 0 && pg.dict != dict_id) return;
+        dict_id = pg.dict;
+        multi |= pg.nvals > pqk::kTileRows;
+    }
+    const DevDict& d = dicts[dict_id];
+    if (d.size < 0 || d.size > 65536 - 64 || d.nvals < 0 || d.nvals > 65535) return;
+    const int64_t ecap = std::min<int64_t>(d.nvals, d.size / 4 + 1);
+    const uint32_t chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
+    const uint32_t dict_bytes = 16 + chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
+    const pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes);
+    if (pl.blocks_per_cu == 0) return;
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+    c->pipe = true;
+    c->pipe_count = multi && c->max_def > 0;
+    c->pipe_dict = dict_id;
+    c->pipe_dict_chars_bytes = chars_bytes;
+    c->pipe_dict_bytes = dict_bytes;
+    c->pipe_lds = pl.lds;
+    c->pipe_grid = cus * pl.blocks_per_cu;
 }
 
 // Decide whether every chunk of the column can take the fused BYTE_ARRAY
@@ -379,6 +427,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
+    if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
     if (std::strcmp(key, "regex_win") == 0) {
         if (value < 1024 || value > 32768 || value % 16) return set_err(ctx, PQ_ERR_ARG, "regex_win: 1024..32768, multiple of 16");
         ctx->opt_regex_win = static_cast<int>(value);
@@ -514,6 +563,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         c->nrows = row_base;
         c->nbytes = static_cast<size_t>(img) + 64;
         plan_fused(ctx, c.get(), hpages, hdicts);
+        plan_pipe(ctx, c.get(), hpages, hdicts);
         c->npages = static_cast<int>(hpages.size());
         c->ndicts = static_cast<int>(hdicts.size());
 
@@ -554,6 +604,12 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         rc |= dalloc(&c->d_total, 1);
         rc |= dalloc(&c->d_scan_scratch, htiles.size() / 8192 + 16);
         if (c->type == PQ_BYTE_ARRAY && !c->fused) rc |= dalloc(&c->d_row_codes, static_cast<size_t>(c->nrows));
+        if (c->pipe) {
+            rc |= dalloc(&c->d_runs, hpages.size() * 2 * pqk::kPipeRunCap);
+            rc |= dalloc(&c->d_info, hpages.size());
+            rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) + 64);
+            rc |= dalloc(&c->d_tile_nn, htiles.size());
+        }
         if (c->fused && !c->hbatches.empty()) {
             rc |= dalloc(&c->d_batches, c->hbatches.size());
             rc |= dalloc(&c->d_bstatus, c->hbatches.size());
@@ -689,7 +745,39 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
                                  c->d_dict_err, c->d_flags, c->type, c->plain_width);
     }
-    if (c->fused) {
+    if (c->pipe && ctx->opt_pipe) {
+        pqk::PipeLaunch P{};
+        P.bytes = c->d_bytes; P.pages = c->d_pages; P.npages = c->npages; P.tiles = c->d_tiles;
+        P.ntiles = c->ntiles; P.page_tile0 = c->d_page_tile0; P.max_def = c->max_def; P.max_rep = c->max_rep;
+        P.dicts = c->d_dicts; P.dict_id = c->pipe_dict; P.entries = c->d_entries; P.dict_count = c->d_dict_count;
+        P.runs = c->d_runs; P.info = c->d_info; P.tile_nn = c->d_tile_nn; P.codes = c->d_codes;
+        P.tile_chars = c->d_tile_chars; P.tile_base = c->d_tile_base; P.total = c->d_total;
+        P.nrows_total = c->nrows; P.capacity = out->capacity_bytes; P.overflow = c->d_flags + 1;
+        P.validity = out->d_validity; P.offsets = out->d_offsets; P.chars = out->d_values;
+        P.page_err = c->d_page_err; P.err_any = c->d_flags;
+        P.dict_chars_bytes = c->pipe_dict_chars_bytes; P.dict_bytes = c->pipe_dict_bytes; P.lds = c->pipe_lds;
+        P.grid = c->pipe_grid;
+        P.debug = ctx->opt_debug;
+        {
+            Timed t(ctx, "pipe_runs");
+            pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->npages, c->max_def, c->max_rep, c->d_runs, c->d_info);
+        }
+        if (c->pipe_count) {
+            Timed t(ctx, "pipe_count");
+            pqk::launch_pipe_codes(s, P, true);
+        }
+        {
+            Timed t(ctx, "pipe_codes");
+            pqk::launch_pipe_codes(s, P, false);
+        }
+        {
+            Timed t(ctx, "scan");
+            pqk::launch_scan_i64(s, c->d_tile_chars, c->d_tile_base, c->ntiles, c->d_total, c->d_scan_scratch);
+        }
+        if (c->ntiles == 0) (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
+        Timed t(ctx, "pipe_write");
+        pqk::launch_pipe_write(s, P);
+    } else if (c->fused) {
         const size_t nr = c->ranges.size();
         (void)hipMemsetAsync(c->d_status, 0, std::max<size_t>(c->npages, 1) * sizeof(uint64_t), s);
         (void)hipMemsetAsync(c->d_tickets, 0, nr * sizeof(int32_t), s);

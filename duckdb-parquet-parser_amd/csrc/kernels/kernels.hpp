@@ -81,6 +81,50 @@ void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int
                   const DevDict* dicts, const int32_t* dict_count, ColumnParams cp,
                   uint32_t* validity, uint8_t* values, DevErr* page_err, int32_t* err_any);
 
+// ── three-pass dictionary BYTE_ARRAY path (dict_pipe.hip) ──────────────────
+constexpr uint32_t kPipeRunCap = 128;  // run records per stream per page
+
+struct PipeLaunch {
+    const uint8_t* bytes;
+    const DevPage* pages;
+    int32_t npages;
+    const DevTile* tiles;
+    int32_t ntiles;
+    const int32_t* page_tile0;
+    int32_t max_def, max_rep;
+    const DevDict* dicts;
+    int32_t dict_id;
+    const uint64_t* entries;
+    const int32_t* dict_count;
+    const uint2* runs;          // npages x 2 x kPipeRunCap
+    const uint32_t* info;       // per page: run counts, index bit width, fallback flag
+    int32_t* tile_nn;           // per tile non-null rows (pages > 512 rows with def levels)
+    uint16_t* codes;            // per row dictionary index, 0xFFFF = NULL
+    int64_t* tile_chars;
+    const int64_t* tile_base;
+    const int64_t* total;
+    int64_t nrows_total;
+    int64_t capacity;
+    int32_t* overflow;
+    uint32_t* validity;
+    int64_t* offsets;
+    uint8_t* chars;
+    DevErr* page_err;
+    int32_t* err_any;
+    uint32_t dict_chars_bytes, dict_bytes, lds;
+    int grid;
+    int debug;  // ablation bits (k_pipe_write)
+};
+struct PipePlan {
+    uint32_t lds;       // dynamic LDS bytes of k_pipe_write
+    int blocks_per_cu;  // 0: the dictionary does not fit
+};
+PipePlan plan_pipe_lds(uint32_t dict_bytes);
+void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
+                      int32_t max_rep, uint2* runs, uint32_t* info);
+void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
+void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
+
 // ── tile-parallel PLAIN fixed-width path (fixed_fast.hip) ──────────────────
 void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,
                         int ntiles, const int32_t* page_tile0, ColumnParams cp, uint32_t* validity,

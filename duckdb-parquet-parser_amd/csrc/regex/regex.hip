@@ -216,11 +216,6 @@ __device__ __forceinline__ uint32_t dfa_step_full(const uint16_t* T, uint32_t e,
     return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(T) + (e & 0x7FFFu) + 2 * b);
 }
 
-__device__ __forceinline__ uint32_t win_byte(const uint4& w, uint32_t i) {
-    const uint32_t d = (i & 8) ? ((i & 4) ? w.w : w.z) : ((i & 4) ? w.y : w.x);
-    return (d >> (8 * (i & 3))) & 0xFFu;
-}
-
 __device__ __forceinline__ void lane_err(DevErr* e, int32_t* any, int code, uint32_t pos, uint32_t need,
                                          uint32_t size) {
     e->code = code;

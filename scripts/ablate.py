@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Ablation timings of the BYTE_ARRAY dictionary kernels (C2 shape) on one GPU.
 
-Paths: batch (dict_batch.hip), fused (dict_fused.hip), generic (decode.hip).
+Paths: pipe (dict_pipe.hip), batch (dict_batch.hip), fused (dict_fused.hip),
+generic (decode.hip).
 fused_debug bits (timing only; the output is not valid with bits set):
   1 = skip the decoupled look-back (fake page bases)
   2 = skip the characters
@@ -19,7 +20,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "duckdb-parquet-parser_amd")]
 from pqgpu import capi, gen  # noqa: E402
 
-KERNELS = ("dict_index", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather")
+KERNELS = ("dict_index", "pipe_runs", "pipe_count", "pipe_codes", "pipe_write", "ba_batch", "ba_fused", "ba_rows",
+           "scan", "ba_gather")
 BATCH_PHASES = ("p_waitbuf", "p_stage", "p_walk", "p_lookback", "batches",
                 "w_wait", "w_runs", "w_rows", "w_chars", "pages", "p_defwalk")
 
@@ -32,6 +34,7 @@ ctx = capi.Context(0)
 
 
 def setp(path, dbg=0, waves=0, bbytes=12288, claim=1):
+    ctx.set_option("dict_pipe", int(path == "pipe"))
     ctx.set_option("fused_claim", claim)
     ctx.set_option("fused_ba", int(path != "generic"))
     ctx.set_option("batch", int(path == "batch"))
@@ -40,8 +43,10 @@ def setp(path, dbg=0, waves=0, bbytes=12288, claim=1):
     ctx.set_option("batch_bytes", bbytes)
 
 
-variants = [("fused", 0, 0, 12288, 1), ("batch", 0, 0, 12288, 1), ("batch", 1, 0, 12288, 1),
-            ("batch", 3, 0, 12288, 1), ("batch", 0, 0, 16384, 1), ("batch", 0, 0, 8192, 1)]
+variants = [("pipe", 0, 0, 12288, 1), ("pipe", 2, 0, 12288, 1), ("pipe", 4, 0, 12288, 1),
+            ("pipe", 6, 0, 12288, 1), ("fused", 0, 0, 12288, 1)]
+if "batch" in sys.argv:
+    variants += [("batch", 0, 0, 12288, 1), ("batch", 1, 0, 12288, 1), ("batch", 3, 0, 12288, 1)]
 for path, dbg, waves, bb, claim in variants:
     setp(path, dbg, waves, bb, claim)
     dc = ctx.upload(f, chunks)
@@ -63,7 +68,7 @@ for path, dbg, waves, bb, claim in variants:
     dc.free()
 
 ctx.set_option("fused_prof", 1)
-for path in ("batch", "fused"):
+for path in (("batch", "fused") if "prof" in sys.argv else ()):
     setp(path)
     dc = ctx.upload(f, chunks)
     dc.decode_async()

@@ -12,8 +12,10 @@ from pqgpu import capi, gen  # noqa: E402
 
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 ctx = capi.Context(0)
-KERNELS = ("dict_index", "dict_entries", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain")
-for name, cols, layout, seed in [("C3", gen.c3_cols(), gen.REF_LAYOUT, 3),
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_count", "pipe_codes", "pipe_write", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain")
+for name, cols, layout, seed in [("C2", gen.c2_cols(), gen.REF_LAYOUT, 2),
+                                 ("C2a", gen.c2_cols(), gen.ARROW_LAYOUT, 2),
+                                 ("C3", gen.c3_cols(), gen.REF_LAYOUT, 3),
                                  ("C4", gen.c4_cols(), gen.ARROW_LAYOUT, 4)]:
     f = gen.build(cols, rows, 1, seed=seed, layout=layout)
     F = capi.File(f)

@@ -35,16 +35,18 @@ SMALL = [
 ]
 
 
-@pytest.fixture(params=["batch", "fused", "generic"])
+@pytest.fixture(params=["pipe", "batch", "fused", "generic"])
 def path(request, ctx):
-    """Every kernel path: BYTE_ARRAY batched dictionary (dict_batch.hip),
-    per-page fused (dict_fused.hip) and generic (decode.hip); fixed-width
-    PLAIN tile-parallel (fixed_fast.hip) except under "generic", which runs
-    decode.hip's per-page k_fixed."""
+    """Every kernel path: BYTE_ARRAY three-pass dictionary (dict_pipe.hip),
+    batched dictionary (dict_batch.hip), per-page fused (dict_fused.hip) and
+    generic (decode.hip); fixed-width PLAIN tile-parallel (fixed_fast.hip)
+    except under "generic", which runs decode.hip's per-page k_fixed."""
+    ctx.set_option("dict_pipe", int(request.param == "pipe"))
     ctx.set_option("fused_ba", int(request.param != "generic"))
     ctx.set_option("batch", int(request.param == "batch"))
     ctx.set_option("fixed_plain", int(request.param != "generic"))
     yield request.param
+    ctx.set_option("dict_pipe", 1)
     ctx.set_option("fused_ba", 1)
     ctx.set_option("batch", 0)
     ctx.set_option("fixed_plain", 1)
@@ -140,6 +142,13 @@ CRAFTED = {
     "zero_count_rle_after_lit": lambda: _dict_ba_file(bytes([2]) + B.bitpack([1, 2, 3, 0, 1, 2, 3, 0], 2) + B.rle(0, 3, 2) + bytes([0x1b, 0xe4]), 16, DICT),
     # more runs than the batched path's run list holds for this page size
     "many_tiny_runs": lambda: _dict_ba_file(bytes([2]) + b"".join(B.rle(1, i % 4, 2) for i in range(40)), 40, DICT),
+    # more runs per stream than the three-pass path's run table holds
+    "runs_200": lambda: _dict_ba_file(bytes([2]) + b"".join(B.rle(1 + i % 3, i % 4, 2) for i in range(200)), 400, DICT),
+    # index stream ends inside a run header (truncated varint)
+    "trunc_varint": lambda: _dict_ba_file(bytes([2]) + B.rle(3, 1, 2) + bytes([0x85]), 10, DICT),
+    # literal def-level run reading past the level section into the page
+    "def_lit_overrun": lambda: _dict_ba_file(bytes([2]) + B.rle(16, 3, 2), 16, DICT,
+                                             def_stream=bytes([(2 << 1) | 1, 0xFF])),
     # multi-byte varint run header (count 300)
     "long_rle_run": lambda: _dict_ba_file(bytes([2]) + B.rle(300, 2, 2), 300, DICT),
     # def levels + nulls, RLE and bit-packed level runs
