@@ -31,6 +31,8 @@ struct PendingTimer {
 struct pq_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;            // dictionary decode beside the run-table pass
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     bool timing = false;
     std::vector<PendingTimer> pending;
@@ -48,6 +50,7 @@ struct pq_ctx {
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
+    int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
 };
 
 struct pq_chunk {
@@ -92,6 +95,7 @@ struct pq_chunk {
     uint32_t* d_info = nullptr;
     uint16_t* d_codes = nullptr;
     int32_t* d_tile_nn = nullptr;
+    unsigned long long* d_bsum = nullptr;
     // tile-parallel PLAIN fixed-width decode (fixed_fast.hip)
     bool fixed_plain = false;
     int32_t* d_tile_rank = nullptr;
@@ -173,7 +177,8 @@ struct Timed {
     pq_ctx* ctx;
     PendingTimer t{};
     bool on;
-    Timed(pq_ctx* c, const char* name) : ctx(c), on(c->timing) {
+    hipStream_t st;
+    Timed(pq_ctx* c, const char* name, hipStream_t s = nullptr) : ctx(c), on(c->timing), st(s ? s : c->stream) {
         if (!on) return;
         t.name = name;
         if (!ctx->free_events.empty()) {
@@ -184,11 +189,11 @@ struct Timed {
             (void)hipEventCreate(&t.a);
             (void)hipEventCreate(&t.b);
         }
-        (void)hipEventRecord(t.a, ctx->stream);
+        (void)hipEventRecord(t.a, st);
     }
     ~Timed() {
         if (!on) return;
-        (void)hipEventRecord(t.b, ctx->stream);
+        (void)hipEventRecord(t.b, st);
         ctx->pending.push_back(t);
     }
 };
@@ -237,6 +242,7 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_info);
     dfree(c->d_codes);
     dfree(c->d_tile_nn);
+    dfree(c->d_bsum);
     dfree(c->d_page_pos);
     dfree(c->d_tile_base);
     dfree(c->d_total);
@@ -396,6 +402,14 @@ pq_ctx* pq_ctx_create(int device) {
             delete c;
             return nullptr;
         }
+        if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+            if (c->side) (void)hipStreamDestroy(c->side);
+            (void)hipStreamDestroy(c->stream);
+            delete c;
+            return nullptr;
+        }
         return c;
     } catch (...) {
         return nullptr;
@@ -409,6 +423,10 @@ void pq_ctx_destroy(pq_ctx* ctx) {
     for (auto& p : ctx->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto& p : ctx->free_events) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
     if (ctx->d_prof) (void)hipFree(ctx->d_prof);
+    (void)hipStreamSynchronize(ctx->side);
+    (void)hipEventDestroy(ctx->ev_fork);
+    (void)hipEventDestroy(ctx->ev_join);
+    (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -428,6 +446,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
+    if (std::strcmp(key, "pipe_run_pages") == 0) { ctx->opt_run_pages = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "regex_win") == 0) {
         if (value < 1024 || value > 32768 || value % 16) return set_err(ctx, PQ_ERR_ARG, "regex_win: 1024..32768, multiple of 16");
         ctx->opt_regex_win = static_cast<int>(value);
@@ -609,6 +628,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc |= dalloc(&c->d_info, hpages.size());
             rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) + 64);
             rc |= dalloc(&c->d_tile_nn, htiles.size());
+            rc |= dalloc(&c->d_bsum, static_cast<size_t>(c->pipe_grid));
         }
         if (c->fused && !c->hbatches.empty()) {
             rc |= dalloc(&c->d_batches, c->hbatches.size());
@@ -736,7 +756,19 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
     (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), s);
     (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
-    if (c->ndicts && c->type == PQ_BYTE_ARRAY) {
+    const bool pipe = c->pipe && ctx->opt_pipe;
+    if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
+        // the dictionary (one workgroup) decodes on the side stream while the
+        // run-table pass runs; k_pipe_codes waits for both
+        (void)hipEventRecord(ctx->ev_fork, s);
+        (void)hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0);
+        {
+            Timed t(ctx, "dict_index", ctx->side);
+            pqk::launch_dict_index(ctx->side, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
+                                   c->d_dict_err, c->d_flags, c->max_dict_bytes);
+        }
+        (void)hipEventRecord(ctx->ev_join, ctx->side);
+    } else if (c->ndicts && c->type == PQ_BYTE_ARRAY) {
         Timed t(ctx, "dict_index");
         pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
                                c->d_dict_err, c->d_flags, c->max_dict_bytes);
@@ -745,13 +777,13 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
                                  c->d_dict_err, c->d_flags, c->type, c->plain_width);
     }
-    if (c->pipe && ctx->opt_pipe) {
+    if (pipe) {
         pqk::PipeLaunch P{};
         P.bytes = c->d_bytes; P.pages = c->d_pages; P.npages = c->npages; P.tiles = c->d_tiles;
         P.ntiles = c->ntiles; P.page_tile0 = c->d_page_tile0; P.max_def = c->max_def; P.max_rep = c->max_rep;
         P.dicts = c->d_dicts; P.dict_id = c->pipe_dict; P.entries = c->d_entries; P.dict_count = c->d_dict_count;
         P.runs = c->d_runs; P.info = c->d_info; P.tile_nn = c->d_tile_nn; P.codes = c->d_codes;
-        P.tile_chars = c->d_tile_chars; P.tile_base = c->d_tile_base; P.total = c->d_total;
+        P.tile_chars = c->d_tile_chars; P.bsum = c->d_bsum; P.total = c->d_total;
         P.nrows_total = c->nrows; P.capacity = out->capacity_bytes; P.overflow = c->d_flags + 1;
         P.validity = out->d_validity; P.offsets = out->d_offsets; P.chars = out->d_values;
         P.page_err = c->d_page_err; P.err_any = c->d_flags;
@@ -760,21 +792,23 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         P.debug = ctx->opt_debug;
         {
             Timed t(ctx, "pipe_runs");
-            pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->npages, c->max_def, c->max_rep, c->d_runs, c->d_info);
+            pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->npages, c->max_def, c->max_rep, c->d_runs, c->d_info,
+                                  ctx->opt_run_pages);
         }
+        if (c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
         if (c->pipe_count) {
             Timed t(ctx, "pipe_count");
             pqk::launch_pipe_codes(s, P, true);
         }
+        (void)hipMemsetAsync(c->d_bsum, 0, static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long), s);
         {
             Timed t(ctx, "pipe_codes");
             pqk::launch_pipe_codes(s, P, false);
         }
-        {
-            Timed t(ctx, "scan");
-            pqk::launch_scan_i64(s, c->d_tile_chars, c->d_tile_base, c->ntiles, c->d_total, c->d_scan_scratch);
+        if (c->ntiles == 0) {
+            (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
+            (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
         }
-        if (c->ntiles == 0) (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
         Timed t(ctx, "pipe_write");
         pqk::launch_pipe_write(s, P);
     } else if (c->fused) {

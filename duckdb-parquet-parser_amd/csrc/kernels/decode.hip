@@ -348,6 +348,30 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_apply(const int64_t* __rest
     }
 }
 
+// One workgroup scans up to kScanBlock * kScanSingle elements in one launch.
+constexpr int kScanSingle = 32;
+__global__ void __launch_bounds__(kScanBlock) k_scan_single(const int64_t* __restrict__ in, int64_t n,
+                                                            int64_t* __restrict__ out,
+                                                            int64_t* __restrict__ total) {
+    __shared__ int64_t sh[kScanBlock / kWave];
+    const int64_t base = static_cast<int64_t>(threadIdx.x) * kScanSingle;
+    int64_t v[kScanSingle];
+    int64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < kScanSingle; i++) {
+        v[i] = base + i < n ? in[base + i] : 0;
+        acc += v[i];
+    }
+    int64_t tot;
+    int64_t ex = block_excl_scan(acc, sh, &tot);
+#pragma unroll
+    for (int i = 0; i < kScanSingle; i++) {
+        if (base + i < n) out[base + i] = ex;
+        ex += v[i];
+    }
+    if (threadIdx.x == 0) *total = tot;
+}
+
 // ── BYTE_ARRAY gather: offsets, validity, chars ────────────────────────────
 constexpr int kGatherWindow = 2048;  // 16-byte output blocks per window (32 KiB)
 struct GatherLds {
@@ -640,6 +664,10 @@ void launch_scan_i64(hipStream_t s, const int64_t* in, int64_t* out_excl, int64_
                      int64_t* total, int64_t* scratch) {
     if (n <= 0) {
         (void)hipMemsetAsync(total, 0, sizeof(int64_t), s);
+        return;
+    }
+    if (n <= static_cast<int64_t>(kScanBlock) * kScanSingle) {
+        hipLaunchKernelGGL(k_scan_single, dim3(1), dim3(kScanBlock), 0, s, in, n, out_excl, total);
         return;
     }
     const int64_t per = static_cast<int64_t>(kScanBlock) * kScanItems;

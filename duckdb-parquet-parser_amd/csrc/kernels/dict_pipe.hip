@@ -35,13 +35,13 @@ namespace {
 using namespace dev;
 
 constexpr int kRunWaves = 4;
-constexpr int kRunPages = 32;                 // pages per wavefront (2 streams each)
+constexpr int kRunPages = 32;                 // max pages per wavefront (2 streams each)
 constexpr uint32_t kRunStage = 16384;         // staged payload bytes per wavefront
 constexpr uint32_t kFallback = 1u << 31;      // info flag: exact serial decode
 constexpr int kCodeWaves = 4;
 constexpr uint16_t kNull = 0xFFFFu;
-constexpr int kWriteWaves = 8;
-constexpr uint32_t kWin = 512;                // 16-byte output blocks per window
+constexpr int kWriteWaves = 6;
+constexpr uint32_t kWin = 1024;               // 16-byte output blocks per window
 constexpr uint32_t kFront = 16;               // zero bytes before the LDS dictionary
 constexpr uint32_t kLitCapP = 16;
 
@@ -52,16 +52,89 @@ __device__ __forceinline__ uint32_t rr_lit(uint2 r) { return r.y >> 31; }
 __device__ __forceinline__ uint32_t rr_pay(uint2 r) { return r.y & 0x7FFFFFFFu; }
 
 
+// One hybrid stream per lane, walked with every lane in lock step: each
+// step parses one run header (rle_decoder.hpp:36-95) and appends one record.
+struct RunWalk {
+    bool alive;
+    uint32_t q, end, bw, n, sbase;
+    uint2* out;
+    const uint8_t* gp;
+};
+
+template <bool kStaged>
+__device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uint32_t& flag, uint32_t& nrec) {
+    const uint32_t nbv = (W.bw + 7) / 8;
+    const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+    const uint32_t litpay = W.bw ? 0x80000000u : 0u;
+    const uint32_t litmul = W.bw ? 8u : 0u;
+    uint32_t cnt = 0, q = W.q, nr = nrec, fl = flag;
+    bool alive = W.alive && W.n > 0;
+    // branch-free step: every quantity is computed, one predicated store
+    while (__ballot(alive)) {
+        uint32_t x0, x1;
+        if (kStaged) {
+            const uint32_t a = W.sbase + q, wi = a >> 2, sh = a & 3;
+            const uint32_t w0 = stage[wi], w1 = stage[wi + 1], w2 = stage[wi + 2];
+            x0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        } else {
+            const uint64_t x = alive ? gld8(W.gp, q) : 0ull;
+            x0 = static_cast<uint32_t>(x);
+            x1 = static_cast<uint32_t>(x >> 32);
+        }
+        const uint32_t exh = q >= W.end ? 1u : 0u;  // rest of the batch is 0 (rle_decoder.hpp:20-23)
+        // varint header (76-86): at most 5 bytes, inside the stream
+        const uint32_t st0 = ~x0 & 0x80808080u;
+        const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;
+        const uint32_t hl5 = (~x1 & 0x80u) ? 5u : 9u;
+        const uint32_t hl = st0 ? hl4 : hl5;
+        const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
+        const uint32_t x0m = x0 & lm;
+        const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
+        const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
+                             ((x0m >> 3) & 0xFE00000u) | top;
+        const uint32_t g = ind >> 1;
+        const uint32_t lit = ind & 1u;
+        const uint32_t left = W.n - cnt;
+        const uint32_t qh = q + hl;
+        const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, hl);
+        const uint32_t vb = x1 >> (8 * ((hl - 4) & 3));
+        const uint32_t vraw = (hl < 4) ? va : vb;
+        const uint32_t cl = (g >= (left + 7) / 8) ? left : g * 8;
+        const uint32_t cr = min(g, left);
+        const uint32_t c = lit ? cl : cr;
+        // zero-count runs (counter wrap / stale literal cursor), truncated headers or values
+        const uint32_t badh = (hl > 5 ? 1u : 0u) | (qh > W.end ? 1u : 0u) | (g == 0 ? 1u : 0u) |
+                              ((lit ^ 1u) & (qh + nbv > W.end ? 1u : 0u));
+        const uint32_t full = nr >= kPipeRunCap ? 1u : 0u;
+        const uint32_t ok = (alive ? 1u : 0u) & (full ^ 1u) & (exh | (badh ^ 1u));
+        const uint32_t rx = cnt | ((exh ? left : c) << 16);
+        const uint32_t pl = lit ? (litpay | (qh * litmul)) : (vraw & vmask);
+        const uint32_t ry = exh ? 0u : pl;
+        if (ok) W.out[nr] = make_uint2(rx, ry);
+        fl |= (alive ? 1u : 0u) & (ok ^ 1u);
+        nr += ok;
+        const uint64_t nql = static_cast<uint64_t>(qh) + static_cast<uint64_t>(g) * W.bw;
+        const uint32_t nqlc = nql > W.end ? W.end : static_cast<uint32_t>(nql);
+        const uint32_t nq = lit ? nqlc : qh + nbv;
+        cnt = exh ? W.n : cnt + c;
+        q = ok ? nq : q;
+        alive = ok && !exh && cnt < W.n;
+    }
+    nrec = nr;
+    flag = fl;
+}
+
 __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __restrict__ bytes,
                                                               const DevPage* __restrict__ pages, int npages,
                                                               int32_t max_def, int32_t max_rep,
                                                               uint2* __restrict__ runs,
-                                                              uint32_t* __restrict__ info) {
+                                                              uint32_t* __restrict__ info, int ppw) {
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[kRunWaves][kRunStage / 4 + 8];
     const uint32_t wv = threadIdx.x / kWave;
-    const int g0 = (blockIdx.x * kRunWaves + static_cast<int>(wv)) * kRunPages;
+    const int g0 = (blockIdx.x * kRunWaves + static_cast<int>(wv)) * ppw;
     if (g0 >= npages) return;
-    const int g1 = min(npages, g0 + kRunPages);
+    const int g1 = min(npages, g0 + ppw);
     uint32_t* stage = stage_all[wv];
     const uint64_t wlo = pages[g0].off;
     const DevPage lastp = pages[g1 - 1];
@@ -86,15 +159,18 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
 
     const uint32_t s = lane() & 1;
     const int p = g0 + static_cast<int>(lane() >> 1);
-    const bool act = p < g1;
+    const bool act = p < g1 && static_cast<int>(lane() >> 1) < ppw;
     uint32_t flag = 0, nrec = 0, bwi = 0;
+    RunWalk W{};
     if (act) {
         const DevPage pg = pages[p];
         const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
         const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
         const uint32_t sbase = static_cast<uint32_t>(pg.off - wlo);
         const uint8_t* gp = bytes + pg.off;
-        auto rd = [&](uint32_t a) -> uint64_t { return staged ? lds_u64(stage, sbase + a) : gld8(gp, a); };
+        auto rd = [&](uint32_t a) -> uint32_t {
+            return staged ? static_cast<uint32_t>(lds_u64(stage, sbase + a)) : static_cast<uint32_t>(gld8(gp, a));
+        };
         // prologue (column_reader.cpp:146-182); any error -> exact decoder
         uint32_t pos = 0, dbase = 0, dlen = 0;
         if (n > 65535u) flag = 1;
@@ -122,53 +198,18 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
         }
         if (!flag && bwi > 16) flag = 1;
         if (!flag && (s == 1 || max_def > 0)) {
-            const uint32_t base = s ? pos : dbase;
-            const uint32_t end = s ? size : dbase + dlen;
-            const uint32_t bw = s ? bwi : level_bw(max_def);
-            const uint32_t nbv = (bw + 7) / 8;
-            uint2* out = runs + (static_cast<size_t>(p) * 2 + s) * kPipeRunCap;
-            uint32_t cnt = 0, q = base;
-            while (cnt < n) {
-                if (nrec == kPipeRunCap) { flag = 1; break; }
-                if (q >= end) {  // exhausted: the rest of the batch is 0 (rle_decoder.hpp:20-23)
-                    out[nrec++] = make_uint2(cnt | ((n - cnt) << 16), 0u);
-                    break;
-                }
-                const uint64_t x = rd(q);
-                // varint header (76-86), at most 5 bytes, inside the stream
-                const uint64_t stop = ~x & 0x8080808080ull;
-                if (!stop) { flag = 1; break; }
-                const uint32_t hl = static_cast<uint32_t>(__builtin_ctzll(stop)) / 8 + 1;
-                if (q + hl > end) { flag = 1; break; }
-                const uint64_t xm = hl >= 8 ? x : (x & ((1ull << (8 * hl)) - 1));
-                const uint32_t ind = static_cast<uint32_t>((xm & 0x7Full) | ((xm >> 1) & 0x3F80ull) |
-                                                           ((xm >> 2) & 0x1FC000ull) | ((xm >> 3) & 0xFE00000ull) |
-                                                           ((xm >> 4) & 0xF0000000ull));
-                q += hl;
-                const uint32_t left = n - cnt;
-                if (ind & 1u) {  // literal run: (ind >> 1) groups of 8 (41-46)
-                    const uint32_t g = ind >> 1;
-                    if (g == 0) { flag = 1; break; }  // zero-group run: counter wraps
-                    const uint64_t c8 = static_cast<uint64_t>(g) * 8;
-                    const uint32_t c = c8 < left ? static_cast<uint32_t>(c8) : left;
-                    out[nrec++] = bw ? make_uint2(cnt | (c << 16), 0x80000000u | (q * 8))
-                                     : make_uint2(cnt | (c << 16), 0u);
-                    cnt += c;
-                    const uint64_t nq = static_cast<uint64_t>(q) + static_cast<uint64_t>(g) * bw;
-                    q = nq > end ? end : static_cast<uint32_t>(nq);
-                } else {  // repeated run (48-50, 88-95)
-                    const uint32_t rep = ind >> 1;
-                    if (rep == 0) { flag = 1; break; }  // zero-count run: stale literal cursor
-                    if (q + nbv > end) { flag = 1; break; }
-                    const uint32_t v = nbv ? static_cast<uint32_t>(x >> (8 * hl)) & ((1u << (8 * nbv)) - 1u) : 0u;
-                    const uint32_t c = rep < left ? rep : left;
-                    out[nrec++] = make_uint2(cnt | (c << 16), v);
-                    cnt += c;
-                    q += nbv;
-                }
-            }
+            W.alive = true;
+            W.q = s ? pos : dbase;
+            W.end = s ? size : dbase + dlen;
+            W.bw = s ? bwi : level_bw(max_def);
+            W.n = n;
+            W.out = runs + (static_cast<size_t>(p) * 2 + s) * kPipeRunCap;
+            W.sbase = sbase;
+            W.gp = gp;
         }
     }
+    if (staged) walk_runs<true>(W, stage, flag, nrec);
+    else walk_runs<false>(W, stage, flag, nrec);
     const uint32_t oflag = static_cast<uint32_t>(__shfl_xor(static_cast<int>(flag), 1));
     const uint32_t orec = static_cast<uint32_t>(__shfl_xor(static_cast<int>(nrec), 1));
     if (act && s == 0)
@@ -202,7 +243,17 @@ struct CodeArgs {
     int64_t* tile_chars;
     DevErr* page_err;
     int32_t* err_any;
+    unsigned long long* bsum;  // characters per k_pipe_write workgroup (its tiles)
+    int per;                   // tiles per k_pipe_write wavefront
 };
+
+// Characters of tile t also go to the k_pipe_write workgroup that writes it.
+__device__ __forceinline__ void tile_done(const CodeArgs& a, int t, uint32_t chars) {
+    if (lane() == 0) {
+        a.tile_chars[t] = chars;
+        if (chars) atomicAdd(&a.bsum[(t / a.per) / kWriteWaves], static_cast<unsigned long long>(chars));
+    }
+}
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return bcast_last(wave_incl_scan(v)); }
 
@@ -318,7 +369,7 @@ __device__ void exact_page(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n
             if (j < m) a.codes[pg.first_row + r0 + j] = code;
         }
         chars = wave_sum(chars);
-        if (lane() == 0) a.tile_chars[t0 + ti] = chars;
+        tile_done(a, t0 + static_cast<int>(ti), chars);
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -452,14 +503,17 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_codes(CodeArgs a) {
         if (j < m) a.codes[pg.first_row + r0 + j] = code;
     }
     chars = wave_sum(chars);
-    if (lane() == 0) a.tile_chars[t] = chars;
+    tile_done(a, t, chars);
 }
 
 // ── offsets, validity, characters ──────────────────────────────────────────
+constexpr int kRowsPerLane = kTileRows / kWave;
+
 struct WriteLds {
     uint2 ri[kTileRows + 1];  // (tile-relative first byte, dictionary byte) per row
     uint16_t brow[kWin];      // row holding each block's first byte
-    uint32_t pad[2];
+    uint8_t vb[kWave];        // validity bits of rows 8l .. 8l + 7
+    uint32_t pad[4];
 };
 
 struct WriteArgs {
@@ -472,36 +526,20 @@ struct WriteArgs {
     const uint64_t* entries;
     const int32_t* dict_count;
     const uint16_t* codes;
-    const int64_t* tile_base;
+    const int64_t* tile_chars;
+    const unsigned long long* bsum;
+    int per;
     int64_t nrows_total;
-    const int64_t* total;
+    int64_t* total;
     int64_t capacity;
     int32_t* overflow;
     uint32_t* validity;
     int64_t* offsets;
     uint8_t* chars;
     uint32_t dict_chars_bytes, dict_bytes;
-    int debug;  // ablation: 2 = no characters, 4 = no offsets/validity stores
+    int debug;  // ablation: 2 = no characters, 4 = no offsets/validity stores, 8 = prologue only,
+                //           16 = no block marking
 };
-
-// bits [R, R + cnt) of the validity bitmap from a 64-row ballot; words wholly
-// inside [lo, hi) and [R, R + cnt) are stored, the others ORed.
-__device__ __forceinline__ void put_valid(uint32_t* validity, int64_t R, uint32_t cnt, uint64_t vm, int64_t lo,
-                                          int64_t hi) {
-    const uint32_t sh = static_cast<uint32_t>(R & 31);
-    const int64_t w0 = R >> 5;
-    if (lane() < 3) {
-        const uint32_t part = lane() == 0 ? static_cast<uint32_t>(vm << sh)
-                            : lane() == 1 ? static_cast<uint32_t>(sh ? (vm >> (32 - sh)) : (vm >> 32))
-                                          : (sh ? static_cast<uint32_t>(vm >> (64 - sh)) : 0u);
-        const int64_t wlo = (w0 + lane()) * 32;
-        const int64_t rhi = R + cnt;
-        if (wlo < rhi && wlo + 32 > R) {
-            if (wlo >= lo && wlo + 32 <= hi && wlo >= R && wlo + 32 <= rhi) validity[w0 + lane()] = part;
-            else if (part) atomicOr(&validity[w0 + lane()], part);
-        }
-    }
-}
 
 __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -511,8 +549,19 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
     uint32_t* dtab = reinterpret_cast<uint32_t*>(smem + kFront + a.dict_chars_bytes);
     const uint32_t wv = threadIdx.x / kWave;
     WriteLds& S = reinterpret_cast<WriteLds*>(smem + a.dict_bytes)[wv];
+    __shared__ uint4 MT[17 * 17];  // MT[lo * 17 + hi]: bytes [lo, hi) of a 16-byte block
     const DevDict d = a.dicts[a.dict_id];
     const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    for (uint32_t i = threadIdx.x; i < 17 * 17; i += blockDim.x) {
+        const uint32_t lo = i / 17, hi = i % 17;
+        uint32_t w[4];
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t l = min(max(lo, 4 * q), 4 * q + 4) - 4 * q, h = min(max(hi, 4 * q), 4 * q + 4) - 4 * q;
+            const uint64_t mh = (1ull << (8 * h)) - 1, ml = (1ull << (8 * l)) - 1;
+            w[q] = h > l ? static_cast<uint32_t>(mh & ~ml) : 0u;
+        }
+        MT[i] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
         uint4* dst = reinterpret_cast<uint4*>(dw);
@@ -526,19 +575,51 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
     // each wavefront owns a contiguous run of tiles (consecutive rows): the
     // descriptors of up to 64 tiles are loaded at once, one per lane, and the
     // next tile's codes are loaded before this tile's stores are issued
-    const int nw = static_cast<int>(gridDim.x) * kWriteWaves;
-    const int per = (a.ntiles + nw - 1) / nw;
-    const int ta = static_cast<int>(blockIdx.x * kWriteWaves + wv) * per;
+    const int per = a.per;
+    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * kWriteWaves + wv) * per);
     const int tb = min(a.ntiles, ta + per);
+    // first output byte of the range: the workgroups before this one (bsum,
+    // summed by k_pipe_codes), then this workgroup's earlier tiles
+    __shared__ unsigned long long red[kWriteWaves];
+    auto wave_sum64 = [](unsigned long long v) {
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
+            const uint32_t hi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v >> 32), d));
+            v += (static_cast<unsigned long long>(hi) << 32) | lo;
+        }
+        return v;
+    };
+    {
+        unsigned long long acc = 0;
+        for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) acc += a.bsum[b];
+        acc = wave_sum64(acc);
+        if (lane() == 0) red[wv] = acc;
+    }
+    __syncthreads();
+    int64_t Grun = 0;
+    for (int w = 0; w < kWriteWaves; w++) Grun += static_cast<int64_t>(red[w]);
+    if (a.debug & 8) return;
+    {
+        const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * kWriteWaves) * per);
+        unsigned long long in = 0;
+        for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
+        Grun += static_cast<int64_t>(wave_sum64(in));
+    }
     for (int c0 = ta; c0 < tb; c0 += kWave) {
         const int cn = min(kWave, tb - c0);
         int64_t myR0 = 0, myG0 = 0;
         uint32_t mym = 0;
+        uint32_t myc = 0;
         if (static_cast<int>(lane()) < cn) {
             const DevTile T = a.tiles[c0 + lane()];
             myR0 = a.pages[T.page].first_row + T.row0;
             mym = static_cast<uint32_t>(T.nrows);
-            myG0 = a.tile_base[c0 + lane()];
+            myc = static_cast<uint32_t>(a.tile_chars[c0 + lane()]);
+        }
+        {  // tile characters < 2^25 each: a 32-bit scan over <= 64 tiles
+            const uint32_t inc = wave_incl_scan(myc);
+            myG0 = Grun + static_cast<int64_t>(inc - myc);
+            Grun += static_cast<int64_t>(bcast_last(inc));
         }
         auto rl64 = [](int64_t v, int i) -> int64_t {
             const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
@@ -550,8 +631,8 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
             const int64_t R = rl64(myR0, i);
             const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
 #pragma unroll
-            for (int k = 0; k < kTileRows / kWave; k++) {
-                const uint32_t j = k * kWave + lane();
+            for (int k = 0; k < kRowsPerLane; k++) {
+                const uint32_t j = lane() * kRowsPerLane + k;
                 cd[k] = j < mm ? a.codes[R + j] : kNull;
             }
         };
@@ -564,32 +645,69 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
 #pragma unroll
             for (int k = 0; k < kTileRows / kWave; k++) cur[k] = cd[k];
             if (i + 1 < cn) load_codes(i + 1);
-            uint32_t run = 0;
+            // this lane's rows 8l .. 8l + 7: lengths, dictionary offsets, validity
+            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0;
 #pragma unroll
-            for (int k = 0; k < kTileRows / kWave; k++) {
-                const uint32_t j0 = k * kWave;
-                if (j0 >= m) break;
-                const uint32_t j = j0 + lane();
-                const bool in = j < m;
-                const uint32_t code = cur[k];
-                const bool valid = code < dict_n;
-                const uint32_t e = valid ? dtab[code] : 0u;
-                const uint32_t len = e >> 16;
-                const uint32_t inc = wave_incl_scan(len);
-                const uint32_t ex = run + inc - len;
-                if (in) {
-                    S.ri[j] = make_uint2(ex, e & 0xFFFFu);
-                    if (!(a.debug & 4)) a.offsets[R0 + j] = G0 + ex;
-                }
-                run += bcast_last(inc);
-                const uint64_t vmask = __ballot(valid);
-                if (!(a.debug & 4)) put_valid(a.validity, R0 + j0, min(64u, m - j0), vmask, R0, R0 + m);
+            for (int k = 0; k < kRowsPerLane; k++) {
+                const bool valid = cur[k] < dict_n;
+                const uint32_t e = valid ? dtab[cur[k]] : 0u;
+                len[k] = e >> 16;
+                src[k] = e & 0xFFFFu;
+                vb |= (valid ? 1u : 0u) << k;
+                acc += len[k];
             }
-            if (lane() == 0) S.ri[m] = make_uint2(run, 0u);
-            if (R0 + m == a.nrows_total && lane() == 0) a.offsets[a.nrows_total] = *a.total;
+            const uint32_t incl = wave_incl_scan(acc);
+            const uint32_t total = bcast_last(incl);
+            const uint32_t mis = static_cast<uint32_t>(G0 & 15);
+            const uint32_t nb = total ? static_cast<uint32_t>(((G0 + total - 1) >> 4) - (G0 >> 4) + 1) : 0u;
+            const bool direct = nb <= kWin;  // brow filled here, one window
+            {
+                uint32_t o = incl - acc;
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++) {
+                    const uint32_t j = lane() * kRowsPerLane + k;
+                    if (j < m) {
+                        S.ri[j] = make_uint2(o, src[k]);
+                        // row j owns the blocks whose first in-tile byte lies in it
+                        if (direct && len[k] && !(a.debug & 16)) {
+                            const uint32_t blo = o == 0 ? 0u : (o + mis + 15) >> 4;
+                            const uint32_t bhi = ((o + len[k] + mis + 15) >> 4) - 1;
+                            for (uint32_t b = blo; b <= bhi; b++) S.brow[b] = static_cast<uint16_t>(j);
+                        }
+                    }
+                    o += len[k];
+                }
+            }
+            S.vb[lane()] = static_cast<uint8_t>(vb);
+            if (lane() == 0) S.ri[m] = make_uint2(total, 0u);
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            const uint32_t total = run;
+            if (!(a.debug & 4)) {
+                // offsets, row j = 64k + lane (coalesced)
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++) {
+                    const uint32_t j = k * kWave + lane();
+                    if (j < m) a.offsets[R0 + j] = G0 + S.ri[j].x;
+                }
+                // validity words [R0 >> 5, (R0 + m - 1) >> 5]: tile word t = vb bytes 4t .. 4t + 3
+                const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
+                const uint32_t sh = static_cast<uint32_t>(R0 & 31);
+                const int64_t g = gfirst + lane();
+                if (g <= glast) {
+                    auto tw = [&](int t) -> uint32_t {
+                        return (t >= 0 && t < kWave / 4) ? reinterpret_cast<const uint32_t*>(S.vb)[t] : 0u;
+                    };
+                    const int t = static_cast<int>(lane());
+                    const uint32_t val = (tw(t) << sh) | (sh ? (tw(t - 1) >> (32 - sh)) : 0u);
+                    const bool whole = g * 32 >= R0 && g * 32 + 32 <= R0 + m;
+                    if (whole) a.validity[g] = val;
+                    else if (val) atomicOr(&a.validity[g], val);
+                }
+            }
+            if (R0 + m == a.nrows_total && lane() == 0) {
+                a.offsets[a.nrows_total] = G0 + total;
+                *a.total = G0 + total;
+            }
             if (total == 0 || (a.debug & 2)) continue;
             if (G0 + total > a.capacity) {  // output too small: the host grows it and re-runs
                 if (lane() == 0) atomicOr(a.overflow, 1);
@@ -597,57 +715,65 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
             }
             const int64_t G1 = G0 + total;
             const int64_t B0 = G0 >> 4;
-            const uint32_t nb = static_cast<uint32_t>(((G1 - 1) >> 4) - B0 + 1);
-            const uint32_t mis = static_cast<uint32_t>(G0 & 15);
             for (uint32_t w0 = 0; w0 < nb; w0 += kWin) {
                 const uint32_t w1 = min(nb, w0 + kWin);
-                // row r owns the blocks whose first in-tile byte lies in it
-                for (uint32_t r = lane(); r < m; r += kWave) {
-                    const uint32_t s = S.ri[r].x, e = S.ri[r + 1].x;
-                    if (e <= s) continue;
-                    uint32_t blo = s == 0 ? 0u : (s + mis + 15) / 16;
-                    uint32_t bhi = (e + mis + 15) / 16 - 1;
-                    blo = max(blo, w0);
-                    bhi = min(bhi, w1 - 1);
-                    for (uint32_t b = blo; b <= bhi; b++) S.brow[b - w0] = static_cast<uint16_t>(r);
+                if (!direct) {  // row r owns the blocks whose first in-tile byte lies in it
+                    for (uint32_t r = lane(); r < m; r += kWave) {
+                        const uint32_t s = S.ri[r].x, e = S.ri[r + 1].x;
+                        if (e <= s) continue;
+                        uint32_t blo = s == 0 ? 0u : (s + mis + 15) / 16;
+                        uint32_t bhi = (e + mis + 15) / 16 - 1;
+                        blo = max(blo, w0);
+                        bhi = min(bhi, w1 - 1);
+                        for (uint32_t b = blo; b <= bhi; b++) S.brow[b - w0] = static_cast<uint16_t>(r);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                for (uint32_t b = w0 + lane(); b < w1; b += kWave) {
+                auto do_block = [&](uint32_t bq) {
+                    const uint32_t b = min(bq, w1 - 1);
+                    const bool st = bq < w1;
                     // tile-relative byte of the block start (negative before G0);
                     // each overlapping row contributes one masked 16-byte segment
                     const int32_t a0 = static_cast<int32_t>(b * 16) - static_cast<int32_t>(mis);
-                    uint32_t r = S.brow[b - w0];
-                    uint2 cur = S.ri[r], nxt = S.ri[r + 1];
+                    const uint32_t r = S.brow[b - w0];
+                    const uint2 A = S.ri[r], Bn = S.ri[r + 1], Cn = S.ri[min(r + 2, m)];
                     uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
-                    for (;;) {
-                        const int32_t lo = max(static_cast<int32_t>(cur.x) - a0, 0);
-                        const int32_t hi = min(static_cast<int32_t>(nxt.x) - a0, 16);
-                        if (hi > lo) {
-                            const uint32_t base = cur.y + kFront + static_cast<uint32_t>(a0 - static_cast<int32_t>(cur.x));
-                            const uint32_t wi = base >> 2, sh = base & 3;
-                            const uint32_t s0 = dwa[wi], s1 = dwa[wi + 1], s2 = dwa[wi + 2], s3 = dwa[wi + 3],
-                                           s4 = dwa[wi + 4];
-                            auto fmask = [](int32_t x, uint64_t& ml, uint64_t& mh) {
-                                ml = x >= 8 ? ~0ull : ((1ull << (8 * x)) - 1);
-                                mh = x <= 8 ? 0ull : (x >= 16 ? ~0ull : ((1ull << (8 * (x - 8))) - 1));
-                            };
-                            uint64_t hl, hh, ll, lh;
-                            fmask(hi, hl, hh);
-                            fmask(lo, ll, lh);
-                            const uint64_t ml = hl & ~ll, mh = hh & ~lh;
-                            o0 |= __builtin_amdgcn_alignbyte(s1, s0, sh) & static_cast<uint32_t>(ml);
-                            o1 |= __builtin_amdgcn_alignbyte(s2, s1, sh) & static_cast<uint32_t>(ml >> 32);
-                            o2 |= __builtin_amdgcn_alignbyte(s3, s2, sh) & static_cast<uint32_t>(mh);
-                            o3 |= __builtin_amdgcn_alignbyte(s4, s3, sh) & static_cast<uint32_t>(mh >> 32);
+                    // bytes [max(rs - a0, 0), min(re - a0, 16)) of the block from the
+                    // dictionary at sr: a 20-byte window, funnel-shifted, masked (MT)
+                    auto seg = [&](uint32_t rs, uint32_t re, uint32_t sr) {
+                        const int32_t lo = max(static_cast<int32_t>(rs) - a0, 0);
+                        const int32_t hi = min(static_cast<int32_t>(re) - a0, 16);
+                        if (hi <= lo) return;
+                        const uint32_t base = sr + kFront + static_cast<uint32_t>(a0 - static_cast<int32_t>(rs));
+                        const uint32_t wi = base >> 2, sh = base & 3;
+                        const uint32_t s0 = dwa[wi], s1 = dwa[wi + 1], s2 = dwa[wi + 2], s3 = dwa[wi + 3],
+                                       s4 = dwa[wi + 4];
+                        const uint4 mk = MT[(lo << 4) + lo + hi];
+                        o0 |= __builtin_amdgcn_alignbyte(s1, s0, sh) & mk.x;
+                        o1 |= __builtin_amdgcn_alignbyte(s2, s1, sh) & mk.y;
+                        o2 |= __builtin_amdgcn_alignbyte(s3, s2, sh) & mk.z;
+                        o3 |= __builtin_amdgcn_alignbyte(s4, s3, sh) & mk.w;
+                    };
+                    seg(A.x, Bn.x, A.y);
+                    const int32_t bend = a0 + 16;
+                    if (static_cast<int32_t>(Bn.x) < bend && r + 1 < m) {
+                        seg(Bn.x, Cn.x, Bn.y);
+                        if (static_cast<int32_t>(Cn.x) < bend && r + 2 < m) {  // rows shorter than a block
+                            uint32_t q = r + 2;
+                            uint2 cur = Cn;
+                            for (;;) {
+                                const uint2 nxt = S.ri[q + 1];
+                                seg(cur.x, nxt.x, cur.y);
+                                if (static_cast<int32_t>(nxt.x) >= bend || q + 1 >= m) break;
+                                q++;
+                                cur = nxt;
+                            }
                         }
-                        if (static_cast<int32_t>(nxt.x) >= a0 + 16 || r + 1 >= m) break;
-                        r++;
-                        cur = nxt;
-                        nxt = S.ri[r + 1];
                     }
                     const uint32_t ow[4] = {o0, o1, o2, o3};
                     const int64_t blk = (B0 + b) << 4;
+                    if (!st) return;
                     if (blk >= G0 && blk + 16 <= G1) {
                         *reinterpret_cast<uint4*>(a.chars + blk) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
                     } else {
@@ -657,6 +783,11 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
                             a.chars[x] = static_cast<uint8_t>(ow[at >> 2] >> (8 * (at & 3)));
                         }
                     }
+                };
+                // two blocks per step: their LDS round trips overlap
+                for (uint32_t b = w0 + lane(); b < w1; b += 2 * kWave) {
+                    do_block(b);
+                    do_block(b + kWave);
                 }
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -670,23 +801,37 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
 PipePlan plan_pipe_lds(uint32_t dict_bytes) {
     PipePlan pl{};
     pl.lds = dict_bytes + kWriteWaves * static_cast<uint32_t>(sizeof(WriteLds));
-    pl.blocks_per_cu = pl.lds <= 160u * 1024 ? static_cast<int>((160u * 1024) / pl.lds) : 0;
+    const uint32_t all = pl.lds + 17 * 17 * 16;  // + the static mask table
+    pl.blocks_per_cu = all <= 160u * 1024 ? static_cast<int>((160u * 1024) / all) : 0;
     if (pl.blocks_per_cu > 4) pl.blocks_per_cu = 4;
     return pl;
 }
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
-                      int32_t max_rep, uint2* runs, uint32_t* info) {
+                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave) {
     if (npages <= 0) return;
-    const int per = kRunWaves * kRunPages;
+    const int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
+    const int per = kRunWaves * ppw;
     hipLaunchKernelGGL(k_pipe_runs, dim3((npages + per - 1) / per), dim3(kRunWaves * kWave), 0, s, bytes, pages,
-                       npages, max_def, max_rep, runs, info);
+                       npages, max_def, max_rep, runs, info, ppw);
+}
+
+// k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's
+// characters under the workgroup that will write it).
+static void write_shape(const PipeLaunch& P, int* grid, int* per) {
+    const int need = (P.ntiles + kWriteWaves - 1) / kWriteWaves;
+    *grid = max(1, min(need, P.grid));
+    const int nw = *grid * kWriteWaves;
+    *per = max(1, (P.ntiles + nw - 1) / nw);
 }
 
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     if (P.ntiles <= 0) return;
+    int wgrid = 0, per = 0;
+    write_shape(P, &wgrid, &per);
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
-               P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any};
+               P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
+               P.bsum, per};
     const dim3 grid((P.ntiles + kCodeWaves - 1) / kCodeWaves);
     if (count_pass) hipLaunchKernelGGL(k_pipe_codes<true>, grid, dim3(kCodeWaves * kWave), 0, s, a);
     else hipLaunchKernelGGL(k_pipe_codes<false>, grid, dim3(kCodeWaves * kWave), 0, s, a);
@@ -700,11 +845,11 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(P.lds));
         attr = P.lds;
     }
+    int grid = 0, per = 0;
+    write_shape(P, &grid, &per);
     WriteArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.dicts, P.dict_id, P.entries, P.dict_count, P.codes,
-                P.tile_base, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets, P.chars,
-                P.dict_chars_bytes, P.dict_bytes, P.debug};
-    const int need = (P.ntiles + kWriteWaves - 1) / kWriteWaves;
-    const int grid = max(1, min(need, P.grid));
+                P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
+                P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug};
     hipLaunchKernelGGL(k_pipe_write, dim3(grid), dim3(kWriteWaves * kWave), P.lds, s, a);
 }
 

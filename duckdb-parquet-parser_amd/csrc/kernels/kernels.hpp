@@ -101,8 +101,8 @@ struct PipeLaunch {
     int32_t* tile_nn;           // per tile non-null rows (pages > 512 rows with def levels)
     uint16_t* codes;            // per row dictionary index, 0xFFFF = NULL
     int64_t* tile_chars;
-    const int64_t* tile_base;
-    const int64_t* total;
+    unsigned long long* bsum;   // per k_pipe_write workgroup characters (zeroed, P.grid entries)
+    int64_t* total;
     int64_t nrows_total;
     int64_t capacity;
     int32_t* overflow;
@@ -121,7 +121,7 @@ struct PipePlan {
 };
 PipePlan plan_pipe_lds(uint32_t dict_bytes);
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
-                      int32_t max_rep, uint2* runs, uint32_t* info);
+                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave);
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 

@@ -33,7 +33,8 @@ chunks = [F.chunk(0, 0)]
 ctx = capi.Context(0)
 
 
-def setp(path, dbg=0, waves=0, bbytes=12288, claim=1):
+def setp(path, dbg=0, waves=0, bbytes=12288, claim=1, rp=32):
+    ctx.set_option("pipe_run_pages", rp)
     ctx.set_option("dict_pipe", int(path == "pipe"))
     ctx.set_option("fused_claim", claim)
     ctx.set_option("fused_ba", int(path != "generic"))
@@ -45,10 +46,16 @@ def setp(path, dbg=0, waves=0, bbytes=12288, claim=1):
 
 variants = [("pipe", 0, 0, 12288, 1), ("pipe", 2, 0, 12288, 1), ("pipe", 4, 0, 12288, 1),
             ("pipe", 6, 0, 12288, 1), ("fused", 0, 0, 12288, 1)]
+if "write" in sys.argv:
+    variants = [("pipe", d, 0, 12288, 1) for d in (0, 2, 6, 8, 6 | 16)]
+if "runpages" in sys.argv:
+    variants = [("pipe", 0, 0, 12288, 1, rp) for rp in (32, 16, 8, 4)]
 if "batch" in sys.argv:
     variants += [("batch", 0, 0, 12288, 1), ("batch", 1, 0, 12288, 1), ("batch", 3, 0, 12288, 1)]
-for path, dbg, waves, bb, claim in variants:
-    setp(path, dbg, waves, bb, claim)
+for v in variants:
+    path, dbg, waves, bb, claim = v[:5]
+    rp = v[5] if len(v) > 5 else 32
+    setp(path, dbg, waves, bb, claim, rp)
     dc = ctx.upload(f, chunks)
     dc.decode_async()
     ctx.sync()
@@ -63,7 +70,8 @@ for path, dbg, waves, bb, claim in variants:
         if n:
             res[k] = round(ms / n, 4)
     ctx.timing(False)
-    print(json.dumps({"path": path, "debug": dbg, "waves": waves, "batch_bytes": bb, "claim": claim, "ms": res}),
+    print(json.dumps({"path": path, "debug": dbg, "waves": waves, "batch_bytes": bb, "claim": claim, "run_pages": rp,
+                      "ms": res}),
           flush=True)
     dc.free()
 
