@@ -509,12 +509,22 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_codes(CodeArgs a) {
 // ── offsets, validity, characters ──────────────────────────────────────────
 constexpr int kRowsPerLane = kTileRows / kWave;
 
+constexpr uint32_t kRing = 4096;  // per-wave staging of one 64-row group's characters
+
 struct WriteLds {
-    uint2 ri[kTileRows + 1];  // (tile-relative first byte, dictionary byte) per row
-    uint16_t brow[kWin];      // row holding each block's first byte
-    uint8_t vb[kWave];        // validity bits of rows 8l .. 8l + 7
-    uint32_t pad[4];
+    uint32_t off[kTileRows + 1];  // tile-relative first byte per row
+    uint16_t src[kTileRows];      // dictionary byte per row
+    uint8_t vb[kWave];            // validity bits of rows 8l .. 8l + 7
+    union {
+        uint4 ring[kRing / 16];   // characters, 16-byte aligned to the output
+        uint16_t brow[kWin];      // fallback: row holding each block's first byte
+    };
 };
+
+struct __attribute__((packed, aligned(1))) U16B { uint32_t x, y, z, w; };
+struct __attribute__((packed, aligned(1))) U8B { uint32_t x, y; };
+struct __attribute__((packed, aligned(1))) U4B { uint32_t x; };
+struct __attribute__((packed, aligned(1))) U2B { uint16_t x; };
 
 struct WriteArgs {
     const uint8_t* bytes;
@@ -538,7 +548,7 @@ struct WriteArgs {
     uint8_t* chars;
     uint32_t dict_chars_bytes, dict_bytes;
     int debug;  // ablation: 2 = no characters, 4 = no offsets/validity stores, 8 = prologue only,
-                //           16 = no block marking
+                //           16 = no block marking, 32 = no character stores, 64 = no ring copy
 };
 
 __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
@@ -549,19 +559,8 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
     uint32_t* dtab = reinterpret_cast<uint32_t*>(smem + kFront + a.dict_chars_bytes);
     const uint32_t wv = threadIdx.x / kWave;
     WriteLds& S = reinterpret_cast<WriteLds*>(smem + a.dict_bytes)[wv];
-    __shared__ uint4 MT[17 * 17];  // MT[lo * 17 + hi]: bytes [lo, hi) of a 16-byte block
     const DevDict d = a.dicts[a.dict_id];
     const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    for (uint32_t i = threadIdx.x; i < 17 * 17; i += blockDim.x) {
-        const uint32_t lo = i / 17, hi = i % 17;
-        uint32_t w[4];
-        for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t l = min(max(lo, 4 * q), 4 * q + 4) - 4 * q, h = min(max(hi, 4 * q), 4 * q + 4) - 4 * q;
-            const uint64_t mh = (1ull << (8 * h)) - 1, ml = (1ull << (8 * l)) - 1;
-            w[q] = h > l ? static_cast<uint32_t>(mh & ~ml) : 0u;
-        }
-        MT[i] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
         uint4* dst = reinterpret_cast<uint4*>(dw);
@@ -641,12 +640,12 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
             const int64_t R0 = rl64(myR0, i);
             const int64_t G0 = rl64(myG0, i);
             const uint32_t m = __builtin_amdgcn_readlane(mym, i);
-            uint32_t cur[kTileRows / kWave];
+            uint32_t cur[kRowsPerLane];
 #pragma unroll
-            for (int k = 0; k < kTileRows / kWave; k++) cur[k] = cd[k];
+            for (int k = 0; k < kRowsPerLane; k++) cur[k] = cd[k];
             if (i + 1 < cn) load_codes(i + 1);
             // this lane's rows 8l .. 8l + 7: lengths, dictionary offsets, validity
-            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0;
+            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0, lmax = 0;
 #pragma unroll
             for (int k = 0; k < kRowsPerLane; k++) {
                 const bool valid = cur[k] < dict_n;
@@ -655,31 +654,30 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
                 src[k] = e & 0xFFFFu;
                 vb |= (valid ? 1u : 0u) << k;
                 acc += len[k];
+                lmax = max(lmax, len[k]);
             }
             const uint32_t incl = wave_incl_scan(acc);
             const uint32_t total = bcast_last(incl);
-            const uint32_t mis = static_cast<uint32_t>(G0 & 15);
-            const uint32_t nb = total ? static_cast<uint32_t>(((G0 + total - 1) >> 4) - (G0 >> 4) + 1) : 0u;
-            const bool direct = nb <= kWin;  // brow filled here, one window
             {
                 uint32_t o = incl - acc;
 #pragma unroll
                 for (int k = 0; k < kRowsPerLane; k++) {
                     const uint32_t j = lane() * kRowsPerLane + k;
                     if (j < m) {
-                        S.ri[j] = make_uint2(o, src[k]);
-                        // row j owns the blocks whose first in-tile byte lies in it
-                        if (direct && len[k] && !(a.debug & 16)) {
-                            const uint32_t blo = o == 0 ? 0u : (o + mis + 15) >> 4;
-                            const uint32_t bhi = ((o + len[k] + mis + 15) >> 4) - 1;
-                            for (uint32_t b = blo; b <= bhi; b++) S.brow[b] = static_cast<uint16_t>(j);
-                        }
+                        S.off[j] = o;
+                        S.src[j] = static_cast<uint16_t>(src[k]);
                     }
                     o += len[k];
                 }
             }
+            // a 64-row group is 8 lanes: the ring must hold any group's characters
+            uint32_t g8 = acc;
+            g8 += __shfl_xor(g8, 1);
+            g8 += __shfl_xor(g8, 2);
+            g8 += __shfl_xor(g8, 4);
+            const bool ringable = __ballot(g8 + 32 > kRing) == 0;
             S.vb[lane()] = static_cast<uint8_t>(vb);
-            if (lane() == 0) S.ri[m] = make_uint2(total, 0u);
+            if (lane() == 0) S.off[m] = total;
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             if (!(a.debug & 4)) {
@@ -687,7 +685,7 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
 #pragma unroll
                 for (int k = 0; k < kRowsPerLane; k++) {
                     const uint32_t j = k * kWave + lane();
-                    if (j < m) a.offsets[R0 + j] = G0 + S.ri[j].x;
+                    if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
                 }
                 // validity words [R0 >> 5, (R0 + m - 1) >> 5]: tile word t = vb bytes 4t .. 4t + 3
                 const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
@@ -714,80 +712,130 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
                 continue;
             }
             const int64_t G1 = G0 + total;
-            const int64_t B0 = G0 >> 4;
-            for (uint32_t w0 = 0; w0 < nb; w0 += kWin) {
-                const uint32_t w1 = min(nb, w0 + kWin);
-                if (!direct) {  // row r owns the blocks whose first in-tile byte lies in it
-                    for (uint32_t r = lane(); r < m; r += kWave) {
-                        const uint32_t s = S.ri[r].x, e = S.ri[r + 1].x;
-                        if (e <= s) continue;
-                        uint32_t blo = s == 0 ? 0u : (s + mis + 15) / 16;
-                        uint32_t bhi = (e + mis + 15) / 16 - 1;
-                        blo = max(blo, w0);
-                        bhi = min(bhi, w1 - 1);
-                        for (uint32_t b = blo; b <= bhi; b++) S.brow[b - w0] = static_cast<uint16_t>(r);
+            if (ringable && !(a.debug & 128)) {
+                // per 64-row group: each lane copies its row into the ring with
+                // unaligned 16/8/4/2/1-byte LDS moves, then the wave stores the
+                // complete 16-byte blocks; a partial last block moves to ring[0]
+                uint8_t* ring = reinterpret_cast<uint8_t*>(S.ring);
+                const uint8_t* cb = reinterpret_cast<const uint8_t*>(dwa);
+                int64_t RB = G0 & ~static_cast<int64_t>(15);  // output address of ring[0]
+                for (uint32_t g0 = 0; g0 < m; g0 += kWave) {
+                    const uint32_t r = g0 + lane();
+                    if (r < m && !(a.debug & 64)) {
+                        // aligned LDS moves only: head bytes up to a dword boundary of
+                        // the ring, dwords funnel-shifted from the dictionary, tail bytes
+                        const uint32_t s0 = S.off[r], ln = S.off[r + 1] - s0;
+                        const uint32_t p = static_cast<uint32_t>(G0 + s0 - RB);
+                        const uint32_t q = S.src[r] + kFront;
+                        const uint32_t h = min((4u - (p & 3u)) & 3u, ln);
+                        {  // head: up to 3 bytes, all loads issued together
+                            const uint32_t b0 = cb[q], b1 = cb[q + 1], b2 = cb[q + 2];
+                            if (h > 0) ring[p] = static_cast<uint8_t>(b0);
+                            if (h > 1) ring[p + 1] = static_cast<uint8_t>(b1);
+                            if (h > 2) ring[p + 2] = static_cast<uint8_t>(b2);
+                        }
+                        const uint32_t p2 = p + h, q2 = q + h, rem = ln - h;
+                        const uint32_t nd = rem >> 2, sh = q2 & 3u;
+                        uint32_t* rw = reinterpret_cast<uint32_t*>(ring) + (p2 >> 2);
+                        const uint32_t* sw = dwa + (q2 >> 2);
+                        // body: four ring dwords per step from five dictionary dwords
+                        for (uint32_t d2 = 0; d2 < nd; d2 += 4) {
+                            const uint32_t s0 = sw[d2], s1 = sw[d2 + 1], s2 = sw[d2 + 2], s3 = sw[d2 + 3],
+                                           s4 = sw[d2 + 4];
+                            rw[d2] = __builtin_amdgcn_alignbyte(s1, s0, sh);
+                            if (d2 + 1 < nd) rw[d2 + 1] = __builtin_amdgcn_alignbyte(s2, s1, sh);
+                            if (d2 + 2 < nd) rw[d2 + 2] = __builtin_amdgcn_alignbyte(s3, s2, sh);
+                            if (d2 + 3 < nd) rw[d2 + 3] = __builtin_amdgcn_alignbyte(s4, s3, sh);
+                        }
+                        {  // tail: up to 3 bytes
+                            const uint32_t t = rem & 3u, pt = p2 + 4 * nd, qt = q2 + 4 * nd;
+                            const uint32_t b0 = cb[qt], b1 = cb[qt + 1], b2 = cb[qt + 2];
+                            if (t > 0) ring[pt] = static_cast<uint8_t>(b0);
+                            if (t > 1) ring[pt + 1] = static_cast<uint8_t>(b1);
+                            if (t > 2) ring[pt + 2] = static_cast<uint8_t>(b2);
+                        }
                     }
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                }
-                auto do_block = [&](uint32_t bq) {
-                    const uint32_t b = min(bq, w1 - 1);
-                    const bool st = bq < w1;
-                    // tile-relative byte of the block start (negative before G0);
-                    // each overlapping row contributes one masked 16-byte segment
-                    const int32_t a0 = static_cast<int32_t>(b * 16) - static_cast<int32_t>(mis);
-                    const uint32_t r = S.brow[b - w0];
-                    const uint2 A = S.ri[r], Bn = S.ri[r + 1], Cn = S.ri[min(r + 2, m)];
-                    uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
-                    // bytes [max(rs - a0, 0), min(re - a0, 16)) of the block from the
-                    // dictionary at sr: a 20-byte window, funnel-shifted, masked (MT)
-                    auto seg = [&](uint32_t rs, uint32_t re, uint32_t sr) {
-                        const int32_t lo = max(static_cast<int32_t>(rs) - a0, 0);
-                        const int32_t hi = min(static_cast<int32_t>(re) - a0, 16);
-                        if (hi <= lo) return;
-                        const uint32_t base = sr + kFront + static_cast<uint32_t>(a0 - static_cast<int32_t>(rs));
-                        const uint32_t wi = base >> 2, sh = base & 3;
-                        const uint32_t s0 = dwa[wi], s1 = dwa[wi + 1], s2 = dwa[wi + 2], s3 = dwa[wi + 3],
-                                       s4 = dwa[wi + 4];
-                        const uint4 mk = MT[(lo << 4) + lo + hi];
-                        o0 |= __builtin_amdgcn_alignbyte(s1, s0, sh) & mk.x;
-                        o1 |= __builtin_amdgcn_alignbyte(s2, s1, sh) & mk.y;
-                        o2 |= __builtin_amdgcn_alignbyte(s3, s2, sh) & mk.z;
-                        o3 |= __builtin_amdgcn_alignbyte(s4, s3, sh) & mk.w;
-                    };
-                    seg(A.x, Bn.x, A.y);
-                    const int32_t bend = a0 + 16;
-                    if (static_cast<int32_t>(Bn.x) < bend && r + 1 < m) {
-                        seg(Bn.x, Cn.x, Bn.y);
-                        if (static_cast<int32_t>(Cn.x) < bend && r + 2 < m) {  // rows shorter than a block
-                            uint32_t q = r + 2;
-                            uint2 cur = Cn;
-                            for (;;) {
-                                const uint2 nxt = S.ri[q + 1];
-                                seg(cur.x, nxt.x, cur.y);
-                                if (static_cast<int32_t>(nxt.x) >= bend || q + 1 >= m) break;
-                                q++;
-                                cur = nxt;
+                    const bool last = g0 + kWave >= m;
+                    const int64_t gend = G0 + S.off[min(g0 + kWave, m)];
+                    const uint32_t nfull = static_cast<uint32_t>((gend - RB) >> 4);
+                    const uint32_t nblk = last ? static_cast<uint32_t>((gend - RB + 15) >> 4) : nfull;
+                    for (uint32_t b = lane(); b < nblk && !(a.debug & 32); b += kWave) {
+                        const uint4 v = S.ring[b];
+                        const int64_t blk = RB + 16 * static_cast<int64_t>(b);
+                        if (blk >= G0 && blk + 16 <= G1) {
+                            *reinterpret_cast<uint4*>(a.chars + blk) = v;
+                        } else {
+                            const uint32_t ow[4] = {v.x, v.y, v.z, v.w};
+                            const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
+                            for (int64_t x = gs; x < ge; x++) {
+                                const uint32_t at = static_cast<uint32_t>(x - blk);
+                                a.chars[x] = static_cast<uint8_t>(ow[at >> 2] >> (8 * (at & 3)));
                             }
                         }
                     }
-                    const uint32_t ow[4] = {o0, o1, o2, o3};
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    if (!last) {
+                        if (lane() == 0 && nfull) S.ring[0] = S.ring[nfull];
+                        RB += 16 * static_cast<int64_t>(nfull);
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    }
+                }
+                continue;
+            }
+            // long strings: pull each 16-byte block from the rows it spans
+            const int64_t B0 = G0 >> 4;
+            const uint32_t nb = static_cast<uint32_t>(((G1 - 1) >> 4) - B0 + 1);
+            const uint32_t mis = static_cast<uint32_t>(G0 & 15);
+            for (uint32_t w0 = 0; w0 < nb; w0 += kWin) {
+                const uint32_t w1 = min(nb, w0 + kWin);
+                for (uint32_t r = lane(); r < m; r += kWave) {
+                    const uint32_t s0 = S.off[r], e0 = S.off[r + 1];
+                    if (e0 <= s0) continue;
+                    uint32_t blo = s0 == 0 ? 0u : (s0 + mis + 15) / 16;
+                    uint32_t bhi = (e0 + mis + 15) / 16 - 1;
+                    blo = max(blo, w0);
+                    bhi = min(bhi, w1 - 1);
+                    for (uint32_t b = blo; b <= bhi; b++) S.brow[b - w0] = static_cast<uint16_t>(r);
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                for (uint32_t b = w0 + lane(); b < w1; b += kWave) {
+                    const int32_t a0 = static_cast<int32_t>(b * 16) - static_cast<int32_t>(mis);
+                    uint32_t r = S.brow[b - w0];
+                    uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+                    for (;;) {
+                        const uint32_t rs = S.off[r], re = S.off[r + 1];
+                        const int32_t lo = max(static_cast<int32_t>(rs) - a0, 0);
+                        const int32_t hi = min(static_cast<int32_t>(re) - a0, 16);
+                        if (hi > lo) {
+                            const uint32_t base = S.src[r] + kFront + static_cast<uint32_t>(a0 - static_cast<int32_t>(rs));
+                            const U16B v = *reinterpret_cast<const U16B*>(reinterpret_cast<const uint8_t*>(dwa) + base);
+                            auto bm = [](int32_t x) -> uint32_t {  // bytes [0, x) of a dword, x clamped to 0..4
+                                return x <= 0 ? 0u : (x >= 4 ? 0xFFFFFFFFu : ((1u << (8 * x)) - 1u));
+                            };
+                            o0 |= v.x & (bm(hi) & ~bm(lo));
+                            o1 |= v.y & (bm(hi - 4) & ~bm(lo - 4));
+                            o2 |= v.z & (bm(hi - 8) & ~bm(lo - 8));
+                            o3 |= v.w & (bm(hi - 12) & ~bm(lo - 12));
+                        }
+                        if (static_cast<int32_t>(re) >= a0 + 16 || r + 1 >= m) break;
+                        r++;
+                    }
                     const int64_t blk = (B0 + b) << 4;
-                    if (!st) return;
                     if (blk >= G0 && blk + 16 <= G1) {
-                        *reinterpret_cast<uint4*>(a.chars + blk) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+                        *reinterpret_cast<uint4*>(a.chars + blk) = make_uint4(o0, o1, o2, o3);
                     } else {
+                        const uint32_t ow[4] = {o0, o1, o2, o3};
                         const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
                         for (int64_t x = gs; x < ge; x++) {
                             const uint32_t at = static_cast<uint32_t>(x - blk);
                             a.chars[x] = static_cast<uint8_t>(ow[at >> 2] >> (8 * (at & 3)));
                         }
                     }
-                };
-                // two blocks per step: their LDS round trips overlap
-                for (uint32_t b = w0 + lane(); b < w1; b += 2 * kWave) {
-                    do_block(b);
-                    do_block(b + kWave);
                 }
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -801,7 +849,7 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
 PipePlan plan_pipe_lds(uint32_t dict_bytes) {
     PipePlan pl{};
     pl.lds = dict_bytes + kWriteWaves * static_cast<uint32_t>(sizeof(WriteLds));
-    const uint32_t all = pl.lds + 17 * 17 * 16;  // + the static mask table
+    const uint32_t all = pl.lds;
     pl.blocks_per_cu = all <= 160u * 1024 ? static_cast<int>((160u * 1024) / all) : 0;
     if (pl.blocks_per_cu > 4) pl.blocks_per_cu = 4;
     return pl;
