@@ -89,13 +89,15 @@ struct pq_chunk {
     // three-pass dictionary BYTE_ARRAY decode (dict_pipe.hip)
     bool pipe = false, pipe_count = false;
     int32_t pipe_dict = -1;
-    uint32_t pipe_dict_chars_bytes = 0, pipe_dict_bytes = 0, pipe_lds = 0;
+    uint32_t pipe_dict_chars_bytes = 0, pipe_dict_bytes = 0, pipe_lds = 0, pipe_ecap = 0;
+    int pipe_cus = 256;
     int pipe_grid = 0;
     uint2* d_runs = nullptr;
     uint32_t* d_info = nullptr;
     uint16_t* d_codes = nullptr;
     int32_t* d_tile_nn = nullptr;
     unsigned long long* d_bsum = nullptr;
+    int32_t* d_flist = nullptr;
     // tile-parallel PLAIN fixed-width decode (fixed_fast.hip)
     bool fixed_plain = false;
     int32_t* d_tile_rank = nullptr;
@@ -243,6 +245,7 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_codes);
     dfree(c->d_tile_nn);
     dfree(c->d_bsum);
+    dfree(c->d_flist);
     dfree(c->d_page_pos);
     dfree(c->d_tile_base);
     dfree(c->d_total);
@@ -290,6 +293,8 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->pipe_dict_bytes = dict_bytes;
     c->pipe_lds = pl.lds;
     c->pipe_grid = cus * pl.blocks_per_cu;
+    c->pipe_ecap = static_cast<uint32_t>(ecap);
+    c->pipe_cus = cus;
 }
 
 // Decide whether every chunk of the column can take the fused BYTE_ARRAY
@@ -629,6 +634,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) + 64);
             rc |= dalloc(&c->d_tile_nn, htiles.size());
             rc |= dalloc(&c->d_bsum, static_cast<size_t>(c->pipe_grid));
+            rc |= dalloc(&c->d_flist, hpages.size() + 1);
         }
         if (c->fused && !c->hbatches.empty()) {
             rc |= dalloc(&c->d_batches, c->hbatches.size());
@@ -782,7 +788,7 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         P.bytes = c->d_bytes; P.pages = c->d_pages; P.npages = c->npages; P.tiles = c->d_tiles;
         P.ntiles = c->ntiles; P.page_tile0 = c->d_page_tile0; P.max_def = c->max_def; P.max_rep = c->max_rep;
         P.dicts = c->d_dicts; P.dict_id = c->pipe_dict; P.entries = c->d_entries; P.dict_count = c->d_dict_count;
-        P.runs = c->d_runs; P.info = c->d_info; P.tile_nn = c->d_tile_nn; P.codes = c->d_codes;
+        P.runs = c->d_runs; P.info = c->d_info; P.flist = c->d_flist; P.tile_nn = c->d_tile_nn; P.codes = c->d_codes;
         P.tile_chars = c->d_tile_chars; P.bsum = c->d_bsum; P.total = c->d_total;
         P.nrows_total = c->nrows; P.capacity = out->capacity_bytes; P.overflow = c->d_flags + 1;
         P.validity = out->d_validity; P.offsets = out->d_offsets; P.chars = out->d_values;
@@ -790,10 +796,12 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         P.dict_chars_bytes = c->pipe_dict_chars_bytes; P.dict_bytes = c->pipe_dict_bytes; P.lds = c->pipe_lds;
         P.grid = c->pipe_grid;
         P.debug = ctx->opt_debug;
+        P.dict_entries_cap = c->pipe_ecap;
+        P.cus = c->pipe_cus;
         {
             Timed t(ctx, "pipe_runs");
             pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->npages, c->max_def, c->max_rep, c->d_runs, c->d_info,
-                                  ctx->opt_run_pages);
+                                  ctx->opt_run_pages, c->d_flist);
         }
         if (c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
         if (c->pipe_count) {

@@ -129,7 +129,8 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
                                                               const DevPage* __restrict__ pages, int npages,
                                                               int32_t max_def, int32_t max_rep,
                                                               uint2* __restrict__ runs,
-                                                              uint32_t* __restrict__ info, int ppw) {
+                                                              uint32_t* __restrict__ info, int ppw,
+                                                              int32_t* __restrict__ flist) {
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[kRunWaves][kRunStage / 4 + 8];
     const uint32_t wv = threadIdx.x / kWave;
     const int g0 = (blockIdx.x * kRunWaves + static_cast<int>(wv)) * ppw;
@@ -214,6 +215,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
     const uint32_t orec = static_cast<uint32_t>(__shfl_xor(static_cast<int>(nrec), 1));
     if (act && s == 0)
         info[p] = ((flag | oflag) ? kFallback : 0u) | nrec | (orec << 8) | (bwi << 16);
+    if (act && s == 0 && (flag | oflag)) flist[1 + atomicAdd(flist, 1)] = p;  // for k_pipe_exact
 }
 
 // ── per-tile codes ─────────────────────────────────────────────────────────
@@ -245,6 +247,7 @@ struct CodeArgs {
     int32_t* err_any;
     unsigned long long* bsum;  // characters per k_pipe_write workgroup (its tiles)
     int per;                   // tiles per k_pipe_write wavefront
+    int debug;                 // 256: skip the exact decoder (timing only)
 };
 
 // Characters of tile t also go to the k_pipe_write workgroup that writes it.
@@ -504,6 +507,236 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_codes(CodeArgs a) {
     }
     chars = wave_sum(chars);
     tile_done(a, t, chars);
+}
+
+// Persistent per-tile codes: the dictionary's entry lengths in LDS, each
+// wavefront's rows 8l .. 8l + 7 contiguous (one wave scan per quantity), the
+// page payload staged in LDS for literal runs.
+constexpr int kCodeWaves2 = 8;
+constexpr uint32_t kCodeStage = 2048;
+struct CodeLds2 {
+    CodeLds c;
+    uint32_t stage[kCodeStage / 4 + 4];
+};
+
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane i <- lane i - 1, lane 0 <- 0
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x138, 0xf, 0xf, true));
+}
+
+__global__ void __launch_bounds__(kCodeWaves2 * 64, 3) k_pipe_codes2(CodeArgs a, uint32_t lt_n) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lens[];
+    __shared__ CodeLds2 lds_all[kCodeWaves2];
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    CodeLds2& L2 = lds_all[wv];
+    CodeLds& L = L2.c;
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    const uint32_t nl = min(dict_n, lt_n);
+    for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x)
+        lens[k] = static_cast<uint16_t>(a.entries[ebase + k] >> 32);
+    __syncthreads();
+    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
+    // each wavefront owns a contiguous run of tiles; descriptors of up to 64
+    // tiles load at once (one per lane) and the next tile's run records and
+    // payload load into registers while this tile is decoded
+    const int nw = static_cast<int>(gridDim.x) * kCodeWaves2;
+    const int per = (a.ntiles + nw - 1) / nw;
+    const int ta = min(a.ntiles, (static_cast<int>(blockIdx.x) * kCodeWaves2 + wv) * per);
+    const int tb = min(a.ntiles, ta + per);
+    auto rl64 = [](uint64_t v, int i) -> uint64_t {
+        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
+        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), i);
+        return (static_cast<uint64_t>(hi) << 32) | lo;
+    };
+    for (int c0 = ta; c0 < tb; c0 += kWave) {
+        const int cn = min(kWave, tb - c0);
+        uint32_t myp = 0, myrow0 = 0, mym = 0, myinf = kFallback, mysize = 0;
+        uint64_t myoff = 0, myfirst = 0;
+        if (static_cast<int>(lane()) < cn) {
+            const DevTile T = a.tiles[c0 + lane()];
+            const DevPage pg = a.pages[T.page];
+            myp = static_cast<uint32_t>(T.page);
+            myrow0 = static_cast<uint32_t>(T.row0);
+            mym = static_cast<uint32_t>(T.nrows);
+            myinf = a.info[T.page];
+            mysize = static_cast<uint32_t>(max(pg.size, 0));
+            myoff = pg.off;
+            myfirst = static_cast<uint64_t>(pg.first_row);
+        }
+        uint2 rq0, rq1, rq2, rq3;
+        uint4 sq0, sq1, sq2;
+        auto prefetch = [&](int i) {
+            const uint32_t inf = __builtin_amdgcn_readlane(myinf, i);
+            const uint32_t pp = __builtin_amdgcn_readlane(myp, i);
+            const uint32_t sz = __builtin_amdgcn_readlane(mysize, i);
+            const uint64_t off = rl64(myoff, i);
+            const uint32_t nd = (inf & kFallback) ? 0u : (inf & 0xFFu), ni = (inf & kFallback) ? 0u : ((inf >> 8) & 0xFFu);
+            const uint2* rd_ = a.runs + static_cast<size_t>(pp) * 2 * kPipeRunCap;
+            const uint2 z = make_uint2(0u, 0u);
+            rq0 = lane() < nd ? rd_[lane()] : z;
+            rq1 = lane() + kWave < nd ? rd_[lane() + kWave] : z;
+            rq2 = lane() < ni ? rd_[kPipeRunCap + lane()] : z;
+            rq3 = lane() + kWave < ni ? rd_[kPipeRunCap + lane() + kWave] : z;
+            const uint32_t nb = (inf & kFallback) || sz + 16 > kCodeStage ? 0u : (sz + 15) / 16 + 1;
+            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + off);
+            const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+            sq0 = lane() < nb ? src[lane()] : z4;
+            sq1 = lane() + kWave < nb ? src[lane() + kWave] : z4;
+            sq2 = lane() + 2 * kWave < nb ? src[lane() + 2 * kWave] : z4;
+        };
+        prefetch(0);
+        for (int i = 0; i < cn; i++) {
+            const int t = c0 + i;
+            const uint32_t inf = __builtin_amdgcn_readlane(myinf, i);
+            const int p = static_cast<int>(__builtin_amdgcn_readlane(myp, i));
+            const uint32_t r0 = __builtin_amdgcn_readlane(myrow0, i), m = __builtin_amdgcn_readlane(mym, i);
+            const uint32_t size = __builtin_amdgcn_readlane(mysize, i);
+            const uint8_t* page = a.bytes + rl64(myoff, i);
+            const int64_t first_row = static_cast<int64_t>(rl64(myfirst, i));
+            // this tile's records and payload -> LDS, then the next tile's loads
+            L.recd[lane()] = rq0;
+            L.recd[lane() + kWave] = rq1;
+            L.reci[lane()] = rq2;
+            L.reci[lane() + kWave] = rq3;
+            reinterpret_cast<uint4*>(L2.stage)[lane()] = sq0;
+            reinterpret_cast<uint4*>(L2.stage)[lane() + kWave] = sq1;
+            if (lane() + 2 * kWave < (kCodeStage / 4 + 4) / 4) reinterpret_cast<uint4*>(L2.stage)[lane() + 2 * kWave] = sq2;
+            if (i + 1 < cn) prefetch(i + 1);
+            if (inf & kFallback) continue;  // k_pipe_exact
+            if (a.debug & 512) {  // timing: loads and the tile loop only
+                if (lane() == 0) a.tile_chars[t] = 0;
+                continue;
+            }
+            const uint32_t nd = inf & 0xFFu, ni = (inf >> 8) & 0xFFu, bwi = (inf >> 16) & 0xFFu;
+            const bool staged = size + 16 <= kCodeStage;
+            const uint32_t l8 = lane() * 8;
+            if (l8 < m) *reinterpret_cast<uint2*>(L.mark + l8) = make_uint2(0u, 0u);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            auto bits = [&](uint64_t b, uint32_t bw) -> uint32_t {
+                return staged ? lds_bits(L2.stage, size, b, bw) : gbits(page, size, b, bw);
+            };
+            // def levels of this lane's rows r0 + 8l .. r0 + 8l + 7
+            uint32_t vb = 0;
+            if (a.max_def > 0) {
+                const uint32_t rd0 = run_at(L.recd, nd, r0);
+                for (uint32_t k = lane(); k < nd; k += kWave) {
+                    const uint32_t st = rr_start(L.recd[k]);
+                    if (k > rd0 && st < r0 + m) L.mark[st - r0] = static_cast<uint8_t>(k - rd0);
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint2 mk = l8 < m ? *reinterpret_cast<const uint2*>(L.mark + l8) : make_uint2(0u, 0u);
+                uint32_t rm[8], run = 0;
+    #pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
+                    rm[k] = run;
+                }
+                const uint32_t ex = wave_shr1(wave_incl_max(run));
+                bool above = false;
+    #pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t j = l8 + k;
+                    const uint2 R = L.recd[rd0 + max(ex, rm[k])];
+                    uint32_t lvl = rr_pay(R);
+                    if (rr_lit(R) && j < m) lvl = bits(rr_pay(R) + static_cast<uint64_t>(r0 + j - rr_start(R)) * bwd, bwd);
+                    vb |= (j < m && lvl == md ? 1u : 0u) << k;
+                    above |= j < m && lvl > md;
+                }
+                if (__ballot(above)) {  // levels above max_def: outside the supported format
+                    set_err(a.page_err + p, a.err_any, PQ_ERR_UNSUPPORTED, 0, 0, size);
+                    for (uint32_t j = lane(); j < m; j += kWave) a.codes[first_row + r0 + j] = kNull;
+                    if (lane() == 0) a.tile_chars[t] = 0;
+                    __builtin_amdgcn_wave_barrier();
+                    continue;
+                }
+            } else {
+                vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
+            }
+            const uint32_t nnl = __popc(vb);
+            const uint32_t nincl = wave_incl_scan(nnl);
+            const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
+            uint32_t k0 = r0;
+            if (a.max_def > 0) {
+                const int32_t tp = a.page_tile0[p];
+                uint32_t sum = 0;
+                for (int32_t q = tp + static_cast<int32_t>(lane()); q < t; q += kWave) sum += static_cast<uint32_t>(a.tile_nn[q]);
+                k0 = wave_sum(sum);
+            }
+            // dictionary index runs over ranks [k0, k0 + nn): run of each rank -> mark2
+            uint32_t ri0 = 0;
+            if (a.debug & 1024) {  // timing: def levels only
+                if (lane() == 0) a.tile_chars[t] = nn;
+                continue;
+            }
+            if (nn) {
+                if (l8 < nn) *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(0u, 0u);
+                __builtin_amdgcn_wave_barrier();
+                ri0 = run_at(L.reci, ni, k0);
+                for (uint32_t k = lane(); k < ni; k += kWave) {
+                    const uint32_t st = rr_start(L.reci[k]);
+                    if (k > ri0 && st < k0 + nn) L.mark2[st - k0] = static_cast<uint8_t>(k - ri0);
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint2 mk = l8 < nn ? *reinterpret_cast<const uint2*>(L.mark2 + l8) : make_uint2(0u, 0u);
+                uint32_t rm[8], run = 0;
+    #pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
+                    rm[k] = run;
+                }
+                const uint32_t ex = wave_shr1(wave_incl_max(run));
+                uint32_t w0 = 0, w1 = 0;
+    #pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t v = max(ex, rm[k]);
+                    if (k < 4) w0 |= v << (8 * k);
+                    else w1 |= v << (8 * (k - 4));
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (l8 < nn) *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(w0, w1);
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            uint32_t chars = 0;
+            const int64_t R0 = first_row + r0;
+    #pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t j = l8 + k;
+                uint32_t code = kNull;
+                if ((vb >> k) & 1u) {
+                    const uint32_t rk = rbase + __popc(vb & ((1u << k) - 1u));
+                    const uint2 R = L.reci[ri0 + L.mark2[rk]];
+                    uint32_t v = rr_pay(R);
+                    if (rr_lit(R)) v = bits(rr_pay(R) + static_cast<uint64_t>(k0 + rk - rr_start(R)) * bwi, bwi);
+                    if (v < dict_n) {
+                        code = v;
+                        chars += v < nl ? lens[v] : static_cast<uint32_t>(a.entries[ebase + v] >> 32);
+                    }
+                }
+                if (j < m) a.codes[R0 + j] = static_cast<uint16_t>(code);
+            }
+            chars = wave_sum(chars);
+            tile_done(a, t, chars);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// Marked pages (listed by k_pipe_runs): the exact serial decoder, one
+// wavefront per page.
+__global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_exact(CodeArgs a, const int32_t* __restrict__ flist) {
+    __shared__ CodeLds lds_all[kCodeWaves];
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    const int n = flist[0];
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    for (int i = static_cast<int>(blockIdx.x) * kCodeWaves + wv; i < n; i += static_cast<int>(gridDim.x) * kCodeWaves) {
+        exact_page(a, lds_all[wv], flist[1 + i], dict_n, ebase);
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // ── offsets, validity, characters ──────────────────────────────────────────
@@ -852,16 +1085,25 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes) {
     const uint32_t all = pl.lds;
     pl.blocks_per_cu = all <= 160u * 1024 ? static_cast<int>((160u * 1024) / all) : 0;
     if (pl.blocks_per_cu > 4) pl.blocks_per_cu = 4;
+    if (pl.blocks_per_cu > 0) {  // registers may allow fewer
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_write),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(pl.lds));
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k_pipe_write),
+                                                         kWriteWaves * kWave, pl.lds) == hipSuccess && occ > 0)
+            pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
+    }
     return pl;
 }
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
-                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave) {
+                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist) {
+    (void)hipMemsetAsync(flist, 0, sizeof(int32_t), s);
     if (npages <= 0) return;
     const int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
     const int per = kRunWaves * ppw;
     hipLaunchKernelGGL(k_pipe_runs, dim3((npages + per - 1) / per), dim3(kRunWaves * kWave), 0, s, bytes, pages,
-                       npages, max_def, max_rep, runs, info, ppw);
+                       npages, max_def, max_rep, runs, info, ppw, flist);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's
@@ -879,10 +1121,32 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     write_shape(P, &wgrid, &per);
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.bsum, per};
-    const dim3 grid((P.ntiles + kCodeWaves - 1) / kCodeWaves);
-    if (count_pass) hipLaunchKernelGGL(k_pipe_codes<true>, grid, dim3(kCodeWaves * kWave), 0, s, a);
-    else hipLaunchKernelGGL(k_pipe_codes<false>, grid, dim3(kCodeWaves * kWave), 0, s, a);
+               P.bsum, per, P.debug};
+    if (count_pass) {
+        const dim3 grid((P.ntiles + kCodeWaves - 1) / kCodeWaves);
+        hipLaunchKernelGGL(k_pipe_codes<true>, grid, dim3(kCodeWaves * kWave), 0, s, a);
+        return;
+    }
+    // persistent: the entry-length table (u16 per entry) is loaded once per workgroup
+    const uint32_t lt_n = P.dict_entries_cap;
+    const uint32_t lds = (lt_n * 2 + 15) / 16 * 16;
+    static uint32_t attr = 0;
+    if (lds > attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_codes2),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+        attr = lds;
+    }
+    // resident workgroups per CU (LDS and registers), so the grid is one wave of blocks
+    int bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(k_pipe_codes2),
+                                                     kCodeWaves2 * kWave, lds) != hipSuccess || bpc < 1)
+        bpc = 1;
+    const int need = (P.ntiles + kCodeWaves2 - 1) / kCodeWaves2;
+    const int grid = max(1, min(need, P.cus * bpc));
+    hipLaunchKernelGGL(k_pipe_codes2, dim3(grid), dim3(kCodeWaves2 * kWave), lds, s, a, lt_n);
+    // pages the run-table pass marked: exact decoder (each wave exits unless its tile starts one)
+    hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, (P.npages + kCodeWaves - 1) / kCodeWaves))),
+                       dim3(kCodeWaves * kWave), 0, s, a, P.flist);
 }
 
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
@@ -894,7 +1158,7 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
         attr = P.lds;
     }
     int grid = 0, per = 0;
-    write_shape(P, &grid, &per);
+    write_shape(P, &grid, &per);  // P.grid: resident workgroups (plan_pipe_lds + occupancy)
     WriteArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.dicts, P.dict_id, P.entries, P.dict_count, P.codes,
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
                 P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug};

@@ -98,6 +98,7 @@ struct PipeLaunch {
     const int32_t* dict_count;
     const uint2* runs;          // npages x 2 x kPipeRunCap
     const uint32_t* info;       // per page: run counts, index bit width, fallback flag
+    const int32_t* flist;       // [count, pages...] marked for the exact decoder
     int32_t* tile_nn;           // per tile non-null rows (pages > 512 rows with def levels)
     uint16_t* codes;            // per row dictionary index, 0xFFFF = NULL
     int64_t* tile_chars;
@@ -114,6 +115,8 @@ struct PipeLaunch {
     uint32_t dict_chars_bytes, dict_bytes, lds;
     int grid;
     int debug;  // ablation bits (k_pipe_write)
+    uint32_t dict_entries_cap;  // entry-table capacity of the dictionary (k_pipe_codes length table)
+    int cus;
 };
 struct PipePlan {
     uint32_t lds;       // dynamic LDS bytes of k_pipe_write
@@ -121,7 +124,7 @@ struct PipePlan {
 };
 PipePlan plan_pipe_lds(uint32_t dict_bytes);
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
-                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave);
+                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist);
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 

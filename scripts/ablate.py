@@ -46,6 +46,8 @@ def setp(path, dbg=0, waves=0, bbytes=12288, claim=1, rp=32):
 
 variants = [("pipe", 0, 0, 12288, 1), ("pipe", 2, 0, 12288, 1), ("pipe", 4, 0, 12288, 1),
             ("pipe", 6, 0, 12288, 1), ("fused", 0, 0, 12288, 1)]
+if "codes" in sys.argv:
+    variants = [("pipe", d, 0, 12288, 1) for d in (0, 512, 1024)]
 if "write" in sys.argv:
     variants = [("pipe", d, 0, 12288, 1) for d in (0, 2, 128, 128 | 32)]
 if "runpages" in sys.argv:
