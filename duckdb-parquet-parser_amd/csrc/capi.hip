@@ -50,6 +50,7 @@ struct pq_ctx {
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
+    bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
 };
 
@@ -98,6 +99,14 @@ struct pq_chunk {
     int32_t* d_tile_nn = nullptr;
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
+    // PLAIN BYTE_ARRAY, REQUIRED (plain_ba.hip)
+    bool plain = false;
+    std::vector<pqk::DevBatch> hpwins;
+    pqk::DevBatch* d_pwins = nullptr;
+    uint32_t* d_rowinfo = nullptr;
+    int64_t* d_wchars = nullptr;
+    unsigned long long* d_pbsum = nullptr;
+    int plain_grid = 0;
     // tile-parallel PLAIN fixed-width decode (fixed_fast.hip)
     bool fixed_plain = false;
     int32_t* d_tile_rank = nullptr;
@@ -240,6 +249,10 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_row_codes);
     dfree(c->d_tile_chars);
     dfree(c->d_tile_rank);
+    dfree(c->d_pwins);
+    dfree(c->d_rowinfo);
+    dfree(c->d_wchars);
+    dfree(c->d_pbsum);
     dfree(c->d_runs);
     dfree(c->d_info);
     dfree(c->d_codes);
@@ -295,6 +308,42 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->pipe_grid = cus * pl.blocks_per_cu;
     c->pipe_ecap = static_cast<uint32_t>(ecap);
     c->pipe_cus = cus;
+}
+
+// PLAIN BYTE_ARRAY chunks without levels go through plain_ba.hip: windows of
+// consecutive page slots of at most kPWin bytes.
+void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
+    c->plain = false;
+    c->hpwins.clear();
+    if (c->type != PQ_BYTE_ARRAY || c->max_def != 0 || c->max_rep != 0 || pages.empty()) return;
+    auto slot = [](const DevPage& p) {
+        return (static_cast<uint64_t>(std::max(p.size, 0)) + 15) / 16 * 16 + 16;
+    };
+    for (const auto& pg : pages)
+        if (pg.mode != pqk::MODE_PLAIN || slot(pg) > pqk::kPWin || pg.nvals < 0) return;
+    size_t p = 0;
+    while (p < pages.size()) {
+        pqk::DevBatch b{};
+        b.p0 = static_cast<int32_t>(p);
+        b.img_lo = pages[p].off;
+        uint64_t hi = b.img_lo;
+        size_t q = p;
+        while (q < pages.size() && q - p < 64 && pages[q].off >= b.img_lo) {
+            const uint64_t e = pages[q].off + slot(pages[q]);
+            if (e - b.img_lo > pqk::kPWin) break;
+            hi = e;
+            q++;
+        }
+        b.np = static_cast<int32_t>(q - p);
+        b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
+        c->hpwins.push_back(b);
+        p = q;
+    }
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+    c->plain_grid = cus * pqk::plain_write_blocks_per_cu();
+    c->plain = true;
 }
 
 // Decide whether every chunk of the column can take the fused BYTE_ARRAY
@@ -451,6 +500,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
+    if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
     if (std::strcmp(key, "pipe_run_pages") == 0) { ctx->opt_run_pages = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "regex_win") == 0) {
         if (value < 1024 || value > 32768 || value % 16) return set_err(ctx, PQ_ERR_ARG, "regex_win: 1024..32768, multiple of 16");
@@ -588,6 +638,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         c->nbytes = static_cast<size_t>(img) + 64;
         plan_fused(ctx, c.get(), hpages, hdicts);
         plan_pipe(ctx, c.get(), hpages, hdicts);
+        plan_plain(ctx, c.get(), hpages);
         c->npages = static_cast<int>(hpages.size());
         c->ndicts = static_cast<int>(hdicts.size());
 
@@ -636,6 +687,12 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc |= dalloc(&c->d_bsum, static_cast<size_t>(c->pipe_grid));
             rc |= dalloc(&c->d_flist, hpages.size() + 1);
         }
+        if (c->plain) {
+            rc |= dalloc(&c->d_pwins, c->hpwins.size());
+            rc |= dalloc(&c->d_rowinfo, static_cast<size_t>(c->nrows) + 64);
+            rc |= dalloc(&c->d_wchars, c->hpwins.size());
+            rc |= dalloc(&c->d_pbsum, static_cast<size_t>(c->plain_grid));
+        }
         if (c->fused && !c->hbatches.empty()) {
             rc |= dalloc(&c->d_batches, c->hbatches.size());
             rc |= dalloc(&c->d_bstatus, c->hbatches.size());
@@ -667,6 +724,8 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc = hip_check(ctx, hipMemcpyAsync(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc) (void)hipMemsetAsync(c->d_page_err, 0, std::max<size_t>(hpages.size(), 1) * sizeof(DevErr), s);
         if (!rc) (void)hipMemsetAsync(c->d_dict_err, 0, std::max<size_t>(hdicts.size(), 1) * sizeof(DevErr), s);
+        if (!rc && c->d_pwins)
+            rc = hip_check(ctx, hipMemcpyAsync(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice, s), "upload");
         if (!rc && c->d_batches)
             rc = hip_check(ctx, hipMemcpyAsync(c->d_batches, c->hbatches.data(), c->hbatches.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice, s), "upload");
         if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
@@ -783,7 +842,20 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
                                  c->d_dict_err, c->d_flags, c->type, c->plain_width);
     }
-    if (pipe) {
+    if (c->plain && ctx->opt_plain) {
+        pqk::PlainLaunch P{};
+        P.bytes = c->d_bytes; P.pages = c->d_pages; P.wins = c->d_pwins;
+        P.nwins = static_cast<int32_t>(c->hpwins.size()); P.rowinfo = c->d_rowinfo; P.wchars = c->d_wchars;
+        P.bsum = c->d_pbsum; P.grid = c->plain_grid; P.nrows_total = c->nrows; P.total = c->d_total;
+        P.capacity = out->capacity_bytes; P.overflow = c->d_flags + 1; P.validity = out->d_validity;
+        P.offsets = out->d_offsets; P.chars = out->d_values; P.page_err = c->d_page_err; P.err_any = c->d_flags;
+        if (c->nrows == 0) {
+            (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
+            (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
+        }
+        Timed t(ctx, "plain_ba");
+        pqk::launch_plain_ba(s, P);
+    } else if (pipe) {
         pqk::PipeLaunch P{};
         P.bytes = c->d_bytes; P.pages = c->d_pages; P.npages = c->npages; P.tiles = c->d_tiles;
         P.ntiles = c->ntiles; P.page_tile0 = c->d_page_tile0; P.max_def = c->max_def; P.max_rep = c->max_rep;

@@ -220,4 +220,28 @@ uint32_t fused_wave_bytes(uint32_t rows_cap, uint32_t stage_bytes);
 int fused_occupancy_waves(uint32_t lds_bytes_per_block, int waves_per_block);
 int fused_prof_slots();
 
+// ── PLAIN BYTE_ARRAY, REQUIRED (plain_ba.hip) ────────────────────────────
+constexpr uint32_t kPWin = 8192;  // window bytes (consecutive page slots)
+struct PlainLaunch {
+    const uint8_t* bytes;
+    const DevPage* pages;
+    const DevBatch* wins;        // windows: p0, np, img_lo, img_bytes
+    int32_t nwins;
+    uint32_t* rowinfo;           // per row: position in window | length << 16
+    int64_t* wchars;             // per window characters
+    unsigned long long* bsum;    // per k_plain_write workgroup characters
+    int per, grid;
+    int64_t nrows_total;
+    int64_t* total;
+    int64_t capacity;
+    int32_t* overflow;
+    uint32_t* validity;
+    int64_t* offsets;
+    uint8_t* chars;
+    DevErr* page_err;
+    int32_t* err_any;
+};
+int plain_write_blocks_per_cu();
+void launch_plain_ba(hipStream_t s, PlainLaunch P);
+
 }  // namespace pqk

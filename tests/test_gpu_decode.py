@@ -37,16 +37,19 @@ SMALL = [
 
 @pytest.fixture(params=["pipe", "batch", "fused", "generic"])
 def path(request, ctx):
-    """Every kernel path: BYTE_ARRAY three-pass dictionary (dict_pipe.hip),
+    """Every kernel path: BYTE_ARRAY three-pass dictionary (dict_pipe.hip) and
+    two-pass PLAIN (plain_ba.hip),
     batched dictionary (dict_batch.hip), per-page fused (dict_fused.hip) and
     generic (decode.hip); fixed-width PLAIN tile-parallel (fixed_fast.hip)
     except under "generic", which runs decode.hip's per-page k_fixed."""
     ctx.set_option("dict_pipe", int(request.param == "pipe"))
+    ctx.set_option("plain_ba", int(request.param == "pipe"))
     ctx.set_option("fused_ba", int(request.param != "generic"))
     ctx.set_option("batch", int(request.param == "batch"))
     ctx.set_option("fixed_plain", int(request.param != "generic"))
     yield request.param
     ctx.set_option("dict_pipe", 1)
+    ctx.set_option("plain_ba", 1)
     ctx.set_option("fused_ba", 1)
     ctx.set_option("batch", 0)
     ctx.set_option("fixed_plain", 1)
@@ -149,6 +152,10 @@ CRAFTED = {
     # literal def-level run reading past the level section into the page
     "def_lit_overrun": lambda: _dict_ba_file(bytes([2]) + B.rle(16, 3, 2), 16, DICT,
                                              def_stream=bytes([(2 << 1) | 1, 0xFF])),
+    # PLAIN BYTE_ARRAY over several pages, empty strings, a 5000-byte string
+    "plain_pages": lambda: B.build_file([B.data_header(len(B.plain_ba(v)), len(v), 0) + B.plain_ba(v) for v in
+                                         ([b"a", b"", b"bcd"], [b"x" * 5000], [b"", b""], [b"tail-%d" % i for i in range(300)])],
+                                        gen.BYTE_ARRAY, False, 306),
     # multi-byte varint run header (count 300)
     "long_rle_run": lambda: _dict_ba_file(bytes([2]) + B.rle(300, 2, 2), 300, DICT),
     # def levels + nulls, RLE and bit-packed level runs
@@ -193,6 +200,10 @@ ERRORS = {
     # truncated PLAIN BYTE_ARRAY value
     "truncated_plain": lambda: B.build_file([B.data_header(9, 2, 0) + struct.pack("<I", 2) + b"ab" + struct.pack("<I", 9)[:3]],
                                             gen.BYTE_ARRAY, False, 2),
+    # PLAIN BYTE_ARRAY: the chain runs out in the second page
+    "plain_short_page2": lambda: B.build_file([B.data_header(len(B.plain_ba([b"ok"])), 1, 0) + B.plain_ba([b"ok"]),
+                                               B.data_header(len(B.plain_ba([b"abc", b"de"])), 3, 0) + B.plain_ba([b"abc", b"de"])],
+                                              gen.BYTE_ARRAY, False, 4),
     # def_len beyond the page
     "def_len_overrun": lambda: B.build_file([B.data_header(6, 3, 0) + struct.pack("<I", 50) + b"xy"], gen.INT32, True, 3),
     # dictionary page index stream without the bit-width byte
