@@ -21,6 +21,7 @@
 #include "kernels/device_common.hpp"
 #include "kernels/kernels.hpp"
 #include "kernels/lane_walk.hpp"
+#include "kernels/run_walk.hpp"
 #include "kernels/stream.hpp"
 #include "pq_gpu.h"
 
@@ -92,23 +93,14 @@ __global__ void __launch_bounds__(256) k_fixed_req(const uint8_t* __restrict__ b
     }
 }
 
-// One wavefront per page.  tile_rank[t] = non-null rows of the page before
-// tile t; page_pos[p] = the byte where the page's values start.
-__global__ void __launch_bounds__(256) k_fixed_levels(const uint8_t* __restrict__ bytes,
-                                                      const DevPage* __restrict__ pages, int npages,
-                                                      const int32_t* __restrict__ page_tile0, ColumnParams cp,
-                                                      uint32_t* __restrict__ validity,
-                                                      int32_t* __restrict__ tile_rank,
-                                                      int32_t* __restrict__ page_pos,
-                                                      DevErr* __restrict__ page_err,
-                                                      int32_t* __restrict__ err_any) {
-    __shared__ LitRun lits_all[kTilesPerBlock][kLitCapF];
-    __shared__ uint32_t bits_all[kTilesPerBlock][kTileRows / 32];
-    const int wv = static_cast<int>(threadIdx.x / kWave);
-    const int p = blockIdx.x * kTilesPerBlock + wv;
-    if (p >= npages) return;
-    LitRun* lits = lits_all[wv];
-    uint32_t* bits = bits_all[wv];
+// Exact serial form, one wavefront per page (pages the run-table form does
+// not take).  tile_rank[t] = non-null rows of the page before tile t;
+// page_pos[p] = the byte where the page's values start.
+__device__ void levels_serial(const uint8_t* __restrict__ bytes, const DevPage* __restrict__ pages, int p,
+                              const int32_t* __restrict__ page_tile0, ColumnParams cp,
+                              uint32_t* __restrict__ validity, int32_t* __restrict__ tile_rank,
+                              int32_t* __restrict__ page_pos, DevErr* __restrict__ page_err,
+                              int32_t* __restrict__ err_any, LitRun* lits, uint32_t* bits) {
     const DevPage pg = pages[p];
     const uint8_t* page = bytes + pg.off;
     const uint32_t size = static_cast<uint32_t>(pg.size);
@@ -183,6 +175,184 @@ __global__ void __launch_bounds__(256) k_fixed_levels(const uint8_t* __restrict_
     if (lane() == 0) page_pos[p] = static_cast<int32_t>(pos);
 }
 
+// One workgroup (8 waves) per page: the page's level bytes staged in LDS,
+// one lane walks the def stream into an LDS run table (run_walk.hpp), then
+// the waves expand 512-row tiles in parallel (max-scan over run starts, rows
+// 8l .. 8l + 7 per lane) into validity words and per-tile non-null counts.
+// Pages outside that shape (long level sections, > kLvRec runs, zero-count
+// runs, ...) take levels_serial on wave 0.
+constexpr int kLvWaves = 8;
+constexpr uint32_t kLvStage = 16384;
+constexpr uint32_t kLvRec = 1024;
+constexpr uint32_t kLvTiles = 128;
+
+__global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* __restrict__ bytes,
+                                                                const DevPage* __restrict__ pages,
+                                                                const int32_t* __restrict__ page_tile0,
+                                                                ColumnParams cp, uint32_t* __restrict__ validity,
+                                                                int32_t* __restrict__ tile_rank,
+                                                                int32_t* __restrict__ page_pos,
+                                                                DevErr* __restrict__ page_err,
+                                                                int32_t* __restrict__ err_any) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kLvStage / 4 + 8];
+    __shared__ uint2 rec[kLvRec];
+    __shared__ __attribute__((aligned(16))) uint16_t mark_all[kLvWaves][kTileRows];
+    __shared__ uint8_t vb_all[kLvWaves][kWave];
+    __shared__ uint32_t tnn[kLvTiles];
+    __shared__ uint32_t sh[4];  // status, nrec, pos
+    __shared__ LitRun lits[kLitCapF];
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    const int p = blockIdx.x;
+    const DevPage pg = pages[p];
+    const uint8_t* page = bytes + pg.off;
+    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    const uint32_t md = static_cast<uint32_t>(cp.max_def), bw = level_bw(cp.max_def);
+    if (wv == 0) {  // prologue (column_reader.cpp:146-164): 0 ok, 1 serial form, 2 error
+        uint32_t st = 0, pos = 0, dlen = 0;
+        if (cp.max_def == 0) st = 1;  // repetition levels only: the serial form
+        else if (pos + 4 > size) { set_err(page_err + p, err_any, PQ_ERR_BUFFER, pos, 4, size); st = 2; }
+        else {
+            dlen = static_cast<uint32_t>(gld8(page, 0));
+            pos = 4;
+            if (static_cast<uint64_t>(pos) + dlen > size) { set_err(page_err + p, err_any, PQ_ERR_BUFFER, pos, dlen, size); st = 2; }
+            else pos += dlen;
+        }
+        if (!st && cp.max_rep > 0) {
+            if (pos + 4 > size) { set_err(page_err + p, err_any, PQ_ERR_BUFFER, pos, 4, size); st = 2; }
+            else {
+                const uint32_t rl = static_cast<uint32_t>(gld8(page, pos));
+                pos += 4;
+                if (static_cast<uint64_t>(pos) + rl > size) { set_err(page_err + p, err_any, PQ_ERR_BUFFER, pos, rl, size); st = 2; }
+                else pos += rl;
+            }
+        }
+        if (!st && (n > 65535u || 4 + dlen + 16 > kLvStage || n > kLvTiles * kTileRows)) st = 1;
+        if (lane() == 0) { sh[0] = st; sh[1] = 0; sh[2] = pos; sh[3] = dlen; }
+    }
+    __syncthreads();
+    if (sh[0] == 2) return;
+    const uint32_t dlen = sh[3];
+    if (sh[0] == 0) {  // level bytes -> LDS
+        const uint4* src = reinterpret_cast<const uint4*>(page);
+        uint4* dst = reinterpret_cast<uint4*>(stage);
+        const uint32_t nb = (4 + dlen + 15) / 16 + 1;
+        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    if (sh[0] == 0 && wv == 0) {
+        RunWalk W{};
+        W.alive = lane() == 0;
+        W.q = 4;
+        W.end = 4 + dlen;
+        W.bw = bw;
+        W.n = n;
+        W.sbase = 0;
+        W.cap = kLvRec;
+        W.out = rec;
+        W.gp = page;
+        uint32_t flag = 0, nrec = 0;
+        walk_runs<true>(W, stage, flag, nrec);
+        if (lane() == 0) { sh[1] = nrec; if (flag) sh[0] = 1; }
+    }
+    __syncthreads();
+    if (sh[0] == 1) {
+        if (wv == 0)
+            levels_serial(bytes, pages, p, page_tile0, cp, validity, tile_rank, page_pos, page_err, err_any, lits,
+                          reinterpret_cast<uint32_t*>(mark_all[1]));
+        return;
+    }
+    const uint32_t nrec = sh[1];
+    const uint32_t staged_bytes = 4 + dlen + 16;
+    auto bits = [&](uint64_t b) -> uint32_t {
+        return (b >> 3) + 8 < staged_bytes ? lds_bits(stage, staged_bytes, b, bw) : gbits(page, size, b, bw);
+    };
+    uint16_t* mark = mark_all[wv];
+    const uint32_t ntiles = (n + kTileRows - 1) / kTileRows;
+    for (uint32_t ti = static_cast<uint32_t>(wv); ti < ntiles; ti += kLvWaves) {
+        const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
+        // first run covering r0
+        uint32_t c = 0;
+        for (uint32_t k0 = 0; k0 < nrec; k0 += kWave) {
+            const uint32_t k = k0 + lane();
+            c += __popcll(__ballot(k < nrec && (rec[k].x & 0xFFFFu) <= r0));
+        }
+        const uint32_t rd0 = c - 1;
+        const uint32_t l8 = lane() * 8;
+        if (l8 < m) *reinterpret_cast<uint4*>(mark + l8) = make_uint4(0u, 0u, 0u, 0u);
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t k = rd0 + 1 + lane(); k < nrec; k += kWave) {
+            const uint32_t st = rec[k].x & 0xFFFFu;
+            if (st >= r0 + m) break;
+            mark[st - r0] = static_cast<uint16_t>(k - rd0);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint4 mk = l8 < m ? *reinterpret_cast<const uint4*>(mark + l8) : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
+        uint32_t rm[8], run = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            run = max(run, (mw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+            rm[k] = run;
+        }
+        const uint32_t ex = static_cast<uint32_t>(
+            __builtin_amdgcn_update_dpp(0, static_cast<int>(wave_incl_max(run)), 0x138, 0xf, 0xf, true));
+        uint32_t vb = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t j = l8 + k;
+            if (j < m) {
+                const uint2 R = rec[rd0 + max(ex, rm[k])];
+                uint32_t lvl = R.y & 0x7FFFFFFFu;
+                if (R.y >> 31) lvl = bits((R.y & 0x7FFFFFFFu) + static_cast<uint64_t>(r0 + j - (R.x & 0xFFFFu)) * bw);
+                vb |= (lvl >= md ? 1u : 0u) << k;
+            }
+        }
+        // validity words of rows [R0, R0 + m): tile word t = vb bytes 4t .. 4t + 3
+        vb_all[wv][lane()] = static_cast<uint8_t>(vb);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int64_t R0 = pg.first_row + r0;
+        const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
+        const uint32_t shf = static_cast<uint32_t>(R0 & 31);
+        const int64_t g = gfirst + lane();
+        if (g <= glast) {
+            auto tw = [&](int t) -> uint32_t {
+                return (t >= 0 && t < kWave / 4) ? reinterpret_cast<const uint32_t*>(vb_all[wv])[t] : 0u;
+            };
+            const int t = static_cast<int>(lane());
+            const uint32_t val = (tw(t) << shf) | (shf ? (tw(t - 1) >> (32 - shf)) : 0u);
+            const int64_t plo = pg.first_row, phi = pg.first_row + n;
+            const bool whole = g * 32 >= plo && g * 32 + 32 <= phi && g * 32 >= R0 && g * 32 + 32 <= R0 + m;
+            if (whole) validity[g] = val;
+            else if (val) atomicOr(&validity[g], val);
+        }
+        const uint32_t nn = bcast_last(wave_incl_scan(__popc(vb)));
+        if (lane() == 0) tnn[ti] = nn;
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    if (wv == 0) {  // tile ranks, value start, PLAIN bounds check (ByteBuffer::check)
+        uint32_t carry = 0;
+        const int32_t t0 = page_tile0[p];
+        for (uint32_t i0 = 0; i0 < ntiles; i0 += kWave) {
+            const uint32_t i = i0 + lane();
+            const uint32_t v = i < ntiles ? tnn[i] : 0u;
+            const uint32_t inc = wave_incl_scan(v);
+            if (i < ntiles) tile_rank[t0 + static_cast<int32_t>(i)] = static_cast<int32_t>(carry + inc - v);
+            carry += bcast_last(inc);
+        }
+        const uint32_t pos = sh[2];
+        const uint32_t w = static_cast<uint32_t>(cp.plain_width);
+        if (static_cast<uint64_t>(pos) + static_cast<uint64_t>(carry) * w > size) {
+            const uint32_t k = (size - pos) / w;
+            set_err(page_err + p, err_any, PQ_ERR_BUFFER, pos + k * w, w, size);
+        }
+        if (lane() == 0) page_pos[p] = static_cast<int32_t>(pos);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_fixed_scatter(const uint8_t* __restrict__ bytes,
                                                        const DevPage* __restrict__ pages,
                                                        const DevTile* __restrict__ tiles, int ntiles,
@@ -237,9 +407,8 @@ void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* page
                            validity, values, page_err, err_any);
         return;
     }
-    const int pb = (npages + kTilesPerBlock - 1) / kTilesPerBlock;
-    hipLaunchKernelGGL(k_fixed_levels, dim3(pb), dim3(kTilesPerBlock * kWave), 0, s, bytes, pages, npages, page_tile0,
-                       cp, validity, tile_rank, page_pos, page_err, err_any);
+    hipLaunchKernelGGL(k_fixed_levels2, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0, cp,
+                       validity, tile_rank, page_pos, page_err, err_any);
     hipLaunchKernelGGL(k_fixed_scatter, dim3(tb), dim3(kTilesPerBlock * kWave), 0, s, bytes, pages, tiles, ntiles, pw,
                        validity, tile_rank, page_pos, page_err, values);
 }

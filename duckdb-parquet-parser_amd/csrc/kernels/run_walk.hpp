@@ -1,0 +1,86 @@
+// run_walk.hpp — the lock-step run-header walk shared by the run-table
+// kernels (dict_pipe.hip k_pipe_runs, fixed_fast.hip k_fixed_levels2): one
+// hybrid RLE/bit-packed stream per lane (rle_decoder.hpp:36-95), one run
+// record per step.
+#pragma once
+#include "kernels/device_common.hpp"
+#include "kernels/lane_walk.hpp"
+
+namespace pqk {
+namespace dev {
+
+// One hybrid stream per lane, walked with every lane in lock step: each
+// step parses one run header (rle_decoder.hpp:36-95) and appends one record.
+struct RunWalk {
+    bool alive;
+    uint32_t q, end, bw, n, sbase, cap;
+    uint2* out;
+    const uint8_t* gp;
+};
+
+template <bool kStaged>
+__device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uint32_t& flag, uint32_t& nrec) {
+    const uint32_t nbv = (W.bw + 7) / 8;
+    const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+    const uint32_t litpay = W.bw ? 0x80000000u : 0u;
+    const uint32_t litmul = W.bw ? 8u : 0u;
+    uint32_t cnt = 0, q = W.q, nr = nrec, fl = flag;
+    bool alive = W.alive && W.n > 0;
+    // branch-free step: every quantity is computed, one predicated store
+    while (__ballot(alive)) {
+        uint32_t x0, x1;
+        if (kStaged) {
+            const uint32_t a = W.sbase + q, wi = a >> 2, sh = a & 3;
+            const uint32_t w0 = stage[wi], w1 = stage[wi + 1], w2 = stage[wi + 2];
+            x0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        } else {
+            const uint64_t x = alive ? gld8(W.gp, q) : 0ull;
+            x0 = static_cast<uint32_t>(x);
+            x1 = static_cast<uint32_t>(x >> 32);
+        }
+        const uint32_t exh = q >= W.end ? 1u : 0u;  // rest of the batch is 0 (rle_decoder.hpp:20-23)
+        // varint header (76-86): at most 5 bytes, inside the stream
+        const uint32_t st0 = ~x0 & 0x80808080u;
+        const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;
+        const uint32_t hl5 = (~x1 & 0x80u) ? 5u : 9u;
+        const uint32_t hl = st0 ? hl4 : hl5;
+        const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
+        const uint32_t x0m = x0 & lm;
+        const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
+        const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
+                             ((x0m >> 3) & 0xFE00000u) | top;
+        const uint32_t g = ind >> 1;
+        const uint32_t lit = ind & 1u;
+        const uint32_t left = W.n - cnt;
+        const uint32_t qh = q + hl;
+        const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, hl);
+        const uint32_t vb = x1 >> (8 * ((hl - 4) & 3));
+        const uint32_t vraw = (hl < 4) ? va : vb;
+        const uint32_t cl = (g >= (left + 7) / 8) ? left : g * 8;
+        const uint32_t cr = min(g, left);
+        const uint32_t c = lit ? cl : cr;
+        // zero-count runs (counter wrap / stale literal cursor), truncated headers or values
+        const uint32_t badh = (hl > 5 ? 1u : 0u) | (qh > W.end ? 1u : 0u) | (g == 0 ? 1u : 0u) |
+                              ((lit ^ 1u) & (qh + nbv > W.end ? 1u : 0u));
+        const uint32_t full = nr >= W.cap ? 1u : 0u;
+        const uint32_t ok = (alive ? 1u : 0u) & (full ^ 1u) & (exh | (badh ^ 1u));
+        const uint32_t rx = cnt | ((exh ? left : c) << 16);
+        const uint32_t pl = lit ? (litpay | (qh * litmul)) : (vraw & vmask);
+        const uint32_t ry = exh ? 0u : pl;
+        if (ok) W.out[nr] = make_uint2(rx, ry);
+        fl |= (alive ? 1u : 0u) & (ok ^ 1u);
+        nr += ok;
+        const uint64_t nql = static_cast<uint64_t>(qh) + static_cast<uint64_t>(g) * W.bw;
+        const uint32_t nqlc = nql > W.end ? W.end : static_cast<uint32_t>(nql);
+        const uint32_t nq = lit ? nqlc : qh + nbv;
+        cnt = exh ? W.n : cnt + c;
+        q = ok ? nq : q;
+        alive = ok && !exh && cnt < W.n;
+    }
+    nrec = nr;
+    flag = fl;
+}
+
+}  // namespace dev
+}  // namespace pqk
