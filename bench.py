@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--regex-rows", type=int, default=ROWS)
     ap.add_argument("--pattern", default="special.*requests")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--c4-rows", type=int, default=ROWS)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
 
@@ -243,7 +245,25 @@ def main():
                            "reported_pages": int(flags.sum()),
                            "kernel": rkern, "kernel_ms": rms / rn if rn else None,
                            "payload_GBs": rdc.payload_bytes / (rms / rn * 1e-3) / 1e9 if rn else None}
+        # C3 decode (R-PLAIN BYTE_ARRAY) on the same upload
+        result["c3_decode"] = _time_decode(ctx, rdc, max(3, args.steps // 2), barrier, dist, local, world)
         rdc.free()
+
+    # ── C4: 8 mixed columns, one row group per GPU ───────────────
+    if not args.no_c4:
+        cfile = gen.build(gen.c4_cols(), args.c4_rows, 1, seed=gen.CONFIG_SEEDS["C4"], layout=gen.ARROW_LAYOUT,
+                          first_rg=my_rgs[0])
+        CF = capi.File(cfile)
+        cols, total_ms = {}, 0.0
+        for ci, col in enumerate(gen.c4_cols()):
+            cdc = ctx.upload(cfile, [CF.chunk(0, ci)])
+            r = _time_decode(ctx, cdc, max(3, args.steps // 4), barrier, dist, local, world)
+            cdc.free()
+            cols[col.name] = {"ms": r["ms_per_decode"], "kernels_ms": r["kernel_ms"]}
+            total_ms += r["ms_per_decode"]
+        result["c4"] = {"values_per_s": 8 * args.c4_rows * world / (total_ms * 1e-3), "rows_per_gpu": args.c4_rows,
+                        "ms_per_row_group": total_ms, "columns": cols, "layout": "arrow"}
+        del cfile
 
     # ── CPU baseline beside it (rank 0, N=1 only) ──────────────────────────
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -256,6 +276,37 @@ def main():
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _time_decode(ctx, dc, steps, barrier, dist, local, world):
+    """Wall time of `steps` decodes of an uploaded chunk (max over ranks) and
+    the per-kernel HIP-event averages."""
+    dc.decode_async()
+    ctx.sync()
+    dc.decode_check()
+    ctx.timing(True)
+    ctx.timing_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dc.decode_async()
+    ctx.sync()
+    t1 = time.perf_counter()
+    barrier()
+    ctx.timing(False)
+    dc.decode_check()
+    el = t1 - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kern = {}
+    for name in KERNELS + ("plain_ba", "fixed_plain", "fixed"):
+        ms, n = ctx.timing_get(name)
+        if n:
+            kern[name] = ms / n
+    return {"ms_per_decode": el / steps * 1e3, "values_per_s": dc.num_rows * steps * world / el,
+            "payload_bytes": dc.payload_bytes, "kernel_ms": kern}
 
 
 def _cpu_model():
