@@ -942,9 +942,13 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     } else if (c->type == PQ_BYTE_ARRAY) {
         {
             Timed t(ctx, "ba_rows");
+            const uint32_t big = (c->max_def == 0 && c->max_rep == 0 && ctx->opt_plain) ? pqk::ba_rows_stage_bytes() : 0u;
             pqk::launch_ba_rows(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_entries,
                                 c->d_dict_count, cp, c->d_row_codes, c->d_tile_chars,
-                                c->d_page_tile0, c->d_page_err, c->d_flags);
+                                c->d_page_tile0, c->d_page_err, c->d_flags, big);
+            if (big)
+                pqk::launch_plain_big_rows(s, c->d_bytes, c->d_pages, c->npages, big, c->d_row_codes,
+                                           c->d_tile_chars, c->d_page_tile0, c->d_page_err, c->d_flags);
         }
         {
             Timed t(ctx, "scan");

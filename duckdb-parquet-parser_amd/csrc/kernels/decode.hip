@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(256) k_ba_rows(const uint8_t* __restrict__ byt
                                                  int64_t* __restrict__ tile_chars,
                                                  const int32_t* __restrict__ page_tile0,
                                                  DevErr* __restrict__ page_err,
-                                                 int32_t* __restrict__ err_any) {
+                                                 int32_t* __restrict__ err_any, uint32_t big_plain_min) {
     __shared__ RowsLds lds_all[kWavesPerBlock];
     const int wv = threadIdx.x / kWave;
     const int p = blockIdx.x * kWavesPerBlock + wv;
@@ -151,6 +151,10 @@ __global__ void __launch_bounds__(256) k_ba_rows(const uint8_t* __restrict__ byt
     DevErr* err = page_err + p;
     const uint8_t* g = bytes + pg.off;
     const uint32_t size = static_cast<uint32_t>(pg.size);
+    // REQUIRED PLAIN pages above big_plain_min: k_plain_big_rows (plain_ba.hip)
+    if (big_plain_min && cp.max_def == 0 && cp.max_rep == 0 && pg.mode == MODE_PLAIN && size > big_plain_min &&
+        pg.nvals <= 256 * kTileRows)
+        return;
     Src s{nullptr, g, size};
     if (size <= kStageWords * 4) {
         stage_page(L.stage, g, size);
@@ -652,13 +656,15 @@ void launch_dict_entries(hipStream_t s, const uint8_t* bytes, const DevDict* dic
 void launch_ba_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
                     const DevDict* dicts, const uint64_t* entries, const int32_t* dict_count,
                     ColumnParams cp, uint64_t* row_codes, int64_t* tile_chars,
-                    const int32_t* page_tile0, DevErr* page_err, int32_t* err_any) {
+                    const int32_t* page_tile0, DevErr* page_err, int32_t* err_any, uint32_t big_plain_min) {
     if (npages <= 0) return;
     int blocks = (npages + kWavesPerBlock - 1) / kWavesPerBlock;
     hipLaunchKernelGGL(k_ba_rows, dim3(blocks), dim3(256), 0, s, bytes, pages, npages, dicts,
                        entries, dict_count, cp, row_codes, tile_chars, page_tile0, page_err,
-                       err_any);
+                       err_any, big_plain_min);
 }
+
+uint32_t ba_rows_stage_bytes() { return kStageWords * 4; }
 
 void launch_scan_i64(hipStream_t s, const int64_t* in, int64_t* out_excl, int64_t n,
                      int64_t* total, int64_t* scratch) {

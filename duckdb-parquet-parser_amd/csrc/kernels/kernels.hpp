@@ -65,7 +65,8 @@ void launch_dict_entries(hipStream_t s, const uint8_t* bytes, const DevDict* dic
 void launch_ba_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
                     const DevDict* dicts, const uint64_t* entries, const int32_t* dict_count,
                     ColumnParams cp, uint64_t* row_codes, int64_t* tile_chars,
-                    const int32_t* page_tile0, DevErr* page_err, int32_t* err_any);
+                    const int32_t* page_tile0, DevErr* page_err, int32_t* err_any, uint32_t big_plain_min);
+uint32_t ba_rows_stage_bytes();
 
 void launch_scan_i64(hipStream_t s, const int64_t* in, int64_t* out_excl, int64_t n,
                      int64_t* total, int64_t* scratch);
@@ -242,6 +243,11 @@ struct PlainLaunch {
     int32_t* err_any;
 };
 int plain_write_blocks_per_cu();
+// REQUIRED PLAIN BYTE_ARRAY pages larger than min_size bytes: row codes and
+// tile characters for the generic gather (k_ba_rows skips these pages)
+void launch_plain_big_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, uint32_t min_size,
+                           uint64_t* row_codes, int64_t* tile_chars, const int32_t* page_tile0, DevErr* page_err,
+                           int32_t* err_any);
 void launch_plain_ba(hipStream_t s, PlainLaunch P);
 
 }  // namespace pqk

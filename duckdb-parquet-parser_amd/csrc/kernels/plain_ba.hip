@@ -225,6 +225,144 @@ __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
     }
 }
 
+// ── pages larger than a window (generic path) ─────────────────────────────
+// One workgroup (16 waves) per REQUIRED PLAIN page larger than the generic
+// kernel's LDS stage: 32 KiB windows of the page go to LDS; wave v walks the
+// length chain of slice v speculatively from each of its first 64 byte
+// offsets; one thread links the slices (the true chain enters slice v where
+// slice v-1 left it) and the chosen lanes emit (len << 32 | position) row
+// codes for k_ba_gather.  Entries longer than 60 bytes that straddle a slice
+// edge, the string count limit and every bounds error are handled by the
+// linking thread's exact walk (same error position and text as the
+// reference, column_reader.cpp:249-253).
+constexpr int kBigWaves = 16;
+constexpr uint32_t kBigWin = 32768;
+constexpr uint32_t kBigSlice = kBigWin / kBigWaves;
+constexpr uint32_t kBigTiles = 256;
+constexpr uint32_t kBadExit = 0xFFFFFFFFu;
+
+__global__ void __launch_bounds__(kBigWaves * 64) k_plain_big_rows(const uint8_t* __restrict__ bytes,
+                                                                  const DevPage* __restrict__ pages,
+                                                                  uint32_t min_size, uint64_t* __restrict__ row_codes,
+                                                                  int64_t* __restrict__ tile_chars,
+                                                                  const int32_t* __restrict__ page_tile0,
+                                                                  DevErr* __restrict__ page_err,
+                                                                  int32_t* __restrict__ err_any) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kBigWin / 4 + 16];
+    __shared__ uint32_t ex[kBigWaves * kWave], ec[kBigWaves * kWave];
+    __shared__ int32_t seg_lane[kBigWaves];
+    __shared__ uint32_t seg_base[kBigWaves];
+    __shared__ unsigned long long tch[kBigTiles];
+    __shared__ uint32_t sh[3];  // chain position, strings so far, stop
+    const int p = blockIdx.x;
+    const DevPage pg = pages[p];
+    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    if (pg.mode != MODE_PLAIN || size <= min_size || n > kBigTiles * kTileRows) return;  // k_ba_rows' pages
+    const uint8_t* page = bytes + pg.off;
+    uint64_t* codes = row_codes + pg.first_row;
+    const uint32_t wv = threadIdx.x / kWave;
+    for (uint32_t i = threadIdx.x; i < kBigTiles; i += blockDim.x) tch[i] = 0;
+    if (threadIdx.x == 0) { sh[0] = 0; sh[1] = 0; sh[2] = 0; }
+    for (;;) {
+        __syncthreads();
+        const uint32_t wlo = sh[0], k0 = sh[1];
+        if (sh[2] || k0 >= n) break;
+        const uint32_t ab = wlo & ~15u;  // page byte ab sits at stage byte 0
+        const uint32_t wbytes = wlo < size ? min(size - wlo, kBigWin - 16) : 0u;
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(page + ab);
+            uint4* dst = reinterpret_cast<uint4*>(stage);
+            const uint32_t nb = min((wlo - ab + wbytes + 15) / 16 + 1, kBigWin / 16 + 1);
+            for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) dst[i] = src[i];
+        }
+        __syncthreads();
+        const uint32_t wend = wlo + wbytes;
+        {
+            const uint32_t a0 = wlo + wv * kBigSlice, a1 = min(a0 + kBigSlice, wend);
+            uint32_t q = a0 + lane(), cnt = 0;
+            bool bad = q >= a1 || (wv == 0 && lane() != 0);
+            while (!bad && q < a1) {
+                if (q + 4 > size) { bad = true; break; }
+                const uint32_t x = q - ab;
+                const uint32_t len = __builtin_amdgcn_alignbyte(stage[(x >> 2) + 1], stage[x >> 2], x & 3);
+                if (static_cast<uint64_t>(q) + 4 + len > size) { bad = true; break; }
+                q += 4 + len;
+                cnt++;
+            }
+            ex[threadIdx.x] = bad ? kBadExit : q;
+            ec[threadIdx.x] = cnt;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // link the slices
+            uint32_t t = wlo, kk = k0, stop = 0;
+            for (uint32_t v = 0; v < kBigWaves; v++) {
+                seg_lane[v] = -1;
+                const uint32_t a0 = wlo + v * kBigSlice, a1 = min(a0 + kBigSlice, wend);
+                if (stop || a0 >= wend || t >= a1 || kk >= n) continue;
+                const uint32_t c = t - a0;
+                if (c < kWave && ex[v * kWave + c] != kBadExit && kk + ec[v * kWave + c] <= n) {
+                    seg_lane[v] = static_cast<int32_t>(c);
+                    seg_base[v] = kk;
+                    kk += ec[v * kWave + c];
+                    t = ex[v * kWave + c];
+                    continue;
+                }
+                while (t < a1 && kk < n) {  // exact walk
+                    if (t + 4 > size) { set_err(page_err + p, err_any, PQ_ERR_BUFFER, t, 4, size); stop = 1; break; }
+                    const uint32_t x = t - ab;
+                    const uint32_t len = __builtin_amdgcn_alignbyte(stage[(x >> 2) + 1], stage[x >> 2], x & 3);
+                    if (static_cast<uint64_t>(t) + 4 + len > size) {
+                        set_err(page_err + p, err_any, PQ_ERR_BUFFER, t + 4, len, size);
+                        stop = 1;
+                        break;
+                    }
+                    codes[kk] = (static_cast<uint64_t>(len) << 32) | (t + 4);
+                    tch[kk / kTileRows] += len;
+                    kk++;
+                    t += 4 + len;
+                }
+            }
+            // past the window with strings left: the next window starts at t
+            // (a string count reached with bytes left ends the page)
+            if (!stop && kk < n && t >= size) {
+                set_err(page_err + p, err_any, PQ_ERR_BUFFER, t, 4, size);
+                stop = 1;
+            }
+            sh[0] = t;
+            sh[1] = kk;
+            sh[2] = stop;
+        }
+        __syncthreads();
+        if (seg_lane[wv] == static_cast<int32_t>(lane())) {
+            uint32_t q = wlo + wv * kBigSlice + lane(), kk = seg_base[wv];
+            const uint32_t m = ec[threadIdx.x];
+            uint32_t tsum = 0, tcur = kk / kTileRows;
+            for (uint32_t j = 0; j < m; j++) {
+                const uint32_t x = q - ab;
+                const uint32_t len = __builtin_amdgcn_alignbyte(stage[(x >> 2) + 1], stage[x >> 2], x & 3);
+                codes[kk] = (static_cast<uint64_t>(len) << 32) | (q + 4);
+                if (kk / kTileRows != tcur) {
+                    atomicAdd(&tch[tcur], static_cast<unsigned long long>(tsum));
+                    tsum = 0;
+                    tcur = kk / kTileRows;
+                }
+                tsum += len;
+                kk++;
+                q += 4 + len;
+            }
+            if (tsum) atomicAdd(&tch[tcur], static_cast<unsigned long long>(tsum));
+        }
+    }
+    __syncthreads();
+    const bool failed = sh[2] != 0;
+    if (failed)  // rows after the error: NULL codes, nothing gathered
+        for (uint32_t j = sh[1] + threadIdx.x; j < n; j += blockDim.x) codes[j] = 0xFFFFFFFFFFFFFFFFull;
+    const int32_t t0 = page_tile0[p];
+    for (uint32_t i = threadIdx.x; i * kTileRows < n; i += blockDim.x)
+        tile_chars[t0 + static_cast<int32_t>(i)] = failed ? 0 : static_cast<int64_t>(tch[i]);
+}
+
 }  // namespace
 
 uint32_t plain_write_lds() { return kPWWaves * static_cast<uint32_t>(sizeof(PWLds)); }
@@ -245,6 +383,14 @@ int plain_write_blocks_per_cu() {
                                                      kPWWaves * kWave, lds) != hipSuccess || occ < 1)
         occ = 1;
     return occ;
+}
+
+void launch_plain_big_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, uint32_t min_size,
+                           uint64_t* row_codes, int64_t* tile_chars, const int32_t* page_tile0, DevErr* page_err,
+                           int32_t* err_any) {
+    if (npages <= 0) return;
+    hipLaunchKernelGGL(k_plain_big_rows, dim3(npages), dim3(kBigWaves * kWave), 0, s, bytes, pages, min_size,
+                       row_codes, tile_chars, page_tile0, page_err, err_any);
 }
 
 void launch_plain_ba(hipStream_t s, PlainLaunch P) {

@@ -111,6 +111,24 @@ def _dict_ba_file(idx_stream: bytes, nvals: int, dict_vals, def_stream: bytes | 
 DICT = [b"alpha", b"", b"gamma-gamma", b"d"]
 
 
+def _big_plain_file(seed, cut=None):
+    """REQUIRED PLAIN BYTE_ARRAY pages of 40-110 KB; `cut` truncates the second
+    page's payload at that many bytes (the chain runs past the page)."""
+    rng = np.random.default_rng(seed)
+    pages, total = [], 0
+    for k in range(3):
+        vals = [bytes(rng.integers(97, 123, int(rng.choice([rng.integers(0, 30), rng.integers(60, 200)]))).astype(np.uint8))
+                for _ in range(int(rng.integers(900, 1800)))]
+        if k == 1:
+            vals.insert(7, b"y" * 50000)
+        pay = B.plain_ba(vals)
+        if cut is not None and k == 1:
+            pay = pay[:cut]
+        pages.append(B.data_header(len(pay), len(vals), 0) + pay)
+        total += len(vals)
+    return B.build_file(pages, gen.BYTE_ARRAY, False, total)
+
+
 def _opt_fixed_file(ptype, fmt, nvals, seed, rle_levels=False, drop=0):
     """One OPTIONAL PLAIN fixed-width page; `drop` trailing values removed
     from the payload (the read overruns on the last non-null rows)."""
@@ -156,6 +174,9 @@ CRAFTED = {
     "plain_pages": lambda: B.build_file([B.data_header(len(B.plain_ba(v)), len(v), 0) + B.plain_ba(v) for v in
                                          ([b"a", b"", b"bcd"], [b"x" * 5000], [b"", b""], [b"tail-%d" % i for i in range(300)])],
                                         gen.BYTE_ARRAY, False, 306),
+    # PLAIN BYTE_ARRAY pages larger than every LDS window: speculative chain
+    # walk, strings longer than a slice's candidate range, a 50 KB string
+    "plain_big": lambda: _big_plain_file(seed=21),
     # multi-byte varint run header (count 300)
     "long_rle_run": lambda: _dict_ba_file(bytes([2]) + B.rle(300, 2, 2), 300, DICT),
     # def levels + nulls, RLE and bit-packed level runs
@@ -204,6 +225,8 @@ ERRORS = {
     "plain_short_page2": lambda: B.build_file([B.data_header(len(B.plain_ba([b"ok"])), 1, 0) + B.plain_ba([b"ok"]),
                                                B.data_header(len(B.plain_ba([b"abc", b"de"])), 3, 0) + B.plain_ba([b"abc", b"de"])],
                                               gen.BYTE_ARRAY, False, 4),
+    # PLAIN BYTE_ARRAY page of 60 KB whose chain overruns in its second window
+    "plain_big_overrun": lambda: _big_plain_file(seed=22, cut=40000),
     # def_len beyond the page
     "def_len_overrun": lambda: B.build_file([B.data_header(6, 3, 0) + struct.pack("<I", 50) + b"xy"], gen.INT32, True, 3),
     # dictionary page index stream without the bit-width byte
