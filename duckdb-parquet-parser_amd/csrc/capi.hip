@@ -81,6 +81,7 @@ struct pq_chunk {
     uint64_t* d_entries = nullptr;
     int64_t nentries = 0;
     uint32_t max_dict_bytes = 0;        // largest dictionary payload
+    uint32_t max_page_bytes = 0;        // largest data-page payload
     int32_t* d_dict_count = nullptr;
     DevErr* d_page_err = nullptr;
     DevErr* d_dict_err = nullptr;
@@ -652,6 +653,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
                                          std::min(pqk::kTileRows, hpages[p].nvals - r), 0});
         }
         c->ntiles = static_cast<int>(htiles.size());
+        for (const auto& pg : hpages) c->max_page_bytes = std::max<uint32_t>(c->max_page_bytes, static_cast<uint32_t>(std::max(pg.size, 0)));
         // every data page PLAIN, a fixed-width type whose bytes are copied as is
         c->fixed_plain = (c->type == PQ_INT32 || c->type == PQ_INT64 || c->type == PQ_FLOAT ||
                           c->type == PQ_DOUBLE || c->type == PQ_INT96) &&
@@ -945,7 +947,7 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             const uint32_t big = (c->max_def == 0 && c->max_rep == 0 && ctx->opt_plain) ? pqk::ba_rows_stage_bytes() : 0u;
             pqk::launch_ba_rows(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_entries,
                                 c->d_dict_count, cp, c->d_row_codes, c->d_tile_chars,
-                                c->d_page_tile0, c->d_page_err, c->d_flags, big);
+                                c->d_page_tile0, c->d_page_err, c->d_flags, big, c->max_page_bytes);
             if (big)
                 pqk::launch_plain_big_rows(s, c->d_bytes, c->d_pages, c->npages, big, c->d_row_codes,
                                            c->d_tile_chars, c->d_page_tile0, c->d_page_err, c->d_flags);

@@ -125,14 +125,18 @@ __global__ void __launch_bounds__(64) k_dict_entries(const uint8_t* __restrict__
 }
 
 // ── BYTE_ARRAY rows: every row -> (len << 32 | source offset) or NULL ──────
+template <uint32_t kSW>
 struct RowsLds {
-    uint32_t stage[kStageWords];
+    uint32_t stage[kSW];
     uint32_t lv[kTileRows];   // def levels of the current tile
     uint32_t a[kTileRows];    // dict index / plain chars offset per non-null rank
     uint32_t b[kTileRows];    // plain length per non-null rank
 };
 
-__global__ void __launch_bounds__(256) k_ba_rows(const uint8_t* __restrict__ bytes,
+// kSW: LDS stage words per wave (pages up to 4 KiB, or up to 32 KiB with one
+// wave per workgroup); kWPB: waves per workgroup.
+template <uint32_t kSW, int kWPB>
+__global__ void __launch_bounds__(kWPB * 64) k_ba_rows(const uint8_t* __restrict__ bytes,
                                                  const DevPage* __restrict__ pages, int npages,
                                                  const DevDict* __restrict__ dicts,
                                                  const uint64_t* __restrict__ entries,
@@ -142,11 +146,11 @@ __global__ void __launch_bounds__(256) k_ba_rows(const uint8_t* __restrict__ byt
                                                  const int32_t* __restrict__ page_tile0,
                                                  DevErr* __restrict__ page_err,
                                                  int32_t* __restrict__ err_any, uint32_t big_plain_min) {
-    __shared__ RowsLds lds_all[kWavesPerBlock];
+    __shared__ RowsLds<kSW> lds_all[kWPB];
     const int wv = threadIdx.x / kWave;
-    const int p = blockIdx.x * kWavesPerBlock + wv;
+    const int p = blockIdx.x * kWPB + wv;
     if (p >= npages) return;
-    RowsLds& L = lds_all[wv];
+    RowsLds<kSW>& L = lds_all[wv];
     const DevPage pg = pages[p];
     DevErr* err = page_err + p;
     const uint8_t* g = bytes + pg.off;
@@ -156,7 +160,7 @@ __global__ void __launch_bounds__(256) k_ba_rows(const uint8_t* __restrict__ byt
         pg.nvals <= 256 * kTileRows)
         return;
     Src s{nullptr, g, size};
-    if (size <= kStageWords * 4) {
+    if (size <= kSW * 4) {
         stage_page(L.stage, g, size);
         s.lds = L.stage;
     }
@@ -656,11 +660,18 @@ void launch_dict_entries(hipStream_t s, const uint8_t* bytes, const DevDict* dic
 void launch_ba_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
                     const DevDict* dicts, const uint64_t* entries, const int32_t* dict_count,
                     ColumnParams cp, uint64_t* row_codes, int64_t* tile_chars,
-                    const int32_t* page_tile0, DevErr* page_err, int32_t* err_any, uint32_t big_plain_min) {
+                    const int32_t* page_tile0, DevErr* page_err, int32_t* err_any, uint32_t big_plain_min,
+                    uint32_t max_page) {
     if (npages <= 0) return;
+    if (max_page > kStageWords * 4) {  // pages up to 32 KiB decode from LDS too
+        hipLaunchKernelGGL((k_ba_rows<8192, 1>), dim3(npages), dim3(64), 0, s, bytes, pages, npages, dicts,
+                           entries, dict_count, cp, row_codes, tile_chars, page_tile0, page_err, err_any,
+                           big_plain_min);
+        return;
+    }
     int blocks = (npages + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL(k_ba_rows, dim3(blocks), dim3(256), 0, s, bytes, pages, npages, dicts,
-                       entries, dict_count, cp, row_codes, tile_chars, page_tile0, page_err,
+    hipLaunchKernelGGL((k_ba_rows<kStageWords, kWavesPerBlock>), dim3(blocks), dim3(256), 0, s, bytes, pages,
+                       npages, dicts, entries, dict_count, cp, row_codes, tile_chars, page_tile0, page_err,
                        err_any, big_plain_min);
 }
 
