@@ -421,6 +421,7 @@ __global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__
 // strings; then all 64 lanes match the listed strings, two per lane, so two
 // DFA chains (one LDS lookup per byte each) are in flight per lane.
 constexpr uint32_t kPlainWaves = 8;
+constexpr uint32_t kStrPerLane = 4;  // strings interleaved per lane (independent DFA chains)
 
 
 __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
@@ -536,11 +537,11 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
         lbase[lane()] = pay / 4;
         const uint32_t total = bcast_last(inc);
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t g0 = 0; g0 < total; g0 += 2 * kWave) {
-            uint32_t e2[2], off2[2], len2[2], pg2[2];
-            bool ok2[2];
+        for (uint32_t g0 = 0; g0 < total; g0 += kStrPerLane * kWave) {
+            uint32_t e2[kStrPerLane], off2[kStrPerLane], len2[kStrPerLane], pg2[kStrPerLane];
+            bool ok2[kStrPerLane];
 #pragma unroll
-            for (uint32_t h = 0; h < 2; h++) {
+            for (uint32_t h = 0; h < kStrPerLane; h++) {
                 const uint32_t g = g0 + h * kWave + lane();
                 ok2[h] = g < total;
                 // first page lane whose inclusive count exceeds g
@@ -556,39 +557,46 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
                 pg2[h] = gl;
                 e2[h] = full ? (DFA_START * kDfaRowBytes) : DFA_START;
             }
-            const uint32_t maxl = max(len2[0], len2[1]);
-            for (uint32_t b0 = 0; __ballot(maxl > b0); b0 += 16) {
+            uint32_t maxl = 0;
 #pragma unroll
-                for (uint32_t h = 0; h < 2; h++) {
+            for (uint32_t h = 0; h < kStrPerLane; h++) maxl = max(maxl, len2[h]);
+            for (uint32_t b0 = 0; __ballot(maxl > b0); b0 += 16) {
+                uint32_t A[kStrPerLane][4], rem[kStrPerLane];
+#pragma unroll
+                for (uint32_t h = 0; h < kStrPerLane; h++) {
                     const uint32_t a = off2[h] + b0;
                     const uint32_t i0 = a >> 2, sh = a & 3;
                     uint32_t d[5];
 #pragma unroll
                     for (uint32_t j = 0; j < 5; j++) d[j] = stage[i0 + j];
-                    uint32_t A[4];
 #pragma unroll
-                    for (uint32_t j = 0; j < 4; j++) A[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
-                    const uint32_t rem = len2[h] > b0 ? len2[h] - b0 : 0u;
-                    uint32_t e = e2[h];
-                    if (full) {
+                    for (uint32_t j = 0; j < 4; j++) A[h][j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+                    rem[h] = len2[h] > b0 ? len2[h] - b0 : 0u;
+                }
+                // the chains advance one byte each per step, interleaved
+                if (full) {
 #pragma unroll
-                        for (uint32_t i = 0; i < 16; i++) {
-                            const uint32_t t = dfa_step_full(T, e, (A[i >> 2] >> (8 * (i & 3))) & 0xFFu);
-                            e = i < rem ? t : e;
-                        }
-                    } else {
+                    for (uint32_t i = 0; i < 16; i++) {
 #pragma unroll
-                        for (uint32_t i = 0; i < 16; i++) {
-                            const uint32_t bt = (A[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-                            const uint32_t t = T[(e & 0x7FFFu) * nc + D->cls_of[bt]];
-                            e = i < rem ? t : e;
+                        for (uint32_t h = 0; h < kStrPerLane; h++) {
+                            const uint32_t t = dfa_step_full(T, e2[h], (A[h][i >> 2] >> (8 * (i & 3))) & 0xFFu);
+                            e2[h] = i < rem[h] ? t : e2[h];
                         }
                     }
-                    e2[h] = e;
+                } else {
+#pragma unroll
+                    for (uint32_t i = 0; i < 16; i++) {
+#pragma unroll
+                        for (uint32_t h = 0; h < kStrPerLane; h++) {
+                            const uint32_t bt = (A[h][i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                            const uint32_t t = T[(e2[h] & 0x7FFFu) * nc + D->cls_of[bt]];
+                            e2[h] = i < rem[h] ? t : e2[h];
+                        }
+                    }
                 }
             }
 #pragma unroll
-            for (uint32_t h = 0; h < 2; h++) {
+            for (uint32_t h = 0; h < kStrPerLane; h++) {
                 const uint32_t e = e2[h];
                 const uint32_t st = full ? (e & 0x7FFFu) / kDfaRowBytes : (e & 0x7FFFu);
                 const bool m = len2[h] == 0 ? empty_ok : (trivial || st == DFA_ACCEPT || (e >> 15) != 0);
