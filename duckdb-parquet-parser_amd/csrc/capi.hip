@@ -7,7 +7,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <map>
 #include <memory>
 #include <string>
@@ -151,6 +153,23 @@ struct pq_chunk {
 };
 
 namespace {
+
+// fn(0 .. n-1) on up to hardware_concurrency host threads (inline when n == 1).
+template <class Fn>
+void parallel_for(int n, Fn&& fn) {
+    if (n <= 1) {
+        if (n == 1) fn(0);
+        return;
+    }
+    const int nt = std::max(1, std::min<int>(n, static_cast<int>(std::thread::hardware_concurrency())));
+    std::atomic<int> next{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+        th.emplace_back([&]() {
+            for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) fn(i);
+        });
+    for (auto& x : th) x.join();
+}
 
 template <class T>
 int dalloc(T** p, size_t n) {
@@ -578,8 +597,11 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             img += (static_cast<int64_t>(size) + 15) / 16 * 16 + 16;
             return at;
         };
+        // the chunks' page walks are independent: host threads
+        std::vector<pqfmt::WalkResult> walks(static_cast<size_t>(nchunks));
+        parallel_for(nchunks, [&](int k) { walks[static_cast<size_t>(k)] = pqfmt::walk_chunk(file, file_len, chunks[k]); });
         for (int k = 0; k < nchunks; k++) {
-            pqfmt::WalkResult w = pqfmt::walk_chunk(file, file_len, chunks[k]);
+            pqfmt::WalkResult& w = walks[static_cast<size_t>(k)];
             int64_t base_walk = static_cast<int64_t>(c->walked.size());
             std::vector<int32_t> dict_of_walk(w.pages.size(), -1);
             pq_chunk::Range rg;
@@ -709,10 +731,17 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (chunk upload)");
         }
         std::vector<uint8_t> image(c->nbytes, 0);
-        for (size_t i = 0; i < copies.size(); i++) {  // zero padding past EOF
-            int64_t lo = copies[i].first, n = copy_size[i];
-            int64_t hi = std::min<int64_t>(lo + n, static_cast<int64_t>(file_len));
-            if (hi > lo) std::memcpy(image.data() + copies[i].second, file + lo, static_cast<size_t>(hi - lo));
+        {  // payloads into their slots (zero padding past EOF), split over host threads
+            const int parts = copies.size() > 4096 ? 16 : 1;
+            parallel_for(parts, [&](int part) {
+                const size_t a = copies.size() * static_cast<size_t>(part) / parts;
+                const size_t b = copies.size() * static_cast<size_t>(part + 1) / parts;
+                for (size_t i = a; i < b; i++) {
+                    int64_t lo = copies[i].first, n = copy_size[i];
+                    int64_t hi = std::min<int64_t>(lo + n, static_cast<int64_t>(file_len));
+                    if (hi > lo) std::memcpy(image.data() + copies[i].second, file + lo, static_cast<size_t>(hi - lo));
+                }
+            });
         }
         hipStream_t s = ctx->stream;
         rc = hip_check(ctx, hipMemcpyAsync(c->d_bytes, image.data(), c->nbytes, hipMemcpyHostToDevice, s), "upload");
