@@ -452,7 +452,7 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane i <- lane i
     return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x138, 0xf, 0xf, true));
 }
 
-__global__ void __launch_bounds__(kCodeWaves2 * 64, 3) k_pipe_codes2(CodeArgs a, uint32_t lt_n) {
+__global__ void __launch_bounds__(kCodeWaves2 * 64) k_pipe_codes2(CodeArgs a, uint32_t lt_n) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lens[];
     __shared__ CodeLds2 lds_all[kCodeWaves2];
     const int wv = static_cast<int>(threadIdx.x / kWave);
