@@ -102,6 +102,10 @@ struct pq_chunk {
     int32_t* d_tile_nn = nullptr;
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
+    bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
+    std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
+    int32_t* d_bigp = nullptr;
+    uint32_t big_max_bytes = 0;
     // PLAIN BYTE_ARRAY, REQUIRED (plain_ba.hip)
     bool plain = false;
     std::vector<pqk::DevBatch> hpwins;
@@ -279,6 +283,7 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_tile_nn);
     dfree(c->d_bsum);
     dfree(c->d_flist);
+    dfree(c->d_bigp);
     dfree(c->d_page_pos);
     dfree(c->d_tile_base);
     dfree(c->d_total);
@@ -299,16 +304,30 @@ void free_chunk_device(pq_chunk* c) {
 void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, const std::vector<DevDict>& dicts) {
     c->pipe = false;
     c->pipe_count = false;
+    c->pipe_small = false;
+    c->hbig.clear();
+    c->big_max_bytes = 0;
     if (c->type != PQ_BYTE_ARRAY || c->max_def > 254 || c->max_def < 0 || c->max_rep < 0 || pages.empty()) return;
     int32_t dict_id = -1;
-    bool multi = false;
-    for (const auto& pg : pages) {
-        // pages of up to 2048 rows (the run table holds kPipeRunCap runs per stream)
-        if (pg.mode != pqk::MODE_DICT || pg.nvals > 2048 || pg.size > (1 << 27)) return;
+    bool multi = false, small = false;
+    std::vector<int32_t> big;
+    uint32_t big_bytes = 0;
+    for (size_t i = 0; i < pages.size(); i++) {
+        const DevPage& pg = pages[i];
+        if (pg.mode != pqk::MODE_DICT || pg.size > (1 << 27) || pg.size < 0) return;
+        if (pg.nvals > pqk::kPipeSmallRows) {
+            // k_pipe_big: the page's jump table and up to kBigTiles tiles in one workgroup
+            if (pg.nvals > pqk::kBigTiles * pqk::kTileRows || static_cast<uint32_t>(pg.size) > pqk::kBigMaxBytes) return;
+            big.push_back(static_cast<int32_t>(i));
+            big_bytes = std::max(big_bytes, static_cast<uint32_t>(pg.size));
+        } else {
+            small = true;
+            multi |= pg.nvals > pqk::kTileRows;
+        }
         if (dict_id >= 0 && pg.dict != dict_id) return;
         dict_id = pg.dict;
-        multi |= pg.nvals > pqk::kTileRows;
     }
+    if (!big.empty() && pqk::pipe_big_lds(big_bytes) > 160u * 1024) return;
     const DevDict& d = dicts[dict_id];
     if (d.size < 0 || d.size > 65536 - 64 || d.nvals < 0 || d.nvals > 65535) return;
     const int64_t ecap = std::min<int64_t>(d.nvals, d.size / 4 + 1);
@@ -320,7 +339,10 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
     c->pipe = true;
+    c->pipe_small = small;
     c->pipe_count = multi && c->max_def > 0;
+    c->hbig = std::move(big);
+    c->big_max_bytes = big_bytes;
     c->pipe_dict = dict_id;
     c->pipe_dict_chars_bytes = chars_bytes;
     c->pipe_dict_bytes = dict_bytes;
@@ -710,6 +732,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc |= dalloc(&c->d_tile_nn, htiles.size());
             rc |= dalloc(&c->d_bsum, static_cast<size_t>(c->pipe_grid));
             rc |= dalloc(&c->d_flist, hpages.size() + 1);
+            if (!c->hbig.empty()) rc |= dalloc(&c->d_bigp, c->hbig.size());
         }
         if (c->plain) {
             rc |= dalloc(&c->d_pwins, c->hpwins.size());
@@ -755,6 +778,8 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc = hip_check(ctx, hipMemcpyAsync(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc) (void)hipMemsetAsync(c->d_page_err, 0, std::max<size_t>(hpages.size(), 1) * sizeof(DevErr), s);
         if (!rc) (void)hipMemsetAsync(c->d_dict_err, 0, std::max<size_t>(hdicts.size(), 1) * sizeof(DevErr), s);
+        if (!rc && c->d_bigp)
+            rc = hip_check(ctx, hipMemcpyAsync(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc && c->d_pwins)
             rc = hip_check(ctx, hipMemcpyAsync(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice, s), "upload");
         if (!rc && c->d_batches)
@@ -903,15 +928,19 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         P.cus = c->pipe_cus;
         {
             Timed t(ctx, "pipe_runs");
-            pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->npages, c->max_def, c->max_rep, c->d_runs, c->d_info,
-                                  ctx->opt_run_pages, c->d_flist);
+            pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
+                                  c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist);
         }
         if (c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
+        (void)hipMemsetAsync(c->d_bsum, 0, static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long), s);
+        if (!c->hbig.empty()) {
+            Timed t(ctx, "pipe_big");
+            pqk::launch_pipe_big(s, P, c->d_bigp, static_cast<int>(c->hbig.size()), c->big_max_bytes);
+        }
         if (c->pipe_count) {
             Timed t(ctx, "pipe_count");
             pqk::launch_pipe_codes(s, P, true);
         }
-        (void)hipMemsetAsync(c->d_bsum, 0, static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long), s);
         {
             Timed t(ctx, "pipe_codes");
             pqk::launch_pipe_codes(s, P, false);

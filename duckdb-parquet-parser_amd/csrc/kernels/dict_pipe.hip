@@ -39,6 +39,8 @@ constexpr int kRunWaves = 4;
 constexpr int kRunPages = 32;                 // max pages per wavefront (2 streams each)
 constexpr uint32_t kRunStage = 16384;         // staged payload bytes per wavefront
 constexpr uint32_t kFallback = 1u << 31;      // info flag: exact serial decode
+constexpr uint32_t kBig = 1u << 30;           // info flag: k_pipe_big wrote the page's codes
+constexpr uint32_t kSkip = kFallback | kBig;  // k_pipe_codes2 leaves the page alone
 constexpr int kCodeWaves = 4;
 constexpr uint16_t kNull = 0xFFFFu;
 constexpr int kWriteWaves = 6;
@@ -88,7 +90,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
 
     const uint32_t s = lane() & 1;
     const int p = g0 + static_cast<int>(lane() >> 1);
-    const bool act = p < g1 && static_cast<int>(lane() >> 1) < ppw;
+    const bool act = p < g1 && static_cast<int>(lane() >> 1) < ppw && pages[p].nvals <= kPipeSmallRows;
     uint32_t flag = 0, nrec = 0, bwi = 0;
     RunWalk W{};
     if (act) {
@@ -326,6 +328,7 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_codes(CodeArgs a) {
     const uint32_t inf = a.info[p];
     const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
     const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    if (inf & kBig) return;
     if (inf & kFallback) {
         if (!kCount && T.row0 == 0) exact_page(a, L, p, dict_n, ebase);
         return;
@@ -499,14 +502,14 @@ __global__ void __launch_bounds__(kCodeWaves2 * 64) k_pipe_codes2(CodeArgs a, ui
             const uint32_t pp = __builtin_amdgcn_readlane(myp, i);
             const uint32_t sz = __builtin_amdgcn_readlane(mysize, i);
             const uint64_t off = rl64(myoff, i);
-            const uint32_t nd = (inf & kFallback) ? 0u : (inf & 0xFFu), ni = (inf & kFallback) ? 0u : ((inf >> 8) & 0xFFu);
+            const uint32_t nd = (inf & kSkip) ? 0u : (inf & 0xFFu), ni = (inf & kSkip) ? 0u : ((inf >> 8) & 0xFFu);
             const uint2* rd_ = a.runs + static_cast<size_t>(pp) * 2 * kPipeRunCap;
             const uint2 z = make_uint2(0u, 0u);
             rq0 = lane() < nd ? rd_[lane()] : z;
             rq1 = lane() + kWave < nd ? rd_[lane() + kWave] : z;
             rq2 = lane() < ni ? rd_[kPipeRunCap + lane()] : z;
             rq3 = lane() + kWave < ni ? rd_[kPipeRunCap + lane() + kWave] : z;
-            const uint32_t nb = (inf & kFallback) || sz + 16 > kCodeStage ? 0u : (sz + 15) / 16 + 1;
+            const uint32_t nb = (inf & kSkip) || sz + 16 > kCodeStage ? 0u : (sz + 15) / 16 + 1;
             const uint4* src = reinterpret_cast<const uint4*>(a.bytes + off);
             const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
             sq0 = lane() < nb ? src[lane()] : z4;
@@ -531,7 +534,7 @@ __global__ void __launch_bounds__(kCodeWaves2 * 64) k_pipe_codes2(CodeArgs a, ui
             reinterpret_cast<uint4*>(L2.stage)[lane() + kWave] = sq1;
             if (lane() + 2 * kWave < (kCodeStage / 4 + 4) / 4) reinterpret_cast<uint4*>(L2.stage)[lane() + 2 * kWave] = sq2;
             if (i + 1 < cn) prefetch(i + 1);
-            if (inf & kFallback) continue;  // k_pipe_exact
+            if (inf & kSkip) continue;  // k_pipe_exact / k_pipe_big
             if (a.debug & 512) {  // timing: loads and the tile loop only
                 if (lane() == 0) a.tile_chars[t] = 0;
                 continue;
@@ -1006,7 +1009,382 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
     }
 }
 
+// ── pages of more than kPipeSmallRows rows (arrow layout) ──────────────────
+// One workgroup per page.  A stream of ~1-2k runs is too long for the lane
+// walk above, so its run headers are found by a speculative parse instead:
+//   1. every byte position j of both streams is parsed as if a run header
+//      started there (rle_decoder.hpp:36-50, 76-95): next header position
+//      and value count, one u32 per byte in LDS (kBStop: bad header or the
+//      stream end is reached);
+//   2. kBJumpLog pointer-doubling rounds turn that into kBJump-run jumps;
+//   3. one lane per stream follows the jumps from the stream start, listing
+//      every kBJump-th header of the real chain (a few hundred dependent LDS
+//      reads instead of a few thousand parses);
+//   4. one lane per listed header re-parses its kBJump runs exactly (the same
+//      step as walk_runs) into the run records, which replace the jump table;
+//   5. the page's 512-row tiles: def levels (one wave per tile), a scan of the
+//      tiles' non-null counts, then dictionary indices and codes, as
+//      k_pipe_codes2 does with the tile's records found by binary search.
+// Anything outside the fast shape (bad headers, record overflow, levels above
+// max_def) marks the page for k_pipe_exact.
+constexpr int kBigWaves = 16;
+constexpr int kBigThreads = kBigWaves * kWave;
+constexpr uint32_t kBStop = 0xFFFFu;
+constexpr int kBJumpLog = 3;
+constexpr uint32_t kBJump = 1u << kBJumpLog;
+constexpr uint32_t kBigPerThread = kBigMaxBytes / kBigThreads;  // jump-table slots per thread
+static_assert(kBigMaxBytes % kBigThreads == 0, "jump table split");
+
+struct BigLayout {  // dynamic LDS of k_pipe_big for a page of `size` payload bytes
+    uint32_t P, LC, tab, list, mark, tvb, misc, total;
+};
+__host__ __device__ inline BigLayout big_layout(uint32_t size) {
+    BigLayout L{};
+    L.P = (size + 16 + 15) / 16 * 16;           // positions (u32 each; later P / 2 run records)
+    L.LC = L.P / 16 + 8;                        // listed headers per stream
+    L.tab = 0;
+    L.list = L.tab + 4 * L.P;
+    L.mark = L.list + 8 * L.LC;                 // per wave: u16 run index per row of a tile
+    L.tvb = L.mark + kBigWaves * kTileRows * 2; // per tile: validity bits of rows 8l .. 8l + 7
+    L.misc = L.tvb + kBigTiles * kWave;         // tile non-null counts, first ranks, flags
+    L.total = L.misc + 4 * (2 * kBigTiles + 16);
+    return L;
+}
+
+// Exact run steps from header position q with `cnt` values before it: the
+// walk_runs step restated for one lane over the page in HBM.  Emits at most
+// `steps` records at out[0 ..); returns the records written, or ~0u on a
+// header outside the fast shape or a full record table.
+__device__ uint32_t big_fill(const uint8_t* page, uint32_t q, uint32_t cnt, uint32_t end, uint32_t bw, uint32_t n,
+                             uint2* out, uint32_t room, uint32_t steps) {
+    const uint32_t nbv = (bw + 7) / 8;
+    const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+    const uint32_t litpay = bw ? 0x80000000u : 0u;
+    const uint32_t litmul = bw ? 8u : 0u;
+    uint32_t nr = 0;
+    for (uint32_t s = 0; s < steps && cnt < n; s++) {
+        const uint32_t left = n - cnt;
+        if (nr >= room) return ~0u;
+        if (q >= end) {  // exhausted: the rest of the batch is 0 (rle_decoder.hpp:20-23)
+            out[nr++] = make_uint2(cnt | (left << 16), 0u);
+            break;
+        }
+        const uint64_t x = gld8(page, q);
+        const uint32_t x0 = static_cast<uint32_t>(x), x1 = static_cast<uint32_t>(x >> 32);
+        const uint32_t st0 = ~x0 & 0x80808080u;
+        const uint32_t hl = st0 ? (__builtin_ctz(st0) >> 3) + 1 : ((~x1 & 0x80u) ? 5u : 9u);
+        const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
+        const uint32_t x0m = x0 & lm;
+        const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
+        const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
+                             ((x0m >> 3) & 0xFE00000u) | top;
+        const uint32_t g = ind >> 1, lit = ind & 1u, qh = q + hl;
+        if (hl > 5 || qh > end || g == 0 || (!lit && qh + nbv > end)) return ~0u;
+        const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, hl);
+        const uint32_t vb = x1 >> (8 * ((hl - 4) & 3));
+        const uint32_t vraw = (hl < 4) ? va : vb;
+        const uint32_t c = lit ? ((g >= (left + 7) / 8) ? left : g * 8) : min(g, left);
+        out[nr++] = make_uint2(cnt | (c << 16), lit ? (litpay | (qh * litmul)) : (vraw & vmask));
+        const uint64_t nql = static_cast<uint64_t>(qh) + static_cast<uint64_t>(g) * bw;
+        q = lit ? (nql > end ? end : static_cast<uint32_t>(nql)) : qh + nbv;
+        cnt += c;
+    }
+    return nr;
+}
+
+// Largest k < nr with start(rec[k]) <= v (rec[0] starts at 0); wave-uniform.
+__device__ __forceinline__ uint32_t big_search(const uint2* rec, uint32_t nr, uint32_t v) {
+    uint32_t lo = 0, hi = nr;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rr_start(rec[mid]) <= v) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Per lane: the record index (relative to k0) of values v0 + 8l .. v0 + 8l + 7,
+// from marks m[v - v0] = record index - k0 at each record start.
+__device__ __forceinline__ void big_runs8(const uint16_t* mark, uint32_t l8, uint32_t m, uint32_t rm[8]) {
+    uint4 mk = make_uint4(0u, 0u, 0u, 0u);
+    if (l8 < m) mk = *reinterpret_cast<const uint4*>(mark + l8);
+    const uint32_t w[4] = {mk.x, mk.y, mk.z, mk.w};
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        run = max(run, (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+        rm[k] = run;
+    }
+    const uint32_t ex = wave_shr1(wave_incl_max(run));
+#pragma unroll
+    for (int k = 0; k < 8; k++) rm[k] = max(ex, rm[k]);
+}
+
+// Marks the starts of records k0 + 1 .. that begin inside [v0, v0 + m).
+__device__ __forceinline__ void big_mark(uint16_t* mark, const uint2* rec, uint32_t nr, uint32_t k0, uint32_t v0,
+                                         uint32_t m) {
+    const uint32_t l8 = lane() * 8;
+    if (l8 < m) *reinterpret_cast<uint4*>(mark + l8) = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    for (uint32_t kb = k0 + 1;; kb += kWave) {
+        const uint32_t k = kb + lane();
+        const uint32_t st = k < nr ? rr_start(rec[k]) : 0xFFFFFFFFu;
+        const bool in = k < nr && st < v0 + m;
+        if (in) mark[st - v0] = static_cast<uint16_t>(k - k0);
+        if (!__ballot(in)) break;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int32_t* __restrict__ bigp,
+                                                          int32_t* __restrict__ flist, uint32_t* __restrict__ info) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int p = bigp[blockIdx.x];
+    const DevPage pg = a.pages[p];
+    const uint8_t* page = a.bytes + pg.off;
+    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    const BigLayout Ly = big_layout(size);
+    uint32_t* tab = reinterpret_cast<uint32_t*>(smem + Ly.tab);
+    uint32_t* list = reinterpret_cast<uint32_t*>(smem + Ly.list);
+    uint8_t* tvb = smem + Ly.tvb;
+    uint32_t* misc = reinterpret_cast<uint32_t*>(smem + Ly.misc);
+    uint32_t* tnn = misc;                 // [kBigTiles]
+    uint32_t* tk0 = misc + kBigTiles;     // [kBigTiles]
+    uint32_t* sh = misc + 2 * kBigTiles;  // [0] flag, [1] def list, [2] idx list, [3] def records, [4] idx records
+    const uint32_t tid = threadIdx.x, wv = tid / kWave;
+    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
+    const uint32_t ntp = (n + kTileRows - 1) / kTileRows;
+
+    // prologue (column_reader.cpp:146-182), wave-uniform; any error -> k_pipe_exact
+    bool flag = n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes;
+    uint32_t pos = 0, dbase = 0, dlen = 0, bwi = 0;
+    if (!flag && a.max_def > 0) {
+        if (size < 4) flag = true;
+        else {
+            dlen = static_cast<uint32_t>(gld8(page, 0));
+            pos = 4;
+            if (static_cast<uint64_t>(pos) + dlen > size) flag = true;
+            else { dbase = 4; pos += dlen; }
+        }
+    }
+    if (!flag && a.max_rep > 0) {
+        if (pos + 4 > size) flag = true;
+        else {
+            const uint32_t rl = static_cast<uint32_t>(gld8(page, pos));
+            pos += 4;
+            if (static_cast<uint64_t>(pos) + rl > size) flag = true;
+            else pos += rl;
+        }
+    }
+    if (!flag) {
+        if (pos + 1 > size) flag = true;
+        else { bwi = static_cast<uint32_t>(gld8(page, pos)) & 0xFFu; pos += 1; }
+    }
+    if (!flag && bwi > 16) flag = true;
+    auto to_exact = [&]() {
+        if (tid == 0) {
+            info[p] = kFallback;
+            flist[1 + atomicAdd(flist, 1)] = p;
+        }
+    };
+    if (flag) return to_exact();
+    const bool hasd = a.max_def > 0;
+    const uint32_t dend = dbase + dlen, ibase = pos, iend = size;
+
+    // 1. speculative headers at every byte of both streams
+    for (uint32_t j = tid; j < size; j += kBigThreads) {
+        const bool ind_ = j >= ibase;
+        const bool ind_d = hasd && j >= dbase && j < dend;
+        if (!ind_ && !ind_d) continue;
+        const uint32_t e = ind_ ? iend : dend, bw = ind_ ? bwi : bwd, nbv = (bw + 7) / 8;
+        const uint64_t x = gld8(page, j);
+        const uint32_t x0 = static_cast<uint32_t>(x), x1 = static_cast<uint32_t>(x >> 32);
+        const uint32_t st0 = ~x0 & 0x80808080u;
+        const uint32_t hl = st0 ? (__builtin_ctz(st0) >> 3) + 1 : ((~x1 & 0x80u) ? 5u : 9u);
+        const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
+        const uint32_t x0m = x0 & lm;
+        const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
+        const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
+                             ((x0m >> 3) & 0xFE00000u) | top;
+        const uint32_t g = ind >> 1, lit = ind & 1u, qh = j + hl;
+        const bool bad = hl > 5 || qh > e || g == 0 || (!lit && qh + nbv > e);
+        const uint64_t nx = lit ? static_cast<uint64_t>(qh) + static_cast<uint64_t>(g) * bw : qh + nbv;
+        const uint32_t c = min(lit ? (g > 8191u ? 65535u : g * 8u) : g, 65535u);
+        tab[j] = ((bad || nx >= e) ? kBStop : static_cast<uint32_t>(nx)) | (c << 16);
+    }
+    __syncthreads();
+    // 2. kBJump-run jumps by pointer doubling (counts saturate at 65535)
+    for (int r = 0; r < kBJumpLog; r++) {
+        uint32_t nv[kBigPerThread];
+#pragma unroll
+        for (uint32_t i = 0; i < kBigPerThread; i++) {
+            const uint32_t j = tid + i * kBigThreads;
+            nv[i] = 0;
+            if (j < size && ((j >= ibase) || (hasd && j >= dbase && j < dend))) {
+                const uint32_t t = tab[j];
+                nv[i] = t;
+                if ((t & 0xFFFFu) != kBStop) {
+                    const uint32_t u = tab[t & 0xFFFFu];
+                    nv[i] = (u & 0xFFFFu) | (min((t >> 16) + (u >> 16), 65535u) << 16);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t i = 0; i < kBigPerThread; i++) {
+            const uint32_t j = tid + i * kBigThreads;
+            if (j < size && ((j >= ibase) || (hasd && j >= dbase && j < dend))) tab[j] = nv[i];
+        }
+        __syncthreads();
+    }
+    // 3. one lane per stream follows the jumps: every kBJump-th header, with
+    //    the values before it
+    const uint32_t rcap = Ly.P / 2;                           // records in the table's space
+    const uint32_t rcap_d = hasd ? min(rcap / 2, dlen / 2 + 2 * kBJump + 2) : 0u;
+    const uint32_t rcap_i = rcap - rcap_d;
+    if (tid == 0 || tid == kWave) {
+        const bool isd = tid == 0;
+        uint32_t k = 0;
+        if (!isd || hasd) {
+            const uint32_t e = isd ? dend : iend;
+            uint32_t q = isd ? dbase : ibase, c = 0;
+            uint32_t* L = list + (isd ? 0u : Ly.LC);
+            const uint32_t lcap = min(Ly.LC, (isd ? rcap_d : rcap_i) / kBJump);
+            for (;;) {
+                if (k >= lcap) { k = ~0u; break; }
+                L[k++] = q | (c << 16);
+                if (q >= e) break;
+                const uint32_t t = tab[q];
+                if ((t & 0xFFFFu) == kBStop) break;
+                c += t >> 16;
+                if (c >= n) break;
+                q = t & 0xFFFFu;
+            }
+        }
+        sh[isd ? 1 : 2] = k;
+    }
+    if (tid == 0) sh[0] = 0;
+    __syncthreads();
+    const uint32_t nld = sh[1], nli = sh[2];
+    if (nld == ~0u || nli == ~0u) return to_exact();
+    // 4. exact records, kBJump runs per listed header (the jump table is dead)
+    uint2* recd = reinterpret_cast<uint2*>(smem + Ly.tab);
+    uint2* reci = recd + rcap_d;
+    for (uint32_t i = tid; i < nld + nli; i += kBigThreads) {
+        const bool isd = i < nld;
+        const uint32_t li = isd ? i : i - nld, nl = isd ? nld : nli;
+        const uint32_t e = list[(isd ? 0u : Ly.LC) + li];
+        const bool last = li + 1 == nl;
+        uint2* out = (isd ? recd : reci) + li * kBJump;
+        const uint32_t room = (isd ? rcap_d : rcap_i) - li * kBJump;
+        const uint32_t r = big_fill(page, e & 0xFFFFu, e >> 16, isd ? dend : iend, isd ? bwd : bwi, n, out, room,
+                                    last ? kBJump + 1 : kBJump);
+        if (r == ~0u || (!last && r != kBJump)) atomicOr(&sh[0], 1u);
+        else if (last) sh[isd ? 3 : 4] = li * kBJump + r;
+    }
+    __syncthreads();
+    if (sh[0]) return to_exact();
+    const uint32_t nd = hasd ? sh[3] : 0u, ni = sh[4];
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    const int32_t t0 = a.page_tile0[p];
+    const int64_t first_row = pg.first_row;
+    uint16_t* mark = reinterpret_cast<uint16_t*>(smem + Ly.mark) + wv * kTileRows;
+    const uint32_t l8 = lane() * 8;
+
+    // 5a. def levels per tile -> validity bits, non-null counts
+    for (uint32_t ti = wv; ti < ntp; ti += kBigWaves) {
+        const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
+        uint32_t vb = 0;
+        bool above = false;
+        if (hasd) {
+            const uint32_t rd0 = big_search(recd, nd, r0);
+            big_mark(mark, recd, nd, rd0, r0, m);
+            uint32_t rm[8];
+            big_runs8(mark, l8, m, rm);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t j = l8 + k;
+                const uint2 R = recd[rd0 + rm[k]];
+                uint32_t lvl = rr_pay(R);
+                if (rr_lit(R) && j < m)
+                    lvl = gbits(page, size, rr_pay(R) + static_cast<uint64_t>(r0 + j - rr_start(R)) * bwd, bwd);
+                vb |= (j < m && lvl == md ? 1u : 0u) << k;
+                above |= j < m && lvl > md;
+            }
+        } else {
+            vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
+        }
+        if (__ballot(above)) atomicOr(&sh[0], 1u);  // levels above max_def: outside the fast shape
+        tvb[ti * kWave + lane()] = static_cast<uint8_t>(vb);
+        const uint32_t nn = bcast_last(wave_incl_scan(__popc(vb)));
+        if (lane() == 0) tnn[ti] = nn;
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    if (sh[0]) return to_exact();
+    if (wv == 0) {  // first rank of each tile (ntp <= 64)
+        const uint32_t v = lane() < ntp ? tnn[lane()] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        if (lane() < ntp) tk0[lane()] = inc - v;
+    }
+    if (tid == 0) info[p] = kBig;
+    __syncthreads();
+    // 5b. dictionary indices of each tile's ranks -> codes, tile characters
+    for (uint32_t ti = wv; ti < ntp; ti += kBigWaves) {
+        const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
+        const uint32_t vb = tvb[ti * kWave + lane()];
+        const uint32_t nnl = __popc(vb);
+        const uint32_t rbase = wave_incl_scan(nnl) - nnl;
+        const uint32_t nn = tnn[ti], k0 = tk0[ti];
+        uint32_t ri0 = 0, rm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (nn) {
+            ri0 = big_search(reci, ni, k0);
+            big_mark(mark, reci, ni, ri0, k0, nn);
+            big_runs8(mark, l8, nn, rm);
+            // rank -> record, held per rank: lane l has ranks 8l .. 8l + 7
+            __builtin_amdgcn_wave_barrier();
+            if (l8 < nn) {
+                uint4 w;
+                w.x = rm[0] | (rm[1] << 16);
+                w.y = rm[2] | (rm[3] << 16);
+                w.z = rm[4] | (rm[5] << 16);
+                w.w = rm[6] | (rm[7] << 16);
+                *reinterpret_cast<uint4*>(mark + l8) = w;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        uint32_t chars = 0;
+        const int64_t R0 = first_row + r0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t j = l8 + k;
+            uint32_t code = kNull;
+            if ((vb >> k) & 1u) {
+                const uint32_t rk = rbase + __popc(vb & ((1u << k) - 1u));
+                const uint2 R = reci[ri0 + mark[rk]];
+                uint32_t v = rr_pay(R);
+                if (rr_lit(R)) v = gbits(page, size, rr_pay(R) + static_cast<uint64_t>(k0 + rk - rr_start(R)) * bwi, bwi);
+                if (v < dict_n) {
+                    code = v;
+                    chars += static_cast<uint32_t>(a.entries[ebase + v] >> 32);
+                }
+            }
+            if (j < m) a.codes[R0 + j] = static_cast<uint16_t>(code);
+        }
+        chars = wave_sum(chars);
+        tile_done(a, t0 + static_cast<int>(ti), chars);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 }  // namespace
+
+uint32_t pipe_big_lds(uint32_t max_page_bytes) { return big_layout(max_page_bytes).total; }
 
 PipePlan plan_pipe_lds(uint32_t dict_bytes) {
     PipePlan pl{};
@@ -1092,6 +1470,24 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
                 P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug};
     hipLaunchKernelGGL(k_pipe_write, dim3(grid), dim3(kWriteWaves * kWave), P.lds, s, a);
+}
+
+void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes) {
+    if (nbig <= 0) return;
+    int wgrid = 0, per = 0;
+    write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_write's workgroups
+    CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
+               P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
+               P.bsum, per, P.debug};
+    const uint32_t lds = big_layout(max_page_bytes).total;
+    static uint32_t attr = 0;
+    if (lds > attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_big),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+        attr = lds;
+    }
+    hipLaunchKernelGGL(k_pipe_big, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
+                       const_cast<int32_t*>(P.flist), const_cast<uint32_t*>(P.info));
 }
 
 }  // namespace pqk

@@ -85,6 +85,9 @@ void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int
 
 // ── three-pass dictionary BYTE_ARRAY path (dict_pipe.hip) ──────────────────
 constexpr uint32_t kPipeRunCap = 128;  // run records per stream per page
+constexpr int32_t kPipeSmallRows = 2048;   // larger pages take k_pipe_big (one workgroup per page)
+constexpr uint32_t kBigMaxBytes = 28672;   // k_pipe_big: payload bytes per page (jump table in LDS)
+constexpr int32_t kBigTiles = 64;          // k_pipe_big: 512-row tiles per page
 
 struct PipeLaunch {
     const uint8_t* bytes;
@@ -129,6 +132,10 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist);
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
+// pages of more than kPipeSmallRows rows: run tables by speculative parse,
+// then codes and tile characters (one workgroup per listed page)
+uint32_t pipe_big_lds(uint32_t max_page_bytes);
+void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes);
 
 // ── tile-parallel PLAIN fixed-width path (fixed_fast.hip) ──────────────────
 void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,

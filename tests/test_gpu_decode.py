@@ -108,6 +108,48 @@ def _dict_ba_file(idx_stream: bytes, nvals: int, dict_vals, def_stream: bytes | 
         0 for _ in extra_pages), dict_at_start=True)
 
 
+def _hybrid(values, bw, rng, max_groups=63):
+    """A hybrid RLE/bit-packed stream of `values`: RLE runs for repeats of 8
+    or more, bit-packed groups (1..max_groups per run) otherwise."""
+    out, i, n = [], 0, len(values)
+    while i < n:
+        j = i
+        while j < n and values[j] == values[i]:
+            j += 1
+        if j - i >= 8:
+            out.append(B.rle(j - i, values[i], bw))
+            i = j
+            continue
+        g = int(rng.integers(1, max_groups + 1))
+        chunk = values[i:i + 8 * g]
+        out.append(B.bitpack(chunk, bw))
+        i += len(chunk)
+    return b"".join(out)
+
+
+def _big_dict_file(nvals, seed, optional=True, bw=3, dict_vals=None, tail=b"", cut=0, max_groups=63, run=12):
+    """One dictionary page and one data page of `nvals` > kPipeSmallRows rows
+    (the k_pipe_big path): runs of repeated indices, some out of range, 10%
+    NULL; `tail` is appended to the index stream, `cut` bytes removed."""
+    rng = np.random.default_rng(seed)
+    dv = dict_vals if dict_vals is not None else [b"v%d-" % i * (1 + i % 3) for i in range((1 << bw) - 2)]
+    idx = []
+    while len(idx) < nvals:
+        idx += [int(rng.integers(0, 1 << bw))] * int(rng.integers(1, run))
+    idx = idx[:nvals]
+    defs = None
+    if optional:
+        defs = [int(x) for x in rng.random(nvals) > 0.1]
+        for k in range(0, nvals, 997):  # long valid stretches: RLE level runs
+            defs[k:k + 40] = [1] * len(defs[k:k + 40])
+        idx = [v for v, d in zip(idx, defs) if d]
+    stream = bytes([bw]) + _hybrid(idx, bw, rng, max_groups) + tail
+    if cut:
+        stream = stream[:-cut]
+    dstream = _hybrid(defs, 1, rng) if optional else None
+    return _dict_ba_file(stream, nvals, dv, def_stream=dstream)
+
+
 DICT = [b"alpha", b"", b"gamma-gamma", b"d"]
 
 
@@ -207,6 +249,26 @@ CRAFTED = {
     # REQUIRED INT32 over several tiles, pages of different sizes
     "req_int32_tiles": lambda: B.build_file([B.data_header(4 * n, n, 0) + struct.pack(f"<{n}i", *range(-n, 0))
                                              for n in (1500, 1, 513)], gen.INT32, False, 2014),
+    # pages over kPipeSmallRows rows (k_pipe_big): speculative run headers,
+    # pointer-doubled jumps, one tile per wave
+    "big_opt": lambda: _big_dict_file(5000, seed=31),
+    "big_opt_full": lambda: _big_dict_file(32768, seed=32, bw=5),
+    "big_required": lambda: _big_dict_file(9000, seed=33, optional=False, bw=4),
+    "big_short_literals": lambda: _big_dict_file(4000, seed=34, max_groups=1, run=3),
+    "big_long_literals": lambda: _big_dict_file(6000, seed=35, max_groups=63, run=2),
+    # index stream runs out: zero fill of the remaining ranks
+    "big_exhausted": lambda: _big_dict_file(3000, seed=36, cut=40),
+    # zero-count RLE run after a literal run (exact decoder)
+    "big_zero_count": lambda: _big_dict_file(3000, seed=37, tail=B.rle(0, 3, 3) + bytes([0x1b, 0xe4]) * 8),
+    # index bit width 0 with tiny runs: more runs than the record table holds
+    "big_bw0_tiny_runs": lambda: _dict_ba_file(bytes([0]) + b"".join(B.rle(1, 0, 0) for _ in range(3000)), 3000,
+                                               DICT),
+    # pages past the k_pipe_big limits (rows, bytes) next to small pages
+    "big_and_small_pages": lambda: B.build_file(
+        [B.dict_header(len(B.plain_ba(DICT)), len(DICT)) + B.plain_ba(DICT)] +
+        [B.data_header(len(pay), nv, 8) + pay for nv, pay in
+         ((600, bytes([2]) + B.rle(600, 2, 2)), (3000, bytes([2]) + B.rle(2999, 1, 2) + B.rle(1, 3, 2)),
+          (100, bytes([2]) + B.rle(100, 3, 2)))], gen.BYTE_ARRAY, False, 3700, dict_at_start=True),
     # empty chunk
     "empty": lambda: B.build_file([], gen.INT64, False, 0),
     # multiple dictionary pages: the latest one is in force
@@ -273,13 +335,14 @@ def test_error_pages(ctx, path, case):
 
 
 @pytest.mark.slow
-def test_c2_full_size_properties(ctx):
-    """BASELINE config #2 at full size (10M rows): validity/length/content
-    properties against the generator's own values plus sha256 parity with the
-    oracle's dump (both computed here, same seed)."""
+@pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT], ids=["ref", "arrow"])
+def test_c2_full_size_properties(ctx, layout):
+    """BASELINE config #2 at full size (10M rows), in both layouts (arrow =
+    20,000-row pages, the k_pipe_big path): validity/length/content properties
+    plus sha256 of the canonical dump against the generator's own values."""
     cols = gen.c2_cols()
     n = 10_000_000
-    f = gen.build(cols, n, 1, seed=gen.CONFIG_SEEDS["C2"])
+    f = gen.build(cols, n, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
     chunks = file_chunks(f, 0)
     dc = ctx.upload(f, chunks)
     dc.decode()
