@@ -327,10 +327,11 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
         if (dict_id >= 0 && pg.dict != dict_id) return;
         dict_id = pg.dict;
     }
-    if (!big.empty() && pqk::pipe_big_lds(big_bytes) > 160u * 1024) return;
     const DevDict& d = dicts[dict_id];
     if (d.size < 0 || d.size > 65536 - 64 || d.nvals < 0 || d.nvals > 65535) return;
     const int64_t ecap = std::min<int64_t>(d.nvals, d.size / 4 + 1);
+    if (!big.empty() && pqk::pipe_big_lds(big_bytes, std::min<uint32_t>(static_cast<uint32_t>(ecap), pqk::kBigLens)) > 160u * 1024)
+        return;
     const uint32_t chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
     const uint32_t dict_bytes = 16 + chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
     const pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes);
@@ -926,6 +927,7 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         P.debug = ctx->opt_debug;
         P.dict_entries_cap = c->pipe_ecap;
         P.cus = c->pipe_cus;
+        P.has_small = c->pipe_small;
         {
             Timed t(ctx, "pipe_runs");
             pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,

@@ -1010,86 +1010,82 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
 }
 
 // ── pages of more than kPipeSmallRows rows (arrow layout) ──────────────────
-// One workgroup per page.  A stream of ~1-2k runs is too long for the lane
-// walk above, so its run headers are found by a speculative parse instead:
+// One workgroup per page, its payload staged in LDS.  A stream of ~1-2k runs
+// is too long for the lane walk above, so its run headers are found by a
+// speculative parse instead:
 //   1. every byte position j of both streams is parsed as if a run header
-//      started there (rle_decoder.hpp:36-50, 76-95): next header position
-//      and value count, one u32 per byte in LDS (kBStop: bad header or the
-//      stream end is reached);
+//      started there (rle_decoder.hpp:36-50, 76-95): the next header's
+//      position, or kBStop for a bad header or the end of the stream;
 //   2. kBJumpLog pointer-doubling rounds turn that into kBJump-run jumps;
 //   3. one lane per stream follows the jumps from the stream start, listing
-//      every kBJump-th header of the real chain (a few hundred dependent LDS
-//      reads instead of a few thousand parses);
-//   4. one lane per listed header re-parses its kBJump runs exactly (the same
-//      step as walk_runs) into the run records, which replace the jump table;
-//   5. the page's 512-row tiles: def levels (one wave per tile), a scan of the
-//      tiles' non-null counts, then dictionary indices and codes, as
-//      k_pipe_codes2 does with the tile's records found by binary search.
-// Anything outside the fast shape (bad headers, record overflow, levels above
-// max_def) marks the page for k_pipe_exact.
-constexpr int kBigWaves = 16;
+//      every kBJump-th header of the real chain (~100 dependent LDS reads
+//      instead of ~1500 header parses);
+//   4. one lane per listed header re-parses its kBJump runs exactly into run
+//      records with untruncated counts (the jump table's space is reused);
+//   5. a scan of the listed headers' value counts gives every record its
+//      first value; records past the page's value count are dropped, the one
+//      crossing it is truncated and an exhausted stream gets its zero run
+//      (rle_decoder.hpp:20-23): the records k_pipe_runs writes for a page;
+//   6. the page's 512-row tiles: def levels (one wave per tile), a scan of
+//      the tiles' non-null counts, then dictionary indices and codes as in
+//      k_pipe_codes2, each tile's first record found by binary search.
+// Anything outside the fast shape (a bad header before the value count,
+// record overflow, levels above max_def) sends the page to k_pipe_exact.
+constexpr int kBigWaves = 8;
 constexpr int kBigThreads = kBigWaves * kWave;
 constexpr uint32_t kBStop = 0xFFFFu;
-constexpr int kBJumpLog = 3;
+constexpr int kBJumpLog = 4;
 constexpr uint32_t kBJump = 1u << kBJumpLog;
 constexpr uint32_t kBigPerThread = kBigMaxBytes / kBigThreads;  // jump-table slots per thread
+constexpr uint32_t kBCountCap = 1u << 20;                       // count clamp (pages hold <= 32768 values)
 static_assert(kBigMaxBytes % kBigThreads == 0, "jump table split");
+static_assert(kBigMaxBytes + 32 < kBStop, "u16 positions");
 
 struct BigLayout {  // dynamic LDS of k_pipe_big for a page of `size` payload bytes
-    uint32_t P, LC, tab, list, mark, tvb, misc, total;
+    uint32_t P, LC, stage, tab, esum, ent, lens, mark, tvb, misc, total;
 };
-__host__ __device__ inline BigLayout big_layout(uint32_t size) {
+__host__ __device__ inline BigLayout big_layout(uint32_t size, uint32_t nlens) {
     BigLayout L{};
-    L.P = (size + 16 + 15) / 16 * 16;           // positions (u32 each; later P / 2 run records)
-    L.LC = L.P / 16 + 8;                        // listed headers per stream
-    L.tab = 0;
-    L.list = L.tab + 4 * L.P;
-    L.mark = L.list + 8 * L.LC;                 // per wave: u16 run index per row of a tile
-    L.tvb = L.mark + kBigWaves * kTileRows * 2; // per tile: validity bits of rows 8l .. 8l + 7
-    L.misc = L.tvb + kBigTiles * kWave;         // tile non-null counts, first ranks, flags
-    L.total = L.misc + 4 * (2 * kBigTiles + 16);
+    L.P = (size + 16 + 15) / 16 * 16;            // = the payload slot (capi.hip)
+    L.LC = L.P / (2 * kBJump) + 8;               // listed headers per stream (runs are >= 2 bytes)
+    L.stage = 0;                                 // P bytes: the payload slot
+    L.tab = L.stage + L.P;                       // u16 per position; then P / 4 run records
+    L.esum = L.tab + 2 * L.P;                    // u32 per listed header: values, then their exclusive scan
+    L.ent = L.esum + 8 * L.LC;                   // u32 per listed header: position, then fill results
+    L.lens = L.ent + 8 * L.LC;                   // u16 per dictionary entry: length
+    L.mark = L.lens + (2 * nlens + 15) / 16 * 16;  // per wave: u16 per row of a tile
+    L.tvb = L.mark + kBigWaves * kTileRows * 2;  // per tile: validity bits of rows 8l .. 8l + 7
+    L.misc = L.tvb + kBigTiles * kWave;          // tile non-null counts, first ranks, scan partials, flags
+    L.total = L.misc + 4 * (2 * kBigTiles + kBigWaves + 16);
     return L;
 }
 
-// Exact run steps from header position q with `cnt` values before it: the
-// walk_runs step restated for one lane over the page in HBM.  Emits at most
-// `steps` records at out[0 ..); returns the records written, or ~0u on a
-// header outside the fast shape or a full record table.
-__device__ uint32_t big_fill(const uint8_t* page, uint32_t q, uint32_t cnt, uint32_t end, uint32_t bw, uint32_t n,
-                             uint2* out, uint32_t room, uint32_t steps) {
-    const uint32_t nbv = (bw + 7) / 8;
-    const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
-    const uint32_t litpay = bw ? 0x80000000u : 0u;
-    const uint32_t litmul = bw ? 8u : 0u;
-    uint32_t nr = 0;
-    for (uint32_t s = 0; s < steps && cnt < n; s++) {
-        const uint32_t left = n - cnt;
-        if (nr >= room) return ~0u;
-        if (q >= end) {  // exhausted: the rest of the batch is 0 (rle_decoder.hpp:20-23)
-            out[nr++] = make_uint2(cnt | (left << 16), 0u);
-            break;
-        }
-        const uint64_t x = gld8(page, q);
-        const uint32_t x0 = static_cast<uint32_t>(x), x1 = static_cast<uint32_t>(x >> 32);
-        const uint32_t st0 = ~x0 & 0x80808080u;
-        const uint32_t hl = st0 ? (__builtin_ctz(st0) >> 3) + 1 : ((~x1 & 0x80u) ? 5u : 9u);
-        const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
-        const uint32_t x0m = x0 & lm;
-        const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
-        const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
-                             ((x0m >> 3) & 0xFE00000u) | top;
-        const uint32_t g = ind >> 1, lit = ind & 1u, qh = q + hl;
-        if (hl > 5 || qh > end || g == 0 || (!lit && qh + nbv > end)) return ~0u;
-        const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, hl);
-        const uint32_t vb = x1 >> (8 * ((hl - 4) & 3));
-        const uint32_t vraw = (hl < 4) ? va : vb;
-        const uint32_t c = lit ? ((g >= (left + 7) / 8) ? left : g * 8) : min(g, left);
-        out[nr++] = make_uint2(cnt | (c << 16), lit ? (litpay | (qh * litmul)) : (vraw & vmask));
-        const uint64_t nql = static_cast<uint64_t>(qh) + static_cast<uint64_t>(g) * bw;
-        q = lit ? (nql > end ? end : static_cast<uint32_t>(nql)) : qh + nbv;
-        cnt += c;
-    }
-    return nr;
+// A run header at LDS byte q of the staged page (the walk_runs parse).
+struct BigHdr {
+    uint32_t hl, g, lit, qh, vraw;
+};
+__device__ __forceinline__ BigHdr big_hdr(const uint32_t* stw, uint32_t q) {
+    const uint64_t x = lds_u64(stw, q);
+    const uint32_t x0 = static_cast<uint32_t>(x), x1 = static_cast<uint32_t>(x >> 32);
+    const uint32_t st0 = ~x0 & 0x80808080u;
+    BigHdr h;
+    h.hl = st0 ? (__builtin_ctz(st0) >> 3) + 1 : ((~x1 & 0x80u) ? 5u : 9u);
+    const uint32_t lm = (h.hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (h.hl & 3))) - 1u);
+    const uint32_t x0m = x0 & lm;
+    const uint32_t top = (h.hl >= 5) ? (x1 << 28) : 0u;
+    const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
+                         ((x0m >> 3) & 0xFE00000u) | top;
+    h.g = ind >> 1;
+    h.lit = ind & 1u;
+    h.qh = q + h.hl;
+    const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, h.hl);
+    const uint32_t vb = x1 >> (8 * ((h.hl - 4) & 3));
+    h.vraw = (h.hl < 4) ? va : vb;
+    return h;
+}
+// zero-count runs, headers past the stream, RLE values cut by its end
+__device__ __forceinline__ bool big_bad(const BigHdr& h, uint32_t e, uint32_t nbv) {
+    return h.hl > 5 || h.qh > e || h.g == 0 || (!h.lit && h.qh + nbv > e);
 }
 
 // Largest k < nr with start(rec[k]) <= v (rec[0] starts at 0); wave-uniform.
@@ -1103,24 +1099,8 @@ __device__ __forceinline__ uint32_t big_search(const uint2* rec, uint32_t nr, ui
     return lo;
 }
 
-// Per lane: the record index (relative to k0) of values v0 + 8l .. v0 + 8l + 7,
-// from marks m[v - v0] = record index - k0 at each record start.
-__device__ __forceinline__ void big_runs8(const uint16_t* mark, uint32_t l8, uint32_t m, uint32_t rm[8]) {
-    uint4 mk = make_uint4(0u, 0u, 0u, 0u);
-    if (l8 < m) mk = *reinterpret_cast<const uint4*>(mark + l8);
-    const uint32_t w[4] = {mk.x, mk.y, mk.z, mk.w};
-    uint32_t run = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        run = max(run, (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-        rm[k] = run;
-    }
-    const uint32_t ex = wave_shr1(wave_incl_max(run));
-#pragma unroll
-    for (int k = 0; k < 8; k++) rm[k] = max(ex, rm[k]);
-}
-
-// Marks the starts of records k0 + 1 .. that begin inside [v0, v0 + m).
+// Marks the starts of records k0 + 1 .. that begin inside [v0, v0 + m):
+// mark[start - v0] = record - k0.
 __device__ __forceinline__ void big_mark(uint16_t* mark, const uint2* rec, uint32_t nr, uint32_t k0, uint32_t v0,
                                          uint32_t m) {
     const uint32_t l8 = lane() * 8;
@@ -1138,25 +1118,70 @@ __device__ __forceinline__ void big_mark(uint16_t* mark, const uint2* rec, uint3
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Per lane: the record (relative to k0) of values v0 + 8l .. v0 + 8l + 7.
+__device__ __forceinline__ void big_runs8(const uint16_t* mark, uint32_t l8, uint32_t m, uint32_t rm[8]) {
+    uint4 mk = make_uint4(0u, 0u, 0u, 0u);
+    if (l8 < m) mk = *reinterpret_cast<const uint4*>(mark + l8);
+    const uint32_t w[4] = {mk.x, mk.y, mk.z, mk.w};
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        run = max(run, (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+        rm[k] = run;
+    }
+    const uint32_t ex = wave_shr1(wave_incl_max(run));
+#pragma unroll
+    for (int k = 0; k < 8; k++) rm[k] = max(ex, rm[k]);
+}
+
+// Exclusive scan of v[0 .. m) in place (all threads of the workgroup);
+// `part` holds kBigWaves words.
+__device__ void big_scan(uint32_t* v, uint32_t m, uint32_t* part) {
+    const uint32_t tid = threadIdx.x, wv = tid / kWave;
+    const uint32_t per = (m + kBigThreads - 1) / kBigThreads;
+    const uint32_t a0 = min(m, tid * per), a1 = min(m, a0 + per);
+    uint32_t s = 0;
+    for (uint32_t i = a0; i < a1; i++) s += v[i];
+    const uint32_t inc = wave_incl_scan(s);
+    if (lane() == kWave - 1) part[wv] = inc;
+    __syncthreads();
+    uint32_t base = inc - s;
+    for (uint32_t w = 0; w < wv; w++) base += part[w];
+    for (uint32_t i = a0; i < a1; i++) {
+        const uint32_t x = v[i];
+        v[i] = base;
+        base += x;
+    }
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int32_t* __restrict__ bigp,
-                                                          int32_t* __restrict__ flist, uint32_t* __restrict__ info) {
+                                                          int32_t* __restrict__ flist, uint32_t* __restrict__ info,
+                                                          uint32_t nlens) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int p = bigp[blockIdx.x];
     const DevPage pg = a.pages[p];
     const uint8_t* page = a.bytes + pg.off;
     const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
     const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
-    const BigLayout Ly = big_layout(size);
-    uint32_t* tab = reinterpret_cast<uint32_t*>(smem + Ly.tab);
-    uint32_t* list = reinterpret_cast<uint32_t*>(smem + Ly.list);
+    const BigLayout Ly = big_layout(size, nlens);
+    uint32_t* stw = reinterpret_cast<uint32_t*>(smem + Ly.stage);
+    uint16_t* tab = reinterpret_cast<uint16_t*>(smem + Ly.tab);
+    uint32_t* esum = reinterpret_cast<uint32_t*>(smem + Ly.esum);
+    uint32_t* ent = reinterpret_cast<uint32_t*>(smem + Ly.ent);
+    uint16_t* lens = reinterpret_cast<uint16_t*>(smem + Ly.lens);
     uint8_t* tvb = smem + Ly.tvb;
     uint32_t* misc = reinterpret_cast<uint32_t*>(smem + Ly.misc);
-    uint32_t* tnn = misc;                 // [kBigTiles]
-    uint32_t* tk0 = misc + kBigTiles;     // [kBigTiles]
-    uint32_t* sh = misc + 2 * kBigTiles;  // [0] flag, [1] def list, [2] idx list, [3] def records, [4] idx records
+    uint32_t* tnn = misc;                     // [kBigTiles]
+    uint32_t* tk0 = misc + kBigTiles;         // [kBigTiles]
+    uint32_t* part = misc + 2 * kBigTiles;    // [kBigWaves]
+    uint32_t* sh = part + kBigWaves;          // [0] flag, [1] def list, [2] idx list, [3] def records, [4] idx records
     const uint32_t tid = threadIdx.x, wv = tid / kWave;
     const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
     const uint32_t ntp = (n + kTileRows - 1) / kTileRows;
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    const uint32_t nl = min(dict_n, nlens);
 
     // prologue (column_reader.cpp:146-182), wave-uniform; any error -> k_pipe_exact
     bool flag = n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes;
@@ -1193,109 +1218,141 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     if (flag) return to_exact();
     const bool hasd = a.max_def > 0;
     const uint32_t dend = dbase + dlen, ibase = pos, iend = size;
+    auto in_stream = [&](uint32_t j) { return j >= ibase || (hasd && j >= dbase && j < dend); };
 
+    // 0. the payload slot and the dictionary's entry lengths -> LDS
+    for (uint32_t i = tid; i < Ly.P / 16; i += kBigThreads)
+        reinterpret_cast<uint4*>(stw)[i] = reinterpret_cast<const uint4*>(page)[i];
+    for (uint32_t k = tid; k < nl; k += kBigThreads) lens[k] = static_cast<uint16_t>(a.entries[ebase + k] >> 32);
+    if (tid < 8) sh[tid] = 0;
+    __syncthreads();
     // 1. speculative headers at every byte of both streams
     for (uint32_t j = tid; j < size; j += kBigThreads) {
-        const bool ind_ = j >= ibase;
-        const bool ind_d = hasd && j >= dbase && j < dend;
-        if (!ind_ && !ind_d) continue;
-        const uint32_t e = ind_ ? iend : dend, bw = ind_ ? bwi : bwd, nbv = (bw + 7) / 8;
-        const uint64_t x = gld8(page, j);
-        const uint32_t x0 = static_cast<uint32_t>(x), x1 = static_cast<uint32_t>(x >> 32);
-        const uint32_t st0 = ~x0 & 0x80808080u;
-        const uint32_t hl = st0 ? (__builtin_ctz(st0) >> 3) + 1 : ((~x1 & 0x80u) ? 5u : 9u);
-        const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
-        const uint32_t x0m = x0 & lm;
-        const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
-        const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
-                             ((x0m >> 3) & 0xFE00000u) | top;
-        const uint32_t g = ind >> 1, lit = ind & 1u, qh = j + hl;
-        const bool bad = hl > 5 || qh > e || g == 0 || (!lit && qh + nbv > e);
-        const uint64_t nx = lit ? static_cast<uint64_t>(qh) + static_cast<uint64_t>(g) * bw : qh + nbv;
-        const uint32_t c = min(lit ? (g > 8191u ? 65535u : g * 8u) : g, 65535u);
-        tab[j] = ((bad || nx >= e) ? kBStop : static_cast<uint32_t>(nx)) | (c << 16);
+        if (!in_stream(j)) continue;
+        const bool isi = j >= ibase;
+        const uint32_t e = isi ? iend : dend, bw = isi ? bwi : bwd;
+        const BigHdr h = big_hdr(stw, j);
+        const uint64_t nx = h.lit ? static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw : h.qh + (bw + 7) / 8;
+        tab[j] = static_cast<uint16_t>((big_bad(h, e, (bw + 7) / 8) || nx >= e) ? kBStop : static_cast<uint32_t>(nx));
     }
     __syncthreads();
-    // 2. kBJump-run jumps by pointer doubling (counts saturate at 65535)
+    // 2. kBJump-run jumps by pointer doubling
     for (int r = 0; r < kBJumpLog; r++) {
         uint32_t nv[kBigPerThread];
 #pragma unroll
         for (uint32_t i = 0; i < kBigPerThread; i++) {
             const uint32_t j = tid + i * kBigThreads;
-            nv[i] = 0;
-            if (j < size && ((j >= ibase) || (hasd && j >= dbase && j < dend))) {
-                const uint32_t t = tab[j];
-                nv[i] = t;
-                if ((t & 0xFFFFu) != kBStop) {
-                    const uint32_t u = tab[t & 0xFFFFu];
-                    nv[i] = (u & 0xFFFFu) | (min((t >> 16) + (u >> 16), 65535u) << 16);
-                }
+            uint32_t t = kBStop;
+            if (j < size && in_stream(j)) {
+                t = tab[j];
+                if (t != kBStop) t = tab[t];
             }
+            nv[i] = t;
         }
         __syncthreads();
 #pragma unroll
         for (uint32_t i = 0; i < kBigPerThread; i++) {
             const uint32_t j = tid + i * kBigThreads;
-            if (j < size && ((j >= ibase) || (hasd && j >= dbase && j < dend))) tab[j] = nv[i];
+            if (j < size && in_stream(j)) tab[j] = static_cast<uint16_t>(nv[i]);
         }
         __syncthreads();
     }
-    // 3. one lane per stream follows the jumps: every kBJump-th header, with
-    //    the values before it
-    const uint32_t rcap = Ly.P / 2;                           // records in the table's space
+    if (a.debug & 4096) return;  // timing: jump table only
+    // 3. one lane per stream follows the jumps: every kBJump-th header
+    const uint32_t rcap = Ly.P / 4;  // run records in the jump table's space
     const uint32_t rcap_d = hasd ? min(rcap / 2, dlen / 2 + 2 * kBJump + 2) : 0u;
     const uint32_t rcap_i = rcap - rcap_d;
     if (tid == 0 || tid == kWave) {
         const bool isd = tid == 0;
         uint32_t k = 0;
         if (!isd || hasd) {
-            const uint32_t e = isd ? dend : iend;
-            uint32_t q = isd ? dbase : ibase, c = 0;
-            uint32_t* L = list + (isd ? 0u : Ly.LC);
-            const uint32_t lcap = min(Ly.LC, (isd ? rcap_d : rcap_i) / kBJump);
+            const uint32_t e = isd ? dend : iend, rc = isd ? rcap_d : rcap_i;
+            const uint32_t lcap = rc > kBJump + 1 ? min(Ly.LC, (rc - kBJump - 1) / kBJump + 1) : 0u;
+            uint32_t* L = ent + (isd ? 0u : Ly.LC);
+            uint32_t q = isd ? dbase : ibase;
             for (;;) {
                 if (k >= lcap) { k = ~0u; break; }
-                L[k++] = q | (c << 16);
+                L[k++] = q;
                 if (q >= e) break;
                 const uint32_t t = tab[q];
-                if ((t & 0xFFFFu) == kBStop) break;
-                c += t >> 16;
-                if (c >= n) break;
-                q = t & 0xFFFFu;
+                if (t == kBStop) break;
+                q = t;
             }
         }
         sh[isd ? 1 : 2] = k;
     }
-    if (tid == 0) sh[0] = 0;
     __syncthreads();
     const uint32_t nld = sh[1], nli = sh[2];
+    if (a.debug & 8192) return;  // timing: + chain walk
     if (nld == ~0u || nli == ~0u) return to_exact();
-    // 4. exact records, kBJump runs per listed header (the jump table is dead)
+    // 4. exact runs of each listed header: untruncated counts, bad-header step
     uint2* recd = reinterpret_cast<uint2*>(smem + Ly.tab);
     uint2* reci = recd + rcap_d;
-    for (uint32_t i = tid; i < nld + nli; i += kBigThreads) {
+    const uint32_t ne = nld + nli;
+    for (uint32_t i = tid; i < ne; i += kBigThreads) {
         const bool isd = i < nld;
-        const uint32_t li = isd ? i : i - nld, nl = isd ? nld : nli;
-        const uint32_t e = list[(isd ? 0u : Ly.LC) + li];
-        const bool last = li + 1 == nl;
+        const uint32_t li = isd ? i : i - nld;
+        const uint32_t slot = isd ? i : Ly.LC + li;
+        uint32_t q = ent[slot];
+        const uint32_t e = isd ? dend : iend, bw = isd ? bwd : bwi, nbv = (bw + 7) / 8;
+        const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+        const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
         uint2* out = (isd ? recd : reci) + li * kBJump;
-        const uint32_t room = (isd ? rcap_d : rcap_i) - li * kBJump;
-        const uint32_t r = big_fill(page, e & 0xFFFFu, e >> 16, isd ? dend : iend, isd ? bwd : bwi, n, out, room,
-                                    last ? kBJump + 1 : kBJump);
-        if (r == ~0u || (!last && r != kBJump)) atomicOr(&sh[0], 1u);
-        else if (last) sh[isd ? 3 : 4] = li * kBJump + r;
+        uint32_t s = 0, sum = 0, bad = kBJump, ended = 0;
+        for (; s < kBJump; s++) {
+            if (q >= e) { ended = 1; break; }
+            const BigHdr h = big_hdr(stw, q);
+            if (big_bad(h, e, nbv)) { bad = s; break; }
+            const uint32_t c = h.lit ? min(h.g, kBCountCap / 8) * 8 : min(h.g, kBCountCap);
+            out[s] = make_uint2(c, h.lit ? (litpay | (h.qh * litmul)) : (h.vraw & vmask));
+            sum = min(sum + c, kBCountCap);
+            const uint64_t nql = static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw;
+            q = h.lit ? (nql > e ? e : static_cast<uint32_t>(nql)) : h.qh + nbv;
+        }
+        if (s == kBJump && q >= e) ended = 1;
+        esum[i] = sum;
+        ent[slot] = s | (bad << 8) | (ended << 16);
     }
     __syncthreads();
-    if (sh[0]) return to_exact();
+    // 5. first value of every record: scan of the headers' counts, then
+    //    truncation at the page's value count and the exhaustion run
+    big_scan(esum, ne, part);
+    const uint32_t dtot = nld < ne ? esum[nld] : 0u;
+    for (uint32_t i = tid; i < ne; i += kBigThreads) {
+        const bool isd = i < nld;
+        const uint32_t li = isd ? i : i - nld, nlst = isd ? nld : nli;
+        const uint32_t meta = ent[isd ? i : Ly.LC + li];
+        const uint32_t nr = meta & 0xFFu, bad = (meta >> 8) & 0xFFu, ended = meta >> 16;
+        const uint32_t base = esum[i] - (isd ? 0u : dtot);
+        if (base >= n) continue;
+        uint2* out = (isd ? recd : reci) + li * kBJump;
+        const uint32_t room = (isd ? rcap_d : rcap_i) - li * kBJump;
+        uint32_t c0 = base, kept = 0;
+        for (uint32_t s = 0; s < nr && c0 < n; s++) {
+            const uint32_t c = out[s].x;
+            out[s].x = c0 | (min(c, n - c0) << 16);
+            c0 += c;
+            kept = s + 1;
+        }
+        if (c0 >= n) {
+            sh[isd ? 3 : 4] = li * kBJump + kept;
+        } else if (bad < kBJump || (li + 1 == nlst && (!ended || nr >= room))) {
+            atomicOr(&sh[0], 1u);  // a bad header before the value count (or a broken chain)
+        } else if (li + 1 == nlst) {  // exhausted: the rest of the values are 0
+            out[nr] = make_uint2(c0 | ((n - c0) << 16), 0u);
+            sh[isd ? 3 : 4] = li * kBJump + nr + 1;
+        }
+    }
+    __syncthreads();
+    if (a.debug & 16384) return;  // timing: + exact records
     const uint32_t nd = hasd ? sh[3] : 0u, ni = sh[4];
-    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    if (sh[0] || (hasd && nd == 0) || ni == 0) return to_exact();
     const int32_t t0 = a.page_tile0[p];
     const int64_t first_row = pg.first_row;
     uint16_t* mark = reinterpret_cast<uint16_t*>(smem + Ly.mark) + wv * kTileRows;
     const uint32_t l8 = lane() * 8;
 
-    // 5a. def levels per tile -> validity bits, non-null counts
+    // 6a. def levels per tile -> validity bits, non-null counts
     for (uint32_t ti = wv; ti < ntp; ti += kBigWaves) {
         const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
         uint32_t vb = 0;
@@ -1311,20 +1368,21 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
                 const uint2 R = recd[rd0 + rm[k]];
                 uint32_t lvl = rr_pay(R);
                 if (rr_lit(R) && j < m)
-                    lvl = gbits(page, size, rr_pay(R) + static_cast<uint64_t>(r0 + j - rr_start(R)) * bwd, bwd);
+                    lvl = lds_bits(stw, size, rr_pay(R) + static_cast<uint64_t>(r0 + j - rr_start(R)) * bwd, bwd);
                 vb |= (j < m && lvl == md ? 1u : 0u) << k;
                 above |= j < m && lvl > md;
             }
         } else {
             vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
         }
-        if (__ballot(above)) atomicOr(&sh[0], 1u);  // levels above max_def: outside the fast shape
+        if (__ballot(above) && lane() == 0) atomicOr(&sh[0], 1u);  // levels above max_def: exact decoder
         tvb[ti * kWave + lane()] = static_cast<uint8_t>(vb);
         const uint32_t nn = bcast_last(wave_incl_scan(__popc(vb)));
         if (lane() == 0) tnn[ti] = nn;
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
+    if (a.debug & 32768) return;  // timing: + def levels
     if (sh[0]) return to_exact();
     if (wv == 0) {  // first rank of each tile (ntp <= 64)
         const uint32_t v = lane() < ntp ? tnn[lane()] : 0u;
@@ -1333,21 +1391,21 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     }
     if (tid == 0) info[p] = kBig;
     __syncthreads();
-    // 5b. dictionary indices of each tile's ranks -> codes, tile characters
+    // 6b. dictionary indices of each tile's ranks -> codes, tile characters
     for (uint32_t ti = wv; ti < ntp; ti += kBigWaves) {
         const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
         const uint32_t vb = tvb[ti * kWave + lane()];
         const uint32_t nnl = __popc(vb);
         const uint32_t rbase = wave_incl_scan(nnl) - nnl;
         const uint32_t nn = tnn[ti], k0 = tk0[ti];
-        uint32_t ri0 = 0, rm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t ri0 = 0;
         if (nn) {
+            uint32_t rm[8];
             ri0 = big_search(reci, ni, k0);
             big_mark(mark, reci, ni, ri0, k0, nn);
             big_runs8(mark, l8, nn, rm);
-            // rank -> record, held per rank: lane l has ranks 8l .. 8l + 7
             __builtin_amdgcn_wave_barrier();
-            if (l8 < nn) {
+            if (l8 < nn) {  // record of every rank of the tile
                 uint4 w;
                 w.x = rm[0] | (rm[1] << 16);
                 w.y = rm[2] | (rm[3] << 16);
@@ -1368,10 +1426,11 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
                 const uint32_t rk = rbase + __popc(vb & ((1u << k) - 1u));
                 const uint2 R = reci[ri0 + mark[rk]];
                 uint32_t v = rr_pay(R);
-                if (rr_lit(R)) v = gbits(page, size, rr_pay(R) + static_cast<uint64_t>(k0 + rk - rr_start(R)) * bwi, bwi);
+                if (rr_lit(R))
+                    v = lds_bits(stw, size, rr_pay(R) + static_cast<uint64_t>(k0 + rk - rr_start(R)) * bwi, bwi);
                 if (v < dict_n) {
                     code = v;
-                    chars += static_cast<uint32_t>(a.entries[ebase + v] >> 32);
+                    chars += v < nl ? lens[v] : static_cast<uint32_t>(a.entries[ebase + v] >> 32);
                 }
             }
             if (j < m) a.codes[R0 + j] = static_cast<uint16_t>(code);
@@ -1384,7 +1443,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
 
 }  // namespace
 
-uint32_t pipe_big_lds(uint32_t max_page_bytes) { return big_layout(max_page_bytes).total; }
+uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens) { return big_layout(max_page_bytes, nlens).total; }
 
 PipePlan plan_pipe_lds(uint32_t dict_bytes) {
     PipePlan pl{};
@@ -1450,7 +1509,7 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
         bpc = 1;
     const int need = (P.ntiles + kCodeWaves2 - 1) / kCodeWaves2;
     const int grid = max(1, min(need, P.cus * bpc));
-    hipLaunchKernelGGL(k_pipe_codes2, dim3(grid), dim3(kCodeWaves2 * kWave), lds, s, a, lt_n);
+    if (P.has_small) hipLaunchKernelGGL(k_pipe_codes2, dim3(grid), dim3(kCodeWaves2 * kWave), lds, s, a, lt_n);
     // pages the run-table pass marked: exact decoder (each wave exits unless its tile starts one)
     hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, (P.npages + kCodeWaves - 1) / kCodeWaves))),
                        dim3(kCodeWaves * kWave), 0, s, a, P.flist);
@@ -1473,13 +1532,14 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
 }
 
 void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes) {
+    const uint32_t nlens = min(P.dict_entries_cap, kBigLens);
     if (nbig <= 0) return;
     int wgrid = 0, per = 0;
     write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_write's workgroups
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
                P.bsum, per, P.debug};
-    const uint32_t lds = big_layout(max_page_bytes).total;
+    const uint32_t lds = big_layout(max_page_bytes, nlens).total;
     static uint32_t attr = 0;
     if (lds > attr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_big),
@@ -1487,7 +1547,7 @@ void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_page
         attr = lds;
     }
     hipLaunchKernelGGL(k_pipe_big, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
-                       const_cast<int32_t*>(P.flist), const_cast<uint32_t*>(P.info));
+                       const_cast<int32_t*>(P.flist), const_cast<uint32_t*>(P.info), nlens);
 }
 
 }  // namespace pqk

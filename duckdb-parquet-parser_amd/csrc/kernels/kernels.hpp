@@ -86,7 +86,8 @@ void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int
 // ── three-pass dictionary BYTE_ARRAY path (dict_pipe.hip) ──────────────────
 constexpr uint32_t kPipeRunCap = 128;  // run records per stream per page
 constexpr int32_t kPipeSmallRows = 2048;   // larger pages take k_pipe_big (one workgroup per page)
-constexpr uint32_t kBigMaxBytes = 28672;   // k_pipe_big: payload bytes per page (jump table in LDS)
+constexpr uint32_t kBigMaxBytes = 24576;   // k_pipe_big: payload bytes per page (staged, jump table in LDS)
+constexpr uint32_t kBigLens = 8192;        // k_pipe_big: dictionary entry lengths held in LDS
 constexpr int32_t kBigTiles = 64;          // k_pipe_big: 512-row tiles per page
 
 struct PipeLaunch {
@@ -122,6 +123,7 @@ struct PipeLaunch {
     int debug;  // ablation bits (k_pipe_write)
     uint32_t dict_entries_cap;  // entry-table capacity of the dictionary (k_pipe_codes length table)
     int cus;
+    bool has_small;             // some pages of <= kPipeSmallRows rows (k_pipe_runs / k_pipe_codes2)
 };
 struct PipePlan {
     uint32_t lds;       // dynamic LDS bytes of k_pipe_write
@@ -134,7 +136,7 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,
 // then codes and tile characters (one workgroup per listed page)
-uint32_t pipe_big_lds(uint32_t max_page_bytes);
+uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens);
 void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes);
 
 // ── tile-parallel PLAIN fixed-width path (fixed_fast.hip) ──────────────────

@@ -8,6 +8,8 @@ fused_debug bits (timing only; the output is not valid with bits set):
   2 = skip the characters
   4 = skip the offsets stores
   8/16/32 = dict_fused.hip writer internals (see the kernel)
+  4096/8192/16384/32768 = k_pipe_big stops after the jump table / chain walk /
+      exact records / def levels (`ablate.py arrow big`)
 Prints one JSON line per variant with per-kernel average milliseconds, then
 per-phase shader-clock cycles (option fused_prof) for the batch and fused
 kernels.
@@ -20,7 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "duckdb-parquet-parser_amd")]
 from pqgpu import capi, gen  # noqa: E402
 
-KERNELS = ("dict_index", "pipe_runs", "pipe_count", "pipe_codes", "pipe_write", "ba_batch", "ba_fused", "ba_rows",
+KERNELS = ("dict_index", "pipe_runs", "pipe_big", "pipe_count", "pipe_codes", "pipe_write", "ba_batch", "ba_fused", "ba_rows",
            "scan", "ba_gather")
 BATCH_PHASES = ("p_waitbuf", "p_stage", "p_walk", "p_lookback", "batches",
                 "w_wait", "w_runs", "w_rows", "w_chars", "pages", "p_defwalk")
@@ -52,13 +54,18 @@ if "write" in sys.argv:
     variants = [("pipe", d, 0, 12288, 1) for d in (0, 2, 128, 128 | 32)]
 if "runpages" in sys.argv:
     variants = [("pipe", 0, 0, 12288, 1, rp) for rp in (32, 16, 8, 4)]
+if "big" in sys.argv:  # k_pipe_big phases (arrow layout): jump table, walk, records, def levels, all
+    variants = [("pipe", d, 0, 12288, 1) for d in (4096, 8192, 16384, 32768, 0)]
 if "batch" in sys.argv:
     variants += [("batch", 0, 0, 12288, 1), ("batch", 1, 0, 12288, 1), ("batch", 3, 0, 12288, 1)]
 for v in variants:
     path, dbg, waves, bb, claim = v[:5]
     rp = v[5] if len(v) > 5 else 32
-    setp(path, dbg, waves, bb, claim, rp)
+    setp(path, 0, waves, bb, claim, rp)
     dc = ctx.upload(f, chunks)
+    dc.decode_async()  # valid intermediate buffers before any ablation bit is set
+    ctx.sync()
+    ctx.set_option("fused_debug", dbg)
     dc.decode_async()
     ctx.sync()
     ctx.timing(True)
