@@ -18,9 +18,8 @@
 //                 (stream.hpp), one wavefront per page.
 //   (scan)        exclusive scan of the tile character counts (decode.hip).
 //   k_pipe_write  persistent workgroups with the dictionary in LDS: int64
-//                 offsets, validity words and the characters, every 16-byte
-//                 output block assembled in registers from the LDS dictionary
-//                 and stored once.
+//                 offsets, validity words and the characters, each row copied
+//                 from the LDS dictionary to HBM with unaligned 16-byte moves.
 // Only pages of more than 512 rows with def levels need tile_nn, the
 // non-null counts of the earlier tiles of their page (k_pipe_codes<true>).
 #include "kernels/device_common.hpp"
@@ -44,7 +43,6 @@ constexpr uint32_t kSkip = kFallback | kBig;  // k_pipe_codes2 leaves the page a
 constexpr int kCodeWaves = 4;
 constexpr uint16_t kNull = 0xFFFFu;
 constexpr int kWriteWaves = 6;
-constexpr uint32_t kWin = 1024;               // 16-byte output blocks per window
 constexpr uint32_t kFront = 16;               // zero bytes before the LDS dictionary
 constexpr uint32_t kLitCapP = 16;
 
@@ -674,22 +672,58 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_exact(CodeArgs a, cons
 // ── offsets, validity, characters ──────────────────────────────────────────
 constexpr int kRowsPerLane = kTileRows / kWave;
 
-constexpr uint32_t kRing = 4096;  // per-wave staging of one 64-row group's characters
+constexpr int kWBatch = 4;          // tiles whose codes k_pipe_write loads at once
+constexpr uint32_t kLongRow = 128;  // longer rows are copied by the whole wave
 
 struct WriteLds {
     uint32_t off[kTileRows + 1];  // tile-relative first byte per row
     uint16_t src[kTileRows];      // dictionary byte per row
     uint8_t vb[kWave];            // validity bits of rows 8l .. 8l + 7
-    union {
-        uint4 ring[kRing / 16];   // characters, 16-byte aligned to the output
-        uint16_t brow[kWin];      // fallback: row holding each block's first byte
-    };
 };
 
 struct __attribute__((packed, aligned(1))) U16B { uint32_t x, y, z, w; };
 struct __attribute__((packed, aligned(1))) U8B { uint32_t x, y; };
 struct __attribute__((packed, aligned(1))) U4B { uint32_t x; };
 struct __attribute__((packed, aligned(1))) U2B { uint16_t x; };
+
+__device__ __forceinline__ uint32_t dword_of(const uint4& v, uint32_t i) {  // register select, no scratch
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+// Bytes [x, y) (0 <= x < y <= 16) of the 16-byte aligned output block at
+// `blk`, as naturally aligned 8/4/2/1-byte stores.
+__device__ __forceinline__ void store_part(uint8_t* chars, int64_t blk, const uint4& v, uint32_t x, uint32_t y) {
+    if (x == 0 && y == 16) {
+        *reinterpret_cast<uint4*>(chars + blk) = v;
+        return;
+    }
+    while (x < y) {
+        const uint32_t w = dword_of(v, x >> 2);
+        if ((x & 7) == 0 && x + 8 <= y) {
+            *reinterpret_cast<uint2*>(chars + blk + x) = make_uint2(w, dword_of(v, (x >> 2) + 1));
+            x += 8;
+        } else if ((x & 3) == 0 && x + 4 <= y) {
+            *reinterpret_cast<uint32_t*>(chars + blk + x) = w;
+            x += 4;
+        } else if ((x & 1) == 0 && x + 2 <= y) {
+            *reinterpret_cast<uint16_t*>(chars + blk + x) = static_cast<uint16_t>(w >> (8 * (x & 3)));
+            x += 2;
+        } else {
+            chars[blk + x] = static_cast<uint8_t>(w >> (8 * (x & 3)));
+            x += 1;
+        }
+    }
+}
+// 16 bytes at LDS byte address A of a dword array: dword-aligned reads and
+// v_alignbyte (byte-unaligned ds_read_b128 is much slower).  Bytes before A
+// may be read (A >= 1 .. 3 bytes past a 4-aligned start is fine); the caller
+// keeps 20 readable bytes past A.  A may be below the row start when the
+// caller masks (block pulls).
+__device__ __forceinline__ uint4 lds16(const uint32_t* w, uint32_t A) {
+    const uint32_t i = A >> 2, sh = A & 3u;
+    const uint32_t w0 = w[i], w1 = w[i + 1], w2 = w[i + 2], w3 = w[i + 3], w4 = w[i + 4];
+    return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                      __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+}
 
 struct WriteArgs {
     const uint8_t* bytes;
@@ -712,8 +746,7 @@ struct WriteArgs {
     int64_t* offsets;
     uint8_t* chars;
     uint32_t dict_chars_bytes, dict_bytes;
-    int debug;  // ablation: 2 = no characters, 4 = no offsets/validity stores, 8 = prologue only,
-                //           16 = no block marking, 32 = no character stores, 64 = no ring copy
+    int debug;  // ablation: 2 = no characters, 4 = no offsets/validity stores, 8 = prologue only
 };
 
 __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
@@ -790,27 +823,41 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
             const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), i);
             return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
         };
-        uint32_t cd[kTileRows / kWave];
-        auto load_codes = [&](int i) {
-            const int64_t R = rl64(myR0, i);
-            const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
-#pragma unroll
-            for (int k = 0; k < kRowsPerLane; k++) {
-                const uint32_t j = lane() * kRowsPerLane + k;
-                cd[k] = j < mm ? a.codes[R + j] : kNull;
-            }
-        };
-        load_codes(0);
-        for (int i = 0; i < cn; i++) {
+        // codes of kWBatch tiles at a time -> LDS: the only global loads of
+        // the tile loop, so one wait (which also drains this wave's earlier
+        // stores: loads and stores share vmcnt) per batch, not per tile
+        const uint32_t l8 = lane() * kRowsPerLane;
+        for (int ib = 0; ib < cn; ib += kWBatch) {
+            // four named registers (an indexed array would go to scratch)
+            static_assert(kWBatch == 4, "batch registers");
+            auto ld = [&](int i) -> uint4 {
+                uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+                if (i < cn) {
+                    const int64_t R = rl64(myR0, i);
+                    const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
+                    if (l8 < mm) {
+                        const U16B x = *reinterpret_cast<const U16B*>(a.codes + R + l8);
+                        v = make_uint4(x.x, x.y, x.z, x.w);
+                    }
+                }
+                return v;
+            };
+            const uint4 cv0 = ld(ib), cv1 = ld(ib + 1), cv2 = ld(ib + 2), cv3 = ld(ib + 3);
+        for (int i = ib; i < min(cn, ib + kWBatch); i++) {
             const int64_t R0 = rl64(myR0, i);
             const int64_t G0 = rl64(myG0, i);
             const uint32_t m = __builtin_amdgcn_readlane(mym, i);
             uint32_t cur[kRowsPerLane];
+            {
+                const int u = i - ib;  // register select (no dynamic indexing into cv)
+                const uint4 w = u == 0 ? cv0 : (u == 1 ? cv1 : (u == 2 ? cv2 : cv3));
+                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-            for (int k = 0; k < kRowsPerLane; k++) cur[k] = cd[k];
-            if (i + 1 < cn) load_codes(i + 1);
+                for (int k = 0; k < kRowsPerLane; k++)
+                    cur[k] = l8 + k < m ? (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : kNull;
+            }
             // this lane's rows 8l .. 8l + 7: lengths, dictionary offsets, validity
-            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0, lmax = 0;
+            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0;
 #pragma unroll
             for (int k = 0; k < kRowsPerLane; k++) {
                 const bool valid = cur[k] < dict_n;
@@ -819,7 +866,6 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
                 src[k] = e & 0xFFFFu;
                 vb |= (valid ? 1u : 0u) << k;
                 acc += len[k];
-                lmax = max(lmax, len[k]);
             }
             const uint32_t incl = wave_incl_scan(acc);
             const uint32_t total = bcast_last(incl);
@@ -835,12 +881,6 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
                     o += len[k];
                 }
             }
-            // a 64-row group is 8 lanes: the ring must hold any group's characters
-            uint32_t g8 = acc;
-            g8 += __shfl_xor(g8, 1);
-            g8 += __shfl_xor(g8, 2);
-            g8 += __shfl_xor(g8, 4);
-            const bool ringable = __ballot(g8 + 32 > kRing) == 0;
             S.vb[lane()] = static_cast<uint8_t>(vb);
             if (lane() == 0) S.off[m] = total;
             __builtin_amdgcn_wave_barrier();
@@ -876,135 +916,69 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
                 if (lane() == 0) atomicOr(a.overflow, 1);
                 continue;
             }
+            // characters, 64 consecutive rows per step: each lane copies its
+            // row from the LDS dictionary to HBM as unaligned 16-byte moves
+            // (the last one overlapping the row's earlier bytes), rows under
+            // 16 bytes as two overlapping 8/4/2-byte moves, so no store leaves
+            // its row and the L2 merges the partial lines.  Rows longer than
+            // kLongRow are copied afterwards by the whole wave, 16-byte
+            // aligned blocks across the lanes.  (Assembling aligned blocks in
+            // LDS first costs more than it saves: byte-unaligned LDS accesses
+            // are slow; scripts/probe/unaligned_store.hip)
             const int64_t G1 = G0 + total;
-            if (ringable && !(a.debug & 128)) {
-                // per 64-row group: each lane copies its row into the ring with
-                // unaligned 16/8/4/2/1-byte LDS moves, then the wave stores the
-                // complete 16-byte blocks; a partial last block moves to ring[0]
-                uint8_t* ring = reinterpret_cast<uint8_t*>(S.ring);
-                const uint8_t* cb = reinterpret_cast<const uint8_t*>(dwa);
-                int64_t RB = G0 & ~static_cast<int64_t>(15);  // output address of ring[0]
-                for (uint32_t g0 = 0; g0 < m; g0 += kWave) {
-                    const uint32_t r = g0 + lane();
-                    if (r < m && !(a.debug & 64)) {
-                        // aligned LDS moves only: head bytes up to a dword boundary of
-                        // the ring, dwords funnel-shifted from the dictionary, tail bytes
-                        const uint32_t s0 = S.off[r], ln = S.off[r + 1] - s0;
-                        const uint32_t p = static_cast<uint32_t>(G0 + s0 - RB);
-                        const uint32_t q = S.src[r] + kFront;
-                        const uint32_t h = min((4u - (p & 3u)) & 3u, ln);
-                        {  // head: up to 3 bytes, all loads issued together
-                            const uint32_t b0 = cb[q], b1 = cb[q + 1], b2 = cb[q + 2];
-                            if (h > 0) ring[p] = static_cast<uint8_t>(b0);
-                            if (h > 1) ring[p + 1] = static_cast<uint8_t>(b1);
-                            if (h > 2) ring[p + 2] = static_cast<uint8_t>(b2);
-                        }
-                        const uint32_t p2 = p + h, q2 = q + h, rem = ln - h;
-                        const uint32_t nd = rem >> 2, sh = q2 & 3u;
-                        uint32_t* rw = reinterpret_cast<uint32_t*>(ring) + (p2 >> 2);
-                        const uint32_t* sw = dwa + (q2 >> 2);
-                        // body: four ring dwords per step from five dictionary dwords
-                        for (uint32_t d2 = 0; d2 < nd; d2 += 4) {
-                            const uint32_t s0 = sw[d2], s1 = sw[d2 + 1], s2 = sw[d2 + 2], s3 = sw[d2 + 3],
-                                           s4 = sw[d2 + 4];
-                            rw[d2] = __builtin_amdgcn_alignbyte(s1, s0, sh);
-                            if (d2 + 1 < nd) rw[d2 + 1] = __builtin_amdgcn_alignbyte(s2, s1, sh);
-                            if (d2 + 2 < nd) rw[d2 + 2] = __builtin_amdgcn_alignbyte(s3, s2, sh);
-                            if (d2 + 3 < nd) rw[d2 + 3] = __builtin_amdgcn_alignbyte(s4, s3, sh);
-                        }
-                        {  // tail: up to 3 bytes
-                            const uint32_t t = rem & 3u, pt = p2 + 4 * nd, qt = q2 + 4 * nd;
-                            const uint32_t b0 = cb[qt], b1 = cb[qt + 1], b2 = cb[qt + 2];
-                            if (t > 0) ring[pt] = static_cast<uint8_t>(b0);
-                            if (t > 1) ring[pt + 1] = static_cast<uint8_t>(b1);
-                            if (t > 2) ring[pt + 2] = static_cast<uint8_t>(b2);
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    const bool last = g0 + kWave >= m;
-                    const int64_t gend = G0 + S.off[min(g0 + kWave, m)];
-                    const uint32_t nfull = static_cast<uint32_t>((gend - RB) >> 4);
-                    const uint32_t nblk = last ? static_cast<uint32_t>((gend - RB + 15) >> 4) : nfull;
-                    for (uint32_t b = lane(); b < nblk && !(a.debug & 32); b += kWave) {
-                        const uint4 v = S.ring[b];
-                        const int64_t blk = RB + 16 * static_cast<int64_t>(b);
-                        if (blk >= G0 && blk + 16 <= G1) {
-                            *reinterpret_cast<uint4*>(a.chars + blk) = v;
-                        } else {
-                            const uint32_t ow[4] = {v.x, v.y, v.z, v.w};
-                            const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
-                            for (int64_t x = gs; x < ge; x++) {
-                                const uint32_t at = static_cast<uint32_t>(x - blk);
-                                a.chars[x] = static_cast<uint8_t>(ow[at >> 2] >> (8 * (at & 3)));
-                            }
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    if (!last) {
-                        if (lane() == 0 && nfull) S.ring[0] = S.ring[nfull];
-                        RB += 16 * static_cast<int64_t>(nfull);
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    }
+            for (uint32_t g0 = 0; g0 < m; g0 += kWave) {
+                const uint32_t r = g0 + lane();
+                uint32_t s0 = 0, ln = 0, sa = 0;
+                if (r < m) {
+                    s0 = S.off[r];
+                    ln = S.off[r + 1] - s0;
+                    sa = kFront + S.src[r];
                 }
-                continue;
-            }
-            // long strings: pull each 16-byte block from the rows it spans
-            const int64_t B0 = G0 >> 4;
-            const uint32_t nb = static_cast<uint32_t>(((G1 - 1) >> 4) - B0 + 1);
-            const uint32_t mis = static_cast<uint32_t>(G0 & 15);
-            for (uint32_t w0 = 0; w0 < nb; w0 += kWin) {
-                const uint32_t w1 = min(nb, w0 + kWin);
-                for (uint32_t r = lane(); r < m; r += kWave) {
-                    const uint32_t s0 = S.off[r], e0 = S.off[r + 1];
-                    if (e0 <= s0) continue;
-                    uint32_t blo = s0 == 0 ? 0u : (s0 + mis + 15) / 16;
-                    uint32_t bhi = (e0 + mis + 15) / 16 - 1;
-                    blo = max(blo, w0);
-                    bhi = min(bhi, w1 - 1);
-                    for (uint32_t b = blo; b <= bhi; b++) S.brow[b - w0] = static_cast<uint16_t>(r);
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                for (uint32_t b = w0 + lane(); b < w1; b += kWave) {
-                    const int32_t a0 = static_cast<int32_t>(b * 16) - static_cast<int32_t>(mis);
-                    uint32_t r = S.brow[b - w0];
-                    uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0;
-                    for (;;) {
-                        const uint32_t rs = S.off[r], re = S.off[r + 1];
-                        const int32_t lo = max(static_cast<int32_t>(rs) - a0, 0);
-                        const int32_t hi = min(static_cast<int32_t>(re) - a0, 16);
-                        if (hi > lo) {
-                            const uint32_t base = S.src[r] + kFront + static_cast<uint32_t>(a0 - static_cast<int32_t>(rs));
-                            const U16B v = *reinterpret_cast<const U16B*>(reinterpret_cast<const uint8_t*>(dwa) + base);
-                            auto bm = [](int32_t x) -> uint32_t {  // bytes [0, x) of a dword, x clamped to 0..4
-                                return x <= 0 ? 0u : (x >= 4 ? 0xFFFFFFFFu : ((1u << (8 * x)) - 1u));
-                            };
-                            o0 |= v.x & (bm(hi) & ~bm(lo));
-                            o1 |= v.y & (bm(hi - 4) & ~bm(lo - 4));
-                            o2 |= v.z & (bm(hi - 8) & ~bm(lo - 8));
-                            o3 |= v.w & (bm(hi - 12) & ~bm(lo - 12));
+                const bool lng = ln > kLongRow;
+                if (!lng && ln) {
+                    uint8_t* d = a.chars + G0 + s0;
+                    if (ln >= 16) {
+                        for (uint32_t x = 0; x + 16 < ln; x += 16) {
+                            const uint4 v = lds16(dwa, sa + x);
+                            *reinterpret_cast<U16B*>(d + x) = U16B{v.x, v.y, v.z, v.w};
                         }
-                        if (static_cast<int32_t>(re) >= a0 + 16 || r + 1 >= m) break;
-                        r++;
-                    }
-                    const int64_t blk = (B0 + b) << 4;
-                    if (blk >= G0 && blk + 16 <= G1) {
-                        *reinterpret_cast<uint4*>(a.chars + blk) = make_uint4(o0, o1, o2, o3);
+                        const uint4 v = lds16(dwa, sa + ln - 16);
+                        *reinterpret_cast<U16B*>(d + ln - 16) = U16B{v.x, v.y, v.z, v.w};
                     } else {
-                        const uint32_t ow[4] = {o0, o1, o2, o3};
-                        const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
-                        for (int64_t x = gs; x < ge; x++) {
-                            const uint32_t at = static_cast<uint32_t>(x - blk);
-                            a.chars[x] = static_cast<uint8_t>(ow[at >> 2] >> (8 * (at & 3)));
+                        const uint4 v = lds16(dwa, sa);           // bytes 0 .. 15 of the row's source
+                        const uint32_t t = ln >= 8 ? ln - 8 : (ln >= 4 ? ln - 4 : (ln >= 2 ? ln - 2 : 0u));
+                        const uint4 u = lds16(dwa, sa + t);       // bytes t .. t + 15
+                        if (ln >= 8) {
+                            *reinterpret_cast<U8B*>(d) = U8B{v.x, v.y};
+                            *reinterpret_cast<U8B*>(d + t) = U8B{u.x, u.y};
+                        } else if (ln >= 4) {
+                            *reinterpret_cast<U4B*>(d) = U4B{v.x};
+                            *reinterpret_cast<U4B*>(d + t) = U4B{u.x};
+                        } else if (ln >= 2) {
+                            *reinterpret_cast<U2B*>(d) = U2B{static_cast<uint16_t>(v.x)};
+                            *reinterpret_cast<U2B*>(d + t) = U2B{static_cast<uint16_t>(u.x)};
+                        } else {
+                            d[0] = static_cast<uint8_t>(v.x);
                         }
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                uint64_t lm = __ballot(lng);
+                while (lm) {  // long rows: the whole wave, aligned destination blocks
+                    const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
+                    lm &= lm - 1;
+                    const int64_t A0 = G0 + __builtin_amdgcn_readlane(s0, l);
+                    const int64_t A1 = A0 + __builtin_amdgcn_readlane(ln, l);
+                    const uint32_t src0 = __builtin_amdgcn_readlane(sa, l);
+                    const int64_t b0 = A0 & ~static_cast<int64_t>(15);
+                    for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < A1; blk += 16 * kWave) {
+                        const uint4 v = lds16(dwa, static_cast<uint32_t>(src0 + (blk - A0)));
+                        store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, A0) - blk),
+                                   static_cast<uint32_t>(min(blk + 16, A1) - blk));
+                    }
+                }
             }
+            (void)G1;
+        }
         }
     }
 }

@@ -35,7 +35,7 @@ chunks = [F.chunk(0, 0)]
 ctx = capi.Context(0)
 
 
-def setp(path, dbg=0, waves=0, bbytes=12288, claim=1, rp=32):
+def setp(path, dbg=0, waves=0, bbytes=12288, claim=1, rp=32, wmode=0):
     ctx.set_option("pipe_run_pages", rp)
     ctx.set_option("dict_pipe", int(path == "pipe"))
     ctx.set_option("fused_claim", claim)
@@ -51,7 +51,7 @@ variants = [("pipe", 0, 0, 12288, 1), ("pipe", 2, 0, 12288, 1), ("pipe", 4, 0, 1
 if "codes" in sys.argv:
     variants = [("pipe", d, 0, 12288, 1) for d in (0, 512, 1024)]
 if "write" in sys.argv:
-    variants = [("pipe", d, 0, 12288, 1) for d in (0, 2, 128, 128 | 32)]
+    variants = [("pipe", d, 0, 12288, 1, 32, wm) for wm in (0,) for d in (0, 2, 4, 6)]
 if "runpages" in sys.argv:
     variants = [("pipe", 0, 0, 12288, 1, rp) for rp in (32, 16, 8, 4)]
 if "big" in sys.argv:  # k_pipe_big phases (arrow layout): jump table, walk, records, def levels, all
@@ -61,7 +61,8 @@ if "batch" in sys.argv:
 for v in variants:
     path, dbg, waves, bb, claim = v[:5]
     rp = v[5] if len(v) > 5 else 32
-    setp(path, 0, waves, bb, claim, rp)
+    wm = v[6] if len(v) > 6 else 0
+    setp(path, 0, waves, bb, claim, rp, wm)
     dc = ctx.upload(f, chunks)
     dc.decode_async()  # valid intermediate buffers before any ablation bit is set
     ctx.sync()
@@ -79,7 +80,7 @@ for v in variants:
         if n:
             res[k] = round(ms / n, 4)
     ctx.timing(False)
-    print(json.dumps({"path": path, "debug": dbg, "waves": waves, "batch_bytes": bb, "claim": claim, "run_pages": rp,
+    print(json.dumps({"path": path, "debug": dbg, "write_mode": wm, "waves": waves, "batch_bytes": bb, "claim": claim, "run_pages": rp,
                       "ms": res}),
           flush=True)
     dc.free()

@@ -358,3 +358,4 @@ def test_c2_full_size_properties(ctx, layout):
     got = hashlib.sha256(capi.canonical_dump(host)).hexdigest()
     exp = hashlib.sha256(gen.values_dump(cols[0], 0, n, 0, gen.CONFIG_SEEDS["C2"])).hexdigest()
     assert got == exp
+
