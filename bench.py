@@ -31,8 +31,9 @@ for _p in (ROOT, PKG):
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel timers (HIP events on the decode stream, capi.hip Timed)
-KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_count", "pipe_codes", "pipe_write", "ba_batch",
-           "ba_fused", "ba_rows", "scan", "ba_gather")
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "pipe_count", "pipe_codes", "pipe_write",
+           "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather")
+REGEX_KERNELS = ("regex_dict", "regex_codes", "regex_lanes", "regex_plain", "regex_pages")
 ROWS = 10_000_000
 
 
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--c4-rows", type=int, default=ROWS)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--c5-rgs", type=int, default=4, help="C5 row groups of 10M rows per GPU (1B rows / 8 GPUs = 12.5)")
     return ap.parse_args()
 
 
@@ -265,6 +268,11 @@ def main():
                         "ms_per_row_group": total_ms, "columns": cols, "layout": "arrow"}
         del cfile
 
+    # ── C5: C2's distribution, arrow layout, one dictionary per
+    #    10M-row row group, decode + dictionary-first regex, row groups per GPU
+    if not args.no_c5:
+        result["c5"] = _c5_leg(ctx, args, barrier, dist, local, world, my_rgs[0])
+
     # ── CPU baseline beside it (rank 0, N=1 only) ──────────────────────────
     if rank == 0 and world == 1 and not args.no_cpu:
         sample = gen.build(gen.c2_cols(), 1_000_000, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
@@ -307,6 +315,82 @@ def _time_decode(ctx, dc, steps, barrier, dist, local, world):
             kern[name] = ms / n
     return {"ms_per_decode": el / steps * 1e3, "values_per_s": dc.num_rows * steps * world / el,
             "payload_bytes": dc.payload_bytes, "kernel_ms": kern}
+
+
+def _c5_leg(ctx, args, barrier, dist, local, world, rg0):
+    """C5 at --c5-rgs row groups of 10M rows per GPU: every row group is its
+    own chunk (ColumnReader is per chunk; each has its own dictionary page).
+    One step = decode all of them + the regex page filter over all of them
+    (dictionary-first: the pattern runs on each dictionary, then pages are
+    tested through their indices)."""
+    from pqgpu import capi, gen
+    rows = 10_000_000
+    f = gen.build(gen.c2_cols(), rows, args.c5_rgs, seed=gen.CONFIG_SEEDS["C5"], layout=gen.ARROW_LAYOUT,
+                  first_rg=rg0 * args.c5_rgs)
+    F = capi.File(f)
+    dcs = [ctx.upload(f, [F.chunk(rg, 0)]) for rg in range(F.num_row_groups)]
+    del f
+    for dc in dcs:
+        dc.decode()
+        dc.regex_pages(args.pattern)
+    steps = max(2, args.steps // 4)
+
+    def timed(fn, check):
+        fn()
+        ctx.sync()
+        ctx.timing(True)
+        ctx.timing_reset()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        ctx.sync()
+        t1 = time.perf_counter()
+        barrier()
+        ctx.timing(False)
+        check()
+        el = t1 - t0
+        if dist is not None:
+            import torch
+            t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        kern = {}
+        for name in KERNELS + REGEX_KERNELS:
+            ms, n = ctx.timing_get(name)
+            if n:
+                kern[name] = ms / steps  # all launches of one step
+        return el / steps, kern
+
+    def dec():
+        for dc in dcs:
+            dc.decode_async()
+
+    def dec_check():
+        for dc in dcs:
+            dc.decode_check()
+
+    def rx():
+        for dc in dcs:
+            dc.regex_pages_async(args.pattern)
+
+    def rx_check():
+        for dc in dcs:
+            dc.regex_pages_result()
+
+    dsec, dkern = timed(dec, dec_check)
+    rsec, rkern = timed(rx, rx_check)
+    nrows = sum(dc.num_rows for dc in dcs)
+    npages = sum(dc.num_pages for dc in dcs)
+    reported = int(sum(int(dc.regex_pages(args.pattern).sum()) for dc in dcs))
+    for dc in dcs:
+        dc.free()
+    return {"rows_per_gpu": nrows, "row_groups_per_gpu": len(dcs), "pages_per_gpu": npages, "layout": "arrow",
+            "decode_values_per_s": nrows * world / dsec, "decode_ms": dsec * 1e3,
+            "regex_pages_per_s": npages * world / rsec, "regex_ms": rsec * 1e3, "pattern": args.pattern,
+            "reported_pages": reported,
+            "step_values_per_s": nrows * world / (dsec + rsec),
+            "kernel_ms_per_step": {**dkern, **rkern}}
 
 
 def _cpu_model():

@@ -49,6 +49,7 @@ struct pq_ctx {
     int opt_batch_bytes = 12288; // "batch_bytes": payload bytes per batch buffer
     bool opt_regex_dfa = true;   // "regex_dfa": DFA kernels (else the NFA kernel)
     bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
+    bool opt_regex_codes = true; // "regex_codes": dictionary chunks on the pipe path: match bits over the decode's codes
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
@@ -106,6 +107,7 @@ struct pq_chunk {
     std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
     int32_t* d_bigp = nullptr;
     uint32_t big_max_bytes = 0;
+    int32_t pipe_entry_base = 0;        // entry-table slot of the pipe dictionary's first entry
     // PLAIN BYTE_ARRAY, REQUIRED (plain_ba.hip)
     bool plain = false;
     std::vector<pqk::DevBatch> hpwins;
@@ -345,6 +347,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->hbig = std::move(big);
     c->big_max_bytes = big_bytes;
     c->pipe_dict = dict_id;
+    c->pipe_entry_base = d.entry_base;
     c->pipe_dict_chars_bytes = chars_bytes;
     c->pipe_dict_bytes = dict_bytes;
     c->pipe_lds = pl.lds;
@@ -541,6 +544,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     }
     if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
+    if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
@@ -866,6 +870,54 @@ static void launch_gather(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
                           out->d_values);
 }
 
+// Launch parameters of the three-pass dictionary path (dict_pipe.hip); `out`
+// may be null when only the codes are wanted (regex page filter).
+static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
+    pqk::PipeLaunch P{};
+    P.bytes = c->d_bytes; P.pages = c->d_pages; P.npages = c->npages; P.tiles = c->d_tiles;
+    P.ntiles = c->ntiles; P.page_tile0 = c->d_page_tile0; P.max_def = c->max_def; P.max_rep = c->max_rep;
+    P.dicts = c->d_dicts; P.dict_id = c->pipe_dict; P.entries = c->d_entries; P.dict_count = c->d_dict_count;
+    P.runs = c->d_runs; P.info = c->d_info; P.flist = c->d_flist; P.tile_nn = c->d_tile_nn; P.codes = c->d_codes;
+    P.tile_chars = c->d_tile_chars; P.bsum = c->d_bsum; P.total = c->d_total;
+    P.nrows_total = c->nrows; P.overflow = c->d_flags + 1;
+    if (out) {
+        P.capacity = out->capacity_bytes;
+        P.validity = out->d_validity; P.offsets = out->d_offsets; P.chars = out->d_values;
+    }
+    P.page_err = c->d_page_err; P.err_any = c->d_flags;
+    P.dict_chars_bytes = c->pipe_dict_chars_bytes; P.dict_bytes = c->pipe_dict_bytes; P.lds = c->pipe_lds;
+    P.grid = c->pipe_grid;
+    P.debug = ctx->opt_debug;
+    P.dict_entries_cap = c->pipe_ecap;
+    P.cus = c->pipe_cus;
+    P.has_small = c->pipe_small;
+    return P;
+}
+
+// Run tables and per-row codes (k_pipe_runs, k_pipe_big, k_pipe_codes2,
+// k_pipe_exact).  With dict_on_side the dictionary decodes on ctx->side and
+// the codes wait for it (ev_join).
+static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side) {
+    hipStream_t s = ctx->stream;
+    {
+        Timed t(ctx, "pipe_runs");
+        pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
+                              c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist);
+    }
+    if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
+    (void)hipMemsetAsync(c->d_bsum, 0, static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long), s);
+    if (!c->hbig.empty()) {
+        Timed t(ctx, "pipe_big");
+        pqk::launch_pipe_big(s, P, c->d_bigp, static_cast<int>(c->hbig.size()), c->big_max_bytes);
+    }
+    if (c->pipe_count) {
+        Timed t(ctx, "pipe_count");
+        pqk::launch_pipe_codes(s, P, true);
+    }
+    Timed t(ctx, "pipe_codes");
+    pqk::launch_pipe_codes(s, P, false);
+}
+
 int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (!ctx || !c || !out) return PQ_ERR_ARG;
     if (c->type == PQ_BYTE_ARRAY) {
@@ -913,40 +965,8 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         Timed t(ctx, "plain_ba");
         pqk::launch_plain_ba(s, P);
     } else if (pipe) {
-        pqk::PipeLaunch P{};
-        P.bytes = c->d_bytes; P.pages = c->d_pages; P.npages = c->npages; P.tiles = c->d_tiles;
-        P.ntiles = c->ntiles; P.page_tile0 = c->d_page_tile0; P.max_def = c->max_def; P.max_rep = c->max_rep;
-        P.dicts = c->d_dicts; P.dict_id = c->pipe_dict; P.entries = c->d_entries; P.dict_count = c->d_dict_count;
-        P.runs = c->d_runs; P.info = c->d_info; P.flist = c->d_flist; P.tile_nn = c->d_tile_nn; P.codes = c->d_codes;
-        P.tile_chars = c->d_tile_chars; P.bsum = c->d_bsum; P.total = c->d_total;
-        P.nrows_total = c->nrows; P.capacity = out->capacity_bytes; P.overflow = c->d_flags + 1;
-        P.validity = out->d_validity; P.offsets = out->d_offsets; P.chars = out->d_values;
-        P.page_err = c->d_page_err; P.err_any = c->d_flags;
-        P.dict_chars_bytes = c->pipe_dict_chars_bytes; P.dict_bytes = c->pipe_dict_bytes; P.lds = c->pipe_lds;
-        P.grid = c->pipe_grid;
-        P.debug = ctx->opt_debug;
-        P.dict_entries_cap = c->pipe_ecap;
-        P.cus = c->pipe_cus;
-        P.has_small = c->pipe_small;
-        {
-            Timed t(ctx, "pipe_runs");
-            pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
-                                  c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist);
-        }
-        if (c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
-        (void)hipMemsetAsync(c->d_bsum, 0, static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long), s);
-        if (!c->hbig.empty()) {
-            Timed t(ctx, "pipe_big");
-            pqk::launch_pipe_big(s, P, c->d_bigp, static_cast<int>(c->hbig.size()), c->big_max_bytes);
-        }
-        if (c->pipe_count) {
-            Timed t(ctx, "pipe_count");
-            pqk::launch_pipe_codes(s, P, true);
-        }
-        {
-            Timed t(ctx, "pipe_codes");
-            pqk::launch_pipe_codes(s, P, false);
-        }
+        const pqk::PipeLaunch P = pipe_launch(ctx, c, out);
+        pipe_front(ctx, c, P, true);
         if (c->ntiles == 0) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
             (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
@@ -1256,7 +1276,14 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
                                     c->d_dict_count, c->d_dict_match);
         }
-        if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {
+        if (c->pipe && ctx->opt_pipe && ctx->opt_regex_codes) {
+            // dictionary-first on the decode's own codes: the pattern ran on
+            // every entry above; the pipe passes give each row its index
+            const pqk::PipeLaunch P = pipe_launch(ctx, c, nullptr);
+            pipe_front(ctx, c, P, false);
+            Timed t(ctx, "regex_codes");
+            pqk::launch_pipe_match(s, P, c->d_dict_match + c->pipe_entry_base, neg, c->d_page_flags);
+        } else if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {
             (void)hipMemsetAsync(c->d_rwin_ticket, 0, sizeof(int32_t), s);
             Timed t(ctx, "regex_plain");
             pqre::launch_regex_plain(s, c->d_dfa, c->dfa_bytes, c->rwin_bytes, c->d_bytes, c->d_pages, c->d_rwins,

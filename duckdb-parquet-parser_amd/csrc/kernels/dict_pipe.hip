@@ -1415,6 +1415,36 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     }
 }
 
+// ── regex page filter over the codes (README.md:54-64, SURVEY §8a R-REGEX) ─
+// After k_pipe_runs / k_pipe_big / k_pipe_codes2 / k_pipe_exact: one wave per
+// tile tests its rows' codes against the dictionary's match bits (the pattern
+// ran once per entry, k_regex_dict).  A page whose tiles hold no non-null
+// value that matches (with --neg-regex: that fails to match) stays reported.
+// NULL rows and out-of-range indices (code 0xFFFF) never count.
+constexpr int kMatchWaves = 4;
+__global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match(const DevTile* __restrict__ tiles, int ntiles,
+                                                                 const DevPage* __restrict__ pages,
+                                                                 const uint16_t* __restrict__ codes,
+                                                                 const uint8_t* __restrict__ match, int neg,
+                                                                 uint8_t* __restrict__ page_flags) {
+    const int t = static_cast<int>(blockIdx.x) * kMatchWaves + static_cast<int>(threadIdx.x / kWave);
+    if (t >= ntiles) return;
+    const DevTile T = tiles[t];
+    const int64_t R0 = pages[T.page].first_row + T.row0;
+    const uint32_t m = static_cast<uint32_t>(T.nrows), l8 = lane() * 8;
+    bool hit = false;
+    if (l8 < m) {
+        const U16B v = *reinterpret_cast<const U16B*>(codes + R0 + l8);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t c = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+            hit |= l8 + k < m && c != kNull && ((match[c] != 0) != (neg != 0));
+        }
+    }
+    if (__ballot(hit) && lane() == 0) page_flags[T.page] = 0;
+}
+
 }  // namespace
 
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens) { return big_layout(max_page_bytes, nlens).total; }
@@ -1522,6 +1552,13 @@ void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_page
     }
     hipLaunchKernelGGL(k_pipe_big, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
                        const_cast<int32_t*>(P.flist), const_cast<uint32_t*>(P.info), nlens);
+}
+
+void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags) {
+    (void)hipMemsetAsync(page_flags, 1, static_cast<size_t>(P.npages), s);
+    if (P.ntiles <= 0) return;
+    hipLaunchKernelGGL(k_pipe_match, dim3((P.ntiles + kMatchWaves - 1) / kMatchWaves), dim3(kMatchWaves * kWave), 0, s,
+                       P.tiles, P.ntiles, P.pages, P.codes, match, neg, page_flags);
 }
 
 }  // namespace pqk

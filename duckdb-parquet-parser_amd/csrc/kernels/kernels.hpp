@@ -138,6 +138,9 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // then codes and tile characters (one workgroup per listed page)
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens);
 void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes);
+// regex page filter on the codes: page_flags[p] = 1 unless a non-null row of
+// page p matches (neg: fails to match); match = dictionary match bits
+void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags);
 
 // ── tile-parallel PLAIN fixed-width path (fixed_fast.hip) ──────────────────
 void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 PATTERNS = ["special.*requests", "^(carefully|quickly) ", "[0-9]", "e", "^$", "s$",
             "(ironic|bold) (foxes|ideas)", "a.{3}e", "[^a-z ]", r"\bx" if False else "ly\\s",
-            "qu?i(ck|et)ly", "^[a-z]{1,4} "]
+            "qu?i(ck|et)ly", "^[a-z]{1,4} ", "^[a-m]"]
 
 
 def golden_pages(f: bytes, chunks, pattern: str, neg: bool) -> np.ndarray:
@@ -50,24 +50,36 @@ CASES = [
     ("c2_dict_arrow", gen.c2_cols(), 20000, gen.ARROW_LAYOUT),
     ("c3_optional", [gen.Col("c", gen.COMMENT, gen.BYTE_ARRAY, optional=True, null_frac=0.3,
                              len_min=3, len_max=20)], 5000, gen.REF_LAYOUT),
+    # 20,000-row arrow pages (k_pipe_big on the codes path)
+    ("c2_dict_arrow_big", gen.c2_cols(), 50000, gen.ARROW_LAYOUT),
+    # short dictionary entries: "e", "s$", "a.{3}e" split the pages
+    ("dict_short", [gen.Col("w", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.2, dict_size=300,
+                            len_min=1, len_max=5, max_run=3)], 30000, gen.ARROW_LAYOUT),
+    # eight entries in runs of up to 3000 rows: "^[a-m]" splits the pages
+    ("dict_runs_big", [gen.Col("w", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.05, dict_size=8,
+                               len_min=1, len_max=3, max_run=3000)], 60000, gen.ARROW_LAYOUT),
 ]
 
 
-@pytest.fixture(params=["window", "lanes", "nfa"])
+@pytest.fixture(params=["window", "codes", "lanes", "nfa"])
 def kernel(request, ctx):
     """Every page kernel: windowed DFA (default for chunks without dictionary
-    pages), lane-per-page DFA (dictionary chunks) and wave-per-page NFA."""
+    pages), match bits over the pipe decode's codes (default for dictionary
+    chunks the pipe path takes), lane-per-page DFA (other dictionary chunks)
+    and wave-per-page NFA."""
     ctx.set_option("regex_dfa", int(request.param != "nfa"))
     ctx.set_option("regex_plain", int(request.param == "window"))
+    ctx.set_option("regex_codes", int(request.param in ("window", "codes")))
     yield request.param
     ctx.set_option("regex_dfa", 1)
     ctx.set_option("regex_plain", 1)
+    ctx.set_option("regex_codes", 1)
 
 
 @pytest.mark.parametrize("neg", [False, True], ids=["like", "notlike"])
 @pytest.mark.parametrize("name,cols,n,layout", CASES, ids=[c[0] for c in CASES])
 def test_regex_pages(ctx, kernel, name, cols, n, layout, neg):
-    f = gen.build(cols, n, 2, seed=7, layout=layout, rows_per_page=700)
+    f = gen.build(cols, n, 2, seed=7, layout=layout, rows_per_page=0 if name.endswith("_big") else 700)
     chunks = file_chunks(f, 0)
     dc = ctx.upload(f, chunks)
     for p in PATTERNS:
