@@ -55,6 +55,10 @@ __device__ __forceinline__ bool nfa_match(const DevProg& P, uint32_t n, B&& byte
     return (D & P.accept_end) != 0;
 }
 
+// One entry per thread, entries spread over gridDim.y workgroups per
+// dictionary; string bytes come 16 at a time (unaligned global loads; the
+// payload slot has >= 16 zero bytes after the page), not one load per byte.
+struct __attribute__((packed, aligned(1))) U16B { uint32_t x, y, z, w; };
 __global__ void __launch_bounds__(256) k_regex_dict(const DevProg* __restrict__ prog,
                                                     const uint8_t* __restrict__ bytes,
                                                     const DevDict* __restrict__ dicts,
@@ -66,11 +70,21 @@ __global__ void __launch_bounds__(256) k_regex_dict(const DevProg* __restrict__ 
     const DevDict d = dicts[blockIdx.x];
     const int32_t n = dict_count[blockIdx.x];
     const uint8_t* base = bytes + d.off;
-    for (int32_t k = threadIdx.x; k < n; k += blockDim.x) {
-        uint64_t e = entries[d.entry_base + k];
+    for (int32_t k = blockIdx.y * blockDim.x + threadIdx.x; k < n; k += blockDim.x * gridDim.y) {
+        const uint64_t e = entries[d.entry_base + k];
         const uint8_t* s = base + static_cast<uint32_t>(e);
-        uint32_t len = static_cast<uint32_t>(e >> 32);
-        dict_match[d.entry_base + k] = nfa_match(P, len, [&](uint32_t i) { return static_cast<uint32_t>(s[i]); });
+        const uint32_t len = static_cast<uint32_t>(e >> 32);
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, blk = ~0u;
+        dict_match[d.entry_base + k] = nfa_match(P, len, [&](uint32_t i) {
+            if ((i >> 4) != blk) {
+                blk = i >> 4;
+                const U16B v = *reinterpret_cast<const U16B*>(s + 16 * blk);
+                w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
+            }
+            const uint32_t q = (i >> 2) & 3u;
+            const uint32_t w = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
+            return (w >> (8 * (i & 3u))) & 0xFFu;
+        });
     }
 }
 
@@ -642,7 +656,7 @@ void launch_regex_dict(hipStream_t s, const DeviceProgram* prog, const uint8_t* 
                        const DevDict* dicts, int ndicts, const uint64_t* entries,
                        const int32_t* dict_count, uint8_t* dict_match) {
     if (ndicts <= 0) return;
-    hipLaunchKernelGGL(k_regex_dict, dim3(ndicts), dim3(256), 0, s, prog->d, bytes, dicts, entries,
+    hipLaunchKernelGGL(k_regex_dict, dim3(ndicts, 16), dim3(256), 0, s, prog->d, bytes, dicts, entries,
                        dict_count, dict_match);
 }
 
