@@ -309,7 +309,7 @@ def _time_decode(ctx, dc, steps, barrier, dist, local, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     kern = {}
-    for name in KERNELS + ("plain_ba", "fixed_plain", "fixed"):
+    for name in KERNELS + ("plain_spec", "plain_ba", "fixed_plain", "fixed"):
         ms, n = ctx.timing_get(name)
         if n:
             kern[name] = ms / n

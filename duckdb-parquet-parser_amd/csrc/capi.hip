@@ -54,6 +54,7 @@ struct pq_ctx {
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
+    bool opt_plain_rows = false; // "plain_rows": rows pass one lane per page from HBM (k_plain_rows), else k_plain_walk (LDS windows)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
 };
 
@@ -116,6 +117,18 @@ struct pq_chunk {
     int64_t* d_wchars = nullptr;
     unsigned long long* d_pbsum = nullptr;
     int plain_grid = 0;
+    // pages larger than a window: speculative chunk chains (plain_ba.hip k_plain_spec)
+    bool plain_spec = false, spec_failed = false;
+    std::vector<int32_t> hchunk_base;
+    std::vector<uint2> hchunks;
+    int32_t* d_chunk_base = nullptr;
+    uint2* d_chunks = nullptr;
+    uint4* d_cand = nullptr;
+    DevPage* d_ppages = nullptr;
+    DevErr* d_perr = nullptr;
+    pq_column* last_out = nullptr;      // output of the last pq_decode_async (collect re-runs into it)
+    std::vector<int32_t> hunit_win;     // page (or chunk, spec path) -> its window (k_plain_rows)
+    int32_t* d_unit_win = nullptr;
     // tile-parallel PLAIN fixed-width decode (fixed_fast.hip)
     bool fixed_plain = false;
     int32_t* d_tile_rank = nullptr;
@@ -286,6 +299,12 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_bsum);
     dfree(c->d_flist);
     dfree(c->d_bigp);
+    dfree(c->d_chunk_base);
+    dfree(c->d_unit_win);
+    dfree(c->d_chunks);
+    dfree(c->d_cand);
+    dfree(c->d_ppages);
+    dfree(c->d_perr);
     dfree(c->d_page_pos);
     dfree(c->d_tile_base);
     dfree(c->d_total);
@@ -360,30 +379,67 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
 // consecutive page slots of at most kPWin bytes.
 void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
     c->plain = false;
+    c->plain_spec = false;
     c->hpwins.clear();
+    c->hchunk_base.clear();
+    c->hchunks.clear();
+    c->hunit_win.clear();
     if (c->type != PQ_BYTE_ARRAY || c->max_def != 0 || c->max_rep != 0 || pages.empty()) return;
     auto slot = [](const DevPage& p) {
         return (static_cast<uint64_t>(std::max(p.size, 0)) + 15) / 16 * 16 + 16;
     };
-    for (const auto& pg : pages)
-        if (pg.mode != pqk::MODE_PLAIN || slot(pg) > pqk::kPWin || pg.nvals < 0) return;
-    size_t p = 0;
-    while (p < pages.size()) {
-        pqk::DevBatch b{};
-        b.p0 = static_cast<int32_t>(p);
-        b.img_lo = pages[p].off;
-        uint64_t hi = b.img_lo;
-        size_t q = p;
-        while (q < pages.size() && q - p < 64 && pages[q].off >= b.img_lo) {
-            const uint64_t e = pages[q].off + slot(pages[q]);
-            if (e - b.img_lo > pqk::kPWin) break;
-            hi = e;
-            q++;
+    bool big = false;
+    for (const auto& pg : pages) {
+        if (pg.mode != pqk::MODE_PLAIN || pg.nvals < 0) return;
+        big |= slot(pg) > pqk::kPWin;
+    }
+    if (big) {
+        // every page in kPChunk-byte chunks, windows of kPChunkGroup chunks
+        // (the pseudo pages k_plain_link writes, one per chunk)
+        if (pages.size() > (1u << 24)) return;
+        int64_t nch = 0;
+        for (size_t p = 0; p < pages.size(); p++) {
+            const uint32_t size = static_cast<uint32_t>(std::max(pages[p].size, 0));
+            const uint32_t k = std::max<uint32_t>(1, (size + pqk::kPChunk - 1) / pqk::kPChunk);
+            c->hchunk_base.push_back(static_cast<int32_t>(nch));
+            for (uint32_t i = 0; i < k; i++) {
+                c->hchunks.push_back(make_uint2(static_cast<uint32_t>(p), i));
+                c->hunit_win.push_back(static_cast<int32_t>(c->hpwins.size() + i / pqk::kPChunkGroup));
+            }
+            const uint64_t se = pages[p].off + slot(pages[p]);
+            for (uint32_t g = 0; g < k; g += pqk::kPChunkGroup) {
+                pqk::DevBatch b{};
+                b.p0 = static_cast<int32_t>(nch + g);
+                b.np = static_cast<int32_t>(std::min(pqk::kPChunkGroup, k - g));
+                b.img_lo = pages[p].off + static_cast<uint64_t>(g) * pqk::kPChunk;
+                b.img_bytes = static_cast<uint32_t>(std::min<uint64_t>(pqk::kPWin, se - b.img_lo));
+                c->hpwins.push_back(b);
+            }
+            nch += k;
+            if (nch > (1ll << 30)) return;
         }
-        b.np = static_cast<int32_t>(q - p);
-        b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
-        c->hpwins.push_back(b);
-        p = q;
+        c->hchunk_base.push_back(static_cast<int32_t>(nch));
+        c->plain_spec = true;
+    } else {
+        size_t p = 0;
+        while (p < pages.size()) {
+            pqk::DevBatch b{};
+            b.p0 = static_cast<int32_t>(p);
+            b.img_lo = pages[p].off;
+            uint64_t hi = b.img_lo;
+            size_t q = p;
+            while (q < pages.size() && q - p < 64 && pages[q].off >= b.img_lo) {
+                const uint64_t e = pages[q].off + slot(pages[q]);
+                if (e - b.img_lo > pqk::kPWin) break;
+                hi = e;
+                q++;
+            }
+            b.np = static_cast<int32_t>(q - p);
+            b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
+            for (size_t r = p; r < q; r++) c->hunit_win.push_back(static_cast<int32_t>(c->hpwins.size()));
+            c->hpwins.push_back(b);
+            p = q;
+        }
     }
     int cus = 256;
     hipDeviceProp_t prop;
@@ -545,6 +601,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
+    if (std::strcmp(key, "plain_rows") == 0) { ctx->opt_plain_rows = value != 0; return 0; }
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
@@ -744,6 +801,15 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc |= dalloc(&c->d_rowinfo, static_cast<size_t>(c->nrows) + 64);
             rc |= dalloc(&c->d_wchars, c->hpwins.size());
             rc |= dalloc(&c->d_pbsum, static_cast<size_t>(c->plain_grid));
+            rc |= dalloc(&c->d_unit_win, c->hunit_win.size());
+            if (c->plain_spec) {
+                const size_t nch = c->hchunks.size();
+                rc |= dalloc(&c->d_chunk_base, c->hchunk_base.size());
+                rc |= dalloc(&c->d_chunks, nch);
+                rc |= dalloc(&c->d_cand, nch * pqk::kPCand);
+                rc |= dalloc(&c->d_ppages, nch);
+                rc |= dalloc(&c->d_perr, nch);
+            }
         }
         if (c->fused && !c->hbatches.empty()) {
             rc |= dalloc(&c->d_batches, c->hbatches.size());
@@ -783,6 +849,13 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc = hip_check(ctx, hipMemcpyAsync(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc) (void)hipMemsetAsync(c->d_page_err, 0, std::max<size_t>(hpages.size(), 1) * sizeof(DevErr), s);
         if (!rc) (void)hipMemsetAsync(c->d_dict_err, 0, std::max<size_t>(hdicts.size(), 1) * sizeof(DevErr), s);
+        if (!rc && c->d_unit_win)
+            rc = hip_check(ctx, hipMemcpyAsync(c->d_unit_win, c->hunit_win.data(), c->hunit_win.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
+        if (!rc && c->d_chunks) {
+            rc = hip_check(ctx, hipMemcpyAsync(c->d_chunks, c->hchunks.data(), c->hchunks.size() * sizeof(uint2), hipMemcpyHostToDevice, s), "upload");
+            if (!rc) rc = hip_check(ctx, hipMemcpyAsync(c->d_chunk_base, c->hchunk_base.data(), c->hchunk_base.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
+            if (!rc) (void)hipMemsetAsync(c->d_perr, 0, c->hchunks.size() * sizeof(DevErr), s);
+        }
         if (!rc && c->d_bigp)
             rc = hip_check(ctx, hipMemcpyAsync(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc && c->d_pwins)
@@ -951,16 +1024,37 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
                                  c->d_dict_err, c->d_flags, c->type, c->plain_width);
     }
-    if (c->plain && ctx->opt_plain) {
+    c->last_out = out;
+    if (c->plain && ctx->opt_plain && !(c->plain_spec && c->spec_failed)) {
         pqk::PlainLaunch P{};
         P.bytes = c->d_bytes; P.pages = c->d_pages; P.wins = c->d_pwins;
         P.nwins = static_cast<int32_t>(c->hpwins.size()); P.rowinfo = c->d_rowinfo; P.wchars = c->d_wchars;
         P.bsum = c->d_pbsum; P.grid = c->plain_grid; P.nrows_total = c->nrows; P.total = c->d_total;
         P.capacity = out->capacity_bytes; P.overflow = c->d_flags + 1; P.validity = out->d_validity;
         P.offsets = out->d_offsets; P.chars = out->d_values; P.page_err = c->d_page_err; P.err_any = c->d_flags;
+        if (ctx->opt_plain_rows) {  // lane per page (k_plain_rows) instead of lane per page within a window wave
+            P.unit_win = c->d_unit_win;
+            P.nunits = c->plain_spec ? static_cast<int32_t>(c->hchunks.size()) : c->npages;
+        }
         if (c->nrows == 0) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
             (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
+        }
+        if (c->plain_spec) {
+            // pseudo pages from speculative chunk chains; a fallback flag
+            // (d_flags[2]) skips the two passes and collect() re-runs the
+            // chunk on the generic path
+            pqk::SpecLaunch S{};
+            S.bytes = c->d_bytes; S.pages = c->d_pages; S.npages = c->npages; S.chunk_base = c->d_chunk_base;
+            S.chunks = c->d_chunks; S.nchunks = static_cast<int32_t>(c->hchunks.size()); S.cand = c->d_cand;
+            S.ppages = c->d_ppages; S.page_err = c->d_page_err; S.err_any = c->d_flags; S.fallback = c->d_flags + 2;
+            {
+                Timed t(ctx, "plain_spec");
+                pqk::launch_plain_spec(s, S);
+            }
+            P.pages = c->d_ppages;
+            P.page_err = c->d_perr;
+            P.gate = c->d_flags + 2;
         }
         Timed t(ctx, "plain_ba");
         pqk::launch_plain_ba(s, P);
@@ -1061,6 +1155,17 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (int rc = hip_check(ctx, hipMemcpyAsync(flags, c->d_flags, sizeof flags, hipMemcpyDeviceToHost, ctx->stream), "flags"))
         return rc;
     if (int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync")) return rc;
+    if (flags[2] && c->plain_spec && !c->spec_failed) {
+        // the speculative chunk chains did not resolve (strings longer than
+        // the candidate range or the window): this chunk takes the generic
+        // path from now on; decode it again
+        c->spec_failed = true;
+        if (c->npages) (void)hipMemsetAsync(c->d_page_err, 0, c->npages * sizeof(DevErr), ctx->stream);
+        if (!out) out = c->last_out;
+        if (!out) return set_err(ctx, PQ_ERR_ARG, "decode check without an output column");
+        if (int rc = pq_decode_async(ctx, c, out)) return rc;
+        return collect(ctx, c, out);
+    }
     int64_t best_seq = c->walk_error ? c->walk_error_seq : INT64_MAX;
     int best_code = c->walk_error;
     std::string best_msg = c->walk_message;
@@ -1094,13 +1199,7 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             if (dalloc(&out->d_values, static_cast<size_t>(total + 64)))
                 return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (chars)");
             out->capacity_bytes = total;
-            if (c->fused) {
-                if (int rc = pq_decode_async(ctx, c, out)) return rc;
-            } else {
-                (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), ctx->stream);
-                (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, ctx->stream);
-                launch_gather(ctx, c, out);
-            }
+            if (int rc = pq_decode_async(ctx, c, out)) return rc;  // every path writes the whole column
             return hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync");
         }
     } else if (out) {

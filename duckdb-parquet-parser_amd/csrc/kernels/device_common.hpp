@@ -87,6 +87,34 @@ __device__ inline void stage_page(uint32_t* lds, const uint8_t* g, uint32_t size
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 }
 
+// ── bulk copies: kU loads in flight per thread ────────────────────────────
+// dst[i] = f(src[i]) for i = t, t + nt, ... < n.  A plain strided loop makes
+// each iteration wait for its own load before the next is issued (one HBM
+// latency per iteration, vmcnt(0) before the LDS store); batching kU loads
+// before their stores pays one latency per batch.
+template <int kU = 8, class D, class S, class F>
+__device__ __forceinline__ void copy_map(D* __restrict__ dst, const S* __restrict__ src, uint32_t n, uint32_t t,
+                                         uint32_t nt, F&& f) {
+    for (uint32_t i0 = t; i0 < n; i0 += kU * nt) {
+        S v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t i = i0 + static_cast<uint32_t>(u) * nt;
+            if (i < n) v[u] = src[i];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t i = i0 + static_cast<uint32_t>(u) * nt;
+            if (i < n) dst[i] = f(v[u]);
+        }
+    }
+}
+template <int kU = 8, class T>
+__device__ __forceinline__ void copy_blocks(T* __restrict__ dst, const T* __restrict__ src, uint32_t n, uint32_t t,
+                                            uint32_t nt) {
+    copy_map<kU>(dst, src, n, t, nt, [](const T& x) { return x; });
+}
+
 // ── hybrid RLE / bit-packed decoder: rle_decoder.hpp state machine ─────────
 struct Rle {
     uint32_t base;      // stream start (page byte offset)

@@ -399,7 +399,7 @@ __device__ void batch_produce(const BArgs& a, const BLayout& L, uint8_t* base, C
         {  // payload of the batch's pages, one contiguous image range
             const uint4* src = reinterpret_cast<const uint4*>(a.bytes + B.img_lo);
             uint4* dst = reinterpret_cast<uint4*>(buf + L.b_pay);
-            for (uint32_t i = lane(); i < B.img_bytes / 16; i += kWave) dst[i] = src[i];
+            copy_blocks(dst, src, B.img_bytes / 16, lane(), kWave);
         }
         __builtin_amdgcn_wave_barrier();
         P.mark(BP_STAGE);
@@ -860,11 +860,10 @@ __global__ void __launch_bounds__(1024) k_ba_batch(BArgs a) {
         dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
         uint4* dst = reinterpret_cast<uint4*>(dwords);
-        for (uint32_t i = threadIdx.x; i < a.dict_chars_bytes / 16; i += blockDim.x) dst[i] = src[i];
-        for (uint32_t k = threadIdx.x; k < dict_n; k += blockDim.x) {
-            const uint64_t e = a.entries[d.entry_base + k];
-            dtab[k] = static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
-        }
+        copy_blocks(dst, src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
+        copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
+            return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
+        });
     }
     uint8_t* base = smem + a.dict_bytes;
     Ctrl* ctrl = reinterpret_cast<Ctrl*>(base + L.ctrl);

@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(kDictWaves * 64) k_dict_index(const uint8_t* _
         const uint4* src = reinterpret_cast<const uint4*>(page);
         uint4* dst = reinterpret_cast<uint4*>(words);
         const uint32_t n16 = (size + 15) / 16 + 1;
-        for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+        copy_blocks(dst, src, n16, threadIdx.x, blockDim.x);
     }
     __syncthreads();
     const uint32_t w = threadIdx.x / kWave, l = lane();
@@ -818,7 +818,7 @@ __global__ void __launch_bounds__(1024) k_ba_fused(FusedArgs a) {
         dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
         uint4* dst = reinterpret_cast<uint4*>(dwords);
-        for (uint32_t i = threadIdx.x; i < a.dict_chars_bytes / 16; i += blockDim.x) dst[i] = src[i];
+        copy_blocks(dst, src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
         for (uint32_t k = threadIdx.x; k < dict_n; k += blockDim.x) {
             uint64_t e = a.entries[d.entry_base + k];
             dtab[k] = static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);

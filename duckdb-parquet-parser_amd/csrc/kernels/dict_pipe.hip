@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
         const uint4* src = reinterpret_cast<const uint4*>(bytes + wlo);
         uint4* dst = reinterpret_cast<uint4*>(stage);
         const uint32_t nb = static_cast<uint32_t>((whi - wlo + 15) / 16) + 1;
-        for (uint32_t i = lane(); i < nb; i += kWave) dst[i] = src[i];
+        copy_blocks(dst, src, nb, lane(), kWave);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -462,8 +462,8 @@ __global__ void __launch_bounds__(kCodeWaves2 * 64) k_pipe_codes2(CodeArgs a, ui
     const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
     const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
     const uint32_t nl = min(dict_n, lt_n);
-    for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x)
-        lens[k] = static_cast<uint16_t>(a.entries[ebase + k] >> 32);
+    copy_map(lens, a.entries + ebase, nl, threadIdx.x, blockDim.x,
+             [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
     __syncthreads();
     const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
     // each wavefront owns a contiguous run of tiles; descriptors of up to 64
@@ -762,11 +762,10 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
         uint4* dst = reinterpret_cast<uint4*>(dw);
-        for (uint32_t i = threadIdx.x; i < a.dict_chars_bytes / 16; i += blockDim.x) dst[i] = src[i];
-        for (uint32_t k = threadIdx.x; k < dict_n; k += blockDim.x) {
-            const uint64_t e = a.entries[d.entry_base + k];
-            dtab[k] = static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
-        }
+        copy_blocks(dst, src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
+        copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
+            return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
+        });
     }
     __syncthreads();
     // each wavefront owns a contiguous run of tiles (consecutive rows): the
@@ -1195,9 +1194,8 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     auto in_stream = [&](uint32_t j) { return j >= ibase || (hasd && j >= dbase && j < dend); };
 
     // 0. the payload slot and the dictionary's entry lengths -> LDS
-    for (uint32_t i = tid; i < Ly.P / 16; i += kBigThreads)
-        reinterpret_cast<uint4*>(stw)[i] = reinterpret_cast<const uint4*>(page)[i];
-    for (uint32_t k = tid; k < nl; k += kBigThreads) lens[k] = static_cast<uint16_t>(a.entries[ebase + k] >> 32);
+    copy_blocks(reinterpret_cast<uint4*>(stw), reinterpret_cast<const uint4*>(page), Ly.P / 16, tid, kBigThreads);
+    copy_map(lens, a.entries + ebase, nl, tid, kBigThreads, [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
     if (tid < 8) sh[tid] = 0;
     __syncthreads();
     // 1. speculative headers at every byte of both streams

@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
         const uint4* src = reinterpret_cast<const uint4*>(page);
         uint4* dst = reinterpret_cast<uint4*>(stage);
         const uint32_t nb = (4 + dlen + 15) / 16 + 1;
-        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) dst[i] = src[i];
+        copy_blocks(dst, src, nb, threadIdx.x, blockDim.x);
     }
     __syncthreads();
     if (sh[0] == 0 && wv == 0) {

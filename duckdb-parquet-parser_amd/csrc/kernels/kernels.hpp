@@ -254,8 +254,35 @@ struct PlainLaunch {
     uint8_t* chars;
     DevErr* page_err;
     int32_t* err_any;
+    const int32_t* gate;         // non-null: skip everything when *gate != 0 (the spec path fell back)
+    const int32_t* unit_win;     // non-null: k_plain_rows, one lane per page, page -> its window
+    int32_t nunits;              // pages (or pseudo pages) for k_plain_rows
 };
 int plain_write_blocks_per_cu();
+
+// PLAIN BYTE_ARRAY pages larger than a window (plain_ba.hip k_plain_spec /
+// k_plain_link): each page is cut into kPChunk-byte chunks; the chunks' string
+// chains are found speculatively and linked per page into pseudo pages (one
+// per chunk, whole strings only) that k_plain_walk / k_plain_write decode in
+// windows of kPChunkGroup chunks.  Anything the link cannot resolve sets
+// *fallback and the host re-runs the chunk on the generic path.
+constexpr uint32_t kPChunk = 2048;
+constexpr uint32_t kPChunkGroup = 3;
+constexpr uint32_t kPCand = 4;  // candidate chain starts kept per chunk
+struct SpecLaunch {
+    const uint8_t* bytes;
+    const DevPage* pages;        // the real pages
+    int32_t npages;
+    const int32_t* chunk_base;   // per real page: its first chunk (npages + 1 entries)
+    const uint2* chunks;         // per chunk: real page, chunk number in the page
+    int32_t nchunks;
+    uint4* cand;                 // per chunk kPCand candidate records
+    DevPage* ppages;             // per chunk: the pseudo page
+    DevErr* page_err;            // per real page
+    int32_t* err_any;
+    int32_t* fallback;
+};
+void launch_plain_spec(hipStream_t s, const SpecLaunch& S);
 // REQUIRED PLAIN BYTE_ARRAY pages larger than min_size bytes: row codes and
 // tile characters for the generic gather (k_ba_rows skips these pages)
 void launch_plain_big_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, uint32_t min_size,

@@ -44,14 +44,14 @@ __global__ void __launch_bounds__(kWalkWaves * 64) k_plain_walk(PlainLaunch a) {
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[kWalkWaves][kPWin / 4 + 8];
     const int wv = static_cast<int>(threadIdx.x / kWave);
     const int w = static_cast<int>(blockIdx.x) * kWalkWaves + wv;
-    if (w >= a.nwins) return;
+    if (w >= a.nwins || (a.gate && *a.gate)) return;
     uint32_t* stage = stage_all[wv];
     const DevBatch W = a.wins[w];
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + W.img_lo);
         uint4* dst = reinterpret_cast<uint4*>(stage);
         const uint32_t nb = (W.img_bytes + 15) / 16 + 1;
-        for (uint32_t i = lane(); i < nb; i += kWave) dst[i] = src[i];
+        copy_blocks(dst, src, nb, lane(), kWave);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -89,6 +89,7 @@ struct PWLds {
 
 __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.gate && *a.gate) return;
     const int wv = static_cast<int>(threadIdx.x / kWave);
     PWLds& S = reinterpret_cast<PWLds*>(smem)[wv];
     const int per = a.per;
@@ -132,7 +133,7 @@ __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
             const uint4* src = reinterpret_cast<const uint4*>(a.bytes + W.img_lo);
             uint4* dst = reinterpret_cast<uint4*>(S.stage);
             const uint32_t nb = (W.img_bytes + 15) / 16 + 1;
-            for (uint32_t i = lane(); i < nb; i += kWave) dst[i] = src[i];
+            copy_blocks(dst, src, nb, lane(), kWave);
         }
         // validity: every row of a REQUIRED column is set
         {
@@ -274,7 +275,7 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_plain_big_rows(const uint8_t
             const uint4* src = reinterpret_cast<const uint4*>(page + ab);
             uint4* dst = reinterpret_cast<uint4*>(stage);
             const uint32_t nb = min((wlo - ab + wbytes + 15) / 16 + 1, kBigWin / 16 + 1);
-            for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) dst[i] = src[i];
+            copy_blocks(dst, src, nb, threadIdx.x, blockDim.x);
         }
         __syncthreads();
         const uint32_t wend = wlo + wbytes;
@@ -363,6 +364,233 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_plain_big_rows(const uint8_t
         tile_chars[t0 + static_cast<int32_t>(i)] = failed ? 0 : static_cast<int64_t>(tch[i]);
 }
 
+
+// ── pages larger than a window: speculative chunk chains ──────────────────
+// k_plain_spec: kSpecChunks kPChunk-byte chunks per wave, kPCand lanes per
+// chunk.  A string starts in a chunk's first 64 bytes (strings of <= 60
+// bytes); every offset whose u32 could be a length (it and its bytes fit in
+// the page) is a candidate, chunk 0's start the only one.  The first kPCand
+// candidates walk the length chain (read_plain_value, column_reader.cpp:
+// 249-253) from the HBM image (L2) until it leaves the chunk, recording where
+// it left, how many strings it read and its first bounds error.  For text the
+// false candidates die at once: four bytes of text are never a length that
+// fits in the page.
+constexpr int kSpecWaves = 4;
+constexpr int kSpecChunks = kWave / static_cast<int>(kPCand);  // chunks per wave
+constexpr int kSpecStageChunks = 4;                            // chunks staged in LDS at a time
+constexpr uint32_t kSpecStage = kSpecStageChunks * kPChunk + 32;
+
+__global__ void __launch_bounds__(kSpecWaves * 64) k_plain_spec(SpecLaunch a) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage_all[kSpecWaves][kSpecStage / 4];
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    const int cw = (static_cast<int>(blockIdx.x) * kSpecWaves + wv) * kSpecChunks;
+    if (cw >= a.nchunks) return;
+    uint32_t* stage = stage_all[wv];
+    const int j = static_cast<int>(lane() / kPCand), sl = static_cast<int>(lane() % kPCand);
+    // kSpecStageChunks chunks at a time: their bytes -> LDS (one image range
+    // when they belong to one page; otherwise read from HBM), candidate
+    // offsets one chunk per pass, then each chunk's kPCand lanes walk
+    for (int g0 = 0; g0 < kSpecChunks; g0 += kSpecStageChunks) {
+        const int ca = cw + g0, cb = min(a.nchunks, ca + kSpecStageChunks);
+        if (ca >= a.nchunks) break;
+        const uint2 cha = a.chunks[ca], chb = a.chunks[cb - 1];
+        const bool one_page = cha.x == chb.x;
+        const DevPage pga = a.pages[cha.x];
+        const uint32_t sa = cha.y * kPChunk;  // page byte at stage byte 0
+        if (one_page) {
+            const uint32_t sz = static_cast<uint32_t>(max(pga.size, 0));
+            const uint32_t se = min(chb.y * kPChunk + kPChunk, sz);
+            const uint32_t nb = se > sa ? (se - sa + 15) / 16 + 1 : 1u;
+            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + pga.off + sa);
+            uint4* dst = reinterpret_cast<uint4*>(stage);
+            copy_blocks(dst, src, nb, lane(), kWave);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint64_t mk = 0;  // this lane's chunk's candidate mask (lanes 4j .. 4j + 3 of chunk ca + j - g0)
+        for (int c = ca; c < cb; c++) {
+            const uint2 ch = a.chunks[c];
+            const DevPage pg = a.pages[ch.x];
+            const uint8_t* page = a.bytes + pg.off;
+            const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+            const uint32_t cs = ch.y * kPChunk, ce = min(cs + kPChunk, size), q = cs + lane();
+            bool plaus;
+            if (ch.y == 0) {
+                plaus = lane() == 0;
+            } else {
+                const uint32_t len = one_page ? st_u32(stage, q - sa) : gword(page, q);
+                plaus = q < ce && q + 4 <= size && static_cast<uint64_t>(q) + 4 + len <= size;
+            }
+            const uint64_t m = __ballot(plaus);
+            if (j == c - cw) mk = m;
+        }
+        const int c = cw + j;
+        if (j >= g0 && j < g0 + kSpecStageChunks && c < cb) {
+            uint64_t m = mk;
+            for (int i = 0; i < sl; i++) m &= m - 1;  // this lane's candidate: the sl-th set bit
+            uint4 rec = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+            if (m) {
+                const uint2 ch = a.chunks[c];
+                const DevPage pg = a.pages[ch.x];
+                const uint8_t* page = a.bytes + pg.off;
+                const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+                const uint32_t cs = ch.y * kPChunk, ce = min(cs + kPChunk, size);
+                const uint32_t q0 = cs + static_cast<uint32_t>(__builtin_ctzll(m));
+                uint32_t q = q0, cnt = 0, err = 0, need = 0;
+                while (q < ce) {
+                    if (q + 4 > size) { err = 1; need = 4; break; }
+                    const uint32_t len = one_page ? st_u32(stage, q - sa) : gword(page, q);
+                    if (static_cast<uint64_t>(q) + 4 + len > size) { err = 1; need = len; q += 4; break; }
+                    q += 4 + len;
+                    cnt++;
+                }
+                rec = make_uint4(q0 | (err << 31), q, cnt, need);
+            }
+            a.cand[static_cast<size_t>(c) * kPCand + sl] = rec;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// k_plain_link: one wave per page.  The page's candidate records are staged in
+// LDS; lane 0 follows the true chain chunk to chunk (the entry of chunk k is
+// where the chain left chunk k - 1), cuts it at the page's value count, and
+// records each chunk's chosen candidate and first row; then every lane writes
+// pseudo pages.  A bounds error before the value count is the page's error
+// record (the reference's ByteBuffer position and size).  An entry that is
+// not a candidate (a string longer than 60 bytes crossing a chunk edge) or a
+// chain leaving its window sets the fallback flag.
+constexpr uint32_t kLinkStage = 256;  // chunks per staging round
+
+__global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
+    __shared__ uint4 cand[kLinkStage * kPCand];
+    __shared__ uint32_t pick[kLinkStage];  // entry offset in the chunk | candidate << 16 (0xFFFF: none)
+    __shared__ uint32_t first[kLinkStage], take[kLinkStage];
+    const int p = blockIdx.x;
+    if (p >= a.npages) return;
+    const DevPage pg = a.pages[p];
+    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    const int32_t c0 = a.chunk_base[p], c1 = a.chunk_base[p + 1];
+    const uint32_t slot_end = (size + 15) / 16 * 16 + 16;
+    uint32_t q = 0, rows = 0, stop = 0, fb = 0;
+    for (int32_t cb = c0; cb < c1; cb += kLinkStage) {
+        const int32_t cend = min(c1, cb + static_cast<int32_t>(kLinkStage));
+        copy_blocks(cand, a.cand + static_cast<size_t>(cb) * kPCand, static_cast<uint32_t>(cend - cb) * kPCand, lane(), kWave);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane() == 0) {
+            for (int32_t c = cb; c < cend; c++) {
+                const uint32_t i = static_cast<uint32_t>(c - cb), k = static_cast<uint32_t>(c - c0);
+                const uint32_t chs = k * kPChunk;
+                uint32_t pk = 0xFFFFFFFFu, tk = 0;
+                first[i] = rows;
+                if (!stop && !fb && rows < n && q < chs + kPChunk && q < size) {
+                    const uint4 r0 = cand[i * kPCand], r1 = cand[i * kPCand + 1], r2 = cand[i * kPCand + 2],
+                                r3 = cand[i * kPCand + 3];
+                    const uint32_t e0 = r0.x & 0x7FFFFFFFu, e1 = r1.x & 0x7FFFFFFFu, e2 = r2.x & 0x7FFFFFFFu,
+                                   e3 = r3.x & 0x7FFFFFFFu;
+                    const int hit = (r0.x != 0xFFFFFFFFu && e0 == q) ? 0
+                                  : (r1.x != 0xFFFFFFFFu && e1 == q) ? 1
+                                  : (r2.x != 0xFFFFFFFFu && e2 == q) ? 2
+                                  : (r3.x != 0xFFFFFFFFu && e3 == q) ? 3 : -1;
+                    if (hit < 0) {
+                        fb = 1;
+                    } else {
+                        const uint4 r = hit == 0 ? r0 : (hit == 1 ? r1 : (hit == 2 ? r2 : r3));
+                        // the chunk's strings must lie inside its staged window
+                        const uint32_t g = k / kPChunkGroup;
+                        if (r.y > min(g * kPChunkGroup * kPChunk + kPWin, slot_end)) fb = 1;
+                        pk = (q - chs) | (static_cast<uint32_t>(hit) << 16);
+                        if (rows + r.z >= n) {  // the value count ends here: later bytes are never read
+                            tk = n - rows;
+                            stop = 1;
+                        } else if (r.x >> 31) {  // a bounds error before the value count
+                            DevErr* e = a.page_err + p;
+                            e->code = PQ_ERR_BUFFER;
+                            e->pos = static_cast<int32_t>(r.y);
+                            e->need = static_cast<int32_t>(r.w);
+                            e->size = static_cast<int32_t>(size);
+                            atomicOr(a.err_any, 1);
+                            tk = r.z;
+                            stop = 1;
+                        } else {
+                            tk = r.z;
+                            q = r.y;
+                        }
+                        rows += tk;
+                    }
+                }
+                pick[i] = pk;
+                take[i] = tk;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t i = lane(); i < static_cast<uint32_t>(cend - cb); i += kWave) {
+            const uint32_t k = static_cast<uint32_t>(cb - c0) + i, pk = pick[i];
+            const uint32_t ent = pk == 0xFFFFFFFFu ? 0u : (pk & 0xFFFFu);
+            DevPage pp{};
+            pp.mode = MODE_PLAIN;
+            pp.dict = -1;
+            pp.off = pg.off + k * kPChunk + ent;
+            pp.size = static_cast<int32_t>(size > k * kPChunk + ent ? size - k * kPChunk - ent : 0u);
+            pp.nvals = static_cast<int32_t>(take[i]);
+            pp.first_row = pg.first_row + first[i];
+            a.ppages[cb + static_cast<int32_t>(i)] = pp;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane() == 0) {
+        if (!fb && !stop && rows < n) {  // the chain ended before the value count: the read at q fails
+            DevErr* e = a.page_err + p;
+            e->code = PQ_ERR_BUFFER;
+            e->pos = static_cast<int32_t>(q);
+            e->need = 4;
+            e->size = static_cast<int32_t>(size);
+            atomicOr(a.err_any, 1);
+        }
+        if (fb) atomicOr(a.fallback, 1);
+    }
+}
+
+// k_plain_rows: one lane per page (or pseudo page), 64 per wave: the length
+// chain (column_reader.cpp:249-253) from the HBM image, each row's (position
+// in its window | length << 16) and the window's characters, filed under the
+// k_plain_write workgroup that writes it.  A chain that runs past its page is
+// the reference's ByteBuffer error at that position.
+constexpr int kRowsWaves = 4;
+
+__global__ void __launch_bounds__(kRowsWaves * 64) k_plain_rows(PlainLaunch a) {
+    if (a.gate && *a.gate) return;
+    const int u = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (u >= a.nunits) return;
+    const DevPage pg = a.pages[u];
+    const int w = a.unit_win[u];
+    const DevBatch W = a.wins[w];
+    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    const uint32_t base = static_cast<uint32_t>(pg.off - W.img_lo);
+    const uint8_t* page = a.bytes + pg.off;
+    uint32_t* ri = a.rowinfo + pg.first_row;
+    uint32_t pos = 0, k = 0;
+    unsigned long long chars = 0;
+    for (; k < n; k++) {
+        if (pos + 4 > size) { lane_err(a.page_err + u, a.err_any, pos, 4, size); break; }
+        const uint32_t len = gword(page, pos);
+        pos += 4;
+        if (static_cast<uint64_t>(pos) + len > size) { lane_err(a.page_err + u, a.err_any, pos, len, size); break; }
+        ri[k] = (base + pos) | (len << 16);
+        chars += len;
+        pos += len;
+    }
+    for (; k < n; k++) ri[k] = 0;  // a failed page: empty rows (the decode reports the error)
+    if (chars) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.wchars + w), chars);
+        atomicAdd(&a.bsum[(w / a.per) / kPWWaves], chars);
+    }
+}
+
 }  // namespace
 
 uint32_t plain_write_lds() { return kPWWaves * static_cast<uint32_t>(sizeof(PWLds)); }
@@ -399,8 +627,22 @@ void launch_plain_ba(hipStream_t s, PlainLaunch P) {
     plain_shape(P, &grid, &per);
     P.per = per;
     (void)hipMemsetAsync(P.bsum, 0, static_cast<size_t>(grid) * sizeof(unsigned long long), s);
-    hipLaunchKernelGGL(k_plain_walk, dim3((P.nwins + kWalkWaves - 1) / kWalkWaves), dim3(kWalkWaves * kWave), 0, s, P);
+    if (P.unit_win) {  // lane per page: rows and window characters (k_plain_rows)
+        (void)hipMemsetAsync(P.wchars, 0, static_cast<size_t>(P.nwins) * sizeof(int64_t), s);
+        if (P.nunits > 0)
+            hipLaunchKernelGGL(k_plain_rows, dim3((P.nunits + kRowsWaves * kWave - 1) / (kRowsWaves * kWave)),
+                               dim3(kRowsWaves * kWave), 0, s, P);
+    } else {
+        hipLaunchKernelGGL(k_plain_walk, dim3((P.nwins + kWalkWaves - 1) / kWalkWaves), dim3(kWalkWaves * kWave), 0, s, P);
+    }
     hipLaunchKernelGGL(k_plain_write, dim3(grid), dim3(kPWWaves * kWave), plain_write_lds(), s, P);
+}
+
+void launch_plain_spec(hipStream_t s, const SpecLaunch& S) {
+    if (S.nchunks <= 0) return;
+    const int per_block = kSpecWaves * kSpecChunks;
+    hipLaunchKernelGGL(k_plain_spec, dim3((S.nchunks + per_block - 1) / per_block), dim3(kSpecWaves * kWave), 0, s, S);
+    hipLaunchKernelGGL(k_plain_link, dim3(S.npages), dim3(kWave), 0, s, S);
 }
 
 }  // namespace pqk

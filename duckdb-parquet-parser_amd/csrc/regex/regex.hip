@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__
     {
         const uint4* src = reinterpret_cast<const uint4*>(dfa_img);
         uint4* dst = reinterpret_cast<uint4*>(dsm);
-        for (uint32_t i = threadIdx.x; i < dfa_bytes / 16; i += blockDim.x) dst[i] = src[i];
+        copy_blocks(dst, src, dfa_bytes / 16, threadIdx.x, blockDim.x);
     }
     __syncthreads();
     const DevDfa* D = reinterpret_cast<const DevDfa*>(dsm);
@@ -452,7 +452,7 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
     {
         const uint4* src = reinterpret_cast<const uint4*>(dfa_img);
         uint4* dst = reinterpret_cast<uint4*>(dsm);
-        for (uint32_t i = threadIdx.x; i < dfa_bytes / 16; i += blockDim.x) dst[i] = src[i];
+        copy_blocks(dst, src, dfa_bytes / 16, threadIdx.x, blockDim.x);
     }
     __syncthreads();
     const DevDfa* D = reinterpret_cast<const DevDfa*>(dsm);
@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
         {
             const uint4* src = reinterpret_cast<const uint4*>(bytes + B.img_lo);
             uint4* dst = reinterpret_cast<uint4*>(stage);
-            for (uint32_t i = lane(); i < B.img_bytes / 16; i += kWave) dst[i] = src[i];
+            copy_blocks(dst, src, B.img_bytes / 16, lane(), kWave);
             if (lane() == 0) { dst[B.img_bytes / 16] = make_uint4(0, 0, 0, 0); hit[0] = 0; hit[1] = 0; }
         }
         __builtin_amdgcn_wave_barrier();

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel decode timings for the SURVEY §8d configs C3 (PLAIN BYTE_ARRAY)
 and C4 (mixed INT64/DOUBLE/dict/plain, one 10M-row row group per column) on
-one GPU.  usage: decode_configs.py [rows]"""
+one GPU.  usage: decode_configs.py [rows] [config[:column],...]"""
 import json
 import os
 import sys
@@ -11,8 +11,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "duckdb-parquet-parser_amd")]
 from pqgpu import capi, gen  # noqa: E402
 
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+only = sys.argv[2].split(",") if len(sys.argv) > 2 else None  # e.g. "C4:c7,C3"
 ctx = capi.Context(0)
-KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "pipe_count", "pipe_codes", "pipe_write", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba")
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "plain_spec", "pipe_count", "pipe_codes", "pipe_write", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba")
 for name, cols, layout, seed in [("C2", gen.c2_cols(), gen.REF_LAYOUT, 2),
                                  ("C2a", gen.c2_cols(), gen.ARROW_LAYOUT, 2),
                                  ("C3", gen.c3_cols(), gen.REF_LAYOUT, 3),
@@ -20,6 +21,8 @@ for name, cols, layout, seed in [("C2", gen.c2_cols(), gen.REF_LAYOUT, 2),
     f = gen.build(cols, rows, 1, seed=seed, layout=layout)
     F = capi.File(f)
     for ci, c in enumerate(cols):
+        if only and name not in only and f"{name}:{c.name}" not in only:
+            continue
         dc = ctx.upload(f, [F.chunk(0, ci)])
         dc.decode()
         ctx.timing(True)

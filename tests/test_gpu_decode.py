@@ -35,21 +35,25 @@ SMALL = [
 ]
 
 
-@pytest.fixture(params=["pipe", "batch", "fused", "generic"])
+@pytest.fixture(params=["pipe", "walk", "batch", "fused", "generic"])
 def path(request, ctx):
     """Every kernel path: BYTE_ARRAY three-pass dictionary (dict_pipe.hip) and
-    two-pass PLAIN (plain_ba.hip),
-    batched dictionary (dict_batch.hip), per-page fused (dict_fused.hip) and
-    generic (decode.hip); fixed-width PLAIN tile-parallel (fixed_fast.hip)
-    except under "generic", which runs decode.hip's per-page k_fixed."""
-    ctx.set_option("dict_pipe", int(request.param == "pipe"))
-    ctx.set_option("plain_ba", int(request.param == "pipe"))
+    two-pass PLAIN (plain_ba.hip: rows one lane per page, or under "walk" one
+    wave per window), batched dictionary (dict_batch.hip), per-page fused
+    (dict_fused.hip) and generic (decode.hip); fixed-width PLAIN
+    tile-parallel (fixed_fast.hip) except under "generic", which runs
+    decode.hip's per-page k_fixed."""
+    pipe = request.param in ("pipe", "walk")
+    ctx.set_option("dict_pipe", int(pipe))
+    ctx.set_option("plain_ba", int(pipe))
+    ctx.set_option("plain_rows", int(request.param == "pipe"))
     ctx.set_option("fused_ba", int(request.param != "generic"))
     ctx.set_option("batch", int(request.param == "batch"))
     ctx.set_option("fixed_plain", int(request.param != "generic"))
     yield request.param
     ctx.set_option("dict_pipe", 1)
     ctx.set_option("plain_ba", 1)
+    ctx.set_option("plain_rows", 1)
     ctx.set_option("fused_ba", 1)
     ctx.set_option("batch", 0)
     ctx.set_option("fixed_plain", 1)
@@ -171,6 +175,28 @@ def _big_plain_file(seed, cut=None):
     return B.build_file(pages, gen.BYTE_ARRAY, False, total)
 
 
+def _spec_plain_file(seed, n=3000, cut=None, nvals=None, binary=False, pages=2, lmax=44):
+    """REQUIRED PLAIN BYTE_ARRAY pages of `n` short strings (16-100 KB: the
+    speculative chunk path); `cut` drops bytes from the end of the last page,
+    `nvals` overrides the header value count, `binary` draws string bytes from
+    0..255 (more plausible false chain starts)."""
+    rng = np.random.default_rng(seed)
+    out, total = [], 0
+    for k in range(pages):
+        lo, hi = (0, 256) if binary else (97, 123)
+        vals = [bytes(rng.integers(lo, hi, int(rng.integers(0, lmax + 1))).astype(np.uint8)) for _ in range(n)]
+        pay = B.plain_ba(vals)
+        nv = n
+        if k == pages - 1:
+            if cut:
+                pay = pay[:-cut]
+            if nvals is not None:
+                nv = nvals
+        out.append(B.data_header(len(pay), nv, 0) + pay)
+        total += nv
+    return B.build_file(out, gen.BYTE_ARRAY, False, total)
+
+
 def _opt_fixed_file(ptype, fmt, nvals, seed, rle_levels=False, drop=0):
     """One OPTIONAL PLAIN fixed-width page; `drop` trailing values removed
     from the payload (the read overruns on the last non-null rows)."""
@@ -219,6 +245,15 @@ CRAFTED = {
     # PLAIN BYTE_ARRAY pages larger than every LDS window: speculative chain
     # walk, strings longer than a slice's candidate range, a 50 KB string
     "plain_big": lambda: _big_plain_file(seed=21),
+    # PLAIN pages over a window: speculative chunk chains linked per page
+    "plain_spec": lambda: _spec_plain_file(seed=41),
+    "plain_spec_binary": lambda: _spec_plain_file(seed=42, binary=True),
+    "plain_spec_empty_strings": lambda: _spec_plain_file(seed=43, lmax=3, n=9000),
+    # fewer values declared than the page holds: later bytes are never read
+    "plain_spec_extra": lambda: _spec_plain_file(seed=44, nvals=2100),
+    "plain_spec_extra_trunc": lambda: _spec_plain_file(seed=45, nvals=1000, cut=500),
+    # 60-byte strings: chains entering chunks past the candidate range (fallback)
+    "plain_spec_long": lambda: _spec_plain_file(seed=46, lmax=120),
     # multi-byte varint run header (count 300)
     "long_rle_run": lambda: _dict_ba_file(bytes([2]) + B.rle(300, 2, 2), 300, DICT),
     # def levels + nulls, RLE and bit-packed level runs
@@ -289,6 +324,11 @@ ERRORS = {
                                               gen.BYTE_ARRAY, False, 4),
     # PLAIN BYTE_ARRAY page of 60 KB whose chain overruns in its second window
     "plain_big_overrun": lambda: _big_plain_file(seed=22, cut=40000),
+    # speculative chunk path: the last page's chain runs past its end
+    "plain_spec_trunc": lambda: _spec_plain_file(seed=47, cut=700),
+    "plain_spec_trunc_len": lambda: _spec_plain_file(seed=48, cut=2),
+    # more values declared than the page holds: the read at the page end fails
+    "plain_spec_short": lambda: _spec_plain_file(seed=49, nvals=3100),
     # def_len beyond the page
     "def_len_overrun": lambda: B.build_file([B.data_header(6, 3, 0) + struct.pack("<I", 50) + b"xy"], gen.INT32, True, 3),
     # dictionary page index stream without the bit-width byte
