@@ -1,3 +1,4 @@
+#include <cstdio>
 // capi.hip — implementation of the C ABI declared in include/pq_gpu.h.
 //
 // Host side of the boundary: the page walk runs on the CPU (pqfmt), page
@@ -1156,6 +1157,15 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         return rc;
     if (int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync")) return rc;
     if (flags[2] && c->plain_spec && !c->spec_failed) {
+        if (std::getenv("PQ_DEBUG_SPEC"))
+        {
+            std::fprintf(stderr, "plain spec fallback: flags %d (reason %d, chunk %d)\n", flags[2], flags[2] & 0xFF, flags[2] >> 8);
+            std::vector<uint4> cd(std::min<size_t>(c->hchunks.size(), 4) * pqk::kPCand);
+            (void)hipMemcpy(cd.data(), c->d_cand, cd.size() * sizeof(uint4), hipMemcpyDeviceToHost);
+            for (size_t i = 0; i < cd.size(); i++)
+                std::fprintf(stderr, "  cand chunk %zu slot %zu: entry %u err %u exit %u cnt %u w %u\n", i / pqk::kPCand,
+                             i % pqk::kPCand, cd[i].x & 0x7FFFFFFFu, cd[i].x >> 31, cd[i].y, cd[i].z, cd[i].w);
+        }
         // the speculative chunk chains did not resolve (strings longer than
         // the candidate range or the window): this chunk takes the generic
         // path from now on; decode it again

@@ -374,98 +374,101 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_plain_big_rows(const uint8_t
 // 249-253) from the HBM image (L2) until it leaves the chunk, recording where
 // it left, how many strings it read and its first bounds error.  For text the
 // false candidates die at once: four bytes of text are never a length that
-// fits in the page.
+// fits in the page.  Descriptors load once per wave (lane j: chunk j) and the
+// 16 chunks' candidate tests are issued together.
 constexpr int kSpecWaves = 4;
 constexpr int kSpecChunks = kWave / static_cast<int>(kPCand);  // chunks per wave
-constexpr int kSpecStageChunks = 4;                            // chunks staged in LDS at a time
-constexpr uint32_t kSpecStage = kSpecStageChunks * kPChunk + 32;
 
 __global__ void __launch_bounds__(kSpecWaves * 64) k_plain_spec(SpecLaunch a) {
-    __shared__ __attribute__((aligned(16))) uint32_t stage_all[kSpecWaves][kSpecStage / 4];
     const int wv = static_cast<int>(threadIdx.x / kWave);
     const int cw = (static_cast<int>(blockIdx.x) * kSpecWaves + wv) * kSpecChunks;
     if (cw >= a.nchunks) return;
-    uint32_t* stage = stage_all[wv];
-    const int j = static_cast<int>(lane() / kPCand), sl = static_cast<int>(lane() % kPCand);
-    // kSpecStageChunks chunks at a time: their bytes -> LDS (one image range
-    // when they belong to one page; otherwise read from HBM), candidate
-    // offsets one chunk per pass, then each chunk's kPCand lanes walk
-    for (int g0 = 0; g0 < kSpecChunks; g0 += kSpecStageChunks) {
-        const int ca = cw + g0, cb = min(a.nchunks, ca + kSpecStageChunks);
-        if (ca >= a.nchunks) break;
-        const uint2 cha = a.chunks[ca], chb = a.chunks[cb - 1];
-        const bool one_page = cha.x == chb.x;
-        const DevPage pga = a.pages[cha.x];
-        const uint32_t sa = cha.y * kPChunk;  // page byte at stage byte 0
-        if (one_page) {
-            const uint32_t sz = static_cast<uint32_t>(max(pga.size, 0));
-            const uint32_t se = min(chb.y * kPChunk + kPChunk, sz);
-            const uint32_t nb = se > sa ? (se - sa + 15) / 16 + 1 : 1u;
-            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + pga.off + sa);
-            uint4* dst = reinterpret_cast<uint4*>(stage);
-            copy_blocks(dst, src, nb, lane(), kWave);
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint64_t mk = 0;  // this lane's chunk's candidate mask (lanes 4j .. 4j + 3 of chunk ca + j - g0)
-        for (int c = ca; c < cb; c++) {
-            const uint2 ch = a.chunks[c];
-            const DevPage pg = a.pages[ch.x];
-            const uint8_t* page = a.bytes + pg.off;
-            const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
-            const uint32_t cs = ch.y * kPChunk, ce = min(cs + kPChunk, size), q = cs + lane();
-            bool plaus;
-            if (ch.y == 0) {
-                plaus = lane() == 0;
-            } else {
-                const uint32_t len = one_page ? st_u32(stage, q - sa) : gword(page, q);
-                plaus = q < ce && q + 4 <= size && static_cast<uint64_t>(q) + 4 + len <= size;
-            }
-            const uint64_t m = __ballot(plaus);
-            if (j == c - cw) mk = m;
-        }
-        const int c = cw + j;
-        if (j >= g0 && j < g0 + kSpecStageChunks && c < cb) {
-            uint64_t m = mk;
-            for (int i = 0; i < sl; i++) m &= m - 1;  // this lane's candidate: the sl-th set bit
-            uint4 rec = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
-            if (m) {
-                const uint2 ch = a.chunks[c];
-                const DevPage pg = a.pages[ch.x];
-                const uint8_t* page = a.bytes + pg.off;
-                const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
-                const uint32_t cs = ch.y * kPChunk, ce = min(cs + kPChunk, size);
-                const uint32_t q0 = cs + static_cast<uint32_t>(__builtin_ctzll(m));
-                uint32_t q = q0, cnt = 0, err = 0, need = 0;
-                while (q < ce) {
-                    if (q + 4 > size) { err = 1; need = 4; break; }
-                    const uint32_t len = one_page ? st_u32(stage, q - sa) : gword(page, q);
-                    if (static_cast<uint64_t>(q) + 4 + len > size) { err = 1; need = len; q += 4; break; }
-                    q += 4 + len;
-                    cnt++;
-                }
-                rec = make_uint4(q0 | (err << 31), q, cnt, need);
-            }
-            a.cand[static_cast<size_t>(c) * kPCand + sl] = rec;
-        }
-        __builtin_amdgcn_wave_barrier();
+    // lane j < 16: chunk cw + j's page offset, size, chunk start
+    uint32_t d_lo = 0, d_hi = 0, d_size = 0, d_cs = 0, d_first = 0;
+    if (static_cast<int>(lane()) < kSpecChunks && cw + static_cast<int>(lane()) < a.nchunks) {
+        const uint2 ch = a.chunks[cw + lane()];
+        const DevPage pg = a.pages[ch.x];
+        d_lo = static_cast<uint32_t>(pg.off);
+        d_hi = static_cast<uint32_t>(pg.off >> 32);
+        d_size = static_cast<uint32_t>(max(pg.size, 0));
+        d_cs = ch.y * kPChunk;
+        d_first = ch.y == 0 ? 1u : 0u;
     }
+    auto desc = [&](int j, const uint8_t*& page, uint32_t& size, uint32_t& cs, uint32_t& first) {
+        const uint64_t off = (static_cast<uint64_t>(__builtin_amdgcn_readlane(d_hi, j)) << 32) |
+                             __builtin_amdgcn_readlane(d_lo, j);
+        page = a.bytes + off;
+        size = __builtin_amdgcn_readlane(d_size, j);
+        cs = __builtin_amdgcn_readlane(d_cs, j);
+        first = __builtin_amdgcn_readlane(d_first, j);
+    };
+    // candidate offsets: lane l tests offset l of every chunk (loads issued together)
+    uint32_t lens[kSpecChunks];
+#pragma unroll
+    for (int j = 0; j < kSpecChunks; j++) {
+        const uint8_t* page; uint32_t size, cs, first;
+        desc(j, page, size, cs, first);
+        const uint32_t q = cs + lane();
+        lens[j] = (cw + j < a.nchunks && q + 4 <= size) ? gword(page, q) : 0xFFFFFFFFu;
+    }
+    uint64_t mk = 0;
+    const int jm = static_cast<int>(lane() / kPCand), sl = static_cast<int>(lane() % kPCand);
+#pragma unroll
+    for (int j = 0; j < kSpecChunks; j++) {
+        const uint8_t* page; uint32_t size, cs, first;
+        desc(j, page, size, cs, first);
+        const uint32_t q = cs + lane(), ce = min(cs + kPChunk, size);
+        bool plaus = q < ce && q + 4 <= size && static_cast<uint64_t>(q) + 4 + lens[j] <= size;
+        if (first) plaus = lane() == 0;  // the page's first string starts at 0
+        const uint64_t m = __ballot(cw + j < a.nchunks && plaus);
+        if (j == jm) mk = m;
+    }
+    // this lane's chunk descriptor from lane jm: shuffles with every lane
+    // active (a bpermute from a lane outside exec reads 0)
+    const uint64_t off = (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(d_hi), jm))) << 32) |
+                         static_cast<uint32_t>(__shfl(static_cast<int>(d_lo), jm));
+    const uint32_t size = static_cast<uint32_t>(__shfl(static_cast<int>(d_size), jm));
+    const uint32_t cs = static_cast<uint32_t>(__shfl(static_cast<int>(d_cs), jm));
+    const uint8_t* page = a.bytes + off;
+    const int c = cw + jm;
+    if (c >= a.nchunks) return;
+    for (int i = 0; i < sl; i++) mk &= mk - 1;  // this lane's candidate: the sl-th set bit
+    uint4 rec = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+    if (mk) {
+        const uint32_t ce = min(cs + kPChunk, size);
+        const uint32_t q0 = cs + static_cast<uint32_t>(__builtin_ctzll(mk));
+        uint32_t q = q0, cnt = 0, err = 0, need = 0;
+        while (q < ce) {
+            if (q + 4 > size) { err = 1; need = 4; break; }
+            const uint32_t len = gword(page, q);
+            if (static_cast<uint64_t>(q) + 4 + len > size) { err = 1; need = len; q += 4; break; }
+            q += 4 + len;
+            cnt++;
+        }
+        rec = make_uint4(q0 | (err << 31), q, cnt, need);
+    }
+    a.cand[static_cast<size_t>(c) * kPCand + sl] = rec;
 }
 
-// k_plain_link: one wave per page.  The page's candidate records are staged in
-// LDS; lane 0 follows the true chain chunk to chunk (the entry of chunk k is
-// where the chain left chunk k - 1), cuts it at the page's value count, and
-// records each chunk's chosen candidate and first row; then every lane writes
-// pseudo pages.  A bounds error before the value count is the page's error
-// record (the reference's ByteBuffer position and size).  An entry that is
-// not a candidate (a string longer than 60 bytes crossing a chunk edge) or a
-// chain leaving its window sets the fallback flag.
-constexpr uint32_t kLinkStage = 256;  // chunks per staging round
+// k_plain_link: one wave per page, rounds of kLinkStage chunks.  Lane i takes
+// chunk i of the round: its candidate records (registers) and a 64-entry
+// table in LDS, entry offset -> exit (0xFFFFFFFF: no candidate there; bit 31:
+// the walk hit a bounds error).  Lane 0 then follows the true chain through
+// the tables, one LDS read per chunk (the entry of chunk k is where the chain
+// left chunk k - 1).  Afterwards every lane turns its chunk's pick into a
+// pseudo page: rows before it by a wave scan of the picked counts, cut at the
+// page's value count (later bytes are never read), the page's error record at
+// the first bounds error before the count (the reference's ByteBuffer
+// position and size), the fallback flag for an entry that is not a candidate
+// (a string longer than 60 bytes crossing a chunk edge) or a chain leaving
+// its window.
+constexpr uint32_t kLinkStage = 64;
+constexpr uint32_t kLNone = 0xFFFFFFFFu;
+constexpr uint32_t kPickHit = 1u << 16, kPickSkip = 1u << 17, kPickFail = 1u << 18, kPickNone = 1u << 19;
 
 __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
-    __shared__ uint4 cand[kLinkStage * kPCand];
-    __shared__ uint32_t pick[kLinkStage];  // entry offset in the chunk | candidate << 16 (0xFFFF: none)
-    __shared__ uint32_t first[kLinkStage], take[kLinkStage];
+    __shared__ uint32_t tab[kLinkStage * 64];
+    __shared__ uint32_t pick[kLinkStage];
     const int p = blockIdx.x;
     if (p >= a.npages) return;
     const DevPage pg = a.pages[p];
@@ -473,76 +476,113 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
     const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
     const int32_t c0 = a.chunk_base[p], c1 = a.chunk_base[p + 1];
     const uint32_t slot_end = (size + 15) / 16 * 16 + 16;
-    uint32_t q = 0, rows = 0, stop = 0, fb = 0;
+    uint32_t q = 0, dead = 0;                // serial chain state (lane 0's values are used)
+    uint32_t rows = 0, done = 0, fb = 0;     // wave-uniform: rows before the round, count reached / error, fallback
     for (int32_t cb = c0; cb < c1; cb += kLinkStage) {
         const int32_t cend = min(c1, cb + static_cast<int32_t>(kLinkStage));
-        copy_blocks(cand, a.cand + static_cast<size_t>(cb) * kPCand, static_cast<uint32_t>(cend - cb) * kPCand, lane(), kWave);
+        const uint32_t i = lane();
+        const int32_t c = cb + static_cast<int32_t>(i);
+        const bool act = c < cend;
+        const uint32_t k = static_cast<uint32_t>(c - c0), chs = k * kPChunk;
+        uint4 r[kPCand];
+#pragma unroll
+        for (uint32_t s = 0; s < kPCand; s++)
+            r[s] = act ? a.cand[static_cast<size_t>(c) * kPCand + s] : make_uint4(kLNone, 0u, 0u, 0u);
+        uint4* row = reinterpret_cast<uint4*>(tab + i * 64);
+#pragma unroll
+        for (int w = 0; w < 16; w++) row[w] = make_uint4(kLNone, kLNone, kLNone, kLNone);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t s = 0; s < kPCand; s++)
+            if (act && r[s].x != kLNone) tab[i * 64 + ((r[s].x & 0x7FFFFFFFu) - chs)] = r[s].y | (r[s].x & 0x80000000u);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane() == 0) {
-            for (int32_t c = cb; c < cend; c++) {
-                const uint32_t i = static_cast<uint32_t>(c - cb), k = static_cast<uint32_t>(c - c0);
-                const uint32_t chs = k * kPChunk;
-                uint32_t pk = 0xFFFFFFFFu, tk = 0;
-                first[i] = rows;
-                if (!stop && !fb && rows < n && q < chs + kPChunk && q < size) {
-                    const uint4 r0 = cand[i * kPCand], r1 = cand[i * kPCand + 1], r2 = cand[i * kPCand + 2],
-                                r3 = cand[i * kPCand + 3];
-                    const uint32_t e0 = r0.x & 0x7FFFFFFFu, e1 = r1.x & 0x7FFFFFFFu, e2 = r2.x & 0x7FFFFFFFu,
-                                   e3 = r3.x & 0x7FFFFFFFu;
-                    const int hit = (r0.x != 0xFFFFFFFFu && e0 == q) ? 0
-                                  : (r1.x != 0xFFFFFFFFu && e1 == q) ? 1
-                                  : (r2.x != 0xFFFFFFFFu && e2 == q) ? 2
-                                  : (r3.x != 0xFFFFFFFFu && e3 == q) ? 3 : -1;
-                    if (hit < 0) {
-                        fb = 1;
+        if (lane() == 0) {  // the chain: one LDS read per chunk
+            const uint32_t nr = static_cast<uint32_t>(cend - cb);
+            for (uint32_t j = 0; j < nr; j++) {
+                const uint32_t js = (static_cast<uint32_t>(cb - c0) + j) * kPChunk;
+                uint32_t pk;
+                if (dead || q >= size) {
+                    pk = kPickNone;
+                    dead = 1;
+                } else if (q >= js + kPChunk) {
+                    pk = kPickSkip;  // a string spans this chunk
+                } else if (q - js >= 64) {
+                    pk = kPickFail;
+                    dead = 1;
+                } else {
+                    const uint32_t t = tab[j * 64 + (q - js)];
+                    if (t == kLNone) {
+                        pk = kPickFail;
+                        dead = 1;
                     } else {
-                        const uint4 r = hit == 0 ? r0 : (hit == 1 ? r1 : (hit == 2 ? r2 : r3));
-                        // the chunk's strings must lie inside its staged window
-                        const uint32_t g = k / kPChunkGroup;
-                        if (r.y > min(g * kPChunkGroup * kPChunk + kPWin, slot_end)) fb = 1;
-                        pk = (q - chs) | (static_cast<uint32_t>(hit) << 16);
-                        if (rows + r.z >= n) {  // the value count ends here: later bytes are never read
-                            tk = n - rows;
-                            stop = 1;
-                        } else if (r.x >> 31) {  // a bounds error before the value count
-                            DevErr* e = a.page_err + p;
-                            e->code = PQ_ERR_BUFFER;
-                            e->pos = static_cast<int32_t>(r.y);
-                            e->need = static_cast<int32_t>(r.w);
-                            e->size = static_cast<int32_t>(size);
-                            atomicOr(a.err_any, 1);
-                            tk = r.z;
-                            stop = 1;
-                        } else {
-                            tk = r.z;
-                            q = r.y;
-                        }
-                        rows += tk;
+                        pk = kPickHit | (q - js);
+                        if (t >> 31) dead = 1;  // the chain stops at its bounds error
+                        else q = t;
                     }
                 }
-                pick[i] = pk;
-                take[i] = tk;
+                pick[j] = pk;
             }
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t i = lane(); i < static_cast<uint32_t>(cend - cb); i += kWave) {
-            const uint32_t k = static_cast<uint32_t>(cb - c0) + i, pk = pick[i];
-            const uint32_t ent = pk == 0xFFFFFFFFu ? 0u : (pk & 0xFFFFu);
+        const uint32_t pk = act ? pick[i] : kPickNone;
+        uint4 rr = make_uint4(kLNone, 0u, 0u, 0u);
+        if (pk & kPickHit) {
+            const uint32_t e = chs + (pk & 0xFFFFu);
+#pragma unroll
+            for (uint32_t s = 0; s < kPCand; s++)
+                if (r[s].x != kLNone && (r[s].x & 0x7FFFFFFFu) == e) rr = r[s];
+        }
+        const bool hit = (pk & kPickHit) != 0;
+        const uint32_t cnt = hit ? rr.z : 0u;
+        const uint32_t incl = wave_incl_scan(cnt);
+        const uint32_t before = rows + incl - cnt;
+        const bool live = !done && before < n;             // the reference still reads values here
+        const bool cend_here = live && hit && before + cnt >= n;
+        const bool err_here = live && hit && !cend_here && (rr.x >> 31);
+        const uint32_t g = k / kPChunkGroup;
+        const bool fail_here = live && ((pk & kPickFail) || (hit && rr.y > min(g * kPChunkGroup * kPChunk + kPWin, slot_end)));
+        // the first stop (count reached or bounds error) ends the page
+        const uint64_t stops = __ballot(cend_here || err_here);
+        const uint32_t first_stop = stops ? static_cast<uint32_t>(__builtin_ctzll(stops)) : kWave;
+        const bool alive = live && i <= first_stop;
+        if (err_here && i == first_stop) {
+            DevErr* e = a.page_err + p;
+            e->code = PQ_ERR_BUFFER;
+            e->pos = static_cast<int32_t>(rr.y);
+            e->need = static_cast<int32_t>(rr.w);
+            e->size = static_cast<int32_t>(size);
+            atomicOr(a.err_any, 1);
+        }
+        {
+            const uint64_t fm = __ballot(fail_here && i <= first_stop);
+            if (fm && !fb) {  // reason bits for diagnostics: 1 pick failed, 2 window; chunk << 8
+                const uint32_t fl = static_cast<uint32_t>(__builtin_ctzll(fm));
+                const uint32_t why = __builtin_amdgcn_readlane((pk & kPickFail) ? 1u : 2u, fl);
+                fb = why | ((static_cast<uint32_t>(cb - c0) + fl) << 8);
+            }
+        }
+        if (act) {
+            const uint32_t take = !alive || !hit ? 0u : (cend_here ? n - before : cnt);
+            const uint32_t ent = hit ? (pk & 0xFFFFu) : 0u;
             DevPage pp{};
             pp.mode = MODE_PLAIN;
             pp.dict = -1;
-            pp.off = pg.off + k * kPChunk + ent;
-            pp.size = static_cast<int32_t>(size > k * kPChunk + ent ? size - k * kPChunk - ent : 0u);
-            pp.nvals = static_cast<int32_t>(take[i]);
-            pp.first_row = pg.first_row + first[i];
-            a.ppages[cb + static_cast<int32_t>(i)] = pp;
+            pp.off = pg.off + chs + ent;
+            pp.size = static_cast<int32_t>(size > chs + ent ? size - chs - ent : 0u);
+            pp.nvals = static_cast<int32_t>(take);
+            pp.first_row = pg.first_row + min(before, n);
+            a.ppages[c] = pp;
         }
+        rows += bcast_last(incl);
+        if (stops) done = 1;
+        q = __builtin_amdgcn_readfirstlane(q);
+        dead = __builtin_amdgcn_readfirstlane(dead);
         __builtin_amdgcn_wave_barrier();
     }
     if (lane() == 0) {
-        if (!fb && !stop && rows < n) {  // the chain ended before the value count: the read at q fails
+        if (!fb && !done && rows < n) {  // the chain ended before the value count: the read at q fails
             DevErr* e = a.page_err + p;
             e->code = PQ_ERR_BUFFER;
             e->pos = static_cast<int32_t>(q);
@@ -550,7 +590,7 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
             e->size = static_cast<int32_t>(size);
             atomicOr(a.err_any, 1);
         }
-        if (fb) atomicOr(a.fallback, 1);
+        if (fb) atomicOr(a.fallback, static_cast<int32_t>(fb));
     }
 }
 
@@ -640,7 +680,7 @@ void launch_plain_ba(hipStream_t s, PlainLaunch P) {
 
 void launch_plain_spec(hipStream_t s, const SpecLaunch& S) {
     if (S.nchunks <= 0) return;
-    const int per_block = kSpecWaves * kSpecChunks;
+    const int per_block = kSpecWaves * kSpecChunks;  // chunks per workgroup
     hipLaunchKernelGGL(k_plain_spec, dim3((S.nchunks + per_block - 1) / per_block), dim3(kSpecWaves * kWave), 0, s, S);
     hipLaunchKernelGGL(k_plain_link, dim3(S.npages), dim3(kWave), 0, s, S);
 }

@@ -399,3 +399,28 @@ def test_c2_full_size_properties(ctx, layout):
     exp = hashlib.sha256(gen.values_dump(cols[0], 0, n, 0, gen.CONFIG_SEEDS["C2"])).hexdigest()
     assert got == exp
 
+
+
+@pytest.mark.parametrize("case", ["plain_spec", "plain_spec_binary", "plain_spec_empty_strings", "plain_spec_extra",
+                                  "plain_spec_extra_trunc"])
+def test_plain_spec_no_fallback(ctx, case):
+    """Pages of short strings stay on the speculative chunk path (no generic
+    re-run): the second decode launches k_plain_spec again."""
+    f, chunk = CRAFTED[case]()
+    dc = ctx.upload(f, [to_desc_(chunk)])
+    dc.decode()
+    ctx.timing(True)
+    ctx.timing_reset()
+    dc.decode_async()
+    ctx.sync()
+    ms, n = ctx.timing_get("plain_spec")
+    gms, gn = ctx.timing_get("ba_rows")
+    ctx.timing(False)
+    dc.decode_check()
+    dc.free()
+    assert n == 1 and gn == 0
+
+
+def to_desc_(chunk):
+    from util import to_desc
+    return chunk if isinstance(chunk, capi.ChunkDesc) else to_desc(chunk)
