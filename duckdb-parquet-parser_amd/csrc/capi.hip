@@ -110,6 +110,9 @@ struct pq_chunk {
     int32_t* d_bigp = nullptr;
     uint32_t big_max_bytes = 0;
     int32_t pipe_entry_base = 0;        // entry-table slot of the pipe dictionary's first entry
+    uint8_t* d_zero = nullptr;          // pipe chunks: [flags][bsum][flist] in one block, cleared by one memset
+    size_t zero_bytes = 4 * sizeof(int32_t);  // bytes of d_flags cleared per decode (flags, bsum, flist[0])
+    bool tiles_aligned32 = false;       // every tile starts on a 32-row boundary: k_pipe_write owns whole validity words
     // PLAIN BYTE_ARRAY, REQUIRED (plain_ba.hip)
     bool plain = false;
     std::vector<pqk::DevBatch> hpwins;
@@ -285,6 +288,12 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_dict_count);
     dfree(c->d_page_err);
     dfree(c->d_dict_err);
+    if (c->d_zero) {  // d_flags, d_bsum and d_flist live in it
+        dfree(c->d_zero);
+        c->d_flags = nullptr;
+        c->d_bsum = nullptr;
+        c->d_flist = nullptr;
+    }
     dfree(c->d_flags);
     dfree(c->d_row_codes);
     dfree(c->d_tile_chars);
@@ -760,6 +769,9 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
                                          std::min(pqk::kTileRows, hpages[p].nvals - r), 0});
         }
         c->ntiles = static_cast<int>(htiles.size());
+        c->tiles_aligned32 = true;
+        for (const auto& t : htiles)
+            c->tiles_aligned32 &= ((hpages[static_cast<size_t>(t.page)].first_row + t.row0) & 31) == 0;
         for (const auto& pg : hpages) c->max_page_bytes = std::max<uint32_t>(c->max_page_bytes, static_cast<uint32_t>(std::max(pg.size, 0)));
         // every data page PLAIN, a fixed-width type whose bytes are copied as is
         c->fixed_plain = (c->type == PQ_INT32 || c->type == PQ_INT64 || c->type == PQ_FLOAT ||
@@ -778,7 +790,18 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         rc |= dalloc(&c->d_dict_count, hdicts.size());
         rc |= dalloc(&c->d_page_err, hpages.size());
         rc |= dalloc(&c->d_dict_err, hdicts.size());
-        rc |= dalloc(&c->d_flags, 4);
+        if (c->pipe) {  // flags | bsum | flist, cleared together
+            const size_t fb = 4 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long);
+            rc |= dalloc(&c->d_zero, fb + bb + (hpages.size() + 1) * sizeof(int32_t));
+            if (c->d_zero) {
+                c->d_flags = reinterpret_cast<int32_t*>(c->d_zero);
+                c->d_bsum = reinterpret_cast<unsigned long long*>(c->d_zero + fb);
+                c->d_flist = reinterpret_cast<int32_t*>(c->d_zero + fb + bb);
+                c->zero_bytes = fb + bb + sizeof(int32_t);
+            }
+        } else {
+            rc |= dalloc(&c->d_flags, 4);
+        }
         rc |= dalloc(&c->d_tile_chars, htiles.size());
         if (c->fixed_plain) {
             rc |= dalloc(&c->d_tile_rank, htiles.size());
@@ -793,8 +816,6 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc |= dalloc(&c->d_info, hpages.size());
             rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) + 64);
             rc |= dalloc(&c->d_tile_nn, htiles.size());
-            rc |= dalloc(&c->d_bsum, static_cast<size_t>(c->pipe_grid));
-            rc |= dalloc(&c->d_flist, hpages.size() + 1);
             if (!c->hbig.empty()) rc |= dalloc(&c->d_bigp, c->hbig.size());
         }
         if (c->plain) {
@@ -976,10 +997,9 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
     {
         Timed t(ctx, "pipe_runs");
         pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
-                              c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist);
+                              c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist);  // flist[0], bsum: cleared with d_flags
     }
     if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
-    (void)hipMemsetAsync(c->d_bsum, 0, static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long), s);
     if (!c->hbig.empty()) {
         Timed t(ctx, "pipe_big");
         pqk::launch_pipe_big(s, P, c->d_bigp, static_cast<int>(c->hbig.size()), c->big_max_bytes);
@@ -1002,9 +1022,13 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     }
     hipStream_t s = ctx->stream;
     pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
-    (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), s);
-    (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
     const bool pipe = c->pipe && ctx->opt_pipe;
+    (void)hipMemsetAsync(c->d_flags, 0, c->zero_bytes, s);  // pipe chunks: flags, bsum and flist[0] at once
+    // k_pipe_write stores whole validity words when every tile starts on a
+    // 32-row boundary; other paths OR bits into zeroed words
+    const bool pipe_path = pipe && !(c->plain && ctx->opt_plain);
+    if (!(pipe_path && c->tiles_aligned32))
+        (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
     if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
         // the dictionary (one workgroup) decodes on the side stream while the
         // run-table pass runs; k_pipe_codes waits for both
@@ -1374,7 +1398,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
         }
         hipStream_t s = ctx->stream;
         pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
-        (void)hipMemsetAsync(c->d_flags, 0, 4 * sizeof(int32_t), s);
+        (void)hipMemsetAsync(c->d_flags, 0, c->zero_bytes, s);
         if (c->ndicts) {
             {
                 Timed t(ctx, "dict_index");

@@ -46,6 +46,24 @@ constexpr int kWriteWaves = 6;
 constexpr uint32_t kFront = 16;               // zero bytes before the LDS dictionary
 constexpr uint32_t kLitCapP = 16;
 
+struct __attribute__((packed, aligned(1))) U16B { uint32_t x, y, z, w; };
+struct __attribute__((packed, aligned(1))) U8B { uint32_t x, y; };
+struct __attribute__((packed, aligned(1))) U4B { uint32_t x; };
+struct __attribute__((packed, aligned(1))) U2B { uint16_t x; };
+
+// Codes of rows 8l .. 8l + 7 (lane l) to codes[R0 + 8l ..]: one 16-byte
+// store when all eight rows are in the tile, else one store per row.
+__device__ __forceinline__ void store_codes8(uint16_t* codes, int64_t R0, uint32_t l8, uint32_t m, const uint32_t c[8]) {
+    if (l8 + 8 <= m) {
+        *reinterpret_cast<U16B*>(codes + R0 + l8) =
+            U16B{c[0] | (c[1] << 16), c[2] | (c[3] << 16), c[4] | (c[5] << 16), c[6] | (c[7] << 16)};
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (l8 + k < m) codes[R0 + l8 + k] = static_cast<uint16_t>(c[k]);
+    }
+}
+
 // run record: x = first value | count << 16, y = literal << 31 | payload
 // (RLE value, or the page bit offset of the literal run's first value)
 __device__ __forceinline__ uint32_t rr_start(uint2 r) { return r.x & 0xFFFFu; }
@@ -453,7 +471,7 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane i <- lane i
     return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x138, 0xf, 0xf, true));
 }
 
-__global__ void __launch_bounds__(kCodeWaves2 * 64) k_pipe_codes2(CodeArgs a, uint32_t lt_n) {
+__global__ void __launch_bounds__(kCodeWaves2 * 64) k_pipe_codes2(CodeArgs a, uint32_t lt_n, const int32_t* __restrict__ flist) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lens[];
     __shared__ CodeLds2 lds_all[kCodeWaves2];
     const int wv = static_cast<int>(threadIdx.x / kWave);
@@ -630,7 +648,7 @@ __global__ void __launch_bounds__(kCodeWaves2 * 64) k_pipe_codes2(CodeArgs a, ui
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            uint32_t chars = 0;
+            uint32_t chars = 0, cw8[8];
             const int64_t R0 = first_row + r0;
     #pragma unroll
             for (int k = 0; k < 8; k++) {
@@ -646,12 +664,21 @@ __global__ void __launch_bounds__(kCodeWaves2 * 64) k_pipe_codes2(CodeArgs a, ui
                         chars += v < nl ? lens[v] : static_cast<uint32_t>(a.entries[ebase + v] >> 32);
                     }
                 }
-                if (j < m) a.codes[R0 + j] = static_cast<uint16_t>(code);
+                cw8[k] = code;
+                (void)j;
             }
+            store_codes8(a.codes, R0, l8, m, cw8);
             chars = wave_sum(chars);
             tile_done(a, t, chars);
             __builtin_amdgcn_wave_barrier();
         }
+    }
+    // pages k_pipe_runs / k_pipe_big marked (complete before this launch):
+    // the exact serial decoder, one wave per page
+    const int nf = flist[0];
+    for (int i = static_cast<int>(blockIdx.x) * kCodeWaves2 + wv; i < nf; i += nw) {
+        exact_page(a, L, flist[1 + i], dict_n, ebase);
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -681,10 +708,6 @@ struct WriteLds {
     uint8_t vb[kWave];            // validity bits of rows 8l .. 8l + 7
 };
 
-struct __attribute__((packed, aligned(1))) U16B { uint32_t x, y, z, w; };
-struct __attribute__((packed, aligned(1))) U8B { uint32_t x, y; };
-struct __attribute__((packed, aligned(1))) U4B { uint32_t x; };
-struct __attribute__((packed, aligned(1))) U2B { uint16_t x; };
 
 __device__ __forceinline__ uint32_t dword_of(const uint4& v, uint32_t i) {  // register select, no scratch
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
@@ -901,7 +924,8 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
                     };
                     const int t = static_cast<int>(lane());
                     const uint32_t val = (tw(t) << sh) | (sh ? (tw(t - 1) >> (32 - sh)) : 0u);
-                    const bool whole = g * 32 >= R0 && g * 32 + 32 <= R0 + m;
+                    // the column's last word belongs to its last tile alone
+                    const bool whole = g * 32 >= R0 && (g * 32 + 32 <= R0 + m || R0 + m == a.nrows_total);
                     if (whole) a.validity[g] = val;
                     else if (val) atomicOr(&a.validity[g], val);
                 }
@@ -1388,7 +1412,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        uint32_t chars = 0;
+        uint32_t chars = 0, cw8[8];
         const int64_t R0 = first_row + r0;
 #pragma unroll
         for (int k = 0; k < 8; k++) {
@@ -1405,8 +1429,10 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
                     chars += v < nl ? lens[v] : static_cast<uint32_t>(a.entries[ebase + v] >> 32);
                 }
             }
-            if (j < m) a.codes[R0 + j] = static_cast<uint16_t>(code);
+            cw8[k] = code;
+            (void)j;
         }
+        store_codes8(a.codes, R0, l8, m, cw8);
         chars = wave_sum(chars);
         tile_done(a, t0 + static_cast<int>(ti), chars);
         __builtin_amdgcn_wave_barrier();
@@ -1466,7 +1492,7 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes) {
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist) {
-    (void)hipMemsetAsync(flist, 0, sizeof(int32_t), s);
+    (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     if (npages <= 0) return;
     const int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
     const int per = kRunWaves * ppw;
@@ -1511,10 +1537,13 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
         bpc = 1;
     const int need = (P.ntiles + kCodeWaves2 - 1) / kCodeWaves2;
     const int grid = max(1, min(need, P.cus * bpc));
-    if (P.has_small) hipLaunchKernelGGL(k_pipe_codes2, dim3(grid), dim3(kCodeWaves2 * kWave), lds, s, a, lt_n);
-    // pages the run-table pass marked: exact decoder (each wave exits unless its tile starts one)
-    hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, (P.npages + kCodeWaves - 1) / kCodeWaves))),
-                       dim3(kCodeWaves * kWave), 0, s, a, P.flist);
+    // also decodes the pages the run-table passes marked (flist)
+    if (P.has_small) {
+        hipLaunchKernelGGL(k_pipe_codes2, dim3(grid), dim3(kCodeWaves2 * kWave), lds, s, a, lt_n, P.flist);
+    } else {  // only k_pipe_big pages: the marked ones need the exact decoder alone
+        hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, (P.npages + kCodeWaves - 1) / kCodeWaves))),
+                           dim3(kCodeWaves * kWave), 0, s, a, P.flist);
+    }
 }
 
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
