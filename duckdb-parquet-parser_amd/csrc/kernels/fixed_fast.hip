@@ -22,6 +22,7 @@
 #include "kernels/kernels.hpp"
 #include "kernels/lane_walk.hpp"
 #include "kernels/run_walk.hpp"
+#include "kernels/run_spec.hpp"
 #include "kernels/stream.hpp"
 #include "pq_gpu.h"
 
@@ -185,6 +186,8 @@ constexpr int kLvWaves = 8;
 constexpr uint32_t kLvStage = 16384;
 constexpr uint32_t kLvRec = 1024;
 constexpr uint32_t kLvTiles = 128;
+constexpr uint32_t kLvSpecMax = 4096;  // level sections up to this size: run_spec.hpp (workgroup) instead of one lane
+constexpr uint32_t kLvSpecList = kLvSpecMax / 2 / kSpJump + 8;
 
 __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* __restrict__ bytes,
                                                                 const DevPage* __restrict__ pages,
@@ -201,6 +204,7 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
     __shared__ uint32_t tnn[kLvTiles];
     __shared__ uint32_t sh[4];  // status, nrec, pos
     __shared__ LitRun lits[kLitCapF];
+    __shared__ uint32_t splist[kLvSpecList], spesum[kLvSpecList], ssh[4];
     const int wv = static_cast<int>(threadIdx.x / kWave);
     const int p = blockIdx.x;
     const DevPage pg = pages[p];
@@ -240,7 +244,15 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
         copy_blocks(dst, src, nb, threadIdx.x, blockDim.x);
     }
     __syncthreads();
-    if (sh[0] == 0 && wv == 0) {
+    static_assert(sizeof(mark_all) >= 2 * kLvSpecMax, "jump table in mark_all");
+    if (sh[0] == 0 && dlen <= kLvSpecMax) {  // the run table by the workgroup (run_spec.hpp)
+        const uint32_t nr = spec_runs<kLvWaves * kWave, kLvSpecMax / (kLvWaves * kWave)>(
+            stage, 4, dlen, bw, n, &mark_all[0][0], splist, spesum, kLvSpecList, rec, kLvRec, ssh);
+        if (threadIdx.x == 0) {
+            if (nr == ~0u) sh[0] = 1;
+            else sh[1] = nr;
+        }
+    } else if (sh[0] == 0 && wv == 0) {
         RunWalk W{};
         W.alive = lane() == 0;
         W.q = 4;

@@ -1,0 +1,177 @@
+// run_spec.hpp — one hybrid RLE/bit-packed stream's run records built by the
+// whole workgroup (rle_decoder.hpp:36-95), the same records walk_runs
+// (run_walk.hpp) writes one header at a time:
+//   x = first value | count << 16, y = literal << 31 | payload
+// (RLE value, or the page bit offset of the literal run's first value).
+// A stream of a few hundred runs is a long serial chain for one lane; here
+//   1. every byte of the stream is parsed as if a run header started there:
+//      the next header's position or kSpStop (bad header, stream end);
+//   2. kSpJumpLog pointer-doubling rounds give kSpJump-run jumps;
+//   3. one lane follows the jumps from the stream start, listing every
+//      kSpJump-th header (a few dozen dependent LDS reads);
+//   4. one thread per listed header re-parses its kSpJump runs exactly, with
+//      untruncated counts;
+//   5. a scan of the counts gives every record its first value; records past
+//      the value count drop, the crossing one is truncated, an exhausted
+//      stream gets its zero run (rle_decoder.hpp:20-23).
+// Zero-count runs, headers cut by the stream end and table overflow before
+// the value count return ~0u (the caller takes its exact serial path).
+#pragma once
+#include "kernels/device_common.hpp"
+
+namespace pqk {
+namespace dev {
+
+constexpr uint32_t kSpStop = 0xFFFFu;
+constexpr int kSpJumpLog = 4;
+constexpr uint32_t kSpJump = 1u << kSpJumpLog;
+constexpr uint32_t kSpCountCap = 1u << 20;
+
+struct SpecHdr {
+    uint32_t hl, g, lit, qh, vraw;
+};
+// A run header at LDS byte q of the staged words (the walk_runs parse).
+__device__ __forceinline__ SpecHdr spec_hdr(const uint32_t* stw, uint32_t q) {
+    const uint64_t x = lds_u64(stw, q);
+    const uint32_t x0 = static_cast<uint32_t>(x), x1 = static_cast<uint32_t>(x >> 32);
+    const uint32_t st0 = ~x0 & 0x80808080u;
+    SpecHdr h;
+    h.hl = st0 ? (__builtin_ctz(st0) >> 3) + 1 : ((~x1 & 0x80u) ? 5u : 9u);
+    const uint32_t lm = (h.hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (h.hl & 3))) - 1u);
+    const uint32_t x0m = x0 & lm;
+    const uint32_t top = (h.hl >= 5) ? (x1 << 28) : 0u;
+    const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
+                         ((x0m >> 3) & 0xFE00000u) | top;
+    h.g = ind >> 1;
+    h.lit = ind & 1u;
+    h.qh = q + h.hl;
+    const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, h.hl);
+    const uint32_t vb = x1 >> (8 * ((h.hl - 4) & 3));
+    h.vraw = (h.hl < 4) ? va : vb;
+    return h;
+}
+// zero-count runs, headers past the stream end, RLE values cut by it
+__device__ __forceinline__ bool spec_bad(const SpecHdr& h, uint32_t e, uint32_t nbv) {
+    return h.hl > 5 || h.qh > e || h.g == 0 || (!h.lit && h.qh + nbv > e);
+}
+
+// The stream is at staged bytes [base, base + len) of `stw` (the page from
+// byte 0, so staged positions are page positions), len <= kThreads *
+// kPerThread.  Scratch: tab (len u16), list and esum (lcap u32 each), sh (4
+// u32).  Records go to rec[0 .. rcap).  Every thread of the workgroup calls
+// this (it holds barriers); returns the record count or ~0u.
+template <int kThreads, int kPerThread>
+__device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, uint32_t bw, uint32_t n,
+                              uint16_t* tab, uint32_t* list, uint32_t* esum, uint32_t lcap, uint2* rec, uint32_t rcap,
+                              uint32_t* sh) {
+    const uint32_t tid = threadIdx.x, e = base + len, nbv = (bw + 7) / 8;
+    // 1. speculative headers
+    for (uint32_t j = tid; j < len; j += kThreads) {
+        const SpecHdr h = spec_hdr(stw, base + j);
+        const uint64_t nx = h.lit ? static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw : h.qh + nbv;
+        tab[j] = static_cast<uint16_t>((spec_bad(h, e, nbv) || nx >= e) ? kSpStop : static_cast<uint32_t>(nx - base));
+    }
+    if (tid < 4) sh[tid] = 0;
+    __syncthreads();
+    // 2. kSpJump-run jumps
+    for (int r = 0; r < kSpJumpLog; r++) {
+        uint32_t nv[kPerThread];
+#pragma unroll
+        for (int i = 0; i < kPerThread; i++) {
+            const uint32_t j = tid + static_cast<uint32_t>(i) * kThreads;
+            uint32_t t = kSpStop;
+            if (j < len) {
+                t = tab[j];
+                if (t != kSpStop) t = tab[t];
+            }
+            nv[i] = t;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kPerThread; i++) {
+            const uint32_t j = tid + static_cast<uint32_t>(i) * kThreads;
+            if (j < len) tab[j] = static_cast<uint16_t>(nv[i]);
+        }
+        __syncthreads();
+    }
+    // 3. every kSpJump-th header of the real chain
+    const uint32_t lmax = rcap > kSpJump + 1 ? min(lcap, (rcap - kSpJump - 1) / kSpJump + 1) : 0u;
+    if (tid == 0) {
+        uint32_t k = 0, q = 0;
+        for (;;) {
+            if (k >= lmax) { k = ~0u; break; }
+            list[k++] = q;
+            if (q >= len) break;
+            const uint32_t t = tab[q];
+            if (t == kSpStop) break;
+            q = t;
+        }
+        sh[0] = k;
+    }
+    __syncthreads();
+    const uint32_t nl = sh[0];
+    if (nl == ~0u) return ~0u;
+    // 4. exact runs of each listed header: untruncated counts, first bad step
+    const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+    const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
+    for (uint32_t i = tid; i < nl; i += kThreads) {
+        uint32_t q = base + list[i];
+        uint2* out = rec + i * kSpJump;
+        uint32_t s = 0, sum = 0, bad = kSpJump, ended = 0;
+        for (; s < kSpJump; s++) {
+            if (q >= e) { ended = 1; break; }
+            const SpecHdr h = spec_hdr(stw, q);
+            if (spec_bad(h, e, nbv)) { bad = s; break; }
+            const uint32_t c = h.lit ? min(h.g, kSpCountCap / 8) * 8 : min(h.g, kSpCountCap);
+            out[s] = make_uint2(c, h.lit ? (litpay | (h.qh * litmul)) : (h.vraw & vmask));
+            sum = min(sum + c, kSpCountCap);
+            const uint64_t nql = static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw;
+            q = h.lit ? (nql > e ? e : static_cast<uint32_t>(nql)) : h.qh + nbv;
+        }
+        if (s == kSpJump && q >= e) ended = 1;
+        esum[i] = sum;
+        list[i] = s | (bad << 8) | (ended << 16);
+    }
+    __syncthreads();
+    // 5. exclusive scan of the counts (wave 0), truncation, exhaustion
+    if (tid < kWave) {
+        const uint32_t per = (nl + kWave - 1) / kWave;
+        const uint32_t a0 = min(nl, tid * per), a1 = min(nl, a0 + per);
+        uint32_t sum = 0;
+        for (uint32_t i = a0; i < a1; i++) sum += esum[i];
+        uint32_t run = wave_incl_scan(sum) - sum;
+        for (uint32_t i = a0; i < a1; i++) {
+            const uint32_t x = esum[i];
+            esum[i] = run;
+            run += x;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nl; i += kThreads) {
+        const uint32_t meta = list[i];
+        const uint32_t nr = meta & 0xFFu, bad = (meta >> 8) & 0xFFu, ended = meta >> 16;
+        const uint32_t b0 = esum[i];
+        if (b0 >= n) continue;
+        uint2* out = rec + i * kSpJump;
+        uint32_t c0 = b0, kept = 0;
+        for (uint32_t s = 0; s < nr && c0 < n; s++) {
+            const uint32_t c = out[s].x;
+            out[s].x = c0 | (min(c, n - c0) << 16);
+            c0 += c;
+            kept = s + 1;
+        }
+        if (c0 >= n) {
+            sh[1] = i * kSpJump + kept;
+        } else if (bad < kSpJump || (i + 1 == nl && (!ended || i * kSpJump + nr >= rcap))) {
+            atomicOr(&sh[2], 1u);  // a bad header before the value count
+        } else if (i + 1 == nl) {  // exhausted: the rest of the values are 0
+            out[nr] = make_uint2(c0 | ((n - c0) << 16), 0u);
+            sh[1] = i * kSpJump + nr + 1;
+        }
+    }
+    __syncthreads();
+    return (sh[2] || sh[1] == 0) ? ~0u : sh[1];
+}
+
+}  // namespace dev
+}  // namespace pqk

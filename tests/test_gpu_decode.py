@@ -197,6 +197,14 @@ def _spec_plain_file(seed, n=3000, cut=None, nvals=None, binary=False, pages=2, 
     return B.build_file(out, gen.BYTE_ARRAY, False, total)
 
 
+def _opt_levels_file(stream: bytes, nvals: int, nn: int, seed: int):
+    """One OPTIONAL INT64 page with the given def-level stream and nn values."""
+    rng = np.random.default_rng(seed)
+    vals = struct.pack(f"<{nn}q", *[int(x) for x in rng.integers(-1 << 40, 1 << 40, nn)])
+    pay = B.levels_section(stream) + vals
+    return B.build_file([B.data_header(len(pay), nvals, 0) + pay], gen.INT64, True, nvals)
+
+
 def _opt_fixed_file(ptype, fmt, nvals, seed, rle_levels=False, drop=0):
     """One OPTIONAL PLAIN fixed-width page; `drop` trailing values removed
     from the payload (the read overruns on the last non-null rows)."""
@@ -281,6 +289,14 @@ CRAFTED = {
     "opt_double_rle_levels": lambda: _opt_fixed_file(gen.DOUBLE, "<d", 1300, seed=6, rle_levels=True),
     # OPTIONAL INT96
     "opt_int96": lambda: _opt_fixed_file(gen.INT96, "<qi", 600, seed=7),
+    # OPTIONAL fixed width, def streams for the workgroup run builder (run_spec.hpp):
+    # exhausted before the value count (zero levels), many one-group literal
+    # runs, a zero-count run (exact serial path)
+    "opt_levels_exhausted": lambda: _opt_levels_file(B.rle(2000, 1, 1), 3000, 2000, seed=51),
+    "opt_levels_tiny_runs": lambda: _opt_levels_file(b"".join(B.bitpack([1, 0, 1, 1, 0, 1, 1, 1], 1) + B.rle(9, 1, 1)
+                                                              for _ in range(300)), 5100, 300 * 15, seed=52),
+    "opt_levels_zero_run": lambda: _opt_levels_file(B.bitpack([1] * 16, 1) + B.rle(0, 1, 1) + B.rle(100, 1, 1),
+                                                    116, 116, seed=53),
     # REQUIRED INT32 over several tiles, pages of different sizes
     "req_int32_tiles": lambda: B.build_file([B.data_header(4 * n, n, 0) + struct.pack(f"<{n}i", *range(-n, 0))
                                              for n in (1500, 1, 513)], gen.INT32, False, 2014),
