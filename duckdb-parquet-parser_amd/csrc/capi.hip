@@ -56,6 +56,9 @@ struct pq_ctx {
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
     bool opt_plain_rows = false; // "plain_rows": rows pass one lane per page from HBM (k_plain_rows), else k_plain_walk (LDS windows)
+    bool opt_graph = false;      // "graph": replay each chunk's decode launches as a captured HIP graph (timing off);
+                                 // measured slower on C2 (0.204 vs 0.174 ms per step), so off by default
+    uint64_t opt_gen = 0;        // bumped by every pq_ctx_set_option (captured graphs record it)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
 };
 
@@ -131,6 +134,19 @@ struct pq_chunk {
     DevPage* d_ppages = nullptr;
     DevErr* d_perr = nullptr;
     pq_column* last_out = nullptr;      // output of the last pq_decode_async (collect re-runs into it)
+    // the decode's launches as a HIP graph, replayed while its key holds
+    hipGraphExec_t gexec = nullptr;
+    bool graph_off = false;             // capture failed once: launch directly
+    struct GraphKey {
+        const void *validity, *values, *offsets;
+        int64_t capacity_bytes;
+        uint64_t opt_gen;
+        bool spec_failed;
+        bool operator==(const GraphKey& o) const {
+            return validity == o.validity && values == o.values && offsets == o.offsets &&
+                   capacity_bytes == o.capacity_bytes && opt_gen == o.opt_gen && spec_failed == o.spec_failed;
+        }
+    } gkey{};
     std::vector<int32_t> hunit_win;     // page (or chunk, spec path) -> its window (k_plain_rows)
     int32_t* d_unit_win = nullptr;
     // tile-parallel PLAIN fixed-width decode (fixed_fast.hip)
@@ -288,6 +304,10 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_dict_count);
     dfree(c->d_page_err);
     dfree(c->d_dict_err);
+    if (c->gexec) {
+        (void)hipGraphExecDestroy(c->gexec);
+        c->gexec = nullptr;
+    }
     if (c->d_zero) {  // d_flags, d_bsum and d_flist live in it
         dfree(c->d_zero);
         c->d_flags = nullptr;
@@ -598,6 +618,7 @@ void pq_ctx_destroy(pq_ctx* ctx) {
 }
 
 int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
+    if (ctx) ctx->opt_gen++;
     if (!ctx || !key) return PQ_ERR_ARG;
     if (std::strcmp(key, "fused_ba") == 0) { ctx->opt_fused = value != 0; return 0; }
     if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
@@ -612,6 +633,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
     if (std::strcmp(key, "plain_rows") == 0) { ctx->opt_plain_rows = value != 0; return 0; }
+    if (std::strcmp(key, "graph") == 0) { ctx->opt_graph = value != 0; return 0; }
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
@@ -1012,6 +1034,8 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
     pqk::launch_pipe_codes(s, P, false);
 }
 
+static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out);
+
 int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (!ctx || !c || !out) return PQ_ERR_ARG;
     if (c->type == PQ_BYTE_ARRAY) {
@@ -1020,6 +1044,39 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     } else {
         if (int rc = ensure_output(ctx, c, out, 0)) return rc;
     }
+    c->last_out = out;
+    if (ctx->timing || !ctx->opt_graph || c->graph_off) return decode_launch(ctx, c, out);
+    // the launch sequence (memsets, kernels, the side-stream fork/join) as a
+    // HIP graph: captured once per output buffers / options, then one launch
+    const pq_chunk::GraphKey key{out->d_validity, out->d_values, out->d_offsets, out->capacity_bytes, ctx->opt_gen,
+                                 c->spec_failed};
+    if (!c->gexec || !(c->gkey == key)) {
+        if (c->gexec) {
+            (void)hipGraphExecDestroy(c->gexec);
+            c->gexec = nullptr;
+        }
+        hipGraph_t g = nullptr;
+        if (hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed) != hipSuccess) {
+            (void)hipGetLastError();
+            c->graph_off = true;
+            return decode_launch(ctx, c, out);
+        }
+        const int rc = decode_launch(ctx, c, out);
+        const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        if (rc || e != hipSuccess || !g || hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0) != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();
+            c->gexec = nullptr;
+            c->graph_off = true;
+            return rc ? rc : decode_launch(ctx, c, out);
+        }
+        (void)hipGraphDestroy(g);
+        c->gkey = key;
+    }
+    return hip_check(ctx, hipGraphLaunch(c->gexec, ctx->stream), "graph launch");
+}
+
+static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     hipStream_t s = ctx->stream;
     pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
     const bool pipe = c->pipe && ctx->opt_pipe;
@@ -1049,7 +1106,6 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
                                  c->d_dict_err, c->d_flags, c->type, c->plain_width);
     }
-    c->last_out = out;
     if (c->plain && ctx->opt_plain && !(c->plain_spec && c->spec_failed)) {
         pqk::PlainLaunch P{};
         P.bytes = c->d_bytes; P.pages = c->d_pages; P.wins = c->d_pwins;

@@ -63,17 +63,28 @@ __global__ void __launch_bounds__(kWalkWaves * 64) k_plain_walk(PlainLaunch a) {
         const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
         const uint32_t base = static_cast<uint32_t>(pg.off - W.img_lo);
         uint32_t* ri = a.rowinfo + pg.first_row;
+        // the pages' length chains in lock step, branch-free (a divergent
+        // loop with early exits spends more on exec-mask bookkeeping than on
+        // the walk): one string per lane per step
         uint32_t pos = 0, k = 0;
-        for (; k < n; k++) {
-            if (pos + 4 > size) { lane_err(a.page_err + p, a.err_any, pos, 4, size); break; }
-            const uint32_t len = st_u32(stage, base + pos);
-            pos += 4;
-            if (static_cast<uint64_t>(pos) + len > size) { lane_err(a.page_err + p, a.err_any, pos, len, size); break; }
-            ri[k] = (base + pos) | (len << 16);
+        bool alive = n > 0, failed = false;
+        while (alive) {
+            const uint32_t len = st_u32(stage, base + min(pos, size));
+            const bool e1 = pos + 4 > size;
+            const bool e2 = !e1 && static_cast<uint64_t>(pos) + 4 + len > size;
+            if (e1 | e2) {  // ByteBuffer::check (common.hpp:162-168): the reference's error position
+                lane_err(a.page_err + p, a.err_any, e1 ? pos : pos + 4, e1 ? 4u : len, size);
+                failed = true;
+                break;
+            }
+            ri[k] = (base + pos + 4) | (len << 16);
             chars += len;
-            pos += len;
+            pos += 4 + len;
+            k++;
+            alive = k < n;
         }
-        for (; k < n; k++) ri[k] = 0;  // a failed page: empty rows (the decode reports the error)
+        if (failed)
+            for (; k < n; k++) ri[k] = 0;  // a failed page: empty rows (the decode reports the error)
     }
     chars = bcast_last(wave_incl_scan(chars));
     if (lane() == 0) {

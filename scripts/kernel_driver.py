@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Run the C2 decode (or the C3 regex scan) a few times — a small target for
-rocprofv3 PMC passes.  usage: kernel_driver.py [decode|regex] [rows] [reps] [fused_debug]"""
+"""Run the C2 decode, the C3 regex scan or the C3 PLAIN decode a few times — a
+small target for rocprofv3 PMC passes.
+usage: kernel_driver.py [decode|regex|plain] [rows] [reps] [fused_debug]"""
 import os
 import sys
 
@@ -16,6 +17,13 @@ ctx = capi.Context(0)
 ctx.set_option("fused_debug", dbg)
 if what == "decode":
     f = gen.build(gen.c2_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C2"])
+    F = capi.File(f)
+    dc = ctx.upload(f, [F.chunk(0, 0)])
+    for _ in range(reps):
+        dc.decode_async()
+    ctx.sync()
+elif what == "plain":
+    f = gen.build(gen.c3_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C3"])
     F = capi.File(f)
     dc = ctx.upload(f, [F.chunk(0, 0)])
     for _ in range(reps):

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """C2 decode step wall time with and without the per-kernel HIP-event
-timers (ctx.timing) inside the timed loop.  usage: step_overhead.py [steps]"""
+timers (ctx.timing) inside the timed loop, with and without the
+captured HIP graph.  usage: step_overhead.py [steps]"""
 import os
 import sys
 import time
@@ -15,7 +16,8 @@ f = gen.build(gen.c2_cols(), 10_000_000, 1, seed=gen.CONFIG_SEEDS["C2"])
 F = capi.File(f)
 dc = ctx.upload(f, [F.chunk(0, 0)])
 dc.decode()
-for timing in (False, True, False):
+for graph, timing in ((1, False), (0, False), (1, True), (1, False)):
+    ctx.set_option("graph", graph)
     ctx.timing(timing)
     for _ in range(5):
         dc.decode_async()
@@ -27,4 +29,4 @@ for timing in (False, True, False):
     ctx.sync()
     t2 = time.perf_counter()
     ctx.timing(False)
-    print(f"timing={timing}: {(t2 - t0) / steps * 1e3:.4f} ms/step wall, host enqueue {(t1 - t0) / steps * 1e3:.4f} ms/step")
+    print(f"graph={graph} timing={timing}: {(t2 - t0) / steps * 1e3:.4f} ms/step wall, host enqueue {(t1 - t0) / steps * 1e3:.4f} ms/step")
