@@ -56,6 +56,10 @@ struct pq_ctx {
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
     bool opt_plain_rows = false; // "plain_rows": rows pass one lane per page from HBM (k_plain_rows), else k_plain_walk (LDS windows)
+    bool opt_page = false;       // "page": k_pipe_page (runs + codes per page) where every small page fits its stage;
+                                 // C2: 0.104 ms vs k_pipe_runs 0.036 + k_pipe_codes3 0.044, so off by default
+    bool opt_codes3 = true;      // "codes3": k_pipe_codes3 (lean tile loop), else k_pipe_codes2
+    bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
     bool opt_graph = false;      // "graph": replay each chunk's decode launches as a captured HIP graph (timing off);
                                  // measured slower on C2 (0.204 vs 0.174 ms per step), so off by default
     uint64_t opt_gen = 0;        // bumped by every pq_ctx_set_option (captured graphs record it)
@@ -109,6 +113,7 @@ struct pq_chunk {
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
     bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
+    bool pipe_page = false;             // every small page fits k_pipe_page's stage
     std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
     int32_t* d_bigp = nullptr;
     uint32_t big_max_bytes = 0;
@@ -356,17 +361,18 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->pipe = false;
     c->pipe_count = false;
     c->pipe_small = false;
+    c->pipe_page = false;
     c->hbig.clear();
     c->big_max_bytes = 0;
     if (c->type != PQ_BYTE_ARRAY || c->max_def > 254 || c->max_def < 0 || c->max_rep < 0 || pages.empty()) return;
     int32_t dict_id = -1;
-    bool multi = false, small = false;
+    bool multi = false, small = false, page_fit = true;
     std::vector<int32_t> big;
     uint32_t big_bytes = 0;
     for (size_t i = 0; i < pages.size(); i++) {
         const DevPage& pg = pages[i];
         if (pg.mode != pqk::MODE_DICT || pg.size > (1 << 27) || pg.size < 0) return;
-        if (pg.nvals > pqk::kPipeSmallRows) {
+        if (pg.nvals > pqk::kPipeSmallRows || ctx->opt_big_all) {
             // k_pipe_big: the page's jump table and up to kBigTiles tiles in one workgroup
             if (pg.nvals > pqk::kBigTiles * pqk::kTileRows || static_cast<uint32_t>(pg.size) > pqk::kBigMaxBytes) return;
             big.push_back(static_cast<int32_t>(i));
@@ -374,6 +380,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
         } else {
             small = true;
             multi |= pg.nvals > pqk::kTileRows;
+            page_fit &= static_cast<uint32_t>(pg.size) + 16 <= pqk::pipe_page_stage();
         }
         if (dict_id >= 0 && pg.dict != dict_id) return;
         dict_id = pg.dict;
@@ -392,6 +399,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
     c->pipe = true;
     c->pipe_small = small;
+    c->pipe_page = small && page_fit;
     c->pipe_count = multi && c->max_def > 0;
     c->hbig = std::move(big);
     c->big_max_bytes = big_bytes;
@@ -633,6 +641,9 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
     if (std::strcmp(key, "plain_rows") == 0) { ctx->opt_plain_rows = value != 0; return 0; }
+    if (std::strcmp(key, "page") == 0) { ctx->opt_page = value != 0; return 0; }
+    if (std::strcmp(key, "codes3") == 0) { ctx->opt_codes3 = value != 0; return 0; }
+    if (std::strcmp(key, "big_all") == 0) { ctx->opt_big_all = value != 0; return 0; }
     if (std::strcmp(key, "graph") == 0) { ctx->opt_graph = value != 0; return 0; }
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
@@ -1008,6 +1019,7 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     P.dict_entries_cap = c->pipe_ecap;
     P.cus = c->pipe_cus;
     P.has_small = c->pipe_small;
+    P.lean_codes = ctx->opt_codes3;
     return P;
 }
 
@@ -1016,10 +1028,21 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
 // the codes wait for it (ev_join).
 static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side) {
     hipStream_t s = ctx->stream;
+    if (c->pipe_page && ctx->opt_page) {  // run tables + codes per page in one pass (needs the dictionary)
+        if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
+        if (!c->hbig.empty()) {
+            Timed t(ctx, "pipe_big");
+            pqk::launch_pipe_big(s, P, c->d_bigp, static_cast<int>(c->hbig.size()), c->big_max_bytes);
+        }
+        Timed t(ctx, "pipe_page");
+        pqk::launch_pipe_page(s, P);
+        return;
+    }
     {
         Timed t(ctx, "pipe_runs");
         pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
-                              c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist);  // flist[0], bsum: cleared with d_flags
+                              c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist,  // flist[0], bsum: cleared with d_flags
+                              ctx->opt_codes3);
     }
     if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
     if (!c->hbig.empty()) {

@@ -22,10 +22,12 @@
 //                 from the LDS dictionary to HBM with unaligned 16-byte moves.
 // Only pages of more than 512 rows with def levels need tile_nn, the
 // non-null counts of the earlier tiles of their page (k_pipe_codes<true>).
+#include <cstddef>
 #include "kernels/device_common.hpp"
 #include "kernels/kernels.hpp"
 #include "kernels/lane_walk.hpp"
 #include "kernels/run_walk.hpp"
+#include "kernels/run_spec.hpp"
 #include "kernels/stream.hpp"
 #include "pq_gpu.h"
 
@@ -76,7 +78,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
                                                               int32_t max_def, int32_t max_rep,
                                                               uint2* __restrict__ runs,
                                                               uint32_t* __restrict__ info, int ppw,
-                                                              int32_t* __restrict__ flist) {
+                                                              int32_t* __restrict__ flist, uint32_t stage_max) {
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[kRunWaves][kRunStage / 4 + 8];
     const uint32_t wv = threadIdx.x / kWave;
     const int g0 = (blockIdx.x * kRunWaves + static_cast<int>(wv)) * ppw;
@@ -120,7 +122,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
         };
         // prologue (column_reader.cpp:146-182); any error -> exact decoder
         uint32_t pos = 0, dbase = 0, dlen = 0;
-        if (n > 65535u) flag = 1;
+        if (n > 65535u || size > stage_max) flag = 1;  // stage_max: k_pipe_codes3's payload stage
         if (!flag && max_def > 0) {
             if (size < 4) flag = 1;
             else {
@@ -693,6 +695,632 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_exact(CodeArgs a, cons
     for (int i = static_cast<int>(blockIdx.x) * kCodeWaves + wv; i < n; i += static_cast<int>(gridDim.x) * kCodeWaves) {
         exact_page(a, lds_all[wv], flist[1 + i], dict_n, ebase);
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ── per-tile codes, lean form ──────────────────────────────────────────────
+// k_pipe_codes3 computes what k_pipe_codes2 does, with three changes:
+//  * no global loads inside a tile.  On gfx9 loads and stores share vmcnt, so
+//    a load in the tile waits for the previous tile's code stores; here the
+//    tile's descriptors, run records, payload and earlier-tile non-null counts
+//    all arrive in the prefetch, and a tile's stores are issued at the top of
+//    the next tile, before that tile's prefetch (one wait per tile, for
+//    operations issued a whole tile earlier);
+//  * bit fields come from the staged payload without branches: two clamped
+//    dword reads and a funnel shift (the slot's zero padding, capi.hip
+//    `slot`, stands for the bytes past the page end);
+//  * every row takes the same instructions (selects, not branches).
+// Pages whose payload does not fit the stage (> kStage3 - 16 bytes), and every
+// page when the dictionary has more entries than the LDS length table, take
+// the exact decoder (exact_page).
+constexpr int kCodeWaves3 = 4;                // 3 waves per SIMD fit its registers: 3 workgroups per CU
+constexpr uint32_t kStage3 = 5120;            // staged payload bytes per tile (5 x 16 B per lane)
+constexpr uint32_t kStage3Blocks = kStage3 / 16;
+static_assert(kStage3Blocks == 5 * kWave, "prefetch registers");
+
+struct CodeLds3 {  // leading fields as CodeLds (exact_page reuses them)
+    uint2 recd[kPipeRunCap];
+    uint2 reci[kPipeRunCap];
+    uint8_t mark[kTileRows];
+    uint8_t mark2[kTileRows];
+    uint32_t stage[kStage3 / 4];
+};
+static_assert(sizeof(CodeLds3) >= sizeof(CodeLds) && offsetof(CodeLds3, mark2) == offsetof(CodeLds, mark2), "layout");
+
+// bw-bit field (mask = 2^bw - 1, bw <= 16) at page bit b of the staged
+// payload; word indices past `zw` (a zero word of the slot's padding) clamp.
+__device__ __forceinline__ uint32_t sbits3(const uint32_t* st, uint32_t b, uint32_t zw, uint32_t mask) {
+    const uint32_t wi = b >> 5;
+    const uint32_t w0 = st[min(wi, zw)], w1 = st[min(wi + 1, zw)];
+    return __builtin_amdgcn_alignbit(w1, w0, b & 31u) & mask;
+}
+
+// Codes of rows 8l .. 8l + 7 packed two per word.
+__device__ __forceinline__ void store_packed8(uint16_t* codes, int64_t R0, uint32_t l8, uint32_t m, const uint32_t w[4]) {
+    if (l8 + 8 <= m) {
+        *reinterpret_cast<U16B*>(codes + R0 + l8) = U16B{w[0], w[1], w[2], w[3]};
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (l8 + k < m) codes[R0 + l8 + k] = static_cast<uint16_t>(w[k >> 1] >> (16 * (k & 1)));
+    }
+}
+
+// (number of records among rec[lane], rec[lane + 64] with start <= v) - 1
+__device__ __forceinline__ uint32_t run_at_reg(uint2 r0, uint2 r1, uint32_t nr, uint32_t v) {
+    const bool a0 = lane() < nr && rr_start(r0) <= v;
+    const bool a1 = lane() + kWave < nr && rr_start(r1) <= v;
+    return static_cast<uint32_t>(__popcll(__ballot(a0)) + __popcll(__ballot(a1))) - 1u;
+}
+
+__global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, uint32_t lt_n, const int32_t* __restrict__ flist) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lens[];
+    __shared__ CodeLds3 lds_all[kCodeWaves3];
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    CodeLds3& L = lds_all[wv];
+    CodeLds& LX = *reinterpret_cast<CodeLds*>(&L);  // exact_page scratch (same leading fields)
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    const uint32_t nl = min(dict_n, lt_n);
+    const bool lean = dict_n <= lt_n;  // every entry length in LDS
+    copy_map(lens, a.entries + ebase, nl, threadIdx.x, blockDim.x,
+             [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
+    __syncthreads();
+    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
+    const uint32_t maskd = (1u << bwd) - 1u;
+    const int nw = static_cast<int>(gridDim.x) * kCodeWaves3;
+    const int per = (a.ntiles + nw - 1) / nw;
+    const int ta = min(a.ntiles, (static_cast<int>(blockIdx.x) * kCodeWaves3 + wv) * per);
+    const int tb = min(a.ntiles, ta + per);
+    const uint32_t l8 = lane() * 8;
+    auto rl64 = [](uint64_t v, int i) -> uint64_t {
+        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
+        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), i);
+        return (static_cast<uint64_t>(hi) << 32) | lo;
+    };
+    // the previous tile's codes and characters, stored at the top of the next
+    bool pend = false;
+    int64_t pR0 = 0;
+    uint32_t pm = 0, pch = 0;
+    int pt = 0;
+    uint32_t pw[4] = {0u, 0u, 0u, 0u};
+    for (int c0 = ta; c0 < tb; c0 += kWave) {
+        const int cn = min(kWave, tb - c0);
+        uint32_t myp = 0, myrow0 = 0, mym = 0, myinf = kFallback, mysize = 0, mytp = 0;
+        uint64_t myoff = 0, myfirst = 0;
+        if (static_cast<int>(lane()) < cn) {
+            const DevTile T = a.tiles[c0 + lane()];
+            const DevPage pg = a.pages[T.page];
+            myp = static_cast<uint32_t>(T.page);
+            myrow0 = static_cast<uint32_t>(T.row0);
+            mym = static_cast<uint32_t>(T.nrows);
+            myinf = a.info[T.page];
+            mytp = static_cast<uint32_t>(a.page_tile0[T.page]);
+            mysize = static_cast<uint32_t>(max(pg.size, 0));
+            myoff = pg.off;
+            myfirst = static_cast<uint64_t>(pg.first_row);
+        }
+        uint2 rq0, rq1, rq2, rq3;
+        uint4 sq0, sq1, sq2, sq3, sq4;
+        uint32_t tnn = 0;
+        auto prefetch = [&](int i) {
+            const uint32_t inf = __builtin_amdgcn_readlane(myinf, i);
+            const uint32_t pp = __builtin_amdgcn_readlane(myp, i);
+            const uint32_t sz = __builtin_amdgcn_readlane(mysize, i);
+            const uint32_t tp = __builtin_amdgcn_readlane(mytp, i);
+            const uint64_t off = rl64(myoff, i);
+            const bool skip = (inf & kSkip) || !lean;  // k_pipe_runs marks pages past the stage
+            const uint32_t nd = skip ? 0u : (inf & 0xFFu), ni = skip ? 0u : ((inf >> 8) & 0xFFu);
+            const uint2* rd_ = a.runs + static_cast<size_t>(pp) * 2 * kPipeRunCap;
+            const uint2 z = make_uint2(0u, 0u);
+            rq0 = lane() < nd ? rd_[lane()] : z;
+            rq1 = lane() + kWave < nd ? rd_[lane() + kWave] : z;
+            rq2 = lane() < ni ? rd_[kPipeRunCap + lane()] : z;
+            rq3 = lane() + kWave < ni ? rd_[kPipeRunCap + lane() + kWave] : z;
+            const uint32_t nb = skip ? 0u : (sz + 15) / 16 + 1;
+            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + off);
+            const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+            sq0 = lane() < nb ? src[lane()] : z4;
+            sq1 = lane() + kWave < nb ? src[lane() + kWave] : z4;
+            sq2 = lane() + 2 * kWave < nb ? src[lane() + 2 * kWave] : z4;
+            sq3 = lane() + 3 * kWave < nb ? src[lane() + 3 * kWave] : z4;
+            sq4 = lane() + 4 * kWave < nb ? src[lane() + 4 * kWave] : z4;
+            // non-null counts of the page's earlier tiles (pages of <= 2048 rows: <= 3)
+            const uint32_t t = static_cast<uint32_t>(c0 + i);
+            tnn = (md > 0 && !skip && tp + lane() < t) ? static_cast<uint32_t>(a.tile_nn[tp + lane()]) : 0u;
+        };
+        prefetch(0);
+        for (int i = 0; i < cn; i++) {
+            const int t = c0 + i;
+            const uint32_t inf = __builtin_amdgcn_readlane(myinf, i);
+            const int p = static_cast<int>(__builtin_amdgcn_readlane(myp, i));
+            const uint32_t r0 = __builtin_amdgcn_readlane(myrow0, i), m = __builtin_amdgcn_readlane(mym, i);
+            const uint32_t size = __builtin_amdgcn_readlane(mysize, i);
+            const int64_t first_row = static_cast<int64_t>(rl64(myfirst, i));
+            const bool skip = (inf & kSkip) || !lean;
+            // this tile's records and payload -> LDS
+            const uint2 d0 = rq0, d1 = rq1, x0 = rq2, x1 = rq3;
+            const uint32_t k0n = tnn;
+            L.recd[lane()] = rq0;
+            L.recd[lane() + kWave] = rq1;
+            L.reci[lane()] = rq2;
+            L.reci[lane() + kWave] = rq3;
+            uint4* st4 = reinterpret_cast<uint4*>(L.stage);
+            st4[lane()] = sq0;
+            st4[lane() + kWave] = sq1;
+            st4[lane() + 2 * kWave] = sq2;
+            st4[lane() + 3 * kWave] = sq3;
+            st4[lane() + 4 * kWave] = sq4;
+            // the previous tile's stores, then the next tile's loads
+            if (pend) {
+                store_packed8(a.codes, pR0, l8, pm, pw);
+                tile_done(a, pt, pch);
+                pend = false;
+            }
+            if (i + 1 < cn) prefetch(i + 1);
+            if (skip) continue;  // marked pages: the exact decoder after the loop (flist)
+            const uint32_t zw = ((size + 15) / 16 + 1) * 4 - 1;  // last word of the slot: zero
+            const uint32_t nd = inf & 0xFFu, ni = (inf >> 8) & 0xFFu, bwi = (inf >> 16) & 0xFFu;
+            const uint32_t maski = (1u << bwi) - 1u;
+            *reinterpret_cast<uint2*>(L.mark + l8) = make_uint2(0u, 0u);
+            *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(0u, 0u);
+            // def levels of rows r0 + 8l .. r0 + 8l + 7
+            uint32_t vb;
+            if (md > 0) {
+                const uint32_t rd0 = run_at_reg(d0, d1, nd, r0);
+                __builtin_amdgcn_wave_barrier();
+                {
+                    const uint32_t k = lane(), st = rr_start(d0);
+                    if (k < nd && k > rd0 && st < r0 + m) L.mark[st - r0] = static_cast<uint8_t>(k - rd0);
+                    const uint32_t k1 = lane() + kWave, st1 = rr_start(d1);
+                    if (k1 < nd && k1 > rd0 && st1 < r0 + m) L.mark[st1 - r0] = static_cast<uint8_t>(k1 - rd0);
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint2 mk = *reinterpret_cast<const uint2*>(L.mark + l8);
+                uint32_t rm[8], run = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
+                    rm[k] = run;
+                }
+                const uint32_t ex = wave_shr1(wave_incl_max(run));
+                vb = 0;
+                bool above = false;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t j = l8 + k;
+                    const uint2 R = L.recd[(rd0 + max(ex, rm[k])) & (kPipeRunCap - 1)];
+                    const uint32_t pay = rr_pay(R);
+                    const uint32_t lb = sbits3(L.stage, pay + (r0 + j - rr_start(R)) * bwd, zw, maskd);
+                    const uint32_t lvl = rr_lit(R) ? lb : pay;
+                    const bool in = j < m;
+                    vb |= (in && lvl == md ? 1u : 0u) << k;
+                    above |= in && lvl > md;
+                }
+                if (__ballot(above)) {  // levels above max_def: outside the supported format
+                    set_err(a.page_err + p, a.err_any, PQ_ERR_UNSUPPORTED, 0, 0, size);
+                    for (uint32_t j = lane(); j < m; j += kWave) a.codes[first_row + r0 + j] = kNull;
+                    if (lane() == 0) a.tile_chars[t] = 0;
+                    __builtin_amdgcn_wave_barrier();
+                    continue;
+                }
+            } else {
+                vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
+            }
+            const uint32_t nnl = __popc(vb);
+            const uint32_t nincl = wave_incl_scan(nnl);
+            const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
+            const uint32_t k0 = md > 0 ? wave_sum(k0n) : r0;
+            // dictionary index runs over ranks [k0, k0 + nn): run of each rank -> mark2
+            const uint32_t ri0 = run_at_reg(x0, x1, ni, k0);
+            if (nn) {
+                __builtin_amdgcn_wave_barrier();
+                {
+                    const uint32_t k = lane(), st = rr_start(x0);
+                    if (k < ni && k > ri0 && st < k0 + nn) L.mark2[st - k0] = static_cast<uint8_t>(k - ri0);
+                    const uint32_t k1 = lane() + kWave, st1 = rr_start(x1);
+                    if (k1 < ni && k1 > ri0 && st1 < k0 + nn) L.mark2[st1 - k0] = static_cast<uint8_t>(k1 - ri0);
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint2 mk = *reinterpret_cast<const uint2*>(L.mark2 + l8);
+                uint32_t rm[8], run = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
+                    rm[k] = run;
+                }
+                const uint32_t ex = wave_shr1(wave_incl_max(run));
+                uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t v = max(ex, rm[k]);
+                    if (k < 4) w0 |= v << (8 * k);
+                    else w1 |= v << (8 * (k - 4));
+                }
+                __builtin_amdgcn_wave_barrier();
+                *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(w0, w1);
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            uint32_t chars = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t rk = min(rbase + __popc(vb & ((1u << k) - 1u)), static_cast<uint32_t>(kTileRows - 1));
+                const uint2 R = L.reci[(ri0 + L.mark2[rk]) & (kPipeRunCap - 1)];
+                const uint32_t pay = rr_pay(R);
+                const uint32_t lb = sbits3(L.stage, pay + (k0 + rk - rr_start(R)) * bwi, zw, maski);
+                const uint32_t v = rr_lit(R) ? lb : pay;
+                const bool ok = ((vb >> k) & 1u) && v < dict_n;
+                const uint32_t len = lens[ok ? v : 0u];
+                chars += ok ? len : 0u;
+                const uint32_t code = ok ? v : static_cast<uint32_t>(kNull);
+                if (k & 1) pw[k >> 1] |= code << 16;
+                else pw[k >> 1] = code;
+            }
+            pch = wave_sum(chars);
+            pend = true;
+            pR0 = first_row + r0;
+            pm = m;
+            pt = t;
+        }
+    }
+    if (pend) {
+        store_packed8(a.codes, pR0, l8, pm, pw);
+        tile_done(a, pt, pch);
+    }
+    // pages k_pipe_runs / k_pipe_big marked (complete before this launch):
+    // the exact serial decoder, one wave per page
+    const int nf = flist[0];
+    for (int i = static_cast<int>(blockIdx.x) * kCodeWaves3 + wv; i < nf; i += nw) {
+        exact_page(a, LX, flist[1 + i], dict_n, ebase);
+        __builtin_amdgcn_wave_barrier();
+    }
+    // a dictionary longer than the length table (not planned: lt_n covers
+    // every entry the page can hold): every unmarked page exactly
+    if (!lean) {
+        for (int t = ta; t < tb; t++) {
+            const DevTile T = a.tiles[t];
+            if (T.row0 == 0 && !(a.info[T.page] & kSkip)) exact_page(a, LX, T.page, dict_n, ebase);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// ── run tables and codes of a page in one wave ─────────────────────────────
+// k_pipe_page replaces k_pipe_runs + k_pipe_codes3 for chunks whose small
+// pages (<= kPipeSmallRows rows) all fit kPageStage.  One wave per page: the
+// payload in LDS; a run header parsed at every byte of both streams (the next
+// header's position, run_spec.hpp); three pointer-doubling rounds give 8-run
+// jumps; lanes 0 and 1 follow the def and index chains listing every 8th
+// header; one lane per listed header re-parses its 8 runs exactly; a wave scan
+// of the run counts gives every record its first value (truncated at the page
+// value count, an exhausted stream gets its zero run).  These are the records
+// k_pipe_runs writes (walk_runs), kept in LDS; the page's tiles are then
+// expanded as in k_pipe_codes3, with the page's non-null count carried from
+// tile to tile (no count pass).  Pages outside that shape (bad headers before
+// the value count, more than kPipeRunCap runs, bit widths > 16, prologue
+// errors) go to flist for the exact decoder.
+constexpr int kPageWaves = 4;
+constexpr uint32_t kPageStage = 2048;         // staged payload bytes (+16 zero) per wave
+constexpr int kPJumpLog = 3;
+constexpr uint32_t kPJump = 1u << kPJumpLog;
+constexpr uint32_t kPList = (kPipeRunCap - kPJump - 1) / kPJump + 1;  // listed headers per stream
+constexpr uint32_t kPStop = 0xFFFFu;
+constexpr int kPPer = kPageStage / kWave;     // byte positions per lane
+
+struct PageLds {
+    uint32_t stage[kPageStage / 4];
+    uint16_t tab[kPageStage];
+    uint2 rec[2][kPipeRunCap];
+    uint32_t list[2][kPList + 1];
+    uint32_t esum[2][kPList + 1];
+    uint8_t mark[kTileRows];
+    uint8_t mark2[kTileRows];
+};
+
+__global__ void __launch_bounds__(kPageWaves * 64) k_pipe_page(CodeArgs a, int npages, uint32_t lt_n,
+                                                               uint32_t* __restrict__ info, int32_t* __restrict__ flist) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lens[];
+    __shared__ PageLds lds_all[kPageWaves];
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    PageLds& L = lds_all[wv];
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    const uint32_t nl = min(dict_n, lt_n);
+    const bool lean = dict_n <= lt_n;
+    copy_map(lens, a.entries + ebase, nl, threadIdx.x, blockDim.x,
+             [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
+    __syncthreads();
+    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
+    const uint32_t maskd = (1u << bwd) - 1u, nbd = (bwd + 7) / 8;
+    const uint32_t l8 = lane() * 8;
+    const int nw = static_cast<int>(gridDim.x) * kPageWaves;
+    for (int p = static_cast<int>(blockIdx.x) * kPageWaves + wv; p < npages; p += nw) {
+        const DevPage pg = a.pages[p];
+        const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+        if (n > static_cast<uint32_t>(kPipeSmallRows)) continue;  // k_pipe_big
+        const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+        const int32_t tile0 = a.page_tile0[p];
+        const int64_t first_row = pg.first_row;
+        bool fail = size + 16 > kPageStage || !lean;
+        if (!fail) {  // payload + the slot's zero padding -> LDS
+            const uint32_t nb = (size + 15) / 16 + 1;
+            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + pg.off);
+            uint4* st4 = reinterpret_cast<uint4*>(L.stage);
+            const uint4 v0 = lane() < nb ? src[lane()] : make_uint4(0u, 0u, 0u, 0u);
+            const uint4 v1 = lane() + kWave < nb ? src[lane() + kWave] : make_uint4(0u, 0u, 0u, 0u);
+            st4[lane()] = v0;
+            st4[lane() + kWave] = v1;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // prologue (column_reader.cpp:146-182): def section, rep section, bit width
+        uint32_t pos = 0, dbase = 0, dlen = 0, bwi = 0;
+        if (!fail && md > 0) {
+            if (size < 4) fail = true;
+            else {
+                dlen = L.stage[0];
+                pos = 4;
+                if (static_cast<uint64_t>(pos) + dlen > size) fail = true;
+                else { dbase = 4; pos += dlen; }
+            }
+        }
+        if (!fail && a.max_rep > 0) {
+            if (pos + 4 > size) fail = true;
+            else {
+                const uint32_t rl = static_cast<uint32_t>(lds_u64(L.stage, pos));
+                pos += 4;
+                if (static_cast<uint64_t>(pos) + rl > size) fail = true;
+                else pos += rl;
+            }
+        }
+        if (!fail) {
+            if (pos + 1 > size) fail = true;
+            else { bwi = static_cast<uint32_t>(lds_u64(L.stage, pos)) & 0xFFu; pos += 1; }
+        }
+        if (!fail && bwi > 16) fail = true;
+        const uint32_t nbi = (bwi + 7) / 8, de = dbase + dlen;
+        uint32_t nrec0 = 0, nrec1 = 0;
+        if (!fail) {
+            // 1. next-header position at every byte of both streams
+            for (uint32_t j = lane(); j < size; j += kWave) {
+                const bool s1 = j >= pos, s0 = md > 0 && j >= dbase && j < de;
+                uint32_t nx = kPStop;
+                if (s0 || s1) {
+                    const uint32_t e = s1 ? size : de, bw = s1 ? bwi : bwd, nbv = s1 ? nbi : nbd;
+                    const SpecHdr h = spec_hdr(L.stage, j);
+                    const uint32_t q = h.lit ? (h.g > 0xFFFFu ? 0x10000u : h.qh + h.g * bw) : h.qh + nbv;
+                    if (!spec_bad(h, e, nbv) && q < e) nx = q;
+                }
+                L.tab[j] = static_cast<uint16_t>(nx);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // 2. 8-run jumps (all reads of a round before its writes)
+            for (int r = 0; r < kPJumpLog; r++) {
+                uint32_t nv[kPPer / 2];
+#pragma unroll
+                for (int i = 0; i < kPPer; i++) {
+                    const uint32_t j = lane() + static_cast<uint32_t>(i) * kWave;
+                    uint32_t t = kPStop;
+                    if (j < size) {
+                        t = L.tab[j];
+                        if (t != kPStop) t = L.tab[t];
+                    }
+                    if (i & 1) nv[i >> 1] |= t << 16;
+                    else nv[i >> 1] = t;
+                }
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int i = 0; i < kPPer; i++) {
+                    const uint32_t j = lane() + static_cast<uint32_t>(i) * kWave;
+                    if (j < size) L.tab[j] = static_cast<uint16_t>(nv[i >> 1] >> (16 * (i & 1)));
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            // 3. every 8th header of each chain (lane 0: def, lane 1: index)
+            uint32_t k = 0;
+            if (lane() < 2 && (lane() == 1 || md > 0)) {
+                const uint32_t s = lane();
+                uint32_t q = s ? pos : dbase;
+                const uint32_t e = s ? size : de;
+                for (;;) {
+                    if (k >= kPList) { k = ~0u; break; }
+                    L.list[s][k++] = q;
+                    if (q >= e) break;
+                    const uint32_t t = L.tab[q];
+                    if (t == kPStop) break;
+                    q = t;
+                }
+            }
+            const uint32_t k0l = __builtin_amdgcn_readlane(k, 0), k1l = __builtin_amdgcn_readlane(k, 1);
+            if (k0l == ~0u || k1l == ~0u) fail = true;
+            const uint32_t nl0 = md > 0 ? k0l : 0u, nl1 = k1l;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // 4. exact runs of each listed header: untruncated counts, first bad step
+            const bool li = lane() < nl0 + nl1;
+            const uint32_t s = lane() >= nl0 ? 1u : 0u, i = s ? lane() - nl0 : lane();
+            uint32_t sum = 0, meta = 0;
+            if (!fail && li) {
+                const uint32_t e = s ? size : de, bw = s ? bwi : bwd, nbv = s ? nbi : nbd;
+                const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+                const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
+                uint32_t q = L.list[s][i], r = 0, bad = kPJump, ended = 0;
+                uint2* out = L.rec[s] + i * kPJump;
+                for (; r < kPJump; r++) {
+                    if (q >= e) { ended = 1; break; }
+                    const SpecHdr h = spec_hdr(L.stage, q);
+                    if (spec_bad(h, e, nbv)) { bad = r; break; }
+                    const uint32_t c = h.lit ? min(h.g, kSpCountCap / 8) * 8 : min(h.g, kSpCountCap);
+                    out[r] = make_uint2(c, h.lit ? (litpay | (h.qh * litmul)) : (h.vraw & vmask));
+                    sum = min(sum + c, kSpCountCap);
+                    const uint64_t nql = static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw;
+                    q = h.lit ? (nql > e ? e : static_cast<uint32_t>(nql)) : h.qh + nbv;
+                }
+                if (r == kPJump && q >= e) ended = 1;
+                meta = r | (bad << 8) | (ended << 16);
+            }
+            // 5. first value of every record (a scan per stream), truncation at n,
+            //    an exhausted stream's zero run
+            const uint32_t incl = wave_incl_scan(li ? sum : 0u);
+            const uint32_t tot0 = nl0 ? __builtin_amdgcn_readlane(incl, static_cast<int>(nl0) - 1) : 0u;
+            const uint32_t b0 = incl - sum - (s ? tot0 : 0u);
+            __builtin_amdgcn_wave_barrier();
+            uint32_t nrec = 0;
+            bool sbad = false;
+            if (!fail && li && b0 < n) {
+                const uint32_t nr = meta & 0xFFu, bad = (meta >> 8) & 0xFFu, ended = meta >> 16;
+                const uint32_t last = s ? nl0 + nl1 - 1 : nl0 - 1;
+                uint2* out = L.rec[s] + i * kPJump;
+                uint32_t c0 = b0, kept = 0;
+                for (uint32_t r = 0; r < nr && c0 < n; r++) {
+                    const uint32_t c = out[r].x;
+                    out[r].x = c0 | (min(c, n - c0) << 16);
+                    c0 += c;
+                    kept = r + 1;
+                }
+                if (c0 >= n) {
+                    nrec = i * kPJump + kept;
+                } else if (bad < kPJump || (lane() == last && (!ended || i * kPJump + nr >= kPipeRunCap))) {
+                    sbad = true;  // a bad header before the value count
+                } else if (lane() == last) {  // exhausted: the rest of the values are 0
+                    out[nr] = make_uint2(c0 | ((n - c0) << 16), 0u);
+                    nrec = i * kPJump + nr + 1;
+                }
+            }
+            if (__ballot(sbad)) fail = true;
+            const uint64_t h0 = __ballot(nrec != 0 && s == 0), h1 = __ballot(nrec != 0 && s == 1);
+            nrec0 = h0 ? __builtin_amdgcn_readlane(nrec, static_cast<int>(__builtin_ctzll(h0))) : 0u;
+            nrec1 = h1 ? __builtin_amdgcn_readlane(nrec, static_cast<int>(__builtin_ctzll(h1))) : 0u;
+            if ((md > 0 && nrec0 == 0 && n > 0) || (nrec1 == 0 && n > 0)) fail = true;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (fail) {  // the exact decoder (k_pipe_exact over flist)
+            if (lane() == 0) {
+                info[p] = kFallback;
+                flist[1 + atomicAdd(flist, 1)] = p;
+            }
+            continue;
+        }
+        if (lane() == 0) info[p] = kBig;  // codes written here
+        // ── the page's tiles: codes and characters ──
+        const uint32_t zw = ((size + 15) / 16 + 1) * 4 - 1;  // last word of the slot: zero
+        const uint32_t maski = (1u << bwi) - 1u;
+        const uint2 d0 = lane() < nrec0 ? L.rec[0][lane()] : make_uint2(0u, 0u);
+        const uint2 d1 = lane() + kWave < nrec0 ? L.rec[0][lane() + kWave] : make_uint2(0u, 0u);
+        const uint2 x0 = lane() < nrec1 ? L.rec[1][lane()] : make_uint2(0u, 0u);
+        const uint2 x1 = lane() + kWave < nrec1 ? L.rec[1][lane() + kWave] : make_uint2(0u, 0u);
+        uint32_t kacc = 0;  // non-null rows of the page's earlier tiles
+        for (uint32_t r0 = 0, ti = 0; r0 < n; r0 += kTileRows, ti++) {
+            const uint32_t m = min(n - r0, static_cast<uint32_t>(kTileRows));
+            const int t = tile0 + static_cast<int>(ti);
+            *reinterpret_cast<uint2*>(L.mark + l8) = make_uint2(0u, 0u);
+            *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(0u, 0u);
+            uint32_t vb;
+            if (md > 0) {
+                const uint32_t rd0 = run_at_reg(d0, d1, nrec0, r0);
+                __builtin_amdgcn_wave_barrier();
+                {
+                    const uint32_t k = lane(), st = rr_start(d0);
+                    if (k < nrec0 && k > rd0 && st < r0 + m) L.mark[st - r0] = static_cast<uint8_t>(k - rd0);
+                    const uint32_t k1 = lane() + kWave, st1 = rr_start(d1);
+                    if (k1 < nrec0 && k1 > rd0 && st1 < r0 + m) L.mark[st1 - r0] = static_cast<uint8_t>(k1 - rd0);
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint2 mk = *reinterpret_cast<const uint2*>(L.mark + l8);
+                uint32_t rm[8], run = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
+                    rm[k] = run;
+                }
+                const uint32_t ex = wave_shr1(wave_incl_max(run));
+                vb = 0;
+                bool above = false;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t j = l8 + k;
+                    const uint2 R = L.rec[0][(rd0 + max(ex, rm[k])) & (kPipeRunCap - 1)];
+                    const uint32_t pay = rr_pay(R);
+                    const uint32_t lb = sbits3(L.stage, pay + (r0 + j - rr_start(R)) * bwd, zw, maskd);
+                    const uint32_t lvl = rr_lit(R) ? lb : pay;
+                    const bool in = j < m;
+                    vb |= (in && lvl == md ? 1u : 0u) << k;
+                    above |= in && lvl > md;
+                }
+                if (__ballot(above)) {  // levels above max_def: outside the supported format
+                    set_err(a.page_err + p, a.err_any, PQ_ERR_UNSUPPORTED, 0, 0, size);
+                    for (uint32_t j = lane(); j < m; j += kWave) a.codes[first_row + r0 + j] = kNull;
+                    if (lane() == 0) a.tile_chars[t] = 0;
+                    __builtin_amdgcn_wave_barrier();
+                    continue;
+                }
+            } else {
+                vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
+            }
+            const uint32_t nnl = __popc(vb);
+            const uint32_t nincl = wave_incl_scan(nnl);
+            const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
+            const uint32_t k0 = md > 0 ? kacc : r0;
+            kacc += nn;
+            const uint32_t ri0 = run_at_reg(x0, x1, nrec1, k0);
+            if (nn) {
+                __builtin_amdgcn_wave_barrier();
+                {
+                    const uint32_t k = lane(), st = rr_start(x0);
+                    if (k < nrec1 && k > ri0 && st < k0 + nn) L.mark2[st - k0] = static_cast<uint8_t>(k - ri0);
+                    const uint32_t k1 = lane() + kWave, st1 = rr_start(x1);
+                    if (k1 < nrec1 && k1 > ri0 && st1 < k0 + nn) L.mark2[st1 - k0] = static_cast<uint8_t>(k1 - ri0);
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint2 mk = *reinterpret_cast<const uint2*>(L.mark2 + l8);
+                uint32_t rm[8], run = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
+                    rm[k] = run;
+                }
+                const uint32_t ex = wave_shr1(wave_incl_max(run));
+                uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t v = max(ex, rm[k]);
+                    if (k < 4) w0 |= v << (8 * k);
+                    else w1 |= v << (8 * (k - 4));
+                }
+                __builtin_amdgcn_wave_barrier();
+                *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(w0, w1);
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            uint32_t chars = 0, pw[4], cw[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t rk = min(rbase + __popc(vb & ((1u << k) - 1u)), static_cast<uint32_t>(kTileRows - 1));
+                const uint2 R = L.rec[1][(ri0 + L.mark2[rk]) & (kPipeRunCap - 1)];
+                const uint32_t pay = rr_pay(R);
+                const uint32_t lb = sbits3(L.stage, pay + (k0 + rk - rr_start(R)) * bwi, zw, maski);
+                const uint32_t v = rr_lit(R) ? lb : pay;
+                const bool ok = ((vb >> k) & 1u) && v < dict_n;
+                const uint32_t len = lens[ok ? v : 0u];
+                chars += ok ? len : 0u;
+                const uint32_t code = ok ? v : static_cast<uint32_t>(kNull);
+                cw[k] = code;
+            }
+            // (packed with v_perm: the |= form crashes instruction selection here)
+#pragma unroll
+            for (int k = 0; k < 4; k++) pw[k] = __builtin_amdgcn_perm(cw[2 * k + 1], cw[2 * k], 0x05040100u);
+            store_packed8(a.codes, first_row + r0, l8, m, pw);
+            tile_done(a, t, wave_sum(chars));
+            __builtin_amdgcn_wave_barrier();
+        }
     }
 }
 
@@ -1491,13 +2119,14 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes) {
 }
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
-                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist) {
+                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
+                      bool lean_codes) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     if (npages <= 0) return;
     const int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
     const int per = kRunWaves * ppw;
     hipLaunchKernelGGL(k_pipe_runs, dim3((npages + per - 1) / per), dim3(kRunWaves * kWave), 0, s, bytes, pages,
-                       npages, max_def, max_rep, runs, info, ppw, flist);
+                       npages, max_def, max_rep, runs, info, ppw, flist, lean_codes ? kStage3 - 16 : 0xFFFFFFFFu);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's
@@ -1524,27 +2153,59 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     // persistent: the entry-length table (u16 per entry) is loaded once per workgroup
     const uint32_t lt_n = P.dict_entries_cap;
     const uint32_t lds = (lt_n * 2 + 15) / 16 * 16;
-    static uint32_t attr = 0;
-    if (lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_codes2),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-        attr = lds;
+    const void* fn = P.lean_codes ? reinterpret_cast<const void*>(k_pipe_codes3) : reinterpret_cast<const void*>(k_pipe_codes2);
+    static uint32_t attr[2] = {0, 0};
+    if (lds > attr[P.lean_codes]) {
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+        attr[P.lean_codes] = lds;
     }
     // resident workgroups per CU (LDS and registers), so the grid is one wave of blocks
     int bpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(k_pipe_codes2),
-                                                     kCodeWaves2 * kWave, lds) != hipSuccess || bpc < 1)
+    const int waves = P.lean_codes ? kCodeWaves3 : kCodeWaves2;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, waves * kWave, lds) != hipSuccess || bpc < 1)
         bpc = 1;
-    const int need = (P.ntiles + kCodeWaves2 - 1) / kCodeWaves2;
+    const int need = (P.ntiles + waves - 1) / waves;
     const int grid = max(1, min(need, P.cus * bpc));
     // also decodes the pages the run-table passes marked (flist)
-    if (P.has_small) {
+    if (P.has_small && P.lean_codes) {
+        hipLaunchKernelGGL(k_pipe_codes3, dim3(grid), dim3(kCodeWaves3 * kWave), lds, s, a, lt_n, P.flist);
+    } else if (P.has_small) {
         hipLaunchKernelGGL(k_pipe_codes2, dim3(grid), dim3(kCodeWaves2 * kWave), lds, s, a, lt_n, P.flist);
     } else {  // only k_pipe_big pages: the marked ones need the exact decoder alone
         hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, (P.npages + kCodeWaves - 1) / kCodeWaves))),
                            dim3(kCodeWaves * kWave), 0, s, a, P.flist);
     }
 }
+
+void launch_pipe_page(hipStream_t s, const PipeLaunch& P) {
+    if (P.npages <= 0) return;
+    int wgrid = 0, per = 0;
+    write_shape(P, &wgrid, &per);
+    CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
+               P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
+               P.bsum, per, P.debug};
+    const uint32_t lt_n = P.dict_entries_cap;
+    const uint32_t lds = (lt_n * 2 + 15) / 16 * 16;
+    static uint32_t attr = 0;
+    if (lds > attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_page), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds));
+        attr = lds;
+    }
+    int bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(k_pipe_page), kPageWaves * kWave,
+                                                     lds) != hipSuccess || bpc < 1)
+        bpc = 1;
+    const int need = (P.npages + kPageWaves - 1) / kPageWaves;
+    const int grid = max(1, min(need, P.cus * bpc));
+    hipLaunchKernelGGL(k_pipe_page, dim3(grid), dim3(kPageWaves * kWave), lds, s, a, P.npages, lt_n,
+                       const_cast<uint32_t*>(P.info), const_cast<int32_t*>(P.flist));
+    // pages it could not take: the exact decoder
+    hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, (P.npages + kCodeWaves - 1) / kCodeWaves))),
+                       dim3(kCodeWaves * kWave), 0, s, a, P.flist);
+}
+
+uint32_t pipe_page_stage() { return kPageStage; }
 
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
     if (P.ntiles <= 0) return;

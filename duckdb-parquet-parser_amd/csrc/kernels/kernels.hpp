@@ -124,6 +124,7 @@ struct PipeLaunch {
     uint32_t dict_entries_cap;  // entry-table capacity of the dictionary (k_pipe_codes length table)
     int cus;
     bool has_small;             // some pages of <= kPipeSmallRows rows (k_pipe_runs / k_pipe_codes2)
+    bool lean_codes;            // k_pipe_codes3 instead of k_pipe_codes2
 };
 struct PipePlan {
     uint32_t lds;       // dynamic LDS bytes of k_pipe_write
@@ -131,9 +132,15 @@ struct PipePlan {
 };
 PipePlan plan_pipe_lds(uint32_t dict_bytes);
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
-                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist);
+                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
+                      bool lean_codes);
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
+// small pages' run tables and codes in one pass (one wave per page), then the
+// exact decoder for the pages it lists; replaces launch_pipe_runs +
+// launch_pipe_codes when every small page's payload fits pipe_page_stage() - 16
+void launch_pipe_page(hipStream_t s, const PipeLaunch& P);
+uint32_t pipe_page_stage();
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,
 // then codes and tile characters (one workgroup per listed page)
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens);

@@ -35,15 +35,20 @@ SMALL = [
 ]
 
 
-@pytest.fixture(params=["pipe", "walk", "batch", "fused", "generic"])
+@pytest.fixture(params=["pipe", "walk", "page", "codes2", "batch", "fused", "generic"])
 def path(request, ctx):
     """Every kernel path: BYTE_ARRAY three-pass dictionary (dict_pipe.hip) and
     two-pass PLAIN (plain_ba.hip: rows one lane per page, or under "walk" one
     wave per window), batched dictionary (dict_batch.hip), per-page fused
     (dict_fused.hip) and generic (decode.hip); fixed-width PLAIN
     tile-parallel (fixed_fast.hip) except under "generic", which runs
-    decode.hip's per-page k_fixed."""
-    pipe = request.param in ("pipe", "walk")
+    decode.hip's per-page k_fixed.  "page" takes k_pipe_page (run tables and
+    codes per page in one pass) and replays the decode as a HIP graph;
+    "codes2" takes k_pipe_codes2 instead of k_pipe_codes3."""
+    pipe = request.param in ("pipe", "walk", "page", "codes2")
+    ctx.set_option("page", int(request.param == "page"))
+    ctx.set_option("graph", int(request.param == "page"))
+    ctx.set_option("codes3", int(request.param != "codes2"))
     ctx.set_option("dict_pipe", int(pipe))
     ctx.set_option("plain_ba", int(pipe))
     ctx.set_option("plain_rows", int(request.param == "pipe"))
@@ -51,6 +56,9 @@ def path(request, ctx):
     ctx.set_option("batch", int(request.param == "batch"))
     ctx.set_option("fixed_plain", int(request.param != "generic"))
     yield request.param
+    ctx.set_option("page", 0)
+    ctx.set_option("graph", 0)
+    ctx.set_option("codes3", 1)
     ctx.set_option("dict_pipe", 1)
     ctx.set_option("plain_ba", 1)
     ctx.set_option("plain_rows", 1)
