@@ -56,6 +56,8 @@ struct pq_ctx {
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
     bool opt_plain_rows = false; // "plain_rows": rows pass one lane per page from HBM (k_plain_rows), else k_plain_walk (LDS windows)
+    bool opt_write2 = false;     // "write2": k_pipe_write2 (loader wave + writer waves), set before upload
+    int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
     bool opt_page = false;       // "page": k_pipe_page (runs + codes per page) where every small page fits its stage;
                                  // C2: 0.104 ms vs k_pipe_runs 0.036 + k_pipe_codes3 0.044, so off by default
     bool opt_codes3 = true;      // "codes3": k_pipe_codes3 (lean tile loop), else k_pipe_codes2
@@ -114,6 +116,8 @@ struct pq_chunk {
     int32_t* d_flist = nullptr;
     bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
     bool pipe_page = false;             // every small page fits k_pipe_page's stage
+    bool pipe_write2 = false;           // planned (LDS, grid) for k_pipe_write2
+    int pipe_wpw = 10;                  // k_pipe_write writer waves per workgroup (planned)
     std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
     int32_t* d_bigp = nullptr;
     uint32_t big_max_bytes = 0;
@@ -392,7 +396,8 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
         return;
     const uint32_t chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
     const uint32_t dict_bytes = 16 + chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
-    const pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes);
+    const int wpw = std::max(1, std::min(16, ctx->opt_write_waves));
+    const pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes, ctx->opt_write2, wpw);
     if (pl.blocks_per_cu == 0) return;
     int cus = 256;
     hipDeviceProp_t prop;
@@ -411,6 +416,8 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->pipe_grid = cus * pl.blocks_per_cu;
     c->pipe_ecap = static_cast<uint32_t>(ecap);
     c->pipe_cus = cus;
+    c->pipe_write2 = ctx->opt_write2;
+    c->pipe_wpw = wpw;
 }
 
 // PLAIN BYTE_ARRAY chunks without levels go through plain_ba.hip: windows of
@@ -641,6 +648,8 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
     if (std::strcmp(key, "plain_rows") == 0) { ctx->opt_plain_rows = value != 0; return 0; }
+    if (std::strcmp(key, "write_waves") == 0) { ctx->opt_write_waves = value; return 0; }
+    if (std::strcmp(key, "write2") == 0) { ctx->opt_write2 = value != 0; return 0; }
     if (std::strcmp(key, "page") == 0) { ctx->opt_page = value != 0; return 0; }
     if (std::strcmp(key, "codes3") == 0) { ctx->opt_codes3 = value != 0; return 0; }
     if (std::strcmp(key, "big_all") == 0) { ctx->opt_big_all = value != 0; return 0; }
@@ -1020,6 +1029,8 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     P.cus = c->pipe_cus;
     P.has_small = c->pipe_small;
     P.lean_codes = ctx->opt_codes3;
+    P.write2 = c->pipe_write2;
+    P.write_waves = c->pipe_wpw;
     return P;
 }
 

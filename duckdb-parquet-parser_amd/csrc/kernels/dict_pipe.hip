@@ -44,7 +44,8 @@ constexpr uint32_t kBig = 1u << 30;           // info flag: k_pipe_big wrote the
 constexpr uint32_t kSkip = kFallback | kBig;  // k_pipe_codes2 leaves the page alone
 constexpr int kCodeWaves = 4;
 constexpr uint16_t kNull = 0xFFFFu;
-constexpr int kWriteWaves = 6;
+constexpr int kWriteMax = 16;                // writer waves per k_pipe_write workgroup: runtime wpw <= this
+constexpr int kLoadGroup = 6;                // k_pipe_write2's loader: tiles whose codes load together
 constexpr uint32_t kFront = 16;               // zero bytes before the LDS dictionary
 constexpr uint32_t kLitCapP = 16;
 
@@ -197,13 +198,14 @@ struct CodeArgs {
     unsigned long long* bsum;  // characters per k_pipe_write workgroup (its tiles)
     int per;                   // tiles per k_pipe_write wavefront
     int debug;                 // 256: skip the exact decoder (timing only)
+    int wpw;                   // k_pipe_write's writer waves per workgroup (bsum index)
 };
 
 // Characters of tile t also go to the k_pipe_write workgroup that writes it.
 __device__ __forceinline__ void tile_done(const CodeArgs& a, int t, uint32_t chars) {
     if (lane() == 0) {
         a.tile_chars[t] = chars;
-        if (chars) atomicAdd(&a.bsum[(t / a.per) / kWriteWaves], static_cast<unsigned long long>(chars));
+        if (chars) atomicAdd(&a.bsum[(t / a.per) / a.wpw], static_cast<unsigned long long>(chars));
     }
 }
 
@@ -1376,6 +1378,11 @@ __device__ __forceinline__ uint4 lds16(const uint32_t* w, uint32_t A) {
                       __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
 }
 
+struct WriteSlot {  // k_pipe_write2: one tile's codes handed from the loader to a writer
+    uint4 c[kWave];
+    uint32_t seq, ack, pad[2];
+};
+
 struct WriteArgs {
     const uint8_t* bytes;
     const DevPage* pages;
@@ -1398,9 +1405,10 @@ struct WriteArgs {
     uint8_t* chars;
     uint32_t dict_chars_bytes, dict_bytes;
     int debug;  // ablation: 2 = no characters, 4 = no offsets/validity stores, 8 = prologue only
+    int wpw;    // writer waves per workgroup
 };
 
-__global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
+__global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // [kFront zero bytes][dictionary payload][entry table][per-wave scratch]
     uint32_t* dwa = reinterpret_cast<uint32_t*>(smem);
@@ -1423,11 +1431,11 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
     // descriptors of up to 64 tiles are loaded at once, one per lane, and the
     // next tile's codes are loaded before this tile's stores are issued
     const int per = a.per;
-    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * kWriteWaves + wv) * per);
+    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
     const int tb = min(a.ntiles, ta + per);
     // first output byte of the range: the workgroups before this one (bsum,
     // summed by k_pipe_codes), then this workgroup's earlier tiles
-    __shared__ unsigned long long red[kWriteWaves];
+    __shared__ unsigned long long red[kWriteMax];
     auto wave_sum64 = [](unsigned long long v) {
         for (int d = 1; d < kWave; d <<= 1) {
             const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
@@ -1444,10 +1452,10 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
     }
     __syncthreads();
     int64_t Grun = 0;
-    for (int w = 0; w < kWriteWaves; w++) Grun += static_cast<int64_t>(red[w]);
+    for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
     if (a.debug & 8) return;
     {
-        const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * kWriteWaves) * per);
+        const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
         unsigned long long in = 0;
         for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
         Grun += static_cast<int64_t>(wave_sum64(in));
@@ -1577,6 +1585,335 @@ __global__ void __launch_bounds__(kWriteWaves * 64) k_pipe_write(WriteArgs a) {
             // LDS first costs more than it saves: byte-unaligned LDS accesses
             // are slow; scripts/probe/unaligned_store.hip)
             const int64_t G1 = G0 + total;
+            if (a.debug & 128) {  // timing only: the tile's bytes as aligned 16-byte blocks of zeros
+                const int64_t b0 = G0 & ~static_cast<int64_t>(15);
+                for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < G1; blk += 16 * kWave) {
+                    const uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                    if (blk >= G0 && blk + 16 <= G1) *reinterpret_cast<uint4*>(a.chars + blk) = v;
+                    else store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, G0) - blk),
+                                    static_cast<uint32_t>(min(blk + 16, G1) - blk));
+                }
+                continue;
+            }
+            for (uint32_t g0 = 0; g0 < m; g0 += kWave) {
+                const uint32_t r = g0 + lane();
+                uint32_t s0 = 0, ln = 0, sa = 0;
+                if (r < m) {
+                    s0 = S.off[r];
+                    ln = S.off[r + 1] - s0;
+                    sa = kFront + S.src[r];
+                }
+                const bool lng = ln > kLongRow;
+                if (!lng && ln) {
+                    uint8_t* d = a.chars + G0 + s0;
+                    if (ln >= 16) {
+                        for (uint32_t x = 0; x + 16 < ln; x += 16) {
+                            const uint4 v = lds16(dwa, sa + x);
+                            *reinterpret_cast<U16B*>(d + x) = U16B{v.x, v.y, v.z, v.w};
+                        }
+                        const uint4 v = lds16(dwa, sa + ln - 16);
+                        *reinterpret_cast<U16B*>(d + ln - 16) = U16B{v.x, v.y, v.z, v.w};
+                    } else {
+                        const uint4 v = lds16(dwa, sa);           // bytes 0 .. 15 of the row's source
+                        const uint32_t t = ln >= 8 ? ln - 8 : (ln >= 4 ? ln - 4 : (ln >= 2 ? ln - 2 : 0u));
+                        const uint4 u = lds16(dwa, sa + t);       // bytes t .. t + 15
+                        if (ln >= 8) {
+                            *reinterpret_cast<U8B*>(d) = U8B{v.x, v.y};
+                            *reinterpret_cast<U8B*>(d + t) = U8B{u.x, u.y};
+                        } else if (ln >= 4) {
+                            *reinterpret_cast<U4B*>(d) = U4B{v.x};
+                            *reinterpret_cast<U4B*>(d + t) = U4B{u.x};
+                        } else if (ln >= 2) {
+                            *reinterpret_cast<U2B*>(d) = U2B{static_cast<uint16_t>(v.x)};
+                            *reinterpret_cast<U2B*>(d + t) = U2B{static_cast<uint16_t>(u.x)};
+                        } else {
+                            d[0] = static_cast<uint8_t>(v.x);
+                        }
+                    }
+                }
+                uint64_t lm = __ballot(lng);
+                while (lm) {  // long rows: the whole wave, aligned destination blocks
+                    const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
+                    lm &= lm - 1;
+                    const int64_t A0 = G0 + __builtin_amdgcn_readlane(s0, l);
+                    const int64_t A1 = A0 + __builtin_amdgcn_readlane(ln, l);
+                    const uint32_t src0 = __builtin_amdgcn_readlane(sa, l);
+                    const int64_t b0 = A0 & ~static_cast<int64_t>(15);
+                    for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < A1; blk += 16 * kWave) {
+                        const uint4 v = lds16(dwa, static_cast<uint32_t>(src0 + (blk - A0)));
+                        store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, A0) - blk),
+                                   static_cast<uint32_t>(min(blk + 16, A1) - blk));
+                    }
+                }
+            }
+            (void)G1;
+        }
+        }
+    }
+}
+
+// k_pipe_write with a loader wave: the writers' only global loads were the
+// codes of their tiles, and on gfx9 a load waits for every store issued
+// before it (vmcnt).  Here a seventh wave loads each writer's next tile into
+// an LDS slot (sequence / acknowledge words), so the writer waves issue
+// stores only and never drain them.
+__global__ void __launch_bounds__((kWriteMax + 1) * 64) k_pipe_write2(WriteArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // [kFront zero bytes][dictionary payload][entry table][per-wave scratch]
+    uint32_t* dwa = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* dw = reinterpret_cast<uint32_t*>(smem + kFront);
+    uint32_t* dtab = reinterpret_cast<uint32_t*>(smem + kFront + a.dict_chars_bytes);
+    const uint32_t wv = threadIdx.x / kWave;
+    WriteLds& S = reinterpret_cast<WriteLds*>(smem + a.dict_bytes)[min(wv, static_cast<uint32_t>(a.wpw - 1))];
+    WriteSlot* slots = reinterpret_cast<WriteSlot*>(smem + a.dict_bytes + a.wpw * sizeof(WriteLds));
+    const DevDict d = a.dicts[a.dict_id];
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
+        uint4* dst = reinterpret_cast<uint4*>(dw);
+        copy_blocks(dst, src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
+        copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
+            return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
+        });
+    }
+    if (wv < a.wpw && lane() == 0) {
+        slots[wv].seq = 0;
+        slots[wv].ack = 0;
+    }
+    __syncthreads();
+    // each wavefront owns a contiguous run of tiles (consecutive rows): the
+    // descriptors of up to 64 tiles are loaded at once, one per lane, and the
+    // next tile's codes are loaded before this tile's stores are issued
+    const int per = a.per;
+    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
+    const int tb = min(a.ntiles, ta + per);
+    auto wave_sum64 = [](unsigned long long v) {
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
+            const uint32_t hi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v >> 32), d));
+            v += (static_cast<unsigned long long>(hi) << 32) | lo;
+        }
+        return v;
+    };
+    if (wv == a.wpw) {  // the loader: codes of every writer's next tile -> its LDS slot
+        if (a.debug & 8) return;
+        const int TA = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
+        const int TB = min(a.ntiles, TA + a.wpw * per);
+        int64_t dR0 = 0, dR1 = 0, dR2 = 0, dR3 = 0;  // tiles TA + lane + 64c (launch: a.wpw * per <= 256)
+        uint32_t dm0 = 0, dm1 = 0, dm2 = 0, dm3 = 0;
+        auto dload = [&](int c, int64_t& R, uint32_t& mm) {
+            const int t = TA + static_cast<int>(lane()) + 64 * c;
+            if (t < TB) {
+                const DevTile T = a.tiles[t];
+                R = a.pages[T.page].first_row + T.row0;
+                mm = static_cast<uint32_t>(T.nrows);
+            }
+        };
+        dload(0, dR0, dm0);
+        dload(1, dR1, dm1);
+        dload(2, dR2, dm2);
+        dload(3, dR3, dm3);
+        const uint32_t l8 = lane() * kRowsPerLane;
+        for (int i = 0; i < per; i++) {
+            // writers in groups of kLoadGroup: their tiles' codes load together, then fill the slots
+            for (int w0 = 0; w0 < a.wpw; w0 += kLoadGroup) {
+                uint4 v[kLoadGroup];
+#pragma unroll
+                for (int u = 0; u < kLoadGroup; u++) {
+                    v[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+                    const int w = w0 + u;
+                    const int t = TA + w * per + i;
+                    if (w < a.wpw && t < TB) {
+                        const int j = t - TA, c = j >> 6, l = j & 63;
+                        const int64_t Rs = c == 0 ? dR0 : (c == 1 ? dR1 : (c == 2 ? dR2 : dR3));
+                        const uint32_t ms = c == 0 ? dm0 : (c == 1 ? dm1 : (c == 2 ? dm2 : dm3));
+                        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(Rs), l);
+                        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(Rs) >> 32), l);
+                        const int64_t R = static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+                        const uint32_t mm = __builtin_amdgcn_readlane(ms, l);
+                        if (l8 < mm) {
+                            const U16B x = *reinterpret_cast<const U16B*>(a.codes + R + l8);
+                            v[u] = make_uint4(x.x, x.y, x.z, x.w);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kLoadGroup; u++) {
+                    const int w = w0 + u;
+                    if (w >= a.wpw || TA + w * per + i >= TB) continue;
+                    volatile uint32_t* ack = &slots[w].ack;
+                    while (*ack != static_cast<uint32_t>(i)) __builtin_amdgcn_s_sleep(1);
+                    asm volatile("" ::: "memory");
+                    slots[w].c[lane()] = v[u];
+                    asm volatile("" ::: "memory");
+                    if (lane() == 0) *reinterpret_cast<volatile uint32_t*>(&slots[w].seq) = static_cast<uint32_t>(i + 1);
+                }
+            }
+        }
+        return;
+    }
+    // a writer takes tile tt's codes from its slot and frees it
+    auto take = [&](int tt) -> uint4 {
+        const uint32_t r = static_cast<uint32_t>(tt - ta);
+        volatile uint32_t* seq = &slots[wv].seq;
+        while (*seq != r + 1) __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        const uint4 v = slots[wv].c[lane()];
+        asm volatile("" ::: "memory");
+        if (lane() == 0) *reinterpret_cast<volatile uint32_t*>(&slots[wv].ack) = r + 1;
+        return v;
+    };
+    // first output byte of the range: the workgroups before this one (bsum,
+    // summed by k_pipe_codes), then this workgroup's earlier tiles
+    int64_t Grun = 0;
+    {
+        unsigned long long acc = 0;
+        for (uint32_t b = lane(); b < blockIdx.x; b += kWave) acc += a.bsum[b];
+        Grun = static_cast<int64_t>(wave_sum64(acc));
+    }
+    if (a.debug & 8) return;
+    {
+        const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
+        unsigned long long in = 0;
+        for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
+        Grun += static_cast<int64_t>(wave_sum64(in));
+    }
+    for (int c0 = ta; c0 < tb; c0 += kWave) {
+        const int cn = min(kWave, tb - c0);
+        int64_t myR0 = 0, myG0 = 0;
+        uint32_t mym = 0;
+        uint32_t myc = 0;
+        if (static_cast<int>(lane()) < cn) {
+            const DevTile T = a.tiles[c0 + lane()];
+            myR0 = a.pages[T.page].first_row + T.row0;
+            mym = static_cast<uint32_t>(T.nrows);
+            myc = static_cast<uint32_t>(a.tile_chars[c0 + lane()]);
+        }
+        {  // tile characters < 2^25 each: a 32-bit scan over <= 64 tiles
+            const uint32_t inc = wave_incl_scan(myc);
+            myG0 = Grun + static_cast<int64_t>(inc - myc);
+            Grun += static_cast<int64_t>(bcast_last(inc));
+        }
+        auto rl64 = [](int64_t v, int i) -> int64_t {
+            const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
+            const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), i);
+            return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+        };
+        // codes of kWBatch tiles at a time -> LDS: the only global loads of
+        // the tile loop, so one wait (which also drains this wave's earlier
+        // stores: loads and stores share vmcnt) per batch, not per tile
+        const uint32_t l8 = lane() * kRowsPerLane;
+        for (int ib = 0; ib < cn; ib += kWBatch) {
+            // four named registers (an indexed array would go to scratch)
+            static_assert(kWBatch == 4, "batch registers");
+            auto ld = [&](int i) -> uint4 {
+                uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+                if (i < cn) {
+                    const int64_t R = rl64(myR0, i);
+                    const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
+                    if (l8 < mm) {
+                        const U16B x = *reinterpret_cast<const U16B*>(a.codes + R + l8);
+                        v = make_uint4(x.x, x.y, x.z, x.w);
+                    }
+                }
+                return v;
+            };
+            (void)ld;
+        for (int i = ib; i < min(cn, ib + kWBatch); i++) {
+            const int64_t R0 = rl64(myR0, i);
+            const int64_t G0 = rl64(myG0, i);
+            const uint32_t m = __builtin_amdgcn_readlane(mym, i);
+            uint32_t cur[kRowsPerLane];
+            {
+                const int u = i - ib;  // register select (no dynamic indexing into cv)
+                (void)u;
+                const uint4 w = take(c0 + i);
+                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++)
+                    cur[k] = l8 + k < m ? (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : kNull;
+            }
+            // this lane's rows 8l .. 8l + 7: lengths, dictionary offsets, validity
+            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0;
+#pragma unroll
+            for (int k = 0; k < kRowsPerLane; k++) {
+                const bool valid = cur[k] < dict_n;
+                const uint32_t e = valid ? dtab[cur[k]] : 0u;
+                len[k] = e >> 16;
+                src[k] = e & 0xFFFFu;
+                vb |= (valid ? 1u : 0u) << k;
+                acc += len[k];
+            }
+            const uint32_t incl = wave_incl_scan(acc);
+            const uint32_t total = bcast_last(incl);
+            {
+                uint32_t o = incl - acc;
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++) {
+                    const uint32_t j = lane() * kRowsPerLane + k;
+                    if (j < m) {
+                        S.off[j] = o;
+                        S.src[j] = static_cast<uint16_t>(src[k]);
+                    }
+                    o += len[k];
+                }
+            }
+            S.vb[lane()] = static_cast<uint8_t>(vb);
+            if (lane() == 0) S.off[m] = total;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            if (!(a.debug & 4)) {
+                // offsets, row j = 64k + lane (coalesced)
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++) {
+                    const uint32_t j = k * kWave + lane();
+                    if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
+                }
+                // validity words [R0 >> 5, (R0 + m - 1) >> 5]: tile word t = vb bytes 4t .. 4t + 3
+                const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
+                const uint32_t sh = static_cast<uint32_t>(R0 & 31);
+                const int64_t g = gfirst + lane();
+                if (g <= glast) {
+                    auto tw = [&](int t) -> uint32_t {
+                        return (t >= 0 && t < kWave / 4) ? reinterpret_cast<const uint32_t*>(S.vb)[t] : 0u;
+                    };
+                    const int t = static_cast<int>(lane());
+                    const uint32_t val = (tw(t) << sh) | (sh ? (tw(t - 1) >> (32 - sh)) : 0u);
+                    // the column's last word belongs to its last tile alone
+                    const bool whole = g * 32 >= R0 && (g * 32 + 32 <= R0 + m || R0 + m == a.nrows_total);
+                    if (whole) a.validity[g] = val;
+                    else if (val) atomicOr(&a.validity[g], val);
+                }
+            }
+            if (R0 + m == a.nrows_total && lane() == 0) {
+                a.offsets[a.nrows_total] = G0 + total;
+                *a.total = G0 + total;
+            }
+            if (total == 0 || (a.debug & 2)) continue;
+            if (G0 + total > a.capacity) {  // output too small: the host grows it and re-runs
+                if (lane() == 0) atomicOr(a.overflow, 1);
+                continue;
+            }
+            // characters, 64 consecutive rows per step: each lane copies its
+            // row from the LDS dictionary to HBM as unaligned 16-byte moves
+            // (the last one overlapping the row's earlier bytes), rows under
+            // 16 bytes as two overlapping 8/4/2-byte moves, so no store leaves
+            // its row and the L2 merges the partial lines.  Rows longer than
+            // kLongRow are copied afterwards by the whole wave, 16-byte
+            // aligned blocks across the lanes.  (Assembling aligned blocks in
+            // LDS first costs more than it saves: byte-unaligned LDS accesses
+            // are slow; scripts/probe/unaligned_store.hip)
+            const int64_t G1 = G0 + total;
+            if (a.debug & 128) {  // timing only: the tile's bytes as aligned 16-byte blocks of zeros
+                const int64_t b0 = G0 & ~static_cast<int64_t>(15);
+                for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < G1; blk += 16 * kWave) {
+                    const uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                    if (blk >= G0 && blk + 16 <= G1) *reinterpret_cast<uint4*>(a.chars + blk) = v;
+                    else store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, G0) - blk),
+                                    static_cast<uint32_t>(min(blk + 16, G1) - blk));
+                }
+                continue;
+            }
             for (uint32_t g0 = 0; g0 < m; g0 += kWave) {
                 const uint32_t r = g0 + lane();
                 uint32_t s0 = 0, ln = 0, sa = 0;
@@ -2101,18 +2438,18 @@ __global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match(const DevTile* 
 
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens) { return big_layout(max_page_bytes, nlens).total; }
 
-PipePlan plan_pipe_lds(uint32_t dict_bytes) {
+PipePlan plan_pipe_lds(uint32_t dict_bytes, bool loader, int wpw) {
     PipePlan pl{};
-    pl.lds = dict_bytes + kWriteWaves * static_cast<uint32_t>(sizeof(WriteLds));
+    pl.lds = dict_bytes + static_cast<uint32_t>(wpw) * static_cast<uint32_t>(sizeof(WriteLds) + (loader ? sizeof(WriteSlot) : 0));
     const uint32_t all = pl.lds;
     pl.blocks_per_cu = all <= 160u * 1024 ? static_cast<int>((160u * 1024) / all) : 0;
     if (pl.blocks_per_cu > 4) pl.blocks_per_cu = 4;
     if (pl.blocks_per_cu > 0) {  // registers may allow fewer
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_write),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(pl.lds));
+        const void* fn = loader ? reinterpret_cast<const void*>(k_pipe_write2) : reinterpret_cast<const void*>(k_pipe_write);
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(pl.lds));
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k_pipe_write),
-                                                         kWriteWaves * kWave, pl.lds) == hipSuccess && occ > 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (wpw + (loader ? 1 : 0)) * kWave, pl.lds) ==
+                hipSuccess && occ > 0)
             pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
     }
     return pl;
@@ -2132,9 +2469,9 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's
 // characters under the workgroup that will write it).
 static void write_shape(const PipeLaunch& P, int* grid, int* per) {
-    const int need = (P.ntiles + kWriteWaves - 1) / kWriteWaves;
+    const int need = (P.ntiles + P.write_waves - 1) / P.write_waves;
     *grid = max(1, min(need, P.grid));
-    const int nw = *grid * kWriteWaves;
+    const int nw = *grid * P.write_waves;
     *per = max(1, (P.ntiles + nw - 1) / nw);
 }
 
@@ -2144,7 +2481,7 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     write_shape(P, &wgrid, &per);
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.bsum, per, P.debug};
+               P.bsum, per, P.debug, P.write_waves};
     if (count_pass) {
         const dim3 grid((P.ntiles + kCodeWaves - 1) / kCodeWaves);
         hipLaunchKernelGGL(k_pipe_codes<true>, grid, dim3(kCodeWaves * kWave), 0, s, a);
@@ -2183,7 +2520,7 @@ void launch_pipe_page(hipStream_t s, const PipeLaunch& P) {
     write_shape(P, &wgrid, &per);
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.bsum, per, P.debug};
+               P.bsum, per, P.debug, P.write_waves};
     const uint32_t lt_n = P.dict_entries_cap;
     const uint32_t lds = (lt_n * 2 + 15) / 16 * 16;
     static uint32_t attr = 0;
@@ -2219,8 +2556,18 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
     write_shape(P, &grid, &per);  // P.grid: resident workgroups (plan_pipe_lds + occupancy)
     WriteArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.dicts, P.dict_id, P.entries, P.dict_count, P.codes,
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
-                P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug};
-    hipLaunchKernelGGL(k_pipe_write, dim3(grid), dim3(kWriteWaves * kWave), P.lds, s, a);
+                P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves};
+    if (P.write2 && per * P.write_waves <= 256) {  // the loader's descriptor registers cover 256 tiles
+        static uint32_t attr2 = 0;
+        if (P.lds > attr2) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_write2),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(P.lds));
+            attr2 = P.lds;
+        }
+        hipLaunchKernelGGL(k_pipe_write2, dim3(grid), dim3((P.write_waves + 1) * kWave), P.lds, s, a);
+        return;
+    }
+    hipLaunchKernelGGL(k_pipe_write, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
 }
 
 void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes) {
@@ -2230,7 +2577,7 @@ void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_page
     write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_write's workgroups
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.bsum, per, P.debug};
+               P.bsum, per, P.debug, P.write_waves};
     const uint32_t lds = big_layout(max_page_bytes, nlens).total;
     static uint32_t attr = 0;
     if (lds > attr) {

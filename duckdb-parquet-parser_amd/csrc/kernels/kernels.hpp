@@ -125,12 +125,14 @@ struct PipeLaunch {
     int cus;
     bool has_small;             // some pages of <= kPipeSmallRows rows (k_pipe_runs / k_pipe_codes2)
     bool lean_codes;            // k_pipe_codes3 instead of k_pipe_codes2
+    bool write2;                // k_pipe_write2 (loader wave) instead of k_pipe_write; P.lds / P.grid planned for it
+    int write_waves;            // writer waves per k_pipe_write workgroup (planned with P.lds / P.grid)
 };
 struct PipePlan {
     uint32_t lds;       // dynamic LDS bytes of k_pipe_write
     int blocks_per_cu;  // 0: the dictionary does not fit
 };
-PipePlan plan_pipe_lds(uint32_t dict_bytes);
+PipePlan plan_pipe_lds(uint32_t dict_bytes, bool loader, int wpw);  // loader: k_pipe_write2 (its LDS slots)
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
                       bool lean_codes);

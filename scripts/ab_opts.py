@@ -29,6 +29,7 @@ ci = next((i for i, c in enumerate(cols) if c.name == colname), 0) if colname el
 f = gen.build(cols, rows, 1, seed=seed, layout=layout)
 F = capi.File(f)
 base = None
+runs = []
 for v in variants:
     ctx = capi.Context(0)
     opts = {} if v == "-" else {k: int(x) for k, x in (kv.split("=") for kv in v.split(","))}
@@ -43,23 +44,34 @@ for v in variants:
     else:
         same = bool(np.array_equal(h.validity, base.validity) and np.array_equal(h.data, base.data) and
                     (h.offsets is None or np.array_equal(h.offsets, base.offsets)))
-    for _ in range(5):
-        dc.decode_async()
-    ctx.sync()
-    steps = 50
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        dc.decode_async()
-    ctx.sync()
-    wall = (time.perf_counter() - t0) / steps * 1e3
-    ctx.timing(True)
-    ctx.timing_reset()
-    for _ in range(10):
-        dc.decode_async()
-    ctx.sync()
-    res = {k: round(ctx.timing_get(k)[0] / 10, 4) for k in KERNELS if ctx.timing_get(k)[1]}
-    ctx.timing(False)
+    runs.append((v, ctx, dc, same))
+# warm the clocks, then three alternating rounds (the median is reported)
+for _ in range(100):
+    runs[0][2].decode_async()
+runs[0][1].sync()
+res = {v: {"wall": [], "ms": []} for v, *_ in runs}
+for rnd in range(3):
+    for v, ctx, dc, same in runs:
+        for _ in range(5):
+            dc.decode_async()
+        ctx.sync()
+        steps = 50
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            dc.decode_async()
+        ctx.sync()
+        res[v]["wall"].append((time.perf_counter() - t0) / steps * 1e3)
+        ctx.timing(True)
+        ctx.timing_reset()
+        for _ in range(10):
+            dc.decode_async()
+        ctx.sync()
+        res[v]["ms"].append({k: ctx.timing_get(k)[0] / 10 for k in KERNELS if ctx.timing_get(k)[1]})
+        ctx.timing(False)
+for v, ctx, dc, same in runs:
+    walls = sorted(res[v]["wall"])
+    wall = walls[len(walls) // 2]
+    ks = res[v]["ms"][0].keys()
+    ms = {k: round(sorted(r[k] for r in res[v]["ms"])[1], 4) for k in ks}
     print(json.dumps({"variant": v, "same_as_first": same, "wall_ms": round(wall, 4),
-                      "Gvalues_s": round(rows / wall / 1e6, 2), "ms": res}), flush=True)
-    dc.free()
-    ctx.close()
+                      "Gvalues_s": round(rows / wall / 1e6, 2), "ms": ms}), flush=True)

@@ -43,11 +43,13 @@ def path(request, ctx):
     (dict_fused.hip) and generic (decode.hip); fixed-width PLAIN
     tile-parallel (fixed_fast.hip) except under "generic", which runs
     decode.hip's per-page k_fixed.  "page" takes k_pipe_page (run tables and
-    codes per page in one pass) and replays the decode as a HIP graph;
+    codes per page in one pass), k_pipe_write2 (loader wave) and replays the
+    decode as a HIP graph;
     "codes2" takes k_pipe_codes2 instead of k_pipe_codes3."""
     pipe = request.param in ("pipe", "walk", "page", "codes2")
     ctx.set_option("page", int(request.param == "page"))
     ctx.set_option("graph", int(request.param == "page"))
+    ctx.set_option("write2", int(request.param == "page"))
     ctx.set_option("codes3", int(request.param != "codes2"))
     ctx.set_option("dict_pipe", int(pipe))
     ctx.set_option("plain_ba", int(pipe))
@@ -58,6 +60,7 @@ def path(request, ctx):
     yield request.param
     ctx.set_option("page", 0)
     ctx.set_option("graph", 0)
+    ctx.set_option("write2", 0)
     ctx.set_option("codes3", 1)
     ctx.set_option("dict_pipe", 1)
     ctx.set_option("plain_ba", 1)
