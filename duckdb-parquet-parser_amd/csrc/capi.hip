@@ -51,6 +51,8 @@ struct pq_ctx {
     bool opt_regex_dfa = true;   // "regex_dfa": DFA kernels (else the NFA kernel)
     bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
     bool opt_regex_codes = true; // "regex_codes": dictionary chunks on the pipe path: match bits over the decode's codes
+    bool opt_regex_stream = false; // "regex_stream": the streaming kernel for chunks without dictionary pages (else
+                                   // windows); C3: 0.52 ms vs 0.33 ms windowed, so off by default
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
@@ -195,6 +197,7 @@ struct pq_chunk {
     uint32_t rwin_bytes = 0, rwin_for_dfa = 0;
     int rwin_grid = 0;
     uint32_t dfa_bytes = 0;
+    bool dfa_full = false;               // the DFA image has full 256-column rows
     std::string prog_pattern;           // pattern of d_prog / d_dfa
     int64_t dict_match_cap = 0;
     pqre::DeviceProgram* d_prog = nullptr;
@@ -645,6 +648,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
         return 0;
     }
     if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
+    if (std::strcmp(key, "regex_stream") == 0) { ctx->opt_regex_stream = value != 0; return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
     if (std::strcmp(key, "plain_rows") == 0) { ctx->opt_plain_rows = value != 0; return 0; }
@@ -1483,6 +1487,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
                 if (int rc2 = hip_check(ctx, hipMemcpy(c->d_dfa, img.data(), img.size(), hipMemcpyHostToDevice), "dfa upload"))
                     return rc2;
                 c->dfa_bytes = static_cast<uint32_t>(img.size());
+                c->dfa_full = reinterpret_cast<const pqre::DevDfa*>(img.data())->full != 0;
             }
             c->prog_pattern = key;
         }
@@ -1506,6 +1511,13 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             pipe_front(ctx, c, P, false);
             Timed t(ctx, "regex_codes");
             pqk::launch_pipe_match(s, P, c->d_dict_match + c->pipe_entry_base, neg, c->d_page_flags);
+        } else if (c->d_dfa && ctx->opt_regex_plain && ctx->opt_regex_stream && c->ndicts == 0) {
+            Timed t(ctx, "regex_stream");
+            int cus = 256;
+            hipDeviceProp_t prop;
+            if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+            pqre::launch_regex_stream(s, c->d_dfa, c->dfa_bytes, c->dfa_full, c->d_bytes, c->d_pages, c->npages, cus, cp,
+                                      neg, c->d_page_flags, c->d_page_err, c->d_flags);
         } else if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {
             (void)hipMemsetAsync(c->d_rwin_ticket, 0, sizeof(int32_t), s);
             Timed t(ctx, "regex_plain");
