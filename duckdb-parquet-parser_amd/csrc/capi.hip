@@ -838,12 +838,15 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         rc |= dalloc(&c->d_dict_err, hdicts.size());
         if (c->pipe) {  // flags | bsum | flist, cleared together
             const size_t fb = 4 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long);
-            rc |= dalloc(&c->d_zero, fb + bb + (hpages.size() + 1) * sizeof(int32_t));
+            // cleared per decode: a multiple of 16 bytes (an odd size takes
+            // a second fill kernel for the tail)
+            const size_t zb = (fb + bb + sizeof(int32_t) + 15) / 16 * 16;
+            rc |= dalloc(&c->d_zero, std::max(zb, fb + bb + (hpages.size() + 1) * sizeof(int32_t)));
             if (c->d_zero) {
                 c->d_flags = reinterpret_cast<int32_t*>(c->d_zero);
                 c->d_bsum = reinterpret_cast<unsigned long long*>(c->d_zero + fb);
                 c->d_flist = reinterpret_cast<int32_t*>(c->d_zero + fb + bb);
-                c->zero_bytes = fb + bb + sizeof(int32_t);
+                c->zero_bytes = zb;
             }
         } else {
             rc |= dalloc(&c->d_flags, 4);
