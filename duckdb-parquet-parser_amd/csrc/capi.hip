@@ -125,6 +125,8 @@ struct pq_chunk {
     uint32_t big_max_bytes = 0;
     int32_t pipe_entry_base = 0;        // entry-table slot of the pipe dictionary's first entry
     uint8_t* d_zero = nullptr;          // pipe chunks: [flags][bsum][flist] in one block, cleared by one memset
+    int32_t* d_dflag = nullptr;         // the side-stream dictionary decode's error flag (sticky, cleared at upload)
+    bool side_synced = false;           // the side stream is ordered after this chunk's upload
     size_t zero_bytes = 4 * sizeof(int32_t);  // bytes of d_flags cleared per decode (flags, bsum, flist[0])
     bool tiles_aligned32 = false;       // every tile starts on a 32-row boundary: k_pipe_write owns whole validity words
     // PLAIN BYTE_ARRAY, REQUIRED (plain_ba.hip)
@@ -350,6 +352,7 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_page_pos);
     dfree(c->d_tile_base);
     dfree(c->d_total);
+    dfree(c->d_dflag);
     dfree(c->d_scan_scratch);
     dfree(c->d_page_flags);
     dfree(c->d_dict_match);
@@ -851,6 +854,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         } else {
             rc |= dalloc(&c->d_flags, 4);
         }
+        if (c->pipe && !hdicts.empty()) rc |= dalloc(&c->d_dflag, 1);
         rc |= dalloc(&c->d_tile_chars, htiles.size());
         if (c->fixed_plain) {
             rc |= dalloc(&c->d_tile_rank, htiles.size());
@@ -920,6 +924,7 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc = hip_check(ctx, hipMemcpyAsync(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc) (void)hipMemsetAsync(c->d_page_err, 0, std::max<size_t>(hpages.size(), 1) * sizeof(DevErr), s);
         if (!rc) (void)hipMemsetAsync(c->d_dict_err, 0, std::max<size_t>(hdicts.size(), 1) * sizeof(DevErr), s);
+        if (!rc && c->d_dflag) (void)hipMemsetAsync(c->d_dflag, 0, sizeof(int32_t), s);
         if (!rc && c->d_unit_win)
             rc = hip_check(ctx, hipMemcpyAsync(c->d_unit_win, c->hunit_win.data(), c->hunit_win.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc && c->d_chunks) {
@@ -1129,13 +1134,21 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
     if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
         // the dictionary (one workgroup) decodes on the side stream while the
-        // run-table pass runs; k_pipe_codes waits for both
-        (void)hipEventRecord(ctx->ev_fork, s);
-        (void)hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0);
+        // run-table pass runs; k_pipe_codes waits for both (ev_join).  The
+        // side stream is ordered after the main stream once per upload (the
+        // image copy): every later dictionary decode of the chunk writes the
+        // same entries, so it may overlap the previous decode's readers.  Its
+        // error flag is its own sticky word (d_dflag), not the per-decode
+        // flags the main stream clears.
+        if (!c->side_synced || ctx->opt_graph) {
+            (void)hipEventRecord(ctx->ev_fork, s);
+            (void)hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0);
+            c->side_synced = !ctx->opt_graph;
+        }
         {
             Timed t(ctx, "dict_index", ctx->side);
             pqk::launch_dict_index(ctx->side, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
-                                   c->d_dict_err, c->d_flags, c->max_dict_bytes);
+                                   c->d_dict_err, c->d_dflag, c->max_dict_bytes);
         }
         (void)hipEventRecord(ctx->ev_join, ctx->side);
     } else if (c->ndicts && c->type == PQ_BYTE_ARRAY) {
@@ -1273,10 +1286,14 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
 
 // Synchronise and turn device error records into the reference's first error.
 static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
-    int32_t flags[4] = {0, 0, 0, 0};
+    int32_t flags[4] = {0, 0, 0, 0}, dflag = 0;
     if (int rc = hip_check(ctx, hipMemcpyAsync(flags, c->d_flags, sizeof flags, hipMemcpyDeviceToHost, ctx->stream), "flags"))
         return rc;
+    if (c->d_dflag)
+        if (int rc = hip_check(ctx, hipMemcpyAsync(&dflag, c->d_dflag, sizeof dflag, hipMemcpyDeviceToHost, ctx->stream), "flags"))
+            return rc;
     if (int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync")) return rc;
+    flags[0] |= dflag;
     if (flags[2] && c->plain_spec && !c->spec_failed) {
         if (std::getenv("PQ_DEBUG_SPEC"))
         {
@@ -1318,7 +1335,9 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             }
         // clear records for the next call
         if (c->npages) (void)hipMemsetAsync(c->d_page_err, 0, c->npages * sizeof(DevErr), ctx->stream);
-        if (c->ndicts) (void)hipMemsetAsync(c->d_dict_err, 0, c->ndicts * sizeof(DevErr), ctx->stream);
+        // (dictionary records of chunks decoded on the side stream stay: the
+        // next decode's dictionary pass may already be writing them again)
+        if (c->ndicts && !c->d_dflag) (void)hipMemsetAsync(c->d_dict_err, 0, c->ndicts * sizeof(DevErr), ctx->stream);
     }
     if (best_code) return set_err(ctx, best_code, best_msg);
     if (c->type == PQ_BYTE_ARRAY && out) {
