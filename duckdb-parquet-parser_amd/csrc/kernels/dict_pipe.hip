@@ -1544,11 +1544,28 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             if (!(a.debug & 4)) {
-                // offsets, row j = 64k + lane (coalesced)
+                // offsets: rows 2j', 2j' + 1 per lane as one 16-byte store when
+                // the tile starts on an even row (coalesced), else row j = 64k + lane
+                if ((R0 & 1) == 0) {
 #pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++) {
-                    const uint32_t j = k * kWave + lane();
-                    if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
+                    for (int k = 0; k < kRowsPerLane / 2; k++) {
+                        const uint32_t j = k * 2 * kWave + 2 * lane();
+                        if (j + 1 < m) {
+                            const uint2 o = *reinterpret_cast<const uint2*>(&S.off[j]);
+                            const int64_t v0 = G0 + o.x, v1 = G0 + o.y;
+                            *reinterpret_cast<uint4*>(a.offsets + R0 + j) =
+                                make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(static_cast<uint64_t>(v0) >> 32),
+                                           static_cast<uint32_t>(v1), static_cast<uint32_t>(static_cast<uint64_t>(v1) >> 32));
+                        } else if (j < m) {
+                            a.offsets[R0 + j] = G0 + S.off[j];
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < kRowsPerLane; k++) {
+                        const uint32_t j = k * kWave + lane();
+                        if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
+                    }
                 }
                 // validity words [R0 >> 5, (R0 + m - 1) >> 5]: tile word t = vb bytes 4t .. 4t + 3
                 const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
