@@ -17,6 +17,9 @@ from pqgpu import capi, gen  # noqa: E402
 
 CONFIGS = {"C2": (gen.c2_cols, gen.REF_LAYOUT, 2), "C2a": (gen.c2_cols, gen.ARROW_LAYOUT, 2),
            "C3": (gen.c3_cols, gen.REF_LAYOUT, 3), "C4": (gen.c4_cols, gen.ARROW_LAYOUT, 4)}
+# library defaults of the options the variants may set (restored after each)
+DEFAULTS = {"write_waves": 10, "codes3": 1, "page": 0, "write2": 0, "graph": 0, "dict_pipe": 1, "plain_ba": 1,
+            "fused_ba": 1, "batch": 0, "fixed_plain": 1, "plain_rows": 0, "big_all": 0, "fused_debug": 0}
 KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "pipe_page", "plain_spec", "pipe_count", "pipe_codes",
            "pipe_write", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba")
 
@@ -28,31 +31,29 @@ cols = mk()
 ci = next((i for i, c in enumerate(cols) if c.name == colname), 0) if colname else 0
 f = gen.build(cols, rows, 1, seed=seed, layout=layout)
 F = capi.File(f)
-base = None
-runs = []
+# one context (several contexts share the process's hardware queues and
+# disturb each other's wall clock); each round uploads the column again under
+# every variant's options, in rotating order; medians are reported
+ctx = capi.Context(0)
+parsed = []
 for v in variants:
-    ctx = capi.Context(0)
-    opts = {} if v == "-" else {k: int(x) for k, x in (kv.split("=") for kv in v.split(","))}
-    for k, x in opts.items():
-        ctx.set_option(k, x)
-    dc = ctx.upload(f, [F.chunk(0, ci)])
-    dc.decode()
-    h = dc.to_host()
-    same = None
-    if base is None:
-        base = h
-    else:
-        same = bool(np.array_equal(h.validity, base.validity) and np.array_equal(h.data, base.data) and
-                    (h.offsets is None or np.array_equal(h.offsets, base.offsets)))
-    runs.append((v, ctx, dc, same))
-# warm the clocks, then three alternating rounds (the median is reported)
-for _ in range(100):
-    runs[0][2].decode_async()
-runs[0][1].sync()
-res = {v: {"wall": [], "ms": []} for v, *_ in runs}
+    parsed.append({} if v == "-" else {k: int(x) for k, x in (kv.split("=") for kv in v.split(","))})
+defaults = {}
+res = [{"wall": [], "ms": [], "same": None} for _ in variants]
+base = None
 for rnd in range(3):
-    for v, ctx, dc, same in runs:
-        for _ in range(5):
+    order = list(range(len(variants)))
+    order = order[rnd % len(order):] + order[:rnd % len(order)]
+    for i in order:
+        for k, x in parsed[i].items():
+            ctx.set_option(k, x)
+        dc = ctx.upload(f, [F.chunk(0, ci)])
+        dc.decode()
+        if rnd == 0:
+            h = dc.to_host()
+            if i == 0:
+                base = h
+        for _ in range(20):
             dc.decode_async()
         ctx.sync()
         steps = 50
@@ -60,18 +61,28 @@ for rnd in range(3):
         for _ in range(steps):
             dc.decode_async()
         ctx.sync()
-        res[v]["wall"].append((time.perf_counter() - t0) / steps * 1e3)
+        res[i]["wall"].append((time.perf_counter() - t0) / steps * 1e3)
         ctx.timing(True)
         ctx.timing_reset()
         for _ in range(10):
             dc.decode_async()
         ctx.sync()
-        res[v]["ms"].append({k: ctx.timing_get(k)[0] / 10 for k in KERNELS if ctx.timing_get(k)[1]})
+        res[i]["ms"].append({k: ctx.timing_get(k)[0] / 10 for k in KERNELS if ctx.timing_get(k)[1]})
         ctx.timing(False)
-for v, ctx, dc, same in runs:
-    walls = sorted(res[v]["wall"])
+        if rnd == 0 and i != 0:
+            res[i]["h"] = dc.to_host()
+        dc.free()
+        for k in parsed[i]:  # back to the defaults of the library
+            ctx.set_option(k, DEFAULTS.get(k, 0))
+for i, v in enumerate(variants):
+    same = None
+    if i and base is not None and "h" in res[i]:
+        h = res[i]["h"]
+        same = bool(np.array_equal(h.validity, base.validity) and np.array_equal(h.data, base.data) and
+                    (h.offsets is None or np.array_equal(h.offsets, base.offsets)))
+    walls = sorted(res[i]["wall"])
     wall = walls[len(walls) // 2]
-    ks = res[v]["ms"][0].keys()
-    ms = {k: round(sorted(r[k] for r in res[v]["ms"])[1], 4) for k in ks}
+    ks = res[i]["ms"][0].keys()
+    ms = {k: round(sorted(r[k] for r in res[i]["ms"])[1], 4) for k in ks}
     print(json.dumps({"variant": v, "same_as_first": same, "wall_ms": round(wall, 4),
                       "Gvalues_s": round(rows / wall / 1e6, 2), "ms": ms}), flush=True)
