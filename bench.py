@@ -40,8 +40,8 @@ ROWS = 10_000_000
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rows", type=int, default=ROWS)
     ap.add_argument("--layout", choices=["ref", "arrow"], default="ref")
     ap.add_argument("--no-regex", action="store_true")
