@@ -53,7 +53,8 @@ struct pq_ctx {
     bool opt_regex_codes = true; // "regex_codes": dictionary chunks on the pipe path: match bits over the decode's codes
     bool opt_regex_stream = false; // "regex_stream": the streaming kernel for chunks without dictionary pages (else
                                    // windows); C3: 0.52 ms vs 0.33 ms windowed, so off by default
-    int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
+    int opt_regex_win = 8192;
+    int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)    // "regex_win": window bytes of the windowed kernel
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
@@ -651,6 +652,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
         return 0;
     }
     if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
+    if (std::strcmp(key, "regex_debug") == 0) { ctx->opt_regex_debug = value; return 0; }
     if (std::strcmp(key, "regex_stream") == 0) { ctx->opt_regex_stream = value != 0; return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
@@ -1544,7 +1546,8 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             (void)hipMemsetAsync(c->d_rwin_ticket, 0, sizeof(int32_t), s);
             Timed t(ctx, "regex_plain");
             pqre::launch_regex_plain(s, c->d_dfa, c->dfa_bytes, c->rwin_bytes, c->d_bytes, c->d_pages, c->d_rwins,
-                                     static_cast<int>(c->hrwins.size()), c->d_rwin_ticket, c->rwin_grid, cp, neg,
+                                     static_cast<int>(c->hrwins.size()), c->d_rwin_ticket, c->rwin_grid, cp,
+                                     (neg ? 1 : 0) | (ctx->opt_regex_debug << 8),
                                      c->d_page_flags, c->d_page_err, c->d_flags);
         } else if (c->d_dfa) {
             Timed t(ctx, "regex_lanes");

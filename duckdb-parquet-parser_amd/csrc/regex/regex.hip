@@ -462,7 +462,8 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
     const bool full = D->full != 0;
     const bool empty_ok = D->empty_string != 0;
     const bool trivial = D->nonempty_trivial != 0;
-    const uint32_t negv = neg != 0;
+    const uint32_t negv = neg & 1;  // bits 8+: timing ablation (1: no DFA pass, 2: no chain walk)
+    const int dbg = neg >> 8;
     const uint32_t wv = threadIdx.x / kWave;
     // per wave: window bytes (+16 zero), string list (u32 per 4 window
     // bytes), per-page inclusive string counts and list bases, hit mask
@@ -494,7 +495,7 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
         const uint32_t* pw = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(stage) + pay);
         const uint32_t size = static_cast<uint32_t>(pg.size);
         uint32_t cnt = 0;
-        if (act) {
+        if (act && !(dbg & 2)) {
             auto rd8 = [&](uint32_t a) { return lds_u64(pw, a); };
             DevErr* err = page_err + pidx;
             uint32_t pos = 0, nn = static_cast<uint32_t>(max(pg.nvals, 0));
@@ -552,7 +553,7 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
         lbase[lane()] = pay / 4;
         const uint32_t total = bcast_last(inc);
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t g0 = 0; g0 < total; g0 += kStrPerLane * kWave) {
+        for (uint32_t g0 = 0; g0 < ((dbg & 1) ? 0u : total); g0 += kStrPerLane * kWave) {
             uint32_t e2[kStrPerLane], off2[kStrPerLane], len2[kStrPerLane], pg2[kStrPerLane];
             bool ok2[kStrPerLane];
 #pragma unroll

@@ -8,6 +8,20 @@
 
 constexpr size_t kTiles = 19531, kA = 4096, kB = 11184;  // bytes per tile (C2: 80 MB + 218 MB)
 
+// lane-contiguous: each lane writes its own run of consecutive blocks of the
+// tile's character range (the layout a lane assembling its own rows would use)
+__global__ void __launch_bounds__(640) k_lanes(uint4* B) {
+    const size_t nw = (size_t)gridDim.x * (blockDim.x / 64);
+    const size_t w = blockIdx.x * (size_t)(blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t l = threadIdx.x & 63;
+    constexpr uint32_t nb = kB / 16, per = (nb + 63) / 64;
+    for (size_t t = w; t < kTiles; t += nw)
+        for (uint32_t i = 0; i < per; i++) {
+            const uint32_t b = l * per + i;
+            if (b < nb) B[t * nb + b] = make_uint4(t, b, 5, 6);
+        }
+}
+
 __global__ void __launch_bounds__(640) k_two(uint4* A, uint4* B, int wa, int wb) {
     const size_t nw = (size_t)gridDim.x * (blockDim.x / 64);
     const size_t w = blockIdx.x * (size_t)(blockDim.x / 64) + threadIdx.x / 64;
@@ -36,6 +50,7 @@ int main() {
                 if (mode == 0) hipLaunchKernelGGL(k_two, dim3(grid), dim3(640), 0, 0, A, B, 1, 1);
                 if (mode == 1) hipLaunchKernelGGL(k_two, dim3(grid), dim3(640), 0, 0, A, B, 1, 0);
                 if (mode == 2) hipLaunchKernelGGL(k_two, dim3(grid), dim3(640), 0, 0, A, B, 0, 1);
+                if (mode == 4) hipLaunchKernelGGL(k_lanes, dim3(grid), dim3(640), 0, 0, B);
                 if (mode == 3) {
                     hipLaunchKernelGGL(k_two, dim3(grid), dim3(640), 0, 0, A, B, 1, 0);
                     hipLaunchKernelGGL(k_two, dim3(grid), dim3(640), 0, 0, A, B, 0, 1);
@@ -45,7 +60,7 @@ int main() {
             hipEventSynchronize(e1);
             float ms = 0;
             hipEventElapsedTime(&ms, e0, e1);
-            const double bytes = (mode == 1 ? kA : mode == 2 ? kB : kA + kB) * (double)kTiles;
+            const double bytes = (mode == 1 ? kA : (mode == 2 || mode == 4) ? kB : kA + kB) * (double)kTiles;
             if (rep) printf("%-28s %8.1f us  %6.2f TB/s\n", name, ms / n * 1e3, bytes / (ms / n * 1e-3) / 1e12);
         }
     };
@@ -53,5 +68,6 @@ int main() {
     run("offsets only", 1);
     run("characters only", 2);
     run("offsets kernel + chars kernel", 3);
+    run("characters, lane-contiguous", 4);
     return 0;
 }

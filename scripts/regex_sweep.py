@@ -15,7 +15,7 @@ f = gen.build(gen.c3_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C3"])
 F = capi.File(f)
 dc = ctx.upload(f, [F.chunk(0, 0)])
 ref = {}
-for win in (8192, 4096, 2048, 16384):
+for win in [int(w) for w in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["8192", "4096", "2048", "16384"])]:
     ctx.set_option("regex_win", win)
     for pat in ("special.*requests", "e", "[0-9]"):
         flags = dc.regex_pages(pat)
