@@ -59,6 +59,7 @@ struct pq_ctx {
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
     bool opt_plain_rows = false; // "plain_rows": rows pass one lane per page from HBM (k_plain_rows), else k_plain_walk (LDS windows)
+    bool opt_zflip = true;       // "zflip": per-decode flags from the block the previous k_pipe_write cleared (else a fill)
     bool opt_write2 = false;     // "write2": k_pipe_write2 (loader wave + writer waves), set before upload
     int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
     bool opt_page = false;       // "page": k_pipe_page (runs + codes per page) where every small page fits its stage;
@@ -125,7 +126,10 @@ struct pq_chunk {
     int32_t* d_bigp = nullptr;
     uint32_t big_max_bytes = 0;
     int32_t pipe_entry_base = 0;        // entry-table slot of the pipe dictionary's first entry
-    uint8_t* d_zero = nullptr;          // pipe chunks: [flags][bsum][flist] in one block, cleared by one memset
+    uint8_t* d_zero = nullptr;          // pipe chunks: two blocks of [flags][bsum][flist], alternating per decode
+    size_t zfull = 0;                   // bytes per block
+    int zsel = 0;                       // block of the current decode
+    bool next_zeroed = false;           // the other block is clear (the last k_pipe_write cleared it)
     int32_t* d_dflag = nullptr;         // the side-stream dictionary decode's error flag (sticky, cleared at upload)
     bool side_synced = false;           // the side stream is ordered after this chunk's upload
     size_t zero_bytes = 4 * sizeof(int32_t);  // bytes of d_flags cleared per decode (flags, bsum, flist[0])
@@ -657,6 +661,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
     if (std::strcmp(key, "plain_rows") == 0) { ctx->opt_plain_rows = value != 0; return 0; }
+    if (std::strcmp(key, "zflip") == 0) { ctx->opt_zflip = value != 0; return 0; }
     if (std::strcmp(key, "write_waves") == 0) { ctx->opt_write_waves = value; return 0; }
     if (std::strcmp(key, "write2") == 0) { ctx->opt_write2 = value != 0; return 0; }
     if (std::strcmp(key, "page") == 0) { ctx->opt_page = value != 0; return 0; }
@@ -846,8 +851,13 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             // cleared per decode: a multiple of 16 bytes (an odd size takes
             // a second fill kernel for the tail)
             const size_t zb = (fb + bb + sizeof(int32_t) + 15) / 16 * 16;
-            rc |= dalloc(&c->d_zero, std::max(zb, fb + bb + (hpages.size() + 1) * sizeof(int32_t)));
+            // two such blocks: a decode uses one while its k_pipe_write clears
+            // the other for the next decode (no fill kernel per decode)
+            const size_t zfull = (std::max(zb, fb + bb + (hpages.size() + 1) * sizeof(int32_t)) + 255) / 256 * 256;
+            rc |= dalloc(&c->d_zero, 2 * zfull);
             if (c->d_zero) {
+                c->zfull = zfull;
+                c->zsel = 0;
                 c->d_flags = reinterpret_cast<int32_t*>(c->d_zero);
                 c->d_bsum = reinterpret_cast<unsigned long long*>(c->d_zero + fb);
                 c->d_flist = reinterpret_cast<int32_t*>(c->d_zero + fb + bb);
@@ -927,6 +937,10 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         if (!rc) (void)hipMemsetAsync(c->d_page_err, 0, std::max<size_t>(hpages.size(), 1) * sizeof(DevErr), s);
         if (!rc) (void)hipMemsetAsync(c->d_dict_err, 0, std::max<size_t>(hdicts.size(), 1) * sizeof(DevErr), s);
         if (!rc && c->d_dflag) (void)hipMemsetAsync(c->d_dflag, 0, sizeof(int32_t), s);
+        if (!rc && c->d_zero) {
+            (void)hipMemsetAsync(c->d_zero, 0, 2 * c->zfull, s);
+            c->next_zeroed = true;
+        }
         if (!rc && c->d_unit_win)
             rc = hip_check(ctx, hipMemcpyAsync(c->d_unit_win, c->hunit_win.data(), c->hunit_win.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc && c->d_chunks) {
@@ -1128,10 +1142,23 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     hipStream_t s = ctx->stream;
     pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
     const bool pipe = c->pipe && ctx->opt_pipe;
-    (void)hipMemsetAsync(c->d_flags, 0, c->zero_bytes, s);  // pipe chunks: flags, bsum and flist[0] at once
     // k_pipe_write stores whole validity words when every tile starts on a
     // 32-row boundary; other paths OR bits into zeroed words
     const bool pipe_path = pipe && !(c->plain && ctx->opt_plain);
+    if (pipe_path && c->d_zero && ctx->opt_zflip) {
+        // flags, bsum and flist[0] of this decode: the other block, which the
+        // previous decode's k_pipe_write cleared (else one fill)
+        c->zsel ^= 1;
+        uint8_t* zb = c->d_zero + static_cast<size_t>(c->zsel) * c->zfull;
+        const size_t fb = 4 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long);
+        c->d_flags = reinterpret_cast<int32_t*>(zb);
+        c->d_bsum = reinterpret_cast<unsigned long long*>(zb + fb);
+        c->d_flist = reinterpret_cast<int32_t*>(zb + fb + bb);
+        if (!c->next_zeroed) (void)hipMemsetAsync(c->d_flags, 0, c->zero_bytes, s);
+        c->next_zeroed = false;
+    } else {
+        (void)hipMemsetAsync(c->d_flags, 0, c->zero_bytes, s);  // pipe chunks: flags, bsum and flist[0] at once
+    }
     if (!(pipe_path && c->tiles_aligned32))
         (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
     if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
@@ -1196,14 +1223,19 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         Timed t(ctx, "plain_ba");
         pqk::launch_plain_ba(s, P);
     } else if (pipe) {
-        const pqk::PipeLaunch P = pipe_launch(ctx, c, out);
+        pqk::PipeLaunch P = pipe_launch(ctx, c, out);
         pipe_front(ctx, c, P, true);
         if (c->ntiles == 0) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
             (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
         }
         Timed t(ctx, "pipe_write");
+        if (c->d_zero) {  // k_pipe_write clears the other block for the next decode
+            P.znext = reinterpret_cast<uint32_t*>(c->d_zero + static_cast<size_t>(c->zsel ^ 1) * c->zfull);
+            P.znext_words = static_cast<uint32_t>(c->zero_bytes / 4);
+        }
         pqk::launch_pipe_write(s, P);
+        if (c->d_zero) c->next_zeroed = true;
     } else if (c->fused) {
         const size_t nr = c->ranges.size();
         (void)hipMemsetAsync(c->d_status, 0, std::max<size_t>(c->npages, 1) * sizeof(uint64_t), s);

@@ -1406,10 +1406,14 @@ struct WriteArgs {
     uint32_t dict_chars_bytes, dict_bytes;
     int debug;  // ablation: 2 = no characters, 4 = no offsets/validity stores, 8 = prologue only
     int wpw;    // writer waves per workgroup
+    uint32_t* znext;  // the next decode's flags/bsum/flist[0] block, cleared here (or null)
+    uint32_t znext_words;
 };
 
 __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.znext)  // the other flags/bsum/flist block, for the next decode (unused by this one)
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.znext_words; i += gridDim.x * blockDim.x) a.znext[i] = 0;
     // [kFront zero bytes][dictionary payload][entry table][per-wave scratch]
     uint32_t* dwa = reinterpret_cast<uint32_t*>(smem);
     uint32_t* dw = reinterpret_cast<uint32_t*>(smem + kFront);
@@ -1676,6 +1680,8 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
 // stores only and never drain them.
 __global__ void __launch_bounds__((kWriteMax + 1) * 64) k_pipe_write2(WriteArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.znext)  // the other flags/bsum/flist block, for the next decode (unused by this one)
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.znext_words; i += gridDim.x * blockDim.x) a.znext[i] = 0;
     // [kFront zero bytes][dictionary payload][entry table][per-wave scratch]
     uint32_t* dwa = reinterpret_cast<uint32_t*>(smem);
     uint32_t* dw = reinterpret_cast<uint32_t*>(smem + kFront);
@@ -2573,7 +2579,7 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
     write_shape(P, &grid, &per);  // P.grid: resident workgroups (plan_pipe_lds + occupancy)
     WriteArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.dicts, P.dict_id, P.entries, P.dict_count, P.codes,
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
-                P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves};
+                P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves, P.znext, P.znext_words};
     if (P.write2 && per * P.write_waves <= 256) {  // the loader's descriptor registers cover 256 tiles
         static uint32_t attr2 = 0;
         if (P.lds > attr2) {

@@ -127,6 +127,8 @@ struct PipeLaunch {
     bool lean_codes;            // k_pipe_codes3 instead of k_pipe_codes2
     bool write2;                // k_pipe_write2 (loader wave) instead of k_pipe_write; P.lds / P.grid planned for it
     int write_waves;            // writer waves per k_pipe_write workgroup (planned with P.lds / P.grid)
+    uint32_t* znext;            // cleared by k_pipe_write (the next decode's flags/bsum/flist[0]), or null
+    uint32_t znext_words;
 };
 struct PipePlan {
     uint32_t lds;       // dynamic LDS bytes of k_pipe_write
