@@ -1472,6 +1472,7 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     uint32_t maxslot = 0;
     for (const auto& p : hp) maxslot = std::max(maxslot, (static_cast<uint32_t>(std::max(p.size, 0)) + 15) / 16 * 16 + 16);
     const uint32_t win = std::max<uint32_t>(static_cast<uint32_t>(ctx->opt_regex_win), maxslot);
+    if (pqre::regex_plain_waves(c->dfa_bytes, win) == 0) return false;
     const uint32_t lds = pqre::regex_plain_lds(c->dfa_bytes, win);
     if (lds > 160 * 1024) return false;
     c->hrwins.clear();
@@ -1505,7 +1506,8 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     const int per_cu = std::max(1, pqre::regex_plain_occupancy(lds));
     c->rwin_bytes = win;
     c->rwin_for_dfa = c->dfa_bytes;
-    c->rwin_grid = std::max(1, std::min<int>(per_cu * cus, static_cast<int>((c->hrwins.size() + 7) / 8)));
+    const int wpb = static_cast<int>(pqre::regex_plain_waves(c->dfa_bytes, win));
+    c->rwin_grid = std::max(1, std::min<int>(per_cu * cus, static_cast<int>((c->hrwins.size() + wpb - 1) / wpb)));
     (void)cus;
     return true;
 }

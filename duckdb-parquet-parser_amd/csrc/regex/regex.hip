@@ -435,11 +435,11 @@ __global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__
 // length chain with one lane per page (LDS latency, not HBM), and lists the
 // strings; then all 64 lanes match the listed strings, two per lane, so two
 // DFA chains (one LDS lookup per byte each) are in flight per lane.
-constexpr uint32_t kPlainWaves = 8;
+constexpr uint32_t kPlainWavesMax = 16;  // waves per workgroup: as many as the LDS holds (host)
 constexpr uint32_t kStrPerLane = 4;  // strings interleaved per lane (independent DFA chains)
 
 
-__global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
+__global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
                                                                   uint32_t dfa_bytes, uint32_t win_bytes,
                                                                   const uint8_t* __restrict__ bytes,
                                                                   const DevPage* __restrict__ pages,
@@ -467,10 +467,10 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
     const uint32_t wv = threadIdx.x / kWave;
     // per wave: window bytes (+16 zero), string list (u32 per 4 window
     // bytes), per-page inclusive string counts and list bases, hit mask
-    uint8_t* wbase = dsm + dfa_bytes + wv * (2 * win_bytes + 16 + 2 * 64 * 4 + 16);
+    uint8_t* wbase = dsm + dfa_bytes + wv * regex_plain_wave_lds(win_bytes);
     uint32_t* stage = reinterpret_cast<uint32_t*>(wbase);
-    uint32_t* list = reinterpret_cast<uint32_t*>(wbase + win_bytes + 16);
-    uint32_t* pref = reinterpret_cast<uint32_t*>(wbase + 2 * win_bytes + 16);
+    uint16_t* list = reinterpret_cast<uint16_t*>(wbase + win_bytes + 16);  // window offset of each string
+    uint32_t* pref = reinterpret_cast<uint32_t*>(wbase + win_bytes + 16 + win_bytes / 2);
     uint32_t* lbase = pref + 64;
     uint32_t* hit = lbase + 64;  // [0..1]: satisfied-page mask of the window
     const uint32_t md = static_cast<uint32_t>(cp.max_def);
@@ -533,13 +533,13 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
                     else pos += rl;
                 }
             }
-            uint32_t* lst = list + pay / 4;  // this page's list region (<= slot / 4 entries)
+            uint16_t* lst = list + pay / 4;  // this page's list region (<= slot / 4 entries)
             for (uint32_t k = 0; k < nn && !code; k++) {  // column_reader.cpp:249-253
                 if (static_cast<uint64_t>(pos) + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; break; }
                 const uint32_t len = static_cast<uint32_t>(rd8(pos));
                 pos += 4;
                 if (static_cast<uint64_t>(pos) + len > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = len; break; }
-                lst[cnt++] = (pay + pos) | (min(len, 0xFFFFu) << 16);  // window offset | length
+                lst[cnt++] = static_cast<uint16_t>(pay + pos);  // window offset (the length is at offset - 4)
                 pos += len;
             }
             if (code) {
@@ -567,9 +567,9 @@ __global__ void __launch_bounds__(kPlainWaves * 64) k_regex_plain(const uint8_t*
                     if (pref[lo + stp - 1] <= g) lo += stp;
                 const uint32_t gl = ok2[h] ? lo : 0u;
                 const uint32_t before = gl ? pref[gl - 1] : 0u;
-                const uint32_t ent = ok2[h] ? list[lbase[gl] + (g - before)] : 0u;
-                off2[h] = ent & 0xFFFFu;
-                len2[h] = ok2[h] ? (ent >> 16) : 0u;
+                const uint32_t ent = ok2[h] ? list[lbase[gl] + (g - before)] : 4u;
+                off2[h] = ent;
+                len2[h] = ok2[h] ? static_cast<uint32_t>(lds_u64(stage, ent - 4)) : 0u;
                 pg2[h] = gl;
                 e2[h] = full ? (DFA_START * kDfaRowBytes) : DFA_START;
             }
@@ -845,8 +845,14 @@ void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, c
                        dicts, dict_count, dict_match, cp, neg, page_flags, page_err, err_any);
 }
 
+uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes) {
+    const uint32_t per = regex_plain_wave_lds(win_bytes);
+    if (dfa_bytes + per > 160u * 1024) return 0;
+    return std::min<uint32_t>(kPlainWavesMax, (160u * 1024 - dfa_bytes) / per);
+}
+
 uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes) {
-    return dfa_bytes + kPlainWaves * (2 * win_bytes + 16 + 2 * 64 * 4 + 16);
+    return dfa_bytes + regex_plain_waves(dfa_bytes, win_bytes) * regex_plain_wave_lds(win_bytes);
 }
 
 void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
@@ -860,18 +866,14 @@ void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, u
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_regex_plain, dim3(grid), dim3(kPlainWaves * kWave), regex_plain_lds(dfa_bytes, win_bytes),
+    hipLaunchKernelGGL(k_regex_plain, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes) * kWave),
+                       regex_plain_lds(dfa_bytes, win_bytes),
                        s, dfa, dfa_bytes, win_bytes, bytes, pages, wins, nwins, ticket, cp, neg, page_flags,
                        page_err, err_any);
 }
 
-int regex_plain_occupancy(uint32_t lds) {
-    int blocks = 0;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_regex_plain),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_regex_plain, kPlainWaves * kWave, lds) != hipSuccess)
-        return 0;
-    return blocks;
+int regex_plain_occupancy(uint32_t lds) {  // the LDS sets it: one workgroup of regex_plain_waves waves per CU
+    return lds <= 160u * 1024 ? 1 : 0;
 }
 
 void launch_regex_pages(hipStream_t s, const DeviceProgram* prog, const uint8_t* bytes,

@@ -80,6 +80,10 @@ void launch_regex_stream(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, 
                          uint8_t* page_flags, pqk::DevErr* page_err, int32_t* err_any);
 
 // Windowed PLAIN scan (chunks without dictionary pages).
+// per wave: the window (+16 zero bytes), a u16 offset per possible string,
+// per-page counts and list bases, the hit mask
+constexpr uint32_t regex_plain_wave_lds(uint32_t win_bytes) { return win_bytes + 16 + win_bytes / 2 + 2 * 64 * 4 + 16; }
+uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes);
 uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes);
 int regex_plain_occupancy(uint32_t lds);
 void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
