@@ -14,6 +14,8 @@
 //                  per-wave ring aligned to 16-byte output blocks (aligned LDS
 //                  moves, 16-byte stores) as in k_pipe_write.  The ring holds a
 //                  whole window, so any group of rows fits.
+#include <algorithm>
+
 #include "kernels/device_common.hpp"
 #include "kernels/kernels.hpp"
 #include "pq_gpu.h"
@@ -43,9 +45,12 @@ __device__ __forceinline__ void lane_err(DevErr* e, int32_t* any, uint32_t pos, 
 __global__ void __launch_bounds__(kWalkWaves * 64) k_plain_walk(PlainLaunch a) {
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[kWalkWaves][kPWin / 4 + 8];
     const int wv = static_cast<int>(threadIdx.x / kWave);
-    const int w = static_cast<int>(blockIdx.x) * kWalkWaves + wv;
-    if (w >= a.nwins || (a.gate && *a.gate)) return;
+    if (a.gate && *a.gate) return;
     uint32_t* stage = stage_all[wv];
+    // persistent: a grid of one wave of workgroups walks the windows in a
+    // grid-stride loop (one workgroup per window group was dispatch-bound)
+    for (int w = static_cast<int>(blockIdx.x) * kWalkWaves + wv; w < a.nwins;
+         w += static_cast<int>(gridDim.x) * kWalkWaves) {
     const DevBatch W = a.wins[w];
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + W.img_lo);
@@ -90,6 +95,8 @@ __global__ void __launch_bounds__(kWalkWaves * 64) k_plain_walk(PlainLaunch a) {
     if (lane() == 0) {
         a.wchars[w] = chars;
         if (chars) atomicAdd(&a.bsum[(w / a.per) / kPWWaves], static_cast<unsigned long long>(chars));
+    }
+    __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -684,7 +691,17 @@ void launch_plain_ba(hipStream_t s, PlainLaunch P) {
             hipLaunchKernelGGL(k_plain_rows, dim3((P.nunits + kRowsWaves * kWave - 1) / (kRowsWaves * kWave)),
                                dim3(kRowsWaves * kWave), 0, s, P);
     } else {
-        hipLaunchKernelGGL(k_plain_walk, dim3((P.nwins + kWalkWaves - 1) / kWalkWaves), dim3(kWalkWaves * kWave), 0, s, P);
+        static int walk_grid = 0;  // resident workgroups of k_plain_walk on this device
+        if (!walk_grid) {
+            int bpc = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(k_plain_walk),
+                                                             kWalkWaves * kWave, 0) != hipSuccess || bpc < 1)
+                bpc = 1;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1) cus = 256;
+            walk_grid = bpc * cus;
+        }
+        const int need = (P.nwins + kWalkWaves - 1) / kWalkWaves;
+        hipLaunchKernelGGL(k_plain_walk, dim3(std::min(need, walk_grid)), dim3(kWalkWaves * kWave), 0, s, P);
     }
     hipLaunchKernelGGL(k_plain_write, dim3(grid), dim3(kPWWaves * kWave), plain_write_lds(), s, P);
 }
