@@ -2,21 +2,24 @@
 // R-PLAIN: column_reader.cpp:213-222 + read_plain_value 249-253, a u32 length
 // then the bytes, per value) in two passes over windows of consecutive pages
 // (one contiguous image range of at most kPWin bytes):
-//   k_plain_walk   one wavefront per window: the window is staged in LDS and
-//                  each lane walks one page's length chain, writing
+//   k_plain_walk   persistent waves, one window at a time: the window is
+//                  staged in LDS and each lane walks one page's length chain, writing
 //                  (position in window, length) per row and the window's
 //                  character count (filed under the k_plain_write workgroup
 //                  that writes the window).  A chain that runs past its page
 //                  is the reference's ByteBuffer error at that position.
 //   k_plain_write  persistent workgroups, each wavefront a contiguous run of
 //                  windows: the window is staged again, rows become int64
-//                  offsets and validity words, and the characters go through a
-//                  per-wave ring aligned to 16-byte output blocks (aligned LDS
-//                  moves, 16-byte stores) as in k_pipe_write.  The ring holds a
-//                  whole window, so any group of rows fits.
+//                  offsets and validity words, and each lane copies its row's
+//                  characters from the staged window with unaligned 16-byte
+//                  moves (row_copy.hpp, as k_pipe_write does; the LDS ring of
+//                  aligned blocks it replaces took 0.44 ms against 0.38 on C3:
+//                  without the ring a wave needs half the LDS, so twice as many
+//                  waves fit a CU).
 #include <algorithm>
 
 #include "kernels/device_common.hpp"
+#include "kernels/row_copy.hpp"
 #include "kernels/kernels.hpp"
 #include "pq_gpu.h"
 
@@ -27,7 +30,6 @@ using namespace dev;
 
 constexpr int kWalkWaves = 4;
 constexpr int kPWWaves = 4;
-constexpr uint32_t kPRing = kPWin + 32;  // a window's characters + the carried partial block
 
 __device__ __forceinline__ uint32_t st_u32(const uint32_t* w, uint32_t a) {
     return __builtin_amdgcn_alignbyte(w[(a >> 2) + 1], w[a >> 2], a & 3);
@@ -102,7 +104,6 @@ __global__ void __launch_bounds__(kWalkWaves * 64) k_plain_walk(PlainLaunch a) {
 
 struct PWLds {
     uint32_t stage[kPWin / 4 + 8];
-    uint4 ring[kPRing / 16];
 };
 
 __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
@@ -137,8 +138,6 @@ __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
         for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.wchars[q]);
         G += static_cast<int64_t>(wave_sum64(in));
     }
-    uint8_t* ring = reinterpret_cast<uint8_t*>(S.ring);
-    const uint8_t* sb = reinterpret_cast<const uint8_t*>(S.stage);
     for (int w = ta; w < tb; w++) {
         const DevBatch W = a.wins[w];
         const int64_t R0 = a.pages[W.p0].first_row;
@@ -172,7 +171,8 @@ __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
         if (!fits && lane() == 0) atomicOr(a.overflow, 1);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        int64_t RB = G0 & ~static_cast<int64_t>(15);  // output address of ring[0]
+        // rows -> int64 offsets (coalesced) and characters, each lane copying
+        // its row from the staged window (row_copy.hpp)
         uint32_t run = 0;
         for (uint32_t g0 = 0; g0 < rows; g0 += kWave) {
             const uint32_t r = g0 + lane();
@@ -182,63 +182,7 @@ __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
             const uint32_t s0 = run + inc - len;
             if (r < rows) a.offsets[R0 + r] = G0 + s0;
             run += bcast_last(inc);
-            if (!fits) continue;
-            if (r < rows && len) {
-                const uint32_t p = static_cast<uint32_t>(G0 + s0 - RB);
-                const uint32_t h = min((4u - (p & 3u)) & 3u, len);
-                {
-                    const uint32_t b0 = sb[q], b1 = sb[q + 1], b2 = sb[q + 2];
-                    if (h > 0) ring[p] = static_cast<uint8_t>(b0);
-                    if (h > 1) ring[p + 1] = static_cast<uint8_t>(b1);
-                    if (h > 2) ring[p + 2] = static_cast<uint8_t>(b2);
-                }
-                const uint32_t p2 = p + h, q2 = q + h, rem = len - h;
-                const uint32_t nd = rem >> 2, sh = q2 & 3u;
-                uint32_t* rw = reinterpret_cast<uint32_t*>(ring) + (p2 >> 2);
-                const uint32_t* sw = S.stage + (q2 >> 2);
-                for (uint32_t d2 = 0; d2 < nd; d2 += 4) {
-                    const uint32_t s0w = sw[d2], s1 = sw[d2 + 1], s2 = sw[d2 + 2], s3 = sw[d2 + 3], s4 = sw[d2 + 4];
-                    rw[d2] = __builtin_amdgcn_alignbyte(s1, s0w, sh);
-                    if (d2 + 1 < nd) rw[d2 + 1] = __builtin_amdgcn_alignbyte(s2, s1, sh);
-                    if (d2 + 2 < nd) rw[d2 + 2] = __builtin_amdgcn_alignbyte(s3, s2, sh);
-                    if (d2 + 3 < nd) rw[d2 + 3] = __builtin_amdgcn_alignbyte(s4, s3, sh);
-                }
-                {
-                    const uint32_t t = rem & 3u, pt = p2 + 4 * nd, qt = q2 + 4 * nd;
-                    const uint32_t b0 = sb[qt], b1 = sb[qt + 1], b2 = sb[qt + 2];
-                    if (t > 0) ring[pt] = static_cast<uint8_t>(b0);
-                    if (t > 1) ring[pt + 1] = static_cast<uint8_t>(b1);
-                    if (t > 2) ring[pt + 2] = static_cast<uint8_t>(b2);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            const bool last = g0 + kWave >= rows;
-            const int64_t gend = G0 + run;
-            const uint32_t nfull = static_cast<uint32_t>((gend - RB) >> 4);
-            const uint32_t nblk = last ? static_cast<uint32_t>((gend - RB + 15) >> 4) : nfull;
-            for (uint32_t b = lane(); b < nblk; b += kWave) {
-                const uint4 v = S.ring[b];
-                const int64_t blk = RB + 16 * static_cast<int64_t>(b);
-                if (blk >= G0 && blk + 16 <= G1) {
-                    *reinterpret_cast<uint4*>(a.chars + blk) = v;
-                } else {
-                    const uint32_t ow[4] = {v.x, v.y, v.z, v.w};
-                    const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
-                    for (int64_t x = gs; x < ge; x++) {
-                        const uint32_t at = static_cast<uint32_t>(x - blk);
-                        a.chars[x] = static_cast<uint8_t>(ow[at >> 2] >> (8 * (at & 3)));
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            if (!last) {
-                if (lane() == 0 && nfull) S.ring[0] = S.ring[nfull];
-                RB += 16 * static_cast<int64_t>(nfull);
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            }
+            if (fits && r < rows && len) rc::copy_row(a.chars + G0 + s0, S.stage, q, len);
         }
         __builtin_amdgcn_wave_barrier();
     }
