@@ -173,16 +173,29 @@ __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // rows -> int64 offsets (coalesced) and characters, each lane copying
         // its row from the staged window (row_copy.hpp)
+        // (the row infos of up to 512 rows load at once: a load inside the
+        // row loop would wait for the previous rows' stores, vmcnt)
         uint32_t run = 0;
-        for (uint32_t g0 = 0; g0 < rows; g0 += kWave) {
-            const uint32_t r = g0 + lane();
-            const uint32_t info = r < rows ? a.rowinfo[R0 + r] : 0u;
-            const uint32_t len = info >> 16, q = info & 0xFFFFu;
-            const uint32_t inc = wave_incl_scan(len);
-            const uint32_t s0 = run + inc - len;
-            if (r < rows) a.offsets[R0 + r] = G0 + s0;
-            run += bcast_last(inc);
-            if (fits && r < rows && len) rc::copy_row(a.chars + G0 + s0, S.stage, q, len);
+        for (uint32_t kb = 0; kb < rows; kb += 8 * kWave) {
+            uint32_t inf[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t r = kb + k * kWave + lane();
+                inf[k] = r < rows ? a.rowinfo[R0 + r] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t g0 = kb + k * kWave;
+                if (g0 >= rows) break;
+                const uint32_t r = g0 + lane();
+                const uint32_t info = inf[k];
+                const uint32_t len = info >> 16, q = info & 0xFFFFu;
+                const uint32_t inc = wave_incl_scan(len);
+                const uint32_t s0 = run + inc - len;
+                if (r < rows) a.offsets[R0 + r] = G0 + s0;
+                run += bcast_last(inc);
+                if (fits && r < rows && len) rc::copy_row(a.chars + G0 + s0, S.stage, q, len);
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
