@@ -53,8 +53,8 @@ struct pq_ctx {
     bool opt_regex_codes = true; // "regex_codes": dictionary chunks on the pipe path: match bits over the decode's codes
     bool opt_regex_stream = false; // "regex_stream": the streaming kernel for chunks without dictionary pages (else
                                    // windows); C3: 0.52 ms vs 0.33 ms windowed, so off by default
-    int opt_regex_win = 8192;
-    int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)    // "regex_win": window bytes of the windowed kernel
+    int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
+    int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
@@ -656,13 +656,17 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
         return 0;
     }
     if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
-    if (std::strcmp(key, "regex_debug") == 0) { ctx->opt_regex_debug = value; return 0; }
+    if (std::strcmp(key, "regex_debug") == 0) { ctx->opt_regex_debug = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "regex_stream") == 0) { ctx->opt_regex_stream = value != 0; return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
     if (std::strcmp(key, "plain_rows") == 0) { ctx->opt_plain_rows = value != 0; return 0; }
     if (std::strcmp(key, "zflip") == 0) { ctx->opt_zflip = value != 0; return 0; }
-    if (std::strcmp(key, "write_waves") == 0) { ctx->opt_write_waves = value; return 0; }
+    if (std::strcmp(key, "write_waves") == 0) {
+        if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "write_waves: 1..16");
+        ctx->opt_write_waves = static_cast<int>(value);
+        return 0;
+    }
     if (std::strcmp(key, "write2") == 0) { ctx->opt_write2 = value != 0; return 0; }
     if (std::strcmp(key, "page") == 0) { ctx->opt_page = value != 0; return 0; }
     if (std::strcmp(key, "codes3") == 0) { ctx->opt_codes3 = value != 0; return 0; }
@@ -671,7 +675,11 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
-    if (std::strcmp(key, "pipe_run_pages") == 0) { ctx->opt_run_pages = static_cast<int>(value); return 0; }
+    if (std::strcmp(key, "pipe_run_pages") == 0) {
+        if (value < 1 || value > 32) return set_err(ctx, PQ_ERR_ARG, "pipe_run_pages: 1..32");
+        ctx->opt_run_pages = static_cast<int>(value);
+        return 0;
+    }
     if (std::strcmp(key, "regex_win") == 0) {
         if (value < 1024 || value > 32768 || value % 16) return set_err(ctx, PQ_ERR_ARG, "regex_win: 1024..32768, multiple of 16");
         ctx->opt_regex_win = static_cast<int>(value);

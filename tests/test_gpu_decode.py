@@ -64,7 +64,7 @@ def path(request, ctx):
     ctx.set_option("codes3", 1)
     ctx.set_option("dict_pipe", 1)
     ctx.set_option("plain_ba", 1)
-    ctx.set_option("plain_rows", 1)
+    ctx.set_option("plain_rows", 0)
     ctx.set_option("fused_ba", 1)
     ctx.set_option("batch", 0)
     ctx.set_option("fixed_plain", 1)
@@ -446,6 +446,16 @@ def test_plain_spec_no_fallback(ctx, case):
     dc.decode_check()
     dc.free()
     assert n == 1 and gn == 0
+
+
+@pytest.mark.parametrize("key,value", [("write_waves", 0), ("write_waves", 17), ("pipe_run_pages", 33),
+                                       ("regex_win", 1000), ("fused_claim", 0), ("no_such_option", 1)])
+def test_set_option_rejects(ctx, key, value):
+    """Out-of-range tuning values and unknown keys fail with PQ_ERR_ARG and
+    leave the setting alone."""
+    with pytest.raises(capi.PqError) as e:
+        ctx.set_option(key, value)
+    assert e.value.code == -20 and key in e.value.msg
 
 
 def to_desc_(chunk):
