@@ -425,7 +425,10 @@ __global__ void __launch_bounds__(kSpecWaves * 64) k_plain_spec(SpecLaunch a) {
     a.cand[static_cast<size_t>(c) * kPCand + sl] = rec;
 }
 
-// k_plain_link: one wave per page, rounds of kLinkStage chunks.  Lane i takes
+// k_plain_link: one wave per page, rounds of kLinkStage chunks.  Each round
+// first tries the speculative link (every chunk's pick from its neighbour's
+// continuing candidate, checked link by link in parallel); when that does not
+// hold for every chunk of the round the serial walk below decides.  Lane i takes
 // chunk i of the round: its candidate records (registers) and a 64-entry
 // table in LDS, entry offset -> exit (0xFFFFFFFF: no candidate there; bit 31:
 // the walk hit a bounds error).  Lane 0 then follows the true chain through
@@ -463,6 +466,35 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
 #pragma unroll
         for (uint32_t s = 0; s < kPCand; s++)
             r[s] = act ? a.cand[static_cast<size_t>(c) * kPCand + s] : make_uint4(kLNone, 0u, 0u, 0u);
+        // Speculation: chunk i is entered where chunk i - 1's first candidate
+        // that continues into chunk i (no bounds error, exit in chunk i's first
+        // 64 bytes) left it.  When every chunk of the round holds a candidate
+        // at that entry whose own exit is the one it advertised, the chain is
+        // consistent link by link and equals the serial walk below (text has
+        // one continuing chain per chunk); anything else takes the serial walk.
+        uint32_t cexit = kLNone;
+#pragma unroll
+        for (int s = static_cast<int>(kPCand) - 1; s >= 0; s--)
+            if (act && r[s].x != kLNone && !(r[s].x >> 31) && r[s].y >= chs + kPChunk && r[s].y < chs + kPChunk + 64)
+                cexit = r[s].y;
+        const uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(cexit), 1));
+        const uint32_t q0 = __builtin_amdgcn_readfirstlane(q), dead0 = __builtin_amdgcn_readfirstlane(dead);
+        const uint32_t e = i == 0 ? ((dead0 || q0 >= size) ? kLNone : q0) : prev;
+        uint4 pr = make_uint4(kLNone, 0u, 0u, 0u);
+        bool found = false;
+#pragma unroll
+        for (uint32_t s = 0; s < kPCand; s++)
+            if (r[s].x != kLNone && (r[s].x & 0x7FFFFFFFu) == e) { pr = r[s]; found = true; }
+        const bool lastc = c + 1 == cend;
+        const bool ok = !act || (found && (lastc || (!(pr.x >> 31) && pr.y == cexit)));
+        uint32_t pk;
+        if (__ballot(!ok) == 0) {
+            pk = act ? (kPickHit | (e - chs)) : kPickNone;
+            const int ll = cend - cb - 1;
+            const uint32_t lerr = __builtin_amdgcn_readlane(pr.x >> 31, ll);
+            if (lerr) dead = 1;
+            else q = __builtin_amdgcn_readlane(pr.y, ll);
+        } else {
         uint4* row = reinterpret_cast<uint4*>(tab + i * 64);
 #pragma unroll
         for (int w = 0; w < 16; w++) row[w] = make_uint4(kLNone, kLNone, kLNone, kLNone);
@@ -501,7 +533,8 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t pk = act ? pick[i] : kPickNone;
+        pk = act ? pick[i] : kPickNone;
+        }
         uint4 rr = make_uint4(kLNone, 0u, 0u, 0u);
         if (pk & kPickHit) {
             const uint32_t e = chs + (pk & 0xFFFFu);

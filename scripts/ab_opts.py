@@ -11,7 +11,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "duckdb-parquet-parser_amd")]
+# AB_PKG: a directory holding another build's pqgpu package (A/B of compile-time constants)
+sys.path[:0] = [ROOT, os.environ.get("AB_PKG") or os.path.join(ROOT, "duckdb-parquet-parser_amd")]
 import numpy as np  # noqa: E402
 from pqgpu import capi, gen  # noqa: E402
 
