@@ -346,20 +346,26 @@ __global__ void __launch_bounds__(kBigWaves * 64) k_plain_big_rows(const uint8_t
 // bytes); every offset whose u32 could be a length (it and its bytes fit in
 // the page) is a candidate, chunk 0's start the only one.  The first kPCand
 // candidates walk the length chain (read_plain_value, column_reader.cpp:
-// 249-253) from the HBM image (L2) until it leaves the chunk, recording where
-// it left, how many strings it read and its first bounds error.  For text the
-// false candidates die at once: four bytes of text are never a length that
-// fits in the page.  Descriptors load once per wave (lane j: chunk j) and the
-// 16 chunks' candidate tests are issued together.
+// 249-253) until it leaves the chunk, recording where it left, how many
+// strings it read and its first bounds error.  For text the false candidates
+// die at once: four bytes of text are never a length that fits in the page.
+// The wave first stages its chunks (kPChunk + 16 bytes each, pages sit in
+// 16-byte aligned slots) in LDS with all loads in flight together, so the
+// candidate tests and the chains read LDS (the chains from HBM/L2 were one
+// dependent load per string: 0.16 ms on C4 c7).
 constexpr int kSpecWaves = 4;
 constexpr int kSpecChunks = kWave / static_cast<int>(kPCand);  // chunks per wave
+constexpr uint32_t kSpecBlocks = kPChunk / 16 + 1;              // 16-byte blocks staged per chunk
+constexpr uint32_t kSpecLoads = (kSpecChunks * kSpecBlocks + kWave - 1) / kWave;
 
 __global__ void __launch_bounds__(kSpecWaves * 64) k_plain_spec(SpecLaunch a) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage_all[kSpecWaves][kSpecChunks * kSpecBlocks * 4 + 4];
     const int wv = static_cast<int>(threadIdx.x / kWave);
     const int cw = (static_cast<int>(blockIdx.x) * kSpecWaves + wv) * kSpecChunks;
     if (cw >= a.nchunks) return;
+    uint32_t* stage = stage_all[wv];
     // lane j < 16: chunk cw + j's page offset, size, chunk start
-    uint32_t d_lo = 0, d_hi = 0, d_size = 0, d_cs = 0, d_first = 0;
+    uint32_t d_lo = 0, d_hi = 0, d_size = 0, d_cs = 0, d_first = 0, d_slot = 0;
     if (static_cast<int>(lane()) < kSpecChunks && cw + static_cast<int>(lane()) < a.nchunks) {
         const uint2 ch = a.chunks[cw + lane()];
         const DevPage pg = a.pages[ch.x];
@@ -368,54 +374,63 @@ __global__ void __launch_bounds__(kSpecWaves * 64) k_plain_spec(SpecLaunch a) {
         d_size = static_cast<uint32_t>(max(pg.size, 0));
         d_cs = ch.y * kPChunk;
         d_first = ch.y == 0 ? 1u : 0u;
+        d_slot = (d_size + 15) / 16 * 16 + 16;  // the page's slot in the image
     }
-    auto desc = [&](int j, const uint8_t*& page, uint32_t& size, uint32_t& cs, uint32_t& first) {
-        const uint64_t off = (static_cast<uint64_t>(__builtin_amdgcn_readlane(d_hi, j)) << 32) |
-                             __builtin_amdgcn_readlane(d_lo, j);
-        page = a.bytes + off;
-        size = __builtin_amdgcn_readlane(d_size, j);
-        cs = __builtin_amdgcn_readlane(d_cs, j);
-        first = __builtin_amdgcn_readlane(d_first, j);
-    };
-    // candidate offsets: lane l tests offset l of every chunk (loads issued together)
-    uint32_t lens[kSpecChunks];
+    // stage: block t of the wave's kSpecChunks x kSpecBlocks (chunk t / kSpecBlocks)
+    {
+        uint4 v[kSpecLoads];
 #pragma unroll
-    for (int j = 0; j < kSpecChunks; j++) {
-        const uint8_t* page; uint32_t size, cs, first;
-        desc(j, page, size, cs, first);
-        const uint32_t q = cs + lane();
-        lens[j] = (cw + j < a.nchunks && q + 4 <= size) ? gword(page, q) : 0xFFFFFFFFu;
+        for (uint32_t u = 0; u < kSpecLoads; u++) {
+            const uint32_t t = lane() + u * kWave;
+            const int j = static_cast<int>(t / kSpecBlocks);
+            const uint32_t blk = t - static_cast<uint32_t>(j) * kSpecBlocks;
+            const int js = min(j, kSpecChunks - 1);  // shuffles with every lane active
+            const uint64_t off = (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(d_hi), js))) << 32) |
+                                 static_cast<uint32_t>(__shfl(static_cast<int>(d_lo), js));
+            const uint32_t cs = static_cast<uint32_t>(__shfl(static_cast<int>(d_cs), js));
+            const uint32_t sl = static_cast<uint32_t>(__shfl(static_cast<int>(d_slot), js));
+            const uint32_t b = cs + blk * 16;
+            v[u] = (j < kSpecChunks && cw + j < a.nchunks && b + 16 <= sl)
+                       ? *reinterpret_cast<const uint4*>(a.bytes + off + b)
+                       : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kSpecLoads; u++) {
+            const uint32_t t = lane() + u * kWave;
+            if (t < kSpecChunks * kSpecBlocks) reinterpret_cast<uint4*>(stage)[t] = v[u];
+        }
     }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // candidate offsets: lane l tests offset l of every chunk
     uint64_t mk = 0;
     const int jm = static_cast<int>(lane() / kPCand), sl = static_cast<int>(lane() % kPCand);
 #pragma unroll
     for (int j = 0; j < kSpecChunks; j++) {
-        const uint8_t* page; uint32_t size, cs, first;
-        desc(j, page, size, cs, first);
+        const uint32_t size = __builtin_amdgcn_readlane(d_size, j);
+        const uint32_t cs = __builtin_amdgcn_readlane(d_cs, j);
+        const uint32_t first = __builtin_amdgcn_readlane(d_first, j);
         const uint32_t q = cs + lane(), ce = min(cs + kPChunk, size);
-        bool plaus = q < ce && q + 4 <= size && static_cast<uint64_t>(q) + 4 + lens[j] <= size;
+        const uint32_t len = q + 4 <= size ? st_u32(stage, static_cast<uint32_t>(j) * kSpecBlocks * 16 + lane()) : 0xFFFFFFFFu;
+        bool plaus = q < ce && q + 4 <= size && static_cast<uint64_t>(q) + 4 + len <= size;
         if (first) plaus = lane() == 0;  // the page's first string starts at 0
         const uint64_t m = __ballot(cw + j < a.nchunks && plaus);
         if (j == jm) mk = m;
     }
-    // this lane's chunk descriptor from lane jm: shuffles with every lane
-    // active (a bpermute from a lane outside exec reads 0)
-    const uint64_t off = (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(d_hi), jm))) << 32) |
-                         static_cast<uint32_t>(__shfl(static_cast<int>(d_lo), jm));
     const uint32_t size = static_cast<uint32_t>(__shfl(static_cast<int>(d_size), jm));
     const uint32_t cs = static_cast<uint32_t>(__shfl(static_cast<int>(d_cs), jm));
-    const uint8_t* page = a.bytes + off;
     const int c = cw + jm;
     if (c >= a.nchunks) return;
     for (int i = 0; i < sl; i++) mk &= mk - 1;  // this lane's candidate: the sl-th set bit
     uint4 rec = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
     if (mk) {
         const uint32_t ce = min(cs + kPChunk, size);
+        const uint32_t sb = static_cast<uint32_t>(jm) * kSpecBlocks * 16 - cs;  // stage byte of page offset 0 (mod 2^32)
         const uint32_t q0 = cs + static_cast<uint32_t>(__builtin_ctzll(mk));
         uint32_t q = q0, cnt = 0, err = 0, need = 0;
         while (q < ce) {
             if (q + 4 > size) { err = 1; need = 4; break; }
-            const uint32_t len = gword(page, q);
+            const uint32_t len = st_u32(stage, sb + q);
             if (static_cast<uint64_t>(q) + 4 + len > size) { err = 1; need = len; q += 4; break; }
             q += 4 + len;
             cnt++;
