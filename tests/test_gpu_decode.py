@@ -28,6 +28,11 @@ SMALL = [
     ("small_int_dict", [gen.Col("i", gen.SMALL_INT, gen.INT64, optional=True, null_frac=0.2, dict_size=7)], 9000),
     ("small_int32_dict", [gen.Col("i", gen.SMALL_INT, gen.INT32, dict_size=300)], 9000),
     ("all_null", [gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=1.0)], 2000),
+    # dictionary entries longer than k_dict_index's 64-byte candidate window:
+    # the fine slices cannot link and the coarse walk decides
+    ("long_dict", [gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, dict_size=600, len_min=40, len_max=300)], 4000),
+    ("mixed_dict", [gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.1, dict_size=3000,
+                            len_min=1, len_max=70)], 6000),
     ("long_strings", [gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.1,
                               dict_size=40, len_min=100, len_max=3000)], 4000),
     ("wide_dict", [gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, dict_size=70000, len_min=1, len_max=6,
