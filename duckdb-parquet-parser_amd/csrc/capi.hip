@@ -44,31 +44,19 @@ struct pq_ctx {
     bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
     int opt_debug = 0;      // "fused_debug": ablation switches for timing studies
     int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
-    uint64_t* d_prof = nullptr;  // "fused_prof": per-phase cycle sums of k_ba_fused / k_ba_batch
-    bool opt_batch = false;      // "batch": batched dictionary path (dict_batch.hip)
+    uint64_t* d_prof = nullptr;  // "fused_prof": per-phase cycle sums of k_ba_fused
     int opt_claim = 1;           // "fused_claim": pages claimed per ticket by k_ba_fused producers (>1 serialises the look-back; diagnostics)
-    int opt_batch_bytes = 12288; // "batch_bytes": payload bytes per batch buffer
     bool opt_regex_dfa = true;   // "regex_dfa": DFA kernels (else the NFA kernel)
     bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
     bool opt_regex_codes = true; // "regex_codes": dictionary chunks on the pipe path: match bits over the decode's codes
-    bool opt_regex_stream = false; // "regex_stream": the streaming kernel for chunks without dictionary pages (else
-                                   // windows); C3: 0.52 ms vs 0.33 ms windowed, so off by default
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
-    bool opt_plain_rows = false; // "plain_rows": rows pass one lane per page from HBM (k_plain_rows), else k_plain_walk (LDS windows)
     bool opt_zflip = true;       // "zflip": per-decode flags from the block the previous k_pipe_write cleared (else a fill)
-    bool opt_write2 = false;     // "write2": k_pipe_write2 (loader wave + writer waves), set before upload
     int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
-    bool opt_page = false;       // "page": k_pipe_page (runs + codes per page) where every small page fits its stage;
-                                 // C2: 0.104 ms vs k_pipe_runs 0.036 + k_pipe_codes3 0.044, so off by default
-    bool opt_codes3 = true;      // "codes3": k_pipe_codes3 (lean tile loop), else k_pipe_codes2
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
-    bool opt_graph = false;      // "graph": replay each chunk's decode launches as a captured HIP graph (timing off);
-                                 // measured slower on C2 (0.204 vs 0.174 ms per step), so off by default
-    uint64_t opt_gen = 0;        // bumped by every pq_ctx_set_option (captured graphs record it)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
 };
 
@@ -119,8 +107,6 @@ struct pq_chunk {
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
     bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
-    bool pipe_page = false;             // every small page fits k_pipe_page's stage
-    bool pipe_write2 = false;           // planned (LDS, grid) for k_pipe_write2
     int pipe_wpw = 10;                  // k_pipe_write writer waves per workgroup (planned)
     std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
     int32_t* d_bigp = nullptr;
@@ -131,7 +117,6 @@ struct pq_chunk {
     int zsel = 0;                       // block of the current decode
     bool next_zeroed = false;           // the other block is clear (the last k_pipe_write cleared it)
     int32_t* d_dflag = nullptr;         // the side-stream dictionary decode's error flag (sticky, cleared at upload)
-    bool side_synced = false;           // the side stream is ordered after this chunk's upload
     size_t zero_bytes = 4 * sizeof(int32_t);  // bytes of d_flags cleared per decode (flags, bsum, flist[0])
     bool tiles_aligned32 = false;       // every tile starts on a 32-row boundary: k_pipe_write owns whole validity words
     // PLAIN BYTE_ARRAY, REQUIRED (plain_ba.hip)
@@ -152,21 +137,6 @@ struct pq_chunk {
     DevPage* d_ppages = nullptr;
     DevErr* d_perr = nullptr;
     pq_column* last_out = nullptr;      // output of the last pq_decode_async (collect re-runs into it)
-    // the decode's launches as a HIP graph, replayed while its key holds
-    hipGraphExec_t gexec = nullptr;
-    bool graph_off = false;             // capture failed once: launch directly
-    struct GraphKey {
-        const void *validity, *values, *offsets;
-        int64_t capacity_bytes;
-        uint64_t opt_gen;
-        bool spec_failed;
-        bool operator==(const GraphKey& o) const {
-            return validity == o.validity && values == o.values && offsets == o.offsets &&
-                   capacity_bytes == o.capacity_bytes && opt_gen == o.opt_gen && spec_failed == o.spec_failed;
-        }
-    } gkey{};
-    std::vector<int32_t> hunit_win;     // page (or chunk, spec path) -> its window (k_plain_rows)
-    int32_t* d_unit_win = nullptr;
     // tile-parallel PLAIN fixed-width decode (fixed_fast.hip)
     bool fixed_plain = false;
     int32_t* d_tile_rank = nullptr;
@@ -180,15 +150,7 @@ struct pq_chunk {
         int32_t p0 = 0, np = 0, dict_id = -1;
         uint32_t rows_cap = 0, stage_bytes = 0, wave_bytes = 0, dict_bytes = 0, dict_chars_bytes = 0;
         int waves = 0, grid = 0;
-        // batched dictionary path (dict_batch.hip)
-        bool batch = false;
-        int32_t batch0 = 0, nbatches = 0;
-        uint32_t batch_bytes = 0, max_slot = 0, blds = 0;
-        int bwriters = 0, bgrid = 0;
     };
-    std::vector<pqk::DevBatch> hbatches;
-    pqk::DevBatch* d_batches = nullptr;
-    uint64_t* d_bstatus = nullptr;
     std::vector<Range> ranges;
     bool fused = false;
     uint64_t* d_status = nullptr;
@@ -323,10 +285,6 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_dict_count);
     dfree(c->d_page_err);
     dfree(c->d_dict_err);
-    if (c->gexec) {
-        (void)hipGraphExecDestroy(c->gexec);
-        c->gexec = nullptr;
-    }
     if (c->d_zero) {  // d_flags, d_bsum and d_flist live in it
         dfree(c->d_zero);
         c->d_flags = nullptr;
@@ -349,7 +307,6 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_flist);
     dfree(c->d_bigp);
     dfree(c->d_chunk_base);
-    dfree(c->d_unit_win);
     dfree(c->d_chunks);
     dfree(c->d_cand);
     dfree(c->d_ppages);
@@ -365,8 +322,6 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_status);
     dfree(c->d_tickets);
     dfree(c->d_bases);
-    dfree(c->d_batches);
-    dfree(c->d_bstatus);
     if (c->d_prog) { pqre::free_device_program(c->d_prog); c->d_prog = nullptr; }
 }
 
@@ -376,12 +331,11 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->pipe = false;
     c->pipe_count = false;
     c->pipe_small = false;
-    c->pipe_page = false;
     c->hbig.clear();
     c->big_max_bytes = 0;
     if (c->type != PQ_BYTE_ARRAY || c->max_def > 254 || c->max_def < 0 || c->max_rep < 0 || pages.empty()) return;
     int32_t dict_id = -1;
-    bool multi = false, small = false, page_fit = true;
+    bool multi = false, small = false;
     std::vector<int32_t> big;
     uint32_t big_bytes = 0;
     for (size_t i = 0; i < pages.size(); i++) {
@@ -395,7 +349,6 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
         } else {
             small = true;
             multi |= pg.nvals > pqk::kTileRows;
-            page_fit &= static_cast<uint32_t>(pg.size) + 16 <= pqk::pipe_page_stage();
         }
         if (dict_id >= 0 && pg.dict != dict_id) return;
         dict_id = pg.dict;
@@ -408,14 +361,13 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     const uint32_t chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
     const uint32_t dict_bytes = 16 + chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
     const int wpw = std::max(1, std::min(16, ctx->opt_write_waves));
-    const pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes, ctx->opt_write2, wpw);
+    const pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes, wpw);
     if (pl.blocks_per_cu == 0) return;
     int cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
     c->pipe = true;
     c->pipe_small = small;
-    c->pipe_page = small && page_fit;
     c->pipe_count = multi && c->max_def > 0;
     c->hbig = std::move(big);
     c->big_max_bytes = big_bytes;
@@ -427,7 +379,6 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->pipe_grid = cus * pl.blocks_per_cu;
     c->pipe_ecap = static_cast<uint32_t>(ecap);
     c->pipe_cus = cus;
-    c->pipe_write2 = ctx->opt_write2;
     c->pipe_wpw = wpw;
 }
 
@@ -439,7 +390,6 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
     c->hpwins.clear();
     c->hchunk_base.clear();
     c->hchunks.clear();
-    c->hunit_win.clear();
     if (c->type != PQ_BYTE_ARRAY || c->max_def != 0 || c->max_rep != 0 || pages.empty()) return;
     auto slot = [](const DevPage& p) {
         return (static_cast<uint64_t>(std::max(p.size, 0)) + 15) / 16 * 16 + 16;
@@ -460,7 +410,6 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
             c->hchunk_base.push_back(static_cast<int32_t>(nch));
             for (uint32_t i = 0; i < k; i++) {
                 c->hchunks.push_back(make_uint2(static_cast<uint32_t>(p), i));
-                c->hunit_win.push_back(static_cast<int32_t>(c->hpwins.size() + i / pqk::kPChunkGroup));
             }
             const uint64_t se = pages[p].off + slot(pages[p]);
             for (uint32_t g = 0; g < k; g += pqk::kPChunkGroup) {
@@ -492,7 +441,6 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
             }
             b.np = static_cast<int32_t>(q - p);
             b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
-            for (size_t r = p; r < q; r++) c->hunit_win.push_back(static_cast<int32_t>(c->hpwins.size()));
             c->hpwins.push_back(b);
             p = q;
         }
@@ -539,50 +487,6 @@ void plan_fused(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages,
             int64_t ecap = std::min<int64_t>(d.nvals, d.size / 4 + 1);
             r.dict_chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
             r.dict_bytes = r.dict_chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
-        }
-        // batched path: every page dictionary-encoded, small pages and rows
-        r.batch = false;
-        if (ctx->opt_batch && dict_id >= 0 && r.rows_cap <= 1024) {
-            bool all_dict = true;
-            uint32_t max_slot = 0;
-            for (int p = r.p0; p < r.p0 + r.np; p++) {
-                all_dict &= pages[p].mode == pqk::MODE_DICT;
-                max_slot = std::max(max_slot, (static_cast<uint32_t>(std::max(pages[p].size, 0)) + 15) / 16 * 16 + 16);
-            }
-            const uint32_t pb = std::max<uint32_t>(static_cast<uint32_t>(ctx->opt_batch_bytes), max_slot);
-            const pqk::BatchPlan bp = pqk::plan_batch_lds(r.rows_cap, pb, max_slot, r.dict_bytes);
-            if (all_dict && max_slot <= 32768 && bp.writers >= 2) {
-                r.batch = true;
-                r.batch_bytes = pb;
-                r.max_slot = max_slot;
-                r.bwriters = bp.writers;
-                r.blds = bp.lds;
-                r.batch0 = static_cast<int32_t>(c->hbatches.size());
-                int p = r.p0;
-                const int pend = r.p0 + r.np;
-                while (p < pend) {
-                    pqk::DevBatch b{};
-                    b.p0 = p;
-                    b.img_lo = pages[p].off;
-                    uint64_t hi = b.img_lo;
-                    int q = p;
-                    while (q < pend && q - p < 64) {
-                        const uint64_t e = pages[q].off + (static_cast<uint64_t>(std::max(pages[q].size, 0)) + 15) / 16 * 16 + 16;
-                        if (e - b.img_lo > pb) break;
-                        hi = e;
-                        q++;
-                    }
-                    b.np = q - p;
-                    b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
-                    c->hbatches.push_back(b);
-                    p = q;
-                }
-                r.nbatches = static_cast<int32_t>(c->hbatches.size()) - r.batch0;
-                int per_cu = pqk::batch_occupancy(r.blds, 1 + r.bwriters);
-                if (per_cu < 1) per_cu = 1;
-                r.bgrid = std::max(1, std::min(per_cu * cus, r.nbatches));
-                continue;
-            }
         }
         if (r.dict_bytes + r.wave_bytes > kLds) return;
         // producer/writer pairs per workgroup (dict_fused.hip)
@@ -644,12 +548,10 @@ void pq_ctx_destroy(pq_ctx* ctx) {
 }
 
 int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
-    if (ctx) ctx->opt_gen++;
     if (!ctx || !key) return PQ_ERR_ARG;
     if (std::strcmp(key, "fused_ba") == 0) { ctx->opt_fused = value != 0; return 0; }
     if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "fused_waves") == 0) { ctx->opt_waves = static_cast<int>(value); return 0; }
-    if (std::strcmp(key, "batch") == 0) { ctx->opt_batch = value != 0; return 0; }
     if (std::strcmp(key, "fused_claim") == 0) {
         if (value < 1 || value > 64) return set_err(ctx, PQ_ERR_ARG, "fused_claim: 1..64");
         ctx->opt_claim = static_cast<int>(value);
@@ -657,21 +559,15 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     }
     if (std::strcmp(key, "regex_dfa") == 0) { ctx->opt_regex_dfa = value != 0; return 0; }
     if (std::strcmp(key, "regex_debug") == 0) { ctx->opt_regex_debug = static_cast<int>(value); return 0; }
-    if (std::strcmp(key, "regex_stream") == 0) { ctx->opt_regex_stream = value != 0; return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
-    if (std::strcmp(key, "plain_rows") == 0) { ctx->opt_plain_rows = value != 0; return 0; }
     if (std::strcmp(key, "zflip") == 0) { ctx->opt_zflip = value != 0; return 0; }
     if (std::strcmp(key, "write_waves") == 0) {
         if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "write_waves: 1..16");
         ctx->opt_write_waves = static_cast<int>(value);
         return 0;
     }
-    if (std::strcmp(key, "write2") == 0) { ctx->opt_write2 = value != 0; return 0; }
-    if (std::strcmp(key, "page") == 0) { ctx->opt_page = value != 0; return 0; }
-    if (std::strcmp(key, "codes3") == 0) { ctx->opt_codes3 = value != 0; return 0; }
     if (std::strcmp(key, "big_all") == 0) { ctx->opt_big_all = value != 0; return 0; }
-    if (std::strcmp(key, "graph") == 0) { ctx->opt_graph = value != 0; return 0; }
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
@@ -683,11 +579,6 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_win") == 0) {
         if (value < 1024 || value > 32768 || value % 16) return set_err(ctx, PQ_ERR_ARG, "regex_win: 1024..32768, multiple of 16");
         ctx->opt_regex_win = static_cast<int>(value);
-        return 0;
-    }
-    if (std::strcmp(key, "batch_bytes") == 0) {
-        if (value < 1024 || value > 65536 || value % 16) return set_err(ctx, PQ_ERR_ARG, "batch_bytes: 1024..65536, multiple of 16");
-        ctx->opt_batch_bytes = static_cast<int>(value);
         return 0;
     }
     if (std::strcmp(key, "fused_prof") == 0) {
@@ -896,7 +787,6 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc |= dalloc(&c->d_rowinfo, static_cast<size_t>(c->nrows) + 64);
             rc |= dalloc(&c->d_wchars, c->hpwins.size());
             rc |= dalloc(&c->d_pbsum, static_cast<size_t>(c->plain_grid));
-            rc |= dalloc(&c->d_unit_win, c->hunit_win.size());
             if (c->plain_spec) {
                 const size_t nch = c->hchunks.size();
                 rc |= dalloc(&c->d_chunk_base, c->hchunk_base.size());
@@ -905,10 +795,6 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
                 rc |= dalloc(&c->d_ppages, nch);
                 rc |= dalloc(&c->d_perr, nch);
             }
-        }
-        if (c->fused && !c->hbatches.empty()) {
-            rc |= dalloc(&c->d_batches, c->hbatches.size());
-            rc |= dalloc(&c->d_bstatus, c->hbatches.size());
         }
         if (c->fused) {
             rc |= dalloc(&c->d_status, hpages.size());
@@ -949,8 +835,6 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             (void)hipMemsetAsync(c->d_zero, 0, 2 * c->zfull, s);
             c->next_zeroed = true;
         }
-        if (!rc && c->d_unit_win)
-            rc = hip_check(ctx, hipMemcpyAsync(c->d_unit_win, c->hunit_win.data(), c->hunit_win.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc && c->d_chunks) {
             rc = hip_check(ctx, hipMemcpyAsync(c->d_chunks, c->hchunks.data(), c->hchunks.size() * sizeof(uint2), hipMemcpyHostToDevice, s), "upload");
             if (!rc) rc = hip_check(ctx, hipMemcpyAsync(c->d_chunk_base, c->hchunk_base.data(), c->hchunk_base.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
@@ -960,8 +844,6 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             rc = hip_check(ctx, hipMemcpyAsync(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
         if (!rc && c->d_pwins)
             rc = hip_check(ctx, hipMemcpyAsync(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice, s), "upload");
-        if (!rc && c->d_batches)
-            rc = hip_check(ctx, hipMemcpyAsync(c->d_batches, c->hbatches.data(), c->hbatches.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice, s), "upload");
         if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
         if (rc) {
             free_chunk_device(c.get());
@@ -1064,8 +946,6 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     P.dict_entries_cap = c->pipe_ecap;
     P.cus = c->pipe_cus;
     P.has_small = c->pipe_small;
-    P.lean_codes = ctx->opt_codes3;
-    P.write2 = c->pipe_write2;
     P.write_waves = c->pipe_wpw;
     return P;
 }
@@ -1075,21 +955,11 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
 // the codes wait for it (ev_join).
 static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side) {
     hipStream_t s = ctx->stream;
-    if (c->pipe_page && ctx->opt_page) {  // run tables + codes per page in one pass (needs the dictionary)
-        if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
-        if (!c->hbig.empty()) {
-            Timed t(ctx, "pipe_big");
-            pqk::launch_pipe_big(s, P, c->d_bigp, static_cast<int>(c->hbig.size()), c->big_max_bytes);
-        }
-        Timed t(ctx, "pipe_page");
-        pqk::launch_pipe_page(s, P);
-        return;
-    }
     {
         Timed t(ctx, "pipe_runs");
         pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
                               c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist,  // flist[0], bsum: cleared with d_flags
-                              ctx->opt_codes3);
+                              true);
     }
     if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
     if (!c->hbig.empty()) {
@@ -1115,35 +985,7 @@ int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         if (int rc = ensure_output(ctx, c, out, 0)) return rc;
     }
     c->last_out = out;
-    if (ctx->timing || !ctx->opt_graph || c->graph_off) return decode_launch(ctx, c, out);
-    // the launch sequence (memsets, kernels, the side-stream fork/join) as a
-    // HIP graph: captured once per output buffers / options, then one launch
-    const pq_chunk::GraphKey key{out->d_validity, out->d_values, out->d_offsets, out->capacity_bytes, ctx->opt_gen,
-                                 c->spec_failed};
-    if (!c->gexec || !(c->gkey == key)) {
-        if (c->gexec) {
-            (void)hipGraphExecDestroy(c->gexec);
-            c->gexec = nullptr;
-        }
-        hipGraph_t g = nullptr;
-        if (hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed) != hipSuccess) {
-            (void)hipGetLastError();
-            c->graph_off = true;
-            return decode_launch(ctx, c, out);
-        }
-        const int rc = decode_launch(ctx, c, out);
-        const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
-        if (rc || e != hipSuccess || !g || hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0) != hipSuccess) {
-            if (g) (void)hipGraphDestroy(g);
-            (void)hipGetLastError();
-            c->gexec = nullptr;
-            c->graph_off = true;
-            return rc ? rc : decode_launch(ctx, c, out);
-        }
-        (void)hipGraphDestroy(g);
-        c->gkey = key;
-    }
-    return hip_check(ctx, hipGraphLaunch(c->gexec, ctx->stream), "graph launch");
+    return decode_launch(ctx, c, out);
 }
 
 static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
@@ -1172,16 +1014,13 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
         // the dictionary (one workgroup) decodes on the side stream while the
         // run-table pass runs; k_pipe_codes waits for both (ev_join).  The
-        // side stream is ordered after the main stream once per upload (the
-        // image copy): every later dictionary decode of the chunk writes the
-        // same entries, so it may overlap the previous decode's readers.  Its
-        // error flag is its own sticky word (d_dflag), not the per-decode
-        // flags the main stream clears.
-        if (!c->side_synced || ctx->opt_graph) {
-            (void)hipEventRecord(ctx->ev_fork, s);
-            (void)hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0);
-            c->side_synced = !ctx->opt_graph;
-        }
+        // side stream first waits for everything already on the main stream
+        // (ev_fork): the previous decode's k_pipe_write / regex k_pipe_match
+        // read the entry table this k_dict_index rewrites.  Its error flag is
+        // its own sticky word (d_dflag), not the per-decode flags the main
+        // stream clears.
+        (void)hipEventRecord(ctx->ev_fork, s);
+        (void)hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0);
         {
             Timed t(ctx, "dict_index", ctx->side);
             pqk::launch_dict_index(ctx->side, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
@@ -1204,10 +1043,6 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         P.bsum = c->d_pbsum; P.grid = c->plain_grid; P.nrows_total = c->nrows; P.total = c->d_total;
         P.capacity = out->capacity_bytes; P.overflow = c->d_flags + 1; P.validity = out->d_validity;
         P.offsets = out->d_offsets; P.chars = out->d_values; P.page_err = c->d_page_err; P.err_any = c->d_flags;
-        if (ctx->opt_plain_rows) {  // lane per page (k_plain_rows) instead of lane per page within a window wave
-            P.unit_win = c->d_unit_win;
-            P.nunits = c->plain_spec ? static_cast<int32_t>(c->hchunks.size()) : c->npages;
-        }
         if (c->nrows == 0) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
             (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
@@ -1243,34 +1078,17 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             P.znext_words = static_cast<uint32_t>(c->zero_bytes / 4);
         }
         pqk::launch_pipe_write(s, P);
-        if (c->d_zero) c->next_zeroed = true;
+        // the other block is clear only if k_pipe_write ran (it returns early on a chunk without tiles)
+        if (c->d_zero) c->next_zeroed = c->ntiles > 0;
     } else if (c->fused) {
         const size_t nr = c->ranges.size();
         (void)hipMemsetAsync(c->d_status, 0, std::max<size_t>(c->npages, 1) * sizeof(uint64_t), s);
         (void)hipMemsetAsync(c->d_tickets, 0, nr * sizeof(int32_t), s);
         (void)hipMemsetAsync(c->d_bases, 0, (nr + 1) * sizeof(int64_t), s);
-        if (c->d_bstatus) (void)hipMemsetAsync(c->d_bstatus, 0, c->hbatches.size() * sizeof(uint64_t), s);
         for (size_t k = 0; k < nr; k++) {
             const auto& r = c->ranges[k];
             if (r.np == 0) {
                 (void)hipMemcpyAsync(c->d_bases + k + 1, c->d_bases + k, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
-                continue;
-            }
-            if (r.batch) {
-                pqk::BatchLaunch B{};
-                B.bytes = c->d_bytes; B.pages = c->d_pages; B.batches = c->d_batches + r.batch0;
-                B.nbatches = r.nbatches; B.last_page = r.p0 + r.np - 1;
-                B.dicts = c->d_dicts; B.dict_id = r.dict_id; B.entries = c->d_entries; B.dict_count = c->d_dict_count;
-                B.max_def = c->max_def; B.max_rep = c->max_rep; B.rows_cap = r.rows_cap;
-                B.batch_bytes = r.batch_bytes; B.max_slot = r.max_slot; B.dict_bytes = r.dict_bytes;
-                B.dict_chars_bytes = r.dict_chars_bytes; B.status = c->d_bstatus + r.batch0;
-                B.ticket = c->d_tickets + k; B.base_in = c->d_bases + k; B.base_out = c->d_bases + k + 1;
-                B.nrows_total = c->nrows; B.validity = out->d_validity; B.offsets = out->d_offsets;
-                B.chars = out->d_values; B.capacity = out->capacity_bytes; B.overflow = c->d_flags + 1;
-                B.page_err = c->d_page_err; B.err_any = c->d_flags; B.debug = ctx->opt_debug; B.prof = ctx->d_prof;
-                B.grid = r.bgrid; B.writers = r.bwriters; B.lds = r.blds;
-                Timed t(ctx, "ba_batch");
-                pqk::launch_ba_batch(s, B);
                 continue;
             }
             pqk::FusedLaunch L{};
@@ -1449,7 +1267,7 @@ int pq_timing_get(pq_ctx* ctx, const char* name, double* total_ms, int64_t* laun
 
 int pq_fused_prof_read(pq_ctx* ctx, uint64_t* out, int n) {
     if (!ctx || !ctx->d_prof) return 0;
-    const int k = std::max(pqk::fused_prof_slots(), pqk::batch_prof_slots());
+    const int k = pqk::fused_prof_slots();
     std::vector<uint64_t> h(static_cast<size_t>(k));
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
     if (hipMemcpy(h.data(), ctx->d_prof, k * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return 0;
@@ -1577,13 +1395,6 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             pipe_front(ctx, c, P, false);
             Timed t(ctx, "regex_codes");
             pqk::launch_pipe_match(s, P, c->d_dict_match + c->pipe_entry_base, neg, c->d_page_flags);
-        } else if (c->d_dfa && ctx->opt_regex_plain && ctx->opt_regex_stream && c->ndicts == 0) {
-            Timed t(ctx, "regex_stream");
-            int cus = 256;
-            hipDeviceProp_t prop;
-            if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
-            pqre::launch_regex_stream(s, c->d_dfa, c->dfa_bytes, c->dfa_full, c->d_bytes, c->d_pages, c->npages, cus, cp,
-                                      neg, c->d_page_flags, c->d_page_err, c->d_flags);
         } else if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {
             (void)hipMemsetAsync(c->d_rwin_ticket, 0, sizeof(int32_t), s);
             Timed t(ctx, "regex_plain");

@@ -41,11 +41,10 @@ constexpr int kRunPages = 32;                 // max pages per wavefront (2 stre
 constexpr uint32_t kRunStage = 16384;         // staged payload bytes per wavefront
 constexpr uint32_t kFallback = 1u << 31;      // info flag: exact serial decode
 constexpr uint32_t kBig = 1u << 30;           // info flag: k_pipe_big wrote the page's codes
-constexpr uint32_t kSkip = kFallback | kBig;  // k_pipe_codes2 leaves the page alone
+constexpr uint32_t kSkip = kFallback | kBig;  // k_pipe_codes3 leaves the page alone
 constexpr int kCodeWaves = 4;
 constexpr uint16_t kNull = 0xFFFFu;
 constexpr int kWriteMax = 16;                // writer waves per k_pipe_write workgroup: runtime wpw <= this
-constexpr int kLoadGroup = 6;                // k_pipe_write2's loader: tiles whose codes load together
 constexpr uint32_t kFront = 16;               // zero bytes before the LDS dictionary
 constexpr uint32_t kLitCapP = 16;
 
@@ -461,229 +460,8 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_codes(CodeArgs a) {
     tile_done(a, t, chars);
 }
 
-// Persistent per-tile codes: the dictionary's entry lengths in LDS, each
-// wavefront's rows 8l .. 8l + 7 contiguous (one wave scan per quantity), the
-// page payload staged in LDS for literal runs.
-constexpr int kCodeWaves2 = 8;
-constexpr uint32_t kCodeStage = 2048;
-struct CodeLds2 {
-    CodeLds c;
-    uint32_t stage[kCodeStage / 4 + 4];
-};
-
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane i <- lane i - 1, lane 0 <- 0
     return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x138, 0xf, 0xf, true));
-}
-
-__global__ void __launch_bounds__(kCodeWaves2 * 64) k_pipe_codes2(CodeArgs a, uint32_t lt_n, const int32_t* __restrict__ flist) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t lens[];
-    __shared__ CodeLds2 lds_all[kCodeWaves2];
-    const int wv = static_cast<int>(threadIdx.x / kWave);
-    CodeLds2& L2 = lds_all[wv];
-    CodeLds& L = L2.c;
-    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
-    const uint32_t nl = min(dict_n, lt_n);
-    copy_map(lens, a.entries + ebase, nl, threadIdx.x, blockDim.x,
-             [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
-    __syncthreads();
-    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
-    // each wavefront owns a contiguous run of tiles; descriptors of up to 64
-    // tiles load at once (one per lane) and the next tile's run records and
-    // payload load into registers while this tile is decoded
-    const int nw = static_cast<int>(gridDim.x) * kCodeWaves2;
-    const int per = (a.ntiles + nw - 1) / nw;
-    const int ta = min(a.ntiles, (static_cast<int>(blockIdx.x) * kCodeWaves2 + wv) * per);
-    const int tb = min(a.ntiles, ta + per);
-    auto rl64 = [](uint64_t v, int i) -> uint64_t {
-        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
-        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), i);
-        return (static_cast<uint64_t>(hi) << 32) | lo;
-    };
-    for (int c0 = ta; c0 < tb; c0 += kWave) {
-        const int cn = min(kWave, tb - c0);
-        uint32_t myp = 0, myrow0 = 0, mym = 0, myinf = kFallback, mysize = 0;
-        uint64_t myoff = 0, myfirst = 0;
-        if (static_cast<int>(lane()) < cn) {
-            const DevTile T = a.tiles[c0 + lane()];
-            const DevPage pg = a.pages[T.page];
-            myp = static_cast<uint32_t>(T.page);
-            myrow0 = static_cast<uint32_t>(T.row0);
-            mym = static_cast<uint32_t>(T.nrows);
-            myinf = a.info[T.page];
-            mysize = static_cast<uint32_t>(max(pg.size, 0));
-            myoff = pg.off;
-            myfirst = static_cast<uint64_t>(pg.first_row);
-        }
-        uint2 rq0, rq1, rq2, rq3;
-        uint4 sq0, sq1, sq2;
-        auto prefetch = [&](int i) {
-            const uint32_t inf = __builtin_amdgcn_readlane(myinf, i);
-            const uint32_t pp = __builtin_amdgcn_readlane(myp, i);
-            const uint32_t sz = __builtin_amdgcn_readlane(mysize, i);
-            const uint64_t off = rl64(myoff, i);
-            const uint32_t nd = (inf & kSkip) ? 0u : (inf & 0xFFu), ni = (inf & kSkip) ? 0u : ((inf >> 8) & 0xFFu);
-            const uint2* rd_ = a.runs + static_cast<size_t>(pp) * 2 * kPipeRunCap;
-            const uint2 z = make_uint2(0u, 0u);
-            rq0 = lane() < nd ? rd_[lane()] : z;
-            rq1 = lane() + kWave < nd ? rd_[lane() + kWave] : z;
-            rq2 = lane() < ni ? rd_[kPipeRunCap + lane()] : z;
-            rq3 = lane() + kWave < ni ? rd_[kPipeRunCap + lane() + kWave] : z;
-            const uint32_t nb = (inf & kSkip) || sz + 16 > kCodeStage ? 0u : (sz + 15) / 16 + 1;
-            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + off);
-            const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-            sq0 = lane() < nb ? src[lane()] : z4;
-            sq1 = lane() + kWave < nb ? src[lane() + kWave] : z4;
-            sq2 = lane() + 2 * kWave < nb ? src[lane() + 2 * kWave] : z4;
-        };
-        prefetch(0);
-        for (int i = 0; i < cn; i++) {
-            const int t = c0 + i;
-            const uint32_t inf = __builtin_amdgcn_readlane(myinf, i);
-            const int p = static_cast<int>(__builtin_amdgcn_readlane(myp, i));
-            const uint32_t r0 = __builtin_amdgcn_readlane(myrow0, i), m = __builtin_amdgcn_readlane(mym, i);
-            const uint32_t size = __builtin_amdgcn_readlane(mysize, i);
-            const uint8_t* page = a.bytes + rl64(myoff, i);
-            const int64_t first_row = static_cast<int64_t>(rl64(myfirst, i));
-            // this tile's records and payload -> LDS, then the next tile's loads
-            L.recd[lane()] = rq0;
-            L.recd[lane() + kWave] = rq1;
-            L.reci[lane()] = rq2;
-            L.reci[lane() + kWave] = rq3;
-            reinterpret_cast<uint4*>(L2.stage)[lane()] = sq0;
-            reinterpret_cast<uint4*>(L2.stage)[lane() + kWave] = sq1;
-            if (lane() + 2 * kWave < (kCodeStage / 4 + 4) / 4) reinterpret_cast<uint4*>(L2.stage)[lane() + 2 * kWave] = sq2;
-            if (i + 1 < cn) prefetch(i + 1);
-            if (inf & kSkip) continue;  // k_pipe_exact / k_pipe_big
-            if (a.debug & 512) {  // timing: loads and the tile loop only
-                if (lane() == 0) a.tile_chars[t] = 0;
-                continue;
-            }
-            const uint32_t nd = inf & 0xFFu, ni = (inf >> 8) & 0xFFu, bwi = (inf >> 16) & 0xFFu;
-            const bool staged = size + 16 <= kCodeStage;
-            const uint32_t l8 = lane() * 8;
-            if (l8 < m) *reinterpret_cast<uint2*>(L.mark + l8) = make_uint2(0u, 0u);
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            auto bits = [&](uint64_t b, uint32_t bw) -> uint32_t {
-                return staged ? lds_bits(L2.stage, size, b, bw) : gbits(page, size, b, bw);
-            };
-            // def levels of this lane's rows r0 + 8l .. r0 + 8l + 7
-            uint32_t vb = 0;
-            if (a.max_def > 0) {
-                const uint32_t rd0 = run_at(L.recd, nd, r0);
-                for (uint32_t k = lane(); k < nd; k += kWave) {
-                    const uint32_t st = rr_start(L.recd[k]);
-                    if (k > rd0 && st < r0 + m) L.mark[st - r0] = static_cast<uint8_t>(k - rd0);
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint2 mk = l8 < m ? *reinterpret_cast<const uint2*>(L.mark + l8) : make_uint2(0u, 0u);
-                uint32_t rm[8], run = 0;
-    #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
-                    rm[k] = run;
-                }
-                const uint32_t ex = wave_shr1(wave_incl_max(run));
-                bool above = false;
-    #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t j = l8 + k;
-                    const uint2 R = L.recd[rd0 + max(ex, rm[k])];
-                    uint32_t lvl = rr_pay(R);
-                    if (rr_lit(R) && j < m) lvl = bits(rr_pay(R) + static_cast<uint64_t>(r0 + j - rr_start(R)) * bwd, bwd);
-                    vb |= (j < m && lvl == md ? 1u : 0u) << k;
-                    above |= j < m && lvl > md;
-                }
-                if (__ballot(above)) {  // levels above max_def: outside the supported format
-                    set_err(a.page_err + p, a.err_any, PQ_ERR_UNSUPPORTED, 0, 0, size);
-                    for (uint32_t j = lane(); j < m; j += kWave) a.codes[first_row + r0 + j] = kNull;
-                    if (lane() == 0) a.tile_chars[t] = 0;
-                    __builtin_amdgcn_wave_barrier();
-                    continue;
-                }
-            } else {
-                vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
-            }
-            const uint32_t nnl = __popc(vb);
-            const uint32_t nincl = wave_incl_scan(nnl);
-            const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
-            uint32_t k0 = r0;
-            if (a.max_def > 0) {
-                const int32_t tp = a.page_tile0[p];
-                uint32_t sum = 0;
-                for (int32_t q = tp + static_cast<int32_t>(lane()); q < t; q += kWave) sum += static_cast<uint32_t>(a.tile_nn[q]);
-                k0 = wave_sum(sum);
-            }
-            // dictionary index runs over ranks [k0, k0 + nn): run of each rank -> mark2
-            uint32_t ri0 = 0;
-            if (a.debug & 1024) {  // timing: def levels only
-                if (lane() == 0) a.tile_chars[t] = nn;
-                continue;
-            }
-            if (nn) {
-                if (l8 < nn) *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(0u, 0u);
-                __builtin_amdgcn_wave_barrier();
-                ri0 = run_at(L.reci, ni, k0);
-                for (uint32_t k = lane(); k < ni; k += kWave) {
-                    const uint32_t st = rr_start(L.reci[k]);
-                    if (k > ri0 && st < k0 + nn) L.mark2[st - k0] = static_cast<uint8_t>(k - ri0);
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint2 mk = l8 < nn ? *reinterpret_cast<const uint2*>(L.mark2 + l8) : make_uint2(0u, 0u);
-                uint32_t rm[8], run = 0;
-    #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
-                    rm[k] = run;
-                }
-                const uint32_t ex = wave_shr1(wave_incl_max(run));
-                uint32_t w0 = 0, w1 = 0;
-    #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t v = max(ex, rm[k]);
-                    if (k < 4) w0 |= v << (8 * k);
-                    else w1 |= v << (8 * (k - 4));
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (l8 < nn) *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(w0, w1);
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-            uint32_t chars = 0, cw8[8];
-            const int64_t R0 = first_row + r0;
-    #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t j = l8 + k;
-                uint32_t code = kNull;
-                if ((vb >> k) & 1u) {
-                    const uint32_t rk = rbase + __popc(vb & ((1u << k) - 1u));
-                    const uint2 R = L.reci[ri0 + L.mark2[rk]];
-                    uint32_t v = rr_pay(R);
-                    if (rr_lit(R)) v = bits(rr_pay(R) + static_cast<uint64_t>(k0 + rk - rr_start(R)) * bwi, bwi);
-                    if (v < dict_n) {
-                        code = v;
-                        chars += v < nl ? lens[v] : static_cast<uint32_t>(a.entries[ebase + v] >> 32);
-                    }
-                }
-                cw8[k] = code;
-                (void)j;
-            }
-            store_codes8(a.codes, R0, l8, m, cw8);
-            chars = wave_sum(chars);
-            tile_done(a, t, chars);
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-    // pages k_pipe_runs / k_pipe_big marked (complete before this launch):
-    // the exact serial decoder, one wave per page
-    const int nf = flist[0];
-    for (int i = static_cast<int>(blockIdx.x) * kCodeWaves2 + wv; i < nf; i += nw) {
-        exact_page(a, L, flist[1 + i], dict_n, ebase);
-        __builtin_amdgcn_wave_barrier();
-    }
 }
 
 // Marked pages (listed by k_pipe_runs): the exact serial decoder, one
@@ -701,7 +479,9 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_exact(CodeArgs a, cons
 }
 
 // ── per-tile codes, lean form ──────────────────────────────────────────────
-// k_pipe_codes3 computes what k_pipe_codes2 does, with three changes:
+// k_pipe_codes3: per-tile codes with the dictionary's entry lengths in LDS,
+// each wavefront's rows 8l .. 8l + 7 contiguous (one wave scan per quantity),
+// and three properties that keep it lean:
 //  * no global loads inside a tile.  On gfx9 loads and stores share vmcnt, so
 //    a load in the tile waits for the previous tile's code stores; here the
 //    tile's descriptors, run records, payload and earlier-tile non-null counts
@@ -990,342 +770,6 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
     }
 }
 
-// ── run tables and codes of a page in one wave ─────────────────────────────
-// k_pipe_page replaces k_pipe_runs + k_pipe_codes3 for chunks whose small
-// pages (<= kPipeSmallRows rows) all fit kPageStage.  One wave per page: the
-// payload in LDS; a run header parsed at every byte of both streams (the next
-// header's position, run_spec.hpp); three pointer-doubling rounds give 8-run
-// jumps; lanes 0 and 1 follow the def and index chains listing every 8th
-// header; one lane per listed header re-parses its 8 runs exactly; a wave scan
-// of the run counts gives every record its first value (truncated at the page
-// value count, an exhausted stream gets its zero run).  These are the records
-// k_pipe_runs writes (walk_runs), kept in LDS; the page's tiles are then
-// expanded as in k_pipe_codes3, with the page's non-null count carried from
-// tile to tile (no count pass).  Pages outside that shape (bad headers before
-// the value count, more than kPipeRunCap runs, bit widths > 16, prologue
-// errors) go to flist for the exact decoder.
-constexpr int kPageWaves = 4;
-constexpr uint32_t kPageStage = 2048;         // staged payload bytes (+16 zero) per wave
-constexpr int kPJumpLog = 3;
-constexpr uint32_t kPJump = 1u << kPJumpLog;
-constexpr uint32_t kPList = (kPipeRunCap - kPJump - 1) / kPJump + 1;  // listed headers per stream
-constexpr uint32_t kPStop = 0xFFFFu;
-constexpr int kPPer = kPageStage / kWave;     // byte positions per lane
-
-struct PageLds {
-    uint32_t stage[kPageStage / 4];
-    uint16_t tab[kPageStage];
-    uint2 rec[2][kPipeRunCap];
-    uint32_t list[2][kPList + 1];
-    uint32_t esum[2][kPList + 1];
-    uint8_t mark[kTileRows];
-    uint8_t mark2[kTileRows];
-};
-
-__global__ void __launch_bounds__(kPageWaves * 64) k_pipe_page(CodeArgs a, int npages, uint32_t lt_n,
-                                                               uint32_t* __restrict__ info, int32_t* __restrict__ flist) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t lens[];
-    __shared__ PageLds lds_all[kPageWaves];
-    const int wv = static_cast<int>(threadIdx.x / kWave);
-    PageLds& L = lds_all[wv];
-    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
-    const uint32_t nl = min(dict_n, lt_n);
-    const bool lean = dict_n <= lt_n;
-    copy_map(lens, a.entries + ebase, nl, threadIdx.x, blockDim.x,
-             [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
-    __syncthreads();
-    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
-    const uint32_t maskd = (1u << bwd) - 1u, nbd = (bwd + 7) / 8;
-    const uint32_t l8 = lane() * 8;
-    const int nw = static_cast<int>(gridDim.x) * kPageWaves;
-    for (int p = static_cast<int>(blockIdx.x) * kPageWaves + wv; p < npages; p += nw) {
-        const DevPage pg = a.pages[p];
-        const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
-        if (n > static_cast<uint32_t>(kPipeSmallRows)) continue;  // k_pipe_big
-        const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
-        const int32_t tile0 = a.page_tile0[p];
-        const int64_t first_row = pg.first_row;
-        bool fail = size + 16 > kPageStage || !lean;
-        if (!fail) {  // payload + the slot's zero padding -> LDS
-            const uint32_t nb = (size + 15) / 16 + 1;
-            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + pg.off);
-            uint4* st4 = reinterpret_cast<uint4*>(L.stage);
-            const uint4 v0 = lane() < nb ? src[lane()] : make_uint4(0u, 0u, 0u, 0u);
-            const uint4 v1 = lane() + kWave < nb ? src[lane() + kWave] : make_uint4(0u, 0u, 0u, 0u);
-            st4[lane()] = v0;
-            st4[lane() + kWave] = v1;
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // prologue (column_reader.cpp:146-182): def section, rep section, bit width
-        uint32_t pos = 0, dbase = 0, dlen = 0, bwi = 0;
-        if (!fail && md > 0) {
-            if (size < 4) fail = true;
-            else {
-                dlen = L.stage[0];
-                pos = 4;
-                if (static_cast<uint64_t>(pos) + dlen > size) fail = true;
-                else { dbase = 4; pos += dlen; }
-            }
-        }
-        if (!fail && a.max_rep > 0) {
-            if (pos + 4 > size) fail = true;
-            else {
-                const uint32_t rl = static_cast<uint32_t>(lds_u64(L.stage, pos));
-                pos += 4;
-                if (static_cast<uint64_t>(pos) + rl > size) fail = true;
-                else pos += rl;
-            }
-        }
-        if (!fail) {
-            if (pos + 1 > size) fail = true;
-            else { bwi = static_cast<uint32_t>(lds_u64(L.stage, pos)) & 0xFFu; pos += 1; }
-        }
-        if (!fail && bwi > 16) fail = true;
-        const uint32_t nbi = (bwi + 7) / 8, de = dbase + dlen;
-        uint32_t nrec0 = 0, nrec1 = 0;
-        if (!fail) {
-            // 1. next-header position at every byte of both streams
-            for (uint32_t j = lane(); j < size; j += kWave) {
-                const bool s1 = j >= pos, s0 = md > 0 && j >= dbase && j < de;
-                uint32_t nx = kPStop;
-                if (s0 || s1) {
-                    const uint32_t e = s1 ? size : de, bw = s1 ? bwi : bwd, nbv = s1 ? nbi : nbd;
-                    const SpecHdr h = spec_hdr(L.stage, j);
-                    const uint32_t q = h.lit ? (h.g > 0xFFFFu ? 0x10000u : h.qh + h.g * bw) : h.qh + nbv;
-                    if (!spec_bad(h, e, nbv) && q < e) nx = q;
-                }
-                L.tab[j] = static_cast<uint16_t>(nx);
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // 2. 8-run jumps (all reads of a round before its writes)
-            for (int r = 0; r < kPJumpLog; r++) {
-                uint32_t nv[kPPer / 2];
-#pragma unroll
-                for (int i = 0; i < kPPer; i++) {
-                    const uint32_t j = lane() + static_cast<uint32_t>(i) * kWave;
-                    uint32_t t = kPStop;
-                    if (j < size) {
-                        t = L.tab[j];
-                        if (t != kPStop) t = L.tab[t];
-                    }
-                    if (i & 1) nv[i >> 1] |= t << 16;
-                    else nv[i >> 1] = t;
-                }
-                __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                for (int i = 0; i < kPPer; i++) {
-                    const uint32_t j = lane() + static_cast<uint32_t>(i) * kWave;
-                    if (j < size) L.tab[j] = static_cast<uint16_t>(nv[i >> 1] >> (16 * (i & 1)));
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-            // 3. every 8th header of each chain (lane 0: def, lane 1: index)
-            uint32_t k = 0;
-            if (lane() < 2 && (lane() == 1 || md > 0)) {
-                const uint32_t s = lane();
-                uint32_t q = s ? pos : dbase;
-                const uint32_t e = s ? size : de;
-                for (;;) {
-                    if (k >= kPList) { k = ~0u; break; }
-                    L.list[s][k++] = q;
-                    if (q >= e) break;
-                    const uint32_t t = L.tab[q];
-                    if (t == kPStop) break;
-                    q = t;
-                }
-            }
-            const uint32_t k0l = __builtin_amdgcn_readlane(k, 0), k1l = __builtin_amdgcn_readlane(k, 1);
-            if (k0l == ~0u || k1l == ~0u) fail = true;
-            const uint32_t nl0 = md > 0 ? k0l : 0u, nl1 = k1l;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // 4. exact runs of each listed header: untruncated counts, first bad step
-            const bool li = lane() < nl0 + nl1;
-            const uint32_t s = lane() >= nl0 ? 1u : 0u, i = s ? lane() - nl0 : lane();
-            uint32_t sum = 0, meta = 0;
-            if (!fail && li) {
-                const uint32_t e = s ? size : de, bw = s ? bwi : bwd, nbv = s ? nbi : nbd;
-                const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
-                const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
-                uint32_t q = L.list[s][i], r = 0, bad = kPJump, ended = 0;
-                uint2* out = L.rec[s] + i * kPJump;
-                for (; r < kPJump; r++) {
-                    if (q >= e) { ended = 1; break; }
-                    const SpecHdr h = spec_hdr(L.stage, q);
-                    if (spec_bad(h, e, nbv)) { bad = r; break; }
-                    const uint32_t c = h.lit ? min(h.g, kSpCountCap / 8) * 8 : min(h.g, kSpCountCap);
-                    out[r] = make_uint2(c, h.lit ? (litpay | (h.qh * litmul)) : (h.vraw & vmask));
-                    sum = min(sum + c, kSpCountCap);
-                    const uint64_t nql = static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw;
-                    q = h.lit ? (nql > e ? e : static_cast<uint32_t>(nql)) : h.qh + nbv;
-                }
-                if (r == kPJump && q >= e) ended = 1;
-                meta = r | (bad << 8) | (ended << 16);
-            }
-            // 5. first value of every record (a scan per stream), truncation at n,
-            //    an exhausted stream's zero run
-            const uint32_t incl = wave_incl_scan(li ? sum : 0u);
-            const uint32_t tot0 = nl0 ? __builtin_amdgcn_readlane(incl, static_cast<int>(nl0) - 1) : 0u;
-            const uint32_t b0 = incl - sum - (s ? tot0 : 0u);
-            __builtin_amdgcn_wave_barrier();
-            uint32_t nrec = 0;
-            bool sbad = false;
-            if (!fail && li && b0 < n) {
-                const uint32_t nr = meta & 0xFFu, bad = (meta >> 8) & 0xFFu, ended = meta >> 16;
-                const uint32_t last = s ? nl0 + nl1 - 1 : nl0 - 1;
-                uint2* out = L.rec[s] + i * kPJump;
-                uint32_t c0 = b0, kept = 0;
-                for (uint32_t r = 0; r < nr && c0 < n; r++) {
-                    const uint32_t c = out[r].x;
-                    out[r].x = c0 | (min(c, n - c0) << 16);
-                    c0 += c;
-                    kept = r + 1;
-                }
-                if (c0 >= n) {
-                    nrec = i * kPJump + kept;
-                } else if (bad < kPJump || (lane() == last && (!ended || i * kPJump + nr >= kPipeRunCap))) {
-                    sbad = true;  // a bad header before the value count
-                } else if (lane() == last) {  // exhausted: the rest of the values are 0
-                    out[nr] = make_uint2(c0 | ((n - c0) << 16), 0u);
-                    nrec = i * kPJump + nr + 1;
-                }
-            }
-            if (__ballot(sbad)) fail = true;
-            const uint64_t h0 = __ballot(nrec != 0 && s == 0), h1 = __ballot(nrec != 0 && s == 1);
-            nrec0 = h0 ? __builtin_amdgcn_readlane(nrec, static_cast<int>(__builtin_ctzll(h0))) : 0u;
-            nrec1 = h1 ? __builtin_amdgcn_readlane(nrec, static_cast<int>(__builtin_ctzll(h1))) : 0u;
-            if ((md > 0 && nrec0 == 0 && n > 0) || (nrec1 == 0 && n > 0)) fail = true;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        if (fail) {  // the exact decoder (k_pipe_exact over flist)
-            if (lane() == 0) {
-                info[p] = kFallback;
-                flist[1 + atomicAdd(flist, 1)] = p;
-            }
-            continue;
-        }
-        if (lane() == 0) info[p] = kBig;  // codes written here
-        // ── the page's tiles: codes and characters ──
-        const uint32_t zw = ((size + 15) / 16 + 1) * 4 - 1;  // last word of the slot: zero
-        const uint32_t maski = (1u << bwi) - 1u;
-        const uint2 d0 = lane() < nrec0 ? L.rec[0][lane()] : make_uint2(0u, 0u);
-        const uint2 d1 = lane() + kWave < nrec0 ? L.rec[0][lane() + kWave] : make_uint2(0u, 0u);
-        const uint2 x0 = lane() < nrec1 ? L.rec[1][lane()] : make_uint2(0u, 0u);
-        const uint2 x1 = lane() + kWave < nrec1 ? L.rec[1][lane() + kWave] : make_uint2(0u, 0u);
-        uint32_t kacc = 0;  // non-null rows of the page's earlier tiles
-        for (uint32_t r0 = 0, ti = 0; r0 < n; r0 += kTileRows, ti++) {
-            const uint32_t m = min(n - r0, static_cast<uint32_t>(kTileRows));
-            const int t = tile0 + static_cast<int>(ti);
-            *reinterpret_cast<uint2*>(L.mark + l8) = make_uint2(0u, 0u);
-            *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(0u, 0u);
-            uint32_t vb;
-            if (md > 0) {
-                const uint32_t rd0 = run_at_reg(d0, d1, nrec0, r0);
-                __builtin_amdgcn_wave_barrier();
-                {
-                    const uint32_t k = lane(), st = rr_start(d0);
-                    if (k < nrec0 && k > rd0 && st < r0 + m) L.mark[st - r0] = static_cast<uint8_t>(k - rd0);
-                    const uint32_t k1 = lane() + kWave, st1 = rr_start(d1);
-                    if (k1 < nrec0 && k1 > rd0 && st1 < r0 + m) L.mark[st1 - r0] = static_cast<uint8_t>(k1 - rd0);
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint2 mk = *reinterpret_cast<const uint2*>(L.mark + l8);
-                uint32_t rm[8], run = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
-                    rm[k] = run;
-                }
-                const uint32_t ex = wave_shr1(wave_incl_max(run));
-                vb = 0;
-                bool above = false;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t j = l8 + k;
-                    const uint2 R = L.rec[0][(rd0 + max(ex, rm[k])) & (kPipeRunCap - 1)];
-                    const uint32_t pay = rr_pay(R);
-                    const uint32_t lb = sbits3(L.stage, pay + (r0 + j - rr_start(R)) * bwd, zw, maskd);
-                    const uint32_t lvl = rr_lit(R) ? lb : pay;
-                    const bool in = j < m;
-                    vb |= (in && lvl == md ? 1u : 0u) << k;
-                    above |= in && lvl > md;
-                }
-                if (__ballot(above)) {  // levels above max_def: outside the supported format
-                    set_err(a.page_err + p, a.err_any, PQ_ERR_UNSUPPORTED, 0, 0, size);
-                    for (uint32_t j = lane(); j < m; j += kWave) a.codes[first_row + r0 + j] = kNull;
-                    if (lane() == 0) a.tile_chars[t] = 0;
-                    __builtin_amdgcn_wave_barrier();
-                    continue;
-                }
-            } else {
-                vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
-            }
-            const uint32_t nnl = __popc(vb);
-            const uint32_t nincl = wave_incl_scan(nnl);
-            const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
-            const uint32_t k0 = md > 0 ? kacc : r0;
-            kacc += nn;
-            const uint32_t ri0 = run_at_reg(x0, x1, nrec1, k0);
-            if (nn) {
-                __builtin_amdgcn_wave_barrier();
-                {
-                    const uint32_t k = lane(), st = rr_start(x0);
-                    if (k < nrec1 && k > ri0 && st < k0 + nn) L.mark2[st - k0] = static_cast<uint8_t>(k - ri0);
-                    const uint32_t k1 = lane() + kWave, st1 = rr_start(x1);
-                    if (k1 < nrec1 && k1 > ri0 && st1 < k0 + nn) L.mark2[st1 - k0] = static_cast<uint8_t>(k1 - ri0);
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint2 mk = *reinterpret_cast<const uint2*>(L.mark2 + l8);
-                uint32_t rm[8], run = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
-                    rm[k] = run;
-                }
-                const uint32_t ex = wave_shr1(wave_incl_max(run));
-                uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t v = max(ex, rm[k]);
-                    if (k < 4) w0 |= v << (8 * k);
-                    else w1 |= v << (8 * (k - 4));
-                }
-                __builtin_amdgcn_wave_barrier();
-                *reinterpret_cast<uint2*>(L.mark2 + l8) = make_uint2(w0, w1);
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-            uint32_t chars = 0, pw[4], cw[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t rk = min(rbase + __popc(vb & ((1u << k) - 1u)), static_cast<uint32_t>(kTileRows - 1));
-                const uint2 R = L.rec[1][(ri0 + L.mark2[rk]) & (kPipeRunCap - 1)];
-                const uint32_t pay = rr_pay(R);
-                const uint32_t lb = sbits3(L.stage, pay + (k0 + rk - rr_start(R)) * bwi, zw, maski);
-                const uint32_t v = rr_lit(R) ? lb : pay;
-                const bool ok = ((vb >> k) & 1u) && v < dict_n;
-                const uint32_t len = lens[ok ? v : 0u];
-                chars += ok ? len : 0u;
-                const uint32_t code = ok ? v : static_cast<uint32_t>(kNull);
-                cw[k] = code;
-            }
-            // (packed with v_perm: the |= form crashes instruction selection here)
-#pragma unroll
-            for (int k = 0; k < 4; k++) pw[k] = __builtin_amdgcn_perm(cw[2 * k + 1], cw[2 * k], 0x05040100u);
-            store_packed8(a.codes, first_row + r0, l8, m, pw);
-            tile_done(a, t, wave_sum(chars));
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-}
-
 // ── offsets, validity, characters ──────────────────────────────────────────
 constexpr int kRowsPerLane = kTileRows / kWave;
 
@@ -1378,10 +822,6 @@ __device__ __forceinline__ uint4 lds16(const uint32_t* w, uint32_t A) {
                       __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
 }
 
-struct WriteSlot {  // k_pipe_write2: one tile's codes handed from the loader to a writer
-    uint4 c[kWave];
-    uint32_t seq, ack, pad[2];
-};
 
 struct WriteArgs {
     const uint8_t* bytes;
@@ -1673,326 +1113,6 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     }
 }
 
-// k_pipe_write with a loader wave: the writers' only global loads were the
-// codes of their tiles, and on gfx9 a load waits for every store issued
-// before it (vmcnt).  Here a seventh wave loads each writer's next tile into
-// an LDS slot (sequence / acknowledge words), so the writer waves issue
-// stores only and never drain them.
-__global__ void __launch_bounds__((kWriteMax + 1) * 64) k_pipe_write2(WriteArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if (a.znext)  // the other flags/bsum/flist block, for the next decode (unused by this one)
-        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.znext_words; i += gridDim.x * blockDim.x) a.znext[i] = 0;
-    // [kFront zero bytes][dictionary payload][entry table][per-wave scratch]
-    uint32_t* dwa = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* dw = reinterpret_cast<uint32_t*>(smem + kFront);
-    uint32_t* dtab = reinterpret_cast<uint32_t*>(smem + kFront + a.dict_chars_bytes);
-    const uint32_t wv = threadIdx.x / kWave;
-    WriteLds& S = reinterpret_cast<WriteLds*>(smem + a.dict_bytes)[min(wv, static_cast<uint32_t>(a.wpw - 1))];
-    WriteSlot* slots = reinterpret_cast<WriteSlot*>(smem + a.dict_bytes + a.wpw * sizeof(WriteLds));
-    const DevDict d = a.dicts[a.dict_id];
-    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
-        uint4* dst = reinterpret_cast<uint4*>(dw);
-        copy_blocks(dst, src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
-        copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
-            return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
-        });
-    }
-    if (wv < a.wpw && lane() == 0) {
-        slots[wv].seq = 0;
-        slots[wv].ack = 0;
-    }
-    __syncthreads();
-    // each wavefront owns a contiguous run of tiles (consecutive rows): the
-    // descriptors of up to 64 tiles are loaded at once, one per lane, and the
-    // next tile's codes are loaded before this tile's stores are issued
-    const int per = a.per;
-    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
-    const int tb = min(a.ntiles, ta + per);
-    auto wave_sum64 = [](unsigned long long v) {
-        for (int d = 1; d < kWave; d <<= 1) {
-            const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
-            const uint32_t hi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v >> 32), d));
-            v += (static_cast<unsigned long long>(hi) << 32) | lo;
-        }
-        return v;
-    };
-    if (wv == a.wpw) {  // the loader: codes of every writer's next tile -> its LDS slot
-        if (a.debug & 8) return;
-        const int TA = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
-        const int TB = min(a.ntiles, TA + a.wpw * per);
-        int64_t dR0 = 0, dR1 = 0, dR2 = 0, dR3 = 0;  // tiles TA + lane + 64c (launch: a.wpw * per <= 256)
-        uint32_t dm0 = 0, dm1 = 0, dm2 = 0, dm3 = 0;
-        auto dload = [&](int c, int64_t& R, uint32_t& mm) {
-            const int t = TA + static_cast<int>(lane()) + 64 * c;
-            if (t < TB) {
-                const DevTile T = a.tiles[t];
-                R = a.pages[T.page].first_row + T.row0;
-                mm = static_cast<uint32_t>(T.nrows);
-            }
-        };
-        dload(0, dR0, dm0);
-        dload(1, dR1, dm1);
-        dload(2, dR2, dm2);
-        dload(3, dR3, dm3);
-        const uint32_t l8 = lane() * kRowsPerLane;
-        for (int i = 0; i < per; i++) {
-            // writers in groups of kLoadGroup: their tiles' codes load together, then fill the slots
-            for (int w0 = 0; w0 < a.wpw; w0 += kLoadGroup) {
-                uint4 v[kLoadGroup];
-#pragma unroll
-                for (int u = 0; u < kLoadGroup; u++) {
-                    v[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-                    const int w = w0 + u;
-                    const int t = TA + w * per + i;
-                    if (w < a.wpw && t < TB) {
-                        const int j = t - TA, c = j >> 6, l = j & 63;
-                        const int64_t Rs = c == 0 ? dR0 : (c == 1 ? dR1 : (c == 2 ? dR2 : dR3));
-                        const uint32_t ms = c == 0 ? dm0 : (c == 1 ? dm1 : (c == 2 ? dm2 : dm3));
-                        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(Rs), l);
-                        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(Rs) >> 32), l);
-                        const int64_t R = static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
-                        const uint32_t mm = __builtin_amdgcn_readlane(ms, l);
-                        if (l8 < mm) {
-                            const U16B x = *reinterpret_cast<const U16B*>(a.codes + R + l8);
-                            v[u] = make_uint4(x.x, x.y, x.z, x.w);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < kLoadGroup; u++) {
-                    const int w = w0 + u;
-                    if (w >= a.wpw || TA + w * per + i >= TB) continue;
-                    volatile uint32_t* ack = &slots[w].ack;
-                    while (*ack != static_cast<uint32_t>(i)) __builtin_amdgcn_s_sleep(1);
-                    asm volatile("" ::: "memory");
-                    slots[w].c[lane()] = v[u];
-                    asm volatile("" ::: "memory");
-                    if (lane() == 0) *reinterpret_cast<volatile uint32_t*>(&slots[w].seq) = static_cast<uint32_t>(i + 1);
-                }
-            }
-        }
-        return;
-    }
-    // a writer takes tile tt's codes from its slot and frees it
-    auto take = [&](int tt) -> uint4 {
-        const uint32_t r = static_cast<uint32_t>(tt - ta);
-        volatile uint32_t* seq = &slots[wv].seq;
-        while (*seq != r + 1) __builtin_amdgcn_s_sleep(1);
-        asm volatile("" ::: "memory");
-        const uint4 v = slots[wv].c[lane()];
-        asm volatile("" ::: "memory");
-        if (lane() == 0) *reinterpret_cast<volatile uint32_t*>(&slots[wv].ack) = r + 1;
-        return v;
-    };
-    // first output byte of the range: the workgroups before this one (bsum,
-    // summed by k_pipe_codes), then this workgroup's earlier tiles
-    int64_t Grun = 0;
-    {
-        unsigned long long acc = 0;
-        for (uint32_t b = lane(); b < blockIdx.x; b += kWave) acc += a.bsum[b];
-        Grun = static_cast<int64_t>(wave_sum64(acc));
-    }
-    if (a.debug & 8) return;
-    {
-        const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
-        unsigned long long in = 0;
-        for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
-        Grun += static_cast<int64_t>(wave_sum64(in));
-    }
-    for (int c0 = ta; c0 < tb; c0 += kWave) {
-        const int cn = min(kWave, tb - c0);
-        int64_t myR0 = 0, myG0 = 0;
-        uint32_t mym = 0;
-        uint32_t myc = 0;
-        if (static_cast<int>(lane()) < cn) {
-            const DevTile T = a.tiles[c0 + lane()];
-            myR0 = a.pages[T.page].first_row + T.row0;
-            mym = static_cast<uint32_t>(T.nrows);
-            myc = static_cast<uint32_t>(a.tile_chars[c0 + lane()]);
-        }
-        {  // tile characters < 2^25 each: a 32-bit scan over <= 64 tiles
-            const uint32_t inc = wave_incl_scan(myc);
-            myG0 = Grun + static_cast<int64_t>(inc - myc);
-            Grun += static_cast<int64_t>(bcast_last(inc));
-        }
-        auto rl64 = [](int64_t v, int i) -> int64_t {
-            const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
-            const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), i);
-            return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
-        };
-        // codes of kWBatch tiles at a time -> LDS: the only global loads of
-        // the tile loop, so one wait (which also drains this wave's earlier
-        // stores: loads and stores share vmcnt) per batch, not per tile
-        const uint32_t l8 = lane() * kRowsPerLane;
-        for (int ib = 0; ib < cn; ib += kWBatch) {
-            // four named registers (an indexed array would go to scratch)
-            static_assert(kWBatch == 4, "batch registers");
-            auto ld = [&](int i) -> uint4 {
-                uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-                if (i < cn) {
-                    const int64_t R = rl64(myR0, i);
-                    const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
-                    if (l8 < mm) {
-                        const U16B x = *reinterpret_cast<const U16B*>(a.codes + R + l8);
-                        v = make_uint4(x.x, x.y, x.z, x.w);
-                    }
-                }
-                return v;
-            };
-            (void)ld;
-        for (int i = ib; i < min(cn, ib + kWBatch); i++) {
-            const int64_t R0 = rl64(myR0, i);
-            const int64_t G0 = rl64(myG0, i);
-            const uint32_t m = __builtin_amdgcn_readlane(mym, i);
-            uint32_t cur[kRowsPerLane];
-            {
-                const int u = i - ib;  // register select (no dynamic indexing into cv)
-                (void)u;
-                const uint4 w = take(c0 + i);
-                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++)
-                    cur[k] = l8 + k < m ? (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : kNull;
-            }
-            // this lane's rows 8l .. 8l + 7: lengths, dictionary offsets, validity
-            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0;
-#pragma unroll
-            for (int k = 0; k < kRowsPerLane; k++) {
-                const bool valid = cur[k] < dict_n;
-                const uint32_t e = valid ? dtab[cur[k]] : 0u;
-                len[k] = e >> 16;
-                src[k] = e & 0xFFFFu;
-                vb |= (valid ? 1u : 0u) << k;
-                acc += len[k];
-            }
-            const uint32_t incl = wave_incl_scan(acc);
-            const uint32_t total = bcast_last(incl);
-            {
-                uint32_t o = incl - acc;
-#pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++) {
-                    const uint32_t j = lane() * kRowsPerLane + k;
-                    if (j < m) {
-                        S.off[j] = o;
-                        S.src[j] = static_cast<uint16_t>(src[k]);
-                    }
-                    o += len[k];
-                }
-            }
-            S.vb[lane()] = static_cast<uint8_t>(vb);
-            if (lane() == 0) S.off[m] = total;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            if (!(a.debug & 4)) {
-                // offsets, row j = 64k + lane (coalesced)
-#pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++) {
-                    const uint32_t j = k * kWave + lane();
-                    if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
-                }
-                // validity words [R0 >> 5, (R0 + m - 1) >> 5]: tile word t = vb bytes 4t .. 4t + 3
-                const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
-                const uint32_t sh = static_cast<uint32_t>(R0 & 31);
-                const int64_t g = gfirst + lane();
-                if (g <= glast) {
-                    auto tw = [&](int t) -> uint32_t {
-                        return (t >= 0 && t < kWave / 4) ? reinterpret_cast<const uint32_t*>(S.vb)[t] : 0u;
-                    };
-                    const int t = static_cast<int>(lane());
-                    const uint32_t val = (tw(t) << sh) | (sh ? (tw(t - 1) >> (32 - sh)) : 0u);
-                    // the column's last word belongs to its last tile alone
-                    const bool whole = g * 32 >= R0 && (g * 32 + 32 <= R0 + m || R0 + m == a.nrows_total);
-                    if (whole) a.validity[g] = val;
-                    else if (val) atomicOr(&a.validity[g], val);
-                }
-            }
-            if (R0 + m == a.nrows_total && lane() == 0) {
-                a.offsets[a.nrows_total] = G0 + total;
-                *a.total = G0 + total;
-            }
-            if (total == 0 || (a.debug & 2)) continue;
-            if (G0 + total > a.capacity) {  // output too small: the host grows it and re-runs
-                if (lane() == 0) atomicOr(a.overflow, 1);
-                continue;
-            }
-            // characters, 64 consecutive rows per step: each lane copies its
-            // row from the LDS dictionary to HBM as unaligned 16-byte moves
-            // (the last one overlapping the row's earlier bytes), rows under
-            // 16 bytes as two overlapping 8/4/2-byte moves, so no store leaves
-            // its row and the L2 merges the partial lines.  Rows longer than
-            // kLongRow are copied afterwards by the whole wave, 16-byte
-            // aligned blocks across the lanes.  (Assembling aligned blocks in
-            // LDS first costs more than it saves: byte-unaligned LDS accesses
-            // are slow; scripts/probe/unaligned_store.hip)
-            const int64_t G1 = G0 + total;
-            if (a.debug & 128) {  // timing only: the tile's bytes as aligned 16-byte blocks of zeros
-                const int64_t b0 = G0 & ~static_cast<int64_t>(15);
-                for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < G1; blk += 16 * kWave) {
-                    const uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                    if (blk >= G0 && blk + 16 <= G1) *reinterpret_cast<uint4*>(a.chars + blk) = v;
-                    else store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, G0) - blk),
-                                    static_cast<uint32_t>(min(blk + 16, G1) - blk));
-                }
-                continue;
-            }
-            for (uint32_t g0 = 0; g0 < m; g0 += kWave) {
-                const uint32_t r = g0 + lane();
-                uint32_t s0 = 0, ln = 0, sa = 0;
-                if (r < m) {
-                    s0 = S.off[r];
-                    ln = S.off[r + 1] - s0;
-                    sa = kFront + S.src[r];
-                }
-                const bool lng = ln > kLongRow;
-                if (!lng && ln) {
-                    uint8_t* d = a.chars + G0 + s0;
-                    if (ln >= 16) {
-                        for (uint32_t x = 0; x + 16 < ln; x += 16) {
-                            const uint4 v = lds16(dwa, sa + x);
-                            *reinterpret_cast<U16B*>(d + x) = U16B{v.x, v.y, v.z, v.w};
-                        }
-                        const uint4 v = lds16(dwa, sa + ln - 16);
-                        *reinterpret_cast<U16B*>(d + ln - 16) = U16B{v.x, v.y, v.z, v.w};
-                    } else {
-                        const uint4 v = lds16(dwa, sa);           // bytes 0 .. 15 of the row's source
-                        const uint32_t t = ln >= 8 ? ln - 8 : (ln >= 4 ? ln - 4 : (ln >= 2 ? ln - 2 : 0u));
-                        const uint4 u = lds16(dwa, sa + t);       // bytes t .. t + 15
-                        if (ln >= 8) {
-                            *reinterpret_cast<U8B*>(d) = U8B{v.x, v.y};
-                            *reinterpret_cast<U8B*>(d + t) = U8B{u.x, u.y};
-                        } else if (ln >= 4) {
-                            *reinterpret_cast<U4B*>(d) = U4B{v.x};
-                            *reinterpret_cast<U4B*>(d + t) = U4B{u.x};
-                        } else if (ln >= 2) {
-                            *reinterpret_cast<U2B*>(d) = U2B{static_cast<uint16_t>(v.x)};
-                            *reinterpret_cast<U2B*>(d + t) = U2B{static_cast<uint16_t>(u.x)};
-                        } else {
-                            d[0] = static_cast<uint8_t>(v.x);
-                        }
-                    }
-                }
-                uint64_t lm = __ballot(lng);
-                while (lm) {  // long rows: the whole wave, aligned destination blocks
-                    const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
-                    lm &= lm - 1;
-                    const int64_t A0 = G0 + __builtin_amdgcn_readlane(s0, l);
-                    const int64_t A1 = A0 + __builtin_amdgcn_readlane(ln, l);
-                    const uint32_t src0 = __builtin_amdgcn_readlane(sa, l);
-                    const int64_t b0 = A0 & ~static_cast<int64_t>(15);
-                    for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < A1; blk += 16 * kWave) {
-                        const uint4 v = lds16(dwa, static_cast<uint32_t>(src0 + (blk - A0)));
-                        store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, A0) - blk),
-                                   static_cast<uint32_t>(min(blk + 16, A1) - blk));
-                    }
-                }
-            }
-            (void)G1;
-        }
-        }
-    }
-}
 
 // ── pages of more than kPipeSmallRows rows (arrow layout) ──────────────────
 // One workgroup per page, its payload staged in LDS.  A stream of ~1-2k runs
@@ -2013,7 +1133,7 @@ __global__ void __launch_bounds__((kWriteMax + 1) * 64) k_pipe_write2(WriteArgs 
 //      (rle_decoder.hpp:20-23): the records k_pipe_runs writes for a page;
 //   6. the page's 512-row tiles: def levels (one wave per tile), a scan of
 //      the tiles' non-null counts, then dictionary indices and codes as in
-//      k_pipe_codes2, each tile's first record found by binary search.
+//      k_pipe_codes3, each tile's first record found by binary search.
 // Anything outside the fast shape (a bad header before the value count,
 // record overflow, levels above max_def) sends the page to k_pipe_exact.
 constexpr int kBigWaves = 8;
@@ -2428,7 +1548,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
 }
 
 // ── regex page filter over the codes (README.md:54-64, SURVEY §8a R-REGEX) ─
-// After k_pipe_runs / k_pipe_big / k_pipe_codes2 / k_pipe_exact: one wave per
+// After k_pipe_runs / k_pipe_big / k_pipe_codes3 / k_pipe_exact: one wave per
 // tile tests its rows' codes against the dictionary's match bits (the pattern
 // ran once per entry, k_regex_dict).  A page whose tiles hold no non-null
 // value that matches (with --neg-regex: that fails to match) stays reported.
@@ -2461,17 +1581,17 @@ __global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match(const DevTile* 
 
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens) { return big_layout(max_page_bytes, nlens).total; }
 
-PipePlan plan_pipe_lds(uint32_t dict_bytes, bool loader, int wpw) {
+PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
     PipePlan pl{};
-    pl.lds = dict_bytes + static_cast<uint32_t>(wpw) * static_cast<uint32_t>(sizeof(WriteLds) + (loader ? sizeof(WriteSlot) : 0));
+    pl.lds = dict_bytes + static_cast<uint32_t>(wpw) * static_cast<uint32_t>(sizeof(WriteLds));
     const uint32_t all = pl.lds;
     pl.blocks_per_cu = all <= 160u * 1024 ? static_cast<int>((160u * 1024) / all) : 0;
     if (pl.blocks_per_cu > 4) pl.blocks_per_cu = 4;
     if (pl.blocks_per_cu > 0) {  // registers may allow fewer
-        const void* fn = loader ? reinterpret_cast<const void*>(k_pipe_write2) : reinterpret_cast<const void*>(k_pipe_write);
+        const void* fn = reinterpret_cast<const void*>(k_pipe_write);
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(pl.lds));
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, (wpw + (loader ? 1 : 0)) * kWave, pl.lds) ==
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, wpw * kWave, pl.lds) ==
                 hipSuccess && occ > 0)
             pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
     }
@@ -2480,13 +1600,13 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, bool loader, int wpw) {
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
-                      bool lean_codes) {
+                      bool) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     if (npages <= 0) return;
     const int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
     const int per = kRunWaves * ppw;
     hipLaunchKernelGGL(k_pipe_runs, dim3((npages + per - 1) / per), dim3(kRunWaves * kWave), 0, s, bytes, pages,
-                       npages, max_def, max_rep, runs, info, ppw, flist, lean_codes ? kStage3 - 16 : 0xFFFFFFFFu);
+                       npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's
@@ -2513,59 +1633,27 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     // persistent: the entry-length table (u16 per entry) is loaded once per workgroup
     const uint32_t lt_n = P.dict_entries_cap;
     const uint32_t lds = (lt_n * 2 + 15) / 16 * 16;
-    const void* fn = P.lean_codes ? reinterpret_cast<const void*>(k_pipe_codes3) : reinterpret_cast<const void*>(k_pipe_codes2);
-    static uint32_t attr[2] = {0, 0};
-    if (lds > attr[P.lean_codes]) {
+    const void* fn = reinterpret_cast<const void*>(k_pipe_codes3);
+    static uint32_t attr = 0;
+    if (lds > attr) {
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-        attr[P.lean_codes] = lds;
+        attr = lds;
     }
     // resident workgroups per CU (LDS and registers), so the grid is one wave of blocks
     int bpc = 0;
-    const int waves = P.lean_codes ? kCodeWaves3 : kCodeWaves2;
+    const int waves = kCodeWaves3;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, waves * kWave, lds) != hipSuccess || bpc < 1)
         bpc = 1;
     const int need = (P.ntiles + waves - 1) / waves;
     const int grid = max(1, min(need, P.cus * bpc));
     // also decodes the pages the run-table passes marked (flist)
-    if (P.has_small && P.lean_codes) {
+    if (P.has_small) {
         hipLaunchKernelGGL(k_pipe_codes3, dim3(grid), dim3(kCodeWaves3 * kWave), lds, s, a, lt_n, P.flist);
-    } else if (P.has_small) {
-        hipLaunchKernelGGL(k_pipe_codes2, dim3(grid), dim3(kCodeWaves2 * kWave), lds, s, a, lt_n, P.flist);
     } else {  // only k_pipe_big pages: the marked ones need the exact decoder alone
         hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, (P.npages + kCodeWaves - 1) / kCodeWaves))),
                            dim3(kCodeWaves * kWave), 0, s, a, P.flist);
     }
 }
-
-void launch_pipe_page(hipStream_t s, const PipeLaunch& P) {
-    if (P.npages <= 0) return;
-    int wgrid = 0, per = 0;
-    write_shape(P, &wgrid, &per);
-    CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
-               P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.bsum, per, P.debug, P.write_waves};
-    const uint32_t lt_n = P.dict_entries_cap;
-    const uint32_t lds = (lt_n * 2 + 15) / 16 * 16;
-    static uint32_t attr = 0;
-    if (lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_page), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(lds));
-        attr = lds;
-    }
-    int bpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(k_pipe_page), kPageWaves * kWave,
-                                                     lds) != hipSuccess || bpc < 1)
-        bpc = 1;
-    const int need = (P.npages + kPageWaves - 1) / kPageWaves;
-    const int grid = max(1, min(need, P.cus * bpc));
-    hipLaunchKernelGGL(k_pipe_page, dim3(grid), dim3(kPageWaves * kWave), lds, s, a, P.npages, lt_n,
-                       const_cast<uint32_t*>(P.info), const_cast<int32_t*>(P.flist));
-    // pages it could not take: the exact decoder
-    hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, (P.npages + kCodeWaves - 1) / kCodeWaves))),
-                       dim3(kCodeWaves * kWave), 0, s, a, P.flist);
-}
-
-uint32_t pipe_page_stage() { return kPageStage; }
 
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
     if (P.ntiles <= 0) return;
@@ -2580,16 +1668,6 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
     WriteArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.dicts, P.dict_id, P.entries, P.dict_count, P.codes,
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
                 P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves, P.znext, P.znext_words};
-    if (P.write2 && per * P.write_waves <= 256) {  // the loader's descriptor registers cover 256 tiles
-        static uint32_t attr2 = 0;
-        if (P.lds > attr2) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_write2),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(P.lds));
-            attr2 = P.lds;
-        }
-        hipLaunchKernelGGL(k_pipe_write2, dim3(grid), dim3((P.write_waves + 1) * kWave), P.lds, s, a);
-        return;
-    }
     hipLaunchKernelGGL(k_pipe_write, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
 }
 

@@ -123,9 +123,7 @@ struct PipeLaunch {
     int debug;  // ablation bits (k_pipe_write)
     uint32_t dict_entries_cap;  // entry-table capacity of the dictionary (k_pipe_codes length table)
     int cus;
-    bool has_small;             // some pages of <= kPipeSmallRows rows (k_pipe_runs / k_pipe_codes2)
-    bool lean_codes;            // k_pipe_codes3 instead of k_pipe_codes2
-    bool write2;                // k_pipe_write2 (loader wave) instead of k_pipe_write; P.lds / P.grid planned for it
+    bool has_small;             // some pages of <= kPipeSmallRows rows (k_pipe_runs / k_pipe_codes3)
     int write_waves;            // writer waves per k_pipe_write workgroup (planned with P.lds / P.grid)
     uint32_t* znext;            // cleared by k_pipe_write (the next decode's flags/bsum/flist[0]), or null
     uint32_t znext_words;
@@ -134,17 +132,11 @@ struct PipePlan {
     uint32_t lds;       // dynamic LDS bytes of k_pipe_write
     int blocks_per_cu;  // 0: the dictionary does not fit
 };
-PipePlan plan_pipe_lds(uint32_t dict_bytes, bool loader, int wpw);  // loader: k_pipe_write2 (its LDS slots)
+PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw);
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
-                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
-                      bool lean_codes);
+                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist, bool);
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
-// small pages' run tables and codes in one pass (one wave per page), then the
-// exact decoder for the pages it lists; replaces launch_pipe_runs +
-// launch_pipe_codes when every small page's payload fits pipe_page_stage() - 16
-void launch_pipe_page(hipStream_t s, const PipeLaunch& P);
-uint32_t pipe_page_stage();
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,
 // then codes and tile characters (one workgroup per listed page)
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens);
@@ -189,7 +181,6 @@ struct FusedLaunch {
     int claim;       // pages per ticket
 };
 
-// ── batched dictionary BYTE_ARRAY path (dict_batch.hip) ────────────────────
 // A run of consecutive data pages whose payload slots form one contiguous
 // image range [img_lo, img_lo + img_bytes).
 struct DevBatch {
@@ -199,43 +190,6 @@ struct DevBatch {
     uint32_t pad;
 };
 
-struct BatchLaunch {
-    const uint8_t* bytes;
-    const DevPage* pages;
-    const DevBatch* batches;
-    int32_t nbatches, last_page;
-    const DevDict* dicts;
-    int32_t dict_id;
-    const uint64_t* entries;
-    const int32_t* dict_count;
-    int32_t max_def, max_rep;
-    uint32_t rows_cap, batch_bytes, max_slot, dict_bytes, dict_chars_bytes;
-    uint64_t* status;
-    int32_t* ticket;
-    const int64_t* base_in;
-    int64_t* base_out;
-    int64_t nrows_total;
-    uint32_t* validity;
-    int64_t* offsets;
-    uint8_t* chars;
-    int64_t capacity;
-    int32_t* overflow;
-    DevErr* page_err;
-    int32_t* err_any;
-    int debug;
-    uint64_t* prof;
-    int grid, writers;
-    uint32_t lds;
-};
-
-struct BatchPlan {
-    int writers;   // writer waves per workgroup (0: does not fit)
-    uint32_t lds;  // dynamic LDS bytes per workgroup
-};
-BatchPlan plan_batch_lds(uint32_t rows_cap, uint32_t batch_bytes, uint32_t max_slot, uint32_t dict_bytes);
-int batch_occupancy(uint32_t lds_bytes, int waves);
-void launch_ba_batch(hipStream_t s, const BatchLaunch& B);
-int batch_prof_slots();
 
 void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
                        uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any,
@@ -266,8 +220,6 @@ struct PlainLaunch {
     DevErr* page_err;
     int32_t* err_any;
     const int32_t* gate;         // non-null: skip everything when *gate != 0 (the spec path fell back)
-    const int32_t* unit_win;     // non-null: k_plain_rows, one lane per page, page -> its window
-    int32_t nunits;              // pages (or pseudo pages) for k_plain_rows
 };
 int plain_write_blocks_per_cu();
 

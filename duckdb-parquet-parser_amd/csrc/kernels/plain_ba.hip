@@ -617,43 +617,6 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
     }
 }
 
-// k_plain_rows: one lane per page (or pseudo page), 64 per wave: the length
-// chain (column_reader.cpp:249-253) from the HBM image, each row's (position
-// in its window | length << 16) and the window's characters, filed under the
-// k_plain_write workgroup that writes it.  A chain that runs past its page is
-// the reference's ByteBuffer error at that position.
-constexpr int kRowsWaves = 4;
-
-__global__ void __launch_bounds__(kRowsWaves * 64) k_plain_rows(PlainLaunch a) {
-    if (a.gate && *a.gate) return;
-    const int u = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
-    if (u >= a.nunits) return;
-    const DevPage pg = a.pages[u];
-    const int w = a.unit_win[u];
-    const DevBatch W = a.wins[w];
-    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
-    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
-    const uint32_t base = static_cast<uint32_t>(pg.off - W.img_lo);
-    const uint8_t* page = a.bytes + pg.off;
-    uint32_t* ri = a.rowinfo + pg.first_row;
-    uint32_t pos = 0, k = 0;
-    unsigned long long chars = 0;
-    for (; k < n; k++) {
-        if (pos + 4 > size) { lane_err(a.page_err + u, a.err_any, pos, 4, size); break; }
-        const uint32_t len = gword(page, pos);
-        pos += 4;
-        if (static_cast<uint64_t>(pos) + len > size) { lane_err(a.page_err + u, a.err_any, pos, len, size); break; }
-        ri[k] = (base + pos) | (len << 16);
-        chars += len;
-        pos += len;
-    }
-    for (; k < n; k++) ri[k] = 0;  // a failed page: empty rows (the decode reports the error)
-    if (chars) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(a.wchars + w), chars);
-        atomicAdd(&a.bsum[(w / a.per) / kPWWaves], chars);
-    }
-}
-
 }  // namespace
 
 uint32_t plain_write_lds() { return kPWWaves * static_cast<uint32_t>(sizeof(PWLds)); }
@@ -690,12 +653,7 @@ void launch_plain_ba(hipStream_t s, PlainLaunch P) {
     plain_shape(P, &grid, &per);
     P.per = per;
     (void)hipMemsetAsync(P.bsum, 0, static_cast<size_t>(grid) * sizeof(unsigned long long), s);
-    if (P.unit_win) {  // lane per page: rows and window characters (k_plain_rows)
-        (void)hipMemsetAsync(P.wchars, 0, static_cast<size_t>(P.nwins) * sizeof(int64_t), s);
-        if (P.nunits > 0)
-            hipLaunchKernelGGL(k_plain_rows, dim3((P.nunits + kRowsWaves * kWave - 1) / (kRowsWaves * kWave)),
-                               dim3(kRowsWaves * kWave), 0, s, P);
-    } else {
+    {
         static int walk_grid = 0;  // resident workgroups of k_plain_walk on this device
         if (!walk_grid) {
             int bpc = 0, cus = 0;

@@ -629,174 +629,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
     }
 }
 
-// ── streaming PLAIN scan ────────────────────────────────────────────────────
-// One lane per page, the page read straight from HBM in 16-byte chunks two
-// ahead of use (three rotating registers, one load per chunk, so the wait
-// for a chunk is vmcnt(2) and never a full drain).  Every byte goes through
-// the same branch-free step: a u32 length prefix byte, or a string byte (one
-// DFA lookup in LDS); a finished string sets the page's hit when it
-// satisfies the predicate.  The whole length chain is validated (a decode
-// error fails the page even after a match, as the windowed kernel does).
-// No per-wave LDS but the DFA, so occupancy is set by registers.
-constexpr int kStreamWaves = 4;
-
-template <bool kFull>
-__global__ void __launch_bounds__(kStreamWaves * 64) k_regex_stream(const uint8_t* __restrict__ dfa_img,
-                                                                    uint32_t dfa_bytes,
-                                                                    const uint8_t* __restrict__ bytes,
-                                                                    const DevPage* __restrict__ pages, int npages,
-                                                                    ColumnParams cp, int neg,
-                                                                    uint8_t* __restrict__ page_flags,
-                                                                    DevErr* __restrict__ page_err,
-                                                                    int32_t* __restrict__ err_any) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(dfa_img);
-        uint4* dst = reinterpret_cast<uint4*>(dsm);
-        copy_blocks(dst, src, dfa_bytes / 16, threadIdx.x, blockDim.x);
-    }
-    __syncthreads();
-    const DevDfa* D = reinterpret_cast<const DevDfa*>(dsm);
-    const uint16_t* T = reinterpret_cast<const uint16_t*>(dsm + sizeof(DevDfa));
-    const uint32_t nc = D->nclasses;
-    const uint32_t empty_ok = D->empty_string != 0 ? 1u : 0u;
-    const bool trivial = D->nonempty_trivial != 0;
-    const uint32_t negv = neg != 0 ? 1u : 0u;
-    const uint32_t start_e = kFull ? DFA_START * kDfaRowBytes : DFA_START;
-    const uint32_t acc_e = kFull ? DFA_ACCEPT * kDfaRowBytes : DFA_ACCEPT;
-    const uint32_t md = static_cast<uint32_t>(cp.max_def);
-    const int wv = static_cast<int>(threadIdx.x / kWave);
-    const int stride = static_cast<int>(gridDim.x) * kStreamWaves * kWave;
-    for (int base = (static_cast<int>(blockIdx.x) * kStreamWaves + wv) * kWave; base < npages; base += stride) {
-        const int p = base + static_cast<int>(lane());
-        const bool act0 = p < npages;
-        DevPage pg{};
-        if (act0) pg = pages[p];
-        const uint8_t* page = bytes + pg.off;
-        const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
-        const uint32_t nv = static_cast<uint32_t>(max(pg.nvals, 0));
-        uint32_t pos = 0, nn = nv, epos = 0, eneed = 0;
-        int ecode = 0;
-        // def levels (column_reader.cpp:146-170): the non-null count
-        if (act0 && cp.max_def > 0) {
-            auto rd8 = [&](uint32_t a) { return gld8(page, a); };
-            if (pos + 4 > size) { ecode = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
-            else {
-                const uint32_t dl = static_cast<uint32_t>(gld8(page, pos));
-                pos += 4;
-                if (static_cast<uint64_t>(pos) + dl > size) { ecode = PQ_ERR_BUFFER; epos = pos; eneed = dl; }
-                else {
-                    LRle r = lrle(pos, dl, level_bw(cp.max_def));
-                    const uint32_t bwd = r.bw;
-                    nn = 0;
-                    const int rc = lane_rle(r, rd8, nv, [&](uint32_t kind, uint32_t k, uint32_t arg) {
-                        if (kind == 0) {
-                            if (arg >= md) nn += k;
-                        } else {
-                            for (uint32_t i = 0; i < k; i++)
-                                if (gbits(page, size, static_cast<uint64_t>(arg) + i * bwd, bwd) >= md) nn++;
-                        }
-                    });
-                    if (rc) { ecode = rc; epos = 0; eneed = 0; }
-                    pos += dl;
-                }
-            }
-        }
-        if (act0 && !ecode && cp.max_rep > 0) {
-            if (pos + 4 > size) { ecode = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
-            else {
-                const uint32_t rl = static_cast<uint32_t>(gld8(page, pos));
-                pos += 4;
-                if (static_cast<uint64_t>(pos) + rl > size) { ecode = PQ_ERR_BUFFER; epos = pos; eneed = rl; }
-                else pos += rl;
-            }
-        }
-        // values (column_reader.cpp:249-253): u32 length + bytes, nn times
-        uint32_t live = (act0 && !ecode && nn > 0) ? 1u : 0u;
-        uint32_t lp = 0, len = 0, rem = 0, e = start_e, k = 0, sp = pos, sat = 0;
-        const uint32_t c0 = pos >> 4, nch = (size + 15) >> 4;
-        const uint32_t nit = live ? nch - c0 : 0u;
-        const uint32_t itmax = bcast_last(wave_incl_max(nit));
-        const uint4* P = reinterpret_cast<const uint4*>(page);
-        const uint32_t clast = nch ? nch - 1 : 0u;
-        auto ld = [&](uint32_t c) -> uint4 { return P[min(c, clast)]; };
-        auto step = [&](const uint4& W, uint32_t c) {
-#pragma unroll 1
-            for (uint32_t q = 0; q < 4; q++) {
-                const uint32_t wd = q == 0 ? W.x : (q == 1 ? W.y : (q == 2 ? W.z : W.w));
-#pragma unroll
-                for (uint32_t j = 0; j < 4; j++) {
-                    const uint32_t x = c * 16 + q * 4 + j;
-                    const uint32_t b = (wd >> (8 * j)) & 0xFFu;
-                    const uint32_t a = live & (x >= pos ? 1u : 0u) & (x < size ? 1u : 0u);
-                    const uint32_t inl = lp < 4 ? 1u : 0u;
-                    const uint32_t isl = a & inl, iss = a & (inl ^ 1u);
-                    len = isl ? (len | (b << (8 * (lp & 3)))) : len;
-                    const uint32_t lp1 = lp + isl;
-                    const uint32_t got = isl & (lp1 == 4 ? 1u : 0u);
-                    const uint32_t over = got & (len > size - (x + 1) ? 1u : 0u);
-                    uint32_t t;
-                    if (kFull) t = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(T) + (e & 0x7FFFu) + 2 * b);
-                    else t = T[(e & 0x7FFFu) * nc + D->cls_of[b]];
-                    e = iss ? t : (got ? start_e : e);
-                    const uint32_t rem1 = got ? len : rem - iss;
-                    const uint32_t empty = got & (len == 0 ? 1u : 0u);
-                    const uint32_t fin = (empty & (over ^ 1u)) | (iss & (rem1 == 0 ? 1u : 0u));
-                    const uint32_t m = empty ? empty_ok : ((trivial || (e & 0x7FFFu) == acc_e || (e >> 15) != 0) ? 1u : 0u);
-                    sat |= fin & (m ^ negv);
-                    k += fin;
-                    lp = fin ? 0u : lp1;
-                    len = fin ? 0u : len;
-                    rem = rem1;
-                    sp = fin ? x + 1 : sp;
-                    if (over) { ecode = PQ_ERR_BUFFER; epos = x + 1; eneed = len; }
-                    live = live & (over ^ 1u) & (k < nn ? 1u : 0u);
-                }
-            }
-        };
-        uint4 W0 = ld(c0), W1 = ld(c0 + 1), W2;
-        for (uint32_t it = 0; it < itmax; it += 3) {
-            W2 = ld(c0 + it + 2);
-            step(W0, c0 + it);
-            W0 = ld(c0 + it + 3);
-            step(W1, c0 + it + 1);
-            W1 = ld(c0 + it + 4);
-            step(W2, c0 + it + 2);
-        }
-        // the chain ended (page end) with values still declared
-        if (act0 && !ecode && k < nn) { ecode = PQ_ERR_BUFFER; epos = sp; eneed = 4; }
-        if (act0) {
-            if (ecode) lane_err(page_err + p, err_any, ecode, epos, eneed, size);
-            page_flags[p] = (sat && !ecode) ? 0 : 1;
-        }
-    }
-}
-
 }  // namespace
-
-void launch_regex_stream(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, bool full, const uint8_t* bytes,
-                         const DevPage* pages, int npages, int cus, ColumnParams cp, int neg, uint8_t* page_flags,
-                         DevErr* page_err, int32_t* err_any) {
-    if (npages <= 0) return;
-    const void* fn = full ? reinterpret_cast<const void*>(k_regex_stream<true>)
-                          : reinterpret_cast<const void*>(k_regex_stream<false>);
-    static bool attr[2] = {false, false};
-    if (!attr[full]) {
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kDfaMaxBytes);
-        attr[full] = true;
-    }
-    int bpc = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kStreamWaves * kWave, dfa_bytes) != hipSuccess || bpc < 1)
-        bpc = 1;
-    const int need = (npages + kStreamWaves * kWave - 1) / (kStreamWaves * kWave);
-    const int grid = std::max(1, std::min(need, cus * bpc));
-    if (full)
-        hipLaunchKernelGGL(k_regex_stream<true>, dim3(grid), dim3(kStreamWaves * kWave), dfa_bytes, s, dfa, dfa_bytes,
-                           bytes, pages, npages, cp, neg, page_flags, page_err, err_any);
-    else
-        hipLaunchKernelGGL(k_regex_stream<false>, dim3(grid), dim3(kStreamWaves * kWave), dfa_bytes, s, dfa, dfa_bytes,
-                           bytes, pages, npages, cp, neg, page_flags, page_err, err_any);
-}
 
 DeviceProgram* upload_program(const Program& p, hipStream_t s) {
     DevProg h;

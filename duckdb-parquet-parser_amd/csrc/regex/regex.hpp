@@ -73,12 +73,6 @@ enum : uint32_t { DFA_DEAD = 0, DFA_ACCEPT = 1, DFA_START = 2 };
 // kernel is used then).
 bool build_dfa(const Program& p, std::vector<uint8_t>* image);
 
-// Streaming PLAIN scan (chunks without dictionary pages): one lane per page,
-// the page read from HBM in 16-byte chunks, a DFA step per byte.
-void launch_regex_stream(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, bool full, const uint8_t* bytes,
-                         const pqk::DevPage* pages, int npages, int cus, pqk::ColumnParams cp, int neg,
-                         uint8_t* page_flags, pqk::DevErr* page_err, int32_t* err_any);
-
 // Windowed PLAIN scan (chunks without dictionary pages).
 // per wave: the window (+16 zero bytes), a u16 offset per possible string,
 // per-page counts and list bases, the hit mask

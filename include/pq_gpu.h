@@ -109,25 +109,21 @@ int pq_ctx_sync(pq_ctx* ctx);
 /* Tuning switches (apply to chunks uploaded afterwards).  Every setting gives
  * the same outputs; they choose between kernels:
  *   "dict_pipe"   1 (default): three-pass dictionary BYTE_ARRAY kernels
- *   "codes3"      1 (default): lean code-expansion pass of the pipe, else codes2
  *   "write_waves" writer waves per workgroup of the pipe's write pass, 1..16 (10)
  *   "zflip"       1 (default): per-decode flags come pre-cleared by the previous
  *                 write pass, else a fill kernel per decode
- *   "page", "write2", "big_all", "graph", "pipe_run_pages" (1..32): measured
- *                 alternatives of the pipe, off / 32 by default
- *   "plain_ba"    1 (default): two-pass PLAIN BYTE_ARRAY kernels;
- *   "plain_rows"  0 (default): rows pass from LDS windows, 1: lane per page
+ *   "big_all"     1: every page of a pipe chunk takes the large-page kernel
+ *                 (k_pipe_big; coverage of that kernel on small pages), 0 (default)
+ *   "pipe_run_pages" pages per wavefront of the run-table pass, 1..32 (32)
+ *   "plain_ba"    1 (default): two-pass PLAIN BYTE_ARRAY kernels
  *   "fixed_plain" 1 (default): tile-parallel PLAIN fixed-width kernels
- *   "fused_ba"    1 (default): per-page fused BYTE_ARRAY kernel when every
- *                 chunk qualifies; 0 forces the generic rows/scan/gather kernels
- *   "batch"       1: batched dictionary kernel (dict_batch.hip) for chunks of
- *                 dictionary pages; 0 (default)
- *   "batch_bytes" payload bytes per batch buffer of the batched kernel
+ *   "fused_ba"    1 (default): per-page fused BYTE_ARRAY kernel for chunks the
+ *                 pipe does not take; 0 forces the generic rows/scan/gather kernels
  *   "fused_waves" waves per workgroup cap (0 = automatic)
  *   "regex_dfa", "regex_plain", "regex_codes" 1 (default): DFA kernels, the
  *                 windowed kernel for dictionary-free chunks, match bits over
- *                 the pipe's codes; "regex_stream" 0 (default); "regex_win"
- *                 window bytes (1024..32768, multiple of 16; 8192)
+ *                 the pipe's codes; "regex_win" window bytes (1024..32768,
+ *                 multiple of 16; 8192)
  * Diagnostics (timing studies only; outputs are not valid with bits set):
  *   "fused_debug", "regex_debug" ablation bits, "fused_prof"
  *   per-phase clocks.

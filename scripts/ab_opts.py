@@ -19,10 +19,10 @@ from pqgpu import capi, gen  # noqa: E402
 CONFIGS = {"C2": (gen.c2_cols, gen.REF_LAYOUT, 2), "C2a": (gen.c2_cols, gen.ARROW_LAYOUT, 2),
            "C3": (gen.c3_cols, gen.REF_LAYOUT, 3), "C4": (gen.c4_cols, gen.ARROW_LAYOUT, 4)}
 # library defaults of the options the variants may set (restored after each)
-DEFAULTS = {"pipe_run_pages": 32, "zflip": 1, "write_waves": 10, "codes3": 1, "page": 0, "write2": 0, "graph": 0, "dict_pipe": 1, "plain_ba": 1,
-            "fused_ba": 1, "batch": 0, "fixed_plain": 1, "plain_rows": 0, "big_all": 0, "fused_debug": 0}
-KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "pipe_page", "plain_spec", "pipe_count", "pipe_codes",
-           "pipe_write", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba")
+DEFAULTS = {"pipe_run_pages": 32, "zflip": 1, "write_waves": 10, "dict_pipe": 1, "plain_ba": 1,
+            "fused_ba": 1, "fixed_plain": 1, "big_all": 0, "fused_debug": 0}
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "plain_spec", "pipe_count", "pipe_codes",
+           "pipe_write", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba")
 
 cfg, _, colname = sys.argv[1].partition(":")
 rows = int(sys.argv[2])

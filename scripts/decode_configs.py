@@ -13,7 +13,7 @@ from pqgpu import capi, gen  # noqa: E402
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 only = sys.argv[2].split(",") if len(sys.argv) > 2 else None  # e.g. "C4:c7,C3"
 ctx = capi.Context(0)
-KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "pipe_page", "plain_spec", "pipe_count", "pipe_codes", "pipe_write", "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba")
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "plain_spec", "pipe_count", "pipe_codes", "pipe_write", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba")
 for name, cols, layout, seed in [("C2", gen.c2_cols(), gen.REF_LAYOUT, 2),
                                  ("C2a", gen.c2_cols(), gen.ARROW_LAYOUT, 2),
                                  ("C3", gen.c3_cols(), gen.REF_LAYOUT, 3),

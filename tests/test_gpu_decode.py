@@ -40,39 +40,27 @@ SMALL = [
 ]
 
 
-@pytest.fixture(params=["pipe", "walk", "page", "codes2", "batch", "fused", "generic"])
+@pytest.fixture(params=["default", "big", "fused", "generic"])
 def path(request, ctx):
-    """Every kernel path: BYTE_ARRAY three-pass dictionary (dict_pipe.hip) and
-    two-pass PLAIN (plain_ba.hip: rows one lane per page, or under "walk" one
-    wave per window), batched dictionary (dict_batch.hip), per-page fused
-    (dict_fused.hip) and generic (decode.hip); fixed-width PLAIN
-    tile-parallel (fixed_fast.hip) except under "generic", which runs
-    decode.hip's per-page k_fixed.  "page" takes k_pipe_page (run tables and
-    codes per page in one pass), k_pipe_write2 (loader wave) and replays the
-    decode as a HIP graph;
-    "codes2" takes k_pipe_codes2 instead of k_pipe_codes3."""
-    pipe = request.param in ("pipe", "walk", "page", "codes2")
-    ctx.set_option("page", int(request.param == "page"))
-    ctx.set_option("graph", int(request.param == "page"))
-    ctx.set_option("write2", int(request.param == "page"))
-    ctx.set_option("codes3", int(request.param != "codes2"))
-    ctx.set_option("dict_pipe", int(pipe))
-    ctx.set_option("plain_ba", int(pipe))
-    ctx.set_option("plain_rows", int(request.param == "pipe"))
-    ctx.set_option("fused_ba", int(request.param != "generic"))
-    ctx.set_option("batch", int(request.param == "batch"))
-    ctx.set_option("fixed_plain", int(request.param != "generic"))
-    yield request.param
-    ctx.set_option("page", 0)
-    ctx.set_option("graph", 0)
-    ctx.set_option("write2", 0)
-    ctx.set_option("codes3", 1)
-    ctx.set_option("dict_pipe", 1)
-    ctx.set_option("plain_ba", 1)
-    ctx.set_option("plain_rows", 0)
-    ctx.set_option("fused_ba", 1)
-    ctx.set_option("batch", 0)
-    ctx.set_option("fixed_plain", 1)
+    """Every kernel path that ships: "default" = what a chunk takes with the
+    default options (three-pass dictionary BYTE_ARRAY, dict_pipe.hip; two-pass
+    PLAIN BYTE_ARRAY, plain_ba.hip; tile-parallel PLAIN fixed width,
+    fixed_fast.hip; the fused and generic kernels for chunks neither
+    takes); "big" puts every page of a dictionary chunk through k_pipe_big
+    (the large-page kernel) so it also meets small pages; "fused" forces the
+    per-page fused BYTE_ARRAY kernel (dict_fused.hip) onto every BYTE_ARRAY
+    chunk it can take; "generic" forces decode.hip's rows/scan/gather and
+    per-page k_fixed."""
+    p = request.param
+    ctx.set_option("big_all", int(p == "big"))
+    ctx.set_option("dict_pipe", int(p in ("default", "big")))
+    ctx.set_option("plain_ba", int(p in ("default", "big")))
+    ctx.set_option("fused_ba", int(p != "generic"))
+    ctx.set_option("fixed_plain", int(p != "generic"))
+    yield p
+    for k in ("dict_pipe", "plain_ba", "fused_ba", "fixed_plain"):
+        ctx.set_option(k, 1)
+    ctx.set_option("big_all", 0)
 
 
 @pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT], ids=["ref", "arrow"])
@@ -91,8 +79,8 @@ def test_generated_columns(ctx, path, name, cols, n, layout):
                                          ("c2_dict", "c4_mixed", "all_null", "long_strings", "wide_dict")],
                          ids=lambda v: v if isinstance(v, str) else "")
 def test_small_arrow_pages(ctx, path, name, cols, n):
-    """Arrow-style pages small enough for the batched path: bit-packed
-    def-level runs, RLE runs >= 8, many pages per batch."""
+    """Arrow-style pages of 700 rows: bit-packed def-level runs, RLE runs
+    >= 8, several tiles per page."""
     f = gen.build(cols, n, 2, seed=12, layout=gen.ARROW_LAYOUT, rows_per_page=700)
     for ci in range(len(cols)):
         chunks = file_chunks(f, ci)

@@ -61,20 +61,18 @@ CASES = [
 ]
 
 
-@pytest.fixture(params=["stream", "window", "codes", "lanes", "nfa"])
+@pytest.fixture(params=["window", "codes", "lanes", "nfa"])
 def kernel(request, ctx):
-    """Every page kernel: streaming DFA, lane per page (default for chunks
-    without dictionary pages), windowed DFA, match bits over the pipe
-    decode's codes (default for dictionary chunks the pipe path takes),
-    lane-per-page DFA (other dictionary chunks) and wave-per-page NFA."""
+    """Every page kernel: windowed DFA (default for chunks without dictionary
+    pages), match bits over the pipe decode's codes (default for dictionary
+    chunks the pipe path takes), lane-per-page DFA (other dictionary chunks)
+    and wave-per-page NFA (patterns whose DFA is over its size cap)."""
     ctx.set_option("regex_dfa", int(request.param != "nfa"))
-    ctx.set_option("regex_plain", int(request.param in ("stream", "window")))
-    ctx.set_option("regex_stream", int(request.param == "stream"))
-    ctx.set_option("regex_codes", int(request.param in ("stream", "window", "codes")))
+    ctx.set_option("regex_plain", int(request.param == "window"))
+    ctx.set_option("regex_codes", int(request.param in ("window", "codes")))
     yield request.param
     ctx.set_option("regex_dfa", 1)
     ctx.set_option("regex_plain", 1)
-    ctx.set_option("regex_stream", 1)
     ctx.set_option("regex_codes", 1)
 
 
