@@ -2,24 +2,43 @@
 """Benchmark: decoded values/s (RLE + dictionary BYTE_ARRAY) and regex pages/s.
 
 Workload (BASELINE.json configs[1] = SURVEY §8d C2): one BYTE_ARRAY UTF8
-OPTIONAL column, 10M rows in one row group, 1000-entry dictionary, runs of
-1+U[0,16) rows, 5% NULL, reference-writer page layout (512 rows/page,
-bit width 10), synthetic data from the deterministic generator.  One step =
-one full ColumnReader::read_all-equivalent decode of the chunk on the GPU
+OPTIONAL column, 1000-entry dictionary, runs of 1+U[0,16) rows, 5% NULL,
+reference-writer page layout (512 rows/page, bit width 10), synthetic data
+from the deterministic generator.  One step = one full
+ColumnReader::read_all-equivalent decode of a rank's pages on the GPU
 (validity bitmap + int64 offsets + chars, all kernels), inputs resident in
-HBM.  With --gpus N each rank decodes its own 10M-row row group (C5-style
-page-range sharding, weak scaling, no collective on the data path).
+HBM.
 
-The regex leg (configs[2] = C3) times the --regex-column page filter over a
-10M-row PLAIN UTF-8 column (~293k pages) and reports pages/s.
+Multi-GPU: the job is ONE such column chunk of N x 10M rows in
+one row group; its data pages are split into N contiguous byte-balanced
+ranges (pqgpu.shard.data_page_ranges) and rank r uploads range r plus the
+dictionary page (pq_chunk_upload_range).  Weak scaling, no collective on the
+data path.  `python bench.py --gpus N` launches the N ranks itself
+(torch.distributed.run) when WORLD_SIZE is not set; the driver's own
+torch.distributed.run launch is used as is.  With N > 1 a strong-scaling
+figure (the 10M-row chunk split N ways) is reported beside it.
+
+Timing: W untimed warmup steps, then R = --repeats timed regions of exactly
+K steps, each bracketed by barrier + device sync on both sides; per region
+the max over ranks; `value` comes from the median region.
+
+Further legs (not `value`): C3 regex page filter (configs[2]) and PLAIN
+decode, C4 8 mixed columns, C5 dictionary decode + regex, end-to-end (host
+walk + H2D + decode), CPU baselines.  Every leg's result is checked against
+the generator's own value dump (pinned to the oracle by the CPU tests) or the
+committed regex page-set digests (tests/golden/bench_expect.json).
 
 Rank 0 prints ONE JSON line (contract in the task statement).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -32,17 +51,19 @@ for _p in (ROOT, PKG):
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel timers (HIP events on the decode stream, capi.hip Timed)
 KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "pipe_count", "pipe_codes", "pipe_write",
-           "ba_batch", "ba_fused", "ba_rows", "scan", "ba_gather")
+           "ba_fused", "ba_rows", "scan", "ba_gather", "plain_spec", "plain_ba", "fixed_plain", "fixed")
 REGEX_KERNELS = ("regex_dict", "regex_codes", "regex_lanes", "regex_plain", "regex_pages")
 ROWS = 10_000_000
+C5_PATTERN = "^qx"  # splits C5's pages (≈7% reported): not an all-miss scan
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--rows", type=int, default=ROWS)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--repeats", type=int, default=5, help="timed regions of --steps steps (median reported)")
+    ap.add_argument("--rows", type=int, default=ROWS, help="C2 rows per GPU")
     ap.add_argument("--layout", choices=["ref", "arrow"], default="ref")
     ap.add_argument("--no-regex", action="store_true")
     ap.add_argument("--regex-rows", type=int, default=ROWS)
@@ -50,368 +71,161 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--c4-rows", type=int, default=ROWS)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=5.0, help="per CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the box's CPU share (<= 16)")
     ap.add_argument("--no-c5", action="store_true")
     ap.add_argument("--c5-rgs", type=int, default=4, help="C5 row groups of 10M rows per GPU (1B rows / 8 GPUs = 12.5)")
+    ap.add_argument("--c5-pattern", default=C5_PATTERN)
+    ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return ap.parse_args()
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc
-    summary (profiles/pmc_latest.json, written by scripts/pmc_summary.py from
-    separate FETCH_SIZE and WRITE_SIZE passes of this same command; FETCH_SIZE
-    doubled for 16-B-per-lane reads on gfx950 as the microarch guide says)."""
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if not os.path.exists(path):
-        return None
+# ── launch ────────────────────────────────────────────────────────────────
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def maybe_spawn(args):
+    """--gpus N without a launcher: start N ranks as CHILD processes (one per
+    GPU, torch.distributed.run) and exit with their status.  Nothing here has
+    touched the GPU yet."""
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd, env=env))
+
+
+# ── measurement plumbing ──────────────────────────────────────────────────
+class Job:
+    def __init__(self, rank, world, local, dist, ctx):
+        self.rank, self.world, self.local, self.dist, self.ctx = rank, world, local, dist, ctx
+
+    def barrier(self):
+        import torch
+        if self.dist is not None:
+            self.dist.barrier()
+        torch.cuda.synchronize()
+        self.ctx.sync()
+
+    def max_all(self, xs):
+        if self.dist is None:
+            return list(xs)
+        import torch
+        t = torch.tensor(list(xs), dtype=torch.float64, device=f"cuda:{self.local}")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return t.tolist()
+
+    def sum_all(self, xs):
+        if self.dist is None:
+            return list(xs)
+        import torch
+        t = torch.tensor(list(xs), dtype=torch.float64, device=f"cuda:{self.local}")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t.tolist()
+
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def timed(self, step, check, steps, repeats, warmup=0, kernels=KERNELS):
+        """`repeats` regions of exactly `steps` steps, each bracketed by a
+        barrier + sync; seconds per region (max over ranks), then the same
+        steps once more with per-kernel HIP events (events perturb the wall
+        clock, so they stay outside the timed regions)."""
+        import torch
+        for _ in range(warmup):
+            step()
+        self.ctx.sync()
+        check()
+        secs = []
+        for _ in range(repeats):
+            self.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            self.ctx.sync()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            self.barrier()
+            secs.append(t1 - t0)
+        check()
+        secs = self.max_all(secs)
+        self.ctx.timing(True)
+        self.ctx.timing_reset()
+        for _ in range(steps):
+            step()
+        self.ctx.sync()
+        self.ctx.timing(False)
+        check()
+        kern = {}
+        for name in kernels:
+            ms, n = self.ctx.timing_get(name)
+            if n:
+                kern[name] = {"ms_per_launch": ms / n, "ms_per_step": ms / steps, "launches_per_step": n / steps}
+        return secs, kern
+
+
+def kernel_source_hash() -> str:
+    """sha256 over the HIP sources (what a PMC summary must have been taken on
+    for its traffic figure to apply to this run)."""
+    h = hashlib.sha256()
+    base = os.path.join(PKG, "csrc")
+    for d, _, fs in sorted(os.walk(base)):
+        for f in sorted(fs):
+            if f.endswith((".hip", ".hpp", ".cpp")):
+                with open(os.path.join(d, f), "rb") as fh:
+                    h.update(f.encode())
+                    h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(path: str, kernel: str):
+    """HBM bytes per launch of `kernel` from a rocprofv3 --pmc summary
+    (scripts/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE passes,
+    corrected per MI355X_MICROARCH.md), used only when it was taken on these
+    same kernel sources; else None."""
+    if not path or not os.path.exists(path):
+        return None, "no PMC summary"
     with open(path) as fh:
         d = json.load(fh)
+    if d.get("kernel_src_sha") != kernel_source_hash():
+        return None, f"PMC summary {d.get('source')} was taken on other kernel sources"
     k = d.get("kernels", {}).get(kernel)
-    return k.get("hbm_bytes_per_launch") if k else None
+    return (k.get("hbm_bytes_per_launch") if k else None), d.get("source")
 
 
-def cpu_baseline(file: bytes, chunk, seconds: float):
-    """The reference's own ColumnReader::read_all (oracle/_ref, compiled from
-    the reference sources) on this host, 1 thread, bounded sample."""
-    from oracle import oracle as O
-    ch = O.Chunk(chunk.num_values, chunk.data_page_offset,
-                 chunk.dictionary_page_offset if chunk.has_dictionary_page_offset else None,
-                 chunk.codec, chunk.type, chunk.max_def_level, chunk.max_rep_level)
-    if O.have_ref():
-        s, nv = O.ref_time_read_all(file, ch, reps=1, threads=1)
-        reps = max(1, int(seconds / max(s, 1e-3)))
-        s, nv = O.ref_time_read_all(file, ch, reps=reps, threads=1)
-        return {"value": nv / s, "unit": "values/s", "cores": 1, "kind": "reference",
-                "sample": f"{reps} x ColumnReader::read_all of a {ch.num_values}-row C2 chunk "
-                          f"(in-memory ReadRangeFunc, -O2), {s:.1f} s"}
-    t0 = time.perf_counter()
-    reps = 0
-    nv = 0
-    while time.perf_counter() - t0 < seconds:
-        rc, msg, col = O.read_all(file, ch)
-        nv += len(col.valid)
-        reps += 1
-    s = time.perf_counter() - t0
-    return {"value": nv / s, "unit": "values/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} x oracle read_all of a {ch.num_values}-row C2 chunk, {s:.1f} s"}
+def sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
 
 
-def main():
-    args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-
-    from pqgpu import capi, gen
-    from pqgpu.shard import rank_row_groups
-
-    # ── decode leg: each rank its own C2-shaped row group ────────────────
-    layout = gen.REF_LAYOUT if args.layout == "ref" else gen.ARROW_LAYOUT
-    my_rgs = rank_row_groups(world, rank, world)  # one 10M-row row group per rank
-    file = gen.build(gen.c2_cols(), args.rows, len(my_rgs), seed=gen.CONFIG_SEEDS["C2"],
-                     layout=layout, first_rg=my_rgs[0])
-    F = capi.File(file)
-    chunks = [F.chunk(rg, 0) for rg in range(F.num_row_groups)]
-    ctx = capi.Context(local)
-    dc = ctx.upload(file, chunks)
-    dc.decode()  # allocate outputs + error check
-    nrows = dc.num_rows
-    total_chars = dc.out.num_bytes
-    host = dc.to_host()
-    nonnull = int(host.validity.sum())
-    del host
-    for _ in range(args.warmup):
-        dc.decode_async()
-    ctx.sync()
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        ctx.sync()
-
-    # the timed region runs without per-kernel events (an event pair around
-    # every launch adds ~15% to the step); the per-kernel HIP-event durations
-    # come from the same steps repeated right after with the timers on
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dc.decode_async()
-    ctx.sync()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    dc.decode_check()
-    elapsed = t1 - t0
-    ctx.timing(True)
-    ctx.timing_reset()
-    for _ in range(args.steps):
-        dc.decode_async()
-    ctx.sync()
-    ctx.timing(False)
-    dc.decode_check()
-    kern = {}
-    for name in KERNELS:
-        ms, n = ctx.timing_get(name)
-        if n:
-            kern[name] = ms / n
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        rows_t = torch.tensor([nrows * args.steps], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(rows_t, op=dist.ReduceOp.SUM)
-        total_values = float(rows_t.item())
-    else:
-        total_values = float(nrows * args.steps)
-    value = total_values / elapsed
-    ms_per_step = elapsed / args.steps * 1e3
-
-    payload = dc.payload_bytes
-    out_bytes = 8 * (nrows + 1) + total_chars + (nrows + 7) // 8
-    b_alg = payload + out_bytes  # SURVEY §8d C2 algorithmic bytes per decode
-    dom = max(kern, key=kern.get) if kern else "ba_fused"
-    dom_ms = kern.get(dom, ms_per_step)
-    # algorithmic bytes of one launch of the dominant kernel (DESIGN.md §4):
-    # the fused/batched kernels read every page payload once and write the
-    # whole column (offsets, characters, validity); the pipelines' stages
-    # split that between them (pipe_write: u16 codes in, the column out).
-    dom_bytes = {"ba_fused": b_alg, "ba_batch": b_alg, "ba_gather": out_bytes,
-                 "ba_rows": payload + 8 * nrows, "pipe_write": out_bytes + 2 * nrows,
-                 "pipe_codes": payload + 2 * nrows}.get(dom, payload)
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    step_kernel_ms = sum(kern.values())
-
-    result = {
-        "metric": "decoded values/sec (RLE+dict BYTE_ARRAY) and regex pages/sec at 1/2/4/8 GPUs",
-        "value": value,
-        "unit": "values/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (deterministic splitmix64 generator, SURVEY §8d C2 shape)",
-        "config": {"workload": f"C2: dict BYTE_ARRAY OPTIONAL, {args.rows} rows/GPU, 1 row group/GPU, "
-                               f"{args.layout}-layout, 1000-entry dict, 5% NULL",
-                   "rows_per_gpu": nrows, "pages_per_gpu": dc.num_pages,
-                   "parallelism": f"page-range shards x{world} (no collective)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(dom),
-                     "kernel": dom, "kernel_ms": dom_ms, "algorithmic_bytes": dom_bytes},
-        "pipeline": {"kernel_ms": kern, "kernel_ms_note": "HIP events on the decode streams, same steps repeated "
-                                                          "after the timed region (events perturb the wall clock)",
-                     "sum_kernel_ms": step_kernel_ms,
-                     "b_alg_bytes": b_alg, "b_alg_GBs_per_step": b_alg / (ms_per_step * 1e-3) / 1e9,
-                     "b_alg_frac_of_peak": b_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "nonnull": nonnull, "chars": total_chars},
-    }
-    dc.free()
-    del file
-
-    # ── regex leg (C3) ─────────────────────────────────────────────────────
-    if not args.no_regex:
-        rfile = gen.build(gen.c3_cols(), args.regex_rows, 1, seed=gen.CONFIG_SEEDS["C3"],
-                          first_rg=my_rgs[0])
-        RF = capi.File(rfile)
-        rdc = ctx.upload(rfile, [RF.chunk(0, 0)])
-        flags = rdc.regex_pages(args.pattern)
-        for _ in range(max(1, args.warmup // 2)):
-            rdc.regex_pages_async(args.pattern)
-        ctx.sync()
-        rsteps = max(3, args.steps // 2)
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(rsteps):
-            rdc.regex_pages_async(args.pattern)
-        ctx.sync()
-        t1 = time.perf_counter()
-        barrier()
-        rdc.regex_pages_result()
-        rel = t1 - t0
-        ctx.timing(True)  # per-kernel events: the same scans again, outside the timed region
-        ctx.timing_reset()
-        for _ in range(rsteps):
-            rdc.regex_pages_async(args.pattern)
-        ctx.sync()
-        ctx.timing(False)
-        rdc.regex_pages_result()
-        if dist is not None:
-            t = torch.tensor([rel], dtype=torch.float64, device=f"cuda:{local}")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            rel = float(t.item())
-        npages = rdc.num_pages
-        rms, rn, rkern = 0.0, 0, None
-        for rk in ("regex_plain", "regex_lanes", "regex_pages"):
-            rms, rn = ctx.timing_get(rk)
-            if rn:
-                rkern = rk
-                break
-        result["regex"] = {"pages_per_s": npages * rsteps * world / rel, "pages_per_gpu": npages,
-                           "ms_per_scan": rel / rsteps * 1e3, "pattern": args.pattern,
-                           "reported_pages": int(flags.sum()),
-                           "kernel": rkern, "kernel_ms": rms / rn if rn else None,
-                           "payload_GBs": rdc.payload_bytes / (rms / rn * 1e-3) / 1e9 if rn else None}
-        # C3 decode (R-PLAIN BYTE_ARRAY) on the same upload
-        result["c3_decode"] = _time_decode(ctx, rdc, max(3, args.steps // 2), barrier, dist, local, world)
-        rdc.free()
-
-    # ── C4 (SURVEY §8d): 8 mixed columns, one row group per GPU ───────────────
-    if not args.no_c4:
-        cfile = gen.build(gen.c4_cols(), args.c4_rows, 1, seed=gen.CONFIG_SEEDS["C4"], layout=gen.ARROW_LAYOUT,
-                          first_rg=my_rgs[0])
-        CF = capi.File(cfile)
-        cols, total_ms = {}, 0.0
-        for ci, col in enumerate(gen.c4_cols()):
-            cdc = ctx.upload(cfile, [CF.chunk(0, ci)])
-            r = _time_decode(ctx, cdc, max(3, args.steps // 4), barrier, dist, local, world)
-            cdc.free()
-            cols[col.name] = {"ms": r["ms_per_decode"], "kernels_ms": r["kernel_ms"]}
-            total_ms += r["ms_per_decode"]
-        result["c4"] = {"values_per_s": 8 * args.c4_rows * world / (total_ms * 1e-3), "rows_per_gpu": args.c4_rows,
-                        "ms_per_row_group": total_ms, "columns": cols, "layout": "arrow"}
-        del cfile
-
-    # ── C5 (SURVEY §8d): C2's distribution, arrow layout, one dictionary per
-    #    10M-row row group, decode + dictionary-first regex, row groups per GPU
-    if not args.no_c5:
-        result["c5"] = _c5_leg(ctx, args, barrier, dist, local, world, my_rgs[0])
-
-    # ── CPU baseline beside it (rank 0, N=1 only) ──────────────────────────
-    if rank == 0 and world == 1 and not args.no_cpu:
-        sample = gen.build(gen.c2_cols(), 1_000_000, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
-        SF = capi.File(sample)
-        result["cpu_baseline"] = cpu_baseline(sample, SF.chunk(0, 0), args.cpu_seconds)
-        result["cpu_baseline"]["host_cpu"] = _cpu_model()
-    ctx.close()
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+def expectations():
+    p = os.path.join(ROOT, "tests", "golden", "bench_expect.json")
+    if os.path.exists(p):
+        with open(p) as fh:
+            return json.load(fh)
+    return {}
 
 
-def _time_decode(ctx, dc, steps, barrier, dist, local, world):
-    """Wall time of `steps` decodes of an uploaded chunk (max over ranks) and
-    the per-kernel HIP-event averages."""
-    dc.decode_async()
-    ctx.sync()
-    dc.decode_check()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        dc.decode_async()
-    ctx.sync()
-    t1 = time.perf_counter()
-    barrier()
-    dc.decode_check()
-    el = t1 - t0
-    ctx.timing(True)  # per-kernel events: the same steps again, outside the timed region
-    ctx.timing_reset()
-    for _ in range(steps):
-        dc.decode_async()
-    ctx.sync()
-    ctx.timing(False)
-    dc.decode_check()
-    if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    kern = {}
-    for name in KERNELS + ("plain_spec", "plain_ba", "fixed_plain", "fixed"):
-        ms, n = ctx.timing_get(name)
-        if n:
-            kern[name] = ms / n
-    return {"ms_per_decode": el / steps * 1e3, "values_per_s": dc.num_rows * steps * world / el,
-            "payload_bytes": dc.payload_bytes, "kernel_ms": kern}
-
-
-def _c5_leg(ctx, args, barrier, dist, local, world, rg0):
-    """C5 at --c5-rgs row groups of 10M rows per GPU: every row group is its
-    own chunk (ColumnReader is per chunk; each has its own dictionary page).
-    One step = decode all of them + the regex page filter over all of them
-    (dictionary-first: the pattern runs on each dictionary, then pages are
-    tested through their indices)."""
-    from pqgpu import capi, gen
-    rows = 10_000_000
-    f = gen.build(gen.c2_cols(), rows, args.c5_rgs, seed=gen.CONFIG_SEEDS["C5"], layout=gen.ARROW_LAYOUT,
-                  first_rg=rg0 * args.c5_rgs)
-    F = capi.File(f)
-    dcs = [ctx.upload(f, [F.chunk(rg, 0)]) for rg in range(F.num_row_groups)]
-    del f
-    for dc in dcs:
-        dc.decode()
-        dc.regex_pages(args.pattern)
-    steps = max(2, args.steps // 4)
-
-    def timed(fn, check):
-        fn()
-        ctx.sync()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            fn()
-        ctx.sync()
-        t1 = time.perf_counter()
-        barrier()
-        check()
-        el = t1 - t0
-        ctx.timing(True)  # per-kernel events: the same steps again, outside the timed region
-        ctx.timing_reset()
-        for _ in range(steps):
-            fn()
-        ctx.sync()
-        ctx.timing(False)
-        check()
-        if dist is not None:
-            import torch
-            t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        kern = {}
-        for name in KERNELS + REGEX_KERNELS:
-            ms, n = ctx.timing_get(name)
-            if n:
-                kern[name] = ms / steps  # all launches of one step
-        return el / steps, kern
-
-    def dec():
-        for dc in dcs:
-            dc.decode_async()
-
-    def dec_check():
-        for dc in dcs:
-            dc.decode_check()
-
-    def rx():
-        for dc in dcs:
-            dc.regex_pages_async(args.pattern)
-
-    def rx_check():
-        for dc in dcs:
-            dc.regex_pages_result()
-
-    dsec, dkern = timed(dec, dec_check)
-    rsec, rkern = timed(rx, rx_check)
-    nrows = sum(dc.num_rows for dc in dcs)
-    npages = sum(dc.num_pages for dc in dcs)
-    reported = int(sum(int(dc.regex_pages(args.pattern).sum()) for dc in dcs))
-    for dc in dcs:
-        dc.free()
-    return {"rows_per_gpu": nrows, "row_groups_per_gpu": len(dcs), "pages_per_gpu": npages, "layout": "arrow",
-            "decode_values_per_s": nrows * world / dsec, "decode_ms": dsec * 1e3,
-            "regex_pages_per_s": npages * world / rsec, "regex_ms": rsec * 1e3, "pattern": args.pattern,
-            "reported_pages": reported,
-            "step_values_per_s": nrows * world / (dsec + rsec),
-            "kernel_ms_per_step": {**dkern, **rkern}}
+def cpu_share(args) -> int:
+    if args.cpu_threads > 0:
+        return args.cpu_threads
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
 
 
 def _cpu_model():
@@ -423,6 +237,444 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+# ── CPU baselines (rank 0, N=1; run before anything touches the GPU) ─────
+def _regex_pages_cpu_worker(job):
+    """Oracle decode (C) of a page range + Python `re` per value (the R-REGEX
+    contract): reported flag per page."""
+    import re
+
+    import numpy as np
+    from oracle import oracle as O
+    sub, desc, pattern, first_rows, counts = job
+    rc, msg, col = O.read_all(sub, desc)
+    assert rc == 0, msg
+    valid = np.asarray(col.valid)
+    off = np.asarray(col.offsets)
+    data = bytes(col.data)
+    rx = re.compile(pattern, re.ASCII)
+    flags = []
+    r = 0
+    for n in counts:
+        rep = 1
+        for i in range(r, r + n):
+            if valid[i] and rx.search(data[off[i]:off[i + 1]].decode("utf-8", "surrogateescape")):
+                rep = 0
+                break
+        flags.append(rep)
+        r += n
+    return flags
+
+
+def cpu_baselines(args):
+    from oracle import oracle as O
+    from pqgpu import capi, gen
+    from pqgpu.shard import data_page_ranges, extract_range
+    threads = cpu_share(args)
+    out = {"host_cpu": _cpu_model(), "cores_used": threads,
+           "cores_note": "threads = min(16, sched_getaffinity): the box's CPU share for one GPU"}
+    if not O.have_ref():
+        return None
+    layout = gen.REF_LAYOUT if args.layout == "ref" else gen.ARROW_LAYOUT
+    rows = 1_000_000
+    f = gen.build(gen.c2_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
+    ch = capi.File(f).chunk(0, 0)
+    def ochunk(d):
+        return O.Chunk(d.num_values, d.data_page_offset,
+                       d.dictionary_page_offset if d.has_dictionary_page_offset else None, d.codec, d.type,
+                       d.max_def_level, d.max_rep_level)
+    och = ochunk(ch)
+
+    def reps_for(fn):
+        s, _ = fn(1)
+        return max(1, int(args.cpu_seconds / max(s, 1e-3)))
+
+    one = lambda reps: O.ref_time_read_all(f, och, reps=reps, threads=1)  # noqa: E731
+    reps = reps_for(one)
+    s, nv = one(reps)
+    out["single_thread"] = {"value": nv / s, "unit": "values/s", "cores": 1, "seconds": s,
+                            "sample": f"{reps} x ColumnReader::read_all of a {rows}-row C2 chunk"}
+    chunkp = lambda reps: O.ref_time_read_all(f, och, reps=reps, threads=threads)  # noqa: E731
+    reps = reps_for(chunkp)
+    s, nv = chunkp(reps)
+    out["chunk_parallel"] = {"value": nv / s, "unit": "values/s", "cores": threads, "seconds": s,
+                             "sample": f"{threads} ColumnReaders x {reps} reads of the {rows}-row C2 chunk "
+                                       "(one reader per chunk: the reference API's parallelism)"}
+    rc, msg, table = capi.build_page_table(f, ch)
+    shards = []
+    for a, b in data_page_ranges(table, 4 * threads):
+        sub, d = extract_range(f, ch, table, a, b)
+        shards.append((sub, ochunk(d)))
+    pagep = lambda reps: O.ref_time_read_all_multi(shards, ch.type, ch.max_def_level, ch.max_rep_level,  # noqa: E731
+                                                   reps=reps, threads=threads)
+    reps = reps_for(pagep)
+    s, nv = pagep(reps)
+    out["page_parallel"] = {"value": nv / s, "unit": "values/s", "cores": threads, "seconds": s,
+                            "sample": f"the {rows}-row C2 chunk as {len(shards)} page-range shards "
+                                      f"(dictionary replicated), {threads} threads, {reps} rounds"}
+    # regex: oracle decode + Python re (RE2 is absent on the box), page-parallel processes
+    rrows = 2_000_000
+    rf = gen.build(gen.c3_cols(), rrows, 1, seed=gen.CONFIG_SEEDS["C3"])
+    rch = capi.File(rf).chunk(0, 0)
+    rc, msg, rtable = capi.build_page_table(rf, rch)
+    jobs = []
+    for a, b in data_page_ranges(rtable, 4 * threads):
+        sub, d = extract_range(rf, rch, rtable, a, b)
+        dp = [p for p in rtable if p.page_type == 0][a:b]
+        jobs.append((sub, ochunk(d), args.pattern, [p.first_row for p in dp],
+                     [p.num_values for p in dp]))
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(threads) as pool:
+        t0 = time.perf_counter()
+        flags = sum(pool.map(_regex_pages_cpu_worker, jobs, chunksize=1), [])
+        s = time.perf_counter() - t0
+    out["regex"] = {"value": len(flags) / s, "unit": "pages/s", "cores": threads, "seconds": s, "kind": "port",
+                    "sample": f"C3 {rrows} rows ({len(flags)} pages), pattern {args.pattern!r}: oracle decode "
+                              "+ Python re.search per value, page-range shards on a process pool",
+                    "reported_pages": int(sum(flags))}
+    return out
+
+
+# ── legs ──────────────────────────────────────────────────────────────────
+def c2_leg(J, args, exp):
+    """The headline: rank r decodes data-page range r of one (N x rows)-row C2
+    chunk."""
+    from pqgpu import capi, gen
+    from pqgpu.shard import data_page_ranges
+    layout = gen.REF_LAYOUT if args.layout == "ref" else gen.ARROW_LAYOUT
+    total_rows = args.rows * J.world
+    t0 = time.perf_counter()
+    f = gen.build(gen.c2_cols(), total_rows, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
+    gen_s = time.perf_counter() - t0
+    ch = capi.File(f).chunk(0, 0)
+    t0 = time.perf_counter()
+    rc, msg, table = capi.build_page_table(f, ch)
+    walk_s = time.perf_counter() - t0
+    assert rc == 0, msg
+    ranges = data_page_ranges(table, J.world)
+    a, b = ranges[J.rank]
+    t0 = time.perf_counter()
+    dc = J.ctx.upload_range(f, ch, table, a, b)
+    upload_s = time.perf_counter() - t0
+    dc.decode()
+    nrows = dc.num_rows
+    host = dc.to_host()
+    nonnull = int(host.validity.sum())
+    chars = int(dc.out.num_bytes)
+    valid = None
+    if not args.no_validate:
+        # this shard's rows against the generator's dump of the whole column:
+        # its byte position there from the shards before it (host scan)
+        mine = capi.canonical_dump(host)
+        sizes = J.gather(len(mine))
+        start = sum(sizes[:J.rank])
+        whole = gen.values_dump(gen.c2_cols()[0], 0, total_rows, 0, gen.CONFIG_SEEDS["C2"])
+        ok = whole[start:start + len(mine)] == mine and (J.rank != J.world - 1 or start + len(mine) == len(whole))
+        valid = all(J.gather(bool(ok)))
+        del whole, mine
+    del host
+    secs, kern = J.timed(dc.decode_async, dc.decode_check, args.steps, args.repeats, warmup=args.warmup)
+    rows_all = J.sum_all([nrows])[0]
+    med = statistics.median(secs)
+    res = {"secs": secs, "median_s": med, "value": rows_all * args.steps / med, "nrows": nrows,
+           "rows_all": rows_all, "nonnull": nonnull, "chars": chars, "payload": dc.payload_bytes,
+           "pages": dc.num_pages, "kern": kern, "validated": valid, "page_range": [a, b],
+           "gen_s": gen_s}
+    if not args.no_e2e and J.rank == 0:
+        # end to end from host file bytes: host page walk + image build + H2D
+        # (+ allocation) + one decode, each the median of 3 (SURVEY §8d: reported
+        # separately from the device-resident rate)
+        payload = dc.payload_bytes
+        dc.free()
+        w, u, d = [], [], []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            rc, msg, tb = capi.build_page_table(f, ch)
+            t1 = time.perf_counter()
+            x = J.ctx.upload_range(f, ch, tb, a, b)
+            t2 = time.perf_counter()
+            x.decode()
+            t3 = time.perf_counter()
+            x.free()
+            w.append(t1 - t0), u.append(t2 - t1), d.append(t3 - t2)
+        wm, um, dm = statistics.median(w), statistics.median(u), statistics.median(d)
+        res["e2e"] = {"walk_ms": wm * 1e3, "upload_ms": um * 1e3, "first_decode_ms": dm * 1e3,
+                      "total_ms": (wm + um + dm) * 1e3, "values_per_s": nrows / (wm + um + dm),
+                      "file_bytes": len(f), "upload_GBs": payload / um / 1e9 if um else None,
+                      "note": "walk = pq_build_page_table of the whole chunk (host); upload = image build + "
+                              "device allocation + H2D + sync; first_decode includes output allocation"}
+    else:
+        dc.free()
+    res["walk_s"] = walk_s
+    res["upload_s"] = upload_s
+    del f
+    return res
+
+
+def strong_leg(J, args):
+    """Strong scaling: the 10M-row C2 chunk split into N page ranges."""
+    from pqgpu import capi, gen
+    from pqgpu.shard import data_page_ranges
+    layout = gen.REF_LAYOUT if args.layout == "ref" else gen.ARROW_LAYOUT
+    f = gen.build(gen.c2_cols(), args.rows, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
+    ch = capi.File(f).chunk(0, 0)
+    rc, msg, table = capi.build_page_table(f, ch)
+    a, b = data_page_ranges(table, J.world)[J.rank]
+    dc = J.ctx.upload_range(f, ch, table, a, b)
+    dc.decode()
+    secs, kern = J.timed(dc.decode_async, dc.decode_check, args.steps, args.repeats, warmup=args.warmup)
+    dc.free()
+    med = statistics.median(secs)
+    return {"rows_total": args.rows, "ms_per_step": med / args.steps * 1e3,
+            "values_per_s": args.rows * args.steps / med, "scaling": "strong"}
+
+
+def c3_legs(J, args, exp):
+    from pqgpu import capi, gen
+    rows = args.regex_rows
+    rfile = gen.build(gen.c3_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C3"], first_rg=J.rank)
+    RF = capi.File(rfile)
+    rch = RF.chunk(0, 0)
+    rdc = J.ctx.upload(rfile, [rch])
+    flags = rdc.regex_pages(args.pattern)
+    rsteps = max(3, args.steps // 2)
+    step = lambda: rdc.regex_pages_async(args.pattern)  # noqa: E731
+    secs, kern = J.timed(step, rdc.regex_pages_result, rsteps, args.repeats, warmup=max(1, args.warmup // 2),
+                         kernels=REGEX_KERNELS)
+    med = statistics.median(secs)
+    npages = rdc.num_pages
+    rkern = next((k for k in ("regex_plain", "regex_lanes", "regex_pages") if k in kern), None)
+    kms = kern[rkern]["ms_per_launch"] if rkern else None
+    e = exp.get(f"c3|{rows}|{args.pattern}") if J.rank == 0 else None
+    regex = {"pages_per_s": npages * rsteps * J.world / med, "pages_per_gpu": npages,
+             "ms_per_scan": med / rsteps * 1e3, "repeats_ms": [s / rsteps * 1e3 for s in secs],
+             "pattern": args.pattern, "reported_pages": int(flags.sum()),
+             "validated": (sha(flags.astype("u1").tobytes()) == e["sha256"]) if e else None,
+             "kernel": rkern, "kernel_ms": kms,
+             "payload_GBs": rdc.payload_bytes / (kms * 1e-3) / 1e9 if kms else None,
+             "roofline_frac": rdc.payload_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS if kms else None}
+    if not args.no_e2e and J.rank == 0:
+        w, u, r = [], [], []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            rc, msg, tb = capi.build_page_table(rfile, rch)
+            t1 = time.perf_counter()
+            x = J.ctx.upload(rfile, [rch])
+            t2 = time.perf_counter()
+            x.regex_pages(args.pattern)
+            t3 = time.perf_counter()
+            x.free()
+            w.append(t1 - t0), u.append(t2 - t1), r.append(t3 - t2)
+        wm, um, rm = statistics.median(w), statistics.median(u), statistics.median(r)
+        regex["e2e"] = {"walk_ms": wm * 1e3, "upload_ms": um * 1e3, "first_scan_ms": rm * 1e3,
+                        "total_ms": (wm + um + rm) * 1e3, "pages_per_s": npages / (wm + um + rm),
+                        "note": "upload includes its own page walk (pq_chunk_upload walks the chunk); walk_ms "
+                                "is that walk alone; first_scan includes the pattern compile"}
+    # C3 PLAIN decode on the same upload
+    dsteps = max(3, args.steps // 2)
+    rdc.decode()
+    ok = None
+    if not args.no_validate:
+        ok = sha(capi.canonical_dump(rdc.to_host())) == sha(
+            gen.values_dump(gen.c3_cols()[0], 0, rows, J.rank, gen.CONFIG_SEEDS["C3"]))
+    secs, dkern = J.timed(rdc.decode_async, rdc.decode_check, dsteps, args.repeats, warmup=2)
+    med = statistics.median(secs)
+    c3d = {"ms_per_decode": med / dsteps * 1e3, "values_per_s": rows * dsteps * J.world / med,
+           "payload_bytes": rdc.payload_bytes, "kernel_ms": {k: v["ms_per_step"] for k, v in dkern.items()},
+           "validated": ok}
+    rdc.free()
+    return regex, c3d
+
+
+def c4_leg(J, args):
+    from pqgpu import capi, gen
+    rows = args.c4_rows
+    cols = gen.c4_cols()
+    cfile = gen.build(cols, rows, 1, seed=gen.CONFIG_SEEDS["C4"], layout=gen.ARROW_LAYOUT, first_rg=J.rank)
+    CF = capi.File(cfile)
+    out, total_ms, ok = {}, 0.0, True
+    steps = max(3, args.steps // 4)
+    for ci, col in enumerate(cols):
+        cdc = J.ctx.upload(cfile, [CF.chunk(0, ci)])
+        cdc.decode()
+        if not args.no_validate:
+            ok &= sha(capi.canonical_dump(cdc.to_host())) == sha(
+                gen.values_dump(col, ci, rows, J.rank, gen.CONFIG_SEEDS["C4"]))
+        secs, kern = J.timed(cdc.decode_async, cdc.decode_check, steps, args.repeats, warmup=2)
+        cdc.free()
+        ms = statistics.median(secs) / steps * 1e3
+        out[col.name] = {"ms": ms, "kernels_ms": {k: v["ms_per_step"] for k, v in kern.items()}}
+        total_ms += ms
+    return {"values_per_s": 8 * rows * J.world / (total_ms * 1e-3), "rows_per_gpu": rows,
+            "ms_per_row_group": total_ms, "columns": out, "layout": "arrow",
+            "validated": None if args.no_validate else all(J.gather(bool(ok)))}
+
+
+def c5_leg(J, args, exp):
+    """C5 at --c5-rgs row groups of 10M rows per GPU: every row group is its
+    own chunk (ColumnReader is per chunk; each has its own dictionary page).
+    Decode all of them, then the regex page filter over all of them
+    (dictionary-first: the pattern runs on each dictionary, then pages are
+    tested through the decode's codes)."""
+    from pqgpu import capi, gen
+    import numpy as np
+    rows = 10_000_000
+    rg0 = J.rank * args.c5_rgs
+    f = gen.build(gen.c2_cols(), rows, args.c5_rgs, seed=gen.CONFIG_SEEDS["C5"], layout=gen.ARROW_LAYOUT,
+                  first_rg=rg0)
+    F = capi.File(f)
+    dcs = [J.ctx.upload(f, [F.chunk(rg, 0)]) for rg in range(F.num_row_groups)]
+    del f
+    ok = True
+    for i, dc in enumerate(dcs):
+        dc.decode()
+        if not args.no_validate:
+            ok &= sha(capi.canonical_dump(dc.to_host())) == sha(
+                gen.values_dump(gen.c2_cols()[0], 0, rows, rg0 + i, gen.CONFIG_SEEDS["C5"]))
+        dc.regex_pages(args.c5_pattern)
+    steps = max(2, args.steps // 4)
+
+    def dec():
+        for dc in dcs:
+            dc.decode_async()
+
+    def dec_check():
+        for dc in dcs:
+            dc.decode_check()
+
+    def rx():
+        for dc in dcs:
+            dc.regex_pages_async(args.c5_pattern)
+
+    def rx_check():
+        for dc in dcs:
+            dc.regex_pages_result()
+
+    dsecs, dkern = J.timed(dec, dec_check, steps, args.repeats, warmup=1)
+    rsecs, rkern = J.timed(rx, rx_check, steps, args.repeats, warmup=1, kernels=KERNELS + REGEX_KERNELS)
+    dsec = statistics.median(dsecs) / steps
+    rsec = statistics.median(rsecs) / steps
+    nrows = sum(dc.num_rows for dc in dcs)
+    npages = sum(dc.num_pages for dc in dcs)
+    flags = np.concatenate([dc.regex_pages(args.c5_pattern) for dc in dcs])
+    e = exp.get(f"c5|{rows}x{args.c5_rgs}|{args.c5_pattern}") if J.rank == 0 else None
+    for dc in dcs:
+        dc.free()
+    return {"rows_per_gpu": nrows, "row_groups_per_gpu": len(dcs), "pages_per_gpu": npages, "layout": "arrow",
+            "decode_values_per_s": nrows * J.world / dsec, "decode_ms": dsec * 1e3,
+            "regex_pages_per_s": npages * J.world / rsec, "regex_ms": rsec * 1e3, "pattern": args.c5_pattern,
+            "reported_pages": int(flags.sum()),
+            "regex_validated": (sha(flags.astype("u1").tobytes()) == e["sha256"]) if e else None,
+            "decode_validated": None if args.no_validate else all(J.gather(bool(ok))),
+            "step_values_per_s": nrows * J.world / (dsec + rsec),
+            "kernel_ms_per_step": {**{k: v["ms_per_step"] for k, v in dkern.items()},
+                                   **{k: v["ms_per_step"] for k, v in rkern.items()}}}
+
+
+def main():
+    args = parse()
+    maybe_spawn(args)
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and rank == 0:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    if args.cpu_only:  # child of the bench process: CPU baselines only, no GPU
+        print(json.dumps(cpu_baselines(args)), flush=True)
+        return
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # in a fresh child interpreter, started before this process touches
+        # the GPU (its own process pool forks; nothing GPU-side is shared)
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-only"] + sys.argv[1:],
+                           stdout=subprocess.PIPE, check=True)
+        cpu = json.loads(r.stdout.decode().strip().splitlines()[-1])
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    from pqgpu import capi
+    ctx = capi.Context(local)
+    J = Job(rank, world, local, dist, ctx)
+    exp = expectations()
+
+    c2 = c2_leg(J, args, exp)
+    nrows = c2["nrows"]
+    med = c2["median_s"]
+    ms_per_step = med / args.steps * 1e3
+    kern = {k: v["ms_per_launch"] for k, v in c2["kern"].items()}
+    total_chars = c2["chars"]
+    payload = c2["payload"]
+    out_bytes = 8 * (nrows + 1) + total_chars + (nrows + 7) // 8
+    b_alg = payload + out_bytes  # SURVEY §8d C2 algorithmic bytes per decode
+    dom = max(kern, key=kern.get) if kern else "pipe_write"
+    dom_ms = kern.get(dom, ms_per_step)
+    # algorithmic bytes of one launch of the dominant kernel (DESIGN.md §4):
+    # pipe_write reads the u16 codes and writes the column (offsets, chars, validity)
+    dom_bytes = {"pipe_write": out_bytes + 2 * nrows, "pipe_codes": payload + 2 * nrows,
+                 "ba_fused": b_alg}.get(dom, payload)
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic(args.pmc_json, dom)
+
+    result = {
+        "metric": "decoded values/sec (RLE+dict BYTE_ARRAY) and regex pages/sec at 1/2/4/8 GPUs",
+        "value": c2["value"],
+        "unit": "values/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (deterministic splitmix64 generator, SURVEY §8d C2 shape)",
+        "config": {"workload": f"C2: dict BYTE_ARRAY OPTIONAL, {args.rows} rows/GPU as page-range shards of one "
+                               f"{args.rows * world}-row chunk, {args.layout}-layout, 1000-entry dict, 5% NULL",
+                   "rows_per_gpu": nrows, "pages_per_gpu": c2["pages"], "page_range_rank0": c2["page_range"],
+                   "parallelism": f"page-range shards x{world} (no collective)"},
+        "timing": {"repeats_ms_per_step": [s / args.steps * 1e3 for s in c2["secs"]],
+                   "statistic": f"median of {args.repeats} regions of {args.steps} steps, max over ranks"},
+        "validated": c2["validated"],
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                     "kernel": dom, "kernel_ms": dom_ms, "algorithmic_bytes": dom_bytes},
+        "pipeline": {"kernel_ms": kern,
+                     "kernel_ms_note": "HIP events on the decode streams, same steps repeated after the timed "
+                                       "regions (events perturb the wall clock)",
+                     "sum_kernel_ms": sum(kern.values()),
+                     "b_alg_bytes": b_alg, "b_alg_GBs_per_step": b_alg / (ms_per_step * 1e-3) / 1e9,
+                     "b_alg_frac_of_peak": b_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "nonnull": c2["nonnull"], "chars": total_chars},
+    }
+    if "e2e" in c2:
+        result["end_to_end"] = {"c2": c2["e2e"]}
+    if world > 1:
+        result["strong"] = strong_leg(J, args)
+
+    if not args.no_regex:
+        result["regex"], result["c3_decode"] = c3_legs(J, args, exp)
+        if "e2e" in result["regex"]:
+            result.setdefault("end_to_end", {})["c3_regex"] = result["regex"].pop("e2e")
+    if not args.no_c4:
+        result["c4"] = c4_leg(J, args)
+    if not args.no_c5:
+        result["c5"] = c5_leg(J, args, exp)
+    if cpu is not None:
+        st = cpu["single_thread"]
+        result["cpu_baseline"] = {"value": st["value"], "unit": "values/s", "cores": 1, "kind": "reference",
+                                  "sample": st["sample"] + " (the reference's own ColumnReader, oracle/_ref, -O2)",
+                                  **{k: v for k, v in cpu.items() if k != "single_thread"}}
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

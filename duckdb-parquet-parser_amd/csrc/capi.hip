@@ -65,6 +65,7 @@ struct pq_chunk {
     int16_t max_def = 0, max_rep = 0;
     int32_t width = 0, plain_width = 0;
     int64_t nrows = 0;
+    int64_t row_offset = 0;             // page-range uploads: global row of the first data page
     int64_t payload_bytes = 0;
     std::vector<pq_page_desc> walked;   // every walked page, all chunks, global rows
     std::vector<int64_t> page_seq;      // walk sequence of each device data page
@@ -620,18 +621,20 @@ int pq_build_page_table(const uint8_t* file, size_t file_len, const pq_chunk_des
     }
 }
 
-int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc* chunks,
-                    int nchunks, pq_chunk** out) {
-    if (!ctx || !file || !chunks || nchunks <= 0 || !out) return PQ_ERR_ARG;
-    *out = nullptr;
+// Builds the device chunk from page walks already made on the host: one walk
+// per input chunk (pq_chunk_upload) or one page-range walk (pq_chunk_upload_range).
+static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc& desc,
+                         std::vector<pqfmt::WalkResult>& walks, int64_t row_offset, pq_chunk** out) {
+    const int nchunks = static_cast<int>(walks.size());
     try {
         (void)hipSetDevice(ctx->device);
         auto c = std::make_unique<pq_chunk>();
-        c->type = chunks[0].type;
-        c->max_def = chunks[0].max_def_level;
-        c->max_rep = chunks[0].max_rep_level;
+        c->type = desc.type;
+        c->max_def = desc.max_def_level;
+        c->max_rep = desc.max_rep_level;
         c->plain_width = plain_width_of(c->type);
         c->width = c->plain_width;
+        c->row_offset = row_offset;
 
         // 1) host walks; every payload gets a 16-byte aligned slot in one image
         std::vector<DevPage> hpages;
@@ -646,9 +649,6 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
             img += (static_cast<int64_t>(size) + 15) / 16 * 16 + 16;
             return at;
         };
-        // the chunks' page walks are independent: host threads (SURVEY §8f rank 1)
-        std::vector<pqfmt::WalkResult> walks(static_cast<size_t>(nchunks));
-        parallel_for(nchunks, [&](int k) { walks[static_cast<size_t>(k)] = pqfmt::walk_chunk(file, file_len, chunks[k]); });
         for (int k = 0; k < nchunks; k++) {
             pqfmt::WalkResult& w = walks[static_cast<size_t>(k)];
             int64_t base_walk = static_cast<int64_t>(c->walked.size());
@@ -871,6 +871,68 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
     }
 }
 
+int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc* chunks,
+                    int nchunks, pq_chunk** out) {
+    if (!ctx || !file || !chunks || nchunks <= 0 || !out) return PQ_ERR_ARG;
+    *out = nullptr;
+    try {
+        // the chunks' page walks are independent: host threads (SURVEY §8f rank 1)
+        std::vector<pqfmt::WalkResult> walks(static_cast<size_t>(nchunks));
+        parallel_for(nchunks, [&](int k) { walks[static_cast<size_t>(k)] = pqfmt::walk_chunk(file, file_len, chunks[k]); });
+        return upload_walked(ctx, file, file_len, chunks[0], walks, 0, out);
+    } catch (const std::exception& e) {
+        return set_err(ctx, PQ_ERR_ALLOC, e.what());
+    }
+}
+
+int pq_chunk_upload_range(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc* chunk,
+                          const pq_page_desc* table, int64_t ntable, int64_t data_begin, int64_t data_end,
+                          pq_chunk** out) {
+    if (!ctx || !file || !chunk || (!table && ntable) || ntable < 0 || !out || data_begin < 0 ||
+        data_end < data_begin)
+        return PQ_ERR_ARG;
+    *out = nullptr;
+    try {
+        // the data pages of the range, in walk order, and the dictionary pages they use
+        std::vector<int64_t> data_idx;
+        int64_t k = 0, row0 = -1, rows_before = 0;  // row0: chunk row of data page `data_begin`
+        for (int64_t i = 0; i < ntable; i++) {
+            if (table[i].page_type != PQ_DATA_PAGE) continue;
+            if (k == data_begin) row0 = table[i].first_row;
+            if (k >= data_begin && k < data_end) data_idx.push_back(i);
+            rows_before = table[i].first_row + table[i].num_values;
+            k++;
+        }
+        if (row0 < 0) row0 = rows_before;  // empty range at the end
+        if (data_end > k) return set_err(ctx, PQ_ERR_ARG, "page range past the chunk's data pages");
+        std::vector<int32_t> remap(static_cast<size_t>(ntable), -1);
+        pqfmt::WalkResult w;
+        for (int64_t i : data_idx) {
+            const int32_t d = table[i].dict_page;
+            if (d < 0) continue;
+            if (d >= ntable || d >= i || table[d].page_type != PQ_DICTIONARY_PAGE)
+                return set_err(ctx, PQ_ERR_ARG, "page table: bad dictionary page index");
+            remap[static_cast<size_t>(d)] = 0;
+        }
+        for (int64_t i = 0; i < ntable; i++)  // dictionary pages first, in walk order
+            if (remap[static_cast<size_t>(i)] == 0) {
+                remap[static_cast<size_t>(i)] = static_cast<int32_t>(w.pages.size());
+                w.pages.push_back(table[i]);
+            }
+        for (int64_t i : data_idx) {
+            pq_page_desc p = table[i];
+            p.first_row -= row0;
+            if (p.dict_page >= 0) p.dict_page = remap[static_cast<size_t>(p.dict_page)];
+            w.pages.push_back(p);
+        }
+        std::vector<pqfmt::WalkResult> walks(1);
+        walks[0] = std::move(w);
+        return upload_walked(ctx, file, file_len, *chunk, walks, row0, out);
+    } catch (const std::exception& e) {
+        return set_err(ctx, PQ_ERR_ALLOC, e.what());
+    }
+}
+
 void pq_chunk_free(pq_ctx* ctx, pq_chunk* c) {
     if (!c) return;
     if (ctx) (void)hipStreamSynchronize(ctx->stream);
@@ -879,6 +941,7 @@ void pq_chunk_free(pq_ctx* ctx, pq_chunk* c) {
 }
 
 int64_t pq_chunk_num_rows(const pq_chunk* c) { return c ? c->nrows : 0; }
+int64_t pq_chunk_first_row(const pq_chunk* c) { return c ? c->row_offset : 0; }
 int64_t pq_chunk_num_pages(const pq_chunk* c) { return c ? c->npages : 0; }
 int64_t pq_chunk_payload_bytes(const pq_chunk* c) { return c ? c->payload_bytes : 0; }
 int pq_chunk_pages(const pq_chunk* c, pq_page_desc* pages, int64_t cap, int64_t* npages) {

@@ -89,7 +89,10 @@ def lib():
                                      C.c_int64, C.POINTER(C.c_int64), C.c_char_p, C.c_size_t], C.c_int),
             "pq_chunk_upload": ([vp, u8p, C.c_size_t, C.POINTER(ChunkDesc), C.c_int,
                                  C.POINTER(vp)], C.c_int),
+            "pq_chunk_upload_range": ([vp, u8p, C.c_size_t, C.POINTER(ChunkDesc), C.POINTER(PageDesc),
+                                       C.c_int64, C.c_int64, C.c_int64, C.POINTER(vp)], C.c_int),
             "pq_chunk_free": ([vp, vp], None),
+            "pq_chunk_first_row": ([vp], C.c_int64),
             "pq_chunk_num_rows": ([vp], C.c_int64),
             "pq_chunk_num_pages": ([vp], C.c_int64),
             "pq_chunk_payload_bytes": ([vp], C.c_int64),
@@ -140,13 +143,23 @@ def _buf(b: bytes):
 
 
 # ── host page walk ─────────────────────────────────────────────────────────
-def build_page_table(file: bytes, chunk: ChunkDesc, cap: int = 1 << 20):
-    pages = (PageDesc * cap)()
-    n = C.c_int64()
-    err = C.create_string_buffer(512)
-    rc = lib().pq_build_page_table(_buf(file), len(file), C.byref(chunk), pages, cap, C.byref(n),
-                                   err, 512)
-    return rc, err.value.decode(errors="replace"), [pages[i] for i in range(min(n.value, cap))]
+def build_page_table(file: bytes, chunk: ChunkDesc, cap: int = 0):
+    """(status, message, pages): the walk's pages as a ctypes PageDesc array
+    (indexable, iterable; pass it back to Context.upload_range as is)."""
+    if cap <= 0:  # a page is >= ~16 bytes of header + payload
+        cap = max(64, min(len(file) // 16 + 64, 1 << 20))
+    while True:
+        pages = (PageDesc * cap)()
+        n = C.c_int64()
+        err = C.create_string_buffer(512)
+        rc = lib().pq_build_page_table(_buf(file), len(file), C.byref(chunk), pages, cap, C.byref(n),
+                                       err, 512)
+        if n.value <= cap:
+            break
+        cap = n.value
+    exact = (PageDesc * n.value)()
+    C.memmove(exact, pages, C.sizeof(PageDesc) * n.value)
+    return rc, err.value.decode(errors="replace"), exact
 
 
 # ── file metadata (ParquetReader::open) ────────────────────────────────────
@@ -250,6 +263,15 @@ class Context:
         self.check(lib().pq_chunk_upload(self.h, _buf(file), len(file), arr, len(chunks), C.byref(h)))
         return DeviceChunk(self, h)
 
+    def upload_range(self, file: bytes, chunk: ChunkDesc, table, data_begin: int, data_end: int) -> "DeviceChunk":
+        """Data pages [data_begin, data_end) of one chunk (+ their dictionary
+        pages) from its page table (build_page_table): a page-range shard."""
+        arr = table if isinstance(table, C.Array) else (PageDesc * max(len(table), 1))(*table)
+        h = vp()
+        self.check(lib().pq_chunk_upload_range(self.h, _buf(file), len(file), C.byref(chunk), arr, len(table),
+                                               data_begin, data_end, C.byref(h)))
+        return DeviceChunk(self, h)
+
     def timing(self, on: bool = True):
         lib().pq_timing_enable(self.h, int(on))
 
@@ -303,6 +325,10 @@ class DeviceChunk:
     @property
     def num_pages(self) -> int:
         return lib().pq_chunk_num_pages(self.h)
+
+    @property
+    def first_row(self) -> int:
+        return lib().pq_chunk_first_row(self.h)
 
     @property
     def payload_bytes(self) -> int:

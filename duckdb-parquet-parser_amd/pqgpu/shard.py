@@ -41,3 +41,86 @@ def shard_row_offsets(rows_per_shard) -> np.ndarray:
     """Global first row of each shard (host exclusive scan, no collective)."""
     r = np.asarray(rows_per_shard, dtype=np.int64)
     return np.concatenate([[0], np.cumsum(r)[:-1]]) if len(r) else r
+
+
+def data_page_ranges(table, world: int) -> list[tuple[int, int]]:
+    """Byte-balanced contiguous ranges of a chunk's DATA pages (ordinals in walk
+    order, the unit pq_chunk_upload_range takes) from its page table
+    (capi.build_page_table).  Dictionary pages are not counted: every shard
+    that needs one gets it replicated."""
+    sizes = [p.payload_size for p in table if p.page_type == 0]
+    return page_ranges(sizes, world)
+
+
+def range_rows(table, begin: int, end: int) -> tuple[int, int]:
+    """(first chunk row, row count) of data pages [begin, end)."""
+    data = [p for p in table if p.page_type == 0]
+    if begin >= end:
+        first = data[begin].first_row if begin < len(data) else sum(p.num_values for p in data)
+        return first, 0
+    return data[begin].first_row, sum(p.num_values for p in data[begin:end])
+
+
+def extract_range(file: bytes, chunk, table, begin: int, end: int):
+    """The bytes one shard needs, as a standalone column chunk: the header and
+    payload of data pages [begin, end) and of every dictionary page they use,
+    in walk order, plus a chunk descriptor that walks exactly those pages.
+    (What a rank reads from storage for its range; the tests decode it with
+    the oracle to check a shard plan without a GPU.)  Returns (bytes, desc)."""
+    from .capi import ChunkDesc
+    data_pos = [i for i, p in enumerate(table) if p.page_type == 0]
+    pick = set(data_pos[begin:end])
+    dicts = {table[i].dict_page for i in pick if table[i].dict_page >= 0}
+    out = bytearray()
+    first_data = None
+    nvals = 0
+    for i, p in enumerate(table):
+        if i not in pick and i not in dicts:
+            continue
+        if i in pick and first_data is None:
+            first_data = len(out)
+        lo, hi = p.header_offset, p.payload_offset + p.payload_size
+        piece = file[lo:min(hi, len(file))]
+        out += piece + bytes(hi - lo - len(piece))
+        if i in pick:
+            nvals += p.num_values
+    d = ChunkDesc()
+    d.num_values = nvals
+    d.data_page_offset = first_data if first_data is not None else len(out)
+    d.dictionary_page_offset = 0
+    d.has_dictionary_page_offset = 1 if dicts else 0
+    d.codec = chunk.codec
+    d.type = chunk.type
+    d.max_def_level = chunk.max_def_level
+    d.max_rep_level = chunk.max_rep_level
+    return bytes(out), d
+
+
+def column_page_shards(page_index, col: int, world: int) -> list[list[tuple[int, int, int]]]:
+    """Global data-page sharding of one column across row groups (R-PAGEIDX
+    order, build_page_index parquet_reader.cpp:559-605): the column's pages
+    split into `world` contiguous byte-balanced ranges; each rank's range as
+    pieces (row_group, first data page, end data page) with page ordinals
+    local to that row group's chunk (what pq_chunk_upload_range takes).
+    `page_index` is File.page_index(): rows (data_offset, data_size, rg, col)."""
+    pi = np.asarray(page_index, dtype=np.int64).reshape(-1, 4)
+    mine = pi[pi[:, 3] == col]
+    rgs = mine[:, 2]
+    # ordinal of every page inside its row group's chunk
+    local = np.zeros(len(mine), dtype=np.int64)
+    for rg in np.unique(rgs):
+        sel = np.nonzero(rgs == rg)[0]
+        local[sel] = np.arange(len(sel))
+    out = []
+    for a, b in page_ranges(mine[:, 1], world):
+        pieces = []
+        i = a
+        while i < b:
+            rg = int(rgs[i])
+            j = i
+            while j < b and rgs[j] == rg:
+                j += 1
+            pieces.append((rg, int(local[i]), int(local[j - 1]) + 1))
+            i = j
+        out.append(pieces)
+    return out

@@ -146,8 +146,22 @@ int pq_build_page_table(const uint8_t* file, size_t file_len, const pq_chunk_des
  * (ParquetReader::read_column concatenation, parquet_reader.cpp:133-144). */
 int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc* chunks,
                     int nchunks, pq_chunk** out);
+/* Page-range shard (the decode-a-page-list entry point; §8e):
+ * uploads data pages [data_begin, data_end) of ONE chunk — ordinals among the
+ * chunk's data pages in walk order — plus every dictionary page they use,
+ * taken from `table`, the chunk's page table as pq_build_page_table returned
+ * it (no re-walk).  Pages decode independently given their dictionary
+ * (column_reader.cpp:140-225), so a shard's decode equals rows
+ * [first_row, first_row + num_rows) of the whole chunk's decode; the unit of
+ * sharding is the global data-page id of build_page_index
+ * (parquet_reader.cpp:559-605).  Output rows start at 0; pq_chunk_first_row
+ * gives the chunk row of the shard's first row. */
+int pq_chunk_upload_range(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc* chunk,
+                          const pq_page_desc* table, int64_t ntable, int64_t data_begin,
+                          int64_t data_end, pq_chunk** out);
 void pq_chunk_free(pq_ctx* ctx, pq_chunk* chunk);
 int64_t pq_chunk_num_rows(const pq_chunk* chunk);
+int64_t pq_chunk_first_row(const pq_chunk* chunk);     /* 0 unless a page-range upload */
 int64_t pq_chunk_num_pages(const pq_chunk* chunk);       /* data pages */
 int64_t pq_chunk_payload_bytes(const pq_chunk* chunk);   /* Σ data + dictionary payload bytes */
 int pq_chunk_pages(const pq_chunk* chunk, pq_page_desc* pages, int64_t cap, int64_t* npages);

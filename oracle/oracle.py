@@ -125,6 +125,10 @@ def ref():
         L.pqref_time_read_all.argtypes = [u8p, C.c_size_t, C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                           C.c_int32, C.c_int16, C.c_int16, C.c_int, C.c_int, i64p]
         L.pqref_time_read_all.restype = C.c_double
+        L.pqref_time_read_all_multi.argtypes = [C.c_int, C.POINTER(u8p), C.POINTER(C.c_size_t), i64p, i64p, i64p,
+                                                C.POINTER(C.c_int32), C.c_int32, C.c_int16, C.c_int16, C.c_int,
+                                                C.c_int, i64p]
+        L.pqref_time_read_all_multi.restype = C.c_double
         L.pqref_free.argtypes = [C.c_void_p]
         _ref = L
     return _ref
@@ -299,3 +303,21 @@ def ref_time_read_all(file: bytes, ch: Chunk, reps: int = 1, threads: int = 1):
                               d if d is not None else 0, 1 if d is not None else 0, ch.type,
                               ch.max_def, ch.max_rep, reps, threads, C.byref(nv))
     return s, nv.value
+
+
+def ref_time_read_all_multi(shards, ptype: int, max_def: int, max_rep: int, reps: int = 1, threads: int = 1):
+    """Wall seconds for `reps` rounds of ColumnReader::read_all over every
+    (file bytes, Chunk) shard, on `threads` readers (page-parallel baseline)."""
+    R = ref()
+    n = len(shards)
+    keep = [C.create_string_buffer(f, len(f) or 1) for f, _ in shards]
+    files = (u8p * n)(*[C.cast(k, u8p) for k in keep])
+    lens = (C.c_size_t * n)(*[len(f) for f, _ in shards])
+    nv = (C.c_int64 * n)(*[c.num_values for _, c in shards])
+    do = (C.c_int64 * n)(*[c.data_page_offset for _, c in shards])
+    dd = (C.c_int64 * n)(*[c.dictionary_page_offset or 0 for _, c in shards])
+    hd = (C.c_int32 * n)(*[1 if c.dictionary_page_offset is not None else 0 for _, c in shards])
+    out = C.c_int64()
+    s = R.pqref_time_read_all_multi(n, files, lens, nv, do, dd, hd, ptype, max_def, max_rep, reps, threads,
+                                    C.byref(out))
+    return s, out.value

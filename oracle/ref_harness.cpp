@@ -15,6 +15,7 @@
 #include "reader/parquet_reader.hpp"
 #include "writer/parquet_writer.hpp"
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -271,6 +272,41 @@ double pqref_time_read_all(const uint8_t* file, size_t flen, int64_t num_values,
         ts.emplace_back([&, t] {
             for (int r = 0; r < reps; r++) {
                 ColumnReader rd(memory_range(file, flen), cc, static_cast<ParquetType>(type),
+                                max_def, max_rep);
+                counts[t] += static_cast<int64_t>(rd.read_all().size());
+            }
+        });
+    }
+    for (auto& th : ts) th.join();
+    double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    int64_t tot = 0;
+    for (auto c : counts) tot += c;
+    if (values_out) *values_out = tot;
+    return s;
+}
+
+// Page-parallel baseline: `n` independent sub-chunks (each a shard's pages
+// extracted as a standalone chunk, pqgpu/shard.py extract_range), read by
+// `threads` ColumnReaders that take shards from a shared counter, `reps`
+// rounds.  Same reference ColumnReader::read_all per shard.
+double pqref_time_read_all_multi(int n, const uint8_t* const* files, const size_t* flens,
+                                 const int64_t* num_values, const int64_t* data_off,
+                                 const int64_t* dict_off, const int32_t* has_dict, int32_t type,
+                                 int16_t max_def, int16_t max_rep, int reps, int threads,
+                                 int64_t* values_out) {
+    std::vector<ColumnChunk> ccs;
+    for (int i = 0; i < n; i++)
+        ccs.push_back(make_chunk(num_values[i], data_off[i], dict_off[i], has_dict[i], 0, type));
+    std::vector<int64_t> counts(threads, 0);
+    std::atomic<int64_t> next{0};
+    const int64_t total = static_cast<int64_t>(n) * reps;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; t++) {
+        ts.emplace_back([&, t] {
+            for (int64_t k = next.fetch_add(1); k < total; k = next.fetch_add(1)) {
+                const int i = static_cast<int>(k % n);
+                ColumnReader rd(memory_range(files[i], flens[i]), ccs[i], static_cast<ParquetType>(type),
                                 max_def, max_rep);
                 counts[t] += static_cast<int64_t>(rd.read_all().size());
             }

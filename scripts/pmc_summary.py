@@ -38,7 +38,10 @@ def counters(pattern):
 def main():
     d = sys.argv[1]
     out = sys.argv[2] if len(sys.argv) > 2 else None
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_source_hash
     res = {"source": os.path.basename(os.path.normpath(d)), "kernels": {},
+           "kernel_src_sha": kernel_source_hash(),
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 wide-read halving); WRITE_SIZE KiB x1024"}
     stats = glob.glob(os.path.join(d, "prof_kt", "*kernel_stats.csv"))
     if stats:

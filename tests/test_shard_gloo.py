@@ -1,9 +1,15 @@
-"""CPU: the multi-GPU sharding plan with world_size-2 gloo.
+"""CPU: the multi-GPU shard plan, single process and with
+world_size-2 gloo.
 
-Shards are contiguous page ranges / row-group blocks with no collective on
-the data path; the only exchange is the host-side gather of per-shard
-results.  The union of shard results must equal the 1-GPU (here: oracle)
-result, byte for byte and in order.
+Shards are contiguous, byte-balanced ranges of a chunk's data pages (the
+product's page table from pq_build_page_table → shard.data_page_ranges), each
+decoded independently given the chunk's dictionary
+(/root/reference/src/reader/column_reader.cpp:140-225), with no collective on
+the data path; row offsets are a host exclusive scan.  Without a GPU the
+shard's bytes (shard.extract_range: its data pages + the dictionary pages
+they use) are decoded by the oracle (the checker); the -m gpu twin in
+test_gpu_shard.py decodes the same ranges with pq_chunk_upload_range.  The
+concatenation of shard dumps must equal the unsharded dump byte for byte.
 """
 import hashlib
 import os
@@ -14,8 +20,9 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pqgpu import gen
-from pqgpu.shard import page_ranges, rank_row_groups, shard_row_offsets
+from pqgpu import capi, gen
+from pqgpu.shard import (data_page_ranges, extract_range, page_ranges, range_rows, rank_row_groups,
+                         shard_row_offsets)
 
 
 def test_page_ranges_cover_and_balance():
@@ -47,6 +54,50 @@ def test_shard_row_offsets():
     assert shard_row_offsets([3, 0, 5]).tolist() == [0, 3, 3]
 
 
+def _cases():
+    """(name, file, chunk) — C2 ref/arrow layout, C4's dictionary and PLAIN
+    string columns and an OPTIONAL DOUBLE, small enough for the oracle."""
+    c2r = gen.build(gen.c2_cols(), 30000, 1, seed=2, layout=gen.REF_LAYOUT)
+    c2a = gen.build(gen.c2_cols(), 30000, 1, seed=2, layout=gen.ARROW_LAYOUT, rows_per_page=1500)
+    c4 = gen.build(gen.c4_cols(), 12000, 1, seed=4, layout=gen.ARROW_LAYOUT, rows_per_page=700)
+    out = [("c2_ref", c2r, capi.File(c2r).chunk(0, 0)), ("c2_arrow", c2a, capi.File(c2a).chunk(0, 0))]
+    F4 = capi.File(c4)
+    for ci in (3, 6, 7):
+        out.append((f"c4_c{ci}", c4, F4.chunk(0, ci)))
+    return out
+
+
+def _oracle_dump(file, desc):
+    from oracle import oracle as O
+    from util import to_oracle_chunk
+    rc, msg, col = O.read_all(file, to_oracle_chunk(desc))
+    assert rc == 0, msg
+    return O.dump_column(col), len(col.valid)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_page_range_shards_equal_whole_chunk(world):
+    for name, f, ch in _cases():
+        rc, msg, table = capi.build_page_table(f, ch)
+        assert rc == 0, msg
+        whole, nrows = _oracle_dump(f, ch)
+        ranges = data_page_ranges(table, world)
+        parts, rows = [], []
+        for a, b in ranges:
+            sub, d = extract_range(f, ch, table, a, b)
+            if b > a:
+                dump, n = _oracle_dump(sub, d)
+            else:
+                dump, n = b"", 0
+            first, cnt = range_rows(table, a, b)
+            assert n == cnt, (name, a, b)
+            parts.append(dump)
+            rows.append(n)
+        assert shard_row_offsets(rows).tolist() == [range_rows(table, a, b)[0] for a, b in ranges]
+        assert sum(rows) == nrows
+        assert b"".join(parts) == whole, name
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -56,31 +107,25 @@ def _free_port():
 
 
 def _worker(rank, world, port, q):
+    """One rank: the product's page table and shard plan, its own range only."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from oracle import oracle as O
-    from pqgpu import capi
-    from util import to_oracle_chunk
-    cols = gen.c4_cols()
-    f = gen.build(cols, 1500, 5, seed=4, layout=gen.ARROW_LAYOUT, rows_per_page=400)
-    F = capi.File(f)
-    mine = rank_row_groups(F.num_row_groups, rank, world)
-    digests = {}
-    for ci in range(len(cols)):
-        parts = []
-        for rg in mine:
-            rc, msg, col = O.read_all(f, to_oracle_chunk(F.chunk(rg, ci)))
-            assert rc == 0, msg
-            parts.append(O.dump_column(col))
-        digests[ci] = (mine, [hashlib.sha256(p).hexdigest() for p in parts])
+    out = {}
+    for name, f, ch in _cases():
+        rc, msg, table = capi.build_page_table(f, ch)
+        assert rc == 0, msg
+        a, b = data_page_ranges(table, world)[rank]
+        sub, d = extract_range(f, ch, table, a, b)
+        dump, n = _oracle_dump(sub, d) if b > a else (b"", 0)
+        out[name] = (n, hashlib.sha256(dump).hexdigest(), dump if len(dump) < (1 << 20) else None)
     gathered = [None] * world
-    dist.all_gather_object(gathered, digests)
+    dist.all_gather_object(gathered, out)
     if rank == 0:
         q.put(gathered)
     dist.destroy_process_group()
 
 
-def test_gloo_two_ranks_union_equals_single():
+def test_gloo_two_ranks_page_shards_equal_single():
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -92,20 +137,11 @@ def test_gloo_two_ranks_union_equals_single():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # single-process reference: every row group in order
-    from oracle import oracle as O
-    from pqgpu import capi
-    from util import to_oracle_chunk
-    cols = gen.c4_cols()
-    f = gen.build(cols, 1500, 5, seed=4, layout=gen.ARROW_LAYOUT, rows_per_page=400)
-    F = capi.File(f)
-    for ci in range(len(cols)):
-        single = []
-        for rg in range(F.num_row_groups):
-            rc, msg, col = O.read_all(f, to_oracle_chunk(F.chunk(rg, ci)))
-            single.append(hashlib.sha256(O.dump_column(col)).hexdigest())
-        union = []
-        for r in range(world):
-            rgs, ds = gathered[r][ci]
-            union += ds
-        assert union == single
+    for name, f, ch in _cases():
+        whole, nrows = _oracle_dump(f, ch)
+        rows = [gathered[r][name][0] for r in range(world)]
+        offs = shard_row_offsets(rows)
+        assert offs[-1] + rows[-1] == nrows
+        parts = [gathered[r][name][2] for r in range(world)]
+        assert all(p is not None for p in parts)
+        assert b"".join(parts) == whole, name
