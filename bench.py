@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse N ranks on fewer GPUs (control path only; the data path has no collective)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return ap.parse_args()
 
@@ -116,21 +118,20 @@ class Job:
         torch.cuda.synchronize()
         self.ctx.sync()
 
-    def max_all(self, xs):
+    def _reduce(self, xs, op):
         if self.dist is None:
             return list(xs)
         import torch
-        t = torch.tensor(list(xs), dtype=torch.float64, device=f"cuda:{self.local}")
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        dev = "cpu" if self.dist.get_backend() == "gloo" else f"cuda:{self.local}"
+        t = torch.tensor(list(xs), dtype=torch.float64, device=dev)
+        self.dist.all_reduce(t, op=op)
         return t.tolist()
 
+    def max_all(self, xs):
+        return self._reduce(xs, self.dist.ReduceOp.MAX if self.dist else None)
+
     def sum_all(self, xs):
-        if self.dist is None:
-            return list(xs)
-        import torch
-        t = torch.tensor(list(xs), dtype=torch.float64, device=f"cuda:{self.local}")
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return t.tolist()
+        return self._reduce(xs, self.dist.ReduceOp.SUM if self.dist else None)
 
     def gather(self, obj):
         if self.dist is None:
@@ -596,8 +597,9 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        local = local % max(1, torch.cuda.device_count())  # == LOCAL_RANK unless rehearsing on fewer GPUs
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
     from pqgpu import capi
     ctx = capi.Context(local)
     J = Job(rank, world, local, dist, ctx)
