@@ -878,7 +878,9 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
     try {
         // the chunks' page walks are independent: host threads
         std::vector<pqfmt::WalkResult> walks(static_cast<size_t>(nchunks));
-        parallel_for(nchunks, [&](int k) { walks[static_cast<size_t>(k)] = pqfmt::walk_chunk(file, file_len, chunks[k]); });
+        const int hw = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+        const int per = std::max(1, hw / nchunks);  // threads per chunk walk
+        parallel_for(nchunks, [&](int k) { walks[static_cast<size_t>(k)] = pqfmt::walk_chunk(file, file_len, chunks[k], per); });
         return upload_walked(ctx, file, file_len, chunks[0], walks, 0, out);
     } catch (const std::exception& e) {
         return set_err(ctx, PQ_ERR_ALLOC, e.what());
@@ -1571,6 +1573,7 @@ int pq_file_chunk(const pq_file* f, int rg, int col, pq_chunk_desc* out) {
     out->type = lc.type;
     out->max_def_level = lc.max_def;
     out->max_rep_level = lc.max_rep;
+    out->total_compressed_size = cc.meta->total_compressed;
     return 0;
 }
 int64_t pq_file_row_group_rows(const pq_file* f, int rg) {

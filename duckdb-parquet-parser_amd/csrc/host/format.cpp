@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <thread>
 
 namespace pqfmt {
 
@@ -286,7 +287,265 @@ PageHeader read_page_header(const uint8_t* file, size_t len, size_t off) {  // m
     return h;
 }
 
-WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c) {
+namespace {
+
+// Non-throwing page-header parse over the same 256-byte window (zeros past
+// EOF).  For every header read_page_header accepts it yields the identical
+// PageHeader; on any condition where read_page_header would throw it returns
+// false (the walk then re-parses with read_page_header for the exact error).
+// No allocation: the walk calls it once per page, the speculative walk at
+// candidate positions.
+class FastHdr {
+public:
+    FastHdr(const uint8_t* file, size_t len, size_t off) {
+        if (off < len && len - off >= 256) {
+            p_ = file + off;
+        } else {
+            std::memset(win_, 0, sizeof win_);
+            if (off < len) std::memcpy(win_, file + off, len - off);
+            p_ = win_;
+        }
+        b_ = p_;
+        e_ = p_ + 256;
+    }
+    bool parse(PageHeader& h) {
+        int16_t last = 0;
+        for (;;) {
+            int16_t id;
+            uint8_t ty;
+            if (!field(last, id, ty)) return false;
+            if (ty == 0 && id == 0) break;
+            switch (id) {
+                case 1: if (!i32(h.type)) return false; break;
+                case 2: if (!i32(h.uncompressed)) return false; break;
+                case 3: if (!i32(h.compressed)) return false; break;
+                case 4: { int32_t x; if (!i32(x)) return false; break; }
+                case 5: {
+                    h.has_data = true;
+                    h.data_num_values = 0;
+                    h.data_encoding = 0;
+                    int16_t l2 = 0;
+                    for (;;) {
+                        int16_t i2; uint8_t t2;
+                        if (!field(l2, i2, t2)) return false;
+                        if (t2 == 0 && i2 == 0) break;
+                        int32_t x;
+                        if (i2 == 1) { if (!i32(h.data_num_values)) return false; }
+                        else if (i2 == 2) { if (!i32(h.data_encoding)) return false; }
+                        else if (i2 == 3 || i2 == 4) { if (!i32(x)) return false; }
+                        else if (!skip(t2, 0)) return false;
+                    }
+                    break;
+                }
+                case 7: {
+                    h.has_dict = true;
+                    h.dict_num_values = 0;
+                    int16_t l2 = 0;
+                    for (;;) {
+                        int16_t i2; uint8_t t2;
+                        if (!field(l2, i2, t2)) return false;
+                        if (t2 == 0 && i2 == 0) break;
+                        int32_t x;
+                        if (i2 == 1) { if (!i32(h.dict_num_values)) return false; }
+                        else if (i2 == 2) { if (!i32(x)) return false; }
+                        else if (i2 == 3) { /* read_bool: no bytes */ }
+                        else if (!skip(t2, 0)) return false;
+                    }
+                    break;
+                }
+                default: if (!skip(ty, 0)) return false;
+            }
+        }
+        h.header_size = static_cast<size_t>(p_ - b_);
+        return true;
+    }
+
+private:
+    bool byte(uint8_t& v) { if (p_ >= e_) return false; v = *p_++; return true; }
+    bool varint(uint64_t& r) {
+        r = 0;
+        for (int shift = 0;; shift += 7) {
+            if (shift > 63) return false;
+            uint8_t b;
+            if (!byte(b)) return false;
+            r |= static_cast<uint64_t>(b & 0x7F) << shift;
+            if ((b & 0x80) == 0) return true;
+        }
+    }
+    bool zigzag(int64_t& v) {
+        uint64_t u;
+        if (!varint(u)) return false;
+        v = static_cast<int64_t>((u >> 1) ^ (~(u & 1) + 1));
+        return true;
+    }
+    bool i32(int32_t& v) { int64_t x; if (!zigzag(x)) return false; v = static_cast<int32_t>(x); return true; }
+    // id = 0, type = 0 at STOP
+    bool field(int16_t& last, int16_t& id, uint8_t& type) {
+        uint8_t b;
+        if (!byte(b)) return false;
+        if (b == 0) { id = 0; type = 0; return true; }
+        type = b & 0x0F;
+        const int16_t delta = (b >> 4) & 0x0F;
+        if (delta) {
+            id = static_cast<int16_t>(last + delta);
+        } else {
+            int64_t z;
+            if (!zigzag(z)) return false;
+            id = static_cast<int16_t>(z);
+        }
+        last = id;
+        if (type == 0) type = 0x10;  // a field of wire type 0 is not STOP: skip() rejects it like Thrift::skip
+        return true;
+    }
+    bool bytes(uint64_t n) { if (n > static_cast<uint64_t>(e_ - p_)) return false; p_ += n; return true; }
+    bool skip(uint8_t type, int depth) {
+        if (depth > 256) return false;
+        uint64_t u;
+        switch (type) {
+            case 1: case 2: return true;
+            case 3: { uint8_t b; return byte(b); }
+            case 4: case 5: case 6: return varint(u);
+            case 7: return bytes(8);
+            case 8: return varint(u) && bytes(static_cast<uint32_t>(u));
+            case 9: case 10: {
+                uint8_t b;
+                if (!byte(b)) return false;
+                const uint8_t et = b & 0x0F;
+                int32_t n = (b >> 4) & 0x0F;
+                if (n == 0x0F) { if (!varint(u)) return false; n = static_cast<int32_t>(u); }
+                if (et == 1 || et == 2) return true;  // bool elements take no bytes (n may be ~2^31)
+                for (int32_t i = 0; i < n; i++) if (!skip(et, depth + 1)) return false;
+                return true;
+            }
+            case 11: {
+                if (!varint(u)) return false;
+                const int32_t n = static_cast<int32_t>(u);
+                if (n > 0) {
+                    uint8_t kv;
+                    if (!byte(kv)) return false;
+                    const uint8_t kt = (kv >> 4) & 0x0F, vt = kv & 0x0F;
+                    if ((kt == 1 || kt == 2) && (vt == 1 || vt == 2)) return true;  // entries take no bytes
+                    for (int32_t i = 0; i < n; i++)
+                        if (!skip((kv >> 4) & 0x0F, depth + 1) || !skip(kv & 0x0F, depth + 1)) return false;
+                }
+                return true;
+            }
+            case 12: {
+                int16_t last = 0;
+                for (;;) {
+                    int16_t id; uint8_t t;
+                    if (!field(last, id, t)) return false;
+                    if (t == 0 && id == 0) return true;
+                    if (!skip(t, depth + 1)) return false;
+                }
+            }
+            default: return false;
+        }
+    }
+    uint8_t win_[256];
+    const uint8_t *p_, *b_, *e_;
+};
+
+// Exact header at `cur`: the fast parse, or read_page_header's exception.
+inline PageHeader header_at(const uint8_t* file, size_t len, size_t cur) {
+    PageHeader h;
+    if (FastHdr(file, len, cur).parse(h)) return h;
+    return read_page_header(file, len, cur);  // throws the reference's error
+}
+
+}  // namespace
+
+namespace {
+
+// A header the fast parse accepts and that a real page chain could hold.
+inline bool plausible(const PageHeader& h, size_t pos, size_t end) {
+    if (h.type < 0 || h.type > 3 || h.compressed < 0 || h.uncompressed < 0 || h.header_size < 2) return false;
+    if (h.type == PQ_DATA_PAGE && !h.has_data) return false;
+    if (h.type == PQ_DICTIONARY_PAGE && !h.has_dict) return false;
+    return pos + h.header_size + static_cast<size_t>(h.compressed) <= end;
+}
+
+// Speculative page-chain segments of [start, end): the
+// range is cut into nseg byte segments; segment 0 walks from the true start,
+// segment k > 0 from the first position of its range where a plausible header
+// begins a plausible three-page chain.  Each records the headers it meets
+// until it leaves its range (or a parse fails).  The exact walk then follows
+// the real chain and takes a recorded header only where the positions agree,
+// so a false start costs time, never correctness.
+struct SpecSeg {
+    size_t lo = 0, hi = 0;
+    std::vector<std::pair<size_t, PageHeader>> recs;
+};
+
+// Each thread interleaves kSpecLanes segments: one hop of every chain in
+// turn, the next header's line prefetched as soon as its position is known,
+// so a thread keeps several independent DRAM misses in flight (a single
+// chain is one dependent miss per page).
+constexpr int kSpecLanes = 16;
+
+std::vector<SpecSeg> speculate(const uint8_t* file, size_t len, size_t start, size_t end, int threads) {
+    const int nseg = threads * kSpecLanes;
+    std::vector<SpecSeg> segs(static_cast<size_t>(nseg));
+    const size_t span = end - start;
+    for (int k = 0; k < nseg; k++) {
+        segs[k].lo = start + span * static_cast<size_t>(k) / static_cast<size_t>(nseg);
+        segs[k].hi = start + span * static_cast<size_t>(k + 1) / static_cast<size_t>(nseg);
+        segs[k].recs.reserve(64);
+    }
+    auto find_start = [&](int k) {
+        const SpecSeg& sg = segs[static_cast<size_t>(k)];
+        size_t pos = sg.lo;
+        if (k == 0) return pos;
+        for (; pos < sg.hi; pos++) {
+            PageHeader h;
+            if (!FastHdr(file, len, pos).parse(h) || !plausible(h, pos, end)) continue;
+            size_t q = pos + h.header_size + static_cast<size_t>(h.compressed);
+            bool ok = true;
+            for (int hop = 0; hop < 2 && ok && q < end; hop++) {
+                PageHeader h2;
+                ok = FastHdr(file, len, q).parse(h2) && plausible(h2, q, end);
+                if (ok) q += h2.header_size + static_cast<size_t>(h2.compressed);
+            }
+            if (ok) break;
+        }
+        return pos;
+    };
+    auto work = [&](int t) {
+        size_t pos[kSpecLanes];
+        int live = 0;
+        for (int l = 0; l < kSpecLanes; l++) {
+            pos[l] = find_start(t * kSpecLanes + l);
+            live += pos[l] < segs[static_cast<size_t>(t * kSpecLanes + l)].hi;
+        }
+        while (live > 0) {
+            live = 0;
+            for (int l = 0; l < kSpecLanes; l++) {
+                SpecSeg& sg = segs[static_cast<size_t>(t * kSpecLanes + l)];
+                if (pos[l] >= sg.hi) continue;
+                PageHeader h;
+                if (!FastHdr(file, len, pos[l]).parse(h) || h.compressed < 0) {
+                    pos[l] = sg.hi;
+                    continue;
+                }
+                sg.recs.emplace_back(pos[l], h);
+                pos[l] += h.header_size + static_cast<size_t>(h.compressed);
+                if (pos[l] < sg.hi) {
+                    if (pos[l] + 64 < len) { __builtin_prefetch(file + pos[l]); __builtin_prefetch(file + pos[l] + 64); }
+                    live++;
+                }
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    return segs;
+}
+
+}  // namespace
+
+WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, int threads) {
     WalkResult w;
     try {
         if (c.codec != 0) throw Error(PQ_ERR_CODEC, "Only uncompressed parquet files are supported");
@@ -295,8 +554,27 @@ WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c) {
         size_t cur = static_cast<size_t>(off);
         int64_t values_read = 0, row = 0;
         int32_t page_num = 0, dict_page = -1;
+        // speculative segments when the chunk's extent is known and large
+        std::vector<SpecSeg> segs;
+        w.pages.reserve(c.total_compressed_size > 0 ? static_cast<size_t>(std::min<int64_t>(c.total_compressed_size / 256, 1 << 22)) : 16);
+        if (threads <= 0) threads = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+        if (c.total_compressed_size >= kSpecMinBytes && threads > 1 && off >= 0 &&
+            static_cast<size_t>(off) < len) {
+            const size_t end = std::min(len, static_cast<size_t>(off) + static_cast<size_t>(c.total_compressed_size));
+            if (end > cur) segs = speculate(file, len, cur, end, threads);
+        }
+        size_t sk = 0, si = 0;
+        auto spec_at = [&](size_t pos, PageHeader& h) {
+            while (sk < segs.size() && segs[sk].hi <= pos) { sk++; si = 0; }
+            if (sk >= segs.size()) return false;
+            auto& r = segs[sk].recs;
+            while (si < r.size() && r[si].first < pos) si++;
+            if (si < r.size() && r[si].first == pos) { h = r[si++].second; return true; }
+            return false;
+        };
         while (values_read < c.num_values) {  // column_reader.cpp:31-68
-            PageHeader h = read_page_header(file, len, cur);
+            PageHeader h;
+            if (!spec_at(cur, h)) h = header_at(file, len, cur);
             pq_page_desc p{};
             p.header_offset = static_cast<int64_t>(cur);
             cur += h.header_size;
@@ -351,7 +629,7 @@ std::vector<std::array<int64_t, 4>> page_index(const uint8_t* file, size_t len, 
             while (values_read < m.num_values) {
                 if (cur > len + 256)  // corrupt chunk: the reference would loop forever here
                     throw Error(PQ_ERR_UNSUPPORTED, "page walk ran past end of file");
-                PageHeader h = read_page_header(file, len, cur);
+                PageHeader h = header_at(file, len, cur);
                 cur += h.header_size;
                 if (h.type == PQ_DATA_PAGE || h.type == PQ_DATA_PAGE_V2) {
                     out.push_back({static_cast<int64_t>(cur), static_cast<int64_t>(static_cast<size_t>(h.compressed)),

@@ -38,6 +38,7 @@ class ChunkDesc(C.Structure):
         ("type", C.c_int32),
         ("max_def_level", C.c_int16),
         ("max_rep_level", C.c_int16),
+        ("total_compressed_size", C.c_int64),
     ]
 
 

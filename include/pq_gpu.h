@@ -66,6 +66,9 @@ typedef struct {
     int32_t type;           /* ParquetType of the leaf column */
     int16_t max_def_level;
     int16_t max_rep_level;
+    int64_t total_compressed_size; /* ColumnMetaData.total_compressed_size, or 0 if unknown:
+                                      only an extent hint (chunks of >= 1 MiB walk their
+                                      page chain speculatively on host threads) */
 } pq_chunk_desc;
 
 /* One page of the walk (dictionary, data and skipped pages alike). */

@@ -1,0 +1,87 @@
+"""CPU: the speculative parallel page walk (format.cpp
+walk_chunk) yields exactly the serial walk's page table, status and message —
+the serial walk being ColumnReader::read_all's header loop
+(/root/reference/src/reader/column_reader.cpp:18-71), pinned to the compiled
+reference by test_oracle_golden.py.  A chunk of >= 1 MiB with
+total_compressed_size set walks speculatively; 0 forces the serial walk."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from pqgpu import capi, gen
+
+
+def _walk(f, ch, total):
+    d = capi.ChunkDesc()
+    C.memmove(C.byref(d), C.byref(ch), C.sizeof(ch))
+    d.total_compressed_size = total
+    rc, msg, t = capi.build_page_table(f, d)
+    return rc, msg, bytes(t)
+
+
+def _check(f, ch, totals=None):
+    serial = _walk(f, ch, 0)
+    for tot in totals or [ch.total_compressed_size]:
+        assert _walk(f, ch, tot) == serial, tot
+    return serial
+
+
+def _files():
+    return {
+        "c3_ref": gen.build(gen.c3_cols(), 200_000, 1, seed=3),
+        "c2_ref": gen.build(gen.c2_cols(), 2_000_000, 1, seed=2),
+        "c2_arrow": gen.build(gen.c2_cols(), 2_000_000, 1, seed=2, layout=gen.ARROW_LAYOUT, rows_per_page=3000),
+    }
+
+
+@pytest.mark.parametrize("name", ["c3_ref", "c2_ref", "c2_arrow"])
+def test_spec_walk_equals_serial(name):
+    f = _files()[name]
+    ch = capi.File(f).chunk(0, 0)
+    assert ch.total_compressed_size >= 1 << 20
+    rc, msg, t = _check(f, ch, [ch.total_compressed_size, ch.total_compressed_size // 3,
+                                ch.total_compressed_size * 2, 1 << 20])
+    assert rc == 0
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_spec_walk_corrupted_bytes(seed):
+    """Random byte damage inside the chunk (headers and payload alike): both
+    walks meet the same pages, then the same error text."""
+    base = _files()["c3_ref" if seed % 2 == 0 else "c2_ref"]
+    ch = capi.File(base).chunk(0, 0)
+    rng = np.random.default_rng(seed)
+    b = bytearray(base)
+    lo, hi = 4, 4 + ch.total_compressed_size
+    for pos in rng.integers(lo + (hi - lo) // 4, hi, size=3 + seed):
+        b[int(pos)] = int(rng.integers(0, 256))
+    # and a header's compressed size at a page boundary of the true chain
+    rc0, msg0, t = capi.build_page_table(base, ch)
+    mid = t[len(t) // 2]
+    b[mid.header_offset + 6] = 0x7F
+    _check(bytes(b), ch)
+
+
+def test_spec_walk_truncated_file():
+    f = _files()["c3_ref"]
+    ch = capi.File(f).chunk(0, 0)
+    cut = f[: int(len(f) * 0.6)]
+    rc, msg, t = _check(cut, ch)
+    assert rc != 0 or len(t) > 0
+
+
+def test_spec_walk_pyarrow_statistics(tmp_path):
+    pa = pytest.importorskip("pyarrow")
+    pq = pytest.importorskip("pyarrow.parquet")
+    rng = np.random.default_rng(5)
+    words = np.array([b"alpha", b"beta", b"gamma", b"delta", b"epsilon"])
+    vals = [b" ".join(rng.choice(words, size=int(k))).decode() for k in rng.integers(1, 9, size=150_000)]
+    p = tmp_path / "s.parquet"
+    pq.write_table(pa.table({"s": vals}), p, compression="NONE", data_page_version="1.0", use_dictionary=False,
+                   write_statistics=True, data_page_size=4096)
+    f = p.read_bytes()
+    ch = capi.File(f).chunk(0, 0)
+    assert ch.total_compressed_size >= 1 << 20
+    rc, msg, t = _check(f, ch)
+    assert rc == 0 and len(t) > 100
