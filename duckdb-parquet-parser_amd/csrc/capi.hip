@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <thread>
 #include <map>
@@ -20,6 +21,7 @@
 #include "kernels/kernels.hpp"
 #include "pq_gpu.h"
 #include "regex/regex.hpp"
+#include "stage.hpp"
 
 using pqk::DevDict;
 using pqk::DevErr;
@@ -33,7 +35,17 @@ struct PendingTimer {
 
 struct pq_ctx {
     int device = 0;
+    int cus = 256;                         // compute units (queried once: the property call costs ms)
     hipStream_t stream = nullptr;
+    hipStream_t copy = nullptr;            // uploads (pinned staging), beside the decode stream
+    hipStream_t copy2 = nullptr;           // second DMA queue of the upload ring (option "stage_streams")
+    int opt_stage_streams = 2;
+    pqstage::Stager stager;
+    uint8_t* d_raw = nullptr;              // raw chunk bytes of the current upload (relayout source)
+    size_t raw_cap = 0;
+    pqk::RelayoutEntry* d_relay = nullptr; // relayout entries of the current upload
+    size_t relay_cap = 0;
+    bool opt_raw = true;                   // "raw_upload": DMA raw chunk bytes during the walk, relayout on the GPU
     hipStream_t side = nullptr;            // dictionary decode beside the run-table pass
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
@@ -58,6 +70,7 @@ struct pq_ctx {
     int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
+    int opt_stage_bufs = 6;      // "stage_bufs" / "stage_piece_kb": pinned upload ring (stage.hpp)
 };
 
 struct pq_chunk {
@@ -250,6 +263,22 @@ struct Timed {
     }
 };
 
+// Host-side phase timer (wall ms) filed under `name` in the same table as the
+// kernel timers while timing is on (upload phases: up_walk, up_plan,
+// up_alloc, up_h2d).
+struct HostTimed {
+    pq_ctx* ctx;
+    const char* name;
+    std::chrono::steady_clock::time_point t0;
+    HostTimed(pq_ctx* c, const char* n) : ctx(c), name(n), t0(std::chrono::steady_clock::now()) {}
+    ~HostTimed() {
+        if (!ctx->timing) return;
+        auto& e = ctx->timers[name];
+        e.first += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        e.second += 1;
+    }
+};
+
 void resolve_timers(pq_ctx* ctx) {
     if (ctx->pending.empty()) return;
     (void)hipStreamSynchronize(ctx->stream);
@@ -364,9 +393,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     const int wpw = std::max(1, std::min(16, ctx->opt_write_waves));
     const pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes, wpw);
     if (pl.blocks_per_cu == 0) return;
-    int cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+    const int cus = ctx->cus;
     c->pipe = true;
     c->pipe_small = small;
     c->pipe_count = multi && c->max_def > 0;
@@ -446,9 +473,7 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
             p = q;
         }
     }
-    int cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+    const int cus = ctx->cus;
     c->plain_grid = cus * pqk::plain_write_blocks_per_cu();
     c->plain = true;
 }
@@ -460,9 +485,7 @@ void plan_fused(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages,
                 const std::vector<DevDict>& dicts) {
     c->fused = false;
     if (!ctx->opt_fused || c->type != PQ_BYTE_ARRAY || c->max_def > 255 || c->max_def < 0 || c->ranges.empty()) return;
-    int cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+    const int cus = ctx->cus;
     const uint32_t kLds = 160 * 1024;
     for (auto& r : c->ranges) {
         int32_t dict_id = -1;
@@ -515,14 +538,21 @@ pq_ctx* pq_ctx_create(int device) {
         if (hipSetDevice(device) != hipSuccess) return nullptr;
         auto* c = new pq_ctx();
         c->device = device;
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            c->cus = cus;
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
             delete c;
             return nullptr;
         }
         if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->copy2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
             if (c->side) (void)hipStreamDestroy(c->side);
+            if (c->copy) (void)hipStreamDestroy(c->copy);
+            if (c->copy2) (void)hipStreamDestroy(c->copy2);
             (void)hipStreamDestroy(c->stream);
             delete c;
             return nullptr;
@@ -544,6 +574,13 @@ void pq_ctx_destroy(pq_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_fork);
     (void)hipEventDestroy(ctx->ev_join);
     (void)hipStreamDestroy(ctx->side);
+    ctx->stager.release();
+    if (ctx->d_raw) (void)hipFree(ctx->d_raw);
+    if (ctx->d_relay) (void)hipFree(ctx->d_relay);
+    (void)hipStreamSynchronize(ctx->copy);
+    (void)hipStreamDestroy(ctx->copy);
+    (void)hipStreamSynchronize(ctx->copy2);
+    (void)hipStreamDestroy(ctx->copy2);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -575,6 +612,23 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "pipe_run_pages") == 0) {
         if (value < 1 || value > 32) return set_err(ctx, PQ_ERR_ARG, "pipe_run_pages: 1..32");
         ctx->opt_run_pages = static_cast<int>(value);
+        return 0;
+    }
+    if (std::strcmp(key, "stage_bufs") == 0) {
+        if (value < 2 || value > pqstage::kMaxBufs) return set_err(ctx, PQ_ERR_ARG, "stage_bufs: 2..16");
+        ctx->stager.configure(static_cast<int>(value), ctx->stager.piece());
+        ctx->opt_stage_bufs = static_cast<int>(value);
+        return 0;
+    }
+    if (std::strcmp(key, "raw_upload") == 0) { ctx->opt_raw = value != 0; return 0; }
+    if (std::strcmp(key, "stage_streams") == 0) {
+        if (value < 1 || value > 2) return set_err(ctx, PQ_ERR_ARG, "stage_streams: 1..2");
+        ctx->opt_stage_streams = static_cast<int>(value);
+        return 0;
+    }
+    if (std::strcmp(key, "stage_piece_kb") == 0) {
+        if (value < 64 || value > 65536) return set_err(ctx, PQ_ERR_ARG, "stage_piece_kb: 64..65536");
+        ctx->stager.configure(ctx->opt_stage_bufs, static_cast<size_t>(value) << 10);
         return 0;
     }
     if (std::strcmp(key, "regex_win") == 0) {
@@ -621,10 +675,83 @@ int pq_build_page_table(const uint8_t* file, size_t file_len, const pq_chunk_des
     }
 }
 
+// Raw path of an upload: the chunk's byte extents, exactly
+// as the file holds them, go to HBM (ctx->d_raw) through the pinned ring on a
+// host thread that starts before the page walk, so the H2D overlaps the walk
+// and the planning; a GPU pass (k_relayout) then builds the slot image.
+struct RawStage {
+    std::vector<std::pair<int64_t, int64_t>> ext;  // (file offset, bytes), in d_raw order
+    std::vector<int64_t> base;                     // d_raw offset of each extent
+    int64_t total = 0;
+    std::thread th;
+    hipError_t err = hipSuccess;
+    bool active = false;
+    void join() {
+        if (th.joinable()) th.join();
+    }
+    ~RawStage() { join(); }
+};
+
+static void raw_start(pq_ctx* ctx, const uint8_t* file, size_t file_len, RawStage& R) {
+    R.active = false;
+    if (!ctx->opt_raw || R.ext.empty()) return;
+    R.total = 0;
+    R.base.clear();
+    for (auto& e : R.ext) {
+        e.first = std::max<int64_t>(0, e.first);
+        e.second = std::max<int64_t>(0, std::min<int64_t>(e.second, static_cast<int64_t>(file_len) - e.first));
+        R.base.push_back(R.total);
+        R.total += (e.second + 15) / 16 * 16;  // each extent 16-byte aligned in d_raw
+    }
+    if (R.total <= 0) return;
+    const size_t need = static_cast<size_t>(R.total) + 64;
+    if (ctx->raw_cap < need) {
+        if (ctx->d_raw) (void)hipFree(ctx->d_raw);
+        ctx->d_raw = nullptr;
+        ctx->raw_cap = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&ctx->d_raw), need) != hipSuccess) {
+            ctx->d_raw = nullptr;
+            return;
+        }
+        ctx->raw_cap = need;
+    }
+    R.active = true;
+    const int hw = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+    R.th = std::thread([ctx, file, &R, hw]() {
+        auto fill = [&](uint8_t* dst, size_t a, size_t z) {
+            // extents overlapping [a, z) of d_raw
+            size_t k = static_cast<size_t>(std::upper_bound(R.base.begin(), R.base.end(), static_cast<int64_t>(a)) -
+                                           R.base.begin());
+            k = k ? k - 1 : 0;
+            size_t at = a;
+            for (; k < R.ext.size() && at < z; k++) {
+                const size_t b0 = static_cast<size_t>(R.base[k]);
+                const size_t b1 = b0 + static_cast<size_t>(R.ext[k].second);
+                const size_t b2 = b0 + static_cast<size_t>((R.ext[k].second + 15) / 16 * 16);
+                if (b2 <= at) continue;
+                if (at < b1) {
+                    const size_t e = std::min(z, b1);
+                    std::memcpy(dst + (at - a), file + R.ext[k].first + (at - b0), e - at);
+                    at = e;
+                }
+                if (at < z && at < b2) {
+                    const size_t e = std::min(z, b2);
+                    std::memset(dst + (at - a), 0, e - at);
+                    at = e;
+                }
+            }
+            if (at < z) std::memset(dst + (at - a), 0, z - at);
+        };
+        R.err = ctx->stager.upload(ctx->d_raw, static_cast<size_t>(R.total), ctx->copy, hw, fill,
+                                   ctx->opt_stage_streams > 1 ? ctx->copy2 : nullptr);
+    });
+}
+
 // Builds the device chunk from page walks already made on the host: one walk
 // per input chunk (pq_chunk_upload) or one page-range walk (pq_chunk_upload_range).
 static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc& desc,
-                         std::vector<pqfmt::WalkResult>& walks, int64_t row_offset, pq_chunk** out) {
+                         std::vector<pqfmt::WalkResult>& walks, int64_t row_offset, pq_chunk** out,
+                         RawStage* raw) {
     const int nchunks = static_cast<int>(walks.size());
     try {
         (void)hipSetDevice(ctx->device);
@@ -635,6 +762,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         c->plain_width = plain_width_of(c->type);
         c->width = c->plain_width;
         c->row_offset = row_offset;
+        std::unique_ptr<HostTimed> plan_timer(new HostTimed(ctx, "up_plan"));
 
         // 1) host walks; every payload gets a 16-byte aligned slot in one image
         std::vector<DevPage> hpages;
@@ -642,6 +770,16 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         std::vector<std::pair<int64_t, int64_t>> copies;  // (file offset, image offset) per payload
         std::vector<int32_t> copy_size;
         int64_t seq = 0, row_base = 0, img = 0;
+        {
+            size_t tot = 0;
+            for (const auto& w : walks) tot += w.pages.size();
+            hpages.reserve(tot);
+            copies.reserve(tot);
+            copy_size.reserve(tot);
+            c->walked.reserve(tot);
+            c->page_seq.reserve(tot);
+            c->data_walk_idx.reserve(tot);
+        }
         auto slot = [&](int64_t file_off, int32_t size) {
             int64_t at = img;
             copies.push_back({file_off, at});
@@ -717,6 +855,11 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         // tiles
         std::vector<DevTile> htiles;
         std::vector<int32_t> tile0(hpages.size());
+        {
+            size_t nt = 0;
+            for (const auto& pg : hpages) nt += static_cast<size_t>((std::max(pg.nvals, 0) + pqk::kTileRows - 1) / pqk::kTileRows);
+            htiles.reserve(nt);
+        }
         for (size_t p = 0; p < hpages.size(); p++) {
             tile0[p] = static_cast<int32_t>(htiles.size());
             for (int32_t r = 0; r < hpages[p].nvals; r += pqk::kTileRows)
@@ -734,7 +877,9 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                          c->width == c->plain_width && c->max_def >= 0 && c->max_rep >= 0;
         for (const auto& pg : hpages) c->fixed_plain &= pg.mode == pqk::MODE_PLAIN;
 
+        plan_timer.reset();
         // 2) device allocations + one upload
+        std::unique_ptr<HostTimed> alloc_timer(new HostTimed(ctx, "up_alloc"));
         int rc = 0;
         rc |= dalloc(&c->d_bytes, c->nbytes);
         rc |= dalloc(&c->d_pages, hpages.size());
@@ -805,29 +950,128 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             free_chunk_device(c.get());
             return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (chunk upload)");
         }
-        std::vector<uint8_t> image(c->nbytes, 0);
-        {  // payloads into their slots (zero padding past EOF), split over host threads
-            const int parts = copies.size() > 4096 ? 16 : 1;
-            parallel_for(parts, [&](int part) {
-                const size_t a = copies.size() * static_cast<size_t>(part) / parts;
-                const size_t b = copies.size() * static_cast<size_t>(part + 1) / parts;
-                for (size_t i = a; i < b; i++) {
-                    int64_t lo = copies[i].first, n = copy_size[i];
-                    int64_t hi = std::min<int64_t>(lo + n, static_cast<int64_t>(file_len));
-                    if (hi > lo) std::memcpy(image.data() + copies[i].second, file + lo, static_cast<size_t>(hi - lo));
+        // payload bytes into their 16-byte slots, zero padding in between and
+        // past EOF: written piece by piece straight into pinned buffers by host
+        // threads while earlier pieces are in flight to HBM
+        alloc_timer.reset();
+        HostTimed h2d_timer(ctx, "up_h2d");
+        hipStream_t s = ctx->copy;
+        const int hw = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+        const int64_t img_end = img;
+        auto fill_image = [&](uint8_t* dst, size_t a, size_t z) {
+            // first payload whose slot ends after a (slots are in image order)
+            size_t k = static_cast<size_t>(std::upper_bound(copies.begin(), copies.end(), static_cast<int64_t>(a),
+                                                            [](int64_t v, const std::pair<int64_t, int64_t>& cp) {
+                                                                return v < cp.second;
+                                                            }) - copies.begin());
+            k = k ? k - 1 : 0;
+            size_t at = a;
+            for (; k < copies.size() && at < z; k++) {
+                const int64_t s0 = copies[k].second;
+                const int64_t n = copy_size[k];
+                const int64_t s1 = s0 + (n + 15) / 16 * 16 + 16;  // slot end
+                if (static_cast<size_t>(s1) <= at) continue;
+                if (static_cast<size_t>(s0) > at) {  // (no gaps between slots; defensive)
+                    const size_t g = std::min(z, static_cast<size_t>(s0)) - at;
+                    std::memset(dst + (at - a), 0, g);
+                    at += g;
+                    if (at >= z) break;
                 }
-            });
+                // payload part [s0, s0 + avail) from the file, rest of the slot zero
+                const int64_t lo = copies[k].first;
+                const int64_t avail = std::max<int64_t>(0, std::min<int64_t>(n, static_cast<int64_t>(file_len) - lo));
+                const size_t pe = static_cast<size_t>(s0 + avail), se = std::min(z, static_cast<size_t>(s1));
+                if (at < pe) {
+                    const size_t e = std::min(se, pe);
+                    std::memcpy(dst + (at - a), file + lo + (static_cast<int64_t>(at) - s0), e - at);
+                    at = e;
+                }
+                if (at < se) {
+                    std::memset(dst + (at - a), 0, se - at);
+                    at = se;
+                }
+            }
+            if (at < z) std::memset(dst + (at - a), 0, z - at);  // image tail (past img_end)
+            (void)img_end;
+        };
+        bool relaid = false;
+        if (raw && raw->active) {
+            raw->join();  // the raw bytes are in HBM (the ring is free again)
+            if (raw->err != hipSuccess) {
+                rc = hip_check(ctx, raw->err, "raw upload");
+            } else {
+                std::vector<pqk::RelayoutEntry> ents;
+                ents.reserve(copies.size());
+                bool inside = true;
+                size_t e = 0;
+                for (size_t k = 0; k < copies.size() && inside; k++) {
+                    const int64_t lo = copies[k].first, n = copy_size[k];
+                    const int64_t avail = std::max<int64_t>(0, std::min<int64_t>(n, static_cast<int64_t>(file_len) - lo));
+                    pqk::RelayoutEntry r{};
+                    r.dst = static_cast<uint64_t>(copies[k].second);
+                    r.avail = static_cast<uint32_t>(avail);
+                    r.slot = static_cast<uint32_t>((n + 15) / 16 * 16 + 16);
+                    if (avail > 0) {  // the extent holding the payload (extents and payloads both ascend, mostly)
+                        auto in = [&](size_t j) {
+                            return lo >= raw->ext[j].first && lo + avail <= raw->ext[j].first + raw->ext[j].second;
+                        };
+                        if (!in(e)) {
+                            size_t j = 0;
+                            while (j < raw->ext.size() && !in(j)) j++;
+                            if (j == raw->ext.size()) { inside = false; break; }
+                            e = j;
+                        }
+                        r.src = static_cast<uint64_t>(raw->base[e] + (lo - raw->ext[e].first));
+                    }
+                    ents.push_back(r);
+                }
+                if (inside) {
+                    const size_t need = std::max<size_t>(ents.size(), 1);
+                    if (ctx->relay_cap < need) {
+                        dfree(ctx->d_relay);
+                        ctx->relay_cap = 0;
+                        if (dalloc(&ctx->d_relay, need) == 0) ctx->relay_cap = need;
+                    }
+                    if (ctx->relay_cap >= need) {
+                        rc = hip_check(ctx, ctx->stager.upload(reinterpret_cast<uint8_t*>(ctx->d_relay),
+                                                               ents.size() * sizeof(pqk::RelayoutEntry), s, 1,
+                                                               [&](uint8_t* dst, size_t a, size_t z) {
+                                                                   std::memcpy(dst, reinterpret_cast<const uint8_t*>(ents.data()) + a, z - a);
+                                                               }),
+                                       "upload");
+                        if (!rc) {
+                            pqk::launch_relayout(s, ctx->d_raw, c->d_bytes, ctx->d_relay, static_cast<int32_t>(ents.size()));
+                            (void)hipMemsetAsync(c->d_bytes + img, 0, c->nbytes - static_cast<size_t>(img), s);
+                            relaid = true;
+                        }
+                    }
+                }
+            }
         }
-        hipStream_t s = ctx->stream;
-        rc = hip_check(ctx, hipMemcpyAsync(c->d_bytes, image.data(), c->nbytes, hipMemcpyHostToDevice, s), "upload");
-        if (!rc && !hpages.empty())
-            rc = hip_check(ctx, hipMemcpyAsync(c->d_pages, hpages.data(), hpages.size() * sizeof(DevPage), hipMemcpyHostToDevice, s), "upload");
-        if (!rc && !hdicts.empty())
-            rc = hip_check(ctx, hipMemcpyAsync(c->d_dicts, hdicts.data(), hdicts.size() * sizeof(DevDict), hipMemcpyHostToDevice, s), "upload");
-        if (!rc && !htiles.empty())
-            rc = hip_check(ctx, hipMemcpyAsync(c->d_tiles, htiles.data(), htiles.size() * sizeof(DevTile), hipMemcpyHostToDevice, s), "upload");
-        if (!rc && !tile0.empty())
-            rc = hip_check(ctx, hipMemcpyAsync(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
+        if (!rc && !relaid)
+            rc = hip_check(ctx, ctx->stager.upload(c->d_bytes, c->nbytes, s, copies.size() > 64 ? hw : 1, fill_image,
+                                                   ctx->opt_stage_streams > 1 ? ctx->copy2 : nullptr),
+                           "upload");
+        if (ctx->timing) {
+            auto& f = ctx->timers["up_fill"];
+            f.first += ctx->stager.fill_ms;
+            f.second += 1;
+            auto& w = ctx->timers["up_wait"];
+            w.first += ctx->stager.wait_ms;
+            w.second += 1;
+        }
+        auto put = [&](void* d, const void* h, size_t bytes) {
+            if (rc || bytes == 0) return;
+            rc = hip_check(ctx, ctx->stager.upload(static_cast<uint8_t*>(d), bytes, s, bytes > (32u << 20) ? hw : 1,
+                                                   [&](uint8_t* dst, size_t a, size_t z) {
+                                                       std::memcpy(dst, static_cast<const uint8_t*>(h) + a, z - a);
+                                                   }),
+                           "upload");
+        };
+        put(c->d_pages, hpages.data(), hpages.size() * sizeof(DevPage));
+        put(c->d_dicts, hdicts.data(), hdicts.size() * sizeof(DevDict));
+        put(c->d_tiles, htiles.data(), htiles.size() * sizeof(DevTile));
+        put(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t));
         if (!rc) (void)hipMemsetAsync(c->d_page_err, 0, std::max<size_t>(hpages.size(), 1) * sizeof(DevErr), s);
         if (!rc) (void)hipMemsetAsync(c->d_dict_err, 0, std::max<size_t>(hdicts.size(), 1) * sizeof(DevErr), s);
         if (!rc && c->d_dflag) (void)hipMemsetAsync(c->d_dflag, 0, sizeof(int32_t), s);
@@ -836,14 +1080,12 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             c->next_zeroed = true;
         }
         if (!rc && c->d_chunks) {
-            rc = hip_check(ctx, hipMemcpyAsync(c->d_chunks, c->hchunks.data(), c->hchunks.size() * sizeof(uint2), hipMemcpyHostToDevice, s), "upload");
-            if (!rc) rc = hip_check(ctx, hipMemcpyAsync(c->d_chunk_base, c->hchunk_base.data(), c->hchunk_base.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
+            put(c->d_chunks, c->hchunks.data(), c->hchunks.size() * sizeof(uint2));
+            put(c->d_chunk_base, c->hchunk_base.data(), c->hchunk_base.size() * sizeof(int32_t));
             if (!rc) (void)hipMemsetAsync(c->d_perr, 0, c->hchunks.size() * sizeof(DevErr), s);
         }
-        if (!rc && c->d_bigp)
-            rc = hip_check(ctx, hipMemcpyAsync(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t), hipMemcpyHostToDevice, s), "upload");
-        if (!rc && c->d_pwins)
-            rc = hip_check(ctx, hipMemcpyAsync(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice, s), "upload");
+        if (c->d_bigp) put(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t));
+        if (c->d_pwins) put(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch));
         if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
         if (rc) {
             free_chunk_device(c.get());
@@ -880,8 +1122,21 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         std::vector<pqfmt::WalkResult> walks(static_cast<size_t>(nchunks));
         const int hw = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
         const int per = std::max(1, hw / nchunks);  // threads per chunk walk
-        parallel_for(nchunks, [&](int k) { walks[static_cast<size_t>(k)] = pqfmt::walk_chunk(file, file_len, chunks[k], per); });
-        return upload_walked(ctx, file, file_len, chunks[0], walks, 0, out);
+        // chunk extents known from the footer: their bytes start for HBM now
+        RawStage raw;
+        bool extents = true;
+        for (int k = 0; k < nchunks && extents; k++) {
+            int64_t lo = chunks[k].data_page_offset;
+            if (chunks[k].has_dictionary_page_offset) lo = std::min(lo, chunks[k].dictionary_page_offset);
+            extents = chunks[k].total_compressed_size > 0 && lo >= 0;
+            raw.ext.push_back({lo, chunks[k].total_compressed_size});
+        }
+        if (extents) raw_start(ctx, file, file_len, raw);
+        {
+            HostTimed ht(ctx, "up_walk");
+            parallel_for(nchunks, [&](int k) { walks[static_cast<size_t>(k)] = pqfmt::walk_chunk(file, file_len, chunks[k], per); });
+        }
+        return upload_walked(ctx, file, file_len, chunks[0], walks, 0, out, &raw);
     } catch (const std::exception& e) {
         return set_err(ctx, PQ_ERR_ALLOC, e.what());
     }
@@ -927,9 +1182,19 @@ int pq_chunk_upload_range(pq_ctx* ctx, const uint8_t* file, size_t file_len, con
             if (p.dict_page >= 0) p.dict_page = remap[static_cast<size_t>(p.dict_page)];
             w.pages.push_back(p);
         }
+        // extents: each page's header + payload, contiguous runs merged
+        RawStage raw;
+        for (const auto& p : w.pages) {
+            const int64_t lo = p.header_offset, hi = p.payload_offset + std::max(p.payload_size, 0);
+            if (!raw.ext.empty() && raw.ext.back().first + raw.ext.back().second == lo)
+                raw.ext.back().second += hi - lo;
+            else
+                raw.ext.push_back({lo, hi - lo});
+        }
+        raw_start(ctx, file, file_len, raw);
         std::vector<pqfmt::WalkResult> walks(1);
         walks[0] = std::move(w);
-        return upload_walked(ctx, file, file_len, *chunk, walks, row0, out);
+        return upload_walked(ctx, file, file_len, *chunk, walks, row0, out, &raw);
     } catch (const std::exception& e) {
         return set_err(ctx, PQ_ERR_ALLOC, e.what());
     }
@@ -1391,9 +1656,7 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     if (!c->hrwins.empty() &&
         hipMemcpy(c->d_rwins, c->hrwins.data(), c->hrwins.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice) != hipSuccess)
         return false;
-    int cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+    const int cus = ctx->cus;
     const int per_cu = std::max(1, pqre::regex_plain_occupancy(lds));
     c->rwin_bytes = win;
     c->rwin_for_dfa = c->dfa_bytes;

@@ -558,6 +558,7 @@ WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, i
         std::vector<SpecSeg> segs;
         w.pages.reserve(c.total_compressed_size > 0 ? static_cast<size_t>(std::min<int64_t>(c.total_compressed_size / 256, 1 << 22)) : 16);
         if (threads <= 0) threads = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+        threads = static_cast<int>(std::min<int64_t>(threads, c.total_compressed_size / (2 << 20)));
         if (c.total_compressed_size >= kSpecMinBytes && threads > 1 && off >= 0 &&
             static_cast<size_t>(off) < len) {
             const size_t end = std::min(len, static_cast<size_t>(off) + static_cast<size_t>(c.total_compressed_size));

@@ -128,9 +128,10 @@ struct WalkResult {
 // ColumnReader::read_all's walk (column_reader.cpp:18-71): every page until
 // Σ DATA_PAGE num_values >= chunk num_values; unknown pages are skipped.
 // Chunks of at least kSpecMinBytes (pq_chunk_desc.total_compressed_size)
-// walk speculatively on `threads` host threads (0 = up to 16), with results
+// walk speculatively on `threads` host threads (0 = up to 16; at most one
+// per 2 MiB), with results
 // identical to the serial walk.
-constexpr int64_t kSpecMinBytes = 1 << 20;
+constexpr int64_t kSpecMinBytes = 4 << 20;
 WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, int threads = 0);
 
 // build_page_index: (data_offset, data_size, rg, col) per data page.

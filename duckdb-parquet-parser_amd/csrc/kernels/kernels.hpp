@@ -49,6 +49,15 @@ struct DevErr {
     int32_t size;
 };
 
+// One payload of the raw-bytes → slot-image relayout (relayout.hip).
+struct RelayoutEntry {
+    uint64_t src;    // offset of the payload in the raw byte buffer
+    uint64_t dst;    // slot offset in the image (16-byte aligned)
+    uint32_t avail;  // payload bytes present (compressed_page_size, cut at EOF)
+    uint32_t slot;   // slot bytes (multiple of 16): avail..slot are zero-filled
+};
+void launch_relayout(hipStream_t s, const uint8_t* raw, uint8_t* img, const RelayoutEntry* ent, int32_t n);
+
 struct ColumnParams {
     int32_t type;
     int16_t max_def;

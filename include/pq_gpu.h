@@ -123,6 +123,12 @@ int pq_ctx_sync(pq_ctx* ctx);
  *   "fused_ba"    1 (default): per-page fused BYTE_ARRAY kernel for chunks the
  *                 pipe does not take; 0 forces the generic rows/scan/gather kernels
  *   "fused_waves" waves per workgroup cap (0 = automatic)
+ *   "stage_bufs" pinned buffers of the upload ring, 2..16 (6); "stage_piece_kb"
+ *                 bytes per buffer / H2D piece in KiB, 64..65536 (8192);
+ *                 "stage_streams" DMA queues the pieces alternate over, 1..2 (2);
+ *                 "raw_upload" 1 (default): chunks with a known byte extent go to
+ *                 HBM as raw file bytes while the host walks, the slot image is
+ *                 then built on the GPU (0: the host builds it)
  *   "regex_dfa", "regex_plain", "regex_codes" 1 (default): DFA kernels, the
  *                 windowed kernel for dictionary-free chunks, match bits over
  *                 the pipe's codes; "regex_win" window bytes (1024..32768,

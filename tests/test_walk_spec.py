@@ -2,8 +2,9 @@
 walk_chunk) yields exactly the serial walk's page table, status and message —
 the serial walk being ColumnReader::read_all's header loop
 (/root/reference/src/reader/column_reader.cpp:18-71), pinned to the compiled
-reference by test_oracle_golden.py.  A chunk of >= 1 MiB with
-total_compressed_size set walks speculatively; 0 forces the serial walk."""
+reference by test_oracle_golden.py.  A chunk of >= 4 MiB with
+total_compressed_size set walks speculatively (one thread per 2 MiB); 0
+forces the serial walk."""
 import ctypes as C
 
 import numpy as np
@@ -29,19 +30,19 @@ def _check(f, ch, totals=None):
 
 def _files():
     return {
-        "c3_ref": gen.build(gen.c3_cols(), 200_000, 1, seed=3),
-        "c2_ref": gen.build(gen.c2_cols(), 2_000_000, 1, seed=2),
-        "c2_arrow": gen.build(gen.c2_cols(), 2_000_000, 1, seed=2, layout=gen.ARROW_LAYOUT, rows_per_page=3000),
+        "c3_ref": gen.build(gen.c3_cols(), 500_000, 1, seed=3),
+        "c2_ref": gen.build(gen.c2_cols(), 12_000_000, 1, seed=2),
+        "c3_arrow": gen.build(gen.c3_cols(), 500_000, 1, seed=3, layout=gen.ARROW_LAYOUT, rows_per_page=3000),
     }
 
 
-@pytest.mark.parametrize("name", ["c3_ref", "c2_ref", "c2_arrow"])
+@pytest.mark.parametrize("name", ["c3_ref", "c2_ref", "c3_arrow"])
 def test_spec_walk_equals_serial(name):
     f = _files()[name]
     ch = capi.File(f).chunk(0, 0)
-    assert ch.total_compressed_size >= 1 << 20
-    rc, msg, t = _check(f, ch, [ch.total_compressed_size, ch.total_compressed_size // 3,
-                                ch.total_compressed_size * 2, 1 << 20])
+    assert ch.total_compressed_size >= 8 << 20
+    rc, msg, t = _check(f, ch, [ch.total_compressed_size, ch.total_compressed_size // 2,
+                                ch.total_compressed_size * 2, 8 << 20])
     assert rc == 0
 
 
@@ -49,7 +50,7 @@ def test_spec_walk_equals_serial(name):
 def test_spec_walk_corrupted_bytes(seed):
     """Random byte damage inside the chunk (headers and payload alike): both
     walks meet the same pages, then the same error text."""
-    base = _files()["c3_ref" if seed % 2 == 0 else "c2_ref"]
+    base = _files()["c3_ref" if seed % 2 == 0 else "c3_arrow"]
     ch = capi.File(base).chunk(0, 0)
     rng = np.random.default_rng(seed)
     b = bytearray(base)
@@ -76,12 +77,12 @@ def test_spec_walk_pyarrow_statistics(tmp_path):
     pq = pytest.importorskip("pyarrow.parquet")
     rng = np.random.default_rng(5)
     words = np.array([b"alpha", b"beta", b"gamma", b"delta", b"epsilon"])
-    vals = [b" ".join(rng.choice(words, size=int(k))).decode() for k in rng.integers(1, 9, size=150_000)]
+    vals = [b" ".join(rng.choice(words, size=int(k))).decode() for k in rng.integers(1, 9, size=400_000)]
     p = tmp_path / "s.parquet"
     pq.write_table(pa.table({"s": vals}), p, compression="NONE", data_page_version="1.0", use_dictionary=False,
                    write_statistics=True, data_page_size=4096)
     f = p.read_bytes()
     ch = capi.File(f).chunk(0, 0)
-    assert ch.total_compressed_size >= 1 << 20
+    assert ch.total_compressed_size >= 8 << 20
     rc, msg, t = _check(f, ch)
     assert rc == 0 and len(t) > 100
