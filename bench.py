@@ -496,6 +496,15 @@ def c3_legs(J, args, exp):
     c3d = {"ms_per_decode": med / dsteps * 1e3, "values_per_s": rows * dsteps * J.world / med,
            "payload_bytes": rdc.payload_bytes, "kernel_ms": {k: v["ms_per_step"] for k, v in dkern.items()},
            "validated": ok}
+    # the example driver's 4 KiB chunker over the decoded column (main.cpp:17-32)
+    rdc.decode()
+    ct = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ids, nchunks = rdc.chunk_assign(4096)
+        ct.append(time.perf_counter() - t0)
+    c3d["chunker"] = {"ms": statistics.median(ct) * 1e3, "chunks": nchunks,
+                      "note": "pq_chunk_assign incl. the tuple_to_chunk copy to host (80 MB)"}
     rdc.free()
     return regex, c3d
 

@@ -45,6 +45,8 @@ struct pq_ctx {
     size_t raw_cap = 0;
     pqk::RelayoutEntry* d_relay = nullptr; // relayout entries of the current upload
     size_t relay_cap = 0;
+    uint8_t* d_chunker = nullptr;          // pq_chunk_assign scratch and (no caller buffer) output
+    size_t chunker_cap = 0;
     bool opt_raw = true;                   // "raw_upload": DMA raw chunk bytes during the walk, relayout on the GPU
     hipStream_t side = nullptr;            // dictionary decode beside the run-table pass
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -577,6 +579,7 @@ void pq_ctx_destroy(pq_ctx* ctx) {
     ctx->stager.release();
     if (ctx->d_raw) (void)hipFree(ctx->d_raw);
     if (ctx->d_relay) (void)hipFree(ctx->d_relay);
+    if (ctx->d_chunker) (void)hipFree(ctx->d_chunker);
     (void)hipStreamSynchronize(ctx->copy);
     (void)hipStreamDestroy(ctx->copy);
     (void)hipStreamSynchronize(ctx->copy2);
@@ -1568,6 +1571,32 @@ int pq_column_copy_out(pq_ctx* ctx, const pq_column* col, uint32_t* validity, ui
         rc |= hip_check(ctx, hipMemcpyAsync(offsets, col->d_offsets, static_cast<size_t>(col->num_rows + 1) * 8, hipMemcpyDeviceToHost, s), "copy offsets");
     rc |= hip_check(ctx, hipStreamSynchronize(s), "copy sync");
     return rc ? PQ_ERR_HIP : 0;
+}
+
+int pq_chunk_assign(pq_ctx* ctx, const pq_column* col, int64_t chunk_bytes, int64_t* d_tuple_to_chunk,
+                    int64_t* h_tuple_to_chunk, int64_t* num_chunks) {
+    if (!ctx || !col || !num_chunks || chunk_bytes < 0) return PQ_ERR_ARG;
+    if (col->type != PQ_BYTE_ARRAY || (col->num_rows > 0 && (!col->d_validity || !col->d_offsets)))
+        return set_err(ctx, PQ_ERR_ARG, "pq_chunk_assign: a decoded BYTE_ARRAY column is required");
+    (void)hipSetDevice(ctx->device);
+    const int64_t n = col->num_rows;
+    const size_t out_bytes = d_tuple_to_chunk ? 0 : (static_cast<size_t>(std::max<int64_t>(n, 1)) * 8 + 255) / 256 * 256;
+    const size_t need = pqk::chunk_assign_scratch(n) + out_bytes;
+    if (ctx->chunker_cap < need) {
+        dfree(ctx->d_chunker);
+        ctx->chunker_cap = 0;
+        if (dalloc(&ctx->d_chunker, need)) return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (chunker)");
+        ctx->chunker_cap = need;
+    }
+    int64_t* out = d_tuple_to_chunk ? d_tuple_to_chunk : reinterpret_cast<int64_t*>(ctx->d_chunker);
+    int rc = pqk::chunk_assign(ctx->stream, col->d_validity, col->d_offsets, n, chunk_bytes, out,
+                               ctx->d_chunker + out_bytes, num_chunks);
+    if (rc == -2) return set_err(ctx, PQ_ERR_UNSUPPORTED, "pq_chunk_assign: column too large");
+    if (rc) return set_err(ctx, PQ_ERR_HIP, "pq_chunk_assign: HIP failure");
+    if (h_tuple_to_chunk && n > 0)
+        return hip_check(ctx, hipMemcpy(h_tuple_to_chunk, out, static_cast<size_t>(n) * 8, hipMemcpyDeviceToHost),
+                         "chunker copy-out");
+    return 0;
 }
 
 void pq_column_free(pq_ctx* ctx, pq_column* col) {

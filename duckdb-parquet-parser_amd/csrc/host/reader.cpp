@@ -365,6 +365,44 @@ StringColumnIterator ParquetReader::column_iterator(const std::string& name) {  
     return StringColumnIterator(decode_column(c, 0, static_cast<int>(num_row_groups())));
 }
 
+// The example driver's 4 KiB chunker (main.cpp:17-32) over column_iterator's
+// strings, on the device: tuple_to_chunk (num_rows, NULL rows 0) and the chunk
+// count main.cpp prints (chunk_id + 1).
+std::pair<std::vector<size_t>, size_t> ParquetReader::chunk_assign(const std::string& name, size_t chunk_size) {
+    int c = find_column(name);
+    if (c < 0) throw std::runtime_error("Column not found: " + name);
+    if (columns_[c].type != ParquetType::BYTE_ARRAY)
+        throw std::runtime_error("Column '" + name + "' is not BYTE_ARRAY (type: " + type_name(columns_[c].type) + ")");
+    std::vector<pq_chunk_desc> descs;
+    for (int rg = 0; rg < static_cast<int>(num_row_groups()); rg++) {
+        pq_chunk_desc d{};
+        int rc = pq_file_chunk(file_, rg, c, &d);
+        if (rc) raise(rc == PQ_ERR_OPTIONAL ? 0 : rc, "ColumnChunk has no metadata");
+        descs.push_back(d);
+    }
+    std::pair<std::vector<size_t>, size_t> res;
+    if (descs.empty()) {
+        res.second = 1;
+        return res;
+    }
+    pq_ctx* ctx = dev_.ctx();
+    pq_chunk* ch = nullptr;
+    int rc = pq_chunk_upload(ctx, data_.data(), data_.size(), descs.data(), static_cast<int>(descs.size()), &ch);
+    if (rc) raise(rc, pq_last_error(ctx));
+    pq_column out{};
+    rc = pq_decode(ctx, ch, &out);
+    std::vector<int64_t> ids(static_cast<size_t>(std::max<int64_t>(out.num_rows, 0)));
+    int64_t nchunks = 1;
+    if (!rc) rc = pq_chunk_assign(ctx, &out, static_cast<int64_t>(chunk_size), nullptr, ids.data(), &nchunks);
+    std::string msg = rc ? pq_last_error(ctx) : "";
+    pq_column_free(ctx, &out);
+    pq_chunk_free(ctx, ch);
+    if (rc) raise(rc, msg);
+    res.first.assign(ids.begin(), ids.end());
+    res.second = static_cast<size_t>(nchunks);
+    return res;
+}
+
 size_t ParquetReader::num_pages() const { return page_index_.size(); }
 std::vector<uint8_t> ParquetReader::read_range(size_t off, size_t len) {
     std::vector<uint8_t> b(len, 0);

@@ -58,6 +58,12 @@ struct RelayoutEntry {
 };
 void launch_relayout(hipStream_t s, const uint8_t* raw, uint8_t* img, const RelayoutEntry* ent, int32_t n);
 
+// 4 KiB chunker (chunker.hip, src/main.cpp:17-32): device scratch bytes for
+// n rows, and the launch sequence (synchronises the stream; 0 = OK).
+size_t chunk_assign_scratch(int64_t n);
+int chunk_assign(hipStream_t st, const uint32_t* validity, const int64_t* offsets, int64_t n, int64_t chunk_bytes,
+                 int64_t* out, uint8_t* scratch, int64_t* num_chunks);
+
 struct ColumnParams {
     int32_t type;
     int16_t max_def;

@@ -20,6 +20,7 @@
 #include <stdexcept>
 #include <string>
 #include <tuple>
+#include <utility>
 #include <variant>
 #include <vector>
 
@@ -187,6 +188,9 @@ public:
     HostColumn read_column_columnar(const std::string& col_name);
 
     StringColumnIterator column_iterator(const std::string& col_name);
+    // The example driver's chunk assignment (src/main.cpp:17-32) over
+    // column_iterator(col_name), on the GPU: (tuple_to_chunk, chunk_id + 1).
+    std::pair<std::vector<size_t>, size_t> chunk_assign(const std::string& col_name, size_t chunk_size = 4096);
 
     size_t num_pages() const;
     std::vector<uint8_t> read_page_data(size_t global_page_id) const;

@@ -103,6 +103,7 @@ def lib():
             "pq_decode_check": ([vp, vp], C.c_int),
             "pq_column_copy_out": ([vp, C.POINTER(ColumnOut), vp, vp, vp], C.c_int),
             "pq_column_free": ([vp, C.POINTER(ColumnOut)], None),
+            "pq_chunk_assign": ([vp, C.POINTER(ColumnOut), C.c_int64, vp, vp, C.POINTER(C.c_int64)], C.c_int),
             "pq_regex_compile_check": ([C.c_char_p, C.c_char_p, C.c_size_t], C.c_int),
             "pq_regex_pages": ([vp, vp, C.c_char_p, C.c_int, vp], C.c_int),
             "pq_regex_pages_async": ([vp, vp, C.c_char_p, C.c_int], C.c_int),
@@ -363,6 +364,16 @@ class DeviceChunk:
             offs.ctypes.data_as(vp) if offs is not None else None))
         valid = np.unpackbits(words.view(np.uint8), bitorder="little")[:n].astype(np.uint8)
         return HostColumn(o.type, valid, data[:o.num_bytes], offs)
+
+    def chunk_assign(self, chunk_bytes: int = 4096):
+        """(tuple_to_chunk int64[num_rows], num_chunks) of the decoded column
+        (the example driver's 4 KiB chunker, src/main.cpp:17-32)."""
+        n = self.out.num_rows
+        out = np.zeros(max(n, 1), dtype=np.int64)
+        k = C.c_int64()
+        self.ctx.check(lib().pq_chunk_assign(self.ctx.h, C.byref(self.out), chunk_bytes, None,
+                                             out.ctypes.data_as(vp), C.byref(k)))
+        return out[:n], k.value
 
     def regex_pages(self, pattern: str, neg: bool = False) -> np.ndarray:
         flags = np.zeros(max(self.num_pages, 1), dtype=np.uint8)

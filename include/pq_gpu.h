@@ -187,6 +187,18 @@ int pq_column_copy_out(pq_ctx* ctx, const pq_column* col, uint32_t* validity, ui
                        int64_t* offsets);
 void pq_column_free(pq_ctx* ctx, pq_column* col);
 
+/* ── 4 KiB string chunker (the example driver's loop, src/main.cpp:17-32) ── */
+/* Over a decoded BYTE_ARRAY column (pq_decode output; its non-NULL strings in
+ * row order, as StringColumnIterator yields them, parquet_reader.cpp:282-473):
+ * a chunk is closed before a string once it holds >= chunk_bytes bytes, each
+ * string adding to_string(len).size() + len bytes.  Writes the chunk id of
+ * every row (NULL rows 0: the zero-initialised std::vector<size_t>) to
+ * d_tuple_to_chunk (device, num_rows int64; NULL = a context buffer) and,
+ * when h_tuple_to_chunk is not NULL, copies it there; *num_chunks =
+ * chunk_id + 1 as main.cpp prints it.  Synchronous. */
+int pq_chunk_assign(pq_ctx* ctx, const pq_column* col, int64_t chunk_bytes, int64_t* d_tuple_to_chunk,
+                    int64_t* h_tuple_to_chunk, int64_t* num_chunks);
+
 /* ── regex page filter (README.md:54-64, SURVEY §8a R-REGEX) ───────────── */
 /* page_flags[i] = 1 iff data page i of the chunk is REPORTED: no non-null
  * value matches (neg = 0) / no non-null value fails to match (neg = 1). */

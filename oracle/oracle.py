@@ -98,6 +98,9 @@ def lib():
         L.pqo_dump.argtypes = [C.POINTER(PqoColumn), C.POINTER(u8p), C.POINTER(C.c_size_t)]
         L.pqo_free_buf.argtypes = [C.c_void_p]
         L.pqo_rle_decode.argtypes = [u8p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int32), C.c_uint32]
+        L.pqo_chunk_assign.argtypes = [u8p, C.POINTER(C.c_int64), C.c_int64, C.c_int64, C.POINTER(C.c_int64),
+                                       C.POINTER(C.c_int64)]
+        L.pqo_chunk_assign.restype = None
         _lib = L
     return _lib
 
@@ -321,3 +324,17 @@ def ref_time_read_all_multi(shards, ptype: int, max_def: int, max_rep: int, reps
     s = R.pqref_time_read_all_multi(n, files, lens, nv, do, dd, hd, ptype, max_def, max_rep, reps, threads,
                                     C.byref(out))
     return s, out.value
+
+
+def chunk_assign(col: Column, chunk_size: int = 4096):
+    """src/main.cpp:17-32 restated (pqo_chunk_assign) over an oracle column:
+    (tuple_to_chunk int64[nrows], num_chunks)."""
+    import numpy as np
+    n = len(col.valid)
+    valid = np.ascontiguousarray(np.asarray(col.valid, dtype=np.uint8))
+    offs = np.ascontiguousarray(np.asarray(col.offsets, dtype=np.int64))
+    out = np.zeros(max(n, 1), dtype=np.int64)
+    k = C.c_int64()
+    lib().pqo_chunk_assign(valid.ctypes.data_as(u8p), offs.ctypes.data_as(C.POINTER(C.c_int64)), n, chunk_size,
+                           out.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(k))
+    return out[:n], k.value

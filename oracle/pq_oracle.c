@@ -726,3 +726,24 @@ int pqo_dump(const pqo_column* col, uint8_t** out, size_t* out_len) {
 }
 
 void pqo_free_buf(void* p) { free(p); }
+
+/* src/main.cpp:17-32: `if (chunk.size() >= chunk_size) { clear; chunk_id++; }`
+ * before each non-NULL string, then `chunk += to_string(len) + string` and
+ * tuple_to_chunk[pos] = chunk_id.  Only the chunk's size matters here. */
+void pqo_chunk_assign(const uint8_t* valid, const int64_t* offsets, int64_t nrows,
+                      int64_t chunk_size, int64_t* out, int64_t* num_chunks) {
+    int64_t size = 0, chunk_id = 0;
+    for (int64_t r = 0; r < nrows; r++) {
+        out[r] = 0;  /* std::vector<size_t> tuple_to_chunk(num_rows) */
+        if (!valid[r]) continue;
+        if (size >= chunk_size) {
+            size = 0;
+            chunk_id++;
+        }
+        uint64_t len = (uint64_t)(offsets[r + 1] - offsets[r]), d = 1;
+        for (uint64_t v = len; v >= 10; v /= 10) d++;
+        size += (int64_t)(d + len);
+        out[r] = chunk_id;
+    }
+    *num_chunks = chunk_id + 1;
+}

@@ -90,6 +90,14 @@ void pqo_free_buf(void* p);
 int pqo_rle_decode(const uint8_t* data, uint32_t size, uint32_t bit_width,
                    int32_t* out, uint32_t count);
 
+/* The example driver's 4 KiB chunker (src/main.cpp:17-32) over a decoded
+ * BYTE_ARRAY column: non-NULL strings in row order, a chunk closed before a
+ * string once it holds >= chunk_size bytes, each string adding
+ * to_string(len).size() + len bytes.  out[row] = chunk id (NULL rows 0);
+ * *num_chunks = chunk_id + 1 as main.cpp prints it. */
+void pqo_chunk_assign(const uint8_t* valid, const int64_t* offsets, int64_t nrows,
+                      int64_t chunk_size, int64_t* out, int64_t* num_chunks);
+
 #ifdef __cplusplus
 }
 #endif
