@@ -1,37 +1,3 @@
-# INTEGRATION — binding the reference's C++ API to the MI355X path
-
-The reference (sputnik89/duckdb-parquet-parser) is C++17, so the binding is C++. It is plain C++
-calls into the C ABI `include/pq_gpu.h`, linked against `libpqgpu.so`. No FFI layer is needed. There
-are two ways to adopt it.
-
-## A. Use the mirror classes (no reference edits)
-
-`duckdb-parquet-parser_amd/include/pqgpu/reader.hpp` declares `pqgpu::ColumnReader`,
-`pqgpu::ParquetReader`, `pqgpu::PageIterator`, `pqgpu::StringColumnIterator` and `pqgpu::Value`. They
-have the reference's names, signatures, argument meanings and exception texts
-(`include/reader/column_reader.hpp:10-42`, `include/reader/parquet_reader.hpp:12-138`). A caller
-switches namespaces and links `-lpqgpu`:
-
-```cpp
-#include "pqgpu/reader.hpp"
-pqgpu::ParquetReader r;                 // was: ParquetReader r;
-r.open("file.parquet");
-auto vals = r.read_column("s");         // same std::vector<Value> semantics
-auto ids  = r.regex_pages("comment", "special.*requests");   // README.md:54-64
-```
-
-`tools/pqgpu_parser.cpp` is the README's CLI (`--regex-column/--regex/--neg-regex`) built this way.
-
-## B. Replace the decode inside the reference's own `ColumnReader`
-
-The decode is `ColumnReader::read_all` (`src/reader/column_reader.cpp:18-71`). A maintainer keeps
-the class and swaps its body for the GPU path. The code below is `integration/column_reader_gpu.cpp`
-verbatim; `tests/test_integration.py` checks that this page and the file agree, compiles the file
-against the reference's headers, and (on the GPU) links it into the reference's own reader sources
-in place of the CPU body (`make -C oracle refgpu`): the reference's `ParquetReader::read_column` then
-returns what its CPU path returns on every golden fixture.
-
-```cpp
 // src/reader/column_reader.cpp (reference side) — GPU-backed read_all.
 // The reference's ColumnReader keeps its constructor, members and read_pages;
 // read_all's body becomes the MI355X path through the C ABI (pq_gpu.h).
@@ -125,32 +91,3 @@ std::vector<Value> ColumnReader::read_all() {
     }
     return out;
 }
-```
-
-The page walk, the 256-byte header window, zero padding past EOF, and error precedence (first error
-in walk order, with the reference's message text) all happen inside `pq_chunk_upload` / `pq_decode`.
-The exception texts therefore match what the CPU `read_all` throws. `read_pages` binds the same way,
-and `pq_chunk_pages` returns the per-page `(page_num, type, num_values, first_row)` records.
-
-The regex filter has no source in the reference. A maintainer adds it to `src/main.cpp` beside the
-README's CLI flags:
-
-```cpp
-std::vector<uint8_t> flags(npages);
-pq_regex_pages(gpu(), ch, pattern.c_str(), neg ? 1 : 0, flags.data());   // 1 = page reported
-```
-
-It needs one chunk per row group, with page ids taken in `build_page_index` order
-(`parquet_reader.cpp:559-605`).
-
-## Multi-GPU
-
-Use one `pq_ctx` per device (`pq_ctx_create(d)`), each driven from its own host thread or process,
-and give each its own row groups / page ranges (`pqgpu/shard.py`). No collective is involved.
-
-## Build
-
-* `make -C duckdb-parquet-parser_amd` → `pqgpu/libpqgpu.so` (hipcc `--offload-arch=gfx950`) and the
-  tools.
-* `python -c "import __graft_entry__ as g; g.build()"` does the same, plus the oracle and
-  `oracle/_ref`.

@@ -269,15 +269,39 @@ def ref_open(path: str, meta_cap: int = 4096, pidx_cap: int = 1 << 22):
     return chunks, rows, pidx[:4 * npages].reshape(-1, 4)
 
 
-def ref_read_column(path: str, name: str):
-    R = ref()
+def ref_read_column(path: str, name: str, lib_=None):
+    R = lib_ or ref()
     p = u8p()
     n = C.c_size_t()
     err = C.create_string_buffer(512)
     rc = R.pqref_read_column(path.encode(), name.encode(), C.byref(p), C.byref(n), err, 512)
     if rc != 0:
         return rc, err.value.decode(errors="replace"), None
-    return 0, "", _take(p, n.value)
+    b = C.string_at(p, n.value) if n.value else b""
+    R.pqref_free(p)
+    return 0, "", b
+
+
+_REF_GPU = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "librefgpu.so")
+_ref_gpu = None
+
+
+def have_ref_gpu() -> bool:
+    return os.path.exists(_REF_GPU)
+
+
+def ref_gpu():
+    """The reference's own ParquetReader / ColumnReader with read_all's body
+    replaced by INTEGRATION.md path B (integration/column_reader_gpu.cpp over
+    libpqgpu.so): the maintainer-side binding, built by `make refgpu`."""
+    global _ref_gpu
+    if _ref_gpu is None:
+        L = C.CDLL(_REF_GPU)
+        L.pqref_read_column.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(u8p), C.POINTER(C.c_size_t), C.c_char_p,
+                                        C.c_size_t]
+        L.pqref_free.argtypes = [C.c_void_p]
+        _ref_gpu = L
+    return _ref_gpu
 
 
 def ref_write(path: str, cols: list, nrows: int):
