@@ -45,6 +45,11 @@ struct pq_ctx {
     size_t raw_cap = 0;
     pqk::RelayoutEntry* d_relay = nullptr; // relayout entries of the current upload
     size_t relay_cap = 0;
+    pqk::CodecEntry* d_codec = nullptr;    // compressed / V2 pages of the current upload (codec.hip)
+    size_t codec_cap = 0;
+    uint32_t* d_codec_st = nullptr;        // their status words
+    uint8_t* d_zsrc = nullptr;             // their payloads, when not in d_raw
+    size_t zsrc_cap = 0;
     uint8_t* d_chunker = nullptr;          // pq_chunk_assign scratch and (no caller buffer) output
     size_t chunker_cap = 0;
     bool opt_raw = true;                   // "raw_upload": DMA raw chunk bytes during the walk, relayout on the GPU
@@ -579,6 +584,9 @@ void pq_ctx_destroy(pq_ctx* ctx) {
     ctx->stager.release();
     if (ctx->d_raw) (void)hipFree(ctx->d_raw);
     if (ctx->d_relay) (void)hipFree(ctx->d_relay);
+    if (ctx->d_codec) (void)hipFree(ctx->d_codec);
+    if (ctx->d_codec_st) (void)hipFree(ctx->d_codec_st);
+    if (ctx->d_zsrc) (void)hipFree(ctx->d_zsrc);
     if (ctx->d_chunker) (void)hipFree(ctx->d_chunker);
     (void)hipStreamSynchronize(ctx->copy);
     (void)hipStreamDestroy(ctx->copy);
@@ -783,8 +791,39 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             c->page_seq.reserve(tot);
             c->data_walk_idx.reserve(tot);
         }
+        // pages the codec pass rebuilds (compressed or DATA_PAGE_V2): their slot
+        // holds the V1-layout payload; the image build leaves it zero
+        std::vector<pqk::CodecEntry> cents;
+        std::vector<int64_t> cent_file;  // payload file offset per codec entry
+        auto codec_page = [&](const pq_page_desc& p, int32_t* out_len) -> bool {
+            if (!(p.flags & (PQ_PAGE_COMPRESSED | PQ_PAGE_V2))) return false;
+            const bool v2 = (p.flags & PQ_PAGE_V2) != 0, comp = (p.flags & PQ_PAGE_COMPRESSED) != 0;
+            const int64_t lv = v2 ? static_cast<int64_t>(p.v2_def_len) + p.v2_rep_len : 0;
+            const int64_t vals = (comp ? static_cast<int64_t>(p.uncompressed_size) : static_cast<int64_t>(p.payload_size)) - lv;
+            const int64_t n = vals + (v2 && desc.max_def_level > 0 ? 4 + p.v2_def_len : 0) +
+                              (v2 && desc.max_rep_level > 0 ? 4 + p.v2_rep_len : 0);
+            if (vals < 0 || n > (1ll << 31) - 64 || p.payload_size < 0)
+                throw pqfmt::Error(PQ_ERR_DECOMPRESS, "page header: uncompressed_page_size out of range");
+            pqk::CodecEntry e{};
+            e.src_len = static_cast<uint32_t>(std::max<int64_t>(0, std::min<int64_t>(p.payload_size, static_cast<int64_t>(file_len) - p.payload_offset)));
+            e.out_len = static_cast<uint32_t>(n);
+            e.def_len = v2 ? static_cast<uint32_t>(p.v2_def_len) : 0u;
+            e.rep_len = v2 ? static_cast<uint32_t>(p.v2_rep_len) : 0u;
+            e.codec = comp ? static_cast<uint32_t>((p.flags >> 8) & 0xFF) : 0u;
+            e.flags = v2 ? (pqk::kCodecV2 | (desc.max_def_level > 0 ? pqk::kCodecDefPrefix : 0u) |
+                            (desc.max_rep_level > 0 ? pqk::kCodecRepPrefix : 0u))
+                         : 0u;
+            cents.push_back(e);
+            cent_file.push_back(p.payload_offset);
+            *out_len = static_cast<int32_t>(n);
+            return true;
+        };
         auto slot = [&](int64_t file_off, int32_t size) {
             int64_t at = img;
+            if (!cents.empty() && cents.back().dst == ~0ull) {  // the codec entry just made
+                cents.back().dst = static_cast<uint64_t>(at);
+                file_off = -1;
+            }
             copies.push_back({file_off, at});
             copy_size.push_back(size);
             img += (static_cast<int64_t>(size) + 15) / 16 * 16 + 16;
@@ -799,36 +838,40 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             for (size_t i = 0; i < w.pages.size(); i++) {
                 pq_page_desc p = w.pages[i];
                 int64_t sq = seq + static_cast<int64_t>(i);
+                int32_t psize = p.payload_size;
+                if ((p.page_type == PQ_DICTIONARY_PAGE || p.page_type == PQ_DATA_PAGE) && codec_page(p, &psize))
+                    cents.back().dst = ~0ull;  // placed by slot()
                 if (p.page_type == PQ_DICTIONARY_PAGE) {
                     DevDict d{};
-                    d.off = static_cast<uint64_t>(slot(p.payload_offset, p.payload_size));
-                    d.size = p.payload_size;
+                    d.off = static_cast<uint64_t>(slot(p.payload_offset, psize));
+                    d.size = psize;
                     d.nvals = p.num_values;
                     d.entry_base = static_cast<int32_t>(c->nentries);
-                    c->max_dict_bytes = std::max<uint32_t>(c->max_dict_bytes, static_cast<uint32_t>(std::max(p.payload_size, 0)));
+                    c->max_dict_bytes = std::max<uint32_t>(c->max_dict_bytes, static_cast<uint32_t>(std::max(psize, 0)));
                     int64_t cap = c->type == PQ_BYTE_ARRAY
-                                      ? std::min<int64_t>(p.num_values, p.payload_size / 4 + 1)
+                                      ? std::min<int64_t>(p.num_values, psize / 4 + 1)
                                       : 0;
                     c->nentries += std::max<int64_t>(cap, 0);
                     dict_of_walk[i] = static_cast<int32_t>(hdicts.size());
                     hdicts.push_back(d);
                     c->dict_seq.push_back(sq);
-                    c->payload_bytes += p.payload_size;
+                    c->payload_bytes += psize;
                 } else if (p.page_type == PQ_DATA_PAGE) {
                     DevPage d{};
-                    d.off = static_cast<uint64_t>(slot(p.payload_offset, p.payload_size));
-                    d.size = p.payload_size;
+                    d.off = static_cast<uint64_t>(slot(p.payload_offset, psize));
+                    d.size = psize;
                     d.nvals = p.num_values;
                     d.first_row = row_base + p.first_row;
                     int dict_dev = p.dict_page >= 0 ? dict_of_walk[p.dict_page] : -1;
                     bool enc_dict = p.encoding == 2 || p.encoding == 8;
                     d.mode = (enc_dict && dict_dev >= 0) ? pqk::MODE_DICT
-                             : (c->type == PQ_BOOLEAN ? pqk::MODE_BOOL : pqk::MODE_PLAIN);
+                             : (c->type == PQ_BOOLEAN ? ((desc.ext_flags && p.encoding == 3) ? pqk::MODE_BOOL_RLE : pqk::MODE_BOOL)
+                                                      : pqk::MODE_PLAIN);
                     d.dict = d.mode == pqk::MODE_DICT ? dict_dev : -1;
                     hpages.push_back(d);
                     c->page_seq.push_back(sq);
                     c->data_walk_idx.push_back(base_walk + static_cast<int64_t>(i));
-                    c->payload_bytes += p.payload_size;
+                    c->payload_bytes += psize;
                 }
                 p.first_row += row_base;
                 c->walked.push_back(p);
@@ -981,8 +1024,9 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                     if (at >= z) break;
                 }
                 // payload part [s0, s0 + avail) from the file, rest of the slot zero
+                // (codec pages, lo < 0: all zero until the codec pass)
                 const int64_t lo = copies[k].first;
-                const int64_t avail = std::max<int64_t>(0, std::min<int64_t>(n, static_cast<int64_t>(file_len) - lo));
+                const int64_t avail = lo < 0 ? 0 : std::max<int64_t>(0, std::min<int64_t>(n, static_cast<int64_t>(file_len) - lo));
                 const size_t pe = static_cast<size_t>(s0 + avail), se = std::min(z, static_cast<size_t>(s1));
                 if (at < pe) {
                     const size_t e = std::min(se, pe);
@@ -1009,7 +1053,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                 size_t e = 0;
                 for (size_t k = 0; k < copies.size() && inside; k++) {
                     const int64_t lo = copies[k].first, n = copy_size[k];
-                    const int64_t avail = std::max<int64_t>(0, std::min<int64_t>(n, static_cast<int64_t>(file_len) - lo));
+                    const int64_t avail = lo < 0 ? 0 : std::max<int64_t>(0, std::min<int64_t>(n, static_cast<int64_t>(file_len) - lo));
                     pqk::RelayoutEntry r{};
                     r.dst = static_cast<uint64_t>(copies[k].second);
                     r.avail = static_cast<uint32_t>(avail);
@@ -1055,6 +1099,75 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             rc = hip_check(ctx, ctx->stager.upload(c->d_bytes, c->nbytes, s, copies.size() > 64 ? hw : 1, fill_image,
                                                    ctx->opt_stage_streams > 1 ? ctx->copy2 : nullptr),
                            "upload");
+        // compressed / DATA_PAGE_V2 pages: their payloads
+        // (in d_raw when the raw path holds them, else gathered and uploaded)
+        // are rebuilt into their slots by the codec pass (codec.hip)
+        if (!rc && !cents.empty()) {
+            const uint8_t* csrc = nullptr;
+            bool in_raw = relaid && raw && raw->active;
+            for (size_t k = 0, e = 0; k < cents.size() && in_raw; k++) {
+                const int64_t lo = cent_file[k], n = cents[k].src_len;
+                auto in = [&](size_t j) {
+                    return lo >= raw->ext[j].first && lo + n <= raw->ext[j].first + raw->ext[j].second;
+                };
+                if (!in(e)) {
+                    size_t j = 0;
+                    while (j < raw->ext.size() && !in(j)) j++;
+                    if (j == raw->ext.size()) { in_raw = false; break; }
+                    e = j;
+                }
+                cents[k].src = static_cast<uint64_t>(raw->base[e] + (lo - raw->ext[e].first));
+            }
+            if (in_raw) {
+                csrc = ctx->d_raw;
+            } else {  // gather the payloads, each 16-byte aligned
+                std::vector<int64_t> at(cents.size());
+                int64_t tot = 0;
+                for (size_t k = 0; k < cents.size(); k++) {
+                    at[k] = tot;
+                    cents[k].src = static_cast<uint64_t>(tot);
+                    tot += (static_cast<int64_t>(cents[k].src_len) + 15) / 16 * 16;
+                }
+                const size_t need = static_cast<size_t>(tot) + 64;
+                if (ctx->zsrc_cap < need) {
+                    dfree(ctx->d_zsrc);
+                    ctx->zsrc_cap = 0;
+                    if (dalloc(&ctx->d_zsrc, need) == 0) ctx->zsrc_cap = need;
+                }
+                if (ctx->zsrc_cap < need) rc = set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (compressed pages)");
+                if (!rc)
+                    rc = hip_check(ctx, ctx->stager.upload(ctx->d_zsrc, need, s, cents.size() > 64 ? hw : 1,
+                                                           [&](uint8_t* dst, size_t a, size_t z) {
+                        size_t k = static_cast<size_t>(std::upper_bound(at.begin(), at.end(), static_cast<int64_t>(a)) - at.begin());
+                        k = k ? k - 1 : 0;
+                        std::memset(dst, 0, z - a);
+                        for (; k < cents.size() && static_cast<size_t>(at[k]) < z; k++) {
+                            const size_t b0 = static_cast<size_t>(at[k]), b1 = b0 + cents[k].src_len;
+                            const size_t x0 = std::max(a, b0), x1 = std::min(z, b1);
+                            if (x0 < x1) std::memcpy(dst + (x0 - a), file + cent_file[k] + (x0 - b0), x1 - x0);
+                        }
+                    }), "upload");
+                csrc = ctx->d_zsrc;
+            }
+            const size_t n = cents.size();
+            if (!rc && ctx->codec_cap < n) {
+                dfree(ctx->d_codec);
+                dfree(ctx->d_codec_st);
+                ctx->codec_cap = 0;
+                if (dalloc(&ctx->d_codec, n) == 0 && dalloc(&ctx->d_codec_st, n) == 0) ctx->codec_cap = n;
+                else rc = set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (compressed pages)");
+            }
+            if (!rc)
+                rc = hip_check(ctx, ctx->stager.upload(reinterpret_cast<uint8_t*>(ctx->d_codec), n * sizeof(pqk::CodecEntry), s, 1,
+                                                       [&](uint8_t* dst, size_t a, size_t z) {
+                                                           std::memcpy(dst, reinterpret_cast<const uint8_t*>(cents.data()) + a, z - a);
+                                                       }),
+                               "upload");
+            if (!rc) {
+                HostTimed ct(ctx, "up_codec");
+                pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus);
+            }
+        }
         if (ctx->timing) {
             auto& f = ctx->timers["up_fill"];
             f.first += ctx->stager.fill_ms;
@@ -1090,6 +1203,19 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         if (c->d_bigp) put(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t));
         if (c->d_pwins) put(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch));
         if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
+        if (!rc && !cents.empty()) {
+            std::vector<uint32_t> st(cents.size());
+            rc = hip_check(ctx, hipMemcpy(st.data(), ctx->d_codec_st, st.size() * sizeof(uint32_t), hipMemcpyDeviceToHost),
+                           "codec status");
+            for (size_t k = 0; k < st.size() && !rc; k++) {
+                if (!st[k]) continue;
+                static const char* what[] = {"", "corrupt compressed data", "decompressed size differs from the page header",
+                                             "unsupported codec"};
+                rc = set_err(ctx, PQ_ERR_DECOMPRESS,
+                             "page at file offset " + std::to_string(cent_file[k]) + " (codec " +
+                                 std::to_string(cents[k].codec) + "): " + what[std::min<uint32_t>(st[k], 3)]);
+            }
+        }
         if (rc) {
             free_chunk_device(c.get());
             return rc;
@@ -1292,7 +1418,7 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
         Timed t(ctx, "pipe_runs");
         pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
                               c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist,  // flist[0], bsum: cleared with d_flags
-                              true);
+                              ctx->opt_debug);
     }
     if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
     if (!c->hbig.empty()) {

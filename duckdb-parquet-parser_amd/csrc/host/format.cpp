@@ -266,6 +266,21 @@ PageHeader read_page_header(const uint8_t* file, size_t len, size_t off) {  // m
                 t.pop();
                 break;
             }
+            case 8: {  // DataPageHeaderV2 (parquet.thrift; skipped by the reference)
+                t.push();
+                h.has_v2 = true;
+                int16_t i2; uint8_t t2;
+                while (t.field(i2, t2)) {
+                    if (t2 == 5 && i2 == 1) h.v2_num_values = t.i32();
+                    else if (t2 == 5 && i2 == 4) h.v2_encoding = t.i32();
+                    else if (t2 == 5 && i2 == 5) h.v2_def_len = t.i32();
+                    else if (t2 == 5 && i2 == 6) h.v2_rep_len = t.i32();
+                    else if ((t2 == 1 || t2 == 2) && i2 == 7) h.v2_compressed = t2 == 1;
+                    else t.skip(t2);
+                }
+                t.pop();
+                break;
+            }
             case 7: {  // DictionaryPageHeader, metadata.cpp:106-117
                 t.push();
                 h.has_dict = true;
@@ -333,6 +348,22 @@ public:
                         if (i2 == 1) { if (!i32(h.data_num_values)) return false; }
                         else if (i2 == 2) { if (!i32(h.data_encoding)) return false; }
                         else if (i2 == 3 || i2 == 4) { if (!i32(x)) return false; }
+                        else if (!skip(t2, 0)) return false;
+                    }
+                    break;
+                }
+                case 8: {  // DataPageHeaderV2
+                    h.has_v2 = true;
+                    int16_t l2 = 0;
+                    for (;;) {
+                        int16_t i2; uint8_t t2;
+                        if (!field(l2, i2, t2)) return false;
+                        if (t2 == 0 && i2 == 0) break;
+                        if (t2 == 5 && i2 == 1) { if (!i32(h.v2_num_values)) return false; }
+                        else if (t2 == 5 && i2 == 4) { if (!i32(h.v2_encoding)) return false; }
+                        else if (t2 == 5 && i2 == 5) { if (!i32(h.v2_def_len)) return false; }
+                        else if (t2 == 5 && i2 == 6) { if (!i32(h.v2_rep_len)) return false; }
+                        else if ((t2 == 1 || t2 == 2) && i2 == 7) h.v2_compressed = t2 == 1;
                         else if (!skip(t2, 0)) return false;
                     }
                     break;
@@ -548,7 +579,12 @@ std::vector<SpecSeg> speculate(const uint8_t* file, size_t len, size_t start, si
 WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, int threads) {
     WalkResult w;
     try {
-        if (c.codec != 0) throw Error(PQ_ERR_CODEC, "Only uncompressed parquet files are supported");
+        const bool ext_codecs = (c.ext_flags & PQ_EXT_CODECS) != 0, ext_v2 = (c.ext_flags & PQ_EXT_PAGE_V2) != 0;
+        if (c.codec != 0 && !ext_codecs) throw Error(PQ_ERR_CODEC, "Only uncompressed parquet files are supported");
+        if (c.codec != 0 && c.codec != 1 && c.codec != 2 && c.codec != 5 && c.codec != 7)
+            throw Error(PQ_ERR_CODEC, "Unsupported compression codec " + std::to_string(c.codec) +
+                                          " (SNAPPY, GZIP, LZ4 and LZ4_RAW are decoded)");
+        const int32_t cflag = c.codec != 0 ? (PQ_PAGE_COMPRESSED | (c.codec << 8)) : 0;
         int64_t off = c.data_page_offset;
         if (c.has_dictionary_page_offset) off = std::min(off, c.dictionary_page_offset);
         size_t cur = static_cast<size_t>(off);
@@ -585,6 +621,7 @@ WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, i
             p.dict_page = dict_page;
             p.first_row = row;
             p.page_num = -1;
+            p.uncompressed_size = h.uncompressed;
             if (h.compressed < 0)
                 throw Error(PQ_ERR_ALLOC, "cannot create std::vector larger than max_size()");
             if (h.type == PQ_DICTIONARY_PAGE) {
@@ -592,6 +629,7 @@ WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, i
                 if (h.dict_num_values < 0) throw Error(PQ_ERR_ALLOC, "vector::reserve");
                 p.num_values = h.dict_num_values;
                 p.page_num = page_num++;
+                p.flags = cflag;
                 dict_page = static_cast<int32_t>(w.pages.size());
                 p.dict_page = dict_page;
             } else if (h.type == PQ_DATA_PAGE) {
@@ -601,8 +639,25 @@ WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, i
                 p.num_values = h.data_num_values;
                 p.encoding = h.data_encoding;
                 p.page_num = page_num++;
+                p.flags = cflag;
                 values_read += h.data_num_values;
                 if (h.data_num_values > 0) row += h.data_num_values;
+            } else if (h.type == PQ_DATA_PAGE_V2 && ext_v2) {
+                // listed as a data page: the device rebuilds it in the V1 layout
+                if (!h.has_v2) throw Error(PQ_ERR_OPTIONAL, "bad optional access");
+                if (h.v2_num_values < 0 || h.v2_def_len < 0 || h.v2_rep_len < 0 ||
+                    static_cast<int64_t>(h.v2_def_len) + h.v2_rep_len > h.compressed ||
+                    static_cast<int64_t>(h.v2_def_len) + h.v2_rep_len > h.uncompressed)
+                    throw Error(PQ_ERR_UNSUPPORTED, "DATA_PAGE_V2 header: level sections outside the page");
+                p.page_type = PQ_DATA_PAGE;
+                p.num_values = h.v2_num_values;
+                p.encoding = h.v2_encoding;
+                p.page_num = page_num++;
+                p.flags = PQ_PAGE_V2 | (h.v2_compressed ? cflag : 0);
+                p.v2_def_len = h.v2_def_len;
+                p.v2_rep_len = h.v2_rep_len;
+                values_read += h.v2_num_values;
+                row += h.v2_num_values;
             } else {
                 page_num++;  // read_pages counts skipped pages (column_reader.cpp:122)
             }
@@ -636,6 +691,9 @@ std::vector<std::array<int64_t, 4>> page_index(const uint8_t* file, size_t len, 
                     out.push_back({static_cast<int64_t>(cur), static_cast<int64_t>(static_cast<size_t>(h.compressed)),
                                    static_cast<int64_t>(rg), static_cast<int64_t>(col)});
                     if (h.type == PQ_DATA_PAGE && h.has_data) values_read += h.data_num_values;
+                    // V2 values count too (the reference does not count them and walks
+                    // past the chunk: outside its parity scope, SURVEY §8a R-WALK)
+                    if (h.type == PQ_DATA_PAGE_V2 && h.has_v2) values_read += h.v2_num_values;
                 }
                 cur += static_cast<size_t>(h.compressed);
             }

@@ -115,6 +115,9 @@ struct PageHeader {
     bool has_data = false, has_dict = false;
     int32_t data_num_values = 0, data_encoding = 0;
     int32_t dict_num_values = 0;
+    // DataPageHeaderV2 (field 8; the reference skips it): read for extended walks
+    bool has_v2 = false, v2_compressed = true;
+    int32_t v2_num_values = 0, v2_encoding = 0, v2_def_len = 0, v2_rep_len = 0;
     size_t header_size = 0;
 };
 // Parses a header from the 256-byte window at `off` (zeros past EOF).
@@ -127,6 +130,8 @@ struct WalkResult {
 };
 // ColumnReader::read_all's walk (column_reader.cpp:18-71): every page until
 // Σ DATA_PAGE num_values >= chunk num_values; unknown pages are skipped.
+// pq_chunk_desc.ext_flags widen it (pq_gpu.h PQ_EXT_*): compressed chunks,
+// and DATA_PAGE_V2 pages walked as data pages (flags PQ_PAGE_V2).
 // Chunks of at least kSpecMinBytes (pq_chunk_desc.total_compressed_size)
 // walk speculatively on `threads` host threads (0 = up to 16; at most one
 // per 2 MiB), with results

@@ -1,0 +1,642 @@
+// codec.hip — compressed pages and DATA_PAGE_V2 pages on the GPU (SURVEY §8f
+// rank 4; outside the reference's parity scope: the reference rejects any
+// codec, column_reader.cpp:13-15, and does not decode V2 pages, 56-67).
+//
+// Each entry turns one page payload, as the file holds it (raw chunk bytes in
+// HBM), into the payload the decode kernels read, written to the page's slot
+// in the chunk image (capi.hip `slot`):
+//   V1 page, codec C:  decompress(payload)
+//   V2 page:           [u32 def_len][def levels] (max_def > 0)
+//                      [u32 rep_len][rep levels] (max_rep > 0)
+//                      values (decompressed when the page says is_compressed)
+// i.e. the V1 layout in the order the reference reads it (column_reader.cpp:
+// 146-170), so every decode and regex kernel runs unchanged on the result.
+//
+// One wavefront per page (persistent grid-stride loop).  The compressed input
+// is staged through an 8 KiB LDS window; the output goes through a 64 KiB LDS
+// ring that holds the whole back-reference history (SNAPPY and LZ4 offsets
+// are < 2^16, DEFLATE's < 2^15) and is flushed to HBM 1 KiB at a time as
+// aligned 16-byte stores.  The command stream (literal runs and copies) is
+// parsed wave-uniformly; each command is executed 64 bytes per step by the
+// whole wave.  A copy's byte j reads the ring at c0 - d + (j mod d) for
+// overlapping copies (d < 64) or c0 - d + j, relative to the step's first
+// output byte c0: bytes before c0 are final, and a step's LDS reads issue
+// before its writes, so one step never reads its own output.
+//   SNAPPY   (codec 1): format_description.txt of google/snappy
+//   GZIP     (codec 2): RFC 1952 members holding RFC 1951 DEFLATE (zlib RFC
+//                       1950 framing also accepted); Huffman symbols decoded
+//                       through 10-bit LDS lookup tables, longer codes by the
+//                       canonical bit-serial walk
+//   LZ4      (codec 5): Hadoop framing ([u32 BE raw][u32 BE packed] blocks)
+//   LZ4_RAW  (codec 7): one LZ4 block
+#include <algorithm>
+
+#include "kernels/device_common.hpp"
+#include "kernels/kernels.hpp"
+#include "pq_gpu.h"
+
+namespace pqk {
+namespace {
+
+using dev::lane;
+
+constexpr uint32_t kRing = 65536;
+constexpr uint32_t kRingMask = kRing - 1;
+constexpr uint32_t kInWin = 8192;  // staged input bytes (+16 slack)
+constexpr uint32_t kFlush = 1024;  // output bytes per flush step (16 per lane)
+constexpr uint32_t kFast = 10;     // Huffman lookup bits
+
+struct CodecLds {
+    uint8_t ring[kRing];
+    uint8_t in[kInWin + 32];
+    uint16_t lt[1 << kFast];  // litlen: sym << 4 | len (0 = longer code)
+    uint16_t dt[1 << kFast];  // distance
+    uint16_t sym[320];        // symbols in canonical order: litlen [0, 288), dist [288, 320)
+    uint16_t code[320];       // canonical code per symbol
+    uint16_t cnt[2][16];      // code count per length
+    uint8_t lens[320];        // code lengths: litlen [0, 288), dist [288, 320)
+    uint16_t nxt[16], offs[16];  // build_code: next code / next symbol slot per length
+    uint32_t scratch[4];
+};
+
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ── staged input ───────────────────────────────────────────────────────────
+struct In {
+    const uint8_t* g;  // page input in HBM
+    uint32_t len;      // input bytes
+    uint32_t wlo;      // input byte held at in[sh]
+    uint32_t sh;
+    uint8_t* w;
+    __device__ void refill(uint32_t p) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(g) + p;
+        const uintptr_t A = a & ~static_cast<uintptr_t>(15);
+        const uintptr_t e = reinterpret_cast<uintptr_t>(g) + len;  // blocks at or past e are not loaded
+        wlo = p;
+        sh = static_cast<uint32_t>(a - A);
+        const uint4* src = reinterpret_cast<const uint4*>(A);
+        uint4* dst = reinterpret_cast<uint4*>(w);
+        constexpr uint32_t nb = kInWin / 16;
+        uint4 v[nb / kWave];
+#pragma unroll
+        for (uint32_t k = 0; k < nb / kWave; k++) {
+            const uint32_t b = lane() + k * kWave;
+            v[k] = A + 16u * b < e ? src[b] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < nb / kWave; k++) dst[lane() + k * kWave] = v[k];
+        if (lane() < 2) dst[nb + lane()] = make_uint4(0u, 0u, 0u, 0u);
+        wsync();
+    }
+    // bytes [p, p + k) staged (k <= 16)
+    __device__ __forceinline__ void ensure(uint32_t p, uint32_t k) {
+        if (p < wlo || p + k + sh > wlo + kInWin) refill(p);
+    }
+    __device__ __forceinline__ uint32_t at(uint32_t p) const { return min(p - wlo + sh, kInWin + 16u); }
+    __device__ __forceinline__ uint32_t byte(uint32_t p) const { return w[at(p)]; }
+    __device__ __forceinline__ uint32_t u16le(uint32_t p) const { return byte(p) | (byte(p + 1) << 8); }
+    __device__ __forceinline__ uint32_t u32le(uint32_t p) const {
+        return byte(p) | (byte(p + 1) << 8) | (byte(p + 2) << 16) | (byte(p + 3) << 24);
+    }
+    __device__ __forceinline__ uint32_t u32be(uint32_t p) const {
+        return (byte(p) << 24) | (byte(p + 1) << 16) | (byte(p + 2) << 8) | byte(p + 3);
+    }
+};
+
+enum : uint32_t { ST_OK = 0, ST_CORRUPT = 1, ST_SIZE = 2, ST_UNSUPPORTED = 3 };
+
+// ── output ring ────────────────────────────────────────────────────────────
+struct Out {
+    uint8_t* ring;
+    uint8_t* dst;   // the page slot (16-byte aligned)
+    uint32_t op;    // bytes produced
+    uint32_t fl;    // bytes flushed to dst (multiple of 16 until the end)
+    uint32_t cap;   // bytes the slot's payload holds
+    uint32_t vbase; // first byte of the decompressed stream (after a V2 prologue)
+    uint32_t st;    // ST_*
+    __device__ void flush(bool final) {
+        while (op - fl >= kFlush || (final && fl < op)) {
+            const uint32_t n = min(kFlush, op - fl);
+            const uint32_t b = fl + 16u * lane();
+            if (b < fl + n) {
+                uint4 v = *reinterpret_cast<const uint4*>(ring + (b & kRingMask));
+                if (b + 16 > op) {  // bytes past the payload stay zero (slot padding)
+                    const int32_t keep = static_cast<int32_t>(op - b);
+                    auto mk = [&](int j) -> uint32_t {
+                        const int32_t kb = keep - 4 * j;
+                        return kb >= 4 ? 0xFFFFFFFFu : (kb <= 0 ? 0u : ((1u << (8 * kb)) - 1u));
+                    };
+                    v = make_uint4(v.x & mk(0), v.y & mk(1), v.z & mk(2), v.w & mk(3));
+                }
+                *reinterpret_cast<uint4*>(dst + b) = v;
+            }
+            fl += n;
+            wsync();
+        }
+    }
+    __device__ __forceinline__ bool room(uint32_t n) {
+        if (op + n > cap || op + n < op) { st = ST_SIZE; return false; }
+        return true;
+    }
+    // literal bytes [p, p + n) of the input
+    __device__ void lit(In& I, uint32_t p, uint32_t n) {
+        if (!room(n)) return;
+        for (uint32_t d = 0; d < n; d += kWave) {
+            I.ensure(p + d, kWave);
+            const uint32_t m = min(static_cast<uint32_t>(kWave), n - d);
+            if (lane() < m) ring[(op + lane()) & kRingMask] = static_cast<uint8_t>(I.byte(p + d + lane()));
+            op += m;
+            wsync();
+            if (op - fl >= kFlush) flush(false);
+        }
+    }
+    // copy of n bytes from distance d: 64 bytes per step, byte c0 + j of a
+    // step from c0 - d + (j mod d) (d < 64) or c0 - d + j: before c0, final
+    __device__ void copy(uint32_t d, uint32_t n) {
+        if (d == 0 || d > op - vbase || d > kRing - 1) { st = ST_CORRUPT; return; }
+        if (!room(n)) return;
+        const uint32_t r = d >= static_cast<uint32_t>(kWave) ? lane() : lane() % d;
+        for (uint32_t k = 0; k < n; k += kWave) {
+            const uint32_t m = min(static_cast<uint32_t>(kWave), n - k);
+            if (lane() < m) {
+                const uint32_t v = ring[(op - d + r) & kRingMask];
+                ring[(op + lane()) & kRingMask] = static_cast<uint8_t>(v);
+            }
+            op += m;
+            wsync();
+            if (op - fl >= kFlush) flush(false);
+        }
+    }
+    __device__ __forceinline__ void put1(uint32_t b) {
+        if (!room(1)) return;
+        if (lane() == 0) ring[op & kRingMask] = static_cast<uint8_t>(b);
+        op++;
+        if (op - fl >= kFlush) {
+            wsync();
+            flush(false);
+        }
+    }
+    __device__ void put_u32(uint32_t v) {
+        if (!room(4)) return;
+        if (lane() < 4) ring[(op + lane()) & kRingMask] = static_cast<uint8_t>(v >> (8 * lane()));
+        wsync();
+        op += 4;
+        flush(false);
+    }
+};
+
+// ── SNAPPY ─────────────────────────────────────────────────────────────────
+__device__ void snappy(In& I, Out& O, uint32_t p, uint32_t end, uint32_t expect) {
+    uint32_t ulen = 0;
+    I.ensure(p, 8);
+    for (uint32_t k = 0;; k++) {
+        if (k == 5 || p >= end) { O.st = ST_CORRUPT; return; }
+        const uint32_t b = I.byte(p++);
+        ulen |= (b & 0x7Fu) << (7 * k);
+        if (!(b & 0x80u)) break;
+    }
+    if (ulen != expect) { O.st = ST_SIZE; return; }
+    while (p < end && O.st == ST_OK) {
+        I.ensure(p, 8);
+        const uint32_t t = uni(I.byte(p));
+        const uint32_t ty = t & 3u;
+        if (ty == 0) {
+            uint32_t n = (t >> 2) + 1;
+            p += 1;
+            if (n > 60) {
+                const uint32_t nb = n - 60;
+                const uint32_t x = I.u32le(p);
+                n = (nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u))) + 1;
+                p += nb;
+            }
+            n = uni(n);
+            if (p > end || n > end - p || n == 0) { O.st = ST_CORRUPT; return; }
+            O.lit(I, p, n);
+            p += n;
+        } else {
+            uint32_t n, d;
+            if (ty == 1) {
+                n = 4 + ((t >> 2) & 7u);
+                d = ((t >> 5) << 8) | I.byte(p + 1);
+                p += 2;
+            } else if (ty == 2) {
+                n = (t >> 2) + 1;
+                d = I.u16le(p + 1);
+                p += 3;
+            } else {
+                n = (t >> 2) + 1;
+                d = I.u32le(p + 1);
+                p += 5;
+            }
+            if (p > end) { O.st = ST_CORRUPT; return; }
+            O.copy(uni(d), uni(n));
+        }
+    }
+    if (O.st == ST_OK && O.op - O.vbase != expect) O.st = ST_SIZE;
+}
+
+// ── LZ4 block ──────────────────────────────────────────────────────────────
+__device__ void lz4_block(In& I, Out& O, uint32_t p, uint32_t end) {
+    for (;;) {
+        if (p >= end) { O.st = ST_CORRUPT; return; }
+        I.ensure(p, 1);
+        const uint32_t tok = uni(I.byte(p++));
+        uint32_t n = tok >> 4;
+        if (n == 15) {
+            uint32_t b;
+            do {
+                if (p >= end) { O.st = ST_CORRUPT; return; }
+                I.ensure(p, 1);
+                b = uni(I.byte(p++));
+                n += b;
+            } while (b == 255);
+        }
+        if (n > end - p) { O.st = ST_CORRUPT; return; }
+        if (n) O.lit(I, p, n);
+        if (O.st != ST_OK) return;
+        p += n;
+        if (p == end) return;  // the last sequence holds literals only
+        if (end - p < 2) { O.st = ST_CORRUPT; return; }
+        I.ensure(p, 2);
+        const uint32_t d = uni(I.u16le(p));
+        p += 2;
+        uint32_t m = tok & 15u;
+        if (m == 15) {
+            uint32_t b;
+            do {
+                if (p >= end) { O.st = ST_CORRUPT; return; }
+                I.ensure(p, 1);
+                b = uni(I.byte(p++));
+                m += b;
+            } while (b == 255);
+        }
+        O.copy(d, m + 4);
+        if (O.st != ST_OK) return;
+    }
+}
+
+// Hadoop framing (codec LZ4): blocks of [u32 BE raw bytes][u32 BE packed bytes][LZ4 block].
+__device__ void lz4_hadoop(In& I, Out& O, uint32_t p, uint32_t end) {
+    while (p < end && O.st == ST_OK) {
+        if (end - p < 8) { O.st = ST_CORRUPT; return; }
+        I.ensure(p, 8);
+        const uint32_t raw = uni(I.u32be(p)), packed = uni(I.u32be(p + 4));
+        p += 8;
+        if (packed > end - p) { O.st = ST_CORRUPT; return; }
+        const uint32_t o0 = O.op;
+        lz4_block(I, O, p, p + packed);
+        if (O.st == ST_OK && O.op - o0 != raw) O.st = ST_SIZE;
+        p += packed;
+    }
+}
+
+// ── DEFLATE ────────────────────────────────────────────────────────────────
+__constant__ uint16_t kLBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                    35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t kLExt[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t kDBase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
+                                    193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t kDExt[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct Bits {
+    uint64_t buf;
+    uint32_t cnt, p, end;
+    uint32_t pad;  // zero bytes supplied past the input end (a valid stream never consumes them)
+    __device__ __forceinline__ void need(In& I, uint32_t n) {
+        while (cnt < n) {
+            if (p >= end) {
+                pad++;
+                cnt += 8;
+                continue;
+            }
+            I.ensure(p, 4);
+            const uint32_t k = min(4u, end - p);
+            uint32_t v = I.u32le(p);
+            if (k < 4) v &= (1u << (8 * k)) - 1u;
+            buf |= static_cast<uint64_t>(v) << cnt;
+            cnt += 8 * k;
+            p += k;
+        }
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t n) const { return static_cast<uint32_t>(buf) & ((1u << n) - 1u); }
+    __device__ __forceinline__ void drop(uint32_t n) { buf >>= n; cnt -= n; }
+    __device__ __forceinline__ uint32_t take(In& I, uint32_t n) {
+        if (n == 0) return 0;
+        need(I, n);
+        const uint32_t v = peek(n);
+        drop(n);
+        return v;
+    }
+    // bits consumed past the input end
+    __device__ __forceinline__ bool overrun() const {
+        return 8ull * (static_cast<uint64_t>(p) + pad) - cnt > 8ull * end;
+    }
+    // byte position of the next unread bit (after dropping to a byte
+    // boundary); > end when the stream consumed bits it does not have
+    __device__ __forceinline__ uint32_t align_byte() {
+        drop(cnt & 7u);
+        const uint32_t q = p + pad - cnt / 8;
+        buf = 0;
+        cnt = 0;
+        pad = 0;
+        p = q;
+        return q;
+    }
+};
+
+// Canonical Huffman code over lens[base, base + n): counts, codes, symbols
+// in code order, and the kFast-bit lookup table.  Returns false for an
+// over-subscribed code.
+__device__ bool build_code(CodecLds& L, int which, uint32_t base, uint32_t n, uint16_t* table) {
+    uint16_t* cnt = L.cnt[which];
+    if (lane() < 16) cnt[lane()] = 0;
+    wsync();
+    if (lane() == 0) {
+        for (uint32_t s = 0; s < n; s++) cnt[L.lens[base + s]]++;
+        cnt[0] = 0;
+        uint16_t* next = L.nxt;
+        uint16_t* offs = L.offs;
+        int32_t left = 1;
+        uint32_t code = 0, idx = 0;
+        bool bad = false;
+        for (uint32_t l = 1; l < 16; l++) {
+            left = (left << 1) - cnt[l];
+            bad |= left < 0;
+            code = (code + (l > 1 ? cnt[l - 1] : 0u)) << 1;
+            next[l] = static_cast<uint16_t>(code);
+            offs[l] = static_cast<uint16_t>(idx);
+            idx += cnt[l];
+        }
+        for (uint32_t s = 0; s < n; s++) {
+            const uint32_t l = L.lens[base + s];
+            if (l) {
+                L.code[base + s] = next[l]++;
+                L.sym[base + offs[l]++] = static_cast<uint16_t>(s);
+            }
+        }
+        L.scratch[which] = bad ? 1u : 0u;
+    }
+    for (uint32_t i = lane(); i < (1u << kFast); i += kWave) table[i] = 0;
+    wsync();
+    for (uint32_t s = lane(); s < n; s += kWave) {
+        const uint32_t l = L.lens[base + s];
+        if (l == 0 || l > kFast) continue;
+        const uint32_t rev = __builtin_bitreverse32(L.code[base + s]) >> (32 - l);
+        const uint16_t e = static_cast<uint16_t>((s << 4) | l);
+        for (uint32_t k = 0; k < (1u << (kFast - l)); k++) table[rev | (k << l)] = e;
+    }
+    wsync();
+    return uni(L.scratch[which]) == 0;
+}
+
+// One Huffman symbol: the lookup table, else the canonical bit-serial walk.
+__device__ int32_t decode_sym(CodecLds& L, In& I, Bits& B, const uint16_t* table, int which, uint32_t base) {
+    B.need(I, 15);
+    const uint32_t e = uni(table[B.peek(kFast)]);
+    if (e & 15u) {
+        B.drop(e & 15u);
+        return static_cast<int32_t>(e >> 4);
+    }
+    const uint16_t* cnt = L.cnt[which];
+    int32_t code = 0, first = 0, index = 0;
+    for (uint32_t l = 1; l < 16; l++) {
+        code |= static_cast<int32_t>(B.peek(1));
+        B.drop(1);
+        const int32_t c = cnt[l];
+        if (code - c < first) return static_cast<int32_t>(uni(L.sym[base + static_cast<uint32_t>(index + code - first)]));
+        index += c;
+        first = (first + c) << 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+__device__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
+    for (;;) {
+        const uint32_t fin = B.take(I, 1);
+        const uint32_t ty = B.take(I, 2);
+        if (ty == 0) {  // stored
+            uint32_t q = B.align_byte();
+            if (q > B.end || B.end - q < 4) { O.st = ST_CORRUPT; return; }
+            I.ensure(q, 4);
+            const uint32_t n = uni(I.u16le(q)), nn = uni(I.u16le(q + 2));
+            q += 4;
+            if ((n ^ 0xFFFFu) != nn || n > B.end - q) { O.st = ST_CORRUPT; return; }
+            if (n) O.lit(I, q, n);
+            B.p = q + n;
+        } else if (ty == 1 || ty == 2) {
+            uint32_t nl = 288, nd = 30;
+            if (ty == 1) {
+                for (uint32_t s = lane(); s < 320; s += kWave)
+                    L.lens[s] = s < 144 ? 8 : (s < 256 ? 9 : (s < 280 ? 7 : (s < 288 ? 8 : 5)));
+                wsync();
+            } else {
+                nl = B.take(I, 5) + 257;
+                nd = B.take(I, 5) + 1;
+                const uint32_t nc = B.take(I, 4) + 4;
+                if (nl > 286 || nd > 30) { O.st = ST_CORRUPT; return; }
+                // code-length code (lengths in kClOrder), built in the distance slots
+                for (uint32_t s = lane(); s < 19; s += kWave) L.lens[288 + s] = 0;
+                wsync();
+                for (uint32_t k = 0; k < nc; k++) {
+                    const uint32_t v = B.take(I, 3);
+                    if (lane() == 0) L.lens[288 + kClOrder[k]] = static_cast<uint8_t>(v);
+                }
+                wsync();
+                if (!build_code(L, 1, 288, 19, L.dt)) { O.st = ST_CORRUPT; return; }
+                uint32_t i = 0, prev = 0;
+                while (i < nl + nd) {
+                    const int32_t sy = decode_sym(L, I, B, L.dt, 1, 288);
+                    uint32_t rep = 1, val = 0;
+                    if (sy < 0) { O.st = ST_CORRUPT; return; }
+                    if (sy < 16) {
+                        val = static_cast<uint32_t>(sy);
+                        prev = val;
+                    } else if (sy == 16) {
+                        if (i == 0) { O.st = ST_CORRUPT; return; }
+                        val = prev;
+                        rep = 3 + B.take(I, 2);
+                    } else if (sy == 17) {
+                        rep = 3 + B.take(I, 3);
+                    } else {
+                        rep = 11 + B.take(I, 7);
+                    }
+                    if (i + rep > nl + nd) { O.st = ST_CORRUPT; return; }
+                    // lengths i .. i + rep: litlen [0, nl) -> lens[0 ..], dist -> lens[288 ..] (after the
+                    // code-length table is no longer needed: written into a staging copy first)
+                    for (uint32_t k = lane(); k < rep; k += kWave) {
+                        const uint32_t j = i + k;
+                        // the code-length code lives in lens[288, 307): distance lengths go to
+                        // sym[] (free until build_code) and are moved after the loop
+                        if (j < nl) L.lens[j] = static_cast<uint8_t>(val);
+                        else L.sym[j - nl] = static_cast<uint16_t>(val);
+                    }
+                    wsync();
+                    i += rep;
+                }
+                for (uint32_t s = lane(); s < 288; s += kWave)
+                    if (s >= nl) L.lens[s] = 0;
+                for (uint32_t s = lane(); s < 32; s += kWave) L.lens[288 + s] = s < nd ? static_cast<uint8_t>(L.sym[s]) : 0;
+                wsync();
+                if (L.lens[256] == 0) { O.st = ST_CORRUPT; return; }
+            }
+            if (!build_code(L, 0, 0, 288, L.lt) || !build_code(L, 1, 288, 32, L.dt)) {
+                O.st = ST_CORRUPT;
+                return;
+            }
+            for (;;) {
+                const int32_t sy = decode_sym(L, I, B, L.lt, 0, 0);
+                if (sy < 0 || sy > 285) { O.st = ST_CORRUPT; return; }
+                if (sy < 256) {
+                    O.put1(static_cast<uint32_t>(sy));
+                } else if (sy == 256) {
+                    break;
+                } else {
+                    const uint32_t li = static_cast<uint32_t>(sy) - 257;
+                    const uint32_t n = kLBase[li] + B.take(I, kLExt[li]);
+                    const int32_t ds = decode_sym(L, I, B, L.dt, 1, 288);
+                    if (ds < 0 || ds > 29) { O.st = ST_CORRUPT; return; }
+                    const uint32_t d = kDBase[ds] + B.take(I, kDExt[ds]);
+                    wsync();
+                    O.copy(uni(d), uni(n));
+                }
+                if (O.st != ST_OK || B.overrun()) {
+                    if (O.st == ST_OK) O.st = ST_CORRUPT;
+                    return;
+                }
+            }
+            wsync();
+        } else {
+            O.st = ST_CORRUPT;
+            return;
+        }
+        if (O.st != ST_OK || B.overrun()) {
+            if (O.st == ST_OK) O.st = ST_CORRUPT;
+            return;
+        }
+        if (fin) return;
+    }
+}
+
+// GZIP members (RFC 1952) or one zlib stream (RFC 1950).
+__device__ void gzip(CodecLds& L, In& I, Out& O, uint32_t p, uint32_t end) {
+    bool first = true;
+    while (O.st == ST_OK && (first || p < end)) {
+        if (end - p < 2) { O.st = ST_CORRUPT; return; }
+        I.ensure(p, 16);
+        const uint32_t b0 = I.byte(p), b1 = I.byte(p + 1);
+        const uint32_t o0 = O.op;
+        bool zlib = false;
+        if (b0 == 0x1f && b1 == 0x8b) {
+            if (end - p < 18 || I.byte(p + 2) != 8) { O.st = ST_CORRUPT; return; }
+            const uint32_t flg = I.byte(p + 3);
+            p += 10;
+            if (flg & 4) {
+                I.ensure(p, 2);
+                p += 2 + I.u16le(p);
+            }
+            for (uint32_t f = 8; f <= 16; f <<= 1) {
+                if (!(flg & f)) continue;
+                for (;;) {  // zero-terminated name / comment
+                    if (p >= end) { O.st = ST_CORRUPT; return; }
+                    I.ensure(p, 1);
+                    if (I.byte(p++) == 0) break;
+                }
+            }
+            if (flg & 2) p += 2;
+        } else if (first && (b0 & 0x0f) == 8 && ((b0 << 8) | b1) % 31 == 0 && !(b1 & 0x20)) {
+            zlib = true;
+            p += 2;
+        } else {
+            O.st = ST_CORRUPT;
+            return;
+        }
+        if (p > end) { O.st = ST_CORRUPT; return; }
+        Bits B{0ull, 0u, p, end, 0u};
+        inflate(L, I, O, B);
+        if (O.st != ST_OK) return;
+        p = B.align_byte();
+        const uint32_t tail = zlib ? 4u : 8u;
+        if (p > end || end - p < tail) { O.st = ST_CORRUPT; return; }
+        if (!zlib) {
+            I.ensure(p, 8);
+            if (I.u32le(p + 4) != O.op - o0) { O.st = ST_SIZE; return; }
+        }
+        p += tail;
+        first = false;
+        if (zlib) break;
+    }
+}
+
+__global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src, uint8_t* __restrict__ img,
+                                                 const CodecEntry* __restrict__ ent, int32_t n,
+                                                 uint32_t* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    CodecLds& L = *reinterpret_cast<CodecLds*>(smem);
+    for (int32_t i = static_cast<int32_t>(blockIdx.x); i < n; i += static_cast<int32_t>(gridDim.x)) {
+        const CodecEntry e = ent[i];
+        In I{src + e.src, e.src_len, 0u, 0u, L.in};
+        I.refill(0);
+        Out O{L.ring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
+        uint32_t p = 0;
+        if (e.flags & kCodecV2) {  // level sections, as is, behind their V1 length prefixes
+            const uint32_t lv = e.def_len + e.rep_len;
+            if (lv > e.src_len) O.st = ST_CORRUPT;
+            // V2 pages hold repetition then definition levels; the reference reads
+            // [u32 def_len][def][u32 rep_len][rep] (column_reader.cpp:146-170)
+            if (O.st == ST_OK && (e.flags & kCodecDefPrefix)) {
+                O.put_u32(e.def_len);
+                if (O.st == ST_OK && e.def_len) O.lit(I, e.rep_len, e.def_len);
+            }
+            if (O.st == ST_OK && (e.flags & kCodecRepPrefix)) {
+                O.put_u32(e.rep_len);
+                if (O.st == ST_OK && e.rep_len) O.lit(I, 0, e.rep_len);
+            }
+            p = lv;
+        }
+        O.vbase = O.op;
+        const uint32_t end = e.src_len;
+        const uint32_t expect = e.out_len - O.op;
+        if (O.st == ST_OK) {
+            switch (e.codec) {
+                case 0: O.lit(I, p, end - p); break;
+                case 1: snappy(I, O, p, end, expect); break;
+                case 2: gzip(L, I, O, p, end); break;
+                case 5: lz4_hadoop(I, O, p, end); break;
+                case 7: lz4_block(I, O, p, end); break;
+                default: O.st = ST_UNSUPPORTED;
+            }
+        }
+        if (O.st == ST_OK && O.op != e.out_len) O.st = ST_SIZE;
+        if (O.st == ST_OK) O.flush(true);
+        if (lane() == 0) status[i] = O.st;
+        wsync();
+    }
+}
+
+}  // namespace
+
+size_t codec_lds_bytes() { return sizeof(CodecLds); }
+
+void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
+                  uint32_t* status, int cus) {
+    if (n <= 0) return;
+    const uint32_t lds = static_cast<uint32_t>(sizeof(CodecLds));
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_codec), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds));
+        attr = true;
+    }
+    const int per_cu = std::max(1, static_cast<int>((160u * 1024u) / lds));
+    const int grid = std::min(n, std::max(1, cus) * per_cu);
+    hipLaunchKernelGGL(k_codec, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
+}
+
+}  // namespace pqk

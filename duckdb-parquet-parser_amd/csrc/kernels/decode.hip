@@ -537,6 +537,13 @@ __global__ void __launch_bounds__(256) k_fixed(const uint8_t* __restrict__ bytes
     Rle ix;
     uint32_t dict_n = 0;
     Src ds{nullptr, nullptr, 0};
+    if (mode == MODE_BOOL_RLE) {  // [u32 len][hybrid RLE/bit-packed, bit width 1]
+        if (pos + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); return; }
+        const uint32_t bl = src_u32(s, pos);
+        pos += 4;
+        if (static_cast<uint64_t>(pos) + bl > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, bl, size); return; }
+        rle_init(ix, pos, bl, 1);
+    }
     if (mode == MODE_DICT) {
         if (pos + 1 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 1, size); return; }
         uint32_t bw = src_byte(s, pos);
@@ -568,7 +575,7 @@ __global__ void __launch_bounds__(256) k_fixed(const uint8_t* __restrict__ bytes
         }
         if (rc == 0 && dict && above) rc = PQ_ERR_UNSUPPORTED;
         if (rc) { set_err(err, err_any, rc, 0, 0, size); return; }
-        if (dict) {
+        if (dict || mode == MODE_BOOL_RLE) {
             rc = rle_decode(ix, s, nn, [&](uint32_t j, uint32_t v) { L.a[j] = v; });
             if (rc) { set_err(err, err_any, rc, 0, 0, size); return; }
         } else if (nn > 0) {
@@ -614,6 +621,8 @@ __global__ void __launch_bounds__(256) k_fixed(const uint8_t* __restrict__ bytes
                         if (cp.type == PQ_BOOLEAN) w[0] = src_byte(ds, at) != 0;
                         else for (uint32_t q = 0; q < (W + 3) / 4; q++) w[q] = src_u32(ds, at + 4 * q);
                     }
+                } else if (mode == MODE_BOOL_RLE) {
+                    w[0] = L.a[k] & 1u;
                 } else if (mode == MODE_BOOL) {
                     uint32_t kk = rank_base + k;
                     w[0] = (src_byte(s, pos + kk / 8) >> (kk % 8)) & 1u;

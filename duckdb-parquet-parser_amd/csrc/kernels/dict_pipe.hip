@@ -78,7 +78,8 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
                                                               int32_t max_def, int32_t max_rep,
                                                               uint2* __restrict__ runs,
                                                               uint32_t* __restrict__ info, int ppw,
-                                                              int32_t* __restrict__ flist, uint32_t stage_max) {
+                                                              int32_t* __restrict__ flist, uint32_t stage_max,
+                                                              int debug) {
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[kRunWaves][kRunStage / 4 + 8];
     const uint32_t wv = threadIdx.x / kWave;
     const int g0 = (blockIdx.x * kRunWaves + static_cast<int>(wv)) * ppw;
@@ -153,6 +154,11 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
             W.bw = s ? bwi : level_bw(max_def);
             W.n = n;
             W.out = runs + (static_cast<size_t>(p) * 2 + s) * kPipeRunCap;
+            W.stride = (debug & 0x1000) ? 0u : 1u;  // timing probes: no record stores
+            if (debug & 0x4000) {                    // timing probe: lane-interleaved records
+                W.out = runs + static_cast<size_t>(g0) * 2 * kPipeRunCap + lane();
+                W.stride = kWave;
+            }
             W.cap = kPipeRunCap;
             W.sbase = sbase;
             W.gp = gp;
@@ -1600,13 +1606,13 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
-                      bool) {
+                      int debug) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     if (npages <= 0) return;
     const int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
     const int per = kRunWaves * ppw;
     hipLaunchKernelGGL(k_pipe_runs, dim3((npages + per - 1) / per), dim3(kRunWaves * kWave), 0, s, bytes, pages,
-                       npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16);
+                       npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16, debug);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's

@@ -11,7 +11,9 @@ constexpr int kWave = 64;
 constexpr int kTileRows = 512;        // rows per decode tile (ref-layout page = 1 tile)
 constexpr uint32_t kNullCode = 0xFFFFFFFFu;
 
-enum PageMode : int32_t { MODE_DICT = 0, MODE_PLAIN = 1, MODE_BOOL = 2 };
+// MODE_BOOL_RLE: BOOLEAN values in the RLE encoding ([u32 len][hybrid stream,
+// bit width 1]; DATA_PAGE_V2 writers use it), extended walks only
+enum PageMode : int32_t { MODE_DICT = 0, MODE_PLAIN = 1, MODE_BOOL = 2, MODE_BOOL_RLE = 3 };
 
 // One data page, as the kernels see it (32 B, HBM-resident).
 struct DevPage {
@@ -57,6 +59,23 @@ struct RelayoutEntry {
     uint32_t slot;   // slot bytes (multiple of 16): avail..slot are zero-filled
 };
 void launch_relayout(hipStream_t s, const uint8_t* raw, uint8_t* img, const RelayoutEntry* ent, int32_t n);
+
+// One compressed or DATA_PAGE_V2 payload → its slot (codec.hip).
+enum : uint32_t { kCodecV2 = 1, kCodecDefPrefix = 2, kCodecRepPrefix = 4 };
+struct CodecEntry {
+    uint64_t src;      // payload offset in the source buffer (raw chunk bytes)
+    uint64_t dst;      // slot offset in the image (16-byte aligned)
+    uint32_t src_len;  // compressed_page_size (cut at EOF)
+    uint32_t out_len;  // payload bytes the slot receives (V1 layout)
+    uint32_t def_len;  // V2: definition / repetition level bytes
+    uint32_t rep_len;
+    uint32_t codec;    // 0: values stored as is (V2, is_compressed = false), else CompressionCodec
+    uint32_t flags;    // kCodec*
+};
+size_t codec_lds_bytes();
+// status[i]: 0 ok, 1 corrupt input, 2 size mismatch, 3 unsupported
+void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
+                  uint32_t* status, int cus);
 
 // 4 KiB chunker (chunker.hip, src/main.cpp:17-32): device scratch bytes for
 // n rows, and the launch sequence (synchronises the stream; 0 = OK).
@@ -149,7 +168,7 @@ struct PipePlan {
 };
 PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw);
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
-                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist, bool);
+                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist, int debug);
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,

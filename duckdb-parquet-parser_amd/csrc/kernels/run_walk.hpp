@@ -14,6 +14,7 @@ namespace dev {
 struct RunWalk {
     bool alive;
     uint32_t q, end, bw, n, sbase, cap;
+    uint32_t stride;  // record stride in uint2 (1: contiguous per stream)
     uint2* out;
     const uint8_t* gp;
 };
@@ -68,7 +69,7 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
         const uint32_t rx = cnt | ((exh ? left : c) << 16);
         const uint32_t pl = lit ? (litpay | (qh * litmul)) : (vraw & vmask);
         const uint32_t ry = exh ? 0u : pl;
-        if (ok) W.out[nr] = make_uint2(rx, ry);
+        if (ok && W.stride) W.out[static_cast<size_t>(nr) * W.stride] = make_uint2(rx, ry);
         fl |= (alive ? 1u : 0u) & (ok ^ 1u);
         nr += ok;
         const uint64_t nql = static_cast<uint64_t>(qh) + static_cast<uint64_t>(g) * W.bw;

@@ -15,8 +15,10 @@ from . import _paths
 
 PQ_ERRORS = {
     -1: "CODEC", -2: "BUFFER", -3: "OPTIONAL", -4: "FLBA", -5: "TYPE", -6: "THRIFT",
-    -7: "ALLOC", -8: "UNSUPPORTED", -20: "ARG", -21: "HIP", -22: "REGEX",
+    -7: "ALLOC", -8: "UNSUPPORTED", -9: "DECOMPRESS", -20: "ARG", -21: "HIP", -22: "REGEX",
 }
+EXT_CODECS, EXT_PAGE_V2 = 1, 2          # pq_chunk_desc.ext_flags
+PAGE_COMPRESSED, PAGE_V2 = 1, 2         # pq_page_desc.flags (codec in bits 8..15)
 BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FLBA = range(8)
 WIDTH = {BOOLEAN: 1, INT32: 4, FLOAT: 4, INT64: 8, DOUBLE: 8, INT96: 12}
 
@@ -39,6 +41,8 @@ class ChunkDesc(C.Structure):
         ("max_def_level", C.c_int16),
         ("max_rep_level", C.c_int16),
         ("total_compressed_size", C.c_int64),
+        ("ext_flags", C.c_int32),
+        ("ext_reserved", C.c_int32),
     ]
 
 
@@ -53,6 +57,10 @@ class PageDesc(C.Structure):
         ("page_num", C.c_int32),
         ("dict_page", C.c_int32),
         ("first_row", C.c_int64),
+        ("uncompressed_size", C.c_int32),
+        ("flags", C.c_int32),
+        ("v2_def_len", C.c_int32),
+        ("v2_rep_len", C.c_int32),
     ]
 
 

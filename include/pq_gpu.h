@@ -43,6 +43,7 @@ enum {
     PQ_ERR_THRIFT = -6,       /* ThriftReader::skip unknown type / "varint too long"                      */
     PQ_ERR_ALLOC = -7,        /* negative sizes (std::vector length_error / bad_alloc)                    */
     PQ_ERR_UNSUPPORTED = -8,  /* input outside the parity scope (reference behaviour undefined)          */
+    PQ_ERR_DECOMPRESS = -9,   /* extended mode: a compressed page failed to decompress (corrupt input)    */
     PQ_ERR_ARG = -20,         /* bad argument to this API                                                 */
     PQ_ERR_HIP = -21,         /* HIP runtime failure / no device                                          */
     PQ_ERR_REGEX = -22        /* pattern outside the supported RE2/Python-re subset                       */
@@ -69,7 +70,22 @@ typedef struct {
     int64_t total_compressed_size; /* ColumnMetaData.total_compressed_size, or 0 if unknown:
                                       only an extent hint (chunks of >= 1 MiB walk their
                                       page chain speculatively on host threads) */
+    int32_t ext_flags;      /* 0 (pq_file_chunk's default): the reference's format scope.
+                               PQ_EXT_* bits widen it beyond the reference */
+    int32_t ext_reserved;   /* 0 */
 } pq_chunk_desc;
+
+/* pq_chunk_desc.ext_flags.  The reference rejects every compression codec
+ * ("Only uncompressed parquet files are supported", column_reader.cpp:13-15)
+ * and walks past DATA_PAGE_V2 pages without counting them (56-67).  With
+ *   PQ_EXT_CODECS   pages of SNAPPY (1), GZIP (2), LZ4 (5, Hadoop framing) and
+ *                   LZ4_RAW (7) chunks are decompressed on the GPU at upload;
+ *   PQ_EXT_PAGE_V2  DATA_PAGE_V2 pages count as data pages: their level
+ *                   sections and (decompressed) values are rebuilt on the GPU
+ *                   into the V1 layout the reference reads
+ *                   ([u32 def_len][def][u32 rep_len][rep][values]).
+ * Outputs are checked against pyarrow. */
+enum { PQ_EXT_CODECS = 1, PQ_EXT_PAGE_V2 = 2 };
 
 /* One page of the walk (dictionary, data and skipped pages alike). */
 typedef struct {
@@ -82,7 +98,17 @@ typedef struct {
     int32_t page_num;        /* ColumnReader::read_pages page_num                  */
     int32_t dict_page;       /* index of the dictionary page in force, or -1       */
     int64_t first_row;       /* data pages: first output row                       */
+    int32_t uncompressed_size; /* PageHeader.uncompressed_page_size                 */
+    int32_t flags;           /* PQ_PAGE_* (extended walks only)                    */
+    int32_t v2_def_len;      /* DATA_PAGE_V2 level section bytes                   */
+    int32_t v2_rep_len;
 } pq_page_desc;
+
+/* pq_page_desc.flags.  PQ_PAGE_COMPRESSED: the payload (V2: its values
+ * section) is compressed with the chunk's codec, held in bits 8..15.  PQ_PAGE_V2: a DATA_PAGE_V2
+ * page of an extended walk; it is listed with page_type PQ_DATA_PAGE because
+ * the device holds it in the V1 layout. */
+enum { PQ_PAGE_COMPRESSED = 1, PQ_PAGE_V2 = 2 };
 
 /* Device-resident columnar result (SURVEY §8b "pq_column_out"):
  *   validity  LSB-first bitmap, bit i = row i non-null; ceil(n/32) words

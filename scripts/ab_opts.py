@@ -49,7 +49,10 @@ for rnd in range(3):
         for k, x in parsed[i].items():
             ctx.set_option(k, x)
         dc = ctx.upload(f, [F.chunk(0, ci)])
-        dc.decode()
+        try:
+            dc.decode()
+        except capi.PqError as e:  # timing probes (debug bits) may leave invalid output
+            print(f"variant {variants[i]}: {e}", file=sys.stderr)
         if rnd == 0:
             h = dc.to_host()
             if i == 0:

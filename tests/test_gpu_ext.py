@@ -1,0 +1,129 @@
+"""GPU parity for the extended format scope: compressed
+pages (SNAPPY, GZIP, LZ4_RAW; codec.hip) and DATA_PAGE_V2 pages, decoded
+through the C ABI with PQ_EXT_* flags and compared bit for bit with pyarrow's
+reading of the same file (the oracle for this row; the reference decodes
+neither).  Expectations: tests/golden/ext/manifest.json (make_ext.py)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from ext_util import EXT_ALL, ext_chunks, load, manifest, sha
+from pqgpu import capi
+
+pytestmark = pytest.mark.gpu
+MAN = manifest()
+FILES = sorted(MAN["files"])
+COLS = ["s_dict", "s_plain", "i64", "f64", "i32d", "b"]
+
+
+def decode(ctx, f, col, flags=EXT_ALL):
+    dc = ctx.upload(f, ext_chunks(f, col, flags))
+    try:
+        dc.decode()
+        return dc.to_host()
+    finally:
+        dc.free()
+
+
+@pytest.mark.parametrize("name", FILES)
+@pytest.mark.parametrize("ci", range(len(COLS)))
+def test_ext_decode_matches_pyarrow(ctx, name, ci):
+    f = load(name)
+    got = capi.canonical_dump(decode(ctx, f, ci))
+    exp = MAN["files"][name]["columns"][COLS[ci]]
+    assert len(got) == exp["len"] and sha(got) == exp["sha256"], (name, COLS[ci])
+
+
+@pytest.mark.parametrize("version", ["1", "2"])
+def test_ext_regex_same_across_codecs(ctx, version):
+    """The regex page filter on a compressed chunk equals the one on the
+    uncompressed file (same table, same page boundaries)."""
+    for pattern, neg in (("^[a-d][a-e]", False), ("q", True), ("x.*y", False)):
+        base = None
+        for codec in ("none", "snappy", "gzip", "lz4"):
+            f = load(f"ext_{codec}_v{version}.parquet")
+            dc = ctx.upload(f, ext_chunks(f, 1))
+            try:
+                flags = dc.regex_pages(pattern, neg)
+            finally:
+                dc.free()
+            if base is None:
+                base = flags
+                assert len(flags) > 8
+            else:
+                assert np.array_equal(flags, base), (pattern, codec)
+
+
+def test_ext_repeat_uploads(ctx):
+    """The codec pass reuses its context buffers across uploads of different sizes."""
+    for name in ("ext_gzip_v1.parquet", "ext_snappy_v2.parquet", "ext_lz4_v1.parquet", "ext_gzip_v2.parquet"):
+        f = load(name)
+        got = capi.canonical_dump(decode(ctx, f, 0))
+        assert sha(got) == MAN["files"][name]["columns"]["s_dict"]["sha256"]
+
+
+def test_ext_host_fill_path(ctx):
+    """Without the raw-upload path (option raw_upload = 0) the compressed
+    payloads are gathered and uploaded separately: same result."""
+    ctx.set_option("raw_upload", 0)
+    try:
+        for name in ("ext_snappy_v1.parquet", "ext_gzip_v2.parquet"):
+            f = load(name)
+            for ci in (0, 1, 5):
+                got = capi.canonical_dump(decode(ctx, f, ci))
+                assert sha(got) == MAN["files"][name]["columns"][COLS[ci]]["sha256"]
+    finally:
+        ctx.set_option("raw_upload", 1)
+
+
+@pytest.mark.parametrize("name", ["ext_snappy_v1.parquet", "ext_gzip_v1.parquet", "ext_lz4_v2.parquet"])
+def test_ext_corrupt_page_fails_cleanly(ctx, name):
+    """Damaged compressed bytes end in an error (decompression or decode), never a fault."""
+    f = bytearray(load(name))
+    d = ext_chunks(bytes(f), 1)[0]
+    rc, msg, table = capi.build_page_table(bytes(f), d)
+    assert rc == 0
+    p = [q for q in table if q.page_type == 0][1]
+    rng = np.random.default_rng(5)
+    for k in rng.integers(0, p.payload_size, 24):
+        f[p.payload_offset + int(k)] ^= 0x5A
+    try:
+        dc = ctx.upload(bytes(f), ext_chunks(bytes(f), 1))
+    except capi.PqError as e:
+        assert e.code in (-9, -2, -8), e
+        return
+    try:
+        dc.decode()
+    except capi.PqError:
+        pass
+    finally:
+        dc.free()
+
+
+pa = None
+try:
+    import pyarrow as pa  # noqa: F811
+    import pyarrow.parquet as pq
+except ImportError:  # pragma: no cover
+    pass
+
+
+@pytest.mark.skipif(pa is None, reason="pyarrow not importable")
+@pytest.mark.parametrize("codec", ["snappy", "gzip", "lz4"])
+@pytest.mark.parametrize("version", ["1.0", "2.0"])
+def test_ext_large_pages_vs_pyarrow(ctx, tmp_path, codec, version):
+    """1 MiB pages (pyarrow's default), 400k rows: dictionary and PLAIN
+    strings plus INT64 through every codec, against pyarrow's reading."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden", "ext"))
+    from make_ext import canonical_dump, table
+    t = table(400_000, seed=11).select(["s_dict", "s_plain", "i64"])
+    path = tmp_path / f"big_{codec}_{version}.parquet"
+    pq.write_table(t, path, compression=codec.upper() if codec != "lz4" else "LZ4", data_page_version=version,
+                   use_dictionary=["s_dict"], row_group_size=400_000)
+    f = path.read_bytes()
+    back = pq.read_table(path)
+    for ci, c in enumerate(back.column_names):
+        got = capi.canonical_dump(decode(ctx, f, ci))
+        assert sha(got) == sha(canonical_dump(back.column(c))), c
