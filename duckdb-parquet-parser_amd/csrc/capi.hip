@@ -1087,7 +1087,10 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                                                                }),
                                        "upload");
                         if (!rc) {
-                            pqk::launch_relayout(s, ctx->d_raw, c->d_bytes, ctx->d_relay, static_cast<int32_t>(ents.size()));
+                            {
+                                Timed rt(ctx, "relayout", s);
+                                pqk::launch_relayout(s, ctx->d_raw, c->d_bytes, ctx->d_relay, static_cast<int32_t>(ents.size()));
+                            }
                             (void)hipMemsetAsync(c->d_bytes + img, 0, c->nbytes - static_cast<size_t>(img), s);
                             relaid = true;
                         }
@@ -1164,7 +1167,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                                                        }),
                                "upload");
             if (!rc) {
-                HostTimed ct(ctx, "up_codec");
+                Timed ct(ctx, "codec", s);
                 pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus);
             }
         }

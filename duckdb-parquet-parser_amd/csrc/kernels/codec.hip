@@ -73,7 +73,7 @@ struct In {
     uint32_t wlo;      // input byte held at in[sh]
     uint32_t sh;
     uint8_t* w;
-    __device__ void refill(uint32_t p) {
+    __device__ __forceinline__ void refill(uint32_t p) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(g) + p;
         const uintptr_t A = a & ~static_cast<uintptr_t>(15);
         const uintptr_t e = reinterpret_cast<uintptr_t>(g) + len;  // blocks at or past e are not loaded
@@ -119,7 +119,7 @@ struct Out {
     uint32_t cap;   // bytes the slot's payload holds
     uint32_t vbase; // first byte of the decompressed stream (after a V2 prologue)
     uint32_t st;    // ST_*
-    __device__ void flush(bool final) {
+    __device__ __forceinline__ void flush(bool final) {
         while (op - fl >= kFlush || (final && fl < op)) {
             const uint32_t n = min(kFlush, op - fl);
             const uint32_t b = fl + 16u * lane();
@@ -144,7 +144,7 @@ struct Out {
         return true;
     }
     // literal bytes [p, p + n) of the input
-    __device__ void lit(In& I, uint32_t p, uint32_t n) {
+    __device__ __forceinline__ void lit(In& I, uint32_t p, uint32_t n) {
         if (!room(n)) return;
         for (uint32_t d = 0; d < n; d += kWave) {
             I.ensure(p + d, kWave);
@@ -157,7 +157,7 @@ struct Out {
     }
     // copy of n bytes from distance d: 64 bytes per step, byte c0 + j of a
     // step from c0 - d + (j mod d) (d < 64) or c0 - d + j: before c0, final
-    __device__ void copy(uint32_t d, uint32_t n) {
+    __device__ __forceinline__ void copy(uint32_t d, uint32_t n) {
         if (d == 0 || d > op - vbase || d > kRing - 1) { st = ST_CORRUPT; return; }
         if (!room(n)) return;
         const uint32_t r = d >= static_cast<uint32_t>(kWave) ? lane() : lane() % d;
@@ -181,7 +181,7 @@ struct Out {
             flush(false);
         }
     }
-    __device__ void put_u32(uint32_t v) {
+    __device__ __forceinline__ void put_u32(uint32_t v) {
         if (!room(4)) return;
         if (lane() < 4) ring[(op + lane()) & kRingMask] = static_cast<uint8_t>(v >> (8 * lane()));
         wsync();
@@ -191,7 +191,7 @@ struct Out {
 };
 
 // ── SNAPPY ─────────────────────────────────────────────────────────────────
-__device__ void snappy(In& I, Out& O, uint32_t p, uint32_t end, uint32_t expect) {
+__device__ __forceinline__ void snappy(In& I, Out& O, uint32_t p, uint32_t end, uint32_t expect) {
     uint32_t ulen = 0;
     I.ensure(p, 8);
     for (uint32_t k = 0;; k++) {
@@ -241,7 +241,7 @@ __device__ void snappy(In& I, Out& O, uint32_t p, uint32_t end, uint32_t expect)
 }
 
 // ── LZ4 block ──────────────────────────────────────────────────────────────
-__device__ void lz4_block(In& I, Out& O, uint32_t p, uint32_t end) {
+__device__ __forceinline__ void lz4_block(In& I, Out& O, uint32_t p, uint32_t end) {
     for (;;) {
         if (p >= end) { O.st = ST_CORRUPT; return; }
         I.ensure(p, 1);
@@ -281,7 +281,7 @@ __device__ void lz4_block(In& I, Out& O, uint32_t p, uint32_t end) {
 }
 
 // Hadoop framing (codec LZ4): blocks of [u32 BE raw bytes][u32 BE packed bytes][LZ4 block].
-__device__ void lz4_hadoop(In& I, Out& O, uint32_t p, uint32_t end) {
+__device__ __forceinline__ void lz4_hadoop(In& I, Out& O, uint32_t p, uint32_t end) {
     while (p < end && O.st == ST_OK) {
         if (end - p < 8) { O.st = ST_CORRUPT; return; }
         I.ensure(p, 8);
@@ -353,7 +353,7 @@ struct Bits {
 // Canonical Huffman code over lens[base, base + n): counts, codes, symbols
 // in code order, and the kFast-bit lookup table.  Returns false for an
 // over-subscribed code.
-__device__ bool build_code(CodecLds& L, int which, uint32_t base, uint32_t n, uint16_t* table) {
+__device__ __forceinline__ bool build_code(CodecLds& L, int which, uint32_t base, uint32_t n, uint16_t* table) {
     uint16_t* cnt = L.cnt[which];
     if (lane() < 16) cnt[lane()] = 0;
     wsync();
@@ -396,7 +396,7 @@ __device__ bool build_code(CodecLds& L, int which, uint32_t base, uint32_t n, ui
 }
 
 // One Huffman symbol: the lookup table, else the canonical bit-serial walk.
-__device__ int32_t decode_sym(CodecLds& L, In& I, Bits& B, const uint16_t* table, int which, uint32_t base) {
+__device__ __forceinline__ int32_t decode_sym(CodecLds& L, In& I, Bits& B, const uint16_t* table, int which, uint32_t base) {
     B.need(I, 15);
     const uint32_t e = uni(table[B.peek(kFast)]);
     if (e & 15u) {
@@ -417,7 +417,7 @@ __device__ int32_t decode_sym(CodecLds& L, In& I, Bits& B, const uint16_t* table
     return -1;
 }
 
-__device__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
+__device__ __forceinline__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
     for (;;) {
         const uint32_t fin = B.take(I, 1);
         const uint32_t ty = B.take(I, 2);
@@ -525,7 +525,7 @@ __device__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
 }
 
 // GZIP members (RFC 1952) or one zlib stream (RFC 1950).
-__device__ void gzip(CodecLds& L, In& I, Out& O, uint32_t p, uint32_t end) {
+__device__ __forceinline__ void gzip(CodecLds& L, In& I, Out& O, uint32_t p, uint32_t end) {
     bool first = true;
     while (O.st == ST_OK && (first || p < end)) {
         if (end - p < 2) { O.st = ST_CORRUPT; return; }
