@@ -186,6 +186,7 @@ struct pq_chunk {
     int32_t* d_rwin_ticket = nullptr;
     uint32_t rwin_bytes = 0, rwin_for_dfa = 0;
     int rwin_grid = 0;
+    int rwin_opt = 0;                   // regex_win the windows were planned with
     uint32_t dfa_bytes = 0;
     bool dfa_full = false;               // the DFA image has full 256-column rows
     std::string prog_pattern;           // pattern of d_prog / d_dfa
@@ -1779,7 +1780,7 @@ int pq_regex_compile_check(const char* pattern, char* err, size_t errlen) {
 // k_regex_plain): <= 64 pages and <= win bytes of image each.  False when a
 // page does not fit (the lane-per-page kernel runs then).
 bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
-    if (c->d_rwins && c->rwin_for_dfa == c->dfa_bytes) return true;
+    if (c->d_rwins && c->rwin_for_dfa == c->dfa_bytes && c->rwin_opt == ctx->opt_regex_win) return true;
     std::vector<DevPage> hp(static_cast<size_t>(c->npages));
     if (c->npages && hipMemcpy(hp.data(), c->d_pages, hp.size() * sizeof(DevPage), hipMemcpyDeviceToHost) != hipSuccess)
         return false;
@@ -1818,8 +1819,9 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     const int per_cu = std::max(1, pqre::regex_plain_occupancy(lds));
     c->rwin_bytes = win;
     c->rwin_for_dfa = c->dfa_bytes;
-    const int wpb = static_cast<int>(pqre::regex_plain_waves(c->dfa_bytes, win));
-    c->rwin_grid = std::max(1, std::min<int>(per_cu * cus, static_cast<int>((c->hrwins.size() + wpb - 1) / wpb)));
+    c->rwin_opt = ctx->opt_regex_win;
+    const int scan = static_cast<int>(pqre::regex_plain_waves(c->dfa_bytes, win));  // waves per workgroup
+    c->rwin_grid = std::max(1, std::min<int>(per_cu * cus, static_cast<int>((c->hrwins.size() + scan - 1) / scan)));
     (void)cus;
     return true;
 }
@@ -1886,7 +1888,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             Timed t(ctx, "regex_plain");
             pqre::launch_regex_plain(s, c->d_dfa, c->dfa_bytes, c->rwin_bytes, c->d_bytes, c->d_pages, c->d_rwins,
                                      static_cast<int>(c->hrwins.size()), c->d_rwin_ticket, c->rwin_grid, cp,
-                                     (neg ? 1 : 0) | (ctx->opt_regex_debug << 8),
+                                     (neg ? 1 : 0) | ((ctx->opt_regex_debug & 0xFF) << 8),
                                      c->d_page_flags, c->d_page_err, c->d_flags);
         } else if (c->d_dfa) {
             Timed t(ctx, "regex_lanes");

@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(256) k_regex_pages(const DevProg* __restrict__
 // into the DFA (one LDS lookup per byte).  A lane stops as soon as its page
 // has a satisfying value.
 __device__ __forceinline__ uint32_t dfa_step_full(const uint16_t* T, uint32_t e, uint32_t b) {
-    return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(T) + (e & 0x7FFFu) + 2 * b);
+    return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(T) + e + 2 * b);
 }
 
 __device__ __forceinline__ void lane_err(DevErr* e, int32_t* any, int code, uint32_t pos, uint32_t need,
@@ -415,8 +415,9 @@ __global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__
                     W1 = W2;
                     W2 = win(wb + 32);
                 }
-                const uint32_t st = full ? (e & 0x7FFFu) / kDfaRowBytes : (e & 0x7FFFu);
-                const bool m = len == 0 ? empty_ok : (trivial || st == DFA_ACCEPT || (e >> 15) != 0);
+                const uint32_t st = full ? e / kDfaRowBytes : (e & 0x7FFFu);
+                const bool acc = full ? dfa_step_full(T, e, 256) != 0 : (e >> 15) != 0;
+                const bool m = len == 0 ? empty_ok : (trivial || st == DFA_ACCEPT || acc);
                 if (act) any = (static_cast<uint32_t>(m) != negv);
             }
         }
@@ -429,15 +430,40 @@ __global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__
 }
 
 // ── windowed PLAIN scan ─────────────────────────────────────────────────────
-// Chunks without dictionary pages: each wave takes windows of consecutive
-// pages (one contiguous image range, <= win_bytes) in ticket order, copies
-// the window into LDS with coalesced 16-byte loads, walks each page's u32
-// length chain with one lane per page (LDS latency, not HBM), and lists the
-// strings; then all 64 lanes match the listed strings, two per lane, so two
-// DFA chains (one LDS lookup per byte each) are in flight per lane.
+// Chunks without dictionary pages.  Each wave takes windows of consecutive
+// pages (one contiguous image range, <= win_bytes) with a static grid stride,
+// and per window:
+//   staging   the window's bytes -> LDS with coalesced 16-byte loads, eight
+//             in flight per lane (copy_blocks); the next window's descriptors
+//             load while this one is scanned.  (A loader wave feeding two LDS
+//             buffers per scanning wave by LDS-DMA measured slower on C3, 0.47
+//             vs 0.40 ms: one loader per CU could not keep up, and the second
+//             buffer cost a third of the scanning waves);
+//   strings   the u32 length chain of every page (column_reader.cpp:249-253)
+//             is walked by L = 64 / pages lanes per page: each lane takes a
+//             byte segment of the page and finds its first candidate string
+//             start (a position whose u32 length fits the page; 16 positions
+//             per aligned read) and walks that chain to the segment end; the
+//             segments link when each starts where the previous one left
+//             (one shuffle), a scan places every segment's strings in the
+//             page's list, and the chains are re-walked to emit them.  A page
+//             whose segments do not link, or whose chain fails before its
+//             value count, is walked again by one lane in the reference order
+//             (exact errors).  (C3: 0.068 ms against 0.082 for one lane per
+//             page);
+//   DFA       all 64 lanes run the DFA over the listed strings, four strings
+//             per lane interleaved, one LDS lookup per byte; table entries are
+//             bare row offsets (the accept-at-end flag sits in column 256 of
+//             a row, read once per string), and the per-byte end-of-string
+//             selects are kept out of SGPR masks (C3: 0.119 ms, was 0.166).
 constexpr uint32_t kPlainWavesMax = 16;  // waves per workgroup: as many as the LDS holds (host)
 constexpr uint32_t kStrPerLane = 4;  // strings interleaved per lane (independent DFA chains)
 
+// The u32 at byte a of the staged window (>= 8 readable bytes past a).
+__device__ __forceinline__ uint32_t st_u32(const uint32_t* st, uint32_t a) {
+    const uint32_t i = a >> 2, sh = a & 3u;
+    return __builtin_amdgcn_alignbyte(st[i + 1], st[i], sh);
+}
 
 __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
                                                                   uint32_t dfa_bytes, uint32_t win_bytes,
@@ -462,62 +488,209 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
     const bool full = D->full != 0;
     const bool empty_ok = D->empty_string != 0;
     const bool trivial = D->nonempty_trivial != 0;
-    const uint32_t negv = neg & 1;  // bits 8+: timing ablation (1: no DFA pass, 2: no chain walk)
-    const int dbg = neg >> 8;
+    const uint32_t negv = neg & 1;  // bits 8..15: timing ablation (1: no DFA pass, 2: no chain walk,
+    const int dbg = (neg >> 8) & 0xFF;  // 4: exact walk for every page)
     const uint32_t wv = threadIdx.x / kWave;
-    // per wave: window bytes (+16 zero), string list (u32 per 4 window
-    // bytes), per-page inclusive string counts and list bases, hit mask
-    uint8_t* wbase = dsm + dfa_bytes + wv * regex_plain_wave_lds(win_bytes);
-    uint32_t* stage = reinterpret_cast<uint32_t*>(wbase);
-    uint16_t* list = reinterpret_cast<uint16_t*>(wbase + win_bytes + 16);  // window offset of each string
-    uint32_t* pref = reinterpret_cast<uint32_t*>(wbase + win_bytes + 16 + win_bytes / 2);
-    uint32_t* lbase = pref + 64;
-    uint32_t* hit = lbase + 64;  // [0..1]: satisfied-page mask of the window
+    const uint32_t wpb = blockDim.x / kWave;
     const uint32_t md = static_cast<uint32_t>(cp.max_def);
-    // windows are independent (no ordering): static grid-stride assignment
     (void)ticket;
-    const int32_t nw_total = static_cast<int32_t>(gridDim.x * (blockDim.x / kWave));
-    for (int32_t w = static_cast<int32_t>(blockIdx.x * (blockDim.x / kWave) + wv); w < nwins; w += nw_total) {
-        const pqk::DevBatch B = wins[w];
-        {
-            const uint4* src = reinterpret_cast<const uint4*>(bytes + B.img_lo);
-            uint4* dst = reinterpret_cast<uint4*>(stage);
-            copy_blocks(dst, src, B.img_bytes / 16, lane(), kWave);
-            if (lane() == 0) { dst[B.img_bytes / 16] = make_uint4(0, 0, 0, 0); hit[0] = 0; hit[1] = 0; }
+    // scanning wave c (1 .. wpb - 1) of workgroup g takes windows
+    // (g * K + c - 1) + i * nwt, i = 0, 1, ...; buffer i & 1
+    const uint32_t K = wpb;
+    const int32_t nwt = static_cast<int32_t>(gridDim.x * K);
+    // ── scanning waves ──────────────────────────────────────────────────
+    const uint32_t c = wv;
+    uint8_t* wbase = dsm + dfa_bytes + c * regex_plain_wave_lds(win_bytes);
+    uint8_t* cur = wbase;  // the window (+32 zero bytes)
+    uint16_t* list = reinterpret_cast<uint16_t*>(wbase + win_bytes + 32);  // window offset of each string
+    uint32_t* pref = reinterpret_cast<uint32_t*>(wbase + win_bytes + 32 + win_bytes / 2);
+    uint32_t* lbase = pref + 64;
+    uint32_t* pcnt = lbase + 64;
+    uint32_t* hit = pcnt + 64;  // [0..1]: satisfied-page mask of the window
+    int32_t w = static_cast<int32_t>(blockIdx.x * K + c);
+    if (w >= nwins) return;
+    // descriptors two windows ahead: the batch of window i + 2 and the
+    // pages of window i + 1 load while window i is scanned
+    pqk::DevBatch B = wins[w];
+    pqk::DevBatch Bn{};
+    if (w + nwt < nwins) Bn = wins[w + nwt];
+    DevPage pg{};
+    if (lane() < static_cast<uint32_t>(B.np)) pg = pages[B.p0 + static_cast<int32_t>(lane())];
+    for (;;) {
+        const pqk::DevBatch Bc = B;
+        const DevPage pgc = pg;
+        const int32_t wn = w + nwt;
+        DevPage pgn{};
+        pqk::DevBatch Bnn{};
+        if (wn < nwins) {
+            if (lane() < static_cast<uint32_t>(Bn.np)) pgn = pages[Bn.p0 + static_cast<int32_t>(lane())];
+            if (wn + nwt < nwins) Bnn = wins[wn + nwt];
+        }
+        copy_blocks(reinterpret_cast<uint4*>(cur), reinterpret_cast<const uint4*>(bytes + Bc.img_lo), Bc.img_bytes / 16,
+                    lane(), kWave);
+        if (lane() < 2) reinterpret_cast<uint4*>(cur + Bc.img_bytes)[lane()] = make_uint4(0, 0, 0, 0);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t* stage = reinterpret_cast<const uint32_t*>(cur);
+        if (lane() == 0) {
+            hit[0] = 0;
+            hit[1] = 0;
         }
         __builtin_amdgcn_wave_barrier();
-        // lane-per-page: levels, then the length chain into the list
-        const bool act = lane() < static_cast<uint32_t>(B.np);
-        const int32_t pidx = B.p0 + static_cast<int32_t>(lane());
-        DevPage pg{};
-        if (act) pg = pages[pidx];
-        const uint32_t pay = static_cast<uint32_t>(pg.off - B.img_lo);
-        const uint32_t* pw = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(stage) + pay);
-        const uint32_t size = static_cast<uint32_t>(pg.size);
-        uint32_t cnt = 0;
-        if (act && !(dbg & 2)) {
+        const uint32_t np = static_cast<uint32_t>(Bc.np);
+        // ── strings: L lanes per page ───────────────────────────────────
+        const uint32_t lg = np <= 1 ? 0u : 32u - __builtin_clz(np - 1);  // ceil log2
+        const uint32_t L = kWave >> lg;
+        const uint32_t q = lane() / L, sg = lane() % L;
+        const bool act = q < np && !(dbg & 2);
+        const uint32_t qs = min(q, 63u);
+        const uint64_t poff = (static_cast<uint64_t>(__shfl(static_cast<int>(pgc.off >> 32), static_cast<int>(qs))) << 32) |
+                              static_cast<uint32_t>(__shfl(static_cast<int>(pgc.off), static_cast<int>(qs)));
+        const uint32_t size = static_cast<uint32_t>(max(__shfl(pgc.size, static_cast<int>(qs)), 0));
+        const uint32_t nvq = static_cast<uint32_t>(max(__shfl(pgc.nvals, static_cast<int>(qs)), 0));
+        const uint32_t pay = static_cast<uint32_t>(poff - Bc.img_lo);
+        // levels (segment 0 lanes; any problem -> the exact walk below)
+        uint32_t pos0 = 0, nn = nvq;
+        bool bad = false;
+        if (act && sg == 0 && (cp.max_def > 0 || cp.max_rep > 0)) {
+            const uint32_t* pw = reinterpret_cast<const uint32_t*>(cur + pay);
             auto rd8 = [&](uint32_t a) { return lds_u64(pw, a); };
-            DevErr* err = page_err + pidx;
-            uint32_t pos = 0, nn = static_cast<uint32_t>(max(pg.nvals, 0));
-            int code = 0;
-            uint32_t epos = 0, eneed = 0;
             if (cp.max_def > 0) {
-                if (pos + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
+                if (pos0 + 4 > size) bad = true;
                 else {
-                    const uint32_t dl = static_cast<uint32_t>(rd8(pos));
-                    pos += 4;
-                    if (static_cast<uint64_t>(pos) + dl > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = dl; }
+                    const uint32_t dl = static_cast<uint32_t>(rd8(pos0));
+                    pos0 += 4;
+                    if (static_cast<uint64_t>(pos0) + dl > size) bad = true;
                     else {
-                        LRle r = lrle(pos, dl, level_bw(cp.max_def));
+                        LRle r = lrle(pos0, dl, level_bw(cp.max_def));
                         const uint32_t bwd = r.bw;
-                        const uint32_t nv = nn;
                         nn = 0;
-                        code = lane_rle(r, rd8, nv, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                        bad = lane_rle(r, rd8, nvq, [&](uint32_t kind, uint32_t k, uint32_t arg) {
                             if (kind == 0) {
                                 if (arg >= md) nn += k;
                             } else {
                                 for (uint32_t i = 0; i < k; i++)
                                     if (lds_bits(pw, size, static_cast<uint64_t>(arg) + i * bwd, bwd) >= md) nn++;
+                            }
+                        }) != 0;
+                        pos0 += dl;
+                    }
+                }
+            }
+            if (!bad && cp.max_rep > 0) {
+                if (pos0 + 4 > size) bad = true;
+                else {
+                    const uint32_t rl = static_cast<uint32_t>(rd8(pos0));
+                    pos0 += 4;
+                    if (static_cast<uint64_t>(pos0) + rl > size) bad = true;
+                    else pos0 += rl;
+                }
+            }
+        }
+        const int src0 = static_cast<int>(q * L);
+        pos0 = static_cast<uint32_t>(__shfl(static_cast<int>(pos0), src0));
+        nn = static_cast<uint32_t>(__shfl(static_cast<int>(nn), src0));
+        bad = __shfl(static_cast<int>(bad), src0) != 0;
+        // this lane's segment of [pos0, size) and its first candidate string
+        // start (a position whose u32 length fits the page), 16 positions
+        // per aligned 16-byte read
+        const uint32_t span = size > pos0 ? size - pos0 : 0u;
+        const uint32_t lo = pos0 + static_cast<uint32_t>((static_cast<uint64_t>(span) * sg) / L);
+        const uint32_t hi = sg + 1 == L ? size : pos0 + static_cast<uint32_t>((static_cast<uint64_t>(span) * (sg + 1)) / L);
+        const uint32_t A = pay;  // window byte of the page's payload
+        uint32_t c0 = ~0u;
+        if (act && !bad) {
+            if (sg == 0) {
+                c0 = pos0;
+            } else {
+                for (uint32_t a = (A + lo) & ~15u; a < A + hi && c0 == ~0u; a += 16) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(cur + a);
+                    const uint32_t d4 = stage[(a >> 2) + 4];
+                    const uint32_t d[5] = {v.x, v.y, v.z, v.w, d4};
+#pragma unroll
+                    for (uint32_t k = 0; k < 16; k++) {
+                        const uint32_t cpos = a + k - A;
+                        const uint32_t len = (k & 3) == 0 ? d[k >> 2] : __builtin_amdgcn_alignbyte(d[(k >> 2) + 1], d[k >> 2], k & 3);
+                        const bool ok = cpos >= lo && cpos < hi && cpos + 4 <= size && len <= size - cpos - 4;
+                        c0 = (ok && c0 == ~0u) ? cpos : c0;
+                    }
+                }
+            }
+        }
+        // its chain to the segment end: exit position, strings, and whether a
+        // read failed (at the exit)
+        uint32_t ex = c0, n = 0;
+        bool fail = false;
+        if (act && c0 != ~0u) {
+            while (ex < hi) {
+                if (ex + 4 > size) { fail = true; break; }
+                const uint32_t len = st_u32(stage, A + ex);
+                if (len > size - ex - 4) { fail = true; break; }
+                ex += 4 + len;
+                n++;
+            }
+        }
+        // link: every segment must start where the previous one left (no
+        // failed chain before the last segment); else the exact walk
+        const uint32_t prev = static_cast<uint32_t>(__shfl(static_cast<int>(ex), static_cast<int>(lane()) - 1));
+        const uint32_t pfail = static_cast<uint32_t>(__shfl(static_cast<int>(fail), static_cast<int>(lane()) - 1));
+        const uint32_t start = c0;
+        const bool mism = act && !bad && (c0 == ~0u || (sg > 0 && (pfail || prev != c0)));
+        // page-local placement of each segment's strings
+        const uint32_t inc = wave_incl_scan(n);
+        const uint32_t pbase = static_cast<uint32_t>(__shfl(static_cast<int>(inc - n), src0));
+        const uint32_t before = inc - n - pbase;
+        const uint32_t last = min(src0 + L - 1, 63u);
+        const uint32_t total = static_cast<uint32_t>(__shfl(static_cast<int>(inc), static_cast<int>(last))) - pbase;
+        // exact walk needed: unlinked segments, a level problem, or fewer than
+        // nn strings before the chain fails / the page ends
+        const uint64_t mm = __ballot(act && (mism || bad));
+        const uint32_t pmis = ((mm >> src0) & ((L >= 64 ? ~0ull : ((1ull << L) - 1ull)))) != 0 ? 1u : 0u;
+        const bool page_ok = act && !pmis && total >= nn && !(dbg & 4);
+        // emit: this segment's strings with page index < nn
+        if (page_ok && start != ~0u && before < nn) {
+            const uint32_t keep = min(n, nn - before);
+            uint16_t* lst = list + pay / 4 + before;
+            uint32_t pos = start;
+            for (uint32_t i = 0; i < keep; i++) {
+                const uint32_t len = st_u32(stage, A + pos);
+                lst[i] = static_cast<uint16_t>(A + pos + 4);
+                pos += 4 + len;
+            }
+        }
+        if (act && sg == 0) pcnt[q] = page_ok ? nn : ~0u;  // ~0: exact walk
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // exact walk (one lane per page) where the segments did not settle it
+        const bool pl = lane() < np;
+        uint32_t cnt = pl && !(dbg & 2) ? pcnt[lane()] : 0u;
+        const uint32_t mpay = static_cast<uint32_t>(pgc.off - Bc.img_lo);
+        if (pl && cnt == ~0u) {
+            cnt = 0;
+            const uint32_t* pw = reinterpret_cast<const uint32_t*>(cur + mpay);
+            auto rd8 = [&](uint32_t a) { return lds_u64(pw, a); };
+            DevErr* err = page_err + Bc.p0 + static_cast<int32_t>(lane());
+            const uint32_t msize = static_cast<uint32_t>(max(pgc.size, 0));
+            uint32_t pos = 0, mnn = static_cast<uint32_t>(max(pgc.nvals, 0));
+            int code = 0;
+            uint32_t epos = 0, eneed = 0;
+            if (cp.max_def > 0) {
+                if (pos + 4 > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
+                else {
+                    const uint32_t dl = static_cast<uint32_t>(rd8(pos));
+                    pos += 4;
+                    if (static_cast<uint64_t>(pos) + dl > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = dl; }
+                    else {
+                        LRle r = lrle(pos, dl, level_bw(cp.max_def));
+                        const uint32_t bwd = r.bw;
+                        const uint32_t nv = mnn;
+                        mnn = 0;
+                        code = lane_rle(r, rd8, nv, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                            if (kind == 0) {
+                                if (arg >= md) mnn += k;
+                            } else {
+                                for (uint32_t i = 0; i < k; i++)
+                                    if (lds_bits(pw, msize, static_cast<uint64_t>(arg) + i * bwd, bwd) >= md) mnn++;
                             }
                         });
                         pos += dl;
@@ -525,51 +698,51 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                 }
             }
             if (!code && cp.max_rep > 0) {
-                if (pos + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
+                if (pos + 4 > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
                 else {
                     const uint32_t rl = static_cast<uint32_t>(rd8(pos));
                     pos += 4;
-                    if (static_cast<uint64_t>(pos) + rl > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = rl; }
+                    if (static_cast<uint64_t>(pos) + rl > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = rl; }
                     else pos += rl;
                 }
             }
-            uint16_t* lst = list + pay / 4;  // this page's list region (<= slot / 4 entries)
-            for (uint32_t k = 0; k < nn && !code; k++) {  // column_reader.cpp:249-253
-                if (static_cast<uint64_t>(pos) + 4 > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; break; }
+            uint16_t* lst = list + mpay / 4;  // this page's list region (<= slot / 4 entries)
+            for (uint32_t k = 0; k < mnn && !code; k++) {  // column_reader.cpp:249-253
+                if (static_cast<uint64_t>(pos) + 4 > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; break; }
                 const uint32_t len = static_cast<uint32_t>(rd8(pos));
                 pos += 4;
-                if (static_cast<uint64_t>(pos) + len > size) { code = PQ_ERR_BUFFER; epos = pos; eneed = len; break; }
-                lst[cnt++] = static_cast<uint16_t>(pay + pos);  // window offset (the length is at offset - 4)
+                if (static_cast<uint64_t>(pos) + len > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = len; break; }
+                lst[cnt++] = static_cast<uint16_t>(mpay + pos);  // window offset (the length is at offset - 4)
                 pos += len;
             }
             if (code) {
-                lane_err(err, err_any, code, epos, eneed, size);
+                lane_err(err, err_any, code, epos, eneed, msize);
                 cnt = 0;
             }
         }
         // flatten: string g of the window -> (page lane, k)
-        const uint32_t inc = wave_incl_scan(cnt);
-        pref[lane()] = inc;
-        lbase[lane()] = pay / 4;
-        const uint32_t total = bcast_last(inc);
+        const uint32_t pinc = wave_incl_scan(cnt);
+        pref[lane()] = pinc;
+        lbase[lane()] = mpay / 4;
+        const uint32_t wtotal = bcast_last(pinc);
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t g0 = 0; g0 < ((dbg & 1) ? 0u : total); g0 += kStrPerLane * kWave) {
+        for (uint32_t g0 = 0; g0 < ((dbg & 1) ? 0u : wtotal); g0 += kStrPerLane * kWave) {
             uint32_t e2[kStrPerLane], off2[kStrPerLane], len2[kStrPerLane], pg2[kStrPerLane];
             bool ok2[kStrPerLane];
 #pragma unroll
             for (uint32_t h = 0; h < kStrPerLane; h++) {
                 const uint32_t g = g0 + h * kWave + lane();
-                ok2[h] = g < total;
+                ok2[h] = g < wtotal;
                 // first page lane whose inclusive count exceeds g
-                uint32_t lo = 0;
+                uint32_t lo2 = 0;
 #pragma unroll
                 for (uint32_t stp = 32; stp >= 1; stp >>= 1)
-                    if (pref[lo + stp - 1] <= g) lo += stp;
-                const uint32_t gl = ok2[h] ? lo : 0u;
-                const uint32_t before = gl ? pref[gl - 1] : 0u;
-                const uint32_t ent = ok2[h] ? list[lbase[gl] + (g - before)] : 4u;
+                    if (pref[lo2 + stp - 1] <= g) lo2 += stp;
+                const uint32_t gl = ok2[h] ? lo2 : 0u;
+                const uint32_t bef = gl ? pref[gl - 1] : 0u;
+                const uint32_t ent = ok2[h] ? list[lbase[gl] + (g - bef)] : 4u;
                 off2[h] = ent;
-                len2[h] = ok2[h] ? static_cast<uint32_t>(lds_u64(stage, ent - 4)) : 0u;
+                len2[h] = ok2[h] ? st_u32(stage, ent - 4) : 0u;
                 pg2[h] = gl;
                 e2[h] = full ? (DFA_START * kDfaRowBytes) : DFA_START;
             }
@@ -577,7 +750,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
 #pragma unroll
             for (uint32_t h = 0; h < kStrPerLane; h++) maxl = max(maxl, len2[h]);
             for (uint32_t b0 = 0; __ballot(maxl > b0); b0 += 16) {
-                uint32_t A[kStrPerLane][4], rem[kStrPerLane];
+                uint32_t Aw[kStrPerLane][4], rem[kStrPerLane];
 #pragma unroll
                 for (uint32_t h = 0; h < kStrPerLane; h++) {
                     const uint32_t a = off2[h] + b0;
@@ -586,7 +759,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
 #pragma unroll
                     for (uint32_t j = 0; j < 5; j++) d[j] = stage[i0 + j];
 #pragma unroll
-                    for (uint32_t j = 0; j < 4; j++) A[h][j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+                    for (uint32_t j = 0; j < 4; j++) Aw[h][j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
                     rem[h] = len2[h] > b0 ? len2[h] - b0 : 0u;
                 }
                 // the chains advance one byte each per step, interleaved
@@ -595,8 +768,12 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                     for (uint32_t i = 0; i < 16; i++) {
 #pragma unroll
                         for (uint32_t h = 0; h < kStrPerLane; h++) {
-                            const uint32_t t = dfa_step_full(T, e2[h], (A[h][i >> 2] >> (8 * (i & 3))) & 0xFFu);
-                            e2[h] = i < rem[h] ? t : e2[h];
+                            const uint32_t t = dfa_step_full(T, e2[h], (Aw[h][i >> 2] >> (8 * (i & 3))) & 0xFFu);
+                            // (opaque to the compiler: the 64 per-byte compares are not
+                            // hoisted into SGPR masks that spill)
+                            uint32_t rv = rem[h];
+                            __asm__ volatile("" : "+v"(rv));
+                            e2[h] = i < rv ? t : e2[h];
                         }
                     }
                 } else {
@@ -604,7 +781,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                     for (uint32_t i = 0; i < 16; i++) {
 #pragma unroll
                         for (uint32_t h = 0; h < kStrPerLane; h++) {
-                            const uint32_t bt = (A[h][i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                            const uint32_t bt = (Aw[h][i >> 2] >> (8 * (i & 3))) & 0xFFu;
                             const uint32_t t = T[(e2[h] & 0x7FFFu) * nc + D->cls_of[bt]];
                             e2[h] = i < rem[h] ? t : e2[h];
                         }
@@ -614,18 +791,24 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
 #pragma unroll
             for (uint32_t h = 0; h < kStrPerLane; h++) {
                 const uint32_t e = e2[h];
-                const uint32_t st = full ? (e & 0x7FFFu) / kDfaRowBytes : (e & 0x7FFFu);
-                const bool m = len2[h] == 0 ? empty_ok : (trivial || st == DFA_ACCEPT || (e >> 15) != 0);
+                const uint32_t st = full ? e / kDfaRowBytes : (e & 0x7FFFu);
+                const bool acc = full ? dfa_step_full(T, e, 256) != 0 : (e >> 15) != 0;
+                const bool m = len2[h] == 0 ? empty_ok : (trivial || st == DFA_ACCEPT || acc);
                 const bool sat = ok2[h] && (static_cast<uint32_t>(m) != negv);
                 if (sat) atomicOr(&hit[pg2[h] >> 5], 1u << (pg2[h] & 31));
             }
         }
         __builtin_amdgcn_wave_barrier();
-        if (act) {
+        if (pl) {
             const bool any = (hit[lane() >> 5] >> (lane() & 31)) & 1u;
-            page_flags[pidx] = any ? 0 : 1;
+            page_flags[Bc.p0 + static_cast<int32_t>(lane())] = any ? 0 : 1;
         }
         __builtin_amdgcn_wave_barrier();
+        if (wn >= nwins) break;
+        B = Bn;
+        Bn = Bnn;
+        pg = pgn;
+        w = wn;
     }
 }
 

@@ -63,7 +63,8 @@ struct DevDfa {
     uint32_t nonempty_trivial;  // every non-empty string matches
     uint32_t bytes;             // header + table, multiple of 16
     uint32_t full;              // 1: one column per byte value, entries = next row's byte
-                                // offset (rows kDfaRowBytes apart) | accept-at-end << 15
+                                // offset (rows kDfaRowBytes apart); column 256 of a row:
+                                // the state accepts at the string end
     uint32_t pad[2];
     uint8_t cls_of[256];        // byte -> class
 };
@@ -73,10 +74,10 @@ enum : uint32_t { DFA_DEAD = 0, DFA_ACCEPT = 1, DFA_START = 2 };
 // kernel is used then).
 bool build_dfa(const Program& p, std::vector<uint8_t>* image);
 
-// Windowed PLAIN scan (chunks without dictionary pages).
-// per wave: the window (+16 zero bytes), a u16 offset per possible string,
-// per-page counts and list bases, the hit mask
-constexpr uint32_t regex_plain_wave_lds(uint32_t win_bytes) { return win_bytes + 16 + win_bytes / 2 + 2 * 64 * 4 + 16; }
+// Windowed PLAIN scan (chunks without dictionary pages).  Per wave: the
+// window (+32 zero bytes), a u16 offset per possible string, per-page counts,
+// list bases and kept counts, the hit mask.
+constexpr uint32_t regex_plain_wave_lds(uint32_t win_bytes) { return win_bytes + 32 + win_bytes / 2 + 3 * 64 * 4 + 16; }
 uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes);
 uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes);
 int regex_plain_occupancy(uint32_t lds);

@@ -573,12 +573,18 @@ bool build_dfa(const Program& p, std::vector<uint8_t>* image) {
         // the next address with one mask and one add.  Rows are 516 bytes
         // apart (129 dwords): the LDS bank of an entry is (state + byte/2) mod
         // 32, so lanes in different states spread over the banks.
+        // Entries are bare offsets (no flag bits to mask on the chain);
+        // column 256 of a row holds whether that state accepts at the string
+        // end ($), read once per string.
         std::vector<uint16_t> pad(sets.size() * (kDfaRowBytes / 2), 0);
-        for (size_t st = 0; st < sets.size(); st++)
+        for (size_t st = 0; st < sets.size(); st++) {
             for (int b = 0; b < 256; b++) {
                 const uint32_t t = full[st * 256 + b];
-                pad[st * (kDfaRowBytes / 2) + b] = static_cast<uint16_t>((t & 0x7FFFu) * kDfaRowBytes | (t & 0x8000u));
+                pad[st * (kDfaRowBytes / 2) + b] = static_cast<uint16_t>((t & 0x7FFFu) * kDfaRowBytes);
             }
+            const bool acc = st == DFA_ACCEPT || (st >= 3 && (sets[st] & p.accept_end) != 0);
+            pad[st * (kDfaRowBytes / 2) + 256] = acc ? 1 : 0;
+        }
         full.swap(pad);
         trans.swap(full);
         nc = 256;
@@ -620,10 +626,12 @@ extern "C" int pq_regex_match_host_dfa(const char* pattern, const uint8_t* s, si
         uint32_t e = pqre::DFA_START * pqre::kDfaRowBytes;
         for (size_t i = 0; i < n; i++) {
             uint16_t v;
-            std::memcpy(&v, tb + (e & 0x7FFFu) + 2 * s[i], 2);
+            std::memcpy(&v, tb + e + 2 * s[i], 2);
             e = v;
         }
-        return ((e & 0x7FFFu) == pqre::DFA_ACCEPT * pqre::kDfaRowBytes || (e >> 15)) ? 1 : 0;
+        uint16_t acc;
+        std::memcpy(&acc, tb + e + 512, 2);
+        return (e == pqre::DFA_ACCEPT * pqre::kDfaRowBytes || acc) ? 1 : 0;
     }
     uint32_t e = pqre::DFA_START;
     for (size_t i = 0; i < n; i++) e = t[(e & 0x7FFFu) * h.nclasses + h.cls_of[s[i]]];

@@ -1,20 +1,29 @@
 #!/usr/bin/env python3
 """Windowed regex kernel phase ablation (option regex_debug): full, no DFA pass,
-no chain walk, staging only.  Output flags are not valid under the ablation."""
-import os, sys, json
+no chain walk, staging only, exact (serial) walk for every page; per window size.  Output flags are not valid
+under the ablation.  usage: regex_ablate.py [win_bytes ...]"""
+import json
+import sys
 sys.path[:0] = ["/root/repo", "/root/repo/duckdb-parquet-parser_amd"]
-from pqgpu import capi, gen
+from pqgpu import capi, gen  # noqa: E402
 ctx = capi.Context(0)
 f = gen.build(gen.c3_cols(), 10_000_000, 1, seed=gen.CONFIG_SEEDS["C3"])
 F = capi.File(f)
-dc = ctx.upload(f, [F.chunk(0, 0)])
-for rep in range(2):
-    for dbg in (0, 1, 2, 3):
+for win in [int(a) for a in sys.argv[1:]] or [8192]:
+    ctx.set_option("regex_win", win)
+    dc = ctx.upload(f, [F.chunk(0, 0)])
+    for dbg in (0, 1, 2, 3, 4):
         ctx.set_option("regex_debug", dbg)
-        for _ in range(3): dc.regex_pages_async("special.*requests", False)
+        for _ in range(3):
+            dc.regex_pages_async("special.*requests", False)
         ctx.sync()
-        ctx.timing(True); ctx.timing_reset()
-        for _ in range(10): dc.regex_pages_async("special.*requests", False)
+        ctx.timing(True)
+        ctx.timing_reset()
+        for _ in range(10):
+            dc.regex_pages_async("special.*requests", False)
         ctx.sync()
-        ms, n = ctx.timing_get("regex_plain"); ctx.timing(False)
-        print(json.dumps({"dbg": dbg, "ms": round(ms / n, 4)}), flush=True)
+        ms, n = ctx.timing_get("regex_plain")
+        ctx.timing(False)
+        print(json.dumps({"win": win, "dbg": dbg, "ms": round(ms / n, 4)}), flush=True)
+    ctx.set_option("regex_debug", 0)
+    dc.free()
