@@ -78,6 +78,7 @@ def parse():
     ap.add_argument("--c5-pattern", default=C5_PATTERN)
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-ext", action="store_true", help="skip the compressed / DATA_PAGE_V2 leg (SURVEY §8f rank 4)")
     ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (control path only; the data path has no collective)")
@@ -533,6 +534,70 @@ def c4_leg(J, args):
             "validated": None if args.no_validate else all(J.gather(bool(ok)))}
 
 
+def ext_leg(J, args):
+    """SURVEY §8f rank 4 (outside the reference's scope): the C3 and C2
+    columns as pyarrow writes them with SNAPPY (V1 pages) and LZ4_RAW
+    (DATA_PAGE_V2), 1 MiB pages; upload with PQ_EXT_CODECS | PQ_EXT_PAGE_V2
+    (the codec pass rebuilds every page on the GPU, codec.hip), then decode.
+    Checked byte for byte against the uncompressed decode of the same column."""
+    import io
+
+    import numpy as np
+    try:
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+    except ImportError:
+        return {"skipped": "pyarrow not importable"}
+    from pqgpu import capi, gen
+    out = {}
+    for name, cols, seed, use_dict, codec, ver in (("c3_snappy_v1", gen.c3_cols(), gen.CONFIG_SEEDS["C3"], False, "SNAPPY", "1.0"),
+                                                   ("c2_lz4raw_v2", gen.c2_cols(), gen.CONFIG_SEEDS["C2"], True, "LZ4", "2.0")):
+        rows = args.rows
+        f = gen.build(cols, rows, 1, seed=seed, first_rg=J.rank)
+        dc = J.ctx.upload(f, [capi.File(f).chunk(0, 0)])
+        dc.decode()
+        h = dc.to_host()
+        dc.free()
+        ref = sha(capi.canonical_dump(h))
+        valid = np.asarray(h.validity)
+        arr = pa.LargeStringArray.from_buffers(
+            h.num_rows, pa.py_buffer(np.asarray(h.offsets, np.int64).tobytes()),
+            pa.py_buffer(np.asarray(h.data, np.uint8).tobytes()),
+            pa.py_buffer(np.packbits(valid.astype(bool), bitorder="little").tobytes()),
+            null_count=int(h.num_rows - valid.sum()))
+        del h
+        b = io.BytesIO()
+        pq.write_table(pa.table({"s": arr}), b, compression=codec, data_page_version=ver, use_dictionary=use_dict,
+                       row_group_size=rows)
+        cf = b.getvalue()
+        d = capi.File(cf).chunk(0, 0)
+        d.ext_flags = capi.EXT_CODECS | capi.EXT_PAGE_V2
+        up, ck = [], []
+        for _ in range(3):
+            J.ctx.timing(True)
+            J.ctx.timing_reset()
+            t0 = time.perf_counter()
+            x = J.ctx.upload(cf, [d])
+            up.append(time.perf_counter() - t0)
+            J.ctx.sync()
+            ck.append(J.ctx.timing_get("codec")[0])
+            J.ctx.timing(False)
+            x.free()
+        x = J.ctx.upload(cf, [d])
+        x.decode()
+        ok = sha(capi.canonical_dump(x.to_host())) == ref
+        steps = max(3, args.steps // 4)
+        secs, kern = J.timed(x.decode_async, x.decode_check, steps, args.repeats, warmup=2)
+        ub = x.payload_bytes
+        x.free()
+        kms = statistics.median(ck)
+        out[name] = {"codec": codec, "page_version": ver, "rows": rows, "file_bytes": len(cf), "uncompressed_payload": ub,
+                     "codec_kernel_ms": kms, "codec_GBs_out": ub / (kms * 1e-3) / 1e9 if kms else None,
+                     "upload_ms": statistics.median(up) * 1e3, "decode_ms": statistics.median(secs) / steps * 1e3,
+                     "validated": ok}
+    return out
+
+
 def c5_leg(J, args, exp):
     """C5 at --c5-rgs row groups of 10M rows per GPU: every row group is its
     own chunk (ColumnReader is per chunk; each has its own dictionary page).
@@ -688,6 +753,8 @@ def main():
         result["c4"] = c4_leg(J, args)
     if not args.no_c5:
         result["c5"] = c5_leg(J, args, exp)
+    if not args.no_ext:
+        result["ext"] = ext_leg(J, args)
     if cpu is not None:
         st = cpu["single_thread"]
         result["cpu_baseline"] = {"value": st["value"], "unit": "values/s", "cores": 1, "kind": "reference",

@@ -73,6 +73,7 @@ struct pq_ctx {
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
+    bool opt_plain_fused = true; // "plain_fused": their one-pass form when the pages' character counts are known
     bool opt_zflip = true;       // "zflip": per-decode flags from the block the previous k_pipe_write cleared (else a fill)
     int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
@@ -144,12 +145,15 @@ struct pq_chunk {
     bool plain = false;
     std::vector<pqk::DevBatch> hpwins;
     pqk::DevBatch* d_pwins = nullptr;
+    std::vector<int64_t> hpwbase;      // k_plain_fused: first output byte per window (+ total), or empty
+    int64_t* d_pwbase = nullptr;
     uint32_t* d_rowinfo = nullptr;
     int64_t* d_wchars = nullptr;
     unsigned long long* d_pbsum = nullptr;
     int plain_grid = 0;
     // pages larger than a window: speculative chunk chains (plain_ba.hip k_plain_spec)
     bool plain_spec = false, spec_failed = false;
+    bool pfused_failed = false;          // k_plain_fused gave up on this chunk: two passes from now on
     std::vector<int32_t> hchunk_base;
     std::vector<uint2> hchunks;
     int32_t* d_chunk_base = nullptr;
@@ -334,6 +338,7 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_tile_chars);
     dfree(c->d_tile_rank);
     dfree(c->d_pwins);
+    dfree(c->d_pwbase);
     dfree(c->d_rowinfo);
     dfree(c->d_wchars);
     dfree(c->d_pbsum);
@@ -424,6 +429,7 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
     c->plain = false;
     c->plain_spec = false;
     c->hpwins.clear();
+    c->hpwbase.clear();
     c->hchunk_base.clear();
     c->hchunks.clear();
     if (c->type != PQ_BYTE_ARRAY || c->max_def != 0 || c->max_rep != 0 || pages.empty()) return;
@@ -480,6 +486,21 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
             c->hpwins.push_back(b);
             p = q;
         }
+        // one-pass form (k_plain_fused): a page's strings fill it exactly, so
+        // its characters are size - 4 * num_values; verified on the device
+        bool known = true;
+        c->hpwbase.reserve(c->hpwins.size() + 1);
+        c->hpwbase.push_back(0);
+        for (const auto& b : c->hpwins) {
+            int64_t ch = 0;
+            for (int32_t q = b.p0; q < b.p0 + b.np; q++) {
+                const int64_t x = static_cast<int64_t>(pages[static_cast<size_t>(q)].size) - 4 * static_cast<int64_t>(pages[static_cast<size_t>(q)].nvals);
+                known &= x >= 0;
+                ch += x;
+            }
+            c->hpwbase.push_back(c->hpwbase.back() + ch);
+        }
+        if (!known) c->hpwbase.clear();
     }
     const int cus = ctx->cus;
     c->plain_grid = cus * pqk::plain_write_blocks_per_cu();
@@ -621,6 +642,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
+    if (std::strcmp(key, "plain_fused") == 0) { ctx->opt_plain_fused = value != 0; return 0; }
     if (std::strcmp(key, "pipe_run_pages") == 0) {
         if (value < 1 || value > 32) return set_err(ctx, PQ_ERR_ARG, "pipe_run_pages: 1..32");
         ctx->opt_run_pages = static_cast<int>(value);
@@ -976,6 +998,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         }
         if (c->plain) {
             rc |= dalloc(&c->d_pwins, c->hpwins.size());
+            if (!c->hpwbase.empty()) rc |= dalloc(&c->d_pwbase, c->hpwbase.size());
             rc |= dalloc(&c->d_rowinfo, static_cast<size_t>(c->nrows) + 64);
             rc |= dalloc(&c->d_wchars, c->hpwins.size());
             rc |= dalloc(&c->d_pbsum, static_cast<size_t>(c->plain_grid));
@@ -1206,6 +1229,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         }
         if (c->d_bigp) put(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t));
         if (c->d_pwins) put(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch));
+        if (c->d_pwbase) put(c->d_pwbase, c->hpwbase.data(), c->hpwbase.size() * sizeof(int64_t));
         if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
         if (!rc && !cents.empty()) {
             std::vector<uint32_t> st(cents.size());
@@ -1525,6 +1549,9 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             P.pages = c->d_ppages;
             P.page_err = c->d_perr;
             P.gate = c->d_flags + 2;
+        } else if (c->d_pwbase && ctx->opt_plain_fused && !c->pfused_failed) {
+            P.wbase = c->d_pwbase;
+            P.redo = c->d_flags + 3;
         }
         Timed t(ctx, "plain_ba");
         pqk::launch_plain_ba(s, P);
@@ -1617,6 +1644,16 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             return rc;
     if (int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync")) return rc;
     flags[0] |= dflag;
+    if (flags[3] && c->plain && !c->plain_spec && !c->pfused_failed) {
+        // a page's strings did not fill it exactly (or its chain failed): the
+        // one-pass PLAIN kernel's character placement does not hold; the two
+        // passes decode the chunk from now on (and report any error)
+        c->pfused_failed = true;
+        if (!out) out = c->last_out;
+        if (!out) return set_err(ctx, PQ_ERR_ARG, "decode check without an output column");
+        if (int rc = pq_decode_async(ctx, c, out)) return rc;
+        return collect(ctx, c, out);
+    }
     if (flags[2] && c->plain_spec && !c->spec_failed) {
         if (std::getenv("PQ_DEBUG_SPEC"))
         {

@@ -868,15 +868,6 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     WriteLds& S = reinterpret_cast<WriteLds*>(smem + a.dict_bytes)[wv];
     const DevDict d = a.dicts[a.dict_id];
     const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
-        uint4* dst = reinterpret_cast<uint4*>(dw);
-        copy_blocks(dst, src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
-        copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
-            return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
-        });
-    }
-    __syncthreads();
     // each wavefront owns a contiguous run of tiles (consecutive rows): the
     // descriptors of up to 64 tiles are loaded at once, one per lane, and the
     // next tile's codes are loaded before this tile's stores are issued
@@ -884,7 +875,8 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
     const int tb = min(a.ntiles, ta + per);
     // first output byte of the range: the workgroups before this one (bsum,
-    // summed by k_pipe_codes), then this workgroup's earlier tiles
+    // summed by k_pipe_codes), then this workgroup's earlier tiles.  Both
+    // sums load together with the dictionary (one wait, one barrier).
     __shared__ unsigned long long red[kWriteMax];
     auto wave_sum64 = [](unsigned long long v) {
         for (int d = 1; d < kWave; d <<= 1) {
@@ -894,22 +886,27 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
         }
         return v;
     };
-    {
-        unsigned long long acc = 0;
-        for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) acc += a.bsum[b];
-        acc = wave_sum64(acc);
-        if (lane() == 0) red[wv] = acc;
-    }
-    __syncthreads();
-    int64_t Grun = 0;
-    for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
-    if (a.debug & 8) return;
+    unsigned long long acc = 0, in = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) acc += a.bsum[b];
     {
         const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
-        unsigned long long in = 0;
         for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
-        Grun += static_cast<int64_t>(wave_sum64(in));
     }
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
+        uint4* dst = reinterpret_cast<uint4*>(dw);
+        copy_blocks(dst, src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
+        copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
+            return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
+        });
+    }
+    acc = wave_sum64(acc);
+    if (lane() == 0) red[wv] = acc;
+    in = wave_sum64(in);
+    __syncthreads();
+    int64_t Grun = static_cast<int64_t>(in);
+    for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
+    if (a.debug & 8) return;
     for (int c0 = ta; c0 < tb; c0 += kWave) {
         const int cn = min(kWave, tb - c0);
         int64_t myR0 = 0, myG0 = 0;

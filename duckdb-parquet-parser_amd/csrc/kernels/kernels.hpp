@@ -254,6 +254,9 @@ struct PlainLaunch {
     DevErr* page_err;
     int32_t* err_any;
     const int32_t* gate;         // non-null: skip everything when *gate != 0 (the spec path fell back)
+    const int64_t* wbase;        // non-null: first output byte of every window (nwins + 1), the one-pass kernel runs
+    int32_t* redo;               // with wbase: set by the one-pass kernel when a page does not fit its
+                                 // form (the host then decodes the chunk with the two passes)
 };
 int plain_write_blocks_per_cu();
 

@@ -1,7 +1,8 @@
 // plain_ba.hip — PLAIN BYTE_ARRAY decode for REQUIRED chunks (SURVEY §8a
 // R-PLAIN: column_reader.cpp:213-222 + read_plain_value 249-253, a u32 length
 // then the bytes, per value) in two passes over windows of consecutive pages
-// (one contiguous image range of at most kPWin bytes):
+// (one contiguous image range of at most kPWin bytes), or in one pass
+// (k_plain_fused, below) when the pages' character counts are known:
 //   k_plain_walk   persistent waves, one window at a time: the window is
 //                  staged in LDS and each lane walks one page's length chain, writing
 //                  (position in window, length) per row and the window's
@@ -198,6 +199,122 @@ __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
             }
         }
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ── one-pass form: walk + write per window ───────────────────────────────
+// For REQUIRED pages whose strings fill the page exactly (the usual layout),
+// a page's characters are size - 4 * num_values, so the host knows every
+// window's first output byte (PlainLaunch.wbase) and one pass can do both
+// jobs: the window is staged once (the next window's bytes load into
+// registers while this one is decoded), each lane walks one page's length
+// chain into an LDS row list, and the rows become offsets and characters as
+// in k_plain_write.  A page whose chain does not end exactly at its end (an
+// error, or bytes after its last string) sets *redo, and the host decodes
+// the chunk again with the two passes (which report the reference's errors).
+constexpr int kPFWaves = 4;
+constexpr uint32_t kPFBlocks = kPWin / 16 + 1;                       // staged 16-byte blocks per window
+constexpr uint32_t kPFLoads = (kPFBlocks + kWave - 1) / kWave;       // prefetch registers per lane
+struct PFLds {
+    uint32_t stage[kPWin / 4 + 8];
+    uint16_t list[kPWin / 4];  // window offset of each row's characters
+};
+
+__global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    PFLds& S = reinterpret_cast<PFLds*>(smem)[wv];
+    const int nw = static_cast<int>(gridDim.x) * kPFWaves;
+    int w = static_cast<int>(blockIdx.x) * kPFWaves + wv;
+    if (w >= a.nwins) return;
+    uint4 pf[kPFLoads];
+    auto fetch = [&](const DevBatch& W) {
+        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + W.img_lo);
+        const uint32_t nb = (W.img_bytes + 15) / 16 + 1;
+#pragma unroll
+        for (uint32_t k = 0; k < kPFLoads; k++) {
+            const uint32_t b = lane() + k * kWave;
+            pf[k] = b < nb ? src[b] : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    DevBatch W = a.wins[w];
+    fetch(W);
+    for (;;) {
+        const DevBatch Wc = W;
+        const int64_t G0 = a.wbase[w];
+#pragma unroll
+        for (uint32_t k = 0; k < kPFLoads; k++) {
+            const uint32_t b = lane() + k * kWave;
+            if (b < kPFBlocks) reinterpret_cast<uint4*>(S.stage)[b] = pf[k];
+        }
+        const int wn = w + nw;
+        if (wn < a.nwins) {
+            W = a.wins[wn];
+            fetch(W);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // one lane per page: the length chain into the row list
+        const bool act = static_cast<int>(lane()) < Wc.np;
+        DevPage pg{};
+        if (act) pg = a.pages[Wc.p0 + static_cast<int>(lane())];
+        const uint32_t n = act ? static_cast<uint32_t>(max(pg.nvals, 0)) : 0u;
+        const uint32_t rinc = wave_incl_scan(n);
+        const uint32_t rows = bcast_last(rinc);
+        if (act) {
+            const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+            const uint32_t base = static_cast<uint32_t>(pg.off - Wc.img_lo);
+            uint16_t* lst = S.list + (rinc - n);
+            uint32_t pos = 0;
+            bool bad = false;
+            for (uint32_t k = 0; k < n; k++) {
+                if (pos + 4 > size) { bad = true; break; }
+                const uint32_t len = st_u32(S.stage, base + pos);
+                if (len > size - pos - 4) { bad = true; break; }
+                lst[k] = static_cast<uint16_t>(base + pos + 4);
+                pos += 4 + len;
+            }
+            if (bad || pos != size) atomicOr(a.redo, 1);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int64_t R0 = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pg.first_row))) |
+                           (static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pg.first_row >> 32))) << 32);
+        const int64_t G1 = a.wbase[w + 1];
+        // validity: every row of a REQUIRED column is set
+        {
+            const int64_t gfirst = R0 >> 5, glast = rows ? (R0 + rows - 1) >> 5 : gfirst - 1;
+            for (int64_t g = gfirst + lane(); g <= glast; g += kWave) {
+                const int64_t lo = max(g * 32, R0), hi = min(g * 32 + 32, R0 + static_cast<int64_t>(rows));
+                const uint32_t nbit = static_cast<uint32_t>(hi - lo), sh = static_cast<uint32_t>(lo - g * 32);
+                const uint32_t val = (nbit >= 32 ? 0xFFFFFFFFu : ((1u << nbit) - 1u)) << sh;
+                if (nbit == 32) a.validity[g] = val;
+                else atomicOr(&a.validity[g], val);
+            }
+        }
+        if (R0 + rows == a.nrows_total && lane() == 0) {
+            a.offsets[a.nrows_total] = G1;
+            *a.total = G1;
+        }
+        const bool fits = G1 <= a.capacity;
+        if (!fits && lane() == 0) atomicOr(a.overflow, 1);
+        uint32_t run = 0;
+        for (uint32_t g0 = 0; g0 < rows; g0 += kWave) {
+            const uint32_t r = g0 + lane();
+            uint32_t q = 4, len = 0;
+            if (r < rows) {
+                q = S.list[r];
+                len = st_u32(S.stage, q - 4);
+            }
+            const uint32_t inc = wave_incl_scan(len);
+            const uint32_t s0 = run + inc - len;
+            if (r < rows) a.offsets[R0 + r] = G0 + s0;
+            run += bcast_last(inc);
+            if (fits && r < rows && len) rc::copy_row(a.chars + G0 + s0, S.stage, q, len);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (wn >= a.nwins) break;
+        w = wn;
     }
 }
 
@@ -649,6 +766,23 @@ void launch_plain_big_rows(hipStream_t s, const uint8_t* bytes, const DevPage* p
 
 void launch_plain_ba(hipStream_t s, PlainLaunch P) {
     if (P.nwins <= 0) return;
+    if (P.wbase) {  // one pass (the host re-runs the two passes if it sets *redo)
+        static int fgrid = 0;
+        const uint32_t lds = kPFWaves * static_cast<uint32_t>(sizeof(PFLds));
+        if (!fgrid) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_plain_fused), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      static_cast<int>(lds));
+            int bpc = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(k_plain_fused),
+                                                             kPFWaves * kWave, lds) != hipSuccess || bpc < 1)
+                bpc = 1;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1) cus = 256;
+            fgrid = bpc * cus;
+        }
+        const int need = (P.nwins + kPFWaves - 1) / kPFWaves;
+        hipLaunchKernelGGL(k_plain_fused, dim3(std::min(need, fgrid)), dim3(kPFWaves * kWave), lds, s, P);
+        return;
+    }
     int grid = 0, per = 0;
     plain_shape(P, &grid, &per);
     P.per = per;

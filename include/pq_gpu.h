@@ -145,6 +145,8 @@ int pq_ctx_sync(pq_ctx* ctx);
  *                 (k_pipe_big; coverage of that kernel on small pages), 0 (default)
  *   "pipe_run_pages" pages per wavefront of the run-table pass, 1..32 (32)
  *   "plain_ba"    1 (default): two-pass PLAIN BYTE_ARRAY kernels
+ *   "plain_fused" 1 (default): their one-pass form when every page's strings
+ *                 fill it exactly (checked on the device; else the two passes)
  *   "fixed_plain" 1 (default): tile-parallel PLAIN fixed-width kernels
  *   "fused_ba"    1 (default): per-page fused BYTE_ARRAY kernel for chunks the
  *                 pipe does not take; 0 forces the generic rows/scan/gather kernels

@@ -22,7 +22,7 @@ rc=$?; tail -3 "$OUT/pytest_gpu.log"; [ $rc -eq 0 ] || { echo "PYTEST rc=$rc"; e
 timeout -k 10 600 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; cat "$OUT/bench.json"; [ $rc -eq 0 ] || { echo "BENCH rc=$rc"; tail -20 "$OUT/bench.err"; exit $rc; }
 
-HEAD_ARGS="--no-cpu --no-c4 --no-c5"
+HEAD_ARGS="--no-cpu --no-c4 --no-c5 --no-ext"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_kt" -o kt --output-format csv -- \
     python3 bench.py --steps 10 --warmup 2 $HEAD_ARGS "$@" > "$OUT/prof_kt.log" 2>&1
 rc=$?; [ $rc -eq 0 ] || { echo "KT rc=$rc"; tail -20 "$OUT/prof_kt.log"; exit $rc; }

@@ -50,15 +50,17 @@ def path(request, ctx):
     (the large-page kernel) so it also meets small pages; "fused" forces the
     per-page fused BYTE_ARRAY kernel (dict_fused.hip) onto every BYTE_ARRAY
     chunk it can take; "generic" forces decode.hip's rows/scan/gather and
-    per-page k_fixed."""
+    per-page k_fixed.  PLAIN BYTE_ARRAY chunks take the one-pass kernel
+    (k_plain_fused) under "default" and the two passes under "big"."""
     p = request.param
     ctx.set_option("big_all", int(p == "big"))
     ctx.set_option("dict_pipe", int(p in ("default", "big")))
     ctx.set_option("plain_ba", int(p in ("default", "big")))
     ctx.set_option("fused_ba", int(p != "generic"))
     ctx.set_option("fixed_plain", int(p != "generic"))
+    ctx.set_option("plain_fused", int(p != "big"))
     yield p
-    for k in ("dict_pipe", "plain_ba", "fused_ba", "fixed_plain"):
+    for k in ("dict_pipe", "plain_ba", "fused_ba", "fixed_plain", "plain_fused"):
         ctx.set_option(k, 1)
     ctx.set_option("big_all", 0)
 
