@@ -261,23 +261,29 @@ __global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
         const uint32_t n = act ? static_cast<uint32_t>(max(pg.nvals, 0)) : 0u;
         const uint32_t rinc = wave_incl_scan(n);
         const uint32_t rows = bcast_last(rinc);
-        if (act) {
+        bool misfit = act && rinc > kPWin / 4;  // more rows than 4-byte strings fit: not this form
+        if (act && !misfit) {
             const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
             const uint32_t base = static_cast<uint32_t>(pg.off - Wc.img_lo);
             uint16_t* lst = S.list + (rinc - n);
             uint32_t pos = 0;
-            bool bad = false;
             for (uint32_t k = 0; k < n; k++) {
-                if (pos + 4 > size) { bad = true; break; }
+                if (pos + 4 > size) { misfit = true; break; }
                 const uint32_t len = st_u32(S.stage, base + pos);
-                if (len > size - pos - 4) { bad = true; break; }
+                if (len > size - pos - 4) { misfit = true; break; }
                 lst[k] = static_cast<uint16_t>(base + pos + 4);
                 pos += 4 + len;
             }
-            if (bad || pos != size) atomicOr(a.redo, 1);
+            misfit |= pos != size;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (__ballot(misfit)) {  // the two passes redo the chunk; this window's row list is not whole
+            if (lane() == 0) atomicOr(a.redo, 1);
+            if (wn >= a.nwins) break;
+            w = wn;
+            continue;
+        }
         const int64_t R0 = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pg.first_row))) |
                            (static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pg.first_row >> 32))) << 32);
         const int64_t G1 = a.wbase[w + 1];
