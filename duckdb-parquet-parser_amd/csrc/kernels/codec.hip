@@ -30,6 +30,7 @@
 //   LZ4      (codec 5): Hadoop framing ([u32 BE raw][u32 BE packed] blocks)
 //   LZ4_RAW  (codec 7): one LZ4 block
 #include <algorithm>
+#include <cstddef>
 
 #include "kernels/device_common.hpp"
 #include "kernels/kernels.hpp"
@@ -59,6 +60,24 @@ struct CodecLds {
     uint32_t scratch[4];
 };
 
+// LDS pointers keep their address space (a generic pointer held in a struct
+// compiles to flat accesses, which also count in the vector memory counter)
+using lds8 = __attribute__((address_space(3))) uint8_t;
+using lds16 = __attribute__((address_space(3))) uint16_t;
+using lds32 = __attribute__((address_space(3))) uint32_t;
+
+__device__ __forceinline__ void lds_put16(lds8* base, uint32_t off, const uint4& v) {
+    lds32* d = reinterpret_cast<lds32*>(base + off);
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+}
+__device__ __forceinline__ uint4 lds_get16(const lds8* base, uint32_t off) {
+    const lds32* d = reinterpret_cast<const lds32*>(base + off);
+    return make_uint4(d[0], d[1], d[2], d[3]);
+}
+
 __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -72,25 +91,26 @@ struct In {
     uint32_t len;      // input bytes
     uint32_t wlo;      // input byte held at in[sh]
     uint32_t sh;
-    uint8_t* w;
+    lds8* w;
     __device__ __forceinline__ void refill(uint32_t p) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(g) + p;
-        const uintptr_t A = a & ~static_cast<uintptr_t>(15);
-        const uintptr_t e = reinterpret_cast<uintptr_t>(g) + len;  // blocks at or past e are not loaded
         wlo = p;
-        sh = static_cast<uint32_t>(a - A);
-        const uint4* src = reinterpret_cast<const uint4*>(A);
-        uint4* dst = reinterpret_cast<uint4*>(w);
+        sh = static_cast<uint32_t>(a & 15u);
+        // (derived from g, so the loads stay global: a pointer made from an
+        // integer would compile to flat loads)
+        const uint4* src = reinterpret_cast<const uint4*>(g + p - sh);  // (g + p) - sh: never below g's buffer
         constexpr uint32_t nb = kInWin / 16;
+        const uint32_t nvalid = (sh + len > p ? (sh + len - p + 15) / 16 : 0u);  // blocks holding input bytes
         uint4 v[nb / kWave];
 #pragma unroll
         for (uint32_t k = 0; k < nb / kWave; k++) {
             const uint32_t b = lane() + k * kWave;
-            v[k] = A + 16u * b < e ? src[b] : make_uint4(0u, 0u, 0u, 0u);
+            const uint4 x = src[min(b, nvalid ? nvalid - 1 : 0u)];
+            v[k] = b < nvalid ? x : make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
-        for (uint32_t k = 0; k < nb / kWave; k++) dst[lane() + k * kWave] = v[k];
-        if (lane() < 2) dst[nb + lane()] = make_uint4(0u, 0u, 0u, 0u);
+        for (uint32_t k = 0; k < nb / kWave; k++) lds_put16(w, 16 * (lane() + k * kWave), v[k]);
+        if (lane() < 2) lds_put16(w, 16 * (nb + lane()), make_uint4(0u, 0u, 0u, 0u));
         wsync();
     }
     // bytes [p, p + k) staged (k <= 16)
@@ -112,7 +132,7 @@ enum : uint32_t { ST_OK = 0, ST_CORRUPT = 1, ST_SIZE = 2, ST_UNSUPPORTED = 3 };
 
 // ── output ring ────────────────────────────────────────────────────────────
 struct Out {
-    uint8_t* ring;
+    lds8* ring;
     uint8_t* dst;   // the page slot (16-byte aligned)
     uint32_t op;    // bytes produced
     uint32_t fl;    // bytes flushed to dst (multiple of 16 until the end)
@@ -124,7 +144,7 @@ struct Out {
             const uint32_t n = min(kFlush, op - fl);
             const uint32_t b = fl + 16u * lane();
             if (b < fl + n) {
-                uint4 v = *reinterpret_cast<const uint4*>(ring + (b & kRingMask));
+                uint4 v = lds_get16(ring, b & kRingMask);
                 if (b + 16 > op) {  // bytes past the payload stay zero (slot padding)
                     const int32_t keep = static_cast<int32_t>(op - b);
                     auto mk = [&](int j) -> uint32_t {
@@ -579,11 +599,13 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
                                                  uint32_t* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     CodecLds& L = *reinterpret_cast<CodecLds*>(smem);
+    lds8* lring = (lds8*)(smem + offsetof(CodecLds, ring));
+    lds8* lin = (lds8*)(smem + offsetof(CodecLds, in));
     for (int32_t i = static_cast<int32_t>(blockIdx.x); i < n; i += static_cast<int32_t>(gridDim.x)) {
         const CodecEntry e = ent[i];
-        In I{src + e.src, e.src_len, 0u, 0u, L.in};
+        In I{src + e.src, e.src_len, 0u, 0u, lin};
         I.refill(0);
-        Out O{L.ring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
+        Out O{lring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
         uint32_t p = 0;
         if (e.flags & kCodecV2) {  // level sections, as is, behind their V1 length prefixes
             const uint32_t lv = e.def_len + e.rep_len;

@@ -78,8 +78,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
                                                               int32_t max_def, int32_t max_rep,
                                                               uint2* __restrict__ runs,
                                                               uint32_t* __restrict__ info, int ppw,
-                                                              int32_t* __restrict__ flist, uint32_t stage_max,
-                                                              int debug) {
+                                                              int32_t* __restrict__ flist, uint32_t stage_max) {
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[kRunWaves][kRunStage / 4 + 8];
     const uint32_t wv = threadIdx.x / kWave;
     const int g0 = (blockIdx.x * kRunWaves + static_cast<int>(wv)) * ppw;
@@ -154,11 +153,6 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
             W.bw = s ? bwi : level_bw(max_def);
             W.n = n;
             W.out = runs + (static_cast<size_t>(p) * 2 + s) * kPipeRunCap;
-            W.stride = (debug & 0x1000) ? 0u : 1u;  // timing probes: no record stores
-            if (debug & 0x4000) {                    // timing probe: lane-interleaved records
-                W.out = runs + static_cast<size_t>(g0) * 2 * kPipeRunCap + lane();
-                W.stride = kWave;
-            }
             W.cap = kPipeRunCap;
             W.sbase = sbase;
             W.gp = gp;
@@ -576,17 +570,23 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
         const int cn = min(kWave, tb - c0);
         uint32_t myp = 0, myrow0 = 0, mym = 0, myinf = kFallback, mysize = 0, mytp = 0;
         uint64_t myoff = 0, myfirst = 0;
-        if (static_cast<int>(lane()) < cn) {
-            const DevTile T = a.tiles[c0 + lane()];
+        {  // (loads from clamped in-bounds indices, selected after: a load under a
+           // lane condition compiles to a flat load from a select with a stack
+           // address, and flat loads also count in lgkmcnt, so every LDS wait of
+           // the tile would wait for the prefetch too)
+            const bool in = static_cast<int>(lane()) < cn;
+            const DevTile T = a.tiles[c0 + min(static_cast<int>(lane()), cn - 1)];
             const DevPage pg = a.pages[T.page];
-            myp = static_cast<uint32_t>(T.page);
-            myrow0 = static_cast<uint32_t>(T.row0);
-            mym = static_cast<uint32_t>(T.nrows);
-            myinf = a.info[T.page];
-            mytp = static_cast<uint32_t>(a.page_tile0[T.page]);
-            mysize = static_cast<uint32_t>(max(pg.size, 0));
-            myoff = pg.off;
-            myfirst = static_cast<uint64_t>(pg.first_row);
+            const uint32_t inf = a.info[T.page];
+            const uint32_t tp = static_cast<uint32_t>(a.page_tile0[T.page]);
+            myp = in ? static_cast<uint32_t>(T.page) : 0u;
+            myrow0 = in ? static_cast<uint32_t>(T.row0) : 0u;
+            mym = in ? static_cast<uint32_t>(T.nrows) : 0u;
+            myinf = in ? inf : kFallback;
+            mytp = in ? tp : 0u;
+            mysize = in ? static_cast<uint32_t>(max(pg.size, 0)) : 0u;
+            myoff = in ? pg.off : 0ull;
+            myfirst = in ? static_cast<uint64_t>(pg.first_row) : 0ull;
         }
         uint2 rq0, rq1, rq2, rq3;
         uint4 sq0, sq1, sq2, sq3, sq4;
@@ -599,23 +599,32 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
             const uint64_t off = rl64(myoff, i);
             const bool skip = (inf & kSkip) || !lean;  // k_pipe_runs marks pages past the stage
             const uint32_t nd = skip ? 0u : (inf & 0xFFu), ni = skip ? 0u : ((inf >> 8) & 0xFFu);
+            // every load from an in-bounds index (the page's 2 x kPipeRunCap
+            // record block; blocks of its payload slot), selected after
             const uint2* rd_ = a.runs + static_cast<size_t>(pp) * 2 * kPipeRunCap;
             const uint2 z = make_uint2(0u, 0u);
-            rq0 = lane() < nd ? rd_[lane()] : z;
-            rq1 = lane() + kWave < nd ? rd_[lane() + kWave] : z;
-            rq2 = lane() < ni ? rd_[kPipeRunCap + lane()] : z;
-            rq3 = lane() + kWave < ni ? rd_[kPipeRunCap + lane() + kWave] : z;
+            const uint2 r0 = rd_[lane()], r1 = rd_[lane() + kWave];
+            const uint2 r2 = rd_[kPipeRunCap + lane()], r3 = rd_[kPipeRunCap + lane() + kWave];
+            rq0 = lane() < nd ? r0 : z;
+            rq1 = lane() + kWave < nd ? r1 : z;
+            rq2 = lane() < ni ? r2 : z;
+            rq3 = lane() + kWave < ni ? r3 : z;
             const uint32_t nb = skip ? 0u : (sz + 15) / 16 + 1;
+            const uint32_t nbl = nb ? nb - 1 : 0u;  // last block of the slot (block 0 always exists)
             const uint4* src = reinterpret_cast<const uint4*>(a.bytes + off);
             const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-            sq0 = lane() < nb ? src[lane()] : z4;
-            sq1 = lane() + kWave < nb ? src[lane() + kWave] : z4;
-            sq2 = lane() + 2 * kWave < nb ? src[lane() + 2 * kWave] : z4;
-            sq3 = lane() + 3 * kWave < nb ? src[lane() + 3 * kWave] : z4;
-            sq4 = lane() + 4 * kWave < nb ? src[lane() + 4 * kWave] : z4;
+            const uint4 b0 = src[min(lane(), nbl)], b1 = src[min(lane() + kWave, nbl)],
+                        b2 = src[min(lane() + 2 * kWave, nbl)], b3 = src[min(lane() + 3 * kWave, nbl)],
+                        b4 = src[min(lane() + 4 * kWave, nbl)];
+            sq0 = lane() < nb ? b0 : z4;
+            sq1 = lane() + kWave < nb ? b1 : z4;
+            sq2 = lane() + 2 * kWave < nb ? b2 : z4;
+            sq3 = lane() + 3 * kWave < nb ? b3 : z4;
+            sq4 = lane() + 4 * kWave < nb ? b4 : z4;
             // non-null counts of the page's earlier tiles (pages of <= 2048 rows: <= 3)
             const uint32_t t = static_cast<uint32_t>(c0 + i);
-            tnn = (md > 0 && !skip && tp + lane() < t) ? static_cast<uint32_t>(a.tile_nn[tp + lane()]) : 0u;
+            const uint32_t tn = static_cast<uint32_t>(a.tile_nn[min(tp + lane(), static_cast<uint32_t>(a.ntiles - 1))]);
+            tnn = (md > 0 && !skip && tp + lane() < t) ? tn : 0u;
         };
         prefetch(0);
         for (int i = 0; i < cn; i++) {
@@ -1333,6 +1342,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     copy_map(lens, a.entries + ebase, nl, tid, kBigThreads, [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
     if (tid < 8) sh[tid] = 0;
     __syncthreads();
+    if (a.debug & 0x10000) return;  // timing: staging only
     // 1. speculative headers at every byte of both streams
     for (uint32_t j = tid; j < size; j += kBigThreads) {
         if (!in_stream(j)) continue;
@@ -1343,6 +1353,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         tab[j] = static_cast<uint16_t>((big_bad(h, e, (bw + 7) / 8) || nx >= e) ? kBStop : static_cast<uint32_t>(nx));
     }
     __syncthreads();
+    if (a.debug & 0x20000) return;  // timing: + header parse
     // 2. kBJump-run jumps by pointer doubling
     for (int r = 0; r < kBJumpLog; r++) {
         uint32_t nv[kBigPerThread];
@@ -1603,13 +1614,13 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
-                      int debug) {
+                      int) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     if (npages <= 0) return;
     const int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
     const int per = kRunWaves * ppw;
     hipLaunchKernelGGL(k_pipe_runs, dim3((npages + per - 1) / per), dim3(kRunWaves * kWave), 0, s, bytes, pages,
-                       npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16, debug);
+                       npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's

@@ -254,7 +254,6 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
         }
     } else if (sh[0] == 0 && wv == 0) {
         RunWalk W{};
-        W.stride = 1;
         W.alive = lane() == 0;
         W.q = 4;
         W.end = 4 + dlen;

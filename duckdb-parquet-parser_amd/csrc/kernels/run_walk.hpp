@@ -14,7 +14,6 @@ namespace dev {
 struct RunWalk {
     bool alive;
     uint32_t q, end, bw, n, sbase, cap;
-    uint32_t stride;  // record stride in uint2 (1: contiguous per stream)
     uint2* out;
     const uint8_t* gp;
 };
@@ -67,14 +66,16 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
         const uint32_t full = nr >= W.cap ? 1u : 0u;
         const uint32_t ok = (alive ? 1u : 0u) & (full ^ 1u) & (exh | (badh ^ 1u));
         const uint32_t rx = cnt | ((exh ? left : c) << 16);
-        const uint32_t pl = lit ? (litpay | (qh * litmul)) : (vraw & vmask);
+        // selects by mask (the compiler turns a ternary on `lit` into a branch)
+        const uint32_t litm = 0u - lit;
+        const uint32_t pl = (litm & (litpay | (qh * litmul))) | (~litm & vraw & vmask);
         const uint32_t ry = exh ? 0u : pl;
-        if (ok && W.stride) W.out[static_cast<size_t>(nr) * W.stride] = make_uint2(rx, ry);
+        if (ok) W.out[nr] = make_uint2(rx, ry);
         fl |= (alive ? 1u : 0u) & (ok ^ 1u);
         nr += ok;
-        const uint64_t nql = static_cast<uint64_t>(qh) + static_cast<uint64_t>(g) * W.bw;
-        const uint32_t nqlc = nql > W.end ? W.end : static_cast<uint32_t>(nql);
-        const uint32_t nq = lit ? nqlc : qh + nbv;
+        // g clamps at 2^16: a longer literal run overruns the stream (<= 64 KiB) either way
+        const uint32_t nqlc = min(qh + min(g, 0x10000u) * W.bw, W.end);
+        const uint32_t nq = (litm & nqlc) | (~litm & (qh + nbv));
         cnt = exh ? W.n : cnt + c;
         q = ok ? nq : q;
         alive = ok && !exh && cnt < W.n;
