@@ -1876,7 +1876,6 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
         int64_t dict_cap = std::max<int64_t>(c->nentries, 1);
         if (c->dict_match_cap < dict_cap) {
             dfree(c->d_dict_match);
-    dfree(c->d_dfa);
             if (dalloc(&c->d_dict_match, static_cast<size_t>(dict_cap)))
                 return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (dict match)");
             c->dict_match_cap = dict_cap;

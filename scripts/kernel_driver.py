@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Run the C2 decode, the C3 regex scan or the C3 PLAIN decode a few times — a
 small target for rocprofv3 PMC passes.
-usage: kernel_driver.py [decode|regex|plain] [rows] [reps] [fused_debug]"""
+usage: kernel_driver.py [decode|regex|plain] [rows] [reps] [fused_debug]
+(env PQ_OPTS="key=value,..." sets further context options)"""
 import os
 import sys
 
@@ -15,6 +16,9 @@ reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 dbg = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 ctx = capi.Context(0)
 ctx.set_option("fused_debug", dbg)
+for kv in filter(None, os.environ.get("PQ_OPTS", "").split(",")):  # e.g. PQ_OPTS=regex_debug=1
+    k, v = kv.split("=")
+    ctx.set_option(k, int(v))
 if what == "decode":
     f = gen.build(gen.c2_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C2"])
     F = capi.File(f)

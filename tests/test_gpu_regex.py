@@ -18,7 +18,12 @@ pytestmark = pytest.mark.gpu
 
 PATTERNS = ["special.*requests", "^(carefully|quickly) ", "[0-9]", "e", "^$", "s$",
             "(ironic|bold) (foxes|ideas)", "a.{3}e", "[^a-z ]", r"\bx" if False else "ly\\s",
-            "qu?i(ck|et)ly", "^[a-z]{1,4} ", "^[a-m]"]
+            "qu?i(ck|et)ly", "^[a-z]{1,4} ", "^[a-m]",
+            "x*",            # every string matches (the scan kernels skip the automaton)
+            # prefilter literals ("pend" also occurs in "dependencies", "ly f"
+            # after both branches, "slyl" with a $ anchor)
+            "pending (foxes|ideas)", "(quick|slow)ly fur", "slyly.*deposits$", "ironic",
+            "a.{5}b.{5}c"]   # over a thousand DFA states: the byte-indexed window DFA does not fit
 
 
 def golden_pages(f: bytes, chunks, pattern: str, neg: bool) -> np.ndarray:
