@@ -467,6 +467,27 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
         }
         c->hchunk_base.push_back(static_cast<int32_t>(nch));
         c->plain_spec = true;
+        // one-pass form over the pseudo pages (k_plain_fused, wpseudo): per
+        // window, its page's first output byte (pages whose strings fill them
+        // exactly: size - 4 * num_values each, verified on the device) minus
+        // the page's image offset plus 4 x its first row
+        bool known = true;
+        std::vector<int64_t> pbase(pages.size());
+        int64_t acc = 0;
+        for (size_t p = 0; p < pages.size(); p++) {
+            pbase[p] = acc;
+            const int64_t x = static_cast<int64_t>(pages[p].size) - 4 * static_cast<int64_t>(pages[p].nvals);
+            known &= x >= 0;
+            acc += x;
+        }
+        if (known) {
+            c->hpwbase.reserve(c->hpwins.size());
+            for (const auto& b : c->hpwins) {
+                const uint2 ch = c->hchunks[static_cast<size_t>(b.p0)];
+                const DevPage& pg = pages[ch.x];
+                c->hpwbase.push_back(pbase[ch.x] - static_cast<int64_t>(pg.off) + 4 * pg.first_row);
+            }
+        }
     } else {
         size_t p = 0;
         while (p < pages.size()) {
@@ -1549,6 +1570,11 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             P.pages = c->d_ppages;
             P.page_err = c->d_perr;
             P.gate = c->d_flags + 2;
+            if (c->d_pwbase && ctx->opt_plain_fused && !c->pfused_failed) {
+                P.wbase = c->d_pwbase;
+                P.redo = c->d_flags + 3;
+                P.wpseudo = 1;
+            }
         } else if (c->d_pwbase && ctx->opt_plain_fused && !c->pfused_failed) {
             P.wbase = c->d_pwbase;
             P.redo = c->d_flags + 3;
@@ -1644,7 +1670,7 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             return rc;
     if (int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync")) return rc;
     flags[0] |= dflag;
-    if (flags[3] && c->plain && !c->plain_spec && !c->pfused_failed) {
+    if (flags[3] && c->plain && !c->pfused_failed && !(flags[2] && c->plain_spec)) {
         // a page's strings did not fill it exactly (or its chain failed): the
         // one-pass PLAIN kernel's character placement does not hold; the two
         // passes decode the chunk from now on (and report any error)

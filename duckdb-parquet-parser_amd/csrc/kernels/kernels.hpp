@@ -255,8 +255,11 @@ struct PlainLaunch {
     int32_t* err_any;
     const int32_t* gate;         // non-null: skip everything when *gate != 0 (the spec path fell back)
     const int64_t* wbase;        // non-null: first output byte of every window (nwins + 1), the one-pass kernel runs
+                                 // (pseudo pages: per window, the first output byte of its real page minus
+                                 // its image offset plus 4 x its first row; the kernel adds its first string's)
     int32_t* redo;               // with wbase: set by the one-pass kernel when a page does not fit its
                                  // form (the host then decodes the chunk with the two passes)
+    int32_t wpseudo;             // with wbase: the pages are k_plain_link's pseudo pages
 };
 int plain_write_blocks_per_cu();
 

@@ -222,6 +222,7 @@ struct PFLds {
 
 __global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.gate && *a.gate) return;  // pseudo pages: the spec pass fell back
     const int wv = static_cast<int>(threadIdx.x / kWave);
     PFLds& S = reinterpret_cast<PFLds*>(smem)[wv];
     const int nw = static_cast<int>(gridDim.x) * kPFWaves;
@@ -241,7 +242,7 @@ __global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
     fetch(W);
     for (;;) {
         const DevBatch Wc = W;
-        const int64_t G0 = a.wbase[w];
+        int64_t G0 = a.wbase[w];
 #pragma unroll
         for (uint32_t k = 0; k < kPFLoads; k++) {
             const uint32_t b = lane() + k * kWave;
@@ -286,7 +287,29 @@ __global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
         }
         const int64_t R0 = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pg.first_row))) |
                            (static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pg.first_row >> 32))) << 32);
-        const int64_t G1 = a.wbase[w + 1];
+        int64_t G1;
+        if (a.wpseudo) {
+            // pseudo pages cut one real page whose strings fill it: the
+            // characters before the window's first string are its offset in
+            // the page minus 4 per earlier row; the window's own characters
+            // are its pages' bytes minus 4 per row
+            const uint64_t sm = __ballot(act && n > 0);
+            if (!sm) {
+                if (wn >= a.nwins) break;
+                w = wn;
+                continue;
+            }
+            const int fl = static_cast<int>(__builtin_ctzll(sm));
+            const int64_t off = static_cast<int64_t>(__shfl(static_cast<long long>(pg.off), fl));
+            const int64_t fr = static_cast<int64_t>(__shfl(static_cast<long long>(pg.first_row), fl));
+            G0 += off - 4 * fr;
+            const int64_t wch = act ? static_cast<int64_t>(max(pg.size, 0)) - 4 * static_cast<int64_t>(n) : 0;
+            uint32_t lo = static_cast<uint32_t>(wch);
+            lo = wave_incl_scan(lo);
+            G1 = G0 + static_cast<int64_t>(bcast_last(lo));
+        } else {
+            G1 = a.wbase[w + 1];
+        }
         // validity: every row of a REQUIRED column is set
         {
             const int64_t gfirst = R0 >> 5, glast = rows ? (R0 + rows - 1) >> 5 : gfirst - 1;
@@ -716,7 +739,11 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
             pp.mode = MODE_PLAIN;
             pp.dict = -1;
             pp.off = pg.off + chs + ent;
-            pp.size = static_cast<int32_t>(size > chs + ent ? size - chs - ent : 0u);
+            // a chunk whose whole chain is taken: exactly its strings' bytes
+            // (the one-pass kernel checks its walk ends there); a chain cut
+            // at the value count: the rest of the page; no strings: empty
+            const uint32_t rest = size > chs + ent ? size - chs - ent : 0u;
+            pp.size = static_cast<int32_t>(take == 0 ? 0u : (take == cnt && rr.y >= chs + ent ? min(rr.y - chs - ent, rest) : rest));
             pp.nvals = static_cast<int32_t>(take);
             pp.first_row = pg.first_row + min(before, n);
             a.ppages[c] = pp;
