@@ -154,6 +154,21 @@ struct pq_chunk {
     // pages larger than a window: speculative chunk chains (plain_ba.hip k_plain_spec)
     bool plain_spec = false, spec_failed = false;
     bool pfused_failed = false;          // k_plain_fused gave up on this chunk: two passes from now on
+    // OPTIONAL chunks on the PLAIN kernels (plain_ba.hip OptLaunch): levels,
+    // value-section pages, dense offsets spread over the rows
+    bool plain_opt = false, popt_failed = false;
+    bool opt_lane_levels = false;       // every page <= kOptLaneRows rows: lane-per-page levels
+    int32_t* d_page_nn = nullptr;
+    int64_t* d_onnv = nullptr;          // per page: non-null values | characters
+    int64_t* d_ochv = nullptr;
+    int64_t* d_opdense = nullptr;       // their exclusive scans
+    int64_t* d_opbase = nullptr;
+    int64_t* d_otot = nullptr;          // [0] non-null values, [1] characters
+    DevPage* d_vpages = nullptr;
+    int64_t* d_doffs = nullptr;         // dense offsets (nrows + 1)
+    DevErr* d_operr = nullptr;          // level / chain errors of this path (not reported: the general path re-runs)
+    std::vector<int32_t> hpwpage;       // spec windows: their real page
+    int32_t* d_pwpage = nullptr;
     std::vector<int32_t> hchunk_base;
     std::vector<uint2> hchunks;
     int32_t* d_chunk_base = nullptr;
@@ -353,6 +368,8 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_chunks);
     dfree(c->d_cand);
     dfree(c->d_ppages);
+    dfree(c->d_page_nn); dfree(c->d_onnv); dfree(c->d_ochv); dfree(c->d_opdense); dfree(c->d_opbase);
+    dfree(c->d_otot); dfree(c->d_vpages); dfree(c->d_doffs); dfree(c->d_operr); dfree(c->d_pwpage);
     dfree(c->d_perr);
     dfree(c->d_page_pos);
     dfree(c->d_tile_base);
@@ -428,11 +445,17 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
 void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
     c->plain = false;
     c->plain_spec = false;
+    c->plain_opt = false;
     c->hpwins.clear();
     c->hpwbase.clear();
+    c->hpwpage.clear();
     c->hchunk_base.clear();
     c->hchunks.clear();
-    if (c->type != PQ_BYTE_ARRAY || c->max_def != 0 || c->max_rep != 0 || pages.empty()) return;
+    if (c->type != PQ_BYTE_ARRAY || c->max_def < 0 || c->max_rep != 0 || pages.empty()) return;
+    // OPTIONAL: the value sections (after the levels) are decoded as
+    // REQUIRED-shaped pages of their non-null values; the windows and chunks
+    // below cover the whole slots, which hold them
+    const bool opt = c->max_def > 0;
     auto slot = [](const DevPage& p) {
         return (static_cast<uint64_t>(std::max(p.size, 0)) + 15) / 16 * 16 + 16;
     };
@@ -467,7 +490,8 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
         }
         c->hchunk_base.push_back(static_cast<int32_t>(nch));
         c->plain_spec = true;
-        // one-pass form over the pseudo pages (k_plain_fused, wpseudo): per
+        for (const auto& b : c->hpwins) c->hpwpage.push_back(static_cast<int32_t>(c->hchunks[static_cast<size_t>(b.p0)].x));
+        // one-pass form over the pseudo pages (k_plain_fused, kWinPseudo): per
         // window, its page's first output byte (pages whose strings fill them
         // exactly: size - 4 * num_values each, verified on the device) minus
         // the page's image offset plus 4 x its first row
@@ -480,7 +504,7 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
             known &= x >= 0;
             acc += x;
         }
-        if (known) {
+        if (known && !opt) {
             c->hpwbase.reserve(c->hpwins.size());
             for (const auto& b : c->hpwins) {
                 const uint2 ch = c->hchunks[static_cast<size_t>(b.p0)];
@@ -521,8 +545,11 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
             }
             c->hpwbase.push_back(c->hpwbase.back() + ch);
         }
-        if (!known) c->hpwbase.clear();
+        if (!known || opt) c->hpwbase.clear();
     }
+    c->plain_opt = opt;
+    c->opt_lane_levels = true;
+    for (const auto& pg : pages) c->opt_lane_levels &= pg.nvals <= pqk::kOptLaneRows;
     const int cus = ctx->cus;
     c->plain_grid = cus * pqk::plain_write_blocks_per_cu();
     c->plain = true;
@@ -1002,13 +1029,26 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         }
         if (c->pipe && !hdicts.empty()) rc |= dalloc(&c->d_dflag, 1);
         rc |= dalloc(&c->d_tile_chars, htiles.size());
-        if (c->fixed_plain) {
+        if (c->fixed_plain || c->plain_opt) {
             rc |= dalloc(&c->d_tile_rank, htiles.size());
             rc |= dalloc(&c->d_page_pos, hpages.size());
         }
+        if (c->plain_opt) {
+            const size_t np = hpages.size();
+            rc |= dalloc(&c->d_page_nn, np);
+            rc |= dalloc(&c->d_onnv, np);
+            rc |= dalloc(&c->d_ochv, np);
+            rc |= dalloc(&c->d_opdense, np);
+            rc |= dalloc(&c->d_opbase, np);
+            rc |= dalloc(&c->d_otot, 2);
+            rc |= dalloc(&c->d_vpages, np);
+            rc |= dalloc(&c->d_doffs, static_cast<size_t>(c->nrows) + 1);
+            rc |= dalloc(&c->d_operr, np);
+            if (!c->hpwpage.empty()) rc |= dalloc(&c->d_pwpage, c->hpwpage.size());
+        }
         rc |= dalloc(&c->d_tile_base, htiles.size());
         rc |= dalloc(&c->d_total, 1);
-        rc |= dalloc(&c->d_scan_scratch, htiles.size() / 8192 + 16);
+        rc |= dalloc(&c->d_scan_scratch, std::max(htiles.size(), hpages.size()) / 8192 + 16);
         if (c->type == PQ_BYTE_ARRAY && !c->fused) rc |= dalloc(&c->d_row_codes, static_cast<size_t>(c->nrows));
         if (c->pipe) {
             rc |= dalloc(&c->d_runs, hpages.size() * 2 * pqk::kPipeRunCap);
@@ -1251,6 +1291,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         if (c->d_bigp) put(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t));
         if (c->d_pwins) put(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch));
         if (c->d_pwbase) put(c->d_pwbase, c->hpwbase.data(), c->hpwbase.size() * sizeof(int64_t));
+        if (c->d_pwpage) put(c->d_pwpage, c->hpwpage.data(), c->hpwpage.size() * sizeof(int32_t));
         if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
         if (!rc && !cents.empty()) {
             std::vector<uint32_t> st(cents.size());
@@ -1502,7 +1543,10 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     const bool pipe = c->pipe && ctx->opt_pipe;
     // k_pipe_write stores whole validity words when every tile starts on a
     // 32-row boundary; other paths OR bits into zeroed words
-    const bool pipe_path = pipe && !(c->plain && ctx->opt_plain);
+    // OPTIONAL chunks take the PLAIN kernels only in their one-pass form
+    const bool plain_go = c->plain && ctx->opt_plain && !(c->plain_spec && c->spec_failed) &&
+                          !(c->plain_opt && (c->popt_failed || !ctx->opt_plain_fused));
+    const bool pipe_path = pipe && !plain_go;
     if (pipe_path && c->d_zero && ctx->opt_zflip) {
         // flags, bsum and flist[0] of this decode: the other block, which the
         // previous decode's k_pipe_write cleared (else one fill)
@@ -1544,7 +1588,49 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
                                  c->d_dict_err, c->d_flags, c->type, c->plain_width);
     }
-    if (c->plain && ctx->opt_plain && !(c->plain_spec && c->spec_failed)) {
+    if (plain_go && c->plain_opt) {
+        // levels -> value-section pages -> one pass over them -> row offsets;
+        // any error or misfit sets d_flags[3] and collect() re-runs the chunk
+        // on the general path (which reports the reference's errors)
+        int32_t* redo = c->d_flags + 3;
+        Timed t(ctx, "plain_opt");
+        (void)hipMemsetAsync(c->d_operr, 0, static_cast<size_t>(c->npages) * sizeof(DevErr), s);
+        if (c->opt_lane_levels)
+            pqk::launch_opt_levels(s, c->d_bytes, c->d_pages, c->npages, c->d_page_tile0, c->max_def, out->d_validity,
+                                   c->d_tile_rank, c->d_page_pos, c->d_page_nn, c->d_operr, redo);
+        else
+            pqk::launch_fixed_levels(s, c->d_bytes, c->d_pages, c->npages, c->d_page_tile0, cp, out->d_validity,
+                                     c->d_tile_rank, c->d_page_pos, c->d_page_nn, c->d_operr, redo);
+        pqk::OptLaunch O{};
+        O.pages = c->d_pages; O.npages = c->npages; O.page_nn = c->d_page_nn; O.page_pos = c->d_page_pos;
+        O.lerr = c->d_operr; O.nnv = c->d_onnv; O.chv = c->d_ochv; O.pdense = c->d_opdense; O.pbase = c->d_opbase;
+        O.scratch = c->d_scan_scratch; O.tot_nn = c->d_otot; O.tot_ch = c->d_otot + 1; O.vpages = c->d_vpages;
+        O.doffs = c->d_doffs; O.redo = redo;
+        pqk::launch_opt_pages(s, O);
+        pqk::PlainLaunch P{};
+        P.bytes = c->d_bytes; P.pages = c->d_vpages; P.wins = c->d_pwins;
+        P.nwins = static_cast<int32_t>(c->hpwins.size()); P.rowinfo = c->d_rowinfo; P.wchars = c->d_wchars;
+        P.bsum = c->d_pbsum; P.grid = c->plain_grid; P.nrows_total = -1; P.total = c->d_total;
+        P.capacity = out->capacity_bytes; P.overflow = c->d_flags + 1; P.validity = nullptr;
+        P.offsets = c->d_doffs; P.chars = out->d_values; P.page_err = c->d_operr; P.err_any = redo;
+        P.redo = redo; P.gate = c->d_flags + 2;
+        P.wmode = pqk::kWinOpt; P.pbase = c->d_opbase; P.pdense = c->d_opdense; P.ppos = c->d_page_pos;
+        if (c->plain_spec) {
+            pqk::SpecLaunch S{};
+            S.bytes = c->d_bytes; S.pages = c->d_pages; S.npages = c->npages; S.chunk_base = c->d_chunk_base;
+            S.chunks = c->d_chunks; S.nchunks = static_cast<int32_t>(c->hchunks.size()); S.cand = c->d_cand;
+            S.ppages = c->d_ppages; S.page_err = c->d_operr; S.err_any = redo; S.fallback = c->d_flags + 2;
+            S.ppos = c->d_page_pos; S.vpages = c->d_vpages;
+            pqk::launch_plain_spec(s, S);
+            P.pages = c->d_ppages;
+            P.wmode = pqk::kWinOptPseudo; P.wpage = c->d_pwpage; P.rpages = c->d_pages;
+        }
+        pqk::launch_plain_ba(s, P);
+        pqk::launch_opt_offsets(s, c->d_pages, c->d_tiles, c->ntiles, c->d_tile_rank, c->d_opdense, out->d_validity,
+                                c->d_doffs, out->d_offsets, redo);
+        (void)hipMemcpyAsync(c->d_total, c->d_otot + 1, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+        (void)hipMemcpyAsync(out->d_offsets + c->nrows, c->d_otot + 1, sizeof(int64_t), hipMemcpyDeviceToDevice, s);
+    } else if (plain_go) {
         pqk::PlainLaunch P{};
         P.bytes = c->d_bytes; P.pages = c->d_pages; P.wins = c->d_pwins;
         P.nwins = static_cast<int32_t>(c->hpwins.size()); P.rowinfo = c->d_rowinfo; P.wchars = c->d_wchars;
@@ -1573,7 +1659,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             if (c->d_pwbase && ctx->opt_plain_fused && !c->pfused_failed) {
                 P.wbase = c->d_pwbase;
                 P.redo = c->d_flags + 3;
-                P.wpseudo = 1;
+                P.wmode = pqk::kWinPseudo;
             }
         } else if (c->d_pwbase && ctx->opt_plain_fused && !c->pfused_failed) {
             P.wbase = c->d_pwbase;
@@ -1670,7 +1756,37 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             return rc;
     if (int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync")) return rc;
     flags[0] |= dflag;
-    if (flags[3] && c->plain && !c->pfused_failed && !(flags[2] && c->plain_spec)) {
+    if ((flags[2] || flags[3]) && c->plain && c->plain_opt && !c->popt_failed) {
+        if (std::getenv("PQ_DEBUG_SPEC")) {
+            std::fprintf(stderr, "plain opt redo: fallback %d flag %d\n", flags[2], flags[3]);
+            std::vector<DevErr> e(static_cast<size_t>(c->npages));
+            std::vector<int32_t> pp(e.size()), pn(e.size());
+            (void)hipMemcpy(e.data(), c->d_operr, e.size() * sizeof(DevErr), hipMemcpyDeviceToHost);
+            (void)hipMemcpy(pp.data(), c->d_page_pos, pp.size() * 4, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(pn.data(), c->d_page_nn, pn.size() * 4, hipMemcpyDeviceToHost);
+            for (size_t i = 0; i < e.size() && i < 8; i++)
+                std::fprintf(stderr, "  page %zu: err %d pos %d need %d size %d; values at %d, %d non-null\n", i, e[i].code,
+                             e[i].pos, e[i].need, e[i].size, pp[i], pn[i]);
+            if (c->plain_spec) {
+                std::vector<uint4> cd(std::min<size_t>(c->hchunks.size(), 8) * pqk::kPCand);
+                (void)hipMemcpy(cd.data(), c->d_cand, cd.size() * sizeof(uint4), hipMemcpyDeviceToHost);
+                for (size_t i = 0; i < cd.size(); i++)
+                    if (cd[i].x != 0xFFFFFFFFu)
+                        std::fprintf(stderr, "  cand chunk %zu slot %zu: entry %u err %u exit %u cnt %u w %u\n", i / pqk::kPCand,
+                                     i % pqk::kPCand, cd[i].x & 0x7FFFFFFFu, cd[i].x >> 31, cd[i].y, cd[i].z, cd[i].w);
+            }
+        }
+        // the OPTIONAL chunk did not fit the PLAIN kernels' form (an error,
+        // or value sections their strings do not fill): the general path
+        // decodes it from now on and reports any error
+        c->popt_failed = true;
+        if (c->npages) (void)hipMemsetAsync(c->d_page_err, 0, c->npages * sizeof(DevErr), ctx->stream);
+        if (!out) out = c->last_out;
+        if (!out) return set_err(ctx, PQ_ERR_ARG, "decode check without an output column");
+        if (int rc = pq_decode_async(ctx, c, out)) return rc;
+        return collect(ctx, c, out);
+    }
+    if (flags[3] && c->plain && !c->plain_opt && !c->pfused_failed && !(flags[2] && c->plain_spec)) {
         // a page's strings did not fill it exactly (or its chain failed): the
         // one-pass PLAIN kernel's character placement does not hold; the two
         // passes decode the chunk from now on (and report any error)

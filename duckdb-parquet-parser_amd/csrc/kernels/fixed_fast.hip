@@ -100,8 +100,9 @@ __global__ void __launch_bounds__(256) k_fixed_req(const uint8_t* __restrict__ b
 __device__ void levels_serial(const uint8_t* __restrict__ bytes, const DevPage* __restrict__ pages, int p,
                               const int32_t* __restrict__ page_tile0, ColumnParams cp,
                               uint32_t* __restrict__ validity, int32_t* __restrict__ tile_rank,
-                              int32_t* __restrict__ page_pos, DevErr* __restrict__ page_err,
-                              int32_t* __restrict__ err_any, LitRun* lits, uint32_t* bits) {
+                              int32_t* __restrict__ page_pos, int32_t* __restrict__ page_nn,
+                              DevErr* __restrict__ page_err, int32_t* __restrict__ err_any, LitRun* lits,
+                              uint32_t* bits) {
     const DevPage pg = pages[p];
     const uint8_t* page = bytes + pg.off;
     const uint32_t size = static_cast<uint32_t>(pg.size);
@@ -174,6 +175,7 @@ __device__ void levels_serial(const uint8_t* __restrict__ bytes, const DevPage* 
         set_err(err, err_any, PQ_ERR_BUFFER, pos + k * w, w, size);
     }
     if (lane() == 0) page_pos[p] = static_cast<int32_t>(pos);
+    if (lane() == 0 && page_nn) page_nn[p] = static_cast<int32_t>(nn);
 }
 
 // One workgroup (8 waves) per page: the page's level bytes staged in LDS,
@@ -184,7 +186,7 @@ __device__ void levels_serial(const uint8_t* __restrict__ bytes, const DevPage* 
 // runs, ...) take levels_serial on wave 0.
 constexpr int kLvWaves = 8;
 constexpr uint32_t kLvStage = 16384;
-constexpr uint32_t kLvRec = 1024;
+constexpr uint32_t kLvRec = 4096;
 constexpr uint32_t kLvTiles = 128;
 constexpr uint32_t kLvSpecMax = 4096;  // level sections up to this size: run_spec.hpp (workgroup) instead of one lane
 constexpr uint32_t kLvSpecList = kLvSpecMax / 2 / kSpJump + 8;
@@ -195,6 +197,7 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
                                                                 ColumnParams cp, uint32_t* __restrict__ validity,
                                                                 int32_t* __restrict__ tile_rank,
                                                                 int32_t* __restrict__ page_pos,
+                                                                int32_t* __restrict__ page_nn,
                                                                 DevErr* __restrict__ page_err,
                                                                 int32_t* __restrict__ err_any) {
     __shared__ __attribute__((aligned(16))) uint32_t stage[kLvStage / 4 + 8];
@@ -270,8 +273,8 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
     __syncthreads();
     if (sh[0] == 1) {
         if (wv == 0)
-            levels_serial(bytes, pages, p, page_tile0, cp, validity, tile_rank, page_pos, page_err, err_any, lits,
-                          reinterpret_cast<uint32_t*>(mark_all[1]));
+            levels_serial(bytes, pages, p, page_tile0, cp, validity, tile_rank, page_pos, page_nn, page_err, err_any,
+                          lits, reinterpret_cast<uint32_t*>(mark_all[1]));
         return;
     }
     const uint32_t nrec = sh[1];
@@ -362,6 +365,7 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
             set_err(page_err + p, err_any, PQ_ERR_BUFFER, pos + k * w, w, size);
         }
         if (lane() == 0) page_pos[p] = static_cast<int32_t>(pos);
+        if (lane() == 0 && page_nn) page_nn[p] = static_cast<int32_t>(carry);
     }
 }
 
@@ -420,9 +424,17 @@ void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* page
         return;
     }
     hipLaunchKernelGGL(k_fixed_levels2, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0, cp,
-                       validity, tile_rank, page_pos, page_err, err_any);
+                       validity, tile_rank, page_pos, static_cast<int32_t*>(nullptr), page_err, err_any);
     hipLaunchKernelGGL(k_fixed_scatter, dim3(tb), dim3(kTilesPerBlock * kWave), 0, s, bytes, pages, tiles, ntiles, pw,
                        validity, tile_rank, page_pos, page_err, values);
+}
+
+void launch_fixed_levels(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
+                         const int32_t* page_tile0, ColumnParams cp, uint32_t* validity, int32_t* tile_rank,
+                         int32_t* page_pos, int32_t* page_nn, DevErr* page_err, int32_t* err_any) {
+    if (npages <= 0) return;
+    hipLaunchKernelGGL(k_fixed_levels2, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0, cp,
+                       validity, tile_rank, page_pos, page_nn, page_err, err_any);
 }
 
 }  // namespace pqk

@@ -180,6 +180,11 @@ void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_page
 void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags);
 
 // ── tile-parallel PLAIN fixed-width path (fixed_fast.hip) ──────────────────
+// OPTIONAL columns' def levels alone (k_fixed_levels2): validity, per-tile
+// ranks, value section start and non-null count of every page
+void launch_fixed_levels(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
+                         const int32_t* page_tile0, ColumnParams cp, uint32_t* validity, int32_t* tile_rank,
+                         int32_t* page_pos, int32_t* page_nn, DevErr* page_err, int32_t* err_any);
 void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,
                         int ntiles, const int32_t* page_tile0, ColumnParams cp, uint32_t* validity,
                         uint8_t* values, int32_t* tile_rank, int32_t* page_pos, DevErr* page_err,
@@ -259,8 +264,17 @@ struct PlainLaunch {
                                  // its image offset plus 4 x its first row; the kernel adds its first string's)
     int32_t* redo;               // with wbase: set by the one-pass kernel when a page does not fit its
                                  // form (the host then decodes the chunk with the two passes)
-    int32_t wpseudo;             // with wbase: the pages are k_plain_link's pseudo pages
+    int32_t wmode;               // one-pass: kWinBase, kWinPseudo, kWinOpt, kWinOptPseudo
+    // OPTIONAL chunks (kWinOpt*): the pages are value sections of the real
+    // pages (k_opt_pages), rows are non-null rows; the one-pass kernel writes
+    // their offsets to a dense array that k_opt_offsets spreads over the rows
+    const int64_t* pbase;        // characters before each real page
+    const int64_t* pdense;       // non-null rows before each real page
+    const int32_t* ppos;         // value section start of each real page
+    const int32_t* wpage;        // kWinOptPseudo: the real page of each window
+    const DevPage* rpages;       // kWinOptPseudo: the real pages
 };
+enum : int32_t { kWinBase = 0, kWinPseudo = 1, kWinOpt = 2, kWinOptPseudo = 3 };
 int plain_write_blocks_per_cu();
 
 // PLAIN BYTE_ARRAY pages larger than a window (plain_ba.hip k_plain_spec /
@@ -287,8 +301,47 @@ struct SpecLaunch {
     DevErr* page_err;            // per real page
     int32_t* err_any;
     int32_t* fallback;
+    // OPTIONAL chunks: the chain of real page p starts at ppos[p] (after its
+    // levels) and reads vpages[p].nvals values, rows from vpages[p].first_row
+    const int32_t* ppos;
+    const DevPage* vpages;
 };
 void launch_plain_spec(hipStream_t s, const SpecLaunch& S);
+
+// OPTIONAL PLAIN BYTE_ARRAY chunks on the PLAIN kernels (plain_ba.hip): after
+// k_fixed_levels2 (validity, tile ranks, value section starts, non-null
+// counts), the per-page value sections become REQUIRED-shaped pages of their
+// non-null values; anything unusual (a level error, a section too short for
+// its values) sets *redo and the host decodes the chunk on the general path.
+struct OptLaunch {
+    const DevPage* pages;        // the real pages
+    int32_t npages;
+    const int32_t* page_nn;      // non-null values per page (k_fixed_levels2)
+    const int32_t* page_pos;     // value section start per page
+    const DevErr* lerr;          // level errors per page
+    int64_t* nnv;                // per page: non-null values, then (scan) values before it
+    int64_t* chv;                // per page: characters, then (scan) characters before it
+    int64_t* pdense;             // exclusive scans of nnv / chv
+    int64_t* pbase;
+    int64_t* scratch;            // scan scratch (npages / 8192 + 16)
+    int64_t* tot_nn;             // scan totals
+    int64_t* tot_ch;
+    DevPage* vpages;             // out: value-section pages
+    int64_t* doffs;              // dense offsets (their entry at the non-null total gets the character total)
+    int32_t* redo;
+};
+void launch_opt_pages(hipStream_t s, const OptLaunch& O);
+// def levels of pages of up to kOptLaneRows rows, one lane per page (the
+// same outputs as launch_fixed_levels for the PLAIN kernels' OPTIONAL form)
+constexpr int32_t kOptLaneRows = 2048;
+void launch_opt_levels(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
+                       const int32_t* page_tile0, int32_t max_def, uint32_t* validity, int32_t* tile_rank,
+                       int32_t* page_pos, int32_t* page_nn, DevErr* lerr, int32_t* redo);
+// offsets of every row from the dense offsets: row R takes entry rank(R)
+// (non-null rows before it), NULL rows included; offsets[nrows] = total
+void launch_opt_offsets(hipStream_t s, const DevPage* pages, const DevTile* tiles, int ntiles,
+                        const int32_t* tile_rank, const int64_t* pdense, const uint32_t* validity,
+                        const int64_t* doffs, int64_t* offsets, const int32_t* redo);
 // REQUIRED PLAIN BYTE_ARRAY pages larger than min_size bytes: row codes and
 // tile characters for the generic gather (k_ba_rows skips these pages)
 void launch_plain_big_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, uint32_t min_size,

@@ -22,6 +22,7 @@
 #include "kernels/device_common.hpp"
 #include "kernels/row_copy.hpp"
 #include "kernels/kernels.hpp"
+#include "kernels/lane_walk.hpp"
 #include "pq_gpu.h"
 
 namespace pqk {
@@ -153,8 +154,9 @@ __global__ void __launch_bounds__(kPWWaves * 64) k_plain_write(PlainLaunch a) {
             const uint32_t nb = (W.img_bytes + 15) / 16 + 1;
             copy_blocks(dst, src, nb, lane(), kWave);
         }
-        // validity: every row of a REQUIRED column is set
-        {
+        // validity: every row of a REQUIRED column is set (OPTIONAL: the
+        // levels pass wrote it)
+        if (a.validity) {
             const int64_t gfirst = R0 >> 5, glast = rows ? (R0 + rows - 1) >> 5 : gfirst - 1;
             for (int64_t g = gfirst + lane(); g <= glast; g += kWave) {
                 const int64_t lo = max(g * 32, R0), hi = min(g * 32 + 32, R0 + static_cast<int64_t>(rows));
@@ -223,6 +225,7 @@ struct PFLds {
 __global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (a.gate && *a.gate) return;  // pseudo pages: the spec pass fell back
+    if (a.wmode >= kWinOpt && *a.redo) return;  // OPTIONAL: the levels or the chains failed
     const int wv = static_cast<int>(threadIdx.x / kWave);
     PFLds& S = reinterpret_cast<PFLds*>(smem)[wv];
     const int nw = static_cast<int>(gridDim.x) * kPFWaves;
@@ -242,7 +245,7 @@ __global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
     fetch(W);
     for (;;) {
         const DevBatch Wc = W;
-        int64_t G0 = a.wbase[w];
+        int64_t G0 = (a.wmode == kWinBase || a.wmode == kWinPseudo) ? a.wbase[w] : 0;
 #pragma unroll
         for (uint32_t k = 0; k < kPFLoads; k++) {
             const uint32_t b = lane() + k * kWave;
@@ -280,7 +283,7 @@ __global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (__ballot(misfit)) {  // the two passes redo the chunk; this window's row list is not whole
-            if (lane() == 0) atomicOr(a.redo, 1);
+            if (lane() == 0) atomicOr(a.redo, 8);
             if (wn >= a.nwins) break;
             w = wn;
             continue;
@@ -288,13 +291,12 @@ __global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
         const int64_t R0 = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pg.first_row))) |
                            (static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pg.first_row >> 32))) << 32);
         int64_t G1;
-        if (a.wpseudo) {
-            // pseudo pages cut one real page whose strings fill it: the
-            // characters before the window's first string are its offset in
-            // the page minus 4 per earlier row; the window's own characters
-            // are its pages' bytes minus 4 per row
+        if (a.wmode == kWinBase) {
+            G1 = a.wbase[w + 1];
+        } else {
+            // the window's own characters are its pages' bytes minus 4 per row
             const uint64_t sm = __ballot(act && n > 0);
-            if (!sm) {
+            if (!sm) {  // no rows
                 if (wn >= a.nwins) break;
                 w = wn;
                 continue;
@@ -302,16 +304,26 @@ __global__ void __launch_bounds__(kPFWaves * 64) k_plain_fused(PlainLaunch a) {
             const int fl = static_cast<int>(__builtin_ctzll(sm));
             const int64_t off = static_cast<int64_t>(__shfl(static_cast<long long>(pg.off), fl));
             const int64_t fr = static_cast<int64_t>(__shfl(static_cast<long long>(pg.first_row), fl));
-            G0 += off - 4 * fr;
+            if (a.wmode == kWinPseudo) {
+                // pseudo pages cut one real page whose strings fill it: the
+                // characters before the window's first string are its offset
+                // in the page minus 4 per earlier row
+                G0 += off - 4 * fr;
+            } else if (a.wmode == kWinOpt) {
+                G0 = a.pbase[Wc.p0];  // value-section pages, one per real page
+            } else {                  // pseudo pages of value sections
+                const int rp = a.wpage[w];
+                const int64_t v0 = static_cast<int64_t>(a.rpages[rp].off) + a.ppos[rp];
+                G0 = a.pbase[rp] + (off - v0) - 4 * (fr - a.pdense[rp]);
+            }
             const int64_t wch = act ? static_cast<int64_t>(max(pg.size, 0)) - 4 * static_cast<int64_t>(n) : 0;
             uint32_t lo = static_cast<uint32_t>(wch);
             lo = wave_incl_scan(lo);
             G1 = G0 + static_cast<int64_t>(bcast_last(lo));
-        } else {
-            G1 = a.wbase[w + 1];
         }
-        // validity: every row of a REQUIRED column is set
-        {
+        // validity: every row of a REQUIRED column is set (OPTIONAL: the
+        // levels pass wrote it)
+        if (a.validity) {
             const int64_t gfirst = R0 >> 5, glast = rows ? (R0 + rows - 1) >> 5 : gfirst - 1;
             for (int64_t g = gfirst + lane(); g <= glast; g += kWave) {
                 const int64_t lo = max(g * 32, R0), hi = min(g * 32 + 32, R0 + static_cast<int64_t>(rows));
@@ -511,7 +523,8 @@ __global__ void __launch_bounds__(kSpecWaves * 64) k_plain_spec(SpecLaunch a) {
     if (cw >= a.nchunks) return;
     uint32_t* stage = stage_all[wv];
     // lane j < 16: chunk cw + j's page offset, size, chunk start
-    uint32_t d_lo = 0, d_hi = 0, d_size = 0, d_cs = 0, d_first = 0, d_slot = 0;
+    // d_start: where the page's chain starts (0, or after an OPTIONAL page's levels)
+    uint32_t d_lo = 0, d_hi = 0, d_size = 0, d_cs = 0, d_start = 0, d_slot = 0;
     if (static_cast<int>(lane()) < kSpecChunks && cw + static_cast<int>(lane()) < a.nchunks) {
         const uint2 ch = a.chunks[cw + lane()];
         const DevPage pg = a.pages[ch.x];
@@ -519,7 +532,7 @@ __global__ void __launch_bounds__(kSpecWaves * 64) k_plain_spec(SpecLaunch a) {
         d_hi = static_cast<uint32_t>(pg.off >> 32);
         d_size = static_cast<uint32_t>(max(pg.size, 0));
         d_cs = ch.y * kPChunk;
-        d_first = ch.y == 0 ? 1u : 0u;
+        d_start = a.ppos ? static_cast<uint32_t>(max(a.ppos[ch.x], 0)) : 0u;
         d_slot = (d_size + 15) / 16 * 16 + 16;  // the page's slot in the image
     }
     // stage: block t of the wave's kSpecChunks x kSpecBlocks (chunk t / kSpecBlocks)
@@ -555,16 +568,20 @@ __global__ void __launch_bounds__(kSpecWaves * 64) k_plain_spec(SpecLaunch a) {
     for (int j = 0; j < kSpecChunks; j++) {
         const uint32_t size = __builtin_amdgcn_readlane(d_size, j);
         const uint32_t cs = __builtin_amdgcn_readlane(d_cs, j);
-        const uint32_t first = __builtin_amdgcn_readlane(d_first, j);
+        const uint32_t start = __builtin_amdgcn_readlane(d_start, j);
         const uint32_t q = cs + lane(), ce = min(cs + kPChunk, size);
         const uint32_t len = q + 4 <= size ? st_u32(stage, static_cast<uint32_t>(j) * kSpecBlocks * 16 + lane()) : 0xFFFFFFFFu;
         bool plaus = q < ce && q + 4 <= size && static_cast<uint64_t>(q) + 4 + len <= size;
-        if (first) plaus = lane() == 0;  // the page's first string starts at 0
+        if (start >= cs && start < cs + kPChunk) plaus = lane() == 0;  // the page's first string: one candidate, at start
+        if (cs + kPChunk <= start) plaus = false;                      // levels, before the values
         const uint64_t m = __ballot(cw + j < a.nchunks && plaus);
         if (j == jm) mk = m;
     }
+    // (shuffles with every lane active: a ds_bpermute under divergence reads
+    // zeros from lanes outside exec)
     const uint32_t size = static_cast<uint32_t>(__shfl(static_cast<int>(d_size), jm));
     const uint32_t cs = static_cast<uint32_t>(__shfl(static_cast<int>(d_cs), jm));
+    const uint32_t st0 = static_cast<uint32_t>(__shfl(static_cast<int>(d_start), jm));
     const int c = cw + jm;
     if (c >= a.nchunks) return;
     for (int i = 0; i < sl; i++) mk &= mk - 1;  // this lane's candidate: the sl-th set bit
@@ -572,7 +589,7 @@ __global__ void __launch_bounds__(kSpecWaves * 64) k_plain_spec(SpecLaunch a) {
     if (mk) {
         const uint32_t ce = min(cs + kPChunk, size);
         const uint32_t sb = static_cast<uint32_t>(jm) * kSpecBlocks * 16 - cs;  // stage byte of page offset 0 (mod 2^32)
-        const uint32_t q0 = cs + static_cast<uint32_t>(__builtin_ctzll(mk));
+        const uint32_t q0 = (st0 >= cs && st0 < cs + kPChunk) ? st0 : cs + static_cast<uint32_t>(__builtin_ctzll(mk));
         uint32_t q = q0, cnt = 0, err = 0, need = 0;
         while (q < ce) {
             if (q + 4 > size) { err = 1; need = 4; break; }
@@ -612,10 +629,18 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
     if (p >= a.npages) return;
     const DevPage pg = a.pages[p];
     const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
-    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    // OPTIONAL pages: the values' count and first row come from the value
+    // section page, the chain starts after the levels
+    const uint32_t n = static_cast<uint32_t>(max(a.vpages ? a.vpages[p].nvals : pg.nvals, 0));
+    const int64_t frow = a.vpages ? a.vpages[p].first_row : pg.first_row;
+    const uint32_t pos0 = a.ppos ? static_cast<uint32_t>(max(a.ppos[p], 0)) : 0u;
     const int32_t c0 = a.chunk_base[p], c1 = a.chunk_base[p + 1];
     const uint32_t slot_end = (size + 15) / 16 * 16 + 16;
-    uint32_t q = 0, dead = 0;                // serial chain state (lane 0's values are used)
+    // the chunk holding pos0 keeps its one candidate (entry pos0) in table slot 0
+    auto tslot = [&](uint32_t entry, uint32_t chunk_start) {
+        return (entry == pos0 && pos0 >= chunk_start && pos0 < chunk_start + kPChunk) ? 0u : entry - chunk_start;
+    };
+    uint32_t q = pos0, dead = 0;             // serial chain state (lane 0's values are used)
     uint32_t rows = 0, done = 0, fb = 0;     // wave-uniform: rows before the round, count reached / error, fallback
     for (int32_t cb = c0; cb < c1; cb += kLinkStage) {
         const int32_t cend = min(c1, cb + static_cast<int32_t>(kLinkStage));
@@ -662,7 +687,7 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (uint32_t s = 0; s < kPCand; s++)
-            if (act && r[s].x != kLNone) tab[i * 64 + ((r[s].x & 0x7FFFFFFFu) - chs)] = r[s].y | (r[s].x & 0x80000000u);
+            if (act && r[s].x != kLNone) tab[i * 64 + tslot(r[s].x & 0x7FFFFFFFu, chs)] = r[s].y | (r[s].x & 0x80000000u);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane() == 0) {  // the chain: one LDS read per chunk
@@ -675,11 +700,11 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
                     dead = 1;
                 } else if (q >= js + kPChunk) {
                     pk = kPickSkip;  // a string spans this chunk
-                } else if (q - js >= 64) {
+                } else if (tslot(q, js) >= 64) {
                     pk = kPickFail;
                     dead = 1;
                 } else {
-                    const uint32_t t = tab[j * 64 + (q - js)];
+                    const uint32_t t = tab[j * 64 + tslot(q, js)];
                     if (t == kLNone) {
                         pk = kPickFail;
                         dead = 1;
@@ -745,7 +770,7 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
             const uint32_t rest = size > chs + ent ? size - chs - ent : 0u;
             pp.size = static_cast<int32_t>(take == 0 ? 0u : (take == cnt && rr.y >= chs + ent ? min(rr.y - chs - ent, rest) : rest));
             pp.nvals = static_cast<int32_t>(take);
-            pp.first_row = pg.first_row + min(before, n);
+            pp.first_row = frow + min(before, n);
             a.ppages[c] = pp;
         }
         rows += bcast_last(incl);
@@ -764,6 +789,160 @@ __global__ void __launch_bounds__(64) k_plain_link(SpecLaunch a) {
             atomicOr(a.err_any, 1);
         }
         if (fb) atomicOr(a.fallback, static_cast<int32_t>(fb));
+    }
+}
+
+
+// ── OPTIONAL chunks on the PLAIN kernels ──────────────────────────────────
+// k_fixed_levels2 has decoded the def levels (validity, per-tile ranks, where
+// each page's values start, non-null counts).  The value section of page p
+// holds nn_p strings (column_reader.cpp:213-222 reads one per non-null row):
+// it becomes a REQUIRED-shaped page of nn_p rows whose first row is the
+// number of non-null rows before it, and whose characters start after the
+// characters of the earlier pages (its bytes minus 4 per value, when its
+// strings fill it; the one-pass kernel checks that).  A level error or a
+// section too short for its values sets *redo: the host then decodes the
+// chunk on the general path, which reports the reference's error.
+__global__ void __launch_bounds__(256) k_opt_prep(OptLaunch o) {
+    const int p = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p >= o.npages) return;
+    const DevPage pg = o.pages[p];
+    const bool bad = o.lerr[p].code != 0;
+    const int64_t pos = bad ? 0 : o.page_pos[p];
+    int64_t nn = bad ? 0 : o.page_nn[p];
+    int64_t ch = static_cast<int64_t>(max(pg.size, 0)) - pos - 4 * nn;
+    if (bad || nn < 0 || pos > pg.size || ch < 0) {
+        atomicOr(o.redo, bad ? 2 : 4);
+        nn = 0;
+        ch = 0;
+    }
+    o.nnv[p] = nn;
+    o.chv[p] = ch;
+}
+
+__global__ void __launch_bounds__(256) k_opt_vpages(OptLaunch o) {
+    const int p = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p >= o.npages) return;
+    const DevPage pg = o.pages[p];
+    const int32_t pos = o.lerr[p].code ? 0 : max(o.page_pos[p], 0);
+    DevPage v{};
+    v.off = pg.off + static_cast<uint32_t>(pos);
+    v.size = max(pg.size - pos, 0);
+    v.nvals = static_cast<int32_t>(o.nnv[p]);
+    v.first_row = o.pdense[p];
+    v.mode = MODE_PLAIN;
+    v.dict = -1;
+    o.vpages[p] = v;
+    if (p == o.npages - 1) o.doffs[o.pdense[p] + o.nnv[p]] = o.pbase[p] + o.chv[p];
+}
+
+// Def levels of small OPTIONAL pages, one lane per page (k_fixed_levels2's
+// workgroup per page is for pages of thousands of rows): the lane walks the
+// level stream with the reference's RleDecoder states (lane_walk.hpp) and ORs
+// the validity bits, the per-tile ranks, the value section start and the
+// non-null count (PLAIN: level >= max_def, column_reader.cpp:166-170).  A
+// malformed section or stream sets *redo (the general path reports it).
+__global__ void __launch_bounds__(256) k_opt_levels(const uint8_t* __restrict__ bytes, const DevPage* __restrict__ pages,
+                                                    int npages, const int32_t* __restrict__ page_tile0, int32_t max_def,
+                                                    uint32_t* __restrict__ validity, int32_t* __restrict__ tile_rank,
+                                                    int32_t* __restrict__ page_pos, int32_t* __restrict__ page_nn,
+                                                    DevErr* __restrict__ lerr, int32_t* __restrict__ redo) {
+    const int p = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+    if (p >= npages) return;
+    const DevPage pg = pages[p];
+    const uint8_t* page = bytes + pg.off;
+    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    const uint32_t md = static_cast<uint32_t>(max_def);
+    auto fail = [&]() {
+        lerr[p].code = PQ_ERR_UNSUPPORTED;
+        atomicOr(redo, 1);
+    };
+    if (size < 4) return fail();
+    const uint32_t dl = static_cast<uint32_t>(gld8(page, 0));
+    if (static_cast<uint64_t>(dl) + 4 > size) return fail();
+    const int32_t t0 = page_tile0[p];
+    const int64_t R0 = pg.first_row;
+    const uint32_t bw = level_bw(max_def);
+    LRle r = lrle(4, dl, bw);
+    auto rd8 = [&](uint32_t a) { return gld8(page, a); };
+    uint32_t cur = 0, nn = 0;
+    // validity bits of rows [a, a + k) of the page
+    auto set_bits = [&](uint32_t a, uint32_t k) {
+        int64_t lo = R0 + a;
+        const int64_t hi = lo + k;
+        while (lo < hi) {
+            const int64_t w = lo >> 5;
+            const uint32_t b0 = static_cast<uint32_t>(lo & 31);
+            const uint32_t cnt = static_cast<uint32_t>(min(static_cast<int64_t>(32 - b0), hi - lo));
+            atomicOr(&validity[w], (cnt == 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u)) << b0);
+            lo += cnt;
+        }
+    };
+    if (n) tile_rank[t0] = 0;
+    const int rc = lane_rle(r, rd8, n, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+        if (kind == 0) {
+            const bool v = arg >= md;
+            // tile boundaries in [cur, cur + k) (the first tile's rank is 0)
+            for (uint32_t b = max((cur + kTileRows - 1) / kTileRows, 1u) * kTileRows; b < cur + k && b < n; b += kTileRows)
+                tile_rank[t0 + static_cast<int32_t>(b / kTileRows)] = static_cast<int32_t>(nn + (v ? b - cur : 0u));
+            if (v) {
+                set_bits(cur, k);
+                nn += k;
+            }
+            cur += k;
+        } else {
+            uint32_t word = 0, wi = 0;
+            bool have = false;
+            for (uint32_t i = 0; i < k; i++, cur++) {
+                if (cur % kTileRows == 0 && cur) tile_rank[t0 + static_cast<int32_t>(cur / kTileRows)] = static_cast<int32_t>(nn);
+                const uint32_t lvl = gbits(page, size, static_cast<uint64_t>(arg) + static_cast<uint64_t>(i) * bw, bw);
+                if (lvl >= md) {
+                    const int64_t row = R0 + cur;
+                    const uint32_t w = static_cast<uint32_t>(row >> 5);
+                    if (have && w != wi) {
+                        atomicOr(&validity[wi], word);
+                        word = 0;
+                    }
+                    wi = w;
+                    have = true;
+                    word |= 1u << (row & 31);
+                    nn++;
+                }
+            }
+            if (have && word) atomicOr(&validity[wi], word);
+        }
+    });
+    if (rc) return fail();
+    page_pos[p] = static_cast<int32_t>(4 + dl);
+    page_nn[p] = static_cast<int32_t>(nn);
+}
+
+// One wave per 512-row tile: row R's offset is the dense offset of its rank
+// (the non-null rows before it), so a NULL row repeats the next value's start.
+constexpr int kOptTiles = 4;
+__global__ void __launch_bounds__(kOptTiles * 64) k_opt_offsets(const DevPage* __restrict__ pages,
+                                                                const DevTile* __restrict__ tiles, int ntiles,
+                                                                const int32_t* __restrict__ tile_rank,
+                                                                const int64_t* __restrict__ pdense,
+                                                                const uint32_t* __restrict__ validity,
+                                                                const int64_t* __restrict__ doffs,
+                                                                int64_t* __restrict__ offsets,
+                                                                const int32_t* __restrict__ redo) {
+    if (redo[0] || redo[-1]) return;  // d_flags[3] / [2]: the chunk is decoded again on the general path
+    const int t = static_cast<int>(blockIdx.x) * kOptTiles + static_cast<int>(threadIdx.x / kWave);
+    if (t >= ntiles) return;
+    const DevTile T = tiles[t];
+    const int64_t R0 = pages[T.page].first_row + T.row0;
+    int64_t rank = pdense[T.page] + tile_rank[t];
+    const uint32_t m = static_cast<uint32_t>(T.nrows);
+    for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
+        const uint32_t j = j0 + lane();
+        const int64_t R = R0 + j;
+        const bool v = j < m && ((validity[R >> 5] >> (R & 31)) & 1u);
+        const uint64_t vm = __ballot(v);
+        if (j < m) offsets[R] = doffs[rank + popc_below(vm)];
+        rank += __popcll(vm);
     }
 }
 
@@ -799,7 +978,7 @@ void launch_plain_big_rows(hipStream_t s, const uint8_t* bytes, const DevPage* p
 
 void launch_plain_ba(hipStream_t s, PlainLaunch P) {
     if (P.nwins <= 0) return;
-    if (P.wbase) {  // one pass (the host re-runs the two passes if it sets *redo)
+    if (P.wbase || P.wmode >= kWinOpt) {  // one pass (the host re-runs the two passes if it sets *redo)
         static int fgrid = 0;
         const uint32_t lds = kPFWaves * static_cast<uint32_t>(sizeof(PFLds));
         if (!fgrid) {
@@ -841,6 +1020,31 @@ void launch_plain_spec(hipStream_t s, const SpecLaunch& S) {
     const int per_block = kSpecWaves * kSpecChunks;  // chunks per workgroup
     hipLaunchKernelGGL(k_plain_spec, dim3((S.nchunks + per_block - 1) / per_block), dim3(kSpecWaves * kWave), 0, s, S);
     hipLaunchKernelGGL(k_plain_link, dim3(S.npages), dim3(kWave), 0, s, S);
+}
+
+void launch_opt_pages(hipStream_t s, const OptLaunch& O) {
+    if (O.npages <= 0) return;
+    const int b = (O.npages + 255) / 256;
+    hipLaunchKernelGGL(k_opt_prep, dim3(b), dim3(256), 0, s, O);
+    launch_scan_i64(s, O.nnv, O.pdense, O.npages, O.tot_nn, O.scratch);
+    launch_scan_i64(s, O.chv, O.pbase, O.npages, O.tot_ch, O.scratch);
+    hipLaunchKernelGGL(k_opt_vpages, dim3(b), dim3(256), 0, s, O);
+}
+
+void launch_opt_levels(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
+                       const int32_t* page_tile0, int32_t max_def, uint32_t* validity, int32_t* tile_rank,
+                       int32_t* page_pos, int32_t* page_nn, DevErr* lerr, int32_t* redo) {
+    if (npages <= 0) return;
+    hipLaunchKernelGGL(k_opt_levels, dim3((npages + 255) / 256), dim3(256), 0, s, bytes, pages, npages, page_tile0,
+                       max_def, validity, tile_rank, page_pos, page_nn, lerr, redo);
+}
+
+void launch_opt_offsets(hipStream_t s, const DevPage* pages, const DevTile* tiles, int ntiles,
+                        const int32_t* tile_rank, const int64_t* pdense, const uint32_t* validity,
+                        const int64_t* doffs, int64_t* offsets, const int32_t* redo) {
+    if (ntiles <= 0) return;
+    hipLaunchKernelGGL(k_opt_offsets, dim3((ntiles + kOptTiles - 1) / kOptTiles), dim3(kOptTiles * kWave), 0, s,
+                       pages, tiles, ntiles, tile_rank, pdense, validity, doffs, offsets, redo);
 }
 
 }  // namespace pqk

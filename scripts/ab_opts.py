@@ -23,7 +23,7 @@ DEFAULTS = {"pipe_run_pages": 32, "zflip": 1, "write_waves": 10, "dict_pipe": 1,
             "fused_ba": 1, "fixed_plain": 1, "big_all": 0, "fused_debug": 0, "plain_fused": 1, "regex_win": 8192,
             "raw_upload": 1}
 KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "plain_spec", "pipe_count", "pipe_codes",
-           "pipe_write", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba")
+           "pipe_write", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba", "plain_opt")
 
 cfg, _, colname = sys.argv[1].partition(":")
 rows = int(sys.argv[2])

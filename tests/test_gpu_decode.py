@@ -37,6 +37,16 @@ SMALL = [
                               dict_size=40, len_min=100, len_max=3000)], 4000),
     ("wide_dict", [gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, dict_size=70000, len_min=1, len_max=6,
                            max_run=2)], 400000),
+    # OPTIONAL PLAIN BYTE_ARRAY (levels, then value sections on the PLAIN
+    # kernels): 1 KiB pages (windows) and 3000-row arrow pages (chunk chains),
+    # sparse, all-NULL, strings over the chunk chains' 60-byte reach
+    ("opt_plain", [gen.Col("s", gen.COMMENT, gen.BYTE_ARRAY, optional=True, null_frac=0.2, len_min=0,
+                           len_max=40)], 6000),
+    ("opt_plain_sparse", [gen.Col("s", gen.COMMENT, gen.BYTE_ARRAY, optional=True, null_frac=0.9, len_min=5,
+                                  len_max=30)], 7000),
+    ("opt_plain_all_null", [gen.Col("s", gen.COMMENT, gen.BYTE_ARRAY, optional=True, null_frac=1.0)], 3000),
+    ("opt_plain_long", [gen.Col("s", gen.COMMENT, gen.BYTE_ARRAY, optional=True, null_frac=0.1, len_min=50,
+                                len_max=200)], 4000),
 ]
 
 
@@ -232,7 +242,36 @@ def _opt_fixed_file(ptype, fmt, nvals, seed, rle_levels=False, drop=0):
     pay = B.levels_section(stream) + vals
     return B.build_file([B.data_header(len(pay), nvals, 0) + pay], ptype, True, nvals)
 
+def _opt_plain_file(nvals, seed, null_frac=0.3, lmax=30, extra=b"", drop=0, all_bitpacked=False):
+    """One OPTIONAL PLAIN BYTE_ARRAY page: bit-packed and RLE def levels,
+    then the non-null strings; `extra` bytes after them, `drop` trailing
+    strings removed (the read overruns)."""
+    rng = np.random.default_rng(seed)
+    defs = [int(x) for x in rng.random(nvals) >= null_frac]
+    head = nvals // 8 * 8 if all_bitpacked else (nvals // 2) // 8 * 8
+    stream = B.bitpack(defs[:head], 1) + (B.rle(nvals - head, 1, 1) if nvals > head else b"")
+    defs = defs[:head] + [1] * (nvals - head)
+    nn = sum(defs) - drop
+    strs = [bytes(rng.integers(97, 123, int(rng.integers(0, lmax + 1))).astype(np.uint8)) for _ in range(nn)]
+    pay = B.levels_section(stream) + B.plain_ba(strs) + extra
+    return B.build_file([B.data_header(len(pay), nvals, 0) + pay], gen.BYTE_ARRAY, True, nvals)
+
+
 CRAFTED = {
+    # OPTIONAL PLAIN BYTE_ARRAY: a window page; a chunk-chain page whose values
+    # start inside chunk 0 past its candidate range, one whose levels fill
+    # several chunks; bytes after the last value (the one-pass form does not
+    # hold: the general path decodes it)
+    "opt_plain_page": lambda: _opt_plain_file(900, seed=61),
+    "opt_plain_spec": lambda: _opt_plain_file(6000, seed=62, lmax=40),
+    "opt_plain_spec_levels": lambda: _opt_plain_file(20000, seed=63, lmax=12, null_frac=0.5, all_bitpacked=True),
+    "opt_plain_extra": lambda: _opt_plain_file(700, seed=64, extra=b"trailing bytes"),
+    "opt_plain_spec_extra": lambda: _opt_plain_file(5000, seed=65, extra=b"\x03\x00\x00\x00abc"),
+    # RLE level runs that start exactly on 512-row tile edges
+    "opt_plain_tile_edges": lambda: B.build_file(
+        [B.data_header(len(pay), 1800, 0) + pay for pay in
+         [B.levels_section(B.rle(512, 1, 1) + B.rle(512, 0, 1) + B.rle(776, 1, 1)) +
+          B.plain_ba([b"v%d" % i for i in range(1288)])]], gen.BYTE_ARRAY, True, 1800),
     # bit width 0: every index is 0
     "bw0_rle": lambda: _dict_ba_file(bytes([0]) + B.rle(10, 0, 0), 10, DICT),
     # literal run then exhaustion -> zero fill
@@ -351,6 +390,9 @@ ERRORS = {
     "plain_spec_trunc_len": lambda: _spec_plain_file(seed=48, cut=2),
     # more values declared than the page holds: the read at the page end fails
     "plain_spec_short": lambda: _spec_plain_file(seed=49, nvals=3100),
+    # OPTIONAL PLAIN BYTE_ARRAY values run out (window page, chunk-chain page)
+    "opt_plain_short": lambda: _opt_plain_file(800, seed=66, drop=2),
+    "opt_plain_spec_short": lambda: _opt_plain_file(6000, seed=67, lmax=40, drop=5),
     # def_len beyond the page
     "def_len_overrun": lambda: B.build_file([B.data_header(6, 3, 0) + struct.pack("<I", 50) + b"xy"], gen.INT32, True, 3),
     # dictionary page index stream without the bit-width byte
