@@ -51,7 +51,7 @@ for _p in (ROOT, PKG):
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel timers (HIP events on the decode stream, capi.hip Timed)
 KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "pipe_count", "pipe_codes", "pipe_write",
-           "ba_fused", "ba_rows", "scan", "ba_gather", "plain_spec", "plain_ba", "fixed_plain", "fixed")
+           "ba_fused", "ba_rows", "scan", "ba_gather", "plain_spec", "plain_ba", "fixed_plain", "fixed", "plain_opt")
 REGEX_KERNELS = ("regex_dict", "regex_codes", "regex_lanes", "regex_plain", "regex_pages")
 ROWS = 10_000_000
 C5_PATTERN = "^qx"  # splits C5's pages (≈7% reported): not an all-miss scan
@@ -507,6 +507,23 @@ def c3_legs(J, args, exp):
     c3d["chunker"] = {"ms": statistics.median(ct) * 1e3, "chunks": nchunks,
                       "note": "pq_chunk_assign incl. the tuple_to_chunk copy to host (80 MB)"}
     rdc.free()
+    # the same strings OPTIONAL with 5 % NULLs in 20,000-row pages (the shape
+    # pyarrow writes by default): levels, then the value sections on the
+    # PLAIN kernels
+    ocol = gen.Col("comment", gen.COMMENT, gen.BYTE_ARRAY, optional=True, null_frac=0.05, len_min=10, len_max=44)
+    ofile = gen.build([ocol], rows, 1, seed=gen.CONFIG_SEEDS["C3"], layout=gen.ARROW_LAYOUT, first_rg=J.rank)
+    OF = capi.File(ofile)
+    odc = J.ctx.upload(ofile, [OF.chunk(0, 0)])
+    odc.decode()
+    ok = None
+    if not args.no_validate:
+        ok = sha(capi.canonical_dump(odc.to_host())) == sha(gen.values_dump(ocol, 0, rows, J.rank, gen.CONFIG_SEEDS["C3"]))
+    secs, okern = J.timed(odc.decode_async, odc.decode_check, dsteps, args.repeats, warmup=2)
+    med = statistics.median(secs)
+    c3d["optional_arrow"] = {"ms_per_decode": med / dsteps * 1e3, "values_per_s": rows * dsteps * J.world / med,
+                             "pages": odc.num_pages, "null_frac": 0.05,
+                             "kernel_ms": {k: v["ms_per_step"] for k, v in okern.items()}, "validated": ok}
+    odc.free()
     return regex, c3d
 
 
