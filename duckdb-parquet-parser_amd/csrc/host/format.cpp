@@ -513,6 +513,7 @@ struct SpecSeg {
 // so a thread keeps several independent DRAM misses in flight (a single
 // chain is one dependent miss per page).
 constexpr int kSpecLanes = 16;
+constexpr size_t kSpecScan = 16384;  // bytes a segment scans for its first header
 
 std::vector<SpecSeg> speculate(const uint8_t* file, size_t len, size_t start, size_t end, int threads) {
     const int nseg = threads * kSpecLanes;
@@ -527,7 +528,10 @@ std::vector<SpecSeg> speculate(const uint8_t* file, size_t len, size_t start, si
         const SpecSeg& sg = segs[static_cast<size_t>(k)];
         size_t pos = sg.lo;
         if (k == 0) return pos;
-        for (; pos < sg.hi; pos++) {
+        // a segment inside one large page finds no start: give up after
+        // kSpecScan bytes (the exact walk crosses it in one hop anyway)
+        const size_t lim = std::min(sg.hi, sg.lo + kSpecScan);
+        for (; pos < lim; pos++) {
             PageHeader h;
             if (!FastHdr(file, len, pos).parse(h) || !plausible(h, pos, end)) continue;
             size_t q = pos + h.header_size + static_cast<size_t>(h.compressed);
@@ -539,7 +543,7 @@ std::vector<SpecSeg> speculate(const uint8_t* file, size_t len, size_t start, si
             }
             if (ok) break;
         }
-        return pos;
+        return pos < lim ? pos : sg.hi;
     };
     auto work = [&](int t) {
         size_t pos[kSpecLanes];
@@ -595,7 +599,20 @@ WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, i
         w.pages.reserve(c.total_compressed_size > 0 ? static_cast<size_t>(std::min<int64_t>(c.total_compressed_size / 256, 1 << 22)) : 16);
         if (threads <= 0) threads = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
         threads = static_cast<int>(std::min<int64_t>(threads, c.total_compressed_size / (2 << 20)));
-        if (c.total_compressed_size >= kSpecMinBytes && threads > 1 && off >= 0 &&
+        // pages of tens of KiB or more: few enough for the exact walk alone
+        // (probe the first headers; a segment would mostly scan page bytes)
+        bool small_pages = true;
+        if (c.total_compressed_size >= kSpecMinBytes && off >= 0 && static_cast<size_t>(off) < len) {
+            size_t q = static_cast<size_t>(off);
+            int k = 0;
+            for (; k < 4 && q < len; k++) {
+                PageHeader h;
+                if (!FastHdr(file, len, q).parse(h) || h.compressed < 0) break;
+                q += h.header_size + static_cast<size_t>(h.compressed);
+            }
+            small_pages = k == 0 || (q - static_cast<size_t>(off)) / static_cast<size_t>(k) < kSpecScan;
+        }
+        if (c.total_compressed_size >= kSpecMinBytes && threads > 1 && off >= 0 && small_pages &&
             static_cast<size_t>(off) < len) {
             const size_t end = std::min(len, static_cast<size_t>(off) + static_cast<size_t>(c.total_compressed_size));
             if (end > cur) segs = speculate(file, len, cur, end, threads);
