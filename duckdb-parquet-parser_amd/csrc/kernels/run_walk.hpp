@@ -23,40 +23,50 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
     const uint32_t nbv = (W.bw + 7) / 8;
     const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
     const uint32_t litpay = W.bw ? 0x80000000u : 0u;
-    const uint32_t litmul = W.bw ? 8u : 0u;
+    const uint32_t litsh = W.bw ? 0xFFFFFFFFu : 0u;  // literal payload: bit offset qh * 8 when bw > 0
     uint32_t cnt = 0, q = W.q, nr = nrec, fl = flag;
     bool alive = W.alive && W.n > 0;
-    // branch-free step: every quantity is computed, one predicated store
-    while (__ballot(alive)) {
-        uint32_t x0, x1;
+    // eight bytes at stream position qq; the next header's bytes are loaded
+    // as soon as its position is known, so the load's latency overlaps the
+    // current step's record (a lane that stops keeps its position)
+    auto load = [&](uint32_t qq, bool live, uint32_t& x0, uint32_t& x1) {
         if (kStaged) {
-            const uint32_t a = W.sbase + q, wi = a >> 2, sh = a & 3;
+            const uint32_t a = W.sbase + qq, wi = a >> 2, sh = a & 3;
             const uint32_t w0 = stage[wi], w1 = stage[wi + 1], w2 = stage[wi + 2];
             x0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
             x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
         } else {
-            const uint64_t x = alive ? gld8(W.gp, q) : 0ull;
+            const uint64_t x = live ? gld8(W.gp, qq) : 0ull;
             x0 = static_cast<uint32_t>(x);
             x1 = static_cast<uint32_t>(x >> 32);
         }
+    };
+    uint32_t x0, x1;
+    load(q, alive, x0, x1);
+    // branch-free step: every quantity is computed, one predicated store
+    while (__ballot(alive)) {
         const uint32_t exh = q >= W.end ? 1u : 0u;  // rest of the batch is 0 (rle_decoder.hpp:20-23)
-        // varint header (76-86): at most 5 bytes, inside the stream
-        const uint32_t st0 = ~x0 & 0x80808080u;
-        const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;
-        const uint32_t hl5 = (~x1 & 0x80u) ? 5u : 9u;
-        const uint32_t hl = st0 ? hl4 : hl5;
-        const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
-        const uint32_t x0m = x0 & lm;
-        const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
-        const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
-                             ((x0m >> 3) & 0xFE00000u) | top;
+        // varint header (76-86): at most 5 bytes, inside the stream.  When
+        // every live header is one byte (runs of < 64 values or groups: what
+        // both writers emit for these pages) the general parse is skipped.
+        uint32_t hl, ind;
+        if (__ballot(alive && !exh && (x0 & 0x80u)) == 0) {
+            hl = 1;
+            ind = x0 & 0x7Fu;
+        } else {
+            const uint32_t st0 = ~x0 & 0x80808080u;
+            const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;
+            const uint32_t hl5 = (~x1 & 0x80u) ? 5u : 9u;
+            hl = st0 ? hl4 : hl5;
+            const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
+            const uint32_t x0m = x0 & lm;
+            const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
+            ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) | ((x0m >> 3) & 0xFE00000u) | top;
+        }
         const uint32_t g = ind >> 1;
         const uint32_t lit = ind & 1u;
         const uint32_t left = W.n - cnt;
         const uint32_t qh = q + hl;
-        const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, hl);
-        const uint32_t vb = x1 >> (8 * ((hl - 4) & 3));
-        const uint32_t vraw = (hl < 4) ? va : vb;
         const uint32_t cl = (g >= (left + 7) / 8) ? left : g * 8;
         const uint32_t cr = min(g, left);
         const uint32_t c = lit ? cl : cr;
@@ -65,20 +75,31 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
                               ((lit ^ 1u) & (qh + nbv > W.end ? 1u : 0u));
         const uint32_t full = nr >= W.cap ? 1u : 0u;
         const uint32_t ok = (alive ? 1u : 0u) & (full ^ 1u) & (exh | (badh ^ 1u));
-        const uint32_t rx = cnt | ((exh ? left : c) << 16);
         // selects by mask (the compiler turns a ternary on `lit` into a branch)
         const uint32_t litm = 0u - lit;
-        const uint32_t pl = (litm & (litpay | (qh * litmul))) | (~litm & vraw & vmask);
+        // g clamps at 2^16: a longer literal run overruns the stream (<= 64 KiB) either way
+        // (24-bit multiplies: g <= 2^16, bw <= 32)
+        const uint32_t nqlc = min(__umul24(min(g, 0x10000u), W.bw) + qh, W.end);
+        const uint32_t nq = (litm & nqlc) | (~litm & (qh + nbv));
+        const uint32_t ncnt = exh ? W.n : cnt + c;
+        const uint32_t qn = (ok & (exh ^ 1u)) ? nq : q;
+        const bool an = ok && !exh && ncnt < W.n;
+        uint32_t y0, y1;
+        load(qn, an, y0, y1);
+        const uint32_t rx = cnt | ((exh ? left : c) << 16);
+        const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, hl);
+        const uint32_t vb = x1 >> (8 * ((hl - 4) & 3));
+        const uint32_t vraw = (hl < 4) ? va : vb;
+        const uint32_t pl = (litm & (litpay | ((qh << 3) & litsh))) | (~litm & vraw & vmask);
         const uint32_t ry = exh ? 0u : pl;
         if (ok) W.out[nr] = make_uint2(rx, ry);
         fl |= (alive ? 1u : 0u) & (ok ^ 1u);
         nr += ok;
-        // g clamps at 2^16: a longer literal run overruns the stream (<= 64 KiB) either way
-        const uint32_t nqlc = min(qh + min(g, 0x10000u) * W.bw, W.end);
-        const uint32_t nq = (litm & nqlc) | (~litm & (qh + nbv));
-        cnt = exh ? W.n : cnt + c;
-        q = ok ? nq : q;
-        alive = ok && !exh && cnt < W.n;
+        cnt = ncnt;
+        q = qn;
+        alive = an;
+        x0 = y0;
+        x1 = y1;
     }
     nrec = nr;
     flag = fl;
