@@ -1148,7 +1148,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
 //      k_pipe_codes3, each tile's first record found by binary search.
 // Anything outside the fast shape (a bad header before the value count,
 // record overflow, levels above max_def) sends the page to k_pipe_exact.
-constexpr int kBigWaves = 8;
+constexpr int kBigWaves = 12;
 constexpr int kBigThreads = kBigWaves * kWave;
 constexpr uint32_t kBStop = 0xFFFFu;
 constexpr int kBJumpLog = 4;
@@ -1169,10 +1169,12 @@ __host__ __device__ inline BigLayout big_layout(uint32_t size, uint32_t nlens) {
     L.tab = L.stage + L.P;                       // u16 per position; then P / 4 run records
     L.esum = L.tab + 2 * L.P;                    // u32 per listed header: values, then their exclusive scan
     L.ent = L.esum + 8 * L.LC;                   // u32 per listed header: position, then fill results
-    L.lens = L.ent + 8 * L.LC;                   // u16 per dictionary entry: length
+    L.tvb = L.esum;                              // per tile: validity bits of rows 8l .. 8l + 7 (phase 6:
+                                                 // over esum / ent, dead after phase 5)
+    const uint32_t x = 16 * L.LC > static_cast<uint32_t>(kBigTiles * kWave) ? 16 * L.LC : static_cast<uint32_t>(kBigTiles * kWave);
+    L.lens = L.esum + x;                         // u16 per dictionary entry: length
     L.mark = L.lens + (2 * nlens + 15) / 16 * 16;  // per wave: u16 per row of a tile
-    L.tvb = L.mark + kBigWaves * kTileRows * 2;  // per tile: validity bits of rows 8l .. 8l + 7
-    L.misc = L.tvb + kBigTiles * kWave;          // tile non-null counts, first ranks, scan partials, flags
+    L.misc = L.mark + kBigWaves * kTileRows * 2;  // tile non-null counts, first ranks, scan partials, flags
     L.total = L.misc + 4 * (2 * kBigTiles + kBigWaves + 16);
     return L;
 }
