@@ -1499,9 +1499,9 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     return P;
 }
 
-// Run tables and per-row codes (k_pipe_runs, k_pipe_big, k_pipe_codes2,
-// k_pipe_exact).  With dict_on_side the dictionary decodes on ctx->side and
-// the codes wait for it (ev_join).
+// Run tables and per-row codes (k_pipe_runs, k_pipe_big, k_pipe_codes3; the
+// exact decoder for pages outside the fast shape).  With dict_on_side the
+// dictionary decodes on ctx->side and the codes wait for it (ev_join).
 static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side) {
     hipStream_t s = ctx->stream;
     {

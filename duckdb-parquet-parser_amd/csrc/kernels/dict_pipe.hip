@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
     const uint32_t orec = static_cast<uint32_t>(__shfl_xor(static_cast<int>(nrec), 1));
     if (act && s == 0)
         info[p] = ((flag | oflag) ? kFallback : 0u) | nrec | (orec << 8) | (bwi << 16);
-    if (act && s == 0 && (flag | oflag)) flist[1 + atomicAdd(flist, 1)] = p;  // for k_pipe_exact
+    if (act && s == 0 && (flag | oflag)) flist[1 + atomicAdd(flist, 1)] = p;  // for k_pipe_codes3's exact decoder
 }
 
 // ── per-tile codes ─────────────────────────────────────────────────────────
@@ -462,20 +462,6 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_codes(CodeArgs a) {
 
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane i <- lane i - 1, lane 0 <- 0
     return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x138, 0xf, 0xf, true));
-}
-
-// Marked pages (listed by k_pipe_runs): the exact serial decoder, one
-// wavefront per page.
-__global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_exact(CodeArgs a, const int32_t* __restrict__ flist) {
-    __shared__ CodeLds lds_all[kCodeWaves];
-    const int wv = static_cast<int>(threadIdx.x / kWave);
-    const int n = flist[0];
-    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
-    for (int i = static_cast<int>(blockIdx.x) * kCodeWaves + wv; i < n; i += static_cast<int>(gridDim.x) * kCodeWaves) {
-        exact_page(a, lds_all[wv], flist[1 + i], dict_n, ebase);
-        __builtin_amdgcn_wave_barrier();
-    }
 }
 
 // ── per-tile codes, lean form ──────────────────────────────────────────────
@@ -1147,7 +1133,8 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
 //      the tiles' non-null counts, then dictionary indices and codes as in
 //      k_pipe_codes3, each tile's first record found by binary search.
 // Anything outside the fast shape (a bad header before the value count,
-// record overflow, levels above max_def) sends the page to k_pipe_exact.
+// record overflow, levels above max_def) is decoded by the exact serial decoder
+// (exact_page), by wave 0 of the page's workgroup.
 constexpr int kBigWaves = 12;
 constexpr int kBigThreads = kBigWaves * kWave;
 constexpr uint32_t kBStop = 0xFFFFu;
@@ -1275,8 +1262,7 @@ __device__ void big_scan(uint32_t* v, uint32_t m, uint32_t* part) {
 }
 
 __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int32_t* __restrict__ bigp,
-                                                          int32_t* __restrict__ flist, uint32_t* __restrict__ info,
-                                                          uint32_t nlens) {
+                                                          uint32_t* __restrict__ info, uint32_t nlens) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int p = bigp[blockIdx.x];
     const DevPage pg = a.pages[p];
@@ -1302,7 +1288,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
     const uint32_t nl = min(dict_n, nlens);
 
-    // prologue (column_reader.cpp:146-182), wave-uniform; any error -> k_pipe_exact
+    // prologue (column_reader.cpp:146-182), wave-uniform; any error -> exact_page
     bool flag = n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes;
     uint32_t pos = 0, dbase = 0, dlen = 0, bwi = 0;
     if (!flag && a.max_def > 0) {
@@ -1328,11 +1314,12 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         else { bwi = static_cast<uint32_t>(gld8(page, pos)) & 0xFFu; pos += 1; }
     }
     if (!flag && bwi > 16) flag = true;
+    // anything outside the fast shape: the exact serial decoder, by wave 0
+    // of this workgroup (the page in HBM; LDS only for its small scratch),
+    // so no further launch is needed after the big pages
     auto to_exact = [&]() {
-        if (tid == 0) {
-            info[p] = kFallback;
-            flist[1 + atomicAdd(flist, 1)] = p;
-        }
+        if (tid == 0) info[p] = kFallback;
+        if (wv == 0) exact_page(a, *reinterpret_cast<CodeLds*>(smem), p, dict_n, ebase);
     };
     if (flag) return to_exact();
     const bool hasd = a.max_def > 0;
@@ -1564,7 +1551,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
 }
 
 // ── regex page filter over the codes (README.md:54-64, SURVEY §8a R-REGEX) ─
-// After k_pipe_runs / k_pipe_big / k_pipe_codes3 / k_pipe_exact: one wave per
+// After k_pipe_runs / k_pipe_big / k_pipe_codes3: one wave per
 // tile tests its rows' codes against the dictionary's match bits (the pattern
 // ran once per entry, k_regex_dict).  A page whose tiles hold no non-null
 // value that matches (with --neg-regex: that fails to match) stays reported.
@@ -1635,7 +1622,7 @@ static void write_shape(const PipeLaunch& P, int* grid, int* per) {
 }
 
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
-    if (P.ntiles <= 0) return;
+    if (P.ntiles <= 0 || (!count_pass && !P.has_small)) return;
     int wgrid = 0, per = 0;
     write_shape(P, &wgrid, &per);
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
@@ -1663,12 +1650,9 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     const int need = (P.ntiles + waves - 1) / waves;
     const int grid = max(1, min(need, P.cus * bpc));
     // also decodes the pages the run-table passes marked (flist)
-    if (P.has_small) {
-        hipLaunchKernelGGL(k_pipe_codes3, dim3(grid), dim3(kCodeWaves3 * kWave), lds, s, a, lt_n, P.flist);
-    } else {  // only k_pipe_big pages: the marked ones need the exact decoder alone
-        hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, (P.npages + kCodeWaves - 1) / kCodeWaves))),
-                           dim3(kCodeWaves * kWave), 0, s, a, P.flist);
-    }
+    // (only k_pipe_big pages: nothing to do, k_pipe_big decoded its own
+    // fallback pages exactly)
+    if (P.has_small) hipLaunchKernelGGL(k_pipe_codes3, dim3(grid), dim3(kCodeWaves3 * kWave), lds, s, a, lt_n, P.flist);
 }
 
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
@@ -1703,7 +1687,7 @@ void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_page
         attr = lds;
     }
     hipLaunchKernelGGL(k_pipe_big, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
-                       const_cast<int32_t*>(P.flist), const_cast<uint32_t*>(P.info), nlens);
+                       const_cast<uint32_t*>(P.info), nlens);
 }
 
 void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags) {
