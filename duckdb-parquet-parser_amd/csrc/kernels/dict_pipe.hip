@@ -1194,13 +1194,20 @@ __device__ __forceinline__ bool big_bad(const BigHdr& h, uint32_t e, uint32_t nb
     return h.hl > 5 || h.qh > e || h.g == 0 || (!h.lit && h.qh + nbv > e);
 }
 
-// Largest k < nr with start(rec[k]) <= v (rec[0] starts at 0); wave-uniform.
+// Largest k < nr with start(rec[k]) <= v (rec[0] starts at 0, starts
+// increase); wave-uniform, called by the whole wave.  Each round the 64 lanes
+// test 64 evenly spaced records and keep the stride after the last one that
+// starts <= v: two dependent LDS reads for up to 4096 records.
 __device__ __forceinline__ uint32_t big_search(const uint2* rec, uint32_t nr, uint32_t v) {
-    uint32_t lo = 0, hi = nr;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (rr_start(rec[mid]) <= v) lo = mid;
-        else hi = mid;
+    uint32_t lo = 0, span = nr;
+    while (span > 1) {
+        const uint32_t st = (span + kWave - 1) / kWave;
+        const uint32_t d = lane() * st;
+        const bool le = d < span && rr_start(rec[lo + min(d, span - 1)]) <= v;
+        const uint64_t b = __ballot(le);  // bit 0 set: rec[lo] starts <= v
+        const uint32_t j = 63u - static_cast<uint32_t>(__builtin_clzll(b | 1ull));
+        lo += j * st;
+        span = min(st, span - j * st);
     }
     return lo;
 }
