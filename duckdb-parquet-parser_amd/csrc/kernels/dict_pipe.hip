@@ -1212,6 +1212,18 @@ __device__ __forceinline__ uint32_t big_search(const uint2* rec, uint32_t nr, ui
     return lo;
 }
 
+// Bits [b, b + bw) of the staged page, bw <= 16.  The stage holds the page
+// and its slot's zero padding (nw words, >= 16 bytes past the page end), so
+// bits past the end read as zero without a bound per word, like lds_bits;
+// offsets past the padding (a literal run cut by the page end) read as zero.
+__device__ __forceinline__ uint32_t big_bits(const uint32_t* stw, uint32_t nw, uint32_t b, uint32_t bw) {
+    const uint32_t wi = b >> 5;
+    const bool in = wi + 1 < nw;
+    const uint32_t i0 = in ? wi : 0u;
+    const uint32_t x = __builtin_amdgcn_alignbit(stw[i0 + 1], stw[i0], b & 31u);
+    return in ? (x & ((1u << bw) - 1u)) : 0u;
+}
+
 // Marks the starts of records k0 + 1 .. that begin inside [v0, v0 + m):
 // mark[start - v0] = record - k0.
 __device__ __forceinline__ void big_mark(uint16_t* mark, const uint2* rec, uint32_t nr, uint32_t k0, uint32_t v0,
@@ -1277,6 +1289,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
     const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
     const BigLayout Ly = big_layout(size, nlens);
+    const uint32_t nw = Ly.P / 4;  // staged words: the page and its slot's zero padding
     uint32_t* stw = reinterpret_cast<uint32_t*>(smem + Ly.stage);
     uint16_t* tab = reinterpret_cast<uint16_t*>(smem + Ly.tab);
     uint32_t* esum = reinterpret_cast<uint32_t*>(smem + Ly.esum);
@@ -1477,12 +1490,11 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
             uint32_t rm[8];
             big_runs8(mark, l8, m, rm);
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
+            for (int k = 0; k < 8; k++) {  // selects, not branches
                 const uint32_t j = l8 + k;
                 const uint2 R = recd[rd0 + rm[k]];
-                uint32_t lvl = rr_pay(R);
-                if (rr_lit(R) && j < m)
-                    lvl = lds_bits(stw, size, rr_pay(R) + static_cast<uint64_t>(r0 + j - rr_start(R)) * bwd, bwd);
+                const uint32_t lb = big_bits(stw, nw, rr_pay(R) + __umul24(r0 + j - rr_start(R), bwd), bwd);
+                const uint32_t lvl = rr_lit(R) ? lb : rr_pay(R);
                 vb |= (j < m && lvl == md ? 1u : 0u) << k;
                 above |= j < m && lvl > md;
             }
@@ -1533,22 +1545,18 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         uint32_t chars = 0, cw8[8];
         const int64_t R0 = first_row + r0;
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t j = l8 + k;
-            uint32_t code = kNull;
-            if ((vb >> k) & 1u) {
-                const uint32_t rk = rbase + __popc(vb & ((1u << k) - 1u));
-                const uint2 R = reci[ri0 + mark[rk]];
-                uint32_t v = rr_pay(R);
-                if (rr_lit(R))
-                    v = lds_bits(stw, size, rr_pay(R) + static_cast<uint64_t>(k0 + rk - rr_start(R)) * bwi, bwi);
-                if (v < dict_n) {
-                    code = v;
-                    chars += v < nl ? lens[v] : static_cast<uint32_t>(a.entries[ebase + v] >> 32);
-                }
-            }
+        for (int k = 0; k < 8; k++) {  // selects, not branches (NULL rows read record ri0)
+            const bool nz = (vb >> k) & 1u;
+            const uint32_t rk = rbase + __popc(vb & ((1u << k) - 1u));
+            const uint2 R = reci[nz ? ri0 + mark[rk] : ri0];
+            const uint32_t lb = big_bits(stw, nw, rr_pay(R) + __umul24(k0 + rk - rr_start(R), bwi), bwi);
+            const uint32_t v = rr_lit(R) ? lb : rr_pay(R);
+            const bool ok = nz && v < dict_n;
+            const uint32_t code = ok ? v : kNull;
+            uint32_t len = lens[ok && v < nl ? v : 0u];
+            if (ok && v >= nl) len = static_cast<uint32_t>(a.entries[ebase + v] >> 32);  // dictionaries over kBigLens
+            chars += ok ? len : 0u;
             cw8[k] = code;
-            (void)j;
         }
         store_codes8(a.codes, R0, l8, m, cw8);
         chars = wave_sum(chars);
