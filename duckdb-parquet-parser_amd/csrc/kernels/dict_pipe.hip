@@ -1344,7 +1344,6 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     if (flag) return to_exact();
     const bool hasd = a.max_def > 0;
     const uint32_t dend = dbase + dlen, ibase = pos, iend = size;
-    auto in_stream = [&](uint32_t j) { return j >= ibase || (hasd && j >= dbase && j < dend); };
 
     // 0. the payload slot and the dictionary's entry lengths -> LDS
     copy_blocks(reinterpret_cast<uint4*>(stw), reinterpret_cast<const uint4*>(page), Ly.P / 16, tid, kBigThreads);
@@ -1352,37 +1351,52 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     if (tid < 8) sh[tid] = 0;
     __syncthreads();
     if (a.debug & 0x10000) return;  // timing: staging only
-    // 1. speculative headers at every byte of both streams
-    for (uint32_t j = tid; j < size; j += kBigThreads) {
-        if (!in_stream(j)) continue;
+    // 1. speculative headers at every byte, two bytes per thread and one
+    //    dword store (bytes outside both streams get entries no chain reads:
+    //    a next position is always inside its stream, else kBStop)
+    auto next_at = [&](uint32_t j) -> uint32_t {
         const bool isi = j >= ibase;
         const uint32_t e = isi ? iend : dend, bw = isi ? bwi : bwd;
         const BigHdr h = big_hdr(stw, j);
-        const uint64_t nx = h.lit ? static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw : h.qh + (bw + 7) / 8;
-        tab[j] = static_cast<uint16_t>((big_bad(h, e, (bw + 7) / 8) || nx >= e) ? kBStop : static_cast<uint32_t>(nx));
-    }
+        // g clamps at 2^16: a longer literal run leaves any stream (<= 24 KiB) either way
+        const uint32_t nx = h.lit ? h.qh + __umul24(min(h.g, 0x10000u), bw) : h.qh + (bw + 7) / 8;
+        return (j >= size || big_bad(h, e, (bw + 7) / 8) || nx >= e) ? kBStop : nx;
+    };
+    for (uint32_t jp = tid; 2 * jp < size; jp += kBigThreads)
+        reinterpret_cast<uint32_t*>(tab)[jp] = next_at(2 * jp) | (next_at(2 * jp + 1) << 16);
     __syncthreads();
     if (a.debug & 0x20000) return;  // timing: + header parse
-    // 2. kBJump-run jumps by pointer doubling
-    for (int r = 0; r < kBJumpLog; r++) {
-        uint32_t nv[kBigPerThread];
+    // 2. kBJump-run jumps by pointer doubling, two positions per thread
+    //    (one dword of the table read and written)
+    {
+        uint32_t* tab32 = reinterpret_cast<uint32_t*>(tab);
+        const uint32_t npair = (size + 1) / 2;
+        auto hop = [&](uint32_t t) {  // kBStop stays
+            const uint32_t u = tab[t == kBStop ? 0u : t];
+            return t == kBStop ? kBStop : u;
+        };
+        for (int r = 0; r < kBJumpLog; r++) {
+            uint32_t nv[kBigPerThread / 2];
 #pragma unroll
-        for (uint32_t i = 0; i < kBigPerThread; i++) {
-            const uint32_t j = tid + i * kBigThreads;
-            uint32_t t = kBStop;
-            if (j < size && in_stream(j)) {
-                t = tab[j];
-                if (t != kBStop) t = tab[t];
+            for (uint32_t i = 0; i < kBigPerThread / 2; i++) {
+                if (i * kBigThreads >= npair) break;  // (uniform)
+                const uint32_t jp = tid + i * kBigThreads;
+                uint32_t w = kBStop | (kBStop << 16);
+                if (jp < npair) {
+                    const uint32_t x = tab32[jp];
+                    w = hop(x & 0xFFFFu) | (hop(x >> 16) << 16);
+                }
+                nv[i] = w;
             }
-            nv[i] = t;
-        }
-        __syncthreads();
+            __syncthreads();
 #pragma unroll
-        for (uint32_t i = 0; i < kBigPerThread; i++) {
-            const uint32_t j = tid + i * kBigThreads;
-            if (j < size && in_stream(j)) tab[j] = static_cast<uint16_t>(nv[i]);
+            for (uint32_t i = 0; i < kBigPerThread / 2; i++) {
+                if (i * kBigThreads >= npair) break;
+                const uint32_t jp = tid + i * kBigThreads;
+                if (jp < npair) tab32[jp] = nv[i];
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
     if (a.debug & 4096) return;  // timing: jump table only
     // 3. one lane per stream follows the jumps: every kBJump-th header
