@@ -1212,6 +1212,15 @@ __device__ __forceinline__ uint32_t big_search(const uint2* rec, uint32_t nr, ui
     return lo;
 }
 
+// x where c holds, else 0, as an and with an opaque mask: a select whose
+// operand is a load would be turned into a branch around the load, which
+// serialises the eight rows' LDS chains of a lane.
+__device__ __forceinline__ uint32_t keep_if(bool c, uint32_t x) {
+    uint32_t m = c ? 0xFFFFFFFFu : 0u;
+    __asm__("" : "+v"(m));
+    return x & m;
+}
+
 // Bits [b, b + bw) of the staged page, bw <= 16.  The stage holds the page
 // and its slot's zero padding (nw words, >= 16 bytes past the page end), so
 // bits past the end read as zero without a bound per word, like lds_bits;
@@ -1221,7 +1230,7 @@ __device__ __forceinline__ uint32_t big_bits(const uint32_t* stw, uint32_t nw, u
     const bool in = wi + 1 < nw;
     const uint32_t i0 = in ? wi : 0u;
     const uint32_t x = __builtin_amdgcn_alignbit(stw[i0 + 1], stw[i0], b & 31u);
-    return in ? (x & ((1u << bw) - 1u)) : 0u;
+    return keep_if(in, x & ((1u << bw) - 1u));
 }
 
 // Marks the starts of records k0 + 1 .. that begin inside [v0, v0 + m):
@@ -1508,7 +1517,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
                 const uint32_t j = l8 + k;
                 const uint2 R = recd[rd0 + rm[k]];
                 const uint32_t lb = big_bits(stw, nw, rr_pay(R) + __umul24(r0 + j - rr_start(R), bwd), bwd);
-                const uint32_t lvl = rr_lit(R) ? lb : rr_pay(R);
+                const uint32_t lvl = keep_if(rr_lit(R), lb) | keep_if(!rr_lit(R), rr_pay(R));
                 vb |= (j < m && lvl == md ? 1u : 0u) << k;
                 above |= j < m && lvl > md;
             }
@@ -1556,21 +1565,26 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        uint32_t chars = 0, cw8[8];
+        uint32_t chars = 0, cw8[8], far = 0;
         const int64_t R0 = first_row + r0;
 #pragma unroll
         for (int k = 0; k < 8; k++) {  // selects, not branches (NULL rows read record ri0)
             const bool nz = (vb >> k) & 1u;
             const uint32_t rk = rbase + __popc(vb & ((1u << k) - 1u));
-            const uint2 R = reci[nz ? ri0 + mark[rk] : ri0];
+            const uint2 R = reci[ri0 + keep_if(nz, mark[nz ? rk : 0u])];
             const uint32_t lb = big_bits(stw, nw, rr_pay(R) + __umul24(k0 + rk - rr_start(R), bwi), bwi);
-            const uint32_t v = rr_lit(R) ? lb : rr_pay(R);
+            const uint32_t v = keep_if(rr_lit(R), lb) | keep_if(!rr_lit(R), rr_pay(R));
             const bool ok = nz && v < dict_n;
-            const uint32_t code = ok ? v : kNull;
-            uint32_t len = lens[ok && v < nl ? v : 0u];
-            if (ok && v >= nl) len = static_cast<uint32_t>(a.entries[ebase + v] >> 32);  // dictionaries over kBigLens
-            chars += ok ? len : 0u;
+            const uint32_t code = keep_if(ok, v) | keep_if(!ok, kNull);
+            const bool inl = ok && v < nl;
+            chars += keep_if(inl, lens[inl ? v : 0u]);
+            far |= (ok && !inl ? 1u : 0u) << k;
             cw8[k] = code;
+        }
+        if (__ballot(far != 0)) {  // entries past the LDS length table (dictionaries over kBigLens)
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                if ((far >> k) & 1u) chars += static_cast<uint32_t>(a.entries[ebase + cw8[k]] >> 32);
         }
         store_codes8(a.codes, R0, l8, m, cw8);
         chars = wave_sum(chars);

@@ -37,6 +37,10 @@ SMALL = [
                               dict_size=40, len_min=100, len_max=3000)], 4000),
     ("wide_dict", [gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, dict_size=70000, len_min=1, len_max=6,
                            max_run=2)], 400000),
+    # pipe-sized dictionary (< 64 KiB) with more entries than k_pipe_big's LDS
+    # length table (kBigLens = 8192): the lengths of later entries come from HBM
+    ("lens_past_lds", [gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.1,
+                               dict_size=9000, len_min=3, len_max=4, max_run=2)], 60000),
     # OPTIONAL PLAIN BYTE_ARRAY (levels, then value sections on the PLAIN
     # kernels): 1 KiB pages (windows) and 3000-row arrow pages (chunk chains),
     # sparse, all-NULL, strings over the chunk chains' 60-byte reach
