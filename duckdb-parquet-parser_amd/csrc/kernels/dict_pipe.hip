@@ -1317,13 +1317,29 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
     const uint32_t nl = min(dict_n, nlens);
 
-    // prologue (column_reader.cpp:146-182), wave-uniform; any error -> exact_page
-    bool flag = n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes;
+    // anything outside the fast shape: the exact serial decoder, by wave 0
+    // of this workgroup (the page in HBM; LDS only for its small scratch),
+    // so no further launch is needed after the big pages
+    auto to_exact = [&]() {
+        if (tid == 0) info[p] = kFallback;
+        if (wv == 0) exact_page(a, *reinterpret_cast<CodeLds*>(smem), p, dict_n, ebase);
+    };
+    if (n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes) return to_exact();
+
+    // 0. the payload slot and the dictionary's entry lengths -> LDS (before
+    //    the prologue, which then reads the stage instead of HBM)
+    copy_blocks(reinterpret_cast<uint4*>(stw), reinterpret_cast<const uint4*>(page), Ly.P / 16, tid, kBigThreads);
+    copy_map(lens, a.entries + ebase, nl, tid, kBigThreads, [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
+    if (tid < 8) sh[tid] = 0;
+    __syncthreads();
+    // prologue (column_reader.cpp:146-182), workgroup-uniform; any error -> exact_page
+    auto rd32 = [&](uint32_t at) { return static_cast<uint32_t>(lds_u64(stw, at)); };
+    bool flag = false;
     uint32_t pos = 0, dbase = 0, dlen = 0, bwi = 0;
-    if (!flag && a.max_def > 0) {
+    if (a.max_def > 0) {
         if (size < 4) flag = true;
         else {
-            dlen = static_cast<uint32_t>(gld8(page, 0));
+            dlen = rd32(0);
             pos = 4;
             if (static_cast<uint64_t>(pos) + dlen > size) flag = true;
             else { dbase = 4; pos += dlen; }
@@ -1332,7 +1348,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     if (!flag && a.max_rep > 0) {
         if (pos + 4 > size) flag = true;
         else {
-            const uint32_t rl = static_cast<uint32_t>(gld8(page, pos));
+            const uint32_t rl = rd32(pos);
             pos += 4;
             if (static_cast<uint64_t>(pos) + rl > size) flag = true;
             else pos += rl;
@@ -1340,25 +1356,15 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     }
     if (!flag) {
         if (pos + 1 > size) flag = true;
-        else { bwi = static_cast<uint32_t>(gld8(page, pos)) & 0xFFu; pos += 1; }
+        else { bwi = rd32(pos) & 0xFFu; pos += 1; }
     }
     if (!flag && bwi > 16) flag = true;
-    // anything outside the fast shape: the exact serial decoder, by wave 0
-    // of this workgroup (the page in HBM; LDS only for its small scratch),
-    // so no further launch is needed after the big pages
-    auto to_exact = [&]() {
-        if (tid == 0) info[p] = kFallback;
-        if (wv == 0) exact_page(a, *reinterpret_cast<CodeLds*>(smem), p, dict_n, ebase);
-    };
-    if (flag) return to_exact();
+    if (flag) {
+        __syncthreads();  // every wave has read the stage before wave 0 reuses it
+        return to_exact();
+    }
     const bool hasd = a.max_def > 0;
     const uint32_t dend = dbase + dlen, ibase = pos, iend = size;
-
-    // 0. the payload slot and the dictionary's entry lengths -> LDS
-    copy_blocks(reinterpret_cast<uint4*>(stw), reinterpret_cast<const uint4*>(page), Ly.P / 16, tid, kBigThreads);
-    copy_map(lens, a.entries + ebase, nl, tid, kBigThreads, [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
-    if (tid < 8) sh[tid] = 0;
-    __syncthreads();
     if (a.debug & 0x10000) return;  // timing: staging only
     // 1. speculative headers at every byte, two bytes per thread and one
     //    dword store (bytes outside both streams get entries no chain reads:
