@@ -777,11 +777,12 @@ constexpr int kRowsPerLane = kTileRows / kWave;
 constexpr int kWBatch = 4;          // tiles whose codes k_pipe_write loads at once
 constexpr uint32_t kLongRow = 128;  // longer rows are copied by the whole wave
 
-struct WriteLds {
-    uint32_t off[kTileRows + 1];  // tile-relative first byte per row
+struct __attribute__((aligned(16))) WriteLds {  // 16-byte aligned: each lane stores its rows as b128
+    uint32_t off[kTileRows + 4];  // tile-relative first byte per row (+ the end at [m])
     uint16_t src[kTileRows];      // dictionary byte per row
     uint8_t vb[kWave];            // validity bits of rows 8l .. 8l + 7
 };
+static_assert(sizeof(WriteLds) % 16 == 0, "per-wave scratch alignment");
 
 
 __device__ __forceinline__ uint32_t dword_of(const uint4& v, uint32_t i) {  // register select, no scratch
@@ -970,16 +971,20 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
             const uint32_t incl = wave_incl_scan(acc);
             const uint32_t total = bcast_last(incl);
             {
-                uint32_t o = incl - acc;
+                // the lane's eight rows as two 16-byte stores of offsets and one
+                // of sources (row-per-element stores would hit each bank 8 and 4
+                // times); rows past m get the tile end and are never read as rows
+                static_assert(kRowsPerLane == 8, "row layout");
+                uint32_t o[kRowsPerLane];
+                o[0] = incl - acc;
 #pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++) {
-                    const uint32_t j = lane() * kRowsPerLane + k;
-                    if (j < m) {
-                        S.off[j] = o;
-                        S.src[j] = static_cast<uint16_t>(src[k]);
-                    }
-                    o += len[k];
-                }
+                for (int k = 1; k < kRowsPerLane; k++) o[k] = o[k - 1] + len[k - 1];
+                uint4* po = reinterpret_cast<uint4*>(&S.off[lane() * kRowsPerLane]);
+                po[0] = make_uint4(o[0], o[1], o[2], o[3]);
+                po[1] = make_uint4(o[4], o[5], o[6], o[7]);
+                *reinterpret_cast<uint4*>(&S.src[lane() * kRowsPerLane]) =
+                    make_uint4(src[0] | (src[1] << 16), src[2] | (src[3] << 16), src[4] | (src[5] << 16),
+                               src[6] | (src[7] << 16));
             }
             S.vb[lane()] = static_cast<uint8_t>(vb);
             if (lane() == 0) S.off[m] = total;
