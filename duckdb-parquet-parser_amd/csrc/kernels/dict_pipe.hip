@@ -1467,8 +1467,9 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
             const uint32_t c = h.lit ? min(h.g, kBCountCap / 8) * 8 : min(h.g, kBCountCap);
             out[s] = make_uint2(c, h.lit ? (litpay | (h.qh * litmul)) : (h.vraw & vmask));
             sum = min(sum + c, kBCountCap);
-            const uint64_t nql = static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw;
-            q = h.lit ? (nql > e ? e : static_cast<uint32_t>(nql)) : h.qh + nbv;
+            // (g clamps at 2^16: a longer literal run ends past the stream either way)
+            const uint32_t nql = h.qh + __umul24(min(h.g, 0x10000u), bw);
+            q = h.lit ? min(nql, e) : h.qh + nbv;
         }
         if (s == kBJump && q >= e) ended = 1;
         esum[i] = sum;
