@@ -78,6 +78,7 @@ struct pq_ctx {
     int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
+    bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
     int opt_stage_bufs = 6;      // "stage_bufs" / "stage_piece_kb": pinned upload ring (stage.hpp)
 };
 
@@ -691,6 +692,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
     if (std::strcmp(key, "plain_fused") == 0) { ctx->opt_plain_fused = value != 0; return 0; }
+    if (std::strcmp(key, "pipe_run_dict") == 0) { ctx->opt_run_dict = value != 0; return 0; }
     if (std::strcmp(key, "pipe_run_pages") == 0) {
         if (value < 1 || value > 32) return set_err(ctx, PQ_ERR_ARG, "pipe_run_pages: 1..32");
         ctx->opt_run_pages = static_cast<int>(value);
@@ -1502,13 +1504,17 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
 // Run tables and per-row codes (k_pipe_runs, k_pipe_big, k_pipe_codes3; the
 // exact decoder for pages outside the fast shape).  With dict_on_side the
 // dictionary decodes on ctx->side and the codes wait for it (ev_join).
-static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side) {
+// With dict_in_runs the dictionary pages decode in k_pipe_runs' leading
+// workgroups (same launch, main stream: ordered after the previous decode's
+// readers of the entry table, no side-stream events).
+static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs) {
     hipStream_t s = ctx->stream;
     {
         Timed t(ctx, "pipe_runs");
+        const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
         pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
                               c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist,  // flist[0], bsum: cleared with d_flags
-                              ctx->opt_debug);
+                              ctx->opt_debug, dict_in_runs ? &rd : nullptr);
     }
     if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
     if (!c->hbig.empty()) {
@@ -1563,7 +1569,12 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     }
     if (!(pipe_path && c->tiles_aligned32))
         (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
-    if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
+    // dictionary pages small enough for k_pipe_runs' workgroups decode there
+    const bool dict_in_runs = pipe && !plain_go && ctx->opt_run_dict && c->ndicts && c->type == PQ_BYTE_ARRAY &&
+                              c->d_dflag && c->max_dict_bytes <= pqk::kRunDictMax;
+    if (dict_in_runs) {
+        // k_pipe_runs (pipe_front) decodes the dictionary
+    } else if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
         // the dictionary (one workgroup) decodes on the side stream while the
         // run-table pass runs; k_pipe_codes waits for both (ev_join).  The
         // side stream first waits for everything already on the main stream
@@ -1669,7 +1680,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_plain_ba(s, P);
     } else if (pipe) {
         pqk::PipeLaunch P = pipe_launch(ctx, c, out);
-        pipe_front(ctx, c, P, true);
+        pipe_front(ctx, c, P, !dict_in_runs, dict_in_runs);
         if (c->ntiles == 0) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
             (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
@@ -2058,7 +2069,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             // dictionary-first on the decode's own codes: the pattern ran on
             // every entry above; the pipe passes give each row its index
             const pqk::PipeLaunch P = pipe_launch(ctx, c, nullptr);
-            pipe_front(ctx, c, P, false);
+            pipe_front(ctx, c, P, false, false);
             Timed t(ctx, "regex_codes");
             pqk::launch_pipe_match(s, P, c->d_dict_match + c->pipe_entry_base, neg, c->d_page_flags);
         } else if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {

@@ -24,6 +24,7 @@
 // non-null counts of the earlier tiles of their page (k_pipe_codes<true>).
 #include <cstddef>
 #include "kernels/device_common.hpp"
+#include "kernels/dict_index.hpp"
 #include "kernels/kernels.hpp"
 #include "kernels/lane_walk.hpp"
 #include "kernels/run_walk.hpp"
@@ -73,15 +74,34 @@ __device__ __forceinline__ uint32_t rr_lit(uint2 r) { return r.y >> 31; }
 __device__ __forceinline__ uint32_t rr_pay(uint2 r) { return r.y & 0x7FFFFFFFu; }
 
 
+// Dictionary pages decoded by k_pipe_runs' leading workgroups (ndicts = 0:
+// none; the dictionary then decodes in its own k_dict_index launch).
+struct RunDictArgs {
+    const DevDict* dicts;
+    int ndicts;
+    uint64_t* entries;
+    int32_t* dict_count;
+    DevErr* dict_err;
+    int32_t* err_any;
+};
+
 __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __restrict__ bytes,
                                                               const DevPage* __restrict__ pages, int npages,
                                                               int32_t max_def, int32_t max_rep,
                                                               uint2* __restrict__ runs,
                                                               uint32_t* __restrict__ info, int ppw,
-                                                              int32_t* __restrict__ flist, uint32_t stage_max) {
+                                                              int32_t* __restrict__ flist, uint32_t stage_max,
+                                                              RunDictArgs d) {
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[kRunWaves][kRunStage / 4 + 8];
+    if (static_cast<int>(blockIdx.x) < d.ndicts) {
+        // leading workgroups: the chunk's dictionary pages (dict_index.hpp),
+        // the page staged over this workgroup's payload windows
+        dict_index_block<kRunWaves>(bytes, d.dicts, static_cast<int>(blockIdx.x), d.entries, d.dict_count,
+                                    d.dict_err, d.err_any, static_cast<uint32_t>(sizeof(stage_all)), &stage_all[0][0]);
+        return;
+    }
     const uint32_t wv = threadIdx.x / kWave;
-    const int g0 = (blockIdx.x * kRunWaves + static_cast<int>(wv)) * ppw;
+    const int g0 = ((static_cast<int>(blockIdx.x) - d.ndicts) * kRunWaves + static_cast<int>(wv)) * ppw;
     if (g0 >= npages) return;
     const int g1 = min(npages, g0 + ppw);
     uint32_t* stage = stage_all[wv];
@@ -1658,13 +1678,17 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
-                      int) {
+                      int, const RunDicts* dicts) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
-    if (npages <= 0) return;
+    const int nd = dicts ? dicts->ndicts : 0;
+    if (npages <= 0 && nd <= 0) return;
     const int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
     const int per = kRunWaves * ppw;
-    hipLaunchKernelGGL(k_pipe_runs, dim3((npages + per - 1) / per), dim3(kRunWaves * kWave), 0, s, bytes, pages,
-                       npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16);
+    const RunDictArgs d = dicts ? RunDictArgs{dicts->dicts, nd, dicts->entries, dicts->dict_count, dicts->dict_err,
+                                              dicts->err_any}
+                                : RunDictArgs{nullptr, 0, nullptr, nullptr, nullptr, nullptr};
+    hipLaunchKernelGGL(k_pipe_runs, dim3(nd + (max(npages, 0) + per - 1) / per), dim3(kRunWaves * kWave), 0, s,
+                       bytes, pages, npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16, d);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's

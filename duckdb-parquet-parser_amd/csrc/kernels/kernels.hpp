@@ -167,8 +167,21 @@ struct PipePlan {
     int blocks_per_cu;  // 0: the dictionary does not fit
 };
 PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw);
+// Dictionary pages for k_pipe_runs' leading workgroups (4 waves each; pages
+// up to kRunDictMax bytes), so the dictionary decodes inside the run-table
+// launch instead of a k_dict_index launch on a side stream.
+struct RunDicts {
+    const DevDict* dicts;
+    int ndicts;
+    uint64_t* entries;
+    int32_t* dict_count;
+    DevErr* dict_err;
+    int32_t* err_any;
+};
+constexpr uint32_t kRunDictMax = 60 * 1024;
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
-                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist, int debug);
+                      int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist, int debug,
+                      const RunDicts* dicts = nullptr);
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,

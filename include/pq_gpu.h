@@ -144,6 +144,9 @@ int pq_ctx_sync(pq_ctx* ctx);
  *   "big_all"     1: every page of a pipe chunk takes the large-page kernel
  *                 (k_pipe_big; coverage of that kernel on small pages), 0 (default)
  *   "pipe_run_pages" pages per wavefront of the run-table pass, 1..32 (32)
+ *   "pipe_run_dict" 1 (default): dictionary pages up to 60 KiB decode in the
+ *                 run-table launch (its leading workgroups), else in their own
+ *                 launch on a side stream
  *   "plain_ba"    1 (default): two-pass PLAIN BYTE_ARRAY kernels
  *   "plain_fused" 1 (default): their one-pass form when every page's strings
  *                 fill it exactly (checked on the device; else the two passes)

@@ -13,7 +13,7 @@ import pytest
 
 import pqbuild as B
 from pqgpu import capi, gen
-from util import file_chunks, gpu_read_column, oracle_read_column
+from util import file_chunks, gpu_read_column, oracle_read_column, to_desc
 
 pytestmark = pytest.mark.gpu
 
@@ -89,6 +89,32 @@ def test_generated_columns(ctx, path, name, cols, n, layout):
         rc_g, msg_g, d_g = gpu_read_column(ctx, f, chunks)
         assert (rc_g, msg_g) == (rc_o, msg_o), (name, ci)
         assert d_g == d_o, (name, ci, len(d_g or b""), len(d_o or b""))
+
+
+@pytest.mark.parametrize("run_dict", [0, 1], ids=["side_stream", "in_runs"])
+@pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT], ids=["ref", "arrow"])
+@pytest.mark.parametrize("name,cols,n", [s for s in SMALL if s[0] in ("c2_dict", "c4_mixed", "long_dict", "mixed_dict")],
+                         ids=lambda v: v if isinstance(v, str) else "")
+def test_dict_decode_placement(ctx, run_dict, layout, name, cols, n):
+    """The pipe's dictionary page decoded by k_pipe_runs' leading workgroups
+    (pipe_run_dict=1, default) and by its own k_dict_index launch on the side
+    stream (0); three decodes per upload, each equal to the oracle."""
+    ctx.set_option("pipe_run_dict", run_dict)
+    try:
+        f = gen.build(cols, n, 2, seed=13, layout=layout, rows_per_page=3000)
+        for ci in range(len(cols)):
+            chunks = file_chunks(f, ci)
+            rc_o, _, d_o = oracle_read_column(f, chunks)
+            assert rc_o == 0
+            dc = ctx.upload(f, [to_desc(c) for c in chunks])
+            try:
+                for _ in range(3):
+                    dc.decode()
+                    assert capi.canonical_dump(dc.to_host()) == d_o, (name, ci)
+            finally:
+                dc.free()
+    finally:
+        ctx.set_option("pipe_run_dict", 1)
 
 
 @pytest.mark.parametrize("name,cols,n", [s for s in SMALL if s[0] in
