@@ -3,6 +3,7 @@
 // hybrid RLE/bit-packed stream per lane (rle_decoder.hpp:36-95), one run
 // record per step.
 #pragma once
+#include <type_traits>
 #include "kernels/device_common.hpp"
 #include "kernels/lane_walk.hpp"
 
@@ -43,14 +44,16 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
     };
     uint32_t x0, x1;
     load(q, alive, x0, x1);
-    // branch-free step: every quantity is computed, one predicated store
-    while (__ballot(alive)) {
+    // branch-free step: every quantity is computed, one predicated store.
+    // kOne: every live header is one byte (runs of < 64 values or groups:
+    // what both writers emit for these pages), so the varint parse, the
+    // header-length selects and the 2^16 group clamp fold away.
+    auto step = [&](auto one) {
+        constexpr bool kOne = decltype(one)::value;
         const uint32_t exh = q >= W.end ? 1u : 0u;  // rest of the batch is 0 (rle_decoder.hpp:20-23)
-        // varint header (76-86): at most 5 bytes, inside the stream.  When
-        // every live header is one byte (runs of < 64 values or groups: what
-        // both writers emit for these pages) the general parse is skipped.
+        // varint header (76-86): at most 5 bytes, inside the stream
         uint32_t hl, ind;
-        if (__ballot(alive && !exh && (x0 & 0x80u)) == 0) {
+        if constexpr (kOne) {
             hl = 1;
             ind = x0 & 0x7Fu;
         } else {
@@ -71,7 +74,7 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
         const uint32_t cr = min(g, left);
         const uint32_t c = lit ? cl : cr;
         // zero-count runs (counter wrap / stale literal cursor), truncated headers or values
-        const uint32_t badh = (hl > 5 ? 1u : 0u) | (qh > W.end ? 1u : 0u) | (g == 0 ? 1u : 0u) |
+        const uint32_t badh = (!kOne && hl > 5 ? 1u : 0u) | (qh > W.end ? 1u : 0u) | (g == 0 ? 1u : 0u) |
                               ((lit ^ 1u) & (qh + nbv > W.end ? 1u : 0u));
         const uint32_t full = nr >= W.cap ? 1u : 0u;
         const uint32_t ok = (alive ? 1u : 0u) & (full ^ 1u) & (exh | (badh ^ 1u));
@@ -79,7 +82,7 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
         const uint32_t litm = 0u - lit;
         // g clamps at 2^16: a longer literal run overruns the stream (<= 64 KiB) either way
         // (24-bit multiplies: g <= 2^16, bw <= 32)
-        const uint32_t nqlc = min(__umul24(min(g, 0x10000u), W.bw) + qh, W.end);
+        const uint32_t nqlc = min(__umul24(kOne ? g : min(g, 0x10000u), W.bw) + qh, W.end);
         const uint32_t nq = (litm & nqlc) | (~litm & (qh + nbv));
         const uint32_t ncnt = exh ? W.n : cnt + c;
         const uint32_t qn = (ok & (exh ^ 1u)) ? nq : q;
@@ -87,9 +90,14 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
         uint32_t y0, y1;
         load(qn, an, y0, y1);
         const uint32_t rx = cnt | ((exh ? left : c) << 16);
-        const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, hl);
-        const uint32_t vb = x1 >> (8 * ((hl - 4) & 3));
-        const uint32_t vraw = (hl < 4) ? va : vb;
+        uint32_t vraw;
+        if constexpr (kOne) {
+            vraw = x0 >> 8;  // the RLE value's (<= 2) bytes after the header
+        } else {
+            const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, hl);
+            const uint32_t vb = x1 >> (8 * ((hl - 4) & 3));
+            vraw = (hl < 4) ? va : vb;
+        }
         const uint32_t pl = (litm & (litpay | ((qh << 3) & litsh))) | (~litm & vraw & vmask);
         const uint32_t ry = exh ? 0u : pl;
         if (ok) W.out[nr] = make_uint2(rx, ry);
@@ -100,6 +108,10 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
         alive = an;
         x0 = y0;
         x1 = y1;
+    };
+    while (__ballot(alive)) {
+        if (__ballot(alive && q < W.end && (x0 & 0x80u)) == 0) step(std::true_type{});
+        else step(std::false_type{});
     }
     nrec = nr;
     flag = fl;
