@@ -105,16 +105,22 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
     if (g0 >= npages) return;
     const int g1 = min(npages, g0 + ppw);
     uint32_t* stage = stage_all[wv];
-    const uint64_t wlo = pages[g0].off;
-    const DevPage lastp = pages[g1 - 1];
-    const uint64_t whi = lastp.off + static_cast<uint32_t>(max(lastp.size, 0));
+    // one load of the group's page records (lane 2i, 2i + 1: page g0 + i;
+    // lanes past the group re-read its last page): the window bounds and the
+    // inside test come from it, and so does each lane's own page below
+    const uint32_t gl = static_cast<uint32_t>(g1 - 1 - g0);
+    const DevPage mine = pages[g0 + static_cast<int>(min(lane() >> 1, gl))];
+    auto rl64 = [](uint64_t v, uint32_t i) -> uint64_t {
+        return (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), i)) << 32) |
+               __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
+    };
+    const uint64_t wlo = rl64(mine.off, 0);
+    const uint64_t whi = rl64(mine.off, 2 * gl) +
+                         static_cast<uint32_t>(max(static_cast<int32_t>(__builtin_amdgcn_readlane(
+                                                       static_cast<uint32_t>(mine.size), 2 * gl)), 0));
     bool staged = whi >= wlo && whi - wlo <= kRunStage;
     if (staged) {  // every page of the group inside the window (image order)
-        bool inside = true;
-        for (int q = g0 + static_cast<int>(lane()); q < g1; q += kWave) {
-            const DevPage pq = pages[q];
-            inside &= pq.off >= wlo && pq.off + static_cast<uint32_t>(max(pq.size, 0)) <= whi;
-        }
+        const bool inside = mine.off >= wlo && mine.off + static_cast<uint32_t>(max(mine.size, 0)) <= whi;
         staged = __ballot(!inside) == 0;
     }
     if (staged) {  // payload slots are 16-byte aligned with >= 16 zero bytes after each
@@ -128,11 +134,11 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
 
     const uint32_t s = lane() & 1;
     const int p = g0 + static_cast<int>(lane() >> 1);
-    const bool act = p < g1 && static_cast<int>(lane() >> 1) < ppw && pages[p].nvals <= kPipeSmallRows;
+    const bool act = p < g1 && static_cast<int>(lane() >> 1) < ppw && mine.nvals <= kPipeSmallRows;
     uint32_t flag = 0, nrec = 0, bwi = 0;
     RunWalk W{};
     if (act) {
-        const DevPage pg = pages[p];
+        const DevPage pg = mine;
         const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
         const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
         const uint32_t sbase = static_cast<uint32_t>(pg.off - wlo);
