@@ -528,3 +528,32 @@ def test_set_option_rejects(ctx, key, value):
 def to_desc_(chunk):
     from util import to_desc
     return chunk if isinstance(chunk, capi.ChunkDesc) else to_desc(chunk)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT], ids=["ref", "arrow"])
+def test_row_groups_over_two_contexts(ctx, layout):
+    """Row groups alternated over two contexts (two HIP streams, as bench.py's
+    C5 leg runs them): after one sizing decode, rounds of decodes queued on
+    both streams before any check; every row group then equals the oracle."""
+    cols = gen.c2_cols()
+    f = gen.build(cols, 30000, 4, seed=17, layout=layout, rows_per_page=20000)
+    chunks = file_chunks(f, 0)
+    ctx2 = capi.Context(0)
+    try:
+        dcs = [(ctx if i % 2 == 0 else ctx2).upload(f, [to_desc(c)]) for i, c in enumerate(chunks)]
+        for dc in dcs:  # sizes the outputs (decode_check does not fill the column record)
+            dc.decode()
+        for _ in range(3):
+            for dc in dcs:
+                dc.decode_async()
+            for dc in dcs:
+                dc.decode_check()
+        for c, dc in zip(chunks, dcs):
+            rc_o, _, d_o = oracle_read_column(f, [c])
+            assert rc_o == 0
+            assert capi.canonical_dump(dc.to_host()) == d_o
+        for dc in dcs:
+            dc.free()
+    finally:
+        ctx2.close()
