@@ -79,6 +79,7 @@ struct pq_ctx {
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
     bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
+    bool opt_front = false;      // "pipe_front": windowed one-wave front (k_pipe_front) where the pages allow it
     int opt_stage_bufs = 6;      // "stage_bufs" / "stage_piece_kb": pinned upload ring (stage.hpp)
 };
 
@@ -130,6 +131,9 @@ struct pq_chunk {
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
     bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
+    bool pipe_fr = false;               // every page <= kTileRows rows, every slot <= kFrontWin: k_pipe_front
+    std::vector<pqk::DevBatch> hfwins;  // its windows of consecutive pages
+    pqk::DevBatch* d_fwins = nullptr;
     int pipe_wpw = 10;                  // k_pipe_write writer waves per workgroup (planned)
     std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
     int32_t* d_bigp = nullptr;
@@ -255,6 +259,20 @@ int hip_check(pq_ctx* ctx, hipError_t e, const char* what) {
     return set_err(ctx, PQ_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Every entry point that touches the GPU runs on its context's device: a host
+// thread may drive contexts on several devices, and HIP's
+// current device is per thread.  Restores the caller's device on return.
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(const pq_ctx* c) {
+        int cur = 0;
+        if (c && hipGetDevice(&cur) == hipSuccess && cur != c->device && hipSetDevice(c->device) == hipSuccess) prev = cur;
+    }
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 int plain_width_of(int32_t type) {
     switch (type) {
         case PQ_BOOLEAN: return 1;
@@ -365,6 +383,7 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_bsum);
     dfree(c->d_flist);
     dfree(c->d_bigp);
+    dfree(c->d_fwins);
     dfree(c->d_chunk_base);
     dfree(c->d_chunks);
     dfree(c->d_cand);
@@ -392,13 +411,15 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->pipe = false;
     c->pipe_count = false;
     c->pipe_small = false;
+    c->pipe_fr = false;
+    c->hfwins.clear();
     c->hbig.clear();
     c->big_max_bytes = 0;
     if (c->type != PQ_BYTE_ARRAY || c->max_def > 254 || c->max_def < 0 || c->max_rep < 0 || pages.empty()) return;
     int32_t dict_id = -1;
     bool multi = false, small = false;
     std::vector<int32_t> big;
-    uint32_t big_bytes = 0;
+    uint32_t big_bytes = 0, small_bytes = 0;
     for (size_t i = 0; i < pages.size(); i++) {
         const DevPage& pg = pages[i];
         if (pg.mode != pqk::MODE_DICT || pg.size > (1 << 27) || pg.size < 0) return;
@@ -410,6 +431,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
         } else {
             small = true;
             multi |= pg.nvals > pqk::kTileRows;
+            small_bytes = std::max(small_bytes, static_cast<uint32_t>(pg.size));
         }
         if (dict_id >= 0 && pg.dict != dict_id) return;
         dict_id = pg.dict;
@@ -439,6 +461,34 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->pipe_ecap = static_cast<uint32_t>(ecap);
     c->pipe_cus = cus;
     c->pipe_wpw = wpw;
+    // windows of consecutive pages for the whole front in one wavefront each (k_pipe_front)
+    c->hfwins.clear();
+    c->pipe_fr = small && !multi && c->hbig.empty() && pqk::pipe_front_slot(small_bytes) <= pqk::kFrontWin;
+    if (c->pipe_fr) {
+        size_t p = 0;
+        while (p < pages.size()) {
+            pqk::DevBatch b{};
+            b.p0 = static_cast<int32_t>(p);
+            b.img_lo = pages[p].off;
+            uint64_t hi = b.img_lo;
+            size_t q = p;
+            while (q < pages.size() && q - p < pqk::pipe_front_win_pages() && pages[q].off >= b.img_lo) {
+                const uint64_t e = pages[q].off + pqk::pipe_front_slot(static_cast<uint32_t>(std::max(pages[q].size, 0)));
+                if (e - b.img_lo > pqk::kFrontWin || (q > p && pages[q].off != hi)) break;  // contiguous slots only
+                hi = e;
+                q++;
+            }
+            if (q == p) {  // (slots are contiguous and <= kFrontWin: unreachable)
+                c->pipe_fr = false;
+                c->hfwins.clear();
+                break;
+            }
+            b.np = static_cast<int32_t>(q - p);
+            b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
+            c->hfwins.push_back(b);
+            p = q;
+        }
+    }
 }
 
 // PLAIN BYTE_ARRAY chunks without levels go through plain_ba.hip: windows of
@@ -669,6 +719,7 @@ void pq_ctx_destroy(pq_ctx* ctx) {
 
 int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (!ctx || !key) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
     if (std::strcmp(key, "fused_ba") == 0) { ctx->opt_fused = value != 0; return 0; }
     if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "fused_waves") == 0) { ctx->opt_waves = static_cast<int>(value); return 0; }
@@ -693,6 +744,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
     if (std::strcmp(key, "plain_fused") == 0) { ctx->opt_plain_fused = value != 0; return 0; }
     if (std::strcmp(key, "pipe_run_dict") == 0) { ctx->opt_run_dict = value != 0; return 0; }
+    if (std::strcmp(key, "pipe_front") == 0) { ctx->opt_front = value != 0; return 0; }
     if (std::strcmp(key, "pipe_run_pages") == 0) {
         if (value < 1 || value > 32) return set_err(ctx, PQ_ERR_ARG, "pipe_run_pages: 1..32");
         ctx->opt_run_pages = static_cast<int>(value);
@@ -738,6 +790,7 @@ const char* pq_last_error(const pq_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 void* pq_ctx_stream(pq_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
 int pq_ctx_sync(pq_ctx* ctx) {
     if (!ctx) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
     return hip_check(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
 }
 
@@ -802,6 +855,7 @@ static void raw_start(pq_ctx* ctx, const uint8_t* file, size_t file_len, RawStag
     R.active = true;
     const int hw = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
     R.th = std::thread([ctx, file, &R, hw]() {
+        (void)hipSetDevice(ctx->device);  // a new host thread starts on device 0
         auto fill = [&](uint8_t* dst, size_t a, size_t z) {
             // extents overlapping [a, z) of d_raw
             size_t k = static_cast<size_t>(std::upper_bound(R.base.begin(), R.base.end(), static_cast<int64_t>(a)) -
@@ -1058,6 +1112,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) + 64);
             rc |= dalloc(&c->d_tile_nn, htiles.size());
             if (!c->hbig.empty()) rc |= dalloc(&c->d_bigp, c->hbig.size());
+            if (!c->hfwins.empty()) rc |= dalloc(&c->d_fwins, c->hfwins.size());
         }
         if (c->plain) {
             rc |= dalloc(&c->d_pwins, c->hpwins.size());
@@ -1254,8 +1309,14 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                                                        }),
                                "upload");
             if (!rc) {
+                // every status word starts non-OK: an entry the pass never
+                // reached (a failed launch) cannot read as a clean decode
+                rc = hip_check(ctx, hipMemsetAsync(ctx->d_codec_st, 0xFF, n * sizeof(uint32_t), s), "codec status");
+            }
+            if (!rc) {
                 Timed ct(ctx, "codec", s);
                 pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus);
+                rc = hip_check(ctx, hipGetLastError(), "codec launch");
             }
         }
         if (ctx->timing) {
@@ -1291,6 +1352,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             if (!rc) (void)hipMemsetAsync(c->d_perr, 0, c->hchunks.size() * sizeof(DevErr), s);
         }
         if (c->d_bigp) put(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t));
+        if (c->d_fwins) put(c->d_fwins, c->hfwins.data(), c->hfwins.size() * sizeof(pqk::DevBatch));
         if (c->d_pwins) put(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch));
         if (c->d_pwbase) put(c->d_pwbase, c->hpwbase.data(), c->hpwbase.size() * sizeof(int64_t));
         if (c->d_pwpage) put(c->d_pwpage, c->hpwpage.data(), c->hpwpage.size() * sizeof(int32_t));
@@ -1302,10 +1364,10 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             for (size_t k = 0; k < st.size() && !rc; k++) {
                 if (!st[k]) continue;
                 static const char* what[] = {"", "corrupt compressed data", "decompressed size differs from the page header",
-                                             "unsupported codec"};
+                                             "unsupported codec", "decompression pass did not run"};
                 rc = set_err(ctx, PQ_ERR_DECOMPRESS,
                              "page at file offset " + std::to_string(cent_file[k]) + " (codec " +
-                                 std::to_string(cents[k].codec) + "): " + what[std::min<uint32_t>(st[k], 3)]);
+                                 std::to_string(cents[k].codec) + "): " + what[std::min<uint32_t>(st[k], 4)]);
             }
         }
         if (rc) {
@@ -1337,6 +1399,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
 int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc* chunks,
                     int nchunks, pq_chunk** out) {
     if (!ctx || !file || !chunks || nchunks <= 0 || !out) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
     *out = nullptr;
     try {
         // the chunks' page walks are independent: host threads
@@ -1369,6 +1432,7 @@ int pq_chunk_upload_range(pq_ctx* ctx, const uint8_t* file, size_t file_len, con
     if (!ctx || !file || !chunk || (!table && ntable) || ntable < 0 || !out || data_begin < 0 ||
         data_end < data_begin)
         return PQ_ERR_ARG;
+    DevGuard dg(ctx);
     *out = nullptr;
     try {
         // the data pages of the range, in walk order, and the dictionary pages they use
@@ -1423,6 +1487,7 @@ int pq_chunk_upload_range(pq_ctx* ctx, const uint8_t* file, size_t file_len, con
 
 void pq_chunk_free(pq_ctx* ctx, pq_chunk* c) {
     if (!c) return;
+    DevGuard dg(ctx);
     if (ctx) (void)hipStreamSynchronize(ctx->stream);
     free_chunk_device(c);
     delete c;
@@ -1507,8 +1572,15 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
 // With dict_in_runs the dictionary pages decode in k_pipe_runs' leading
 // workgroups (same launch, main stream: ordered after the previous decode's
 // readers of the entry table, no side-stream events).
+static bool front_path(pq_ctx* ctx, const pq_chunk* c) { return c->pipe_fr && c->d_fwins && ctx->opt_front; }
+
 static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs) {
     hipStream_t s = ctx->stream;
+    if (front_path(ctx, c)) {  // the dictionary decoded before (main stream)
+        Timed t(ctx, "pipe_front");
+        pqk::launch_pipe_front(s, P, c->d_fwins, static_cast<int>(c->hfwins.size()), pqk::kFrontWin);
+        return;
+    }
     {
         Timed t(ctx, "pipe_runs");
         const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
@@ -1533,6 +1605,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out);
 
 int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (!ctx || !c || !out) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
     if (c->type == PQ_BYTE_ARRAY) {
         int64_t cap = std::max<int64_t>(out->capacity_bytes, c->char_estimate);
         if (int rc = ensure_output(ctx, c, out, cap)) return rc;
@@ -1570,11 +1643,12 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (!(pipe_path && c->tiles_aligned32))
         (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
     // dictionary pages small enough for k_pipe_runs' workgroups decode there
-    const bool dict_in_runs = pipe && !plain_go && ctx->opt_run_dict && c->ndicts && c->type == PQ_BYTE_ARRAY &&
+    const bool front = pipe && !plain_go && front_path(ctx, c);
+    const bool dict_in_runs = pipe && !plain_go && !front && ctx->opt_run_dict && c->ndicts && c->type == PQ_BYTE_ARRAY &&
                               c->d_dflag && c->max_dict_bytes <= pqk::kRunDictMax;
     if (dict_in_runs) {
         // k_pipe_runs (pipe_front) decodes the dictionary
-    } else if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
+    } else if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe && !front) {
         // the dictionary (one workgroup) decodes on the side stream while the
         // run-table pass runs; k_pipe_codes waits for both (ev_join).  The
         // side stream first waits for everything already on the main stream
@@ -1680,7 +1754,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_plain_ba(s, P);
     } else if (pipe) {
         pqk::PipeLaunch P = pipe_launch(ctx, c, out);
-        pipe_front(ctx, c, P, !dict_in_runs, dict_in_runs);
+        pipe_front(ctx, c, P, !dict_in_runs && !front, dict_in_runs);
         if (c->ntiles == 0) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
             (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
@@ -1871,9 +1945,14 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     return 0;
 }
 
-int pq_decode_check(pq_ctx* ctx, pq_chunk* c) { return (!ctx || !c) ? PQ_ERR_ARG : collect(ctx, c, nullptr); }
+int pq_decode_check(pq_ctx* ctx, pq_chunk* c) {
+    if (!ctx || !c) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
+    return collect(ctx, c, nullptr);
+}
 
 int pq_decode(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
+    DevGuard dg(ctx);
     if (int rc = pq_decode_async(ctx, c, out)) return rc;
     return collect(ctx, c, out);
 }
@@ -1881,6 +1960,7 @@ int pq_decode(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
 int pq_column_copy_out(pq_ctx* ctx, const pq_column* col, uint32_t* validity, uint8_t* values,
                        int64_t* offsets) {
     if (!ctx || !col) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
     hipStream_t s = ctx->stream;
     int rc = 0;
     if (validity && col->num_rows)
@@ -1896,6 +1976,7 @@ int pq_column_copy_out(pq_ctx* ctx, const pq_column* col, uint32_t* validity, ui
 int pq_chunk_assign(pq_ctx* ctx, const pq_column* col, int64_t chunk_bytes, int64_t* d_tuple_to_chunk,
                     int64_t* h_tuple_to_chunk, int64_t* num_chunks) {
     if (!ctx || !col || !num_chunks || chunk_bytes < 0) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
     if (col->type != PQ_BYTE_ARRAY || (col->num_rows > 0 && (!col->d_validity || !col->d_offsets)))
         return set_err(ctx, PQ_ERR_ARG, "pq_chunk_assign: a decoded BYTE_ARRAY column is required");
     (void)hipSetDevice(ctx->device);
@@ -1920,6 +2001,7 @@ int pq_chunk_assign(pq_ctx* ctx, const pq_column* col, int64_t chunk_bytes, int6
 }
 
 void pq_column_free(pq_ctx* ctx, pq_column* col) {
+    DevGuard dg(ctx);
     if (!col) return;
     if (ctx) (void)hipStreamSynchronize(ctx->stream);
     dfree(col->d_validity);
@@ -1931,11 +2013,13 @@ void pq_column_free(pq_ctx* ctx, pq_column* col) {
 void pq_timing_enable(pq_ctx* ctx, int enable) { if (ctx) ctx->timing = enable != 0; }
 void pq_timing_reset(pq_ctx* ctx) {
     if (!ctx) return;
+    DevGuard dg(ctx);
     resolve_timers(ctx);
     ctx->timers.clear();
 }
 int pq_timing_get(pq_ctx* ctx, const char* name, double* total_ms, int64_t* launches) {
     if (!ctx || !name) return 0;
+    DevGuard dg(ctx);
     resolve_timers(ctx);
     auto it = ctx->timers.find(name);
     if (it == ctx->timers.end()) return 0;
@@ -1946,6 +2030,7 @@ int pq_timing_get(pq_ctx* ctx, const char* name, double* total_ms, int64_t* laun
 
 int pq_fused_prof_read(pq_ctx* ctx, uint64_t* out, int n) {
     if (!ctx || !ctx->d_prof) return 0;
+    DevGuard dg(ctx);
     const int k = pqk::fused_prof_slots();
     std::vector<uint64_t> h(static_cast<size_t>(k));
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) return 0;
@@ -2018,6 +2103,7 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
 
 int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg) {
     if (!ctx || !c || !pattern) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
     if (c->type != PQ_BYTE_ARRAY) return set_err(ctx, PQ_ERR_ARG, "regex page filter needs a BYTE_ARRAY column");
     try {
         std::string msg;
@@ -2098,6 +2184,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
 
 int pq_regex_pages_result(pq_ctx* ctx, pq_chunk* c, uint8_t* page_flags) {
     if (!ctx || !c) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
     if (int rc = collect(ctx, c, nullptr)) return rc;
     if (page_flags && c->npages)
         return hip_check(ctx, hipMemcpy(page_flags, c->d_page_flags, static_cast<size_t>(c->npages), hipMemcpyDeviceToHost), "copy page flags");
@@ -2105,6 +2192,7 @@ int pq_regex_pages_result(pq_ctx* ctx, pq_chunk* c, uint8_t* page_flags) {
 }
 
 int pq_regex_pages(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg, uint8_t* page_flags) {
+    DevGuard dg(ctx);
     if (int rc = pq_regex_pages_async(ctx, c, pattern, neg)) return rc;
     return pq_regex_pages_result(ctx, c, page_flags);
 }

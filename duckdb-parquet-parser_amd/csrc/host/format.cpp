@@ -267,6 +267,10 @@ PageHeader read_page_header(const uint8_t* file, size_t len, size_t off) {  // m
                 break;
             }
             case 8: {  // DataPageHeaderV2 (parquet.thrift; skipped by the reference)
+                if (ty != 12) {  // not a struct: skipped by its wire type, as the reference does
+                    t.skip(ty);
+                    break;
+                }
                 t.push();
                 h.has_v2 = true;
                 int16_t i2; uint8_t t2;
@@ -353,6 +357,10 @@ public:
                     break;
                 }
                 case 8: {  // DataPageHeaderV2
+                    if (ty != 12) {  // not a struct: skipped by its wire type (metadata.cpp:149-151)
+                        if (!skip(ty, 0)) return false;
+                        break;
+                    }
                     h.has_v2 = true;
                     int16_t l2 = 0;
                     for (;;) {

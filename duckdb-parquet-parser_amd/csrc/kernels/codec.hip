@@ -58,6 +58,7 @@ struct CodecLds {
     uint8_t lens[320];        // code lengths: litlen [0, 288), dist [288, 320)
     uint16_t nxt[16], offs[16];  // build_code: next code / next symbol slot per length
     uint32_t scratch[4];
+    uint32_t crc_tab[256];    // CRC-32 (gzip trailers): byte table
 };
 
 // LDS pointers keep their address space (a generic pointer held in a struct
@@ -130,6 +131,30 @@ struct In {
 
 enum : uint32_t { ST_OK = 0, ST_CORRUPT = 1, ST_SIZE = 2, ST_UNSUPPORTED = 3 };
 
+// ── CRC-32 of GZIP members (RFC 1952; reflected polynomial 0xEDB88320) ─────
+constexpr uint32_t kCrcPoly = 0xEDB88320u;
+// a(x) * b(x) mod P(x) in the reflected representation (zlib's multmodp),
+// branch-free: 32 steps
+__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int k = 31; k >= 0; k--) {
+        p ^= (0u - ((a >> k) & 1u)) & b;
+        b = (b >> 1) ^ ((0u - (b & 1u)) & kCrcPoly);
+    }
+    return p;
+}
+// x^(8 * nbytes) mod P (x2nmodp(nbytes, 3)): the shift crc32_combine applies
+__device__ __forceinline__ uint32_t crc_xpow8(uint32_t nbytes) {
+    uint32_t p = 1u << 31, sq = 1u << 23;  // x^0; x^(8 * 2^0) = x^8
+    while (nbytes) {
+        if (nbytes & 1u) p = crc_mulmod(sq, p);
+        sq = crc_mulmod(sq, sq);
+        nbytes >>= 1;
+    }
+    return p;
+}
+
 // ── output ring ────────────────────────────────────────────────────────────
 struct Out {
     lds8* ring;
@@ -139,9 +164,44 @@ struct Out {
     uint32_t cap;   // bytes the slot's payload holds
     uint32_t vbase; // first byte of the decompressed stream (after a V2 prologue)
     uint32_t st;    // ST_*
+    // running CRC-32 of the output since crc_pos0 (GZIP members): bytes
+    // [crc_pos0, crc_pos) are in `crc` (finalized form); they are folded in
+    // from the ring before it can be overwritten (at every flush)
+    bool crc_on = false;
+    uint32_t crc = 0, crc_pos = 0;
+    const lds32* crc_tab = nullptr;
+    __device__ void crc_upto(uint32_t to) {
+        if (!crc_on || to <= crc_pos) return;
+        const uint32_t len = uni(to - crc_pos), s = len / kWave;  // 64 segments of s bytes, then a tail
+        if (s) {
+            uint32_t c = 0xFFFFFFFFu;
+            const uint32_t b0 = crc_pos + lane() * s;
+            for (uint32_t j = 0; j < s; j++) c = crc_tab[(c ^ ring[(b0 + j) & kRingMask]) & 0xFFu] ^ (c >> 8);
+            c = ~c;
+            // tree of crc32_combine over the lanes: round r joins lanes i, i + 2^r
+            uint32_t pw = crc_xpow8(s);  // shift by 2^r segments
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                const uint32_t other = static_cast<uint32_t>(__shfl_down(static_cast<int>(c), 1 << r));
+                const uint32_t joined = crc_mulmod(c, pw) ^ other;
+                c = (lane() & ((2u << r) - 1u)) == 0 ? joined : c;
+                pw = crc_mulmod(pw, pw);
+            }
+            // pw: shift by 64 segments; fold the block (lane 0) into the running value
+            crc = uni(crc_mulmod(crc, pw) ^ static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c)));
+            crc_pos += kWave * s;
+        }
+        if (crc_pos < to) {  // the tail (< 64 bytes): lane 0, byte by byte
+            uint32_t c = ~crc;
+            for (uint32_t q = crc_pos; q < to; q++) c = crc_tab[(c ^ ring[q & kRingMask]) & 0xFFu] ^ (c >> 8);
+            crc = uni(~c);
+            crc_pos = to;
+        }
+    }
     __device__ __forceinline__ void flush(bool final) {
         while (op - fl >= kFlush || (final && fl < op)) {
             const uint32_t n = min(kFlush, op - fl);
+            crc_upto(fl + n);
             const uint32_t b = fl + 16u * lane();
             if (b < fl + n) {
                 uint4 v = lds_get16(ring, b & kRingMask);
@@ -475,9 +535,10 @@ __device__ __forceinline__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
                     const int32_t sy = decode_sym(L, I, B, L.dt, 1, 288);
                     uint32_t rep = 1, val = 0;
                     if (sy < 0) { O.st = ST_CORRUPT; return; }
+                    // code 16 repeats the last length WRITTEN, zeros of a 17/18 run
+                    // included (RFC 1951 3.2.7; zlib's lens[have - 1])
                     if (sy < 16) {
                         val = static_cast<uint32_t>(sy);
-                        prev = val;
                     } else if (sy == 16) {
                         if (i == 0) { O.st = ST_CORRUPT; return; }
                         val = prev;
@@ -487,6 +548,7 @@ __device__ __forceinline__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
                     } else {
                         rep = 11 + B.take(I, 7);
                     }
+                    prev = val;
                     if (i + rep > nl + nd) { O.st = ST_CORRUPT; return; }
                     // lengths i .. i + rep: litlen [0, nl) -> lens[0 ..], dist -> lens[288 ..] (after the
                     // code-length table is no longer needed: written into a staging copy first)
@@ -579,6 +641,9 @@ __device__ __forceinline__ void gzip(CodecLds& L, In& I, Out& O, uint32_t p, uin
         }
         if (p > end) { O.st = ST_CORRUPT; return; }
         Bits B{0ull, 0u, p, end, 0u};
+        O.crc_on = !zlib;  // zlib streams end in an Adler-32 (not checked)
+        O.crc = 0;
+        O.crc_pos = O.op;
         inflate(L, I, O, B);
         if (O.st != ST_OK) return;
         p = B.align_byte();
@@ -587,6 +652,9 @@ __device__ __forceinline__ void gzip(CodecLds& L, In& I, Out& O, uint32_t p, uin
         if (!zlib) {
             I.ensure(p, 8);
             if (I.u32le(p + 4) != O.op - o0) { O.st = ST_SIZE; return; }
+            O.crc_upto(O.op);  // the member's last bytes (still in the ring)
+            if (I.u32le(p) != O.crc) { O.st = ST_CORRUPT; return; }
+            O.crc_on = false;
         }
         p += tail;
         first = false;
@@ -601,11 +669,19 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
     CodecLds& L = *reinterpret_cast<CodecLds*>(smem);
     lds8* lring = (lds8*)(smem + offsetof(CodecLds, ring));
     lds8* lin = (lds8*)(smem + offsetof(CodecLds, in));
+    lds32* lcrc = (lds32*)(smem + offsetof(CodecLds, crc_tab));
+    for (uint32_t b = lane(); b < 256; b += kWave) {  // CRC-32 byte table
+        uint32_t c = b;
+        for (int k = 0; k < 8; k++) c = (c >> 1) ^ ((0u - (c & 1u)) & kCrcPoly);
+        lcrc[b] = c;
+    }
+    wsync();
     for (int32_t i = static_cast<int32_t>(blockIdx.x); i < n; i += static_cast<int32_t>(gridDim.x)) {
         const CodecEntry e = ent[i];
         In I{src + e.src, e.src_len, 0u, 0u, lin};
         I.refill(0);
         Out O{lring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
+        O.crc_tab = lcrc;
         uint32_t p = 0;
         if (e.flags & kCodecV2) {  // level sections, as is, behind their V1 length prefixes
             const uint32_t lv = e.def_len + e.rep_len;
@@ -650,12 +726,7 @@ void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEn
                   uint32_t* status, int cus) {
     if (n <= 0) return;
     const uint32_t lds = static_cast<uint32_t>(sizeof(CodecLds));
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_codec), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(lds));
-        attr = true;
-    }
+    ensure_dyn_lds(reinterpret_cast<const void*>(k_codec), lds);
     const int per_cu = std::max(1, static_cast<int>((160u * 1024u) / lds));
     const int grid = std::min(n, std::max(1, cus) * per_cu);
     hipLaunchKernelGGL(k_codec, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);

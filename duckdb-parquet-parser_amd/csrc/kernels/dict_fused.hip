@@ -738,12 +738,7 @@ void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts
                        uint32_t max_dict_bytes) {
     if (ndicts <= 0) return;
     constexpr uint32_t kCap = 128 * 1024;  // + 18.2 KiB static tables < 160 KiB
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_dict_index),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kCap);
-        attr = true;
-    }
+    ensure_dyn_lds(reinterpret_cast<const void*>(k_dict_index), kCap);
     uint32_t lds = std::min<uint32_t>(kCap, (max_dict_bytes + 15) / 16 * 16 + 32);
     hipLaunchKernelGGL(k_dict_index, dim3(ndicts), dim3(kDictWaves * kWave), lds, s, bytes, dicts, entries,
                        dict_count, dict_err, err_any, lds);
@@ -751,13 +746,8 @@ void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts
 
 namespace {
 void set_fused_attrs() {
-    static bool attr = false;
-    if (attr) return;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ba_fused<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ba_fused<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
+    ensure_dyn_lds(reinterpret_cast<const void*>(k_ba_fused<false>), 160 * 1024);
+    ensure_dyn_lds(reinterpret_cast<const void*>(k_ba_fused<true>), 160 * 1024);
 }
 }  // namespace
 

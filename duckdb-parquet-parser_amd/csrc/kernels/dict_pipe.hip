@@ -244,7 +244,9 @@ __device__ void fail_page(const CodeArgs& a, const DevPage& pg, int32_t t0, uint
 
 // Exact decoder for a marked page: the reference state machine (stream.hpp)
 // over the page in HBM, tile by tile; same error order as k_ba_fused.
-__device__ void exact_page(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n, uint32_t ebase) {
+// (the body is inlined where the scratch is a dynamic per-wave LDS area —
+// a call would pass it as a generic pointer — and called elsewhere)
+__device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n, uint32_t ebase) {
     const DevPage pg = a.pages[p];
     const uint8_t* page = a.bytes + pg.off;
     const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
@@ -353,6 +355,10 @@ __device__ void exact_page(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n
     }
 }
 
+__device__ __noinline__ void exact_page(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n, uint32_t ebase) {
+    exact_page_body(a, L, p, dict_n, ebase);
+}
+
 // The run covering value `v` among `nr` records held two per lane in LDS:
 // (number of starts <= v) - 1.
 __device__ __forceinline__ uint32_t run_at(const uint2* rec, uint32_t nr, uint32_t v) {
@@ -375,7 +381,7 @@ __global__ void __launch_bounds__(kCodeWaves * 64) k_pipe_codes(CodeArgs a) {
     const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
     if (inf & kBig) return;
     if (inf & kFallback) {
-        if (!kCount && T.row0 == 0) exact_page(a, L, p, dict_n, ebase);
+        if (!kCount && T.row0 == 0) exact_page_body(a, L, p, dict_n, ebase);
         return;
     }
     const DevPage pg = a.pages[p];
@@ -783,7 +789,7 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
     // the exact serial decoder, one wave per page
     const int nf = flist[0];
     for (int i = static_cast<int>(blockIdx.x) * kCodeWaves3 + wv; i < nf; i += nw) {
-        exact_page(a, LX, flist[1 + i], dict_n, ebase);
+        exact_page_body(a, LX, flist[1 + i], dict_n, ebase);
         __builtin_amdgcn_wave_barrier();
     }
     // a dictionary longer than the length table (not planned: lt_n covers
@@ -791,7 +797,7 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
     if (!lean) {
         for (int t = ta; t < tb; t++) {
             const DevTile T = a.tiles[t];
-            if (T.row0 == 0 && !(a.info[T.page] & kSkip)) exact_page(a, LX, T.page, dict_n, ebase);
+            if (T.row0 == 0 && !(a.info[T.page] & kSkip)) exact_page_body(a, LX, T.page, dict_n, ebase);
             __builtin_amdgcn_wave_barrier();
         }
     }
@@ -1353,7 +1359,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     // so no further launch is needed after the big pages
     auto to_exact = [&]() {
         if (tid == 0) info[p] = kFallback;
-        if (wv == 0) exact_page(a, *reinterpret_cast<CodeLds*>(smem), p, dict_n, ebase);
+        if (wv == 0) exact_page_body(a, *reinterpret_cast<CodeLds*>(smem), p, dict_n, ebase);
     };
     if (n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes) return to_exact();
 
@@ -1661,6 +1667,407 @@ __global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match(const DevTile* 
     if (__ballot(hit) && lane() == 0) page_flags[T.page] = 0;
 }
 
+// ── the whole front of windows of pages of <= 512 rows ─────────────────────
+// k_pipe_front replaces k_pipe_runs + k_pipe_codes3 for chunks whose data
+// pages hold one tile each (the reference writer's layout).  Each wavefront
+// takes a window of consecutive pages (host-planned, <= kFrPages pages whose
+// payload slots span <= `win` bytes of the image) and keeps everything in its
+// own LDS area; no run table goes to HBM:
+//   A1. the window's slots -> LDS; one lane per page reads its prologue
+//       (column_reader.cpp:146-182: def_len, rep_len, index bit width);
+//   A2. every byte of every hybrid stream of the window is parsed as if a
+//       run header started there (rle_decoder.hpp:36-50, 76-95), all lanes,
+//       two bytes per lane and step, branch-free: the position of the next
+//       header, or the stop entry;
+//   A3. one lane per (page, stream) follows that table from the stream start,
+//       all chains of the window in one lock-step loop (one LDS read per
+//       header), listing the real headers in place over the table;
+//   B.  per page: one lane per listed header parses it exactly into a run
+//       record, a wave scan of the run lengths gives every record its first
+//       value (records past the value count drop; an exhausted stream gets its
+//       zero run, rle_decoder.hpp:20-23); then def levels, ranks and
+//       dictionary indices of the 512 rows, 8 per lane (as k_pipe_codes3),
+//       u16 codes and the tile's characters.
+// Pages outside that shape (bad headers before the value count, more than
+// kFrRuns runs, levels above max_def, bit widths > 16) are listed for
+// k_pipe_exact, the reference state machine.
+constexpr int kFrWaves = 4;
+constexpr uint32_t kFrRuns = 128;   // run records per stream
+constexpr uint32_t kFrPages = 32;   // pages per window (two chains each: 64 lanes)
+
+struct FrLayout {
+    uint32_t stage, tab, pinfo, pmap, recd, reci, mark, mark2, total;
+};
+__host__ __device__ inline FrLayout fr_layout(uint32_t win) {  // win: window bytes (multiple of 16)
+    FrLayout L{};
+    L.stage = 0;                                  // win + 32 bytes: the slots, then zeros
+    L.tab = win + 32;                             // u16 per window byte (+ the stop entry at [win])
+    L.pinfo = L.tab + (2 * win + 4 + 15) / 16 * 16;  // uint4 per page
+    L.pmap = L.pinfo + 16 * kFrPages;             // u8 per 16-byte block: its page
+    L.recd = L.pmap + (win / 16 + 15) / 16 * 16;  // uint2 x kFrRuns: run records
+    L.reci = L.recd + 8 * kFrRuns;
+    L.mark = L.reci + 8 * kFrRuns;                // u8 per row / rank
+    L.mark2 = L.mark + kTileRows;
+    L.total = L.mark2 + kTileRows;
+    return L;
+}
+
+// Branch-free header parse of the bytes x0:x1 at position q (as big_hdr).
+__device__ __forceinline__ BigHdr hdr_x(uint32_t x0, uint32_t x1, uint32_t q) {
+    const uint32_t st0 = ~x0 & 0x80808080u;
+    BigHdr h;
+    const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;  // (st0 == 0 gives 32 -> 5, replaced below)
+    const uint32_t hl5 = (~x1 & 0x80u) ? 5u : 9u;
+    h.hl = st0 ? hl4 : hl5;
+    const uint32_t lm = (h.hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (h.hl & 3))) - 1u);
+    const uint32_t x0m = x0 & lm;
+    const uint32_t top = (h.hl >= 5) ? (x1 << 28) : 0u;
+    const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
+                         ((x0m >> 3) & 0xFE00000u) | top;
+    h.g = ind >> 1;
+    h.lit = ind & 1u;
+    h.qh = q + h.hl;
+    const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, h.hl);
+    const uint32_t vb = x1 >> (8 * ((h.hl - 4) & 3));
+    h.vraw = (h.hl < 4) ? va : vb;
+    return h;
+}
+
+// Records of one stream from its listed headers (step B): rec[i] = (first
+// value, literal << 31 | payload) for the runs that start before value n,
+// plus the zero run of an exhausted stream.  Returns the record count, or
+// ~0u when the page needs the exact decoder.
+__device__ __forceinline__ uint32_t fr_records(const uint32_t* stw, const uint16_t* list, uint32_t nl, bool capped,
+                                               uint32_t e, uint32_t bw, uint32_t n, uint2* rec) {
+    const uint32_t nbv = (bw + 7) / 8;
+    const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+    const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
+    uint32_t cbase = 0, nrec = 0;
+    for (uint32_t r = 0; r < nl; r += kWave) {
+        const uint32_t i = r + lane();
+        const bool act = i < nl;
+        const uint32_t q = list[act ? i : 0u];
+        const BigHdr h = big_hdr(stw, q);
+        const bool bad = act && big_bad(h, e, nbv);
+        const uint32_t cl = min(h.g, 1u << 17) * 8, cr = min(h.g, 1u << 20);
+        const uint32_t c = (act && !bad) ? (h.lit ? cl : cr) : 0u;
+        const uint32_t incl = wave_incl_scan(c);
+        const uint32_t start = cbase + incl - c;
+        if (__ballot(bad && start < n)) return ~0u;  // a bad header before the value count
+        const bool keep = act && !bad && start < n;
+        const uint32_t pay = h.lit ? (litpay | (h.qh * litmul)) : (h.vraw & vmask);
+        if (keep) rec[i] = make_uint2(start, pay);
+        nrec += static_cast<uint32_t>(__popcll(__ballot(keep)));
+        cbase += bcast_last(incl);
+    }
+    if (cbase < n) {
+        // the listed runs hold fewer values than needed: a chain cut at
+        // kFrRuns headers, or the stream's end (the rest of the batch is 0;
+        // a bad last header was caught above: its first value is cbase < n)
+        if (capped || nrec >= kFrRuns) return ~0u;
+        if (lane() == 0) rec[nrec] = make_uint2(cbase, 0u);
+        nrec++;
+    }
+    return nrec;
+}
+
+// Per lane: the record (among nrec) of positions 8l .. 8l + 7 of a value
+// range of m positions, by marking record starts and a max scan.
+__device__ __forceinline__ void fr_runs8(uint8_t* mark, const uint2* rec, uint32_t nrec, uint32_t m, uint32_t rid[8]) {
+    const uint32_t l8 = lane() * 8;
+    *reinterpret_cast<uint2*>(mark + l8) = make_uint2(0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    for (uint32_t k = lane(); k < nrec; k += kWave) {
+        const uint32_t st = rec[k].x;
+        if (k > 0 && st < m) mark[st] = static_cast<uint8_t>(k);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint2 mk = *reinterpret_cast<const uint2*>(mark + l8);
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
+        rid[k] = run;
+    }
+    const uint32_t ex = wave_shr1(wave_incl_max(run));
+#pragma unroll
+    for (int k = 0; k < 8; k++) rid[k] = max(ex, rid[k]);
+}
+
+// page info (pinfo): x = dbase | dend << 16, y = ibase | iend << 16 (window
+// positions), z = bwi | fallback << 8 | (slot start / 16) << 16, w = rows
+__global__ void __launch_bounds__(kFrWaves * 64) k_pipe_front(CodeArgs a, const DevBatch* __restrict__ wins, int nwins,
+                                                              uint32_t lt_n, uint32_t win, int32_t* __restrict__ flist) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const FrLayout Ly = fr_layout(win);
+    const uint32_t lens_bytes = (lt_n * 2 + 15) / 16 * 16;
+    uint16_t* lens = reinterpret_cast<uint16_t*>(smem);
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    uint8_t* base = smem + lens_bytes + static_cast<uint32_t>(wv) * Ly.total;
+    uint32_t* stw = reinterpret_cast<uint32_t*>(base + Ly.stage);
+    uint16_t* tab = reinterpret_cast<uint16_t*>(base + Ly.tab);
+    uint4* pinfo = reinterpret_cast<uint4*>(base + Ly.pinfo);
+    uint8_t* pmap = base + Ly.pmap;
+    uint2* recd = reinterpret_cast<uint2*>(base + Ly.recd);
+    uint2* reci = reinterpret_cast<uint2*>(base + Ly.reci);
+    uint8_t* mark = base + Ly.mark;
+    uint8_t* mark2 = base + Ly.mark2;
+
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    const bool lean = dict_n <= lt_n;
+    copy_map(lens, a.entries + ebase, min(dict_n, lt_n), threadIdx.x, blockDim.x,
+             [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
+    __syncthreads();
+    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
+    const bool hasd = a.max_def > 0;
+    const uint32_t maskd = (1u << bwd) - 1u, nbvd = (bwd + 7) / 8;
+    const uint32_t l8 = lane() * 8;
+    const uint32_t kStop = win;  // the stop entry: tab[win] = win
+    const int nw = static_cast<int>(gridDim.x) * kFrWaves;
+    for (int w = static_cast<int>(blockIdx.x) * kFrWaves + wv; w < nwins; w += nw) {
+        const DevBatch B = wins[w];
+        const int p0 = B.p0, np = B.np;
+        // A1. slots -> LDS (16-byte aligned, >= 16 zero bytes after each payload), 32 zero bytes after
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + B.img_lo);
+            uint4* dst = reinterpret_cast<uint4*>(stw);
+            const uint32_t nb = B.img_bytes / 16;
+            for (uint32_t i = lane(); i < nb + 2; i += kWave) dst[i] = i < nb ? src[i] : make_uint4(0u, 0u, 0u, 0u);
+            for (uint32_t d = lane(); d < (win / 16 + 3) / 4; d += kWave) reinterpret_cast<uint32_t*>(pmap)[d] = 0u;
+            if (lane() == 0) tab[kStop] = static_cast<uint16_t>(kStop);
+        }
+        // one lane per page: its descriptor (kept in registers for B) and prologue
+        const bool pl = static_cast<int>(lane()) < np;
+        const DevPage pg = a.pages[p0 + (pl ? static_cast<int>(lane()) : 0)];
+        const uint32_t psize = static_cast<uint32_t>(max(pg.size, 0)), prows = static_cast<uint32_t>(max(pg.nvals, 0));
+        const uint32_t s0 = static_cast<uint32_t>(pg.off - B.img_lo);  // slot start (window position)
+        const int32_t ptile = a.page_tile0[p0 + (pl ? static_cast<int>(lane()) : 0)];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (pl && lane() > 0) pmap[s0 >> 4] = static_cast<uint8_t>(lane());
+        uint32_t fb = (!lean || prows > static_cast<uint32_t>(kTileRows)) ? 1u : 0u;
+        uint32_t pos = 0, dbase = 0, dlen = 0, bwi = 0;
+        if (hasd) {
+            if (psize < 4) fb = 1;
+            else {
+                dlen = static_cast<uint32_t>(lds_u64(stw, s0));
+                pos = 4;
+                if (static_cast<uint64_t>(pos) + dlen > psize) fb = 1;
+                else { dbase = 4; pos += dlen; }
+            }
+        }
+        if (!fb && a.max_rep > 0) {
+            if (pos + 4 > psize) fb = 1;
+            else {
+                const uint32_t rl = static_cast<uint32_t>(lds_u64(stw, s0 + pos));
+                pos += 4;
+                if (static_cast<uint64_t>(pos) + rl > psize) fb = 1;
+                else pos += rl;
+            }
+        }
+        if (!fb) {
+            if (pos + 1 > psize) fb = 1;
+            else { bwi = static_cast<uint32_t>(lds_u64(stw, s0 + pos)) & 0xFFu; pos += 1; }
+        }
+        if (bwi > 16) fb = 1;
+        if (!pl) fb = 1;
+        // window positions of the streams; a fallback page has empty streams
+        const uint32_t wdb = fb ? 0u : s0 + dbase, wde = fb ? 0u : s0 + dbase + dlen;
+        const uint32_t wib = fb ? 0u : s0 + pos, wie = fb ? 0u : s0 + psize;
+        if (pl) pinfo[lane()] = make_uint4(wdb | (wde << 16), wib | (wie << 16), bwi | (fb << 8) | ((s0 >> 4) << 16), prows);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        {   // page of every 16-byte block: max scan of the page starts (two blocks per lane... up to win / 16)
+            uint32_t* pm32 = reinterpret_cast<uint32_t*>(pmap);
+            const uint32_t nbk = (win / 16 + 3) / 4;  // dwords of the map
+            uint32_t carry = 0;
+            for (uint32_t d0 = 0; d0 < nbk; d0 += kWave) {
+                const uint32_t d = d0 + lane();
+                const uint32_t x = d < nbk ? pm32[d] : 0u;
+                uint32_t r0 = x & 0xFFu, r1 = max(r0, (x >> 8) & 0xFFu), r2 = max(r1, (x >> 16) & 0xFFu),
+                         r3 = max(r2, x >> 24);
+                const uint32_t ex = max(wave_shr1(wave_incl_max(r3)), carry);
+                carry = max(carry, bcast_last(wave_incl_max(r3)));
+                r0 = max(r0, ex); r1 = max(r1, ex); r2 = max(r2, ex); r3 = max(r3, ex);
+                if (d < nbk) pm32[d] = r0 | (r1 << 8) | (r2 << 16) | (r3 << 24);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (a.debug & 0x100000) continue;  // timing: staging + prologue only
+        // A2. next-header table over the window, two positions per lane and step
+        {
+            uint32_t* tab32 = reinterpret_cast<uint32_t*>(tab);
+            const uint32_t npair = B.img_bytes / 2;
+            for (uint32_t jp = lane(); jp < npair; jp += kWave) {
+                const uint32_t j = 2 * jp, i = j >> 2, sh = j & 3u;
+                const uint4 P = pinfo[pmap[j >> 4]];
+                const uint32_t w0 = stw[i], w1 = stw[i + 1], w2 = stw[i + 2];
+                const uint32_t dbj = P.x & 0xFFFFu, dej = P.x >> 16, ibj = P.y & 0xFFFFu, iej = P.y >> 16;
+                const uint32_t bwj = P.z & 0xFFu;
+                auto next_at = [&](uint32_t q, uint32_t x0, uint32_t x1) -> uint32_t {
+                    const bool isi = q >= ibj && q < iej, isd = q >= dbj && q < dej;
+                    const uint32_t e = isi ? iej : dej, bw = isi ? bwj : bwd, nbv = isi ? (bwj + 7) / 8 : nbvd;
+                    const BigHdr h = hdr_x(x0, x1, q);
+                    const uint32_t litm = 0u - h.lit;
+                    const uint32_t nx = (litm & (h.qh + __umul24(min(h.g, 0x10000u), bw))) | (~litm & (h.qh + nbv));
+                    const bool bad = h.hl > 5 || h.qh > e || h.g == 0 || (!h.lit && h.qh + nbv > e);
+                    return ((isi || isd) && !bad && nx < e) ? nx : kStop;
+                };
+                const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, sh), a1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh + 1), b1 = __builtin_amdgcn_alignbyte(w2, w1, sh + 1);
+                tab32[jp] = next_at(j, a0, a1) | (next_at(j + 1, b0, b1) << 16);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (a.debug & 0x200000) continue;  // timing: + next-header table
+        // A3. lane 2k lists page k's def-stream headers, lane 2k + 1 its index
+        //     stream's, in place: entry c of a list at (stream start + c) <= the
+        //     c-th header's position, behind the chain's reads
+        uint32_t cnt = 0, capped = 0;
+        {
+            const uint32_t k = lane() >> 1;
+            const bool isd = (lane() & 1u) == 0;
+            const uint4 P = pinfo[min(k, kFrPages - 1)];
+            const uint32_t q0 = isd ? (P.x & 0xFFFFu) : (P.y & 0xFFFFu), e = isd ? (P.x >> 16) : (P.y >> 16);
+            bool go = static_cast<int>(k) < np && (!isd || hasd) && q0 < e;
+            uint32_t q = q0, nx = kStop;
+            while (go) {
+                nx = tab[q];
+                tab[q0 + cnt] = static_cast<uint16_t>(q);
+                cnt++;
+                go = nx != kStop && cnt < kFrRuns;
+                q = nx;
+            }
+            capped = (cnt >= kFrRuns && nx != kStop) ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (a.debug & 0x400000) continue;  // timing: + header lists
+        // B. per page
+        for (int k = 0; k < np; k++) {
+            const uint4 P = pinfo[k];
+            const int p = p0 + k;
+            const uint32_t n = P.w;
+            const int32_t t = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(ptile), k));
+            if ((P.z >> 8) & 1u) {  // outside the fast shape: listed for the exact decoder (k_pipe_exact)
+                if (lane() == 0) flist[1 + atomicAdd(flist, 1)] = p;
+                continue;
+            }
+            if (n == 0) continue;  // (no tile)
+            const uint32_t dbk = P.x & 0xFFFFu, dek = P.x >> 16, ibk = P.y & 0xFFFFu, iek = P.y >> 16, bwi = P.z & 0xFFu;
+            const uint32_t zw = ((P.z >> 16) * 16 + (iek - ((P.z >> 16) * 16) + 15) / 16 * 16 + 16) / 4 - 1;  // slot's last (zero) word
+            const uint32_t nld = __builtin_amdgcn_readlane(cnt, 2 * k), nli = __builtin_amdgcn_readlane(cnt, 2 * k + 1);
+            const bool capd = __builtin_amdgcn_readlane(capped, 2 * k) != 0, capi = __builtin_amdgcn_readlane(capped, 2 * k + 1) != 0;
+            const int64_t R0 = static_cast<int64_t>(
+                (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(pg.first_row) >> 32), k)) << 32) |
+                __builtin_amdgcn_readlane(static_cast<uint32_t>(pg.first_row), k));
+            bool fbk = false;
+            // def levels -> validity bits of rows 8l .. 8l + 7
+            uint32_t vb = l8 >= n ? 0u : (n - l8 >= 8 ? 0xFFu : ((1u << (n - l8)) - 1u));
+            if (hasd) {
+                const uint32_t nrd = fr_records(stw, tab + dbk, nld, capd, dek, bwd, n, recd);
+                if (nrd == ~0u) fbk = true;
+                else {
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    uint32_t rid[8];
+                    fr_runs8(mark, recd, nrd, n, rid);
+                    vb = 0;
+                    bool above = false;
+#pragma unroll
+                    for (int kk = 0; kk < 8; kk++) {
+                        const uint32_t j = l8 + kk;
+                        const uint2 R = recd[rid[kk] & (kFrRuns - 1)];
+                        const uint32_t pay = rr_pay(R);
+                        const uint32_t lb = sbits3(stw, pay + (j - R.x) * bwd, zw, maskd);
+                        const uint32_t lvl = rr_lit(R) ? lb : pay;
+                        const bool in = j < n;
+                        vb |= (in && lvl == md ? 1u : 0u) << kk;
+                        above |= in && lvl > md;
+                    }
+                    if (__ballot(above)) fbk = true;  // levels above max_def: the exact decoder's error
+                }
+            }
+            if (a.debug & 0x800000) continue;  // timing: + def levels
+            uint32_t pw[4] = {0u, 0u, 0u, 0u}, chars = 0;
+            if (!fbk) {
+                const uint32_t nnl = __popc(vb);
+                const uint32_t nincl = wave_incl_scan(nnl);
+                const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
+                uint32_t nri = 0;
+                if (nn) {
+                    nri = fr_records(stw, tab + ibk, nli, capi, iek, bwi, nn, reci);
+                    if (nri == ~0u) fbk = true;
+                }
+                if (!fbk) {
+                    if (nn) {
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        uint32_t rid[8];
+                        fr_runs8(mark2, reci, nri, nn, rid);
+                        // record of every rank, for the rows' random access below
+                        uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+                        for (int kk = 0; kk < 8; kk++) {
+                            if (kk < 4) w0 |= rid[kk] << (8 * kk);
+                            else w1 |= rid[kk] << (8 * (kk - 4));
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        *reinterpret_cast<uint2*>(mark2 + l8) = make_uint2(w0, w1);
+                    } else {
+                        *reinterpret_cast<uint2*>(mark2 + l8) = make_uint2(0u, 0u);
+                        if (lane() == 0) reci[0] = make_uint2(0u, 0u);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const uint32_t maski = (1u << bwi) - 1u;
+#pragma unroll
+                    for (int kk = 0; kk < 8; kk++) {
+                        const uint32_t rk = min(rbase + __popc(vb & ((1u << kk) - 1u)), static_cast<uint32_t>(kTileRows - 1));
+                        const uint2 R = reci[mark2[rk] & (kFrRuns - 1)];
+                        const uint32_t pay = rr_pay(R);
+                        const uint32_t lb = sbits3(stw, pay + (rk - R.x) * bwi, zw, maski);
+                        const uint32_t v = rr_lit(R) ? lb : pay;
+                        const bool ok = ((vb >> kk) & 1u) && v < dict_n;
+                        const uint32_t len = lens[ok ? v : 0u];
+                        chars += ok ? len : 0u;
+                        const uint32_t code = ok ? v : static_cast<uint32_t>(kNull);
+                        if (kk & 1) pw[kk >> 1] |= code << 16;
+                        else pw[kk >> 1] = code;
+                    }
+                }
+            }
+            if (fbk) {
+                if (lane() == 0) flist[1 + atomicAdd(flist, 1)] = p;
+                continue;
+            }
+            if (a.debug & 0x1000000) continue;  // timing: no stores
+            store_packed8(a.codes, R0, l8, n, pw);
+            tile_done(a, t, wave_sum(chars));
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// The pages k_pipe_front listed: the reference state machine, one wave per
+// page (a separate launch: its registers would cost the front its occupancy).
+__global__ void __launch_bounds__(64) k_pipe_exact(CodeArgs a, const int32_t* __restrict__ flist) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // one CodeLds: one wave per workgroup
+    CodeLds& L = *reinterpret_cast<CodeLds*>(smem);
+    const int nf = flist[0];
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    for (int i = static_cast<int>(blockIdx.x); i < nf; i += static_cast<int>(gridDim.x)) {
+        exact_page(a, L, flist[1 + i], dict_n, ebase);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 }  // namespace
 
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens) { return big_layout(max_page_bytes, nlens).total; }
@@ -1672,12 +2079,8 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
     pl.blocks_per_cu = all <= 160u * 1024 ? static_cast<int>((160u * 1024) / all) : 0;
     if (pl.blocks_per_cu > 4) pl.blocks_per_cu = 4;
     if (pl.blocks_per_cu > 0) {  // registers may allow fewer
-        const void* fn = reinterpret_cast<const void*>(k_pipe_write);
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(pl.lds));
-        int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, wpw * kWave, pl.lds) ==
-                hipSuccess && occ > 0)
-            pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
+        const int occ = resident_blocks(reinterpret_cast<const void*>(k_pipe_write), wpw * kWave, pl.lds);
+        pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
     }
     return pl;
 }
@@ -1722,16 +2125,9 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     const uint32_t lt_n = P.dict_entries_cap;
     const uint32_t lds = (lt_n * 2 + 15) / 16 * 16;
     const void* fn = reinterpret_cast<const void*>(k_pipe_codes3);
-    static uint32_t attr = 0;
-    if (lds > attr) {
-        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-        attr = lds;
-    }
     // resident workgroups per CU (LDS and registers), so the grid is one wave of blocks
-    int bpc = 0;
     const int waves = kCodeWaves3;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, waves * kWave, lds) != hipSuccess || bpc < 1)
-        bpc = 1;
+    const int bpc = max(1, resident_blocks(fn, waves * kWave, lds));
     const int need = (P.ntiles + waves - 1) / waves;
     const int grid = max(1, min(need, P.cus * bpc));
     // also decodes the pages the run-table passes marked (flist)
@@ -1742,12 +2138,7 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
 
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
     if (P.ntiles <= 0) return;
-    static uint32_t attr = 0;
-    if (P.lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_write),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(P.lds));
-        attr = P.lds;
-    }
+    ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_write), P.lds);
     int grid = 0, per = 0;
     write_shape(P, &grid, &per);  // P.grid: resident workgroups (plan_pipe_lds + occupancy)
     WriteArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.dicts, P.dict_id, P.entries, P.dict_count, P.codes,
@@ -1765,14 +2156,32 @@ void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_page
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
                P.bsum, per, P.debug, P.write_waves};
     const uint32_t lds = big_layout(max_page_bytes, nlens).total;
-    static uint32_t attr = 0;
-    if (lds > attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pipe_big),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-        attr = lds;
-    }
+    ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_big), lds);
     hipLaunchKernelGGL(k_pipe_big, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
                        const_cast<uint32_t*>(P.info), nlens);
+}
+
+uint32_t pipe_front_slot(uint32_t max_page_bytes) { return (max_page_bytes + 15) / 16 * 16 + 16; }
+
+uint32_t pipe_front_win_pages() { return kFrPages; }
+
+void launch_pipe_front(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, int nwins, uint32_t win) {
+    if (P.ntiles <= 0) return;
+    int wgrid = 0, per = 0;
+    write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_write's workgroups
+    CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
+               P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
+               P.bsum, per, P.debug, P.write_waves};
+    const uint32_t lt_n = P.dict_entries_cap;
+    const uint32_t lds = (lt_n * 2 + 15) / 16 * 16 + kFrWaves * fr_layout(win).total;
+    const void* fn = reinterpret_cast<const void*>(k_pipe_front);
+    const int bpc = max(1, resident_blocks(fn, kFrWaves * kWave, lds));
+    const int need = (nwins + kFrWaves - 1) / kFrWaves;
+    const int grid = max(1, min(need, P.cus * bpc));
+    int32_t* flist = const_cast<int32_t*>(P.flist);  // [0] cleared with the decode's flags
+    hipLaunchKernelGGL(k_pipe_front, dim3(grid), dim3(kFrWaves * kWave), lds, s, a, wins, nwins, lt_n, win, flist);
+    // listed pages (none on well-formed ref-layout chunks)
+    hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, P.npages))), dim3(kWave), sizeof(CodeLds), s, a, P.flist);
 }
 
 void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags) {

@@ -83,6 +83,14 @@ size_t chunk_assign_scratch(int64_t n);
 int chunk_assign(hipStream_t st, const uint32_t* validity, const int64_t* offsets, int64_t n, int64_t chunk_bytes,
                  int64_t* out, uint8_t* scratch, int64_t* num_chunks);
 
+// Per-device launch facts (host/launch_attr.cpp), thread-safe and keyed by
+// the current device: the dynamic-LDS limit of a kernel (raised when needed;
+// false if the device refuses), resident workgroups per CU for (kernel,
+// block threads, dynamic LDS), and the device's compute units.
+bool ensure_dyn_lds(const void* fn, uint32_t bytes);
+int resident_blocks(const void* fn, int threads, uint32_t lds);
+int device_cus();
+
 struct ColumnParams {
     int32_t type;
     int16_t max_def;
@@ -183,6 +191,15 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist, int debug,
                       const RunDicts* dicts = nullptr);
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
+// k_pipe_front: the whole front (run headers -> u16 codes, tile characters)
+// of chunks whose pages hold <= kTileRows rows, one wavefront per window of
+// consecutive pages (<= pipe_front_win_pages() pages whose slots span <= win
+// bytes; every slot <= win); k_pipe_exact then decodes the pages it listed
+uint32_t pipe_front_slot(uint32_t max_page_bytes);
+uint32_t pipe_front_win_pages();
+constexpr uint32_t kFrontWin = 2048;     // window bytes (pages with larger slots take the run-table passes)
+struct DevBatch;
+void launch_pipe_front(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, int nwins, uint32_t win);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,
 // then codes and tile characters (one workgroup per listed page)

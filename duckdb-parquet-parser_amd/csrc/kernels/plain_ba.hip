@@ -958,14 +958,7 @@ static void plain_shape(const PlainLaunch& P, int* grid, int* per) {
 }
 
 int plain_write_blocks_per_cu() {
-    const uint32_t lds = plain_write_lds();
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_plain_write), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds));
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k_plain_write),
-                                                     kPWWaves * kWave, lds) != hipSuccess || occ < 1)
-        occ = 1;
-    return occ;
+    return max(1, resident_blocks(reinterpret_cast<const void*>(k_plain_write), kPWWaves * kWave, plain_write_lds()));
 }
 
 void launch_plain_big_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, uint32_t min_size,
@@ -979,18 +972,9 @@ void launch_plain_big_rows(hipStream_t s, const uint8_t* bytes, const DevPage* p
 void launch_plain_ba(hipStream_t s, PlainLaunch P) {
     if (P.nwins <= 0) return;
     if (P.wbase || P.wmode >= kWinOpt) {  // one pass (the host re-runs the two passes if it sets *redo)
-        static int fgrid = 0;
         const uint32_t lds = kPFWaves * static_cast<uint32_t>(sizeof(PFLds));
-        if (!fgrid) {
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_plain_fused), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      static_cast<int>(lds));
-            int bpc = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(k_plain_fused),
-                                                             kPFWaves * kWave, lds) != hipSuccess || bpc < 1)
-                bpc = 1;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1) cus = 256;
-            fgrid = bpc * cus;
-        }
+        const int fgrid = max(1, resident_blocks(reinterpret_cast<const void*>(k_plain_fused), kPFWaves * kWave, lds)) *
+                          device_cus();
         const int need = (P.nwins + kPFWaves - 1) / kPFWaves;
         hipLaunchKernelGGL(k_plain_fused, dim3(std::min(need, fgrid)), dim3(kPFWaves * kWave), lds, s, P);
         return;
@@ -1000,15 +984,9 @@ void launch_plain_ba(hipStream_t s, PlainLaunch P) {
     P.per = per;
     (void)hipMemsetAsync(P.bsum, 0, static_cast<size_t>(grid) * sizeof(unsigned long long), s);
     {
-        static int walk_grid = 0;  // resident workgroups of k_plain_walk on this device
-        if (!walk_grid) {
-            int bpc = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void*>(k_plain_walk),
-                                                             kWalkWaves * kWave, 0) != hipSuccess || bpc < 1)
-                bpc = 1;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus < 1) cus = 256;
-            walk_grid = bpc * cus;
-        }
+        // resident workgroups of k_plain_walk on this device
+        const int walk_grid = max(1, resident_blocks(reinterpret_cast<const void*>(k_plain_walk), kWalkWaves * kWave, 0)) *
+                              device_cus();
         const int need = (P.nwins + kWalkWaves - 1) / kWalkWaves;
         hipLaunchKernelGGL(k_plain_walk, dim3(std::min(need, walk_grid)), dim3(kWalkWaves * kWave), 0, s, P);
     }

@@ -850,12 +850,7 @@ void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, c
                         const uint8_t* dict_match, ColumnParams cp, int neg, uint8_t* page_flags,
                         DevErr* page_err, int32_t* err_any) {
     if (npages <= 0) return;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_regex_lanes),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kDfaMaxBytes);
-        attr = true;
-    }
+    pqk::ensure_dyn_lds(reinterpret_cast<const void*>(k_regex_lanes), kDfaMaxBytes);
     const int blocks = (npages + 255) / 256;
     hipLaunchKernelGGL(k_regex_lanes, dim3(blocks), dim3(256), dfa_bytes, s, dfa, dfa_bytes, bytes, pages, npages,
                        dicts, dict_count, dict_match, cp, neg, page_flags, page_err, err_any);
@@ -876,12 +871,7 @@ void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, u
                         int32_t* ticket, int grid, ColumnParams cp, int neg, uint8_t* page_flags,
                         DevErr* page_err, int32_t* err_any) {
     if (nwins <= 0) return;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_regex_plain),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
+    pqk::ensure_dyn_lds(reinterpret_cast<const void*>(k_regex_plain), 160 * 1024);
     hipLaunchKernelGGL(k_regex_plain, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes) * kWave),
                        regex_plain_lds(dfa_bytes, win_bytes),
                        s, dfa, dfa_bytes, win_bytes, bytes, pages, wins, nwins, ticket, cp, neg, page_flags,

@@ -21,8 +21,8 @@ CONFIGS = {"C2": (gen.c2_cols, gen.REF_LAYOUT, 2), "C2a": (gen.c2_cols, gen.ARRO
 # library defaults of the options the variants may set (restored after each)
 DEFAULTS = {"pipe_run_pages": 32, "zflip": 1, "write_waves": 10, "dict_pipe": 1, "plain_ba": 1,
             "fused_ba": 1, "fixed_plain": 1, "big_all": 0, "fused_debug": 0, "plain_fused": 1, "regex_win": 8192,
-            "raw_upload": 1}
-KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "plain_spec", "pipe_count", "pipe_codes",
+            "raw_upload": 1, "pipe_front": 0}
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_front", "pipe_big", "plain_spec", "pipe_count", "pipe_codes",
            "pipe_write", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba", "plain_opt")
 
 cfg, _, colname = sys.argv[1].partition(":")
@@ -88,6 +88,6 @@ for i, v in enumerate(variants):
     walls = sorted(res[i]["wall"])
     wall = walls[len(walls) // 2]
     ks = res[i]["ms"][0].keys()
-    ms = {k: round(sorted(r[k] for r in res[i]["ms"])[1], 4) for k in ks}
+    ms = {k: round(sorted(r.get(k, 0.0) for r in res[i]["ms"])[1], 4) for k in ks}
     print(json.dumps({"variant": v, "same_as_first": same, "wall_ms": round(wall, 4),
                       "Gvalues_s": round(rows / wall / 1e6, 2), "ms": ms}), flush=True)

@@ -84,8 +84,10 @@ class TW:
         return self
 
 
-def data_header(size: int, nvals: int, enc: int = 0, ptype: int = 0, with_dph: bool = True) -> bytes:
-    t = TW().i32(1, ptype).i32(2, size).i32(3, size)
+def data_header(size: int, nvals: int, enc: int = 0, ptype: int = 0, with_dph: bool = True,
+                usize: int | None = None) -> bytes:
+    """usize: uncompressed_page_size when it differs (compressed pages)."""
+    t = TW().i32(1, ptype).i32(2, size if usize is None else usize).i32(3, size)
     if with_dph:
         t.begin(5).i32(1, nvals).i32(2, enc).i32(3, 3).i32(4, 3).end()
     return bytes(t.stop().b)
@@ -118,7 +120,7 @@ def plain_ba(values) -> bytes:
 
 
 def build_file(pages: list[bytes], ptype: int, optional: bool, num_values: int,
-               dict_at_start: bool = False, name: bytes = b"c", pad_footer: bool = True):
+               dict_at_start: bool = False, name: bytes = b"c", pad_footer: bool = True, codec: int = 0):
     """pages: list of (header + payload) blobs laid out back to back.
     Returns (file bytes, chunk dict for the oracle/C ABI)."""
     body = b"PAR1"
@@ -143,7 +145,7 @@ def build_file(pages: list[bytes], ptype: int, optional: bool, num_values: int,
     t.b += zigzag(0)
     t.list_begin(3, 8, 1)
     t.b += varint(len(name)) + name
-    t.i32(4, 0)
+    t.i32(4, codec)
     t.i64(5, num_values)
     t.i64(6, end - start)
     t.i64(7, end - start)
@@ -163,6 +165,6 @@ def build_file(pages: list[bytes], ptype: int, optional: bool, num_values: int,
     footer = bytes(t.b)
     data = body + footer + struct.pack("<I", len(footer)) + b"PAR1"
     chunk = dict(num_values=num_values, data_page_offset=start,
-                 dictionary_page_offset=start if dict_at_start else None, codec=0, type=ptype,
+                 dictionary_page_offset=start if dict_at_start else None, codec=codec, type=ptype,
                  max_def=1 if optional else 0, max_rep=0)
     return data, chunk

@@ -54,31 +54,6 @@ SMALL = [
 ]
 
 
-@pytest.fixture(params=["default", "big", "fused", "generic"])
-def path(request, ctx):
-    """Every kernel path that ships: "default" = what a chunk takes with the
-    default options (three-pass dictionary BYTE_ARRAY, dict_pipe.hip; two-pass
-    PLAIN BYTE_ARRAY, plain_ba.hip; tile-parallel PLAIN fixed width,
-    fixed_fast.hip; the fused and generic kernels for chunks neither
-    takes); "big" puts every page of a dictionary chunk through k_pipe_big
-    (the large-page kernel) so it also meets small pages; "fused" forces the
-    per-page fused BYTE_ARRAY kernel (dict_fused.hip) onto every BYTE_ARRAY
-    chunk it can take; "generic" forces decode.hip's rows/scan/gather and
-    per-page k_fixed.  PLAIN BYTE_ARRAY chunks take the one-pass kernel
-    (k_plain_fused) under "default" and the two passes under "big"."""
-    p = request.param
-    ctx.set_option("big_all", int(p == "big"))
-    ctx.set_option("dict_pipe", int(p in ("default", "big")))
-    ctx.set_option("plain_ba", int(p in ("default", "big")))
-    ctx.set_option("fused_ba", int(p != "generic"))
-    ctx.set_option("fixed_plain", int(p != "generic"))
-    ctx.set_option("plain_fused", int(p != "big"))
-    yield p
-    for k in ("dict_pipe", "plain_ba", "fused_ba", "fixed_plain", "plain_fused"):
-        ctx.set_option(k, 1)
-    ctx.set_option("big_all", 0)
-
-
 @pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT], ids=["ref", "arrow"])
 @pytest.mark.parametrize("name,cols,n", SMALL, ids=[s[0] for s in SMALL])
 def test_generated_columns(ctx, path, name, cols, n, layout):

@@ -66,21 +66,6 @@ CASES = [
 ]
 
 
-@pytest.fixture(params=["window", "codes", "lanes", "nfa"])
-def kernel(request, ctx):
-    """Every page kernel: windowed DFA (default for chunks without dictionary
-    pages), match bits over the pipe decode's codes (default for dictionary
-    chunks the pipe path takes), lane-per-page DFA (other dictionary chunks)
-    and wave-per-page NFA (patterns whose DFA is over its size cap)."""
-    ctx.set_option("regex_dfa", int(request.param != "nfa"))
-    ctx.set_option("regex_plain", int(request.param == "window"))
-    ctx.set_option("regex_codes", int(request.param in ("window", "codes")))
-    yield request.param
-    ctx.set_option("regex_dfa", 1)
-    ctx.set_option("regex_plain", 1)
-    ctx.set_option("regex_codes", 1)
-
-
 @pytest.mark.parametrize("neg", [False, True], ids=["like", "notlike"])
 @pytest.mark.parametrize("name,cols,n,layout", CASES, ids=[c[0] for c in CASES])
 def test_regex_pages(ctx, kernel, name, cols, n, layout, neg):
