@@ -80,6 +80,7 @@ struct pq_ctx {
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
     bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
     bool opt_front = false;      // "pipe_front": windowed one-wave front (k_pipe_front) where the pages allow it
+    int opt_write_bpc = 0;       // "write_bpc": cap on k_pipe_write workgroups per CU (0: as many as fit; set before upload)
     int opt_stage_bufs = 6;      // "stage_bufs" / "stage_piece_kb": pinned upload ring (stage.hpp)
 };
 
@@ -444,8 +445,9 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     const uint32_t chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
     const uint32_t dict_bytes = 16 + chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
     const int wpw = std::max(1, std::min(16, ctx->opt_write_waves));
-    const pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes, wpw);
+    pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes, wpw);
     if (pl.blocks_per_cu == 0) return;
+    if (ctx->opt_write_bpc > 0) pl.blocks_per_cu = std::min(pl.blocks_per_cu, ctx->opt_write_bpc);
     const int cus = ctx->cus;
     c->pipe = true;
     c->pipe_small = small;
@@ -659,6 +661,51 @@ void plan_fused(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages,
 
 extern "C" {
 
+int pq_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+int pq_plan_page_ranges(const pq_page_desc* table, int64_t ntable, int world, int64_t* ranges) {
+    if ((!table && ntable) || ntable < 0 || world <= 0 || !ranges) return PQ_ERR_ARG;
+    // cumulative payload bytes of the data pages (shard.py page_ranges)
+    std::vector<int64_t> cum;
+    cum.reserve(static_cast<size_t>(ntable));
+    int64_t acc = 0;
+    for (int64_t i = 0; i < ntable; i++) {
+        if (table[i].page_type != PQ_DATA_PAGE) continue;
+        acc += std::max<int64_t>(table[i].payload_size, 0);
+        cum.push_back(acc);
+    }
+    const int64_t n = static_cast<int64_t>(cum.size());
+    int64_t prev = 0;
+    for (int k = 0; k < world; k++) {
+        int64_t cut = n;
+        if (k + 1 < world) {
+            if (n == 0) {
+                cut = 0;
+            } else {
+                // first page whose running total reaches (k + 1) / world of the sum, plus one
+                // (the float64 quotient of the exact product, as shard.py computes it)
+                const double target = static_cast<double>(acc * (k + 1)) / world;
+                const int64_t c = static_cast<int64_t>(
+                    std::lower_bound(cum.begin(), cum.end(), target,
+                                     [](int64_t v, double t) { return static_cast<double>(v) < t; }) -
+                    cum.begin()) + 1;
+                cut = std::min(std::max(c, prev), n);
+            }
+        }
+        ranges[2 * k] = prev;
+        ranges[2 * k + 1] = cut;
+        prev = cut;
+    }
+    return 0;
+}
+
 pq_ctx* pq_ctx_create(int device) {
     try {
         int n = 0;
@@ -745,6 +792,11 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "plain_fused") == 0) { ctx->opt_plain_fused = value != 0; return 0; }
     if (std::strcmp(key, "pipe_run_dict") == 0) { ctx->opt_run_dict = value != 0; return 0; }
     if (std::strcmp(key, "pipe_front") == 0) { ctx->opt_front = value != 0; return 0; }
+    if (std::strcmp(key, "write_bpc") == 0) {
+        if (value < 0 || value > 4) return set_err(ctx, PQ_ERR_ARG, "write_bpc: 0..4");
+        ctx->opt_write_bpc = static_cast<int>(value);
+        return 0;
+    }
     if (std::strcmp(key, "pipe_run_pages") == 0) {
         if (value < 1 || value > 32) return set_err(ctx, PQ_ERR_ARG, "pipe_run_pages: 1..32");
         ctx->opt_run_pages = static_cast<int>(value);

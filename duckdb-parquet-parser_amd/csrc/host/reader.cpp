@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <exception>
+#include <thread>
 #include <fstream>
 #include <iostream>
 #include <sstream>
@@ -70,7 +72,54 @@ HostColumn decode_chunks(Device& dev, const uint8_t* file, size_t len, const std
     return h;
 }
 
+// Shard `b`..`e` (data-page ordinals) of one chunk on `dev`.
+HostColumn decode_range(Device& dev, const uint8_t* file, size_t len, const pq_chunk_desc& desc,
+                        const std::vector<pq_page_desc>& table, int64_t b, int64_t e) {
+    pq_ctx* ctx = dev.ctx();
+    pq_chunk* ch = nullptr;
+    int rc = pq_chunk_upload_range(ctx, file, len, &desc, table.data(), static_cast<int64_t>(table.size()), b, e, &ch);
+    if (rc) raise(rc, pq_last_error(ctx));
+    pq_column out{};
+    rc = pq_decode(ctx, ch, &out);
+    if (rc) {
+        std::string msg = pq_last_error(ctx);
+        pq_column_free(ctx, &out);
+        pq_chunk_free(ctx, ch);
+        raise(rc, msg);
+    }
+    HostColumn h;
+    h.type = static_cast<ParquetType>(desc.type);
+    h.num_rows = out.num_rows;
+    h.validity.assign(static_cast<size_t>((out.num_rows + 31) / 32) + 1, 0);
+    h.values.assign(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)), 0);
+    if (desc.type == PQ_BYTE_ARRAY) h.offsets.assign(static_cast<size_t>(out.num_rows + 1), 0);
+    rc = pq_column_copy_out(ctx, &out, h.validity.data(), h.values.data(),
+                            h.offsets.empty() ? nullptr : h.offsets.data());
+    h.values.resize(static_cast<size_t>(out.num_bytes));
+    pq_column_free(ctx, &out);
+    pq_chunk_free(ctx, ch);
+    if (rc) raise(rc, "device copy failed");
+    return h;
+}
+
+// a followed by b (rows, validity bits, values; offsets rebased)
+void append_column(HostColumn& a, const HostColumn& b) {
+    const int64_t n0 = a.num_rows, n = n0 + b.num_rows;
+    a.validity.resize(static_cast<size_t>((n + 31) / 32) + 1, 0);
+    for (int64_t i = 0; i < b.num_rows; i++)
+        if (b.valid(i)) a.validity[static_cast<size_t>((n0 + i) >> 5)] |= 1u << ((n0 + i) & 31);
+    const int64_t base = static_cast<int64_t>(a.values.size());
+    a.values.insert(a.values.end(), b.values.begin(), b.values.end());
+    if (a.type == ParquetType::BYTE_ARRAY) {
+        if (a.offsets.empty()) a.offsets.push_back(0);
+        for (int64_t i = 1; i <= b.num_rows; i++) a.offsets.push_back(base + b.offsets[static_cast<size_t>(i)]);
+    }
+    a.num_rows = n;
+}
+
 }  // namespace
+
+int Device::count() { return pq_device_count(); }
 
 std::string Value::to_string() const {  // common.hpp:189-200
     if (is_null) return "NULL";
@@ -349,6 +398,88 @@ HostColumn ParquetReader::read_column_columnar(const std::string& name) {
     if (c < 0) throw std::runtime_error("Column not found: " + name);
     return decode_column(c, 0, static_cast<int>(num_row_groups()));
 }
+HostColumn ParquetReader::read_column_columnar(const std::string& name, const std::vector<Device*>& devices) {
+    int c = find_column(name);
+    if (c < 0) throw std::runtime_error("Column not found: " + name);
+    const int nrg = static_cast<int>(num_row_groups());
+    const int D = static_cast<int>(devices.size());
+    if (D <= 1) return D == 1 ? decode_column_on(*devices[0], c) : read_column_columnar(name);
+    std::vector<pq_chunk_desc> descs(static_cast<size_t>(nrg));
+    std::vector<std::vector<pq_page_desc>> tables(static_cast<size_t>(nrg));
+    std::vector<std::vector<int64_t>> plans(static_cast<size_t>(nrg), std::vector<int64_t>(2 * static_cast<size_t>(D)));
+    for (int rg = 0; rg < nrg; rg++) {
+        pq_chunk_desc& d = descs[static_cast<size_t>(rg)];
+        int rc = pq_file_chunk(file_, rg, c, &d);
+        if (rc) raise(rc == PQ_ERR_OPTIONAL ? 0 : rc, "ColumnChunk has no metadata");
+        if (d.codec != 0) throw std::runtime_error("Only uncompressed parquet files are supported");
+        // the chunk's page table (host walk), grown until it holds every page
+        std::vector<pq_page_desc>& t = tables[static_cast<size_t>(rg)];
+        int64_t n = 0;
+        t.resize(1024);
+        for (;;) {
+            rc = pq_build_page_table(data_.data(), data_.size(), &d, t.data(), static_cast<int64_t>(t.size()), &n,
+                                     nullptr, 0);
+            if (n <= static_cast<int64_t>(t.size())) break;
+            t.resize(static_cast<size_t>(n));
+        }
+        t.resize(static_cast<size_t>(n));
+        // a walk error: the one-device path reports it exactly as the reference
+        if (rc) return decode_column_on(*devices[0], c);
+        pq_plan_page_ranges(t.data(), n, D, plans[static_cast<size_t>(rg)].data());
+    }
+    // one host thread per device: its range of every row group, in order
+    std::vector<std::vector<HostColumn>> parts(static_cast<size_t>(D), std::vector<HostColumn>(static_cast<size_t>(nrg)));
+    std::vector<std::exception_ptr> errs(static_cast<size_t>(D) * static_cast<size_t>(nrg));
+    std::vector<std::thread> th;
+    for (int k = 0; k < D; k++) {
+        th.emplace_back([&, k]() {
+            for (int rg = 0; rg < nrg; rg++) {
+                const auto& pl = plans[static_cast<size_t>(rg)];
+                try {
+                    parts[static_cast<size_t>(k)][static_cast<size_t>(rg)] =
+                        decode_range(*devices[static_cast<size_t>(k)], data_.data(), data_.size(),
+                                     descs[static_cast<size_t>(rg)], tables[static_cast<size_t>(rg)],
+                                     pl[2 * static_cast<size_t>(k)], pl[2 * static_cast<size_t>(k) + 1]);
+                } catch (...) {
+                    errs[static_cast<size_t>(rg) * D + k] = std::current_exception();
+                    return;  // (later row groups of this device are never reached by the reference)
+                }
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    // the first error in page order (row group, then shard) is the reference's first error
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
+    HostColumn out;
+    out.type = columns_[static_cast<size_t>(c)].type;
+    for (int rg = 0; rg < nrg; rg++)
+        for (int k = 0; k < D; k++) append_column(out, parts[static_cast<size_t>(k)][static_cast<size_t>(rg)]);
+    if (out.type == ParquetType::BYTE_ARRAY && out.offsets.empty()) out.offsets.push_back(0);
+    out.validity.resize(static_cast<size_t>((out.num_rows + 31) / 32) + 1, 0);
+    return out;
+}
+
+std::vector<Value> ParquetReader::read_column(const std::string& name, const std::vector<Device*>& devices) {
+    HostColumn h = read_column_columnar(name, devices);
+    std::vector<Value> v;
+    v.reserve(static_cast<size_t>(h.num_rows));
+    for (int64_t i = 0; i < h.num_rows; i++) v.push_back(h.value(i));
+    return v;
+}
+
+HostColumn ParquetReader::decode_column_on(Device& dev, int col_idx) {
+    std::vector<pq_chunk_desc> descs;
+    for (int rg = 0; rg < static_cast<int>(num_row_groups()); rg++) {
+        pq_chunk_desc d{};
+        int rc = pq_file_chunk(file_, rg, col_idx, &d);
+        if (rc) raise(rc == PQ_ERR_OPTIONAL ? 0 : rc, "ColumnChunk has no metadata");
+        if (d.codec != 0) throw std::runtime_error("Only uncompressed parquet files are supported");
+        descs.push_back(d);
+    }
+    return decode_chunks(dev, data_.data(), data_.size(), descs, nullptr);
+}
+
 std::vector<Value> ParquetReader::read_column(const std::string& name) {  // parquet_reader.cpp:125-144
     HostColumn h = read_column_columnar(name);
     std::vector<Value> v;

@@ -85,6 +85,7 @@ public:
     Device& operator=(const Device&) = delete;
     pq_ctx* ctx() const { return ctx_; }
     static Device& default_device();
+    static int count();  // visible HIP devices
 
 private:
     pq_ctx* ctx_;
@@ -186,6 +187,15 @@ public:
     std::vector<Value> read_column(const std::string& col_name);
     std::vector<Value> read_column_by_idx(int row_group_idx, int col_idx);
     HostColumn read_column_columnar(const std::string& col_name);
+    // Page-range sharding over several devices (the global page
+    // order of build_page_index, parquet_reader.cpp:559-605): every row
+    // group's chunk is cut into byte-balanced data-page ranges
+    // (pq_plan_page_ranges), one per device; one host thread per device
+    // uploads and decodes its ranges (pq_chunk_upload_range: the range's pages
+    // plus their dictionary page, no collective); the shards are joined in
+    // page order.  Same result and errors as the one-device calls.
+    HostColumn read_column_columnar(const std::string& col_name, const std::vector<Device*>& devices);
+    std::vector<Value> read_column(const std::string& col_name, const std::vector<Device*>& devices);
 
     StringColumnIterator column_iterator(const std::string& col_name);
     // The example driver's chunk assignment (src/main.cpp:17-32) over
@@ -209,6 +219,7 @@ public:
 
 private:
     HostColumn decode_column(int col_idx, int rg_first, int rg_count);
+    HostColumn decode_column_on(Device& dev, int col_idx);
     Device& dev_;
     std::vector<uint8_t> data_;
     pq_file* file_ = nullptr;

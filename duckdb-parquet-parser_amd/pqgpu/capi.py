@@ -88,6 +88,8 @@ def lib():
     if _lib is None:
         L = C.CDLL(_paths.lib_path("libpqgpu.so"))
         sig = {
+            "pq_device_count": ([], C.c_int),
+            "pq_plan_page_ranges": ([C.POINTER(PageDesc), C.c_int64, C.c_int, C.POINTER(C.c_int64)], C.c_int),
             "pq_ctx_create": ([C.c_int], vp),
             "pq_ctx_destroy": ([vp], None),
             "pq_last_error": ([vp], C.c_char_p),
@@ -170,6 +172,17 @@ def build_page_table(file: bytes, chunk: ChunkDesc, cap: int = 0):
     exact = (PageDesc * n.value)()
     C.memmove(exact, pages, C.sizeof(PageDesc) * n.value)
     return rc, err.value.decode(errors="replace"), exact
+
+
+def plan_page_ranges(table, world: int) -> list[tuple[int, int]]:
+    """pq_plan_page_ranges: byte-balanced contiguous data-page ranges of a
+    chunk's page table (build_page_table) for `world` shards."""
+    arr = table if isinstance(table, C.Array) else (PageDesc * max(len(table), 1))(*table)
+    out = (C.c_int64 * (2 * world))()
+    rc = lib().pq_plan_page_ranges(arr, len(table), world, out)
+    if rc:
+        raise PqError(rc, "pq_plan_page_ranges failed")
+    return [(int(out[2 * k]), int(out[2 * k + 1])) for k in range(world)]
 
 
 # ── file metadata (ParquetReader::open) ────────────────────────────────────

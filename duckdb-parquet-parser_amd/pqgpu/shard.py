@@ -46,8 +46,15 @@ def shard_row_offsets(rows_per_shard) -> np.ndarray:
 def data_page_ranges(table, world: int) -> list[tuple[int, int]]:
     """Byte-balanced contiguous ranges of a chunk's DATA pages (ordinals in walk
     order, the unit pq_chunk_upload_range takes) from its page table
-    (capi.build_page_table).  Dictionary pages are not counted: every shard
-    that needs one gets it replicated."""
+    (capi.build_page_table): the library's planner, pq_plan_page_ranges
+    (csrc/capi.hip).  Dictionary pages are not counted: every shard that needs
+    one gets it replicated."""
+    from . import capi
+    return capi.plan_page_ranges(table, world)
+
+
+def data_page_ranges_py(table, world: int) -> list[tuple[int, int]]:
+    """The same plan in numpy (page_ranges): the cross-check of the C planner."""
     sizes = [p.payload_size for p in table if p.page_type == 0]
     return page_ranges(sizes, world)
 

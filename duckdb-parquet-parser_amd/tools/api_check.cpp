@@ -6,9 +6,12 @@
 //   api_check <file> column_reader <rg> <col>      ColumnReader(read_range,...).read_all
 //   api_check <file> read_pages <rg> <col>         ColumnReader::read_pages (page records on stderr)
 //   api_check <file> iterator <name>               StringColumnIterator (pos, len, bytes)
+//   api_check <file> sharded <name> <k>            read_column over k Devices (device i % count),
+//                                                  one host thread each
 #include <cstdio>
 #include <cstring>
 #include <iostream>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -42,6 +45,17 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> out;
         if (mode == "read_column") {
             for (const auto& v : r.read_column(argv[3])) dump(v, out);
+        } else if (mode == "sharded") {
+            int k = argc > 4 ? std::atoi(argv[4]) : 2;
+            int nd = pqgpu::Device::count();
+            if (nd < 1) throw std::runtime_error("no HIP device");
+            std::vector<std::unique_ptr<pqgpu::Device>> own;
+            std::vector<pqgpu::Device*> devs;
+            for (int i = 0; i < k; i++) {
+                own.emplace_back(new pqgpu::Device(i % nd));
+                devs.push_back(own.back().get());
+            }
+            for (const auto& v : r.read_column(argv[3], devs)) dump(v, out);
         } else if (mode == "iterator") {
             auto it = r.column_iterator(argv[3]);
             while (it.has_next()) {

@@ -132,6 +132,10 @@ typedef struct {
 } pq_column;
 
 /* ── context ─────────────────────────────────────────────────────────────── */
+/* One context per device; several contexts (also on one device) may be
+ * driven from different host threads at once, each from one thread at a
+ * time.  pq_device_count: visible devices (0 without a GPU). */
+int pq_device_count(void);
 pq_ctx* pq_ctx_create(int device);
 void pq_ctx_destroy(pq_ctx* ctx);
 const char* pq_last_error(const pq_ctx* ctx);
@@ -201,6 +205,14 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
 int pq_chunk_upload_range(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc* chunk,
                           const pq_page_desc* table, int64_t ntable, int64_t data_begin,
                           int64_t data_end, pq_chunk** out);
+/* Page-range plan for N shards: `world` contiguous ranges of the
+ * chunk's DATA pages (ordinals in walk order, as pq_chunk_upload_range takes
+ * them) balanced by payload bytes: range k ends where the running payload
+ * total first reaches k/world of the chunk's sum (dictionary pages are not
+ * counted; every shard that needs one gets it).  ranges[2k], ranges[2k + 1]
+ * = [begin, end) of shard k.  Host only; the order is the reference's global
+ * page order within a chunk (build_page_index, parquet_reader.cpp:559-605). */
+int pq_plan_page_ranges(const pq_page_desc* table, int64_t ntable, int world, int64_t* ranges);
 void pq_chunk_free(pq_ctx* ctx, pq_chunk* chunk);
 int64_t pq_chunk_num_rows(const pq_chunk* chunk);
 int64_t pq_chunk_first_row(const pq_chunk* chunk);     /* 0 unless a page-range upload */

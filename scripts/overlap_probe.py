@@ -22,7 +22,7 @@ F = capi.File(f)
 ch = F.chunk(0, 0)
 rc, msg, table = capi.build_page_table(f, ch)
 assert rc == 0, msg
-ctxs = [capi.Context(0) for _ in range(4)]
+ctxs = [capi.Context(0) for _ in range(int(os.environ.get("NCTX", "2")))]
 
 ref = ctxs[0].upload(f, [ch])
 ref.decode()
@@ -77,4 +77,4 @@ for v in variants:
         d.free()
     for c in ctxs[:S]:
         for k in opts:
-            c.set_option(k, 1 if k in ("pipe_front", "dict_pipe") else 0)
+            c.set_option(k, {"dict_pipe": 1, "write_waves": 10}.get(k, 0))

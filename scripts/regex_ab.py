@@ -12,8 +12,11 @@ sys.path[:0] = [ROOT, os.environ.get("AB_PKG") or os.path.join(ROOT, "duckdb-par
 import numpy as np  # noqa: E402
 from pqgpu import capi, gen  # noqa: E402
 
-pats = sys.argv[1:] or ["special.*requests", "ironic", "(quick|slow)ly fur", "^[a-z ]+$"]
+pats = sys.argv[1:] or ["special.*requests", "^(carefully|quickly) ", "[0-9]", "e"]
 ctx = capi.Context(0)
+for kv in filter(None, os.environ.get("PQ_OPTS", "").split(",")):  # e.g. PQ_OPTS=regex_debug=1
+    k, v = kv.split("=")
+    ctx.set_option(k, int(v))
 f = gen.build(gen.c3_cols(), 10_000_000, 1, seed=gen.CONFIG_SEEDS["C3"])
 F = capi.File(f)
 dc = ctx.upload(f, [F.chunk(0, 0)])

@@ -115,3 +115,39 @@ def test_cli_regex_matches_golden(tmp_path):
     r = run("pqgpu_parser", path)
     assert r.returncode == 0 and b"comment (BYTE_ARRAY" in r.stdout
     assert r.stdout.count(b"\npage ") == len(pidx)
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_read_column_sharded_over_devices(mixed, k):
+    """ParquetReader::read_column(name, devices): every row group's chunk cut
+    into k byte-balanced page ranges, one host thread per Device (here k
+    contexts on the box's GPU(s)); == the oracle's read_column."""
+    f, path, cols = mixed
+    for ci, c in enumerate(cols):
+        r = run("api_check", path, "sharded", c.name, str(k))
+        assert r.returncode == 0, r.stderr
+        assert r.stdout == oracle_read_column(f, file_chunks(f, ci))[2], c.name
+
+
+def test_read_column_sharded_error_matches(tmp_path):
+    f, ch = B.build_file([B.data_header(9, 2, 0) + struct.pack("<I", 2) + b"ab" + b"\x09\x00\x00"],
+                         gen.BYTE_ARRAY, False, 2)
+    path = str(tmp_path / "bad.parquet")
+    with open(path, "wb") as fh:
+        fh.write(f)
+    rc, msg, _ = oracle_read_column(f, [ch])
+    r = run("api_check", path, "sharded", "c", "2")
+    assert r.returncode == 1
+    assert r.stderr.decode().strip() == msg
+
+
+def test_read_column_sharded_c2(tmp_path):
+    cols = gen.c2_cols()
+    n = 1_000_000
+    f = gen.build(cols, n, 1, seed=gen.CONFIG_SEEDS["C2"], layout=gen.ARROW_LAYOUT)
+    path = str(tmp_path / "c2.parquet")
+    with open(path, "wb") as fh:
+        fh.write(f)
+    r = run("api_check", path, "sharded", cols[0].name, "4")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == gen.values_dump(cols[0], 0, n, 0, gen.CONFIG_SEEDS["C2"])

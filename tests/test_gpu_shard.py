@@ -100,3 +100,46 @@ def test_empty_and_single_page_ranges(ctx):
     assert b"".join(dumps) == exp
     with pytest.raises(capi.PqError):
         ctx.upload_range(f, ch, table, 0, ndata + 1)
+
+
+@pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT])
+def test_two_threads_two_contexts(layout):
+    """Two host threads, each driving its own context (one per device in a
+    multi-GPU run; both on this box's GPU here), decode alternate page ranges
+    of one chunk concurrently, several rounds; the joined shards == the whole
+    chunk (generator's oracle-pinned dump)."""
+    import threading
+    cols = gen.c2_cols()
+    n = 2_000_000
+    f = gen.build(cols, n, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
+    ch = capi.File(f).chunk(0, 0)
+    rc, msg, table = capi.build_page_table(f, ch)
+    assert rc == 0, msg
+    ranges = data_page_ranges(table, 8)
+    ctxs = [capi.Context(0), capi.Context(0)]
+    out = [None] * len(ranges)
+    errs = []
+
+    def work(t):
+        try:
+            for rnd in range(3):
+                for i in range(t, len(ranges), 2):
+                    dc = ctxs[t].upload_range(f, ch, table, *ranges[i])
+                    dc.decode()
+                    d = capi.canonical_dump(dc.to_host())
+                    assert out[i] is None or out[i] == d
+                    out[i] = d
+                    dc.free()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for c in ctxs:
+        c.close()
+    assert not errs, errs
+    exp = hashlib.sha256(gen.values_dump(cols[0], 0, n, 0, gen.CONFIG_SEEDS["C2"])).hexdigest()
+    assert hashlib.sha256(b"".join(out)).hexdigest() == exp

@@ -21,8 +21,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from pqgpu import capi, gen
-from pqgpu.shard import (data_page_ranges, extract_range, page_ranges, range_rows, rank_row_groups,
-                         shard_row_offsets)
+from pqgpu.shard import (data_page_ranges, data_page_ranges_py, extract_range, page_ranges, range_rows,
+                         rank_row_groups, shard_row_offsets)
 
 
 def test_page_ranges_cover_and_balance():
@@ -41,6 +41,32 @@ def test_page_ranges_cover_and_balance():
 def test_page_ranges_degenerate():
     assert page_ranges([], 4) == [(0, 0)] * 4
     assert page_ranges([5], 2)[0][0] == 0 and page_ranges([5], 2)[-1][1] == 1
+
+
+def test_c_planner_equals_numpy_plan():
+    """pq_plan_page_ranges (the library planner ParquetReader::read_column's
+    device sharding uses) == the numpy plan, on random tables with dictionary
+    pages interleaved, empty tables and world > pages."""
+    rng = np.random.default_rng(5)
+    for trial in range(60):
+        n = int(rng.integers(0, 300))
+        table = []
+        for i in range(n):
+            dict_page = bool(rng.random() < 0.05)
+            table.append(capi.PageDesc(payload_size=int(rng.integers(0, 1 << int(rng.integers(1, 22)))),
+                                       page_type=2 if dict_page else 0))
+        for world in (1, 2, 3, 5, 8, 17, 400):
+            assert data_page_ranges(table, world) == data_page_ranges_py(table, world), (trial, world)
+    with pytest.raises(capi.PqError):
+        capi.plan_page_ranges([], 0)
+
+
+def test_c_planner_on_real_tables():
+    for name, f, ch in _cases():
+        rc, msg, table = capi.build_page_table(f, ch)
+        assert rc == 0, msg
+        for world in (2, 4, 8):
+            assert data_page_ranges(table, world) == data_page_ranges_py(table, world), name
 
 
 def test_rank_row_groups_partition():
