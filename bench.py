@@ -9,11 +9,10 @@ ColumnReader::read_all-equivalent decode of a rank's pages on the GPU
 (validity bitmap + int64 offsets + chars, all kernels), inputs resident in
 HBM.
 
-Multi-GPU: the job is ONE such column chunk of N x 10M rows in
-one row group; its data pages are split into N contiguous byte-balanced
-ranges (pqgpu.shard.data_page_ranges) and rank r uploads range r plus the
-dictionary page (pq_chunk_upload_range).  Weak scaling, no collective on the
-data path.  `python bench.py --gpus N` launches the N ranks itself
+Multi-GPU: the job is the C2 column at N x 10M rows in N row
+groups of 10M rows; rank r generates, decodes and validates row group r only
+(the global page order cut at row-group boundaries).  Weak scaling, no
+collective on the data path.  `python bench.py --gpus N` launches the N ranks itself
 (torch.distributed.run) when WORLD_SIZE is not set; the driver's own
 torch.distributed.run launch is used as is.  With N > 1 a strong-scaling
 figure (the 10M-row chunk split N ways) is reported beside it.
@@ -54,6 +53,7 @@ KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "pipe_count", 
            "ba_fused", "ba_rows", "scan", "ba_gather", "plain_spec", "plain_ba", "fixed_plain", "fixed", "plain_opt")
 REGEX_KERNELS = ("regex_dict", "regex_codes", "regex_lanes", "regex_plain", "regex_pages")
 ROWS = 10_000_000
+C3_PATTERNS = ("special.*requests", "^(carefully|quickly) ", "[0-9]", "e")
 C5_PATTERN = "^qx"  # splits C5's pages (≈7% reported): not an all-miss scan
 
 
@@ -70,17 +70,19 @@ def parse():
     ap.add_argument("--pattern", default="special.*requests")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
-    ap.add_argument("--c4-rows", type=int, default=ROWS)
+    ap.add_argument("--c4-rows", type=int, default=ROWS, help="C4 rows per row group")
+    ap.add_argument("--c4-rows-per-gpu", type=int, default=12_500_000, help="C4: 100M rows / 8 GPUs")
     ap.add_argument("--cpu-seconds", type=float, default=5.0, help="per CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: the box's CPU share (<= 16)")
     ap.add_argument("--no-c5", action="store_true")
-    ap.add_argument("--c5-rgs", type=int, default=4, help="C5 row groups of 10M rows per GPU (1B rows / 8 GPUs = 12.5)")
+    ap.add_argument("--c5-rgs", type=int, default=12, help="C5 row groups of 10M rows per GPU (1B rows / 8 GPUs = 12.5)")
     ap.add_argument("--c5-pattern", default=C5_PATTERN)
     ap.add_argument("--c5-streams", type=int, default=2,
                     help="contexts (HIP streams) the C5 row groups alternate over: one row group's "
                          "run/code kernels overlap another's write pass")
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-wide", action="store_true", help="skip the 100k-entry dictionary leg")
     ap.add_argument("--no-ext", action="store_true", help="skip the compressed / DATA_PAGE_V2 leg (SURVEY §8f rank 4)")
     ap.add_argument("--cpu-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -329,6 +331,37 @@ def cpu_baselines(args):
         dp = [p for p in rtable if p.page_type == 0][a:b]
         jobs.append((sub, ochunk(d), args.pattern, [p.first_row for p in dp],
                      [p.num_values for p in dp]))
+    # native: the reference's ColumnReader::read_all per page-range shard,
+    # values tested with the build's host DFA (regex_host.cpp, the table
+    # k_regex_plain walks), page-parallel on `threads` threads, at C3's full size
+    nrows_n = args.regex_rows
+    nf = gen.build(gen.c3_cols(), nrows_n, 1, seed=gen.CONFIG_SEEDS["C3"])
+    nch = capi.File(nf).chunk(0, 0)
+    rc, msg, ntable = capi.build_page_table(nf, nch)
+    ndata = [p for p in ntable if p.page_type == 0]
+    nshards, ncounts = [], []
+    for a, b in data_page_ranges(ntable, 8 * threads):
+        sub, d = extract_range(nf, nch, ntable, a, b)
+        nshards.append((sub, ochunk(d)))
+        ncounts.append([p.num_values for p in ndata[a:b]])
+    del nf
+    nat = {}
+    for neg in (False, True):
+        run = lambda reps: O.ref_time_regex_pages_multi(nshards, nch.type, nch.max_def_level,  # noqa: E731
+                                                        nch.max_rep_level, ncounts, args.pattern, neg,
+                                                        reps=reps, threads=threads)
+        s1, _ = run(1)
+        reps = max(1, int(args.cpu_seconds / max(s1, 1e-3)))
+        s, fl = run(reps)
+        nat["neg" if neg else "pos"] = {"value": len(ndata) * reps / s, "unit": "pages/s", "seconds": s,
+                                        "reps": reps, "reported_pages": int(fl.sum())}
+    out["regex_native"] = {**nat["pos"], "cores": threads, "kind": "reference",
+                           "neg": nat["neg"],
+                           "sample": f"C3 {nrows_n} rows ({len(ndata)} pages), pattern {args.pattern!r}: the "
+                                     "reference ColumnReader::read_all (oracle/_ref) per page-range shard, "
+                                     "values tested with the build's host DFA (regex_host.cpp) until one "
+                                     f"satisfies the predicate, {threads} threads"}
+    del nshards
     import multiprocessing as mp
     with mp.get_context("fork").Pool(threads) as pool:
         t0 = time.perf_counter()
@@ -343,24 +376,21 @@ def cpu_baselines(args):
 
 # ── legs ──────────────────────────────────────────────────────────────────
 def c2_leg(J, args, exp):
-    """The headline: rank r decodes data-page range r of one (N x rows)-row C2
-    chunk."""
+    """The headline: the (N x rows)-row C2 column as N row groups, one per
+    rank (the global page order cut at row-group boundaries); every rank
+    generates, decodes and validates only its own row group (first_rg=rank)."""
     from pqgpu import capi, gen
-    from pqgpu.shard import data_page_ranges
     layout = gen.REF_LAYOUT if args.layout == "ref" else gen.ARROW_LAYOUT
-    total_rows = args.rows * J.world
     t0 = time.perf_counter()
-    f = gen.build(gen.c2_cols(), total_rows, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout)
+    f = gen.build(gen.c2_cols(), args.rows, 1, seed=gen.CONFIG_SEEDS["C2"], layout=layout, first_rg=J.rank)
     gen_s = time.perf_counter() - t0
     ch = capi.File(f).chunk(0, 0)
     t0 = time.perf_counter()
     rc, msg, table = capi.build_page_table(f, ch)
     walk_s = time.perf_counter() - t0
     assert rc == 0, msg
-    ranges = data_page_ranges(table, J.world)
-    a, b = ranges[J.rank]
     t0 = time.perf_counter()
-    dc = J.ctx.upload_range(f, ch, table, a, b)
+    dc = J.ctx.upload(f, [ch])
     upload_s = time.perf_counter() - t0
     dc.decode()
     nrows = dc.num_rows
@@ -369,22 +399,17 @@ def c2_leg(J, args, exp):
     chars = int(dc.out.num_bytes)
     valid = None
     if not args.no_validate:
-        # this shard's rows against the generator's dump of the whole column:
-        # its byte position there from the shards before it (host scan)
-        mine = capi.canonical_dump(host)
-        sizes = J.gather(len(mine))
-        start = sum(sizes[:J.rank])
-        whole = gen.values_dump(gen.c2_cols()[0], 0, total_rows, 0, gen.CONFIG_SEEDS["C2"])
-        ok = whole[start:start + len(mine)] == mine and (J.rank != J.world - 1 or start + len(mine) == len(whole))
+        # this rank's row group against the generator's dump of it
+        ok = sha(capi.canonical_dump(host)) == sha(
+            gen.values_dump(gen.c2_cols()[0], 0, args.rows, J.rank, gen.CONFIG_SEEDS["C2"]))
         valid = all(J.gather(bool(ok)))
-        del whole, mine
     del host
     secs, kern = J.timed(dc.decode_async, dc.decode_check, args.steps, args.repeats, warmup=args.warmup)
     rows_all = J.sum_all([nrows])[0]
     med = statistics.median(secs)
     res = {"secs": secs, "median_s": med, "value": rows_all * args.steps / med, "nrows": nrows,
            "rows_all": rows_all, "nonnull": nonnull, "chars": chars, "payload": dc.payload_bytes,
-           "pages": dc.num_pages, "kern": kern, "validated": valid, "page_range": [a, b],
+           "pages": dc.num_pages, "kern": kern, "validated": valid, "row_group": J.rank,
            "gen_s": gen_s}
     if not args.no_e2e and J.rank == 0:
         # end to end from host file bytes: host page walk + image build + H2D
@@ -396,14 +421,8 @@ def c2_leg(J, args, exp):
         J.ctx.timing(True)
         J.ctx.timing_reset()
         for _ in range(3):
-            t0 = time.perf_counter()
-            if J.world == 1:  # the whole chunk: pq_chunk_upload walks it itself
-                t1 = t0
-                x = J.ctx.upload(f, [ch])
-            else:  # this rank's page range of the chunk's page table
-                rc, msg, tb = capi.build_page_table(f, ch)
-                t1 = time.perf_counter()
-                x = J.ctx.upload_range(f, ch, tb, a, b)
+            t0 = t1 = time.perf_counter()
+            x = J.ctx.upload(f, [ch])  # pq_chunk_upload walks the chunk itself
             t2 = time.perf_counter()
             x.decode()
             t3 = time.perf_counter()
@@ -415,7 +434,7 @@ def c2_leg(J, args, exp):
         res["e2e"] = {"table_ms": wm * 1e3, "upload_ms": um * 1e3, "first_decode_ms": dm * 1e3,
                       "total_ms": (wm + um + dm) * 1e3, "values_per_s": nrows / (wm + um + dm),
                       "file_bytes": len(f), "upload_phases_ms_mean": phases,
-                      "note": "from host file bytes: [N>1: pq_build_page_table] + upload (walk, planning, allocation, "
+                      "note": "from host file bytes: upload (walk, planning, allocation, "
                               "pinned H2D of the raw chunk bytes overlapped with the walk, GPU relayout) + first decode "
                               "(includes output allocation)"}
     else:
@@ -437,11 +456,21 @@ def strong_leg(J, args):
     a, b = data_page_ranges(table, J.world)[J.rank]
     dc = J.ctx.upload_range(f, ch, table, a, b)
     dc.decode()
+    valid = None
+    if not args.no_validate:
+        # this shard's dump sits in the whole column's dump after the shards before it
+        mine = capi.canonical_dump(dc.to_host())
+        sizes = J.gather(len(mine))
+        start = sum(sizes[:J.rank])
+        whole = gen.values_dump(gen.c2_cols()[0], 0, args.rows, 0, gen.CONFIG_SEEDS["C2"])
+        ok = whole[start:start + len(mine)] == mine and (J.rank != J.world - 1 or start + len(mine) == len(whole))
+        valid = all(J.gather(bool(ok)))
+        del whole, mine
     secs, kern = J.timed(dc.decode_async, dc.decode_check, args.steps, args.repeats, warmup=args.warmup)
     dc.free()
     med = statistics.median(secs)
-    return {"rows_total": args.rows, "ms_per_step": med / args.steps * 1e3,
-            "values_per_s": args.rows * args.steps / med, "scaling": "strong"}
+    return {"rows_total": args.rows, "ms_per_step": med / args.steps * 1e3, "page_range_rank0": J.gather([a, b])[0],
+            "values_per_s": args.rows * args.steps / med, "scaling": "strong", "validated": valid}
 
 
 def c3_legs(J, args, exp):
@@ -460,11 +489,16 @@ def c3_legs(J, args, exp):
     npages = rdc.num_pages
     rkern = next((k for k in ("regex_plain", "regex_lanes", "regex_pages") if k in kern), None)
     kms = kern[rkern]["ms_per_launch"] if rkern else None
-    e = exp.get(f"c3|{rows}|{args.pattern}") if J.rank == 0 else None
+    def check(fl, pat, neg):
+        e = exp.get(f"c3|{rows}|rg{J.rank}|{pat}|{int(neg)}")
+        ok = (sha(fl.astype("u1").tobytes()) == e["sha256"]) if e else None
+        oks = J.gather(ok)
+        return None if any(o is None for o in oks) else all(oks)
+
     regex = {"pages_per_s": npages * rsteps * J.world / med, "pages_per_gpu": npages,
              "ms_per_scan": med / rsteps * 1e3, "repeats_ms": [s / rsteps * 1e3 for s in secs],
              "pattern": args.pattern, "reported_pages": int(flags.sum()),
-             "validated": (sha(flags.astype("u1").tobytes()) == e["sha256"]) if e else None,
+             "validated": check(flags, args.pattern, False),
              "kernel": rkern, "kernel_ms": kms,
              "payload_GBs": rdc.payload_bytes / (kms * 1e-3) / 1e9 if kms else None,
              "roofline_frac": rdc.payload_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS if kms else None}
@@ -488,6 +522,22 @@ def c3_legs(J, args, exp):
                         "payload_bytes": rdc.payload_bytes,
                         "note": "from host file bytes: pq_chunk_upload (speculative page walk, device planning, "
                                 "allocation, pinned multi-buffered H2D) + one regex scan incl. pattern compile"}
+    # the four patterns, each with and without --neg-regex,
+    # timed and checked against the oracle's page sets (make_bench_expect.py)
+    sweep = {}
+    for pat in C3_PATTERNS:
+        for neg in (False, True):
+            fl = rdc.regex_pages(pat, neg)
+            st = lambda p=pat, n=neg: rdc.regex_pages_async(p, n)  # noqa: E731
+            secs, kern = J.timed(st, rdc.regex_pages_result, rsteps, 3, warmup=1, kernels=REGEX_KERNELS)
+            med = statistics.median(secs)
+            k = next((k for k in ("regex_plain", "regex_lanes", "regex_pages") if k in kern), None)
+            sweep[f"{pat}{' (neg)' if neg else ''}"] = {
+                "pages_per_s": npages * rsteps * J.world / med, "ms_per_scan": med / rsteps * 1e3,
+                "kernel": k, "kernel_ms": kern[k]["ms_per_launch"] if k else None,
+                "reported_pages": int(fl.sum()), "validated": check(fl, pat, neg)}
+    regex["patterns"] = sweep
+    regex["all_validated"] = all(v["validated"] for v in sweep.values()) and bool(regex["validated"])
     # C3 PLAIN decode on the same upload
     dsteps = max(3, args.steps // 2)
     rdc.decode()
@@ -530,57 +580,135 @@ def c3_legs(J, args, exp):
     return regex, c3d
 
 
+def _rows_slice(h, r0: int, r1: int):
+    """Rows [r0, r1) of a host column (offsets rebased)."""
+    from pqgpu import capi
+    if h.offsets is not None:
+        o = h.offsets[r0:r1 + 1]
+        return capi.HostColumn(h.type, h.validity[r0:r1], h.data[o[0]:o[-1]], o - o[0])
+    w = len(h.data) // max(h.num_rows, 1)
+    return capi.HostColumn(h.type, h.validity[r0:r1], h.data[r0 * w:r1 * w], None)
+
+
 def c4_leg(J, args):
+    """the 8-column mixed file at --c4-rows-per-gpu x N rows
+    (100M at N = 8) in row groups of --c4-rows rows, data pages sharded across
+    the ranks: rank r owns the pages whose first row falls in its row range
+    (shard.row_page_range; ranges cross row-group boundaries), generates only
+    the row groups those pages live in and uploads each column's pages with
+    pq_chunk_upload_range.  Validation: every touched row group decoded whole
+    against the generator's dump, and every shard against its rows of that."""
     from pqgpu import capi, gen
-    rows = args.c4_rows
+    from pqgpu.shard import row_page_range
     cols = gen.c4_cols()
-    cfile = gen.build(cols, rows, 1, seed=gen.CONFIG_SEEDS["C4"], layout=gen.ARROW_LAYOUT, first_rg=J.rank)
-    CF = capi.File(cfile)
-    out, total_ms, ok = {}, 0.0, True
-    steps = max(3, args.steps // 4)
-    for ci, col in enumerate(cols):
-        cdc = J.ctx.upload(cfile, [CF.chunk(0, ci)])
-        cdc.decode()
-        if not args.no_validate:
-            ok &= sha(capi.canonical_dump(cdc.to_host())) == sha(
-                gen.values_dump(col, ci, rows, J.rank, gen.CONFIG_SEEDS["C4"]))
-        secs, kern = J.timed(cdc.decode_async, cdc.decode_check, steps, args.repeats, warmup=2)
-        cdc.free()
-        ms = statistics.median(secs) / steps * 1e3
-        out[col.name] = {"ms": ms, "kernels_ms": {k: v["ms_per_step"] for k, v in kern.items()}}
-        total_ms += ms
-    # the whole row group: its 8 column chunks alternated over --c5-streams
-    # contexts (HIP streams), all queued before any check, so latency-bound
-    # kernels of one column overlap bandwidth-bound ones of another
+    seed = gen.CONFIG_SEEDS["C4"]
+    rg_rows, per_gpu = args.c4_rows, args.c4_rows_per_gpu
+    total = per_gpu * J.world
+    lo, hi = per_gpu * J.rank, per_gpu * (J.rank + 1)
     ctxs = [J.ctx] + [capi.Context(J.local) for _ in range(max(1, args.c5_streams) - 1)]
-    cdcs = [ctxs[ci % len(ctxs)].upload(cfile, [CF.chunk(0, ci)]) for ci in range(len(cols))]
-    for ci, cdc in enumerate(cdcs):
-        cdc.decode()
-        if not args.no_validate:
-            ok &= sha(capi.canonical_dump(cdc.to_host())) == sha(
-                gen.values_dump(cols[ci], ci, rows, J.rank, gen.CONFIG_SEEDS["C4"]))
+    pieces = {ci: [] for ci in range(len(cols))}  # column -> its shard pieces (device chunks)
+    ok = True
+    nrg = 0
+    for g in range(lo // rg_rows, (hi - 1) // rg_rows + 1):
+        n_g = min(rg_rows, total - g * rg_rows)
+        f = gen.build(cols, n_g, 1, seed=seed, layout=gen.ARROW_LAYOUT, first_rg=g)
+        F = capi.File(f)
+        nrg += 1
+        for ci, col in enumerate(cols):
+            ch = F.chunk(0, ci)
+            rc, msg, table = capi.build_page_table(f, ch)
+            assert rc == 0, msg
+            a, b = row_page_range(table, g * rg_rows, lo, hi)
+            if a == b:
+                continue
+            dc = ctxs[ci % len(ctxs)].upload_range(f, ch, table, a, b)
+            dc.decode()
+            if not args.no_validate:
+                whole = J.ctx.upload(f, [ch])
+                whole.decode()
+                h = whole.to_host()
+                whole.free()
+                ok &= sha(capi.canonical_dump(h)) == sha(gen.values_dump(col, ci, n_g, g, seed))
+                r0 = dc.first_row
+                ok &= capi.canonical_dump(dc.to_host()) == capi.canonical_dump(_rows_slice(h, r0, r0 + dc.num_rows))
+                del h
+            pieces[ci].append(dc)
+        del f, F
+    steps = max(3, args.steps // 4)
+    out, total_ms = {}, 0.0
+    for ci, col in enumerate(cols):
+        ps = pieces[ci]
+        st = lambda ps=ps: [p.decode_async() for p in ps]  # noqa: E731
+        ck = lambda ps=ps: [p.decode_check() for p in ps]  # noqa: E731
+        secs, kern = J.timed(st, ck, steps, args.repeats, warmup=2)
+        ms = statistics.median(secs) / steps * 1e3
+        out[col.name] = {"ms": ms, "pieces": len(ps), "kernels_ms": {k: v["ms_per_step"] for k, v in kern.items()}}
+        total_ms += ms
+    # the rank's whole share: every column's pieces alternated over
+    # --c5-streams contexts (HIP streams), all queued before any check, so
+    # latency-bound kernels of one column overlap bandwidth-bound ones of another
+    alld = [p for ci in pieces for p in pieces[ci]]
 
     def rg_step():
-        for cdc in cdcs:
-            cdc.decode_async()
+        for p in alld:
+            p.decode_async()
 
     def rg_check():
-        for cdc in cdcs:
-            cdc.decode_check()
+        for p in alld:
+            p.decode_check()
 
     secs, _ = J.timed(rg_step, rg_check, steps, args.repeats, warmup=2)
-    for cdc in cdcs:
-        cdc.free()
+    nvals = sum(p.num_rows for p in alld)
+    nvals_all = J.sum_all([nvals])[0]
+    for p in alld:
+        p.free()
     for c in ctxs[1:]:
         c.close()
-    rg_ms = statistics.median(secs) / steps * 1e3
-    return {"values_per_s": 8 * rows * J.world / (rg_ms * 1e-3), "rows_per_gpu": rows,
-            "ms_per_row_group": rg_ms, "streams": len(ctxs),
-            "serial_ms_per_row_group": total_ms, "serial_values_per_s": 8 * rows * J.world / (total_ms * 1e-3),
-            "note": "values_per_s: the row group's 8 columns decoded together over `streams` contexts; "
-                    "serial_*: the sum of the columns timed one at a time (per-column times in `columns`)",
-            "columns": out, "layout": "arrow",
+    ms = statistics.median(secs) / steps * 1e3
+    return {"values_per_s": nvals_all / (ms * 1e-3), "rows_per_gpu": nvals // len(cols), "row_groups_touched": nrg,
+            "rows_total": total, "row_group_rows": rg_rows, "ms_per_step": ms, "streams": len(ctxs),
+            "serial_ms": total_ms, "serial_values_per_s": nvals_all / (total_ms * 1e-3),
+            "note": "values_per_s: the rank's page shards of all 8 columns decoded together over `streams` contexts "
+                    "(max over ranks); serial_*: the sum of the columns timed one at a time (`columns`)",
+            "columns": out, "layout": "arrow", "sharding": "data pages by global first row (row_page_range)",
             "validated": None if args.no_validate else all(J.gather(bool(ok)))}
+
+
+def wide_dict_leg(J, args):
+    """the C2 column shape with a 100,000-entry dictionary
+    (1.0 MB dictionary page: pyarrow's 1 MiB dictionary_pagesize_limit,
+    17-bit indices, 20,000-row pages), 10M rows per rank (row group = rank).
+    Decode timed and checked against the generator's dump; roofline on the
+    whole step's algorithmic bytes (payload in, column out)."""
+    from pqgpu import capi, gen
+    col = gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.05, dict_size=100_000,
+                  len_min=4, len_max=9, max_run=16)
+    rows = args.rows
+    f = gen.build([col], rows, 1, seed=gen.CONFIG_SEEDS["C2"], layout=gen.ARROW_LAYOUT, first_rg=J.rank)
+    ch = capi.File(f).chunk(0, 0)
+    dc = J.ctx.upload(f, [ch])
+    del f
+    dc.decode()
+    h = dc.to_host()
+    ok = None
+    if not args.no_validate:
+        ok = sha(capi.canonical_dump(h)) == sha(gen.values_dump(col, 0, rows, J.rank, gen.CONFIG_SEEDS["C2"]))
+        ok = all(J.gather(bool(ok)))
+    out_bytes = 8 * (rows + 1) + int(h.offsets[-1]) + (rows + 7) // 8
+    del h
+    steps = max(3, args.steps // 2)
+    secs, kern = J.timed(dc.decode_async, dc.decode_check, steps, args.repeats, warmup=2)
+    med = statistics.median(secs) / steps
+    b_alg = dc.payload_bytes + out_bytes
+    res = {"rows_per_gpu": rows, "dict_entries": 100_000, "dict_page_bytes": None, "pages": dc.num_pages,
+           "ms_per_decode": med * 1e3, "values_per_s": rows * J.world / med,
+           "b_alg_bytes": b_alg, "b_alg_GBs": b_alg / med / 1e9, "b_alg_frac_of_peak": b_alg / med / 1e9 / HBM_PEAK_GBS,
+           "kernel_ms": {k: v["ms_per_step"] for k, v in kern.items()}, "validated": ok}
+    pages = dc.pages()
+    if pages:
+        res["dict_page_bytes"] = int(pages[0].payload_size)
+    dc.free()
+    return res
 
 
 def ext_leg(J, args):
@@ -698,8 +826,13 @@ def c5_leg(J, args, exp):
     rsec = statistics.median(rsecs) / steps
     nrows = sum(dc.num_rows for dc in dcs)
     npages = sum(dc.num_pages for dc in dcs)
-    flags = np.concatenate([dc.regex_pages(args.c5_pattern) for dc in dcs])
-    e = exp.get(f"c5|{rows}x{args.c5_rgs}|{args.c5_pattern}") if J.rank == 0 else None
+    per_rg = [dc.regex_pages(args.c5_pattern) for dc in dcs]
+    flags = np.concatenate(per_rg)
+    es = [exp.get(f"c5|{rows}|rg{rg0 + i}|{args.c5_pattern}") for i in range(len(dcs))]
+    rx_ok = None if any(e is None for e in es) else all(
+        sha(fl.astype("u1").tobytes()) == e["sha256"] for fl, e in zip(per_rg, es))
+    rx_oks = J.gather(rx_ok)
+    rx_ok = None if any(o is None for o in rx_oks) else all(rx_oks)
     for dc in dcs:
         dc.free()
     for c in ctxs[1:]:
@@ -709,7 +842,7 @@ def c5_leg(J, args, exp):
             "decode_values_per_s": nrows * J.world / dsec, "decode_ms": dsec * 1e3,
             "regex_pages_per_s": npages * J.world / rsec, "regex_ms": rsec * 1e3, "pattern": args.c5_pattern,
             "reported_pages": int(flags.sum()),
-            "regex_validated": (sha(flags.astype("u1").tobytes()) == e["sha256"]) if e else None,
+            "regex_validated": rx_ok,
             "decode_validated": None if args.no_validate else all(J.gather(bool(ok))),
             "step_values_per_s": nrows * J.world / (dsec + rsec),
             "kernel_ms_note": "HIP events of the first context's row groups only",
@@ -780,10 +913,10 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (deterministic splitmix64 generator, SURVEY §8d C2 shape)",
-        "config": {"workload": f"C2: dict BYTE_ARRAY OPTIONAL, {args.rows} rows/GPU as page-range shards of one "
-                               f"{args.rows * world}-row chunk, {args.layout}-layout, 1000-entry dict, 5% NULL",
-                   "rows_per_gpu": nrows, "pages_per_gpu": c2["pages"], "page_range_rank0": c2["page_range"],
-                   "parallelism": f"page-range shards x{world} (no collective)"},
+        "config": {"workload": f"C2: dict BYTE_ARRAY OPTIONAL, {args.rows} rows/GPU (one row group per rank of an "
+                               f"{args.rows * world}-row column), {args.layout}-layout, 1000-entry dict, 5% NULL",
+                   "rows_per_gpu": nrows, "pages_per_gpu": c2["pages"],
+                   "parallelism": f"row-group shards x{world} (no collective)"},
         "timing": {"repeats_ms_per_step": [s / args.steps * 1e3 for s in c2["secs"]],
                    "statistic": f"median of {args.repeats} regions of {args.steps} steps, max over ranks"},
         "validated": c2["validated"],
@@ -811,6 +944,8 @@ def main():
         result["c4"] = c4_leg(J, args)
     if not args.no_c5:
         result["c5"] = c5_leg(J, args, exp)
+    if not args.no_wide:
+        result["wide_dict"] = wide_dict_leg(J, args)
     if not args.no_ext:
         result["ext"] = ext_leg(J, args)
     if cpu is not None:

@@ -68,6 +68,7 @@ struct pq_ctx {
     bool opt_regex_dfa = true;   // "regex_dfa": DFA kernels (else the NFA kernel)
     bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
     bool opt_regex_codes = true; // "regex_codes": dictionary chunks on the pipe path: match bits over the decode's codes
+    bool opt_regex_reuse = true; // "regex_reuse": ... reusing the codes of an earlier checked decode of the chunk
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
@@ -112,6 +113,10 @@ struct pq_chunk {
     uint64_t* d_entries = nullptr;
     int64_t nentries = 0;
     uint32_t max_dict_bytes = 0;        // largest dictionary payload
+    // dictionary pages too large for k_dict_index's LDS (launch_dict_big)
+    struct BigDict { int di; pqk::DevDict d; size_t cand_off, scr_off; };
+    std::vector<BigDict> hbigd;
+    uint8_t* d_bigd = nullptr;          // their scratch
     uint32_t max_page_bytes = 0;        // largest data-page payload
     int32_t* d_dict_count = nullptr;
     DevErr* d_page_err = nullptr;
@@ -128,6 +133,10 @@ struct pq_chunk {
     uint2* d_runs = nullptr;
     uint32_t* d_info = nullptr;
     uint16_t* d_codes = nullptr;
+    // the per-row codes (and dictionary entry table) depend only on the
+    // chunk's bytes: once a pipe pass that wrote them was checked error-free
+    // (collect), regex scans read them instead of recomputing
+    bool codes_pending = false, codes_ok = false;
     int32_t* d_tile_nn = nullptr;
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
@@ -369,6 +378,7 @@ void free_chunk_device(pq_chunk* c) {
         c->d_flist = nullptr;
     }
     dfree(c->d_flags);
+    dfree(c->d_bigd);
     dfree(c->d_row_codes);
     dfree(c->d_tile_chars);
     dfree(c->d_tile_rank);
@@ -779,6 +789,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_debug") == 0) { ctx->opt_regex_debug = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
+    if (std::strcmp(key, "regex_reuse") == 0) { ctx->opt_regex_reuse = value != 0; return 0; }
     if (std::strcmp(key, "zflip") == 0) { ctx->opt_zflip = value != 0; return 0; }
     if (std::strcmp(key, "write_waves") == 0) {
         if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "write_waves: 1..16");
@@ -1136,6 +1147,20 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             rc |= dalloc(&c->d_flags, 4);
         }
         if (c->pipe && !hdicts.empty()) rc |= dalloc(&c->d_dflag, 1);
+        {
+            size_t off = 0;
+            for (size_t i = 0; i < hdicts.size(); i++) {
+                const uint32_t sz = static_cast<uint32_t>(std::max(hdicts[i].size, 0));
+                if (static_cast<uint64_t>(sz) + 32 <= pqk::kDictLdsCap) continue;
+                const size_t nsl = pqk::dict_big_slices(sz);
+                pq_chunk::BigDict b{static_cast<int>(i), hdicts[i], off, 0};
+                off += (nsl * pqk::kPCandDHost * sizeof(uint2) + 255) / 256 * 256;
+                b.scr_off = off;
+                off += ((3 * nsl + 4) * sizeof(uint32_t) + 255) / 256 * 256;
+                c->hbigd.push_back(b);
+            }
+            if (off) rc |= dalloc(&c->d_bigd, off);
+        }
         rc |= dalloc(&c->d_tile_chars, htiles.size());
         if (c->fixed_plain || c->plain_opt) {
             rc |= dalloc(&c->d_tile_rank, htiles.size());
@@ -1624,6 +1649,18 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
 // With dict_in_runs the dictionary pages decode in k_pipe_runs' leading
 // workgroups (same launch, main stream: ordered after the previous decode's
 // readers of the entry table, no side-stream events).
+// k_dict_index for every dictionary page of a BYTE_ARRAY chunk, and the
+// multi-workgroup index for pages too large for its LDS.
+static void launch_dicts(pq_chunk* c, hipStream_t s, int32_t* err_any) {
+    pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, err_any,
+                           c->max_dict_bytes);
+    for (const auto& b : c->hbigd)
+        pqk::launch_dict_big(s, c->d_bytes + b.d.off, static_cast<uint32_t>(b.d.size), static_cast<uint32_t>(std::max(b.d.nvals, 0)),
+                             c->d_entries + b.d.entry_base, c->d_dict_count + b.di, c->d_dict_err + b.di, err_any,
+                             reinterpret_cast<uint2*>(c->d_bigd + b.cand_off),
+                             reinterpret_cast<uint32_t*>(c->d_bigd + b.scr_off));
+}
+
 static bool front_path(pq_ctx* ctx, const pq_chunk* c) { return c->pipe_fr && c->d_fwins && ctx->opt_front; }
 
 static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs) {
@@ -1678,6 +1715,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     const bool plain_go = c->plain && ctx->opt_plain && !(c->plain_spec && c->spec_failed) &&
                           !(c->plain_opt && (c->popt_failed || !ctx->opt_plain_fused));
     const bool pipe_path = pipe && !plain_go;
+    if (pipe_path) c->codes_pending = true;
     if (pipe_path && c->d_zero && ctx->opt_zflip) {
         // flags, bsum and flist[0] of this decode: the other block, which the
         // previous decode's k_pipe_write cleared (else one fill)
@@ -1712,14 +1750,12 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         (void)hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0);
         {
             Timed t(ctx, "dict_index", ctx->side);
-            pqk::launch_dict_index(ctx->side, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
-                                   c->d_dict_err, c->d_dflag, c->max_dict_bytes);
+            launch_dicts(c, ctx->side, c->d_dflag);
         }
         (void)hipEventRecord(ctx->ev_join, ctx->side);
     } else if (c->ndicts && c->type == PQ_BYTE_ARRAY) {
         Timed t(ctx, "dict_index");
-        pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
-                               c->d_dict_err, c->d_flags, c->max_dict_bytes);
+        launch_dicts(c, s, c->d_flags);
     } else if (c->ndicts) {
         Timed t(ctx, "dict_entries");
         pqk::launch_dict_entries(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
@@ -1978,7 +2014,12 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         // next decode's dictionary pass may already be writing them again)
         if (c->ndicts && !c->d_dflag) (void)hipMemsetAsync(c->d_dict_err, 0, c->ndicts * sizeof(DevErr), ctx->stream);
     }
-    if (best_code) return set_err(ctx, best_code, best_msg);
+    if (best_code) {
+        c->codes_pending = false;
+        return set_err(ctx, best_code, best_msg);
+    }
+    if (c->codes_pending) c->codes_ok = true;
+    c->codes_pending = false;
     if (c->type == PQ_BYTE_ARRAY && out) {
         int64_t total = 0;
         (void)hipMemcpy(&total, c->d_total, sizeof total, hipMemcpyDeviceToHost);
@@ -2193,21 +2234,26 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
         hipStream_t s = ctx->stream;
         pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
         (void)hipMemsetAsync(c->d_flags, 0, c->zero_bytes, s);
+        const bool on_codes = c->pipe && ctx->opt_pipe && ctx->opt_regex_codes;
+        const bool reuse = on_codes && ctx->opt_regex_reuse && c->codes_ok;
         if (c->ndicts) {
-            {
+            if (!reuse) {
                 Timed t(ctx, "dict_index");
-                pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
-                                       c->d_dict_count, c->d_dict_err, c->d_flags, c->max_dict_bytes);
+                launch_dicts(c, s, c->d_flags);
             }
             Timed t(ctx, "regex_dict");
             pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
                                     c->d_dict_count, c->d_dict_match);
         }
-        if (c->pipe && ctx->opt_pipe && ctx->opt_regex_codes) {
+        if (on_codes) {
             // dictionary-first on the decode's own codes: the pattern ran on
             // every entry above; the pipe passes give each row its index
+            // (or a checked earlier decode already did)
             const pqk::PipeLaunch P = pipe_launch(ctx, c, nullptr);
-            pipe_front(ctx, c, P, false, false);
+            if (!reuse) {
+                pipe_front(ctx, c, P, false, false);
+                c->codes_pending = true;
+            }
             Timed t(ctx, "regex_codes");
             pqk::launch_pipe_match(s, P, c->d_dict_match + c->pipe_entry_base, neg, c->d_page_flags);
         } else if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {

@@ -64,6 +64,172 @@ __global__ void __launch_bounds__(kDictWaves * 64) k_dict_index(const uint8_t* _
                                  lds_cap, words);
 }
 
+// ── dictionary pages larger than LDS (k_dict_index's serial walk) ───────────
+// The fine-slice scheme of dict_index_fine over HBM, as three launches:
+//   k_dict_cand  per 256-byte slice (each wave stages 16 slices in LDS): the
+//                first kPCandD plausible entry starts among its first 64
+//                bytes and the chain from each to the slice end;
+//   k_dict_link  one workgroup: slice t is entered at slice t-1's exit (the
+//                exit of its latest continuing candidate), every slice must
+//                hold a candidate at that entry leaving where it advertised;
+//                a scan of the chosen chains' counts; anything uncertain (a
+//                failed link, a bounds error in the last chain short of the
+//                count) falls back to the serial walk here, which also gives
+//                the reference's exact error (column_reader.cpp:128-138);
+//   k_dict_fill  one lane per slice re-walks its chosen chain writing
+//                (len << 32 | pos) entries.
+constexpr uint32_t kBSlices = 16;  // slices per wave in k_dict_cand
+
+__global__ void __launch_bounds__(256) k_dict_cand(const uint8_t* __restrict__ page, uint32_t size, uint32_t nsl,
+                                                   uint2* __restrict__ cand) {
+    __shared__ uint32_t stw[4][(kBSlices * kDSlice + 16) / 4 + 2];
+    const uint32_t w = threadIdx.x / kWave, l = lane();
+    const uint32_t g = (blockIdx.x * 4 + w) * kBSlices;
+    if (g >= nsl) return;
+    uint32_t* words = stw[w];
+    const uint32_t base = g * kDSlice;  // a multiple of 256: the page is 16-byte aligned in the image
+    {
+        const uint32_t nb = min(kBSlices * kDSlice + 16, (size - base + 15) / 16 * 16 + 16) / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(page + base);
+        for (uint32_t i = l; i < nb; i += kWave) reinterpret_cast<uint4*>(words)[i] = src[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t jm = l / kPCandD, sl = l % kPCandD;
+    uint64_t mk = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kBSlices; j++) {
+        const uint32_t sc = g + j, cs = sc * kDSlice;
+        const uint32_t q = cs + l, ce = min(cs + kDSlice, size);
+        bool plaus = sc < nsl && q < ce && q + 4 <= size &&
+                     static_cast<uint64_t>(q) + 4 + lds_u32(words, min(q, size) - base) <= size;
+        if (sc == 0) plaus = l == 0;
+        const uint64_t m = __ballot(plaus);
+        if (j == jm) mk = m;
+    }
+    const uint32_t sc = g + jm;
+    for (uint32_t i = 0; i < sl; i++) mk &= mk - 1;
+    if (sc >= nsl) return;
+    uint2 rec = make_uint2(kDNone, kDNone);
+    if (mk) {
+        const uint32_t cs = sc * kDSlice, ce = min(cs + kDSlice, size);
+        const uint32_t e = static_cast<uint32_t>(__builtin_ctzll(mk));
+        uint32_t q = cs + e, cnt = 0, bad = 0;
+        while (q < ce) {
+            if (q + 4 > size) { bad = 1; break; }
+            const uint32_t len = lds_u32(words, q - base);
+            if (static_cast<uint64_t>(q) + 4 + len > size) { bad = 1; break; }
+            q += 4 + len;
+            cnt++;
+        }
+        rec = make_uint2(q, cnt | (e << 8) | (bad << 31));
+    }
+    cand[sc * kPCandD + sl] = rec;
+}
+
+// slice t's chosen chain: entry = exit advertised by slice t-1
+__device__ __forceinline__ uint32_t big_cexit(const uint2* cand, uint32_t t) {
+    const uint32_t se = (t + 1) * kDSlice;
+    uint32_t cx = kDNone;
+#pragma unroll
+    for (int k = static_cast<int>(kPCandD) - 1; k >= 0; k--) {
+        const uint2 r = cand[t * kPCandD + k];
+        if (r.x != kDNone && !(r.y >> 31) && r.x >= se && r.x < se + 64) cx = r.x;
+    }
+    return cx;
+}
+
+// scratch: cnt[nsl], ent[nsl], bef[nsl], then misc[4] (mode: 1 = fill)
+__global__ void __launch_bounds__(1024) k_dict_link(const uint8_t* __restrict__ page, uint32_t size, uint32_t n,
+                                                    uint32_t nsl, const uint2* __restrict__ cand,
+                                                    uint32_t* __restrict__ scr, uint64_t* __restrict__ out,
+                                                    int32_t* __restrict__ count, DevErr* __restrict__ err,
+                                                    int32_t* __restrict__ err_any) {
+    __shared__ uint32_t wsum[16];
+    __shared__ int all_ok;
+    __shared__ uint32_t carry, last_bad;
+    uint32_t* cnt = scr;
+    uint32_t* ent = scr + nsl;
+    uint32_t* bef = scr + 2 * nsl;
+    uint32_t* misc = scr + 3 * nsl;
+    const uint32_t t0 = threadIdx.x, w = t0 / kWave, l = lane();
+    if (t0 == 0) { all_ok = n > 0 && size > 0; carry = 0; last_bad = 0; }
+    __syncthreads();
+    for (uint32_t b = 0; b < nsl; b += blockDim.x) {
+        const uint32_t t = b + t0;
+        uint32_t c = 0;
+        if (t < nsl) {
+            const uint32_t e = t == 0 ? 0u : big_cexit(cand, t - 1);
+            const uint32_t cx = big_cexit(cand, t);
+            uint2 pr = make_uint2(kDNone, kDNone);
+#pragma unroll
+            for (uint32_t k = 0; k < kPCandD; k++) {
+                const uint2 r = cand[t * kPCandD + k];
+                if (r.x != kDNone && t * kDSlice + ((r.y >> 8) & 0x3Fu) == e) pr = r;
+            }
+            const bool lastc = t + 1 == nsl;
+            const bool ok = pr.x != kDNone && (lastc || (!(pr.y >> 31) && pr.x == cx));
+            if (!ok) all_ok = 0;
+            if (lastc) last_bad = pr.y >> 31;
+            c = ok ? (pr.y & 0xFFu) : 0u;
+            cnt[t] = c;
+            ent[t] = e;
+        }
+        const uint32_t inc = wave_incl_scan(c);
+        if (l == kWave - 1) wsum[w] = inc;
+        __syncthreads();
+        uint32_t before = carry + inc - c;
+        uint32_t tot = 0;
+        for (uint32_t v = 0; v < blockDim.x / kWave; v++) {
+            if (v < w) before += wsum[v];
+            tot += wsum[v];
+        }
+        if (t < nsl) bef[t] = before;
+        __syncthreads();
+        if (t0 == 0) carry += tot;
+        __syncthreads();
+    }
+    const uint32_t total = carry;
+    const bool fine = all_ok && !(total < n && last_bad);
+    if (w != 0) return;
+    if (fine) {
+        if (total < n) set_err(err, err_any, PQ_ERR_BUFFER, size, 4, size);
+        if (l == 0) {
+            *count = static_cast<int32_t>(min(total, n));
+            misc[0] = 1;
+        }
+        return;
+    }
+    // serial walk (wave 0, scalar loads): the reference's order and errors
+    if (l == 0) misc[0] = 0;
+    uint32_t pos = 0, k = 0;
+    for (; k < n; k++) {
+        if (static_cast<uint64_t>(pos) + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); break; }
+        const uint32_t len = suni(sload_u32(page, pos));
+        pos += 4;
+        if (static_cast<uint64_t>(pos) + len > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, len, size); break; }
+        if (l == 0) out[k] = entry_code(len, pos);
+        pos += len;
+    }
+    if (l == 0) *count = static_cast<int32_t>(k);
+}
+
+__global__ void __launch_bounds__(256) k_dict_fill(const uint8_t* __restrict__ page, uint32_t n, uint32_t nsl,
+                                                   const uint32_t* __restrict__ scr, uint64_t* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (scr[3 * nsl] != 1 || t >= nsl) return;
+    const uint32_t before = scr[2 * nsl + t];
+    if (before >= n) return;
+    const uint32_t m = min(scr[t], n - before);
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(page);
+    uint32_t q = scr[nsl + t];
+    for (uint32_t k = 0; k < m; k++) {
+        const uint32_t len = __builtin_amdgcn_alignbyte(pw[(q >> 2) + 1], pw[q >> 2], q & 3);
+        out[before + k] = entry_code(len, q + 4);
+        q += 4 + len;
+    }
+}
+
 // ── fused page decode + gather ──────────────────────────────────────────────
 //
 // On gfx9 vector loads and stores share one counter (vmcnt), so a wave that
@@ -737,7 +903,7 @@ void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts
                        uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any,
                        uint32_t max_dict_bytes) {
     if (ndicts <= 0) return;
-    constexpr uint32_t kCap = 128 * 1024;  // + 18.2 KiB static tables < 160 KiB
+    constexpr uint32_t kCap = kDictLdsCap;  // + 18.2 KiB static tables < 160 KiB
     ensure_dyn_lds(reinterpret_cast<const void*>(k_dict_index), kCap);
     uint32_t lds = std::min<uint32_t>(kCap, (max_dict_bytes + 15) / 16 * 16 + 32);
     hipLaunchKernelGGL(k_dict_index, dim3(ndicts), dim3(kDictWaves * kWave), lds, s, bytes, dicts, entries,
@@ -750,6 +916,23 @@ void set_fused_attrs() {
     ensure_dyn_lds(reinterpret_cast<const void*>(k_ba_fused<true>), 160 * 1024);
 }
 }  // namespace
+
+uint32_t dict_big_slices(uint32_t size) { return (size + kDSlice - 1) / kDSlice; }
+
+void launch_dict_big(hipStream_t s, const uint8_t* page, uint32_t size, uint32_t nvals, uint64_t* entries,
+                     int32_t* count, DevErr* err, int32_t* err_any, uint2* cand, uint32_t* scr) {
+    const uint32_t nsl = dict_big_slices(size);
+    if (nsl == 0) {
+        hipLaunchKernelGGL(k_dict_link, dim3(1), dim3(1024), 0, s, page, size, nvals, 0u, cand, scr, entries, count,
+                           err, err_any);
+        return;
+    }
+    hipLaunchKernelGGL(k_dict_cand, dim3((nsl + 4 * kBSlices - 1) / (4 * kBSlices)), dim3(256), 0, s, page, size, nsl,
+                       cand);
+    hipLaunchKernelGGL(k_dict_link, dim3(1), dim3(1024), 0, s, page, size, nvals, nsl, cand, scr, entries, count, err,
+                       err_any);
+    hipLaunchKernelGGL(k_dict_fill, dim3((nsl + 255) / 256), dim3(256), 0, s, page, nvals, nsl, scr, entries);
+}
 
 int fused_occupancy_waves(uint32_t lds_bytes_per_block, int waves_per_block) {
     int blocks = 0;

@@ -40,7 +40,7 @@ __device__ __forceinline__ uint64_t entry_code(uint32_t len, uint32_t pos) {
 // (which produce the reference's exact error).  Returns true when done.
 constexpr uint32_t kDSlice = 256;
 constexpr uint32_t kDSliceMax = 128 * 1024 / kDSlice;  // pages up to the LDS cap
-constexpr uint32_t kPCandD = 4;
+constexpr uint32_t kPCandD = kPCandDHost;
 constexpr uint32_t kDNone = 0xFFFFFFFFu;
 // candidate record: exit (18 bits) | count << 18 (7 bits) | entry << 25 (6 bits) | error << 31
 __device__ __forceinline__ uint32_t dc_exit(uint32_t r) { return r & 0x3FFFFu; }
@@ -172,8 +172,10 @@ __device__ void dict_index_block(const uint8_t* __restrict__ bytes, const DevDic
     uint64_t* out = entries + d.entry_base;
     const uint8_t* page = bytes + d.off;
 
-    if (size + 32 > lds_cap) {  // too large for LDS: serial scalar walk by wave 0
-        if (threadIdx.x >= kWave) return;
+    if (size + 32 > lds_cap) {
+        // too large for LDS: k_dict_index leaves it to launch_dict_big; other
+        // callers (never given such pages) walk it serially with wave 0
+        if (lds_cap == kDictLdsCap || threadIdx.x >= kWave) return;
         uint32_t pos = 0, k = 0;
         for (; k < n; k++) {
             if (static_cast<uint64_t>(pos) + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); break; }

@@ -260,9 +260,18 @@ struct DevBatch {
 };
 
 
+// Dictionary pages whose payload + 32 bytes exceed kDictLdsCap are skipped
+// by k_dict_index and decoded by launch_dict_big (one call per such page:
+// page = its payload in the image, entries/count/err = its slots; scratch:
+// cand dict_big_slices(size) * 4 uint2, scr 3 * slices + 4 u32).
+constexpr uint32_t kDictLdsCap = 128 * 1024;
+constexpr uint32_t kPCandDHost = 4;  // candidates per slice (dict_index.hpp kPCandD)
 void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
                        uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any,
                        uint32_t max_dict_bytes);
+uint32_t dict_big_slices(uint32_t size);
+void launch_dict_big(hipStream_t s, const uint8_t* page, uint32_t size, uint32_t nvals, uint64_t* entries,
+                     int32_t* count, DevErr* err, int32_t* err_any, uint2* cand, uint32_t* scr);
 void launch_ba_fused(hipStream_t s, const FusedLaunch& L);
 uint32_t fused_wave_bytes(uint32_t rows_cap, uint32_t stage_bytes);
 int fused_occupancy_waves(uint32_t lds_bytes_per_block, int waves_per_block);

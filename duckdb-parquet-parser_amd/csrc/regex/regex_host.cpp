@@ -660,3 +660,54 @@ extern "C" int pq_regex_match_host(const char* pattern, const uint8_t* s, size_t
     if (pqre::compile(pattern ? pattern : "", &p, &msg)) return PQ_ERR_REGEX;
     return pqre::match_host(p, s, n) ? 1 : 0;
 }
+
+// Prebuilt host DFA handle (the same table k_regex_plain walks), for the CPU
+// regex baseline (bench.py cpu_baseline: the reference ColumnReader's values
+// matched with this DFA on the host's threads).  Not used by any product
+// path.  pq_regex_host_new returns NULL for a bad pattern or an oversized DFA.
+struct pq_regex_host {
+    pqre::DevDfa h;
+    std::vector<uint8_t> img;
+};
+
+extern "C" pq_regex_host* pq_regex_host_new(const char* pattern) {
+    pqre::Program p;
+    std::string msg;
+    if (pqre::compile(pattern ? pattern : "", &p, &msg)) return nullptr;
+    auto* r = new pq_regex_host;
+    if (!pqre::build_dfa(p, &r->img)) {
+        delete r;
+        return nullptr;
+    }
+    std::memcpy(&r->h, r->img.data(), sizeof r->h);
+    return r;
+}
+
+extern "C" void pq_regex_host_free(pq_regex_host* r) { delete r; }
+
+extern "C" int pq_regex_host_match(const pq_regex_host* r, const uint8_t* s, size_t n) {
+    const pqre::DevDfa& h = r->h;
+    if (n == 0) return h.empty_string ? 1 : 0;
+    if (h.nonempty_trivial) return 1;
+    const uint8_t* tb = r->img.data() + sizeof h;
+    if (h.full) {
+        constexpr uint32_t kAcc = pqre::DFA_ACCEPT * pqre::kDfaRowBytes;
+        uint32_t e = pqre::DFA_START * pqre::kDfaRowBytes;
+        for (size_t i = 0; i < n; i++) {
+            uint16_t v;
+            std::memcpy(&v, tb + e + 2 * s[i], 2);
+            e = v;
+            if (e == kAcc) return 1;  // ACCEPT absorbs
+        }
+        uint16_t acc;
+        std::memcpy(&acc, tb + e + 512, 2);
+        return acc ? 1 : 0;
+    }
+    const uint16_t* t = reinterpret_cast<const uint16_t*>(tb);
+    uint32_t e = pqre::DFA_START;
+    for (size_t i = 0; i < n; i++) {
+        e = t[(e & 0x7FFFu) * h.nclasses + h.cls_of[s[i]]];
+        if ((e & 0x7FFFu) == pqre::DFA_ACCEPT) return 1;
+    }
+    return (e >> 15) ? 1 : 0;
+}

@@ -59,6 +59,20 @@ def data_page_ranges_py(table, world: int) -> list[tuple[int, int]]:
     return page_ranges(sizes, world)
 
 
+def row_page_range(table, chunk_first_row: int, lo: int, hi: int) -> tuple[int, int]:
+    """Data-page range [a, b) of a chunk (page table from build_page_table)
+    owned by the shard whose global rows are [lo, hi): the pages whose first
+    row, offset by the chunk's global first row, falls in [lo, hi).  Shards
+    with disjoint row ranges covering the column own every page exactly once,
+    and every rank plans its part from its own row groups' tables (C4 leg of
+    bench.py: rows balanced instead of bytes, no rank generates another's
+    row groups)."""
+    firsts = [chunk_first_row + p.first_row for p in table if p.page_type == 0]
+    a = sum(1 for x in firsts if x < lo)
+    b = sum(1 for x in firsts if x < hi)
+    return a, b
+
+
 def range_rows(table, begin: int, end: int) -> tuple[int, int]:
     """(first chunk row, row count) of data pages [begin, end)."""
     data = [p for p in table if p.page_type == 0]

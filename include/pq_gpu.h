@@ -169,7 +169,10 @@ int pq_ctx_sync(pq_ctx* ctx);
  *   "regex_dfa", "regex_plain", "regex_codes" 1 (default): DFA kernels, the
  *                 windowed kernel for dictionary-free chunks, match bits over
  *                 the pipe's codes; "regex_win" window bytes (1024..32768,
- *                 multiple of 16; 8192)
+ *                 multiple of 16; 8192); "regex_reuse" 1 (default): a scan
+ *                 of a chunk whose earlier pipe decode was checked error-free
+ *                 (pq_decode / pq_decode_check) reads that decode's codes
+ *                 instead of recomputing them
  * Diagnostics (timing studies only; outputs are not valid with bits set):
  *   "fused_debug", "regex_debug" ablation bits, "fused_prof"
  *   per-phase clocks.

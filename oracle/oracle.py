@@ -350,6 +350,49 @@ def ref_time_read_all_multi(shards, ptype: int, max_def: int, max_rep: int, reps
     return s, out.value
 
 
+def ref_time_regex_pages_multi(shards, ptype: int, max_def: int, max_rep: int, page_counts, pattern: str,
+                               neg: bool = False, reps: int = 1, threads: int = 1):
+    """Regex CPU baseline: `reps` rounds of ColumnReader::read_all over every
+    shard on `threads` threads, each page's values tested with the build's
+    host DFA (libpqgpu pq_regex_host_match) until one satisfies the
+    predicate.  page_counts[i]: shard i's data-page row counts.  Returns
+    (wall seconds, page flags)."""
+    import numpy as np
+    from pqgpu import capi
+    R = ref()
+    L = capi.lib()
+    L.pq_regex_host_new.restype = C.c_void_p
+    L.pq_regex_host_new.argtypes = [C.c_char_p]
+    L.pq_regex_host_free.argtypes = [C.c_void_p]
+    h = L.pq_regex_host_new(pattern.encode())
+    if not h:
+        raise ValueError(f"pattern {pattern!r}: no host DFA")
+    n = len(shards)
+    keep = [C.create_string_buffer(f, len(f) or 1) for f, _ in shards]
+    files = (u8p * n)(*[C.cast(k, u8p) for k in keep])
+    lens = (C.c_size_t * n)(*[len(f) for f, _ in shards])
+    nv = (C.c_int64 * n)(*[c.num_values for _, c in shards])
+    do = (C.c_int64 * n)(*[c.data_page_offset for _, c in shards])
+    dd = (C.c_int64 * n)(*[c.dictionary_page_offset or 0 for _, c in shards])
+    hd = (C.c_int32 * n)(*[1 if c.dictionary_page_offset is not None else 0 for _, c in shards])
+    first = np.concatenate([[0], np.cumsum([len(c) for c in page_counts])]).astype(np.int64)
+    cnt = np.ascontiguousarray(np.concatenate([np.asarray(c, np.int32) for c in page_counts]), dtype=np.int32)
+    flags = np.zeros(max(int(first[-1]), 1), dtype=np.uint8)
+    fn = C.cast(L.pq_regex_host_match, C.c_void_p)
+    R.pqref_time_regex_pages_multi.restype = C.c_double
+    R.pqref_time_regex_pages_multi.argtypes = [
+        C.c_int, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+        C.POINTER(C.c_int64), C.POINTER(C.c_int32), C.c_int32, C.c_int16, C.c_int16, C.c_void_p, C.c_void_p,
+        C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    try:
+        s = R.pqref_time_regex_pages_multi(n, files, lens, nv, do, dd, hd, ptype, max_def, max_rep,
+                                           first.ctypes.data, cnt.ctypes.data, fn, h, int(neg), reps, threads,
+                                           flags.ctypes.data)
+    finally:
+        L.pq_regex_host_free(h)
+    return s, flags[:int(first[-1])]
+
+
 def chunk_assign(col: Column, chunk_size: int = 4096):
     """src/main.cpp:17-32 restated (pqo_chunk_assign) over an oracle column:
     (tuple_to_chunk int64[nrows], num_chunks)."""

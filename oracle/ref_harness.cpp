@@ -320,6 +320,54 @@ double pqref_time_read_all_multi(int n, const uint8_t* const* files, const size_
     return s;
 }
 
+// Regex CPU baseline: the page-parallel read above, then
+// every page's non-null values tested with `match` (the build's host DFA,
+// pq_regex_host_match, passed in as a function pointer) until one satisfies
+// the predicate (match != neg); flags[page] = 1 if none does (the page is
+// REPORTED, README.md:54-64).  page_first[i] .. page_first[i + 1] index
+// shard i's data-page row counts in `counts`.  `reps` rounds; wall seconds.
+double pqref_time_regex_pages_multi(int n, const uint8_t* const* files, const size_t* flens,
+                                    const int64_t* num_values, const int64_t* data_off,
+                                    const int64_t* dict_off, const int32_t* has_dict, int32_t type,
+                                    int16_t max_def, int16_t max_rep, const int64_t* page_first,
+                                    const int32_t* counts, int (*match)(const void*, const uint8_t*, size_t),
+                                    const void* mstate, int neg, int reps, int threads, uint8_t* flags) {
+    std::vector<ColumnChunk> ccs;
+    for (int i = 0; i < n; i++)
+        ccs.push_back(make_chunk(num_values[i], data_off[i], dict_off[i], has_dict[i], 0, type));
+    std::atomic<int64_t> next{0};
+    const int64_t total = static_cast<int64_t>(n) * reps;
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; t++) {
+        ts.emplace_back([&] {
+            for (int64_t k = next.fetch_add(1); k < total; k = next.fetch_add(1)) {
+                const int i = static_cast<int>(k % n);
+                ColumnReader rd(memory_range(files[i], flens[i]), ccs[i], static_cast<ParquetType>(type),
+                                max_def, max_rep);
+                std::vector<Value> vals = rd.read_all();
+                size_t row = 0;
+                for (int64_t pg = page_first[i]; pg < page_first[i + 1]; pg++) {
+                    uint8_t rep = 1;
+                    const size_t end = row + static_cast<size_t>(counts[pg]);
+                    for (size_t r = row; r < end && r < vals.size(); r++) {
+                        if (vals[r].is_null) continue;
+                        const std::string& s = std::get<std::string>(vals[r].data);
+                        if ((match(mstate, reinterpret_cast<const uint8_t*>(s.data()), s.size()) != 0) != (neg != 0)) {
+                            rep = 0;
+                            break;
+                        }
+                    }
+                    flags[pg] = rep;
+                    row = end;
+                }
+            }
+        });
+    }
+    for (auto& th : ts) th.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 void pqref_free(void* p) { std::free(p); }
 
 }  // extern "C"

@@ -56,27 +56,51 @@ def entry(flags: np.ndarray) -> dict:
             "sha256": hashlib.sha256(flags.tobytes()).hexdigest()}
 
 
-def main():
+ROWS = 10_000_000
+# four patterns, each with and without --neg-regex
+C3_PATTERNS = ["special.*requests", "^(carefully|quickly) ", "[0-9]", "e"]
+C5_PATTERNS = ["^qx"]
+
+
+def c3_job(rank: int) -> dict:
+    """bench.py c3_legs on rank `rank`: its own 10M-row row group (first_rg=rank)."""
+    f = gen.build(gen.c3_cols(), ROWS, 1, seed=gen.CONFIG_SEEDS["C3"], first_rg=rank)
+    ch = capi.File(f).chunk(0, 0)
     out = {}
-    rows = 10_000_000
-    c3 = gen.build(gen.c3_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C3"])
-    ch = capi.File(c3).chunk(0, 0)
-    for pat in ("special.*requests",):
-        out[f"c3|{rows}|{pat}"] = entry(page_flags(c3, ch, pat))
-    del c3
-    c5_rgs = int(os.environ.get("C5_RGS", "4"))
-    c5 = gen.build(gen.c2_cols(), rows, c5_rgs, seed=gen.CONFIG_SEEDS["C5"], layout=gen.ARROW_LAYOUT)
-    F = capi.File(c5)
-    for pat in sys.argv[1:] or ["^qx"]:
-        fl = np.concatenate([page_flags(c5, F.chunk(rg, 0), pat) for rg in range(c5_rgs)])
-        out[f"c5|{rows}x{c5_rgs}|{pat}"] = entry(fl)
-        print(pat, out[f"c5|{rows}x{c5_rgs}|{pat}"], flush=True)
+    for pat in C3_PATTERNS:
+        for neg in (0, 1):
+            out[f"c3|{ROWS}|rg{rank}|{pat}|{neg}"] = entry(page_flags(f, ch, pat, bool(neg)))
+    return out
+
+
+def c5_job(rg: int) -> dict:
+    """bench.py c5_leg: row group `rg` of the C5 column (rank r holds row
+    groups [r * c5_rgs, (r + 1) * c5_rgs))."""
+    f = gen.build(gen.c2_cols(), ROWS, 1, seed=gen.CONFIG_SEEDS["C5"], layout=gen.ARROW_LAYOUT, first_rg=rg)
+    ch = capi.File(f).chunk(0, 0)
+    return {f"c5|{ROWS}|rg{rg}|{pat}": entry(page_flags(f, ch, pat)) for pat in C5_PATTERNS}
+
+
+def main():
+    """usage: make_bench_expect.py [ranks] [c5_rgs_per_rank] [processes]"""
+    import multiprocessing as mp
+    ranks = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    c5_rgs = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+    procs = int(sys.argv[3]) if len(sys.argv) > 3 else 6
+    jobs = [(c3_job, r) for r in range(ranks)] + [(c5_job, g) for g in range(ranks * c5_rgs)]
+    out = {}
+    with mp.get_context("fork").Pool(procs) as pool:
+        for d in pool.imap_unordered(_run, jobs):
+            out.update(d)
+            print(len(out), flush=True)
     path = os.path.join(ROOT, "tests", "golden", "bench_expect.json")
-    old = json.load(open(path)) if os.path.exists(path) else {}
-    old.update(out)
     with open(path, "w") as fh:
-        json.dump(old, fh, indent=1, sort_keys=True)
-    print(json.dumps(out, indent=1))
+        json.dump(out, fh, indent=0, sort_keys=True)
+
+
+def _run(job):
+    fn, arg = job
+    return fn(arg)
 
 
 if __name__ == "__main__":

@@ -262,7 +262,33 @@ def _opt_plain_file(nvals, seed, null_frac=0.3, lmax=30, extra=b"", drop=0, all_
     return B.build_file([B.data_header(len(pay), nvals, 0) + pay], gen.BYTE_ARRAY, True, nvals)
 
 
+def _huge_dict_file(n: int, seed: int, lmin: int = 1, lmax: int = 14, decl: int | None = None, tail: bytes = b"",
+                    cut: int = 0, nrows: int = 5000):
+    """A dictionary page beyond k_dict_index's LDS (> 128 KiB: the
+    multi-workgroup index, launch_dict_big) and one data page of indices
+    spread over the whole dictionary (17-bit codes when n > 65,536)."""
+    rng = np.random.default_rng(seed)
+    vals = [bytes(rng.integers(97, 123, size=int(rng.integers(lmin, lmax + 1)), dtype=np.uint8)) for _ in range(n)]
+    dpay = B.plain_ba(vals) + tail
+    if cut:
+        dpay = dpay[:-cut]
+    bw = max(1, int(n - 1).bit_length())
+    idx = [int(x) for x in rng.integers(0, n, size=nrows)]
+    stream = bytes([bw]) + b"".join(B.rle(1, v, bw) for v in idx)
+    return B.build_file([B.dict_header(len(dpay), n if decl is None else decl) + dpay,
+                         B.data_header(len(stream), nrows, 8) + stream], gen.BYTE_ARRAY, False, nrows,
+                        dict_at_start=True)
+
+
 CRAFTED = {
+    # dictionary pages beyond LDS: short entries (the parallel slices link),
+    # entries over 64 bytes (uncovered slice entries: the serial walk), bytes
+    # after the declared entries, 17-bit indices
+    "huge_dict_short": lambda: _huge_dict_file(40000, seed=81),
+    "huge_dict_wide": lambda: _huge_dict_file(100000, seed=82, lmin=4, lmax=9),
+    "huge_dict_long": lambda: _huge_dict_file(3000, seed=83, lmin=60, lmax=140),
+    "huge_dict_tail": lambda: _huge_dict_file(30000, seed=84, tail=b"\x07\x00\x00\x00garbage!" * 5),
+    "huge_dict_fewer_used": lambda: _huge_dict_file(30000, seed=85, decl=20000),
     # OPTIONAL PLAIN BYTE_ARRAY: a window page; a chunk-chain page whose values
     # start inside chunk 0 past its candidate range, one whose levels fill
     # several chunks; bytes after the last value (the one-pass form does not
@@ -381,6 +407,10 @@ CRAFTED = {
 }
 
 ERRORS = {
+    # dictionary pages beyond LDS: a truncated last entry; more entries
+    # declared than the page holds (the chain ends at the page end)
+    "huge_dict_truncated": lambda: _huge_dict_file(30000, seed=86, cut=3),
+    "huge_dict_short_count": lambda: _huge_dict_file(30000, seed=87, decl=30001),
     # truncated PLAIN BYTE_ARRAY value
     "truncated_plain": lambda: B.build_file([B.data_header(9, 2, 0) + struct.pack("<I", 2) + b"ab" + struct.pack("<I", 9)[:3]],
                                             gen.BYTE_ARRAY, False, 2),

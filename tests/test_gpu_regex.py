@@ -95,3 +95,54 @@ def test_regex_reports_decode_errors(ctx, kernel):
         dc.regex_pages("special", False)
     assert ei.value.code == rc_o and ei.value.msg == msg_o
     dc.free()
+
+
+@pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT])
+def test_regex_reuses_checked_decode_codes(ctx, layout):
+    """regex_reuse: after a checked decode the scan reads that decode's codes
+    (no dict/run/codes passes); page sets equal the oracle's, interleaved
+    with further decodes, and the decode's output stays correct."""
+    cols = gen.c2_cols()
+    f = gen.build(cols, 40000, 2, seed=9, layout=layout, rows_per_page=0 if layout == gen.REF_LAYOUT else 3000)
+    chunks = file_chunks(f, 0)
+    dc = ctx.upload(f, chunks)
+    pats = ["^qx", "e", "^[a-m]", "a.{3}e"]
+    exp = {(p, n): golden_pages(f, chunks, p, n) for p in pats for n in (False, True)}
+    dc.decode()
+    ref = capi.canonical_dump(dc.to_host())
+    ctx.timing(True)
+    ctx.timing_reset()
+    for p in pats:
+        for n in (False, True):
+            assert np.array_equal(dc.regex_pages(p, n), exp[(p, n)]), (p, n)
+        dc.decode_async()
+        dc.regex_pages_async(p, True)
+        assert np.array_equal(dc.regex_pages_result(), exp[(p, True)])
+    ctx.timing(False)
+    for k in ("pipe_runs", "pipe_codes", "pipe_front", "pipe_big"):
+        ms, n = ctx.timing_get(k)
+        assert n == len(pats), (k, n)  # only the decodes ran the front passes
+    assert capi.canonical_dump(dc.to_host()) == ref
+    dc.free()
+
+
+def test_regex_reuse_not_taken_after_failed_decode(ctx):
+    """A decode that failed leaves no reusable codes: the scan reports the
+    same error itself (a zero-count RLE run before any literal run, which the
+    reference rejects)."""
+    import pqbuild as B
+    dpay = B.plain_ba([b"alpha", b"", b"gamma-gamma", b"d"])
+    idx = bytes([2]) + B.rle(0, 1, 2) + B.rle(3, 1, 2)
+    f, ch = B.build_file([B.dict_header(len(dpay), 4) + dpay, B.data_header(len(idx), 3, 8) + idx],
+                         gen.BYTE_ARRAY, False, 3, dict_at_start=True)
+    rc_o, msg_o, _ = O.read_all(f, to_oracle_chunk(ch))
+    assert rc_o != 0
+    dc = ctx.upload(f, [to_desc(ch)])
+    for _ in range(2):
+        with pytest.raises(capi.PqError) as ei:
+            dc.decode()
+        assert ei.value.msg == msg_o
+        with pytest.raises(capi.PqError) as ei:
+            dc.regex_pages("a", False)
+        assert ei.value.msg == msg_o
+    dc.free()

@@ -89,3 +89,33 @@ def test_reference_harness_reproduces_manifest(name):
             assert (rc, msg) == (rec["rc"], rec["msg"])
             if rc == 0:
                 assert hashlib.sha256(dump).hexdigest() == rec["sha256"]
+
+
+@pytest.mark.skipif(not O.have_ref(), reason="reference harness not built")
+@pytest.mark.parametrize("neg", [False, True])
+def test_native_regex_baseline_matches_python_re(neg):
+    """bench.py's native regex CPU baseline (reference ColumnReader + the
+    build's host DFA, page-parallel) reports the same pages as the oracle
+    decode + Python `re` (make_bench_expect.page_flags) for the four C3
+    patterns."""
+    import sys
+    import numpy as np
+    from pqgpu import gen
+    from pqgpu.shard import data_page_ranges, extract_range
+    from util import to_oracle_chunk
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    from make_bench_expect import page_flags
+    f = gen.build(gen.c3_cols(), 60000, 1, seed=3)
+    ch = capi.File(f).chunk(0, 0)
+    rc, msg, table = capi.build_page_table(f, ch)
+    assert rc == 0, msg
+    data = [p for p in table if p.page_type == 0]
+    shards, counts = [], []
+    for a, b in data_page_ranges(table, 7):
+        sub, d = extract_range(f, ch, table, a, b)
+        shards.append((sub, to_oracle_chunk(d)))
+        counts.append([p.num_values for p in data[a:b]])
+    for pat in ("special.*requests", "^(carefully|quickly) ", "[0-9]", "e"):
+        s, fl = O.ref_time_regex_pages_multi(shards, ch.type, ch.max_def_level, ch.max_rep_level, counts, pat,
+                                             neg, reps=2, threads=3)
+        assert np.array_equal(fl, page_flags(f, ch, pat, neg)), pat

@@ -171,3 +171,28 @@ def test_gloo_two_ranks_page_shards_equal_single():
         parts = [gathered[r][name][2] for r in range(world)]
         assert all(p is not None for p in parts)
         assert b"".join(parts) == whole, name
+
+
+def test_row_page_range_partitions_pages():
+    """Ranks with disjoint row ranges covering a multi-row-group column own
+    every data page exactly once (bench.py C4 leg)."""
+    from pqgpu.shard import row_page_range
+    rg_rows = 9000
+    f = gen.build(gen.c4_cols(), rg_rows, 3, seed=4, layout=gen.ARROW_LAYOUT, rows_per_page=700)
+    F = capi.File(f)
+    for ci in (0, 3, 6, 7):
+        tables = []
+        for g in range(3):
+            rc, msg, t = capi.build_page_table(f, F.chunk(g, ci))
+            assert rc == 0, msg
+            tables.append(t)
+        for world in (1, 2, 3, 5, 8):
+            per = -(-3 * rg_rows // world)
+            owned = [0] * 3
+            for r in range(world):
+                lo, hi = per * r, min(per * (r + 1), 3 * rg_rows)
+                for g in range(3):
+                    a, b = row_page_range(tables[g], g * rg_rows, lo, hi)
+                    assert a == owned[g]  # contiguous, in rank order
+                    owned[g] = b
+            assert owned == [sum(1 for p in t if p.page_type == 0) for t in tables]
