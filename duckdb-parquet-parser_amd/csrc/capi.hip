@@ -72,6 +72,7 @@ struct pq_ctx {
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
+    bool opt_fixed_fused = false; // "fixed_fused": OPTIONAL ones scatter their values in the levels launch (slower: DESIGN §5)
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
     bool opt_plain_fused = true; // "plain_fused": their one-pass form when the pages' character counts are known
@@ -137,6 +138,7 @@ struct pq_chunk {
     // chunk's bytes: once a pipe pass that wrote them was checked error-free
     // (collect), regex scans read them instead of recomputing
     bool codes_pending = false, codes_ok = false;
+    bool entries_pending = false, entries_ok = false;  // the same for the dictionary entry table
     int32_t* d_tile_nn = nullptr;
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
@@ -798,6 +800,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     }
     if (std::strcmp(key, "big_all") == 0) { ctx->opt_big_all = value != 0; return 0; }
     if (std::strcmp(key, "fixed_plain") == 0) { ctx->opt_fixed_plain = value != 0; return 0; }
+    if (std::strcmp(key, "fixed_fused") == 0) { ctx->opt_fixed_fused = value != 0; return 0; }
     if (std::strcmp(key, "dict_pipe") == 0) { ctx->opt_pipe = value != 0; return 0; }
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
     if (std::strcmp(key, "plain_fused") == 0) { ctx->opt_plain_fused = value != 0; return 0; }
@@ -1716,6 +1719,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
                           !(c->plain_opt && (c->popt_failed || !ctx->opt_plain_fused));
     const bool pipe_path = pipe && !plain_go;
     if (pipe_path) c->codes_pending = true;
+    if (c->ndicts && c->type == PQ_BYTE_ARRAY) c->entries_pending = true;
     if (pipe_path && c->d_zero && ctx->opt_zflip) {
         // flags, bsum and flist[0] of this decode: the other block, which the
         // previous decode's k_pipe_write cleared (else one fill)
@@ -1909,7 +1913,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         Timed t(ctx, "fixed_plain");
         pqk::launch_fixed_plain(s, c->d_bytes, c->d_pages, c->npages, c->d_tiles, c->ntiles, c->d_page_tile0, cp,
                                 out->d_validity, out->d_values, c->d_tile_rank, c->d_page_pos, c->d_page_err,
-                                c->d_flags);
+                                c->d_flags, ctx->opt_fixed_fused);
     } else {
         Timed t(ctx, "fixed");
         pqk::launch_fixed(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_dict_count, cp,
@@ -2015,11 +2019,12 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         if (c->ndicts && !c->d_dflag) (void)hipMemsetAsync(c->d_dict_err, 0, c->ndicts * sizeof(DevErr), ctx->stream);
     }
     if (best_code) {
-        c->codes_pending = false;
+        c->codes_pending = c->entries_pending = false;
         return set_err(ctx, best_code, best_msg);
     }
     if (c->codes_pending) c->codes_ok = true;
-    c->codes_pending = false;
+    if (c->entries_pending) c->entries_ok = true;
+    c->codes_pending = c->entries_pending = false;
     if (c->type == PQ_BYTE_ARRAY && out) {
         int64_t total = 0;
         (void)hipMemcpy(&total, c->d_total, sizeof total, hipMemcpyDeviceToHost);
@@ -2237,7 +2242,8 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
         const bool on_codes = c->pipe && ctx->opt_pipe && ctx->opt_regex_codes;
         const bool reuse = on_codes && ctx->opt_regex_reuse && c->codes_ok;
         if (c->ndicts) {
-            if (!reuse) {
+            if (!(ctx->opt_regex_reuse && c->entries_ok)) {
+                c->entries_pending = true;
                 Timed t(ctx, "dict_index");
                 launch_dicts(c, s, c->d_flags);
             }

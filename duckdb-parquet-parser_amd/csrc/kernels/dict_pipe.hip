@@ -1644,27 +1644,46 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
 // value that matches (with --neg-regex: that fails to match) stays reported.
 // NULL rows and out-of-range indices (code 0xFFFF) never count.
 constexpr int kMatchWaves = 4;
+constexpr int kMatchBatch = 4;  // tiles whose codes a wave loads before testing any
+// Each wave takes kMatchBatch consecutive tiles per step (grid-stride), all
+// their codes loaded before the first test, so a wave keeps several 1 KiB
+// reads in flight instead of one.
 __global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match(const DevTile* __restrict__ tiles, int ntiles,
                                                                  const DevPage* __restrict__ pages,
                                                                  const uint16_t* __restrict__ codes,
                                                                  const uint8_t* __restrict__ match, int neg,
                                                                  uint8_t* __restrict__ page_flags) {
-    const int t = static_cast<int>(blockIdx.x) * kMatchWaves + static_cast<int>(threadIdx.x / kWave);
-    if (t >= ntiles) return;
-    const DevTile T = tiles[t];
-    const int64_t R0 = pages[T.page].first_row + T.row0;
-    const uint32_t m = static_cast<uint32_t>(T.nrows), l8 = lane() * 8;
-    bool hit = false;
-    if (l8 < m) {
-        const U16B v = *reinterpret_cast<const U16B*>(codes + R0 + l8);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const int nw = static_cast<int>(gridDim.x) * kMatchWaves;
+    const uint32_t l8 = lane() * 8;
+    for (int t0 = (static_cast<int>(blockIdx.x) * kMatchWaves + static_cast<int>(threadIdx.x / kWave)) * kMatchBatch;
+         t0 < ntiles; t0 += nw * kMatchBatch) {
+        U16B v[kMatchBatch];
+        uint32_t m[kMatchBatch];
+        int pg[kMatchBatch];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t c = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-            hit |= l8 + k < m && c != kNull && ((match[c] != 0) != (neg != 0));
+        for (int i = 0; i < kMatchBatch; i++) {
+            m[i] = 0;
+            pg[i] = -1;
+            v[i] = U16B{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            if (t0 + i < ntiles) {
+                const DevTile T = tiles[t0 + i];
+                pg[i] = T.page;
+                m[i] = static_cast<uint32_t>(T.nrows);
+                if (l8 < m[i]) v[i] = *reinterpret_cast<const U16B*>(codes + pages[T.page].first_row + T.row0 + l8);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kMatchBatch; i++) {
+            const uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+            bool hit = false;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t c = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                hit |= l8 + k < m[i] && c != kNull && ((match[c] != 0) != (neg != 0));
+            }
+            if (__ballot(hit) && lane() == 0) page_flags[pg[i]] = 0;
         }
     }
-    if (__ballot(hit) && lane() == 0) page_flags[T.page] = 0;
 }
 
 // ── the whole front of windows of pages of <= 512 rows ─────────────────────
@@ -2187,7 +2206,9 @@ void launch_pipe_front(hipStream_t s, const PipeLaunch& P, const DevBatch* wins,
 void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags) {
     (void)hipMemsetAsync(page_flags, 1, static_cast<size_t>(P.npages), s);
     if (P.ntiles <= 0) return;
-    hipLaunchKernelGGL(k_pipe_match, dim3((P.ntiles + kMatchWaves - 1) / kMatchWaves), dim3(kMatchWaves * kWave), 0, s,
+    const int need = (P.ntiles + kMatchWaves * kMatchBatch - 1) / (kMatchWaves * kMatchBatch);
+    const int grid = max(1, min(need, 8 * max(P.cus, 1)));
+    hipLaunchKernelGGL(k_pipe_match, dim3(grid), dim3(kMatchWaves * kWave), 0, s,
                        P.tiles, P.ntiles, P.pages, P.codes, match, neg, page_flags);
 }
 

@@ -178,6 +178,15 @@ __device__ void levels_serial(const uint8_t* __restrict__ bytes, const DevPage* 
     if (lane() == 0 && page_nn) page_nn[p] = static_cast<int32_t>(nn);
 }
 
+// The page's tiles scattered by the workgroup that decoded its levels (its
+// validity words, tile ranks and value start are in HBM; the barrier orders
+// them).  Nothing is read past a page whose values overrun it.
+__device__ __forceinline__ void fused_scatter(const uint8_t* __restrict__ bytes, const DevPage* __restrict__ pages, int p,
+                                              const int32_t* __restrict__ page_tile0, const DevTile* __restrict__ tiles,
+                                              ColumnParams cp, const uint32_t* validity, const int32_t* tile_rank,
+                                              const int32_t* page_pos, const DevErr* page_err,
+                                              uint8_t* __restrict__ values);
+
 // One workgroup (8 waves) per page: the page's level bytes staged in LDS,
 // one lane walks the def stream into an LDS run table (run_walk.hpp), then
 // the waves expand 512-row tiles in parallel (max-scan over run starts, rows
@@ -191,6 +200,9 @@ constexpr uint32_t kLvTiles = 128;
 constexpr uint32_t kLvSpecMax = 4096;  // level sections up to this size: run_spec.hpp (workgroup) instead of one lane
 constexpr uint32_t kLvSpecList = kLvSpecMax / 2 / kSpJump + 8;
 
+// kScatter: the PLAIN fixed-width values too (k_fixed_scatter's work for the
+// page's tiles, after its levels), one launch instead of two.
+template <bool kScatter>
 __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* __restrict__ bytes,
                                                                 const DevPage* __restrict__ pages,
                                                                 const int32_t* __restrict__ page_tile0,
@@ -199,7 +211,9 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
                                                                 int32_t* __restrict__ page_pos,
                                                                 int32_t* __restrict__ page_nn,
                                                                 DevErr* __restrict__ page_err,
-                                                                int32_t* __restrict__ err_any) {
+                                                                int32_t* __restrict__ err_any,
+                                                                const DevTile* __restrict__ tiles,
+                                                                uint8_t* __restrict__ values) {
     __shared__ __attribute__((aligned(16))) uint32_t stage[kLvStage / 4 + 8];
     __shared__ uint2 rec[kLvRec];
     __shared__ __attribute__((aligned(16))) uint16_t mark_all[kLvWaves][kTileRows];
@@ -275,6 +289,7 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
         if (wv == 0)
             levels_serial(bytes, pages, p, page_tile0, cp, validity, tile_rank, page_pos, page_nn, page_err, err_any,
                           lits, reinterpret_cast<uint32_t*>(mark_all[1]));
+        if (kScatter) fused_scatter(bytes, pages, p, page_tile0, tiles, cp, validity, tile_rank, page_pos, page_err, values);
         return;
     }
     const uint32_t nrec = sh[1];
@@ -367,25 +382,18 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
         if (lane() == 0) page_pos[p] = static_cast<int32_t>(pos);
         if (lane() == 0 && page_nn) page_nn[p] = static_cast<int32_t>(carry);
     }
+    if (kScatter) fused_scatter(bytes, pages, p, page_tile0, tiles, cp, validity, tile_rank, page_pos, page_err, values);
 }
 
-__global__ void __launch_bounds__(256) k_fixed_scatter(const uint8_t* __restrict__ bytes,
-                                                       const DevPage* __restrict__ pages,
-                                                       const DevTile* __restrict__ tiles, int ntiles,
-                                                       uint32_t pw, const uint32_t* __restrict__ validity_in,
-                                                       const int32_t* __restrict__ tile_rank,
-                                                       const int32_t* __restrict__ page_pos,
-                                                       const DevErr* __restrict__ page_err,
-                                                       uint8_t* __restrict__ values) {
-    const int t = blockIdx.x * kTilesPerBlock + static_cast<int>(threadIdx.x / kWave);
-    if (t >= ntiles) return;
-    const DevTile T = tiles[t];
-    if (page_err[T.page].code) return;  // the decode fails; nothing may be read past the page
+// Tile t's rows: NULL rows zero, row j of rank k copies value k of the page
+// (k_fixed_scatter, and the fused tail of k_fixed_levels2<.., true>).
+__device__ __forceinline__ void scatter_tile(const uint8_t* __restrict__ bytes, const DevPage* __restrict__ pages,
+                                             const DevTile& T, uint32_t pw, const uint32_t* __restrict__ validity_in,
+                                             uint32_t rank, uint32_t pos, uint8_t* __restrict__ values) {
     const DevPage pg = pages[T.page];
-    const uint8_t* src = bytes + pg.off + static_cast<uint32_t>(page_pos[T.page]);
+    const uint8_t* src = bytes + pg.off + pos;
     const uint32_t m = static_cast<uint32_t>(T.nrows);
     const int64_t R0 = pg.first_row + T.row0;
-    uint32_t rank = static_cast<uint32_t>(tile_rank[t]);
     for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
         const uint32_t j = j0 + lane();
         const int64_t R = R0 + j;
@@ -409,12 +417,47 @@ __global__ void __launch_bounds__(256) k_fixed_scatter(const uint8_t* __restrict
     }
 }
 
+__global__ void __launch_bounds__(256) k_fixed_scatter(const uint8_t* __restrict__ bytes,
+                                                       const DevPage* __restrict__ pages,
+                                                       const DevTile* __restrict__ tiles, int ntiles,
+                                                       uint32_t pw, const uint32_t* __restrict__ validity_in,
+                                                       const int32_t* __restrict__ tile_rank,
+                                                       const int32_t* __restrict__ page_pos,
+                                                       const DevErr* __restrict__ page_err,
+                                                       uint8_t* __restrict__ values) {
+    const int t = blockIdx.x * kTilesPerBlock + static_cast<int>(threadIdx.x / kWave);
+    if (t >= ntiles) return;
+    const DevTile T = tiles[t];
+    if (page_err[T.page].code) return;  // the decode fails; nothing may be read past the page
+    scatter_tile(bytes, pages, T, pw, validity_in, static_cast<uint32_t>(tile_rank[t]),
+                 static_cast<uint32_t>(page_pos[T.page]), values);
+}
+
+__device__ __forceinline__ void fused_scatter(const uint8_t* __restrict__ bytes, const DevPage* __restrict__ pages, int p,
+                                              const int32_t* __restrict__ page_tile0, const DevTile* __restrict__ tiles,
+                                              ColumnParams cp, const uint32_t* validity, const int32_t* tile_rank,
+                                              const int32_t* page_pos, const DevErr* page_err,
+                                              uint8_t* __restrict__ values) {
+    __syncthreads();  // (workgroup fence: this workgroup's validity, ranks and value start)
+    if (page_err[p].code) return;
+    const DevPage pg = pages[p];
+    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    const int32_t t0 = page_tile0[p];
+    const uint32_t nt = (n + kTileRows - 1) / kTileRows;
+    const uint32_t pw = static_cast<uint32_t>(cp.plain_width);
+    const uint32_t pos = static_cast<uint32_t>(page_pos[p]);
+    for (uint32_t i = threadIdx.x / kWave; i < nt; i += blockDim.x / kWave) {
+        const int32_t t = t0 + static_cast<int32_t>(i);
+        scatter_tile(bytes, pages, tiles[t], pw, validity, static_cast<uint32_t>(tile_rank[t]), pos, values);
+    }
+}
+
 }  // namespace
 
 void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,
                         int ntiles, const int32_t* page_tile0, ColumnParams cp, uint32_t* validity,
                         uint8_t* values, int32_t* tile_rank, int32_t* page_pos, DevErr* page_err,
-                        int32_t* err_any) {
+                        int32_t* err_any, bool fused) {
     if (ntiles <= 0) return;
     const uint32_t pw = static_cast<uint32_t>(cp.plain_width);
     const int tb = (ntiles + kTilesPerBlock - 1) / kTilesPerBlock;
@@ -423,8 +466,15 @@ void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* page
                            validity, values, page_err, err_any);
         return;
     }
-    hipLaunchKernelGGL(k_fixed_levels2, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0, cp,
-                       validity, tile_rank, page_pos, static_cast<int32_t*>(nullptr), page_err, err_any);
+    if (fused) {
+        hipLaunchKernelGGL(k_fixed_levels2<true>, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0,
+                           cp, validity, tile_rank, page_pos, static_cast<int32_t*>(nullptr), page_err, err_any, tiles,
+                           values);
+        return;
+    }
+    hipLaunchKernelGGL(k_fixed_levels2<false>, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0, cp,
+                       validity, tile_rank, page_pos, static_cast<int32_t*>(nullptr), page_err, err_any,
+                       static_cast<const DevTile*>(nullptr), static_cast<uint8_t*>(nullptr));
     hipLaunchKernelGGL(k_fixed_scatter, dim3(tb), dim3(kTilesPerBlock * kWave), 0, s, bytes, pages, tiles, ntiles, pw,
                        validity, tile_rank, page_pos, page_err, values);
 }
@@ -433,8 +483,9 @@ void launch_fixed_levels(hipStream_t s, const uint8_t* bytes, const DevPage* pag
                          const int32_t* page_tile0, ColumnParams cp, uint32_t* validity, int32_t* tile_rank,
                          int32_t* page_pos, int32_t* page_nn, DevErr* page_err, int32_t* err_any) {
     if (npages <= 0) return;
-    hipLaunchKernelGGL(k_fixed_levels2, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0, cp,
-                       validity, tile_rank, page_pos, page_nn, page_err, err_any);
+    hipLaunchKernelGGL(k_fixed_levels2<false>, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0, cp,
+                       validity, tile_rank, page_pos, page_nn, page_err, err_any, static_cast<const DevTile*>(nullptr),
+                       static_cast<uint8_t*>(nullptr));
 }
 
 }  // namespace pqk

@@ -218,7 +218,7 @@ void launch_fixed_levels(hipStream_t s, const uint8_t* bytes, const DevPage* pag
 void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,
                         int ntiles, const int32_t* page_tile0, ColumnParams cp, uint32_t* validity,
                         uint8_t* values, int32_t* tile_rank, int32_t* page_pos, DevErr* page_err,
-                        int32_t* err_any);
+                        int32_t* err_any, bool fused = true);
 
 // ── fused BYTE_ARRAY path (dict_fused.hip) ─────────────────────────────────
 struct FusedLaunch {

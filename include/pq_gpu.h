@@ -157,6 +157,8 @@ int pq_ctx_sync(pq_ctx* ctx);
  *   "plain_fused" 1 (default): their one-pass form when every page's strings
  *                 fill it exactly (checked on the device; else the two passes)
  *   "fixed_plain" 1 (default): tile-parallel PLAIN fixed-width kernels
+ *   "fixed_fused" 0 (default): OPTIONAL PLAIN fixed-width chunks scatter their
+ *                 values in a second launch; 1: inside the def-level launch
  *   "fused_ba"    1 (default): per-page fused BYTE_ARRAY kernel for chunks the
  *                 pipe does not take; 0 forces the generic rows/scan/gather kernels
  *   "fused_waves" waves per workgroup cap (0 = automatic)

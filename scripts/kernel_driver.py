@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Run the C2 decode, the C3 regex scan or the C3 PLAIN decode a few times — a
 small target for rocprofv3 PMC passes.
-usage: kernel_driver.py [decode|regex|plain] [rows] [reps] [fused_debug]
+usage: kernel_driver.py [decode|regex|plain|c4|wide] [rows] [reps] [fused_debug]
+(c4: env PQ_COLS="3,7" picks the C4 columns; wide: the 100k-entry dictionary)
 (env PQ_OPTS="key=value,..." sets further context options)"""
 import os
 import sys
@@ -23,6 +24,24 @@ if what == "decode":
     f = gen.build(gen.c2_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C2"])
     F = capi.File(f)
     dc = ctx.upload(f, [F.chunk(0, 0)])
+    for _ in range(reps):
+        dc.decode_async()
+    ctx.sync()
+elif what == "c4":
+    cols = gen.c4_cols()
+    f = gen.build(cols, rows, 1, seed=gen.CONFIG_SEEDS["C4"], layout=gen.ARROW_LAYOUT)
+    F = capi.File(f)
+    for ci in [int(x) for x in os.environ.get("PQ_COLS", "3").split(",")]:
+        dc = ctx.upload(f, [F.chunk(0, ci)])
+        for _ in range(reps):
+            dc.decode_async()
+        ctx.sync()
+        dc.free()
+elif what == "wide":
+    col = gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.05, dict_size=100_000,
+                  len_min=4, len_max=9, max_run=16)
+    f = gen.build([col], rows, 1, seed=gen.CONFIG_SEEDS["C2"], layout=gen.ARROW_LAYOUT)
+    dc = ctx.upload(f, [capi.File(f).chunk(0, 0)])
     for _ in range(reps):
         dc.decode_async()
     ctx.sync()

@@ -46,10 +46,12 @@ def path(request, ctx):
     ctx.set_option("fused_ba", int(p != "generic"))
     ctx.set_option("fixed_plain", int(p != "generic"))
     ctx.set_option("plain_fused", int(p != "big"))
+    ctx.set_option("fixed_fused", int(p == "big"))
     ctx.set_option("pipe_front", int(p == "front"))
     yield p
     for k in ("dict_pipe", "plain_ba", "fused_ba", "fixed_plain", "plain_fused"):
         ctx.set_option(k, 1)
+    ctx.set_option("fixed_fused", 0)
     ctx.set_option("pipe_front", 0)
     ctx.set_option("big_all", 0)
 

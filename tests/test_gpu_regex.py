@@ -97,20 +97,25 @@ def test_regex_reports_decode_errors(ctx, kernel):
     dc.free()
 
 
+@pytest.mark.parametrize("nrg", [1, 2])
 @pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT])
-def test_regex_reuses_checked_decode_codes(ctx, layout):
+def test_regex_reuses_checked_decode_codes(ctx, layout, nrg):
     """regex_reuse: after a checked decode the scan reads that decode's codes
     (no dict/run/codes passes); page sets equal the oracle's, interleaved
     with further decodes, and the decode's output stays correct."""
     cols = gen.c2_cols()
-    f = gen.build(cols, 40000, 2, seed=9, layout=layout, rows_per_page=0 if layout == gen.REF_LAYOUT else 3000)
+    f = gen.build(cols, 40000, nrg, seed=9, layout=layout, rows_per_page=0 if layout == gen.REF_LAYOUT else 3000)
     chunks = file_chunks(f, 0)
     dc = ctx.upload(f, chunks)
     pats = ["^qx", "e", "^[a-m]", "a.{3}e"]
     exp = {(p, n): golden_pages(f, chunks, p, n) for p in pats for n in (False, True)}
     dc.decode()
     ref = capi.canonical_dump(dc.to_host())
+    fronts = ("dict_index", "pipe_runs", "pipe_codes", "pipe_front", "pipe_big", "pipe_count")
     ctx.timing(True)
+    ctx.timing_reset()
+    dc.decode()
+    base = {k: ctx.timing_get(k)[1] for k in fronts}
     ctx.timing_reset()
     for p in pats:
         for n in (False, True):
@@ -119,30 +124,37 @@ def test_regex_reuses_checked_decode_codes(ctx, layout):
         dc.regex_pages_async(p, True)
         assert np.array_equal(dc.regex_pages_result(), exp[(p, True)])
     ctx.timing(False)
-    for k in ("pipe_runs", "pipe_codes", "pipe_front", "pipe_big"):
-        ms, n = ctx.timing_get(k)
-        assert n == len(pats), (k, n)  # only the decodes ran the front passes
+    for k in fronts:  # only the decodes ran the front passes
+        assert ctx.timing_get(k)[1] == len(pats) * base[k], (k, base)
     assert capi.canonical_dump(dc.to_host()) == ref
     dc.free()
 
 
-def test_regex_reuse_not_taken_after_failed_decode(ctx):
-    """A decode that failed leaves no reusable codes: the scan reports the
-    same error itself (a zero-count RLE run before any literal run, which the
-    reference rejects)."""
+@pytest.mark.parametrize("case", ["zero_count", "dict_truncated", "missing_bw"])
+def test_regex_reuse_not_taken_after_failed_decode(ctx, case):
+    """A decode that failed leaves no reusable codes or entries: the scan
+    reports the decode's error itself, every time."""
+    import struct
     import pqbuild as B
-    dpay = B.plain_ba([b"alpha", b"", b"gamma-gamma", b"d"])
-    idx = bytes([2]) + B.rle(0, 1, 2) + B.rle(3, 1, 2)
-    f, ch = B.build_file([B.dict_header(len(dpay), 4) + dpay, B.data_header(len(idx), 3, 8) + idx],
-                         gen.BYTE_ARRAY, False, 3, dict_at_start=True)
+    dvals = [b"alpha", b"", b"gamma-gamma", b"d"]
+    dpay = B.plain_ba(dvals)
+    if case == "zero_count":  # a zero-count RLE run before any literal run
+        idx, nv, opt = bytes([2]) + B.rle(0, 1, 2) + B.rle(3, 1, 2), 3, False
+    elif case == "dict_truncated":
+        dpay, idx, nv, opt = struct.pack("<I", 1) + b"a" + b"\x05", bytes([1]) + B.rle(2, 0, 1), 2, False
+    else:  # the index stream has no bit-width byte
+        idx, nv, opt = B.levels_section(B.rle(4, 0, 1)), 4, True
+    ndict = 2 if case == "dict_truncated" else len(dvals)
+    f, ch = B.build_file([B.dict_header(len(dpay), ndict) + dpay, B.data_header(len(idx), nv, 8) + idx],
+                         gen.BYTE_ARRAY, opt, nv, dict_at_start=True)
     rc_o, msg_o, _ = O.read_all(f, to_oracle_chunk(ch))
     assert rc_o != 0
     dc = ctx.upload(f, [to_desc(ch)])
     for _ in range(2):
-        with pytest.raises(capi.PqError) as ei:
+        with pytest.raises(capi.PqError) as e1:
             dc.decode()
-        assert ei.value.msg == msg_o
-        with pytest.raises(capi.PqError) as ei:
+        assert e1.value.code == rc_o
+        with pytest.raises(capi.PqError) as e2:
             dc.regex_pages("a", False)
-        assert ei.value.msg == msg_o
+        assert (e2.value.code, e2.value.msg) == (e1.value.code, e1.value.msg)
     dc.free()
