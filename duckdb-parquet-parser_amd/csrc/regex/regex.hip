@@ -726,15 +726,8 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
         lbase[lane()] = mpay / 4;
         const uint32_t wtotal = bcast_last(pinc);
         __builtin_amdgcn_wave_barrier();
-        // pages already satisfied (a value matched, or failed under neg) skip
-        // their remaining strings; the scan stops once every page is
-        const uint64_t allp = np >= 64 ? ~0ull : ((1ull << np) - 1ull);
         for (uint32_t g0 = 0; g0 < ((dbg & 1) ? 0u : wtotal); g0 += kStrPerLane * kWave) {
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint64_t sat0 = (static_cast<uint64_t>(hit[1]) << 32) | hit[0];
-            if ((sat0 & allp) == allp) break;
-            uint32_t e2[kStrPerLane], off2[kStrPerLane], len2[kStrPerLane], pg2[kStrPerLane], lim[kStrPerLane];
+            uint32_t e2[kStrPerLane], off2[kStrPerLane], len2[kStrPerLane], pg2[kStrPerLane];
             bool ok2[kStrPerLane];
 #pragma unroll
             for (uint32_t h = 0; h < kStrPerLane; h++) {
@@ -752,12 +745,10 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                 len2[h] = ok2[h] ? st_u32(stage, ent - 4) : 0u;
                 pg2[h] = gl;
                 e2[h] = full ? (DFA_START * kDfaRowBytes) : DFA_START;
-                ok2[h] = ok2[h] && !((sat0 >> gl) & 1ull);
-                lim[h] = ok2[h] ? len2[h] : 0u;
             }
             uint32_t maxl = 0;
 #pragma unroll
-            for (uint32_t h = 0; h < kStrPerLane; h++) maxl = max(maxl, lim[h]);
+            for (uint32_t h = 0; h < kStrPerLane; h++) maxl = max(maxl, len2[h]);
             for (uint32_t b0 = 0; __ballot(maxl > b0); b0 += 16) {
                 uint32_t Aw[kStrPerLane][4], rem[kStrPerLane];
 #pragma unroll
@@ -769,7 +760,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                     for (uint32_t j = 0; j < 5; j++) d[j] = stage[i0 + j];
 #pragma unroll
                     for (uint32_t j = 0; j < 4; j++) Aw[h][j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
-                    rem[h] = lim[h] > b0 ? lim[h] - b0 : 0u;
+                    rem[h] = len2[h] > b0 ? len2[h] - b0 : 0u;
                 }
                 // the chains advance one byte each per step, interleaved
                 if (full) {
@@ -795,17 +786,6 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                             e2[h] = i < rem[h] ? t : e2[h];
                         }
                     }
-                }
-                // a chain in DEAD or ACCEPT (both absorbing, and neither
-                // changes at the string end) stops here
-                maxl = 0;
-#pragma unroll
-                for (uint32_t h = 0; h < kStrPerLane; h++) {
-                    const uint32_t st = full ? e2[h] : (e2[h] & 0x7FFFu);
-                    const bool absorbed = full ? (st == DFA_DEAD * kDfaRowBytes || st == DFA_ACCEPT * kDfaRowBytes)
-                                               : (st == DFA_DEAD || st == DFA_ACCEPT);
-                    if (absorbed) lim[h] = min(lim[h], b0 + 16);
-                    maxl = max(maxl, lim[h]);
                 }
             }
 #pragma unroll
