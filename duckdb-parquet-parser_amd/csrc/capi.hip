@@ -60,6 +60,11 @@ struct pq_ctx {
     std::vector<PendingTimer> pending;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
     std::map<std::string, std::pair<double, int64_t>> timers;
+    // upload scratch (upload_walked): per-page host tables, reused
+    std::vector<pqk::DevPage> s_hpages;
+    std::vector<std::pair<int64_t, int64_t>> s_copies;
+    std::vector<int32_t> s_copy_size, s_tile0;
+    std::vector<pqk::DevTile> s_htiles;
     bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
     int opt_debug = 0;      // "fused_debug": ablation switches for timing studies
     int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
@@ -93,10 +98,9 @@ struct pq_chunk {
     int64_t nrows = 0;
     int64_t row_offset = 0;             // page-range uploads: global row of the first data page
     int64_t payload_bytes = 0;
-    std::vector<pq_page_desc> walked;   // every walked page, all chunks, global rows
+    pqfmt::PageList walked;             // every walked page, all chunks, global rows
     std::vector<int64_t> page_seq;      // walk sequence of each device data page
     std::vector<int64_t> dict_seq;      // walk sequence of each device dict page
-    std::vector<int64_t> data_walk_idx; // index into `walked` of each device data page
     int walk_error = 0;
     std::string walk_message;
     int64_t walk_error_seq = 0;
@@ -967,12 +971,19 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         c->width = c->plain_width;
         c->row_offset = row_offset;
         std::unique_ptr<HostTimed> plan_timer(new HostTimed(ctx, "up_plan"));
+        std::unique_ptr<HostTimed> sub_timer(new HostTimed(ctx, "up_plan_pages"));
 
         // 1) host walks; every payload gets a 16-byte aligned slot in one image
-        std::vector<DevPage> hpages;
+        // per-page host tables: the context's scratch (capacity kept across
+        // uploads, so a reader walking many row groups does not page-fault
+        // fresh tables in each time; a context serves one thread at a time)
+        std::vector<DevPage>& hpages = ctx->s_hpages;
         std::vector<DevDict> hdicts;
-        std::vector<std::pair<int64_t, int64_t>> copies;  // (file offset, image offset) per payload
-        std::vector<int32_t> copy_size;
+        std::vector<std::pair<int64_t, int64_t>>& copies = ctx->s_copies;  // (file offset, image offset) per payload
+        std::vector<int32_t>& copy_size = ctx->s_copy_size;
+        hpages.clear();
+        copies.clear();
+        copy_size.clear();
         int64_t seq = 0, row_base = 0, img = 0;
         {
             size_t tot = 0;
@@ -980,9 +991,8 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             hpages.reserve(tot);
             copies.reserve(tot);
             copy_size.reserve(tot);
-            c->walked.reserve(tot);
+            if (nchunks > 1) c->walked.reserve(tot);
             c->page_seq.reserve(tot);
-            c->data_walk_idx.reserve(tot);
         }
         // pages the codec pass rebuilds (compressed or DATA_PAGE_V2): their slot
         // holds the V1-layout payload; the image build leaves it zero
@@ -1024,7 +1034,6 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         };
         for (int k = 0; k < nchunks; k++) {
             pqfmt::WalkResult& w = walks[static_cast<size_t>(k)];
-            int64_t base_walk = static_cast<int64_t>(c->walked.size());
             std::vector<int32_t> dict_of_walk(w.pages.size(), -1);
             pq_chunk::Range rg;
             rg.p0 = static_cast<int32_t>(hpages.size());
@@ -1063,11 +1072,10 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                     d.dict = d.mode == pqk::MODE_DICT ? dict_dev : -1;
                     hpages.push_back(d);
                     c->page_seq.push_back(sq);
-                    c->data_walk_idx.push_back(base_walk + static_cast<int64_t>(i));
                     c->payload_bytes += psize;
                 }
                 p.first_row += row_base;
-                c->walked.push_back(p);
+                if (nchunks > 1) c->walked.push_back(p);
             }
             rg.np = static_cast<int32_t>(hpages.size()) - rg.p0;
             c->ranges.push_back(rg);
@@ -1083,17 +1091,24 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                 break;
             }
         }
+        if (nchunks == 1) c->walked = std::move(walks[0].pages);  // rows start at 0: the walk's table as is
         c->nrows = row_base;
         c->nbytes = static_cast<size_t>(img) + 64;
+        sub_timer.reset(new HostTimed(ctx, "up_plan_fused"));
         plan_fused(ctx, c.get(), hpages, hdicts);
+        sub_timer.reset(new HostTimed(ctx, "up_plan_pipe"));
         plan_pipe(ctx, c.get(), hpages, hdicts);
+        sub_timer.reset(new HostTimed(ctx, "up_plan_plain"));
         plan_plain(ctx, c.get(), hpages);
+        sub_timer.reset(new HostTimed(ctx, "up_plan_rest"));
         c->npages = static_cast<int>(hpages.size());
         c->ndicts = static_cast<int>(hdicts.size());
 
         // tiles
-        std::vector<DevTile> htiles;
-        std::vector<int32_t> tile0(hpages.size());
+        std::vector<DevTile>& htiles = ctx->s_htiles;
+        std::vector<int32_t>& tile0 = ctx->s_tile0;
+        htiles.clear();
+        tile0.resize(hpages.size());
         {
             size_t nt = 0;
             for (const auto& pg : hpages) nt += static_cast<size_t>((std::max(pg.nvals, 0) + pqk::kTileRows - 1) / pqk::kTileRows);
@@ -1116,6 +1131,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                          c->width == c->plain_width && c->max_def >= 0 && c->max_rep >= 0;
         for (const auto& pg : hpages) c->fixed_plain &= pg.mode == pqk::MODE_PLAIN;
 
+        sub_timer.reset();
         plan_timer.reset();
         // 2) device allocations + one upload
         std::unique_ptr<HostTimed> alloc_timer(new HostTimed(ctx, "up_alloc"));

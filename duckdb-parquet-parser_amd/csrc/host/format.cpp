@@ -586,6 +586,165 @@ std::vector<SpecSeg> speculate(const uint8_t* file, size_t len, size_t start, si
     return segs;
 }
 
+// The exact walk over linked speculative segments, on the same threads: when
+// every segment the true chain enters starts its records exactly where the
+// previous one's chain left, and no segment's chain broke inside its range,
+// the segments' records ARE the chain from `start`.  The page table then
+// follows from prefix sums (values, rows, the dictionary in force) instead of
+// one serial pass.  Anything the serial loop would stop on (a header error
+// before the value count, a chain that ends first, num_values <= 0) returns
+// false: the caller runs the serial loop, which produces the reference's
+// exact pages and error.
+bool linked_walk(std::vector<SpecSeg>& segs, size_t start, const pq_chunk_desc& c, bool ext_v2, int32_t cflag,
+                 int threads, WalkResult& w) {
+    if (c.num_values <= 0) return false;
+    std::vector<int> parts;     // segments on the chain, in order
+    std::vector<size_t> first;  // the record of each where the true chain enters
+    size_t expect = start;
+    for (size_t k = 0; k < segs.size(); k++) {
+        const SpecSeg& sg = segs[k];
+        if (expect >= sg.hi) continue;  // the chain jumps over this segment
+        // a segment that started on a false chain usually meets the true one
+        // a few pages later: enter at the record where the positions agree
+        const auto it = std::lower_bound(sg.recs.begin(), sg.recs.end(), expect,
+                                         [](const std::pair<size_t, PageHeader>& r, size_t v) { return r.first < v; });
+        if (it == sg.recs.end() || it->first != expect) return false;
+        const auto& last = sg.recs.back();
+        const size_t exit = last.first + last.second.header_size + static_cast<size_t>(last.second.compressed);
+        if (exit < sg.hi) return false;  // the segment's chain broke inside it
+        parts.push_back(static_cast<int>(k));
+        first.push_back(static_cast<size_t>(it - sg.recs.begin()));
+        expect = exit;
+    }
+    const size_t np = parts.size();
+    if (np == 0) return false;
+    // per part: data values, rows, records, first error, last dictionary page
+    struct Sum { int64_t vals = 0, rows = 0; size_t n = 0, err = SIZE_MAX; int64_t last_dict = -1; };
+    std::vector<Sum> sum(np);
+    auto kind = [&](const PageHeader& h, int64_t* vals, bool* bad) {  // 0 other, 1 dict, 2 data, 3 v2
+        *vals = 0;
+        *bad = false;
+        if (h.compressed < 0) { *bad = true; return 0; }
+        if (h.type == PQ_DICTIONARY_PAGE) {
+            *bad = !h.has_dict || h.dict_num_values < 0;
+            return 1;
+        }
+        if (h.type == PQ_DATA_PAGE) {
+            *bad = !h.has_data || h.data_num_values < 0;
+            *vals = h.data_num_values;
+            return 2;
+        }
+        if (h.type == PQ_DATA_PAGE_V2 && ext_v2) {
+            *bad = !h.has_v2 || h.v2_num_values < 0 || h.v2_def_len < 0 || h.v2_rep_len < 0 ||
+                   static_cast<int64_t>(h.v2_def_len) + h.v2_rep_len > h.compressed ||
+                   static_cast<int64_t>(h.v2_def_len) + h.v2_rep_len > h.uncompressed;
+            *vals = h.v2_num_values;
+            return 3;
+        }
+        return 0;
+    };
+    auto par = [&](auto&& fn) {
+        const int nt = std::max(1, std::min<int>(threads, static_cast<int>(np)));
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; t++) th.emplace_back([&, t] { for (size_t i = t; i < np; i += nt) fn(i); });
+        for (size_t i = 0; i < np; i += nt) fn(i);
+        for (auto& x : th) x.join();
+    };
+    par([&](size_t i) {
+        const auto& r = segs[static_cast<size_t>(parts[i])].recs;
+        const size_t j0 = first[i];
+        Sum& S = sum[i];
+        S.n = r.size() - j0;
+        for (size_t j = j0; j < r.size(); j++) {
+            int64_t v;
+            bool bad;
+            const int kd = kind(r[j].second, &v, &bad);
+            if (bad) { S.err = j - j0; break; }
+            S.vals += v;
+            S.rows += v;
+            if (kd == 1) S.last_dict = static_cast<int64_t>(j - j0);
+        }
+    });
+    // the cut: the page at which the values read reach num_values (serial
+    // over parts, then within the one part)
+    std::vector<size_t> base(np + 1, 0);
+    std::vector<int64_t> vbase(np, 0), dict_in(np, -1);
+    int64_t acc = 0, dict = -1;
+    size_t cut_part = np, total = 0;
+    for (size_t i = 0; i < np; i++) {
+        base[i] = total;
+        vbase[i] = acc;
+        dict_in[i] = dict;
+        if (sum[i].err != SIZE_MAX || acc + sum[i].vals >= c.num_values) { cut_part = i; break; }
+        acc += sum[i].vals;
+        if (sum[i].last_dict >= 0) dict = static_cast<int64_t>(total) + sum[i].last_dict;
+        total += sum[i].n;
+    }
+    if (cut_part == np) return false;  // the chain ends before the value count
+    size_t cut = 0;                    // records of cut_part kept
+    {
+        const auto& r = segs[static_cast<size_t>(parts[cut_part])].recs;
+        int64_t a = acc;
+        for (size_t j = first[cut_part]; j < r.size(); j++) {
+            int64_t v;
+            bool bad;
+            kind(r[j].second, &v, &bad);
+            if (bad) return false;  // an error before the count: the serial loop reports it
+            a += v;
+            if (a >= c.num_values) { cut = j + 1 - first[cut_part]; break; }
+        }
+        if (cut == 0) return false;
+    }
+    const size_t npages = base[cut_part] + cut;
+    w.pages.resize(npages);
+    par([&](size_t i) {
+        if (i > cut_part) return;
+        const auto& r = segs[static_cast<size_t>(parts[i])].recs;
+        const size_t j0 = first[i];
+        const size_t m = i == cut_part ? cut : r.size() - j0;
+        int64_t row = vbase[i], d = dict_in[i];
+        for (size_t j = 0; j < m; j++) {
+            const size_t pos = r[j0 + j].first;
+            const PageHeader& h = r[j0 + j].second;
+            const size_t idx = base[i] + j;
+            int64_t v;
+            bool bad;
+            const int kd = kind(h, &v, &bad);
+            pq_page_desc p{};
+            p.header_offset = static_cast<int64_t>(pos);
+            p.payload_offset = static_cast<int64_t>(pos + h.header_size);
+            p.payload_size = h.compressed;
+            p.page_type = h.type;
+            p.first_row = row;
+            p.page_num = -1;
+            p.uncompressed_size = h.uncompressed;
+            if (kd == 1) {
+                d = static_cast<int64_t>(idx);
+                p.num_values = h.dict_num_values;
+                p.page_num = static_cast<int32_t>(idx);
+                p.flags = cflag;
+            } else if (kd == 2) {
+                p.num_values = h.data_num_values;
+                p.encoding = h.data_encoding;
+                p.page_num = static_cast<int32_t>(idx);
+                p.flags = cflag;
+            } else if (kd == 3) {
+                p.page_type = PQ_DATA_PAGE;
+                p.num_values = h.v2_num_values;
+                p.encoding = h.v2_encoding;
+                p.page_num = static_cast<int32_t>(idx);
+                p.flags = PQ_PAGE_V2 | (h.v2_compressed ? cflag : 0);
+                p.v2_def_len = h.v2_def_len;
+                p.v2_rep_len = h.v2_rep_len;
+            }
+            p.dict_page = static_cast<int32_t>(d);
+            row += v;
+            w.pages[idx] = p;
+        }
+    });
+    return true;
+}
+
 }  // namespace
 
 WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, int threads) {
@@ -624,6 +783,7 @@ WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, i
             static_cast<size_t>(off) < len) {
             const size_t end = std::min(len, static_cast<size_t>(off) + static_cast<size_t>(c.total_compressed_size));
             if (end > cur) segs = speculate(file, len, cur, end, threads);
+            if (!segs.empty() && linked_walk(segs, cur, c, ext_v2, cflag, threads, w)) return w;
         }
         size_t sk = 0, si = 0;
         auto spec_at = [&](size_t pos, PageHeader& h) {

@@ -16,6 +16,8 @@
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <memory>
+#include <utility>
 #include <vector>
 
 #include "pq_gpu.h"
@@ -123,8 +125,25 @@ struct PageHeader {
 // Parses a header from the 256-byte window at `off` (zeros past EOF).
 PageHeader read_page_header(const uint8_t* file, size_t len, size_t off);
 
+// Allocator whose resize leaves trivially constructible elements
+// uninitialised (page tables are filled in parallel right after; no serial
+// zero fill of tens of MB).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind { using other = NoInitAlloc<U>; };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+using PageList = std::vector<pq_page_desc, NoInitAlloc<pq_page_desc>>;
+
 struct WalkResult {
-    std::vector<pq_page_desc> pages;
+    PageList pages;
     int error = 0;            // first error met by the walk (after `pages`)
     std::string message;
 };

@@ -73,12 +73,17 @@ def c3_job(rank: int) -> dict:
     return out
 
 
-def c5_job(rg: int) -> dict:
+def c5_job(rg: int, layout: int = gen.ARROW_LAYOUT) -> dict:
     """bench.py c5_leg: row group `rg` of the C5 column (rank r holds row
-    groups [r * c5_rgs, (r + 1) * c5_rgs))."""
-    f = gen.build(gen.c2_cols(), ROWS, 1, seed=gen.CONFIG_SEEDS["C5"], layout=gen.ARROW_LAYOUT, first_rg=rg)
+    groups [r * c5_rgs, (r + 1) * c5_rgs)), arrow or reference layout."""
+    f = gen.build(gen.c2_cols(), ROWS, 1, seed=gen.CONFIG_SEEDS["C5"], layout=layout, first_rg=rg)
     ch = capi.File(f).chunk(0, 0)
-    return {f"c5|{ROWS}|rg{rg}|{pat}": entry(page_flags(f, ch, pat)) for pat in C5_PATTERNS}
+    key = "c5" if layout == gen.ARROW_LAYOUT else "c5ref"
+    return {f"{key}|{ROWS}|rg{rg}|{pat}": entry(page_flags(f, ch, pat)) for pat in C5_PATTERNS}
+
+
+def c5ref_job(rg: int) -> dict:
+    return c5_job(rg, gen.REF_LAYOUT)
 
 
 def main():
@@ -87,13 +92,16 @@ def main():
     ranks = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     c5_rgs = int(sys.argv[2]) if len(sys.argv) > 2 else 12
     procs = int(sys.argv[3]) if len(sys.argv) > 3 else 6
-    jobs = [(c3_job, r) for r in range(ranks)] + [(c5_job, g) for g in range(ranks * c5_rgs)]
-    out = {}
+    only = os.environ.get("ONLY", "c3,c5,c5ref").split(",")
+    jobs = ([(c3_job, r) for r in range(ranks)] if "c3" in only else []) + \
+           ([(c5_job, g) for g in range(ranks * c5_rgs)] if "c5" in only else []) + \
+           ([(c5ref_job, g) for g in range(ranks * c5_rgs)] if "c5ref" in only else [])
+    path = os.path.join(ROOT, "tests", "golden", "bench_expect.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
     with mp.get_context("fork").Pool(procs) as pool:
         for d in pool.imap_unordered(_run, jobs):
             out.update(d)
             print(len(out), flush=True)
-    path = os.path.join(ROOT, "tests", "golden", "bench_expect.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=0, sort_keys=True)
 
