@@ -143,6 +143,11 @@ struct pq_chunk {
     // (collect), regex scans read them instead of recomputing
     bool codes_pending = false, codes_ok = false;
     bool entries_pending = false, entries_ok = false;  // the same for the dictionary entry table
+    // pq_decode_regex_async: the decode about to launch also runs the page
+    // filter (k_regex_dict before k_pipe_write, match bits in the writer)
+    bool arm = false;
+    int arm_neg = 0;
+    int32_t pipe_dict_nvals = 0;  // declared entries of the pipe's dictionary (arming bound)
     int32_t* d_tile_nn = nullptr;
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
@@ -471,6 +476,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->hbig = std::move(big);
     c->big_max_bytes = big_bytes;
     c->pipe_dict = dict_id;
+    c->pipe_dict_nvals = d.nvals;
     c->pipe_entry_base = d.entry_base;
     c->pipe_dict_chars_bytes = chars_bytes;
     c->pipe_dict_bytes = dict_bytes;
@@ -1863,6 +1869,14 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     } else if (pipe) {
         pqk::PipeLaunch P = pipe_launch(ctx, c, out);
         pipe_front(ctx, c, P, !dict_in_runs && !front, dict_in_runs);
+        if (c->arm) {  // the page filter in the same pass: match bits per entry, then the writer tests them
+            Timed t(ctx, "regex_dict");
+            pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
+                                    c->d_dict_match, c->d_page_flags, c->npages);
+            P.match = c->d_dict_match + c->pipe_entry_base;
+            P.match_neg = c->arm_neg;
+            P.page_flags = c->d_page_flags;
+        }
         if (c->ntiles == 0) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
             (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
@@ -2215,9 +2229,9 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     return true;
 }
 
-int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg) {
-    if (!ctx || !c || !pattern) return PQ_ERR_ARG;
-    DevGuard dg(ctx);
+// The compiled pattern (cached per chunk), page flags and the per-entry
+// match buffer of a BYTE_ARRAY chunk.
+static int regex_prepare(pq_ctx* ctx, pq_chunk* c, const char* pattern) {
     if (c->type != PQ_BYTE_ARRAY) return set_err(ctx, PQ_ERR_ARG, "regex page filter needs a BYTE_ARRAY column");
     try {
         std::string msg;
@@ -2252,11 +2266,25 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             }
             c->prog_pattern = key;
         }
+        return 0;
+    } catch (const std::exception& e) {
+        return set_err(ctx, PQ_ERR_ALLOC, e.what());
+    }
+}
+
+int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg) {
+    if (!ctx || !c || !pattern) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
+    if (int rc = regex_prepare(ctx, c, pattern)) return rc;
+    try {
         hipStream_t s = ctx->stream;
         pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
-        (void)hipMemsetAsync(c->d_flags, 0, c->zero_bytes, s);
         const bool on_codes = c->pipe && ctx->opt_pipe && ctx->opt_regex_codes;
         const bool reuse = on_codes && ctx->opt_regex_reuse && c->codes_ok;
+        // over a checked decode's codes: k_regex_dict clears the status words
+        // and sets the page flags itself (no fill kernels)
+        const bool fold = reuse && c->ndicts && c->entries_ok && c->zero_bytes % 4 == 0;
+        if (!fold) (void)hipMemsetAsync(c->d_flags, 0, c->zero_bytes, s);
         if (c->ndicts) {
             if (!(ctx->opt_regex_reuse && c->entries_ok)) {
                 c->entries_pending = true;
@@ -2265,7 +2293,9 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             }
             Timed t(ctx, "regex_dict");
             pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries,
-                                    c->d_dict_count, c->d_dict_match);
+                                    c->d_dict_count, c->d_dict_match, fold ? c->d_page_flags : nullptr,
+                                    fold ? c->npages : 0, fold ? reinterpret_cast<uint32_t*>(c->d_flags) : nullptr,
+                                    fold ? static_cast<int64_t>(c->zero_bytes / 4) : 0);
         }
         if (on_codes) {
             // dictionary-first on the decode's own codes: the pattern ran on
@@ -2277,7 +2307,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
                 c->codes_pending = true;
             }
             Timed t(ctx, "regex_codes");
-            pqk::launch_pipe_match(s, P, c->d_dict_match + c->pipe_entry_base, neg, c->d_page_flags);
+            pqk::launch_pipe_match(s, P, c->d_dict_match + c->pipe_entry_base, neg, c->d_page_flags, fold);
         } else if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {
             (void)hipMemsetAsync(c->d_rwin_ticket, 0, sizeof(int32_t), s);
             Timed t(ctx, "regex_plain");
@@ -2309,6 +2339,27 @@ int pq_regex_pages_result(pq_ctx* ctx, pq_chunk* c, uint8_t* page_flags) {
     if (page_flags && c->npages)
         return hip_check(ctx, hipMemcpy(page_flags, c->d_page_flags, static_cast<size_t>(c->npages), hipMemcpyDeviceToHost), "copy page flags");
     return 0;
+}
+
+int pq_decode_regex_async(pq_ctx* ctx, pq_chunk* c, pq_column* out, const char* pattern, int neg) {
+    if (!ctx || !c || !out || !pattern) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
+    if (int rc = regex_prepare(ctx, c, pattern)) return rc;
+    // one pass when the decode takes the pipe (dictionary pages only, one
+    // dictionary small enough for the writer's mask); else the decode, then
+    // the scan over its codes
+    const bool plain_go = c->plain && ctx->opt_plain;
+    const bool one = c->pipe && ctx->opt_pipe && ctx->opt_regex_codes && !plain_go && c->ndicts > 0 &&
+                     c->pipe_dict_nvals >= 0 && static_cast<uint32_t>(c->pipe_dict_nvals) <= pqk::kArmEntries;
+    if (!one) {
+        if (int rc = pq_decode_async(ctx, c, out)) return rc;
+        return pq_regex_pages_async(ctx, c, pattern, neg);
+    }
+    c->arm = true;
+    c->arm_neg = neg ? 1 : 0;
+    const int rc = pq_decode_async(ctx, c, out);
+    c->arm = false;
+    return rc;
 }
 
 int pq_regex_pages(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg, uint8_t* page_flags) {

@@ -882,8 +882,17 @@ struct WriteArgs {
     int wpw;    // writer waves per workgroup
     uint32_t* znext;  // the next decode's flags/bsum/flist[0] block, cleared here (or null)
     uint32_t znext_words;
+    // armed regex page filter (pq_decode_regex_async): the dictionary's match
+    // bytes (k_regex_dict ran before), or null; pages with a satisfying row
+    // get flag 0 (the flags were set to 1 by k_regex_dict)
+    const uint8_t* match;
+    int match_neg;
+    uint8_t* page_flags;
 };
 
+constexpr uint32_t kArmWords = 512;  // armed filter: dictionaries up to 16,384 entries (host checks)
+
+template <bool kArmed>
 __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (a.znext)  // the other flags/bsum/flist block, for the next decode (unused by this one)
@@ -896,6 +905,17 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     WriteLds& S = reinterpret_cast<WriteLds*>(smem + a.dict_bytes)[wv];
     const DevDict d = a.dicts[a.dict_id];
     const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    __shared__ uint32_t mbits[kArmed ? kArmWords : 1];
+    constexpr bool armed = kArmed;
+    if (armed)
+        for (uint32_t w = threadIdx.x; w < kArmWords; w += blockDim.x) {
+            uint32_t m = 0;
+            for (uint32_t k = 0; k < 32; k++) {
+                const uint32_t e = w * 32 + k;
+                m |= (e < dict_n && a.match[e] != 0 ? 1u : 0u) << k;
+            }
+            mbits[w] = m ^ (a.match_neg ? 0xFFFFFFFFu : 0u);  // bit = this entry satisfies the predicate
+        }
     // each wavefront owns a contiguous run of tiles (consecutive rows): the
     // descriptors of up to 64 tiles are loaded at once, one per lane, and the
     // next tile's codes are loaded before this tile's stores are issued
@@ -939,9 +959,10 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
         const int cn = min(kWave, tb - c0);
         int64_t myR0 = 0, myG0 = 0;
         uint32_t mym = 0;
-        uint32_t myc = 0;
+        uint32_t myc = 0, myp = 0;
         if (static_cast<int>(lane()) < cn) {
             const DevTile T = a.tiles[c0 + lane()];
+            myp = static_cast<uint32_t>(T.page);
             myR0 = a.pages[T.page].first_row + T.row0;
             mym = static_cast<uint32_t>(T.nrows);
             myc = static_cast<uint32_t>(a.tile_chars[c0 + lane()]);
@@ -999,6 +1020,13 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
                 src[k] = e & 0xFFFFu;
                 vb |= (valid ? 1u : 0u) << k;
                 acc += len[k];
+            }
+            if (armed) {  // the page filter: any row of the tile whose entry satisfies the predicate
+                bool hit = false;
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++)
+                    hit |= ((vb >> k) & 1u) && ((mbits[(cur[k] >> 5) & (kArmWords - 1)] >> (cur[k] & 31u)) & 1u);
+                if (__ballot(hit) && lane() == 0) a.page_flags[__builtin_amdgcn_readlane(myp, i)] = 0;
             }
             const uint32_t incl = wave_incl_scan(acc);
             const uint32_t total = bcast_last(incl);
@@ -1645,14 +1673,40 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
 // NULL rows and out-of-range indices (code 0xFFFF) never count.
 constexpr int kMatchWaves = 4;
 constexpr int kMatchBatch = 4;  // tiles whose codes a wave loads before testing any
-// Each wave takes kMatchBatch consecutive tiles per step (grid-stride), all
-// their codes loaded before the first test, so a wave keeps several 1 KiB
-// reads in flight instead of one.
+// Persistent workgroups; each first packs the dictionary's match bytes into
+// an LDS bit mask (a u16 code indexes at most 64 Ki entries: 8 KiB), then
+// each wave takes kMatchBatch consecutive tiles per step (grid-stride), all
+// their codes loaded before the first test, and tests them with LDS reads.
 __global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match(const DevTile* __restrict__ tiles, int ntiles,
                                                                  const DevPage* __restrict__ pages,
                                                                  const uint16_t* __restrict__ codes,
-                                                                 const uint8_t* __restrict__ match, int neg,
-                                                                 uint8_t* __restrict__ page_flags) {
+                                                                 const uint8_t* __restrict__ match,
+                                                                 const int32_t* __restrict__ dict_count, int dict_id,
+                                                                 int neg, uint8_t* __restrict__ page_flags) {
+    __shared__ uint32_t mbits[65536 / 32];
+    const uint32_t dn = min(static_cast<uint32_t>(max(dict_count[dict_id], 0)), 65535u);
+    const uint32_t nwd = (dn + 31) / 32;
+    for (uint32_t wd = threadIdx.x; wd < nwd; wd += blockDim.x) {
+        uint32_t m = 0;
+        if (wd * 32 + 32 <= dn) {  // 32 bytes as eight dwords (match bytes are 0 or 1)
+            const uint8_t* src = match + wd * 32;
+            for (uint32_t q = 0; q < 8; q++) {
+                uint32_t x;
+                __builtin_memcpy(&x, src + 4 * q, 4);
+                x = (x | (x >> 7) | (x >> 14) | (x >> 21)) & 0xFu;  // bytes 0..3 -> bits 0..3
+                m |= x << (4 * q);
+            }
+        } else {
+            for (uint32_t k = 0; k < 32; k++) {
+                const uint32_t e = wd * 32 + k;
+                m |= (e < dn && match[e] != 0 ? 1u : 0u) << k;
+            }
+        }
+        // a NULL / out-of-range code never satisfies either predicate: its
+        // bit is set where it must not count (neg flips the test below)
+        mbits[wd] = m;
+    }
+    __syncthreads();
     const int nw = static_cast<int>(gridDim.x) * kMatchWaves;
     const uint32_t l8 = lane() * 8;
     for (int t0 = (static_cast<int>(blockIdx.x) * kMatchWaves + static_cast<int>(threadIdx.x / kWave)) * kMatchBatch;
@@ -1679,7 +1733,9 @@ __global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match(const DevTile* 
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const uint32_t c = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                hit |= l8 + k < m[i] && c != kNull && ((match[c] != 0) != (neg != 0));
+                const bool live = l8 + k < m[i] && c < dn;
+                const uint32_t bit = (mbits[live ? (c >> 5) : 0u] >> (c & 31u)) & 1u;
+                hit |= live && (bit != static_cast<uint32_t>(neg != 0));
             }
             if (__ballot(hit) && lane() == 0) page_flags[pg[i]] = 0;
         }
@@ -2098,7 +2154,9 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
     pl.blocks_per_cu = all <= 160u * 1024 ? static_cast<int>((160u * 1024) / all) : 0;
     if (pl.blocks_per_cu > 4) pl.blocks_per_cu = 4;
     if (pl.blocks_per_cu > 0) {  // registers may allow fewer
-        const int occ = resident_blocks(reinterpret_cast<const void*>(k_pipe_write), wpw * kWave, pl.lds);
+        // (planned on the plain instance; the armed one, 2 KiB more static LDS,
+        // runs the same grid: its workgroups never wait on one another)
+        const int occ = resident_blocks(reinterpret_cast<const void*>(k_pipe_write<false>), wpw * kWave, pl.lds);
         pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
     }
     return pl;
@@ -2157,13 +2215,18 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
 
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
     if (P.ntiles <= 0) return;
-    ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_write), P.lds);
+    ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_write<false>), P.lds);
+    ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_write<true>), P.lds);
     int grid = 0, per = 0;
     write_shape(P, &grid, &per);  // P.grid: resident workgroups (plan_pipe_lds + occupancy)
     WriteArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.dicts, P.dict_id, P.entries, P.dict_count, P.codes,
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
-                P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves, P.znext, P.znext_words};
-    hipLaunchKernelGGL(k_pipe_write, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
+                P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves, P.znext, P.znext_words,
+                P.match, P.match_neg, P.page_flags};
+    if (P.match)
+        hipLaunchKernelGGL(k_pipe_write<true>, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
+    else
+        hipLaunchKernelGGL(k_pipe_write<false>, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
 }
 
 void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes) {
@@ -2203,13 +2266,14 @@ void launch_pipe_front(hipStream_t s, const PipeLaunch& P, const DevBatch* wins,
     hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, P.npages))), dim3(kWave), sizeof(CodeLds), s, a, P.flist);
 }
 
-void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags) {
-    (void)hipMemsetAsync(page_flags, 1, static_cast<size_t>(P.npages), s);
+void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags,
+                       bool flags_set) {
+    if (!flags_set) (void)hipMemsetAsync(page_flags, 1, static_cast<size_t>(P.npages), s);
     if (P.ntiles <= 0) return;
     const int need = (P.ntiles + kMatchWaves * kMatchBatch - 1) / (kMatchWaves * kMatchBatch);
-    const int grid = max(1, min(need, 8 * max(P.cus, 1)));
+    const int grid = max(1, min(need, 4 * max(P.cus, 1)));
     hipLaunchKernelGGL(k_pipe_match, dim3(grid), dim3(kMatchWaves * kWave), 0, s,
-                       P.tiles, P.ntiles, P.pages, P.codes, match, neg, page_flags);
+                       P.tiles, P.ntiles, P.pages, P.codes, match, P.dict_count, P.dict_id, neg, page_flags);
 }
 
 }  // namespace pqk

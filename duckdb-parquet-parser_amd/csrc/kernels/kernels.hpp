@@ -169,7 +169,11 @@ struct PipeLaunch {
     int write_waves;            // writer waves per k_pipe_write workgroup (planned with P.lds / P.grid)
     uint32_t* znext;            // cleared by k_pipe_write (the next decode's flags/bsum/flist[0]), or null
     uint32_t znext_words;
+    const uint8_t* match = nullptr;  // armed page filter (k_pipe_write), dictionaries <= kArmEntries
+    int match_neg = 0;
+    uint8_t* page_flags = nullptr;
 };
+constexpr uint32_t kArmEntries = 16384;
 struct PipePlan {
     uint32_t lds;       // dynamic LDS bytes of k_pipe_write
     int blocks_per_cu;  // 0: the dictionary does not fit
@@ -207,7 +211,8 @@ uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens);
 void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes);
 // regex page filter on the codes: page_flags[p] = 1 unless a non-null row of
 // page p matches (neg: fails to match); match = dictionary match bits
-void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags);
+void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags,
+                       bool flags_set = false);  // flags_set: page_flags already 1 (k_regex_dict set them)
 
 // ── tile-parallel PLAIN fixed-width path (fixed_fast.hip) ──────────────────
 // OPTIONAL columns' def levels alone (k_fixed_levels2): validity, per-tile

@@ -65,8 +65,16 @@ __global__ void __launch_bounds__(256) k_regex_dict(const DevProg* __restrict__ 
                                                     const DevDict* __restrict__ dicts,
                                                     const uint64_t* __restrict__ entries,
                                                     const int32_t* __restrict__ dict_count,
-                                                    uint8_t* __restrict__ dict_match) {
+                                                    uint8_t* __restrict__ dict_match,
+                                                    uint8_t* __restrict__ fill1, int64_t nfill1,
+                                                    uint32_t* __restrict__ zero, int64_t nzero) {
     __shared__ DevProg P;
+    {
+        const int64_t t = (static_cast<int64_t>(blockIdx.x) * gridDim.y + blockIdx.y) * blockDim.x + threadIdx.x;
+        const int64_t nt = static_cast<int64_t>(gridDim.x) * gridDim.y * blockDim.x;
+        for (int64_t i = t; i < nfill1; i += nt) fill1[i] = 1;
+        for (int64_t i = t; i < nzero; i += nt) zero[i] = 0;
+    }
     load_prog(&P, prog);
     const DevDict d = dicts[blockIdx.x];
     const int32_t n = dict_count[blockIdx.x];
@@ -839,10 +847,11 @@ void free_device_program(DeviceProgram* p) {
 
 void launch_regex_dict(hipStream_t s, const DeviceProgram* prog, const uint8_t* bytes,
                        const DevDict* dicts, int ndicts, const uint64_t* entries,
-                       const int32_t* dict_count, uint8_t* dict_match) {
+                       const int32_t* dict_count, uint8_t* dict_match, uint8_t* fill1, int64_t nfill1,
+                       uint32_t* zero, int64_t nzero) {
     if (ndicts <= 0) return;
     hipLaunchKernelGGL(k_regex_dict, dim3(ndicts, 16), dim3(256), 0, s, prog->d, bytes, dicts, entries,
-                       dict_count, dict_match);
+                       dict_count, dict_match, fill1, nfill1, zero, nzero);
 }
 
 void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, const uint8_t* bytes,

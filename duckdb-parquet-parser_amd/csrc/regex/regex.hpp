@@ -99,9 +99,13 @@ void build_dev(const Program& p, DevProg* out);
 DeviceProgram* upload_program(const Program& p, hipStream_t s);
 void free_device_program(DeviceProgram* p);
 
+// fill1/nfill1: bytes set to 1 (page flags), zero/nzero: u32 words cleared
+// (the chunk's status words), both in the same launch (the scan over the
+// codes of a checked decode then needs no fill kernels); may be null / 0.
 void launch_regex_dict(hipStream_t s, const DeviceProgram* prog, const uint8_t* bytes,
                        const pqk::DevDict* dicts, int ndicts, const uint64_t* entries,
-                       const int32_t* dict_count, uint8_t* dict_match);
+                       const int32_t* dict_count, uint8_t* dict_match, uint8_t* fill1 = nullptr,
+                       int64_t nfill1 = 0, uint32_t* zero = nullptr, int64_t nzero = 0);
 
 void launch_regex_pages(hipStream_t s, const DeviceProgram* prog, const uint8_t* bytes,
                         const pqk::DevPage* pages, int npages, const pqk::DevDict* dicts,

@@ -116,6 +116,7 @@ def lib():
             "pq_chunk_assign": ([vp, C.POINTER(ColumnOut), C.c_int64, vp, vp, C.POINTER(C.c_int64)], C.c_int),
             "pq_regex_compile_check": ([C.c_char_p, C.c_char_p, C.c_size_t], C.c_int),
             "pq_regex_pages": ([vp, vp, C.c_char_p, C.c_int, vp], C.c_int),
+            "pq_decode_regex_async": ([vp, vp, C.POINTER(ColumnOut), C.c_char_p, C.c_int], C.c_int),
             "pq_regex_pages_async": ([vp, vp, C.c_char_p, C.c_int], C.c_int),
             "pq_regex_pages_result": ([vp, vp, vp], C.c_int),
             "pq_regex_match_host": ([C.c_char_p, u8p, C.c_size_t], C.c_int),
@@ -404,6 +405,12 @@ class DeviceChunk:
 
     def regex_pages_async(self, pattern: str, neg: bool = False):
         self.ctx.check(lib().pq_regex_pages_async(self.ctx.h, self.h, pattern.encode(), int(neg)))
+
+    def decode_regex_async(self, pattern: str, neg: bool = False):
+        """pq_decode_regex_async: decode + page filter in one pass (flags via
+        regex_pages_result, the column via decode_check / to_host)."""
+        self.ctx.check(lib().pq_decode_regex_async(self.ctx.h, self.h, C.byref(self.out), pattern.encode(),
+                                                   int(neg)))
 
     def regex_pages_result(self) -> np.ndarray:
         flags = np.zeros(max(self.num_pages, 1), dtype=np.uint8)

@@ -158,3 +158,29 @@ def test_regex_reuse_not_taken_after_failed_decode(ctx, case):
             dc.regex_pages("a", False)
         assert (e2.value.code, e2.value.msg) == (e1.value.code, e1.value.msg)
     dc.free()
+
+
+@pytest.mark.parametrize("neg", [False, True])
+@pytest.mark.parametrize("name,cols,n,layout", [c for c in CASES if c[0] != "c3_optional"],
+                         ids=[c[0] for c in CASES if c[0] != "c3_optional"])
+def test_decode_regex_one_pass(ctx, name, cols, n, layout, neg):
+    """pq_decode_regex_async: the page flags equal the separate scan's and the
+    oracle's, and the column equals the plain decode's, on every case (the
+    writer's armed filter on pipe chunks, decode + scan elsewhere); repeated
+    passes and plain decodes in between keep both right."""
+    f = gen.build(cols, n, 1, seed=11, layout=layout, rows_per_page=0 if name.endswith("_big") else 700)
+    chunks = file_chunks(f, 0)
+    dc = ctx.upload(f, chunks)
+    dc.decode()
+    ref = capi.canonical_dump(dc.to_host())
+    for p in ("^qx", "e", "^[a-m]", "a.{3}e", "special.*requests"):
+        exp = golden_pages(f, chunks, p, neg)
+        for _ in range(2):
+            dc.decode_regex_async(p, neg)
+            got = dc.regex_pages_result()
+            dc.decode_check()
+            assert np.array_equal(got, exp), (p, neg)
+            assert capi.canonical_dump(dc.to_host()) == ref
+        dc.decode_async()
+        dc.decode_check()
+    dc.free()
