@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run the C2 decode, the C3 regex scan or the C3 PLAIN decode a few times — a
 small target for rocprofv3 PMC passes.
-usage: kernel_driver.py [decode|regex|plain|optplain|c4|wide] [rows] [reps] [fused_debug]
+usage: kernel_driver.py [decode|regex|plain|optplain|c4|c5|wide] [rows] [reps] [fused_debug]
 (c4: env PQ_COLS="3,7" picks the C4 columns; wide: the 100k-entry dictionary)
 (env PQ_OPTS="key=value,..." sets further context options)"""
 import os
@@ -43,6 +43,15 @@ elif what == "optplain":  # C3's strings OPTIONAL, 5 % NULL, arrow 20,000-row pa
     dc = ctx.upload(f, [capi.File(f).chunk(0, 0)])
     for _ in range(reps):
         dc.decode_async()
+    ctx.sync()
+elif what == "c5":  # C5 arrow row group(s): decode + one-pass filter
+    f = gen.build(gen.c2_cols(), rows, 1, seed=gen.CONFIG_SEEDS["C5"], layout=gen.ARROW_LAYOUT)
+    dc = ctx.upload(f, [capi.File(f).chunk(0, 0)])
+    dc.decode()
+    for _ in range(reps):
+        dc.decode_async()
+    for _ in range(reps):
+        dc.decode_regex_async("^qx")
     ctx.sync()
 elif what == "wide":
     col = gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.05, dict_size=100_000,
