@@ -74,6 +74,7 @@ struct pq_ctx {
     bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
     bool opt_regex_codes = true; // "regex_codes": dictionary chunks on the pipe path: match bits over the decode's codes
     bool opt_regex_reuse = true; // "regex_reuse": ... reusing the codes of an earlier checked decode of the chunk
+    bool opt_regex_index = true; // "regex_index": REQUIRED PLAIN chunks keep the string index of their first scan
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
@@ -147,6 +148,11 @@ struct pq_chunk {
     // filter (k_regex_dict before k_pipe_write, match bits in the writer)
     bool arm = false;
     int arm_neg = 0;
+    // string index of a REQUIRED PLAIN chunk (u16 window offset per row),
+    // filed by the first error-free windowed scan, read by the later ones
+    uint16_t* d_rx_index = nullptr;
+    bool rx_index_ok = false, rx_index_pending = false;
+    uint32_t rx_index_win = 0;
     int32_t pipe_dict_nvals = 0;  // declared entries of the pipe's dictionary (arming bound)
     int32_t* d_tile_nn = nullptr;
     unsigned long long* d_bsum = nullptr;
@@ -390,6 +396,7 @@ void free_chunk_device(pq_chunk* c) {
     }
     dfree(c->d_flags);
     dfree(c->d_bigd);
+    dfree(c->d_rx_index);
     dfree(c->d_row_codes);
     dfree(c->d_tile_chars);
     dfree(c->d_tile_rank);
@@ -802,6 +809,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
     if (std::strcmp(key, "regex_reuse") == 0) { ctx->opt_regex_reuse = value != 0; return 0; }
+    if (std::strcmp(key, "regex_index") == 0) { ctx->opt_regex_index = value != 0; return 0; }
     if (std::strcmp(key, "zflip") == 0) { ctx->opt_zflip = value != 0; return 0; }
     if (std::strcmp(key, "write_waves") == 0) {
         if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "write_waves: 1..16");
@@ -2049,12 +2057,13 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         if (c->ndicts && !c->d_dflag) (void)hipMemsetAsync(c->d_dict_err, 0, c->ndicts * sizeof(DevErr), ctx->stream);
     }
     if (best_code) {
-        c->codes_pending = c->entries_pending = false;
+        c->codes_pending = c->entries_pending = c->rx_index_pending = false;
         return set_err(ctx, best_code, best_msg);
     }
     if (c->codes_pending) c->codes_ok = true;
     if (c->entries_pending) c->entries_ok = true;
-    c->codes_pending = c->entries_pending = false;
+    if (c->rx_index_pending) c->rx_index_ok = true;
+    c->codes_pending = c->entries_pending = c->rx_index_pending = false;
     if (c->type == PQ_BYTE_ARRAY && out) {
         int64_t total = 0;
         (void)hipMemcpy(&total, c->d_total, sizeof total, hipMemcpyDeviceToHost);
@@ -2309,12 +2318,28 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             Timed t(ctx, "regex_codes");
             pqk::launch_pipe_match(s, P, c->d_dict_match + c->pipe_entry_base, neg, c->d_page_flags, fold);
         } else if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {
-            (void)hipMemsetAsync(c->d_rwin_ticket, 0, sizeof(int32_t), s);
+            // REQUIRED chunks: the first error-free scan files every string's
+            // window offset (row-indexed); later scans read it instead of
+            // walking the length chains (same windows: same window size)
+            const uint16_t* idx_in = nullptr;
+            uint16_t* idx_out = nullptr;
+            if (ctx->opt_regex_index && c->max_def == 0 && c->max_rep == 0 && c->nrows > 0 && !ctx->opt_regex_debug) {
+                if (c->rx_index_ok && c->rx_index_win == c->rwin_bytes) {
+                    idx_in = c->d_rx_index;
+                } else {
+                    c->rx_index_ok = false;
+                    if (c->d_rx_index || !dalloc(&c->d_rx_index, static_cast<size_t>(c->nrows))) {
+                        idx_out = c->d_rx_index;
+                        c->rx_index_pending = true;
+                        c->rx_index_win = c->rwin_bytes;
+                    }
+                }
+            }
             Timed t(ctx, "regex_plain");
             pqre::launch_regex_plain(s, c->d_dfa, c->dfa_bytes, c->rwin_bytes, c->d_bytes, c->d_pages, c->d_rwins,
                                      static_cast<int>(c->hrwins.size()), c->d_rwin_ticket, c->rwin_grid, cp,
                                      (neg ? 1 : 0) | ((ctx->opt_regex_debug & 0xFF) << 8),
-                                     c->d_page_flags, c->d_page_err, c->d_flags);
+                                     c->d_page_flags, c->d_page_err, c->d_flags, idx_in, idx_out);
         } else if (c->d_dfa) {
             Timed t(ctx, "regex_lanes");
             pqre::launch_regex_lanes(s, c->d_dfa, c->dfa_bytes, c->d_bytes, c->d_pages, c->npages, c->d_dicts,

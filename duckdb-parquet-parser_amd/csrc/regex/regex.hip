@@ -482,7 +482,9 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                                                                   ColumnParams cp, int neg,
                                                                   uint8_t* __restrict__ page_flags,
                                                                   DevErr* __restrict__ page_err,
-                                                                  int32_t* __restrict__ err_any) {
+                                                                  int32_t* __restrict__ err_any,
+                                                                  const uint16_t* __restrict__ index_in,
+                                                                  uint16_t* __restrict__ index_out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
     {
         const uint4* src = reinterpret_cast<const uint4*>(dfa_img);
@@ -546,192 +548,212 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
         }
         __builtin_amdgcn_wave_barrier();
         const uint32_t np = static_cast<uint32_t>(Bc.np);
-        // ── strings: L lanes per page ───────────────────────────────────
-        const uint32_t lg = np <= 1 ? 0u : 32u - __builtin_clz(np - 1);  // ceil log2
-        const uint32_t L = kWave >> lg;
-        const uint32_t q = lane() / L, sg = lane() % L;
-        const bool act = q < np && !(dbg & 2);
-        const uint32_t qs = min(q, 63u);
-        const uint64_t poff = (static_cast<uint64_t>(__shfl(static_cast<int>(pgc.off >> 32), static_cast<int>(qs))) << 32) |
-                              static_cast<uint32_t>(__shfl(static_cast<int>(pgc.off), static_cast<int>(qs)));
-        const uint32_t size = static_cast<uint32_t>(max(__shfl(pgc.size, static_cast<int>(qs)), 0));
-        const uint32_t nvq = static_cast<uint32_t>(max(__shfl(pgc.nvals, static_cast<int>(qs)), 0));
-        const uint32_t pay = static_cast<uint32_t>(poff - Bc.img_lo);
-        // levels (segment 0 lanes; any problem -> the exact walk below)
-        uint32_t pos0 = 0, nn = nvq;
-        bool bad = false;
-        if (act && sg == 0 && (cp.max_def > 0 || cp.max_rep > 0)) {
-            const uint32_t* pw = reinterpret_cast<const uint32_t*>(cur + pay);
-            auto rd8 = [&](uint32_t a) { return lds_u64(pw, a); };
-            if (cp.max_def > 0) {
-                if (pos0 + 4 > size) bad = true;
-                else {
-                    const uint32_t dl = static_cast<uint32_t>(rd8(pos0));
-                    pos0 += 4;
-                    if (static_cast<uint64_t>(pos0) + dl > size) bad = true;
-                    else {
-                        LRle r = lrle(pos0, dl, level_bw(cp.max_def));
-                        const uint32_t bwd = r.bw;
-                        nn = 0;
-                        bad = lane_rle(r, rd8, nvq, [&](uint32_t kind, uint32_t k, uint32_t arg) {
-                            if (kind == 0) {
-                                if (arg >= md) nn += k;
-                            } else {
-                                for (uint32_t i = 0; i < k; i++)
-                                    if (lds_bits(pw, size, static_cast<uint64_t>(arg) + i * bwd, bwd) >= md) nn++;
-                            }
-                        }) != 0;
-                        pos0 += dl;
-                    }
-                }
-            }
-            if (!bad && cp.max_rep > 0) {
-                if (pos0 + 4 > size) bad = true;
-                else {
-                    const uint32_t rl = static_cast<uint32_t>(rd8(pos0));
-                    pos0 += 4;
-                    if (static_cast<uint64_t>(pos0) + rl > size) bad = true;
-                    else pos0 += rl;
-                }
-            }
-        }
-        const int src0 = static_cast<int>(q * L);
-        pos0 = static_cast<uint32_t>(__shfl(static_cast<int>(pos0), src0));
-        nn = static_cast<uint32_t>(__shfl(static_cast<int>(nn), src0));
-        bad = __shfl(static_cast<int>(bad), src0) != 0;
-        // this lane's segment of [pos0, size) and its first candidate string
-        // start (a position whose u32 length fits the page), 16 positions
-        // per aligned 16-byte read
-        const uint32_t span = size > pos0 ? size - pos0 : 0u;
-        const uint32_t lo = pos0 + static_cast<uint32_t>((static_cast<uint64_t>(span) * sg) / L);
-        const uint32_t hi = sg + 1 == L ? size : pos0 + static_cast<uint32_t>((static_cast<uint64_t>(span) * (sg + 1)) / L);
-        const uint32_t A = pay;  // window byte of the page's payload
-        uint32_t c0 = ~0u;
-        if (act && !bad) {
-            if (sg == 0) {
-                c0 = pos0;
-            } else {
-                for (uint32_t a = (A + lo) & ~15u; a < A + hi && c0 == ~0u; a += 16) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(cur + a);
-                    const uint32_t d4 = stage[(a >> 2) + 4];
-                    const uint32_t d[5] = {v.x, v.y, v.z, v.w, d4};
-#pragma unroll
-                    for (uint32_t k = 0; k < 16; k++) {
-                        const uint32_t cpos = a + k - A;
-                        const uint32_t len = (k & 3) == 0 ? d[k >> 2] : __builtin_amdgcn_alignbyte(d[(k >> 2) + 1], d[k >> 2], k & 3);
-                        const bool ok = cpos >= lo && cpos < hi && cpos + 4 <= size && len <= size - cpos - 4;
-                        c0 = (ok && c0 == ~0u) ? cpos : c0;
-                    }
-                }
-            }
-        }
-        // its chain to the segment end: exit position, strings, and whether a
-        // read failed (at the exit)
-        uint32_t ex = c0, n = 0;
-        bool fail = false;
-        if (act && c0 != ~0u) {
-            while (ex < hi) {
-                if (ex + 4 > size) { fail = true; break; }
-                const uint32_t len = st_u32(stage, A + ex);
-                if (len > size - ex - 4) { fail = true; break; }
-                ex += 4 + len;
-                n++;
-            }
-        }
-        // link: every segment must start where the previous one left (no
-        // failed chain before the last segment); else the exact walk
-        const uint32_t prev = static_cast<uint32_t>(__shfl(static_cast<int>(ex), static_cast<int>(lane()) - 1));
-        const uint32_t pfail = static_cast<uint32_t>(__shfl(static_cast<int>(fail), static_cast<int>(lane()) - 1));
-        const uint32_t start = c0;
-        const bool mism = act && !bad && (c0 == ~0u || (sg > 0 && (pfail || prev != c0)));
-        // page-local placement of each segment's strings
-        const uint32_t inc = wave_incl_scan(n);
-        const uint32_t pbase = static_cast<uint32_t>(__shfl(static_cast<int>(inc - n), src0));
-        const uint32_t before = inc - n - pbase;
-        const uint32_t last = min(src0 + L - 1, 63u);
-        const uint32_t total = static_cast<uint32_t>(__shfl(static_cast<int>(inc), static_cast<int>(last))) - pbase;
-        // exact walk needed: unlinked segments, a level problem, or fewer than
-        // nn strings before the chain fails / the page ends
-        const uint64_t mm = __ballot(act && (mism || bad));
-        const uint32_t pmis = ((mm >> src0) & ((L >= 64 ? ~0ull : ((1ull << L) - 1ull)))) != 0 ? 1u : 0u;
-        const bool page_ok = act && !pmis && total >= nn && !(dbg & 4);
-        // emit: this segment's strings with page index < nn
-        if (page_ok && start != ~0u && before < nn) {
-            const uint32_t keep = min(n, nn - before);
-            uint16_t* lst = list + pay / 4 + before;
-            uint32_t pos = start;
-            for (uint32_t i = 0; i < keep; i++) {
-                const uint32_t len = st_u32(stage, A + pos);
-                lst[i] = static_cast<uint16_t>(A + pos + 4);
-                pos += 4 + len;
-            }
-        }
-        if (act && sg == 0) pcnt[q] = page_ok ? nn : ~0u;  // ~0: exact walk
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // exact walk (one lane per page) where the segments did not settle it
+        // The strings of the window's pages, as window offsets in `list`:
+        // from the chunk's string index when an earlier scan built it
+        // (REQUIRED chunks: string k of page p is row first_row(p) + k), else
+        // by the lane-parallel walk below (which then files the index).
         const bool pl = lane() < np;
-        uint32_t cnt = pl && !(dbg & 2) ? pcnt[lane()] : 0u;
         const uint32_t mpay = static_cast<uint32_t>(pgc.off - Bc.img_lo);
-        if (pl && cnt == ~0u) {
-            cnt = 0;
-            const uint32_t* pw = reinterpret_cast<const uint32_t*>(cur + mpay);
-            auto rd8 = [&](uint32_t a) { return lds_u64(pw, a); };
-            DevErr* err = page_err + Bc.p0 + static_cast<int32_t>(lane());
-            const uint32_t msize = static_cast<uint32_t>(max(pgc.size, 0));
-            uint32_t pos = 0, mnn = static_cast<uint32_t>(max(pgc.nvals, 0));
-            int code = 0;
-            uint32_t epos = 0, eneed = 0;
-            if (cp.max_def > 0) {
-                if (pos + 4 > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
-                else {
-                    const uint32_t dl = static_cast<uint32_t>(rd8(pos));
-                    pos += 4;
-                    if (static_cast<uint64_t>(pos) + dl > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = dl; }
+        uint32_t cnt = 0, lb = mpay / 4;
+        if (index_in) {
+            const int64_t fr0 = static_cast<int64_t>(
+                static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(pgc.first_row), 0))) |
+                (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(pgc.first_row >> 32), 0))) << 32));
+            const int64_t fr = pl ? pgc.first_row : fr0;
+            cnt = pl ? static_cast<uint32_t>(max(pgc.nvals, 0)) : 0u;
+            lb = static_cast<uint32_t>(fr - fr0);
+            const uint32_t tot = bcast_last(wave_incl_scan(cnt));
+            for (uint32_t k = lane(); k < tot; k += kWave) list[k] = index_in[fr0 + k];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            // ── strings: L lanes per page ───────────────────────────────────
+            const uint32_t lg = np <= 1 ? 0u : 32u - __builtin_clz(np - 1);  // ceil log2
+            const uint32_t L = kWave >> lg;
+            const uint32_t q = lane() / L, sg = lane() % L;
+            const bool act = q < np && !(dbg & 2);
+            const uint32_t qs = min(q, 63u);
+            const uint64_t poff = (static_cast<uint64_t>(__shfl(static_cast<int>(pgc.off >> 32), static_cast<int>(qs))) << 32) |
+                                  static_cast<uint32_t>(__shfl(static_cast<int>(pgc.off), static_cast<int>(qs)));
+            const uint32_t size = static_cast<uint32_t>(max(__shfl(pgc.size, static_cast<int>(qs)), 0));
+            const uint32_t nvq = static_cast<uint32_t>(max(__shfl(pgc.nvals, static_cast<int>(qs)), 0));
+            const uint32_t pay = static_cast<uint32_t>(poff - Bc.img_lo);
+            // levels (segment 0 lanes; any problem -> the exact walk below)
+            uint32_t pos0 = 0, nn = nvq;
+            bool bad = false;
+            if (act && sg == 0 && (cp.max_def > 0 || cp.max_rep > 0)) {
+                const uint32_t* pw = reinterpret_cast<const uint32_t*>(cur + pay);
+                auto rd8 = [&](uint32_t a) { return lds_u64(pw, a); };
+                if (cp.max_def > 0) {
+                    if (pos0 + 4 > size) bad = true;
                     else {
-                        LRle r = lrle(pos, dl, level_bw(cp.max_def));
-                        const uint32_t bwd = r.bw;
-                        const uint32_t nv = mnn;
-                        mnn = 0;
-                        code = lane_rle(r, rd8, nv, [&](uint32_t kind, uint32_t k, uint32_t arg) {
-                            if (kind == 0) {
-                                if (arg >= md) mnn += k;
-                            } else {
-                                for (uint32_t i = 0; i < k; i++)
-                                    if (lds_bits(pw, msize, static_cast<uint64_t>(arg) + i * bwd, bwd) >= md) mnn++;
-                            }
-                        });
-                        pos += dl;
+                        const uint32_t dl = static_cast<uint32_t>(rd8(pos0));
+                        pos0 += 4;
+                        if (static_cast<uint64_t>(pos0) + dl > size) bad = true;
+                        else {
+                            LRle r = lrle(pos0, dl, level_bw(cp.max_def));
+                            const uint32_t bwd = r.bw;
+                            nn = 0;
+                            bad = lane_rle(r, rd8, nvq, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                                if (kind == 0) {
+                                    if (arg >= md) nn += k;
+                                } else {
+                                    for (uint32_t i = 0; i < k; i++)
+                                        if (lds_bits(pw, size, static_cast<uint64_t>(arg) + i * bwd, bwd) >= md) nn++;
+                                }
+                            }) != 0;
+                            pos0 += dl;
+                        }
+                    }
+                }
+                if (!bad && cp.max_rep > 0) {
+                    if (pos0 + 4 > size) bad = true;
+                    else {
+                        const uint32_t rl = static_cast<uint32_t>(rd8(pos0));
+                        pos0 += 4;
+                        if (static_cast<uint64_t>(pos0) + rl > size) bad = true;
+                        else pos0 += rl;
                     }
                 }
             }
-            if (!code && cp.max_rep > 0) {
-                if (pos + 4 > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
-                else {
-                    const uint32_t rl = static_cast<uint32_t>(rd8(pos));
-                    pos += 4;
-                    if (static_cast<uint64_t>(pos) + rl > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = rl; }
-                    else pos += rl;
+            const int src0 = static_cast<int>(q * L);
+            pos0 = static_cast<uint32_t>(__shfl(static_cast<int>(pos0), src0));
+            nn = static_cast<uint32_t>(__shfl(static_cast<int>(nn), src0));
+            bad = __shfl(static_cast<int>(bad), src0) != 0;
+            // this lane's segment of [pos0, size) and its first candidate string
+            // start (a position whose u32 length fits the page), 16 positions
+            // per aligned 16-byte read
+            const uint32_t span = size > pos0 ? size - pos0 : 0u;
+            const uint32_t lo = pos0 + static_cast<uint32_t>((static_cast<uint64_t>(span) * sg) / L);
+            const uint32_t hi = sg + 1 == L ? size : pos0 + static_cast<uint32_t>((static_cast<uint64_t>(span) * (sg + 1)) / L);
+            const uint32_t A = pay;  // window byte of the page's payload
+            uint32_t c0 = ~0u;
+            if (act && !bad) {
+                if (sg == 0) {
+                    c0 = pos0;
+                } else {
+                    for (uint32_t a = (A + lo) & ~15u; a < A + hi && c0 == ~0u; a += 16) {
+                        const uint4 v = *reinterpret_cast<const uint4*>(cur + a);
+                        const uint32_t d4 = stage[(a >> 2) + 4];
+                        const uint32_t d[5] = {v.x, v.y, v.z, v.w, d4};
+    #pragma unroll
+                        for (uint32_t k = 0; k < 16; k++) {
+                            const uint32_t cpos = a + k - A;
+                            const uint32_t len = (k & 3) == 0 ? d[k >> 2] : __builtin_amdgcn_alignbyte(d[(k >> 2) + 1], d[k >> 2], k & 3);
+                            const bool ok = cpos >= lo && cpos < hi && cpos + 4 <= size && len <= size - cpos - 4;
+                            c0 = (ok && c0 == ~0u) ? cpos : c0;
+                        }
+                    }
                 }
             }
-            uint16_t* lst = list + mpay / 4;  // this page's list region (<= slot / 4 entries)
-            for (uint32_t k = 0; k < mnn && !code; k++) {  // column_reader.cpp:249-253
-                if (static_cast<uint64_t>(pos) + 4 > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; break; }
-                const uint32_t len = static_cast<uint32_t>(rd8(pos));
-                pos += 4;
-                if (static_cast<uint64_t>(pos) + len > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = len; break; }
-                lst[cnt++] = static_cast<uint16_t>(mpay + pos);  // window offset (the length is at offset - 4)
-                pos += len;
+            // its chain to the segment end: exit position, strings, and whether a
+            // read failed (at the exit)
+            uint32_t ex = c0, n = 0;
+            bool fail = false;
+            if (act && c0 != ~0u) {
+                while (ex < hi) {
+                    if (ex + 4 > size) { fail = true; break; }
+                    const uint32_t len = st_u32(stage, A + ex);
+                    if (len > size - ex - 4) { fail = true; break; }
+                    ex += 4 + len;
+                    n++;
+                }
             }
-            if (code) {
-                lane_err(err, err_any, code, epos, eneed, msize);
+            // link: every segment must start where the previous one left (no
+            // failed chain before the last segment); else the exact walk
+            const uint32_t prev = static_cast<uint32_t>(__shfl(static_cast<int>(ex), static_cast<int>(lane()) - 1));
+            const uint32_t pfail = static_cast<uint32_t>(__shfl(static_cast<int>(fail), static_cast<int>(lane()) - 1));
+            const uint32_t start = c0;
+            const bool mism = act && !bad && (c0 == ~0u || (sg > 0 && (pfail || prev != c0)));
+            // page-local placement of each segment's strings
+            const uint32_t inc = wave_incl_scan(n);
+            const uint32_t pbase = static_cast<uint32_t>(__shfl(static_cast<int>(inc - n), src0));
+            const uint32_t before = inc - n - pbase;
+            const uint32_t last = min(src0 + L - 1, 63u);
+            const uint32_t total = static_cast<uint32_t>(__shfl(static_cast<int>(inc), static_cast<int>(last))) - pbase;
+            // exact walk needed: unlinked segments, a level problem, or fewer than
+            // nn strings before the chain fails / the page ends
+            const uint64_t mm = __ballot(act && (mism || bad));
+            const uint32_t pmis = ((mm >> src0) & ((L >= 64 ? ~0ull : ((1ull << L) - 1ull)))) != 0 ? 1u : 0u;
+            const bool page_ok = act && !pmis && total >= nn && !(dbg & 4);
+            // emit: this segment's strings with page index < nn
+            if (page_ok && start != ~0u && before < nn) {
+                const uint32_t keep = min(n, nn - before);
+                uint16_t* lst = list + pay / 4 + before;
+                uint32_t pos = start;
+                for (uint32_t i = 0; i < keep; i++) {
+                    const uint32_t len = st_u32(stage, A + pos);
+                    lst[i] = static_cast<uint16_t>(A + pos + 4);
+                    pos += 4 + len;
+                }
+            }
+            if (act && sg == 0) pcnt[q] = page_ok ? nn : ~0u;  // ~0: exact walk
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // exact walk (one lane per page) where the segments did not settle it
+            cnt = pl && !(dbg & 2) ? pcnt[lane()] : 0u;
+            if (pl && cnt == ~0u) {
                 cnt = 0;
+                const uint32_t* pw = reinterpret_cast<const uint32_t*>(cur + mpay);
+                auto rd8 = [&](uint32_t a) { return lds_u64(pw, a); };
+                DevErr* err = page_err + Bc.p0 + static_cast<int32_t>(lane());
+                const uint32_t msize = static_cast<uint32_t>(max(pgc.size, 0));
+                uint32_t pos = 0, mnn = static_cast<uint32_t>(max(pgc.nvals, 0));
+                int code = 0;
+                uint32_t epos = 0, eneed = 0;
+                if (cp.max_def > 0) {
+                    if (pos + 4 > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
+                    else {
+                        const uint32_t dl = static_cast<uint32_t>(rd8(pos));
+                        pos += 4;
+                        if (static_cast<uint64_t>(pos) + dl > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = dl; }
+                        else {
+                            LRle r = lrle(pos, dl, level_bw(cp.max_def));
+                            const uint32_t bwd = r.bw;
+                            const uint32_t nv = mnn;
+                            mnn = 0;
+                            code = lane_rle(r, rd8, nv, [&](uint32_t kind, uint32_t k, uint32_t arg) {
+                                if (kind == 0) {
+                                    if (arg >= md) mnn += k;
+                                } else {
+                                    for (uint32_t i = 0; i < k; i++)
+                                        if (lds_bits(pw, msize, static_cast<uint64_t>(arg) + i * bwd, bwd) >= md) mnn++;
+                                }
+                            });
+                            pos += dl;
+                        }
+                    }
+                }
+                if (!code && cp.max_rep > 0) {
+                    if (pos + 4 > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; }
+                    else {
+                        const uint32_t rl = static_cast<uint32_t>(rd8(pos));
+                        pos += 4;
+                        if (static_cast<uint64_t>(pos) + rl > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = rl; }
+                        else pos += rl;
+                    }
+                }
+                uint16_t* lst = list + mpay / 4;  // this page's list region (<= slot / 4 entries)
+                for (uint32_t k = 0; k < mnn && !code; k++) {  // column_reader.cpp:249-253
+                    if (static_cast<uint64_t>(pos) + 4 > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = 4; break; }
+                    const uint32_t len = static_cast<uint32_t>(rd8(pos));
+                    pos += 4;
+                    if (static_cast<uint64_t>(pos) + len > msize) { code = PQ_ERR_BUFFER; epos = pos; eneed = len; break; }
+                    lst[cnt++] = static_cast<uint16_t>(mpay + pos);  // window offset (the length is at offset - 4)
+                    pos += len;
+                }
+                if (code) {
+                    lane_err(err, err_any, code, epos, eneed, msize);
+                    cnt = 0;
+                }
             }
+            if (index_out && pl)
+                for (uint32_t k = 0; k < cnt; k++) index_out[pgc.first_row + k] = list[mpay / 4 + k];
         }
         // flatten: string g of the window -> (page lane, k)
         const uint32_t pinc = wave_incl_scan(cnt);
         pref[lane()] = pinc;
-        lbase[lane()] = mpay / 4;
+        lbase[lane()] = lb;
         const uint32_t wtotal = bcast_last(pinc);
         __builtin_amdgcn_wave_barrier();
         for (uint32_t g0 = 0; g0 < ((dbg & 1) ? 0u : wtotal); g0 += kStrPerLane * kWave) {
@@ -878,13 +900,13 @@ uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes) {
 void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
                         const uint8_t* bytes, const DevPage* pages, const pqk::DevBatch* wins, int nwins,
                         int32_t* ticket, int grid, ColumnParams cp, int neg, uint8_t* page_flags,
-                        DevErr* page_err, int32_t* err_any) {
+                        DevErr* page_err, int32_t* err_any, const uint16_t* index_in, uint16_t* index_out) {
     if (nwins <= 0) return;
     pqk::ensure_dyn_lds(reinterpret_cast<const void*>(k_regex_plain), 160 * 1024);
     hipLaunchKernelGGL(k_regex_plain, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes) * kWave),
                        regex_plain_lds(dfa_bytes, win_bytes),
                        s, dfa, dfa_bytes, win_bytes, bytes, pages, wins, nwins, ticket, cp, neg, page_flags,
-                       page_err, err_any);
+                       page_err, err_any, index_in, index_out);
 }
 
 int regex_plain_occupancy(uint32_t lds) {  // the LDS sets it: one workgroup of regex_plain_waves waves per CU

@@ -84,7 +84,8 @@ int regex_plain_occupancy(uint32_t lds);
 void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
                         const uint8_t* bytes, const pqk::DevPage* pages, const pqk::DevBatch* wins, int nwins,
                         int32_t* ticket, int grid, pqk::ColumnParams cp, int neg, uint8_t* page_flags,
-                        pqk::DevErr* page_err, int32_t* err_any);
+                        pqk::DevErr* page_err, int32_t* err_any,
+                        const uint16_t* index_in = nullptr, uint16_t* index_out = nullptr);
 
 void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, const uint8_t* bytes,
                         const pqk::DevPage* pages, int npages, const pqk::DevDict* dicts,

@@ -174,7 +174,9 @@ int pq_ctx_sync(pq_ctx* ctx);
  *                 multiple of 16; 8192); "regex_reuse" 1 (default): a scan
  *                 of a chunk whose earlier pipe decode was checked error-free
  *                 (pq_decode / pq_decode_check) reads that decode's codes
- *                 instead of recomputing them
+ *                 instead of recomputing them; "regex_index" 1 (default): a
+ *                 REQUIRED PLAIN chunk's first error-free windowed scan keeps
+ *                 every string's window offset (2 B per row) for later scans
  * Diagnostics (timing studies only; outputs are not valid with bits set):
  *   "fused_debug", "regex_debug" ablation bits, "fused_prof"
  *   per-phase clocks.

@@ -184,3 +184,44 @@ def test_decode_regex_one_pass(ctx, name, cols, n, layout, neg):
         dc.decode_async()
         dc.decode_check()
     dc.free()
+
+
+@pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT])
+def test_string_index_reuse(ctx, layout):
+    """REQUIRED PLAIN chunks: the first error-free windowed scan files the
+    string index, later scans read it; a window-size change rebuilds it; the
+    page sets stay the oracle's throughout, with the index on and off."""
+    cols = gen.c3_cols()
+    f = gen.build(cols, 30000, 1, seed=13, layout=layout, rows_per_page=0 if layout == gen.REF_LAYOUT else 2500)
+    chunks = file_chunks(f, 0)
+    pats = ["special.*requests", "e", "^(carefully|quickly) ", "[0-9]", "ly\\s"]
+    exp = {(p, n): golden_pages(f, chunks, p, n) for p in pats for n in (False, True)}
+    dc = ctx.upload(f, chunks)
+    try:
+        for win in (8192, 4096, 8192):
+            ctx.set_option("regex_win", win)
+            for idx in (1, 0, 1):
+                ctx.set_option("regex_index", idx)
+                for p in pats:
+                    for n in (False, True):
+                        assert np.array_equal(dc.regex_pages(p, n), exp[(p, n)]), (win, idx, p, n)
+    finally:
+        ctx.set_option("regex_win", 8192)
+        ctx.set_option("regex_index", 1)
+        dc.free()
+
+
+def test_string_index_not_filed_on_error(ctx):
+    """A chunk whose scan fails files no index: every later scan reports the
+    same error."""
+    import struct
+    import pqbuild as B
+    pay = struct.pack("<I", 7) + b"special" + struct.pack("<I", 50) + b"xy"
+    f, ch = B.build_file([B.data_header(len(pay), 2, 0) + pay], gen.BYTE_ARRAY, False, 2)
+    rc_o, msg_o, _ = O.read_all(f, to_oracle_chunk(ch))
+    dc = ctx.upload(f, [to_desc(ch)])
+    for _ in range(3):
+        with pytest.raises(capi.PqError) as ei:
+            dc.regex_pages("special", False)
+        assert ei.value.code == rc_o and ei.value.msg == msg_o
+    dc.free()
