@@ -86,3 +86,30 @@ def test_spec_walk_pyarrow_statistics(tmp_path):
     assert ch.total_compressed_size >= 8 << 20
     rc, msg, t = _check(f, ch)
     assert rc == 0 and len(t) > 100
+
+
+def test_header_field8_not_struct_is_skipped():
+    """PageHeader field 8 with a non-struct wire type (an i32 here) is skipped
+    like any unknown field (metadata.cpp:149-151): the walk finds the same
+    pages and header sizes as the reference, whose decode is unaffected."""
+    import struct
+    import pqbuild as B
+    from oracle import oracle as O
+    from util import to_oracle_chunk
+    vals = [b"ab", b"cde", b"f"]
+    pay = B.plain_ba(vals)
+    hdr = bytes(B.TW().i32(1, 0).i32(2, len(pay)).i32(3, len(pay)).begin(5).i32(1, 3).i32(2, 0).i32(3, 3)
+                .i32(4, 3).end().i32(8, 12345).stop().b)
+    f, ch = B.build_file([hdr + pay, hdr + pay], gen.BYTE_ARRAY, False, 6)
+    rc_o, msg_o, col = O.read_all(f, to_oracle_chunk(ch))
+    assert rc_o == 0, msg_o
+    rc, msg, t = capi.build_page_table(f, _desc(ch))
+    assert rc == 0, msg
+    assert len(t) == 2 and [p.num_values for p in t] == [3, 3]
+    assert t[0].payload_offset - t[0].header_offset == len(hdr)
+    assert t[1].header_offset == t[0].payload_offset + len(pay)
+
+
+def _desc(ch):
+    from util import to_desc
+    return to_desc(ch)
