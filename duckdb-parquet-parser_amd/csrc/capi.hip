@@ -2199,6 +2199,9 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     uint32_t maxslot = 0;
     for (const auto& p : hp) maxslot = std::max(maxslot, (static_cast<uint32_t>(std::max(p.size, 0)) + 15) / 16 * 16 + 16);
     const uint32_t win = std::max<uint32_t>(static_cast<uint32_t>(ctx->opt_regex_win), maxslot);
+    // the kernel lists strings by u16 window offsets (and the string index
+    // keeps them): pages whose slot leaves no room take k_regex_lanes
+    if (win + 32 > 65535u) return false;
     if (pqre::regex_plain_waves(c->dfa_bytes, win) == 0) return false;
     const uint32_t lds = pqre::regex_plain_lds(c->dfa_bytes, win);
     if (lds > 160 * 1024) return false;

@@ -186,13 +186,16 @@ def test_decode_regex_one_pass(ctx, name, cols, n, layout, neg):
     dc.free()
 
 
-@pytest.mark.parametrize("layout", [gen.REF_LAYOUT, gen.ARROW_LAYOUT])
-def test_string_index_reuse(ctx, layout):
+@pytest.mark.parametrize("layout,rpp", [(gen.REF_LAYOUT, 0), (gen.ARROW_LAYOUT, 700), (gen.ARROW_LAYOUT, 1300),
+                                        (gen.ARROW_LAYOUT, 2500)], ids=["ref", "arrow_21k", "arrow_40k", "arrow_77k"])
+def test_string_index_reuse(ctx, layout, rpp):
     """REQUIRED PLAIN chunks: the first error-free windowed scan files the
     string index, later scans read it; a window-size change rebuilds it; the
-    page sets stay the oracle's throughout, with the index on and off."""
+    page sets stay the oracle's throughout, with the index on and off.  Pages
+    of ~21, ~40 and ~77 KB: windows up to the u16 offset limit, and pages
+    past it (k_regex_lanes)."""
     cols = gen.c3_cols()
-    f = gen.build(cols, 30000, 1, seed=13, layout=layout, rows_per_page=0 if layout == gen.REF_LAYOUT else 2500)
+    f = gen.build(cols, 30000, 1, seed=13, layout=layout, rows_per_page=rpp)
     chunks = file_chunks(f, 0)
     pats = ["special.*requests", "e", "^(carefully|quickly) ", "[0-9]", "ly\\s"]
     exp = {(p, n): golden_pages(f, chunks, p, n) for p in pats for n in (False, True)}
