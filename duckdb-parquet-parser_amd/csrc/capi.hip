@@ -153,7 +153,7 @@ struct pq_chunk {
     uint16_t* d_rx_index = nullptr;
     bool rx_index_ok = false, rx_index_pending = false;
     uint32_t rx_index_win = 0;
-    int32_t pipe_dict_nvals = 0;  // declared entries of the pipe's dictionary (arming bound)
+    uint32_t pipe_dict_payload = ~0u;  // payload bytes of the pipe's dictionary (arming bound)
     int32_t* d_tile_nn = nullptr;
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
@@ -483,7 +483,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
     c->hbig = std::move(big);
     c->big_max_bytes = big_bytes;
     c->pipe_dict = dict_id;
-    c->pipe_dict_nvals = d.nvals;
+    c->pipe_dict_payload = static_cast<uint32_t>(d.size);
     c->pipe_entry_base = d.entry_base;
     c->pipe_dict_chars_bytes = chars_bytes;
     c->pipe_dict_bytes = dict_bytes;
@@ -2374,11 +2374,11 @@ int pq_decode_regex_async(pq_ctx* ctx, pq_chunk* c, pq_column* out, const char* 
     DevGuard dg(ctx);
     if (int rc = regex_prepare(ctx, c, pattern)) return rc;
     // one pass when the decode takes the pipe (dictionary pages only, one
-    // dictionary small enough for the writer's mask); else the decode, then
-    // the scan over its codes
+    // dictionary of < 32 KiB: the writer keeps each entry's match bit beside
+    // its length); else the decode, then the scan over its codes
     const bool plain_go = c->plain && ctx->opt_plain;
     const bool one = c->pipe && ctx->opt_pipe && ctx->opt_regex_codes && !plain_go && c->ndicts > 0 &&
-                     c->pipe_dict_nvals >= 0 && static_cast<uint32_t>(c->pipe_dict_nvals) <= pqk::kArmEntries;
+                     c->pipe_dict_payload < pqk::kArmDictBytes;
     if (!one) {
         if (int rc = pq_decode_async(ctx, c, out)) return rc;
         return pq_regex_pages_async(ctx, c, pattern, neg);

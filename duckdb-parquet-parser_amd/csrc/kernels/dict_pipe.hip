@@ -890,7 +890,6 @@ struct WriteArgs {
     uint8_t* page_flags;
 };
 
-constexpr uint32_t kArmWords = 512;  // armed filter: dictionaries up to 16,384 entries (host checks)
 
 template <bool kArmed>
 __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
@@ -905,17 +904,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     WriteLds& S = reinterpret_cast<WriteLds*>(smem + a.dict_bytes)[wv];
     const DevDict d = a.dicts[a.dict_id];
     const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    __shared__ uint32_t mbits[kArmed ? kArmWords : 1];
     constexpr bool armed = kArmed;
-    if (armed)
-        for (uint32_t w = threadIdx.x; w < kArmWords; w += blockDim.x) {
-            uint32_t m = 0;
-            for (uint32_t k = 0; k < 32; k++) {
-                const uint32_t e = w * 32 + k;
-                m |= (e < dict_n && a.match[e] != 0 ? 1u : 0u) << k;
-            }
-            mbits[w] = m ^ (a.match_neg ? 0xFFFFFFFFu : 0u);  // bit = this entry satisfies the predicate
-        }
     // each wavefront owns a contiguous run of tiles (consecutive rows): the
     // descriptors of up to 64 tiles are loaded at once, one per lane, and the
     // next tile's codes are loaded before this tile's stores are issued
@@ -944,9 +933,20 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
         uint4* dst = reinterpret_cast<uint4*>(dw);
         copy_blocks(dst, src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
-        copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
-            return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
-        });
+        if (armed) {
+            // entry = pos | len << 16 | satisfies-the-predicate << 31 (the
+            // host arms only dictionaries under 32 KiB: len < 2^15)
+            const uint64_t* es = a.entries + d.entry_base;
+            for (uint32_t k = threadIdx.x; k < dict_n; k += blockDim.x) {
+                const uint64_t e = es[k];
+                const uint32_t sat = (a.match[k] != 0) != (a.match_neg != 0) ? 1u : 0u;
+                dtab[k] = static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16) | (sat << 31);
+            }
+        } else {
+            copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
+                return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
+            });
+        }
     }
     acc = wave_sum64(acc);
     if (lane() == 0) red[wv] = acc;
@@ -1011,23 +1011,19 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
                     cur[k] = l8 + k < m ? (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : kNull;
             }
             // this lane's rows 8l .. 8l + 7: lengths, dictionary offsets, validity
-            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0;
+            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0, sat = 0;
 #pragma unroll
             for (int k = 0; k < kRowsPerLane; k++) {
                 const bool valid = cur[k] < dict_n;
                 const uint32_t e = valid ? dtab[cur[k]] : 0u;
-                len[k] = e >> 16;
+                len[k] = armed ? ((e >> 16) & 0x7FFFu) : (e >> 16);
+                if (armed) sat |= e;
                 src[k] = e & 0xFFFFu;
                 vb |= (valid ? 1u : 0u) << k;
                 acc += len[k];
             }
-            if (armed) {  // the page filter: any row of the tile whose entry satisfies the predicate
-                bool hit = false;
-#pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++)
-                    hit |= ((vb >> k) & 1u) && ((mbits[(cur[k] >> 5) & (kArmWords - 1)] >> (cur[k] & 31u)) & 1u);
-                if (__ballot(hit) && lane() == 0) a.page_flags[__builtin_amdgcn_readlane(myp, i)] = 0;
-            }
+            if (armed && __ballot(sat >> 31) && lane() == 0)  // the page filter: a row whose entry satisfies it
+                a.page_flags[__builtin_amdgcn_readlane(myp, i)] = 0;
             const uint32_t incl = wave_incl_scan(acc);
             const uint32_t total = bcast_last(incl);
             {

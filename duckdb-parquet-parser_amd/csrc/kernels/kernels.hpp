@@ -169,11 +169,11 @@ struct PipeLaunch {
     int write_waves;            // writer waves per k_pipe_write workgroup (planned with P.lds / P.grid)
     uint32_t* znext;            // cleared by k_pipe_write (the next decode's flags/bsum/flist[0]), or null
     uint32_t znext_words;
-    const uint8_t* match = nullptr;  // armed page filter (k_pipe_write), dictionaries <= kArmEntries
+    const uint8_t* match = nullptr;  // armed page filter (k_pipe_write), dictionary payloads < kArmDictBytes
     int match_neg = 0;
     uint8_t* page_flags = nullptr;
 };
-constexpr uint32_t kArmEntries = 16384;
+constexpr uint32_t kArmDictBytes = 32768;  // every entry length < 2^15: the match bit rides in the entry word
 struct PipePlan {
     uint32_t lds;       // dynamic LDS bytes of k_pipe_write
     int blocks_per_cu;  // 0: the dictionary does not fit

@@ -261,8 +261,9 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* chunk, const char* pattern, int 
 int pq_regex_pages_result(pq_ctx* ctx, pq_chunk* chunk, uint8_t* page_flags);
 /* ColumnReader::read_all and the --regex-column filter of the same chunk in
  * one pass (the C5 shape: decode + filter): on dictionary chunks the pipe
- * takes, the pattern runs once per dictionary entry and k_pipe_write tests
- * every row's entry while it writes the column; otherwise the decode, then
+ * takes (dictionary payload < 32 KiB), the pattern runs once per dictionary
+ * entry and k_pipe_write tests every row's entry while it writes the column;
+ * otherwise the decode, then
  * pq_regex_pages_async over its codes.  Results: pq_decode_check /
  * pq_column_copy_out for the column (decode the chunk once with pq_decode
  * first, so the output is sized), pq_regex_pages_result for the flags. */
