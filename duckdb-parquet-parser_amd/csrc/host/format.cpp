@@ -2,7 +2,10 @@
 #include "format.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 namespace pqfmt {
@@ -579,10 +582,7 @@ std::vector<SpecSeg> speculate(const uint8_t* file, size_t len, size_t start, si
             }
         }
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < threads; t++) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
+    parallel_run(threads, threads, work);
     return segs;
 }
 
@@ -644,11 +644,7 @@ bool linked_walk(std::vector<SpecSeg>& segs, size_t start, const pq_chunk_desc& 
         return 0;
     };
     auto par = [&](auto&& fn) {
-        const int nt = std::max(1, std::min<int>(threads, static_cast<int>(np)));
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; t++) th.emplace_back([&, t] { for (size_t i = t; i < np; i += nt) fn(i); });
-        for (size_t i = 0; i < np; i += nt) fn(i);
-        for (auto& x : th) x.join();
+        parallel_run(static_cast<int>(np), threads, [&](int i) { fn(static_cast<size_t>(i)); });
     };
     par([&](size_t i) {
         const auto& r = segs[static_cast<size_t>(parts[i])].recs;
@@ -747,6 +743,86 @@ bool linked_walk(std::vector<SpecSeg>& segs, size_t start, const pq_chunk_desc& 
 
 }  // namespace
 
+namespace {
+struct HostPool {
+    std::mutex busy;  // one job at a time
+    std::mutex m;
+    std::condition_variable cv, done_cv;
+    std::vector<std::thread> workers;
+    const std::function<void(int)>* fn = nullptr;
+    int n = 0, want = 0, finished = 0;
+    uint64_t gen = 0;
+    bool stop = false;
+    std::atomic<int> next{0};
+    void worker(int id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* f;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return stop || (gen != seen && id < want); });
+                if (stop) return;
+                seen = gen;
+                f = fn;
+            }
+            for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) (*f)(i);
+            std::lock_guard<std::mutex> lk(m);
+            if (++finished == want) done_cv.notify_one();
+        }
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : workers) t.join();
+    }
+};
+HostPool& host_pool() {
+    static HostPool p;
+    return p;
+}
+}  // namespace
+
+void parallel_run(int n, int threads, const std::function<void(int)>& fn) {
+    if (n <= 0) return;
+    threads = std::max(1, std::min(threads, n));
+    if (threads == 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    HostPool& P = host_pool();
+    std::unique_lock<std::mutex> job(P.busy, std::try_to_lock);
+    if (!job.owns_lock()) {  // another host thread's job holds the pool
+        std::atomic<int> next{0};
+        std::vector<std::thread> th;
+        for (int t = 1; t < threads; t++)
+            th.emplace_back([&] { for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) fn(i); });
+        for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) fn(i);
+        for (auto& x : th) x.join();
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> lk(P.m);
+        while (static_cast<int>(P.workers.size()) < threads - 1) {
+            const int id = static_cast<int>(P.workers.size());
+            P.workers.emplace_back([&P, id] { P.worker(id); });
+        }
+        P.fn = &fn;
+        P.n = n;
+        P.want = threads - 1;
+        P.finished = 0;
+        P.next.store(0);
+        P.gen++;
+    }
+    P.cv.notify_all();
+    for (int i = P.next.fetch_add(1); i < n; i = P.next.fetch_add(1)) fn(i);
+    std::unique_lock<std::mutex> lk(P.m);
+    P.done_cv.wait(lk, [&] { return P.finished == P.want; });
+    P.fn = nullptr;
+}
+
 WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, int threads) {
     WalkResult w;
     try {
@@ -765,7 +841,7 @@ WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, i
         std::vector<SpecSeg> segs;
         w.pages.reserve(c.total_compressed_size > 0 ? static_cast<size_t>(std::min<int64_t>(c.total_compressed_size / 256, 1 << 22)) : 16);
         if (threads <= 0) threads = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
-        threads = static_cast<int>(std::min<int64_t>(threads, c.total_compressed_size / (2 << 20)));
+        threads = static_cast<int>(std::min<int64_t>(threads, c.total_compressed_size / (1 << 20)));
         // pages of tens of KiB or more: few enough for the exact walk alone
         // (probe the first headers; a segment would mostly scan page bytes)
         bool small_pages = true;

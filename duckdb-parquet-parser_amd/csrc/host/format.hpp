@@ -13,6 +13,7 @@
 #include <array>
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -153,9 +154,14 @@ struct WalkResult {
 // and DATA_PAGE_V2 pages walked as data pages (flags PQ_PAGE_V2).
 // Chunks of at least kSpecMinBytes (pq_chunk_desc.total_compressed_size)
 // walk speculatively on `threads` host threads (0 = up to 16; at most one
-// per 2 MiB), with results
+// per MiB), with results
 // identical to the serial walk.
 constexpr int64_t kSpecMinBytes = 4 << 20;
+// fn(0 .. n-1) on up to `threads` threads (the caller and a process-wide pool
+// of host workers, created once, so a walk does not pay a thread spawn per
+// call); a call that finds the pool busy (another host thread's walk) uses
+// fresh threads instead.
+void parallel_run(int n, int threads, const std::function<void(int)>& fn);
 WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, int threads = 0);
 
 // build_page_index: (data_offset, data_size, rg, col) per data page.

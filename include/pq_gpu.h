@@ -70,7 +70,7 @@ typedef struct {
     int64_t total_compressed_size; /* ColumnMetaData.total_compressed_size, or 0 if unknown:
                                       only an extent hint (a chunk of >= kSpecMinBytes = 4 MiB
                                       whose pages are small walks its page chain speculatively
-                                      on host threads, one per >= 2 MiB of extent;
+                                      on host threads, one per >= 1 MiB of extent;
                                       csrc/host/format.hpp) */
     int32_t ext_flags;      /* 0 (pq_file_chunk's default): the reference's format scope.
                                PQ_EXT_* bits widen it beyond the reference */

@@ -3,7 +3,7 @@ walk_chunk) yields exactly the serial walk's page table, status and message —
 the serial walk being ColumnReader::read_all's header loop
 (/root/reference/src/reader/column_reader.cpp:18-71), pinned to the compiled
 reference by test_oracle_golden.py.  A chunk of >= 4 MiB with
-total_compressed_size set walks speculatively (one thread per 2 MiB); 0
+total_compressed_size set walks speculatively (one thread per MiB); 0
 forces the serial walk."""
 import ctypes as C
 
