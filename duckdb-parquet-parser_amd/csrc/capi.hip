@@ -28,6 +28,10 @@ using pqk::DevErr;
 using pqk::DevPage;
 using pqk::DevTile;
 
+// host tables filled by index from several threads: no zero fill on resize
+template <class T>
+using HVec = std::vector<T, pqfmt::NoInitAlloc<T>>;
+
 struct PendingTimer {
     std::string name;
     hipEvent_t a, b;
@@ -61,10 +65,10 @@ struct pq_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
     std::map<std::string, std::pair<double, int64_t>> timers;
     // upload scratch (upload_walked): per-page host tables, reused
-    std::vector<pqk::DevPage> s_hpages;
-    std::vector<std::pair<int64_t, int64_t>> s_copies;
-    std::vector<int32_t> s_copy_size, s_tile0;
-    std::vector<pqk::DevTile> s_htiles;
+    HVec<pqk::DevPage> s_hpages;
+    HVec<std::pair<int64_t, int64_t>> s_copies;
+    HVec<int32_t> s_copy_size, s_tile0;
+    HVec<pqk::DevTile> s_htiles;
     bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
     int opt_debug = 0;      // "fused_debug": ablation switches for timing studies
     int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
@@ -100,7 +104,7 @@ struct pq_chunk {
     int64_t row_offset = 0;             // page-range uploads: global row of the first data page
     int64_t payload_bytes = 0;
     pqfmt::PageList walked;             // every walked page, all chunks, global rows
-    std::vector<int64_t> page_seq;      // walk sequence of each device data page
+    HVec<int64_t> page_seq;             // walk sequence of each device data page
     std::vector<int64_t> dict_seq;      // walk sequence of each device dict page
     int walk_error = 0;
     std::string walk_message;
@@ -436,7 +440,7 @@ void free_chunk_device(pq_chunk* c) {
 
 // The three-pass dictionary path (dict_pipe.hip) takes a BYTE_ARRAY chunk
 // whose data pages all use one dictionary page that fits in LDS.
-void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, const std::vector<DevDict>& dicts) {
+void plan_pipe(pq_ctx* ctx, pq_chunk* c, const HVec<DevPage>& pages, const std::vector<DevDict>& dicts) {
     c->pipe = false;
     c->pipe_count = false;
     c->pipe_small = false;
@@ -524,7 +528,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages, cons
 
 // PLAIN BYTE_ARRAY chunks without levels go through plain_ba.hip: windows of
 // consecutive page slots of at most kPWin bytes.
-void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
+void plan_plain(pq_ctx* ctx, pq_chunk* c, const HVec<DevPage>& pages) {
     c->plain = false;
     c->plain_spec = false;
     c->plain_opt = false;
@@ -595,39 +599,63 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
             }
         }
     } else {
-        size_t p = 0;
-        while (p < pages.size()) {
-            pqk::DevBatch b{};
-            b.p0 = static_cast<int32_t>(p);
-            b.img_lo = pages[p].off;
-            uint64_t hi = b.img_lo;
-            size_t q = p;
-            while (q < pages.size() && q - p < 64 && pages[q].off >= b.img_lo) {
-                const uint64_t e = pages[q].off + slot(pages[q]);
-                if (e - b.img_lo > pqk::kPWin) break;
-                hi = e;
-                q++;
+        // greedy windows from the start of each page range (one range per
+        // host thread; a range start also starts a window), with each
+        // window's characters for the one-pass form (k_plain_fused): a page's
+        // strings fill it exactly, so its characters are size - 4 *
+        // num_values; verified on the device
+        const size_t NP = pages.size();
+        const int T = static_cast<int>(std::min<size_t>(16, std::max<size_t>(1, NP / 16384)));
+        const size_t per = (NP + static_cast<size_t>(T) - 1) / static_cast<size_t>(T);
+        std::vector<std::vector<pqk::DevBatch>> wparts(static_cast<size_t>(T));
+        std::vector<std::vector<int64_t>> cparts(static_cast<size_t>(T));
+        std::vector<char> kparts(static_cast<size_t>(T), 1);
+        pqfmt::parallel_run(T, T, [&](int t) {
+            auto& W = wparts[static_cast<size_t>(t)];
+            auto& C = cparts[static_cast<size_t>(t)];
+            const size_t end = std::min(NP, (static_cast<size_t>(t) + 1) * per);
+            W.reserve((end - std::min(end, static_cast<size_t>(t) * per)) / 4 + 1);
+            C.reserve(W.capacity());
+            bool known = true;
+            size_t p = static_cast<size_t>(t) * per;
+            while (p < end) {
+                pqk::DevBatch b{};
+                b.p0 = static_cast<int32_t>(p);
+                b.img_lo = pages[p].off;
+                uint64_t hi = b.img_lo;
+                size_t q = p;
+                int64_t ch = 0;
+                while (q < end && q - p < 64 && pages[q].off >= b.img_lo) {
+                    const uint64_t e = pages[q].off + slot(pages[q]);
+                    if (e - b.img_lo > pqk::kPWin) break;
+                    hi = e;
+                    const int64_t x = static_cast<int64_t>(pages[q].size) - 4 * static_cast<int64_t>(pages[q].nvals);
+                    known &= x >= 0;
+                    ch += x;
+                    q++;
+                }
+                b.np = static_cast<int32_t>(q - p);
+                b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
+                W.push_back(b);
+                C.push_back(ch);
+                p = q;
             }
-            b.np = static_cast<int32_t>(q - p);
-            b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
-            c->hpwins.push_back(b);
-            p = q;
-        }
-        // one-pass form (k_plain_fused): a page's strings fill it exactly, so
-        // its characters are size - 4 * num_values; verified on the device
+            kparts[static_cast<size_t>(t)] = known;
+        });
         bool known = true;
-        c->hpwbase.reserve(c->hpwins.size() + 1);
-        c->hpwbase.push_back(0);
-        for (const auto& b : c->hpwins) {
-            int64_t ch = 0;
-            for (int32_t q = b.p0; q < b.p0 + b.np; q++) {
-                const int64_t x = static_cast<int64_t>(pages[static_cast<size_t>(q)].size) - 4 * static_cast<int64_t>(pages[static_cast<size_t>(q)].nvals);
-                known &= x >= 0;
-                ch += x;
-            }
-            c->hpwbase.push_back(c->hpwbase.back() + ch);
+        size_t nw = 0;
+        for (int t = 0; t < T; t++) {
+            nw += wparts[static_cast<size_t>(t)].size();
+            known &= kparts[static_cast<size_t>(t)] != 0;
         }
-        if (!known || opt) c->hpwbase.clear();
+        c->hpwins.reserve(nw);
+        for (const auto& W : wparts) c->hpwins.insert(c->hpwins.end(), W.begin(), W.end());
+        if (known && !opt) {
+            c->hpwbase.reserve(nw + 1);
+            c->hpwbase.push_back(0);
+            for (const auto& C : cparts)
+                for (int64_t ch : C) c->hpwbase.push_back(c->hpwbase.back() + ch);
+        }
     }
     c->plain_opt = opt;
     c->opt_lane_levels = true;
@@ -640,7 +668,7 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages) {
 // Decide whether every chunk of the column can take the fused BYTE_ARRAY
 // path (dict_fused.hip) and size its LDS carve-up; otherwise the generic
 // rows -> scan -> gather path runs.
-void plan_fused(pq_ctx* ctx, pq_chunk* c, const std::vector<DevPage>& pages,
+void plan_fused(pq_ctx* ctx, pq_chunk* c, const HVec<DevPage>& pages,
                 const std::vector<DevDict>& dicts) {
     c->fused = false;
     if (!ctx->opt_fused || c->type != PQ_BYTE_ARRAY || c->max_def > 255 || c->max_def < 0 || c->ranges.empty()) return;
@@ -969,6 +997,129 @@ static void raw_start(pq_ctx* ctx, const uint8_t* file, size_t file_len, RawStag
     });
 }
 
+// The host page tables of one walk (dictionary and data pages, their image
+// slots and copy list) on host threads: per-range counts, then every page
+// written at its index.  Same tables as upload_walked's page loop, which
+// runs instead when a page goes through the codec pass (returns false).
+static bool plan_pages_parallel(pq_chunk* c, const pq_chunk_desc& desc, const pqfmt::WalkResult& w, bool keep_walk,
+                                int hw, int64_t seq, int64_t& row_base, int64_t& img, HVec<DevPage>& hpages,
+                                std::vector<DevDict>& hdicts, HVec<std::pair<int64_t, int64_t>>& copies,
+                                HVec<int32_t>& copy_size) {
+    const size_t N = w.pages.size();
+    const int T = static_cast<int>(std::min<size_t>(static_cast<size_t>(hw), std::max<size_t>(1, N / 16384)));
+    const size_t per = (N + static_cast<size_t>(T) - 1) / static_cast<size_t>(T);
+    struct Part {
+        int64_t nslot = 0, ndata = 0, bytes = 0, rows = 0, payload = 0;
+        bool codec = false;
+        std::vector<size_t> dicts;
+    };
+    std::vector<Part> parts(static_cast<size_t>(T));
+    auto slot_bytes = [](int32_t size) { return (static_cast<int64_t>(size) + 15) / 16 * 16 + 16; };
+    pqfmt::parallel_run(T, T, [&](int t) {
+        Part& P = parts[static_cast<size_t>(t)];
+        const size_t a = static_cast<size_t>(t) * per, b = std::min(N, a + per);
+        for (size_t i = a; i < b; i++) {
+            const pq_page_desc& p = w.pages[i];
+            const bool dict = p.page_type == PQ_DICTIONARY_PAGE, data = p.page_type == PQ_DATA_PAGE;
+            if (!dict && !data) continue;
+            P.codec |= (p.flags & (PQ_PAGE_COMPRESSED | PQ_PAGE_V2)) != 0;
+            P.nslot++;
+            P.bytes += slot_bytes(p.payload_size);
+            P.payload += p.payload_size;
+            if (dict) P.dicts.push_back(i);
+            else {
+                P.ndata++;
+                P.rows += p.num_values;
+            }
+        }
+    });
+    for (const auto& P : parts)
+        if (P.codec) return false;
+    // dictionary pages (few) in walk order: device index, entry base
+    std::vector<size_t> dpos;  // walk index of each, ascending
+    const int32_t d0 = static_cast<int32_t>(hdicts.size());
+    for (const auto& P : parts)
+        for (size_t i : P.dicts) {
+            const pq_page_desc& p = w.pages[i];
+            DevDict d{};
+            d.size = p.payload_size;
+            d.nvals = p.num_values;
+            d.entry_base = static_cast<int32_t>(c->nentries);
+            c->max_dict_bytes = std::max<uint32_t>(c->max_dict_bytes, static_cast<uint32_t>(std::max(p.payload_size, 0)));
+            const int64_t cap = c->type == PQ_BYTE_ARRAY ? std::min<int64_t>(p.num_values, p.payload_size / 4 + 1) : 0;
+            c->nentries += std::max<int64_t>(cap, 0);
+            hdicts.push_back(d);
+            c->dict_seq.push_back(seq + static_cast<int64_t>(i));
+            dpos.push_back(i);
+        }
+    auto dict_dev = [&](int64_t walk_idx) -> int32_t {
+        auto it = std::lower_bound(dpos.begin(), dpos.end(), static_cast<size_t>(walk_idx));
+        return (walk_idx >= 0 && it != dpos.end() && *it == static_cast<size_t>(walk_idx))
+                   ? d0 + static_cast<int32_t>(it - dpos.begin())
+                   : -1;
+    };
+    // bases of each range
+    std::vector<int64_t> img0(static_cast<size_t>(T)), slot0(static_cast<size_t>(T)), data0(static_cast<size_t>(T));
+    int64_t ti = 0, ts = 0, td = 0, rows = 0;
+    for (int t = 0; t < T; t++) {
+        const Part& P = parts[static_cast<size_t>(t)];
+        img0[static_cast<size_t>(t)] = ti;
+        slot0[static_cast<size_t>(t)] = ts;
+        data0[static_cast<size_t>(t)] = td;
+        ti += P.bytes;
+        ts += P.nslot;
+        td += P.ndata;
+        rows += P.rows;
+        c->payload_bytes += P.payload;
+    }
+    const size_t cp0 = copies.size(), hp0 = hpages.size(), ps0 = c->page_seq.size(), wk0 = c->walked.size();
+    copies.resize(cp0 + static_cast<size_t>(ts));
+    copy_size.resize(cp0 + static_cast<size_t>(ts));
+    hpages.resize(hp0 + static_cast<size_t>(td));
+    c->page_seq.resize(ps0 + static_cast<size_t>(td));
+    if (keep_walk) c->walked.resize(wk0 + N);
+    const int64_t img_base = img, rb = row_base;
+    pqfmt::parallel_run(T, T, [&](int t) {
+        const size_t a = static_cast<size_t>(t) * per, b = std::min(N, a + per);
+        int64_t at = img_base + img0[static_cast<size_t>(t)];
+        size_t si = cp0 + static_cast<size_t>(slot0[static_cast<size_t>(t)]);
+        size_t di = hp0 + static_cast<size_t>(data0[static_cast<size_t>(t)]);
+        for (size_t i = a; i < b; i++) {
+            pq_page_desc p = w.pages[i];
+            if (p.page_type == PQ_DICTIONARY_PAGE || p.page_type == PQ_DATA_PAGE) {
+                copies[si] = {p.payload_offset, at};
+                copy_size[si] = p.payload_size;
+                si++;
+                if (p.page_type == PQ_DICTIONARY_PAGE) {
+                    hdicts[static_cast<size_t>(dict_dev(static_cast<int64_t>(i)))].off = static_cast<uint64_t>(at);
+                } else {
+                    DevPage d{};
+                    d.off = static_cast<uint64_t>(at);
+                    d.size = p.payload_size;
+                    d.nvals = p.num_values;
+                    d.first_row = rb + p.first_row;
+                    const int32_t dd = p.dict_page >= 0 ? dict_dev(p.dict_page) : -1;
+                    const bool enc_dict = p.encoding == 2 || p.encoding == 8;
+                    d.mode = (enc_dict && dd >= 0) ? pqk::MODE_DICT
+                             : (c->type == PQ_BOOLEAN ? ((desc.ext_flags && p.encoding == 3) ? pqk::MODE_BOOL_RLE : pqk::MODE_BOOL)
+                                                      : pqk::MODE_PLAIN);
+                    d.dict = d.mode == pqk::MODE_DICT ? dd : -1;
+                    c->page_seq[ps0 + (di - hp0)] = seq + static_cast<int64_t>(i);
+                    hpages[di++] = d;
+                }
+                at += slot_bytes(p.payload_size);
+            }
+            if (keep_walk) {
+                p.first_row += rb;
+                c->walked[wk0 + i] = p;
+            }
+        }
+    });
+    img += ti;
+    row_base += rows;
+    return true;
+}
+
 // Builds the device chunk from page walks already made on the host: one walk
 // per input chunk (pq_chunk_upload) or one page-range walk (pq_chunk_upload_range).
 static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_chunk_desc& desc,
@@ -991,10 +1142,10 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         // per-page host tables: the context's scratch (capacity kept across
         // uploads, so a reader walking many row groups does not page-fault
         // fresh tables in each time; a context serves one thread at a time)
-        std::vector<DevPage>& hpages = ctx->s_hpages;
+        HVec<DevPage>& hpages = ctx->s_hpages;
         std::vector<DevDict> hdicts;
-        std::vector<std::pair<int64_t, int64_t>>& copies = ctx->s_copies;  // (file offset, image offset) per payload
-        std::vector<int32_t>& copy_size = ctx->s_copy_size;
+        HVec<std::pair<int64_t, int64_t>>& copies = ctx->s_copies;  // (file offset, image offset) per payload
+        HVec<int32_t>& copy_size = ctx->s_copy_size;
         hpages.clear();
         copies.clear();
         copy_size.clear();
@@ -1046,11 +1197,25 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             img += (static_cast<int64_t>(size) + 15) / 16 * 16 + 16;
             return at;
         };
+        const int hw_plan = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
         for (int k = 0; k < nchunks; k++) {
             pqfmt::WalkResult& w = walks[static_cast<size_t>(k)];
-            std::vector<int32_t> dict_of_walk(w.pages.size(), -1);
             pq_chunk::Range rg;
             rg.p0 = static_cast<int32_t>(hpages.size());
+            if (plan_pages_parallel(c.get(), desc, w, nchunks > 1, hw_plan, seq, row_base, img, hpages, hdicts, copies,
+                                    copy_size)) {
+                rg.np = static_cast<int32_t>(hpages.size()) - rg.p0;
+                c->ranges.push_back(rg);
+                seq += static_cast<int64_t>(w.pages.size());
+                if (w.error) {
+                    c->walk_error = w.error;
+                    c->walk_message = w.message;
+                    c->walk_error_seq = seq;
+                    break;
+                }
+                continue;
+            }
+            std::vector<int32_t> dict_of_walk(w.pages.size(), -1);
             for (size_t i = 0; i < w.pages.size(); i++) {
                 pq_page_desc p = w.pages[i];
                 int64_t sq = seq + static_cast<int64_t>(i);
@@ -1119,31 +1284,63 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         c->ndicts = static_cast<int>(hdicts.size());
 
         // tiles
-        std::vector<DevTile>& htiles = ctx->s_htiles;
-        std::vector<int32_t>& tile0 = ctx->s_tile0;
-        htiles.clear();
-        tile0.resize(hpages.size());
+        HVec<DevTile>& htiles = ctx->s_htiles;
+        HVec<int32_t>& tile0 = ctx->s_tile0;
+        // per page range on host threads: tile counts, then the tiles at their
+        // indices, with the chunk-wide flags reduced per range
         {
+            const size_t NP = hpages.size();
+            const int T = static_cast<int>(std::min<size_t>(static_cast<size_t>(hw_plan), std::max<size_t>(1, NP / 16384)));
+            const size_t per = (NP + static_cast<size_t>(T) - 1) / static_cast<size_t>(T);
+            struct TPart {
+                size_t nt = 0;
+                bool aligned = true, plain = true;
+                uint32_t maxb = 0;
+            };
+            std::vector<TPart> tp(static_cast<size_t>(T));
+            auto ntile = [](const DevPage& pg) {
+                return static_cast<size_t>((std::max(pg.nvals, 0) + pqk::kTileRows - 1) / pqk::kTileRows);
+            };
+            pqfmt::parallel_run(T, T, [&](int t) {
+                TPart& P = tp[static_cast<size_t>(t)];
+                for (size_t p = static_cast<size_t>(t) * per; p < std::min(NP, (static_cast<size_t>(t) + 1) * per); p++) {
+                    P.nt += ntile(hpages[p]);
+                    P.maxb = std::max<uint32_t>(P.maxb, static_cast<uint32_t>(std::max(hpages[p].size, 0)));
+                    P.plain &= hpages[p].mode == pqk::MODE_PLAIN;
+                }
+            });
+            std::vector<size_t> tb(static_cast<size_t>(T));
             size_t nt = 0;
-            for (const auto& pg : hpages) nt += static_cast<size_t>((std::max(pg.nvals, 0) + pqk::kTileRows - 1) / pqk::kTileRows);
-            htiles.reserve(nt);
+            for (int t = 0; t < T; t++) {
+                tb[static_cast<size_t>(t)] = nt;
+                nt += tp[static_cast<size_t>(t)].nt;
+            }
+            htiles.resize(nt);
+            tile0.resize(NP);
+            pqfmt::parallel_run(T, T, [&](int t) {
+                TPart& P = tp[static_cast<size_t>(t)];
+                size_t k = tb[static_cast<size_t>(t)];
+                for (size_t p = static_cast<size_t>(t) * per; p < std::min(NP, (static_cast<size_t>(t) + 1) * per); p++) {
+                    tile0[p] = static_cast<int32_t>(k);
+                    const DevPage& pg = hpages[p];
+                    for (int32_t r = 0; r < pg.nvals; r += pqk::kTileRows) {
+                        htiles[k++] = DevTile{static_cast<int32_t>(p), r, std::min(pqk::kTileRows, pg.nvals - r), 0};
+                        P.aligned &= ((pg.first_row + r) & 31) == 0;
+                    }
+                }
+            });
+            c->ntiles = static_cast<int>(nt);
+            c->tiles_aligned32 = true;
+            // every data page PLAIN, a fixed-width type whose bytes are copied as is
+            c->fixed_plain = (c->type == PQ_INT32 || c->type == PQ_INT64 || c->type == PQ_FLOAT ||
+                              c->type == PQ_DOUBLE || c->type == PQ_INT96) &&
+                             c->width == c->plain_width && c->max_def >= 0 && c->max_rep >= 0;
+            for (const auto& P : tp) {
+                c->tiles_aligned32 &= P.aligned;
+                c->max_page_bytes = std::max(c->max_page_bytes, P.maxb);
+                c->fixed_plain &= P.plain;
+            }
         }
-        for (size_t p = 0; p < hpages.size(); p++) {
-            tile0[p] = static_cast<int32_t>(htiles.size());
-            for (int32_t r = 0; r < hpages[p].nvals; r += pqk::kTileRows)
-                htiles.push_back(DevTile{static_cast<int32_t>(p), r,
-                                         std::min(pqk::kTileRows, hpages[p].nvals - r), 0});
-        }
-        c->ntiles = static_cast<int>(htiles.size());
-        c->tiles_aligned32 = true;
-        for (const auto& t : htiles)
-            c->tiles_aligned32 &= ((hpages[static_cast<size_t>(t.page)].first_row + t.row0) & 31) == 0;
-        for (const auto& pg : hpages) c->max_page_bytes = std::max<uint32_t>(c->max_page_bytes, static_cast<uint32_t>(std::max(pg.size, 0)));
-        // every data page PLAIN, a fixed-width type whose bytes are copied as is
-        c->fixed_plain = (c->type == PQ_INT32 || c->type == PQ_INT64 || c->type == PQ_FLOAT ||
-                          c->type == PQ_DOUBLE || c->type == PQ_INT96) &&
-                         c->width == c->plain_width && c->max_def >= 0 && c->max_rep >= 0;
-        for (const auto& pg : hpages) c->fixed_plain &= pg.mode == pqk::MODE_PLAIN;
 
         sub_timer.reset();
         plan_timer.reset();
@@ -1299,31 +1496,42 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             if (raw->err != hipSuccess) {
                 rc = hip_check(ctx, raw->err, "raw upload");
             } else {
-                std::vector<pqk::RelayoutEntry> ents;
-                ents.reserve(copies.size());
-                bool inside = true;
-                size_t e = 0;
-                for (size_t k = 0; k < copies.size() && inside; k++) {
-                    const int64_t lo = copies[k].first, n = copy_size[k];
-                    const int64_t avail = lo < 0 ? 0 : std::max<int64_t>(0, std::min<int64_t>(n, static_cast<int64_t>(file_len) - lo));
-                    pqk::RelayoutEntry r{};
-                    r.dst = static_cast<uint64_t>(copies[k].second);
-                    r.avail = static_cast<uint32_t>(avail);
-                    r.slot = static_cast<uint32_t>((n + 15) / 16 * 16 + 16);
-                    if (avail > 0) {  // the extent holding the payload (extents and payloads both ascend, mostly)
-                        auto in = [&](size_t j) {
-                            return lo >= raw->ext[j].first && lo + avail <= raw->ext[j].first + raw->ext[j].second;
-                        };
-                        if (!in(e)) {
-                            size_t j = 0;
-                            while (j < raw->ext.size() && !in(j)) j++;
-                            if (j == raw->ext.size()) { inside = false; break; }
-                            e = j;
+                HVec<pqk::RelayoutEntry> ents;
+                ents.resize(copies.size());
+                std::atomic<bool> inside_all{true};
+                {
+                    const size_t NC = copies.size();
+                    const int T = static_cast<int>(std::min<size_t>(static_cast<size_t>(hw_plan), std::max<size_t>(1, NC / 16384)));
+                    const size_t per = (NC + static_cast<size_t>(T) - 1) / static_cast<size_t>(T);
+                    pqfmt::parallel_run(T, T, [&](int t) {
+                        size_t e = 0;
+                        for (size_t k = static_cast<size_t>(t) * per; k < std::min(NC, (static_cast<size_t>(t) + 1) * per); k++) {
+                            const int64_t lo = copies[k].first, n = copy_size[k];
+                            const int64_t avail = lo < 0 ? 0 : std::max<int64_t>(0, std::min<int64_t>(n, static_cast<int64_t>(file_len) - lo));
+                            pqk::RelayoutEntry r{};
+                            r.dst = static_cast<uint64_t>(copies[k].second);
+                            r.avail = static_cast<uint32_t>(avail);
+                            r.slot = static_cast<uint32_t>((n + 15) / 16 * 16 + 16);
+                            if (avail > 0) {  // the extent holding the payload (extents and payloads both ascend, mostly)
+                                auto in = [&](size_t j) {
+                                    return lo >= raw->ext[j].first && lo + avail <= raw->ext[j].first + raw->ext[j].second;
+                                };
+                                if (!in(e)) {
+                                    size_t j = 0;
+                                    while (j < raw->ext.size() && !in(j)) j++;
+                                    if (j == raw->ext.size()) {
+                                        inside_all = false;
+                                        return;
+                                    }
+                                    e = j;
+                                }
+                                r.src = static_cast<uint64_t>(raw->base[e] + (lo - raw->ext[e].first));
+                            }
+                            ents[k] = r;
                         }
-                        r.src = static_cast<uint64_t>(raw->base[e] + (lo - raw->ext[e].first));
-                    }
-                    ents.push_back(r);
+                    });
                 }
+                const bool inside = inside_all;
                 if (inside) {
                     const size_t need = std::max<size_t>(ents.size(), 1);
                     if (ctx->relay_cap < need) {

@@ -560,8 +560,16 @@ std::vector<SpecSeg> speculate(const uint8_t* file, size_t len, size_t start, si
         size_t pos[kSpecLanes];
         int live = 0;
         for (int l = 0; l < kSpecLanes; l++) {
+            SpecSeg& sg = segs[static_cast<size_t>(t * kSpecLanes + l)];
             pos[l] = find_start(t * kSpecLanes + l);
-            live += pos[l] < segs[static_cast<size_t>(t * kSpecLanes + l)].hi;
+            live += pos[l] < sg.hi;
+            // room for the segment's records at its first page's size (no
+            // regrowth copies when the pages are alike)
+            PageHeader h;
+            if (pos[l] < sg.hi && FastHdr(file, len, pos[l]).parse(h) && h.compressed >= 0) {
+                const size_t est = (sg.hi - pos[l]) / std::max<size_t>(h.header_size + static_cast<size_t>(h.compressed), 16) + 16;
+                sg.recs.reserve(est + est / 4);
+            }
         }
         while (live > 0) {
             live = 0;
