@@ -32,6 +32,30 @@ using pqk::DevTile;
 template <class T>
 using HVec = std::vector<T, pqfmt::NoInitAlloc<T>>;
 
+// ... and in pinned memory: the page and tile tables go to HBM by DMA
+// straight from where the plan wrote them (no staging copy)
+template <class T>
+struct PinnedAlloc : pqfmt::NoInitAlloc<T> {
+    using value_type = T;
+    template <class U>
+    struct rebind { using other = PinnedAlloc<U>; };
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U>&) noexcept {}
+    T* allocate(size_t n) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t) noexcept { (void)hipHostFree(p); }
+};
+template <class A, class B>
+bool operator==(const PinnedAlloc<A>&, const PinnedAlloc<B>&) { return true; }
+template <class A, class B>
+bool operator!=(const PinnedAlloc<A>&, const PinnedAlloc<B>&) { return false; }
+template <class T>
+using PVec = std::vector<T, PinnedAlloc<T>>;
+
 struct PendingTimer {
     std::string name;
     hipEvent_t a, b;
@@ -65,10 +89,12 @@ struct pq_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
     std::map<std::string, std::pair<double, int64_t>> timers;
     // upload scratch (upload_walked): per-page host tables, reused
-    HVec<pqk::DevPage> s_hpages;
+    PVec<pqk::DevPage> s_hpages;
     HVec<std::pair<int64_t, int64_t>> s_copies;
-    HVec<int32_t> s_copy_size, s_tile0;
-    HVec<pqk::DevTile> s_htiles;
+    HVec<int32_t> s_copy_size;
+    PVec<int32_t> s_tile0;
+    PVec<pqk::DevTile> s_htiles;
+    PVec<pqk::RelayoutEntry> s_ents;
     bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
     int opt_debug = 0;      // "fused_debug": ablation switches for timing studies
     int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
@@ -440,7 +466,7 @@ void free_chunk_device(pq_chunk* c) {
 
 // The three-pass dictionary path (dict_pipe.hip) takes a BYTE_ARRAY chunk
 // whose data pages all use one dictionary page that fits in LDS.
-void plan_pipe(pq_ctx* ctx, pq_chunk* c, const HVec<DevPage>& pages, const std::vector<DevDict>& dicts) {
+void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::vector<DevDict>& dicts) {
     c->pipe = false;
     c->pipe_count = false;
     c->pipe_small = false;
@@ -528,7 +554,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const HVec<DevPage>& pages, const std::
 
 // PLAIN BYTE_ARRAY chunks without levels go through plain_ba.hip: windows of
 // consecutive page slots of at most kPWin bytes.
-void plan_plain(pq_ctx* ctx, pq_chunk* c, const HVec<DevPage>& pages) {
+void plan_plain(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages) {
     c->plain = false;
     c->plain_spec = false;
     c->plain_opt = false;
@@ -668,7 +694,7 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const HVec<DevPage>& pages) {
 // Decide whether every chunk of the column can take the fused BYTE_ARRAY
 // path (dict_fused.hip) and size its LDS carve-up; otherwise the generic
 // rows -> scan -> gather path runs.
-void plan_fused(pq_ctx* ctx, pq_chunk* c, const HVec<DevPage>& pages,
+void plan_fused(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages,
                 const std::vector<DevDict>& dicts) {
     c->fused = false;
     if (!ctx->opt_fused || c->type != PQ_BYTE_ARRAY || c->max_def > 255 || c->max_def < 0 || c->ranges.empty()) return;
@@ -1002,7 +1028,7 @@ static void raw_start(pq_ctx* ctx, const uint8_t* file, size_t file_len, RawStag
 // written at its index.  Same tables as upload_walked's page loop, which
 // runs instead when a page goes through the codec pass (returns false).
 static bool plan_pages_parallel(pq_chunk* c, const pq_chunk_desc& desc, const pqfmt::WalkResult& w, bool keep_walk,
-                                int hw, int64_t seq, int64_t& row_base, int64_t& img, HVec<DevPage>& hpages,
+                                int hw, int64_t seq, int64_t& row_base, int64_t& img, PVec<DevPage>& hpages,
                                 std::vector<DevDict>& hdicts, HVec<std::pair<int64_t, int64_t>>& copies,
                                 HVec<int32_t>& copy_size) {
     const size_t N = w.pages.size();
@@ -1142,7 +1168,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         // per-page host tables: the context's scratch (capacity kept across
         // uploads, so a reader walking many row groups does not page-fault
         // fresh tables in each time; a context serves one thread at a time)
-        HVec<DevPage>& hpages = ctx->s_hpages;
+        PVec<DevPage>& hpages = ctx->s_hpages;
         std::vector<DevDict> hdicts;
         HVec<std::pair<int64_t, int64_t>>& copies = ctx->s_copies;  // (file offset, image offset) per payload
         HVec<int32_t>& copy_size = ctx->s_copy_size;
@@ -1284,8 +1310,8 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         c->ndicts = static_cast<int>(hdicts.size());
 
         // tiles
-        HVec<DevTile>& htiles = ctx->s_htiles;
-        HVec<int32_t>& tile0 = ctx->s_tile0;
+        PVec<DevTile>& htiles = ctx->s_htiles;
+        PVec<int32_t>& tile0 = ctx->s_tile0;
         // per page range on host threads: tile counts, then the tiles at their
         // indices, with the chunk-wide flags reduced per range
         {
@@ -1496,7 +1522,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             if (raw->err != hipSuccess) {
                 rc = hip_check(ctx, raw->err, "raw upload");
             } else {
-                HVec<pqk::RelayoutEntry> ents;
+                PVec<pqk::RelayoutEntry>& ents = ctx->s_ents;
                 ents.resize(copies.size());
                 std::atomic<bool> inside_all{true};
                 {
@@ -1540,11 +1566,8 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                         if (dalloc(&ctx->d_relay, need) == 0) ctx->relay_cap = need;
                     }
                     if (ctx->relay_cap >= need) {
-                        rc = hip_check(ctx, ctx->stager.upload(reinterpret_cast<uint8_t*>(ctx->d_relay),
-                                                               ents.size() * sizeof(pqk::RelayoutEntry), s, 1,
-                                                               [&](uint8_t* dst, size_t a, size_t z) {
-                                                                   std::memcpy(dst, reinterpret_cast<const uint8_t*>(ents.data()) + a, z - a);
-                                                               }),
+                        rc = hip_check(ctx, hipMemcpyAsync(ctx->d_relay, ents.data(), ents.size() * sizeof(pqk::RelayoutEntry),
+                                                           hipMemcpyHostToDevice, s),
                                        "upload");
                         if (!rc) {
                             {
@@ -1653,10 +1676,14 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                                                    }),
                            "upload");
         };
-        put(c->d_pages, hpages.data(), hpages.size() * sizeof(DevPage));
+        auto put_pinned = [&](void* d, const void* h, size_t bytes) {
+            if (rc || bytes == 0) return;
+            rc = hip_check(ctx, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s), "upload");
+        };
+        put_pinned(c->d_pages, hpages.data(), hpages.size() * sizeof(DevPage));
         put(c->d_dicts, hdicts.data(), hdicts.size() * sizeof(DevDict));
-        put(c->d_tiles, htiles.data(), htiles.size() * sizeof(DevTile));
-        put(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t));
+        put_pinned(c->d_tiles, htiles.data(), htiles.size() * sizeof(DevTile));
+        put_pinned(c->d_page_tile0, tile0.data(), tile0.size() * sizeof(int32_t));
         if (!rc) (void)hipMemsetAsync(c->d_page_err, 0, std::max<size_t>(hpages.size(), 1) * sizeof(DevErr), s);
         if (!rc) (void)hipMemsetAsync(c->d_dict_err, 0, std::max<size_t>(hdicts.size(), 1) * sizeof(DevErr), s);
         if (!rc && c->d_dflag) (void)hipMemsetAsync(c->d_dflag, 0, sizeof(int32_t), s);
@@ -1674,7 +1701,10 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         if (c->d_pwins) put(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch));
         if (c->d_pwbase) put(c->d_pwbase, c->hpwbase.data(), c->hpwbase.size() * sizeof(int64_t));
         if (c->d_pwpage) put(c->d_pwpage, c->hpwpage.data(), c->hpwpage.size() * sizeof(int32_t));
-        if (!rc) rc = hip_check(ctx, hipStreamSynchronize(s), "upload sync");
+        {  // (also after an error: the pinned tables may still be in flight)
+            const hipError_t e = hipStreamSynchronize(s);
+            if (!rc) rc = hip_check(ctx, e, "upload sync");
+        }
         if (!rc && !cents.empty()) {
             std::vector<uint32_t> st(cents.size());
             rc = hip_check(ctx, hipMemcpy(st.data(), ctx->d_codec_st, st.size() * sizeof(uint32_t), hipMemcpyDeviceToHost),
@@ -2401,11 +2431,7 @@ int pq_regex_compile_check(const char* pattern, char* err, size_t errlen) {
 // page does not fit (the lane-per-page kernel runs then).
 bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     if (c->d_rwins && c->rwin_for_dfa == c->dfa_bytes && c->rwin_opt == ctx->opt_regex_win) return true;
-    std::vector<DevPage> hp(static_cast<size_t>(c->npages));
-    if (c->npages && hipMemcpy(hp.data(), c->d_pages, hp.size() * sizeof(DevPage), hipMemcpyDeviceToHost) != hipSuccess)
-        return false;
-    uint32_t maxslot = 0;
-    for (const auto& p : hp) maxslot = std::max(maxslot, (static_cast<uint32_t>(std::max(p.size, 0)) + 15) / 16 * 16 + 16);
+    const uint32_t maxslot = c->npages ? (c->max_page_bytes + 15) / 16 * 16 + 16 : 0u;
     const uint32_t win = std::max<uint32_t>(static_cast<uint32_t>(ctx->opt_regex_win), maxslot);
     // the kernel lists strings by u16 window offsets (and the string index
     // keeps them): pages whose slot leaves no room take k_regex_lanes
@@ -2414,6 +2440,14 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     const uint32_t lds = pqre::regex_plain_lds(c->dfa_bytes, win);
     if (lds > 160 * 1024) return false;
     c->hrwins.clear();
+    // the PLAIN decode's windows are the same kind (<= 64 consecutive page
+    // slots, <= kPWin bytes; planned on host threads at upload): no page
+    // table read back
+    const bool same = c->plain && !c->plain_spec && win == pqk::kPWin && !c->hpwins.empty();
+    std::vector<DevPage> hp(same ? 0 : static_cast<size_t>(c->npages));
+    if (same) c->hrwins = c->hpwins;
+    else if (c->npages && hipMemcpy(hp.data(), c->d_pages, hp.size() * sizeof(DevPage), hipMemcpyDeviceToHost) != hipSuccess)
+        return false;
     size_t p = 0;
     while (p < hp.size()) {
         pqk::DevBatch b{};

@@ -543,6 +543,11 @@ std::vector<SpecSeg> speculate(const uint8_t* file, size_t len, size_t start, si
         // kSpecScan bytes (the exact walk crosses it in one hop anyway)
         const size_t lim = std::min(sg.hi, sg.lo + kSpecScan);
         for (; pos < lim; pos++) {
+            // a header opens with a short-form field header of an i32 or a
+            // struct field (type 5 / 12); other bytes are not parsed (a
+            // long-form opening only costs the exact walk, never a result)
+            const uint8_t b0 = file[pos], ft = b0 & 0x0F;
+            if ((b0 >> 4) == 0 || (ft != 5 && ft != 12)) continue;
             PageHeader h;
             if (!FastHdr(file, len, pos).parse(h) || !plausible(h, pos, end)) continue;
             size_t q = pos + h.header_size + static_cast<size_t>(h.compressed);
