@@ -96,6 +96,9 @@ struct pq_ctx {
     PVec<pqk::DevTile> s_htiles;
     PVec<pqk::RelayoutEntry> s_ents;
     bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
+    bool opt_wide_rows = true;  // "wide_rows": generic BYTE_ARRAY rows by a workgroup per page (k_wide_rows)
+    bool opt_levels_small = true;  // "levels_small": k_fixed_levels2 in its 35 KB LDS form (4 workgroups per CU)
+    bool opt_gather_rows = true;  // "gather_rows": k_ba_gather copies characters row per lane (0: byte-wise blocks)
     int opt_debug = 0;      // "fused_debug": ablation switches for timing studies
     int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
     uint64_t* d_prof = nullptr;  // "fused_prof": per-phase cycle sums of k_ba_fused
@@ -851,6 +854,9 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (!ctx || !key) return PQ_ERR_ARG;
     DevGuard dg(ctx);
     if (std::strcmp(key, "fused_ba") == 0) { ctx->opt_fused = value != 0; return 0; }
+    if (std::strcmp(key, "wide_rows") == 0) { ctx->opt_wide_rows = value != 0; return 0; }
+    if (std::strcmp(key, "levels_small") == 0) { ctx->opt_levels_small = value != 0; return 0; }
+    if (std::strcmp(key, "gather_rows") == 0) { ctx->opt_gather_rows = value != 0; return 0; }
     if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "fused_waves") == 0) { ctx->opt_waves = static_cast<int>(value); return 0; }
     if (std::strcmp(key, "fused_claim") == 0) {
@@ -1886,7 +1892,7 @@ static void launch_gather(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     pqk::launch_ba_gather(ctx->stream, c->d_bytes, c->d_pages, c->d_tiles, c->ntiles, c->d_dicts,
                           c->d_entries, c->d_row_codes, c->d_tile_base, c->nrows, c->d_total,
                           out->capacity_bytes, c->d_flags + 1, out->d_validity, out->d_offsets,
-                          out->d_values);
+                          out->d_values, !ctx->opt_gather_rows);
 }
 
 // Launch parameters of the three-pass dictionary path (dict_pipe.hip); `out`
@@ -2045,7 +2051,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
                                    c->d_tile_rank, c->d_page_pos, c->d_page_nn, c->d_operr, redo);
         else
             pqk::launch_fixed_levels(s, c->d_bytes, c->d_pages, c->npages, c->d_page_tile0, cp, out->d_validity,
-                                     c->d_tile_rank, c->d_page_pos, c->d_page_nn, c->d_operr, redo);
+                                     c->d_tile_rank, c->d_page_pos, c->d_page_nn, c->d_operr, redo, ctx->opt_levels_small);
         pqk::OptLaunch O{};
         O.pages = c->d_pages; O.npages = c->npages; O.page_nn = c->d_page_nn; O.page_pos = c->d_page_pos;
         O.lerr = c->d_operr; O.nnv = c->d_onnv; O.chv = c->d_ochv; O.pdense = c->d_opdense; O.pbase = c->d_opbase;
@@ -2171,7 +2177,8 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             const uint32_t big = (c->max_def == 0 && c->max_rep == 0 && ctx->opt_plain) ? pqk::ba_rows_stage_bytes() : 0u;
             pqk::launch_ba_rows(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_entries,
                                 c->d_dict_count, cp, c->d_row_codes, c->d_tile_chars,
-                                c->d_page_tile0, c->d_page_err, c->d_flags, big, c->max_page_bytes);
+                                c->d_page_tile0, c->d_page_err, c->d_flags, big, c->max_page_bytes,
+                                ctx->opt_wide_rows && c->ndicts > 0);
             if (big)
                 pqk::launch_plain_big_rows(s, c->d_bytes, c->d_pages, c->npages, big, c->d_row_codes,
                                            c->d_tile_chars, c->d_page_tile0, c->d_page_err, c->d_flags);
@@ -2189,7 +2196,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         Timed t(ctx, "fixed_plain");
         pqk::launch_fixed_plain(s, c->d_bytes, c->d_pages, c->npages, c->d_tiles, c->ntiles, c->d_page_tile0, cp,
                                 out->d_validity, out->d_values, c->d_tile_rank, c->d_page_pos, c->d_page_err,
-                                c->d_flags, ctx->opt_fixed_fused);
+                                c->d_flags, ctx->opt_fixed_fused, ctx->opt_levels_small);
     } else {
         Timed t(ctx, "fixed");
         pqk::launch_fixed(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_dict_count, cp,

@@ -19,7 +19,12 @@
 #include "kernels.hpp"
 
 #include "kernels/device_common.hpp"
+#include "kernels/lane_walk.hpp"
+#include "kernels/row_copy.hpp"
+#include "kernels/run_spec.hpp"
 #include "pq_gpu.h"
+
+#include <algorithm>
 
 namespace pqk {
 namespace {
@@ -133,37 +138,30 @@ struct RowsLds {
     uint32_t b[kTileRows];    // plain length per non-null rank
 };
 
-// kSW: LDS stage words per wave (pages up to 4 KiB, or up to 32 KiB with one
-// wave per workgroup); kWPB: waves per workgroup.
-template <uint32_t kSW, int kWPB>
-__global__ void __launch_bounds__(kWPB * 64) k_ba_rows(const uint8_t* __restrict__ bytes,
-                                                 const DevPage* __restrict__ pages, int npages,
-                                                 const DevDict* __restrict__ dicts,
-                                                 const uint64_t* __restrict__ entries,
-                                                 const int32_t* __restrict__ dict_count,
-                                                 ColumnParams cp, uint64_t* __restrict__ row_codes,
-                                                 int64_t* __restrict__ tile_chars,
-                                                 const int32_t* __restrict__ page_tile0,
-                                                 DevErr* __restrict__ page_err,
-                                                 int32_t* __restrict__ err_any, uint32_t big_plain_min) {
-    __shared__ RowsLds<kSW> lds_all[kWPB];
-    const int wv = threadIdx.x / kWave;
-    const int p = blockIdx.x * kWPB + wv;
-    if (p >= npages) return;
-    RowsLds<kSW>& L = lds_all[wv];
-    const DevPage pg = pages[p];
+// REQUIRED PLAIN pages above big_plain_min: k_plain_big_rows (plain_ba.hip)
+__device__ __forceinline__ bool big_plain_page(const DevPage& pg, const ColumnParams& cp, uint32_t big_plain_min) {
+    return big_plain_min && cp.max_def == 0 && cp.max_rep == 0 && pg.mode == MODE_PLAIN &&
+           static_cast<uint32_t>(pg.size) > big_plain_min && pg.nvals <= 256 * kTileRows;
+}
+
+// One page by one wavefront, the reference state machine in order (def
+// levels, then indices or the PLAIN length chain, tile by tile).  `staged`:
+// the page's payload words already in LDS, or nullptr (read from HBM);
+// lv / a / b: kTileRows words each of this wave's LDS scratch.
+__device__ void ba_rows_page(const uint8_t* __restrict__ bytes, const DevPage& pg, int p, const uint32_t* staged,
+                             uint32_t* lv_s, uint32_t* a_s, uint32_t* b_s, const DevDict* __restrict__ dicts,
+                             const uint64_t* __restrict__ entries, const int32_t* __restrict__ dict_count,
+                             ColumnParams cp, uint64_t* __restrict__ row_codes, int64_t* __restrict__ tile_chars,
+                             const int32_t* __restrict__ page_tile0, DevErr* __restrict__ page_err,
+                             int32_t* __restrict__ err_any) {
+    struct {
+        uint32_t* lv;
+        uint32_t* a;
+        uint32_t* b;
+    } L{lv_s, a_s, b_s};
     DevErr* err = page_err + p;
-    const uint8_t* g = bytes + pg.off;
     const uint32_t size = static_cast<uint32_t>(pg.size);
-    // REQUIRED PLAIN pages above big_plain_min: k_plain_big_rows (plain_ba.hip)
-    if (big_plain_min && cp.max_def == 0 && cp.max_rep == 0 && pg.mode == MODE_PLAIN && size > big_plain_min &&
-        pg.nvals <= 256 * kTileRows)
-        return;
-    Src s{nullptr, g, size};
-    if (size <= kSW * 4) {
-        stage_page(L.stage, g, size);
-        s.lds = L.stage;
-    }
+    Src s{staged, bytes + pg.off, size};
     const int32_t tile0 = page_tile0[p];
     const int32_t nv = pg.nvals;
 
@@ -271,6 +269,309 @@ __global__ void __launch_bounds__(kWPB * 64) k_ba_rows(const uint8_t* __restrict
             tile_sum += v;
         }
         if (lane() == 0) tile_chars[tile0 + t] = failed ? 0 : static_cast<int64_t>(tile_sum);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// kSW: LDS stage words per wave (pages up to 4 KiB, or up to 32 KiB with one
+// wave per workgroup); kWPB: waves per workgroup.
+template <uint32_t kSW, int kWPB>
+__global__ void __launch_bounds__(kWPB * 64) k_ba_rows(const uint8_t* __restrict__ bytes,
+                                                 const DevPage* __restrict__ pages, int npages,
+                                                 const DevDict* __restrict__ dicts,
+                                                 const uint64_t* __restrict__ entries,
+                                                 const int32_t* __restrict__ dict_count,
+                                                 ColumnParams cp, uint64_t* __restrict__ row_codes,
+                                                 int64_t* __restrict__ tile_chars,
+                                                 const int32_t* __restrict__ page_tile0,
+                                                 DevErr* __restrict__ page_err,
+                                                 int32_t* __restrict__ err_any, uint32_t big_plain_min) {
+    __shared__ RowsLds<kSW> lds_all[kWPB];
+    const int wv = threadIdx.x / kWave;
+    const int p = blockIdx.x * kWPB + wv;
+    if (p >= npages) return;
+    RowsLds<kSW>& L = lds_all[wv];
+    const DevPage pg = pages[p];
+    if (big_plain_page(pg, cp, big_plain_min)) return;
+    const uint32_t size = static_cast<uint32_t>(pg.size);
+    const uint32_t* st = nullptr;
+    if (size <= kSW * 4) {
+        stage_page(L.stage, bytes + pg.off, size);
+        st = L.stage;
+    }
+    ba_rows_page(bytes, pg, p, st, L.lv, L.a, L.b, dicts, entries, dict_count, cp, row_codes, tile_chars, page_tile0,
+                 page_err, err_any);
+}
+
+// ── dictionary pages by a workgroup: k_wide_rows ───────────────────────────
+// k_ba_rows walks a page's two hybrid streams one header at a time; a
+// 20,000-row page with 17-bit indices (a 100k-entry dictionary, beyond the
+// pipe's LDS dictionary) holds ~2,000 runs per stream, a serial chain of
+// dependent reads.  Here one 16-wave workgroup owns a page (column_reader.cpp
+// :174-196, max_def <= 1, no rep levels):
+//   1. the payload -> LDS;
+//   2. the def stream's run records by the whole workgroup (run_spec.hpp),
+//      expanded per 512-row tile into a page validity bitmap in LDS and per-tile
+//      non-null counts (def == max_def), scanned to tile ranks;
+//   3. the index stream's records (num_non_null values, same scheme; the table
+//      and the records reuse one region);
+//   4. per tile: the tile's rank range expanded to indices (max-scan over the
+//      record starts, 8 ranks per lane), then rows in order: NULL, index out
+//      of range -> ~0, else the dictionary entry word (HBM/L2) -> row code and
+//      the tile's character sum, exactly what k_ba_rows writes.
+// Anything the record scheme does not take (non-dictionary pages, a level or
+// prologue error, zero-count runs, table overflow, bw > 24) runs ba_rows_page
+// on wave 0 over the staged payload, which also reports the reference's error.
+constexpr int kWdWaves = 16;
+constexpr uint32_t kWdThreads = kWdWaves * kWave;
+constexpr uint32_t kWdPer = 48;  // spec positions per thread: streams up to 49,152 bytes (64 spill)
+constexpr uint32_t kWdMaxRows = 65535;
+constexpr uint32_t kWdTiles = (kWdMaxRows + kTileRows) / kTileRows;
+constexpr uint32_t kWdWaveScratch = kTileRows * 2 + kTileRows * 4;  // mark u16 + ranks' indices u32
+static_assert(kWdWaveScratch * kWdWaves >= 3 * kTileRows * 4, "exact path scratch fits the wave scratch");
+
+struct WideLayout {
+    uint32_t stage, stage_bytes;   // payload
+    uint32_t tab, tab_bytes;       // speculative table, then the records (rcap), then wave scratch
+    uint32_t rcap, scratch;        // records; wave scratch offset (inside the tab region)
+    uint32_t list, esum, lcap;     // spec lists
+    uint32_t pvalid;               // page validity bytes (kWdMaxRows / 8 + 16)
+    uint32_t tnn, trank, sh;       // per-tile counts and ranks, scalars
+    uint32_t bytes;
+};
+
+__host__ __device__ inline uint32_t wd_al16(uint32_t x) { return (x + 15u) & ~15u; }
+
+__host__ inline WideLayout wide_layout(uint32_t max_page) {
+    WideLayout L{};
+    uint32_t o = 0;
+    L.stage = o; L.stage_bytes = wd_al16(max_page) + 32; o += L.stage_bytes;
+    const uint32_t scr = kWdWaveScratch * kWdWaves;
+    const uint32_t tab_min = 2 * wd_al16(max_page) + 16;
+    const uint32_t rec_min = 8 * std::max<uint32_t>(1024u, wd_al16(max_page) / 4);
+    L.tab_bytes = wd_al16(std::max(tab_min, rec_min + scr));
+    L.tab = o; o += L.tab_bytes;
+    L.scratch = L.tab + L.tab_bytes - scr;
+    L.rcap = (L.scratch - L.tab) / 8;
+    L.lcap = L.rcap / kSpJump + 8;
+    L.list = o; o += wd_al16(4 * L.lcap);
+    L.esum = o; o += wd_al16(4 * L.lcap);
+    L.pvalid = o; o += wd_al16(kWdMaxRows / 8 + 16);
+    L.tnn = o; o += 4 * kWdTiles;
+    L.trank = o; o += 4 * kWdTiles;
+    L.sh = o; o += 64;
+    L.bytes = o;
+    return L;
+}
+
+// First record of rec[0 .. nrec) whose start (x & 0xFFFF) is <= v, searched
+// from `from` (records are sorted by start; v never lies before rec[from]).
+__device__ __forceinline__ uint32_t wd_find(const uint2* rec, uint32_t nrec, uint32_t from, uint32_t v) {
+    uint32_t c = from;
+    for (uint32_t k0 = from + 1; k0 < nrec; k0 += kWave) {
+        const uint32_t k = k0 + lane();
+        const uint64_t le = __ballot(k < nrec && (rec[k].x & 0xFFFFu) <= v);
+        c += __popcll(le);
+        if (le != ~0ull) break;
+    }
+    return c;
+}
+
+// Values [v0, v0 + m) (m <= kTileRows) of a stream with records rec: lane l
+// produces values v0 + 8l .. 8l + 7 into out[8l ..] (a max-scan over the
+// record starts marked in `mark`).  Returns the record holding v0.
+template <class F>
+__device__ __forceinline__ uint32_t wd_expand(const uint2* rec, uint32_t nrec, uint32_t rd_from, uint32_t v0,
+                                              uint32_t m, uint16_t* mark, F&& value) {
+    const uint32_t rd0 = wd_find(rec, nrec, rd_from, v0);
+    const uint32_t l8 = lane() * 8;
+    if (l8 < kTileRows) *reinterpret_cast<uint4*>(mark + l8) = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    for (uint32_t k = rd0 + 1 + lane(); k < nrec; k += kWave) {
+        const uint32_t st = rec[k].x & 0xFFFFu;
+        if (st >= v0 + m) break;
+        mark[st - v0] = static_cast<uint16_t>(k - rd0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint4 mk = *reinterpret_cast<const uint4*>(mark + l8);
+    const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
+    uint32_t rm[8], run = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        run = max(run, (mw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+        rm[k] = run;
+    }
+    const uint32_t ex = static_cast<uint32_t>(
+        __builtin_amdgcn_update_dpp(0, static_cast<int>(wave_incl_max(run)), 0x138, 0xf, 0xf, true));
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t j = l8 + k;
+        if (j < m) {
+            const uint2 R = rec[rd0 + max(ex, rm[k])];
+            value(j, R, v0 + j - (R.x & 0xFFFFu));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return rd0;
+}
+
+__global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restrict__ bytes,
+                                                         const DevPage* __restrict__ pages,
+                                                         const DevDict* __restrict__ dicts,
+                                                         const uint64_t* __restrict__ entries,
+                                                         const int32_t* __restrict__ dict_count, ColumnParams cp,
+                                                         uint64_t* __restrict__ row_codes,
+                                                         int64_t* __restrict__ tile_chars,
+                                                         const int32_t* __restrict__ page_tile0,
+                                                         DevErr* __restrict__ page_err, int32_t* __restrict__ err_any,
+                                                         uint32_t big_plain_min, WideLayout Lo) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* stage = reinterpret_cast<uint32_t*>(smem + Lo.stage);
+    uint16_t* tab = reinterpret_cast<uint16_t*>(smem + Lo.tab);
+    uint2* rec = reinterpret_cast<uint2*>(smem + Lo.tab);
+    uint32_t* list = reinterpret_cast<uint32_t*>(smem + Lo.list);
+    uint32_t* esum = reinterpret_cast<uint32_t*>(smem + Lo.esum);
+    uint8_t* pvalid = smem + Lo.pvalid;
+    uint32_t* tnn = reinterpret_cast<uint32_t*>(smem + Lo.tnn);
+    uint32_t* trank = reinterpret_cast<uint32_t*>(smem + Lo.trank);
+    uint32_t* sh = reinterpret_cast<uint32_t*>(smem + Lo.sh);
+    const uint32_t wv = threadIdx.x / kWave;
+    uint8_t* wscr = smem + Lo.scratch + wv * kWdWaveScratch;
+    uint16_t* mark = reinterpret_cast<uint16_t*>(wscr);
+    uint32_t* ixv = reinterpret_cast<uint32_t*>(wscr + 2 * kTileRows);
+
+    const int p = blockIdx.x;
+    const DevPage pg = pages[p];
+    if (big_plain_page(pg, cp, big_plain_min)) return;
+    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
+    const uint32_t n = static_cast<uint32_t>(max(pg.nvals, 0));
+    const bool staged = size + 32 <= Lo.stage_bytes;
+    if (staged) copy_blocks(reinterpret_cast<uint4*>(stage), reinterpret_cast<const uint4*>(bytes + pg.off),
+                            (size + 15) / 16 + 1, threadIdx.x, kWdThreads);
+    if (threadIdx.x == 0) {  // prologue (column_reader.cpp:146-182): sh = fast, def len, index base, index bw
+        uint32_t fast = staged && pg.mode == MODE_DICT && pg.dict >= 0 && n <= kWdMaxRows && cp.max_rep == 0 &&
+                        cp.max_def <= 1;
+        uint32_t pos = 0, dlen = 0, ibw = 0;
+        if (fast && cp.max_def == 1) {
+            if (4 > size) fast = 0;
+            else {
+                dlen = static_cast<uint32_t>(gld8(bytes + pg.off, 0));
+                if (4ull + dlen > size || dlen > kWdThreads * kWdPer) fast = 0;
+                else pos = 4 + dlen;
+            }
+        }
+        if (fast) {
+            if (pos + 1 > size) fast = 0;
+            else {
+                ibw = bytes[pg.off + pos];
+                pos += 1;
+                if (ibw > 24 || size - pos > kWdThreads * kWdPer) fast = 0;
+            }
+        }
+        sh[4] = fast;
+        sh[5] = dlen;
+        sh[6] = pos;
+        sh[7] = ibw;
+    }
+    __syncthreads();
+    uint32_t fast = sh[4];
+    const uint32_t dlen = sh[5], ibase = sh[6], ibw = sh[7];
+    const uint32_t staged_bytes = size + 16;
+    const uint32_t ntiles = (n + kTileRows - 1) / kTileRows;
+    // 2. def records -> validity bytes, tile counts
+    if (fast && cp.max_def == 1) {
+        const uint32_t nd = spec_runs<kWdThreads, kWdPer, true>(stage, 4, dlen, 1, n, tab, list, esum, Lo.lcap, rec, Lo.rcap, sh);
+        if (nd == ~0u) fast = 0;
+        else {
+            uint32_t rd = 0;
+            for (uint32_t ti = wv; ti < ntiles; ti += kWdWaves) {
+                const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
+                uint32_t vb = 0;
+                rd = wd_expand(rec, nd, rd, r0, m, mark, [&](uint32_t j, const uint2& R, uint32_t off) {
+                    const uint32_t lvl = (R.y >> 31) ? lds_bits(stage, staged_bytes, (R.y & 0x7FFFFFFFu) + off, 1)
+                                                     : (R.y & 0x7FFFFFFFu);
+                    vb |= (lvl == 1u ? 1u : 0u) << (j & 7);
+                });
+                pvalid[(r0 >> 3) + lane()] = static_cast<uint8_t>(vb);
+                const uint32_t c = bcast_last(wave_incl_scan(__popc(vb)));
+                if (lane() == 0) tnn[ti] = c;
+            }
+        }
+    } else if (fast) {
+        for (uint32_t i = threadIdx.x; i < (n + 7) / 8; i += kWdThreads) {
+            const uint32_t r = i * 8;
+            pvalid[i] = static_cast<uint8_t>(n - r >= 8 ? 0xFFu : ((1u << (n - r)) - 1u));
+        }
+        for (uint32_t ti = threadIdx.x; ti < ntiles; ti += kWdThreads) tnn[ti] = min(n - ti * kTileRows, kTileRows);
+    }
+    __syncthreads();
+    if (fast && wv == 0) {  // tile ranks
+        uint32_t carry = 0;
+        for (uint32_t i0 = 0; i0 < ntiles; i0 += kWave) {
+            const uint32_t i = i0 + lane();
+            const uint32_t v = i < ntiles ? tnn[i] : 0u;
+            const uint32_t inc = wave_incl_scan(v);
+            if (i < ntiles) trank[i] = carry + inc - v;
+            carry += bcast_last(inc);
+        }
+        if (lane() == 0) sh[8] = carry;
+    }
+    __syncthreads();
+    // 3. index records (num_non_null values; column_reader.cpp:180-182)
+    uint32_t ni = 0;
+    const uint32_t nn = fast ? sh[8] : 0u;
+    if (fast && nn > 0) {
+        ni = spec_runs<kWdThreads, kWdPer, true>(stage, ibase, size - ibase, ibw, nn, tab, list, esum, Lo.lcap, rec, Lo.rcap,
+                                           sh);
+        if (ni == ~0u) fast = 0;
+    }
+    if (!fast) {  // the exact per-page walk (reports the reference's errors)
+        if (wv == 0) {
+            uint32_t* scr = reinterpret_cast<uint32_t*>(smem + Lo.scratch);
+            ba_rows_page(bytes, pg, p, staged ? stage : nullptr, scr, scr + kTileRows, scr + 2 * kTileRows, dicts,
+                         entries, dict_count, cp, row_codes, tile_chars, page_tile0, page_err, err_any);
+        }
+        return;
+    }
+    // 4. rows
+    const uint32_t dict_n = static_cast<uint32_t>(max(dict_count[pg.dict], 0));
+    const uint64_t* ent = entries + dicts[pg.dict].entry_base;
+    const int32_t tile0 = page_tile0[p];
+    const uint32_t lmask = (1u << ibw) - 1u;
+    uint32_t rd = 0;
+    for (uint32_t ti = wv; ti < ntiles; ti += kWdWaves) {
+        const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
+        const uint32_t cnt = tnn[ti];
+        if (cnt) {
+            rd = wd_expand(rec, ni, rd, trank[ti], cnt, mark, [&](uint32_t j, const uint2& R, uint32_t off) {
+                ixv[j] = (R.y >> 31) ? (lds_bits(stage, staged_bytes,
+                                                 (R.y & 0x7FFFFFFFu) + static_cast<uint64_t>(off) * ibw, ibw) & lmask)
+                                     : (R.y & 0x7FFFFFFFu);
+            });
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        uint32_t run = 0;
+        uint64_t sum = 0;
+        uint64_t* out = row_codes + pg.first_row + r0;
+#pragma unroll 2
+        for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
+            const uint32_t j = j0 + lane();
+            const bool v = j < m && ((pvalid[(r0 + j) >> 3] >> (j & 7)) & 1u);
+            const uint64_t vm = __ballot(v);
+            uint64_t code = ~0ull;
+            if (v) {
+                const uint32_t idx = ixv[run + popc_below(vm)];
+                if (idx < dict_n) code = ent[idx];
+            }
+            run += __popcll(vm);
+            if (j < m) out[j] = code;
+            sum += code == ~0ull ? 0u : (code >> 32);
+        }
+#pragma unroll
+        for (int dd = 32; dd >= 1; dd >>= 1) sum += __shfl_xor(sum, dd, kWave);
+        if (lane() == 0) tile_chars[tile0 + ti] = static_cast<int64_t>(sum);
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -388,6 +689,55 @@ struct GatherLds {
     uint16_t blockrow[kGatherWindow];
 };
 
+// The byte-wise form (option "gather_rows" 0): 16-byte output blocks, each
+// assembled from the rows that cover it.
+__device__ void gather_bytes(GatherLds& L, const uint8_t* __restrict__ srcbase, uint32_t n, int64_t G0, int64_t G1,
+                             int64_t B0, int64_t nb, uint8_t* __restrict__ chars) {
+    for (int64_t w0 = 0; w0 < nb; w0 += kGatherWindow) {
+        const int64_t w1 = min(nb, w0 + static_cast<int64_t>(kGatherWindow));
+        // scatter: row r owns the blocks whose first in-tile byte lies in it
+        for (uint32_t r = lane(); r < n; r += kWave) {
+            uint32_t s = L.loff[r], e = L.loff[r + 1];
+            if (e <= s) continue;
+            int64_t blo = s == 0 ? 0 : ((s + G0 + 15) >> 4) - B0;
+            int64_t bhi = ((e + G0 + 15) >> 4) - B0 - 1;
+            blo = max(blo, w0);
+            bhi = min(bhi, w1 - 1);
+            for (int64_t b = blo; b <= bhi; b++) L.blockrow[b - w0] = static_cast<uint16_t>(r);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (int64_t b = w0 + lane(); b < w1; b += kWave) {
+            const int64_t blk = (B0 + b) << 4;
+            const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
+            uint32_t r = L.blockrow[b - w0];
+            uint32_t q = static_cast<uint32_t>(gs - G0);
+            uint32_t p = q - L.loff[r];
+            uint32_t outw[4] = {0, 0, 0, 0};
+            const uint32_t cnt = static_cast<uint32_t>(ge - gs);
+            const uint32_t first = static_cast<uint32_t>(gs - blk);
+            for (uint32_t k = 0; k < cnt; k++) {
+                while (r + 1 < n && p >= L.loff[r + 1] - L.loff[r]) { r++; p = 0; }
+                uint32_t byte = srcbase[L.src[r] + p];
+                p++;
+                uint32_t at = first + k;
+                outw[at >> 2] |= byte << (8 * (at & 3));
+            }
+            if (cnt == 16) {
+                *reinterpret_cast<uint4*>(chars + blk) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+            } else {
+                for (uint32_t k = 0; k < cnt; k++) {
+                    uint32_t at = first + k;
+                    chars[blk + at] = static_cast<uint8_t>(outw[at >> 2] >> (8 * (at & 3)));
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+}
+
+
 __global__ void __launch_bounds__(256) k_ba_gather(const uint8_t* __restrict__ bytes,
                                                    const DevPage* __restrict__ pages,
                                                    const DevTile* __restrict__ tiles, int ntiles,
@@ -399,7 +749,7 @@ __global__ void __launch_bounds__(256) k_ba_gather(const uint8_t* __restrict__ b
                                                    int64_t capacity, int32_t* __restrict__ overflow,
                                                    uint32_t* __restrict__ validity,
                                                    int64_t* __restrict__ offsets,
-                                                   uint8_t* __restrict__ chars) {
+                                                   uint8_t* __restrict__ chars, bool byte_gather) {
     __shared__ GatherLds lds_all[kWavesPerBlock];
     const int wv = threadIdx.x / kWave;
     const int t = blockIdx.x * kWavesPerBlock + wv;
@@ -451,50 +801,19 @@ __global__ void __launch_bounds__(256) k_ba_gather(const uint8_t* __restrict__ b
         if (lane() == 0) atomicOr(overflow, 1);
         return;
     }
-    const int64_t G1 = G0 + total;
-    const int64_t B0 = G0 >> 4;
-    const int64_t nb = ((G1 - 1) >> 4) - B0 + 1;
-    for (int64_t w0 = 0; w0 < nb; w0 += kGatherWindow) {
-        const int64_t w1 = min(nb, w0 + static_cast<int64_t>(kGatherWindow));
-        // scatter: row r owns the blocks whose first in-tile byte lies in it
-        for (uint32_t r = lane(); r < n; r += kWave) {
-            uint32_t s = L.loff[r], e = L.loff[r + 1];
-            if (e <= s) continue;
-            int64_t blo = s == 0 ? 0 : ((s + G0 + 15) >> 4) - B0;
-            int64_t bhi = ((e + G0 + 15) >> 4) - B0 - 1;
-            blo = max(blo, w0);
-            bhi = min(bhi, w1 - 1);
-            for (int64_t b = blo; b <= bhi; b++) L.blockrow[b - w0] = static_cast<uint16_t>(r);
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        for (int64_t b = w0 + lane(); b < w1; b += kWave) {
-            const int64_t blk = (B0 + b) << 4;
-            const int64_t gs = max(blk, G0), ge = min(blk + 16, G1);
-            uint32_t r = L.blockrow[b - w0];
-            uint32_t q = static_cast<uint32_t>(gs - G0);
-            uint32_t p = q - L.loff[r];
-            uint32_t outw[4] = {0, 0, 0, 0};
-            const uint32_t cnt = static_cast<uint32_t>(ge - gs);
-            const uint32_t first = static_cast<uint32_t>(gs - blk);
-            for (uint32_t k = 0; k < cnt; k++) {
-                while (r + 1 < n && p >= L.loff[r + 1] - L.loff[r]) { r++; p = 0; }
-                uint32_t byte = srcbase[L.src[r] + p];
-                p++;
-                uint32_t at = first + k;
-                outw[at >> 2] |= byte << (8 * (at & 3));
-            }
-            if (cnt == 16) {
-                *reinterpret_cast<uint4*>(chars + blk) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
-            } else {
-                for (uint32_t k = 0; k < cnt; k++) {
-                    uint32_t at = first + k;
-                    chars[blk + at] = static_cast<uint8_t>(outw[at >> 2] >> (8 * (at & 3)));
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // characters: row per lane, unaligned 16-byte moves (row_copy.hpp); the
+    // rows of neighbouring lanes are adjacent in the output
+    if (byte_gather) {
+        const int64_t G1 = G0 + total;
+        const int64_t B0 = G0 >> 4;
+        const int64_t nb = ((G1 - 1) >> 4) - B0 + 1;
+        gather_bytes(L, srcbase, n, G0, G1, B0, nb, chars);
+        return;
+    }
+    uint8_t* out = chars + G0;
+    for (uint32_t r = lane(); r < n; r += kWave) {
+        const uint32_t s = L.loff[r], e = L.loff[r + 1];
+        rc::copy_row_g(out + s, srcbase + L.src[r], e - s);
     }
 }
 
@@ -670,8 +989,16 @@ void launch_ba_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, i
                     const DevDict* dicts, const uint64_t* entries, const int32_t* dict_count,
                     ColumnParams cp, uint64_t* row_codes, int64_t* tile_chars,
                     const int32_t* page_tile0, DevErr* page_err, int32_t* err_any, uint32_t big_plain_min,
-                    uint32_t max_page) {
+                    uint32_t max_page, bool wide) {
     if (npages <= 0) return;
+    if (wide && cp.max_rep == 0 && cp.max_def <= 1) {
+        const WideLayout Lo = wide_layout(max_page);
+        if (Lo.bytes <= 160 * 1024 && ensure_dyn_lds(reinterpret_cast<const void*>(k_wide_rows), Lo.bytes)) {
+            hipLaunchKernelGGL(k_wide_rows, dim3(npages), dim3(kWdThreads), Lo.bytes, s, bytes, pages, dicts, entries,
+                               dict_count, cp, row_codes, tile_chars, page_tile0, page_err, err_any, big_plain_min, Lo);
+            return;
+        }
+    }
     if (max_page > kStageWords * 4) {  // pages up to 32 KiB decode from LDS too
         hipLaunchKernelGGL((k_ba_rows<8192, 1>), dim3(npages), dim3(64), 0, s, bytes, pages, npages, dicts,
                            entries, dict_count, cp, row_codes, tile_chars, page_tile0, page_err, err_any,
@@ -710,13 +1037,13 @@ void launch_ba_gather(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
                       const uint64_t* entries, const uint64_t* row_codes,
                       const int64_t* tile_base, int64_t nrows_total, const int64_t* total,
                       int64_t capacity, int32_t* overflow, uint32_t* validity, int64_t* offsets,
-                      uint8_t* chars) {
+                      uint8_t* chars, bool byte_gather) {
     (void)entries;
     if (ntiles <= 0) return;
     int blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     hipLaunchKernelGGL(k_ba_gather, dim3(blocks), dim3(256), 0, s, bytes, pages, tiles, ntiles,
                        dicts, row_codes, tile_base, nrows_total, total, capacity, overflow,
-                       validity, offsets, chars);
+                       validity, offsets, chars, byte_gather);
 }
 
 void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,

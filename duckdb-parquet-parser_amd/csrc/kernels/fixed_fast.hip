@@ -196,13 +196,18 @@ __device__ __forceinline__ void fused_scatter(const uint8_t* __restrict__ bytes,
 constexpr int kLvWaves = 8;
 constexpr uint32_t kLvStage = 16384;
 constexpr uint32_t kLvRec = 4096;
+constexpr uint32_t kLvStageS = 8192;
+constexpr uint32_t kLvRecS = 2048;
 constexpr uint32_t kLvTiles = 128;
 constexpr uint32_t kLvSpecMax = 4096;  // level sections up to this size: run_spec.hpp (workgroup) instead of one lane
 constexpr uint32_t kLvSpecList = kLvSpecMax / 2 / kSpJump + 8;
 
 // kScatter: the PLAIN fixed-width values too (k_fixed_scatter's work for the
-// page's tiles, after its levels), one launch instead of two.
-template <bool kScatter>
+// page's tiles, after its levels), one launch instead of two.  kStage / kRec:
+// LDS bytes for the level section and run records (the small form, 8 KiB /
+// 2,048 runs, ~35 KB per workgroup, fits four workgroups per CU instead of two;
+// longer sections or more runs take the serial form).
+template <bool kScatter, uint32_t kStage = kLvStage, uint32_t kRec = kLvRec>
 __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* __restrict__ bytes,
                                                                 const DevPage* __restrict__ pages,
                                                                 const int32_t* __restrict__ page_tile0,
@@ -214,8 +219,8 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
                                                                 int32_t* __restrict__ err_any,
                                                                 const DevTile* __restrict__ tiles,
                                                                 uint8_t* __restrict__ values) {
-    __shared__ __attribute__((aligned(16))) uint32_t stage[kLvStage / 4 + 8];
-    __shared__ uint2 rec[kLvRec];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kStage / 4 + 8];
+    __shared__ uint2 rec[kRec];
     __shared__ __attribute__((aligned(16))) uint16_t mark_all[kLvWaves][kTileRows];
     __shared__ uint8_t vb_all[kLvWaves][kWave];
     __shared__ uint32_t tnn[kLvTiles];
@@ -248,7 +253,7 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
                 else pos += rl;
             }
         }
-        if (!st && (n > 65535u || 4 + dlen + 16 > kLvStage || n > kLvTiles * kTileRows)) st = 1;
+        if (!st && (n > 65535u || 4 + dlen + 16 > kStage || n > kLvTiles * kTileRows)) st = 1;
         if (lane() == 0) { sh[0] = st; sh[1] = 0; sh[2] = pos; sh[3] = dlen; }
     }
     __syncthreads();
@@ -264,7 +269,7 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
     static_assert(sizeof(mark_all) >= 2 * kLvSpecMax, "jump table in mark_all");
     if (sh[0] == 0 && dlen <= kLvSpecMax) {  // the run table by the workgroup (run_spec.hpp)
         const uint32_t nr = spec_runs<kLvWaves * kWave, kLvSpecMax / (kLvWaves * kWave)>(
-            stage, 4, dlen, bw, n, &mark_all[0][0], splist, spesum, kLvSpecList, rec, kLvRec, ssh);
+            stage, 4, dlen, bw, n, &mark_all[0][0], splist, spesum, kLvSpecList, rec, kRec, ssh);
         if (threadIdx.x == 0) {
             if (nr == ~0u) sh[0] = 1;
             else sh[1] = nr;
@@ -277,7 +282,7 @@ __global__ void __launch_bounds__(kLvWaves * 64) k_fixed_levels2(const uint8_t* 
         W.bw = bw;
         W.n = n;
         W.sbase = 0;
-        W.cap = kLvRec;
+        W.cap = kRec;
         W.out = rec;
         W.gp = page;
         uint32_t flag = 0, nrec = 0;
@@ -457,7 +462,7 @@ __device__ __forceinline__ void fused_scatter(const uint8_t* __restrict__ bytes,
 void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,
                         int ntiles, const int32_t* page_tile0, ColumnParams cp, uint32_t* validity,
                         uint8_t* values, int32_t* tile_rank, int32_t* page_pos, DevErr* page_err,
-                        int32_t* err_any, bool fused) {
+                        int32_t* err_any, bool fused, bool small) {
     if (ntiles <= 0) return;
     const uint32_t pw = static_cast<uint32_t>(cp.plain_width);
     const int tb = (ntiles + kTilesPerBlock - 1) / kTilesPerBlock;
@@ -472,20 +477,30 @@ void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* page
                            values);
         return;
     }
-    hipLaunchKernelGGL(k_fixed_levels2<false>, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0, cp,
-                       validity, tile_rank, page_pos, static_cast<int32_t*>(nullptr), page_err, err_any,
-                       static_cast<const DevTile*>(nullptr), static_cast<uint8_t*>(nullptr));
+    if (small)
+        hipLaunchKernelGGL((k_fixed_levels2<false, kLvStageS, kLvRecS>), dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes,
+                           pages, page_tile0, cp, validity, tile_rank, page_pos, static_cast<int32_t*>(nullptr), page_err,
+                           err_any, static_cast<const DevTile*>(nullptr), static_cast<uint8_t*>(nullptr));
+    else
+        hipLaunchKernelGGL(k_fixed_levels2<false>, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0,
+                           cp, validity, tile_rank, page_pos, static_cast<int32_t*>(nullptr), page_err, err_any,
+                           static_cast<const DevTile*>(nullptr), static_cast<uint8_t*>(nullptr));
     hipLaunchKernelGGL(k_fixed_scatter, dim3(tb), dim3(kTilesPerBlock * kWave), 0, s, bytes, pages, tiles, ntiles, pw,
                        validity, tile_rank, page_pos, page_err, values);
 }
 
 void launch_fixed_levels(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
                          const int32_t* page_tile0, ColumnParams cp, uint32_t* validity, int32_t* tile_rank,
-                         int32_t* page_pos, int32_t* page_nn, DevErr* page_err, int32_t* err_any) {
+                         int32_t* page_pos, int32_t* page_nn, DevErr* page_err, int32_t* err_any, bool small) {
     if (npages <= 0) return;
-    hipLaunchKernelGGL(k_fixed_levels2<false>, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0, cp,
-                       validity, tile_rank, page_pos, page_nn, page_err, err_any, static_cast<const DevTile*>(nullptr),
-                       static_cast<uint8_t*>(nullptr));
+    if (small)
+        hipLaunchKernelGGL((k_fixed_levels2<false, kLvStageS, kLvRecS>), dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes,
+                           pages, page_tile0, cp, validity, tile_rank, page_pos, page_nn, page_err, err_any,
+                           static_cast<const DevTile*>(nullptr), static_cast<uint8_t*>(nullptr));
+    else
+        hipLaunchKernelGGL(k_fixed_levels2<false>, dim3(npages), dim3(kLvWaves * kWave), 0, s, bytes, pages, page_tile0,
+                           cp, validity, tile_rank, page_pos, page_nn, page_err, err_any,
+                           static_cast<const DevTile*>(nullptr), static_cast<uint8_t*>(nullptr));
 }
 
 }  // namespace pqk

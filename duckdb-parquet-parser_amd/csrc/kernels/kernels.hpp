@@ -108,7 +108,7 @@ void launch_ba_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, i
                     const DevDict* dicts, const uint64_t* entries, const int32_t* dict_count,
                     ColumnParams cp, uint64_t* row_codes, int64_t* tile_chars,
                     const int32_t* page_tile0, DevErr* page_err, int32_t* err_any, uint32_t big_plain_min,
-                    uint32_t max_page);
+                    uint32_t max_page, bool wide);
 uint32_t ba_rows_stage_bytes();
 
 void launch_scan_i64(hipStream_t s, const int64_t* in, int64_t* out_excl, int64_t n,
@@ -119,7 +119,7 @@ void launch_ba_gather(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
                       const uint64_t* entries, const uint64_t* row_codes,
                       const int64_t* tile_base, int64_t nrows_total, const int64_t* total,
                       int64_t capacity, int32_t* overflow, uint32_t* validity, int64_t* offsets,
-                      uint8_t* chars);
+                      uint8_t* chars, bool byte_gather);
 
 void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
                   const DevDict* dicts, const int32_t* dict_count, ColumnParams cp,
@@ -219,11 +219,11 @@ void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match,
 // ranks, value section start and non-null count of every page
 void launch_fixed_levels(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages,
                          const int32_t* page_tile0, ColumnParams cp, uint32_t* validity, int32_t* tile_rank,
-                         int32_t* page_pos, int32_t* page_nn, DevErr* page_err, int32_t* err_any);
+                         int32_t* page_pos, int32_t* page_nn, DevErr* page_err, int32_t* err_any, bool small);
 void launch_fixed_plain(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, const DevTile* tiles,
                         int ntiles, const int32_t* page_tile0, ColumnParams cp, uint32_t* validity,
                         uint8_t* values, int32_t* tile_rank, int32_t* page_pos, DevErr* page_err,
-                        int32_t* err_any, bool fused = true);
+                        int32_t* err_any, bool fused, bool small);
 
 // ── fused BYTE_ARRAY path (dict_fused.hip) ─────────────────────────────────
 struct FusedLaunch {

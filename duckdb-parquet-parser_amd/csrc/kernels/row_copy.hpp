@@ -53,6 +53,29 @@ __device__ __forceinline__ void copy_row(uint8_t* d, const uint32_t* w, uint32_t
     }
 }
 
+// Bytes s[0 .. ln) (global memory, any alignment, >= 16 readable bytes past
+// the row: image slots are zero padded) to d[0 .. ln), the same move shapes.
+__device__ __forceinline__ void copy_row_g(uint8_t* d, const uint8_t* s, uint32_t ln) {
+    if (ln >= 16) {
+        for (uint32_t x = 0; x + 16 < ln; x += 16) *reinterpret_cast<B16*>(d + x) = *reinterpret_cast<const B16*>(s + x);
+        *reinterpret_cast<B16*>(d + ln - 16) = *reinterpret_cast<const B16*>(s + ln - 16);
+    } else if (ln >= 8) {
+        const B8 a = *reinterpret_cast<const B8*>(s), b = *reinterpret_cast<const B8*>(s + ln - 8);
+        *reinterpret_cast<B8*>(d) = a;
+        *reinterpret_cast<B8*>(d + ln - 8) = b;
+    } else if (ln >= 4) {
+        const B4 a = *reinterpret_cast<const B4*>(s), b = *reinterpret_cast<const B4*>(s + ln - 4);
+        *reinterpret_cast<B4*>(d) = a;
+        *reinterpret_cast<B4*>(d + ln - 4) = b;
+    } else if (ln >= 2) {
+        const B2 a = *reinterpret_cast<const B2*>(s), b = *reinterpret_cast<const B2*>(s + ln - 2);
+        *reinterpret_cast<B2*>(d) = a;
+        *reinterpret_cast<B2*>(d + ln - 2) = b;
+    } else if (ln) {
+        d[0] = s[0];
+    }
+}
+
 }  // namespace rc
 }  // namespace dev
 }  // namespace pqk

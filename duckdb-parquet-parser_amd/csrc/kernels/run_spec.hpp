@@ -60,7 +60,7 @@ __device__ __forceinline__ bool spec_bad(const SpecHdr& h, uint32_t e, uint32_t 
 // kPerThread.  Scratch: tab (len u16), list and esum (lcap u32 each), sh (4
 // u32).  Records go to rec[0 .. rcap).  Every thread of the workgroup calls
 // this (it holds barriers); returns the record count or ~0u.
-template <int kThreads, int kPerThread>
+template <int kThreads, int kPerThread, bool kBlocked = false>
 __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, uint32_t bw, uint32_t n,
                               uint16_t* tab, uint32_t* list, uint32_t* esum, uint32_t lcap, uint2* rec, uint32_t rcap,
                               uint32_t* sh) {
@@ -73,26 +73,60 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
     }
     if (tid < 4) sh[tid] = 0;
     __syncthreads();
-    // 2. kSpJump-run jumps
-    for (int r = 0; r < kSpJumpLog; r++) {
-        uint32_t nv[kPerThread];
+    // 2. kSpJump-run jumps.  kBlocked: thread t owns positions
+    //    [t * kPerThread, (t + 1) * kPerThread) as 16-byte LDS vectors (tab
+    //    16-byte aligned, kPerThread % 8 == 0), so a round holds kPerThread
+    //    u16 jumps in kPerThread / 2 registers; else positions t + i * kThreads.
+    if constexpr (kBlocked) {
+        static_assert(kPerThread % 8 == 0, "blocked rounds load 8 jumps at once");
+        constexpr int kV = kPerThread / 8;
+        uint4* t4 = reinterpret_cast<uint4*>(tab);
+        for (int r = 0; r < kSpJumpLog; r++) {
+            uint4 nv[kV];
 #pragma unroll
-        for (int i = 0; i < kPerThread; i++) {
-            const uint32_t j = tid + static_cast<uint32_t>(i) * kThreads;
-            uint32_t t = kSpStop;
-            if (j < len) {
-                t = tab[j];
-                if (t != kSpStop) t = tab[t];
+            for (int v = 0; v < kV; v++) {
+                const uint32_t j = tid * kPerThread + static_cast<uint32_t>(v) * 8;
+                uint4 c = j < len ? t4[j / 8] : make_uint4(~0u, ~0u, ~0u, ~0u);
+                uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    uint32_t lo = w[h] & 0xFFFFu, hi = w[h] >> 16;
+                    if (lo != kSpStop) lo = tab[lo];
+                    if (hi != kSpStop) hi = tab[hi];
+                    w[h] = lo | (hi << 16);
+                }
+                nv[v] = make_uint4(w[0], w[1], w[2], w[3]);
             }
-            nv[i] = t;
-        }
-        __syncthreads();
+            __syncthreads();
 #pragma unroll
-        for (int i = 0; i < kPerThread; i++) {
-            const uint32_t j = tid + static_cast<uint32_t>(i) * kThreads;
-            if (j < len) tab[j] = static_cast<uint16_t>(nv[i]);
+            for (int v = 0; v < kV; v++) {
+                const uint32_t j = tid * kPerThread + static_cast<uint32_t>(v) * 8;
+                if (j < len) t4[j / 8] = nv[v];
+            }
+            __syncthreads();
         }
-        __syncthreads();
+    } else {
+        for (int r = 0; r < kSpJumpLog; r++) {
+            uint32_t nv[(kPerThread + 1) / 2];  // two u16 jumps per register
+#pragma unroll
+            for (int i = 0; i < kPerThread; i++) {
+                const uint32_t j = tid + static_cast<uint32_t>(i) * kThreads;
+                uint32_t t = kSpStop;
+                if (j < len) {
+                    t = tab[j];
+                    if (t != kSpStop) t = tab[t];
+                }
+                if (i & 1) nv[i >> 1] |= t << 16;
+                else nv[i >> 1] = t;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < kPerThread; i++) {
+                const uint32_t j = tid + static_cast<uint32_t>(i) * kThreads;
+                if (j < len) tab[j] = static_cast<uint16_t>(nv[i >> 1] >> (16 * (i & 1)));
+            }
+            __syncthreads();
+        }
     }
     // 3. every kSpJump-th header of the real chain
     const uint32_t lmax = rcap > kSpJump + 1 ? min(lcap, (rcap - kSpJump - 1) / kSpJump + 1) : 0u;
@@ -112,7 +146,7 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
     const uint32_t nl = sh[0];
     if (nl == ~0u) return ~0u;
     // 4. exact runs of each listed header: untruncated counts, first bad step
-    const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+    const uint32_t vmask = nbv >= 3 ? 0xFFFFFFu : nbv == 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);  // RLE values of bw <= 24 exact
     const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
     for (uint32_t i = tid; i < nl; i += kThreads) {
         uint32_t q = base + list[i];

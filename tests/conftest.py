@@ -25,7 +25,7 @@ def ctx():
 
 
 # Kernel-path fixtures shared by the GPU parity tests.
-@pytest.fixture(params=["default", "front", "big", "fused", "generic"])
+@pytest.fixture(params=["default", "front", "big", "fused", "generic", "serial"])
 def path(request, ctx):
     """Every kernel path that ships: "default" = what a chunk takes with the
     default options (dictionary BYTE_ARRAY on dict_pipe.hip: the run-table
@@ -37,14 +37,19 @@ def path(request, ctx):
     (the large-page kernel) so it also meets small pages; "fused" forces the
     per-page fused BYTE_ARRAY kernel (dict_fused.hip) onto every BYTE_ARRAY
     chunk it can take; "generic" forces decode.hip's rows/scan/gather and
-    per-page k_fixed.  PLAIN BYTE_ARRAY chunks take the one-pass kernel
+    per-page k_fixed (dictionary chunks: rows by k_wide_rows, a workgroup per
+    page); "serial" is "generic" with the wave-per-page k_ba_rows, the byte-wise
+    gather and k_fixed_levels2's large-LDS form.  PLAIN BYTE_ARRAY chunks take the one-pass kernel
     (k_plain_fused) under "default" and the two passes under "big"."""
     p = request.param
     ctx.set_option("big_all", int(p == "big"))
     ctx.set_option("dict_pipe", int(p in ("default", "front", "big")))
     ctx.set_option("plain_ba", int(p in ("default", "front", "big")))
-    ctx.set_option("fused_ba", int(p != "generic"))
-    ctx.set_option("fixed_plain", int(p != "generic"))
+    ctx.set_option("fused_ba", int(p not in ("generic", "serial")))
+    ctx.set_option("fixed_plain", int(p not in ("generic", "serial")))
+    ctx.set_option("wide_rows", int(p != "serial"))
+    ctx.set_option("gather_rows", int(p != "serial"))
+    ctx.set_option("levels_small", int(p != "serial"))
     ctx.set_option("plain_fused", int(p != "big"))
     ctx.set_option("fixed_fused", int(p == "big"))
     ctx.set_option("pipe_front", int(p == "front"))
@@ -54,6 +59,9 @@ def path(request, ctx):
     ctx.set_option("fixed_fused", 0)
     ctx.set_option("pipe_front", 0)
     ctx.set_option("big_all", 0)
+    ctx.set_option("wide_rows", 1)
+    ctx.set_option("gather_rows", 1)
+    ctx.set_option("levels_small", 1)
 
 
 @pytest.fixture(params=["window", "codes", "codes_front", "lanes", "nfa"])

@@ -562,3 +562,30 @@ def test_row_groups_over_two_contexts(ctx, layout):
             dc.free()
     finally:
         ctx2.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wide", [1, 0], ids=["wide_rows", "serial"])
+@pytest.mark.parametrize("name,col,rows", [
+    ("dict100k_opt", gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.05, dict_size=100_000,
+                             len_min=4, len_max=12, max_run=1), 120_000),
+    ("dict100k_req", gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, dict_size=100_000, len_min=4, len_max=12,
+                             max_run=3), 200_000),
+    ("dict_bw19_sparse", gen.Col("s", gen.DICT_STRINGS, gen.BYTE_ARRAY, optional=True, null_frac=0.6,
+                                 dict_size=3_000_000, len_min=5, len_max=8, max_run=1), 700_000),
+], ids=lambda v: v if isinstance(v, str) else "")
+def test_wide_dictionary_20k_pages(ctx, wide, name, col, rows):
+    """Dictionaries beyond the pipe's LDS (17-20-bit indices) on pyarrow-sized
+    20,000-row pages: the generic rows pass by a workgroup per page
+    (k_wide_rows: speculative run records for both streams) and by the
+    wave-per-page walk, both equal to the oracle."""
+    ctx.set_option("wide_rows", wide)
+    try:
+        f = gen.build([col], rows, 1, seed=21, layout=gen.ARROW_LAYOUT)
+        chunks = file_chunks(f, 0)
+        rc_o, msg_o, d_o = oracle_read_column(f, chunks)
+        rc_g, msg_g, d_g = gpu_read_column(ctx, f, chunks)
+        assert (rc_g, msg_g) == (rc_o, msg_o)
+        assert d_g == d_o
+    finally:
+        ctx.set_option("wide_rows", 1)
