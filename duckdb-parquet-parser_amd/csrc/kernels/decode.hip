@@ -325,6 +325,7 @@ __global__ void __launch_bounds__(kWPB * 64) k_ba_rows(const uint8_t* __restrict
 constexpr int kWdWaves = 16;
 constexpr uint32_t kWdThreads = kWdWaves * kWave;
 constexpr uint32_t kWdPer = 48;  // spec positions per thread: streams up to 49,152 bytes (64 spill)
+constexpr int kWdJumpLog = 6;  // 64-run jumps: the serial list walk is a quarter of kSpJumpLog's
 constexpr uint32_t kWdMaxRows = 65535;
 constexpr uint32_t kWdTiles = (kWdMaxRows + kTileRows) / kTileRows;
 constexpr uint32_t kWdWaveScratch = kTileRows * 2 + kTileRows * 4;  // mark u16 + ranks' indices u32
@@ -353,7 +354,7 @@ __host__ inline WideLayout wide_layout(uint32_t max_page) {
     L.tab = o; o += L.tab_bytes;
     L.scratch = L.tab + L.tab_bytes - scr;
     L.rcap = (L.scratch - L.tab) / 8;
-    L.lcap = L.rcap / kSpJump + 8;
+    L.lcap = L.rcap / 16 + 8;
     L.list = o; o += wd_al16(4 * L.lcap);
     L.esum = o; o += wd_al16(4 * L.lcap);
     L.pvalid = o; o += wd_al16(kWdMaxRows / 8 + 16);
@@ -482,7 +483,7 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
     const uint32_t ntiles = (n + kTileRows - 1) / kTileRows;
     // 2. def records -> validity bytes, tile counts
     if (fast && cp.max_def == 1) {
-        const uint32_t nd = spec_runs<kWdThreads, kWdPer, true>(stage, 4, dlen, 1, n, tab, list, esum, Lo.lcap, rec, Lo.rcap, sh);
+        const uint32_t nd = spec_runs<kWdThreads, kWdPer, true, kWdJumpLog>(stage, 4, dlen, 1, n, tab, list, esum, Lo.lcap, rec, Lo.rcap, sh);
         if (nd == ~0u) fast = 0;
         else {
             uint32_t rd = 0;
@@ -523,7 +524,7 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
     uint32_t ni = 0;
     const uint32_t nn = fast ? sh[8] : 0u;
     if (fast && nn > 0) {
-        ni = spec_runs<kWdThreads, kWdPer, true>(stage, ibase, size - ibase, ibw, nn, tab, list, esum, Lo.lcap, rec, Lo.rcap,
+        ni = spec_runs<kWdThreads, kWdPer, true, kWdJumpLog>(stage, ibase, size - ibase, ibw, nn, tab, list, esum, Lo.lcap, rec, Lo.rcap,
                                            sh);
         if (ni == ~0u) fast = 0;
     }

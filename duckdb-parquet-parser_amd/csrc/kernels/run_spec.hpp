@@ -60,10 +60,11 @@ __device__ __forceinline__ bool spec_bad(const SpecHdr& h, uint32_t e, uint32_t 
 // kPerThread.  Scratch: tab (len u16), list and esum (lcap u32 each), sh (4
 // u32).  Records go to rec[0 .. rcap).  Every thread of the workgroup calls
 // this (it holds barriers); returns the record count or ~0u.
-template <int kThreads, int kPerThread, bool kBlocked = false>
+template <int kThreads, int kPerThread, bool kBlocked = false, int kJumpLog = kSpJumpLog>
 __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, uint32_t bw, uint32_t n,
                               uint16_t* tab, uint32_t* list, uint32_t* esum, uint32_t lcap, uint2* rec, uint32_t rcap,
                               uint32_t* sh) {
+    constexpr uint32_t kJump = 1u << kJumpLog;
     const uint32_t tid = threadIdx.x, e = base + len, nbv = (bw + 7) / 8;
     // 1. speculative headers
     for (uint32_t j = tid; j < len; j += kThreads) {
@@ -73,7 +74,7 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
     }
     if (tid < 4) sh[tid] = 0;
     __syncthreads();
-    // 2. kSpJump-run jumps.  kBlocked: thread t owns positions
+    // 2. kJump-run jumps.  kBlocked: thread t owns positions
     //    [t * kPerThread, (t + 1) * kPerThread) as 16-byte LDS vectors (tab
     //    16-byte aligned, kPerThread % 8 == 0), so a round holds kPerThread
     //    u16 jumps in kPerThread / 2 registers; else positions t + i * kThreads.
@@ -81,7 +82,7 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
         static_assert(kPerThread % 8 == 0, "blocked rounds load 8 jumps at once");
         constexpr int kV = kPerThread / 8;
         uint4* t4 = reinterpret_cast<uint4*>(tab);
-        for (int r = 0; r < kSpJumpLog; r++) {
+        for (int r = 0; r < kJumpLog; r++) {
             uint4 nv[kV];
 #pragma unroll
             for (int v = 0; v < kV; v++) {
@@ -106,7 +107,7 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
             __syncthreads();
         }
     } else {
-        for (int r = 0; r < kSpJumpLog; r++) {
+        for (int r = 0; r < kJumpLog; r++) {
             uint32_t nv[(kPerThread + 1) / 2];  // two u16 jumps per register
 #pragma unroll
             for (int i = 0; i < kPerThread; i++) {
@@ -128,8 +129,8 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
             __syncthreads();
         }
     }
-    // 3. every kSpJump-th header of the real chain
-    const uint32_t lmax = rcap > kSpJump + 1 ? min(lcap, (rcap - kSpJump - 1) / kSpJump + 1) : 0u;
+    // 3. every kJump-th header of the real chain
+    const uint32_t lmax = rcap > kJump + 1 ? min(lcap, (rcap - kJump - 1) / kJump + 1) : 0u;
     if (tid == 0) {
         uint32_t k = 0, q = 0;
         for (;;) {
@@ -150,9 +151,9 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
     const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
     for (uint32_t i = tid; i < nl; i += kThreads) {
         uint32_t q = base + list[i];
-        uint2* out = rec + i * kSpJump;
-        uint32_t s = 0, sum = 0, bad = kSpJump, ended = 0;
-        for (; s < kSpJump; s++) {
+        uint2* out = rec + i * kJump;
+        uint32_t s = 0, sum = 0, bad = kJump, ended = 0;
+        for (; s < kJump; s++) {
             if (q >= e) { ended = 1; break; }
             const SpecHdr h = spec_hdr(stw, q);
             if (spec_bad(h, e, nbv)) { bad = s; break; }
@@ -162,7 +163,7 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
             const uint64_t nql = static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw;
             q = h.lit ? (nql > e ? e : static_cast<uint32_t>(nql)) : h.qh + nbv;
         }
-        if (s == kSpJump && q >= e) ended = 1;
+        if (s == kJump && q >= e) ended = 1;
         esum[i] = sum;
         list[i] = s | (bad << 8) | (ended << 16);
     }
@@ -186,7 +187,7 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
         const uint32_t nr = meta & 0xFFu, bad = (meta >> 8) & 0xFFu, ended = meta >> 16;
         const uint32_t b0 = esum[i];
         if (b0 >= n) continue;
-        uint2* out = rec + i * kSpJump;
+        uint2* out = rec + i * kJump;
         uint32_t c0 = b0, kept = 0;
         for (uint32_t s = 0; s < nr && c0 < n; s++) {
             const uint32_t c = out[s].x;
@@ -195,12 +196,12 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
             kept = s + 1;
         }
         if (c0 >= n) {
-            sh[1] = i * kSpJump + kept;
-        } else if (bad < kSpJump || (i + 1 == nl && (!ended || i * kSpJump + nr >= rcap))) {
+            sh[1] = i * kJump + kept;
+        } else if (bad < kJump || (i + 1 == nl && (!ended || i * kJump + nr >= rcap))) {
             atomicOr(&sh[2], 1u);  // a bad header before the value count
         } else if (i + 1 == nl) {  // exhausted: the rest of the values are 0
             out[nr] = make_uint2(c0 | ((n - c0) << 16), 0u);
-            sh[1] = i * kSpJump + nr + 1;
+            sh[1] = i * kJump + nr + 1;
         }
     }
     __syncthreads();

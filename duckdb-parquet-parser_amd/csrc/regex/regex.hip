@@ -239,6 +239,19 @@ __device__ __forceinline__ uint32_t dfa_step_full(const uint16_t* T, uint32_t e,
     return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(T) + e + 2 * b);
 }
 
+// i < rem ? t : e, as one compare into VCC and one select: opaque to the
+// compiler, so the 64 per-byte compares of a block are not hoisted into SGPR
+// masks that spill (and no copy of rem is made per byte).
+template <class I>
+__device__ __forceinline__ uint32_t sel_below(I i, uint32_t rem, uint32_t t, uint32_t e) {
+    uint32_t r;
+    __asm__("v_cmp_lt_u32 vcc, %3, %2\n\tv_cndmask_b32 %0, %4, %1, vcc"
+            : "=v"(r)
+            : "v"(t), "v"(rem), "n"(static_cast<uint32_t>(i)), "v"(e)
+            : "vcc");
+    return r;
+}
+
 __device__ __forceinline__ void lane_err(DevErr* e, int32_t* any, int code, uint32_t pos, uint32_t need,
                                          uint32_t size) {
     e->code = code;
@@ -799,11 +812,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
 #pragma unroll
                         for (uint32_t h = 0; h < kStrPerLane; h++) {
                             const uint32_t t = dfa_step_full(T, e2[h], (Aw[h][i >> 2] >> (8 * (i & 3))) & 0xFFu);
-                            // (opaque to the compiler: the 64 per-byte compares are not
-                            // hoisted into SGPR masks that spill)
-                            uint32_t rv = rem[h];
-                            __asm__ volatile("" : "+v"(rv));
-                            e2[h] = i < rv ? t : e2[h];
+                            e2[h] = sel_below(i, rem[h], t, e2[h]);
                         }
                     }
                 } else {
