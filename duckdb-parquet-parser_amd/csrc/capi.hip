@@ -2178,7 +2178,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             pqk::launch_ba_rows(s, c->d_bytes, c->d_pages, c->npages, c->d_dicts, c->d_entries,
                                 c->d_dict_count, cp, c->d_row_codes, c->d_tile_chars,
                                 c->d_page_tile0, c->d_page_err, c->d_flags, big, c->max_page_bytes,
-                                ctx->opt_wide_rows && c->ndicts > 0);
+                                ctx->opt_wide_rows && c->ndicts > 0, ctx->d_prof);
             if (big)
                 pqk::launch_plain_big_rows(s, c->d_bytes, c->d_pages, c->npages, big, c->d_row_codes,
                                            c->d_tile_chars, c->d_page_tile0, c->d_page_err, c->d_flags);

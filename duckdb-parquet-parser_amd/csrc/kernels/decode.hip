@@ -325,7 +325,7 @@ __global__ void __launch_bounds__(kWPB * 64) k_ba_rows(const uint8_t* __restrict
 constexpr int kWdWaves = 16;
 constexpr uint32_t kWdThreads = kWdWaves * kWave;
 constexpr uint32_t kWdPer = 48;  // spec positions per thread: streams up to 49,152 bytes (64 spill)
-constexpr int kWdJumpLog = 6;  // 64-run jumps: the serial list walk is a quarter of kSpJumpLog's
+constexpr int kWdJumpLog = 4;  // 16-run jumps (64 measured slower: 0.206 -> 0.275 ms on the W column)
 constexpr uint32_t kWdMaxRows = 65535;
 constexpr uint32_t kWdTiles = (kWdMaxRows + kTileRows) / kTileRows;
 constexpr uint32_t kWdWaveScratch = kTileRows * 2 + kTileRows * 4;  // mark u16 + ranks' indices u32
@@ -406,16 +406,28 @@ __device__ __forceinline__ uint32_t wd_expand(const uint2* rec, uint32_t nrec, u
     }
     const uint32_t ex = static_cast<uint32_t>(
         __builtin_amdgcn_update_dpp(0, static_cast<int>(wave_incl_max(run)), 0x138, 0xf, 0xf, true));
+    // the eight records first (unconditional: past m the scan still names a
+    // record of the tile), then the values, branch-free
+    uint2 R[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const uint32_t j = l8 + k;
-        if (j < m) {
-            const uint2 R = rec[rd0 + max(ex, rm[k])];
-            value(j, R, v0 + j - (R.x & 0xFFFFu));
-        }
-    }
+    for (int k = 0; k < 8; k++) R[k] = rec[rd0 + max(ex, rm[k])];
+#pragma unroll
+    for (int k = 0; k < 8; k++) value(l8 + k, R[k], v0 + l8 + k - (R[k].x & 0xFFFFu));
     __builtin_amdgcn_wave_barrier();
     return rd0;
+}
+
+// Value of run record R at `off` values into it: the RLE value, or bw bits of
+// the staged page (words past `nwords` read as zero, like bytes past the
+// page), with clamped unconditional LDS reads and selects.
+__device__ __forceinline__ uint32_t wd_value(const uint32_t* stage, uint32_t nwords, const uint2& R, uint32_t off,
+                                             uint32_t bw) {
+    const uint64_t b = static_cast<uint64_t>(R.y & 0x7FFFFFFFu) + static_cast<uint64_t>(off) * bw;
+    const uint32_t wi = static_cast<uint32_t>(min(b >> 5, static_cast<uint64_t>(0x7FFFFFF0u)));
+    const uint32_t lo = stage[min(wi, nwords - 1)], hi = stage[min(wi + 1, nwords - 1)];
+    const uint64_t v = (static_cast<uint64_t>(wi + 1 < nwords ? hi : 0u) << 32) | (wi < nwords ? lo : 0u);
+    const uint32_t x = static_cast<uint32_t>(v >> (b & 31)) & ((bw >= 32 ? 0u : (1u << bw)) - 1u);
+    return (R.y >> 31) ? x : (R.y & 0x7FFFFFFFu);
 }
 
 __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restrict__ bytes,
@@ -427,8 +439,19 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
                                                          int64_t* __restrict__ tile_chars,
                                                          const int32_t* __restrict__ page_tile0,
                                                          DevErr* __restrict__ page_err, int32_t* __restrict__ err_any,
-                                                         uint32_t big_plain_min, WideLayout Lo) {
+                                                         uint32_t big_plain_min, WideLayout Lo,
+                                                         uint64_t* __restrict__ prof) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // "fused_prof": thread 0's shader-clock time per phase (slots 0-5), fallback
+    // pages (6) and pages (7), summed over workgroups
+    uint64_t tprev = prof ? __builtin_amdgcn_s_memtime() : 0;
+    auto pmark = [&](int slot) {
+        if (prof && threadIdx.x == 0) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            atomicAdd(reinterpret_cast<unsigned long long*>(prof + slot), now - tprev);
+            tprev = now;
+        }
+    };
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem + Lo.stage);
     uint16_t* tab = reinterpret_cast<uint16_t*>(smem + Lo.tab);
     uint2* rec = reinterpret_cast<uint2*>(smem + Lo.tab);
@@ -477,13 +500,15 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
         sh[7] = ibw;
     }
     __syncthreads();
+    pmark(0);
     uint32_t fast = sh[4];
     const uint32_t dlen = sh[5], ibase = sh[6], ibw = sh[7];
-    const uint32_t staged_bytes = size + 16;
+    const uint32_t swords = (size + 16) / 4;  // staged words: the payload, then slot padding (zeros)
     const uint32_t ntiles = (n + kTileRows - 1) / kTileRows;
     // 2. def records -> validity bytes, tile counts
     if (fast && cp.max_def == 1) {
         const uint32_t nd = spec_runs<kWdThreads, kWdPer, true, kWdJumpLog>(stage, 4, dlen, 1, n, tab, list, esum, Lo.lcap, rec, Lo.rcap, sh);
+        pmark(1);
         if (nd == ~0u) fast = 0;
         else {
             uint32_t rd = 0;
@@ -491,9 +516,7 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
                 const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
                 uint32_t vb = 0;
                 rd = wd_expand(rec, nd, rd, r0, m, mark, [&](uint32_t j, const uint2& R, uint32_t off) {
-                    const uint32_t lvl = (R.y >> 31) ? lds_bits(stage, staged_bytes, (R.y & 0x7FFFFFFFu) + off, 1)
-                                                     : (R.y & 0x7FFFFFFFu);
-                    vb |= (lvl == 1u ? 1u : 0u) << (j & 7);
+                    vb |= (j < m && wd_value(stage, swords, R, off, 1) == 1u ? 1u : 0u) << (j & 7);
                 });
                 pvalid[(r0 >> 3) + lane()] = static_cast<uint8_t>(vb);
                 const uint32_t c = bcast_last(wave_incl_scan(__popc(vb)));
@@ -508,6 +531,7 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
         for (uint32_t ti = threadIdx.x; ti < ntiles; ti += kWdThreads) tnn[ti] = min(n - ti * kTileRows, kTileRows);
     }
     __syncthreads();
+    pmark(2);
     if (fast && wv == 0) {  // tile ranks
         uint32_t carry = 0;
         for (uint32_t i0 = 0; i0 < ntiles; i0 += kWave) {
@@ -520,6 +544,7 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
         if (lane() == 0) sh[8] = carry;
     }
     __syncthreads();
+    pmark(3);
     // 3. index records (num_non_null values; column_reader.cpp:180-182)
     uint32_t ni = 0;
     const uint32_t nn = fast ? sh[8] : 0u;
@@ -527,6 +552,11 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
         ni = spec_runs<kWdThreads, kWdPer, true, kWdJumpLog>(stage, ibase, size - ibase, ibw, nn, tab, list, esum, Lo.lcap, rec, Lo.rcap,
                                            sh);
         if (ni == ~0u) fast = 0;
+    }
+    pmark(4);
+    if (prof && threadIdx.x == 0) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(prof + 7), 1ull);
+        if (!fast) atomicAdd(reinterpret_cast<unsigned long long*>(prof + 6), 1ull);
     }
     if (!fast) {  // the exact per-page walk (reports the reference's errors)
         if (wv == 0) {
@@ -540,40 +570,48 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
     const uint32_t dict_n = static_cast<uint32_t>(max(dict_count[pg.dict], 0));
     const uint64_t* ent = entries + dicts[pg.dict].entry_base;
     const int32_t tile0 = page_tile0[p];
-    const uint32_t lmask = (1u << ibw) - 1u;
     uint32_t rd = 0;
     for (uint32_t ti = wv; ti < ntiles; ti += kWdWaves) {
         const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
         const uint32_t cnt = tnn[ti];
         if (cnt) {
             rd = wd_expand(rec, ni, rd, trank[ti], cnt, mark, [&](uint32_t j, const uint2& R, uint32_t off) {
-                ixv[j] = (R.y >> 31) ? (lds_bits(stage, staged_bytes,
-                                                 (R.y & 0x7FFFFFFFu) + static_cast<uint64_t>(off) * ibw, ibw) & lmask)
-                                     : (R.y & 0x7FFFFFFFu);
+                ixv[j] = wd_value(stage, swords, R, off, ibw);
             });
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+        // every row group's dictionary load is issued before any is used
+        // (one L2/HBM latency per tile, not one per 64 rows)
         uint32_t run = 0;
-        uint64_t sum = 0;
-        uint64_t* out = row_codes + pg.first_row + r0;
-#pragma unroll 2
-        for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
-            const uint32_t j = j0 + lane();
+        uint64_t code[kTileRows / kWave];
+#pragma unroll
+        for (uint32_t u = 0; u < kTileRows / kWave; u++) {
+            const uint32_t j = u * kWave + lane();
             const bool v = j < m && ((pvalid[(r0 + j) >> 3] >> (j & 7)) & 1u);
             const uint64_t vm = __ballot(v);
-            uint64_t code = ~0ull;
+            code[u] = ~0ull;
             if (v) {
                 const uint32_t idx = ixv[run + popc_below(vm)];
-                if (idx < dict_n) code = ent[idx];
+                if (idx < dict_n) code[u] = ent[idx];
             }
             run += __popcll(vm);
-            if (j < m) out[j] = code;
-            sum += code == ~0ull ? 0u : (code >> 32);
+        }
+        uint64_t sum = 0;
+        uint64_t* out = row_codes + pg.first_row + r0;
+#pragma unroll
+        for (uint32_t u = 0; u < kTileRows / kWave; u++) {
+            const uint32_t j = u * kWave + lane();
+            if (j < m) out[j] = code[u];
+            sum += code[u] == ~0ull ? 0u : (code[u] >> 32);
         }
 #pragma unroll
         for (int dd = 32; dd >= 1; dd >>= 1) sum += __shfl_xor(sum, dd, kWave);
         if (lane() == 0) tile_chars[tile0 + ti] = static_cast<int64_t>(sum);
         __builtin_amdgcn_wave_barrier();
+    }
+    if (prof) {
+        __syncthreads();
+        pmark(5);
     }
 }
 
@@ -659,27 +697,66 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_apply(const int64_t* __rest
 }
 
 // One workgroup scans up to kScanBlock * kScanSingle elements in one launch.
+// Wave w owns a contiguous range; every load and store is 64 consecutive
+// elements across the lanes (a per-thread run of 32 elements made each load
+// instruction touch 64 cache lines).  Pass 1 sums the range, a scan over the
+// waves' sums gives each range its base, pass 2 re-reads (L2) and scans 64
+// elements per step with a carry.
 constexpr int kScanSingle = 32;
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t x) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const int64_t t = __shfl_up(x, d, kWave);
+        if (lane() >= static_cast<uint32_t>(d)) x += t;
+    }
+    return x;
+}
 __global__ void __launch_bounds__(kScanBlock) k_scan_single(const int64_t* __restrict__ in, int64_t n,
                                                             int64_t* __restrict__ out,
                                                             int64_t* __restrict__ total) {
     __shared__ int64_t sh[kScanBlock / kWave];
-    const int64_t base = static_cast<int64_t>(threadIdx.x) * kScanSingle;
-    int64_t v[kScanSingle];
+    constexpr int kW = kScanBlock / kWave;
+    const int w = static_cast<int>(threadIdx.x / kWave);
+    const int64_t per = (n + kW - 1) / kW;
+    const int64_t lo = min(n, w * per), hi = min(n, lo + per);
+    constexpr int kB = 8;  // 64-element groups loaded per batch (one latency per batch)
     int64_t acc = 0;
+    for (int64_t b0 = lo; b0 < hi; b0 += kB * kWave) {
+        int64_t v[kB];
 #pragma unroll
-    for (int i = 0; i < kScanSingle; i++) {
-        v[i] = base + i < n ? in[base + i] : 0;
-        acc += v[i];
-    }
-    int64_t tot;
-    int64_t ex = block_excl_scan(acc, sh, &tot);
+        for (int u = 0; u < kB; u++) {
+            const int64_t i = b0 + u * kWave + lane();
+            v[u] = i < hi ? in[i] : 0;
+        }
 #pragma unroll
-    for (int i = 0; i < kScanSingle; i++) {
-        if (base + i < n) out[base + i] = ex;
-        ex += v[i];
+        for (int u = 0; u < kB; u++) acc += v[u];
     }
-    if (threadIdx.x == 0) *total = tot;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, kWave);
+    if (lane() == 0) sh[w] = acc;
+    __syncthreads();
+    int64_t carry = 0;
+    for (int k = 0; k < w; k++) carry += sh[k];
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+        for (int k = 0; k < kW; k++) t += sh[k];
+        *total = t;
+    }
+    for (int64_t b0 = lo; b0 < hi; b0 += kB * kWave) {
+        int64_t v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int64_t i = b0 + u * kWave + lane();
+            v[u] = i < hi ? in[i] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int64_t i = b0 + u * kWave + lane();
+            const int64_t inc = wave_incl_scan64(v[u]);
+            if (i < hi) out[i] = carry + inc - v[u];
+            carry += __shfl(inc, kWave - 1, kWave);
+        }
+    }
 }
 
 // ── BYTE_ARRAY gather: offsets, validity, chars ────────────────────────────
@@ -990,13 +1067,14 @@ void launch_ba_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, i
                     const DevDict* dicts, const uint64_t* entries, const int32_t* dict_count,
                     ColumnParams cp, uint64_t* row_codes, int64_t* tile_chars,
                     const int32_t* page_tile0, DevErr* page_err, int32_t* err_any, uint32_t big_plain_min,
-                    uint32_t max_page, bool wide) {
+                    uint32_t max_page, bool wide, uint64_t* prof) {
     if (npages <= 0) return;
     if (wide && cp.max_rep == 0 && cp.max_def <= 1) {
         const WideLayout Lo = wide_layout(max_page);
         if (Lo.bytes <= 160 * 1024 && ensure_dyn_lds(reinterpret_cast<const void*>(k_wide_rows), Lo.bytes)) {
             hipLaunchKernelGGL(k_wide_rows, dim3(npages), dim3(kWdThreads), Lo.bytes, s, bytes, pages, dicts, entries,
-                               dict_count, cp, row_codes, tile_chars, page_tile0, page_err, err_any, big_plain_min, Lo);
+                               dict_count, cp, row_codes, tile_chars, page_tile0, page_err, err_any, big_plain_min, Lo,
+                               prof);
             return;
         }
     }

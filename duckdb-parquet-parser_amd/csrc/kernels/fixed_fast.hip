@@ -399,6 +399,41 @@ __device__ __forceinline__ void scatter_tile(const uint8_t* __restrict__ bytes, 
     const uint8_t* src = bytes + pg.off + pos;
     const uint32_t m = static_cast<uint32_t>(T.nrows);
     const int64_t R0 = pg.first_row + T.row0;
+    if ((pw == 8 || pw == 4) && m <= kTileRows) {
+        // the tile's validity words in one load (lane i: word i), every row
+        // group's ranks from shuffled words, then all value loads in flight
+        // before any store: two memory latencies per tile, not two per 64 rows
+        const int64_t wfirst = R0 >> 5, wlast = (R0 + m - 1) >> 5;
+        const uint32_t sh = static_cast<uint32_t>(R0 & 31);
+        const uint32_t myw = wfirst + lane() <= wlast ? validity_in[wfirst + lane()] : 0u;
+        constexpr uint32_t kU = kTileRows / kWave;
+        uint2 x[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t j = u * kWave + lane();
+            const uint32_t b = sh + j;
+            const uint32_t wd = static_cast<uint32_t>(__shfl(static_cast<int>(myw), static_cast<int>(min(b >> 5, 63u))));
+            const bool v = j < m && ((wd >> (b & 31)) & 1u);
+            const uint64_t vm = __ballot(v);
+            const uint32_t k = rank + popc_below(vm);
+            rank += __popcll(vm);
+            x[u] = make_uint2(0u, 0u);
+            if (v) {
+                if (pw == 8) x[u] = *reinterpret_cast<const uint2*>(src + static_cast<uint64_t>(k) * 8);
+                else x[u].x = *reinterpret_cast<const uint32_t*>(src + static_cast<uint64_t>(k) * 4);
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t j = u * kWave + lane();
+            if (j < m) {
+                uint8_t* o = values + static_cast<uint64_t>(R0 + j) * pw;
+                if (pw == 8) *reinterpret_cast<uint2*>(o) = x[u];
+                else *reinterpret_cast<uint32_t*>(o) = x[u].x;
+            }
+        }
+        return;
+    }
     for (uint32_t j0 = 0; j0 < m; j0 += kWave) {
         const uint32_t j = j0 + lane();
         const int64_t R = R0 + j;

@@ -108,7 +108,7 @@ void launch_ba_rows(hipStream_t s, const uint8_t* bytes, const DevPage* pages, i
                     const DevDict* dicts, const uint64_t* entries, const int32_t* dict_count,
                     ColumnParams cp, uint64_t* row_codes, int64_t* tile_chars,
                     const int32_t* page_tile0, DevErr* page_err, int32_t* err_any, uint32_t big_plain_min,
-                    uint32_t max_page, bool wide);
+                    uint32_t max_page, bool wide, uint64_t* prof = nullptr);
 uint32_t ba_rows_stage_bytes();
 
 void launch_scan_i64(hipStream_t s, const int64_t* in, int64_t* out_excl, int64_t n,

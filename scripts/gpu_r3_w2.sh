@@ -18,4 +18,6 @@ for i in 1 2; do
     done
 done
 tail -n 2 "$OUT"/w_*.json
+timeout -k 10 200 python scripts/wide_prof.py > "$OUT/wide_prof.json" 2>&1 || { tail "$OUT/wide_prof.json"; exit 1; }
+cat "$OUT/wide_prof.json"
 echo R3W2_OK
