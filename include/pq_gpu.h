@@ -161,6 +161,13 @@ int pq_ctx_sync(pq_ctx* ctx);
  *                 values in a second launch; 1: inside the def-level launch
  *   "fused_ba"    1 (default): per-page fused BYTE_ARRAY kernel for chunks the
  *                 pipe does not take; 0 forces the generic rows/scan/gather kernels
+ *   "wide_rows"   1 (default): generic BYTE_ARRAY chunks with dictionary pages
+ *                 resolve rows by a workgroup per page (k_wide_rows); 0: one wave
+ *                 per page (k_ba_rows)
+ *   "gather_rows" 1 (default): the generic gather copies characters row per
+ *                 lane; 0: byte-wise 16-byte blocks
+ *   "levels_small" 1 (default): OPTIONAL fixed-width def levels in the 35 KB LDS
+ *                 form (four workgroups per CU); 0: the 58 KB form
  *   "fused_waves" waves per workgroup cap (0 = automatic)
  *   "stage_bufs" pinned buffers of the upload ring, 2..16 (6); "stage_piece_kb"
  *                 bytes per buffer / H2D piece in KiB, 64..65536 (8192);
@@ -179,7 +186,8 @@ int pq_ctx_sync(pq_ctx* ctx);
  *                 every string's window offset (2 B per row) for later scans
  * Diagnostics (timing studies only; outputs are not valid with bits set):
  *   "fused_debug", "regex_debug" ablation bits, "fused_prof"
- *   per-phase clocks.
+ *   per-phase clocks (k_ba_fused; k_wide_rows: slots 0-5 phases, 6 fallback
+ *   pages, 7 pages).
  * Unknown keys and out-of-range values return PQ_ERR_ARG. */
 int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value);
 
