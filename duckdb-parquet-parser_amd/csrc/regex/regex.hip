@@ -499,7 +499,24 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                                                                   const uint16_t* __restrict__ index_in,
                                                                   uint16_t* __restrict__ index_out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-    {
+    // Full tables are rebuilt in LDS as bytes: T8[state << 8 | byte] = next
+    // state, A8[state] = accepts at the string end (a full table has < 64
+    // states).  The DFA step is then one v_perm (state and byte into the
+    // address) and one ds_read_u8, against a shift, an add and a ds_read_u16
+    // over the u16 byte-offset rows.  Class tables are copied as they are.
+    const DevDfa* Dg = reinterpret_cast<const DevDfa*>(dfa_img);
+    if (Dg->full) {
+        const uint4* src = reinterpret_cast<const uint4*>(dfa_img);
+        uint4* dst = reinterpret_cast<uint4*>(dsm);
+        copy_blocks(dst, src, static_cast<uint32_t>(sizeof(DevDfa)) / 16, threadIdx.x, blockDim.x);
+        const uint16_t* Tg = reinterpret_cast<const uint16_t*>(dfa_img + sizeof(DevDfa));
+        uint8_t* T8w = dsm + sizeof(DevDfa);
+        const uint32_t nst = Dg->nstates;
+        for (uint32_t i = threadIdx.x; i < nst * 256; i += blockDim.x)
+            T8w[i] = static_cast<uint8_t>(Tg[(i >> 8) * (kDfaRowBytes / 2) + (i & 255)] / kDfaRowBytes);
+        for (uint32_t st = threadIdx.x; st < nst; st += blockDim.x)
+            T8w[nst * 256 + st] = Tg[st * (kDfaRowBytes / 2) + 256] != 0 ? 1 : 0;
+    } else {
         const uint4* src = reinterpret_cast<const uint4*>(dfa_img);
         uint4* dst = reinterpret_cast<uint4*>(dsm);
         copy_blocks(dst, src, dfa_bytes / 16, threadIdx.x, blockDim.x);
@@ -507,6 +524,12 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
     __syncthreads();
     const DevDfa* D = reinterpret_cast<const DevDfa*>(dsm);
     const uint16_t* T = reinterpret_cast<const uint16_t*>(dsm + sizeof(DevDfa));
+    const uint8_t* T8 = dsm + sizeof(DevDfa);
+    const uint8_t* A8 = T8 + D->nstates * 256;
+    // T8 as an LDS address constant: dsm is this kernel's only LDS object, so
+    // it starts at LDS address 0 and the table lookup needs no base add
+    using lds_u8 = const __attribute__((address_space(3))) uint8_t;
+    lds_u8* T8c = reinterpret_cast<lds_u8*>(static_cast<uintptr_t>(sizeof(DevDfa)));
     const uint32_t nc = D->nclasses;
     const bool full = D->full != 0;
     const bool empty_ok = D->empty_string != 0;
@@ -787,7 +810,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                 off2[h] = ent;
                 len2[h] = ok2[h] ? st_u32(stage, ent - 4) : 0u;
                 pg2[h] = gl;
-                e2[h] = full ? (DFA_START * kDfaRowBytes) : DFA_START;
+                e2[h] = DFA_START;
             }
             uint32_t maxl = 0;
 #pragma unroll
@@ -811,7 +834,9 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                     for (uint32_t i = 0; i < 16; i++) {
 #pragma unroll
                         for (uint32_t h = 0; h < kStrPerLane; h++) {
-                            const uint32_t t = dfa_step_full(T, e2[h], (Aw[h][i >> 2] >> (8 * (i & 3))) & 0xFFu);
+                            // address = state << 8 | byte i of the block (one v_perm)
+                            const uint32_t a = __builtin_amdgcn_perm(e2[h], Aw[h][i >> 2], 0x0C0C0400u | (i & 3));
+                            const uint32_t t = T8c[a];
                             e2[h] = sel_below(i, rem[h], t, e2[h]);
                         }
                     }
@@ -830,8 +855,8 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
 #pragma unroll
             for (uint32_t h = 0; h < kStrPerLane; h++) {
                 const uint32_t e = e2[h];
-                const uint32_t st = full ? e / kDfaRowBytes : (e & 0x7FFFu);
-                const bool acc = full ? dfa_step_full(T, e, 256) != 0 : (e >> 15) != 0;
+                const uint32_t st = full ? e : (e & 0x7FFFu);
+                const bool acc = full ? A8[e] != 0 : (e >> 15) != 0;
                 const bool m = len2[h] == 0 ? empty_ok : (trivial || st == DFA_ACCEPT || acc);
                 const bool sat = ok2[h] && (static_cast<uint32_t>(m) != negv);
                 if (sat) atomicOr(&hit[pg2[h] >> 5], 1u << (pg2[h] & 31));
