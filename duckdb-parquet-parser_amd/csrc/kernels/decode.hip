@@ -354,7 +354,7 @@ __host__ inline WideLayout wide_layout(uint32_t max_page) {
     L.tab = o; o += L.tab_bytes;
     L.scratch = L.tab + L.tab_bytes - scr;
     L.rcap = (L.scratch - L.tab) / 8;
-    L.lcap = L.rcap / 16 + 8;
+    L.lcap = L.rcap / 16 + 24;  // both streams' lists (spec_runs2) fit
     L.list = o; o += wd_al16(4 * L.lcap);
     L.esum = o; o += wd_al16(4 * L.lcap);
     L.pvalid = o; o += wd_al16(kWdMaxRows / 8 + 16);
@@ -482,7 +482,7 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
             if (4 > size) fast = 0;
             else {
                 dlen = static_cast<uint32_t>(gld8(bytes + pg.off, 0));
-                if (4ull + dlen > size || dlen > kWdThreads * kWdPer) fast = 0;
+                if (4ull + dlen > size || size - 5 > kWdThreads * kWdPer) fast = 0;  // both streams in one table
                 else pos = 4 + dlen;
             }
         }
@@ -505,9 +505,26 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
     const uint32_t dlen = sh[5], ibase = sh[6], ibw = sh[7];
     const uint32_t swords = (size + 16) / 4;  // staged words: the payload, then slot padding (zeros)
     const uint32_t ntiles = (n + kTileRows - 1) / kTileRows;
-    // 2. def records -> validity bytes, tile counts
+    // 2. run records of both streams in one pass (spec_runs2: def levels at
+    //    [4, 4 + dlen), indices from ibase to the page end, the latter over
+    //    all n rows as an upper bound of num_non_null: only ranks < nn are
+    //    read), then def records -> validity bytes, tile counts
+    uint2* irec = rec;
+    uint32_t ni = 0;
     if (fast && cp.max_def == 1) {
-        const uint32_t nd = spec_runs<kWdThreads, kWdPer, true, kWdJumpLog>(stage, 4, dlen, 1, n, tab, list, esum, Lo.lcap, rec, Lo.rcap, sh);
+        constexpr uint32_t kJ = 1u << kWdJumpLog;
+        const uint32_t rc0 = min(Lo.rcap / 2, (dlen / 2 + 3 * kJ + 15) & ~15u);  // def runs <= dlen / 2 + 1
+        const uint32_t base2[2] = {4u, ibase}, len2[2] = {dlen, size - ibase}, bw2[2] = {1u, ibw}, n2[2] = {n, n};
+        const uint32_t rcap2[2] = {rc0, Lo.rcap - rc0};
+        const uint32_t lcap2[2] = {rc0 / kJ + 8, (Lo.rcap - rc0) / kJ + 8};
+        uint2* const rec2[2] = {rec, rec + rc0};
+        uint32_t cnt2[2];
+        spec_runs2<kWdThreads, kWdPer, kWdJumpLog>(stage, base2, len2, bw2, n2, tab, list, esum, lcap2, rec2, rcap2,
+                                                   sh + 8, cnt2);
+        irec = rec + rc0;
+        ni = cnt2[1];
+        if (ni == ~0u) fast = 0;
+        const uint32_t nd = fast ? cnt2[0] : ~0u;
         pmark(1);
         if (nd == ~0u) fast = 0;
         else {
@@ -545,10 +562,10 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
     }
     __syncthreads();
     pmark(3);
-    // 3. index records (num_non_null values; column_reader.cpp:180-182)
-    uint32_t ni = 0;
+    // 3. index records (num_non_null values; column_reader.cpp:180-182):
+    //    REQUIRED chunks here (all rows non-null), OPTIONAL ones above
     const uint32_t nn = fast ? sh[8] : 0u;
-    if (fast && nn > 0) {
+    if (fast && cp.max_def == 0 && nn > 0) {
         ni = spec_runs<kWdThreads, kWdPer, true, kWdJumpLog>(stage, ibase, size - ibase, ibw, nn, tab, list, esum, Lo.lcap, rec, Lo.rcap,
                                            sh);
         if (ni == ~0u) fast = 0;
@@ -575,7 +592,7 @@ __global__ void __launch_bounds__(kWdThreads) k_wide_rows(const uint8_t* __restr
         const uint32_t r0 = ti * kTileRows, m = min(n - r0, static_cast<uint32_t>(kTileRows));
         const uint32_t cnt = tnn[ti];
         if (cnt) {
-            rd = wd_expand(rec, ni, rd, trank[ti], cnt, mark, [&](uint32_t j, const uint2& R, uint32_t off) {
+            rd = wd_expand(irec, ni, rd, trank[ti], cnt, mark, [&](uint32_t j, const uint2& R, uint32_t off) {
                 ixv[j] = wd_value(stage, swords, R, off, ibw);
             });
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

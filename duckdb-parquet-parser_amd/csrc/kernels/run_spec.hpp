@@ -208,5 +208,159 @@ __device__ uint32_t spec_runs(const uint32_t* stw, uint32_t base, uint32_t len, 
     return (sh[2] || sh[1] == 0) ? ~0u : sh[1];
 }
 
+
+// Two streams of one page at once (k_wide_rows: the def levels and the
+// dictionary indices): one table over both streams' positions (stream 0 at
+// [0, len0), stream 1 at [len0, len0 + len1); a chain never leaves its stream
+// because each stops at its own end), one set of doubling rounds and
+// barriers, the two list walks on different waves at the same time, the
+// exact re-parse and the scans of both in the same passes.  Records of stream
+// s go to rec_s[0 .. rcap_s); list/esum hold lcap0 + lcap1 entries.  Returns
+// both record counts in out[0], out[1] (~0u: that stream needs the serial
+// path).  Blocked rounds as spec_runs<.., true, ..>; len0 + len1 <= kThreads
+// * kPerThread < 65535.
+template <int kThreads, int kPerThread, int kJumpLog = kSpJumpLog>
+__device__ void spec_runs2(const uint32_t* stw, const uint32_t base_[2], const uint32_t len_[2], const uint32_t bw_[2],
+                           const uint32_t n_[2], uint16_t* tab, uint32_t* list, uint32_t* esum, const uint32_t lcap_[2],
+                           uint2* const rec_[2], const uint32_t rcap_[2], uint32_t* sh, uint32_t out[2]) {
+    constexpr uint32_t kJump = 1u << kJumpLog;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t L0 = len_[0], L = len_[0] + len_[1];
+    // 1. speculative headers of both streams
+    for (uint32_t j = tid; j < L; j += kThreads) {
+        const uint32_t s = j < L0 ? 0u : 1u;
+        const uint32_t off = s ? L0 : 0u, base = base_[s], bw = bw_[s], e = base + len_[s], nbv = (bw + 7) / 8;
+        const SpecHdr h = spec_hdr(stw, base + (j - off));
+        const uint64_t nx = h.lit ? static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw : h.qh + nbv;
+        tab[j] = static_cast<uint16_t>((spec_bad(h, e, nbv) || nx >= e) ? kSpStop
+                                                                        : off + static_cast<uint32_t>(nx - base));
+    }
+    if (tid < 8) sh[tid] = 0;
+    __syncthreads();
+    // 2. kJump-run jumps (blocked, as spec_runs)
+    {
+        static_assert(kPerThread % 8 == 0, "blocked rounds load 8 jumps at once");
+        constexpr int kV = kPerThread / 8;
+        uint4* t4 = reinterpret_cast<uint4*>(tab);
+        for (int r = 0; r < kJumpLog; r++) {
+            uint4 nv[kV];
+#pragma unroll
+            for (int v = 0; v < kV; v++) {
+                const uint32_t j = tid * kPerThread + static_cast<uint32_t>(v) * 8;
+                uint4 c = j < L ? t4[j / 8] : make_uint4(~0u, ~0u, ~0u, ~0u);
+                uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    uint32_t lo = w[h] & 0xFFFFu, hi = w[h] >> 16;
+                    if (lo != kSpStop) lo = tab[lo];
+                    if (hi != kSpStop) hi = tab[hi];
+                    w[h] = lo | (hi << 16);
+                }
+                nv[v] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int v = 0; v < kV; v++) {
+                const uint32_t j = tid * kPerThread + static_cast<uint32_t>(v) * 8;
+                if (j < L) t4[j / 8] = nv[v];
+            }
+            __syncthreads();
+        }
+    }
+    // 3. every kJump-th header of each chain: stream 0 by thread 0, stream 1
+    //    by thread kWave (another wave), concurrently; positions stream-local
+    if (tid == 0 || tid == kWave) {
+        const uint32_t s = tid == 0 ? 0u : 1u;
+        const uint32_t off = s ? L0 : 0u, len = len_[s], rcap = rcap_[s];
+        uint32_t* lst = list + (s ? lcap_[0] : 0u);
+        const uint32_t lmax = rcap > kJump + 1 ? min(lcap_[s], (rcap - kJump - 1) / kJump + 1) : 0u;
+        uint32_t k = 0, q = 0;
+        for (;;) {
+            if (k >= lmax) { k = ~0u; break; }
+            lst[k++] = q;
+            if (q >= len) break;
+            const uint32_t t = tab[off + q];
+            if (t == kSpStop) break;
+            q = t - off;
+        }
+        sh[4 * s] = k;
+    }
+    __syncthreads();
+    const uint32_t nl_[2] = {sh[0], sh[4]};
+    const uint32_t nla = nl_[0] == ~0u ? 0u : nl_[0], nlb = nl_[1] == ~0u ? 0u : nl_[1];
+    // 4. exact runs of each listed header (both streams)
+    for (uint32_t g = tid; g < nla + nlb; g += kThreads) {
+        const uint32_t s = g < nla ? 0u : 1u, i = s ? g - nla : g;
+        const uint32_t base = base_[s], bw = bw_[s], e = base + len_[s], nbv = (bw + 7) / 8;
+        const uint32_t vmask = nbv >= 3 ? 0xFFFFFFu : nbv == 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+        const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
+        uint32_t* lst = list + (s ? lcap_[0] : 0u);
+        uint32_t* es = esum + (s ? lcap_[0] : 0u);
+        uint32_t q = base + lst[i];
+        uint2* o = rec_[s] + i * kJump;
+        uint32_t st = 0, sum = 0, bad = kJump, ended = 0;
+        for (; st < kJump; st++) {
+            if (q >= e) { ended = 1; break; }
+            const SpecHdr h = spec_hdr(stw, q);
+            if (spec_bad(h, e, nbv)) { bad = st; break; }
+            const uint32_t c = h.lit ? min(h.g, kSpCountCap / 8) * 8 : min(h.g, kSpCountCap);
+            o[st] = make_uint2(c, h.lit ? (litpay | (h.qh * litmul)) : (h.vraw & vmask));
+            sum = min(sum + c, kSpCountCap);
+            const uint64_t nql = static_cast<uint64_t>(h.qh) + static_cast<uint64_t>(h.g) * bw;
+            q = h.lit ? (nql > e ? e : static_cast<uint32_t>(nql)) : h.qh + nbv;
+        }
+        if (st == kJump && q >= e) ended = 1;
+        es[i] = sum;
+        lst[i] = st | (bad << 8) | (ended << 16);
+    }
+    __syncthreads();
+    // 5. exclusive scans of the counts: stream 0 by wave 0, stream 1 by wave 1
+    const uint32_t wv = tid / kWave;
+    if (wv < 2) {
+        const uint32_t s = wv, nl = s ? nlb : nla, ln = tid % kWave;
+        uint32_t* es = esum + (s ? lcap_[0] : 0u);
+        const uint32_t per = (nl + kWave - 1) / kWave;
+        const uint32_t a0 = min(nl, ln * per), a1 = min(nl, a0 + per);
+        uint32_t sum = 0;
+        for (uint32_t i = a0; i < a1; i++) sum += es[i];
+        uint32_t run = wave_incl_scan(sum) - sum;
+        for (uint32_t i = a0; i < a1; i++) {
+            const uint32_t x = es[i];
+            es[i] = run;
+            run += x;
+        }
+    }
+    __syncthreads();
+    for (uint32_t g = tid; g < nla + nlb; g += kThreads) {
+        const uint32_t s = g < nla ? 0u : 1u, i = s ? g - nla : g, nl = s ? nlb : nla, n = n_[s];
+        const uint32_t* lst = list + (s ? lcap_[0] : 0u);
+        const uint32_t* es = esum + (s ? lcap_[0] : 0u);
+        const uint32_t meta = lst[i];
+        const uint32_t nr = meta & 0xFFu, bad = (meta >> 8) & 0xFFu, ended = meta >> 16;
+        const uint32_t b0 = es[i];
+        if (b0 >= n) continue;
+        uint2* o = rec_[s] + i * kJump;
+        uint32_t c0 = b0, kept = 0;
+        for (uint32_t t = 0; t < nr && c0 < n; t++) {
+            const uint32_t c = o[t].x;
+            o[t].x = c0 | (min(c, n - c0) << 16);
+            c0 += c;
+            kept = t + 1;
+        }
+        if (c0 >= n) {
+            sh[4 * s + 1] = i * kJump + kept;
+        } else if (bad < kJump || (i + 1 == nl && (!ended || i * kJump + nr >= rcap_[s]))) {
+            atomicOr(&sh[4 * s + 2], 1u);  // a bad header before the value count
+        } else if (i + 1 == nl) {  // exhausted: the rest of the values are 0
+            o[nr] = make_uint2(c0 | ((n - c0) << 16), 0u);
+            sh[4 * s + 1] = i * kJump + nr + 1;
+        }
+    }
+    __syncthreads();
+    for (uint32_t s = 0; s < 2; s++)
+        out[s] = (nl_[s] == ~0u || sh[4 * s + 2] || sh[4 * s + 1] == 0) ? ~0u : sh[4 * s + 1];
+    __syncthreads();
+}
+
 }  // namespace dev
 }  // namespace pqk
