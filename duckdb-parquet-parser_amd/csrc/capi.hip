@@ -324,9 +324,10 @@ int hip_check(pq_ctx* ctx, hipError_t e, const char* what) {
 // current device is per thread.  Restores the caller's device on return.
 struct DevGuard {
     int prev = -1;
-    explicit DevGuard(const pq_ctx* c) {
+    explicit DevGuard(const pq_ctx* c) : DevGuard(c ? c->device : -1) {}
+    explicit DevGuard(int device) {
         int cur = 0;
-        if (c && hipGetDevice(&cur) == hipSuccess && cur != c->device && hipSetDevice(c->device) == hipSuccess) prev = cur;
+        if (device >= 0 && hipGetDevice(&cur) == hipSuccess && cur != device && hipSetDevice(device) == hipSuccess) prev = cur;
     }
     ~DevGuard() {
         if (prev >= 0) (void)hipSetDevice(prev);
@@ -796,7 +797,9 @@ pq_ctx* pq_ctx_create(int device) {
     try {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return nullptr;
-        if (hipSetDevice(device) != hipSuccess) return nullptr;
+        DevGuard dg(device);  // the caller's current device comes back on return
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess || cur != device) return nullptr;
         auto* c = new pq_ctx();
         c->device = device;
         int cus = 0;
@@ -826,7 +829,8 @@ pq_ctx* pq_ctx_create(int device) {
 
 void pq_ctx_destroy(pq_ctx* ctx) {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
+    {
+    DevGuard dg(ctx);
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& p : ctx->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto& p : ctx->free_events) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
@@ -847,6 +851,7 @@ void pq_ctx_destroy(pq_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->copy2);
     (void)hipStreamDestroy(ctx->copy2);
     (void)hipStreamDestroy(ctx->stream);
+    }
     delete ctx;
 }
 
@@ -2569,7 +2574,8 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             }
             Timed t(ctx, "regex_codes");
             pqk::launch_pipe_match(s, P, c->d_dict_match + c->pipe_entry_base, neg, c->d_page_flags, fold);
-        } else if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && plan_regex_windows(ctx, c)) {
+        } else if (c->d_dfa && ctx->opt_regex_plain && c->ndicts == 0 && pqre::regex_plain_lds_ok() &&
+                   plan_regex_windows(ctx, c)) {
             // REQUIRED chunks: the first error-free scan files every string's
             // window offset (row-indexed); later scans read it instead of
             // walking the length chains (same windows: same window size)
@@ -2629,7 +2635,11 @@ int pq_decode_regex_async(pq_ctx* ctx, pq_chunk* c, pq_column* out, const char* 
     const bool one = c->pipe && ctx->opt_pipe && ctx->opt_regex_codes && !plain_go && c->ndicts > 0 &&
                      c->pipe_dict_payload < pqk::kArmDictBytes;
     if (!one) {
+        // the scan clears d_flags, which still holds this decode's status
+        // (err_any, char overflow, the PLAIN redo flags): check the decode
+        // first, so its redo / growth / error runs before the scan starts
         if (int rc = pq_decode_async(ctx, c, out)) return rc;
+        if (int rc = collect(ctx, c, out)) return rc;
         return pq_regex_pages_async(ctx, c, pattern, neg);
     }
     c->arm = true;

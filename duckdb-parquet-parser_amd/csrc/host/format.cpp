@@ -8,6 +8,8 @@
 #include <mutex>
 #include <thread>
 
+#include <unistd.h>
+
 namespace pqfmt {
 
 // common.hpp:136-147 semantics: 7-bit groups, "varint too long" past 63 bits.
@@ -758,6 +760,7 @@ bool linked_walk(std::vector<SpecSeg>& segs, size_t start, const pq_chunk_desc& 
 
 namespace {
 struct HostPool {
+    const pid_t pid = getpid();  // the process whose threads these are
     std::mutex busy;  // one job at a time
     std::mutex m;
     std::condition_variable cv, done_cv;
@@ -792,9 +795,28 @@ struct HostPool {
         for (auto& t : workers) t.join();
     }
 };
+// The pool belongs to the process that started its threads.  A child forked
+// after that (bench.py's fork pools) inherits the pool's memory but none of
+// its threads, and possibly a mutex some parent thread held at the fork: it
+// must not touch that pool.  It builds its own; the inherited one is left
+// alone (leaked), and only the owning process joins its threads at exit.
+struct PoolHolder {
+    std::atomic<HostPool*> pool{nullptr};
+    ~PoolHolder() {
+        HostPool* p = pool.load();
+        if (p && p->pid == getpid()) delete p;
+    }
+};
+PoolHolder g_pools;
 HostPool& host_pool() {
-    static HostPool p;
-    return p;
+    const pid_t me = getpid();
+    HostPool* p = g_pools.pool.load(std::memory_order_acquire);
+    while (!p || p->pid != me) {  // lock-free: no mutex a fork could have caught held
+        HostPool* fresh = new HostPool;
+        if (g_pools.pool.compare_exchange_strong(p, fresh, std::memory_order_acq_rel)) return *fresh;
+        delete fresh;  // another thread of this process installed one first (p now holds it)
+    }
+    return *p;
 }
 }  // namespace
 

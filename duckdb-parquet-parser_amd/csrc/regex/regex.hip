@@ -527,7 +527,9 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
     const uint8_t* T8 = dsm + sizeof(DevDfa);
     const uint8_t* A8 = T8 + D->nstates * 256;
     // T8 as an LDS address constant: dsm is this kernel's only LDS object, so
-    // it starts at LDS address 0 and the table lookup needs no base add
+    // it starts at LDS address 0 and the table lookup needs no base add (the
+    // dsm-relative form costs a VALU add per lookup).  The host verifies the
+    // kernel has no static LDS before it launches it (regex_plain_lds_ok).
     using lds_u8 = const __attribute__((address_space(3))) uint8_t;
     lds_u8* T8c = reinterpret_cast<lds_u8*>(static_cast<uintptr_t>(sizeof(DevDfa)));
     const uint32_t nc = D->nclasses;
@@ -941,6 +943,19 @@ void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, u
                        regex_plain_lds(dfa_bytes, win_bytes),
                        s, dfa, dfa_bytes, win_bytes, bytes, pages, wins, nwins, ticket, cp, neg, page_flags,
                        page_err, err_any, index_in, index_out);
+}
+
+// k_regex_plain reads its byte-state table through a constant LDS address
+// (T8c): that holds only while the kernel has no static LDS, so that the
+// dynamic block dsm starts at LDS address 0.  Checked once from the code
+// object's own attributes; when it fails the caller takes k_regex_lanes.
+bool regex_plain_lds_ok() {
+    static const bool ok = [] {
+        hipFuncAttributes a{};
+        if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_regex_plain)) != hipSuccess) return false;
+        return a.sharedSizeBytes == 0;
+    }();
+    return ok;
 }
 
 int regex_plain_occupancy(uint32_t lds) {  // the LDS sets it: one workgroup of regex_plain_waves waves per CU

@@ -81,6 +81,7 @@ constexpr uint32_t regex_plain_wave_lds(uint32_t win_bytes) { return win_bytes +
 uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes);
 uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes);
 int regex_plain_occupancy(uint32_t lds);
+bool regex_plain_lds_ok();  // k_regex_plain's constant-address LDS table is valid (no static LDS)
 void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
                         const uint8_t* bytes, const pqk::DevPage* pages, const pqk::DevBatch* wins, int nwins,
                         int32_t* ticket, int grid, pqk::ColumnParams cp, int neg, uint8_t* page_flags,

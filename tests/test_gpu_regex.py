@@ -186,6 +186,37 @@ def test_decode_regex_one_pass(ctx, name, cols, n, layout, neg):
     dc.free()
 
 
+FRESH_REDO = ["opt_plain_extra", "opt_plain_spec_extra", "plain_spec_extra", "plain_spec_long",
+              "opt_plain_page", "plain_pages"]
+
+
+@pytest.mark.parametrize("neg", [False, True], ids=["like", "notlike"])
+@pytest.mark.parametrize("case", FRESH_REDO)
+def test_decode_regex_fresh_chunk_redo(ctx, case, neg):
+    """pq_decode_regex_async on a freshly uploaded chunk (no checked decode
+    before it) whose pages do not fit the one-pass PLAIN form (bytes after
+    the strings, fewer values declared than the page holds, OPTIONAL value
+    sections, chains that need the generic path): the decode's redo runs
+    before the scan clears the status words, so both the column and the page
+    flags equal the oracle's on the first call."""
+    import test_gpu_decode as D
+    f, ch = D.CRAFTED[case]()
+    rc_o, msg_o, d_o = O.read_all(f, to_oracle_chunk(ch))
+    assert rc_o == 0, msg_o
+    exp_dump = O.dump_column(d_o)
+    for p in ("a", "^[a-m]", "zz", "q.*x"):
+        exp = golden_pages(f, [ch], p, neg)
+        dc = ctx.upload(f, [to_desc(ch)])
+        try:
+            dc.decode_regex_async(p, neg)
+            got = dc.regex_pages_result()
+            dc.decode_check()
+            assert np.array_equal(got, exp), (case, p, neg)
+            assert capi.canonical_dump(dc.to_host()) == exp_dump, (case, p)
+        finally:
+            dc.free()
+
+
 @pytest.mark.parametrize("layout,rpp", [(gen.REF_LAYOUT, 0), (gen.ARROW_LAYOUT, 700), (gen.ARROW_LAYOUT, 1300),
                                         (gen.ARROW_LAYOUT, 2500)], ids=["ref", "arrow_21k", "arrow_40k", "arrow_77k"])
 def test_string_index_reuse(ctx, layout, rpp):
