@@ -1667,7 +1667,10 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             }
             if (!rc) {
                 Timed ct(ctx, "codec", s);
-                pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus);
+                const bool gz = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec == 2; });
+                const bool other = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec != 2 && e.codec != 0; });
+                if (gz && other) rc = set_err(ctx, PQ_ERR_CODEC, "GZIP pages mixed with other codecs in one upload");
+                else pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus, gz);
                 rc = hip_check(ctx, hipGetLastError(), "codec launch");
             }
         }

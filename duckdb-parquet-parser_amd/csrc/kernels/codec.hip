@@ -155,7 +155,43 @@ __device__ __forceinline__ uint32_t crc_xpow8(uint32_t nbytes) {
     return p;
 }
 
+// CRC-32 of ring bytes [from, to) folded into crc (finalized form): 64
+// lane segments, a crc32_combine tree over the lanes, a byte-wise tail
+__device__ __attribute__((noinline)) uint32_t crc_fold(const lds8* ring, const lds32* crc_tab, uint32_t crc,
+                                                      uint32_t from, uint32_t to) {
+    const uint32_t len = uni(to - from), s = len / kWave;  // 64 segments of s bytes, then a tail
+    if (s) {
+        uint32_t c = 0xFFFFFFFFu;
+        const uint32_t b0 = from + lane() * s;
+        for (uint32_t j = 0; j < s; j++) c = crc_tab[(c ^ ring[(b0 + j) & kRingMask]) & 0xFFu] ^ (c >> 8);
+        c = ~c;
+        // tree of crc32_combine over the lanes: round r joins lanes i, i + 2^r
+        uint32_t pw = crc_xpow8(s);  // shift by 2^r segments
+#pragma unroll
+        for (int r = 0; r < 6; r++) {
+            const uint32_t other = static_cast<uint32_t>(__shfl_down(static_cast<int>(c), 1 << r));
+            const uint32_t joined = crc_mulmod(c, pw) ^ other;
+            c = (lane() & ((2u << r) - 1u)) == 0 ? joined : c;
+            pw = crc_mulmod(pw, pw);
+        }
+        // pw: shift by 64 segments; fold the block (lane 0) into the running value
+        crc = uni(crc_mulmod(crc, pw) ^ static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c)));
+        from += kWave * s;
+    }
+    if (from < to) {  // the tail (< 64 bytes): every lane, byte by byte (uniform result)
+        uint32_t c = ~crc;
+        for (uint32_t q = from; q < to; q++) c = crc_tab[(c ^ ring[q & kRingMask]) & 0xFFu] ^ (c >> 8);
+        crc = uni(~c);
+    }
+    return crc;
+}
+
 // ── output ring ────────────────────────────────────────────────────────────
+// kCrc: the GZIP kernel only.  The CRC fold in flush() would otherwise sit,
+// inlined, in every codec's hot loop (147 VGPRs and 64 B/lane of scratch
+// with it in round 3, against 111 VGPRs and none without): the non-GZIP
+// kernel compiles it out.
+template <bool kCrc>
 struct Out {
     lds8* ring;
     uint8_t* dst;   // the page slot (16-byte aligned)
@@ -166,42 +202,31 @@ struct Out {
     uint32_t st;    // ST_*
     // running CRC-32 of the output since crc_pos0 (GZIP members): bytes
     // [crc_pos0, crc_pos) are in `crc` (finalized form); they are folded in
-    // from the ring before it can be overwritten (at every flush)
+    // from the ring before it can be overwritten: inflate calls crc_keep()
+    // once per symbol (a scalar compare; the fold runs about once per 63 KiB
+    // of output) and folds before each piece of a stored block, so the fold
+    // is out of flush() and out of the per-byte paths
     bool crc_on = false;
     uint32_t crc = 0, crc_pos = 0;
     const lds32* crc_tab = nullptr;
-    __device__ void crc_upto(uint32_t to) {
+    // (the fold is a separate function taking values, not `this`: a call
+    // through `this` puts the whole Out object in scratch)
+    __device__ __forceinline__ void crc_upto(uint32_t to) {
+        if constexpr (!kCrc) return;
         if (!crc_on || to <= crc_pos) return;
-        const uint32_t len = uni(to - crc_pos), s = len / kWave;  // 64 segments of s bytes, then a tail
-        if (s) {
-            uint32_t c = 0xFFFFFFFFu;
-            const uint32_t b0 = crc_pos + lane() * s;
-            for (uint32_t j = 0; j < s; j++) c = crc_tab[(c ^ ring[(b0 + j) & kRingMask]) & 0xFFu] ^ (c >> 8);
-            c = ~c;
-            // tree of crc32_combine over the lanes: round r joins lanes i, i + 2^r
-            uint32_t pw = crc_xpow8(s);  // shift by 2^r segments
-#pragma unroll
-            for (int r = 0; r < 6; r++) {
-                const uint32_t other = static_cast<uint32_t>(__shfl_down(static_cast<int>(c), 1 << r));
-                const uint32_t joined = crc_mulmod(c, pw) ^ other;
-                c = (lane() & ((2u << r) - 1u)) == 0 ? joined : c;
-                pw = crc_mulmod(pw, pw);
-            }
-            // pw: shift by 64 segments; fold the block (lane 0) into the running value
-            crc = uni(crc_mulmod(crc, pw) ^ static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(c)));
-            crc_pos += kWave * s;
-        }
-        if (crc_pos < to) {  // the tail (< 64 bytes): lane 0, byte by byte
-            uint32_t c = ~crc;
-            for (uint32_t q = crc_pos; q < to; q++) c = crc_tab[(c ^ ring[q & kRingMask]) & 0xFFu] ^ (c >> 8);
-            crc = uni(~c);
-            crc_pos = to;
-        }
+        crc = crc_fold(ring, crc_tab, crc, crc_pos, to);
+        crc_pos = to;
+    }
+    // fold before the ring can wrap over bytes not yet in the CRC (the
+    // caller then adds at most kCrcSlack bytes)
+    static constexpr uint32_t kCrcSlack = 1024;
+    __device__ __forceinline__ void crc_keep() {
+        if constexpr (kCrc)
+            if (crc_on && op - crc_pos > kRing - kCrcSlack) crc_upto(op);
     }
     __device__ __forceinline__ void flush(bool final) {
         while (op - fl >= kFlush || (final && fl < op)) {
             const uint32_t n = min(kFlush, op - fl);
-            crc_upto(fl + n);
             const uint32_t b = fl + 16u * lane();
             if (b < fl + n) {
                 uint4 v = lds_get16(ring, b & kRingMask);
@@ -271,7 +296,8 @@ struct Out {
 };
 
 // ── SNAPPY ─────────────────────────────────────────────────────────────────
-__device__ __forceinline__ void snappy(In& I, Out& O, uint32_t p, uint32_t end, uint32_t expect) {
+template <class OutT>
+__device__ __forceinline__ void snappy(In& I, OutT& O, uint32_t p, uint32_t end, uint32_t expect) {
     uint32_t ulen = 0;
     I.ensure(p, 8);
     for (uint32_t k = 0;; k++) {
@@ -321,7 +347,8 @@ __device__ __forceinline__ void snappy(In& I, Out& O, uint32_t p, uint32_t end, 
 }
 
 // ── LZ4 block ──────────────────────────────────────────────────────────────
-__device__ __forceinline__ void lz4_block(In& I, Out& O, uint32_t p, uint32_t end) {
+template <class OutT>
+__device__ __forceinline__ void lz4_block(In& I, OutT& O, uint32_t p, uint32_t end) {
     for (;;) {
         if (p >= end) { O.st = ST_CORRUPT; return; }
         I.ensure(p, 1);
@@ -361,7 +388,8 @@ __device__ __forceinline__ void lz4_block(In& I, Out& O, uint32_t p, uint32_t en
 }
 
 // Hadoop framing (codec LZ4): blocks of [u32 BE raw bytes][u32 BE packed bytes][LZ4 block].
-__device__ __forceinline__ void lz4_hadoop(In& I, Out& O, uint32_t p, uint32_t end) {
+template <class OutT>
+__device__ __forceinline__ void lz4_hadoop(In& I, OutT& O, uint32_t p, uint32_t end) {
     while (p < end && O.st == ST_OK) {
         if (end - p < 8) { O.st = ST_CORRUPT; return; }
         I.ensure(p, 8);
@@ -497,7 +525,7 @@ __device__ __forceinline__ int32_t decode_sym(CodecLds& L, In& I, Bits& B, const
     return -1;
 }
 
-__device__ __forceinline__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
+__device__ __forceinline__ void inflate(CodecLds& L, In& I, Out<true>& O, Bits& B) {
     for (;;) {
         const uint32_t fin = B.take(I, 1);
         const uint32_t ty = B.take(I, 2);
@@ -508,7 +536,11 @@ __device__ __forceinline__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
             const uint32_t n = uni(I.u16le(q)), nn = uni(I.u16le(q + 2));
             q += 4;
             if ((n ^ 0xFFFFu) != nn || n > B.end - q) { O.st = ST_CORRUPT; return; }
-            if (n) O.lit(I, q, n);
+            for (uint32_t d = 0; d < n; d += O.kCrcSlack) {  // pieces of <= kCrcSlack bytes, CRC kept up
+                O.crc_keep();
+                O.lit(I, q + d, min(O.kCrcSlack, n - d));
+                if (O.st != ST_OK) return;
+            }
             B.p = q + n;
         } else if (ty == 1 || ty == 2) {
             uint32_t nl = 288, nd = 30;
@@ -573,6 +605,7 @@ __device__ __forceinline__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
                 return;
             }
             for (;;) {
+                O.crc_keep();  // a symbol adds <= 258 bytes
                 const int32_t sy = decode_sym(L, I, B, L.lt, 0, 0);
                 if (sy < 0 || sy > 285) { O.st = ST_CORRUPT; return; }
                 if (sy < 256) {
@@ -607,7 +640,7 @@ __device__ __forceinline__ void inflate(CodecLds& L, In& I, Out& O, Bits& B) {
 }
 
 // GZIP members (RFC 1952) or one zlib stream (RFC 1950).
-__device__ __forceinline__ void gzip(CodecLds& L, In& I, Out& O, uint32_t p, uint32_t end) {
+__device__ __forceinline__ void gzip(CodecLds& L, In& I, Out<true>& O, uint32_t p, uint32_t end) {
     bool first = true;
     while (O.st == ST_OK && (first || p < end)) {
         if (end - p < 2) { O.st = ST_CORRUPT; return; }
@@ -662,6 +695,10 @@ __device__ __forceinline__ void gzip(CodecLds& L, In& I, Out& O, uint32_t p, uin
     }
 }
 
+// kGzip: the GZIP instantiation (CRC-32 on, DEFLATE); the other one takes
+// every other codec and the V2 rebuild.  A chunk has one codec, so one
+// launch takes one instantiation (launch_codec).
+template <bool kGzip>
 __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src, uint8_t* __restrict__ img,
                                                  const CodecEntry* __restrict__ ent, int32_t n,
                                                  uint32_t* __restrict__ status) {
@@ -670,17 +707,19 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
     lds8* lring = (lds8*)(smem + offsetof(CodecLds, ring));
     lds8* lin = (lds8*)(smem + offsetof(CodecLds, in));
     lds32* lcrc = (lds32*)(smem + offsetof(CodecLds, crc_tab));
-    for (uint32_t b = lane(); b < 256; b += kWave) {  // CRC-32 byte table
-        uint32_t c = b;
-        for (int k = 0; k < 8; k++) c = (c >> 1) ^ ((0u - (c & 1u)) & kCrcPoly);
-        lcrc[b] = c;
+    if constexpr (kGzip) {
+        for (uint32_t b = lane(); b < 256; b += kWave) {  // CRC-32 byte table
+            uint32_t c = b;
+            for (int k = 0; k < 8; k++) c = (c >> 1) ^ ((0u - (c & 1u)) & kCrcPoly);
+            lcrc[b] = c;
+        }
+        wsync();
     }
-    wsync();
     for (int32_t i = static_cast<int32_t>(blockIdx.x); i < n; i += static_cast<int32_t>(gridDim.x)) {
         const CodecEntry e = ent[i];
         In I{src + e.src, e.src_len, 0u, 0u, lin};
         I.refill(0);
-        Out O{lring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
+        Out<kGzip> O{lring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
         O.crc_tab = lcrc;
         uint32_t p = 0;
         if (e.flags & kCodecV2) {  // level sections, as is, behind their V1 length prefixes
@@ -702,13 +741,18 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
         const uint32_t end = e.src_len;
         const uint32_t expect = e.out_len - O.op;
         if (O.st == ST_OK) {
-            switch (e.codec) {
-                case 0: O.lit(I, p, end - p); break;
-                case 1: snappy(I, O, p, end, expect); break;
-                case 2: gzip(L, I, O, p, end); break;
-                case 5: lz4_hadoop(I, O, p, end); break;
-                case 7: lz4_block(I, O, p, end); break;
-                default: O.st = ST_UNSUPPORTED;
+            if constexpr (kGzip) {
+                if (e.codec == 2) gzip(L, I, O, p, end);
+                else if (e.codec == 0) O.lit(I, p, end - p);
+                else O.st = ST_UNSUPPORTED;
+            } else {
+                switch (e.codec) {
+                    case 0: O.lit(I, p, end - p); break;
+                    case 1: snappy(I, O, p, end, expect); break;
+                    case 5: lz4_hadoop(I, O, p, end); break;
+                    case 7: lz4_block(I, O, p, end); break;
+                    default: O.st = ST_UNSUPPORTED;  // (GZIP: the other instantiation)
+                }
             }
         }
         if (O.st == ST_OK && O.op != e.out_len) O.st = ST_SIZE;
@@ -723,13 +767,15 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
 size_t codec_lds_bytes() { return sizeof(CodecLds); }
 
 void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
-                  uint32_t* status, int cus) {
+                  uint32_t* status, int cus, bool gzip) {
     if (n <= 0) return;
     const uint32_t lds = static_cast<uint32_t>(sizeof(CodecLds));
-    ensure_dyn_lds(reinterpret_cast<const void*>(k_codec), lds);
+    const void* k = gzip ? reinterpret_cast<const void*>(k_codec<true>) : reinterpret_cast<const void*>(k_codec<false>);
+    ensure_dyn_lds(k, lds);
     const int per_cu = std::max(1, static_cast<int>((160u * 1024u) / lds));
     const int grid = std::min(n, std::max(1, cus) * per_cu);
-    hipLaunchKernelGGL(k_codec, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
+    if (gzip) hipLaunchKernelGGL(k_codec<true>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
+    else hipLaunchKernelGGL(k_codec<false>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
 }
 
 }  // namespace pqk

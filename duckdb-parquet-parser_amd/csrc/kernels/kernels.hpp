@@ -73,9 +73,11 @@ struct CodecEntry {
     uint32_t flags;    // kCodec*
 };
 size_t codec_lds_bytes();
-// status[i]: 0 ok, 1 corrupt input, 2 size mismatch, 3 unsupported
+// status[i]: 0 ok, 1 corrupt input, 2 size mismatch, 3 unsupported.  gzip:
+// the entries include GZIP pages (the CRC-32 instantiation; it takes codec 0
+// and 2 only, the other one every codec but 2)
 void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
-                  uint32_t* status, int cus);
+                  uint32_t* status, int cus, bool gzip);
 
 // 4 KiB chunker (chunker.hip, src/main.cpp:17-32): device scratch bytes for
 // n rows, and the launch sequence (synchronises the stream; 0 = OK).
