@@ -32,6 +32,16 @@ from test_gpu_decode import CRAFTED, ERRORS  # noqa: E402
 
 DUMP_LIMIT = 64 * 1024
 
+# Crafted pages on which the reference's behaviour is undefined, so it cannot
+# pin them (the oracle's zero-padded reading defines them for the build; the
+# GPU tests still compare with the oracle):
+#   zero_count_no_literal  a zero-count RLE run before any literal run: NULL
+#                          literal pointer dereferenced (rle_decoder.hpp:58-65)
+#   big_exhausted          a literal run whose groups run past the page: bits
+#   trunc_varint           read past the page buffer (rle_decoder.hpp:55-74);
+#                          the result changes from run to run
+REF_UNDEFINED = {"zero_count_no_literal", "big_exhausted", "trunc_varint"}
+
 
 def generated():
     yield "c1_int32_ref", gen.build(gen.c1_cols(), 10000, 1, seed=1)  # BASELINE config #1
@@ -56,7 +66,7 @@ def main():
     manifest = {}
     items = list(generated())
     for name, fn in sorted(CRAFTED.items()) + sorted(ERRORS.items()):
-        if name == "zero_count_no_literal":  # the reference dereferences NULL here
+        if name in REF_UNDEFINED:
             continue
         f, ch = fn()
         items.append(("crafted_" + name, (f, ch)))
@@ -84,6 +94,8 @@ def main():
                 ch = chunks[rg][ci]
                 rc, msg, dump = O.ref_read_all(data, ch)
                 prc, pmsg, pdump, pages = O.ref_read_pages(data, ch)
+                for _ in range(3):  # a fixture the reference reads differently each time pins nothing
+                    assert O.ref_read_all(data, ch) == (rc, msg, dump), ("reference not deterministic", name)
                 rec = {"chunk": [ch.num_values, ch.data_page_offset, ch.dictionary_page_offset,
                                  ch.codec, ch.type, ch.max_def, ch.max_rep],
                        "rc": rc, "msg": msg}
@@ -91,7 +103,7 @@ def main():
                     rec["sha256"] = hashlib.sha256(dump).hexdigest()
                     rec["len"] = len(dump)
                     rec["pages"] = [list(p) for p in pages]
-                    assert pdump == dump
+                    assert pdump == dump, (name, rg, ci)
                     if len(dump) <= DUMP_LIMIT:
                         dname = f"{name}.rg{rg}.c{ci}.dump"
                         with open(os.path.join(HERE, dname), "wb") as fh:

@@ -120,8 +120,14 @@ def plain_ba(values) -> bytes:
 
 
 def build_file(pages: list[bytes], ptype: int, optional: bool, num_values: int,
-               dict_at_start: bool = False, name: bytes = b"c", pad_footer: bool = True, codec: int = 0):
+               dict_at_start: bool = False, name: bytes = b"c", pad_footer: bool = True, codec: int = 0,
+               nested: str | None = None):
     """pages: list of (header + payload) blobs laid out back to back.
+    nested: None (one flat leaf: max_def = optional, max_rep 0), "repeated"
+    (a REPEATED leaf: max_def 1, max_rep 1) or "list" (the LIST shape
+    optional group a / repeated group list / leaf element: max_def 2 +
+    optional, max_rep 1), levels as ParquetReader::build_columns_recursive
+    counts them (parquet_reader.cpp:495-543).
     Returns (file bytes, chunk dict for the oracle/C ABI)."""
     body = b"PAR1"
     start = len(body)
@@ -130,9 +136,21 @@ def build_file(pages: list[bytes], ptype: int, optional: bool, num_values: int,
     end = len(body)
     t = TW()
     t.i32(1, 1)
-    t.list_begin(2, 12, 2)
-    t.push(); t.string(4, b"schema"); t.i32(5, 1); t.stop(); t.pop()
-    t.push(); t.i32(1, ptype); t.i32(3, 1 if optional else 0); t.string(4, name); t.stop(); t.pop()
+    if nested == "list":
+        t.list_begin(2, 12, 4)
+        t.push(); t.string(4, b"schema"); t.i32(5, 1); t.stop(); t.pop()
+        t.push(); t.i32(3, 1); t.string(4, b"a"); t.i32(5, 1); t.i32(6, 3); t.stop(); t.pop()
+        t.push(); t.i32(3, 2); t.string(4, b"list"); t.i32(5, 1); t.stop(); t.pop()
+        t.push(); t.i32(1, ptype); t.i32(3, 1 if optional else 0); t.string(4, name); t.stop(); t.pop()
+        path = [b"a", b"list", name]
+        max_def, max_rep = 2 + (1 if optional else 0), 1
+    else:
+        t.list_begin(2, 12, 2)
+        t.push(); t.string(4, b"schema"); t.i32(5, 1); t.stop(); t.pop()
+        rep = 2 if nested == "repeated" else (1 if optional else 0)
+        t.push(); t.i32(1, ptype); t.i32(3, rep); t.string(4, name); t.stop(); t.pop()
+        path = [name]
+        max_def, max_rep = (1, 1) if nested == "repeated" else (1 if optional else 0, 0)
     t.i64(3, num_values)
     t.list_begin(4, 12, 1)
     t.push()
@@ -143,8 +161,9 @@ def build_file(pages: list[bytes], ptype: int, optional: bool, num_values: int,
     t.i32(1, ptype)
     t.list_begin(2, 5, 1)
     t.b += zigzag(0)
-    t.list_begin(3, 8, 1)
-    t.b += varint(len(name)) + name
+    t.list_begin(3, 8, len(path))
+    for seg in path:
+        t.b += varint(len(seg)) + seg
     t.i32(4, codec)
     t.i64(5, num_values)
     t.i64(6, end - start)
@@ -166,5 +185,5 @@ def build_file(pages: list[bytes], ptype: int, optional: bool, num_values: int,
     data = body + footer + struct.pack("<I", len(footer)) + b"PAR1"
     chunk = dict(num_values=num_values, data_page_offset=start,
                  dictionary_page_offset=start if dict_at_start else None, codec=codec, type=ptype,
-                 max_def=1 if optional else 0, max_rep=0)
+                 max_def=max_def, max_rep=max_rep)
     return data, chunk

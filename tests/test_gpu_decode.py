@@ -280,7 +280,89 @@ def _huge_dict_file(n: int, seed: int, lmin: int = 1, lmax: int = 14, decl: int 
                         dict_at_start=True)
 
 
+def _rep_pages(ptype, nested, optional, rows_per_page, npages, seed, enc=0, dict_vals=None, spec_order=False,
+               rep_len_delta=0, cut_after_def=False):
+    """Pages of a repeated column (max_rep 1) in the order the reference reads
+    them, [u32 def_len][def][u32 rep_len][rep][values] (column_reader.cpp:
+    146-170: definition levels first, repetition levels decoded and dropped);
+    spec_order writes [rep][def] as the Parquet spec (and pyarrow) lay V1
+    pages out, which the reference then reads with the sections swapped.
+    Levels mix RLE and bit-packed runs; values are PLAIN (INT64 / DOUBLE /
+    BOOLEAN / BYTE_ARRAY) or dictionary indices (enc 8, dict_vals)."""
+    rng = np.random.default_rng(seed)
+    max_def = (2 + (1 if optional else 0)) if nested == "list" else 1
+    dbw, rbw = max(1, int(max_def).bit_length()), 1
+    pages = []
+    if dict_vals is not None:
+        dpay = B.plain_ba(dict_vals)
+        pages.append(B.dict_header(len(dpay), len(dict_vals)) + dpay)
+    total = 0
+    for k in range(npages):
+        n = rows_per_page
+        defs, reps, i = [], [], 0
+        while i < n:  # runs of one level (RLE) and stretches of random levels (bit-packed)
+            if rng.random() < 0.4:
+                m = int(min(n - i, rng.integers(8, 60)))
+                defs += [max_def] * m if rng.random() < 0.7 else [int(rng.integers(0, max_def + 1))] * m
+            else:
+                m = int(min(n - i, 8 * rng.integers(1, 6)))
+                defs += [int(x) for x in np.where(rng.random(m) < 0.75, max_def, rng.integers(0, max_def + 1, m))]
+            i += m
+        defs = defs[:n]
+        reps = [0 if (j == 0 or rng.random() < 0.3) else 1 for j in range(n)]
+        dstream = _hybrid(defs, dbw, rng, max_groups=4)
+        rstream = _hybrid(reps, rbw, rng, max_groups=3)
+        nn = sum(1 for d in defs if d == max_def)
+        if dict_vals is not None:
+            bw = max(1, (len(dict_vals) - 1).bit_length())
+            vals = bytes([bw]) + _hybrid([int(x) for x in rng.integers(0, len(dict_vals), nn)], bw, rng)
+        elif ptype == gen.INT64:
+            vals = struct.pack(f"<{nn}q", *[int(x) for x in rng.integers(-1 << 50, 1 << 50, nn)])
+        elif ptype == gen.DOUBLE:
+            vals = struct.pack(f"<{nn}d", *[float(x) for x in rng.standard_normal(nn)])
+        elif ptype == gen.BOOLEAN:
+            vals = bytes(int(x) for x in rng.integers(0, 256, (nn + 7) // 8))
+        else:
+            vals = B.plain_ba([bytes(rng.integers(97, 123, int(rng.integers(0, 25))).astype(np.uint8))
+                               for _ in range(nn)])
+        first, second = (rstream, dstream) if spec_order else (dstream, rstream)
+        if cut_after_def and k == npages - 1:
+            pay = B.levels_section(first) + b"\x01\x00"
+        else:
+            pay = (B.levels_section(first) + struct.pack("<I", len(second) + rep_len_delta) + second + vals)
+        pages.append(B.data_header(len(pay), n, enc) + pay)
+        total += n
+    return B.build_file(pages, ptype, optional, total, dict_at_start=dict_vals is not None, nested=nested)
+
+
+REP_DICT = [b"red", b"", b"green-green", b"blue", b"violet and more", b"k"]
+
 CRAFTED = {
+    # repeated columns (max_rep 1), R-LEVELS: definition levels then
+    # repetition levels in the reference's read order, over every value kind;
+    # LIST shape (max_def 3, bit width 2) and a REPEATED leaf (max_def 1);
+    # 20,000-row pages for the large-page kernels; spec-order pages (the
+    # reference reads the repetition section as definition levels)
+    "rep_list_dict": lambda: _rep_pages(gen.BYTE_ARRAY, "list", True, 700, 3, seed=91, enc=8, dict_vals=REP_DICT),
+    "rep_list_dict_big": lambda: _rep_pages(gen.BYTE_ARRAY, "list", True, 20000, 2, seed=92, enc=8,
+                                            dict_vals=REP_DICT),
+    "rep_list_int64": lambda: _rep_pages(gen.INT64, "list", True, 900, 3, seed=93),
+    "rep_list_int64_required": lambda: _rep_pages(gen.INT64, "list", False, 600, 2, seed=94),
+    "rep_list_double_big": lambda: _rep_pages(gen.DOUBLE, "list", True, 5000, 2, seed=95),
+    "rep_list_plain_ba": lambda: _rep_pages(gen.BYTE_ARRAY, "list", True, 800, 3, seed=96),
+    "rep_list_plain_ba_big": lambda: _rep_pages(gen.BYTE_ARRAY, "list", True, 6000, 2, seed=97),
+    "rep_repeated_plain_ba": lambda: _rep_pages(gen.BYTE_ARRAY, "repeated", False, 500, 3, seed=98),
+    "rep_repeated_dict": lambda: _rep_pages(gen.BYTE_ARRAY, "repeated", False, 1500, 2, seed=99, enc=8,
+                                            dict_vals=REP_DICT),
+    "rep_repeated_bool": lambda: _rep_pages(gen.BOOLEAN, "repeated", False, 700, 2, seed=100),
+    # (spec order with a dictionary needs equal level bit widths: a level above
+    # max_def on a dictionary page is undefined behaviour in the reference,
+    # indices[] read past num_non_null, column_reader.cpp:181-189)
+    "rep_spec_order_repeated_dict": lambda: _rep_pages(gen.BYTE_ARRAY, "repeated", False, 700, 2, seed=101, enc=8,
+                                                       dict_vals=REP_DICT, spec_order=True),
+    "rep_spec_order_list_plain_ba": lambda: _rep_pages(gen.BYTE_ARRAY, "list", True, 640, 3, seed=105,
+                                                       spec_order=True),
+
     # dictionary pages beyond LDS: short entries (the parallel slices link),
     # entries over 64 bytes (uncovered slice entries: the serial walk), bytes
     # after the declared entries, 17-bit indices
@@ -407,6 +489,13 @@ CRAFTED = {
 }
 
 ERRORS = {
+    # repeated columns: the repetition section's length runs past the page;
+    # the page ends before the repetition length word
+    "rep_len_overrun": lambda: _rep_pages(gen.INT64, "list", True, 300, 2, seed=103, rep_len_delta=100000),
+    "rep_len_missing": lambda: _rep_pages(gen.BYTE_ARRAY, "list", True, 300, 2, seed=104, enc=8,
+                                          dict_vals=REP_DICT, cut_after_def=True),
+    # spec order, LIST shape: more rows read as non-null than the page holds values
+    "rep_spec_order_int64_short": lambda: _rep_pages(gen.INT64, "list", True, 640, 2, seed=102, spec_order=True),
     # dictionary pages beyond LDS: a truncated last entry; more entries
     # declared than the page holds (the chain ends at the page end)
     "huge_dict_truncated": lambda: _huge_dict_file(30000, seed=86, cut=3),

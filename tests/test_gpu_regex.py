@@ -259,3 +259,42 @@ def test_string_index_not_filed_on_error(ctx):
             dc.regex_pages("special", False)
         assert ei.value.code == rc_o and ei.value.msg == msg_o
     dc.free()
+
+
+REP_BA = ["rep_list_dict", "rep_list_dict_big", "rep_list_plain_ba", "rep_list_plain_ba_big", "rep_repeated_plain_ba",
+          "rep_repeated_dict", "rep_spec_order_repeated_dict", "rep_spec_order_list_plain_ba"]
+
+
+@pytest.mark.parametrize("neg", [False, True], ids=["like", "notlike"])
+@pytest.mark.parametrize("case", REP_BA)
+def test_regex_repeated_columns(ctx, kernel, case, neg):
+    """Repeated BYTE_ARRAY columns (max_rep 1): every page kernel skips the
+    repetition section as the reference does (column_reader.cpp:156-164) and
+    reports the oracle's page set."""
+    import test_gpu_decode as D
+    f, ch = D.CRAFTED[case]()
+    dc = ctx.upload(f, [to_desc(ch)])
+    try:
+        for p in ("e", "^[a-g]", "re.*n", "zz", "x*"):
+            exp = golden_pages(f, [ch], p, neg)
+            got = dc.regex_pages(p, neg)
+            assert np.array_equal(got, exp), (case, p, neg, np.nonzero(got != exp)[0][:10])
+    finally:
+        dc.free()
+
+
+@pytest.mark.parametrize("case", ["rep_len_overrun", "rep_len_missing"])
+def test_regex_repeated_column_errors(ctx, kernel, case):
+    import test_gpu_decode as D
+    f, ch = D.ERRORS[case]()
+    rc_o, msg_o, _ = O.read_all(f, to_oracle_chunk(ch))
+    assert rc_o != 0
+    if ch["type"] != gen.BYTE_ARRAY:
+        pytest.skip("not a string column")
+    dc = ctx.upload(f, [to_desc(ch)])
+    try:
+        with pytest.raises(capi.PqError) as ei:
+            dc.regex_pages("e", False)
+        assert ei.value.code == rc_o and ei.value.msg == msg_o
+    finally:
+        dc.free()
