@@ -214,6 +214,28 @@ def pmc_traffic(path: str, kernel: str):
     return (k.get("hbm_bytes_per_launch") if k else None), d.get("source")
 
 
+def pmc_step_traffic(path: str, kern: dict):
+    """HBM bytes of one whole step: each step kernel's PMC bytes per launch
+    (a C2-only PMC summary, scripts/gpu_pmc_c2.sh) x its launches per step
+    (the bench's own HIP-event timers); None unless every timed kernel of
+    the step has a PMC figure taken on these kernel sources."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    if d.get("kernel_src_sha") != kernel_source_hash():
+        return None
+    pk = d.get("kernels", {})
+    total, parts = 0.0, {}
+    for name, v in kern.items():
+        e = next((pk[c] for c in (name, name + "3", name.replace("pipe_codes", "pipe_codes3")) if c in pk), None)
+        if not e or "hbm_bytes_per_launch" not in e:
+            return None
+        parts[name] = e["hbm_bytes_per_launch"] * v["launches_per_step"]
+        total += parts[name]
+    return {"bytes": total, "per_kernel": parts, "source": d.get("source")}
+
+
 def sha(b: bytes) -> str:
     return hashlib.sha256(b).hexdigest()
 
@@ -484,25 +506,40 @@ def c3_legs(J, args, exp):
     flags = rdc.regex_pages(args.pattern)
     rsteps = max(3, args.steps // 2)
     step = lambda: rdc.regex_pages_async(args.pattern)  # noqa: E731
+    npages = rdc.num_pages
+
+    def scan_stats(secs, kern):
+        med = statistics.median(secs)
+        k = next((k for k in ("regex_plain", "regex_lanes", "regex_pages") if k in kern), None)
+        kms = kern[k]["ms_per_launch"] if k else None
+        return {"pages_per_s": npages * rsteps * J.world / med, "ms_per_scan": med / rsteps * 1e3,
+                "repeats_ms": [x / rsteps * 1e3 for x in secs], "kernel": k, "kernel_ms": kms,
+                "payload_GBs": rdc.payload_bytes / (kms * 1e-3) / 1e9 if kms else None,
+                "roofline_frac": rdc.payload_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS if kms else None}
+    # the metric: a cold single scan, what --regex-column does once per file:
+    # option regex_index=2 makes every timed scan a first scan (walk the
+    # length chains and file the chunk's string index again)
+    J.ctx.set_option("regex_index", 2)
+    try:
+        cold = scan_stats(*J.timed(step, rdc.regex_pages_result, rsteps, args.repeats, warmup=max(1, args.warmup // 2),
+                                   kernels=REGEX_KERNELS))
+    finally:
+        J.ctx.set_option("regex_index", 1)
+    # warm: repeat scans of the same chunk read the index the first scan filed
     secs, kern = J.timed(step, rdc.regex_pages_result, rsteps, args.repeats, warmup=max(1, args.warmup // 2),
                          kernels=REGEX_KERNELS)
-    med = statistics.median(secs)
-    npages = rdc.num_pages
-    rkern = next((k for k in ("regex_plain", "regex_lanes", "regex_pages") if k in kern), None)
-    kms = kern[rkern]["ms_per_launch"] if rkern else None
+    warm = scan_stats(secs, kern)
+
     def check(fl, pat, neg):
         e = exp.get(f"c3|{rows}|rg{J.rank}|{pat}|{int(neg)}")
         ok = (sha(fl.astype("u1").tobytes()) == e["sha256"]) if e else None
         oks = J.gather(ok)
         return None if any(o is None for o in oks) else all(oks)
 
-    regex = {"pages_per_s": npages * rsteps * J.world / med, "pages_per_gpu": npages,
-             "ms_per_scan": med / rsteps * 1e3, "repeats_ms": [s / rsteps * 1e3 for s in secs],
-             "pattern": args.pattern, "reported_pages": int(flags.sum()),
+    regex = {**cold, "scan": "cold: every timed scan is a first scan (regex_index=2: chain walk + index filed)",
+             "pages_per_gpu": npages, "pattern": args.pattern, "reported_pages": int(flags.sum()),
              "validated": check(flags, args.pattern, False),
-             "kernel": rkern, "kernel_ms": kms,
-             "payload_GBs": rdc.payload_bytes / (kms * 1e-3) / 1e9 if kms else None,
-             "roofline_frac": rdc.payload_bytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS if kms else None}
+             "warm": {**warm, "scan": "warm: repeat scans read the string index the first scan filed"}}
     if not args.no_e2e and J.rank == 0:
         u, r = [], []
         J.ctx.timing(True)
@@ -530,12 +567,16 @@ def c3_legs(J, args, exp):
         for neg in (False, True):
             fl = rdc.regex_pages(pat, neg)
             st = lambda p=pat, n=neg: rdc.regex_pages_async(p, n)  # noqa: E731
-            secs, kern = J.timed(st, rdc.regex_pages_result, rsteps, 3, warmup=1, kernels=REGEX_KERNELS)
-            med = statistics.median(secs)
-            k = next((k for k in ("regex_plain", "regex_lanes", "regex_pages") if k in kern), None)
+            J.ctx.set_option("regex_index", 2)  # cold scans first, then warm (see above)
+            try:
+                c = scan_stats(*J.timed(st, rdc.regex_pages_result, rsteps, 3, warmup=1, kernels=REGEX_KERNELS))
+            finally:
+                J.ctx.set_option("regex_index", 1)
+            w = scan_stats(*J.timed(st, rdc.regex_pages_result, rsteps, 3, warmup=1, kernels=REGEX_KERNELS))
             sweep[f"{pat}{' (neg)' if neg else ''}"] = {
-                "pages_per_s": npages * rsteps * J.world / med, "ms_per_scan": med / rsteps * 1e3,
-                "kernel": k, "kernel_ms": kern[k]["ms_per_launch"] if k else None,
+                "pages_per_s": c["pages_per_s"], "ms_per_scan": c["ms_per_scan"], "kernel": c["kernel"],
+                "kernel_ms": c["kernel_ms"], "roofline_frac": c["roofline_frac"],
+                "warm": {k: w[k] for k in ("pages_per_s", "ms_per_scan", "kernel", "kernel_ms", "roofline_frac")},
                 "reported_pages": int(fl.sum()), "validated": check(fl, pat, neg)}
     regex["patterns"] = sweep
     regex["all_validated"] = all(v["validated"] for v in sweep.values()) and bool(regex["validated"])
@@ -924,6 +965,7 @@ def main():
                  "ba_fused": b_alg}.get(dom, payload)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(args.pmc_json, dom)
+    step_traffic = pmc_step_traffic(args.pmc_json, c2["kern"])
 
     result = {
         "metric": "decoded values/sec (RLE+dict BYTE_ARRAY) and regex pages/sec at 1/2/4/8 GPUs",
@@ -947,7 +989,10 @@ def main():
         "validated": c2["validated"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                     "kernel": dom, "kernel_ms": dom_ms, "algorithmic_bytes": dom_bytes},
+                     "kernel": dom, "kernel_ms": dom_ms, "algorithmic_bytes": dom_bytes,
+                     "step_traffic": step_traffic["bytes"] if step_traffic else None,
+                     "step_traffic_over_b_alg": step_traffic["bytes"] / b_alg if step_traffic else None,
+                     "step_traffic_per_kernel": step_traffic["per_kernel"] if step_traffic else None},
         "pipeline": {"kernel_ms": kern,
                      "kernel_ms_note": "HIP events on the decode streams, same steps repeated after the timed "
                                        "regions (events perturb the wall clock)",

@@ -107,7 +107,8 @@ struct pq_ctx {
     bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
     bool opt_regex_codes = true; // "regex_codes": dictionary chunks on the pipe path: match bits over the decode's codes
     bool opt_regex_reuse = true; // "regex_reuse": ... reusing the codes of an earlier checked decode of the chunk
-    bool opt_regex_index = true; // "regex_index": REQUIRED PLAIN chunks keep the string index of their first scan
+    int opt_regex_index = 1;     // "regex_index": REQUIRED PLAIN chunks keep the string index of their first scan;
+                                 // 2: every scan is a first scan (files the index again: the cold-scan timing)
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
     int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
@@ -874,7 +875,11 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "regex_plain") == 0) { ctx->opt_regex_plain = value != 0; return 0; }
     if (std::strcmp(key, "regex_codes") == 0) { ctx->opt_regex_codes = value != 0; return 0; }
     if (std::strcmp(key, "regex_reuse") == 0) { ctx->opt_regex_reuse = value != 0; return 0; }
-    if (std::strcmp(key, "regex_index") == 0) { ctx->opt_regex_index = value != 0; return 0; }
+    if (std::strcmp(key, "regex_index") == 0) {
+        if (value < 0 || value > 2) return set_err(ctx, PQ_ERR_ARG, "regex_index: 0, 1 or 2");
+        ctx->opt_regex_index = static_cast<int>(value);
+        return 0;
+    }
     if (std::strcmp(key, "zflip") == 0) { ctx->opt_zflip = value != 0; return 0; }
     if (std::strcmp(key, "write_waves") == 0) {
         if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "write_waves: 1..16");
@@ -2585,7 +2590,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             const uint16_t* idx_in = nullptr;
             uint16_t* idx_out = nullptr;
             if (ctx->opt_regex_index && c->max_def == 0 && c->max_rep == 0 && c->nrows > 0 && !ctx->opt_regex_debug) {
-                if (c->rx_index_ok && c->rx_index_win == c->rwin_bytes) {
+                if (c->rx_index_ok && c->rx_index_win == c->rwin_bytes && ctx->opt_regex_index != 2) {
                     idx_in = c->d_rx_index;
                 } else {
                     c->rx_index_ok = false;

@@ -619,10 +619,14 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
             const uint32_t nd = skip ? 0u : (inf & 0xFFu), ni = skip ? 0u : ((inf >> 8) & 0xFFu);
             // every load from an in-bounds index (the page's 2 x kPipeRunCap
             // record block; blocks of its payload slot), selected after
+            // (indices clamped to the page's record counts: lanes past them read
+            // the last record's line again, not the block's unwritten slots, so
+            // a page costs its records' lines, not 2 x kPipeRunCap x 8 bytes)
             const uint2* rd_ = a.runs + static_cast<size_t>(pp) * 2 * kPipeRunCap;
             const uint2 z = make_uint2(0u, 0u);
-            const uint2 r0 = rd_[lane()], r1 = rd_[lane() + kWave];
-            const uint2 r2 = rd_[kPipeRunCap + lane()], r3 = rd_[kPipeRunCap + lane() + kWave];
+            const uint32_t nd1 = nd ? nd - 1 : 0u, ni1 = ni ? ni - 1 : 0u;
+            const uint2 r0 = rd_[min(lane(), nd1)], r1 = rd_[min(lane() + kWave, nd1)];
+            const uint2 r2 = rd_[kPipeRunCap + min(lane(), ni1)], r3 = rd_[kPipeRunCap + min(lane() + kWave, ni1)];
             rq0 = lane() < nd ? r0 : z;
             rq1 = lane() + kWave < nd ? r1 : z;
             rq2 = lane() < ni ? r2 : z;

@@ -610,7 +610,7 @@ def test_plain_spec_no_fallback(ctx, case):
 
 
 @pytest.mark.parametrize("key,value", [("write_waves", 0), ("write_waves", 17), ("pipe_run_pages", 33),
-                                       ("regex_win", 1000), ("fused_claim", 0), ("no_such_option", 1)])
+                                       ("regex_win", 1000), ("fused_claim", 0), ("regex_index", 3), ("no_such_option", 1)])
 def test_set_option_rejects(ctx, key, value):
     """Out-of-range tuning values and unknown keys fail with PQ_ERR_ARG and
     leave the setting alone."""

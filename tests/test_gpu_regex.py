@@ -234,7 +234,7 @@ def test_string_index_reuse(ctx, layout, rpp):
     try:
         for win in (8192, 4096, 8192):
             ctx.set_option("regex_win", win)
-            for idx in (1, 0, 1):
+            for idx in (1, 0, 2, 1):  # 2: every scan files the index again (cold)
                 ctx.set_option("regex_index", idx)
                 for p in pats:
                     for n in (False, True):
