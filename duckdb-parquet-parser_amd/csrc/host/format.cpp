@@ -165,18 +165,32 @@ void skip_key_value(Thrift& t) {  // metadata.cpp:184-194
     }
 }
 
-int skip_subtree(const FileMeta& fm, int idx) {  // parquet_reader.cpp:545-557
+// The schema is a pre-order list whose groups give their child counts.  The
+// reference walks it without bounds (skip_schema_subtree reads past the list
+// when a count overstates the elements left: undefined behaviour); here a
+// count that runs past the list, or nesting deeper than kMaxSchemaDepth, is
+// an error (fuzz_host found the unbounded read).
+constexpr int kMaxSchemaDepth = 1000;
+[[noreturn]] void schema_error() {
+    throw Error(PQ_ERR_UNSUPPORTED, "schema: a group's num_children runs past the schema list");
+}
+
+int skip_subtree(const FileMeta& fm, int idx, int depth) {  // parquet_reader.cpp:545-557
+    const int n = static_cast<int>(fm.schema.size());
+    if (idx >= n || depth > kMaxSchemaDepth) schema_error();
     int children = fm.schema[idx].num_children.value_or(0);
     idx++;
     for (int i = 0; i < children; i++) {
-        if (fm.schema[idx].num_children.value_or(0) > 0) idx = skip_subtree(fm, idx);
+        if (idx >= n) schema_error();
+        if (fm.schema[idx].num_children.value_or(0) > 0) idx = skip_subtree(fm, idx, depth + 1);
         else idx++;
     }
     return idx;
 }
 
 void build_leaves(const FileMeta& fm, int idx, int end, int16_t def, int16_t rep, int& col,
-                  std::vector<LeafColumn>& out) {  // parquet_reader.cpp:495-543
+                  std::vector<LeafColumn>& out, int depth = 0) {  // parquet_reader.cpp:495-543
+    if (depth > kMaxSchemaDepth) schema_error();
     while (idx < end) {
         const SchemaElement& e = fm.schema[idx];
         int16_t d = def, r = rep;
@@ -190,10 +204,10 @@ void build_leaves(const FileMeta& fm, int idx, int end, int16_t def, int16_t rep
             int i = idx, remaining = children;
             while (remaining > 0 && i < end) {
                 remaining--;
-                if (fm.schema[i].num_children.value_or(0) > 0) i = skip_subtree(fm, i);
+                if (fm.schema[i].num_children.value_or(0) > 0) i = skip_subtree(fm, i, depth + 1);
                 else i++;
             }
-            build_leaves(fm, idx, i, d, r, col, out);
+            build_leaves(fm, idx, i, d, r, col, out, depth + 1);
             idx = i;
         } else {
             LeafColumn lc;
@@ -983,6 +997,11 @@ std::vector<std::array<int64_t, 4>> page_index(const uint8_t* file, size_t len, 
                     throw Error(PQ_ERR_UNSUPPORTED, "page walk ran past end of file");
                 PageHeader h = header_at(file, len, cur);
                 cur += h.header_size;
+                // a negative size steps the reference's walk backwards (it never
+                // ends); chunks a corrupt footer overlays could list the file's
+                // bytes many times over: both are errors here
+                if (h.compressed < 0) throw Error(PQ_ERR_UNSUPPORTED, "page walk: negative compressed_page_size");
+                if (out.size() > len) throw Error(PQ_ERR_UNSUPPORTED, "page index: more pages than the file has bytes");
                 if (h.type == PQ_DATA_PAGE || h.type == PQ_DATA_PAGE_V2) {
                     out.push_back({static_cast<int64_t>(cur), static_cast<int64_t>(static_cast<size_t>(h.compressed)),
                                    static_cast<int64_t>(rg), static_cast<int64_t>(col)});
