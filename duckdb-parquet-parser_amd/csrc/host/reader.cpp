@@ -102,6 +102,44 @@ HostColumn decode_range(Device& dev, const uint8_t* file, size_t len, const pq_c
     return h;
 }
 
+// Shard b..e of one chunk on `dev`: the page filter's flags of its data pages
+// (`pattern` set), the decoded column (`col` set), or both in one call.
+void scan_range(Device& dev, const uint8_t* file, size_t len, const pq_chunk_desc& desc,
+                const std::vector<pq_page_desc>& table, int64_t b, int64_t e, const std::string* pattern, bool neg,
+                HostColumn* col, std::vector<uint8_t>* flags) {
+    pq_ctx* ctx = dev.ctx();
+    pq_chunk* ch = nullptr;
+    int rc = pq_chunk_upload_range(ctx, file, len, &desc, table.data(), static_cast<int64_t>(table.size()), b, e, &ch);
+    if (rc) raise(rc, pq_last_error(ctx));
+    pq_column out{};
+    auto fail = [&](int code) {
+        std::string msg = pq_last_error(ctx);
+        pq_column_free(ctx, &out);
+        pq_chunk_free(ctx, ch);
+        raise(code, msg);
+    };
+    flags->assign(static_cast<size_t>(std::max<int64_t>(pq_chunk_num_pages(ch), 1)), 0);
+    if (col) {
+        if ((rc = pq_decode_regex_async(ctx, ch, &out, pattern->c_str(), neg ? 1 : 0))) fail(rc);
+        if ((rc = pq_regex_pages_result(ctx, ch, flags->data()))) fail(rc);
+        if ((rc = pq_decode_check(ctx, ch))) fail(rc);
+        col->type = static_cast<ParquetType>(desc.type);
+        col->num_rows = out.num_rows;
+        col->validity.assign(static_cast<size_t>((out.num_rows + 31) / 32) + 1, 0);
+        col->values.assign(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)), 0);
+        if (desc.type == PQ_BYTE_ARRAY) col->offsets.assign(static_cast<size_t>(out.num_rows + 1), 0);
+        rc = pq_column_copy_out(ctx, &out, col->validity.data(), col->values.data(),
+                                col->offsets.empty() ? nullptr : col->offsets.data());
+        col->values.resize(static_cast<size_t>(out.num_bytes));
+        if (rc) fail(rc);
+    } else if ((rc = pq_regex_pages(ctx, ch, pattern->c_str(), neg ? 1 : 0, flags->data()))) {
+        fail(rc);
+    }
+    flags->resize(static_cast<size_t>(pq_chunk_num_pages(ch)));
+    pq_column_free(ctx, &out);
+    pq_chunk_free(ctx, ch);
+}
+
 // a followed by b (rows, validity bits, values; offsets rebased)
 void append_column(HostColumn& a, const HostColumn& b) {
     const int64_t n0 = a.num_rows, n = n0 + b.num_rows;
@@ -592,20 +630,131 @@ std::vector<size_t> ParquetReader::regex_pages(const std::string& name, const st
     pq_chunk_pages(ch, walked.data(), nw, &nw);
     pq_chunk_free(ctx, ch);
     if (rc) raise(rc, msg);
-    // device data page k <-> the k-th DATA_PAGE of the walk <-> its global id
+    std::vector<int64_t> offs;
+    for (const auto& p : walked)
+        if (p.page_type == PQ_DATA_PAGE) offs.push_back(p.payload_offset);
+    return flagged_page_ids(c, offs, flags);
+}
+
+std::vector<size_t> ParquetReader::regex_pages(const std::string& name, const std::string& pattern, bool neg,
+                                               const std::vector<Device*>& devices) {
+    int c = find_column(name);
+    if (c < 0) throw std::runtime_error("Column not found: " + name);
+    if (devices.size() <= 1 || num_row_groups() == 0) return regex_pages(name, pattern, neg);
+    std::vector<size_t> ids;
+    bool walk_failed = false;
+    sharded_scan(c, pattern, neg, devices, false, &ids, &walk_failed);
+    if (walk_failed) return regex_pages(name, pattern, neg);
+    return ids;
+}
+
+HostColumn ParquetReader::read_column_regex(const std::string& name, const std::string& pattern, bool neg,
+                                            const std::vector<Device*>& devices, std::vector<size_t>* page_ids) {
+    int c = find_column(name);
+    if (c < 0) throw std::runtime_error("Column not found: " + name);
+    if (columns_[static_cast<size_t>(c)].type != ParquetType::BYTE_ARRAY)
+        throw std::runtime_error("regex page filter needs a BYTE_ARRAY column");
+    std::vector<size_t> ids;
+    HostColumn out;
+    bool walk_failed = devices.empty() || num_row_groups() == 0;
+    if (!walk_failed) out = sharded_scan(c, pattern, neg, devices, true, &ids, &walk_failed);
+    if (walk_failed) {  // the one-device calls report the walk's error the reference's way
+        out = read_column_columnar(name);
+        ids = regex_pages(name, pattern, neg);
+    }
+    if (page_ids) *page_ids = std::move(ids);
+    return out;
+}
+
+std::vector<size_t> ParquetReader::flagged_page_ids(int col_idx, const std::vector<int64_t>& data_offsets,
+                                                    const std::vector<uint8_t>& flags) const {
+    // device data page k <-> the k-th DATA_PAGE of the walks <-> its global id
     std::vector<size_t> out;
     size_t k = 0, gid = 0;
-    const int chunk_col = columns_[c].column_index;
+    const int chunk_col = columns_[static_cast<size_t>(col_idx)].column_index;
     std::vector<size_t> ids;
     for (size_t i = 0; i < page_index_.size(); i++)
         if (static_cast<int>(page_index_[i].column_idx) == chunk_col) ids.push_back(i);
-    for (const auto& p : walked) {
-        if (p.page_type != PQ_DATA_PAGE) continue;
-        while (gid < ids.size() && page_index_[ids[gid]].data_offset != static_cast<size_t>(p.payload_offset)) gid++;
-        if (gid < ids.size() && flags[k]) out.push_back(ids[gid]);
+    for (const int64_t off : data_offsets) {
+        while (gid < ids.size() && page_index_[ids[gid]].data_offset != static_cast<size_t>(off)) gid++;
+        if (gid < ids.size() && k < flags.size() && flags[k]) out.push_back(ids[gid]);
         k++;
         gid++;
     }
+    return out;
+}
+
+HostColumn ParquetReader::sharded_scan(int c, const std::string& pattern, bool neg, const std::vector<Device*>& devices,
+                                       bool want_col, std::vector<size_t>* page_ids, bool* walk_failed) {
+    *walk_failed = false;
+    const int nrg = static_cast<int>(num_row_groups());
+    const int D = static_cast<int>(devices.size());
+    std::vector<pq_chunk_desc> descs(static_cast<size_t>(nrg));
+    std::vector<std::vector<pq_page_desc>> tables(static_cast<size_t>(nrg));
+    std::vector<std::vector<int64_t>> plans(static_cast<size_t>(nrg), std::vector<int64_t>(2 * static_cast<size_t>(D)));
+    for (int rg = 0; rg < nrg; rg++) {
+        pq_chunk_desc& d = descs[static_cast<size_t>(rg)];
+        int rc = pq_file_chunk(file_, rg, c, &d);
+        if (rc) raise(rc, "ColumnChunk has no metadata");
+        std::vector<pq_page_desc>& t = tables[static_cast<size_t>(rg)];
+        int64_t n = 0;
+        t.resize(1024);
+        for (;;) {
+            rc = pq_build_page_table(data_.data(), data_.size(), &d, t.data(), static_cast<int64_t>(t.size()), &n,
+                                     nullptr, 0);
+            if (n <= static_cast<int64_t>(t.size())) break;
+            t.resize(static_cast<size_t>(n));
+        }
+        t.resize(static_cast<size_t>(n));
+        if (rc) {  // a walk error: the caller takes the one-device path (the reference's error)
+            *walk_failed = true;
+            return HostColumn{};
+        }
+        pq_plan_page_ranges(t.data(), n, D, plans[static_cast<size_t>(rg)].data());
+    }
+    std::vector<std::vector<HostColumn>> parts(static_cast<size_t>(D), std::vector<HostColumn>(static_cast<size_t>(nrg)));
+    std::vector<std::vector<std::vector<uint8_t>>> fl(static_cast<size_t>(D),
+                                                      std::vector<std::vector<uint8_t>>(static_cast<size_t>(nrg)));
+    std::vector<std::exception_ptr> errs(static_cast<size_t>(D) * static_cast<size_t>(nrg));
+    std::vector<std::thread> th;
+    for (int k = 0; k < D; k++) {
+        th.emplace_back([&, k]() {
+            for (int rg = 0; rg < nrg; rg++) {
+                const auto& pl = plans[static_cast<size_t>(rg)];
+                try {
+                    scan_range(*devices[static_cast<size_t>(k)], data_.data(), data_.size(), descs[static_cast<size_t>(rg)],
+                               tables[static_cast<size_t>(rg)], pl[2 * static_cast<size_t>(k)],
+                               pl[2 * static_cast<size_t>(k) + 1], &pattern, neg,
+                               want_col ? &parts[static_cast<size_t>(k)][static_cast<size_t>(rg)] : nullptr,
+                               &fl[static_cast<size_t>(k)][static_cast<size_t>(rg)]);
+                } catch (...) {
+                    errs[static_cast<size_t>(rg) * D + k] = std::current_exception();
+                    return;  // (later row groups of this device are never reached by the reference)
+                }
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    for (auto& e : errs)  // the first error in page order (row group, then shard)
+        if (e) std::rethrow_exception(e);
+    std::vector<uint8_t> flags;
+    for (int rg = 0; rg < nrg; rg++)
+        for (int k = 0; k < D; k++) {
+            const auto& f = fl[static_cast<size_t>(k)][static_cast<size_t>(rg)];
+            flags.insert(flags.end(), f.begin(), f.end());
+        }
+    std::vector<int64_t> offs;
+    for (const auto& t : tables)
+        for (const auto& p : t)
+            if (p.page_type == PQ_DATA_PAGE) offs.push_back(p.payload_offset);
+    *page_ids = flagged_page_ids(c, offs, flags);
+    HostColumn out;
+    out.type = columns_[static_cast<size_t>(c)].type;
+    if (!want_col) return out;
+    for (int rg = 0; rg < nrg; rg++)
+        for (int k = 0; k < D; k++) append_column(out, parts[static_cast<size_t>(k)][static_cast<size_t>(rg)]);
+    if (out.type == ParquetType::BYTE_ARRAY && out.offsets.empty()) out.offsets.push_back(0);
+    out.validity.resize(static_cast<size_t>((out.num_rows + 31) / 32) + 1, 0);
     return out;
 }
 

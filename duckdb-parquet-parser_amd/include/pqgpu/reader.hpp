@@ -216,10 +216,31 @@ public:
     // pages with no value matching `pattern` (neg: no value failing it).
     std::vector<size_t> regex_pages(const std::string& col_name, const std::string& pattern,
                                     bool neg = false);
+    // The same page filter sharded over devices: each row group's
+    // chunk cut into byte-balanced data-page ranges (pq_plan_page_ranges), one
+    // host thread per device uploading its ranges (pq_chunk_upload_range) and
+    // scanning them; the per-shard page flags are concatenated in page order
+    // (no collective).  Same ids and the same first error as the one-device call.
+    std::vector<size_t> regex_pages(const std::string& col_name, const std::string& pattern, bool neg,
+                                    const std::vector<Device*>& devices);
+    // Decode and page filter in one call per shard (pq_decode_regex_async: one
+    // pass over dictionary pages when the pipe takes the chunk): the column as
+    // read_column_columnar(col_name, devices) returns it, and the page ids as
+    // regex_pages returns them.
+    HostColumn read_column_regex(const std::string& col_name, const std::string& pattern, bool neg,
+                                 const std::vector<Device*>& devices, std::vector<size_t>* page_ids);
 
 private:
     HostColumn decode_column(int col_idx, int rg_first, int rg_count);
     HostColumn decode_column_on(Device& dev, int col_idx);
+    // page ids of column col_idx's data pages flagged in `flags`: data_offsets
+    // holds the payload offset of every data page, in walk order
+    std::vector<size_t> flagged_page_ids(int col_idx, const std::vector<int64_t>& data_offsets,
+                                         const std::vector<uint8_t>& flags) const;
+    // one call per device over every row group's range of the column: regex
+    // (decode: also the column) of the shards, joined in page order
+    HostColumn sharded_scan(int col_idx, const std::string& pattern, bool neg, const std::vector<Device*>& devices,
+                            bool want_col, std::vector<size_t>* page_ids, bool* walk_failed);
     Device& dev_;
     std::vector<uint8_t> data_;
     pq_file* file_ = nullptr;

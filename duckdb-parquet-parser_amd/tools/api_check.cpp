@@ -8,6 +8,11 @@
 //   api_check <file> iterator <name>               StringColumnIterator (pos, len, bytes)
 //   api_check <file> sharded <name> <k>            read_column over k Devices (device i % count),
 //                                                  one host thread each
+//   api_check <file> regex_sharded <name> <k> <pattern> <neg>
+//                                                  regex_pages over k Devices: page ids, one per line
+//   api_check <file> decode_regex_sharded <name> <k> <pattern> <neg>
+//                                                  read_column_regex over k Devices: the column's
+//                                                  dump on stdout, the page ids on stderr
 #include <cstdio>
 #include <cstring>
 #include <iostream>
@@ -45,7 +50,7 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> out;
         if (mode == "read_column") {
             for (const auto& v : r.read_column(argv[3])) dump(v, out);
-        } else if (mode == "sharded") {
+        } else if (mode == "sharded" || mode == "regex_sharded" || mode == "decode_regex_sharded") {
             int k = argc > 4 ? std::atoi(argv[4]) : 2;
             int nd = pqgpu::Device::count();
             if (nd < 1) throw std::runtime_error("no HIP device");
@@ -55,7 +60,25 @@ int main(int argc, char** argv) {
                 own.emplace_back(new pqgpu::Device(i % nd));
                 devs.push_back(own.back().get());
             }
-            for (const auto& v : r.read_column(argv[3], devs)) dump(v, out);
+            if (mode == "sharded") {
+                for (const auto& v : r.read_column(argv[3], devs)) dump(v, out);
+            } else {
+                if (argc < 7) return 2;
+                const std::string pat = argv[5];
+                const bool neg = std::atoi(argv[6]) != 0;
+                std::vector<size_t> ids;
+                if (mode == "regex_sharded") {
+                    ids = r.regex_pages(argv[3], pat, neg, devs);
+                    for (size_t id : ids) {
+                        const std::string ln = std::to_string(id) + "\n";
+                        out.insert(out.end(), ln.begin(), ln.end());
+                    }
+                } else {
+                    pqgpu::HostColumn h = r.read_column_regex(argv[3], pat, neg, devs, &ids);
+                    for (int64_t i = 0; i < h.num_rows; i++) dump(h.value(i), out);
+                    for (size_t id : ids) std::fprintf(stderr, "%zu\n", id);
+                }
+            }
         } else if (mode == "iterator") {
             auto it = r.column_iterator(argv[3]);
             while (it.has_next()) {

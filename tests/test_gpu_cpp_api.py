@@ -151,3 +151,83 @@ def test_read_column_sharded_c2(tmp_path):
     r = run("api_check", path, "sharded", cols[0].name, "4")
     assert r.returncode == 0, r.stderr
     assert r.stdout == gen.values_dump(cols[0], 0, n, 0, gen.CONFIG_SEEDS["C2"])
+
+
+def _oracle_page_ids(f, col, pat, neg):
+    """Global page ids (page index order) of column `col`'s data pages with no
+    satisfying non-null value (README.md:54-64), from the oracle's decode."""
+    F = capi.File(f)
+    pidx = F.page_index()
+    rx = re.compile(pat, re.ASCII)
+    ids = [i for i in range(len(pidx)) if pidx[i][3] == col]
+    out, k = [], 0
+    for rg in range(F.num_row_groups):
+        rc, msg, c = O.read_all(f, to_oracle_chunk(F.chunk(rg, col)))
+        assert rc == 0, msg
+        for (_, pt, _, first, nrows) in c.pages:
+            if pt != 0:
+                continue
+            sat = any((rx.search(bytes(c.data[c.offsets[r]:c.offsets[r + 1]]).decode()) is not None) != neg
+                      for r in range(first, first + nrows) if c.valid[r])
+            if not sat:
+                out.append(ids[k])
+            k += 1
+    return out
+
+
+@pytest.mark.parametrize("k", [1, 2, 3])
+@pytest.mark.parametrize("case", ["c2_ref", "c2_arrow", "c3_ref", "c4_dict", "c4_plain"])
+def test_regex_pages_sharded_over_devices(tmp_path, case, k):
+    """ParquetReader::regex_pages(name, pattern, neg, devices) and
+    read_column_regex (decode + page filter per shard in one call): the page
+    ids of the one-device filter / the oracle, the column of read_column, with
+    every row group's chunk cut into k page ranges, one host thread per
+    Device (k contexts on the box's GPU(s))."""
+    if case.startswith("c2"):
+        cols, n, rgs = gen.c2_cols(), 40000, 2
+        f = gen.build(cols, n, rgs, seed=41, layout=gen.ARROW_LAYOUT if case == "c2_arrow" else gen.REF_LAYOUT,
+                      rows_per_page=3000 if case == "c2_arrow" else 0)
+        col, pats = 0, ["^qx", "e", "^[a-m]"]
+    elif case == "c3_ref":
+        cols = gen.c3_cols()
+        f = gen.build(cols, 9000, 3, seed=42)
+        col, pats = 0, ["special.*requests", "^(carefully|quickly) ", "e"]
+    else:
+        cols = gen.c4_cols()
+        f = gen.build(cols, 4000, 2, seed=43, layout=gen.ARROW_LAYOUT, rows_per_page=700)
+        col, pats = (6 if case == "c4_dict" else 7), ["^[a-d]", "e", "ly"]
+    path = str(tmp_path / f"{case}.parquet")
+    with open(path, "wb") as fh:
+        fh.write(f)
+    name = cols[col].name
+    d_o = oracle_read_column(f, file_chunks(f, col))[2]
+    for pat in pats:
+        for neg in (False, True):
+            exp = _oracle_page_ids(f, col, pat, neg)
+            r = run("api_check", path, "regex_sharded", name, str(k), pat, str(int(neg)))
+            assert r.returncode == 0, r.stderr
+            assert [int(x) for x in r.stdout.split()] == exp, (pat, neg)
+            r = run("api_check", path, "decode_regex_sharded", name, str(k), pat, str(int(neg)))
+            assert r.returncode == 0, r.stderr
+            assert r.stdout == d_o, (pat, neg)
+            assert [int(x) for x in r.stderr.split()] == exp, (pat, neg)
+
+
+@pytest.mark.parametrize("mode", ["regex_sharded", "decode_regex_sharded"])
+def test_regex_sharded_error_matches(tmp_path, mode):
+    """A page that cannot be decoded: the sharded filter reports the
+    reference's first error, as the one-device call does."""
+    good = B.plain_ba([b"special requests", b"quick"] * 20)
+    bad = struct.pack("<I", 7) + b"special" + struct.pack("<I", 50) + b"xy"
+    pages = [B.data_header(len(good), 40, 0) + good] * 3 + [B.data_header(len(bad), 2, 0) + bad] + \
+            [B.data_header(len(good), 40, 0) + good] * 2
+    f, ch = B.build_file(pages, gen.BYTE_ARRAY, False, 202)
+    path = str(tmp_path / "bad.parquet")
+    with open(path, "wb") as fh:
+        fh.write(f)
+    rc, msg, _ = oracle_read_column(f, [ch])
+    assert rc != 0
+    for k in (1, 2, 3):
+        r = run("api_check", path, mode, "c", str(k), "special", "0")
+        assert r.returncode == 1, (k, r.stderr)
+        assert r.stderr.decode().strip().splitlines()[-1] == msg, k
