@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
                                                               uint2* __restrict__ runs,
                                                               uint32_t* __restrict__ info, int ppw,
                                                               int32_t* __restrict__ flist, uint32_t stage_max,
-                                                              RunDictArgs d) {
+                                                              RunDictArgs d, int debug) {
     __shared__ __attribute__((aligned(16))) uint32_t stage_all[kRunWaves][kRunStage / 4 + 8];
     if (static_cast<int>(blockIdx.x) < d.ndicts) {
         // leading workgroups: the chunk's dictionary pages (dict_index.hpp),
@@ -131,6 +131,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (debug & (1 << 26)) return;  // timing ablation: staging only (outputs invalid)
 
     const uint32_t s = lane() & 1;
     const int p = g0 + static_cast<int>(lane() >> 1);
@@ -2164,7 +2165,7 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
-                      int, const RunDicts* dicts) {
+                      int debug, const RunDicts* dicts) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     const int nd = dicts ? dicts->ndicts : 0;
     if (npages <= 0 && nd <= 0) return;
@@ -2174,7 +2175,7 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
                                               dicts->err_any}
                                 : RunDictArgs{nullptr, 0, nullptr, nullptr, nullptr, nullptr};
     hipLaunchKernelGGL(k_pipe_runs, dim3(nd + (max(npages, 0) + per - 1) / per), dim3(kRunWaves * kWave), 0, s,
-                       bytes, pages, npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16, d);
+                       bytes, pages, npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16, d, debug);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's
