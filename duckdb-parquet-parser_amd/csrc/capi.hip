@@ -122,6 +122,8 @@ struct pq_ctx {
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
     bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
     bool opt_front = false;      // "pipe_front": windowed one-wave front (k_pipe_front) where the pages allow it
+    bool opt_pfused = false;     // "pipe_fused": codes + write in one pass (k_pipe_fused), planned at upload
+    int opt_fused_waves = 8;     // "pipe_fused_waves": k_pipe_fused waves per workgroup (1..16), set before upload
     int opt_write_bpc = 0;       // "write_bpc": cap on k_pipe_write workgroups per CU (0: as many as fit; set before upload)
     int opt_stage_bufs = 6;      // "stage_bufs" / "stage_piece_kb": pinned upload ring (stage.hpp)
 };
@@ -200,7 +202,13 @@ struct pq_chunk {
     int32_t* d_bigp = nullptr;
     uint32_t big_max_bytes = 0;
     int32_t pipe_entry_base = 0;        // entry-table slot of the pipe dictionary's first entry
-    uint8_t* d_zero = nullptr;          // pipe chunks: two blocks of [flags][bsum][flist], alternating per decode
+    // k_pipe_fused, planned at upload when the context asks for it
+    bool fused_ok = false;
+    uint32_t fstage = 0, flds = 0;
+    int fgrid = 0, fwaves = 0;
+    int32_t nunits = 0;
+    size_t z_bsum = 0, z_fused = 0, z_flist = 0;  // offsets in a zero block: bsum, fused ticket + look-back words, flist
+    uint8_t* d_zero = nullptr;          // pipe chunks: two blocks of [flags][bsum][fused][flist], alternating per decode
     size_t zfull = 0;                   // bytes per block
     int zsel = 0;                       // block of the current decode
     bool next_zeroed = false;           // the other block is clear (the last k_pipe_write cleared it)
@@ -527,6 +535,19 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     c->pipe_ecap = static_cast<uint32_t>(ecap);
     c->pipe_cus = cus;
     c->pipe_wpw = wpw;
+    c->fused_ok = false;
+    if (ctx->opt_pfused) {  // codes + write in one pass: the largest small page's slot as the stage
+        const uint32_t stage = std::min<uint32_t>(5120u, (small_bytes + 15) / 16 * 16 + 16);
+        const int fw = std::max(1, std::min(16, ctx->opt_fused_waves));
+        const pqk::PipePlan fp = pqk::plan_pipe_fused(dict_bytes, fw, stage);
+        if (fp.blocks_per_cu > 0) {
+            c->fused_ok = true;
+            c->fstage = stage;
+            c->flds = fp.lds;
+            c->fgrid = cus * fp.blocks_per_cu;
+            c->fwaves = fw;
+        }
+    }
     // windows of consecutive pages for the whole front in one wavefront each (k_pipe_front)
     c->hfwins.clear();
     c->pipe_fr = small && !multi && c->hbig.empty() && pqk::pipe_front_slot(small_bytes) <= pqk::kFrontWin;
@@ -894,6 +915,12 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "plain_fused") == 0) { ctx->opt_plain_fused = value != 0; return 0; }
     if (std::strcmp(key, "pipe_run_dict") == 0) { ctx->opt_run_dict = value != 0; return 0; }
     if (std::strcmp(key, "pipe_front") == 0) { ctx->opt_front = value != 0; return 0; }
+    if (std::strcmp(key, "pipe_fused") == 0) { ctx->opt_pfused = value != 0; return 0; }
+    if (std::strcmp(key, "pipe_fused_waves") == 0) {
+        if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "pipe_fused_waves: 1..16");
+        ctx->opt_fused_waves = static_cast<int>(value);
+        return 0;
+    }
     if (std::strcmp(key, "write_bpc") == 0) {
         if (value < 0 || value > 4) return set_err(ctx, PQ_ERR_ARG, "write_bpc: 0..4");
         ctx->opt_write_bpc = static_cast<int>(value);
@@ -1398,21 +1425,25 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         rc |= dalloc(&c->d_dict_count, hdicts.size());
         rc |= dalloc(&c->d_page_err, hpages.size());
         rc |= dalloc(&c->d_dict_err, hdicts.size());
-        if (c->pipe) {  // flags | bsum | flist, cleared together
+        if (c->pipe) {  // flags | bsum | fused ticket + look-back words | flist, cleared together
             const size_t fb = 4 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long);
-            // cleared per decode: a multiple of 16 bytes (an odd size takes
-            // a second fill kernel for the tail)
-            const size_t zb = (fb + bb + sizeof(int32_t) + 15) / 16 * 16;
+            c->nunits = c->fused_ok ? (c->ntiles + pqk::pipe_fused_tiles() - 1) / pqk::pipe_fused_tiles() : 0;
+            c->z_bsum = fb;
+            c->z_fused = (fb + bb + 15) / 16 * 16;
+            c->z_flist = c->z_fused + (c->fused_ok ? 16 + static_cast<size_t>(c->nunits) * sizeof(unsigned long long) : 0);
+            // cleared per decode (through flist[0]): a multiple of 16 bytes (an
+            // odd size takes a second fill kernel for the tail)
+            const size_t zb = (c->z_flist + sizeof(int32_t) + 15) / 16 * 16;
             // two such blocks: a decode uses one while its k_pipe_write clears
             // the other for the next decode (no fill kernel per decode)
-            const size_t zfull = (std::max(zb, fb + bb + (hpages.size() + 1) * sizeof(int32_t)) + 255) / 256 * 256;
+            const size_t zfull = (std::max(zb, c->z_flist + (hpages.size() + 1) * sizeof(int32_t)) + 255) / 256 * 256;
             rc |= dalloc(&c->d_zero, 2 * zfull);
             if (c->d_zero) {
                 c->zfull = zfull;
                 c->zsel = 0;
                 c->d_flags = reinterpret_cast<int32_t*>(c->d_zero);
-                c->d_bsum = reinterpret_cast<unsigned long long*>(c->d_zero + fb);
-                c->d_flist = reinterpret_cast<int32_t*>(c->d_zero + fb + bb);
+                c->d_bsum = reinterpret_cast<unsigned long long*>(c->d_zero + c->z_bsum);
+                c->d_flist = reinterpret_cast<int32_t*>(c->d_zero + c->z_flist);
                 c->zero_bytes = zb;
             }
         } else {
@@ -1953,7 +1984,8 @@ static void launch_dicts(pq_chunk* c, hipStream_t s, int32_t* err_any) {
 
 static bool front_path(pq_ctx* ctx, const pq_chunk* c) { return c->pipe_fr && c->d_fwins && ctx->opt_front; }
 
-static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs) {
+static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs,
+                       bool fused = false) {
     hipStream_t s = ctx->stream;
     if (front_path(ctx, c)) {  // the dictionary decoded before (main stream)
         Timed t(ctx, "pipe_front");
@@ -1965,7 +1997,7 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
         const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
         pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
                               c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist,  // flist[0], bsum: cleared with d_flags
-                              ctx->opt_debug, dict_in_runs ? &rd : nullptr);
+                              ctx->opt_debug, dict_in_runs ? &rd : nullptr, fused ? c->fstage - 16 : 0u);
     }
     if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
     if (!c->hbig.empty()) {
@@ -1976,6 +2008,7 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
         Timed t(ctx, "pipe_count");
         pqk::launch_pipe_codes(s, P, true);
     }
+    if (fused) return;  // k_pipe_fused decodes the codes itself (and runs the exact decoder first)
     Timed t(ctx, "pipe_codes");
     pqk::launch_pipe_codes(s, P, false);
 }
@@ -2005,17 +2038,18 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     const bool plain_go = c->plain && ctx->opt_plain && !(c->plain_spec && c->spec_failed) &&
                           !(c->plain_opt && (c->popt_failed || !ctx->opt_plain_fused));
     const bool pipe_path = pipe && !plain_go;
-    if (pipe_path) c->codes_pending = true;
+    // k_pipe_fused keeps the codes in registers: no codes for a later scan to reuse
+    const bool fused = pipe_path && ctx->opt_pfused && c->fused_ok && !front_path(ctx, c) && c->d_zero;
+    if (pipe_path && !fused) c->codes_pending = true;
     if (c->ndicts && c->type == PQ_BYTE_ARRAY) c->entries_pending = true;
     if (pipe_path && c->d_zero && ctx->opt_zflip) {
         // flags, bsum and flist[0] of this decode: the other block, which the
         // previous decode's k_pipe_write cleared (else one fill)
         c->zsel ^= 1;
         uint8_t* zb = c->d_zero + static_cast<size_t>(c->zsel) * c->zfull;
-        const size_t fb = 4 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long);
         c->d_flags = reinterpret_cast<int32_t*>(zb);
-        c->d_bsum = reinterpret_cast<unsigned long long*>(zb + fb);
-        c->d_flist = reinterpret_cast<int32_t*>(zb + fb + bb);
+        c->d_bsum = reinterpret_cast<unsigned long long*>(zb + c->z_bsum);
+        c->d_flist = reinterpret_cast<int32_t*>(zb + c->z_flist);
         if (!c->next_zeroed) (void)hipMemsetAsync(c->d_flags, 0, c->zero_bytes, s);
         c->next_zeroed = false;
     } else {
@@ -2133,7 +2167,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_plain_ba(s, P);
     } else if (pipe) {
         pqk::PipeLaunch P = pipe_launch(ctx, c, out);
-        pipe_front(ctx, c, P, !dict_in_runs && !front, dict_in_runs);
+        pipe_front(ctx, c, P, !dict_in_runs && !front, dict_in_runs, fused);
         if (c->arm) {  // the page filter in the same pass: match bits per entry, then the writer tests them
             Timed t(ctx, "regex_dict");
             pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
@@ -2146,12 +2180,25 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
             (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
         }
-        Timed t(ctx, "pipe_write");
-        if (c->d_zero) {  // k_pipe_write clears the other block for the next decode
+        if (c->d_zero) {  // k_pipe_write / k_pipe_fused clears the other block for the next decode
             P.znext = reinterpret_cast<uint32_t*>(c->d_zero + static_cast<size_t>(c->zsel ^ 1) * c->zfull);
             P.znext_words = static_cast<uint32_t>(c->zero_bytes / 4);
         }
-        pqk::launch_pipe_write(s, P);
+        if (fused) {
+            uint8_t* zb = reinterpret_cast<uint8_t*>(c->d_flags);  // this decode's zero block
+            P.fticket = reinterpret_cast<int32_t*>(zb + c->z_fused);
+            P.fstatus = reinterpret_cast<unsigned long long*>(zb + c->z_fused + 16);
+            P.nunits = c->nunits;
+            P.fstage = c->fstage;
+            P.flds = c->flds;
+            P.fgrid = c->fgrid;
+            P.fwaves = c->fwaves;
+            Timed t(ctx, "pipe_fused");
+            pqk::launch_pipe_fused(s, P);
+        } else {
+            Timed t(ctx, "pipe_write");
+            pqk::launch_pipe_write(s, P);
+        }
         // the other block is clear only if k_pipe_write ran (it returns early on a chunk without tiles)
         if (c->d_zero) c->next_zeroed = c->ntiles > 0;
     } else if (c->fused) {

@@ -2144,6 +2144,505 @@ __global__ void __launch_bounds__(64) k_pipe_exact(CodeArgs a, const int32_t* __
     }
 }
 
+
+// ── codes and write in one persistent pass (k_pipe_fused) ───────────────────
+// k_pipe_codes3's per-tile decode and k_pipe_write's per-tile write, fused so
+// that the u16 codes never go through HBM and the decode's VALU work of some
+// waves runs while other waves of the same CU wait on their stores (the two
+// kernels otherwise run back to back: the front, VALU/latency-bound, then the
+// writer, HBM-bound).  Work comes in units of kFuseTiles consecutive 512-row
+// tiles, claimed by ticket (an atomic counter: a unit's predecessors were all
+// claimed by running waves, so the look-back below always completes, whatever
+// else shares the GPU).  Per unit, one wave:
+//   1. decodes its tiles' codes into registers (rows 8l .. 8l + 7 per lane,
+//      packed two per dword, the writer's own code layout): run records from
+//      k_pipe_runs and the page payload staged in the wave's LDS scratch, as in
+//      k_pipe_codes3; tiles of pages k_pipe_big or the exact decoder
+//      (k_pipe_exact, launched before) already decoded are read from HBM;
+//   2. sums the unit's characters (entry lengths from the LDS dictionary
+//      table) and takes its first output byte by decoupled look-back over the
+//      units before it (status words: flag and value in one 8-byte word);
+//   3. writes offsets, validity and characters exactly as k_pipe_write does.
+constexpr int kFuseTiles = 4;  // = kWBatch: four tiles' codes in registers
+
+struct FuseDecLds {  // one wave's decode scratch (the stage follows); aliased by WriteLds when writing
+    uint2 recd[kPipeRunCap];
+    uint2 reci[kPipeRunCap];
+    uint8_t mark[kTileRows];
+    uint8_t mark2[kTileRows];
+};
+static_assert(sizeof(FuseDecLds) % 16 == 0, "stage alignment");
+
+struct FusedArgs {
+    const uint8_t* bytes;
+    const DevPage* pages;
+    const DevTile* tiles;
+    int ntiles;
+    const int32_t* page_tile0;
+    int32_t max_def;
+    const DevDict* dicts;
+    int32_t dict_id;
+    const uint64_t* entries;
+    const int32_t* dict_count;
+    const uint2* runs;
+    const uint32_t* info;
+    const int32_t* tile_nn;
+    const uint16_t* codes;  // rows of pages decoded before this pass (k_pipe_big, k_pipe_exact)
+    DevErr* page_err;
+    int32_t* err_any;
+    int64_t nrows_total;
+    int64_t* total;
+    int64_t capacity;
+    int32_t* overflow;
+    uint32_t* validity;
+    int64_t* offsets;
+    uint8_t* chars;
+    uint32_t dict_chars_bytes, dict_bytes;  // LDS: [kFront][dictionary payload][entry table], then per wave scratch
+    uint32_t wave_lds;                      // per-wave scratch: max(FuseDecLds + stage, WriteLds)
+    uint32_t stage_bytes;                   // payload stage (>= every k_pipe_runs page's slot)
+    int32_t nunits;
+    int32_t* ticket;                        // zeroed per decode
+    unsigned long long* status;             // nunits look-back words, zeroed per decode
+    uint32_t* znext;                        // the next decode's zero block (cleared here), or null
+    uint32_t znext_words;
+    const uint8_t* match;                   // armed page filter, as k_pipe_write
+    int match_neg;
+    uint8_t* page_flags;
+    int debug;
+};
+
+constexpr unsigned long long kFAgg = 1ull << 62;
+constexpr unsigned long long kFInc = 2ull << 62;
+constexpr unsigned long long kFValMask = (1ull << 62) - 1;
+
+__device__ __forceinline__ unsigned long long fwave_sum64(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
+        const uint32_t hi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v >> 32), d));
+        v = v + ((static_cast<unsigned long long>(hi) << 32) | lo) - 0;
+    }
+    return v;
+}
+
+// Decoupled look-back over the units (status[u]: kFAgg | aggregate or
+// kFInc | inclusive prefix); returns the exclusive prefix of unit u.
+__device__ unsigned long long unit_look_back(unsigned long long* status, int32_t u, unsigned long long total) {
+    if (u == 0) {
+        if (lane() == 0) __hip_atomic_store(&status[0], kFInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane() == 0) __hip_atomic_store(&status[u], kFAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long prefix = 0;
+    int32_t q = u - 1;
+    uint32_t nap = 1;
+    for (;;) {
+        const int32_t i = q - static_cast<int32_t>(lane());
+        const unsigned long long s =
+            i >= 0 ? __hip_atomic_load(&status[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFInc;
+        const uint64_t incm = __ballot((s >> 62) == 2);
+        const uint64_t notready = __ballot((s >> 62) == 0);
+        const uint32_t first_inc = incm ? static_cast<uint32_t>(__builtin_ctzll(incm)) : 64u;
+        const uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1ull);
+        if (notready & upto) {  // a unit before the first inclusive prefix has not published yet
+            for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(4);
+            nap = nap < 8 ? 2 * nap : 8;
+            continue;
+        }
+        const unsigned long long c = lane() <= first_inc ? (s & kFValMask) : 0ull;
+        prefix += fwave_sum64(c);
+        if (first_inc < 64) break;
+        q -= 64;
+    }
+    if (lane() == 0) __hip_atomic_store(&status[u], kFInc | (prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return prefix;
+}
+
+// One tile's codes (w[4]: rows 8l .. 8l + 7 of the lane, packed) and its
+// characters (wave-uniform).  k_pipe_codes3's decode, with the records and
+// payload loaded and staged here (no cross-tile prefetch).
+template <bool kArmed>
+__device__ __forceinline__ uint32_t fuse_codes(const FusedArgs& a, FuseDecLds& D, uint32_t* stage, const uint32_t* dtab,
+                                               uint32_t dict_n, int t, int p, uint32_t r0, uint32_t m, uint32_t inf,
+                                               uint32_t size, uint64_t off, int64_t R0, uint32_t tp, uint32_t w[4]) {
+    const uint32_t l8 = lane() * 8;
+    auto lenof = [&](uint32_t v, bool ok) -> uint32_t {
+        const uint32_t e = dtab[ok ? v : 0u];
+        return ok ? (kArmed ? ((e >> 16) & 0x7FFFu) : (e >> 16)) : 0u;
+    };
+    if (inf & kSkip) {  // decoded before this pass: the codes are in HBM
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (l8 < m) {
+            const U16B x = *reinterpret_cast<const U16B*>(a.codes + R0 + l8);
+            v = make_uint4(x.x, x.y, x.z, x.w);
+        }
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        uint32_t chars = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t c = l8 + k < m ? (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : kNull;
+            chars += lenof(c, c < dict_n);
+        }
+        return wave_sum(chars);
+    }
+    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
+    const uint32_t maskd = (1u << bwd) - 1u;
+    const uint32_t nd = inf & 0xFFu, ni = (inf >> 8) & 0xFFu, bwi = (inf >> 16) & 0xFFu;
+    // the page's run records (clamped indices: a page costs its records' lines)
+    const uint2* rd_ = a.runs + static_cast<size_t>(p) * 2 * kPipeRunCap;
+    const uint2 z = make_uint2(0u, 0u);
+    const uint32_t nd1 = nd ? nd - 1 : 0u, ni1 = ni ? ni - 1 : 0u;
+    const uint2 q0 = rd_[min(lane(), nd1)], q1 = rd_[min(lane() + kWave, nd1)];
+    const uint2 q2 = rd_[kPipeRunCap + min(lane(), ni1)], q3 = rd_[kPipeRunCap + min(lane() + kWave, ni1)];
+    const uint2 d0 = lane() < nd ? q0 : z, d1 = lane() + kWave < nd ? q1 : z;
+    const uint2 x0 = lane() < ni ? q2 : z, x1 = lane() + kWave < ni ? q3 : z;
+    // non-null rows of the page's earlier tiles (pages of <= 2048 rows: <= 3)
+    const uint32_t tn = static_cast<uint32_t>(a.tile_nn[min(tp + lane(), static_cast<uint32_t>(a.ntiles - 1))]);
+    const uint32_t k0n = (md > 0 && tp + lane() < static_cast<uint32_t>(t)) ? tn : 0u;
+    // payload -> stage (the slot's >= 16 zero bytes after the payload come along)
+    {
+        const uint32_t nb = (size + 15) / 16 + 1;
+        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + off);
+        uint4* st4 = reinterpret_cast<uint4*>(stage);
+        for (uint32_t b = lane(); b < nb; b += kWave) st4[b] = src[b];
+    }
+    D.recd[lane()] = d0;
+    D.recd[lane() + kWave] = d1;
+    D.reci[lane()] = x0;
+    D.reci[lane() + kWave] = x1;
+    *reinterpret_cast<uint2*>(D.mark + l8) = make_uint2(0u, 0u);
+    *reinterpret_cast<uint2*>(D.mark2 + l8) = make_uint2(0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t zw = ((size + 15) / 16 + 1) * 4 - 1;  // last word of the slot: zero
+    const uint32_t maski = (1u << bwi) - 1u;
+    uint32_t vb;
+    if (md > 0) {  // def levels of rows r0 + 8l .. r0 + 8l + 7
+        const uint32_t rd0 = run_at_reg(d0, d1, nd, r0);
+        {
+            const uint32_t k = lane(), st = rr_start(d0);
+            if (k < nd && k > rd0 && st < r0 + m) D.mark[st - r0] = static_cast<uint8_t>(k - rd0);
+            const uint32_t k1 = lane() + kWave, st1 = rr_start(d1);
+            if (k1 < nd && k1 > rd0 && st1 < r0 + m) D.mark[st1 - r0] = static_cast<uint8_t>(k1 - rd0);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint2 mk = *reinterpret_cast<const uint2*>(D.mark + l8);
+        uint32_t rm[8], run = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
+            rm[k] = run;
+        }
+        const uint32_t ex = wave_shr1(wave_incl_max(run));
+        vb = 0;
+        bool above = false;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t j = l8 + k;
+            const uint2 R = D.recd[(rd0 + max(ex, rm[k])) & (kPipeRunCap - 1)];
+            const uint32_t pay = rr_pay(R);
+            const uint32_t lb = sbits3(stage, pay + (r0 + j - rr_start(R)) * bwd, zw, maskd);
+            const uint32_t lvl = rr_lit(R) ? lb : pay;
+            const bool in = j < m;
+            vb |= (in && lvl == md ? 1u : 0u) << k;
+            above |= in && lvl > md;
+        }
+        if (__ballot(above)) {  // levels above max_def: outside the supported format
+            set_err(a.page_err + p, a.err_any, PQ_ERR_UNSUPPORTED, 0, 0, size);
+            w[0] = w[1] = w[2] = w[3] = 0xFFFFFFFFu;
+            __builtin_amdgcn_wave_barrier();
+            return 0;
+        }
+    } else {
+        vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
+    }
+    const uint32_t nnl = __popc(vb);
+    const uint32_t nincl = wave_incl_scan(nnl);
+    const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
+    const uint32_t k0 = md > 0 ? wave_sum(k0n) : r0;
+    const uint32_t ri0 = run_at_reg(x0, x1, ni, k0);
+    if (nn) {  // dictionary index runs over ranks [k0, k0 + nn): run of each rank -> mark2
+        {
+            const uint32_t k = lane(), st = rr_start(x0);
+            if (k < ni && k > ri0 && st < k0 + nn) D.mark2[st - k0] = static_cast<uint8_t>(k - ri0);
+            const uint32_t k1 = lane() + kWave, st1 = rr_start(x1);
+            if (k1 < ni && k1 > ri0 && st1 < k0 + nn) D.mark2[st1 - k0] = static_cast<uint8_t>(k1 - ri0);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint2 mk = *reinterpret_cast<const uint2*>(D.mark2 + l8);
+        uint32_t rm[8], run = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
+            rm[k] = run;
+        }
+        const uint32_t ex = wave_shr1(wave_incl_max(run));
+        uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t v = max(ex, rm[k]);
+            if (k < 4) w0 |= v << (8 * k);
+            else w1 |= v << (8 * (k - 4));
+        }
+        __builtin_amdgcn_wave_barrier();
+        *reinterpret_cast<uint2*>(D.mark2 + l8) = make_uint2(w0, w1);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    uint32_t chars = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t rk = min(rbase + __popc(vb & ((1u << k) - 1u)), static_cast<uint32_t>(kTileRows - 1));
+        const uint2 R = D.reci[(ri0 + D.mark2[rk]) & (kPipeRunCap - 1)];
+        const uint32_t pay = rr_pay(R);
+        const uint32_t lb = sbits3(stage, pay + (k0 + rk - rr_start(R)) * bwi, zw, maski);
+        const uint32_t v = rr_lit(R) ? lb : pay;
+        const bool ok = ((vb >> k) & 1u) && v < dict_n;
+        chars += lenof(v, ok);
+        const uint32_t code = ok ? v : static_cast<uint32_t>(kNull);
+        if (k & 1) w[k >> 1] |= code << 16;
+        else w[k >> 1] = code;
+    }
+    __builtin_amdgcn_wave_barrier();  // the scratch is rewritten by the next tile / the writer
+    return wave_sum(chars);
+}
+
+template <bool kArmed>
+__global__ void __launch_bounds__(kWriteMax * 64) k_pipe_fused(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.znext)  // the other zero block, for the next decode (unused by this one)
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.znext_words; i += gridDim.x * blockDim.x) a.znext[i] = 0;
+    uint32_t* dwa = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* dw = reinterpret_cast<uint32_t*>(smem + kFront);
+    uint32_t* dtab = reinterpret_cast<uint32_t*>(smem + kFront + a.dict_chars_bytes);
+    const uint32_t wv = threadIdx.x / kWave;
+    uint8_t* scratch = smem + a.dict_bytes + static_cast<size_t>(wv) * a.wave_lds;
+    FuseDecLds& D = *reinterpret_cast<FuseDecLds*>(scratch);
+    uint32_t* stage = reinterpret_cast<uint32_t*>(scratch + sizeof(FuseDecLds));
+    WriteLds& S = *reinterpret_cast<WriteLds*>(scratch);
+    const DevDict d = a.dicts[a.dict_id];
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    {  // the dictionary into LDS (as k_pipe_write)
+        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
+        copy_blocks(reinterpret_cast<uint4*>(dw), src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
+        if (kArmed) {
+            const uint64_t* es = a.entries + d.entry_base;
+            for (uint32_t k = threadIdx.x; k < dict_n; k += blockDim.x) {
+                const uint64_t e = es[k];
+                const uint32_t sat = (a.match[k] != 0) != (a.match_neg != 0) ? 1u : 0u;
+                dtab[k] = static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16) | (sat << 31);
+            }
+        } else {
+            copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
+                return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
+            });
+        }
+    }
+    __syncthreads();
+    auto rl64 = [](int64_t v, int i) -> int64_t {
+        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
+        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), i);
+        return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+    };
+    const uint32_t l8 = lane() * kRowsPerLane;
+    for (;;) {
+        int32_t u = 0;
+        if (lane() == 0) u = atomicAdd(a.ticket, 1);
+        u = static_cast<int32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u)));
+        if (u >= a.nunits) break;
+        const int c0 = u * kFuseTiles;
+        const int cn = min(kFuseTiles, a.ntiles - c0);
+        int64_t myR0 = 0, myoff = 0;
+        uint32_t mym = 0, myp = 0, myr0 = 0, myinf = kFallback, mysize = 0, mytp = 0;
+        {  // (clamped index, selected after: see k_pipe_codes3)
+            const bool in = static_cast<int>(lane()) < cn;
+            const DevTile T = a.tiles[c0 + min(static_cast<int>(lane()), cn - 1)];
+            const DevPage pg = a.pages[T.page];
+            const uint32_t inf = a.info[T.page];
+            const uint32_t tp = static_cast<uint32_t>(a.page_tile0[T.page]);
+            myp = in ? static_cast<uint32_t>(T.page) : 0u;
+            myr0 = in ? static_cast<uint32_t>(T.row0) : 0u;
+            mym = in ? static_cast<uint32_t>(T.nrows) : 0u;
+            myR0 = in ? pg.first_row + T.row0 : 0;
+            myinf = in ? inf : kFallback;
+            mysize = in ? static_cast<uint32_t>(max(pg.size, 0)) : 0u;
+            myoff = in ? static_cast<int64_t>(pg.off) : 0;
+            mytp = in ? tp : 0u;
+        }
+        // 1. codes of the unit's tiles
+        uint4 cv0 = make_uint4(~0u, ~0u, ~0u, ~0u), cv1 = cv0, cv2 = cv0, cv3 = cv0;
+        uint32_t myc = 0;
+        static_assert(kFuseTiles == 4, "code registers");
+        for (int i = 0; i < cn; i++) {
+            uint32_t w[4];
+            const uint32_t ch = fuse_codes<kArmed>(
+                a, D, stage, dtab, dict_n, c0 + i, static_cast<int>(__builtin_amdgcn_readlane(myp, i)),
+                __builtin_amdgcn_readlane(myr0, i), __builtin_amdgcn_readlane(mym, i),
+                __builtin_amdgcn_readlane(myinf, i), __builtin_amdgcn_readlane(mysize, i),
+                static_cast<uint64_t>(rl64(myoff, i)), rl64(myR0, i), __builtin_amdgcn_readlane(mytp, i), w);
+            const uint4 v = make_uint4(w[0], w[1], w[2], w[3]);
+            if (i == 0) cv0 = v;
+            else if (i == 1) cv1 = v;
+            else if (i == 2) cv2 = v;
+            else cv3 = v;
+            myc = static_cast<int>(lane()) == i ? ch : myc;
+        }
+        // 2. the unit's first output byte
+        const uint32_t inc = wave_incl_scan(myc);
+        const unsigned long long prefix = unit_look_back(a.status, u, bcast_last(inc));
+        const int64_t myG0 = static_cast<int64_t>(prefix) + static_cast<int64_t>(inc - myc);
+        if (a.debug & 8) continue;
+        // 3. k_pipe_write's per-tile body
+        for (int i = 0; i < cn; i++) {
+            const int64_t R0 = rl64(myR0, i);
+            const int64_t G0 = rl64(myG0, i);
+            const uint32_t m = __builtin_amdgcn_readlane(mym, i);
+            uint32_t cur[kRowsPerLane];
+            {
+                const uint4 w = i == 0 ? cv0 : (i == 1 ? cv1 : (i == 2 ? cv2 : cv3));
+                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++)
+                    cur[k] = l8 + k < m ? (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : kNull;
+            }
+            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0, sat = 0;
+#pragma unroll
+            for (int k = 0; k < kRowsPerLane; k++) {
+                const bool valid = cur[k] < dict_n;
+                const uint32_t e = valid ? dtab[cur[k]] : 0u;
+                len[k] = kArmed ? ((e >> 16) & 0x7FFFu) : (e >> 16);
+                if (kArmed) sat |= e;
+                src[k] = e & 0xFFFFu;
+                vb |= (valid ? 1u : 0u) << k;
+                acc += len[k];
+            }
+            if (kArmed && __ballot(sat >> 31) && lane() == 0)  // the page filter: a row whose entry satisfies it
+                a.page_flags[__builtin_amdgcn_readlane(myp, i)] = 0;
+            const uint32_t incl = wave_incl_scan(acc);
+            const uint32_t total = bcast_last(incl);
+            {
+                uint32_t o[kRowsPerLane];
+                o[0] = incl - acc;
+#pragma unroll
+                for (int k = 1; k < kRowsPerLane; k++) o[k] = o[k - 1] + len[k - 1];
+                uint4* po = reinterpret_cast<uint4*>(&S.off[lane() * kRowsPerLane]);
+                po[0] = make_uint4(o[0], o[1], o[2], o[3]);
+                po[1] = make_uint4(o[4], o[5], o[6], o[7]);
+                *reinterpret_cast<uint4*>(&S.src[lane() * kRowsPerLane]) =
+                    make_uint4(src[0] | (src[1] << 16), src[2] | (src[3] << 16), src[4] | (src[5] << 16),
+                               src[6] | (src[7] << 16));
+            }
+            S.vb[lane()] = static_cast<uint8_t>(vb);
+            if (lane() == 0) S.off[m] = total;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            if ((R0 & 1) == 0) {  // offsets: rows 2j', 2j' + 1 per lane as one 16-byte store
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane / 2; k++) {
+                    const uint32_t j = k * 2 * kWave + 2 * lane();
+                    if (j + 1 < m) {
+                        const uint2 o = *reinterpret_cast<const uint2*>(&S.off[j]);
+                        const int64_t v0 = G0 + o.x, v1 = G0 + o.y;
+                        *reinterpret_cast<uint4*>(a.offsets + R0 + j) =
+                            make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(static_cast<uint64_t>(v0) >> 32),
+                                       static_cast<uint32_t>(v1), static_cast<uint32_t>(static_cast<uint64_t>(v1) >> 32));
+                    } else if (j < m) {
+                        a.offsets[R0 + j] = G0 + S.off[j];
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++) {
+                    const uint32_t j = k * kWave + lane();
+                    if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
+                }
+            }
+            {  // validity words [R0 >> 5, (R0 + m - 1) >> 5]
+                const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
+                const uint32_t sh = static_cast<uint32_t>(R0 & 31);
+                const int64_t g = gfirst + lane();
+                if (g <= glast) {
+                    auto tw = [&](int tt) -> uint32_t {
+                        return (tt >= 0 && tt < kWave / 4) ? reinterpret_cast<const uint32_t*>(S.vb)[tt] : 0u;
+                    };
+                    const int tt = static_cast<int>(lane());
+                    const uint32_t val = (tw(tt) << sh) | (sh ? (tw(tt - 1) >> (32 - sh)) : 0u);
+                    const bool whole = g * 32 >= R0 && (g * 32 + 32 <= R0 + m || R0 + m == a.nrows_total);
+                    if (whole) a.validity[g] = val;
+                    else if (val) atomicOr(&a.validity[g], val);
+                }
+            }
+            if (R0 + m == a.nrows_total && lane() == 0) {
+                a.offsets[a.nrows_total] = G0 + total;
+                *a.total = G0 + total;
+            }
+            if (total == 0 || (a.debug & 2)) {
+                __builtin_amdgcn_wave_barrier();
+                continue;
+            }
+            if (G0 + total > a.capacity) {  // output too small: the host grows it and re-runs
+                if (lane() == 0) atomicOr(a.overflow, 1);
+                __builtin_amdgcn_wave_barrier();
+                continue;
+            }
+            for (uint32_t g0 = 0; g0 < m; g0 += kWave) {  // characters: row per lane from the LDS dictionary
+                const uint32_t r = g0 + lane();
+                uint32_t s0 = 0, ln = 0, sa = 0;
+                if (r < m) {
+                    s0 = S.off[r];
+                    ln = S.off[r + 1] - s0;
+                    sa = kFront + S.src[r];
+                }
+                const bool lng = ln > kLongRow;
+                if (!lng && ln) {
+                    uint8_t* dp = a.chars + G0 + s0;
+                    if (ln >= 16) {
+                        for (uint32_t x = 0; x + 16 < ln; x += 16) {
+                            const uint4 v = lds16(dwa, sa + x);
+                            *reinterpret_cast<U16B*>(dp + x) = U16B{v.x, v.y, v.z, v.w};
+                        }
+                        const uint4 v = lds16(dwa, sa + ln - 16);
+                        *reinterpret_cast<U16B*>(dp + ln - 16) = U16B{v.x, v.y, v.z, v.w};
+                    } else {
+                        const uint4 v = lds16(dwa, sa);
+                        const uint32_t tt = ln >= 8 ? ln - 8 : (ln >= 4 ? ln - 4 : (ln >= 2 ? ln - 2 : 0u));
+                        const uint4 uu = lds16(dwa, sa + tt);
+                        if (ln >= 8) {
+                            *reinterpret_cast<U8B*>(dp) = U8B{v.x, v.y};
+                            *reinterpret_cast<U8B*>(dp + tt) = U8B{uu.x, uu.y};
+                        } else if (ln >= 4) {
+                            *reinterpret_cast<U4B*>(dp) = U4B{v.x};
+                            *reinterpret_cast<U4B*>(dp + tt) = U4B{uu.x};
+                        } else if (ln >= 2) {
+                            *reinterpret_cast<U2B*>(dp) = U2B{static_cast<uint16_t>(v.x)};
+                            *reinterpret_cast<U2B*>(dp + tt) = U2B{static_cast<uint16_t>(uu.x)};
+                        } else {
+                            dp[0] = static_cast<uint8_t>(v.x);
+                        }
+                    }
+                }
+                uint64_t lm = __ballot(lng);
+                while (lm) {  // long rows: the whole wave, aligned destination blocks
+                    const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
+                    lm &= lm - 1;
+                    const int64_t A0 = G0 + __builtin_amdgcn_readlane(s0, l);
+                    const int64_t A1 = A0 + __builtin_amdgcn_readlane(ln, l);
+                    const uint32_t src0 = __builtin_amdgcn_readlane(sa, l);
+                    const int64_t b0 = A0 & ~static_cast<int64_t>(15);
+                    for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < A1; blk += 16 * kWave) {
+                        const uint4 v = lds16(dwa, static_cast<uint32_t>(src0 + (blk - A0)));
+                        store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, A0) - blk),
+                                   static_cast<uint32_t>(min(blk + 16, A1) - blk));
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // S is rewritten by the next tile / the next unit's decode
+        }
+    }
+}
+
 }  // namespace
 
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens) { return big_layout(max_page_bytes, nlens).total; }
@@ -2165,7 +2664,7 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
-                      int debug, const RunDicts* dicts) {
+                      int debug, const RunDicts* dicts, uint32_t stage_max) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     const int nd = dicts ? dicts->ndicts : 0;
     if (npages <= 0 && nd <= 0) return;
@@ -2175,7 +2674,8 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
                                               dicts->err_any}
                                 : RunDictArgs{nullptr, 0, nullptr, nullptr, nullptr, nullptr};
     hipLaunchKernelGGL(k_pipe_runs, dim3(nd + (max(npages, 0) + per - 1) / per), dim3(kRunWaves * kWave), 0, s,
-                       bytes, pages, npages, max_def, max_rep, runs, info, ppw, flist, kStage3 - 16, d, debug);
+                       bytes, pages, npages, max_def, max_rep, runs, info, ppw, flist,
+                       stage_max ? min(stage_max, kStage3 - 16) : kStage3 - 16, d, debug);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's
@@ -2265,6 +2765,57 @@ void launch_pipe_front(hipStream_t s, const PipeLaunch& P, const DevBatch* wins,
     hipLaunchKernelGGL(k_pipe_front, dim3(grid), dim3(kFrWaves * kWave), lds, s, a, wins, nwins, lt_n, win, flist);
     // listed pages (none on well-formed ref-layout chunks)
     hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, P.npages))), dim3(kWave), sizeof(CodeLds), s, a, P.flist);
+}
+
+int pipe_fused_tiles() { return kFuseTiles; }
+
+static uint32_t fused_wave_lds(uint32_t stage) {
+    const uint32_t dec = static_cast<uint32_t>(sizeof(FuseDecLds)) + stage;
+    return (max(dec, static_cast<uint32_t>(sizeof(WriteLds))) + 15) / 16 * 16;
+}
+
+PipePlan plan_pipe_fused(uint32_t dict_bytes, int wpw, uint32_t stage) {
+    PipePlan pl{};
+    pl.lds = dict_bytes + static_cast<uint32_t>(wpw) * fused_wave_lds(stage);
+    pl.blocks_per_cu = pl.lds <= 160u * 1024 ? static_cast<int>((160u * 1024) / pl.lds) : 0;
+    if (pl.blocks_per_cu > 4) pl.blocks_per_cu = 4;
+    if (pl.blocks_per_cu > 0) {
+        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_fused<false>), pl.lds);
+        const int occ = resident_blocks(reinterpret_cast<const void*>(k_pipe_fused<false>), wpw * kWave, pl.lds);
+        pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
+    }
+    return pl;
+}
+
+void launch_pipe_fused(hipStream_t s, const PipeLaunch& P) {
+    if (P.ntiles <= 0 || P.nunits <= 0) return;
+    int wgrid = 0, per = 0;
+    write_shape(P, &wgrid, &per);
+    if (P.has_small) {  // pages k_pipe_runs listed: the exact decoder writes their codes first
+        CodeArgs ca{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
+                    P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
+                    P.bsum, per, P.debug, P.write_waves};
+        hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, P.npages))), dim3(kWave), sizeof(CodeLds), s, ca, P.flist);
+    }
+    FusedArgs a{};
+    a.bytes = P.bytes; a.pages = P.pages; a.tiles = P.tiles; a.ntiles = P.ntiles; a.page_tile0 = P.page_tile0;
+    a.max_def = P.max_def; a.dicts = P.dicts; a.dict_id = P.dict_id; a.entries = P.entries; a.dict_count = P.dict_count;
+    a.runs = P.runs; a.info = P.info; a.tile_nn = P.tile_nn; a.codes = P.codes; a.page_err = P.page_err;
+    a.err_any = P.err_any; a.nrows_total = P.nrows_total; a.total = P.total; a.capacity = P.capacity;
+    a.overflow = P.overflow; a.validity = P.validity; a.offsets = P.offsets; a.chars = P.chars;
+    a.dict_chars_bytes = P.dict_chars_bytes; a.dict_bytes = P.dict_bytes; a.wave_lds = fused_wave_lds(P.fstage);
+    a.stage_bytes = P.fstage; a.nunits = P.nunits; a.ticket = P.fticket; a.status = P.fstatus;
+    a.znext = P.znext; a.znext_words = P.znext_words; a.match = P.match; a.match_neg = P.match_neg;
+    a.page_flags = P.page_flags; a.debug = P.debug;
+    const int waves = max(1, P.fwaves);
+    const int grid = max(1, min(P.fgrid, (P.nunits + waves - 1) / waves));
+    if (P.match) {
+        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_fused<true>), P.flds);
+        hipLaunchKernelGGL(k_pipe_fused<true>, dim3(grid), dim3(waves * kWave), P.flds, s, a);
+    } else {
+        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_fused<false>), P.flds);
+        hipLaunchKernelGGL(k_pipe_fused<false>, dim3(grid), dim3(waves * kWave), P.flds, s, a);
+    }
 }
 
 void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags,

@@ -174,6 +174,13 @@ struct PipeLaunch {
     const uint8_t* match = nullptr;  // armed page filter (k_pipe_write), dictionary payloads < kArmDictBytes
     int match_neg = 0;
     uint8_t* page_flags = nullptr;
+    // k_pipe_fused (codes + write in one pass): zeroed ticket / look-back
+    // words of the decode, its units, payload stage, LDS, grid and waves
+    int32_t* fticket = nullptr;
+    unsigned long long* fstatus = nullptr;
+    int32_t nunits = 0;
+    uint32_t fstage = 0, flds = 0;
+    int fgrid = 0, fwaves = 0;
 };
 constexpr uint32_t kArmDictBytes = 32768;  // every entry length < 2^15: the match bit rides in the entry word
 struct PipePlan {
@@ -181,6 +188,13 @@ struct PipePlan {
     int blocks_per_cu;  // 0: the dictionary does not fit
 };
 PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw);
+// k_pipe_fused: tiles per unit, and its LDS / resident workgroups per CU for
+// `wpw` waves per workgroup and a payload stage of `stage` bytes per wave
+int pipe_fused_tiles();
+PipePlan plan_pipe_fused(uint32_t dict_bytes, int wpw, uint32_t stage);
+// codes and write in one pass (after k_pipe_runs / k_pipe_big / the count
+// pass; the exact decoder runs first, inside, over the pages k_pipe_runs listed)
+void launch_pipe_fused(hipStream_t s, const PipeLaunch& P);
 // Dictionary pages for k_pipe_runs' leading workgroups (4 waves each; pages
 // up to kRunDictMax bytes), so the dictionary decodes inside the run-table
 // launch instead of a k_dict_index launch on a side stream.
@@ -195,7 +209,7 @@ struct RunDicts {
 constexpr uint32_t kRunDictMax = 60 * 1024;
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist, int debug,
-                      const RunDicts* dicts = nullptr);
+                      const RunDicts* dicts = nullptr, uint32_t stage_max = 0);  // 0: k_pipe_codes3's stage
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 // k_pipe_front: the whole front (run headers -> u16 codes, tile characters)
 // of chunks whose pages hold <= kTileRows rows, one wavefront per window of

@@ -25,7 +25,7 @@ def ctx():
 
 
 # Kernel-path fixtures shared by the GPU parity tests.
-@pytest.fixture(params=["default", "front", "big", "fused", "generic", "serial"])
+@pytest.fixture(params=["default", "pfused", "front", "big", "fused", "generic", "serial"])
 def path(request, ctx):
     """Every kernel path that ships: "default" = what a chunk takes with the
     default options (dictionary BYTE_ARRAY on dict_pipe.hip: the run-table
@@ -40,11 +40,13 @@ def path(request, ctx):
     per-page k_fixed (dictionary chunks: rows by k_wide_rows, a workgroup per
     page); "serial" is "generic" with the wave-per-page k_ba_rows, the byte-wise
     gather and k_fixed_levels2's large-LDS form.  PLAIN BYTE_ARRAY chunks take the one-pass kernel
-    (k_plain_fused) under "default" and the two passes under "big"."""
+    (k_plain_fused) under "default" and the two passes under "big".  "pfused" is "default" with
+    the pipe's codes and write passes in one kernel (k_pipe_fused)."""
     p = request.param
+    ctx.set_option("pipe_fused", int(p == "pfused"))
     ctx.set_option("big_all", int(p == "big"))
-    ctx.set_option("dict_pipe", int(p in ("default", "front", "big")))
-    ctx.set_option("plain_ba", int(p in ("default", "front", "big")))
+    ctx.set_option("dict_pipe", int(p in ("default", "pfused", "front", "big")))
+    ctx.set_option("plain_ba", int(p in ("default", "pfused", "front", "big")))
     ctx.set_option("fused_ba", int(p not in ("generic", "serial")))
     ctx.set_option("fixed_plain", int(p not in ("generic", "serial")))
     ctx.set_option("wide_rows", int(p != "serial"))
@@ -54,6 +56,7 @@ def path(request, ctx):
     ctx.set_option("fixed_fused", int(p == "big"))
     ctx.set_option("pipe_front", int(p == "front"))
     yield p
+    ctx.set_option("pipe_fused", 0)
     for k in ("dict_pipe", "plain_ba", "fused_ba", "fixed_plain", "plain_fused"):
         ctx.set_option(k, 1)
     ctx.set_option("fixed_fused", 0)
