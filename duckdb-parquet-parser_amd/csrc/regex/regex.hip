@@ -785,9 +785,15 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                     cnt = 0;
                 }
             }
-            if (index_out && pl)
-                for (uint32_t k = 0; k < cnt; k++) index_out[pgc.first_row + k] = list[mpay / 4 + k];
         }
+        // the window's first row: with the index being filed (REQUIRED chunk,
+        // pages of consecutive rows), string g of the window is row fr0 + g and
+        // its entry is stored below, coalesced, where the DFA pass reads it
+        // (a failed page files no index: collect() drops it)
+        const int64_t fr0 = static_cast<int64_t>(
+            static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(pgc.first_row), 0))) |
+            (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(pgc.first_row >> 32), 0))) << 32));
+        uint16_t* const idx_w = index_in ? nullptr : index_out;
         // flatten: string g of the window -> (page lane, k)
         const uint32_t pinc = wave_incl_scan(cnt);
         pref[lane()] = pinc;
@@ -809,6 +815,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                 const uint32_t gl = ok2[h] ? lo2 : 0u;
                 const uint32_t bef = gl ? pref[gl - 1] : 0u;
                 const uint32_t ent = ok2[h] ? list[lbase[gl] + (g - bef)] : 4u;
+                if (idx_w && ok2[h]) idx_w[fr0 + g] = static_cast<uint16_t>(ent);
                 off2[h] = ent;
                 len2[h] = ok2[h] ? st_u32(stage, ent - 4) : 0u;
                 pg2[h] = gl;
