@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (control path only; the data path has no collective)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--opt", action="append", default=[],
+                    help="context option key=value set before any upload (repeatable), e.g. pipe_fused=1")
     return ap.parse_args()
 
 
@@ -944,6 +946,9 @@ def main():
         dist.init_process_group(args.dist_backend)
     from pqgpu import capi
     ctx = capi.Context(local)
+    for kv in args.opt:
+        k, _, v = kv.partition("=")
+        ctx.set_option(k, int(v))
     J = Job(rank, world, local, dist, ctx)
     exp = expectations()
 
