@@ -194,6 +194,7 @@ struct pq_chunk {
     unsigned long long* d_bsum = nullptr;
     int32_t* d_flist = nullptr;
     bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
+    uint32_t pipe_small_bytes = 0;      // the largest payload of those pages
     bool pipe_fr = false;               // every page <= kTileRows rows, every slot <= kFrontWin: k_pipe_front
     std::vector<pqk::DevBatch> hfwins;  // its windows of consecutive pages
     pqk::DevBatch* d_fwins = nullptr;
@@ -522,6 +523,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     const int cus = ctx->cus;
     c->pipe = true;
     c->pipe_small = small;
+    c->pipe_small_bytes = small_bytes;
     c->pipe_count = multi && c->max_def > 0;
     c->hbig = std::move(big);
     c->big_max_bytes = big_bytes;
@@ -927,7 +929,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
         return 0;
     }
     if (std::strcmp(key, "pipe_run_pages") == 0) {
-        if (value < 1 || value > 32) return set_err(ctx, PQ_ERR_ARG, "pipe_run_pages: 1..32");
+        if (value < 0 || value > 32) return set_err(ctx, PQ_ERR_ARG, "pipe_run_pages: 0 (auto) .. 32");
         ctx->opt_run_pages = static_cast<int>(value);
         return 0;
     }
@@ -1997,7 +1999,8 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
         const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
         pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
                               c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist,  // flist[0], bsum: cleared with d_flags
-                              ctx->opt_debug, dict_in_runs ? &rd : nullptr, fused ? c->fstage - 16 : 0u);
+                              ctx->opt_debug, dict_in_runs ? &rd : nullptr, fused ? c->fstage - 16 : 0u,
+                              (c->pipe_small_bytes + 15) / 16 * 16 + 16, c->max_dict_bytes, ctx->cus);
     }
     if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
     if (!c->hbig.empty()) {

@@ -91,20 +91,24 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
                                                               uint2* __restrict__ runs,
                                                               uint32_t* __restrict__ info, int ppw,
                                                               int32_t* __restrict__ flist, uint32_t stage_max,
-                                                              RunDictArgs d, int debug) {
-    __shared__ __attribute__((aligned(16))) uint32_t stage_all[kRunWaves][kRunStage / 4 + 8];
+                                                              RunDictArgs d, int debug, uint32_t wstage) {
+    // dynamic LDS: kRunWaves windows of wstage + 32 bytes each (wstage: the
+    // group's pages fit when it is at least ppw page slots), or the leading
+    // workgroups' dictionary page
+    extern __shared__ __attribute__((aligned(16))) uint32_t stage_dyn[];
+    const uint32_t wwords = wstage / 4 + 8;
     if (static_cast<int>(blockIdx.x) < d.ndicts) {
         // leading workgroups: the chunk's dictionary pages (dict_index.hpp),
         // the page staged over this workgroup's payload windows
         dict_index_block<kRunWaves>(bytes, d.dicts, static_cast<int>(blockIdx.x), d.entries, d.dict_count,
-                                    d.dict_err, d.err_any, static_cast<uint32_t>(sizeof(stage_all)), &stage_all[0][0]);
+                                    d.dict_err, d.err_any, kRunWaves * wwords * 4, stage_dyn);
         return;
     }
     const uint32_t wv = threadIdx.x / kWave;
     const int g0 = ((static_cast<int>(blockIdx.x) - d.ndicts) * kRunWaves + static_cast<int>(wv)) * ppw;
     if (g0 >= npages) return;
     const int g1 = min(npages, g0 + ppw);
-    uint32_t* stage = stage_all[wv];
+    uint32_t* stage = stage_dyn + wv * wwords;
     // one load of the group's page records (lane 2i, 2i + 1: page g0 + i;
     // lanes past the group re-read its last page): the window bounds and the
     // inside test come from it, and so does each lane's own page below
@@ -118,7 +122,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
     const uint64_t whi = rl64(mine.off, 2 * gl) +
                          static_cast<uint32_t>(max(static_cast<int32_t>(__builtin_amdgcn_readlane(
                                                        static_cast<uint32_t>(mine.size), 2 * gl)), 0));
-    bool staged = whi >= wlo && whi - wlo <= kRunStage;
+    bool staged = whi >= wlo && whi - wlo <= wstage;
     if (staged) {  // every page of the group inside the window (image order)
         const bool inside = mine.off >= wlo && mine.off + static_cast<uint32_t>(max(mine.size, 0)) <= whi;
         staged = __ballot(!inside) == 0;
@@ -2664,18 +2668,36 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
 
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
-                      int debug, const RunDicts* dicts, uint32_t stage_max) {
+                      int debug, const RunDicts* dicts, uint32_t stage_max, uint32_t slot_max, uint32_t dict_max,
+                      int cus) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     const int nd = dicts ? dicts->ndicts : 0;
     if (npages <= 0 && nd <= 0) return;
-    const int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
+    int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
+    if (pages_per_wave == 0) {  // auto: about two waves per SIMD over the chip, 4 .. 32 pages each
+        const int target = max(1, npages / max(1, cus * 4 * 2));
+        ppw = 4;
+        while (ppw * 2 <= min(target, kRunPages)) ppw *= 2;
+    }
     const int per = kRunWaves * ppw;
     const RunDictArgs d = dicts ? RunDictArgs{dicts->dicts, nd, dicts->entries, dicts->dict_count, dicts->dict_err,
                                               dicts->err_any}
                                 : RunDictArgs{nullptr, 0, nullptr, nullptr, nullptr, nullptr};
-    hipLaunchKernelGGL(k_pipe_runs, dim3(nd + (max(npages, 0) + per - 1) / per), dim3(kRunWaves * kWave), 0, s,
+    // window per wave: ppw page slots (slot_max: the largest small page's
+    // slot; 0: unknown, kRunStage), at most kRunStage; the leading
+    // workgroups' dictionary pages need dict_max + 32 bytes in all
+    uint32_t wstage = slot_max ? static_cast<uint32_t>(ppw) * slot_max : kRunStage;
+    wstage = min(kRunStage, (wstage + 15) / 16 * 16);
+    if (nd) {  // dict_index_block needs the page + 32 bytes within the kRunWaves windows (+ 32 each)
+        const uint32_t per_wave = (dict_max + 32 + kRunWaves - 1) / kRunWaves;
+        const uint32_t ws = ((per_wave > 32 ? per_wave - 32 : 0u) + 15) / 16 * 16;
+        wstage = max(wstage, min(kRunStage, ws));
+    }
+    const uint32_t lds = kRunWaves * (wstage / 4 + 8) * 4;
+    ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_runs), lds);
+    hipLaunchKernelGGL(k_pipe_runs, dim3(nd + (max(npages, 0) + per - 1) / per), dim3(kRunWaves * kWave), lds, s,
                        bytes, pages, npages, max_def, max_rep, runs, info, ppw, flist,
-                       stage_max ? min(stage_max, kStage3 - 16) : kStage3 - 16, d, debug);
+                       stage_max ? min(stage_max, kStage3 - 16) : kStage3 - 16, d, debug, wstage);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's

@@ -209,7 +209,8 @@ struct RunDicts {
 constexpr uint32_t kRunDictMax = 60 * 1024;
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist, int debug,
-                      const RunDicts* dicts = nullptr, uint32_t stage_max = 0);  // 0: k_pipe_codes3's stage
+                      const RunDicts* dicts = nullptr, uint32_t stage_max = 0,  // 0: k_pipe_codes3's stage
+                      uint32_t slot_max = 0, uint32_t dict_max = 0, int cus = 256);  // pages_per_wave 0: auto
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 // k_pipe_front: the whole front (run headers -> u16 codes, tile characters)
 // of chunks whose pages hold <= kTileRows rows, one wavefront per window of
