@@ -87,8 +87,10 @@ def _mutants(n, seed):
             for rec in col:
                 if rec["rc"] == 0 and rec.get("pages"):
                     items.append((name, path, rec["chunk"]))
+    from pqgpu import capi
+    from util import to_desc
     out = []
-    for k in range(n):
+    while len(out) < n:
         name, path, chunk = items[rng.randrange(len(items))]
         with open(path, "rb") as fh:
             f = bytearray(fh.read())
@@ -97,6 +99,11 @@ def _mutants(n, seed):
         for _ in range(rng.randint(1, 3)):
             p = rng.randrange(lo, hi)
             f[p] = rng.choice([f[p] ^ (1 << rng.randrange(8)), rng.randrange(256), (f[p] + 1) & 255, 0])
+        # a mutated count can declare billions of rows: fine for the walk, but
+        # not a case to decode on the CPU oracle (or to hold in host memory)
+        _, _, table = capi.build_page_table(bytes(f), to_desc(O.Chunk(*chunk)))
+        if sum(max(p.num_values, 0) for p in table if p.page_type in (0, 2)) > 2_000_000:
+            continue
         out.append((name, bytes(f), chunk))
     return out
 
