@@ -33,7 +33,10 @@ bool Thrift::field(int16_t& id, uint8_t& type) {  // thrift.cpp:6-21
     int16_t delta = (b >> 4) & 0x0F;
     id = delta ? static_cast<int16_t>(last_ + delta) : static_cast<int16_t>(c_.zigzag());
     last_ = id;
-    return true;
+    // a nonzero byte whose type nibble is 0 (so delta != 0) is a STOP too: every
+    // struct loop of the reference breaks on fh.type == CT_STOP (metadata.cpp:8 ff.,
+    // thrift.cpp:110), not on the byte
+    return type != 0;
 }
 
 std::string Thrift::str() {  // thrift.cpp:35-39
@@ -452,7 +455,7 @@ private:
             id = static_cast<int16_t>(z);
         }
         last = id;
-        if (type == 0) type = 0x10;  // a field of wire type 0 is not STOP: skip() rejects it like Thrift::skip
+        if (type == 0) id = 0;  // type nibble 0 ends the struct like the STOP byte (Thrift::field)
         return true;
     }
     bool bytes(uint64_t n) { if (n > static_cast<uint64_t>(e_ - p_)) return false; p_ += n; return true; }

@@ -165,3 +165,28 @@ def _limited(jobs, q):
     import resource
     resource.setrlimit(resource.RLIMIT_AS, (8 << 30, 8 << 30))
     _ref_worker(jobs, q)
+
+
+@pytest.mark.parametrize("seed", [11, 23])
+def test_mutants_walk_matches_oracle(seed):
+    """The host page walk (pq_build_page_table, format.cpp) fails on a mutant
+    only where the oracle's read_all fails too, and with the same code and
+    message unless a payload error of an earlier page comes first in the
+    reference's read order; a walk that succeeds leaves no header error for
+    the read.  E.g. a header byte whose type nibble is 0 ends its struct like
+    the STOP byte (metadata.cpp:90-104 breaks on fh.type == CT_STOP): it is not
+    a field skipped into "ThriftReader::skip: unknown type 0"."""
+    from pqgpu import capi
+    from util import to_desc
+    same = failed = 0
+    for i, (name, f, chunk) in enumerate(_mutants(240, seed)):
+        ch = O.Chunk(*chunk)
+        rc_w, msg_w, _ = capi.build_page_table(f, to_desc(ch))
+        rc_o, msg_o, _ = O.read_all(f, ch)
+        if rc_w == 0:
+            assert rc_o == 0 or "Thrift" not in msg_o, (name, i, msg_o)
+            continue
+        failed += 1
+        assert rc_o != 0, (name, i, rc_w, msg_w)
+        same += (rc_w, msg_w) == (rc_o, msg_o)
+    assert failed >= 2 and same >= failed - 1, (failed, same)
