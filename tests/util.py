@@ -6,6 +6,8 @@ from pqgpu import capi
 
 
 def to_oracle_chunk(d) -> O.Chunk:
+    if isinstance(d, O.Chunk):
+        return d
     if isinstance(d, dict):
         return O.Chunk(d["num_values"], d["data_page_offset"], d["dictionary_page_offset"],
                        d["codec"], d["type"], d["max_def"], d["max_rep"])
