@@ -2143,7 +2143,7 @@ __global__ void __launch_bounds__(64) k_pipe_exact(CodeArgs a, const int32_t* __
     const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
     const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
     for (int i = static_cast<int>(blockIdx.x); i < nf; i += static_cast<int>(gridDim.x)) {
-        exact_page(a, L, flist[1 + i], dict_n, ebase);
+        exact_page_body(a, L, flist[1 + i], dict_n, ebase);  // inlined: a call spills CodeArgs to scratch
         __builtin_amdgcn_wave_barrier();
     }
 }
