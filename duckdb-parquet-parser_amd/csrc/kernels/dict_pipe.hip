@@ -249,8 +249,8 @@ __device__ void fail_page(const CodeArgs& a, const DevPage& pg, int32_t t0, uint
 
 // Exact decoder for a marked page: the reference state machine (stream.hpp)
 // over the page in HBM, tile by tile; same error order as k_ba_fused.
-// (the body is inlined where the scratch is a dynamic per-wave LDS area —
-// a call would pass it as a generic pointer — and called elsewhere)
+// (always inlined: a call would pass the LDS scratch as a generic pointer and
+// spill CodeArgs to scratch memory)
 __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n, uint32_t ebase) {
     const DevPage pg = a.pages[p];
     const uint8_t* page = a.bytes + pg.off;
@@ -358,10 +358,6 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
         tile_done(a, t0 + static_cast<int>(ti), chars);
         __builtin_amdgcn_wave_barrier();
     }
-}
-
-__device__ __noinline__ void exact_page(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n, uint32_t ebase) {
-    exact_page_body(a, L, p, dict_n, ebase);
 }
 
 // The run covering value `v` among `nr` records held two per lane in LDS:
