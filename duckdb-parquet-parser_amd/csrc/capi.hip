@@ -96,6 +96,7 @@ struct pq_ctx {
     PVec<pqk::DevTile> s_htiles;
     PVec<pqk::RelayoutEntry> s_ents;
     bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
+    bool opt_pipe_wide = true;   // "pipe_wide": dictionaries beyond the writer's LDS / 65,535 entries on the pipe (k_pipe_wwide)
     bool opt_wide_rows = true;  // "wide_rows": generic BYTE_ARRAY rows by a workgroup per page (k_wide_rows)
     bool opt_levels_small = true;  // "levels_small": k_fixed_levels2 in its 35 KB LDS form (4 workgroups per CU)
     bool opt_gather_rows = true;  // "gather_rows": k_ba_gather copies characters row per lane (0: byte-wise blocks)
@@ -195,6 +196,7 @@ struct pq_chunk {
     int32_t* d_flist = nullptr;
     bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
     uint32_t pipe_small_bytes = 0;      // the largest payload of those pages
+    bool pipe_wide = false;             // 32-bit codes, dictionary in HBM (k_pipe_big<true> -> k_pipe_wwide)
     bool pipe_fr = false;               // every page <= kTileRows rows, every slot <= kFrontWin: k_pipe_front
     std::vector<pqk::DevBatch> hfwins;  // its windows of consecutive pages
     pqk::DevBatch* d_fwins = nullptr;
@@ -480,8 +482,51 @@ void free_chunk_device(pq_chunk* c) {
 
 // The three-pass dictionary path (dict_pipe.hip) takes a BYTE_ARRAY chunk
 // whose data pages all use one dictionary page that fits in LDS.
+// Dictionaries the writer's LDS cannot hold (or of more than 65,535 entries):
+// every page through k_pipe_big<true> (32-bit codes, index bit widths up to
+// 24, entry lengths from HBM), then k_pipe_wwide, which reads the entry words
+// and characters from HBM/L2.  Called by plan_pipe after its page checks
+// (dictionary-encoded pages of one dictionary).
+static void plan_pipe_wide(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const DevDict& d, int32_t dict_id) {
+    if (!ctx->opt_pipe_wide) return;
+    std::vector<int32_t> big;
+    uint32_t big_bytes = 0;
+    big.reserve(pages.size());
+    for (size_t i = 0; i < pages.size(); i++) {
+        const DevPage& pg = pages[i];
+        if (pg.nvals > pqk::kBigTiles * pqk::kTileRows || static_cast<uint32_t>(pg.size) > pqk::kBigMaxBytes) return;
+        big.push_back(static_cast<int32_t>(i));
+        big_bytes = std::max(big_bytes, static_cast<uint32_t>(pg.size));
+    }
+    if (pqk::pipe_big_lds(big_bytes, 0) > 160u * 1024) return;
+    const int wpw = std::max(1, std::min(16, ctx->opt_write_waves));
+    pqk::PipePlan pl = pqk::plan_pipe_wide(wpw);
+    if (pl.blocks_per_cu == 0) return;
+    if (ctx->opt_write_bpc > 0) pl.blocks_per_cu = std::min(pl.blocks_per_cu, ctx->opt_write_bpc);
+    c->pipe = true;
+    c->pipe_wide = true;
+    c->pipe_small = false;
+    c->pipe_small_bytes = 0;
+    c->pipe_count = false;
+    c->hbig = std::move(big);
+    c->big_max_bytes = big_bytes;
+    c->pipe_dict = dict_id;
+    c->pipe_dict_payload = static_cast<uint32_t>(d.size);
+    c->pipe_entry_base = d.entry_base;
+    c->pipe_dict_chars_bytes = 0;
+    c->pipe_dict_bytes = 0;
+    c->pipe_lds = pl.lds;
+    c->pipe_grid = ctx->cus * pl.blocks_per_cu;
+    c->pipe_ecap = static_cast<uint32_t>(std::min<int64_t>(d.nvals, d.size / 4 + 1));
+    c->pipe_cus = ctx->cus;
+    c->pipe_wpw = wpw;
+    c->fused_ok = false;
+    c->pipe_fr = false;
+}
+
 void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::vector<DevDict>& dicts) {
     c->pipe = false;
+    c->pipe_wide = false;
     c->pipe_count = false;
     c->pipe_small = false;
     c->pipe_fr = false;
@@ -510,7 +555,8 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
         dict_id = pg.dict;
     }
     const DevDict& d = dicts[dict_id];
-    if (d.size < 0 || d.size > 65536 - 64 || d.nvals < 0 || d.nvals > 65535) return;
+    if (d.size < 0 || d.nvals < 0) return;
+    if (d.size > 65536 - 64 || d.nvals > 65535) return plan_pipe_wide(ctx, c, pages, d, dict_id);
     const int64_t ecap = std::min<int64_t>(d.nvals, d.size / 4 + 1);
     if (!big.empty() && pqk::pipe_big_lds(big_bytes, std::min<uint32_t>(static_cast<uint32_t>(ecap), pqk::kBigLens)) > 160u * 1024)
         return;
@@ -518,7 +564,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     const uint32_t dict_bytes = 16 + chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
     const int wpw = std::max(1, std::min(16, ctx->opt_write_waves));
     pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes, wpw);
-    if (pl.blocks_per_cu == 0) return;
+    if (pl.blocks_per_cu == 0) return plan_pipe_wide(ctx, c, pages, d, dict_id);
     if (ctx->opt_write_bpc > 0) pl.blocks_per_cu = std::min(pl.blocks_per_cu, ctx->opt_write_bpc);
     const int cus = ctx->cus;
     c->pipe = true;
@@ -884,6 +930,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     DevGuard dg(ctx);
     if (std::strcmp(key, "fused_ba") == 0) { ctx->opt_fused = value != 0; return 0; }
     if (std::strcmp(key, "wide_rows") == 0) { ctx->opt_wide_rows = value != 0; return 0; }
+    if (std::strcmp(key, "pipe_wide") == 0) { ctx->opt_pipe_wide = value != 0; return 0; }
     if (std::strcmp(key, "levels_small") == 0) { ctx->opt_levels_small = value != 0; return 0; }
     if (std::strcmp(key, "gather_rows") == 0) { ctx->opt_gather_rows = value != 0; return 0; }
     if (std::strcmp(key, "fused_debug") == 0) { ctx->opt_debug = static_cast<int>(value); return 0; }
@@ -1491,7 +1538,8 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         if (c->pipe) {
             rc |= dalloc(&c->d_runs, hpages.size() * 2 * pqk::kPipeRunCap);
             rc |= dalloc(&c->d_info, hpages.size());
-            rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) + 64);
+            // u16 codes, or u32 on the wide pipe (d_codes then holds 2 per row)
+            rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) * (c->pipe_wide ? 2 : 1) + 64);
             rc |= dalloc(&c->d_tile_nn, htiles.size());
             if (!c->hbig.empty()) rc |= dalloc(&c->d_bigp, c->hbig.size());
             if (!c->hfwins.empty()) rc |= dalloc(&c->d_fwins, c->hfwins.size());
@@ -1949,6 +1997,10 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     P.ntiles = c->ntiles; P.page_tile0 = c->d_page_tile0; P.max_def = c->max_def; P.max_rep = c->max_rep;
     P.dicts = c->d_dicts; P.dict_id = c->pipe_dict; P.entries = c->d_entries; P.dict_count = c->d_dict_count;
     P.runs = c->d_runs; P.info = c->d_info; P.flist = c->d_flist; P.tile_nn = c->d_tile_nn; P.codes = c->d_codes;
+    if (c->pipe_wide) {
+        P.codes32 = reinterpret_cast<uint32_t*>(c->d_codes);
+        P.codes = nullptr;
+    }
     P.tile_chars = c->d_tile_chars; P.bsum = c->d_bsum; P.total = c->d_total;
     P.nrows_total = c->nrows; P.overflow = c->d_flags + 1;
     if (out) {
@@ -2603,7 +2655,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
     try {
         hipStream_t s = ctx->stream;
         pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
-        const bool on_codes = c->pipe && ctx->opt_pipe && ctx->opt_regex_codes;
+        const bool on_codes = c->pipe && !c->pipe_wide && ctx->opt_pipe && ctx->opt_regex_codes;
         const bool reuse = on_codes && ctx->opt_regex_reuse && c->codes_ok;
         // over a checked decode's codes: k_regex_dict clears the status words
         // and sets the page flags itself (no fill kernels)
@@ -2690,7 +2742,7 @@ int pq_decode_regex_async(pq_ctx* ctx, pq_chunk* c, pq_column* out, const char* 
     // dictionary of < 32 KiB: the writer keeps each entry's match bit beside
     // its length); else the decode, then the scan over its codes
     const bool plain_go = c->plain && ctx->opt_plain;
-    const bool one = c->pipe && ctx->opt_pipe && ctx->opt_regex_codes && !plain_go && c->ndicts > 0 &&
+    const bool one = c->pipe && !c->pipe_wide && ctx->opt_pipe && ctx->opt_regex_codes && !plain_go && c->ndicts > 0 &&
                      c->pipe_dict_payload < pqk::kArmDictBytes;
     if (!one) {
         // the scan clears d_flags, which still holds this decode's status

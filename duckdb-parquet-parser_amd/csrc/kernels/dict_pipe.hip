@@ -23,6 +23,7 @@
 // Only pages of more than 512 rows with def levels need tile_nn, the
 // non-null counts of the earlier tiles of their page (k_pipe_codes<true>).
 #include <cstddef>
+#include <type_traits>
 #include "kernels/device_common.hpp"
 #include "kernels/dict_index.hpp"
 #include "kernels/kernels.hpp"
@@ -64,6 +65,21 @@ __device__ __forceinline__ void store_codes8(uint16_t* codes, int64_t R0, uint32
 #pragma unroll
         for (int k = 0; k < 8; k++)
             if (l8 + k < m) codes[R0 + l8 + k] = static_cast<uint16_t>(c[k]);
+    }
+}
+
+// 32-bit codes (dictionaries of more than 65,535 entries or beyond the
+// writer's LDS: k_pipe_big<true> -> k_pipe_wwide); 0xFFFFFFFF = NULL
+constexpr uint32_t kNull32 = 0xFFFFFFFFu;
+__device__ __forceinline__ void store_codes8w(uint32_t* codes, int64_t R0, uint32_t l8, uint32_t m, const uint32_t c[8]) {
+    if (l8 + 8 <= m) {
+        U16B* d = reinterpret_cast<U16B*>(codes + R0 + l8);
+        d[0] = U16B{c[0], c[1], c[2], c[3]};
+        d[1] = U16B{c[4], c[5], c[6], c[7]};
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (l8 + k < m) codes[R0 + l8 + k] = c[k];
     }
 }
 
@@ -229,6 +245,7 @@ struct CodeArgs {
     int per;                   // tiles per k_pipe_write wavefront
     int debug;                 // 256: skip the exact decoder (timing only)
     int wpw;                   // k_pipe_write's writer waves per workgroup (bsum index)
+    uint32_t* codes32 = nullptr;  // wide chunks: 32-bit codes here instead of `codes` (k_pipe_big<true>)
 };
 
 // Characters of tile t also go to the k_pipe_write workgroup that writes it.
@@ -243,7 +260,10 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return bcast_last(wav
 
 // Rows of a page the decode failed on: NULL codes, no characters.
 __device__ void fail_page(const CodeArgs& a, const DevPage& pg, int32_t t0, uint32_t n) {
-    for (uint32_t j = lane(); j < n; j += kWave) a.codes[pg.first_row + j] = kNull;
+    for (uint32_t j = lane(); j < n; j += kWave) {
+        if (a.codes32) a.codes32[pg.first_row + j] = kNull32;
+        else a.codes[pg.first_row + j] = kNull;
+    }
     for (uint32_t t = lane(); t * kTileRows < n; t += kWave) a.tile_chars[t0 + t] = 0;
 }
 
@@ -251,7 +271,10 @@ __device__ void fail_page(const CodeArgs& a, const DevPage& pg, int32_t t0, uint
 // over the page in HBM, tile by tile; same error order as k_ba_fused.
 // (always inlined: a call would pass the LDS scratch as a generic pointer and
 // spill CodeArgs to scratch memory)
+template <bool kWide = false>
 __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n, uint32_t ebase) {
+    using CodeT = typename std::conditional<kWide, uint32_t, uint16_t>::type;
+    constexpr CodeT kNullT = kWide ? static_cast<CodeT>(kNull32) : static_cast<CodeT>(kNull);
     const DevPage pg = a.pages[p];
     const uint8_t* page = a.bytes + pg.off;
     const uint32_t size = static_cast<uint32_t>(max(pg.size, 0));
@@ -259,8 +282,12 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
     const int32_t t0 = a.page_tile0[p];
     DevErr* err = a.page_err + p;
     uint8_t* lv = L.mark;
-    uint16_t* ix = reinterpret_cast<uint16_t*>(L.recd);
-    LitRun* lits = reinterpret_cast<LitRun*>(L.reci);
+    // a tile's indices: u16 in recd; u32 over recd and reci (the literal
+    // runs then go to mark2, unused here)
+    static_assert(sizeof(L.recd) + sizeof(L.reci) >= kTileRows * 4 && sizeof(L.mark2) >= kLitCapP * sizeof(LitRun) &&
+                      offsetof(CodeLds, reci) == sizeof(L.recd), "exact decoder scratch");
+    CodeT* ix = reinterpret_cast<CodeT*>(L.recd);
+    LitRun* lits = kWide ? reinterpret_cast<LitRun*>(L.mark2) : reinterpret_cast<LitRun*>(L.reci);
     const uint32_t md = static_cast<uint32_t>(a.max_def);
     uint32_t pos = 0, dbase = 0, dlen = 0;
     auto fail = [&](int code, uint32_t ep, uint32_t need) {
@@ -318,7 +345,7 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
     srle_init(def, dbase, dlen, bwd);
     srle_init(idx, pos, size - pos, bwi);
     auto put_ix = [&](uint32_t k, uint32_t v) {
-        ix[k] = static_cast<uint16_t>(static_cast<int32_t>(v) >= 0 && v < dict_n ? v : kNull);
+        ix[k] = static_cast<CodeT>(static_cast<int32_t>(v) >= 0 && v < dict_n ? v : static_cast<uint32_t>(kNullT));
     };
     for (uint32_t r0 = 0, ti = 0; r0 < n; r0 += kTileRows, ti++) {
         const uint32_t m = min(n - r0, static_cast<uint32_t>(kTileRows));
@@ -347,12 +374,15 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
             const bool nnul = (vm >> lane()) & 1ull;
             const uint32_t k = rank + popc_below(vm);
             rank += __popcll(vm);
-            uint16_t code = kNull;
+            CodeT code = kNullT;
             if (nnul) {
                 code = ix[k];
-                if (code != kNull) chars += static_cast<uint32_t>(a.entries[ebase + code] >> 32);
+                if (code != kNullT) chars += static_cast<uint32_t>(a.entries[ebase + code] >> 32);
             }
-            if (j < m) a.codes[pg.first_row + r0 + j] = code;
+            if (j < m) {
+                if (kWide) a.codes32[pg.first_row + r0 + j] = code;
+                else a.codes[pg.first_row + r0 + j] = static_cast<uint16_t>(code);
+            }
         }
         chars = wave_sum(chars);
         tile_done(a, t0 + static_cast<int>(ti), chars);
@@ -893,6 +923,7 @@ struct WriteArgs {
     const uint8_t* match;
     int match_neg;
     uint8_t* page_flags;
+    const uint32_t* codes32 = nullptr;  // wide chunks (k_pipe_wwide)
 };
 
 
@@ -1178,6 +1209,257 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
 }
 
 
+// ── the writer for wide dictionaries (k_pipe_wwide) ────────────────────────
+// Dictionaries the writer's LDS cannot hold, or of more than 65,535 entries
+// (pyarrow's 1 MiB dictionary pages): k_pipe_write's structure (persistent
+// workgroups, a contiguous tile range per wave, first output bytes from the
+// per-workgroup character sums k_pipe_big filed) over 32-bit codes, with the
+// entry words (len << 32 | payload position) and the characters read from
+// HBM, where a dictionary of a few MB stays in L2 across the decode.
+struct __attribute__((aligned(16))) WideLds {
+    uint32_t off[kTileRows + 4];  // tile-relative first byte per row (+ the end at [m])
+    uint32_t src[kTileRows];      // dictionary payload byte per row
+    uint8_t vb[kWave];            // validity bits of rows 8l .. 8l + 7
+};
+static_assert(sizeof(WideLds) % 16 == 0, "per-wave scratch alignment");
+constexpr int kWideBatch = 2;  // tiles whose codes a wave loads at once (8 u32 per lane each)
+
+__global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.znext)  // the other flags/bsum/flist block, for the next decode (unused by this one)
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.znext_words; i += gridDim.x * blockDim.x) a.znext[i] = 0;
+    const uint32_t wv = threadIdx.x / kWave;
+    WideLds& S = reinterpret_cast<WideLds*>(smem)[wv];
+    const DevDict d = a.dicts[a.dict_id];
+    const uint32_t dict_n = static_cast<uint32_t>(max(a.dict_count[a.dict_id], 0));
+    const uint64_t* es = a.entries + d.entry_base;
+    const uint8_t* dsrc = a.bytes + d.off;  // the dictionary payload slot (>= 16 zero bytes past its end)
+    const int per = a.per;
+    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
+    const int tb = min(a.ntiles, ta + per);
+    __shared__ unsigned long long red[kWriteMax];
+    auto wave_sum64 = [](unsigned long long v) {
+        for (int dd = 1; dd < kWave; dd <<= 1) {
+            const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), dd));
+            const uint32_t hi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v >> 32), dd));
+            v += (static_cast<unsigned long long>(hi) << 32) | lo;
+        }
+        return v;
+    };
+    unsigned long long acc = 0, in = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) acc += a.bsum[b];
+    {
+        const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
+        for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
+    }
+    acc = wave_sum64(acc);
+    if (lane() == 0) red[wv] = acc;
+    in = wave_sum64(in);
+    __syncthreads();
+    int64_t Grun = static_cast<int64_t>(in);
+    for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
+    if (a.debug & 8) return;
+    const uint32_t l8 = lane() * kRowsPerLane;
+    auto rl64 = [](int64_t v, int i) -> int64_t {
+        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
+        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), i);
+        return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+    };
+    for (int c0 = ta; c0 < tb; c0 += kWave) {
+        const int cn = min(kWave, tb - c0);
+        int64_t myR0 = 0, myG0 = 0;
+        uint32_t mym = 0, myc = 0;
+        if (static_cast<int>(lane()) < cn) {
+            const DevTile T = a.tiles[c0 + lane()];
+            myR0 = a.pages[T.page].first_row + T.row0;
+            mym = static_cast<uint32_t>(T.nrows);
+            myc = static_cast<uint32_t>(a.tile_chars[c0 + lane()]);
+        }
+        {
+            const uint32_t inc = wave_incl_scan(myc);
+            myG0 = Grun + static_cast<int64_t>(inc - myc);
+            Grun += static_cast<int64_t>(bcast_last(inc));
+        }
+        for (int ib = 0; ib < cn; ib += kWideBatch) {
+            static_assert(kWideBatch == 2, "batch registers");
+            auto ld = [&](int i, uint4& lo, uint4& hi) {
+                lo = hi = make_uint4(kNull32, kNull32, kNull32, kNull32);
+                if (i < cn) {
+                    const int64_t R = rl64(myR0, i);
+                    const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
+                    if (l8 + 8 <= mm) {
+                        const U16B* p = reinterpret_cast<const U16B*>(a.codes32 + R + l8);
+                        const U16B x = p[0], y = p[1];
+                        lo = make_uint4(x.x, x.y, x.z, x.w);
+                        hi = make_uint4(y.x, y.y, y.z, y.w);
+                    } else if (l8 < mm) {
+                        uint32_t c[8];
+#pragma unroll
+                        for (int k = 0; k < 8; k++) c[k] = l8 + k < mm ? a.codes32[R + l8 + k] : kNull32;
+                        lo = make_uint4(c[0], c[1], c[2], c[3]);
+                        hi = make_uint4(c[4], c[5], c[6], c[7]);
+                    }
+                }
+            };
+            uint4 c0lo, c0hi, c1lo, c1hi;
+            ld(ib, c0lo, c0hi);
+            ld(ib + 1, c1lo, c1hi);
+            for (int i = ib; i < min(cn, ib + kWideBatch); i++) {
+                const int64_t R0 = rl64(myR0, i);
+                const int64_t G0 = rl64(myG0, i);
+                const uint32_t m = __builtin_amdgcn_readlane(mym, i);
+                const bool first = i == ib;
+                const uint4 lo = first ? c0lo : c1lo, hi = first ? c0hi : c1hi;
+                const uint32_t cur[kRowsPerLane] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+                // this lane's rows 8l .. 8l + 7: entry words (all eight loads in flight)
+                uint64_t e[kRowsPerLane];
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++) e[k] = dict_n ? es[min(cur[k], dict_n - 1u)] : 0ull;
+                uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc8 = 0;
+#pragma unroll
+                for (int k = 0; k < kRowsPerLane; k++) {
+                    const bool valid = cur[k] < dict_n;
+                    len[k] = valid ? static_cast<uint32_t>(e[k] >> 32) : 0u;
+                    src[k] = valid ? static_cast<uint32_t>(e[k]) : 0u;
+                    vb |= (valid ? 1u : 0u) << k;
+                    acc8 += len[k];
+                }
+                const uint32_t incl = wave_incl_scan(acc8);
+                const uint32_t total = bcast_last(incl);
+                {
+                    uint32_t o[kRowsPerLane];
+                    o[0] = incl - acc8;
+#pragma unroll
+                    for (int k = 1; k < kRowsPerLane; k++) o[k] = o[k - 1] + len[k - 1];
+                    uint4* po = reinterpret_cast<uint4*>(&S.off[lane() * kRowsPerLane]);
+                    po[0] = make_uint4(o[0], o[1], o[2], o[3]);
+                    po[1] = make_uint4(o[4], o[5], o[6], o[7]);
+                    uint4* ps = reinterpret_cast<uint4*>(&S.src[lane() * kRowsPerLane]);
+                    ps[0] = make_uint4(src[0], src[1], src[2], src[3]);
+                    ps[1] = make_uint4(src[4], src[5], src[6], src[7]);
+                }
+                S.vb[lane()] = static_cast<uint8_t>(vb);
+                if (lane() == 0) S.off[m] = total;
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                if (!(a.debug & 4)) {  // offsets and validity words as k_pipe_write stores them
+                    if ((R0 & 1) == 0) {
+#pragma unroll
+                        for (int k = 0; k < kRowsPerLane / 2; k++) {
+                            const uint32_t j = k * 2 * kWave + 2 * lane();
+                            if (j + 1 < m) {
+                                const uint2 o = *reinterpret_cast<const uint2*>(&S.off[j]);
+                                const int64_t v0 = G0 + o.x, v1 = G0 + o.y;
+                                *reinterpret_cast<uint4*>(a.offsets + R0 + j) =
+                                    make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(static_cast<uint64_t>(v0) >> 32),
+                                               static_cast<uint32_t>(v1), static_cast<uint32_t>(static_cast<uint64_t>(v1) >> 32));
+                            } else if (j < m) {
+                                a.offsets[R0 + j] = G0 + S.off[j];
+                            }
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < kRowsPerLane; k++) {
+                            const uint32_t j = k * kWave + lane();
+                            if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
+                        }
+                    }
+                    const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
+                    const uint32_t sh = static_cast<uint32_t>(R0 & 31);
+                    const int64_t g = gfirst + lane();
+                    if (g <= glast) {
+                        auto tw = [&](int t) -> uint32_t {
+                            return (t >= 0 && t < kWave / 4) ? reinterpret_cast<const uint32_t*>(S.vb)[t] : 0u;
+                        };
+                        const int t = static_cast<int>(lane());
+                        const uint32_t val = (tw(t) << sh) | (sh ? (tw(t - 1) >> (32 - sh)) : 0u);
+                        const bool whole = g * 32 >= R0 && (g * 32 + 32 <= R0 + m || R0 + m == a.nrows_total);
+                        if (whole) a.validity[g] = val;
+                        else if (val) atomicOr(&a.validity[g], val);
+                    }
+                }
+                if (R0 + m == a.nrows_total && lane() == 0) {
+                    a.offsets[a.nrows_total] = G0 + total;
+                    *a.total = G0 + total;
+                }
+                if (total == 0 || (a.debug & 2)) continue;
+                if (G0 + total > a.capacity) {
+                    if (lane() == 0) atomicOr(a.overflow, 1);
+                    continue;
+                }
+                // characters, 64 consecutive rows per group, row per lane.
+                // Rows of <= 16 bytes: two 8-byte loads per row (bytes 0..7 and
+                // ln-8..ln-1; the slot's zero padding covers reads past the
+                // payload) for four groups before any of their stores, then
+                // two overlapping 8/4/2-byte stores inside the row.
+                for (uint32_t h = 0; h < m; h += 4 * kWave) {
+                    uint32_t s0[4], ln[4];
+                    U8B A[4], B[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t r = h + q * kWave + lane();
+                        s0[q] = 0;
+                        ln[q] = 0;
+                        uint32_t sa = 0;
+                        if (r < m) {
+                            s0[q] = S.off[r];
+                            ln[q] = S.off[r + 1] - s0[q];
+                            sa = S.src[r];
+                        }
+                        const uint32_t l16 = ln[q] <= 16 ? ln[q] : 0u;
+                        A[q] = *reinterpret_cast<const U8B*>(dsrc + sa);
+                        B[q] = *reinterpret_cast<const U8B*>(dsrc + sa + (l16 >= 8 ? l16 - 8 : 0u));
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t L = ln[q];
+                        uint8_t* dd = a.chars + G0 + s0[q];
+                        if (L >= 8 && L <= 16) {
+                            *reinterpret_cast<U8B*>(dd) = A[q];
+                            *reinterpret_cast<U8B*>(dd + L - 8) = B[q];
+                        } else if (L >= 4 && L < 8) {
+                            *reinterpret_cast<U4B*>(dd) = U4B{A[q].x};
+                            *reinterpret_cast<U4B*>(dd + L - 4) = U4B{__builtin_amdgcn_alignbyte(A[q].y, A[q].x, L - 4)};
+                        } else if (L >= 2 && L < 4) {
+                            *reinterpret_cast<U2B*>(dd) = U2B{static_cast<uint16_t>(A[q].x)};
+                            *reinterpret_cast<U2B*>(dd + L - 2) = U2B{static_cast<uint16_t>(A[q].x >> (8 * (L - 2)))};
+                        } else if (L == 1) {
+                            dd[0] = static_cast<uint8_t>(A[q].x);
+                        }
+                    }
+                    // rows of 17 .. kLongRow bytes: the lane's own loop; longer rows: the wave
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t r = h + q * kWave + lane();
+                        const uint32_t L = ln[q];
+                        if (L > 16 && L <= kLongRow) {
+                            const uint8_t* sp = dsrc + S.src[r];
+                            uint8_t* dd = a.chars + G0 + s0[q];
+                            for (uint32_t x = 0; x + 16 < L; x += 16)
+                                *reinterpret_cast<U16B*>(dd + x) = *reinterpret_cast<const U16B*>(sp + x);
+                            *reinterpret_cast<U16B*>(dd + L - 16) = *reinterpret_cast<const U16B*>(sp + L - 16);
+                        }
+                        uint64_t lm = __ballot(L > kLongRow);
+                        while (lm) {
+                            const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
+                            lm &= lm - 1;
+                            const uint32_t rl = h + q * kWave + l;
+                            const uint32_t LL = __builtin_amdgcn_readlane(L, l);
+                            const uint8_t* sp = dsrc + S.src[rl];
+                            uint8_t* dd = a.chars + G0 + __builtin_amdgcn_readlane(s0[q], l);
+                            for (uint32_t x = 16 * lane(); x < LL; x += 16 * kWave) {
+                                const uint32_t xx = min(x, LL - 16);  // the last block overlaps (same bytes)
+                                *reinterpret_cast<U16B*>(dd + xx) = *reinterpret_cast<const U16B*>(sp + xx);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+
 // ── pages of more than kPipeSmallRows rows (arrow layout) ──────────────────
 // One workgroup per page, its payload staged in LDS.  A stream of ~1-2k runs
 // is too long for the lane walk above, so its run headers are found by a
@@ -1355,6 +1637,9 @@ __device__ void big_scan(uint32_t* v, uint32_t m, uint32_t* part) {
     __syncthreads();
 }
 
+// kWide: 32-bit codes (a.codes32) and index bit widths up to 24, entry
+// lengths from the HBM entry table (dictionaries of more than 65,535 entries)
+template <bool kWide>
 __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int32_t* __restrict__ bigp,
                                                           uint32_t* __restrict__ info, uint32_t nlens) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1388,7 +1673,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     // so no further launch is needed after the big pages
     auto to_exact = [&]() {
         if (tid == 0) info[p] = kFallback;
-        if (wv == 0) exact_page_body(a, *reinterpret_cast<CodeLds*>(smem), p, dict_n, ebase);
+        if (wv == 0) exact_page_body<kWide>(a, *reinterpret_cast<CodeLds*>(smem), p, dict_n, ebase);
     };
     if (n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes) return to_exact();
 
@@ -1424,7 +1709,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         if (pos + 1 > size) flag = true;
         else { bwi = rd32(pos) & 0xFFu; pos += 1; }
     }
-    if (!flag && bwi > 16) flag = true;
+    if (!flag && bwi > (kWide ? 24u : 16u)) flag = true;
     if (flag) {
         __syncthreads();  // every wave has read the stage before wave 0 reuses it
         return to_exact();
@@ -1517,7 +1802,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         const uint32_t slot = isd ? i : Ly.LC + li;
         uint32_t q = ent[slot];
         const uint32_t e = isd ? dend : iend, bw = isd ? bwd : bwi, nbv = (bw + 7) / 8;
-        const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
+        const uint32_t vmask = nbv >= 3 ? 0xFFFFFFu : (nbv == 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u));
         const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
         uint2* out = (isd ? recd : reci) + li * kBJump;
         uint32_t s = 0, sum = 0, bad = kBJump, ended = 0;
@@ -1648,18 +1933,23 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
             const uint32_t lb = big_bits(stw, nw, rr_pay(R) + __umul24(k0 + rk - rr_start(R), bwi), bwi);
             const uint32_t v = keep_if(rr_lit(R), lb) | keep_if(!rr_lit(R), rr_pay(R));
             const bool ok = nz && v < dict_n;
-            const uint32_t code = keep_if(ok, v) | keep_if(!ok, kNull);
-            const bool inl = ok && v < nl;
-            chars += keep_if(inl, lens[inl ? v : 0u]);
-            far |= (ok && !inl ? 1u : 0u) << k;
+            const uint32_t code = keep_if(ok, v) | keep_if(!ok, kWide ? kNull32 : kNull);
+            if (kWide) {  // lengths from the entry table (L2): all eight loads in flight
+                if (dict_n) chars += keep_if(ok, static_cast<uint32_t>(a.entries[ebase + (ok ? v : 0u)] >> 32));
+            } else {
+                const bool inl = ok && v < nl;
+                chars += keep_if(inl, lens[inl ? v : 0u]);
+                far |= (ok && !inl ? 1u : 0u) << k;
+            }
             cw8[k] = code;
         }
-        if (__ballot(far != 0)) {  // entries past the LDS length table (dictionaries over kBigLens)
+        if (!kWide && __ballot(far != 0)) {  // entries past the LDS length table (dictionaries over kBigLens)
 #pragma unroll
             for (int k = 0; k < 8; k++)
                 if ((far >> k) & 1u) chars += static_cast<uint32_t>(a.entries[ebase + cw8[k]] >> 32);
         }
-        store_codes8(a.codes, R0, l8, m, cw8);
+        if (kWide) store_codes8w(a.codes32, R0, l8, m, cw8);
+        else store_codes8(a.codes, R0, l8, m, cw8);
         chars = wave_sum(chars);
         tile_done(a, t0 + static_cast<int>(ti), chars);
         __builtin_amdgcn_wave_barrier();
@@ -2732,8 +3022,28 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     if (P.has_small) hipLaunchKernelGGL(k_pipe_codes3, dim3(grid), dim3(kCodeWaves3 * kWave), lds, s, a, lt_n, P.flist);
 }
 
+PipePlan plan_pipe_wide(int wpw) {
+    PipePlan pl{};
+    pl.lds = static_cast<uint32_t>(wpw) * static_cast<uint32_t>(sizeof(WideLds));
+    pl.blocks_per_cu = min(4, static_cast<int>((160u * 1024) / pl.lds));
+    const int occ = resident_blocks(reinterpret_cast<const void*>(k_pipe_wwide), wpw * kWave, pl.lds);
+    pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
+    return pl;
+}
+
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
     if (P.ntiles <= 0) return;
+    if (P.codes32) {  // wide dictionary: codes and dictionary from HBM
+        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_wwide), P.lds);
+        int grid = 0, per = 0;
+        write_shape(P, &grid, &per);
+        WriteArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.dicts, P.dict_id, P.entries, P.dict_count, nullptr,
+                    P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
+                    P.chars, 0u, 0u, P.debug, P.write_waves, P.znext, P.znext_words, nullptr, 0, nullptr};
+        a.codes32 = P.codes32;
+        hipLaunchKernelGGL(k_pipe_wwide, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
+        return;
+    }
     ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_write<false>), P.lds);
     ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_write<true>), P.lds);
     int grid = 0, per = 0;
@@ -2749,17 +3059,25 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
 }
 
 void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes) {
-    const uint32_t nlens = min(P.dict_entries_cap, kBigLens);
+    const bool wide = P.codes32 != nullptr;  // lengths from the HBM entry table
+    const uint32_t nlens = wide ? 0u : min(P.dict_entries_cap, kBigLens);
     if (nbig <= 0) return;
     int wgrid = 0, per = 0;
     write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_write's workgroups
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
                P.bsum, per, P.debug, P.write_waves};
+    a.codes32 = P.codes32;
     const uint32_t lds = big_layout(max_page_bytes, nlens).total;
-    ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_big), lds);
-    hipLaunchKernelGGL(k_pipe_big, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
-                       const_cast<uint32_t*>(P.info), nlens);
+    if (wide) {
+        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_big<true>), lds);
+        hipLaunchKernelGGL(k_pipe_big<true>, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
+                           const_cast<uint32_t*>(P.info), nlens);
+    } else {
+        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_big<false>), lds);
+        hipLaunchKernelGGL(k_pipe_big<false>, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
+                           const_cast<uint32_t*>(P.info), nlens);
+    }
 }
 
 uint32_t pipe_front_slot(uint32_t max_page_bytes) { return (max_page_bytes + 15) / 16 * 16 + 16; }

@@ -181,6 +181,10 @@ struct PipeLaunch {
     int32_t nunits = 0;
     uint32_t fstage = 0, flds = 0;
     int fgrid = 0, fwaves = 0;
+    // wide dictionaries (k_pipe_big<true> -> k_pipe_wwide): 32-bit codes
+    // here (0xFFFFFFFF = NULL) instead of `codes`; P.lds / P.grid are then
+    // plan_pipe_wide's
+    uint32_t* codes32 = nullptr;
 };
 constexpr uint32_t kArmDictBytes = 32768;  // every entry length < 2^15: the match bit rides in the entry word
 struct PipePlan {
@@ -188,6 +192,8 @@ struct PipePlan {
     int blocks_per_cu;  // 0: the dictionary does not fit
 };
 PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw);
+// k_pipe_wwide (dictionary in HBM): per-wave scratch only
+PipePlan plan_pipe_wide(int wpw);
 // k_pipe_fused: tiles per unit, and its LDS / resident workgroups per CU for
 // `wpw` waves per workgroup and a payload stage of `stage` bytes per wave
 int pipe_fused_tiles();
