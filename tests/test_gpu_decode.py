@@ -263,21 +263,40 @@ def _opt_plain_file(nvals, seed, null_frac=0.3, lmax=30, extra=b"", drop=0, all_
 
 
 def _huge_dict_file(n: int, seed: int, lmin: int = 1, lmax: int = 14, decl: int | None = None, tail: bytes = b"",
-                    cut: int = 0, nrows: int = 5000):
+                    cut: int = 0, nrows: int = 5000, pages: int = 1, mixed: bool = False, bw_add: int = 0):
     """A dictionary page beyond k_dict_index's LDS (> 128 KiB: the
-    multi-workgroup index, launch_dict_big) and one data page of indices
-    spread over the whole dictionary (17-bit codes when n > 65,536)."""
+    multi-workgroup index, launch_dict_big) and data pages of indices spread
+    over the whole dictionary (17-bit codes when n > 65,536; the wide pipe,
+    k_pipe_big<true> -> k_pipe_wwide): one RLE run per value, or (mixed)
+    bit-packed groups between RLE runs; bw_add widens the indices past what
+    the pipe's run parse takes (> 24 bits: the exact decoder's 32-bit codes)."""
     rng = np.random.default_rng(seed)
     vals = [bytes(rng.integers(97, 123, size=int(rng.integers(lmin, lmax + 1)), dtype=np.uint8)) for _ in range(n)]
     dpay = B.plain_ba(vals) + tail
     if cut:
         dpay = dpay[:-cut]
-    bw = max(1, int(n - 1).bit_length())
-    idx = [int(x) for x in rng.integers(0, n, size=nrows)]
-    stream = bytes([bw]) + b"".join(B.rle(1, v, bw) for v in idx)
-    return B.build_file([B.dict_header(len(dpay), n if decl is None else decl) + dpay,
-                         B.data_header(len(stream), nrows, 8) + stream], gen.BYTE_ARRAY, False, nrows,
-                        dict_at_start=True)
+    bw = max(1, int(n - 1).bit_length()) + bw_add
+    out = [B.dict_header(len(dpay), n if decl is None else decl) + dpay]
+    per = nrows // pages
+    for k in range(pages):
+        m = per if k < pages - 1 else nrows - per * (pages - 1)
+        idx = [int(x) for x in rng.integers(0, n, size=m)]
+        if mixed:
+            body, i = b"", 0
+            while i < m:
+                if rng.random() < 0.5 and m - i >= 8:
+                    g = int(min((m - i) // 8, rng.integers(1, 9)))
+                    body += B.bitpack(idx[i:i + 8 * g], bw)
+                    i += 8 * g
+                else:
+                    r = int(min(m - i, rng.integers(1, 20)))
+                    body += B.rle(r, idx[i], bw)
+                    i += r
+        else:
+            body = b"".join(B.rle(1, v, bw) for v in idx)
+        stream = bytes([bw]) + body
+        out.append(B.data_header(len(stream), m, 8) + stream)
+    return B.build_file(out, gen.BYTE_ARRAY, False, nrows, dict_at_start=True)
 
 
 def _rep_pages(ptype, nested, optional, rows_per_page, npages, seed, enc=0, dict_vals=None, spec_order=False,
@@ -371,6 +390,16 @@ CRAFTED = {
     "huge_dict_long": lambda: _huge_dict_file(3000, seed=83, lmin=60, lmax=140),
     "huge_dict_tail": lambda: _huge_dict_file(30000, seed=84, tail=b"\x07\x00\x00\x00garbage!" * 5),
     "huge_dict_fewer_used": lambda: _huge_dict_file(30000, seed=85, decl=20000),
+    # the wide pipe: bit-packed 17-bit indices between RLE runs over pages of
+    # 2,500 and of 400 rows (small pages take k_pipe_big there too); indices
+    # past a shorter declared count; 26-bit indices (the exact decoder)
+    "huge_dict_wide_mixed": lambda: _huge_dict_file(100000, seed=88, lmin=4, lmax=9, nrows=10000, pages=4, mixed=True),
+    "huge_dict_wide_small_pages": lambda: _huge_dict_file(90000, seed=89, lmin=2, lmax=30, nrows=4000, pages=10,
+                                                          mixed=True),
+    "huge_dict_wide_oob": lambda: _huge_dict_file(100000, seed=90, lmin=4, lmax=9, decl=70000, nrows=6000, pages=2,
+                                                  mixed=True),
+    "huge_dict_wide_bw26": lambda: _huge_dict_file(100000, seed=91, lmin=4, lmax=9, nrows=3000, pages=2, mixed=True,
+                                                   bw_add=9),
     # OPTIONAL PLAIN BYTE_ARRAY: a window page; a chunk-chain page whose values
     # start inside chunk 0 past its candidate range, one whose levels fill
     # several chunks; bytes after the last value (the one-pass form does not
