@@ -2655,7 +2655,8 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
     try {
         hipStream_t s = ctx->stream;
         pqk::ColumnParams cp{c->type, c->max_def, c->max_rep, c->width, c->plain_width};
-        const bool on_codes = c->pipe && !c->pipe_wide && ctx->opt_pipe && ctx->opt_regex_codes;
+        const bool on_codes = c->pipe && (!c->pipe_wide || pqk::pipe_match_wide_ok(c->pipe_ecap)) && ctx->opt_pipe &&
+                              ctx->opt_regex_codes;
         const bool reuse = on_codes && ctx->opt_regex_reuse && c->codes_ok;
         // over a checked decode's codes: k_regex_dict clears the status words
         // and sets the page flags itself (no fill kernels)

@@ -2033,6 +2033,77 @@ __global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match(const DevTile* 
     }
 }
 
+// The same filter over the wide pipe's 32-bit codes: the match mask in
+// dynamic LDS ((entries + 31) / 32 words, the host bounds the entry count by
+// kMatchWideMax), two 16-byte code loads per lane and tile.
+constexpr uint32_t kMatchWideMax = 1u << 20;
+__global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match_w(const DevTile* __restrict__ tiles, int ntiles,
+                                                                   const DevPage* __restrict__ pages,
+                                                                   const uint32_t* __restrict__ codes,
+                                                                   const uint8_t* __restrict__ match,
+                                                                   const int32_t* __restrict__ dict_count, int dict_id,
+                                                                   uint32_t cap, int neg, uint8_t* __restrict__ page_flags) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t mbw[];
+    const uint32_t dn = min(static_cast<uint32_t>(max(dict_count[dict_id], 0)), cap);
+    const uint32_t nwd = (dn + 31) / 32;
+    for (uint32_t wd = threadIdx.x; wd < nwd; wd += blockDim.x) {
+        uint32_t m = 0;
+        if (wd * 32 + 32 <= dn) {
+            const uint8_t* src = match + wd * 32;
+            for (uint32_t q = 0; q < 8; q++) {
+                uint32_t x;
+                __builtin_memcpy(&x, src + 4 * q, 4);
+                x = (x | (x >> 7) | (x >> 14) | (x >> 21)) & 0xFu;
+                m |= x << (4 * q);
+            }
+        } else {
+            for (uint32_t k = 0; k < 32; k++) {
+                const uint32_t e = wd * 32 + k;
+                m |= (e < dn && match[e] != 0 ? 1u : 0u) << k;
+            }
+        }
+        mbw[wd] = m;
+    }
+    __syncthreads();
+    const int nw = static_cast<int>(gridDim.x) * kMatchWaves;
+    const uint32_t l8 = lane() * 8;
+    for (int t0 = (static_cast<int>(blockIdx.x) * kMatchWaves + static_cast<int>(threadIdx.x / kWave)) * kMatchBatch;
+         t0 < ntiles; t0 += nw * kMatchBatch) {
+        U16B v[kMatchBatch][2];
+        uint32_t m[kMatchBatch];
+        int pg[kMatchBatch];
+#pragma unroll
+        for (int i = 0; i < kMatchBatch; i++) {
+            m[i] = 0;
+            pg[i] = -1;
+            v[i][0] = v[i][1] = U16B{kNull32, kNull32, kNull32, kNull32};
+            if (t0 + i < ntiles) {
+                const DevTile T = tiles[t0 + i];
+                pg[i] = T.page;
+                m[i] = static_cast<uint32_t>(T.nrows);
+                if (l8 < m[i]) {  // (codes past the tile's rows are read, never tested; the buffer has 64 spare rows)
+                    const U16B* p = reinterpret_cast<const U16B*>(codes + pages[T.page].first_row + T.row0 + l8);
+                    v[i][0] = p[0];
+                    v[i][1] = p[1];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kMatchBatch; i++) {
+            const uint32_t w[8] = {v[i][0].x, v[i][0].y, v[i][0].z, v[i][0].w, v[i][1].x, v[i][1].y, v[i][1].z, v[i][1].w};
+            bool hit = false;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t c = w[k];
+                const bool live = l8 + k < m[i] && c < dn;
+                const uint32_t bit = (mbw[live ? (c >> 5) : 0u] >> (c & 31u)) & 1u;
+                hit |= live && (bit != static_cast<uint32_t>(neg != 0));
+            }
+            if (__ballot(hit) && lane() == 0) page_flags[pg[i]] = 0;
+        }
+    }
+}
+
 // ── the whole front of windows of pages of <= 512 rows ─────────────────────
 // k_pipe_front replaces k_pipe_runs + k_pipe_codes3 for chunks whose data
 // pages hold one tile each (the reference writer's layout).  Each wavefront
@@ -2937,6 +3008,8 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_fused(FusedArgs a) {
 
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens) { return big_layout(max_page_bytes, nlens).total; }
 
+bool pipe_match_wide_ok(uint32_t entries_cap) { return entries_cap <= kMatchWideMax; }
+
 PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
     PipePlan pl{};
     pl.lds = dict_bytes + static_cast<uint32_t>(wpw) * static_cast<uint32_t>(sizeof(WriteLds));
@@ -3160,6 +3233,14 @@ void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match,
     if (P.ntiles <= 0) return;
     const int need = (P.ntiles + kMatchWaves * kMatchBatch - 1) / (kMatchWaves * kMatchBatch);
     const int grid = max(1, min(need, 4 * max(P.cus, 1)));
+    if (P.codes32) {  // the wide pipe's codes (P.dict_entries_cap <= kMatchWideMax: pipe_match_wide_ok)
+        const uint32_t cap = min(P.dict_entries_cap, kMatchWideMax);
+        const uint32_t lds = max(16u, (cap + 31) / 32 * 4);
+        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_match_w), lds);
+        hipLaunchKernelGGL(k_pipe_match_w, dim3(grid), dim3(kMatchWaves * kWave), lds, s, P.tiles, P.ntiles, P.pages,
+                           P.codes32, match, P.dict_count, P.dict_id, cap, neg, page_flags);
+        return;
+    }
     hipLaunchKernelGGL(k_pipe_match, dim3(grid), dim3(kMatchWaves * kWave), 0, s,
                        P.tiles, P.ntiles, P.pages, P.codes, match, P.dict_count, P.dict_id, neg, page_flags);
 }

@@ -231,6 +231,8 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,
 // then codes and tile characters (one workgroup per listed page)
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens);
+// the regex filter over the wide pipe's codes holds one match bit per entry in LDS
+bool pipe_match_wide_ok(uint32_t entries_cap);
 void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes);
 // regex page filter on the codes: page_flags[p] = 1 unless a non-null row of
 // page p matches (neg: fails to match); match = dictionary match bits

@@ -298,3 +298,26 @@ def test_regex_repeated_column_errors(ctx, kernel, case):
         assert ei.value.code == rc_o and ei.value.msg == msg_o
     finally:
         dc.free()
+
+
+@pytest.mark.parametrize("case", ["huge_dict_wide_mixed", "huge_dict_wide_small_pages", "huge_dict_wide_oob",
+                                  "huge_dict_wide_bw26"])
+def test_regex_wide_dictionary(ctx, kernel, case):
+    """Dictionaries of more than 65,535 entries (the wide pipe's 32-bit codes:
+    k_pipe_match_w on the codes path), also after a checked decode (codes
+    reused) and through the decode + filter call."""
+    from test_gpu_decode import CRAFTED
+    f, ch = CRAFTED[case]()
+    chunks = [to_desc(ch)]
+    dc = ctx.upload(f, chunks)
+    for p in ("^qx", "e", "a.{3}e", "^[a-m]+$"):
+        for neg in (False, True):
+            exp = golden_pages(f, chunks, p, neg)
+            assert np.array_equal(dc.regex_pages(p, neg), exp), (p, neg)
+    dc.decode()
+    ref = capi.canonical_dump(dc.to_host())
+    rc_o, msg_o, col = O.read_all(f, to_oracle_chunk(ch))
+    assert rc_o == 0 and ref == O.dump_column(col)
+    for neg in (False, True):
+        assert np.array_equal(dc.regex_pages("e", neg), golden_pages(f, chunks, "e", neg))
+    dc.free()
