@@ -454,7 +454,7 @@ def c2_leg(J, args, exp):
             x.free()
             w.append(t1 - t0), u.append(t2 - t1), d.append(t3 - t2)
         J.ctx.timing(False)
-        phases = {k: J.ctx.timing_get(k)[0] / 3 for k in ("up_walk", "up_plan", "up_alloc", "up_h2d")}
+        phases = {k: J.ctx.timing_get(k)[0] / 3 for k in UPLOAD_PHASES}
         wm, um, dm = statistics.median(w), statistics.median(u), statistics.median(d)
         res["e2e"] = {"table_ms": wm * 1e3, "upload_ms": um * 1e3, "first_decode_ms": dm * 1e3,
                       "total_ms": (wm + um + dm) * 1e3, "values_per_s": nrows / (wm + um + dm),
@@ -555,7 +555,7 @@ def c3_legs(J, args, exp):
             x.free()
             u.append(t2 - t1), r.append(t3 - t2)
         J.ctx.timing(False)
-        phases = {k: J.ctx.timing_get(k)[0] / 3 for k in ("up_walk", "up_plan", "up_alloc", "up_h2d")}
+        phases = {k: J.ctx.timing_get(k)[0] / 3 for k in UPLOAD_PHASES}
         um, rm = statistics.median(u), statistics.median(r)
         regex["e2e"] = {"upload_ms": um * 1e3, "first_scan_ms": rm * 1e3, "total_ms": (um + rm) * 1e3,
                         "pages_per_s": npages / (um + rm), "upload_phases_ms_mean": phases,
@@ -716,6 +716,10 @@ def c4_leg(J, args):
                     "(max over ranks); serial_*: the sum of the columns timed one at a time (`columns`)",
             "columns": out, "layout": "arrow", "sharding": "data pages by global first row (row_page_range)",
             "validated": None if args.no_validate else all(J.gather(bool(ok)))}
+
+
+UPLOAD_PHASES = ("up_walk", "up_plan", "up_plan_pages", "up_plan_fused", "up_plan_pipe", "up_plan_plain",
+                 "up_plan_rest", "up_alloc", "up_h2d", "up_fill", "up_wait")
 
 
 def wide_dict_leg(J, args):
