@@ -19,6 +19,9 @@ rc=$?; cat "$OUT/ab_c2.txt"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 scripts/ab_opts.py C2 10000000 - pipe_run_pages=16 pipe_run_pages=8 pipe_run_dict=0 \
     fused_debug=67108864 > "$OUT/ab_c2_runs.txt" 2>&1
 rc=$?; cat "$OUT/ab_c2_runs.txt"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 scripts/ab_opts.py C2a 10000000 - fused_debug=65536 fused_debug=131072 fused_debug=4096 fused_debug=8192 fused_debug=16384 \
+    fused_debug=32768 > "$OUT/ab_c2a_big_phases.txt" 2>&1
+rc=$?; cat "$OUT/ab_c2a_big_phases.txt"; [ $rc -eq 0 ] || exit $rc
 bash scripts/pmc_sq.sh $TAG/sq_decode decode 10000000 3 > "$OUT/sq_decode.txt" 2>&1
 rc=$?; tail -60 "$OUT/sq_decode.txt" | grep -E "^k_|SQ_(WAVES|INSTS_VALU|INSTS_LDS|LDS_BANK|WAVE_CYCLES|WAIT_INST_ANY|ACTIVE_INST_ANY) "; [ $rc -eq 0 ] || exit $rc
 bash scripts/pmc_sq.sh $TAG/sq_regex regex 10000000 3 > "$OUT/sq_regex.txt" 2>&1
