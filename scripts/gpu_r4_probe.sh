@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_lists.py tests/test_gpu_fuzz.py \
-    -m gpu -k "${PROBE_K:-pfused or rep_ or lists or mutants}" -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_probe.log" 2>&1
+    -m gpu -k "${PROBE_K:-pfused or rep_ or lists or mutants}" ${PROBE_X--x} -q --timeout 120 --timeout-method thread > "$OUT/pytest_probe.log" 2>&1
 rc=$?; tail -5 "$OUT/pytest_probe.log"; [ $rc -eq 0 ] || { echo "PYTEST rc=$rc"; exit $rc; }
 timeout -k 10 300 python3 scripts/ab_opts.py W 10000000 pipe_wide=0 - > "$OUT/ab_wide.txt" 2>&1
 rc=$?; cat "$OUT/ab_wide.txt"; [ $rc -eq 0 ] || exit $rc
