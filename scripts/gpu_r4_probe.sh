@@ -8,9 +8,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_lists.py tests/test_gpu_fuzz.py \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_decode.py tests/test_gpu_lists.py tests/test_gpu_fuzz.py tests/test_gpu_regex.py \
     -m gpu -k "${PROBE_K:-pfused or rep_ or lists or mutants}" ${PROBE_X--x} -q --timeout 120 --timeout-method thread > "$OUT/pytest_probe.log" 2>&1
-rc=$?; tail -5 "$OUT/pytest_probe.log"; [ $rc -eq 0 ] || { echo "PYTEST rc=$rc"; exit $rc; }
+rc=$?; tail -5 "$OUT/pytest_probe.log"
+# plain test failures (rc 1) may go on to the timings with PROBE_CONT=1; a
+# crash, abort or time limit never does
+[ $rc -eq 0 ] || [ $rc -eq 1 -a -n "$PROBE_CONT" ] || { echo "PYTEST rc=$rc"; exit $rc; }
 timeout -k 10 300 python3 scripts/ab_opts.py W 10000000 pipe_wide=0 - > "$OUT/ab_wide.txt" 2>&1
 rc=$?; cat "$OUT/ab_wide.txt"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 scripts/ab_opts.py C2 10000000 - pipe_fused=1 "pipe_fused=1,pipe_fused_waves=16" \
