@@ -233,8 +233,9 @@ __global__ void __launch_bounds__(256) k_regex_pages(const DevProg* __restrict__
 // One lane per data page (a wavefront scans 64 pages at once): def levels
 // and dictionary indices with the reference's RLE state machine
 // (lane_walk.hpp), PLAIN strings streamed through a 16-byte register window
-// into the DFA (one LDS lookup per byte).  A lane stops as soon as its page
-// has a satisfying value.
+// into the DFA (one LDS lookup per byte).  Once its page has a satisfying
+// value a lane stops matching but still walks the rest of the page (levels,
+// indices, the length chain), so a later decode error fails the scan.
 __device__ __forceinline__ uint32_t dfa_step_full(const uint16_t* T, uint32_t e, uint32_t b) {
     return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(T) + e + 2 * b);
 }
@@ -360,7 +361,9 @@ __global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__
         uint32_t k = 0, cur = pos;
         int ecode = 0;
         uint32_t epos = 0, eneed = 0;
-        while (__ballot(k < nn && !ecode && !any)) {
+        // (a page that already matched still walks its whole length chain:
+        // an error further on fails the scan as it fails the page's decode)
+        while (__ballot(k < nn && !ecode)) {
             // 1. the next kCollect strings' (offset, length): length chain
             //    (ByteBuffer reads, column_reader.cpp:249-253) and its errors
             constexpr uint32_t kCollect = 8;
