@@ -1488,25 +1488,31 @@ constexpr int kBigThreads = kBigWaves * kWave;
 constexpr uint32_t kBStop = 0xFFFFu;
 constexpr int kBJumpLog = 4;
 constexpr uint32_t kBJump = 1u << kBJumpLog;
-constexpr uint32_t kBigPerThread = kBigMaxBytes / kBigThreads;  // jump-table slots per thread
+constexpr uint32_t kBigPerThread = kBigSegBytes / kBigThreads;  // jump-table slots per thread (one segment)
 constexpr uint32_t kBCountCap = 1u << 20;                       // count clamp (pages hold <= 32768 values)
-static_assert(kBigMaxBytes % kBigThreads == 0, "jump table split");
+static_assert(kBigSegBytes % kBigThreads == 0, "jump table split");
 static_assert(kBigMaxBytes + 32 < kBStop, "u16 positions");
+static_assert(kBigMaxBytes <= 2 * kBigSegBytes, "at most two jump-table segments");
 
 struct BigLayout {  // dynamic LDS of k_pipe_big for a page of `size` payload bytes
-    uint32_t P, LC, stage, tab, esum, ent, lens, mark, tvb, misc, total;
+    uint32_t P, H, nseg, LC, stage, tab, esum, ent, meta, lens, mark, tvb, misc, total;
 };
 __host__ __device__ inline BigLayout big_layout(uint32_t size, uint32_t nlens) {
     BigLayout L{};
     L.P = (size + 16 + 15) / 16 * 16;            // = the payload slot (capi.hip)
+    // the jump table covers the page in one segment, or (pages over
+    // kBigSegBytes) in two halves one after the other
+    L.nseg = size > kBigSegBytes ? 2u : 1u;
+    L.H = L.nseg == 1 ? L.P : ((size + 1) / 2 + 15) / 16 * 16;  // positions per segment (a multiple of 16)
     L.LC = L.P / (2 * kBJump) + 8;               // listed headers per stream (runs are >= 2 bytes)
     L.stage = 0;                                 // P bytes: the payload slot
-    L.tab = L.stage + L.P;                       // u16 per position; then P / 4 run records
-    L.esum = L.tab + 2 * L.P;                    // u32 per listed header: values, then their exclusive scan
-    L.ent = L.esum + 8 * L.LC;                   // u32 per listed header: position, then fill results
+    L.tab = L.stage + L.P;                       // u16 per position of a segment; then H / 4 run records
+    L.esum = L.tab + 2 * L.H;                    // u32 per listed header: values, then their exclusive scan
+    L.ent = L.esum + 8 * L.LC;                   // u32 per listed header: position
+    L.meta = L.ent + 8 * L.LC;                   // u32 per listed header: its re-parse's record count and flags
     L.tvb = L.esum;                              // per tile: validity bits of rows 8l .. 8l + 7 (phase 6:
                                                  // over esum / ent, dead after phase 5)
-    const uint32_t x = 16 * L.LC > static_cast<uint32_t>(kBigTiles * kWave) ? 16 * L.LC : static_cast<uint32_t>(kBigTiles * kWave);
+    const uint32_t x = 24 * L.LC > static_cast<uint32_t>(kBigTiles * kWave) ? 24 * L.LC : static_cast<uint32_t>(kBigTiles * kWave);
     L.lens = L.esum + x;                         // u16 per dictionary entry: length
     L.mark = L.lens + (2 * nlens + 15) / 16 * 16;  // per wave: u16 per row of a tile
     L.misc = L.mark + kBigWaves * kTileRows * 2;  // tile non-null counts, first ranks, scan partials, flags
@@ -1728,66 +1734,74 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         const uint32_t nx = h.lit ? h.qh + __umul24(min(h.g, 0x10000u), bw) : h.qh + (bw + 7) / 8;
         return (j >= size || big_bad(h, e, (bw + 7) / 8) || nx >= e) ? kBStop : nx;
     };
-    for (uint32_t jp = tid; 2 * jp < size; jp += kBigThreads)
-        reinterpret_cast<uint32_t*>(tab)[jp] = next_at(2 * jp) | (next_at(2 * jp + 1) << 16);
-    __syncthreads();
-    if (a.debug & 0x20000) return;  // timing: + header parse
-    // 2. kBJump-run jumps by pointer doubling, two positions per thread
-    //    (one dword of the table read and written)
-    {
-        uint32_t* tab32 = reinterpret_cast<uint32_t*>(tab);
-        const uint32_t npair = (size + 1) / 2;
-        auto hop = [&](uint32_t t) {  // kBStop stays
-            const uint32_t u = tab[t == kBStop ? 0u : t];
-            return t == kBStop ? kBStop : u;
-        };
-        for (int r = 0; r < kBJumpLog; r++) {
-            uint32_t nv[kBigPerThread / 2];
-#pragma unroll
-            for (uint32_t i = 0; i < kBigPerThread / 2; i++) {
-                if (i * kBigThreads >= npair) break;  // (uniform)
-                const uint32_t jp = tid + i * kBigThreads;
-                uint32_t w = kBStop | (kBStop << 16);
-                if (jp < npair) {
-                    const uint32_t x = tab32[jp];
-                    w = hop(x & 0xFFFFu) | (hop(x >> 16) << 16);
-                }
-                nv[i] = w;
-            }
-            __syncthreads();
-#pragma unroll
-            for (uint32_t i = 0; i < kBigPerThread / 2; i++) {
-                if (i * kBigThreads >= npair) break;
-                const uint32_t jp = tid + i * kBigThreads;
-                if (jp < npair) tab32[jp] = nv[i];
-            }
-            __syncthreads();
-        }
-    }
-    if (a.debug & 4096) return;  // timing: jump table only
-    // 3. one lane per stream follows the jumps: every kBJump-th header
-    const uint32_t rcap = Ly.P / 4;  // run records in the jump table's space
+    // (pages over kBigSegBytes: steps 1-3 per half of the page; a jump that
+    // leaves the half stops at the first position past it, where step 3
+    // goes on in the next half)
+    const uint32_t rcap = Ly.H / 4;  // run records in the jump table's space
     const uint32_t rcap_d = hasd ? min(rcap / 2, dlen / 2 + 2 * kBJump + 2) : 0u;
     const uint32_t rcap_i = rcap - rcap_d;
-    if (tid == 0 || tid == kWave) {
-        const bool isd = tid == 0;
-        uint32_t k = 0;
-        if (!isd || hasd) {
-            const uint32_t e = isd ? dend : iend, rc = isd ? rcap_d : rcap_i;
-            const uint32_t lcap = rc > kBJump + 1 ? min(Ly.LC, (rc - kBJump - 1) / kBJump + 1) : 0u;
-            uint32_t* L = ent + (isd ? 0u : Ly.LC);
-            uint32_t q = isd ? dbase : ibase;
-            for (;;) {
-                if (k >= lcap) { k = ~0u; break; }
-                L[k++] = q;
-                if (q >= e) break;
-                const uint32_t t = tab[q];
-                if (t == kBStop) break;
-                q = t;
+    uint32_t* tab32 = reinterpret_cast<uint32_t*>(tab);
+    const bool walker = tid == 0 || tid == kWave, isd_w = tid == 0;
+    uint32_t wq = isd_w ? dbase : ibase, wk = 0;  // step 3's chain position and list length (walker threads)
+    bool wdone = !walker || (isd_w && !hasd);
+    for (uint32_t sg = 0; sg < Ly.nseg; sg++) {
+        const uint32_t base = sg * Ly.H, lim = min(size, base + Ly.H);
+        const uint32_t npair = (lim - base + 1) / 2;
+        for (uint32_t jp = tid; jp < npair; jp += kBigThreads)
+            tab32[jp] = next_at(base + 2 * jp) | (next_at(base + 2 * jp + 1) << 16);
+        __syncthreads();
+        if (a.debug & 0x20000) return;  // timing: + header parse
+        // 2. kBJump-run jumps by pointer doubling, two positions per thread
+        //    (one dword of the table read and written)
+        {
+            auto hop = [&](uint32_t t) {  // kBStop and positions past the segment stay
+                const bool in = t >= base && t < lim;
+                const uint32_t u = tab[in ? t - base : 0u];
+                return in ? u : t;
+            };
+            for (int r = 0; r < kBJumpLog; r++) {
+                uint32_t nv[kBigPerThread / 2];
+#pragma unroll
+                for (uint32_t i = 0; i < kBigPerThread / 2; i++) {
+                    if (i * kBigThreads >= npair) break;  // (uniform)
+                    const uint32_t jp = tid + i * kBigThreads;
+                    uint32_t w = kBStop | (kBStop << 16);
+                    if (jp < npair) {
+                        const uint32_t x = tab32[jp];
+                        w = hop(x & 0xFFFFu) | (hop(x >> 16) << 16);
+                    }
+                    nv[i] = w;
+                }
+                __syncthreads();
+#pragma unroll
+                for (uint32_t i = 0; i < kBigPerThread / 2; i++) {
+                    if (i * kBigThreads >= npair) break;
+                    const uint32_t jp = tid + i * kBigThreads;
+                    if (jp < npair) tab32[jp] = nv[i];
+                }
+                __syncthreads();
             }
         }
-        sh[isd ? 1 : 2] = k;
+        if (a.debug & 4096) return;  // timing: jump table only
+        // 3. one lane per stream follows the jumps: every kBJump-th header
+        //    (and the first header past a segment end)
+        if (walker && !wdone) {
+            const uint32_t e = isd_w ? dend : iend, rc = isd_w ? rcap_d : rcap_i;
+            const uint32_t lcap = rc > kBJump + 1 ? min(Ly.LC, (rc - kBJump - 1) / kBJump + 1) : 0u;
+            uint32_t* L = ent + (isd_w ? 0u : Ly.LC);
+            for (;;) {
+                if (wq < e && wq >= lim) break;  // listed by the next segment
+                if (wk >= lcap) { wk = ~0u; wdone = true; break; }
+                L[wk++] = wq;
+                if (wq >= e) { wdone = true; break; }
+                const uint32_t t = tab[wq - base];
+                if (t == kBStop) { wdone = true; break; }
+                wq = t;
+            }
+        }
+        __syncthreads();  // the next segment rewrites the table
     }
+    if (walker) sh[isd_w ? 1 : 2] = wk;
     __syncthreads();
     const uint32_t nld = sh[1], nli = sh[2];
     if (a.debug & 8192) return;  // timing: + chain walk
@@ -1796,11 +1810,15 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     uint2* recd = reinterpret_cast<uint2*>(smem + Ly.tab);
     uint2* reci = recd + rcap_d;
     const uint32_t ne = nld + nli;
+    uint32_t* meta = reinterpret_cast<uint32_t*>(smem + Ly.meta);
     for (uint32_t i = tid; i < ne; i += kBigThreads) {
         const bool isd = i < nld;
         const uint32_t li = isd ? i : i - nld;
         const uint32_t slot = isd ? i : Ly.LC + li;
         uint32_t q = ent[slot];
+        // the next listed header: kBJump runs on, or fewer where a jump
+        // stopped at a segment end
+        const uint32_t stop = li + 1 < (isd ? nld : nli) ? ent[slot + 1] : 0xFFFFFFFFu;
         const uint32_t e = isd ? dend : iend, bw = isd ? bwd : bwi, nbv = (bw + 7) / 8;
         const uint32_t vmask = nbv >= 3 ? 0xFFFFFFu : (nbv == 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u));
         const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
@@ -1808,6 +1826,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         uint32_t s = 0, sum = 0, bad = kBJump, ended = 0;
         for (; s < kBJump; s++) {
             if (q >= e) { ended = 1; break; }
+            if (q == stop) break;
             const BigHdr h = big_hdr(stw, q);
             if (big_bad(h, e, nbv)) { bad = s; break; }
             const uint32_t c = h.lit ? min(h.g, kBCountCap / 8) * 8 : min(h.g, kBCountCap);
@@ -1819,7 +1838,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         }
         if (s == kBJump && q >= e) ended = 1;
         esum[i] = sum;
-        ent[slot] = s | (bad << 8) | (ended << 16);
+        meta[slot] = s | (bad << 8) | (ended << 16);
     }
     __syncthreads();
     // 5. first value of every record: scan of the headers' counts, then
@@ -1829,8 +1848,8 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     for (uint32_t i = tid; i < ne; i += kBigThreads) {
         const bool isd = i < nld;
         const uint32_t li = isd ? i : i - nld, nlst = isd ? nld : nli;
-        const uint32_t meta = ent[isd ? i : Ly.LC + li];
-        const uint32_t nr = meta & 0xFFu, bad = (meta >> 8) & 0xFFu, ended = meta >> 16;
+        const uint32_t mt = meta[isd ? i : Ly.LC + li];
+        const uint32_t nr = mt & 0xFFu, bad = (mt >> 8) & 0xFFu, ended = mt >> 16;
         const uint32_t base = esum[i] - (isd ? 0u : dtot);
         if (base >= n) continue;
         uint2* out = (isd ? recd : reci) + li * kBJump;
@@ -1849,6 +1868,13 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         } else if (li + 1 == nlst) {  // exhausted: the rest of the values are 0
             out[nr] = make_uint2(c0 | ((n - c0) << 16), 0u);
             sh[isd ? 3 : 4] = li * kBJump + nr + 1;
+        } else if (nr < kBJump) {
+            // a header list entry cut short at a segment end: its unused slots
+            // repeat its last record (same start: every search and mark of
+            // step 6 then finds a copy of that record, never a hole)
+            if (nr == 0) atomicOr(&sh[0], 1u);  // (not produced by step 3; kept exact)
+            else
+                for (uint32_t s = nr; s < kBJump; s++) out[s] = out[nr - 1];
         }
     }
     __syncthreads();

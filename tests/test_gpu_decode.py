@@ -400,6 +400,11 @@ CRAFTED = {
                                                   mixed=True),
     "huge_dict_wide_bw26": lambda: _huge_dict_file(100000, seed=91, lmin=4, lmax=9, nrows=3000, pages=2, mixed=True,
                                                    bw_add=9),
+    # pages of 24-48 KiB: k_pipe_big's jump table in two segments (a wide
+    # dictionary's 17-bit indices, and a 3,000-entry dictionary's 12-bit ones)
+    "huge_dict_wide_bigpage": lambda: _huge_dict_file(100000, seed=92, lmin=4, lmax=9, nrows=20000, pages=1, mixed=True),
+    "dict_bigpage_two_segments": lambda: _huge_dict_file(3000, seed=93, lmin=2, lmax=12, nrows=40000, pages=2,
+                                                         mixed=True),
     # OPTIONAL PLAIN BYTE_ARRAY: a window page; a chunk-chain page whose values
     # start inside chunk 0 past its candidate range, one whose levels fill
     # several chunks; bytes after the last value (the one-pass form does not
