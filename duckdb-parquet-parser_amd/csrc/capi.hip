@@ -2445,7 +2445,9 @@ static int collect(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
 int pq_decode_check(pq_ctx* ctx, pq_chunk* c) {
     if (!ctx || !c) return PQ_ERR_ARG;
     DevGuard dg(ctx);
-    return collect(ctx, c, nullptr);
+    // the column of the chunk's last async decode gets its byte count (and
+    // grows and decodes again if its characters overflowed the estimate)
+    return collect(ctx, c, c->last_out);
 }
 
 int pq_decode(pq_ctx* ctx, pq_chunk* c, pq_column* out) {

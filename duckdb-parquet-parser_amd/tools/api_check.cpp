@@ -13,6 +13,10 @@
 //   api_check <file> decode_regex_sharded <name> <k> <pattern> <neg>
 //                                                  read_column_regex over k Devices: the column's
 //                                                  dump on stdout, the page ids on stderr
+#include <execinfo.h>
+#include <unistd.h>
+
+#include <csignal>
 #include <cstdio>
 #include <cstring>
 #include <iostream>
@@ -41,8 +45,21 @@ static void dump(const pqgpu::Value& v, std::vector<uint8_t>& out) {
     }, v.data);
 }
 
+// a crash prints its native stack to stderr (test diagnostics)
+static void on_crash(int sig) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    const char msg[] = "api_check: fatal signal; stack:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(fr, n, 2);
+    std::signal(sig, SIG_DFL);
+    std::raise(sig);
+}
+
 int main(int argc, char** argv) {
     if (argc < 4) return 2;
+    std::signal(SIGSEGV, on_crash);
+    std::signal(SIGABRT, on_crash);
     try {
         pqgpu::ParquetReader r;
         if (!r.open(argv[1])) return 1;

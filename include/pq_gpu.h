@@ -242,7 +242,10 @@ int pq_chunk_pages(const pq_chunk* chunk, pq_page_desc* pages, int64_t cap, int6
  * the context stream. */
 int pq_decode(pq_ctx* ctx, pq_chunk* chunk, pq_column* out);
 int pq_decode_async(pq_ctx* ctx, pq_chunk* chunk, pq_column* out);
-int pq_decode_check(pq_ctx* ctx, pq_chunk* chunk); /* sync + error collection after _async */
+/* sync + error collection after _async; also completes the column the
+ * chunk's last async decode wrote (its num_bytes; a column whose characters
+ * outgrew the estimate is grown and decoded again), which must still be live */
+int pq_decode_check(pq_ctx* ctx, pq_chunk* chunk);
 int pq_column_copy_out(pq_ctx* ctx, const pq_column* col, uint32_t* validity, uint8_t* values,
                        int64_t* offsets);
 void pq_column_free(pq_ctx* ctx, pq_column* col);
@@ -272,9 +275,8 @@ int pq_regex_pages_result(pq_ctx* ctx, pq_chunk* chunk, uint8_t* page_flags);
  * takes (dictionary payload < 32 KiB), the pattern runs once per dictionary
  * entry and k_pipe_write tests every row's entry while it writes the column;
  * otherwise the decode, then
- * pq_regex_pages_async over its codes.  Results: pq_decode_check /
- * pq_column_copy_out for the column (decode the chunk once with pq_decode
- * first, so the output is sized), pq_regex_pages_result for the flags. */
+ * pq_regex_pages_async over its codes.  Results: pq_regex_pages_result for
+ * the flags, pq_decode_check then pq_column_copy_out for the column. */
 int pq_decode_regex_async(pq_ctx* ctx, pq_chunk* chunk, pq_column* out, const char* pattern, int neg);
 
 /* ── kernel timing (HIP events on the context stream) ───────────────────── */
