@@ -1479,7 +1479,10 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             c->nunits = c->fused_ok ? (c->ntiles + pqk::pipe_fused_tiles() - 1) / pqk::pipe_fused_tiles() : 0;
             c->z_bsum = fb;
             c->z_fused = (fb + bb + 15) / 16 * 16;
-            c->z_flist = c->z_fused + (c->fused_ok ? 16 + static_cast<size_t>(c->nunits) * sizeof(unsigned long long) : 0);
+            // ticket, then per unit its look-back word, then per group of
+            // pipe_fused_super() units their (count, sum) word
+            const size_t nsb = c->fused_ok ? static_cast<size_t>((c->nunits + pqk::pipe_fused_super() - 1) / pqk::pipe_fused_super()) : 0;
+            c->z_flist = c->z_fused + (c->fused_ok ? 16 + (static_cast<size_t>(c->nunits) + nsb) * sizeof(unsigned long long) : 0);
             // cleared per decode (through flist[0]): a multiple of 16 bytes (an
             // odd size takes a second fill kernel for the tail)
             const size_t zb = (c->z_flist + sizeof(int32_t) + 15) / 16 * 16;

@@ -2589,7 +2589,7 @@ struct FusedArgs {
     uint32_t stage_bytes;                   // payload stage (>= every k_pipe_runs page's slot)
     int32_t nunits;
     int32_t* ticket;                        // zeroed per decode
-    unsigned long long* status;             // nunits look-back words, zeroed per decode
+    unsigned long long* status;             // nunits aggregate words, then the superblock words; zeroed per decode
     uint32_t* znext;                        // the next decode's zero block (cleared here), or null
     uint32_t znext_words;
     const uint8_t* match;                   // armed page filter, as k_pipe_write
@@ -2599,7 +2599,6 @@ struct FusedArgs {
 };
 
 constexpr unsigned long long kFAgg = 1ull << 62;
-constexpr unsigned long long kFInc = 2ull << 62;
 constexpr unsigned long long kFValMask = (1ull << 62) - 1;
 
 __device__ __forceinline__ unsigned long long fwave_sum64(unsigned long long v) {
@@ -2612,36 +2611,55 @@ __device__ __forceinline__ unsigned long long fwave_sum64(unsigned long long v) 
     return v;
 }
 
-// Decoupled look-back over the units (status[u]: kFAgg | aggregate or
-// kFInc | inclusive prefix); returns the exclusive prefix of unit u.
-__device__ unsigned long long unit_look_back(unsigned long long* status, int32_t u, unsigned long long total) {
-    if (u == 0) {
-        if (lane() == 0) __hip_atomic_store(&status[0], kFInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return 0;
+// The exclusive prefix of unit u's characters, two-level: units in groups of
+// kFSuper (superblocks).  A unit publishes its aggregate in status[u] and adds
+// (1 << 48) | aggregate to its superblock's word sb[u / kFSuper]; its prefix
+// is the sums of the complete superblocks before its own (unit count reached)
+// plus the aggregates of its superblock's earlier units.  (A per-unit chained
+// look-back serialised here: every resident wave decodes its first unit at
+// once, so the inclusive prefixes propagated one 64-unit poll at a time, about
+// 50 us over C2's ~4,900 units.)  Units are claimed by ticket, so every unit
+// a poll waits for belongs to a running wave.
+constexpr int kFSuper = 64;
+constexpr unsigned long long kFSumMask = (1ull << 48) - 1;
+__device__ unsigned long long unit_prefix(unsigned long long* status, unsigned long long* sb, int32_t u,
+                                          unsigned long long total) {
+    const int32_t s = u / kFSuper, u0 = s * kFSuper;
+    if (lane() == 0) {
+        __hip_atomic_store(&status[u], kFAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&sb[s], (1ull << 48) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (lane() == 0) __hip_atomic_store(&status[u], kFAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long prefix = 0;
-    int32_t q = u - 1;
-    uint32_t nap = 1;
-    for (;;) {
-        const int32_t i = q - static_cast<int32_t>(lane());
-        const unsigned long long s =
-            i >= 0 ? __hip_atomic_load(&status[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFInc;
-        const uint64_t incm = __ballot((s >> 62) == 2);
-        const uint64_t notready = __ballot((s >> 62) == 0);
-        const uint32_t first_inc = incm ? static_cast<uint32_t>(__builtin_ctzll(incm)) : 64u;
-        const uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1ull);
-        if (notready & upto) {  // a unit before the first inclusive prefix has not published yet
+    // complete superblocks before s (all of them hold kFSuper units)
+    for (int32_t b0 = 0; b0 < s; b0 += kWave) {
+        const int32_t b = b0 + static_cast<int32_t>(lane());
+        uint32_t nap = 1;
+        for (;;) {
+            const unsigned long long v =
+                b < s ? __hip_atomic_load(&sb[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (static_cast<unsigned long long>(kFSuper) << 48);
+            if (__ballot((v >> 48) != static_cast<unsigned long long>(kFSuper)) == 0) {
+                prefix += fwave_sum64(b < s ? (v & kFSumMask) : 0ull);
+                break;
+            }
             for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(4);
             nap = nap < 8 ? 2 * nap : 8;
-            continue;
         }
-        const unsigned long long c = lane() <= first_inc ? (s & kFValMask) : 0ull;
-        prefix += fwave_sum64(c);
-        if (first_inc < 64) break;
-        q -= 64;
     }
-    if (lane() == 0) __hip_atomic_store(&status[u], kFInc | (prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // this superblock's units before u
+    if (u > u0) {
+        const int32_t v = u0 + static_cast<int32_t>(lane());
+        uint32_t nap = 1;
+        for (;;) {
+            const unsigned long long x =
+                v < u ? __hip_atomic_load(&status[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFAgg;
+            if (__ballot((x >> 62) == 0) == 0) {
+                prefix += fwave_sum64(v < u ? (x & kFValMask) : 0ull);
+                break;
+            }
+            for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(4);
+            nap = nap < 8 ? 2 * nap : 8;
+        }
+    }
     return prefix;
 }
 
@@ -2878,7 +2896,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_fused(FusedArgs a) {
         }
         // 2. the unit's first output byte
         const uint32_t inc = wave_incl_scan(myc);
-        const unsigned long long prefix = unit_look_back(a.status, u, bcast_last(inc));
+        const unsigned long long prefix = unit_prefix(a.status, a.status + a.nunits, u, bcast_last(inc));
         const int64_t myG0 = static_cast<int64_t>(prefix) + static_cast<int64_t>(inc - myc);
         if (a.debug & 8) continue;
         // 3. k_pipe_write's per-tile body
@@ -3203,6 +3221,7 @@ void launch_pipe_front(hipStream_t s, const PipeLaunch& P, const DevBatch* wins,
 }
 
 int pipe_fused_tiles() { return kFuseTiles; }
+int pipe_fused_super() { return kFSuper; }
 
 static uint32_t fused_wave_lds(uint32_t stage) {
     const uint32_t dec = static_cast<uint32_t>(sizeof(FuseDecLds)) + stage;

@@ -198,6 +198,7 @@ PipePlan plan_pipe_wide(int wpw);
 // k_pipe_fused: tiles per unit, and its LDS / resident workgroups per CU for
 // `wpw` waves per workgroup and a payload stage of `stage` bytes per wave
 int pipe_fused_tiles();
+int pipe_fused_super();  // units per superblock of k_pipe_fused's two-level prefix
 PipePlan plan_pipe_fused(uint32_t dict_bytes, int wpw, uint32_t stage);
 // codes and write in one pass (after k_pipe_runs / k_pipe_big / the count
 // pass; the exact decoder runs first, inside, over the pages k_pipe_runs listed)
