@@ -1509,10 +1509,14 @@ __host__ __device__ inline BigLayout big_layout(uint32_t size, uint32_t nlens) {
     L.tab = L.stage + L.P;                       // u16 per position of a segment; then H / 4 run records
     L.esum = L.tab + 2 * L.H;                    // u32 per listed header: values, then their exclusive scan
     L.ent = L.esum + 8 * L.LC;                   // u32 per listed header: position
-    L.meta = L.ent + 8 * L.LC;                   // u32 per listed header: its re-parse's record count and flags
+    // u32 per listed header: its re-parse's record count and flags (in place
+    // of its position for one segment; two segments read the next header's
+    // position as they parse, so they keep both)
+    L.meta = L.nseg == 1 ? L.ent : L.ent + 8 * L.LC;
     L.tvb = L.esum;                              // per tile: validity bits of rows 8l .. 8l + 7 (phase 6:
                                                  // over esum / ent, dead after phase 5)
-    const uint32_t x = 24 * L.LC > static_cast<uint32_t>(kBigTiles * kWave) ? 24 * L.LC : static_cast<uint32_t>(kBigTiles * kWave);
+    const uint32_t xl = (L.nseg == 1 ? 16u : 24u) * L.LC;
+    const uint32_t x = xl > static_cast<uint32_t>(kBigTiles * kWave) ? xl : static_cast<uint32_t>(kBigTiles * kWave);
     L.lens = L.esum + x;                         // u16 per dictionary entry: length
     L.mark = L.lens + (2 * nlens + 15) / 16 * 16;  // per wave: u16 per row of a tile
     L.misc = L.mark + kBigWaves * kTileRows * 2;  // tile non-null counts, first ranks, scan partials, flags
@@ -1818,7 +1822,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         uint32_t q = ent[slot];
         // the next listed header: kBJump runs on, or fewer where a jump
         // stopped at a segment end
-        const uint32_t stop = li + 1 < (isd ? nld : nli) ? ent[slot + 1] : 0xFFFFFFFFu;
+        const uint32_t stop = Ly.nseg > 1 && li + 1 < (isd ? nld : nli) ? ent[slot + 1] : 0xFFFFFFFFu;
         const uint32_t e = isd ? dend : iend, bw = isd ? bwd : bwi, nbv = (bw + 7) / 8;
         const uint32_t vmask = nbv >= 3 ? 0xFFFFFFu : (nbv == 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u));
         const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
