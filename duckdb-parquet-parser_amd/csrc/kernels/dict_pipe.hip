@@ -1884,6 +1884,10 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     __syncthreads();
     if (a.debug & 16384) return;  // timing: + exact records
     const uint32_t nd = hasd ? sh[3] : 0u, ni = sh[4];
+    if ((a.debug & (1 << 27)) && tid == 0) {  // diagnostics: the step-5 outcome as the page's error record
+        set_err(a.page_err + p, a.err_any, PQ_ERR_BUFFER, nd | (ni << 16), nld | (nli << 16),
+                sh[0] | (Ly.nseg << 8) | (rcap_d << 16));
+    }
     if (sh[0] || (hasd && nd == 0) || ni == 0) return to_exact();
     const int32_t t0 = a.page_tile0[p];
     const int64_t first_row = pg.first_row;
