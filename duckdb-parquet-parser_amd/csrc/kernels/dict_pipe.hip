@@ -205,8 +205,11 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
             W.gp = gp;
         }
     }
-    if (staged) walk_runs<true>(W, stage, flag, nrec);
-    else walk_runs<false>(W, stage, flag, nrec);
+    // (the run table's per-stream rows are kPipeRunCap * 8 = 1 KiB apart:
+    // 16-byte aligned, records stored in pairs)
+    static_assert((kPipeRunCap * sizeof(uint2)) % 16 == 0, "record rows 16-byte aligned");
+    if (staged) walk_runs<true, true>(W, stage, flag, nrec);
+    else walk_runs<false, true>(W, stage, flag, nrec);
     const uint32_t oflag = static_cast<uint32_t>(__shfl_xor(static_cast<int>(flag), 1));
     const uint32_t orec = static_cast<uint32_t>(__shfl_xor(static_cast<int>(nrec), 1));
     if (act && s == 0)

@@ -19,7 +19,10 @@ struct RunWalk {
     const uint8_t* gp;
 };
 
-template <bool kStaged>
+// kPair: records go out two at a time as one 16-byte store (W.out 16-byte
+// aligned, nrec even on entry): half the store instructions, whole 16-byte
+// pieces of the record lines instead of 8-byte ones
+template <bool kStaged, bool kPair = false>
 __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uint32_t& flag, uint32_t& nrec) {
     const uint32_t nbv = (W.bw + 7) / 8;
     const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
@@ -44,6 +47,7 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
     };
     uint32_t x0, x1;
     load(q, alive, x0, x1);
+    uint2 held = make_uint2(0u, 0u);  // kPair: the record at an even index, waiting for its partner
     // branch-free step: every quantity is computed, one predicated store.
     // kOne: every live header is one byte (runs of < 64 values or groups:
     // what both writers emit for these pages), so the varint parse, the
@@ -100,7 +104,12 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
         }
         const uint32_t pl = (litm & (litpay | ((qh << 3) & litsh))) | (~litm & vraw & vmask);
         const uint32_t ry = exh ? 0u : pl;
-        if (ok) W.out[nr] = make_uint2(rx, ry);
+        if constexpr (kPair) {
+            if (ok && (nr & 1u)) *reinterpret_cast<uint4*>(W.out + nr - 1) = make_uint4(held.x, held.y, rx, ry);
+            if (ok && !(nr & 1u)) held = make_uint2(rx, ry);
+        } else {
+            if (ok) W.out[nr] = make_uint2(rx, ry);
+        }
         fl |= (alive ? 1u : 0u) & (ok ^ 1u);
         nr += ok;
         cnt = ncnt;
@@ -112,6 +121,9 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
     while (__ballot(alive)) {
         if (__ballot(alive && q < W.end && (x0 & 0x80u)) == 0) step(std::true_type{});
         else step(std::false_type{});
+    }
+    if constexpr (kPair) {
+        if (nr & 1u) W.out[nr - 1] = held;
     }
     nrec = nr;
     flag = fl;
