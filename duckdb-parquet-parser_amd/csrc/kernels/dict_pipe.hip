@@ -1684,11 +1684,15 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     // anything outside the fast shape: the exact serial decoder, by wave 0
     // of this workgroup (the page in HBM; LDS only for its small scratch),
     // so no further launch is needed after the big pages
-    auto to_exact = [&]() {
+    auto to_exact = [&](uint32_t why) {
+        if (a.debug & (1 << 27)) {  // diagnostics: which step sent the page to the exact decoder
+            if (tid == 0) set_err(a.page_err + p, a.err_any, PQ_ERR_BUFFER, why, static_cast<uint32_t>(p), size);
+            return;
+        }
         if (tid == 0) info[p] = kFallback;
         if (wv == 0) exact_page_body<kWide>(a, *reinterpret_cast<CodeLds*>(smem), p, dict_n, ebase);
     };
-    if (n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes) return to_exact();
+    if (n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes) return to_exact(1);
 
     // 0. the payload slot and the dictionary's entry lengths -> LDS (before
     //    the prologue, which then reads the stage instead of HBM)
@@ -1725,7 +1729,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     if (!flag && bwi > (kWide ? 24u : 16u)) flag = true;
     if (flag) {
         __syncthreads();  // every wave has read the stage before wave 0 reuses it
-        return to_exact();
+        return to_exact(2);
     }
     const bool hasd = a.max_def > 0;
     const uint32_t dend = dbase + dlen, ibase = pos, iend = size;
@@ -1812,7 +1816,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     __syncthreads();
     const uint32_t nld = sh[1], nli = sh[2];
     if (a.debug & 8192) return;  // timing: + chain walk
-    if (nld == ~0u || nli == ~0u) return to_exact();
+    if (nld == ~0u || nli == ~0u) return to_exact(3);
     // 4. exact runs of each listed header: untruncated counts, bad-header step
     uint2* recd = reinterpret_cast<uint2*>(smem + Ly.tab);
     uint2* reci = recd + rcap_d;
@@ -1887,11 +1891,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     __syncthreads();
     if (a.debug & 16384) return;  // timing: + exact records
     const uint32_t nd = hasd ? sh[3] : 0u, ni = sh[4];
-    if ((a.debug & (1 << 27)) && tid == 0) {  // diagnostics: the step-5 outcome as the page's error record
-        set_err(a.page_err + p, a.err_any, PQ_ERR_BUFFER, nd | (ni << 16), nld | (nli << 16),
-                sh[0] | (Ly.nseg << 8) | (rcap_d << 16));
-    }
-    if (sh[0] || (hasd && nd == 0) || ni == 0) return to_exact();
+    if (sh[0] || (hasd && nd == 0) || ni == 0) return to_exact(4 | (sh[0] << 4) | ((nd == 0) << 5) | ((ni == 0) << 6));
     const int32_t t0 = a.page_tile0[p];
     const int64_t first_row = pg.first_row;
     uint16_t* mark = reinterpret_cast<uint16_t*>(smem + Ly.mark) + wv * kTileRows;
@@ -1927,7 +1927,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     }
     __syncthreads();
     if (a.debug & 32768) return;  // timing: + def levels
-    if (sh[0]) return to_exact();
+    if (sh[0]) return to_exact(8);
     if (wv == 0) {  // first rank of each tile (ntp <= 64)
         const uint32_t v = lane() < ntp ? tnn[lane()] : 0u;
         const uint32_t inc = wave_incl_scan(v);

@@ -1,6 +1,7 @@
-"""k_pipe_big step-5 diagnostics (fused_debug bit 27): per page, the def /
-index record counts, header-list lengths, error flag, segments and def
-record capacity, reported through the page error record."""
+"""k_pipe_big diagnostics (fused_debug bit 27): the first page (walk order)
+that a step would send to the exact decoder, as pos = the step (1 shape,
+2 prologue, 3 header lists, 4 records [+16 flag, +32 no def records, +64 no
+index records], 8 levels above max_def), need = the page, size = its bytes."""
 import os
 import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
