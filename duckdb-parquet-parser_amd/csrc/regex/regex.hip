@@ -253,34 +253,6 @@ __device__ __forceinline__ uint32_t sel_below(I i, uint32_t rem, uint32_t t, uin
     return r;
 }
 
-// e ^ (byte K of w): one v_xor_b32 with an SDWA byte select on its second source
-template <uint32_t K>
-__device__ __forceinline__ uint32_t xor_byte(uint32_t e, uint32_t w) {
-    uint32_t r;
-    if constexpr (K == 0)
-        __asm__("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
-                : "=v"(r) : "v"(e), "v"(w));
-    else if constexpr (K == 1)
-        __asm__("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
-                : "=v"(r) : "v"(e), "v"(w));
-    else if constexpr (K == 2)
-        __asm__("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
-                : "=v"(r) : "v"(e), "v"(w));
-    else
-        __asm__("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
-                : "=v"(r) : "v"(e), "v"(w));
-    return r;
-}
-// the same for a byte index the unrolled loops make constant
-__device__ __forceinline__ uint32_t xor_byte_k(uint32_t e, uint32_t w, uint32_t k) {
-    switch (k & 3u) {
-        case 0: return xor_byte<0>(e, w);
-        case 1: return xor_byte<1>(e, w);
-        case 2: return xor_byte<2>(e, w);
-        default: return xor_byte<3>(e, w);
-    }
-}
-
 __device__ __forceinline__ void lane_err(DevErr* e, int32_t* any, int code, uint32_t pos, uint32_t need,
                                          uint32_t size) {
     e->code = code;
@@ -530,17 +502,11 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                                                                   const uint16_t* __restrict__ index_in,
                                                                   uint16_t* __restrict__ index_out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
-    // Full tables are rebuilt in LDS as bytes: T8[state << 8 | (byte ^
-    // (state << 2))] = next state, A8[state] = accepts at the string end (a
-    // full table has < 64 states).  The lane's state register holds
-    // E = state * 0x104 (state << 8 | state << 2), so a step is one SDWA
-    // v_xor (E with byte i of the block: the address), one ds_read_u8 and one
-    // v_mul_u32_u24 for the next E.  The XOR spreads a row's dwords over the
-    // LDS banks by state: with the plain state << 8 | byte layout every lane
-    // reading a byte of the same 4-byte group (text is mostly a few such
-    // groups) hit the same bank, and lanes in different states conflicted
-    // (SQ_LDS_BANK_CONFLICT ~2.9 extra cycles per lookup on C3).  Class
-    // tables are copied as they are.
+    // Full tables are rebuilt in LDS as bytes: T8[state << 8 | byte] = next
+    // state, A8[state] = accepts at the string end (a full table has < 64
+    // states).  The DFA step is then one v_perm (state and byte into the
+    // address) and one ds_read_u8, against a shift, an add and a ds_read_u16
+    // over the u16 byte-offset rows.  Class tables are copied as they are.
     const DevDfa* Dg = reinterpret_cast<const DevDfa*>(dfa_img);
     if (Dg->full) {
         const uint4* src = reinterpret_cast<const uint4*>(dfa_img);
@@ -549,11 +515,8 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
         const uint16_t* Tg = reinterpret_cast<const uint16_t*>(dfa_img + sizeof(DevDfa));
         uint8_t* T8w = dsm + sizeof(DevDfa);
         const uint32_t nst = Dg->nstates;
-        for (uint32_t i = threadIdx.x; i < nst * 256; i += blockDim.x) {  // i = state << 8 | byte
-            const uint32_t st = i >> 8, b = i & 255;
-            T8w[(st << 8) | (b ^ ((st << 2) & 0xFCu))] =
-                static_cast<uint8_t>(Tg[st * (kDfaRowBytes / 2) + b] / kDfaRowBytes);
-        }
+        for (uint32_t i = threadIdx.x; i < nst * 256; i += blockDim.x)
+            T8w[i] = static_cast<uint8_t>(Tg[(i >> 8) * (kDfaRowBytes / 2) + (i & 255)] / kDfaRowBytes);
         for (uint32_t st = threadIdx.x; st < nst; st += blockDim.x)
             T8w[nst * 256 + st] = Tg[st * (kDfaRowBytes / 2) + 256] != 0 ? 1 : 0;
     } else {
@@ -859,7 +822,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                 off2[h] = ent;
                 len2[h] = ok2[h] ? st_u32(stage, ent - 4) : 0u;
                 pg2[h] = gl;
-                e2[h] = full ? DFA_START * 0x104u : DFA_START;
+                e2[h] = DFA_START;
             }
             uint32_t maxl = 0;
 #pragma unroll
@@ -883,10 +846,10 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                     for (uint32_t i = 0; i < 16; i++) {
 #pragma unroll
                         for (uint32_t h = 0; h < kStrPerLane; h++) {
-                            // address = E ^ byte i of the block (one SDWA v_xor)
-                            const uint32_t a = xor_byte_k(e2[h], Aw[h][i >> 2], i);
+                            // address = state << 8 | byte i of the block (one v_perm)
+                            const uint32_t a = __builtin_amdgcn_perm(e2[h], Aw[h][i >> 2], 0x0C0C0400u | (i & 3));
                             const uint32_t t = T8c[a];
-                            e2[h] = sel_below(i, rem[h], __umul24(t, 0x104u), e2[h]);
+                            e2[h] = sel_below(i, rem[h], t, e2[h]);
                         }
                     }
                 } else {
@@ -904,8 +867,8 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
 #pragma unroll
             for (uint32_t h = 0; h < kStrPerLane; h++) {
                 const uint32_t e = e2[h];
-                const uint32_t st = full ? (e >> 8) : (e & 0x7FFFu);
-                const bool acc = full ? A8[st] != 0 : (e >> 15) != 0;
+                const uint32_t st = full ? e : (e & 0x7FFFu);
+                const bool acc = full ? A8[e] != 0 : (e >> 15) != 0;
                 const bool m = len2[h] == 0 ? empty_ok : (trivial || st == DFA_ACCEPT || acc);
                 const bool sat = ok2[h] && (static_cast<uint32_t>(m) != negv);
                 if (sat) atomicOr(&hit[pg2[h] >> 5], 1u << (pg2[h] & 31));
