@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__
 //             bare row offsets (the accept-at-end flag sits in column 256 of
 //             a row, read once per string), and the per-byte end-of-string
 //             selects are kept out of SGPR masks (C3: 0.119 ms, was 0.166).
-constexpr uint32_t kPlainWavesMax = 16;  // waves per workgroup: as many as the LDS holds (host)
+constexpr uint32_t kPlainWavesMax = 12;  // waves per workgroup: as many as the LDS holds (host), <= 3 per SIMD (VGPRs: the prefetch registers)
 constexpr uint32_t kStrPerLane = 4;  // strings interleaved per lane (independent DFA chains)
 
 // The u32 at byte a of the staged window (>= 8 readable bytes past a).
@@ -567,6 +567,12 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
     if (w + nwt < nwins) Bn = wins[w + nwt];
     DevPage pg{};
     if (lane() < static_cast<uint32_t>(B.np)) pg = pages[B.p0 + static_cast<int32_t>(lane())];
+    // the next window's bytes ride in registers while this window is scanned
+    // (windows of <= kPrefetchBlocks * 1 KiB; larger ones are copied in place)
+    constexpr uint32_t kPrefetchBlocks = 8;  // 16-byte blocks per lane
+    // (eight named registers: an array carried around the loop went to scratch)
+    uint4 R0, R1, R2, R3, R4, R5, R6, R7;
+    bool held = false;
     for (;;) {
         const pqk::DevBatch Bc = B;
         const DevPage pgc = pg;
@@ -577,8 +583,22 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
             if (lane() < static_cast<uint32_t>(Bn.np)) pgn = pages[Bn.p0 + static_cast<int32_t>(lane())];
             if (wn + nwt < nwins) Bnn = wins[wn + nwt];
         }
-        copy_blocks(reinterpret_cast<uint4*>(cur), reinterpret_cast<const uint4*>(bytes + Bc.img_lo), Bc.img_bytes / 16,
-                    lane(), kWave);
+        if (held) {
+            const uint32_t nb = Bc.img_bytes / 16;
+            uint4* dst = reinterpret_cast<uint4*>(cur);
+            const uint32_t b = lane();
+            if (b < nb) dst[b] = R0;
+            if (b + 1 * kWave < nb) dst[b + 1 * kWave] = R1;
+            if (b + 2 * kWave < nb) dst[b + 2 * kWave] = R2;
+            if (b + 3 * kWave < nb) dst[b + 3 * kWave] = R3;
+            if (b + 4 * kWave < nb) dst[b + 4 * kWave] = R4;
+            if (b + 5 * kWave < nb) dst[b + 5 * kWave] = R5;
+            if (b + 6 * kWave < nb) dst[b + 6 * kWave] = R6;
+            if (b + 7 * kWave < nb) dst[b + 7 * kWave] = R7;
+        } else {
+            copy_blocks(reinterpret_cast<uint4*>(cur), reinterpret_cast<const uint4*>(bytes + Bc.img_lo), Bc.img_bytes / 16,
+                        lane(), kWave);
+        }
         if (lane() < 2) reinterpret_cast<uint4*>(cur + Bc.img_bytes)[lane()] = make_uint4(0, 0, 0, 0);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -788,6 +808,16 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
                     cnt = 0;
                 }
             }
+        }
+        // the next window's bytes: issued now, stored at the top of the next
+        // iteration (after this window's DFA pass, which reads only LDS)
+        held = wn < nwins && Bn.img_bytes <= kPrefetchBlocks * kWave * 16;
+        if (held) {  // (clamped indices: unconditional loads, no branch around them)
+            const uint4* src = reinterpret_cast<const uint4*>(bytes + Bn.img_lo);
+            const uint32_t nb = Bn.img_bytes / 16, b = lane();
+            auto at = [&](uint32_t k) { return src[b + k * kWave < nb ? b + k * kWave : 0u]; };
+            R0 = at(0); R1 = at(1); R2 = at(2); R3 = at(3);
+            R4 = at(4); R5 = at(5); R6 = at(6); R7 = at(7);
         }
         // the window's first row: with the index being filed (REQUIRED chunk,
         // pages of consecutive rows), string g of the window is row fr0 + g and
