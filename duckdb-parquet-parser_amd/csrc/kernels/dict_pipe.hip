@@ -1654,7 +1654,8 @@ __device__ void big_scan(uint32_t* v, uint32_t m, uint32_t* part) {
 // lengths from the HBM entry table (dictionaries of more than 65,535 entries)
 template <bool kWide>
 __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int32_t* __restrict__ bigp,
-                                                          uint32_t* __restrict__ info, uint32_t nlens) {
+                                                          uint32_t* __restrict__ info, uint32_t nlens,
+                                                          uint32_t lds_cap) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int p = bigp[blockIdx.x];
     const DevPage pg = a.pages[p];
@@ -1692,7 +1693,9 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         if (tid == 0) info[p] = kFallback;
         if (wv == 0) exact_page_body<kWide>(a, *reinterpret_cast<CodeLds*>(smem), p, dict_n, ebase);
     };
-    if (n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes) return to_exact(1);
+    // (a layout past the launch's LDS never happens when the host sized it
+    // with big_lds_max; kept as the guard against reading outside it)
+    if (n > static_cast<uint32_t>(kBigTiles) * kTileRows || size > kBigMaxBytes || Ly.total > lds_cap) return to_exact(1);
 
     // 0. the payload slot and the dictionary's entry lengths -> LDS (before
     //    the prologue, which then reads the stage instead of HBM)
@@ -3061,7 +3064,16 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_fused(FusedArgs a) {
 
 }  // namespace
 
-uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens) { return big_layout(max_page_bytes, nlens).total; }
+// The launch's LDS: the largest layout any page up to max_page_bytes takes.
+// Past kBigSegBytes the jump table is half a page, so a page just under
+// kBigSegBytes (one segment) can need more than the largest page.
+static uint32_t big_lds_max(uint32_t max_page_bytes, uint32_t nlens) {
+    uint32_t t = big_layout(max_page_bytes, nlens).total;
+    if (max_page_bytes > kBigSegBytes) t = max(t, big_layout(kBigSegBytes, nlens).total);
+    return t;
+}
+
+uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens) { return big_lds_max(max_page_bytes, nlens); }
 
 bool pipe_match_wide_ok(uint32_t entries_cap) { return entries_cap <= kMatchWideMax; }
 
@@ -3196,15 +3208,15 @@ void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_page
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
                P.bsum, per, P.debug, P.write_waves};
     a.codes32 = P.codes32;
-    const uint32_t lds = big_layout(max_page_bytes, nlens).total;
+    const uint32_t lds = big_lds_max(max_page_bytes, nlens);
     if (wide) {
         ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_big<true>), lds);
         hipLaunchKernelGGL(k_pipe_big<true>, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
-                           const_cast<uint32_t*>(P.info), nlens);
+                           const_cast<uint32_t*>(P.info), nlens, lds);
     } else {
         ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_big<false>), lds);
         hipLaunchKernelGGL(k_pipe_big<false>, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
-                           const_cast<uint32_t*>(P.info), nlens);
+                           const_cast<uint32_t*>(P.info), nlens, lds);
     }
 }
 
