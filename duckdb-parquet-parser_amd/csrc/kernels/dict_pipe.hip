@@ -1505,20 +1505,20 @@ __host__ __device__ inline BigLayout big_layout(uint32_t size, uint32_t nlens) {
     L.P = (size + 16 + 15) / 16 * 16;            // = the payload slot (capi.hip)
     // the jump table covers the page in one segment, or (pages over
     // kBigSegBytes) in two halves one after the other
-    L.nseg = size > kBigSegBytes ? 2u : 1u;
+    L.nseg = size > kBigOneSeg ? 2u : 1u;
     L.H = L.nseg == 1 ? L.P : ((size + 1) / 2 + 15) / 16 * 16;  // positions per segment (a multiple of 16)
     L.LC = L.P / (2 * kBJump) + 8;               // listed headers per stream (runs are >= 2 bytes)
     L.stage = 0;                                 // P bytes: the payload slot
     L.tab = L.stage + L.P;                       // u16 per position of a segment; then H / 4 run records
     L.esum = L.tab + 2 * L.H;                    // u32 per listed header: values, then their exclusive scan
     L.ent = L.esum + 8 * L.LC;                   // u32 per listed header: position
-    // u32 per listed header: its re-parse's record count and flags (in place
-    // of its position for one segment; two segments read the next header's
-    // position as they parse, so they keep both)
-    L.meta = L.nseg == 1 ? L.ent : L.ent + 8 * L.LC;
+    // u32 per listed header: its re-parse's record count and flags, in place
+    // of its position (step 4 reads every position of a pass of headers
+    // before any of them is overwritten)
+    L.meta = L.ent;
     L.tvb = L.esum;                              // per tile: validity bits of rows 8l .. 8l + 7 (phase 6:
                                                  // over esum / ent, dead after phase 5)
-    const uint32_t xl = (L.nseg == 1 ? 16u : 24u) * L.LC;
+    const uint32_t xl = 16u * L.LC;
     const uint32_t x = xl > static_cast<uint32_t>(kBigTiles * kWave) ? xl : static_cast<uint32_t>(kBigTiles * kWave);
     L.lens = L.esum + x;                         // u16 per dictionary entry: length
     L.mark = L.lens + (2 * nlens + 15) / 16 * 16;  // per wave: u16 per row of a tile
@@ -1825,14 +1825,20 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     uint2* reci = recd + rcap_d;
     const uint32_t ne = nld + nli;
     uint32_t* meta = reinterpret_cast<uint32_t*>(smem + Ly.meta);
-    for (uint32_t i = tid; i < ne; i += kBigThreads) {
+    // (passes of kBigThreads headers: every position of a pass is read before
+    // the barrier, its meta written over it after; the next pass's first
+    // position, a stop of this one, is still unwritten)
+    for (uint32_t i0 = 0; i0 < ne; i0 += kBigThreads) {
+        const uint32_t i = i0 + tid;
         const bool isd = i < nld;
         const uint32_t li = isd ? i : i - nld;
         const uint32_t slot = isd ? i : Ly.LC + li;
-        uint32_t q = ent[slot];
+        uint32_t q = i < ne ? ent[slot] : 0u;
         // the next listed header: kBJump runs on, or fewer where a jump
         // stopped at a segment end
-        const uint32_t stop = Ly.nseg > 1 && li + 1 < (isd ? nld : nli) ? ent[slot + 1] : 0xFFFFFFFFu;
+        const uint32_t stop = i < ne && Ly.nseg > 1 && li + 1 < (isd ? nld : nli) ? ent[slot + 1] : 0xFFFFFFFFu;
+        __syncthreads();
+        if (i >= ne) continue;
         const uint32_t e = isd ? dend : iend, bw = isd ? bwd : bwi, nbv = (bw + 7) / 8;
         const uint32_t vmask = nbv >= 3 ? 0xFFFFFFu : (nbv == 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u));
         const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
@@ -3065,11 +3071,11 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_fused(FusedArgs a) {
 }  // namespace
 
 // The launch's LDS: the largest layout any page up to max_page_bytes takes.
-// Past kBigSegBytes the jump table is half a page, so a page just under
-// kBigSegBytes (one segment) can need more than the largest page.
+// Past kBigOneSeg the jump table is half a page, so a page just under
+// kBigOneSeg (one segment) can need more than the largest page.
 static uint32_t big_lds_max(uint32_t max_page_bytes, uint32_t nlens) {
     uint32_t t = big_layout(max_page_bytes, nlens).total;
-    if (max_page_bytes > kBigSegBytes) t = max(t, big_layout(kBigSegBytes, nlens).total);
+    if (max_page_bytes > kBigOneSeg) t = max(t, big_layout(kBigOneSeg, nlens).total);
     return t;
 }
 

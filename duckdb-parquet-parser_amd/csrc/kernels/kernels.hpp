@@ -130,7 +130,8 @@ void launch_fixed(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int
 // ── three-pass dictionary BYTE_ARRAY path (dict_pipe.hip) ──────────────────
 constexpr uint32_t kPipeRunCap = 128;  // run records per stream per page
 constexpr int32_t kPipeSmallRows = 2048;   // larger pages take k_pipe_big (one workgroup per page)
-constexpr uint32_t kBigSegBytes = 24576;   // k_pipe_big: payload bytes one jump-table segment covers
+constexpr uint32_t kBigSegBytes = 24576;   // k_pipe_big: payload bytes one jump-table segment covers (at most)
+constexpr uint32_t kBigOneSeg = 18432;     // k_pipe_big: larger pages take two segments (two workgroups per CU up to ~26 KiB)
 constexpr uint32_t kBigMaxBytes = 49152;   // k_pipe_big: payload bytes per page (staged; two segments past kBigSegBytes)
 constexpr uint32_t kBigLens = 8192;        // k_pipe_big: dictionary entry lengths held in LDS
 constexpr int32_t kBigTiles = 64;          // k_pipe_big: 512-row tiles per page
