@@ -1758,20 +1758,28 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     const bool walker = tid == 0 || tid == kWave, isd_w = tid == 0;
     uint32_t wq = isd_w ? dbase : ibase, wk = 0;  // step 3's chain position and list length (walker threads)
     bool wdone = !walker || (isd_w && !hasd);
-    for (uint32_t sg = 0; sg < Ly.nseg; sg++) {
-        const uint32_t base = sg * Ly.H, lim = min(size, base + Ly.H);
+    // one body for both shapes; the one-segment instance (kOne) compiles
+    // the round-3 loops exactly (no segment offsets or bounds)
+    auto segment = [&](uint32_t sg, auto one_t) -> bool {
+        constexpr bool kOne = decltype(one_t)::value;
+        const uint32_t base = kOne ? 0u : sg * Ly.H, lim = kOne ? size : min(size, base + Ly.H);
         const uint32_t npair = (lim - base + 1) / 2;
         for (uint32_t jp = tid; jp < npair; jp += kBigThreads)
             tab32[jp] = next_at(base + 2 * jp) | (next_at(base + 2 * jp + 1) << 16);
         __syncthreads();
-        if (a.debug & 0x20000) return;  // timing: + header parse
+        if (a.debug & 0x20000) return false;  // timing: + header parse
         // 2. kBJump-run jumps by pointer doubling, two positions per thread
         //    (one dword of the table read and written)
         {
             auto hop = [&](uint32_t t) {  // kBStop and positions past the segment stay
-                const bool in = t >= base && t < lim;
-                const uint32_t u = tab[in ? t - base : 0u];
-                return in ? u : t;
+                if constexpr (kOne) {
+                    const uint32_t u = tab[t == kBStop ? 0u : t];
+                    return t == kBStop ? kBStop : u;
+                } else {
+                    const bool in = t >= base && t < lim;
+                    const uint32_t u = tab[in ? t - base : 0u];
+                    return in ? u : t;
+                }
             };
             for (int r = 0; r < kBJumpLog; r++) {
                 uint32_t nv[kBigPerThread / 2];
@@ -1796,7 +1804,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
                 __syncthreads();
             }
         }
-        if (a.debug & 4096) return;  // timing: jump table only
+        if (a.debug & 4096) return false;  // timing: jump table only
         // 3. one lane per stream follows the jumps: every kBJump-th header
         //    (and the first header past a segment end)
         if (walker && !wdone) {
@@ -1804,7 +1812,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
             const uint32_t lcap = rc > kBJump + 1 ? min(Ly.LC, (rc - kBJump - 1) / kBJump + 1) : 0u;
             uint32_t* L = ent + (isd_w ? 0u : Ly.LC);
             for (;;) {
-                if (wq < e && wq >= lim) break;  // listed by the next segment
+                if (!kOne && wq < e && wq >= lim) break;  // listed by the next segment
                 if (wk >= lcap) { wk = ~0u; wdone = true; break; }
                 L[wk++] = wq;
                 if (wq >= e) { wdone = true; break; }
@@ -1813,7 +1821,14 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
                 wq = t;
             }
         }
-        __syncthreads();  // the next segment rewrites the table
+        if (!kOne) __syncthreads();  // the next segment rewrites the table
+        return true;
+    };
+    if (Ly.nseg == 1) {
+        if (!segment(0u, std::true_type{})) return;
+    } else {
+        for (uint32_t sg = 0; sg < Ly.nseg; sg++)
+            if (!segment(sg, std::false_type{})) return;
     }
     if (walker) sh[isd_w ? 1 : 2] = wk;
     __syncthreads();
