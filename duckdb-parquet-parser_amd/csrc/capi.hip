@@ -2057,10 +2057,17 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
                               ctx->opt_debug, dict_in_runs ? &rd : nullptr, fused ? c->fstage - 16 : 0u,
                               (c->pipe_small_bytes + 15) / 16 * 16 + 16, c->max_dict_bytes, ctx->cus);
     }
-    if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
+    // the wide pipe's k_pipe_big writes raw indices and needs no dictionary:
+    // it runs beside the dictionary's decode, k_wide_chars after both
+    if (dict_on_side && c->ndicts && !c->pipe_wide) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
     if (!c->hbig.empty()) {
         Timed t(ctx, "pipe_big");
         pqk::launch_pipe_big(s, P, c->d_bigp, static_cast<int>(c->hbig.size()), c->big_max_bytes);
+    }
+    if (c->pipe_wide) {
+        if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
+        Timed t(ctx, "wide_chars");
+        pqk::launch_wide_chars(s, P);
     }
     if (c->pipe_count) {
         Timed t(ctx, "pipe_count");

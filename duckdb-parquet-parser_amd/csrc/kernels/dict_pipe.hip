@@ -347,8 +347,11 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
     SRle def, idx;
     srle_init(def, dbase, dlen, bwd);
     srle_init(idx, pos, size - pos, bwi);
+    // (kWide: the raw index; k_wide_chars and the writer test it against the
+    // dictionary, which may still be decoding while this runs)
     auto put_ix = [&](uint32_t k, uint32_t v) {
-        ix[k] = static_cast<CodeT>(static_cast<int32_t>(v) >= 0 && v < dict_n ? v : static_cast<uint32_t>(kNullT));
+        if constexpr (kWide) ix[k] = v;
+        else ix[k] = static_cast<CodeT>(static_cast<int32_t>(v) >= 0 && v < dict_n ? v : static_cast<uint32_t>(kNullT));
     };
     for (uint32_t r0 = 0, ti = 0; r0 < n; r0 += kTileRows, ti++) {
         const uint32_t m = min(n - r0, static_cast<uint32_t>(kTileRows));
@@ -380,15 +383,17 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
             CodeT code = kNullT;
             if (nnul) {
                 code = ix[k];
-                if (code != kNullT) chars += static_cast<uint32_t>(a.entries[ebase + code] >> 32);
+                if (!kWide && code != kNullT) chars += static_cast<uint32_t>(a.entries[ebase + code] >> 32);
             }
             if (j < m) {
                 if (kWide) a.codes32[pg.first_row + r0 + j] = code;
                 else a.codes[pg.first_row + r0 + j] = static_cast<uint16_t>(code);
             }
         }
-        chars = wave_sum(chars);
-        tile_done(a, t0 + static_cast<int>(ti), chars);
+        if (!kWide) {  // (kWide: k_wide_chars sums the tiles' characters)
+            chars = wave_sum(chars);
+            tile_done(a, t0 + static_cast<int>(ti), chars);
+        }
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -1993,11 +1998,11 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
             const uint2 R = reci[ri0 + keep_if(nz, mark[nz ? rk : 0u])];
             const uint32_t lb = big_bits(stw, nw, rr_pay(R) + __umul24(k0 + rk - rr_start(R), bwi), bwi);
             const uint32_t v = keep_if(rr_lit(R), lb) | keep_if(!rr_lit(R), rr_pay(R));
-            const bool ok = nz && v < dict_n;
+            // kWide: the raw index of every non-NULL row (the dictionary may
+            // still be decoding: k_wide_chars and the writer test it)
+            const bool ok = kWide ? nz : (nz && v < dict_n);
             const uint32_t code = keep_if(ok, v) | keep_if(!ok, kWide ? kNull32 : kNull);
-            if (kWide) {  // lengths from the entry table (L2): all eight loads in flight
-                if (dict_n) chars += keep_if(ok, static_cast<uint32_t>(a.entries[ebase + (ok ? v : 0u)] >> 32));
-            } else {
+            if (!kWide) {
                 const bool inl = ok && v < nl;
                 chars += keep_if(inl, lens[inl ? v : 0u]);
                 far |= (ok && !inl ? 1u : 0u) << k;
@@ -2009,12 +2014,52 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
             for (int k = 0; k < 8; k++)
                 if ((far >> k) & 1u) chars += static_cast<uint32_t>(a.entries[ebase + cw8[k]] >> 32);
         }
-        if (kWide) store_codes8w(a.codes32, R0, l8, m, cw8);
-        else store_codes8(a.codes, R0, l8, m, cw8);
-        chars = wave_sum(chars);
-        tile_done(a, t0 + static_cast<int>(ti), chars);
+        if (kWide) {
+            store_codes8w(a.codes32, R0, l8, m, cw8);
+        } else {
+            store_codes8(a.codes, R0, l8, m, cw8);
+            chars = wave_sum(chars);
+            tile_done(a, t0 + static_cast<int>(ti), chars);
+        }
         __builtin_amdgcn_wave_barrier();
     }
+}
+
+// Wide pipe: each tile's characters from its raw 32-bit codes, once the
+// dictionary is decoded (k_pipe_big<true> ran beside that decode): one wave
+// per tile, the entry words of a lane's eight rows loaded at once; codes at or
+// past the dictionary's entry count are NULL rows (the writer skips them too).
+constexpr int kWideCharWaves = 4;
+__global__ void __launch_bounds__(kWideCharWaves * 64) k_wide_chars(CodeArgs a) {
+    const int t = static_cast<int>(blockIdx.x) * kWideCharWaves + static_cast<int>(threadIdx.x / kWave);
+    if (t >= a.ntiles) return;
+    const DevTile T = a.tiles[t];
+    const uint32_t m = static_cast<uint32_t>(T.nrows), l8 = lane() * 8;
+    const int64_t R0 = a.pages[T.page].first_row + T.row0;
+    const uint32_t dict_n = static_cast<uint32_t>(max(a.dict_count[a.dict_id], 0));
+    const uint64_t* es = a.entries + a.dicts[a.dict_id].entry_base;
+    uint32_t c[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) c[k] = kNull32;
+    if (l8 + 8 <= m) {
+        const U16B* p = reinterpret_cast<const U16B*>(a.codes32 + R0 + l8);
+        const U16B x = p[0], y = p[1];
+        c[0] = x.x; c[1] = x.y; c[2] = x.z; c[3] = x.w; c[4] = y.x; c[5] = y.y; c[6] = y.z; c[7] = y.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (l8 + k < m) c[k] = a.codes32[R0 + l8 + k];
+    }
+    uint32_t chars = 0;
+    if (dict_n) {
+        uint64_t e[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) e[k] = es[min(c[k], dict_n - 1u)];
+#pragma unroll
+        for (int k = 0; k < 8; k++) chars += c[k] < dict_n ? static_cast<uint32_t>(e[k] >> 32) : 0u;
+    }
+    chars = wave_sum(chars);
+    tile_done(a, t, chars);
 }
 
 // ── regex page filter over the codes (README.md:54-64, SURVEY §8a R-REGEX) ─
@@ -3239,6 +3284,18 @@ void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_page
         hipLaunchKernelGGL(k_pipe_big<false>, dim3(nbig), dim3(kBigThreads), lds, s, a, big_pages,
                            const_cast<uint32_t*>(P.info), nlens, lds);
     }
+}
+
+void launch_wide_chars(hipStream_t s, const PipeLaunch& P) {
+    if (P.ntiles <= 0 || !P.codes32) return;
+    int wgrid = 0, per = 0;
+    write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_wwide's workgroups
+    CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
+               P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
+               P.bsum, per, P.debug, P.write_waves};
+    a.codes32 = P.codes32;
+    hipLaunchKernelGGL(k_wide_chars, dim3((P.ntiles + kWideCharWaves - 1) / kWideCharWaves), dim3(kWideCharWaves * kWave),
+                       0, s, a);
 }
 
 uint32_t pipe_front_slot(uint32_t max_page_bytes) { return (max_page_bytes + 15) / 16 * 16 + 16; }

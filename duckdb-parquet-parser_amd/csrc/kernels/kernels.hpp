@@ -237,6 +237,9 @@ uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens);
 // the regex filter over the wide pipe's codes holds one match bit per entry in LDS
 bool pipe_match_wide_ok(uint32_t entries_cap);
 void launch_pipe_big(hipStream_t s, const PipeLaunch& P, const int32_t* big_pages, int nbig, uint32_t max_page_bytes);
+// wide pipe: every tile's characters from the raw 32-bit codes k_pipe_big<true>
+// wrote (after the dictionary decode), filed for k_pipe_wwide
+void launch_wide_chars(hipStream_t s, const PipeLaunch& P);
 // regex page filter on the codes: page_flags[p] = 1 unless a non-null row of
 // page p matches (neg: fails to match); match = dictionary match bits
 void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags,
