@@ -157,7 +157,7 @@ struct pq_chunk {
     int64_t nentries = 0;
     uint32_t max_dict_bytes = 0;        // largest dictionary payload
     // dictionary pages too large for k_dict_index's LDS (launch_dict_big)
-    struct BigDict { int di; pqk::DevDict d; size_t cand_off, scr_off; };
+    struct BigDict { int di; pqk::DevDict d; size_t scr_off, lens_off, pad_off; };
     std::vector<BigDict> hbigd;
     uint8_t* d_bigd = nullptr;          // their scratch
     uint32_t max_page_bytes = 0;        // largest data-page payload
@@ -499,8 +499,12 @@ static void plan_pipe_wide(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages,
         big_bytes = std::max(big_bytes, static_cast<uint32_t>(pg.size));
     }
     if (pqk::pipe_big_lds(big_bytes, 0) > 160u * 1024) return;
-    const int wpw = std::max(1, std::min(16, ctx->opt_write_waves));
-    pqk::PipePlan pl = pqk::plan_pipe_wide(wpw);
+    // a dictionary page past k_dict_index's LDS decodes in launch_dict_big,
+    // which also files its 16-byte entry slots: the writer keeps one per row
+    // of its tile in LDS (12 KiB per wave: four waves per workgroup)
+    const bool pad = static_cast<uint64_t>(std::max(d.size, 0)) + 32 > pqk::kDictLdsCap;
+    const int wpw = std::max(1, std::min(pad ? 4 : 16, ctx->opt_write_waves));
+    pqk::PipePlan pl = pqk::plan_pipe_wide(wpw, pad);
     if (pl.blocks_per_cu == 0) return;
     if (ctx->opt_write_bpc > 0) pl.blocks_per_cu = std::min(pl.blocks_per_cu, ctx->opt_write_bpc);
     c->pipe = true;
@@ -1507,11 +1511,13 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             for (size_t i = 0; i < hdicts.size(); i++) {
                 const uint32_t sz = static_cast<uint32_t>(std::max(hdicts[i].size, 0));
                 if (static_cast<uint64_t>(sz) + 32 <= pqk::kDictLdsCap) continue;
-                const size_t nsl = pqk::dict_big_slices(sz);
-                pq_chunk::BigDict b{static_cast<int>(i), hdicts[i], off, 0};
-                off += (nsl * pqk::kPCandDHost * sizeof(uint2) + 255) / 256 * 256;
-                b.scr_off = off;
-                off += ((3 * nsl + 4) * sizeof(uint32_t) + 255) / 256 * 256;
+                pq_chunk::BigDict b{static_cast<int>(i), hdicts[i], off, 0, 0};
+                off += (pqk::dict_big_scratch(sz) + 255) / 256 * 256;
+                const size_t nv = static_cast<size_t>(std::max(hdicts[i].nvals, 0));
+                b.lens_off = off;  // entry lengths as bytes (+ 16: k_wide_chars stages whole blocks)
+                off += (nv + 16 + 255) / 256 * 256;
+                b.pad_off = off;   // 16-byte entry slots (k_pipe_wwide)
+                off += (nv * 16 + 255) / 256 * 256;
                 c->hbigd.push_back(b);
             }
             if (off) rc |= dalloc(&c->d_bigd, off);
@@ -2003,6 +2009,12 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (c->pipe_wide) {
         P.codes32 = reinterpret_cast<uint32_t*>(c->d_codes);
         P.codes = nullptr;
+        for (const auto& b : c->hbigd)
+            if (b.di == c->pipe_dict) {
+                P.lens8 = c->d_bigd + b.lens_off;
+                P.lens8_cap = static_cast<uint32_t>(std::max(b.d.nvals, 0));
+                P.pad16 = reinterpret_cast<const uint4*>(c->d_bigd + b.pad_off);
+            }
     }
     P.tile_chars = c->d_tile_chars; P.bsum = c->d_bsum; P.total = c->d_total;
     P.nrows_total = c->nrows; P.overflow = c->d_flags + 1;
@@ -2030,13 +2042,14 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
 // k_dict_index for every dictionary page of a BYTE_ARRAY chunk, and the
 // multi-workgroup index for pages too large for its LDS.
 static void launch_dicts(pq_chunk* c, hipStream_t s, int32_t* err_any) {
-    pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, err_any,
+    if (c->hbigd.size() < static_cast<size_t>(c->ndicts))  // k_dict_index leaves the large pages alone
+        pqk::launch_dict_index(s, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, err_any,
                            c->max_dict_bytes);
     for (const auto& b : c->hbigd)
         pqk::launch_dict_big(s, c->d_bytes + b.d.off, static_cast<uint32_t>(b.d.size), static_cast<uint32_t>(std::max(b.d.nvals, 0)),
-                             c->d_entries + b.d.entry_base, c->d_dict_count + b.di, c->d_dict_err + b.di, err_any,
-                             reinterpret_cast<uint2*>(c->d_bigd + b.cand_off),
-                             reinterpret_cast<uint32_t*>(c->d_bigd + b.scr_off));
+                             c->d_entries + b.d.entry_base, c->d_bigd + b.lens_off,
+                             reinterpret_cast<uint4*>(c->d_bigd + b.pad_off), c->d_dict_count + b.di,
+                             c->d_dict_err + b.di, err_any, reinterpret_cast<uint32_t*>(c->d_bigd + b.scr_off));
 }
 
 static bool front_path(pq_ctx* ctx, const pq_chunk* c) { return c->pipe_fr && c->d_fwins && ctx->opt_front; }

@@ -65,31 +65,39 @@ __global__ void __launch_bounds__(kDictWaves * 64) k_dict_index(const uint8_t* _
 }
 
 // ── dictionary pages larger than LDS (k_dict_index's serial walk) ───────────
-// The fine-slice scheme of dict_index_fine over HBM, as three launches:
-//   k_dict_cand  per 256-byte slice (each wave stages 16 slices in LDS): the
-//                first kPCandD plausible entry starts among its first 64
-//                bytes and the chain from each to the slice end;
-//   k_dict_link  one workgroup: slice t is entered at slice t-1's exit (the
-//                exit of its latest continuing candidate), every slice must
-//                hold a candidate at that entry leaving where it advertised;
-//                a scan of the chosen chains' counts; anything uncertain (a
-//                failed link, a bounds error in the last chain short of the
-//                count) falls back to the serial walk here, which also gives
-//                the reference's exact error (column_reader.cpp:128-138);
-//   k_dict_fill  one lane per slice re-walks its chosen chain writing
-//                (len << 32 | pos) entries.
-constexpr uint32_t kBSlices = 16;  // slices per wave in k_dict_cand
+// The fine-slice scheme of dict_index_fine over HBM, as two launches:
+//   k_dict_slices  one wave per kLSlices 256-byte slices, staged in LDS with
+//                  the slice before them: per slice the first kPCandD
+//                  plausible entry starts among its first 64 bytes and the
+//                  chain from each to the slice end; each slice is entered at
+//                  the previous slice's exit (the exit of its first
+//                  continuing candidate; slice 0 at 0) and must hold a
+//                  candidate there leaving where it advertised.  Per slice
+//                  (count | ok | chain error) and its entry; per wave the
+//                  count sum and whether all its slices linked;
+//   k_dict_fill    kFSlices slices per workgroup: every workgroup sums the
+//                  wave words (all linked? entries before it?), stages its
+//                  slices in LDS and re-walks the chosen chains writing
+//                  (len << 32 | pos) entries.  Anything uncertain (a failed
+//                  link, a bounds error in the last chain short of the
+//                  count) is the serial walk of workgroup 0, which gives the
+//                  reference's exact error (column_reader.cpp:128-138).
+// scratch: slice words [nsl], slice entries [nsl], wave words [ceil(nsl / kLSlices)]
+constexpr uint32_t kLSlices = 15;   // new slices per wave in k_dict_slices
+constexpr uint32_t kFSlices = 240;  // slices per workgroup in k_dict_fill (16 k_dict_slices waves)
 
-__global__ void __launch_bounds__(256) k_dict_cand(const uint8_t* __restrict__ page, uint32_t size, uint32_t nsl,
-                                                   uint2* __restrict__ cand) {
-    __shared__ uint32_t stw[4][(kBSlices * kDSlice + 16) / 4 + 2];
+__global__ void __launch_bounds__(256) k_dict_slices(const uint8_t* __restrict__ page, uint32_t size, uint32_t nsl,
+                                                     uint32_t* __restrict__ scr) {
+    __shared__ uint32_t stw[4][(16 * kDSlice + 16) / 4 + 2];
     const uint32_t w = threadIdx.x / kWave, l = lane();
-    const uint32_t g = (blockIdx.x * 4 + w) * kBSlices;
-    if (g >= nsl) return;
+    const uint32_t wv = blockIdx.x * 4 + w;
+    const uint32_t s0 = wv * kLSlices;  // first slice of this wave; slot j holds slice s0 - 1 + j
+    if (s0 >= nsl) return;
+    const uint32_t j0 = s0 == 0 ? 1u : 0u;   // wave 0 has no slice before its own
+    const uint32_t base = (s0 - 1 + j0) * kDSlice;  // a multiple of 256: the page is 16-byte aligned in the image
     uint32_t* words = stw[w];
-    const uint32_t base = g * kDSlice;  // a multiple of 256: the page is 16-byte aligned in the image
     {
-        const uint32_t nb = min(kBSlices * kDSlice + 16, (size - base + 15) / 16 * 16 + 16) / 16;
+        const uint32_t nb = min((16 - j0) * kDSlice + 16, (size - base + 15) / 16 * 16 + 16) / 16;
         const uint4* src = reinterpret_cast<const uint4*>(page + base);
         for (uint32_t i = l; i < nb; i += kWave) reinterpret_cast<uint4*>(words)[i] = src[i];
     }
@@ -98,20 +106,21 @@ __global__ void __launch_bounds__(256) k_dict_cand(const uint8_t* __restrict__ p
     const uint32_t jm = l / kPCandD, sl = l % kPCandD;
     uint64_t mk = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < kBSlices; j++) {
-        const uint32_t sc = g + j, cs = sc * kDSlice;
+    for (uint32_t j = 0; j < 16; j++) {
+        const uint32_t sc = s0 - 1 + j, cs = sc * kDSlice;
+        const bool sv = j >= j0 && sc < nsl;
         const uint32_t q = cs + l, ce = min(cs + kDSlice, size);
-        bool plaus = sc < nsl && q < ce && q + 4 <= size &&
+        bool plaus = sv && q < ce && q + 4 <= size &&
                      static_cast<uint64_t>(q) + 4 + lds_u32(words, min(q, size) - base) <= size;
-        if (sc == 0) plaus = l == 0;
+        if (sv && sc == 0) plaus = l == 0;
         const uint64_t m = __ballot(plaus);
         if (j == jm) mk = m;
     }
-    const uint32_t sc = g + jm;
     for (uint32_t i = 0; i < sl; i++) mk &= mk - 1;
-    if (sc >= nsl) return;
-    uint2 rec = make_uint2(kDNone, kDNone);
-    if (mk) {
+    const uint32_t sc = s0 - 1 + jm;
+    const bool sv = jm >= j0 && sc < nsl;
+    uint32_t rx = kDNone, ry = kDNone;  // exit, count | entry << 8 | error << 31
+    if (sv && mk) {
         const uint32_t cs = sc * kDSlice, ce = min(cs + kDSlice, size);
         const uint32_t e = static_cast<uint32_t>(__builtin_ctzll(mk));
         uint32_t q = cs + e, cnt = 0, bad = 0;
@@ -122,110 +131,128 @@ __global__ void __launch_bounds__(256) k_dict_cand(const uint8_t* __restrict__ p
             q += 4 + len;
             cnt++;
         }
-        rec = make_uint2(q, cnt | (e << 8) | (bad << 31));
+        rx = q;
+        ry = cnt | (e << 8) | (bad << 31);
     }
-    cand[sc * kPCandD + sl] = rec;
-}
-
-// slice t's chosen chain: entry = exit advertised by slice t-1
-__device__ __forceinline__ uint32_t big_cexit(const uint2* cand, uint32_t t) {
-    const uint32_t se = (t + 1) * kDSlice;
-    uint32_t cx = kDNone;
+    // the slot's four candidates (every lane of the slot holds them all)
+    uint32_t cx[kPCandD], cy[kPCandD];
 #pragma unroll
-    for (int k = static_cast<int>(kPCandD) - 1; k >= 0; k--) {
-        const uint2 r = cand[t * kPCandD + k];
-        if (r.x != kDNone && !(r.y >> 31) && r.x >= se && r.x < se + 64) cx = r.x;
+    for (uint32_t k = 0; k < kPCandD; k++) {
+        cx[k] = __shfl(rx, static_cast<int>(jm * kPCandD + k));
+        cy[k] = __shfl(ry, static_cast<int>(jm * kPCandD + k));
     }
-    return cx;
+    // the slot's advertised exit: its first continuing candidate
+    const uint32_t se = (sc + 1) * kDSlice;
+    uint32_t cexit = kDNone;
+#pragma unroll
+    for (int k = static_cast<int>(kPCandD) - 1; k >= 0; k--)
+        if (cx[k] != kDNone && !(cy[k] >> 31) && cx[k] >= se && cx[k] < se + 64) cexit = cx[k];
+    const uint32_t prev = __shfl(cexit, static_cast<int>((jm == 0 ? 0u : jm - 1) * kPCandD));
+    const uint32_t e = sc == 0 ? 0u : prev;
+    uint32_t px = kDNone, py = kDNone;
+#pragma unroll
+    for (uint32_t k = 0; k < kPCandD; k++)
+        if (cx[k] != kDNone && sc * kDSlice + ((cy[k] >> 8) & 0x3Fu) == e) { px = cx[k]; py = cy[k]; }
+    const bool mine = jm >= 1 && sv;  // this wave's own slices
+    const bool lastc = sc + 1 == nsl;
+    const bool ok = px != kDNone && (lastc || (!(py >> 31) && px == cexit));
+    const uint32_t c = (mine && sl == 0 && ok) ? (py & 0xFFu) : 0u;
+    if (mine && sl == 0) {
+        scr[sc] = c | ((py >> 31) << 30) | (ok ? 0x80000000u : 0u);
+        scr[nsl + sc] = e;
+    }
+    const uint32_t tot = __shfl(wave_incl_scan(c), kWave - 1);
+    const bool wok = __ballot(mine && sl == 0 && !ok) == 0;
+    if (l == 0) scr[2 * nsl + wv] = tot | (wok ? 0x80000000u : 0u);
 }
 
-// scratch: cnt[nsl], ent[nsl], bef[nsl], then misc[4] (mode: 1 = fill)
-__global__ void __launch_bounds__(1024) k_dict_link(const uint8_t* __restrict__ page, uint32_t size, uint32_t n,
-                                                    uint32_t nsl, const uint2* __restrict__ cand,
-                                                    uint32_t* __restrict__ scr, uint64_t* __restrict__ out,
-                                                    int32_t* __restrict__ count, DevErr* __restrict__ err,
-                                                    int32_t* __restrict__ err_any) {
-    __shared__ uint32_t wsum[16];
-    __shared__ int all_ok;
-    __shared__ uint32_t carry, last_bad;
-    uint32_t* cnt = scr;
-    uint32_t* ent = scr + nsl;
-    uint32_t* bef = scr + 2 * nsl;
-    uint32_t* misc = scr + 3 * nsl;
+__global__ void __launch_bounds__(256) k_dict_fill(const uint8_t* __restrict__ page, uint32_t size, uint32_t n,
+                                                   uint32_t nsl, const uint32_t* __restrict__ scr,
+                                                   uint64_t* __restrict__ out, uint8_t* __restrict__ lens8,
+                                                   uint4* __restrict__ pad16, int32_t* __restrict__ count,
+                                                   DevErr* __restrict__ err, int32_t* __restrict__ err_any) {
+    __shared__ __attribute__((aligned(16))) uint32_t words[(kFSlices * kDSlice + 48) / 4];
+    __shared__ uint32_t red[3][4];
+    __shared__ uint32_t wsum[4];
     const uint32_t t0 = threadIdx.x, w = t0 / kWave, l = lane();
-    if (t0 == 0) { all_ok = n > 0 && size > 0; carry = 0; last_bad = 0; }
-    __syncthreads();
-    for (uint32_t b = 0; b < nsl; b += blockDim.x) {
-        const uint32_t t = b + t0;
-        uint32_t c = 0;
-        if (t < nsl) {
-            const uint32_t e = t == 0 ? 0u : big_cexit(cand, t - 1);
-            const uint32_t cx = big_cexit(cand, t);
-            uint2 pr = make_uint2(kDNone, kDNone);
-#pragma unroll
-            for (uint32_t k = 0; k < kPCandD; k++) {
-                const uint2 r = cand[t * kPCandD + k];
-                if (r.x != kDNone && t * kDSlice + ((r.y >> 8) & 0x3Fu) == e) pr = r;
-            }
-            const bool lastc = t + 1 == nsl;
-            const bool ok = pr.x != kDNone && (lastc || (!(pr.y >> 31) && pr.x == cx));
-            if (!ok) all_ok = 0;
-            if (lastc) last_bad = pr.y >> 31;
-            c = ok ? (pr.y & 0xFFu) : 0u;
-            cnt[t] = c;
-            ent[t] = e;
-        }
-        const uint32_t inc = wave_incl_scan(c);
-        if (l == kWave - 1) wsum[w] = inc;
-        __syncthreads();
-        uint32_t before = carry + inc - c;
-        uint32_t tot = 0;
-        for (uint32_t v = 0; v < blockDim.x / kWave; v++) {
-            if (v < w) before += wsum[v];
-            tot += wsum[v];
-        }
-        if (t < nsl) bef[t] = before;
-        __syncthreads();
-        if (t0 == 0) carry += tot;
-        __syncthreads();
+    const uint32_t nwv = (nsl + kLSlices - 1) / kLSlices;
+    const uint32_t wb = blockIdx.x * (kFSlices / kLSlices);  // first k_dict_slices wave of this workgroup
+    uint32_t tot = 0, bef = 0, bad = 0;
+    for (uint32_t v = t0; v < nwv; v += blockDim.x) {
+        const uint32_t x = scr[2 * nsl + v];
+        tot += x & 0x7FFFFFFFu;
+        bef += v < wb ? (x & 0x7FFFFFFFu) : 0u;
+        bad |= (x >> 31) ^ 1u;
     }
-    const uint32_t total = carry;
-    const bool fine = all_ok && !(total < n && last_bad);
-    if (w != 0) return;
-    if (fine) {
-        if (total < n) set_err(err, err_any, PQ_ERR_BUFFER, size, 4, size);
-        if (l == 0) {
-            *count = static_cast<int32_t>(min(total, n));
-            misc[0] = 1;
+    tot = __shfl(wave_incl_scan(tot), kWave - 1);
+    bef = __shfl(wave_incl_scan(bef), kWave - 1);
+    bad = __ballot(bad != 0) != 0;
+    if (l == 0) { red[0][w] = tot; red[1][w] = bef; red[2][w] = bad; }
+    __syncthreads();
+    tot = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    bef = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    bad = red[2][0] | red[2][1] | red[2][2] | red[2][3];
+    const bool last_bad = nsl > 0 && ((scr[nsl - 1] >> 30) & 1u);
+    const bool fine = n > 0 && size > 0 && nsl > 0 && !bad && !(tot < n && last_bad);
+    if (!fine) {
+        // serial walk (workgroup 0, wave 0, scalar loads): the reference's order and errors
+        if (blockIdx.x != 0 || w != 0) return;
+        uint32_t pos = 0, k = 0;
+        for (; k < n; k++) {
+            if (static_cast<uint64_t>(pos) + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); break; }
+            const uint32_t len = suni(sload_u32(page, pos));
+            pos += 4;
+            if (static_cast<uint64_t>(pos) + len > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, len, size); break; }
+            if (l == 0) {
+                out[k] = entry_code(len, pos);
+                if (lens8) lens8[k] = static_cast<uint8_t>(min(len, 255u));
+                if (pad16) pad16[k] = make_uint4(0u, 0u, 0u, 0xFF000000u);  // (the entry word's path)
+            }
+            pos += len;
         }
+        if (l == 0) *count = static_cast<int32_t>(k);
         return;
     }
-    // serial walk (wave 0, scalar loads): the reference's order and errors
-    if (l == 0) misc[0] = 0;
-    uint32_t pos = 0, k = 0;
-    for (; k < n; k++) {
-        if (static_cast<uint64_t>(pos) + 4 > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, 4, size); break; }
-        const uint32_t len = suni(sload_u32(page, pos));
-        pos += 4;
-        if (static_cast<uint64_t>(pos) + len > size) { set_err(err, err_any, PQ_ERR_BUFFER, pos, len, size); break; }
-        if (l == 0) out[k] = entry_code(len, pos);
-        pos += len;
+    if (blockIdx.x == 0 && w == 0) {
+        // the chain reached the page end with entries still declared
+        if (tot < n) set_err(err, err_any, PQ_ERR_BUFFER, size, 4, size);
+        if (l == 0) *count = static_cast<int32_t>(min(tot, n));
     }
-    if (l == 0) *count = static_cast<int32_t>(k);
-}
-
-__global__ void __launch_bounds__(256) k_dict_fill(const uint8_t* __restrict__ page, uint32_t n, uint32_t nsl,
-                                                   const uint32_t* __restrict__ scr, uint64_t* __restrict__ out) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (scr[3 * nsl] != 1 || t >= nsl) return;
-    const uint32_t before = scr[2 * nsl + t];
-    if (before >= n) return;
-    const uint32_t m = min(scr[t], n - before);
-    const uint32_t* pw = reinterpret_cast<const uint32_t*>(page);
-    uint32_t q = scr[nsl + t];
+    const uint32_t base = blockIdx.x * kFSlices * kDSlice;
+    {
+        // (+ 32: the characters of an entry starting at the last slice's end)
+        const uint32_t nb = min(kFSlices * kDSlice + 32, (size - base + 15) / 16 * 16 + 16) / 16;
+        const uint4* src = reinterpret_cast<const uint4*>(page + base);
+        for (uint32_t i = t0; i < nb; i += blockDim.x) reinterpret_cast<uint4*>(words)[i] = src[i];
+    }
+    const uint32_t t = blockIdx.x * kFSlices + t0;
+    const bool has = t0 < kFSlices && t < nsl;
+    const uint32_t c = has ? (scr[t] & 0xFFu) : 0u;
+    uint32_t q = has ? scr[nsl + t] : 0u;
+    const uint32_t inc = wave_incl_scan(c);
+    if (l == kWave - 1) wsum[w] = inc;
+    __syncthreads();
+    uint32_t before = bef + inc - c;
+    for (uint32_t v = 0; v < w; v++) before += wsum[v];
+    if (!has || before >= n) return;
+    const uint32_t m = min(c, n - before);
     for (uint32_t k = 0; k < m; k++) {
-        const uint32_t len = __builtin_amdgcn_alignbyte(pw[(q >> 2) + 1], pw[q >> 2], q & 3);
+        const uint32_t len = lds_u32(words, q - base);
         out[before + k] = entry_code(len, q + 4);
+        if (lens8) lens8[before + k] = static_cast<uint8_t>(min(len, 255u));
+        if (pad16) {  // characters 0..14 and the length in byte 15 (0xFF: 16 or more, the entry word's path)
+            uint4 v = make_uint4(0u, 0u, 0u, 0xFF000000u);
+            if (len <= 15) {
+                const uint32_t a = q + 4 - base, wi = a >> 2, sh = a & 3;
+                const uint32_t w0 = words[wi], w1 = words[wi + 1], w2 = words[wi + 2], w3 = words[wi + 3],
+                               w4 = words[wi + 4];
+                v.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                v.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                v.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+                v.w = (__builtin_amdgcn_alignbyte(w4, w3, sh) & 0x00FFFFFFu) | (len << 24);
+            }
+            pad16[before + k] = v;
+        }
         q += 4 + len;
     }
 }
@@ -919,19 +946,18 @@ void set_fused_attrs() {
 
 uint32_t dict_big_slices(uint32_t size) { return (size + kDSlice - 1) / kDSlice; }
 
-void launch_dict_big(hipStream_t s, const uint8_t* page, uint32_t size, uint32_t nvals, uint64_t* entries,
-                     int32_t* count, DevErr* err, int32_t* err_any, uint2* cand, uint32_t* scr) {
+uint32_t dict_big_scratch(uint32_t size) {
     const uint32_t nsl = dict_big_slices(size);
-    if (nsl == 0) {
-        hipLaunchKernelGGL(k_dict_link, dim3(1), dim3(1024), 0, s, page, size, nvals, 0u, cand, scr, entries, count,
-                           err, err_any);
-        return;
-    }
-    hipLaunchKernelGGL(k_dict_cand, dim3((nsl + 4 * kBSlices - 1) / (4 * kBSlices)), dim3(256), 0, s, page, size, nsl,
-                       cand);
-    hipLaunchKernelGGL(k_dict_link, dim3(1), dim3(1024), 0, s, page, size, nvals, nsl, cand, scr, entries, count, err,
-                       err_any);
-    hipLaunchKernelGGL(k_dict_fill, dim3((nsl + 255) / 256), dim3(256), 0, s, page, nvals, nsl, scr, entries);
+    return (2 * nsl + (nsl + kLSlices - 1) / kLSlices) * static_cast<uint32_t>(sizeof(uint32_t));
+}
+
+void launch_dict_big(hipStream_t s, const uint8_t* page, uint32_t size, uint32_t nvals, uint64_t* entries,
+                     uint8_t* lens8, uint4* pad16, int32_t* count, DevErr* err, int32_t* err_any, uint32_t* scr) {
+    const uint32_t nsl = dict_big_slices(size);
+    const uint32_t nwv = (nsl + kLSlices - 1) / kLSlices;
+    if (nwv) hipLaunchKernelGGL(k_dict_slices, dim3((nwv + 3) / 4), dim3(256), 0, s, page, size, nsl, scr);
+    hipLaunchKernelGGL(k_dict_fill, dim3(std::max<uint32_t>(1, (nsl + kFSlices - 1) / kFSlices)), dim3(256), 0, s, page,
+                       size, nvals, nsl, scr, entries, lens8, pad16, count, err, err_any);
 }
 
 int fused_occupancy_waves(uint32_t lds_bytes_per_block, int waves_per_block) {

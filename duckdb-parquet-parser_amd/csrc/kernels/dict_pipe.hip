@@ -249,6 +249,7 @@ struct CodeArgs {
     int debug;                 // 256: skip the exact decoder (timing only)
     int wpw;                   // k_pipe_write's writer waves per workgroup (bsum index)
     uint32_t* codes32 = nullptr;  // wide chunks: 32-bit codes here instead of `codes` (k_pipe_big<true>)
+    const uint8_t* lens8 = nullptr;  // wide chunks: entry lengths as bytes (255: 255 or more), or null
 };
 
 // Characters of tile t also go to the k_pipe_write workgroup that writes it.
@@ -932,6 +933,7 @@ struct WriteArgs {
     int match_neg;
     uint8_t* page_flags;
     const uint32_t* codes32 = nullptr;  // wide chunks (k_pipe_wwide)
+    const uint4* pad16 = nullptr;       // wide chunks: 16-byte entry slots (k_pipe_wwide<true>), or null
 };
 
 
@@ -1231,13 +1233,20 @@ struct __attribute__((aligned(16))) WideLds {
 };
 static_assert(sizeof(WideLds) % 16 == 0, "per-wave scratch alignment");
 constexpr int kWideBatch = 2;  // tiles whose codes a wave loads at once (8 u32 per lane each)
+// kPad: the dictionary's 16-byte entry slots (launch_dict_big's pad16): one
+// load per row gives the length and up to 15 characters, kept per row in LDS
+// (after every wave's WideLds) until the row-per-lane character stores; rows
+// of 16 or more bytes read the entry word and the payload as without
+constexpr uint32_t kWideRowBytes = kTileRows * 16;
 
+template <bool kPad>
 __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     if (a.znext)  // the other flags/bsum/flist block, for the next decode (unused by this one)
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.znext_words; i += gridDim.x * blockDim.x) a.znext[i] = 0;
     const uint32_t wv = threadIdx.x / kWave;
     WideLds& S = reinterpret_cast<WideLds*>(smem)[wv];
+    uint4* rows = reinterpret_cast<uint4*>(smem + a.wpw * sizeof(WideLds) + wv * kWideRowBytes);
     const DevDict d = a.dicts[a.dict_id];
     const uint32_t dict_n = static_cast<uint32_t>(max(a.dict_count[a.dict_id], 0));
     const uint64_t* es = a.entries + d.entry_base;
@@ -1319,18 +1328,47 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                 const bool first = i == ib;
                 const uint4 lo = first ? c0lo : c1lo, hi = first ? c0hi : c1hi;
                 const uint32_t cur[kRowsPerLane] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-                // this lane's rows 8l .. 8l + 7: entry words (all eight loads in flight)
-                uint64_t e[kRowsPerLane];
-#pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++) e[k] = dict_n ? es[min(cur[k], dict_n - 1u)] : 0ull;
                 uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc8 = 0;
+                if constexpr (kPad) {
+                    // this lane's rows 8l .. 8l + 7: entry slots (all eight loads in flight)
+                    uint4 sl[kRowsPerLane];
 #pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++) {
-                    const bool valid = cur[k] < dict_n;
-                    len[k] = valid ? static_cast<uint32_t>(e[k] >> 32) : 0u;
-                    src[k] = valid ? static_cast<uint32_t>(e[k]) : 0u;
-                    vb |= (valid ? 1u : 0u) << k;
-                    acc8 += len[k];
+                    for (int k = 0; k < kRowsPerLane; k++)
+                        sl[k] = dict_n ? a.pad16[min(cur[k], dict_n - 1u)] : make_uint4(0u, 0u, 0u, 0u);
+                    uint32_t far = 0;
+#pragma unroll
+                    for (int k = 0; k < kRowsPerLane; k++) {
+                        const bool valid = cur[k] < dict_n;
+                        len[k] = valid ? (sl[k].w >> 24) : 0u;
+                        src[k] = 0;
+                        far |= (len[k] == 0xFFu ? 1u : 0u) << k;
+                        vb |= (valid ? 1u : 0u) << k;
+                        rows[lane() * kRowsPerLane + k] = sl[k];
+                    }
+                    if (__ballot(far != 0)) {  // rows of 16 or more bytes: the entry word
+#pragma unroll
+                        for (int k = 0; k < kRowsPerLane; k++)
+                            if ((far >> k) & 1u) {
+                                const uint64_t e = es[cur[k]];
+                                len[k] = static_cast<uint32_t>(e >> 32);
+                                src[k] = static_cast<uint32_t>(e);
+                            }
+                    }
+#pragma unroll
+                    for (int k = 0; k < kRowsPerLane; k++) acc8 += len[k];
+                } else {
+                    // this lane's rows 8l .. 8l + 7: entry words (all eight loads in flight)
+                    uint64_t e[kRowsPerLane];
+#pragma unroll
+                    for (int k = 0; k < kRowsPerLane; k++) e[k] = dict_n ? es[min(cur[k], dict_n - 1u)] : 0ull;
+#pragma unroll
+                    for (int k = 0; k < kRowsPerLane; k++) {
+                        const bool valid = cur[k] < dict_n;
+                        len[k] = valid ? static_cast<uint32_t>(e[k] >> 32) : 0u;
+                        src[k] = valid ? static_cast<uint32_t>(e[k]) : 0u;
+                        vb |= (valid ? 1u : 0u) << k;
+                        acc8 += len[k];
+                    }
                 }
                 const uint32_t incl = wave_incl_scan(acc8);
                 const uint32_t total = bcast_last(incl);
@@ -1415,8 +1453,18 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                             sa = S.src[r];
                         }
                         const uint32_t l16 = ln[q] <= 16 ? ln[q] : 0u;
-                        A[q] = *reinterpret_cast<const U8B*>(dsrc + sa);
-                        B[q] = *reinterpret_cast<const U8B*>(dsrc + sa + (l16 >= 8 ? l16 - 8 : 0u));
+                        if (kPad && ln[q] <= 15) {  // from the row's slot: bytes 0..7 and ln-8 .. ln-1
+                            const uint4 x = rows[r < m ? r : 0u];
+                            const uint64_t lo = (static_cast<uint64_t>(x.y) << 32) | x.x;
+                            const uint64_t hi = (static_cast<uint64_t>(x.w) << 32) | x.z;
+                            const uint32_t o = l16 >= 8 ? l16 - 8 : 0u;
+                            const uint64_t b = o ? ((lo >> (8 * o)) | (hi << (64 - 8 * o))) : lo;
+                            A[q] = U8B{x.x, x.y};
+                            B[q] = U8B{static_cast<uint32_t>(b), static_cast<uint32_t>(b >> 32)};
+                        } else {
+                            A[q] = *reinterpret_cast<const U8B*>(dsrc + sa);
+                            B[q] = *reinterpret_cast<const U8B*>(dsrc + sa + (l16 >= 8 ? l16 - 8 : 0u));
+                        }
                     }
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
@@ -2060,6 +2108,75 @@ __global__ void __launch_bounds__(kWideCharWaves * 64) k_wide_chars(CodeArgs a) 
     }
     chars = wave_sum(chars);
     tile_done(a, t, chars);
+}
+
+// The same with the entry lengths as bytes in LDS (launch_dict_big's lens8,
+// dictionaries up to kWideLensLds entries): persistent workgroups of
+// kWideLWaves waves stage the table once, then each wave takes kWideLBatch
+// consecutive tiles per step, all their codes loaded before the first
+// lookup.  A length byte of 255 (255 or more) is read from the entry table.
+constexpr int kWideLWaves = 16;
+constexpr int kWideLBatch = 4;
+constexpr uint32_t kWideLensLds = 120 * 1024;
+__global__ void __launch_bounds__(kWideLWaves * 64) k_wide_chars_lds(CodeArgs a, uint32_t cap) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t l8s[];
+    const uint32_t dict_n = min(static_cast<uint32_t>(max(a.dict_count[a.dict_id], 0)), cap);
+    copy_blocks(reinterpret_cast<uint4*>(l8s), reinterpret_cast<const uint4*>(a.lens8), (dict_n + 15) / 16,
+                threadIdx.x, blockDim.x);
+    __syncthreads();
+    const uint64_t* es = a.entries + a.dicts[a.dict_id].entry_base;
+    const uint32_t l8 = lane() * 8;
+    const int wv = static_cast<int>(threadIdx.x / kWave);
+    for (int b = (static_cast<int>(blockIdx.x) * kWideLWaves + wv) * kWideLBatch; b < a.ntiles;
+         b += static_cast<int>(gridDim.x) * kWideLWaves * kWideLBatch) {
+        // the batch's tile descriptors (lane k: tile b + k), then their rows
+        uint32_t td_m = 0;
+        int64_t td_r = 0;
+        if (lane() < static_cast<uint32_t>(kWideLBatch) && b + static_cast<int>(lane()) < a.ntiles) {
+            const DevTile T = a.tiles[b + lane()];
+            td_m = static_cast<uint32_t>(T.nrows);
+            td_r = a.pages[T.page].first_row + T.row0;
+        }
+        uint32_t c[kWideLBatch][8];
+        uint32_t mm[kWideLBatch];
+#pragma unroll
+        for (int k = 0; k < kWideLBatch; k++) {
+            const uint32_t m = __shfl(td_m, k);
+            const int64_t R0 = __shfl(td_r, k);
+            mm[k] = m;
+#pragma unroll
+            for (int j = 0; j < 8; j++) c[k][j] = kNull32;
+            if (l8 + 8 <= m) {
+                const U16B* p = reinterpret_cast<const U16B*>(a.codes32 + R0 + l8);
+                const U16B x = p[0], y = p[1];
+                c[k][0] = x.x; c[k][1] = x.y; c[k][2] = x.z; c[k][3] = x.w;
+                c[k][4] = y.x; c[k][5] = y.y; c[k][6] = y.z; c[k][7] = y.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (l8 + j < m) c[k][j] = a.codes32[R0 + l8 + j];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kWideLBatch; k++) {
+            if (b + k >= a.ntiles) break;  // (uniform)
+            uint32_t chars = 0, far = 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t v = c[k][j];
+                const uint32_t ln = v < dict_n ? static_cast<uint32_t>(l8s[v]) : 0u;
+                far |= (ln == 255u ? 1u : 0u) << j;
+                chars += ln;
+            }
+            if (__ballot(far != 0)) {  // (255 or more: the entry table's length)
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if ((far >> j) & 1u) chars += static_cast<uint32_t>(es[c[k][j]] >> 32) - 255u;
+            }
+            (void)mm[k];
+            tile_done(a, b + k, wave_sum(chars));
+        }
+    }
 }
 
 // ── regex page filter over the codes (README.md:54-64, SURVEY §8a R-REGEX) ─
@@ -3228,11 +3345,13 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     if (P.has_small) hipLaunchKernelGGL(k_pipe_codes3, dim3(grid), dim3(kCodeWaves3 * kWave), lds, s, a, lt_n, P.flist);
 }
 
-PipePlan plan_pipe_wide(int wpw) {
+PipePlan plan_pipe_wide(int wpw, bool pad) {
     PipePlan pl{};
-    pl.lds = static_cast<uint32_t>(wpw) * static_cast<uint32_t>(sizeof(WideLds));
+    pl.lds = static_cast<uint32_t>(wpw) * static_cast<uint32_t>(sizeof(WideLds) + (pad ? kWideRowBytes : 0u));
     pl.blocks_per_cu = min(4, static_cast<int>((160u * 1024) / pl.lds));
-    const int occ = resident_blocks(reinterpret_cast<const void*>(k_pipe_wwide), wpw * kWave, pl.lds);
+    const int occ = resident_blocks(pad ? reinterpret_cast<const void*>(k_pipe_wwide<true>)
+                                        : reinterpret_cast<const void*>(k_pipe_wwide<false>),
+                                    wpw * kWave, pl.lds);
     pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
     return pl;
 }
@@ -3240,14 +3359,22 @@ PipePlan plan_pipe_wide(int wpw) {
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
     if (P.ntiles <= 0) return;
     if (P.codes32) {  // wide dictionary: codes and dictionary from HBM
-        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_wwide), P.lds);
         int grid = 0, per = 0;
         write_shape(P, &grid, &per);
         WriteArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.dicts, P.dict_id, P.entries, P.dict_count, nullptr,
                     P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
                     P.chars, 0u, 0u, P.debug, P.write_waves, P.znext, P.znext_words, nullptr, 0, nullptr};
         a.codes32 = P.codes32;
-        hipLaunchKernelGGL(k_pipe_wwide, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
+        // (the plan sized P.lds for the slots whenever the dictionary has them)
+        const uint32_t need_pad = static_cast<uint32_t>(P.write_waves) * (sizeof(WideLds) + kWideRowBytes);
+        if (P.pad16 && P.lds >= need_pad && !(P.debug & (1 << 29))) {  // (bit 29: entry words, for A/B)
+            a.pad16 = P.pad16;
+            ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_wwide<true>), P.lds);
+            hipLaunchKernelGGL(k_pipe_wwide<true>, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
+        } else {
+            ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_wwide<false>), P.lds);
+            hipLaunchKernelGGL(k_pipe_wwide<false>, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
+        }
         return;
     }
     ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_write<false>), P.lds);
@@ -3294,6 +3421,15 @@ void launch_wide_chars(hipStream_t s, const PipeLaunch& P) {
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
                P.bsum, per, P.debug, P.write_waves};
     a.codes32 = P.codes32;
+    if (P.lens8 && P.lens8_cap <= kWideLensLds && !(P.debug & (1 << 28))) {  // (bit 28: k_wide_chars, for A/B)
+        const uint32_t lds = (P.lens8_cap + 15) / 16 * 16 + 16;
+        ensure_dyn_lds(reinterpret_cast<const void*>(k_wide_chars_lds), kWideLensLds + 16);
+        a.lens8 = P.lens8;
+        const int need = (P.ntiles + kWideLWaves * kWideLBatch - 1) / (kWideLWaves * kWideLBatch);
+        hipLaunchKernelGGL(k_wide_chars_lds, dim3(std::max(1, std::min(P.cus, need))), dim3(kWideLWaves * kWave), lds, s, a,
+                           P.lens8_cap);
+        return;
+    }
     hipLaunchKernelGGL(k_wide_chars, dim3((P.ntiles + kWideCharWaves - 1) / kWideCharWaves), dim3(kWideCharWaves * kWave),
                        0, s, a);
 }

@@ -187,6 +187,14 @@ struct PipeLaunch {
     // here (0xFFFFFFFF = NULL) instead of `codes`; P.lds / P.grid are then
     // plan_pipe_wide's
     uint32_t* codes32 = nullptr;
+    // the wide dictionary's entry lengths as bytes (255: 255 or more; from
+    // launch_dict_big) and their capacity, or null: k_wide_chars then reads
+    // the entry table
+    const uint8_t* lens8 = nullptr;
+    uint32_t lens8_cap = 0;
+    // the same dictionary as 16-byte slots (launch_dict_big's pad16), or
+    // null: k_pipe_wwide then reads entry words and characters
+    const uint4* pad16 = nullptr;
 };
 constexpr uint32_t kArmDictBytes = 32768;  // every entry length < 2^15: the match bit rides in the entry word
 struct PipePlan {
@@ -194,8 +202,9 @@ struct PipePlan {
     int blocks_per_cu;  // 0: the dictionary does not fit
 };
 PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw);
-// k_pipe_wwide (dictionary in HBM): per-wave scratch only
-PipePlan plan_pipe_wide(int wpw);
+// k_pipe_wwide (dictionary in HBM): per-wave scratch only (pad: + the rows'
+// 16-byte entry slots, k_pipe_wwide<true>)
+PipePlan plan_pipe_wide(int wpw, bool pad);
 // k_pipe_fused: tiles per unit, and its LDS / resident workgroups per CU for
 // `wpw` waves per workgroup and a payload stage of `stage` bytes per wave
 int pipe_fused_tiles();
@@ -298,16 +307,19 @@ struct DevBatch {
 
 // Dictionary pages whose payload + 32 bytes exceed kDictLdsCap are skipped
 // by k_dict_index and decoded by launch_dict_big (one call per such page:
-// page = its payload in the image, entries/count/err = its slots; scratch:
-// cand dict_big_slices(size) * 4 uint2, scr 3 * slices + 4 u32).
+// page = its payload in the image, entries/count/err = its slots, lens8
+// (or null): min(length, 255) per entry, pad16 (or null): per entry its
+// characters 0..14 and its length in byte 15 (0xFF: 16 or more); scratch:
+// dict_big_scratch(size) bytes, no zeroing needed).
 constexpr uint32_t kDictLdsCap = 128 * 1024;
 constexpr uint32_t kPCandDHost = 4;  // candidates per slice (dict_index.hpp kPCandD)
 void launch_dict_index(hipStream_t s, const uint8_t* bytes, const DevDict* dicts, int ndicts,
                        uint64_t* entries, int32_t* dict_count, DevErr* dict_err, int32_t* err_any,
                        uint32_t max_dict_bytes);
 uint32_t dict_big_slices(uint32_t size);
+uint32_t dict_big_scratch(uint32_t size);
 void launch_dict_big(hipStream_t s, const uint8_t* page, uint32_t size, uint32_t nvals, uint64_t* entries,
-                     int32_t* count, DevErr* err, int32_t* err_any, uint2* cand, uint32_t* scr);
+                     uint8_t* lens8, uint4* pad16, int32_t* count, DevErr* err, int32_t* err_any, uint32_t* scr);
 void launch_ba_fused(hipStream_t s, const FusedLaunch& L);
 uint32_t fused_wave_bytes(uint32_t rows_cap, uint32_t stage_bytes);
 int fused_occupancy_waves(uint32_t lds_bytes_per_block, int waves_per_block);
