@@ -111,6 +111,7 @@ struct pq_ctx {
     int opt_regex_index = 1;     // "regex_index": REQUIRED PLAIN chunks keep the string index of their first scan;
                                  // 2: every scan is a first scan (files the index again: the cold-scan timing)
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
+    int opt_regex_pre = 1;       // "regex_prefetch": the next window's bytes in registers (1), or not (0: four waves per SIMD)
     int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_fixed_fused = false; // "fixed_fused": OPTIONAL ones scatter their values in the levels launch (slower: DESIGN §5)
@@ -283,6 +284,7 @@ struct pq_chunk {
     uint32_t rwin_bytes = 0, rwin_for_dfa = 0;
     int rwin_grid = 0;
     int rwin_opt = 0;                   // regex_win the windows were planned with
+    int rwin_pre = -1;                  // and regex_prefetch
     uint32_t dfa_bytes = 0;
     bool dfa_full = false;               // the DFA image has full 256-column rows
     std::string prog_pattern;           // pattern of d_prog / d_dfa
@@ -999,6 +1001,10 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "stage_piece_kb") == 0) {
         if (value < 64 || value > 65536) return set_err(ctx, PQ_ERR_ARG, "stage_piece_kb: 64..65536");
         ctx->stager.configure(ctx->opt_stage_bufs, static_cast<size_t>(value) << 10);
+        return 0;
+    }
+    if (std::strcmp(key, "regex_prefetch") == 0) {
+        ctx->opt_regex_pre = value ? 1 : 0;
         return 0;
     }
     if (std::strcmp(key, "regex_win") == 0) {
@@ -2577,14 +2583,17 @@ int pq_regex_compile_check(const char* pattern, char* err, size_t errlen) {
 // k_regex_plain): <= 64 pages and <= win bytes of image each.  False when a
 // page does not fit (the lane-per-page kernel runs then).
 bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
-    if (c->d_rwins && c->rwin_for_dfa == c->dfa_bytes && c->rwin_opt == ctx->opt_regex_win) return true;
+    const bool pre = ctx->opt_regex_pre != 0;
+    if (c->d_rwins && c->rwin_for_dfa == c->dfa_bytes && c->rwin_opt == ctx->opt_regex_win &&
+        c->rwin_pre == ctx->opt_regex_pre)
+        return true;
     const uint32_t maxslot = c->npages ? (c->max_page_bytes + 15) / 16 * 16 + 16 : 0u;
     const uint32_t win = std::max<uint32_t>(static_cast<uint32_t>(ctx->opt_regex_win), maxslot);
     // the kernel lists strings by u16 window offsets (and the string index
     // keeps them): pages whose slot leaves no room take k_regex_lanes
     if (win + 32 > 65535u) return false;
-    if (pqre::regex_plain_waves(c->dfa_bytes, win) == 0) return false;
-    const uint32_t lds = pqre::regex_plain_lds(c->dfa_bytes, win);
+    if (pqre::regex_plain_waves(c->dfa_bytes, win, pre) == 0) return false;
+    const uint32_t lds = pqre::regex_plain_lds(c->dfa_bytes, win, pre);
     if (lds > 160 * 1024) return false;
     c->hrwins.clear();
     // the PLAIN decode's windows are the same kind (<= 64 consecutive page
@@ -2624,7 +2633,8 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     c->rwin_bytes = win;
     c->rwin_for_dfa = c->dfa_bytes;
     c->rwin_opt = ctx->opt_regex_win;
-    const int scan = static_cast<int>(pqre::regex_plain_waves(c->dfa_bytes, win));  // waves per workgroup
+    c->rwin_pre = ctx->opt_regex_pre;
+    const int scan = static_cast<int>(pqre::regex_plain_waves(c->dfa_bytes, win, pre));  // waves per workgroup
     c->rwin_grid = std::max(1, std::min<int>(per_cu * cus, static_cast<int>((c->hrwins.size() + scan - 1) / scan)));
     (void)cus;
     return true;
@@ -2733,7 +2743,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             pqre::launch_regex_plain(s, c->d_dfa, c->dfa_bytes, c->rwin_bytes, c->d_bytes, c->d_pages, c->d_rwins,
                                      static_cast<int>(c->hrwins.size()), c->d_rwin_ticket, c->rwin_grid, cp,
                                      (neg ? 1 : 0) | ((ctx->opt_regex_debug & 0xFF) << 8),
-                                     c->d_page_flags, c->d_page_err, c->d_flags, idx_in, idx_out);
+                                     c->d_page_flags, c->d_page_err, c->d_flags, idx_in, idx_out, c->rwin_pre != 0);
         } else if (c->d_dfa) {
             Timed t(ctx, "regex_lanes");
             pqre::launch_regex_lanes(s, c->d_dfa, c->dfa_bytes, c->d_bytes, c->d_pages, c->npages, c->d_dicts,

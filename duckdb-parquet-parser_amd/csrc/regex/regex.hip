@@ -480,7 +480,11 @@ __global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__
 //             bare row offsets (the accept-at-end flag sits in column 256 of
 //             a row, read once per string), and the per-byte end-of-string
 //             selects are kept out of SGPR masks (C3: 0.119 ms, was 0.166).
-constexpr uint32_t kPlainWavesMax = 12;  // waves per workgroup: as many as the LDS holds (host), <= 3 per SIMD (VGPRs: the prefetch registers)
+// waves per workgroup: as many as the LDS holds (host); with the next
+// window's bytes prefetched into registers (kPre) <= 3 per SIMD (VGPRs),
+// without <= 4
+constexpr uint32_t kPlainWavesMax = 12;
+constexpr uint32_t kPlainWavesMaxNp = 16;
 constexpr uint32_t kStrPerLane = 4;  // strings interleaved per lane (independent DFA chains)
 
 // The u32 at byte a of the staged window (>= 8 readable bytes past a).
@@ -489,7 +493,8 @@ __device__ __forceinline__ uint32_t st_u32(const uint32_t* st, uint32_t a) {
     return __builtin_amdgcn_alignbyte(st[i + 1], st[i], sh);
 }
 
-__global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
+template <bool kPre>
+__global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
                                                                   uint32_t dfa_bytes, uint32_t win_bytes,
                                                                   const uint8_t* __restrict__ bytes,
                                                                   const DevPage* __restrict__ pages,
@@ -811,7 +816,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
         }
         // the next window's bytes: issued now, stored at the top of the next
         // iteration (after this window's DFA pass, which reads only LDS)
-        held = wn < nwins && Bn.img_bytes <= kPrefetchBlocks * kWave * 16;
+        held = kPre && wn < nwins && Bn.img_bytes <= kPrefetchBlocks * kWave * 16;
         if (held) {  // (clamped indices: unconditional loads, no branch around them)
             const uint4* src = reinterpret_cast<const uint4*>(bytes + Bn.img_lo);
             const uint32_t nb = Bn.img_bytes / 16, b = lane();
@@ -963,26 +968,31 @@ void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, c
                        dicts, dict_count, dict_match, cp, neg, page_flags, page_err, err_any);
 }
 
-uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes) {
+uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes, bool pre) {
     const uint32_t per = regex_plain_wave_lds(win_bytes);
     if (dfa_bytes + per > 160u * 1024) return 0;
-    return std::min<uint32_t>(kPlainWavesMax, (160u * 1024 - dfa_bytes) / per);
+    return std::min<uint32_t>(pre ? kPlainWavesMax : kPlainWavesMaxNp, (160u * 1024 - dfa_bytes) / per);
 }
 
-uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes) {
-    return dfa_bytes + regex_plain_waves(dfa_bytes, win_bytes) * regex_plain_wave_lds(win_bytes);
+uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes, bool pre) {
+    return dfa_bytes + regex_plain_waves(dfa_bytes, win_bytes, pre) * regex_plain_wave_lds(win_bytes);
 }
 
 void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
                         const uint8_t* bytes, const DevPage* pages, const pqk::DevBatch* wins, int nwins,
                         int32_t* ticket, int grid, ColumnParams cp, int neg, uint8_t* page_flags,
-                        DevErr* page_err, int32_t* err_any, const uint16_t* index_in, uint16_t* index_out) {
+                        DevErr* page_err, int32_t* err_any, const uint16_t* index_in, uint16_t* index_out, bool pre) {
     if (nwins <= 0) return;
-    pqk::ensure_dyn_lds(reinterpret_cast<const void*>(k_regex_plain), 160 * 1024);
-    hipLaunchKernelGGL(k_regex_plain, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes) * kWave),
-                       regex_plain_lds(dfa_bytes, win_bytes),
-                       s, dfa, dfa_bytes, win_bytes, bytes, pages, wins, nwins, ticket, cp, neg, page_flags,
-                       page_err, err_any, index_in, index_out);
+    const void* k = pre ? reinterpret_cast<const void*>(k_regex_plain<true>) : reinterpret_cast<const void*>(k_regex_plain<false>);
+    pqk::ensure_dyn_lds(k, 160 * 1024);
+    if (pre)
+        hipLaunchKernelGGL(k_regex_plain<true>, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes, true) * kWave),
+                           regex_plain_lds(dfa_bytes, win_bytes, true), s, dfa, dfa_bytes, win_bytes, bytes, pages, wins,
+                           nwins, ticket, cp, neg, page_flags, page_err, err_any, index_in, index_out);
+    else
+        hipLaunchKernelGGL(k_regex_plain<false>, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes, false) * kWave),
+                           regex_plain_lds(dfa_bytes, win_bytes, false), s, dfa, dfa_bytes, win_bytes, bytes, pages, wins,
+                           nwins, ticket, cp, neg, page_flags, page_err, err_any, index_in, index_out);
 }
 
 // k_regex_plain reads its byte-state table through a constant LDS address
@@ -992,8 +1002,9 @@ void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, u
 bool regex_plain_lds_ok() {
     static const bool ok = [] {
         hipFuncAttributes a{};
-        if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k_regex_plain)) != hipSuccess) return false;
-        return a.sharedSizeBytes == 0;
+        for (const void* k : {reinterpret_cast<const void*>(k_regex_plain<true>), reinterpret_cast<const void*>(k_regex_plain<false>)})
+            if (hipFuncGetAttributes(&a, k) != hipSuccess || a.sharedSizeBytes != 0) return false;
+        return true;
     }();
     return ok;
 }

@@ -23,3 +23,10 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_kt" -o kt --
 rc=$?; [ $rc -eq 0 ] || { echo "KT rc=$rc"; tail -20 "$OUT/prof_kt.log"; exit $rc; }
 cp "$OUT"/prof_kt/*kernel_stats.csv "$OUT/kernel_stats.csv"
 bash scripts/gpu_pmc_c2.sh "$TAG"
+rc=$?; [ $rc -eq 0 ] || exit $rc
+# the wide dictionary pipe's kernels (bench leg `wide_dict`): their own trace
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_wide" -o kw --output-format csv -- \
+    python3 scripts/ab_opts.py W 10000000 - > "$OUT/prof_wide.log" 2>&1
+rc=$?; [ $rc -eq 0 ] || { echo "WIDE KT rc=$rc"; tail -20 "$OUT/prof_wide.log"; exit $rc; }
+cp "$OUT"/prof_wide/*kernel_stats.csv "$OUT/kernel_stats_wide.csv"
+echo done
