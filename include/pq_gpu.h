@@ -153,6 +153,9 @@ int pq_ctx_sync(pq_ctx* ctx);
  *   "pipe_run_dict" 1 (default): dictionary pages up to 60 KiB decode in the
  *                 run-table launch (its leading workgroups), else in their own
  *                 launch on a side stream
+ *   "pipe_wide"   1 (default): dictionaries beyond the writer's LDS (or of more
+ *                 than 65,535 entries) take the wide pipe (32-bit codes, the
+ *                 dictionary decoded beside the front); 0: the generic path
  *   "plain_ba"    1 (default): two-pass PLAIN BYTE_ARRAY kernels
  *   "plain_fused" 1 (default): their one-pass form when every page's strings
  *                 fill it exactly (checked on the device; else the two passes)
@@ -178,7 +181,10 @@ int pq_ctx_sync(pq_ctx* ctx);
  *   "regex_dfa", "regex_plain", "regex_codes" 1 (default): DFA kernels, the
  *                 windowed kernel for dictionary-free chunks, match bits over
  *                 the pipe's codes; "regex_win" window bytes (1024..32768,
- *                 multiple of 16; 8192); "regex_reuse" 1 (default): a scan
+ *                 multiple of 16; 8192); "regex_prefetch" 1 (default): the
+ *                 windowed kernel holds the next window's bytes in registers
+ *                 (0: a lighter build of it, four waves per SIMD where the
+ *                 LDS allows); "regex_reuse" 1 (default): a scan
  *                 of a chunk whose earlier pipe decode was checked error-free
  *                 (pq_decode / pq_decode_check) reads that decode's codes
  *                 instead of recomputing them; "regex_index" 1 (default): a
