@@ -1238,6 +1238,9 @@ constexpr int kWideBatch = 2;  // tiles whose codes a wave loads at once (8 u32 
 // (after every wave's WideLds) until the row-per-lane character stores; rows
 // of 16 or more bytes read the entry word and the payload as without
 constexpr uint32_t kWideRowBytes = kTileRows * 16;
+constexpr uint32_t kWidePadVb = (kTileRows + 4) * 4;                 // k_pipe_wwide<true> per wave: offsets,
+constexpr uint32_t kWidePadRows = (kWidePadVb + kWave + 15) / 16 * 16;  // validity bytes, 16-byte row slots
+constexpr uint32_t kWidePadWave = kWidePadRows + kWideRowBytes;
 
 template <bool kPad>
 __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
@@ -1245,8 +1248,15 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
     if (a.znext)  // the other flags/bsum/flist block, for the next decode (unused by this one)
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.znext_words; i += gridDim.x * blockDim.x) a.znext[i] = 0;
     const uint32_t wv = threadIdx.x / kWave;
-    WideLds& S = reinterpret_cast<WideLds*>(smem)[wv];
-    uint4* rows = reinterpret_cast<uint4*>(smem + a.wpw * sizeof(WideLds) + wv * kWideRowBytes);
+    // per wave: WideLds, or (kPad) the offsets, the validity bytes and the
+    // rows' slots (a row of 16+ bytes keeps its payload position in its
+    // slot's first word)
+    uint8_t* wbase = smem + wv * (kPad ? kWidePadWave : static_cast<uint32_t>(sizeof(WideLds)));
+    uint32_t* offp = reinterpret_cast<uint32_t*>(wbase);
+    uint8_t* vbp = wbase + (kPad ? kWidePadVb : offsetof(WideLds, vb));
+    uint32_t* srcp = reinterpret_cast<uint32_t*>(wbase + offsetof(WideLds, src));  // (not kPad)
+    uint4* rows = reinterpret_cast<uint4*>(wbase + kWidePadRows);                   // (kPad)
+    auto srcof = [&](uint32_t r) -> uint32_t { return kPad ? rows[r].x : srcp[r]; };
     const DevDict d = a.dicts[a.dict_id];
     const uint32_t dict_n = static_cast<uint32_t>(max(a.dict_count[a.dict_id], 0));
     const uint64_t* es = a.entries + d.entry_base;
@@ -1299,12 +1309,25 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
         }
         for (int ib = 0; ib < cn; ib += kWideBatch) {
             static_assert(kWideBatch == 2, "batch registers");
+            // kPad: row 64k + l of the tile in lane l, register k (a gather
+            // instruction then reads 64 consecutive rows: rows of one RLE run
+            // share a slot, so its lanes share cache lines); else rows
+            // 8l .. 8l + 7 in lane l
             auto ld = [&](int i, uint4& lo, uint4& hi) {
                 lo = hi = make_uint4(kNull32, kNull32, kNull32, kNull32);
                 if (i < cn) {
                     const int64_t R = rl64(myR0, i);
                     const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
-                    if (l8 + 8 <= mm) {
+                    if constexpr (kPad) {
+                        uint32_t c[8];
+#pragma unroll
+                        for (int k = 0; k < 8; k++) {
+                            const uint32_t r = k * kWave + lane();
+                            c[k] = r < mm ? a.codes32[R + r] : kNull32;
+                        }
+                        lo = make_uint4(c[0], c[1], c[2], c[3]);
+                        hi = make_uint4(c[4], c[5], c[6], c[7]);
+                    } else if (l8 + 8 <= mm) {
                         const U16B* p = reinterpret_cast<const U16B*>(a.codes32 + R + l8);
                         const U16B x = p[0], y = p[1];
                         lo = make_uint4(x.x, x.y, x.z, x.w);
@@ -1328,22 +1351,27 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                 const bool first = i == ib;
                 const uint4 lo = first ? c0lo : c1lo, hi = first ? c0hi : c1hi;
                 const uint32_t cur[kRowsPerLane] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-                uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc8 = 0;
+                uint32_t len[kRowsPerLane], src[kRowsPerLane], total = 0;
                 if constexpr (kPad) {
-                    // this lane's rows 8l .. 8l + 7: entry slots (all eight loads in flight)
+                    // rows 64k + l: entry slots (all eight loads in flight)
                     uint4 sl[kRowsPerLane];
 #pragma unroll
                     for (int k = 0; k < kRowsPerLane; k++)
                         sl[k] = dict_n ? a.pad16[min(cur[k], dict_n - 1u)] : make_uint4(0u, 0u, 0u, 0u);
                     uint32_t far = 0;
+                    uint32_t* vbw = reinterpret_cast<uint32_t*>(vbp);
 #pragma unroll
                     for (int k = 0; k < kRowsPerLane; k++) {
                         const bool valid = cur[k] < dict_n;
                         len[k] = valid ? (sl[k].w >> 24) : 0u;
                         src[k] = 0;
                         far |= (len[k] == 0xFFu ? 1u : 0u) << k;
-                        vb |= (valid ? 1u : 0u) << k;
-                        rows[lane() * kRowsPerLane + k] = sl[k];
+                        rows[k * kWave + lane()] = sl[k];
+                        const uint64_t bm = __ballot(valid);  // validity words 2k, 2k + 1
+                        if (lane() == 0) {
+                            vbw[2 * k] = static_cast<uint32_t>(bm);
+                            vbw[2 * k + 1] = static_cast<uint32_t>(bm >> 32);
+                        }
                     }
                     if (__ballot(far != 0)) {  // rows of 16 or more bytes: the entry word
 #pragma unroll
@@ -1351,12 +1379,18 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                             if ((far >> k) & 1u) {
                                 const uint64_t e = es[cur[k]];
                                 len[k] = static_cast<uint32_t>(e >> 32);
-                                src[k] = static_cast<uint32_t>(e);
+                                rows[k * kWave + lane()].x = static_cast<uint32_t>(e);
                             }
                     }
+                    // tile-relative first bytes: one wave scan per 64 rows
 #pragma unroll
-                    for (int k = 0; k < kRowsPerLane; k++) acc8 += len[k];
+                    for (int k = 0; k < kRowsPerLane; k++) {
+                        const uint32_t inc = wave_incl_scan(len[k]);
+                        offp[k * kWave + lane()] = total + inc - len[k];
+                        total += bcast_last(inc);
+                    }
                 } else {
+                    uint32_t vb = 0, acc8 = 0;
                     // this lane's rows 8l .. 8l + 7: entry words (all eight loads in flight)
                     uint64_t e[kRowsPerLane];
 #pragma unroll
@@ -1369,23 +1403,21 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                         vb |= (valid ? 1u : 0u) << k;
                         acc8 += len[k];
                     }
-                }
-                const uint32_t incl = wave_incl_scan(acc8);
-                const uint32_t total = bcast_last(incl);
-                {
+                    const uint32_t incl = wave_incl_scan(acc8);
+                    total = bcast_last(incl);
                     uint32_t o[kRowsPerLane];
                     o[0] = incl - acc8;
 #pragma unroll
                     for (int k = 1; k < kRowsPerLane; k++) o[k] = o[k - 1] + len[k - 1];
-                    uint4* po = reinterpret_cast<uint4*>(&S.off[lane() * kRowsPerLane]);
+                    uint4* po = reinterpret_cast<uint4*>(&offp[lane() * kRowsPerLane]);
                     po[0] = make_uint4(o[0], o[1], o[2], o[3]);
                     po[1] = make_uint4(o[4], o[5], o[6], o[7]);
-                    uint4* ps = reinterpret_cast<uint4*>(&S.src[lane() * kRowsPerLane]);
+                    uint4* ps = reinterpret_cast<uint4*>(&srcp[lane() * kRowsPerLane]);
                     ps[0] = make_uint4(src[0], src[1], src[2], src[3]);
                     ps[1] = make_uint4(src[4], src[5], src[6], src[7]);
+                    vbp[lane()] = static_cast<uint8_t>(vb);
                 }
-                S.vb[lane()] = static_cast<uint8_t>(vb);
-                if (lane() == 0) S.off[m] = total;
+                if (lane() == 0) offp[m] = total;
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 if (!(a.debug & 4)) {  // offsets and validity words as k_pipe_write stores them
@@ -1394,20 +1426,20 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                         for (int k = 0; k < kRowsPerLane / 2; k++) {
                             const uint32_t j = k * 2 * kWave + 2 * lane();
                             if (j + 1 < m) {
-                                const uint2 o = *reinterpret_cast<const uint2*>(&S.off[j]);
+                                const uint2 o = *reinterpret_cast<const uint2*>(&offp[j]);
                                 const int64_t v0 = G0 + o.x, v1 = G0 + o.y;
                                 *reinterpret_cast<uint4*>(a.offsets + R0 + j) =
                                     make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(static_cast<uint64_t>(v0) >> 32),
                                                static_cast<uint32_t>(v1), static_cast<uint32_t>(static_cast<uint64_t>(v1) >> 32));
                             } else if (j < m) {
-                                a.offsets[R0 + j] = G0 + S.off[j];
+                                a.offsets[R0 + j] = G0 + offp[j];
                             }
                         }
                     } else {
 #pragma unroll
                         for (int k = 0; k < kRowsPerLane; k++) {
                             const uint32_t j = k * kWave + lane();
-                            if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
+                            if (j < m) a.offsets[R0 + j] = G0 + offp[j];
                         }
                     }
                     const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
@@ -1415,7 +1447,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                     const int64_t g = gfirst + lane();
                     if (g <= glast) {
                         auto tw = [&](int t) -> uint32_t {
-                            return (t >= 0 && t < kWave / 4) ? reinterpret_cast<const uint32_t*>(S.vb)[t] : 0u;
+                            return (t >= 0 && t < kWave / 4) ? reinterpret_cast<const uint32_t*>(vbp)[t] : 0u;
                         };
                         const int t = static_cast<int>(lane());
                         const uint32_t val = (tw(t) << sh) | (sh ? (tw(t - 1) >> (32 - sh)) : 0u);
@@ -1448,9 +1480,9 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                         ln[q] = 0;
                         uint32_t sa = 0;
                         if (r < m) {
-                            s0[q] = S.off[r];
-                            ln[q] = S.off[r + 1] - s0[q];
-                            sa = S.src[r];
+                            s0[q] = offp[r];
+                            ln[q] = offp[r + 1] - s0[q];
+                            sa = srcof(r);
                         }
                         const uint32_t l16 = ln[q] <= 16 ? ln[q] : 0u;
                         if (kPad && ln[q] <= 15) {  // from the row's slot: bytes 0..7 and ln-8 .. ln-1
@@ -1489,7 +1521,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                         const uint32_t r = h + q * kWave + lane();
                         const uint32_t L = ln[q];
                         if (L > 16 && L <= kLongRow) {
-                            const uint8_t* sp = dsrc + S.src[r];
+                            const uint8_t* sp = dsrc + srcof(r);
                             uint8_t* dd = a.chars + G0 + s0[q];
                             for (uint32_t x = 0; x + 16 < L; x += 16)
                                 *reinterpret_cast<U16B*>(dd + x) = *reinterpret_cast<const U16B*>(sp + x);
@@ -1501,7 +1533,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                             lm &= lm - 1;
                             const uint32_t rl = h + q * kWave + l;
                             const uint32_t LL = __builtin_amdgcn_readlane(L, l);
-                            const uint8_t* sp = dsrc + S.src[rl];
+                            const uint8_t* sp = dsrc + srcof(rl);
                             uint8_t* dd = a.chars + G0 + __builtin_amdgcn_readlane(s0[q], l);
                             for (uint32_t x = 16 * lane(); x < LL; x += 16 * kWave) {
                                 const uint32_t xx = min(x, LL - 16);  // the last block overlaps (same bytes)
@@ -2114,7 +2146,8 @@ __global__ void __launch_bounds__(kWideCharWaves * 64) k_wide_chars(CodeArgs a) 
 // dictionaries up to kWideLensLds entries): persistent workgroups of
 // kWideLWaves waves stage the table once, then each wave takes kWideLBatch
 // consecutive tiles per step, all their codes loaded before the first
-// lookup.  A length byte of 255 (255 or more) is read from the entry table.
+// lookup (row 64j + l of a tile in lane l: the lanes of an RLE run read one
+// LDS byte).  A length byte of 255 (255 or more) is read from the entry table.
 constexpr int kWideLWaves = 16;
 constexpr int kWideLBatch = 4;
 constexpr uint32_t kWideLensLds = 120 * 1024;
@@ -2125,7 +2158,6 @@ __global__ void __launch_bounds__(kWideLWaves * 64) k_wide_chars_lds(CodeArgs a,
                 threadIdx.x, blockDim.x);
     __syncthreads();
     const uint64_t* es = a.entries + a.dicts[a.dict_id].entry_base;
-    const uint32_t l8 = lane() * 8;
     const int wv = static_cast<int>(threadIdx.x / kWave);
     for (int b = (static_cast<int>(blockIdx.x) * kWideLWaves + wv) * kWideLBatch; b < a.ntiles;
          b += static_cast<int>(gridDim.x) * kWideLWaves * kWideLBatch) {
@@ -2138,23 +2170,15 @@ __global__ void __launch_bounds__(kWideLWaves * 64) k_wide_chars_lds(CodeArgs a,
             td_r = a.pages[T.page].first_row + T.row0;
         }
         uint32_t c[kWideLBatch][8];
-        uint32_t mm[kWideLBatch];
 #pragma unroll
         for (int k = 0; k < kWideLBatch; k++) {
             const uint32_t m = __shfl(td_m, k);
             const int64_t R0 = __shfl(td_r, k);
-            mm[k] = m;
+            // row 64j + l in lane l (lanes of one RLE run then read one LDS byte)
 #pragma unroll
-            for (int j = 0; j < 8; j++) c[k][j] = kNull32;
-            if (l8 + 8 <= m) {
-                const U16B* p = reinterpret_cast<const U16B*>(a.codes32 + R0 + l8);
-                const U16B x = p[0], y = p[1];
-                c[k][0] = x.x; c[k][1] = x.y; c[k][2] = x.z; c[k][3] = x.w;
-                c[k][4] = y.x; c[k][5] = y.y; c[k][6] = y.z; c[k][7] = y.w;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    if (l8 + j < m) c[k][j] = a.codes32[R0 + l8 + j];
+            for (int j = 0; j < 8; j++) {
+                const uint32_t r = j * kWave + lane();
+                c[k][j] = r < m ? a.codes32[R0 + r] : kNull32;
             }
         }
 #pragma unroll
@@ -2173,7 +2197,6 @@ __global__ void __launch_bounds__(kWideLWaves * 64) k_wide_chars_lds(CodeArgs a,
                 for (int j = 0; j < 8; j++)
                     if ((far >> j) & 1u) chars += static_cast<uint32_t>(es[c[k][j]] >> 32) - 255u;
             }
-            (void)mm[k];
             tile_done(a, b + k, wave_sum(chars));
         }
     }
@@ -3347,7 +3370,7 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
 
 PipePlan plan_pipe_wide(int wpw, bool pad) {
     PipePlan pl{};
-    pl.lds = static_cast<uint32_t>(wpw) * static_cast<uint32_t>(sizeof(WideLds) + (pad ? kWideRowBytes : 0u));
+    pl.lds = static_cast<uint32_t>(wpw) * (pad ? kWidePadWave : static_cast<uint32_t>(sizeof(WideLds)));
     pl.blocks_per_cu = min(4, static_cast<int>((160u * 1024) / pl.lds));
     const int occ = resident_blocks(pad ? reinterpret_cast<const void*>(k_pipe_wwide<true>)
                                         : reinterpret_cast<const void*>(k_pipe_wwide<false>),
@@ -3366,7 +3389,7 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
                     P.chars, 0u, 0u, P.debug, P.write_waves, P.znext, P.znext_words, nullptr, 0, nullptr};
         a.codes32 = P.codes32;
         // (the plan sized P.lds for the slots whenever the dictionary has them)
-        const uint32_t need_pad = static_cast<uint32_t>(P.write_waves) * (sizeof(WideLds) + kWideRowBytes);
+        const uint32_t need_pad = static_cast<uint32_t>(P.write_waves) * kWidePadWave;
         if (P.pad16 && P.lds >= need_pad && !(P.debug & (1 << 29))) {  // (bit 29: entry words, for A/B)
             a.pad16 = P.pad16;
             ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_wwide<true>), P.lds);
