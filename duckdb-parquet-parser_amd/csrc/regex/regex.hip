@@ -578,33 +578,31 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
     // (eight named registers: an array carried around the loop went to scratch)
     uint4 R0, R1, R2, R3, R4, R5, R6, R7;
     bool held = false;
+    // The memory waits of the loop (gfx9: loads and stores share vmcnt, and
+    // a wait for an older load also waits for every later one): the window is
+    // staged at the END of the previous iteration, where the single wait
+    // covers its prefetch (issued before the DFA pass), the descriptors
+    // loaded at the top and the index stores, all long complete; a window's
+    // page flags are stored at the top of the next iteration, so no wait
+    // ever covers a fresh store.  (Staged at the top, the wait for the
+    // prefetch fell right after its issue.)
+    copy_blocks(reinterpret_cast<uint4*>(cur), reinterpret_cast<const uint4*>(bytes + B.img_lo), B.img_bytes / 16,
+                lane(), kWave);
+    if (lane() < 2) reinterpret_cast<uint4*>(cur + B.img_bytes)[lane()] = make_uint4(0, 0, 0, 0);
+    bool pf_on = false;  // the previous window's page flag (one lane per page)
+    int32_t pf_at = 0;
+    uint8_t pf_v = 0;
     for (;;) {
         const pqk::DevBatch Bc = B;
         const DevPage pgc = pg;
         const int32_t wn = w + nwt;
+        if (pf_on) page_flags[pf_at] = pf_v;
         DevPage pgn{};
         pqk::DevBatch Bnn{};
         if (wn < nwins) {
             if (lane() < static_cast<uint32_t>(Bn.np)) pgn = pages[Bn.p0 + static_cast<int32_t>(lane())];
             if (wn + nwt < nwins) Bnn = wins[wn + nwt];
         }
-        if (held) {
-            const uint32_t nb = Bc.img_bytes / 16;
-            uint4* dst = reinterpret_cast<uint4*>(cur);
-            const uint32_t b = lane();
-            if (b < nb) dst[b] = R0;
-            if (b + 1 * kWave < nb) dst[b + 1 * kWave] = R1;
-            if (b + 2 * kWave < nb) dst[b + 2 * kWave] = R2;
-            if (b + 3 * kWave < nb) dst[b + 3 * kWave] = R3;
-            if (b + 4 * kWave < nb) dst[b + 4 * kWave] = R4;
-            if (b + 5 * kWave < nb) dst[b + 5 * kWave] = R5;
-            if (b + 6 * kWave < nb) dst[b + 6 * kWave] = R6;
-            if (b + 7 * kWave < nb) dst[b + 7 * kWave] = R7;
-        } else {
-            copy_blocks(reinterpret_cast<uint4*>(cur), reinterpret_cast<const uint4*>(bytes + Bc.img_lo), Bc.img_bytes / 16,
-                        lane(), kWave);
-        }
-        if (lane() < 2) reinterpret_cast<uint4*>(cur + Bc.img_bytes)[lane()] = make_uint4(0, 0, 0, 0);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t* stage = reinterpret_cast<const uint32_t*>(cur);
@@ -814,8 +812,8 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
                 }
             }
         }
-        // the next window's bytes: issued now, stored at the top of the next
-        // iteration (after this window's DFA pass, which reads only LDS)
+        // the next window's bytes: issued now, stored at the end of this
+        // iteration (after the DFA pass, which reads only LDS)
         held = kPre && wn < nwins && Bn.img_bytes <= kPrefetchBlocks * kWave * 16;
         if (held) {  // (clamped indices: unconditional loads, no branch around them)
             const uint4* src = reinterpret_cast<const uint4*>(bytes + Bn.img_lo);
@@ -910,17 +908,35 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
             }
         }
         __builtin_amdgcn_wave_barrier();
-        if (pl) {
-            const bool any = (hit[lane() >> 5] >> (lane() & 31)) & 1u;
-            page_flags[Bc.p0 + static_cast<int32_t>(lane())] = any ? 0 : 1;
-        }
+        pf_on = pl;
+        pf_at = Bc.p0 + static_cast<int32_t>(lane());
+        pf_v = ((hit[lane() >> 5] >> (lane() & 31)) & 1u) ? 0 : 1;
         __builtin_amdgcn_wave_barrier();
         if (wn >= nwins) break;
+        // the next window -> LDS (this one's DFA pass is done with `cur`)
+        if (held) {
+            const uint32_t nb = Bn.img_bytes / 16;
+            uint4* dst = reinterpret_cast<uint4*>(cur);
+            const uint32_t b = lane();
+            if (b < nb) dst[b] = R0;
+            if (b + 1 * kWave < nb) dst[b + 1 * kWave] = R1;
+            if (b + 2 * kWave < nb) dst[b + 2 * kWave] = R2;
+            if (b + 3 * kWave < nb) dst[b + 3 * kWave] = R3;
+            if (b + 4 * kWave < nb) dst[b + 4 * kWave] = R4;
+            if (b + 5 * kWave < nb) dst[b + 5 * kWave] = R5;
+            if (b + 6 * kWave < nb) dst[b + 6 * kWave] = R6;
+            if (b + 7 * kWave < nb) dst[b + 7 * kWave] = R7;
+        } else {
+            copy_blocks(reinterpret_cast<uint4*>(cur), reinterpret_cast<const uint4*>(bytes + Bn.img_lo), Bn.img_bytes / 16,
+                        lane(), kWave);
+        }
+        if (lane() < 2) reinterpret_cast<uint4*>(cur + Bn.img_bytes)[lane()] = make_uint4(0, 0, 0, 0);
         B = Bn;
         Bn = Bnn;
         pg = pgn;
         w = wn;
     }
+    if (pf_on) page_flags[pf_at] = pf_v;
 }
 
 }  // namespace
