@@ -589,6 +589,11 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
     copy_blocks(reinterpret_cast<uint4*>(cur), reinterpret_cast<const uint4*>(bytes + B.img_lo), B.img_bytes / 16,
                 lane(), kWave);
     if (lane() < 2) reinterpret_cast<uint4*>(cur + B.img_bytes)[lane()] = make_uint4(0, 0, 0, 0);
+    // a warm scan: the next window's string-index entries (<= 256 strings),
+    // loaded into registers one window ahead (entry k in lane k % 64, half
+    // k / 128 of word (k / 64) % 2)
+    bool ix_held = false;
+    uint32_t ix01 = 0, ix23 = 0;
     bool pf_on = false;  // the previous window's page flag (one lane per page)
     int32_t pf_at = 0;
     uint8_t pf_v = 0;
@@ -627,9 +632,36 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
             cnt = pl ? static_cast<uint32_t>(max(pgc.nvals, 0)) : 0u;
             lb = static_cast<uint32_t>(fr - fr0);
             const uint32_t tot = bcast_last(wave_incl_scan(cnt));
-            for (uint32_t k = lane(); k < tot; k += kWave) list[k] = index_in[fr0 + k];
+            if (ix_held && tot <= 4 * kWave) {
+                const uint32_t v[4] = {ix01 & 0xFFFFu, ix01 >> 16, ix23 & 0xFFFFu, ix23 >> 16};
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++)
+                    if (j * kWave + lane() < tot) list[j * kWave + lane()] = static_cast<uint16_t>(v[j]);
+            } else {
+                for (uint32_t k = lane(); k < tot; k += kWave) list[k] = index_in[fr0 + k];
+            }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the next window's entries, while this one is scanned (its page
+            // descriptors arrived with this window's entries)
+            ix_held = false;
+            if (wn < nwins) {
+                const bool pln = lane() < static_cast<uint32_t>(Bn.np);
+                const uint32_t totn = bcast_last(wave_incl_scan(pln ? static_cast<uint32_t>(max(pgn.nvals, 0)) : 0u));
+                const int64_t fr0n = static_cast<int64_t>(
+                    static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(pgn.first_row), 0))) |
+                    (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(pgn.first_row >> 32), 0))) << 32));
+                if (totn > 0 && totn <= 4 * kWave) {  // (clamped indices: unconditional loads)
+                    auto at = [&](uint32_t j) -> uint32_t {
+                        const uint32_t k = j * kWave + lane();
+                        return index_in[fr0n + (k < totn ? k : 0u)];
+                    };
+                    const uint32_t a0 = at(0), a1 = at(1), a2 = at(2), a3 = at(3);
+                    ix01 = a0 | (a1 << 16);
+                    ix23 = a2 | (a3 << 16);
+                    ix_held = totn > 0;
+                }
+            }
         } else {
             // ── strings: L lanes per page ───────────────────────────────────
             const uint32_t lg = np <= 1 ? 0u : 32u - __builtin_clz(np - 1);  // ceil log2
