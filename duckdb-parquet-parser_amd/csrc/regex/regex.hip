@@ -728,16 +728,31 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
                 if (sg == 0) {
                     c0 = pos0;
                 } else {
+                    // (a plausible start holds a length below 2^16, pages
+                    // fitting a window of < 64 KiB: its bytes 2 and 3 are
+                    // zero; only those positions are tested, in order)
                     for (uint32_t a = (A + lo) & ~15u; a < A + hi && c0 == ~0u; a += 16) {
                         const uint4 v = *reinterpret_cast<const uint4*>(cur + a);
                         const uint32_t d4 = stage[(a >> 2) + 4];
                         const uint32_t d[5] = {v.x, v.y, v.z, v.w, d4};
+                        uint32_t zb = 0;  // bit j: byte a + j is zero (j < 20)
     #pragma unroll
-                        for (uint32_t k = 0; k < 16; k++) {
+                        for (uint32_t j = 0; j < 5; j++) {
+                            const uint32_t z = ~(((d[j] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d[j] | 0x7F7F7F7Fu);
+                            zb |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * j);
+                        }
+                        uint32_t cm = (zb >> 2) & (zb >> 3) & 0xFFFFu;
+                        while (cm) {
+                            const uint32_t k = static_cast<uint32_t>(__builtin_ctz(cm));
+                            cm &= cm - 1;
                             const uint32_t cpos = a + k - A;
-                            const uint32_t len = (k & 3) == 0 ? d[k >> 2] : __builtin_amdgcn_alignbyte(d[(k >> 2) + 1], d[k >> 2], k & 3);
-                            const bool ok = cpos >= lo && cpos < hi && cpos + 4 <= size && len <= size - cpos - 4;
-                            c0 = (ok && c0 == ~0u) ? cpos : c0;
+                            if (cpos < lo) continue;
+                            if (cpos >= hi) break;
+                            const uint32_t len = st_u32(stage, a + k);
+                            if (cpos + 4 <= size && len <= size - cpos - 4) {
+                                c0 = cpos;
+                                break;
+                            }
                         }
                     }
                 }
