@@ -1520,7 +1520,9 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                 if (static_cast<uint64_t>(sz) + 32 <= pqk::kDictLdsCap) continue;
                 pq_chunk::BigDict b{static_cast<int>(i), hdicts[i], off, 0, 0};
                 off += (pqk::dict_big_scratch(sz) + 255) / 256 * 256;
-                const size_t nv = static_cast<size_t>(std::max(hdicts[i].nvals, 0));
+                // (a dictionary holds at most size / 4 + 1 entries: a corrupt
+                // header count must not size these buffers)
+                const size_t nv = static_cast<size_t>(std::min<int64_t>(std::max(hdicts[i].nvals, 0), sz / 4 + 1));
                 b.lens_off = off;  // entry lengths as bytes (+ 16: k_wide_chars stages whole blocks)
                 off += (nv + 16 + 255) / 256 * 256;
                 b.pad_off = off;   // 16-byte entry slots (k_pipe_wwide)
@@ -1771,9 +1773,12 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                 Timed ct(ctx, "codec", s);
                 const bool gz = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec == 2; });
                 const bool other = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec != 2 && e.codec != 0; });
-                if (gz && other) rc = set_err(ctx, PQ_ERR_CODEC, "GZIP pages mixed with other codecs in one upload");
-                else pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus, gz);
-                rc = hip_check(ctx, hipGetLastError(), "codec launch");
+                if (gz && other) {
+                    rc = set_err(ctx, PQ_ERR_CODEC, "GZIP pages mixed with other codecs in one upload");
+                } else {
+                    pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus, gz);
+                    rc = hip_check(ctx, hipGetLastError(), "codec launch");
+                }
             }
         }
         if (ctx->timing) {
@@ -2019,7 +2024,7 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         for (const auto& b : c->hbigd)
             if (b.di == c->pipe_dict) {
                 P.lens8 = c->d_bigd + b.lens_off;
-                P.lens8_cap = static_cast<uint32_t>(std::max(b.d.nvals, 0));
+                P.lens8_cap = static_cast<uint32_t>(std::min<int64_t>(std::max(b.d.nvals, 0), b.d.size / 4 + 1));
                 P.pad16 = reinterpret_cast<const uint4*>(c->d_bigd + b.pad_off);
             }
     }
@@ -2477,13 +2482,18 @@ int pq_decode_check(pq_ctx* ctx, pq_chunk* c) {
     DevGuard dg(ctx);
     // the column of the chunk's last async decode gets its byte count (and
     // grows and decodes again if its characters overflowed the estimate)
-    return collect(ctx, c, c->last_out);
+    // (the column is the caller's: once collected, no later call touches it)
+    const int rc = collect(ctx, c, c->last_out);
+    c->last_out = nullptr;
+    return rc;
 }
 
 int pq_decode(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     DevGuard dg(ctx);
     if (int rc = pq_decode_async(ctx, c, out)) return rc;
-    return collect(ctx, c, out);
+    const int rc = collect(ctx, c, out);
+    c->last_out = nullptr;
+    return rc;
 }
 
 int pq_column_copy_out(pq_ctx* ctx, const pq_column* col, uint32_t* validity, uint8_t* values,
