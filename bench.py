@@ -423,10 +423,11 @@ def c2_leg(J, args, exp):
     nonnull = int(host.validity.sum())
     chars = int(dc.out.num_bytes)
     valid = None
+    want = None
     if not args.no_validate:
         # this rank's row group against the generator's dump of it
-        ok = sha(capi.canonical_dump(host)) == sha(
-            gen.values_dump(gen.c2_cols()[0], 0, args.rows, J.rank, gen.CONFIG_SEEDS["C2"]))
+        want = sha(gen.values_dump(gen.c2_cols()[0], 0, args.rows, J.rank, gen.CONFIG_SEEDS["C2"]))
+        ok = sha(capi.canonical_dump(host)) == want
         valid = all(J.gather(bool(ok)))
     del host
     secs, kern = J.timed(dc.decode_async, dc.decode_check, args.steps, args.repeats, warmup=args.warmup)
@@ -466,8 +467,39 @@ def c2_leg(J, args, exp):
         dc.free()
     res["walk_s"] = walk_s
     res["upload_s"] = upload_s
+    if not args.no_e2e and J.rank == 0:
+        res["api_read_all"] = api_read_all_leg(f, want)
     del f
     return res
+
+
+def api_read_all_leg(f: bytes, want):
+    """What a drop-in caller of the reference API gets (the
+    std::vector<Value> path): pqgpu::ColumnReader::read_all on the C2 chunk,
+    host file bytes in, std::vector<Value> out (range read, upload, decode,
+    copy-out, the Value build on up to 16 host threads), timed in the C++ tool
+    (tools/api_check.cpp time_read_all, median of 3 after a warm-up), its
+    values checked against the generator's dump."""
+    import tempfile
+    tool = os.path.join(ROOT, "duckdb-parquet-parser_amd", "pqgpu", "api_check")
+    with tempfile.TemporaryDirectory() as td:
+        path, dump = os.path.join(td, "c2.parquet"), os.path.join(td, "c2.dump")
+        with open(path, "wb") as fh:
+            fh.write(f)
+        r = subprocess.run([tool, path, "time_read_all", "0", "0", "3", dump], stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, timeout=600)
+        if r.returncode != 0:
+            return {"error": r.stderr.decode(errors="replace")[-500:]}
+        js = json.loads(r.stdout.decode().strip().splitlines()[-1])
+        with open(dump, "rb") as fh:
+            got = hashlib.sha256(fh.read()).hexdigest()
+    n = js["values"]
+    return {"values_per_s": n / (js["read_all_ms"] * 1e-3), "read_all_ms": js["read_all_ms"],
+            "read_columnar_ms": js["read_columnar_ms"], "to_values_ms": js["to_values_ms"],
+            "to_values_per_s": n / (js["to_values_ms"] * 1e-3), "threads": js["threads"], "values": n,
+            "validated": (got == want) if want else None,
+            "note": "ColumnReader::read_all from host file bytes to std::vector<Value>; compare cpu_baseline."
+                    "chunk_parallel (the reference's read_all, one thread per chunk) and single_thread"}
 
 
 def strong_leg(J, args):
@@ -1012,6 +1044,8 @@ def main():
     }
     if "e2e" in c2:
         result["end_to_end"] = {"c2": c2["e2e"]}
+    if "api_read_all" in c2:
+        result["api_read_all"] = c2["api_read_all"]
     if world > 1:
         result["strong"] = strong_leg(J, args)
 

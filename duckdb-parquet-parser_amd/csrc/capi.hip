@@ -123,7 +123,12 @@ struct pq_ctx {
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
     bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
-    bool opt_front = false;      // "pipe_front": windowed one-wave front (k_pipe_front) where the pages allow it
+    bool opt_front = false;      // "pipe_front": windowed one-wave front (k_pipe_win) where the pages allow it
+    int opt_win_pages = 8;       // "win_pages": pages per k_pipe_win window (1..16), set before upload
+    int opt_win_bytes = 4096;    // "win_bytes": slot bytes per k_pipe_win window (1024..16384), set before upload
+    int opt_win_rc = 96;         // "win_rc": run records per stream in k_pipe_win (2..255)
+    bool opt_win_dict = false;
+    bool opt_write_self = false; // "write_self": k_pipe_write sums its tiles itself after every front (A/B; always after k_pipe_win)   // "win_dict": the dictionary decodes in k_pipe_win's leading workgroups (else side stream)
     bool opt_pfused = false;     // "pipe_fused": codes + write in one pass (k_pipe_fused), planned at upload
     int opt_fused_waves = 8;     // "pipe_fused_waves": k_pipe_fused waves per workgroup (1..16), set before upload
     int opt_write_bpc = 0;       // "write_bpc": cap on k_pipe_write workgroups per CU (0: as many as fit; set before upload)
@@ -198,8 +203,9 @@ struct pq_chunk {
     bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
     uint32_t pipe_small_bytes = 0;      // the largest payload of those pages
     bool pipe_wide = false;             // 32-bit codes, dictionary in HBM (k_pipe_big<true> -> k_pipe_wwide)
-    bool pipe_fr = false;               // every page <= kTileRows rows, every slot <= kFrontWin: k_pipe_front
+    bool pipe_fr = false;               // every page <= kTileRows rows, flat levels, every slot <= a window: k_pipe_win
     std::vector<pqk::DevBatch> hfwins;  // its windows of consecutive pages
+    uint32_t win_bytes = 0, win_pages = 0;  // the largest window's slot bytes, pages per window (planned)
     pqk::DevBatch* d_fwins = nullptr;
     int pipe_wpw = 10;                  // k_pipe_write writer waves per workgroup (planned)
     std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
@@ -603,9 +609,16 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
             c->fwaves = fw;
         }
     }
-    // windows of consecutive pages for the whole front in one wavefront each (k_pipe_front)
+    // windows of consecutive pages for the whole front in one wavefront each
+    // (k_pipe_win): one-tile pages, flat levels (max_def <= 1, no rep levels)
     c->hfwins.clear();
-    c->pipe_fr = small && !multi && c->hbig.empty() && pqk::pipe_front_slot(small_bytes) <= pqk::kFrontWin;
+    c->win_bytes = 0;
+    c->win_pages = static_cast<uint32_t>(std::max(1, std::min(16, ctx->opt_win_pages)));
+    const uint32_t wcap = static_cast<uint32_t>(ctx->opt_win_bytes);
+    // (the self-summing writer after it holds <= 64 tiles per wave)
+    c->pipe_fr = small && !multi && c->hbig.empty() && c->max_def <= 1 && c->max_rep == 0 &&
+                 pqk::pipe_win_slot(small_bytes) <= wcap &&
+                 pages.size() <= static_cast<size_t>(64) * static_cast<size_t>(c->pipe_grid) * static_cast<size_t>(wpw);
     if (c->pipe_fr) {
         size_t p = 0;
         while (p < pages.size()) {
@@ -614,19 +627,20 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
             b.img_lo = pages[p].off;
             uint64_t hi = b.img_lo;
             size_t q = p;
-            while (q < pages.size() && q - p < pqk::pipe_front_win_pages() && pages[q].off >= b.img_lo) {
-                const uint64_t e = pages[q].off + pqk::pipe_front_slot(static_cast<uint32_t>(std::max(pages[q].size, 0)));
-                if (e - b.img_lo > pqk::kFrontWin || (q > p && pages[q].off != hi)) break;  // contiguous slots only
+            while (q < pages.size() && q - p < c->win_pages && pages[q].off >= b.img_lo) {
+                const uint64_t e = pages[q].off + pqk::pipe_win_slot(static_cast<uint32_t>(std::max(pages[q].size, 0)));
+                if (e - b.img_lo > wcap || (q > p && pages[q].off != hi)) break;  // contiguous slots only
                 hi = e;
                 q++;
             }
-            if (q == p) {  // (slots are contiguous and <= kFrontWin: unreachable)
+            if (q == p) {  // (slots are contiguous and <= wcap: unreachable)
                 c->pipe_fr = false;
                 c->hfwins.clear();
                 break;
             }
             b.np = static_cast<int32_t>(q - p);
             b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
+            c->win_bytes = std::max(c->win_bytes, b.img_bytes);
             c->hfwins.push_back(b);
             p = q;
         }
@@ -971,6 +985,23 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "plain_fused") == 0) { ctx->opt_plain_fused = value != 0; return 0; }
     if (std::strcmp(key, "pipe_run_dict") == 0) { ctx->opt_run_dict = value != 0; return 0; }
     if (std::strcmp(key, "pipe_front") == 0) { ctx->opt_front = value != 0; return 0; }
+    if (std::strcmp(key, "win_dict") == 0) { ctx->opt_win_dict = value != 0; return 0; }
+    if (std::strcmp(key, "write_self") == 0) { ctx->opt_write_self = value != 0; return 0; }
+    if (std::strcmp(key, "win_pages") == 0) {
+        if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "win_pages: 1..16");
+        ctx->opt_win_pages = static_cast<int>(value);
+        return 0;
+    }
+    if (std::strcmp(key, "win_bytes") == 0) {
+        if (value < 1024 || value > 16384 || value % 16) return set_err(ctx, PQ_ERR_ARG, "win_bytes: 1024..16384, a multiple of 16");
+        ctx->opt_win_bytes = static_cast<int>(value);
+        return 0;
+    }
+    if (std::strcmp(key, "win_rc") == 0) {
+        if (value < 2 || value > 255) return set_err(ctx, PQ_ERR_ARG, "win_rc: 2..255");
+        ctx->opt_win_rc = static_cast<int>(value);
+        return 0;
+    }
     if (std::strcmp(key, "pipe_fused") == 0) { ctx->opt_pfused = value != 0; return 0; }
     if (std::strcmp(key, "pipe_fused_waves") == 0) {
         if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "pipe_fused_waves: 1..16");
@@ -1486,7 +1517,8 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         rc |= dalloc(&c->d_page_err, hpages.size());
         rc |= dalloc(&c->d_dict_err, hdicts.size());
         if (c->pipe) {  // flags | bsum | fused ticket + look-back words | flist, cleared together
-            const size_t fb = 4 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long);
+            // (bsum: pipe_grid workgroup sums, then the self-summing writer's ticket)
+            const size_t fb = 4 * sizeof(int32_t), bb = (static_cast<size_t>(c->pipe_grid) + 1) * sizeof(unsigned long long);
             c->nunits = c->fused_ok ? (c->ntiles + pqk::pipe_fused_tiles() - 1) / pqk::pipe_fused_tiles() : 0;
             c->z_bsum = fb;
             c->z_fused = (fb + bb + 15) / 16 * 16;
@@ -2069,9 +2101,19 @@ static bool front_path(pq_ctx* ctx, const pq_chunk* c) { return c->pipe_fr && c-
 static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs,
                        bool fused = false) {
     hipStream_t s = ctx->stream;
-    if (front_path(ctx, c)) {  // the dictionary decoded before (main stream)
-        Timed t(ctx, "pipe_front");
-        pqk::launch_pipe_front(s, P, c->d_fwins, static_cast<int>(c->hfwins.size()), pqk::kFrontWin);
+    if (front_path(ctx, c)) {
+        // k_pipe_win reads no dictionary: it decodes in the leading workgroups
+        // (dict_in_runs), on the side stream (joined here, before the writer),
+        // or was decoded before (regex page filter)
+        {
+            Timed t(ctx, "pipe_front");
+            const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
+            pqk::launch_pipe_win(s, P, c->d_fwins, static_cast<int>(c->hfwins.size()), c->win_bytes, c->win_pages,
+                                 static_cast<uint32_t>(ctx->opt_win_rc), dict_in_runs ? &rd : nullptr, c->max_dict_bytes);
+        }
+        if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
+        Timed t(ctx, "pipe_exact");
+        pqk::launch_pipe_exact(s, P);
         return;
     }
     {
@@ -2149,11 +2191,12 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
     // dictionary pages small enough for k_pipe_runs' workgroups decode there
     const bool front = pipe && !plain_go && front_path(ctx, c);
-    const bool dict_in_runs = pipe && !plain_go && !front && ctx->opt_run_dict && c->ndicts && c->type == PQ_BYTE_ARRAY &&
-                              c->d_dflag && c->max_dict_bytes <= pqk::kRunDictMax;
+    // (k_pipe_win: only with "win_dict", else the dictionary decodes on the side stream beside it)
+    const bool dict_in_runs = pipe && !plain_go && ctx->opt_run_dict && (!front || ctx->opt_win_dict) && c->ndicts &&
+                              c->type == PQ_BYTE_ARRAY && c->d_dflag && c->max_dict_bytes <= pqk::kRunDictMax;
     if (dict_in_runs) {
-        // k_pipe_runs (pipe_front) decodes the dictionary
-    } else if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe && !front) {
+        // k_pipe_runs / k_pipe_win decodes the dictionary
+    } else if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
         // the dictionary (one workgroup) decodes on the side stream while the
         // run-table pass runs; k_pipe_codes waits for both (ev_join).  The
         // side stream first waits for everything already on the main stream
@@ -2257,7 +2300,9 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_plain_ba(s, P);
     } else if (pipe) {
         pqk::PipeLaunch P = pipe_launch(ctx, c, out);
-        pipe_front(ctx, c, P, !dict_in_runs && !front, dict_in_runs, fused);
+        P.self_sum = front || (ctx->opt_write_self && !c->pipe_wide && c->hbig.empty() &&
+                               c->ntiles <= 64 * c->pipe_grid * c->pipe_wpw);  // k_pipe_win files no tile characters
+        pipe_front(ctx, c, P, !dict_in_runs, dict_in_runs, fused);
         if (c->arm) {  // the page filter in the same pass: match bits per entry, then the writer tests them
             Timed t(ctx, "regex_dict");
             pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,

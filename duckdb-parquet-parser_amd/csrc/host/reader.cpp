@@ -193,6 +193,30 @@ Value HostColumn::value(int64_t i) const {
     }
 }
 
+std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned threads) {
+    a = std::max<int64_t>(a, 0);
+    b = std::min<int64_t>(b, h.num_rows);
+    const int64_t n = std::max<int64_t>(b - a, 0);
+    std::vector<Value> out(static_cast<size_t>(n));
+    unsigned t = threads ? threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    // (below ~64k rows a thread costs more than it saves)
+    t = static_cast<unsigned>(std::min<int64_t>(t, std::max<int64_t>(1, n / 65536)));
+    auto part = [&](unsigned k) {
+        const int64_t r0 = n * k / t, r1 = n * (k + 1) / t;
+        for (int64_t r = r0; r < r1; r++) out[static_cast<size_t>(r)] = h.value(a + r);
+    };
+    if (t <= 1) {
+        part(0);
+        return out;
+    }
+    std::vector<std::thread> th;
+    th.reserve(t - 1);
+    for (unsigned k = 1; k < t; k++) th.emplace_back(part, k);
+    part(0);
+    for (auto& x : th) x.join();
+    return out;
+}
+
 // ── Device ─────────────────────────────────────────────────────────────────
 Device::Device(int device) : ctx_(pq_ctx_create(device)) {
     if (!ctx_) throw std::runtime_error("pqgpu: no HIP device " + std::to_string(device));
@@ -253,13 +277,7 @@ HostColumn ColumnReader::read_columnar() {
     return decode_chunks(dev_, image.data(), image.size(), {d}, nullptr);
 }
 
-std::vector<Value> ColumnReader::read_all() {
-    HostColumn h = read_columnar();
-    std::vector<Value> out;
-    out.reserve(static_cast<size_t>(h.num_rows));
-    for (int64_t i = 0; i < h.num_rows; i++) out.push_back(h.value(i));
-    return out;
-}
+std::vector<Value> ColumnReader::read_all() { return to_values(read_columnar()); }
 
 std::vector<PageResult> ColumnReader::read_pages() {
     int64_t start = meta_->data_page_offset;
@@ -280,7 +298,7 @@ std::vector<PageResult> ColumnReader::read_pages() {
             pages.push_back({page_num++, PageType::DICTIONARY_PAGE, ph.dict_num_values, {}});
         } else if (ph.type == 0) {
             PageResult pr{page_num++, PageType::DATA_PAGE, ph.data_num_values, {}};
-            for (int32_t k = 0; k < ph.data_num_values; k++) pr.values.push_back(h.value(row + k));
+            pr.values = to_values(h, row, row + std::max(ph.data_num_values, 0));
             row += ph.data_num_values;
             values_read += ph.data_num_values;
             pages.push_back(std::move(pr));
@@ -420,11 +438,7 @@ HostColumn ParquetReader::decode_column(int col_idx, int rg_first, int rg_count)
 std::vector<Value> ParquetReader::read_column_by_idx(int rg, int col) {  // parquet_reader.cpp:146-165
     if (rg < 0 || rg >= static_cast<int>(num_row_groups())) throw std::runtime_error("Invalid row group index");
     if (col < 0 || col >= static_cast<int>(columns_.size())) throw std::runtime_error("Invalid column index");
-    HostColumn h = decode_column(col, rg, 1);
-    std::vector<Value> v;
-    v.reserve(static_cast<size_t>(h.num_rows));
-    for (int64_t i = 0; i < h.num_rows; i++) v.push_back(h.value(i));
-    return v;
+    return to_values(decode_column(col, rg, 1));
 }
 std::vector<Value> ParquetReader::read_column(const std::string& name, size_t rg) {
     int c = find_column(name);
@@ -499,11 +513,7 @@ HostColumn ParquetReader::read_column_columnar(const std::string& name, const st
 }
 
 std::vector<Value> ParquetReader::read_column(const std::string& name, const std::vector<Device*>& devices) {
-    HostColumn h = read_column_columnar(name, devices);
-    std::vector<Value> v;
-    v.reserve(static_cast<size_t>(h.num_rows));
-    for (int64_t i = 0; i < h.num_rows; i++) v.push_back(h.value(i));
-    return v;
+    return to_values(read_column_columnar(name, devices));
 }
 
 HostColumn ParquetReader::decode_column_on(Device& dev, int col_idx) {
@@ -519,11 +529,7 @@ HostColumn ParquetReader::decode_column_on(Device& dev, int col_idx) {
 }
 
 std::vector<Value> ParquetReader::read_column(const std::string& name) {  // parquet_reader.cpp:125-144
-    HostColumn h = read_column_columnar(name);
-    std::vector<Value> v;
-    v.reserve(static_cast<size_t>(h.num_rows));
-    for (int64_t i = 0; i < h.num_rows; i++) v.push_back(h.value(i));
-    return v;
+    return to_values(read_column_columnar(name));
 }
 
 StringColumnIterator ParquetReader::column_iterator(const std::string& name) {  // parquet_reader.cpp:282-295

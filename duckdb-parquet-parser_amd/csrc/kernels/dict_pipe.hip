@@ -256,7 +256,7 @@ struct CodeArgs {
 __device__ __forceinline__ void tile_done(const CodeArgs& a, int t, uint32_t chars) {
     if (lane() == 0) {
         a.tile_chars[t] = chars;
-        if (chars) atomicAdd(&a.bsum[(t / a.per) / a.wpw], static_cast<unsigned long long>(chars));
+        if (chars && a.bsum) atomicAdd(&a.bsum[(t / a.per) / a.wpw], static_cast<unsigned long long>(chars));
     }
 }
 
@@ -911,8 +911,8 @@ struct WriteArgs {
     const uint64_t* entries;
     const int32_t* dict_count;
     const uint16_t* codes;
-    const int64_t* tile_chars;
-    const unsigned long long* bsum;
+    int64_t* tile_chars;        // (written by the self-summing writer)
+    unsigned long long* bsum;
     int per;
     int64_t nrows_total;
     int64_t* total;
@@ -934,6 +934,11 @@ struct WriteArgs {
     uint8_t* page_flags;
     const uint32_t* codes32 = nullptr;  // wide chunks (k_pipe_wwide)
     const uint4* pad16 = nullptr;       // wide chunks: 16-byte entry slots (k_pipe_wwide<true>), or null
+    // self-summing (after k_pipe_win, which files no characters): every
+    // workgroup sums its own tiles' characters from their codes, publishes its
+    // total in bsum[its ticket] and adds up the totals before it; bsum[gridDim.x]
+    // holds the ticket counter (all zeroed with the decode's flags)
+    int self_sum = 0;
 };
 
 
@@ -955,12 +960,12 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     // descriptors of up to 64 tiles are loaded at once, one per lane, and the
     // next tile's codes are loaded before this tile's stores are issued
     const int per = a.per;
-    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
-    const int tb = min(a.ntiles, ta + per);
-    // first output byte of the range: the workgroups before this one (bsum,
-    // summed by k_pipe_codes), then this workgroup's earlier tiles.  Both
-    // sums load together with the dictionary (one wait, one barrier).
-    __shared__ unsigned long long red[kWriteMax];
+    __shared__ unsigned long long red[kWriteMax], red2[kWriteMax];
+    __shared__ uint32_t ticket;
+    const bool self = a.self_sum != 0;
+    // (self-summing: the workgroup's place in the character prefix is its
+    // ticket, so every workgroup it waits on below had started before it)
+    if (self && threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<unsigned int*>(a.bsum + gridDim.x), 1u);
     auto wave_sum64 = [](unsigned long long v) {
         for (int d = 1; d < kWave; d <<= 1) {
             const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
@@ -969,11 +974,15 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
         }
         return v;
     };
+    // first output byte of the range: the workgroups before this one (bsum,
+    // summed by k_pipe_codes), then this workgroup's earlier tiles.  Both
+    // sums load together with the dictionary (one wait, one barrier).
     unsigned long long acc = 0, in = 0;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) acc += a.bsum[b];
-    {
+    if (!self) {
+        const int ta0 = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
+        for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) acc += a.bsum[b];
         const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
-        for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
+        for (int q = tfirst + static_cast<int>(lane()); q < ta0; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
     }
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
@@ -994,12 +1003,94 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
             });
         }
     }
-    acc = wave_sum64(acc);
-    if (lane() == 0) red[wv] = acc;
-    in = wave_sum64(in);
+    if (!self) {
+        acc = wave_sum64(acc);
+        if (lane() == 0) red[wv] = acc;
+        in = wave_sum64(in);
+    }
     __syncthreads();
-    int64_t Grun = static_cast<int64_t>(in);
-    for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
+    const uint32_t bid = self ? ticket : blockIdx.x;
+    const int ta = min(a.ntiles, static_cast<int>(bid * a.wpw + wv) * per);
+    const int tb = min(a.ntiles, ta + per);
+    int64_t Grun = 0;
+    uint32_t self_chars = 0;
+    if (!self) {
+        Grun = static_cast<int64_t>(in);
+        for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
+    } else {
+        // 1. this wave's tiles (at most 64: the host plans the self-summing
+        //    writer only then): characters of their valid codes (indices past
+        //    the dictionary are NULL rows), kept in lane j for tile ta + j
+        const uint32_t l8 = lane() * kRowsPerLane;
+        const uint32_t lmask = armed ? 0x7FFFu : 0xFFFFu;
+        unsigned long long wsum = 0;
+        for (int c0 = ta; c0 < tb; c0 += kWave) {
+            const int cn = min(kWave, tb - c0);
+            int64_t myR0 = 0;
+            uint32_t mym = 0;
+            if (static_cast<int>(lane()) < cn) {
+                const DevTile T = a.tiles[c0 + lane()];
+                myR0 = a.pages[T.page].first_row + T.row0;
+                mym = static_cast<uint32_t>(T.nrows);
+            }
+            for (int i0 = 0; i0 < cn; i0 += kWBatch) {
+                uint4 cv[kWBatch];
+#pragma unroll
+                for (int u = 0; u < kWBatch; u++) {
+                    cv[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+                    const int i = i0 + u;
+                    if (i < cn) {
+                        const int64_t R = static_cast<int64_t>(
+                            (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(myR0) >> 32), i)) << 32) |
+                            __builtin_amdgcn_readlane(static_cast<uint32_t>(myR0), i));
+                        const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
+                        if (l8 < mm) {
+                            const U16B x = *reinterpret_cast<const U16B*>(a.codes + R + l8);
+                            cv[u] = make_uint4(x.x, x.y, x.z, x.w);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kWBatch; u++) {
+                    const int i = i0 + u;
+                    if (i >= cn) break;
+                    const uint32_t ww[4] = {cv[u].x, cv[u].y, cv[u].z, cv[u].w};
+                    const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
+                    uint32_t sum = 0;
+#pragma unroll
+                    for (int k = 0; k < kRowsPerLane; k++) {
+                        const uint32_t c = (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                        const bool valid = l8 + k < mm && c < dict_n;
+                        sum += valid ? (dtab[valid ? c : 0u] >> 16) & lmask : 0u;
+                    }
+                    sum = wave_sum(sum);
+                    if (static_cast<int>(lane()) == c0 - ta + i) self_chars = sum;
+                    wsum += sum;
+                }
+            }
+        }
+        if (lane() == 0) red[wv] = wsum;
+        __syncthreads();
+        // 2. this workgroup's total, published with the ready bit; the
+        //    totals of every workgroup before it (by ticket)
+        constexpr unsigned long long kReady = 1ull << 63;
+        unsigned long long own = 0;
+        for (int w = 0; w < a.wpw; w++) own += red[w];
+        // (flag and value in one word, relaxed agent-scope atomics: no fence,
+        // which on gfx950 would write back the whole L2)
+        if (threadIdx.x == 0) __hip_atomic_store(&a.bsum[bid], own | kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t b = threadIdx.x; b < bid && !(a.debug & (1 << 24)); b += blockDim.x) {  // (bit 24: timing, no wait)
+            unsigned long long v;
+            while (!((v = __hip_atomic_load(&a.bsum[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & kReady))
+                __builtin_amdgcn_s_sleep(1);
+            acc += v & ~kReady;
+        }
+        acc = wave_sum64(acc);
+        if (lane() == 0) red2[wv] = acc;
+        __syncthreads();
+        Grun = 0;
+        for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red2[w]) + (w < static_cast<int>(wv) ? static_cast<int64_t>(red[w]) : 0);
+    }
     if (a.debug & 8) return;
     for (int c0 = ta; c0 < tb; c0 += kWave) {
         const int cn = min(kWave, tb - c0);
@@ -1011,7 +1102,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
             myp = static_cast<uint32_t>(T.page);
             myR0 = a.pages[T.page].first_row + T.row0;
             mym = static_cast<uint32_t>(T.nrows);
-            myc = static_cast<uint32_t>(a.tile_chars[c0 + lane()]);
+            myc = self ? self_chars : static_cast<uint32_t>(a.tile_chars[c0 + lane()]);
         }
         {  // tile characters < 2^25 each: a 32-bit scan over <= 64 tiles
             const uint32_t inc = wave_incl_scan(myc);
@@ -2350,394 +2441,334 @@ __global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match_w(const DevTile
     }
 }
 
-// ── the whole front of windows of pages of <= 512 rows ─────────────────────
-// k_pipe_front replaces k_pipe_runs + k_pipe_codes3 for chunks whose data
-// pages hold one tile each (the reference writer's layout).  Each wavefront
-// takes a window of consecutive pages (host-planned, <= kFrPages pages whose
-// payload slots span <= `win` bytes of the image) and keeps everything in its
-// own LDS area; no run table goes to HBM:
-//   A1. the window's slots -> LDS; one lane per page reads its prologue
-//       (column_reader.cpp:146-182: def_len, rep_len, index bit width);
-//   A2. every byte of every hybrid stream of the window is parsed as if a
-//       run header started there (rle_decoder.hpp:36-50, 76-95), all lanes,
-//       two bytes per lane and step, branch-free: the position of the next
-//       header, or the stop entry;
-//   A3. one lane per (page, stream) follows that table from the stream start,
-//       all chains of the window in one lock-step loop (one LDS read per
-//       header), listing the real headers in place over the table;
-//   B.  per page: one lane per listed header parses it exactly into a run
-//       record, a wave scan of the run lengths gives every record its first
-//       value (records past the value count drop; an exhausted stream gets its
-//       zero run, rle_decoder.hpp:20-23); then def levels, ranks and
-//       dictionary indices of the 512 rows, 8 per lane (as k_pipe_codes3),
-//       u16 codes and the tile's characters.
-// Pages outside that shape (bad headers before the value count, more than
-// kFrRuns runs, levels above max_def, bit widths > 16) are listed for
-// k_pipe_exact, the reference state machine.
-constexpr int kFrWaves = 4;
-constexpr uint32_t kFrRuns = 128;   // run records per stream
-constexpr uint32_t kFrPages = 32;   // pages per window (two chains each: 64 lanes)
+// ── the whole front of windows of one-tile pages (k_pipe_win) ──────────────
+// Chunks whose data pages each hold <= kTileRows rows (the reference writer's
+// 1 KiB pages), max_def <= 1 and no repetition levels (flat OPTIONAL or
+// REQUIRED columns).  One wavefront per window of <= wp consecutive pages
+// whose payload slots form one contiguous image range (host-planned); nothing
+// but the codes leaves the wave's LDS:
+//   1. the window's slots -> LDS (each slot is followed by >= 16 zero bytes);
+//   2. lane 2k walks page k's def-level stream, lane 2k + 1 its dictionary-
+//      index stream (column_reader.cpp:146-182; rle_decoder.hpp:36-95), all
+//      streams of the window in lock step, one run header per step and one
+//      32-bit record per run in LDS: first value | literal << 10 | (RLE value,
+//      or the window bit offset of the literal run's values) << 11.  A stream
+//      that ends before its value count gets the zero run (rle_decoder.hpp:
+//      20-23);
+//   3. per page, all 64 lanes: each def run (one lane per run) ORs its rows'
+//      validity bits into a 512-bit LDS map (RLE runs of 1 as masks, literal
+//      runs as the stream's own bits: the level bit width is 1); non-null ranks
+//      by a wave scan; the index run of each rank by marking run starts and a
+//      max scan; rows 8l .. 8l + 7 per lane -> u16 codes: the raw index, or
+//      0xFFFF for NULL (k_pipe_write tests indices against the dictionary,
+//      column_reader.cpp:190-194, so no page here waits for the dictionary).
+// Pages outside that shape (a bad or zero-count header before the value
+// count, more than rc runs in a stream, a level above max_def, a bit width
+// > 16, a prologue error) are listed for k_pipe_exact, the reference state
+// machine.  The leading workgroups decode the chunk's dictionary page
+// (dict_index.hpp), as k_pipe_runs' do.
+constexpr int kWinWaves = kRunWaves;   // (the dictionary workgroups run dict_index_block<kRunWaves>)
+constexpr uint32_t kWinPagesMax = 16;  // pages per window: <= 32 walking lanes
+constexpr uint32_t kWinRecMax = 255;   // records per stream: u8 run ids in the rank marks
 
-struct FrLayout {
-    uint32_t stage, tab, pinfo, pmap, recd, reci, mark, mark2, total;
-};
-__host__ __device__ inline FrLayout fr_layout(uint32_t win) {  // win: window bytes (multiple of 16)
-    FrLayout L{};
-    L.stage = 0;                                  // win + 32 bytes: the slots, then zeros
-    L.tab = win + 32;                             // u16 per window byte (+ the stop entry at [win])
-    L.pinfo = L.tab + (2 * win + 4 + 15) / 16 * 16;  // uint4 per page
-    L.pmap = L.pinfo + 16 * kFrPages;             // u8 per 16-byte block: its page
-    L.recd = L.pmap + (win / 16 + 15) / 16 * 16;  // uint2 x kFrRuns: run records
-    L.reci = L.recd + 8 * kFrRuns;
-    L.mark = L.reci + 8 * kFrRuns;                // u8 per row / rank
-    L.mark2 = L.mark + kTileRows;
-    L.total = L.mark2 + kTileRows;
-    return L;
+// per-wave LDS: [stage: wbytes + 64][rank marks: kTileRows][validity map: 64]
+// [records: 2 x wp streams, win_stride(rc) u32 apart]
+// (an odd stride: the walking lanes' stores fall in distinct banks)
+__host__ __device__ constexpr uint32_t win_stride(uint32_t rc) { return (rc + 1) | 1u; }  // (+1: the zero run)
+__host__ __device__ constexpr uint32_t win_wave_lds(uint32_t wbytes, uint32_t wp, uint32_t rc) {
+    return wbytes + 64 + kTileRows + 64 + (2 * wp * win_stride(rc) * 4 + 15) / 16 * 16;
 }
 
-// Branch-free header parse of the bytes x0:x1 at position q (as big_hdr).
-__device__ __forceinline__ BigHdr hdr_x(uint32_t x0, uint32_t x1, uint32_t q) {
-    const uint32_t st0 = ~x0 & 0x80808080u;
-    BigHdr h;
-    const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;  // (st0 == 0 gives 32 -> 5, replaced below)
-    const uint32_t hl5 = (~x1 & 0x80u) ? 5u : 9u;
-    h.hl = st0 ? hl4 : hl5;
-    const uint32_t lm = (h.hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (h.hl & 3))) - 1u);
-    const uint32_t x0m = x0 & lm;
-    const uint32_t top = (h.hl >= 5) ? (x1 << 28) : 0u;
-    const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) |
-                         ((x0m >> 3) & 0xFE00000u) | top;
-    h.g = ind >> 1;
-    h.lit = ind & 1u;
-    h.qh = q + h.hl;
-    const uint32_t va = __builtin_amdgcn_alignbyte(x1, x0, h.hl);
-    const uint32_t vb = x1 >> (8 * ((h.hl - 4) & 3));
-    h.vraw = (h.hl < 4) ? va : vb;
-    return h;
+// 32 bits of the staged window starting at bit b (b >= -31; bits before bit 0
+// read as 0); word indices past zw (the page slot's last, zero word) clamp
+__device__ __forceinline__ uint32_t win_bits32(const uint32_t* st, int32_t b, uint32_t zw) {
+    const uint32_t bp = static_cast<uint32_t>(max(b, 0));
+    const uint32_t wi = bp >> 5;
+    const uint32_t v = __builtin_amdgcn_alignbit(st[min(wi + 1, zw)], st[min(wi, zw)], bp & 31u);
+    return v << (bp - static_cast<uint32_t>(b));
 }
 
-// Records of one stream from its listed headers (step B): rec[i] = (first
-// value, literal << 31 | payload) for the runs that start before value n,
-// plus the zero run of an exhausted stream.  Returns the record count, or
-// ~0u when the page needs the exact decoder.
-__device__ __forceinline__ uint32_t fr_records(const uint32_t* stw, const uint16_t* list, uint32_t nl, bool capped,
-                                               uint32_t e, uint32_t bw, uint32_t n, uint2* rec) {
-    const uint32_t nbv = (bw + 7) / 8;
-    const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
-    const uint32_t litpay = bw ? 0x80000000u : 0u, litmul = bw ? 8u : 0u;
-    uint32_t cbase = 0, nrec = 0;
-    for (uint32_t r = 0; r < nl; r += kWave) {
-        const uint32_t i = r + lane();
-        const bool act = i < nl;
-        const uint32_t q = list[act ? i : 0u];
-        const BigHdr h = big_hdr(stw, q);
-        const bool bad = act && big_bad(h, e, nbv);
-        const uint32_t cl = min(h.g, 1u << 17) * 8, cr = min(h.g, 1u << 20);
-        const uint32_t c = (act && !bad) ? (h.lit ? cl : cr) : 0u;
-        const uint32_t incl = wave_incl_scan(c);
-        const uint32_t start = cbase + incl - c;
-        if (__ballot(bad && start < n)) return ~0u;  // a bad header before the value count
-        const bool keep = act && !bad && start < n;
-        const uint32_t pay = h.lit ? (litpay | (h.qh * litmul)) : (h.vraw & vmask);
-        if (keep) rec[i] = make_uint2(start, pay);
-        nrec += static_cast<uint32_t>(__popcll(__ballot(keep)));
-        cbase += bcast_last(incl);
+template <bool kDict>
+__global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __restrict__ bytes,
+                                                             const DevPage* __restrict__ pages,
+                                                             const DevBatch* __restrict__ wins, int nwins,
+                                                             int32_t max_def, uint16_t* __restrict__ codes,
+                                                             int32_t* __restrict__ flist, uint32_t wbytes,
+                                                             uint32_t wp, uint32_t rc, uint32_t lds_total,
+                                                             RunDictArgs d, int debug) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t win_dyn[];
+    // (kDict: the leading workgroups decode the dictionary pages; its code
+    // costs the page waves registers and 12 KB of static LDS, so by default
+    // the dictionary decodes on the side stream instead)
+    if constexpr (kDict) {
+        if (static_cast<int>(blockIdx.x) < d.ndicts) {
+            dict_index_block<kRunWaves>(bytes, d.dicts, static_cast<int>(blockIdx.x), d.entries, d.dict_count, d.dict_err,
+                                        d.err_any, lds_total, win_dyn);
+            return;
+        }
     }
-    if (cbase < n) {
-        // the listed runs hold fewer values than needed: a chain cut at
-        // kFrRuns headers, or the stream's end (the rest of the batch is 0;
-        // a bad last header was caught above: its first value is cbase < n)
-        if (capped || nrec >= kFrRuns) return ~0u;
-        if (lane() == 0) rec[nrec] = make_uint2(cbase, 0u);
-        nrec++;
+    const uint32_t wv = threadIdx.x / kWave;
+    const int w = (static_cast<int>(blockIdx.x) - d.ndicts) * kWinWaves + static_cast<int>(wv);
+    if (w >= nwins) return;
+    uint8_t* base = reinterpret_cast<uint8_t*>(win_dyn) + wv * win_wave_lds(wbytes, wp, rc);
+    uint32_t* stw = reinterpret_cast<uint32_t*>(base);
+    uint8_t* mk = base + wbytes + 64;
+    uint32_t* vmap = reinterpret_cast<uint32_t*>(mk + kTileRows);
+    uint32_t* recs = vmap + 16;
+    const DevBatch B = wins[w];
+    const uint32_t np = static_cast<uint32_t>(B.np);
+    const uint32_t md = static_cast<uint32_t>(max_def);
+    // 1. the window's slots, then 64 zero bytes
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(bytes + B.img_lo);
+        uint4* dst = reinterpret_cast<uint4*>(stw);
+        const uint32_t nb = B.img_bytes / 16;
+        copy_blocks(dst, src, nb, lane(), kWave);  // (eight loads in flight per lane before the stores)
+        if (lane() < 4) dst[nb + lane()] = make_uint4(0u, 0u, 0u, 0u);
     }
-    return nrec;
-}
-
-// Per lane: the record (among nrec) of positions 8l .. 8l + 7 of a value
-// range of m positions, by marking record starts and a max scan.
-__device__ __forceinline__ void fr_runs8(uint8_t* mark, const uint2* rec, uint32_t nrec, uint32_t m, uint32_t rid[8]) {
-    const uint32_t l8 = lane() * 8;
-    *reinterpret_cast<uint2*>(mark + l8) = make_uint2(0u, 0u);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    for (uint32_t k = lane(); k < nrec; k += kWave) {
-        const uint32_t st = rec[k].x;
-        if (k > 0 && st < m) mark[st] = static_cast<uint8_t>(k);
-    }
+    // one page per lane pair: descriptor and prologue (column_reader.cpp:146-182)
+    const uint32_t pk = min(lane() >> 1, np - 1);
+    const DevPage pg = pages[B.p0 + static_cast<int>(pk)];
+    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0)), n = static_cast<uint32_t>(max(pg.nvals, 0));
+    const uint32_t s0 = static_cast<uint32_t>(pg.off - B.img_lo);
+    const uint32_t zw = (s0 + (size + 15) / 16 * 16 + 16) / 4 - 1;  // the slot's last word (zero)
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint2 mk = *reinterpret_cast<const uint2*>(mark + l8);
-    uint32_t run = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
-        rid[k] = run;
+    if (debug & (1 << 20)) return;  // timing ablation: staging only (outputs invalid)
+    uint32_t fb = n > static_cast<uint32_t>(kTileRows) ? 1u : 0u;
+    uint32_t pos = 0, db = 0, dl = 0, bwi = 0;
+    if (md > 0) {
+        if (size < 4) fb = 1;
+        else {
+            dl = static_cast<uint32_t>(lds_u64(stw, s0));
+            pos = 4;
+            if (static_cast<uint64_t>(pos) + dl > size) fb = 1;
+            else { db = 4; pos += dl; }
+        }
     }
-    const uint32_t ex = wave_shr1(wave_incl_max(run));
-#pragma unroll
-    for (int k = 0; k < 8; k++) rid[k] = max(ex, rid[k]);
-}
-
-// page info (pinfo): x = dbase | dend << 16, y = ibase | iend << 16 (window
-// positions), z = bwi | fallback << 8 | (slot start / 16) << 16, w = rows
-__global__ void __launch_bounds__(kFrWaves * 64) k_pipe_front(CodeArgs a, const DevBatch* __restrict__ wins, int nwins,
-                                                              uint32_t lt_n, uint32_t win, int32_t* __restrict__ flist) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const FrLayout Ly = fr_layout(win);
-    const uint32_t lens_bytes = (lt_n * 2 + 15) / 16 * 16;
-    uint16_t* lens = reinterpret_cast<uint16_t*>(smem);
-    const int wv = static_cast<int>(threadIdx.x / kWave);
-    uint8_t* base = smem + lens_bytes + static_cast<uint32_t>(wv) * Ly.total;
-    uint32_t* stw = reinterpret_cast<uint32_t*>(base + Ly.stage);
-    uint16_t* tab = reinterpret_cast<uint16_t*>(base + Ly.tab);
-    uint4* pinfo = reinterpret_cast<uint4*>(base + Ly.pinfo);
-    uint8_t* pmap = base + Ly.pmap;
-    uint2* recd = reinterpret_cast<uint2*>(base + Ly.recd);
-    uint2* reci = reinterpret_cast<uint2*>(base + Ly.reci);
-    uint8_t* mark = base + Ly.mark;
-    uint8_t* mark2 = base + Ly.mark2;
-
-    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
-    const bool lean = dict_n <= lt_n;
-    copy_map(lens, a.entries + ebase, min(dict_n, lt_n), threadIdx.x, blockDim.x,
-             [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
-    __syncthreads();
-    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
-    const bool hasd = a.max_def > 0;
-    const uint32_t maskd = (1u << bwd) - 1u, nbvd = (bwd + 7) / 8;
+    if (!fb) {
+        if (pos + 1 > size) fb = 1;
+        else { bwi = static_cast<uint32_t>(lds_u64(stw, s0 + pos)) & 0xFFu; pos += 1; }
+    }
+    if (bwi > 16) fb = 1;
+    // 2. lock-step walk: lane 2k the def stream of page k, lane 2k + 1 its
+    //    index stream, to the stream's end (no value counts: the records are
+    //    formed per page below, one lane per run); each step lists one header
+    //    position.  Branch-free: flags are 0/1 words combined with & and |
+    //    (&& / || compile to exec-mask branches).  kOne: every live header is
+    //    one byte, what both writers emit for runs of < 64 values or groups.
+    const bool isi = (lane() & 1u) != 0;
+    const uint32_t bw = isi ? bwi : 1u, nbv = (bw + 7) / 8;
+    const uint32_t e = fb ? 0u : (isi ? s0 + size : s0 + db + dl);
+    uint32_t q = fb ? 0u : (isi ? s0 + pos : s0 + db);
+    uint32_t nr = 0;
+    uint32_t live = ((lane() >> 1) < np && !fb && (isi || md > 0) && n > 0 && q < e) ? 1u : 0u;
+    uint32_t* rec = recs + lane() * win_stride(rc);
+    auto step = [&](auto one, uint32_t x0, uint32_t x1) {
+        constexpr bool kOne = decltype(one)::value;
+        uint32_t hl, ind, hbad = 0;
+        if constexpr (kOne) {
+            hl = 1;
+            ind = x0 & 0x7Fu;
+        } else {
+            const uint32_t st0 = ~x0 & 0x80808080u;
+            const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;
+            hl = st0 ? hl4 : ((~x1 & 0x80u) ? 5u : 9u);
+            const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
+            const uint32_t x0m = x0 & lm;
+            const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
+            ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) | ((x0m >> 3) & 0xFE00000u) | top;
+            hbad = hl > 5 ? 1u : 0u;
+        }
+        const uint32_t g = ind >> 1, lit = ind & 1u, qh = q + hl;
+        const uint32_t litm = 0u - lit;
+        // literal: g groups of 8 values (the end clamps: the reference reads
+        // on past it); RLE: g copies of an nbv-byte value, which must fit
+        const uint32_t nql = min(__umul24(min(g, 0x10000u), bw) + qh, e);
+        const uint32_t nqr = qh + nbv;
+        const uint32_t over = (litm & qh) | (~litm & nqr);
+        const uint32_t ok = live & (nr < rc ? 1u : 0u) & ((hbad | (g == 0 ? 1u : 0u) | (over > e ? 1u : 0u)) ^ 1u);
+        if (ok) rec[nr] = q;
+        nr += ok;
+        q = (litm & nql) | (~litm & nqr);
+        live = ok & (q < e ? 1u : 0u);
+    };
+    while (__ballot(live)) {
+        const uint32_t qa = q >> 2, qs = q & 3u;
+        const uint32_t w0 = stw[qa], w1 = stw[qa + 1];
+        const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, qs);
+        if (__ballot(live & (x0 >> 7)) == 0) {
+            step(std::true_type{}, x0, 0u);
+        } else {
+            const uint32_t w2 = stw[qa + 2];
+            step(std::false_type{}, x0, __builtin_amdgcn_alignbyte(w2, w1, qs));
+        }
+    }
+    // a chain that stopped before its stream's end (a bad header or rc
+    // headers): an error only if its runs hold fewer values than needed
+    const uint32_t cut = (q < e && !fb) ? 1u : 0u;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (debug & (1 << 21)) return;  // timing ablation: + the walk
+    // The records of one listed stream, in place (one lane per run): header
+    // position -> first value (capped at 1023: past any page's rows) |
+    // literal << 10 | (RLE value, or the literal values' window bit offset)
+    // << 11; returns the values the runs hold (capped at 2^30).
+    auto form = [&](uint32_t* rr, uint32_t nrec, uint32_t bwv) -> uint32_t {
+        const uint32_t nbvv = (bwv + 7) / 8;
+        const uint32_t vmv = nbvv >= 2 ? 0xFFFFu : (nbvv ? 0xFFu : 0u);
+        uint32_t base = 0;
+        for (uint32_t r0 = 0; r0 < nrec; r0 += kWave) {
+            const uint32_t r = r0 + lane();
+            const uint32_t act = r < nrec ? 1u : 0u;
+            const uint32_t qq = rr[act ? r : 0u];
+            const uint32_t qa = qq >> 2, qs = qq & 3u;
+            const uint32_t w0 = stw[qa], w1 = stw[qa + 1], w2 = stw[qa + 2];
+            const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, qs), x1 = __builtin_amdgcn_alignbyte(w2, w1, qs);
+            const uint32_t st0 = ~x0 & 0x80808080u;
+            const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;
+            const uint32_t hl = st0 ? hl4 : 5u;  // (listed headers are <= 5 bytes)
+            const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
+            const uint32_t x0m = x0 & lm;
+            const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
+            const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) | ((x0m >> 3) & 0xFE00000u) | top;
+            const uint32_t vraw = hl < 4 ? __builtin_amdgcn_alignbyte(x1, x0, hl) : x1 >> (8 * ((hl - 4) & 3));
+            const uint32_t g = ind >> 1, lit = ind & 1u, litm = 0u - lit;
+            const uint32_t c = act * ((litm & (min(g, 1u << 17) << 3)) | (~litm & min(g, 1u << 20)));
+            const uint32_t incl = wave_incl_scan(c);
+            const uint32_t st = min(base + incl - c, 1023u);
+            const uint32_t pay = (litm & ((qq + hl) << 3)) | (~litm & vraw & vmv);
+            if (act) rr[r] = st | (lit << 10) | (pay << 11);
+            base = min(base + bcast_last(incl), 1u << 30);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        return base;
+    };
+    // 3. per page
     const uint32_t l8 = lane() * 8;
-    const uint32_t kStop = win;  // the stop entry: tab[win] = win
-    const int nw = static_cast<int>(gridDim.x) * kFrWaves;
-    for (int w = static_cast<int>(blockIdx.x) * kFrWaves + wv; w < nwins; w += nw) {
-        const DevBatch B = wins[w];
-        const int p0 = B.p0, np = B.np;
-        // A1. slots -> LDS (16-byte aligned, >= 16 zero bytes after each payload), 32 zero bytes after
-        {
-            const uint4* src = reinterpret_cast<const uint4*>(a.bytes + B.img_lo);
-            uint4* dst = reinterpret_cast<uint4*>(stw);
-            const uint32_t nb = B.img_bytes / 16;
-            for (uint32_t i = lane(); i < nb + 2; i += kWave) dst[i] = i < nb ? src[i] : make_uint4(0u, 0u, 0u, 0u);
-            for (uint32_t d = lane(); d < (win / 16 + 3) / 4; d += kWave) reinterpret_cast<uint32_t*>(pmap)[d] = 0u;
-            if (lane() == 0) tab[kStop] = static_cast<uint16_t>(kStop);
-        }
-        // one lane per page: its descriptor (kept in registers for B) and prologue
-        const bool pl = static_cast<int>(lane()) < np;
-        const DevPage pg = a.pages[p0 + (pl ? static_cast<int>(lane()) : 0)];
-        const uint32_t psize = static_cast<uint32_t>(max(pg.size, 0)), prows = static_cast<uint32_t>(max(pg.nvals, 0));
-        const uint32_t s0 = static_cast<uint32_t>(pg.off - B.img_lo);  // slot start (window position)
-        const int32_t ptile = a.page_tile0[p0 + (pl ? static_cast<int>(lane()) : 0)];
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (pl && lane() > 0) pmap[s0 >> 4] = static_cast<uint8_t>(lane());
-        uint32_t fb = (!lean || prows > static_cast<uint32_t>(kTileRows)) ? 1u : 0u;
-        uint32_t pos = 0, dbase = 0, dlen = 0, bwi = 0;
-        if (hasd) {
-            if (psize < 4) fb = 1;
-            else {
-                dlen = static_cast<uint32_t>(lds_u64(stw, s0));
-                pos = 4;
-                if (static_cast<uint64_t>(pos) + dlen > psize) fb = 1;
-                else { dbase = 4; pos += dlen; }
-            }
-        }
-        if (!fb && a.max_rep > 0) {
-            if (pos + 4 > psize) fb = 1;
-            else {
-                const uint32_t rl = static_cast<uint32_t>(lds_u64(stw, s0 + pos));
-                pos += 4;
-                if (static_cast<uint64_t>(pos) + rl > psize) fb = 1;
-                else pos += rl;
-            }
-        }
-        if (!fb) {
-            if (pos + 1 > psize) fb = 1;
-            else { bwi = static_cast<uint32_t>(lds_u64(stw, s0 + pos)) & 0xFFu; pos += 1; }
-        }
-        if (bwi > 16) fb = 1;
-        if (!pl) fb = 1;
-        // window positions of the streams; a fallback page has empty streams
-        const uint32_t wdb = fb ? 0u : s0 + dbase, wde = fb ? 0u : s0 + dbase + dlen;
-        const uint32_t wib = fb ? 0u : s0 + pos, wie = fb ? 0u : s0 + psize;
-        if (pl) pinfo[lane()] = make_uint4(wdb | (wde << 16), wib | (wie << 16), bwi | (fb << 8) | ((s0 >> 4) << 16), prows);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        {   // page of every 16-byte block: max scan of the page starts (two blocks per lane... up to win / 16)
-            uint32_t* pm32 = reinterpret_cast<uint32_t*>(pmap);
-            const uint32_t nbk = (win / 16 + 3) / 4;  // dwords of the map
-            uint32_t carry = 0;
-            for (uint32_t d0 = 0; d0 < nbk; d0 += kWave) {
-                const uint32_t d = d0 + lane();
-                const uint32_t x = d < nbk ? pm32[d] : 0u;
-                uint32_t r0 = x & 0xFFu, r1 = max(r0, (x >> 8) & 0xFFu), r2 = max(r1, (x >> 16) & 0xFFu),
-                         r3 = max(r2, x >> 24);
-                const uint32_t ex = max(wave_shr1(wave_incl_max(r3)), carry);
-                carry = max(carry, bcast_last(wave_incl_max(r3)));
-                r0 = max(r0, ex); r1 = max(r1, ex); r2 = max(r2, ex); r3 = max(r3, ex);
-                if (d < nbk) pm32[d] = r0 | (r1 << 8) | (r2 << 16) | (r3 << 24);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (a.debug & 0x100000) continue;  // timing: staging + prologue only
-        // A2. next-header table over the window, two positions per lane and step
-        {
-            uint32_t* tab32 = reinterpret_cast<uint32_t*>(tab);
-            const uint32_t npair = B.img_bytes / 2;
-            for (uint32_t jp = lane(); jp < npair; jp += kWave) {
-                const uint32_t j = 2 * jp, i = j >> 2, sh = j & 3u;
-                const uint4 P = pinfo[pmap[j >> 4]];
-                const uint32_t w0 = stw[i], w1 = stw[i + 1], w2 = stw[i + 2];
-                const uint32_t dbj = P.x & 0xFFFFu, dej = P.x >> 16, ibj = P.y & 0xFFFFu, iej = P.y >> 16;
-                const uint32_t bwj = P.z & 0xFFu;
-                auto next_at = [&](uint32_t q, uint32_t x0, uint32_t x1) -> uint32_t {
-                    const bool isi = q >= ibj && q < iej, isd = q >= dbj && q < dej;
-                    const uint32_t e = isi ? iej : dej, bw = isi ? bwj : bwd, nbv = isi ? (bwj + 7) / 8 : nbvd;
-                    const BigHdr h = hdr_x(x0, x1, q);
-                    const uint32_t litm = 0u - h.lit;
-                    const uint32_t nx = (litm & (h.qh + __umul24(min(h.g, 0x10000u), bw))) | (~litm & (h.qh + nbv));
-                    const bool bad = h.hl > 5 || h.qh > e || h.g == 0 || (!h.lit && h.qh + nbv > e);
-                    return ((isi || isd) && !bad && nx < e) ? nx : kStop;
-                };
-                const uint32_t a0 = __builtin_amdgcn_alignbyte(w1, w0, sh), a1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
-                const uint32_t b0 = __builtin_amdgcn_alignbyte(w1, w0, sh + 1), b1 = __builtin_amdgcn_alignbyte(w2, w1, sh + 1);
-                tab32[jp] = next_at(j, a0, a1) | (next_at(j + 1, b0, b1) << 16);
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (a.debug & 0x200000) continue;  // timing: + next-header table
-        // A3. lane 2k lists page k's def-stream headers, lane 2k + 1 its index
-        //     stream's, in place: entry c of a list at (stream start + c) <= the
-        //     c-th header's position, behind the chain's reads
-        uint32_t cnt = 0, capped = 0;
-        {
-            const uint32_t k = lane() >> 1;
-            const bool isd = (lane() & 1u) == 0;
-            const uint4 P = pinfo[min(k, kFrPages - 1)];
-            const uint32_t q0 = isd ? (P.x & 0xFFFFu) : (P.y & 0xFFFFu), e = isd ? (P.x >> 16) : (P.y >> 16);
-            bool go = static_cast<int>(k) < np && (!isd || hasd) && q0 < e;
-            uint32_t q = q0, nx = kStop;
-            while (go) {
-                nx = tab[q];
-                tab[q0 + cnt] = static_cast<uint16_t>(q);
-                cnt++;
-                go = nx != kStop && cnt < kFrRuns;
-                q = nx;
-            }
-            capped = (cnt >= kFrRuns && nx != kStop) ? 1u : 0u;
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (a.debug & 0x400000) continue;  // timing: + header lists
-        // B. per page
-        for (int k = 0; k < np; k++) {
-            const uint4 P = pinfo[k];
-            const int p = p0 + k;
-            const uint32_t n = P.w;
-            const int32_t t = static_cast<int32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(ptile), k));
-            if ((P.z >> 8) & 1u) {  // outside the fast shape: listed for the exact decoder (k_pipe_exact)
-                if (lane() == 0) flist[1 + atomicAdd(flist, 1)] = p;
-                continue;
-            }
-            if (n == 0) continue;  // (no tile)
-            const uint32_t dbk = P.x & 0xFFFFu, dek = P.x >> 16, ibk = P.y & 0xFFFFu, iek = P.y >> 16, bwi = P.z & 0xFFu;
-            const uint32_t zw = ((P.z >> 16) * 16 + (iek - ((P.z >> 16) * 16) + 15) / 16 * 16 + 16) / 4 - 1;  // slot's last (zero) word
-            const uint32_t nld = __builtin_amdgcn_readlane(cnt, 2 * k), nli = __builtin_amdgcn_readlane(cnt, 2 * k + 1);
-            const bool capd = __builtin_amdgcn_readlane(capped, 2 * k) != 0, capi = __builtin_amdgcn_readlane(capped, 2 * k + 1) != 0;
-            const int64_t R0 = static_cast<int64_t>(
-                (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(pg.first_row) >> 32), k)) << 32) |
-                __builtin_amdgcn_readlane(static_cast<uint32_t>(pg.first_row), k));
-            bool fbk = false;
-            // def levels -> validity bits of rows 8l .. 8l + 7
-            uint32_t vb = l8 >= n ? 0u : (n - l8 >= 8 ? 0xFFu : ((1u << (n - l8)) - 1u));
-            if (hasd) {
-                const uint32_t nrd = fr_records(stw, tab + dbk, nld, capd, dek, bwd, n, recd);
-                if (nrd == ~0u) fbk = true;
+    for (uint32_t k = 0; k < np; k++) {
+        const int p = B.p0 + static_cast<int>(k);
+        const uint32_t nk = __builtin_amdgcn_readlane(n, 2 * k);
+        const uint32_t zwk = __builtin_amdgcn_readlane(zw, 2 * k);
+        const uint32_t bwk = __builtin_amdgcn_readlane(bwi, 2 * k);
+        uint32_t nrd = __builtin_amdgcn_readlane(nr, 2 * k), nri = __builtin_amdgcn_readlane(nr, 2 * k + 1);
+        const uint32_t cutd = __builtin_amdgcn_readlane(cut, 2 * k), cuti = __builtin_amdgcn_readlane(cut, 2 * k + 1);
+        bool flk = __builtin_amdgcn_readlane(fb, 2 * k) != 0;
+        if (nk == 0 && !flk) continue;  // (no tile)
+        const int64_t R0 = static_cast<int64_t>(
+            (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(pg.first_row) >> 32), 2 * k)) << 32) |
+            __builtin_amdgcn_readlane(static_cast<uint32_t>(pg.first_row), 2 * k));
+        const uint32_t rowm = l8 >= nk ? 0u : (nk - l8 >= 8 ? 0xFFu : ((1u << (nk - l8)) - 1u));
+        uint32_t vb = rowm;
+        if (!flk && md > 0) {
+            uint32_t* rd = recs + 2 * k * win_stride(rc);
+            const uint32_t totd = form(rd, nrd, 1u);
+            if (totd < nk) {  // the stream ran out: the rest of the levels are 0 (rle_decoder.hpp:20-23)
+                if (cutd) flk = true;  // ... unless its chain stopped at a bad header
                 else {
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    uint32_t rid[8];
-                    fr_runs8(mark, recd, nrd, n, rid);
-                    vb = 0;
-                    bool above = false;
-#pragma unroll
-                    for (int kk = 0; kk < 8; kk++) {
-                        const uint32_t j = l8 + kk;
-                        const uint2 R = recd[rid[kk] & (kFrRuns - 1)];
-                        const uint32_t pay = rr_pay(R);
-                        const uint32_t lb = sbits3(stw, pay + (j - R.x) * bwd, zw, maskd);
-                        const uint32_t lvl = rr_lit(R) ? lb : pay;
-                        const bool in = j < n;
-                        vb |= (in && lvl == md ? 1u : 0u) << kk;
-                        above |= in && lvl > md;
-                    }
-                    if (__ballot(above)) fbk = true;  // levels above max_def: the exact decoder's error
+                    if (lane() == 0) rd[nrd] = totd;
+                    nrd++;
                 }
             }
-            if (a.debug & 0x800000) continue;  // timing: + def levels
-            uint32_t pw[4] = {0u, 0u, 0u, 0u}, chars = 0;
-            if (!fbk) {
-                const uint32_t nnl = __popc(vb);
-                const uint32_t nincl = wave_incl_scan(nnl);
-                const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
-                uint32_t nri = 0;
-                if (nn) {
-                    nri = fr_records(stw, tab + ibk, nli, capi, iek, bwi, nn, reci);
-                    if (nri == ~0u) fbk = true;
-                }
-                if (!fbk) {
-                    if (nn) {
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        uint32_t rid[8];
-                        fr_runs8(mark2, reci, nri, nn, rid);
-                        // record of every rank, for the rows' random access below
-                        uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-                        for (int kk = 0; kk < 8; kk++) {
-                            if (kk < 4) w0 |= rid[kk] << (8 * kk);
-                            else w1 |= rid[kk] << (8 * (kk - 4));
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                        *reinterpret_cast<uint2*>(mark2 + l8) = make_uint2(w0, w1);
-                    } else {
-                        *reinterpret_cast<uint2*>(mark2 + l8) = make_uint2(0u, 0u);
-                        if (lane() == 0) reci[0] = make_uint2(0u, 0u);
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    const uint32_t maski = (1u << bwi) - 1u;
-#pragma unroll
-                    for (int kk = 0; kk < 8; kk++) {
-                        const uint32_t rk = min(rbase + __popc(vb & ((1u << kk) - 1u)), static_cast<uint32_t>(kTileRows - 1));
-                        const uint2 R = reci[mark2[rk] & (kFrRuns - 1)];
-                        const uint32_t pay = rr_pay(R);
-                        const uint32_t lb = sbits3(stw, pay + (rk - R.x) * bwi, zw, maski);
-                        const uint32_t v = rr_lit(R) ? lb : pay;
-                        const bool ok = ((vb >> kk) & 1u) && v < dict_n;
-                        const uint32_t len = lens[ok ? v : 0u];
-                        chars += ok ? len : 0u;
-                        const uint32_t code = ok ? v : static_cast<uint32_t>(kNull);
-                        if (kk & 1) pw[kk >> 1] |= code << 16;
-                        else pw[kk >> 1] = code;
-                    }
-                }
-            }
-            if (fbk) {
-                if (lane() == 0) flist[1 + atomicAdd(flist, 1)] = p;
-                continue;
-            }
-            if (a.debug & 0x1000000) continue;  // timing: no stores
-            store_packed8(a.codes, R0, l8, n, pw);
-            tile_done(a, t, wave_sum(chars));
+            // def runs -> validity map (rows of level 1; literal runs: the stream's bits)
+            if (lane() < 16) vmap[lane()] = 0u;
             __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            bool above = false;
+            for (uint32_t r = lane(); r < nrd && !flk; r += kWave) {
+                const uint32_t R = rd[r];
+                const uint32_t s = R & 0x3FFu, en = min(r + 1 < nrd ? (rd[r + 1] & 0x3FFu) : nk, nk);
+                if (s >= nk) continue;  // (runs past the rows)
+                const uint32_t lit = (R >> 10) & 1u, pay = R >> 11;
+                above |= !lit && pay > md;
+                if ((lit || pay == md) && en > s) {
+                    for (uint32_t wd = s >> 5; wd <= (en - 1) >> 5; wd++) {
+                        const uint32_t lo = max(s, wd * 32) - wd * 32, hi = min(en, wd * 32 + 32) - wd * 32;
+                        const uint32_t m = (hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+                        const uint32_t v = lit ? win_bits32(stw, static_cast<int32_t>(pay + wd * 32) - static_cast<int32_t>(s), zwk)
+                                               : 0xFFFFFFFFu;
+                        if (v & m) atomicOr(&vmap[wd], v & m);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (__ballot(above)) flk = true;  // levels above max_def: the exact decoder's error
+            vb = static_cast<uint32_t>(reinterpret_cast<const uint8_t*>(vmap)[lane()]) & rowm;
         }
+        if (flk) {
+            if (lane() == 0) flist[1 + atomicAdd(flist, 1)] = p;
+            continue;
+        }
+        if (debug & (1 << 22)) continue;  // timing ablation: + validity
+        const uint32_t nnl = __popc(vb);
+        const uint32_t nincl = wave_incl_scan(nnl);
+        const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
+        uint32_t pw[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        uint32_t* ri = recs + (2 * k + 1) * win_stride(rc);
+        if (nn) {
+            const uint32_t toti = form(ri, nri, bwk);
+            if (toti < nn) {  // exhausted: the rest of the indices are 0
+                if (cuti) {
+                    if (lane() == 0) flist[1 + atomicAdd(flist, 1)] = p;
+                    continue;
+                }
+                if (lane() == 0) ri[nri] = toti;
+                nri++;
+            }
+        }
+        if (nn) {
+            *reinterpret_cast<uint2*>(mk + l8) = make_uint2(0u, 0u);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t r = lane(); r < nri; r += kWave) {
+                const uint32_t st = ri[r] & 0x3FFu;
+                if (r > 0 && st < nn) mk[st] = static_cast<uint8_t>(r);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            {   // the record of ranks 8l .. 8l + 7 (max scan of the marks), back to mk
+                const uint2 mv = *reinterpret_cast<const uint2*>(mk + l8);
+                uint32_t rm[8], run = 0;
+#pragma unroll
+                for (int kk = 0; kk < 8; kk++) {
+                    run = max(run, ((kk < 4 ? mv.x : mv.y) >> (8 * (kk & 3))) & 0xFFu);
+                    rm[kk] = run;
+                }
+                const uint32_t ex = wave_shr1(wave_incl_max(run));
+                uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+                for (int kk = 0; kk < 8; kk++) {
+                    const uint32_t v = max(ex, rm[kk]);
+                    if (kk < 4) w0 |= v << (8 * kk);
+                    else w1 |= v << (8 * (kk - 4));
+                }
+                __builtin_amdgcn_wave_barrier();
+                *reinterpret_cast<uint2*>(mk + l8) = make_uint2(w0, w1);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t maski = (1u << bwk) - 1u;
+#pragma unroll
+            for (int kk = 0; kk < 8; kk++) {
+                const uint32_t rk = min(rbase + __popc(vb & ((1u << kk) - 1u)), static_cast<uint32_t>(kTileRows - 1));
+                const uint32_t R = ri[mk[rk]];
+                const uint32_t st = R & 0x3FFu, pay = R >> 11;
+                const uint32_t lb = sbits3(stw, pay + (rk - st) * bwk, zwk, maski);
+                const uint32_t v = ((R >> 10) & 1u) ? lb : pay;
+                const uint32_t code = ((vb >> kk) & 1u) ? v : static_cast<uint32_t>(kNull);
+                if (kk & 1) pw[kk >> 1] = (pw[kk >> 1] & 0xFFFFu) | (code << 16);
+                else pw[kk >> 1] = (pw[kk >> 1] & 0xFFFF0000u) | code;
+            }
+        }
+        if (debug & (1 << 23)) continue;  // timing ablation: no stores
+        store_packed8(codes, R0, l8, nk, pw);
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
-// The pages k_pipe_front listed: the reference state machine, one wave per
+// The pages k_pipe_win listed: the reference state machine, one wave per
 // page (a separate launch: its registers would cost the front its occupancy).
 __global__ void __launch_bounds__(64) k_pipe_exact(CodeArgs a, const int32_t* __restrict__ flist) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // one CodeLds: one wave per workgroup
@@ -3347,7 +3378,7 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     write_shape(P, &wgrid, &per);
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.bsum, per, P.debug, P.write_waves};
+               P.self_sum ? nullptr : P.bsum, per, P.debug, P.write_waves};
     if (count_pass) {
         const dim3 grid((P.ntiles + kCodeWaves - 1) / kCodeWaves);
         hipLaunchKernelGGL(k_pipe_codes<true>, grid, dim3(kCodeWaves * kWave), 0, s, a);
@@ -3408,6 +3439,7 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
                 P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves, P.znext, P.znext_words,
                 P.match, P.match_neg, P.page_flags};
+    a.self_sum = P.self_sum ? 1 : 0;
     if (P.match)
         hipLaunchKernelGGL(k_pipe_write<true>, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
     else
@@ -3457,26 +3489,45 @@ void launch_wide_chars(hipStream_t s, const PipeLaunch& P) {
                        0, s, a);
 }
 
-uint32_t pipe_front_slot(uint32_t max_page_bytes) { return (max_page_bytes + 15) / 16 * 16 + 16; }
+uint32_t pipe_win_slot(uint32_t page_bytes) { return (page_bytes + 15) / 16 * 16 + 16; }
 
-uint32_t pipe_front_win_pages() { return kFrPages; }
+uint32_t pipe_win_lds(uint32_t wbytes, uint32_t wp, uint32_t rc, uint32_t dict_max) {
+    uint32_t lds = static_cast<uint32_t>(kWinWaves) * win_wave_lds(wbytes, wp, rc);
+    if (dict_max) lds = max(lds, (dict_max + 32 + 15) / 16 * 16 + 16);  // dict_index_block: the page + 32 bytes
+    return lds;
+}
 
-void launch_pipe_front(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, int nwins, uint32_t win) {
-    if (P.ntiles <= 0) return;
+bool pipe_win_shape_ok(uint32_t wp, uint32_t rc) { return wp >= 1 && wp <= kWinPagesMax && rc >= 2 && rc <= kWinRecMax; }
+
+void launch_pipe_win(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, int nwins, uint32_t wbytes, uint32_t wp,
+                     uint32_t rc, const RunDicts* dicts, uint32_t dict_max) {
+    const int nd = dicts ? dicts->ndicts : 0;
+    if (nwins <= 0 && nd <= 0) return;
+    const RunDictArgs d = dicts ? RunDictArgs{dicts->dicts, nd, dicts->entries, dicts->dict_count, dicts->dict_err,
+                                              dicts->err_any}
+                                : RunDictArgs{nullptr, 0, nullptr, nullptr, nullptr, nullptr};
+    const uint32_t lds = pipe_win_lds(wbytes, wp, rc, nd ? dict_max : 0u);
+    const void* fn = nd ? reinterpret_cast<const void*>(k_pipe_win<true>) : reinterpret_cast<const void*>(k_pipe_win<false>);
+    ensure_dyn_lds(fn, lds);
+    if (nd)
+        hipLaunchKernelGGL(k_pipe_win<true>, dim3(nd + (max(nwins, 0) + kWinWaves - 1) / kWinWaves), dim3(kWinWaves * kWave),
+                           lds, s, P.bytes, P.pages, wins, nwins, P.max_def, P.codes, const_cast<int32_t*>(P.flist), wbytes,
+                           wp, rc, lds, d, P.debug);
+    else
+        hipLaunchKernelGGL(k_pipe_win<false>, dim3((max(nwins, 0) + kWinWaves - 1) / kWinWaves), dim3(kWinWaves * kWave),
+                           lds, s, P.bytes, P.pages, wins, nwins, P.max_def, P.codes, const_cast<int32_t*>(P.flist), wbytes,
+                           wp, rc, lds, d, P.debug);
+}
+
+void launch_pipe_exact(hipStream_t s, const PipeLaunch& P) {
+    // pages k_pipe_win listed (none on well-formed files): the reference state
+    // machine, after the dictionary; no per-workgroup character sums (the
+    // self-summing k_pipe_write sums every tile itself)
     int wgrid = 0, per = 0;
-    write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_write's workgroups
+    write_shape(P, &wgrid, &per);
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.bsum, per, P.debug, P.write_waves};
-    const uint32_t lt_n = P.dict_entries_cap;
-    const uint32_t lds = (lt_n * 2 + 15) / 16 * 16 + kFrWaves * fr_layout(win).total;
-    const void* fn = reinterpret_cast<const void*>(k_pipe_front);
-    const int bpc = max(1, resident_blocks(fn, kFrWaves * kWave, lds));
-    const int need = (nwins + kFrWaves - 1) / kFrWaves;
-    const int grid = max(1, min(need, P.cus * bpc));
-    int32_t* flist = const_cast<int32_t*>(P.flist);  // [0] cleared with the decode's flags
-    hipLaunchKernelGGL(k_pipe_front, dim3(grid), dim3(kFrWaves * kWave), lds, s, a, wins, nwins, lt_n, win, flist);
-    // listed pages (none on well-formed ref-layout chunks)
+               nullptr, per, P.debug, P.write_waves};
     hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, P.npages))), dim3(kWave), sizeof(CodeLds), s, a, P.flist);
 }
 

@@ -195,6 +195,8 @@ struct PipeLaunch {
     // the same dictionary as 16-byte slots (launch_dict_big's pad16), or
     // null: k_pipe_wwide then reads entry words and characters
     const uint4* pad16 = nullptr;
+    // k_pipe_write sums every tile's characters itself (k_pipe_win files none)
+    bool self_sum = false;
 };
 constexpr uint32_t kArmDictBytes = 32768;  // every entry length < 2^15: the match bit rides in the entry word
 struct PipePlan {
@@ -230,15 +232,20 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
                       const RunDicts* dicts = nullptr, uint32_t stage_max = 0,  // 0: k_pipe_codes3's stage
                       uint32_t slot_max = 0, uint32_t dict_max = 0, int cus = 256);  // pages_per_wave 0: auto
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
-// k_pipe_front: the whole front (run headers -> u16 codes, tile characters)
-// of chunks whose pages hold <= kTileRows rows, one wavefront per window of
-// consecutive pages (<= pipe_front_win_pages() pages whose slots span <= win
-// bytes; every slot <= win); k_pipe_exact then decodes the pages it listed
-uint32_t pipe_front_slot(uint32_t max_page_bytes);
-uint32_t pipe_front_win_pages();
-constexpr uint32_t kFrontWin = 2048;     // window bytes (pages with larger slots take the run-table passes)
+// k_pipe_win: the whole front (run headers -> u16 codes, no characters) of
+// chunks whose pages hold <= kTileRows rows with max_def <= 1 and no rep
+// levels, one wavefront per window of <= wp consecutive pages whose slots
+// (pipe_win_slot bytes each) span <= wbytes; rc run records per stream.
+// k_pipe_exact then decodes the pages it listed; k_pipe_write must run with
+// self_sum.  The leading workgroups decode `dicts` (or null) as k_pipe_runs'.
+uint32_t pipe_win_slot(uint32_t page_bytes);
+uint32_t pipe_win_lds(uint32_t wbytes, uint32_t wp, uint32_t rc, uint32_t dict_max);
+bool pipe_win_shape_ok(uint32_t wp, uint32_t rc);
 struct DevBatch;
-void launch_pipe_front(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, int nwins, uint32_t win);
+void launch_pipe_win(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, int nwins, uint32_t wbytes, uint32_t wp,
+                     uint32_t rc, const RunDicts* dicts, uint32_t dict_max);
+// the pages k_pipe_win listed, once the dictionary is decoded
+void launch_pipe_exact(hipStream_t s, const PipeLaunch& P);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,
 // then codes and tile characters (one workgroup per listed page)

@@ -103,6 +103,13 @@ struct HostColumn {
     Value value(int64_t i) const;    // reference Value semantics (INT96 -> "INT96(hi:lo)")
 };
 
+// The API-parity std::vector<Value> of rows [a, b) of a decoded column
+// (the slow path, multithreaded): contiguous row ranges on
+// `threads` host threads (0: hardware_concurrency, at most 16), each
+// constructing its rows' Values in place.
+std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned threads = 0);
+inline std::vector<Value> to_values(const HostColumn& h, unsigned threads = 0) { return to_values(h, 0, h.num_rows, threads); }
+
 class ColumnReader {
 public:
     ColumnReader(ReadRangeFunc read_range, const ColumnChunk& chunk, ParquetType type,

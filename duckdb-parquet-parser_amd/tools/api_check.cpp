@@ -13,15 +13,23 @@
 //   api_check <file> decode_regex_sharded <name> <k> <pattern> <neg>
 //                                                  read_column_regex over k Devices: the column's
 //                                                  dump on stdout, the page ids on stderr
+//   api_check <file> time_read_all <rg> <col> <reps> <dump path>
+//                                                  times ColumnReader::read_all (host bytes ->
+//                                                  std::vector<Value>), read_columnar and the
+//                                                  Value build alone (median ms, JSON on stdout);
+//                                                  the last read_all's dump goes to the path
 #include <execinfo.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <chrono>
 #include <csignal>
 #include <cstdio>
 #include <cstring>
 #include <iostream>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pq_gpu.h"
@@ -128,6 +136,41 @@ int main(int argc, char** argv) {
                                    ci.type, ci.max_def_level, ci.max_rep_level);
             if (mode == "column_reader") {
                 for (const auto& v : cr.read_all()) dump(v, out);
+            } else if (mode == "time_read_all") {
+                if (argc < 7) return 2;
+                const int reps = std::max(1, std::atoi(argv[5]));
+                auto now = [] { return std::chrono::steady_clock::now(); };
+                auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+                auto med = [](std::vector<double> v) {
+                    std::sort(v.begin(), v.end());
+                    return v[v.size() / 2];
+                };
+                std::vector<double> ta, tc, tv;
+                std::vector<pqgpu::Value> vals = cr.read_all();  // warm-up (device buffers, first-touch pages)
+                for (int i = 0; i < reps; i++) {
+                    vals.clear();
+                    vals.shrink_to_fit();
+                    const auto t0 = now();
+                    vals = cr.read_all();
+                    const auto t1 = now();
+                    pqgpu::HostColumn h = cr.read_columnar();
+                    const auto t2 = now();
+                    std::vector<pqgpu::Value> v2 = pqgpu::to_values(h);
+                    const auto t3 = now();
+                    ta.push_back(ms(t0, t1));
+                    tc.push_back(ms(t1, t2));
+                    tv.push_back(ms(t2, t3));
+                }
+                for (const auto& v : vals) dump(v, out);
+                FILE* fh = std::fopen(argv[6], "wb");
+                if (!fh) throw std::runtime_error("cannot write the dump");
+                std::fwrite(out.data(), 1, out.size(), fh);
+                std::fclose(fh);
+                std::printf("{\"values\": %zu, \"read_all_ms\": %.4f, \"read_columnar_ms\": %.4f, "
+                            "\"to_values_ms\": %.4f, \"threads\": %u}\n",
+                            vals.size(), med(ta), med(tc), med(tv),
+                            std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+                return 0;
             } else {
                 for (const auto& pr : cr.read_pages()) {
                     std::fprintf(stderr, "%d %d %d %zu\n", pr.page_num, static_cast<int>(pr.type),

@@ -225,8 +225,8 @@ def ref_read_all(file: bytes, ch: Chunk):
     return 0, "", _take(p, n.value)
 
 
-def ref_read_pages(file: bytes, ch: Chunk, cap: int = 1 << 20):
-    R = ref()
+def ref_read_pages(file: bytes, ch: Chunk, cap: int = 1 << 20, lib_=None):
+    R = lib_ or ref()
     p = u8p()
     n = C.c_size_t()
     err = C.create_string_buffer(512)
@@ -291,14 +291,18 @@ def have_ref_gpu() -> bool:
 
 
 def ref_gpu():
-    """The reference's own ParquetReader / ColumnReader with read_all's body
-    replaced by INTEGRATION.md path B (integration/column_reader_gpu.cpp over
+    """The reference's own ParquetReader / ColumnReader with the bodies of
+    read_all and read_pages replaced by INTEGRATION.md path B (integration/column_reader_gpu.cpp over
     libpqgpu.so): the maintainer-side binding, built by `make refgpu`."""
     global _ref_gpu
     if _ref_gpu is None:
         L = C.CDLL(_REF_GPU)
         L.pqref_read_column.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(u8p), C.POINTER(C.c_size_t), C.c_char_p,
                                         C.c_size_t]
+        common = [u8p, C.c_size_t, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int32, C.c_int32,
+                  C.c_int16, C.c_int16, C.POINTER(u8p), C.POINTER(C.c_size_t)]
+        L.pqref_read_all.argtypes = common + [C.c_char_p, C.c_size_t]
+        L.pqref_read_pages.argtypes = common + [i64p, C.c_int, C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
         L.pqref_free.argtypes = [C.c_void_p]
         _ref_gpu = L
     return _ref_gpu

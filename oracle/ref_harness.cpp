@@ -62,7 +62,7 @@ uint8_t* to_malloc(const std::vector<uint8_t>& v, size_t* len) {
 }
 
 ColumnChunk make_chunk(int64_t num_values, int64_t data_off, int64_t dict_off, int has_dict,
-                       int32_t codec, int32_t type) {
+                       int32_t codec, int32_t type, size_t flen) {
     ColumnChunk cc;
     ColumnMetaData md;
     md.type = static_cast<ParquetType>(type);
@@ -70,6 +70,10 @@ ColumnChunk make_chunk(int64_t num_values, int64_t data_off, int64_t dict_off, i
     md.num_values = num_values;
     md.data_page_offset = data_off;
     if (has_dict) md.dictionary_page_offset = dict_off;
+    // (the CPU reader never reads it; a reader that fetches the chunk as one
+    // range, INTEGRATION.md path B, gets the bytes up to EOF)
+    const int64_t start = has_dict ? std::min(dict_off, data_off) : data_off;
+    md.total_compressed_size = std::max<int64_t>(static_cast<int64_t>(flen) - start, 0);
     cc.meta_data = md;
     return cc;
 }
@@ -92,7 +96,7 @@ int pqref_read_all(const uint8_t* file, size_t flen, int64_t num_values, int64_t
                    int64_t dict_off, int has_dict, int32_t codec, int32_t type, int16_t max_def,
                    int16_t max_rep, uint8_t** dump, size_t* dump_len, char* err, size_t errlen) {
     try {
-        ColumnChunk cc = make_chunk(num_values, data_off, dict_off, has_dict, codec, type);
+        ColumnChunk cc = make_chunk(num_values, data_off, dict_off, has_dict, codec, type, flen);
         ColumnReader r(memory_range(file, flen), cc, static_cast<ParquetType>(type), max_def,
                        max_rep);
         std::vector<Value> vals = r.read_all();
@@ -116,7 +120,7 @@ int pqref_read_pages(const uint8_t* file, size_t flen, int64_t num_values, int64
                      int16_t max_rep, uint8_t** dump, size_t* dump_len, int64_t* pages, int cap,
                      int* npages, char* err, size_t errlen) {
     try {
-        ColumnChunk cc = make_chunk(num_values, data_off, dict_off, has_dict, codec, type);
+        ColumnChunk cc = make_chunk(num_values, data_off, dict_off, has_dict, codec, type, flen);
         ColumnReader r(memory_range(file, flen), cc, static_cast<ParquetType>(type), max_def,
                        max_rep);
         std::vector<PageResult> prs = r.read_pages();
@@ -264,7 +268,7 @@ int pqref_write(const char* path, int ncols, const char** names, const int32_t* 
 double pqref_time_read_all(const uint8_t* file, size_t flen, int64_t num_values, int64_t data_off,
                            int64_t dict_off, int has_dict, int32_t type, int16_t max_def,
                            int16_t max_rep, int reps, int threads, int64_t* values_out) {
-    ColumnChunk cc = make_chunk(num_values, data_off, dict_off, has_dict, 0, type);
+    ColumnChunk cc = make_chunk(num_values, data_off, dict_off, has_dict, 0, type, flen);
     std::vector<int64_t> counts(threads, 0);
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> ts;
@@ -296,7 +300,7 @@ double pqref_time_read_all_multi(int n, const uint8_t* const* files, const size_
                                  int64_t* values_out) {
     std::vector<ColumnChunk> ccs;
     for (int i = 0; i < n; i++)
-        ccs.push_back(make_chunk(num_values[i], data_off[i], dict_off[i], has_dict[i], 0, type));
+        ccs.push_back(make_chunk(num_values[i], data_off[i], dict_off[i], has_dict[i], 0, type, flens[i]));
     std::vector<int64_t> counts(threads, 0);
     std::atomic<int64_t> next{0};
     const int64_t total = static_cast<int64_t>(n) * reps;
@@ -334,7 +338,7 @@ double pqref_time_regex_pages_multi(int n, const uint8_t* const* files, const si
                                     const void* mstate, int neg, int reps, int threads, uint8_t* flags) {
     std::vector<ColumnChunk> ccs;
     for (int i = 0; i < n; i++)
-        ccs.push_back(make_chunk(num_values[i], data_off[i], dict_off[i], has_dict[i], 0, type));
+        ccs.push_back(make_chunk(num_values[i], data_off[i], dict_off[i], has_dict[i], 0, type, flens[i]));
     std::atomic<int64_t> next{0};
     const int64_t total = static_cast<int64_t>(n) * reps;
     auto t0 = std::chrono::steady_clock::now();

@@ -1,12 +1,14 @@
-"""INTEGRATION.md path B: the maintainer-side binding that swaps the body of
-the reference's ColumnReader::read_all (/root/reference/src/reader/
-column_reader.cpp:18-71) for the MI355X path.  The code published in
+"""INTEGRATION.md path B: the maintainer-side binding that swaps the bodies of
+the reference's ColumnReader::read_all and read_pages (/root/reference/src/
+reader/column_reader.cpp:18-126) for the MI355X path.  The code published in
 INTEGRATION.md is integration/column_reader_gpu.cpp verbatim; CPU: it
 compiles against the reference's headers (/root/reference/include) and
 pq_gpu.h.  GPU: the reference's own ParquetReader::read_column linked with
 that body (oracle/_ref/librefgpu.so, `make -C oracle refgpu`) returns what
-the reference's CPU read_column returns on every golden fixture, and the C1
-ifstream quirk is resolved as DESIGN.md §7 records."""
+the reference's CPU read_column returns on every golden fixture, its
+ColumnReader::read_pages returns the CPU body's page records and values on
+every chunk of them, and the C1 ifstream quirk is resolved as DESIGN.md §7
+records."""
 import glob
 import os
 import re
@@ -16,7 +18,7 @@ import pytest
 
 from oracle import oracle as O
 from pqgpu import capi
-from util import file_chunks, oracle_read_column
+from util import file_chunks, oracle_read_column, to_oracle_chunk
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SNIPPET = os.path.join(ROOT, "integration", "column_reader_gpu.cpp")
@@ -67,6 +69,26 @@ def test_reference_read_column_with_gpu_read_all(path):
             assert rc_gpu == 0 and gpu == exp, (name, msg_cpu, msg_gpu)
         else:
             assert rc_gpu != 0, (name, msg_cpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not (O.have_ref() and O.have_ref_gpu()), reason="oracle/_ref not built")
+@pytest.mark.parametrize("path", _fixtures(), ids=lambda p: os.path.basename(p))
+def test_reference_read_pages_with_gpu_body(path):
+    data = open(path, "rb").read()
+    try:
+        F = capi.File(data)
+    except capi.PqError:
+        pytest.skip("footer outside the fixture set's readable files")
+    for ci in range(len(F.column_names())):
+        for ch in file_chunks(data, ci):
+            och = to_oracle_chunk(ch)
+            cpu = O.ref_read_pages(data, och)
+            gpu = O.ref_read_pages(data, och, lib_=O.ref_gpu())
+            if cpu[0] == 0:
+                assert gpu[0] == 0 and gpu[2:] == cpu[2:], (ci, gpu[1])
+            else:
+                assert gpu[0] != 0, (ci, cpu[1])
 
 
 @pytest.mark.gpu
