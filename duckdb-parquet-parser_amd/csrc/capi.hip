@@ -615,10 +615,8 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     c->win_bytes = 0;
     c->win_pages = static_cast<uint32_t>(std::max(1, std::min(16, ctx->opt_win_pages)));
     const uint32_t wcap = static_cast<uint32_t>(ctx->opt_win_bytes);
-    // (the self-summing writer after it holds <= 64 tiles per wave)
     c->pipe_fr = small && !multi && c->hbig.empty() && c->max_def <= 1 && c->max_rep == 0 &&
-                 pqk::pipe_win_slot(small_bytes) <= wcap &&
-                 pages.size() <= static_cast<size_t>(64) * static_cast<size_t>(c->pipe_grid) * static_cast<size_t>(wpw);
+                 pqk::pipe_win_slot(small_bytes) <= wcap;
     if (c->pipe_fr) {
         size_t p = 0;
         while (p < pages.size()) {
@@ -2112,7 +2110,7 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
                                  static_cast<uint32_t>(ctx->opt_win_rc), dict_in_runs ? &rd : nullptr, c->max_dict_bytes);
         }
         if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
-        Timed t(ctx, "pipe_exact");
+        Timed t(ctx, "pipe_tail");
         pqk::launch_pipe_exact(s, P);
         return;
     }
@@ -2300,8 +2298,9 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_plain_ba(s, P);
     } else if (pipe) {
         pqk::PipeLaunch P = pipe_launch(ctx, c, out);
-        P.self_sum = front || (ctx->opt_write_self && !c->pipe_wide && c->hbig.empty() &&
-                               c->ntiles <= 64 * c->pipe_grid * c->pipe_wpw);  // k_pipe_win files no tile characters
+        // (A/B: the writer sums every tile's characters itself instead of
+        // k_pipe_codes3 / k_pipe_tail filing them)
+        P.self_sum = ctx->opt_write_self && !c->pipe_wide && c->hbig.empty() && c->ntiles <= 64 * c->pipe_grid * c->pipe_wpw;
         pipe_front(ctx, c, P, !dict_in_runs, dict_in_runs, fused);
         if (c->arm) {  // the page filter in the same pass: match bits per entry, then the writer tests them
             Timed t(ctx, "regex_dict");

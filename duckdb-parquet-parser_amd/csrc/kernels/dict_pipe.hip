@@ -2493,7 +2493,8 @@ __global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __re
                                                              const DevPage* __restrict__ pages,
                                                              const DevBatch* __restrict__ wins, int nwins,
                                                              int32_t max_def, uint16_t* __restrict__ codes,
-                                                             int32_t* __restrict__ flist, uint32_t wbytes,
+                                                             int32_t* __restrict__ flist, uint32_t* __restrict__ info,
+                                                             uint32_t wbytes,
                                                              uint32_t wp, uint32_t rc, uint32_t lds_total,
                                                              RunDictArgs d, int debug) {
     extern __shared__ __attribute__((aligned(16))) uint32_t win_dyn[];
@@ -2698,7 +2699,7 @@ __global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __re
             vb = static_cast<uint32_t>(reinterpret_cast<const uint8_t*>(vmap)[lane()]) & rowm;
         }
         if (flk) {
-            if (lane() == 0) flist[1 + atomicAdd(flist, 1)] = p;
+            if (lane() == 0) { flist[1 + atomicAdd(flist, 1)] = p; info[p] = kFallback; }
             continue;
         }
         if (debug & (1 << 22)) continue;  // timing ablation: + validity
@@ -2711,7 +2712,7 @@ __global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __re
             const uint32_t toti = form(ri, nri, bwk);
             if (toti < nn) {  // exhausted: the rest of the indices are 0
                 if (cuti) {
-                    if (lane() == 0) flist[1 + atomicAdd(flist, 1)] = p;
+                    if (lane() == 0) { flist[1 + atomicAdd(flist, 1)] = p; info[p] = kFallback; }
                     continue;
                 }
                 if (lane() == 0) ri[nri] = toti;
@@ -2764,6 +2765,7 @@ __global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __re
         }
         if (debug & (1 << 23)) continue;  // timing ablation: no stores
         store_packed8(codes, R0, l8, nk, pw);
+        if (lane() == 0) info[p] = 0u;  // (k_pipe_tail sums its tiles)
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -2782,6 +2784,81 @@ __global__ void __launch_bounds__(64) k_pipe_exact(CodeArgs a, const int32_t* __
     }
 }
 
+
+// ── after k_pipe_win (k_pipe_tail) ─────────────────────────────────────────
+// Once the dictionary is decoded: the pages k_pipe_win listed, by the
+// reference state machine (their codes, tile characters and per-workgroup
+// sums), then the characters of every other tile from its raw codes (entry
+// lengths in LDS; indices at or past the dictionary's entry count are NULL
+// rows, column_reader.cpp:190-194), filed as k_pipe_codes3 files them for
+// k_pipe_write.  Each wave takes a contiguous tile range; the codes of four
+// tiles load at once.
+constexpr int kTailWaves = 4;
+__global__ void __launch_bounds__(kTailWaves * 64) k_pipe_tail(CodeArgs a, const int32_t* __restrict__ flist,
+                                                               uint32_t lt_n) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // [kTailWaves x CodeLds][lens]
+    CodeLds& L = reinterpret_cast<CodeLds*>(smem)[threadIdx.x / kWave];
+    uint16_t* lens = reinterpret_cast<uint16_t*>(smem + kTailWaves * sizeof(CodeLds));
+    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
+    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
+    const uint32_t nl = min(dict_n, lt_n);
+    copy_map(lens, a.entries + ebase, nl, threadIdx.x, blockDim.x, [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
+    __syncthreads();
+    const int gw = static_cast<int>(blockIdx.x) * kTailWaves + static_cast<int>(threadIdx.x / kWave);
+    const int nw = static_cast<int>(gridDim.x) * kTailWaves;
+    const int nf = flist[0];
+    for (int i = gw; i < nf; i += nw) {
+        exact_page_body(a, L, flist[1 + i], dict_n, ebase);
+        __builtin_amdgcn_wave_barrier();
+    }
+    const uint32_t l8 = lane() * 8;
+    const int pw = (a.ntiles + nw - 1) / nw;
+    const int ta = min(a.ntiles, gw * pw), tb = min(a.ntiles, ta + pw);
+    for (int c0 = ta; c0 < tb; c0 += kWave) {
+        const int cn = min(kWave, tb - c0);
+        int64_t myR0 = 0;
+        uint32_t mym = 0, myskip = 1;
+        if (static_cast<int>(lane()) < cn) {
+            const DevTile T = a.tiles[c0 + lane()];
+            myR0 = a.pages[T.page].first_row + T.row0;
+            mym = static_cast<uint32_t>(T.nrows);
+            myskip = (a.info[T.page] & kFallback) ? 1u : 0u;  // (decoded above)
+        }
+        for (int i0 = 0; i0 < cn; i0 += 4) {
+            uint4 cv[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                cv[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+                const int i = i0 + u;
+                if (i < cn && !__builtin_amdgcn_readlane(myskip, i)) {
+                    const int64_t R = static_cast<int64_t>(
+                        (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(myR0) >> 32), i)) << 32) |
+                        __builtin_amdgcn_readlane(static_cast<uint32_t>(myR0), i));
+                    if (l8 < __builtin_amdgcn_readlane(mym, i)) {
+                        const U16B x = *reinterpret_cast<const U16B*>(a.codes + R + l8);
+                        cv[u] = make_uint4(x.x, x.y, x.z, x.w);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u;
+                if (i >= cn) break;
+                if (__builtin_amdgcn_readlane(myskip, i)) continue;
+                const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
+                const uint32_t ww[4] = {cv[u].x, cv[u].y, cv[u].z, cv[u].w};
+                uint32_t sum = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t c = (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                    const bool ok = l8 + k < mm && c < nl;
+                    sum += ok ? lens[ok ? c : 0u] : 0u;
+                }
+                tile_done(a, c0 + i, wave_sum(sum));
+            }
+        }
+    }
+}
 
 // ── codes and write in one persistent pass (k_pipe_fused) ───────────────────
 // k_pipe_codes3's per-tile decode and k_pipe_write's per-tile write, fused so
@@ -3511,24 +3588,32 @@ void launch_pipe_win(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, i
     ensure_dyn_lds(fn, lds);
     if (nd)
         hipLaunchKernelGGL(k_pipe_win<true>, dim3(nd + (max(nwins, 0) + kWinWaves - 1) / kWinWaves), dim3(kWinWaves * kWave),
-                           lds, s, P.bytes, P.pages, wins, nwins, P.max_def, P.codes, const_cast<int32_t*>(P.flist), wbytes,
-                           wp, rc, lds, d, P.debug);
+                           lds, s, P.bytes, P.pages, wins, nwins, P.max_def, P.codes, const_cast<int32_t*>(P.flist),
+                           const_cast<uint32_t*>(P.info), wbytes, wp, rc, lds, d, P.debug);
     else
         hipLaunchKernelGGL(k_pipe_win<false>, dim3((max(nwins, 0) + kWinWaves - 1) / kWinWaves), dim3(kWinWaves * kWave),
-                           lds, s, P.bytes, P.pages, wins, nwins, P.max_def, P.codes, const_cast<int32_t*>(P.flist), wbytes,
-                           wp, rc, lds, d, P.debug);
+                           lds, s, P.bytes, P.pages, wins, nwins, P.max_def, P.codes, const_cast<int32_t*>(P.flist),
+                           const_cast<uint32_t*>(P.info), wbytes, wp, rc, lds, d, P.debug);
 }
 
 void launch_pipe_exact(hipStream_t s, const PipeLaunch& P) {
-    // pages k_pipe_win listed (none on well-formed files): the reference state
-    // machine, after the dictionary; no per-workgroup character sums (the
-    // self-summing k_pipe_write sums every tile itself)
     int wgrid = 0, per = 0;
-    write_shape(P, &wgrid, &per);
+    write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_write's workgroups
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               nullptr, per, P.debug, P.write_waves};
-    hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, P.npages))), dim3(kWave), sizeof(CodeLds), s, a, P.flist);
+               P.self_sum ? nullptr : P.bsum, per, P.debug, P.write_waves};
+    if (P.self_sum) {  // the self-summing writer sums every tile: the listed pages only
+        hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, P.npages))), dim3(kWave), sizeof(CodeLds), s, a, P.flist);
+        return;
+    }
+    if (P.ntiles <= 0) return;
+    const uint32_t lt_n = P.dict_entries_cap;
+    const uint32_t lds = kTailWaves * static_cast<uint32_t>(sizeof(CodeLds)) + (lt_n * 2 + 15) / 16 * 16;
+    const void* fn = reinterpret_cast<const void*>(k_pipe_tail);
+    ensure_dyn_lds(fn, lds);
+    const int bpc = max(1, resident_blocks(fn, kTailWaves * kWave, lds));
+    const int need = (P.ntiles + kTailWaves * 8 - 1) / (kTailWaves * 8);  // >= 8 tiles per wave
+    hipLaunchKernelGGL(k_pipe_tail, dim3(max(1, min(need, P.cus * bpc))), dim3(kTailWaves * kWave), lds, s, a, P.flist, lt_n);
 }
 
 int pipe_fused_tiles() { return kFuseTiles; }
