@@ -455,11 +455,11 @@ def c2_leg(J, args, exp):
             x.free()
             w.append(t1 - t0), u.append(t2 - t1), d.append(t3 - t2)
         J.ctx.timing(False)
-        phases = {k: J.ctx.timing_get(k)[0] / 3 for k in UPLOAD_PHASES}
+        phases = upload_phases(J.ctx, 3)
         wm, um, dm = statistics.median(w), statistics.median(u), statistics.median(d)
         res["e2e"] = {"table_ms": wm * 1e3, "upload_ms": um * 1e3, "first_decode_ms": dm * 1e3,
                       "total_ms": (wm + um + dm) * 1e3, "values_per_s": nrows / (wm + um + dm),
-                      "file_bytes": len(f), "upload_phases_ms_mean": phases,
+                      "file_bytes": len(f), "upload_phases": phases,
                       "note": "from host file bytes: upload (walk, planning, allocation, "
                               "pinned H2D of the raw chunk bytes overlapped with the walk, GPU relayout) + first decode "
                               "(includes output allocation)"}
@@ -587,10 +587,10 @@ def c3_legs(J, args, exp):
             x.free()
             u.append(t2 - t1), r.append(t3 - t2)
         J.ctx.timing(False)
-        phases = {k: J.ctx.timing_get(k)[0] / 3 for k in UPLOAD_PHASES}
+        phases = upload_phases(J.ctx, 3)
         um, rm = statistics.median(u), statistics.median(r)
         regex["e2e"] = {"upload_ms": um * 1e3, "first_scan_ms": rm * 1e3, "total_ms": (um + rm) * 1e3,
-                        "pages_per_s": npages / (um + rm), "upload_phases_ms_mean": phases,
+                        "pages_per_s": npages / (um + rm), "upload_phases": phases,
                         "payload_bytes": rdc.payload_bytes,
                         "note": "from host file bytes: pq_chunk_upload (speculative page walk, device planning, "
                                 "allocation, pinned multi-buffered H2D) + one regex scan incl. pattern compile"}
@@ -666,6 +666,17 @@ def _rows_slice(h, r0: int, r1: int):
     return capi.HostColumn(h.type, h.validity[r0:r1], h.data[r0 * w:r1 * w], None)
 
 
+def _piece_alg_bytes(p, optional: bool) -> int:
+    """SURVEY §8(d) algorithmic bytes of one decoded device chunk: its page
+    payloads, its values (BYTE_ARRAY: 8(n+1) offsets + chars; else n x width)
+    and, for OPTIONAL columns, its validity bitmap."""
+    from pqgpu import capi
+    n = p.num_rows
+    o = p.out
+    vals = o.num_bytes + (8 * (n + 1) if o.type == capi.BYTE_ARRAY else 0)
+    return p.payload_bytes + vals + ((n + 7) // 8 if optional else 0)
+
+
 def c4_leg(J, args):
     """the 8-column mixed file at --c4-rows-per-gpu x N rows
     (100M at N = 8) in row groups of --c4-rows rows, data pages sharded across
@@ -718,7 +729,14 @@ def c4_leg(J, args):
         ck = lambda ps=ps: [p.decode_check() for p in ps]  # noqa: E731
         secs, kern = J.timed(st, ck, steps, args.repeats, warmup=2)
         ms = statistics.median(secs) / steps * 1e3
-        out[col.name] = {"ms": ms, "pieces": len(ps), "kernels_ms": {k: v["ms_per_step"] for k, v in kern.items()}}
+        # SURVEY §8(d) C4 algorithmic bytes of the column's shard: page payloads
+        # in; values (fixed width: n x width; strings: 8(n+1) offsets + chars)
+        # and the validity bitmap (OPTIONAL columns) out
+        b_alg = sum(_piece_alg_bytes(p, col.optional) for p in ps)
+        gbs = b_alg / (ms * 1e-3) / 1e9
+        out[col.name] = {"ms": ms, "pieces": len(ps), "kernels_ms": {k: v["ms_per_step"] for k, v in kern.items()},
+                         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes": b_alg}}
         total_ms += ms
     # the rank's whole share: every column's pieces alternated over
     # --c5-streams contexts (HIP streams), all queued before any check, so
@@ -736,12 +754,16 @@ def c4_leg(J, args):
     secs, _ = J.timed(rg_step, rg_check, steps, args.repeats, warmup=2)
     nvals = sum(p.num_rows for p in alld)
     nvals_all = J.sum_all([nvals])[0]
+    b_all = sum(_piece_alg_bytes(p, cols[ci].optional) for ci in pieces for p in pieces[ci])
     for p in alld:
         p.free()
     for c in ctxs[1:]:
         c.close()
     ms = statistics.median(secs) / steps * 1e3
     return {"values_per_s": nvals_all / (ms * 1e-3), "rows_per_gpu": nvals // len(cols), "row_groups_touched": nrg,
+            "roofline": {"bound": "hbm", "achieved": b_all / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": b_all / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": b_all,
+                         "note": "the rank's whole share per step (all 8 columns), B_alg as SURVEY §8(d) C4"},
             "rows_total": total, "row_group_rows": rg_rows, "ms_per_step": ms, "streams": len(ctxs),
             "serial_ms": total_ms, "serial_values_per_s": nvals_all / (total_ms * 1e-3),
             "note": "values_per_s: the rank's page shards of all 8 columns decoded together over `streams` contexts "
@@ -752,6 +774,22 @@ def c4_leg(J, args):
 
 UPLOAD_PHASES = ("up_walk", "up_plan", "up_plan_pages", "up_plan_fused", "up_plan_pipe", "up_plan_plain",
                  "up_plan_rest", "up_alloc", "up_h2d", "up_fill", "up_wait")
+UPLOAD_PHASES_NOTE = ("host timers per upload (sum over the uploads / uploads): NOT additive and NOT parts of "
+                      "upload_ms. up_walk, up_plan (with its up_plan_* parts) and up_alloc are wall times on the "
+                      "calling thread; with the raw upload the chunk's bytes go to HBM from a side thread that starts "
+                      "before the walk, so up_h2d (the H2D section, which also waits for that thread and copies the "
+                      "page tables) overlaps up_walk and up_plan; up_fill is CPU time summed over the threads that "
+                      "fill the pinned ring (several at once), up_wait the final wait for its DMA queues; "
+                      "calls_per_upload > 1 means the section ran that often per upload")
+
+
+def upload_phases(ctx, uploads: int) -> dict:
+    out = {"note": UPLOAD_PHASES_NOTE}
+    for k in UPLOAD_PHASES:
+        ms, calls = ctx.timing_get(k)
+        if calls:
+            out[k] = {"ms": ms / uploads, "calls_per_upload": calls / uploads}
+    return out
 
 
 def wide_dict_leg(J, args):

@@ -2110,8 +2110,10 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
                                  static_cast<uint32_t>(ctx->opt_win_rc), dict_in_runs ? &rd : nullptr, c->max_dict_bytes);
         }
         if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
-        Timed t(ctx, "pipe_tail");
-        pqk::launch_pipe_exact(s, P);
+        if (!P.self_sum) {  // (k_pipe_write sums the tiles itself, else k_pipe_tail files them)
+            Timed t(ctx, "pipe_tail");
+            pqk::launch_pipe_exact(s, P);
+        }
         return;
     }
     {
@@ -2300,7 +2302,8 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::PipeLaunch P = pipe_launch(ctx, c, out);
         // (A/B: the writer sums every tile's characters itself instead of
         // k_pipe_codes3 / k_pipe_tail filing them)
-        P.self_sum = ctx->opt_write_self && !c->pipe_wide && c->hbig.empty() && c->ntiles <= 64 * c->pipe_grid * c->pipe_wpw;
+        P.self_sum = (front || ctx->opt_write_self) && !c->pipe_wide && c->hbig.empty() &&
+                     c->ntiles <= 64 * c->pipe_grid * c->pipe_wpw;
         pipe_front(ctx, c, P, !dict_in_runs, dict_in_runs, fused);
         if (c->arm) {  // the page filter in the same pass: match bits per entry, then the writer tests them
             Timed t(ctx, "regex_dict");

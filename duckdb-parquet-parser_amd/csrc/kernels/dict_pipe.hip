@@ -275,7 +275,10 @@ __device__ void fail_page(const CodeArgs& a, const DevPage& pg, int32_t t0, uint
 // over the page in HBM, tile by tile; same error order as k_ba_fused.
 // (always inlined: a call would pass the LDS scratch as a generic pointer and
 // spill CodeArgs to scratch memory)
-template <bool kWide = false>
+// kRaw (k_pipe_win, before the dictionary is decoded): u16 codes hold the raw
+// index (0xFFFF for NULL and for indices that do not fit 16 bits), no tile
+// characters are filed (the self-summing k_pipe_write tests and sums them).
+template <bool kWide = false, bool kRaw = false>
 __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n, uint32_t ebase) {
     using CodeT = typename std::conditional<kWide, uint32_t, uint16_t>::type;
     constexpr CodeT kNullT = kWide ? static_cast<CodeT>(kNull32) : static_cast<CodeT>(kNull);
@@ -352,6 +355,7 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
     // dictionary, which may still be decoding while this runs)
     auto put_ix = [&](uint32_t k, uint32_t v) {
         if constexpr (kWide) ix[k] = v;
+        else if constexpr (kRaw) ix[k] = static_cast<CodeT>(v < 0xFFFFu ? v : static_cast<uint32_t>(kNullT));
         else ix[k] = static_cast<CodeT>(static_cast<int32_t>(v) >= 0 && v < dict_n ? v : static_cast<uint32_t>(kNullT));
     };
     for (uint32_t r0 = 0, ti = 0; r0 < n; r0 += kTileRows, ti++) {
@@ -384,14 +388,14 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
             CodeT code = kNullT;
             if (nnul) {
                 code = ix[k];
-                if (!kWide && code != kNullT) chars += static_cast<uint32_t>(a.entries[ebase + code] >> 32);
+                if (!kWide && !kRaw && code != kNullT) chars += static_cast<uint32_t>(a.entries[ebase + code] >> 32);
             }
             if (j < m) {
                 if (kWide) a.codes32[pg.first_row + r0 + j] = code;
                 else a.codes[pg.first_row + r0 + j] = static_cast<uint16_t>(code);
             }
         }
-        if (!kWide) {  // (kWide: k_wide_chars sums the tiles' characters)
+        if (!kWide && !kRaw) {  // (kWide: k_wide_chars sums the tiles' characters)
             chars = wave_sum(chars);
             tile_done(a, t0 + static_cast<int>(ti), chars);
         }
@@ -2475,8 +2479,10 @@ constexpr uint32_t kWinRecMax = 255;   // records per stream: u8 run ids in the 
 // [records: 2 x wp streams, win_stride(rc) u32 apart]
 // (an odd stride: the walking lanes' stores fall in distinct banks)
 __host__ __device__ constexpr uint32_t win_stride(uint32_t rc) { return (rc + 1) | 1u; }  // (+1: the zero run)
+// (at least one CodeLds: the listed pages' exact decode reuses the area)
 __host__ __device__ constexpr uint32_t win_wave_lds(uint32_t wbytes, uint32_t wp, uint32_t rc) {
-    return wbytes + 64 + kTileRows + 64 + (2 * wp * win_stride(rc) * 4 + 15) / 16 * 16;
+    return max(wbytes + 64 + kTileRows + 64 + (2 * wp * win_stride(rc) * 4 + 15) / 16 * 16,
+               static_cast<uint32_t>((sizeof(CodeLds) + 15) / 16 * 16));
 }
 
 // 32 bits of the staged window starting at bit b (b >= -31; bits before bit 0
@@ -2489,15 +2495,15 @@ __device__ __forceinline__ uint32_t win_bits32(const uint32_t* st, int32_t b, ui
 }
 
 template <bool kDict>
-__global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __restrict__ bytes,
-                                                             const DevPage* __restrict__ pages,
-                                                             const DevBatch* __restrict__ wins, int nwins,
-                                                             int32_t max_def, uint16_t* __restrict__ codes,
-                                                             int32_t* __restrict__ flist, uint32_t* __restrict__ info,
-                                                             uint32_t wbytes,
-                                                             uint32_t wp, uint32_t rc, uint32_t lds_total,
-                                                             RunDictArgs d, int debug) {
+__global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(CodeArgs ea, const DevBatch* __restrict__ wins, int nwins,
+                                                             uint32_t wbytes, uint32_t wp, uint32_t rc, uint32_t lds_total,
+                                                             RunDictArgs d) {
     extern __shared__ __attribute__((aligned(16))) uint32_t win_dyn[];
+    const uint8_t* __restrict__ bytes = ea.bytes;
+    const DevPage* __restrict__ pages = ea.pages;
+    uint16_t* __restrict__ codes = ea.codes;
+    const int32_t max_def = ea.max_def;
+    const int debug = ea.debug;
     // (kDict: the leading workgroups decode the dictionary pages; its code
     // costs the page waves registers and 12 KB of static LDS, so by default
     // the dictionary decodes on the side stream instead)
@@ -2646,10 +2652,10 @@ __global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __re
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         return base;
     };
-    // 3. per page
+    // 3. per page (pages outside the fast shape: bits of `listed`)
     const uint32_t l8 = lane() * 8;
+    uint32_t listed = 0;
     for (uint32_t k = 0; k < np; k++) {
-        const int p = B.p0 + static_cast<int>(k);
         const uint32_t nk = __builtin_amdgcn_readlane(n, 2 * k);
         const uint32_t zwk = __builtin_amdgcn_readlane(zw, 2 * k);
         const uint32_t bwk = __builtin_amdgcn_readlane(bwi, 2 * k);
@@ -2699,7 +2705,7 @@ __global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __re
             vb = static_cast<uint32_t>(reinterpret_cast<const uint8_t*>(vmap)[lane()]) & rowm;
         }
         if (flk) {
-            if (lane() == 0) { flist[1 + atomicAdd(flist, 1)] = p; info[p] = kFallback; }
+            listed |= 1u << k;
             continue;
         }
         if (debug & (1 << 22)) continue;  // timing ablation: + validity
@@ -2712,7 +2718,7 @@ __global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __re
             const uint32_t toti = form(ri, nri, bwk);
             if (toti < nn) {  // exhausted: the rest of the indices are 0
                 if (cuti) {
-                    if (lane() == 0) { flist[1 + atomicAdd(flist, 1)] = p; info[p] = kFallback; }
+                    listed |= 1u << k;
                     continue;
                 }
                 if (lane() == 0) ri[nri] = toti;
@@ -2765,7 +2771,14 @@ __global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(const uint8_t* __re
         }
         if (debug & (1 << 23)) continue;  // timing ablation: no stores
         store_packed8(codes, R0, l8, nk, pw);
-        if (lane() == 0) info[p] = 0u;  // (k_pipe_tail sums its tiles)
+        __builtin_amdgcn_wave_barrier();
+    }
+    // the listed pages: the reference state machine, raw codes (the wave's
+    // LDS area is free now)
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t k = 0; k < np; k++) {
+        if (!((listed >> k) & 1u)) continue;
+        exact_page_body<false, true>(ea, *reinterpret_cast<CodeLds*>(base), B.p0 + static_cast<int>(k), 0u, 0u);
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -3586,14 +3599,15 @@ void launch_pipe_win(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, i
     const uint32_t lds = pipe_win_lds(wbytes, wp, rc, nd ? dict_max : 0u);
     const void* fn = nd ? reinterpret_cast<const void*>(k_pipe_win<true>) : reinterpret_cast<const void*>(k_pipe_win<false>);
     ensure_dyn_lds(fn, lds);
+    CodeArgs ea{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
+                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
+                nullptr, 1, P.debug, P.write_waves};
     if (nd)
         hipLaunchKernelGGL(k_pipe_win<true>, dim3(nd + (max(nwins, 0) + kWinWaves - 1) / kWinWaves), dim3(kWinWaves * kWave),
-                           lds, s, P.bytes, P.pages, wins, nwins, P.max_def, P.codes, const_cast<int32_t*>(P.flist),
-                           const_cast<uint32_t*>(P.info), wbytes, wp, rc, lds, d, P.debug);
+                           lds, s, ea, wins, nwins, wbytes, wp, rc, lds, d);
     else
         hipLaunchKernelGGL(k_pipe_win<false>, dim3((max(nwins, 0) + kWinWaves - 1) / kWinWaves), dim3(kWinWaves * kWave),
-                           lds, s, P.bytes, P.pages, wins, nwins, P.max_def, P.codes, const_cast<int32_t*>(P.flist),
-                           const_cast<uint32_t*>(P.info), wbytes, wp, rc, lds, d, P.debug);
+                           lds, s, ea, wins, nwins, wbytes, wp, rc, lds, d);
 }
 
 void launch_pipe_exact(hipStream_t s, const PipeLaunch& P) {
