@@ -293,6 +293,7 @@ struct pq_chunk {
     int rwin_pre = -1;                  // and regex_prefetch
     uint32_t dfa_bytes = 0;
     bool dfa_full = false;               // the DFA image has full 256-column rows
+    bool dfa_sink = false;               // full rows of an anchored pattern (k_regex_plain<.., true>)
     std::string prog_pattern;           // pattern of d_prog / d_dfa
     int64_t dict_match_cap = 0;
     pqre::DeviceProgram* d_prog = nullptr;
@@ -751,8 +752,10 @@ void plan_plain(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages) {
                     const int64_t x = static_cast<int64_t>(pages[q].size) - 4 * static_cast<int64_t>(pages[q].nvals);
                     known &= x >= 0;
                     ch += x;
+                    b.nrows += static_cast<uint32_t>(std::max(pages[q].nvals, 0));
                     q++;
                 }
+                b.row0 = pages[p].first_row;
                 b.np = static_cast<int32_t>(q - p);
                 b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
                 W.push_back(b);
@@ -2673,8 +2676,10 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
             const uint64_t e = hp[q].off + (static_cast<uint64_t>(std::max(hp[q].size, 0)) + 15) / 16 * 16 + 16;
             if (e - b.img_lo > win) break;
             hi = e;
+            b.nrows += static_cast<uint32_t>(std::max(hp[q].nvals, 0));
             q++;
         }
+        b.row0 = hp[p].first_row;
         b.np = static_cast<int32_t>(q - p);
         b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
         c->hrwins.push_back(b);
@@ -2726,12 +2731,14 @@ static int regex_prepare(pq_ctx* ctx, pq_chunk* c, const char* pattern) {
             std::vector<uint8_t> img;
             dfree(c->d_dfa);
             c->dfa_bytes = 0;
+            c->dfa_sink = false;
             if (ctx->opt_regex_dfa && pqre::build_dfa(prog, &img)) {
                 if (dalloc(&c->d_dfa, img.size())) return set_err(ctx, PQ_ERR_HIP, "hipMalloc failed (dfa)");
                 if (int rc2 = hip_check(ctx, hipMemcpy(c->d_dfa, img.data(), img.size(), hipMemcpyHostToDevice), "dfa upload"))
                     return rc2;
                 c->dfa_bytes = static_cast<uint32_t>(img.size());
                 c->dfa_full = reinterpret_cast<const pqre::DevDfa*>(img.data())->full != 0;
+                c->dfa_sink = c->dfa_full && reinterpret_cast<const pqre::DevDfa*>(img.data())->anchored != 0;
             }
             c->prog_pattern = key;
         }
@@ -2801,7 +2808,8 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             pqre::launch_regex_plain(s, c->d_dfa, c->dfa_bytes, c->rwin_bytes, c->d_bytes, c->d_pages, c->d_rwins,
                                      static_cast<int>(c->hrwins.size()), c->d_rwin_ticket, c->rwin_grid, cp,
                                      (neg ? 1 : 0) | ((ctx->opt_regex_debug & 0xFF) << 8),
-                                     c->d_page_flags, c->d_page_err, c->d_flags, idx_in, idx_out, c->rwin_pre != 0);
+                                     c->d_page_flags, c->d_page_err, c->d_flags, idx_in, idx_out, c->rwin_pre != 0,
+                                     c->dfa_sink);
         } else if (c->d_dfa) {
             Timed t(ctx, "regex_lanes");
             pqre::launch_regex_lanes(s, c->d_dfa, c->dfa_bytes, c->d_bytes, c->d_pages, c->npages, c->d_dicts,

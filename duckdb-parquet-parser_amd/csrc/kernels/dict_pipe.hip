@@ -946,6 +946,173 @@ struct WriteArgs {
 };
 
 
+// One 512-row tile of k_pipe_write: rows 8l .. 8l + 7 of lane l hold the codes
+// `cur` (0xFFFF: NULL; indices at or past dict_n: NULL); R0 is the tile's
+// first output row, G0 its first output byte, m its rows.
+template <bool kArmed>
+__device__ __forceinline__ void write_tile(const WriteArgs& a, WriteLds& S, const uint32_t* dwa, const uint32_t* dtab,
+                                           uint32_t dict_n, int64_t R0, int64_t G0, uint32_t m, uint32_t page,
+                                           const uint32_t cur[kRowsPerLane]) {
+    constexpr bool armed = kArmed;
+    // this lane's rows 8l .. 8l + 7: lengths, dictionary offsets, validity
+    uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0, sat = 0;
+#pragma unroll
+    for (int k = 0; k < kRowsPerLane; k++) {
+        const bool valid = cur[k] < dict_n;
+        const uint32_t e = valid ? dtab[cur[k]] : 0u;
+        len[k] = armed ? ((e >> 16) & 0x7FFFu) : (e >> 16);
+        if (armed) sat |= e;
+        src[k] = e & 0xFFFFu;
+        vb |= (valid ? 1u : 0u) << k;
+        acc += len[k];
+    }
+    if (armed && __ballot(sat >> 31) && lane() == 0)  // the page filter: a row whose entry satisfies it
+        a.page_flags[page] = 0;
+    const uint32_t incl = wave_incl_scan(acc);
+    const uint32_t total = bcast_last(incl);
+    {
+        // the lane's eight rows as two 16-byte stores of offsets and one
+        // of sources (row-per-element stores would hit each bank 8 and 4
+        // times); rows past m get the tile end and are never read as rows
+        static_assert(kRowsPerLane == 8, "row layout");
+        uint32_t o[kRowsPerLane];
+        o[0] = incl - acc;
+#pragma unroll
+        for (int k = 1; k < kRowsPerLane; k++) o[k] = o[k - 1] + len[k - 1];
+        uint4* po = reinterpret_cast<uint4*>(&S.off[lane() * kRowsPerLane]);
+        po[0] = make_uint4(o[0], o[1], o[2], o[3]);
+        po[1] = make_uint4(o[4], o[5], o[6], o[7]);
+        *reinterpret_cast<uint4*>(&S.src[lane() * kRowsPerLane]) =
+            make_uint4(src[0] | (src[1] << 16), src[2] | (src[3] << 16), src[4] | (src[5] << 16),
+                       src[6] | (src[7] << 16));
+    }
+    S.vb[lane()] = static_cast<uint8_t>(vb);
+    if (lane() == 0) S.off[m] = total;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (!(a.debug & 4)) {
+        // offsets: rows 2j', 2j' + 1 per lane as one 16-byte store when
+        // the tile starts on an even row (coalesced), else row j = 64k + lane
+        if ((R0 & 1) == 0) {
+#pragma unroll
+            for (int k = 0; k < kRowsPerLane / 2; k++) {
+                const uint32_t j = k * 2 * kWave + 2 * lane();
+                if (j + 1 < m) {
+                    const uint2 o = *reinterpret_cast<const uint2*>(&S.off[j]);
+                    const int64_t v0 = G0 + o.x, v1 = G0 + o.y;
+                    *reinterpret_cast<uint4*>(a.offsets + R0 + j) =
+                        make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(static_cast<uint64_t>(v0) >> 32),
+                                   static_cast<uint32_t>(v1), static_cast<uint32_t>(static_cast<uint64_t>(v1) >> 32));
+                } else if (j < m) {
+                    a.offsets[R0 + j] = G0 + S.off[j];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kRowsPerLane; k++) {
+                const uint32_t j = k * kWave + lane();
+                if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
+            }
+        }
+        // validity words [R0 >> 5, (R0 + m - 1) >> 5]: tile word t = vb bytes 4t .. 4t + 3
+        const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
+        const uint32_t sh = static_cast<uint32_t>(R0 & 31);
+        const int64_t g = gfirst + lane();
+        if (g <= glast) {
+            auto tw = [&](int t) -> uint32_t {
+                return (t >= 0 && t < kWave / 4) ? reinterpret_cast<const uint32_t*>(S.vb)[t] : 0u;
+            };
+            const int t = static_cast<int>(lane());
+            const uint32_t val = (tw(t) << sh) | (sh ? (tw(t - 1) >> (32 - sh)) : 0u);
+            // the column's last word belongs to its last tile alone
+            const bool whole = g * 32 >= R0 && (g * 32 + 32 <= R0 + m || R0 + m == a.nrows_total);
+            if (whole) a.validity[g] = val;
+            else if (val) atomicOr(&a.validity[g], val);
+        }
+    }
+    if (R0 + m == a.nrows_total && lane() == 0) {
+        a.offsets[a.nrows_total] = G0 + total;
+        *a.total = G0 + total;
+    }
+    if (total == 0 || (a.debug & 2)) return;
+    if (G0 + total > a.capacity) {  // output too small: the host grows it and re-runs
+        if (lane() == 0) atomicOr(a.overflow, 1);
+        return;
+    }
+    // characters, 64 consecutive rows per step: each lane copies its
+    // row from the LDS dictionary to HBM as unaligned 16-byte moves
+    // (the last one overlapping the row's earlier bytes), rows under
+    // 16 bytes as two overlapping 8/4/2-byte moves, so no store leaves
+    // its row and the L2 merges the partial lines.  Rows longer than
+    // kLongRow are copied afterwards by the whole wave, 16-byte
+    // aligned blocks across the lanes.  (Assembling aligned blocks in
+    // LDS first costs more than it saves: byte-unaligned LDS accesses
+    // are slow; scripts/probe/unaligned_store.hip)
+    const int64_t G1 = G0 + total;
+    if (a.debug & 128) {  // timing only: the tile's bytes as aligned 16-byte blocks of zeros
+        const int64_t b0 = G0 & ~static_cast<int64_t>(15);
+        for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < G1; blk += 16 * kWave) {
+            const uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (blk >= G0 && blk + 16 <= G1) *reinterpret_cast<uint4*>(a.chars + blk) = v;
+            else store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, G0) - blk),
+                            static_cast<uint32_t>(min(blk + 16, G1) - blk));
+        }
+        return;
+    }
+    for (uint32_t g0 = 0; g0 < m; g0 += kWave) {
+        const uint32_t r = g0 + lane();
+        uint32_t s0 = 0, ln = 0, sa = 0;
+        if (r < m) {
+            s0 = S.off[r];
+            ln = S.off[r + 1] - s0;
+            sa = kFront + S.src[r];
+        }
+        const bool lng = ln > kLongRow;
+        if (!lng && ln) {
+            uint8_t* d = a.chars + G0 + s0;
+            if (ln >= 16) {
+                for (uint32_t x = 0; x + 16 < ln; x += 16) {
+                    const uint4 v = lds16(dwa, sa + x);
+                    *reinterpret_cast<U16B*>(d + x) = U16B{v.x, v.y, v.z, v.w};
+                }
+                const uint4 v = lds16(dwa, sa + ln - 16);
+                *reinterpret_cast<U16B*>(d + ln - 16) = U16B{v.x, v.y, v.z, v.w};
+            } else {
+                const uint4 v = lds16(dwa, sa);           // bytes 0 .. 15 of the row's source
+                const uint32_t t = ln >= 8 ? ln - 8 : (ln >= 4 ? ln - 4 : (ln >= 2 ? ln - 2 : 0u));
+                const uint4 u = lds16(dwa, sa + t);       // bytes t .. t + 15
+                if (ln >= 8) {
+                    *reinterpret_cast<U8B*>(d) = U8B{v.x, v.y};
+                    *reinterpret_cast<U8B*>(d + t) = U8B{u.x, u.y};
+                } else if (ln >= 4) {
+                    *reinterpret_cast<U4B*>(d) = U4B{v.x};
+                    *reinterpret_cast<U4B*>(d + t) = U4B{u.x};
+                } else if (ln >= 2) {
+                    *reinterpret_cast<U2B*>(d) = U2B{static_cast<uint16_t>(v.x)};
+                    *reinterpret_cast<U2B*>(d + t) = U2B{static_cast<uint16_t>(u.x)};
+                } else {
+                    d[0] = static_cast<uint8_t>(v.x);
+                }
+            }
+        }
+        uint64_t lm = __ballot(lng);
+        while (lm) {  // long rows: the whole wave, aligned destination blocks
+            const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
+            lm &= lm - 1;
+            const int64_t A0 = G0 + __builtin_amdgcn_readlane(s0, l);
+            const int64_t A1 = A0 + __builtin_amdgcn_readlane(ln, l);
+            const uint32_t src0 = __builtin_amdgcn_readlane(sa, l);
+            const int64_t b0 = A0 & ~static_cast<int64_t>(15);
+            for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < A1; blk += 16 * kWave) {
+                const uint4 v = lds16(dwa, static_cast<uint32_t>(src0 + (blk - A0)));
+                store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, A0) - blk),
+                           static_cast<uint32_t>(min(blk + 16, A1) - blk));
+            }
+        }
+    }
+    (void)G1;
+}
+
 template <bool kArmed>
 __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1151,163 +1318,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
                 for (int k = 0; k < kRowsPerLane; k++)
                     cur[k] = l8 + k < m ? (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : kNull;
             }
-            // this lane's rows 8l .. 8l + 7: lengths, dictionary offsets, validity
-            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0, sat = 0;
-#pragma unroll
-            for (int k = 0; k < kRowsPerLane; k++) {
-                const bool valid = cur[k] < dict_n;
-                const uint32_t e = valid ? dtab[cur[k]] : 0u;
-                len[k] = armed ? ((e >> 16) & 0x7FFFu) : (e >> 16);
-                if (armed) sat |= e;
-                src[k] = e & 0xFFFFu;
-                vb |= (valid ? 1u : 0u) << k;
-                acc += len[k];
-            }
-            if (armed && __ballot(sat >> 31) && lane() == 0)  // the page filter: a row whose entry satisfies it
-                a.page_flags[__builtin_amdgcn_readlane(myp, i)] = 0;
-            const uint32_t incl = wave_incl_scan(acc);
-            const uint32_t total = bcast_last(incl);
-            {
-                // the lane's eight rows as two 16-byte stores of offsets and one
-                // of sources (row-per-element stores would hit each bank 8 and 4
-                // times); rows past m get the tile end and are never read as rows
-                static_assert(kRowsPerLane == 8, "row layout");
-                uint32_t o[kRowsPerLane];
-                o[0] = incl - acc;
-#pragma unroll
-                for (int k = 1; k < kRowsPerLane; k++) o[k] = o[k - 1] + len[k - 1];
-                uint4* po = reinterpret_cast<uint4*>(&S.off[lane() * kRowsPerLane]);
-                po[0] = make_uint4(o[0], o[1], o[2], o[3]);
-                po[1] = make_uint4(o[4], o[5], o[6], o[7]);
-                *reinterpret_cast<uint4*>(&S.src[lane() * kRowsPerLane]) =
-                    make_uint4(src[0] | (src[1] << 16), src[2] | (src[3] << 16), src[4] | (src[5] << 16),
-                               src[6] | (src[7] << 16));
-            }
-            S.vb[lane()] = static_cast<uint8_t>(vb);
-            if (lane() == 0) S.off[m] = total;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            if (!(a.debug & 4)) {
-                // offsets: rows 2j', 2j' + 1 per lane as one 16-byte store when
-                // the tile starts on an even row (coalesced), else row j = 64k + lane
-                if ((R0 & 1) == 0) {
-#pragma unroll
-                    for (int k = 0; k < kRowsPerLane / 2; k++) {
-                        const uint32_t j = k * 2 * kWave + 2 * lane();
-                        if (j + 1 < m) {
-                            const uint2 o = *reinterpret_cast<const uint2*>(&S.off[j]);
-                            const int64_t v0 = G0 + o.x, v1 = G0 + o.y;
-                            *reinterpret_cast<uint4*>(a.offsets + R0 + j) =
-                                make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(static_cast<uint64_t>(v0) >> 32),
-                                           static_cast<uint32_t>(v1), static_cast<uint32_t>(static_cast<uint64_t>(v1) >> 32));
-                        } else if (j < m) {
-                            a.offsets[R0 + j] = G0 + S.off[j];
-                        }
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < kRowsPerLane; k++) {
-                        const uint32_t j = k * kWave + lane();
-                        if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
-                    }
-                }
-                // validity words [R0 >> 5, (R0 + m - 1) >> 5]: tile word t = vb bytes 4t .. 4t + 3
-                const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
-                const uint32_t sh = static_cast<uint32_t>(R0 & 31);
-                const int64_t g = gfirst + lane();
-                if (g <= glast) {
-                    auto tw = [&](int t) -> uint32_t {
-                        return (t >= 0 && t < kWave / 4) ? reinterpret_cast<const uint32_t*>(S.vb)[t] : 0u;
-                    };
-                    const int t = static_cast<int>(lane());
-                    const uint32_t val = (tw(t) << sh) | (sh ? (tw(t - 1) >> (32 - sh)) : 0u);
-                    // the column's last word belongs to its last tile alone
-                    const bool whole = g * 32 >= R0 && (g * 32 + 32 <= R0 + m || R0 + m == a.nrows_total);
-                    if (whole) a.validity[g] = val;
-                    else if (val) atomicOr(&a.validity[g], val);
-                }
-            }
-            if (R0 + m == a.nrows_total && lane() == 0) {
-                a.offsets[a.nrows_total] = G0 + total;
-                *a.total = G0 + total;
-            }
-            if (total == 0 || (a.debug & 2)) continue;
-            if (G0 + total > a.capacity) {  // output too small: the host grows it and re-runs
-                if (lane() == 0) atomicOr(a.overflow, 1);
-                continue;
-            }
-            // characters, 64 consecutive rows per step: each lane copies its
-            // row from the LDS dictionary to HBM as unaligned 16-byte moves
-            // (the last one overlapping the row's earlier bytes), rows under
-            // 16 bytes as two overlapping 8/4/2-byte moves, so no store leaves
-            // its row and the L2 merges the partial lines.  Rows longer than
-            // kLongRow are copied afterwards by the whole wave, 16-byte
-            // aligned blocks across the lanes.  (Assembling aligned blocks in
-            // LDS first costs more than it saves: byte-unaligned LDS accesses
-            // are slow; scripts/probe/unaligned_store.hip)
-            const int64_t G1 = G0 + total;
-            if (a.debug & 128) {  // timing only: the tile's bytes as aligned 16-byte blocks of zeros
-                const int64_t b0 = G0 & ~static_cast<int64_t>(15);
-                for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < G1; blk += 16 * kWave) {
-                    const uint4 v = make_uint4(0u, 0u, 0u, 0u);
-                    if (blk >= G0 && blk + 16 <= G1) *reinterpret_cast<uint4*>(a.chars + blk) = v;
-                    else store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, G0) - blk),
-                                    static_cast<uint32_t>(min(blk + 16, G1) - blk));
-                }
-                continue;
-            }
-            for (uint32_t g0 = 0; g0 < m; g0 += kWave) {
-                const uint32_t r = g0 + lane();
-                uint32_t s0 = 0, ln = 0, sa = 0;
-                if (r < m) {
-                    s0 = S.off[r];
-                    ln = S.off[r + 1] - s0;
-                    sa = kFront + S.src[r];
-                }
-                const bool lng = ln > kLongRow;
-                if (!lng && ln) {
-                    uint8_t* d = a.chars + G0 + s0;
-                    if (ln >= 16) {
-                        for (uint32_t x = 0; x + 16 < ln; x += 16) {
-                            const uint4 v = lds16(dwa, sa + x);
-                            *reinterpret_cast<U16B*>(d + x) = U16B{v.x, v.y, v.z, v.w};
-                        }
-                        const uint4 v = lds16(dwa, sa + ln - 16);
-                        *reinterpret_cast<U16B*>(d + ln - 16) = U16B{v.x, v.y, v.z, v.w};
-                    } else {
-                        const uint4 v = lds16(dwa, sa);           // bytes 0 .. 15 of the row's source
-                        const uint32_t t = ln >= 8 ? ln - 8 : (ln >= 4 ? ln - 4 : (ln >= 2 ? ln - 2 : 0u));
-                        const uint4 u = lds16(dwa, sa + t);       // bytes t .. t + 15
-                        if (ln >= 8) {
-                            *reinterpret_cast<U8B*>(d) = U8B{v.x, v.y};
-                            *reinterpret_cast<U8B*>(d + t) = U8B{u.x, u.y};
-                        } else if (ln >= 4) {
-                            *reinterpret_cast<U4B*>(d) = U4B{v.x};
-                            *reinterpret_cast<U4B*>(d + t) = U4B{u.x};
-                        } else if (ln >= 2) {
-                            *reinterpret_cast<U2B*>(d) = U2B{static_cast<uint16_t>(v.x)};
-                            *reinterpret_cast<U2B*>(d + t) = U2B{static_cast<uint16_t>(u.x)};
-                        } else {
-                            d[0] = static_cast<uint8_t>(v.x);
-                        }
-                    }
-                }
-                uint64_t lm = __ballot(lng);
-                while (lm) {  // long rows: the whole wave, aligned destination blocks
-                    const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
-                    lm &= lm - 1;
-                    const int64_t A0 = G0 + __builtin_amdgcn_readlane(s0, l);
-                    const int64_t A1 = A0 + __builtin_amdgcn_readlane(ln, l);
-                    const uint32_t src0 = __builtin_amdgcn_readlane(sa, l);
-                    const int64_t b0 = A0 & ~static_cast<int64_t>(15);
-                    for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < A1; blk += 16 * kWave) {
-                        const uint4 v = lds16(dwa, static_cast<uint32_t>(src0 + (blk - A0)));
-                        store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, A0) - blk),
-                                   static_cast<uint32_t>(min(blk + 16, A1) - blk));
-                    }
-                }
-            }
-            (void)G1;
+            write_tile<kArmed>(a, S, dwa, dtab, dict_n, R0, G0, m, __builtin_amdgcn_readlane(myp, i), cur);
         }
         }
     }

@@ -308,7 +308,8 @@ struct DevBatch {
     int32_t p0, np;
     uint64_t img_lo;
     uint32_t img_bytes;
-    uint32_t pad;
+    uint32_t nrows;  // the pages' values (windows of the regex scan; else 0)
+    int64_t row0;    // first row of page p0 (windows of the regex scan)
 };
 
 

@@ -493,7 +493,12 @@ __device__ __forceinline__ uint32_t st_u32(const uint32_t* st, uint32_t a) {
     return __builtin_amdgcn_alignbyte(st[i + 1], st[i], sh);
 }
 
-template <bool kPre>
+
+
+// kSink (anchored patterns, full tables): a batch stops after its first block
+// once every longer string sits in an absorbing state (DEAD); a template
+// parameter, as the test costs unanchored patterns more than it saves
+template <bool kPre, bool kSink = false>
 __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
                                                                   uint32_t dfa_bytes, uint32_t win_bytes,
                                                                   const uint8_t* __restrict__ bytes,
@@ -589,11 +594,23 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
     copy_blocks(reinterpret_cast<uint4*>(cur), reinterpret_cast<const uint4*>(bytes + B.img_lo), B.img_bytes / 16,
                 lane(), kWave);
     if (lane() < 2) reinterpret_cast<uint4*>(cur + B.img_bytes)[lane()] = make_uint4(0, 0, 0, 0);
-    // a warm scan: the next window's string-index entries (<= 256 strings),
-    // loaded into registers one window ahead (entry k in lane k % 64, half
-    // k / 128 of word (k / 64) % 2)
-    bool ix_held = false;
+    // a warm scan: a window's string-index entries (<= 256 strings, rows
+    // b.row0 .. b.row0 + b.nrows - 1), loaded into registers one window
+    // ahead (entry k in lane k % 64, half k / 128 of word (k / 64) % 2)
+    auto ix_load = [&](const pqk::DevBatch& b, uint32_t& v01, uint32_t& v23) -> bool {
+        const uint32_t tot = b.nrows;
+        if (!index_in || tot == 0 || tot > 4 * kWave) return false;
+        auto at = [&](uint32_t j) -> uint32_t {  // (clamped indices: unconditional loads)
+            const uint32_t k = j * kWave + lane();
+            return index_in[b.row0 + (k < tot ? k : 0u)];
+        };
+        const uint32_t a0 = at(0), a1 = at(1), a2 = at(2), a3 = at(3);
+        v01 = a0 | (a1 << 16);
+        v23 = a2 | (a3 << 16);
+        return true;
+    };
     uint32_t ix01 = 0, ix23 = 0;
+    bool ix_held = ix_load(B, ix01, ix23);
     bool pf_on = false;  // the previous window's page flag (one lane per page)
     int32_t pf_at = 0;
     uint8_t pf_v = 0;
@@ -602,11 +619,28 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
         const DevPage pgc = pg;
         const int32_t wn = w + nwt;
         if (pf_on) page_flags[pf_at] = pf_v;
+        // every load for the next window at once, before this window's work:
+        // its page descriptors, the batch after it, its bytes (registers, up
+        // to kPrefetchBlocks KiB) and a warm scan's index entries; the one
+        // wait at the end of the iteration covers them all (no load of the
+        // loop depends on another load of the same iteration)
         DevPage pgn{};
         pqk::DevBatch Bnn{};
+        uint32_t ixn01 = 0, ixn23 = 0;
+        bool ixn_held = false;
+        held = false;
         if (wn < nwins) {
             if (lane() < static_cast<uint32_t>(Bn.np)) pgn = pages[Bn.p0 + static_cast<int32_t>(lane())];
             if (wn + nwt < nwins) Bnn = wins[wn + nwt];
+            held = kPre && Bn.img_bytes <= kPrefetchBlocks * kWave * 16;
+            if (held) {  // (clamped indices: unconditional loads, no branch around them)
+                const uint4* src = reinterpret_cast<const uint4*>(bytes + Bn.img_lo);
+                const uint32_t nb = Bn.img_bytes / 16, b = lane();
+                auto at = [&](uint32_t k) { return src[b + k * kWave < nb ? b + k * kWave : 0u]; };
+                R0 = at(0); R1 = at(1); R2 = at(2); R3 = at(3);
+                R4 = at(4); R5 = at(5); R6 = at(6); R7 = at(7);
+            }
+            ixn_held = ix_load(Bn, ixn01, ixn23);
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -631,37 +665,17 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
             const int64_t fr = pl ? pgc.first_row : fr0;
             cnt = pl ? static_cast<uint32_t>(max(pgc.nvals, 0)) : 0u;
             lb = static_cast<uint32_t>(fr - fr0);
-            const uint32_t tot = bcast_last(wave_incl_scan(cnt));
-            if (ix_held && tot <= 4 * kWave) {
+            const uint32_t tot = Bc.nrows;  // (= the pages' values; rows from Bc.row0 = fr0)
+            if (ix_held) {
                 const uint32_t v[4] = {ix01 & 0xFFFFu, ix01 >> 16, ix23 & 0xFFFFu, ix23 >> 16};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; j++)
                     if (j * kWave + lane() < tot) list[j * kWave + lane()] = static_cast<uint16_t>(v[j]);
             } else {
-                for (uint32_t k = lane(); k < tot; k += kWave) list[k] = index_in[fr0 + k];
+                for (uint32_t k = lane(); k < tot; k += kWave) list[k] = index_in[Bc.row0 + k];
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // the next window's entries, while this one is scanned (its page
-            // descriptors arrived with this window's entries)
-            ix_held = false;
-            if (wn < nwins) {
-                const bool pln = lane() < static_cast<uint32_t>(Bn.np);
-                const uint32_t totn = bcast_last(wave_incl_scan(pln ? static_cast<uint32_t>(max(pgn.nvals, 0)) : 0u));
-                const int64_t fr0n = static_cast<int64_t>(
-                    static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(pgn.first_row), 0))) |
-                    (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(pgn.first_row >> 32), 0))) << 32));
-                if (totn > 0 && totn <= 4 * kWave) {  // (clamped indices: unconditional loads)
-                    auto at = [&](uint32_t j) -> uint32_t {
-                        const uint32_t k = j * kWave + lane();
-                        return index_in[fr0n + (k < totn ? k : 0u)];
-                    };
-                    const uint32_t a0 = at(0), a1 = at(1), a2 = at(2), a3 = at(3);
-                    ix01 = a0 | (a1 << 16);
-                    ix23 = a2 | (a3 << 16);
-                    ix_held = totn > 0;
-                }
-            }
         } else {
             // ── strings: L lanes per page ───────────────────────────────────
             const uint32_t lg = np <= 1 ? 0u : 32u - __builtin_clz(np - 1);  // ceil log2
@@ -859,16 +873,6 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
                 }
             }
         }
-        // the next window's bytes: issued now, stored at the end of this
-        // iteration (after the DFA pass, which reads only LDS)
-        held = kPre && wn < nwins && Bn.img_bytes <= kPrefetchBlocks * kWave * 16;
-        if (held) {  // (clamped indices: unconditional loads, no branch around them)
-            const uint4* src = reinterpret_cast<const uint4*>(bytes + Bn.img_lo);
-            const uint32_t nb = Bn.img_bytes / 16, b = lane();
-            auto at = [&](uint32_t k) { return src[b + k * kWave < nb ? b + k * kWave : 0u]; };
-            R0 = at(0); R1 = at(1); R2 = at(2); R3 = at(3);
-            R4 = at(4); R5 = at(5); R6 = at(6); R7 = at(7);
-        }
         // the window's first row: with the index being filed (REQUIRED chunk,
         // pages of consecutive rows), string g of the window is row fr0 + g and
         // its entry is stored below, coalesced, where the DFA pass reads it
@@ -883,6 +887,7 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
         lbase[lane()] = lb;
         const uint32_t wtotal = bcast_last(pinc);
         __builtin_amdgcn_wave_barrier();
+        const uint64_t sinks = kSink && full ? (static_cast<uint64_t>(D->sink_hi) << 32) | D->sink_lo : 0ull;
         for (uint32_t g0 = 0; g0 < ((dbg & 1) ? 0u : wtotal); g0 += kStrPerLane * kWave) {
             uint32_t e2[kStrPerLane], off2[kStrPerLane], len2[kStrPerLane], pg2[kStrPerLane];
             bool ok2[kStrPerLane];
@@ -908,6 +913,15 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
 #pragma unroll
             for (uint32_t h = 0; h < kStrPerLane; h++) maxl = max(maxl, len2[h]);
             for (uint32_t b0 = 0; __ballot(maxl > b0); b0 += 16) {
+                // after the first block: stop when every longer string sits in
+                // an absorbing state (an anchored pattern's DEAD); one test per
+                // batch, as a test per block costs more than it saves
+                if (kSink && b0 == 16) {
+                    bool live = false;
+#pragma unroll
+                    for (uint32_t h = 0; h < kStrPerLane; h++) live |= len2[h] > 16 && !((sinks >> (e2[h] & 63u)) & 1u);
+                    if (!__ballot(live)) break;
+                }
                 uint32_t Aw[kStrPerLane][4], rem[kStrPerLane];
 #pragma unroll
                 for (uint32_t h = 0; h < kStrPerLane; h++) {
@@ -982,6 +996,9 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
         Bn = Bnn;
         pg = pgn;
         w = wn;
+        ix01 = ixn01;
+        ix23 = ixn23;
+        ix_held = ixn_held;
     }
     if (pf_on) page_flags[pf_at] = pf_v;
 }
@@ -1044,11 +1061,20 @@ uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes, bool pre) {
 void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
                         const uint8_t* bytes, const DevPage* pages, const pqk::DevBatch* wins, int nwins,
                         int32_t* ticket, int grid, ColumnParams cp, int neg, uint8_t* page_flags,
-                        DevErr* page_err, int32_t* err_any, const uint16_t* index_in, uint16_t* index_out, bool pre) {
+                        DevErr* page_err, int32_t* err_any, const uint16_t* index_in, uint16_t* index_out, bool pre,
+                        bool sink) {
     if (nwins <= 0) return;
-    const void* k = pre ? reinterpret_cast<const void*>(k_regex_plain<true>) : reinterpret_cast<const void*>(k_regex_plain<false>);
+    const void* k = pre ? (sink ? reinterpret_cast<const void*>(k_regex_plain<true, true>)
+                                : reinterpret_cast<const void*>(k_regex_plain<true>))
+                        : reinterpret_cast<const void*>(k_regex_plain<false>);
     pqk::ensure_dyn_lds(k, 160 * 1024);
-    if (pre)
+    if (pre && sink) {
+        void (*fn)(const uint8_t*, uint32_t, uint32_t, const uint8_t*, const DevPage*, const pqk::DevBatch*, int, int32_t*,
+                   ColumnParams, int, uint8_t*, DevErr*, int32_t*, const uint16_t*, uint16_t*) = k_regex_plain<true, true>;
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes, true) * kWave),
+                           regex_plain_lds(dfa_bytes, win_bytes, true), s, dfa, dfa_bytes, win_bytes, bytes, pages, wins,
+                           nwins, ticket, cp, neg, page_flags, page_err, err_any, index_in, index_out);
+    } else if (pre)
         hipLaunchKernelGGL(k_regex_plain<true>, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes, true) * kWave),
                            regex_plain_lds(dfa_bytes, win_bytes, true), s, dfa, dfa_bytes, win_bytes, bytes, pages, wins,
                            nwins, ticket, cp, neg, page_flags, page_err, err_any, index_in, index_out);
@@ -1065,7 +1091,8 @@ void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, u
 bool regex_plain_lds_ok() {
     static const bool ok = [] {
         hipFuncAttributes a{};
-        for (const void* k : {reinterpret_cast<const void*>(k_regex_plain<true>), reinterpret_cast<const void*>(k_regex_plain<false>)})
+        for (const void* k : {reinterpret_cast<const void*>(k_regex_plain<true>), reinterpret_cast<const void*>(k_regex_plain<false>),
+                              reinterpret_cast<const void*>(k_regex_plain<true, true>)})
             if (hipFuncGetAttributes(&a, k) != hipSuccess || a.sharedSizeBytes != 0) return false;
         return true;
     }();

@@ -66,8 +66,12 @@ struct DevDfa {
                                 // offset (rows kDfaRowBytes apart); column 256 of a row:
                                 // the state accepts at the string end
     uint32_t pad[2];
+    uint32_t sink_lo, sink_hi;  // full tables: absorbing states (every byte stays), bit = state
+    uint32_t req;               // a byte every match contains (bits 0..7), bit 8: set (prefilter)
+    uint32_t anchored;          // matches start at byte 0 only (the DFA dies early on most strings)
     uint8_t cls_of[256];        // byte -> class
 };
+static_assert(sizeof(DevDfa) % 16 == 0, "table alignment");
 enum : uint32_t { DFA_DEAD = 0, DFA_ACCEPT = 1, DFA_START = 2 };
 
 // Builds the DFA image; false if it would exceed kDfaMaxBytes (the NFA
@@ -86,7 +90,8 @@ void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, u
                         const uint8_t* bytes, const pqk::DevPage* pages, const pqk::DevBatch* wins, int nwins,
                         int32_t* ticket, int grid, pqk::ColumnParams cp, int neg, uint8_t* page_flags,
                         pqk::DevErr* page_err, int32_t* err_any,
-                        const uint16_t* index_in = nullptr, uint16_t* index_out = nullptr, bool pre = true);
+                        const uint16_t* index_in = nullptr, uint16_t* index_out = nullptr, bool pre = true,
+                        bool sink = false);
 
 void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, const uint8_t* bytes,
                         const pqk::DevPage* pages, int npages, const pqk::DevDict* dicts,

@@ -4,7 +4,9 @@ no chain walk, staging only, exact (serial) walk for every page; per window size
 under the ablation.  usage: regex_ablate.py [win_bytes ...]"""
 import json
 import sys
-sys.path[:0] = ["/root/repo", "/root/repo/duckdb-parquet-parser_amd"]
+import os
+# AB_PKG: a directory holding another build's pqgpu package
+sys.path[:0] = ["/root/repo", os.environ.get("AB_PKG") or "/root/repo/duckdb-parquet-parser_amd"]
 from pqgpu import capi, gen  # noqa: E402
 ctx = capi.Context(0)
 f = gen.build(gen.c3_cols(), 10_000_000, 1, seed=gen.CONFIG_SEEDS["C3"])
@@ -12,7 +14,7 @@ F = capi.File(f)
 for win in [int(a) for a in sys.argv[1:]] or [8192]:
     ctx.set_option("regex_win", win)
     dc = ctx.upload(f, [F.chunk(0, 0)])
-    for dbg in (0, 1, 2, 3, 4):
+    for dbg in [int(x) for x in os.environ.get("RX_DBG", "0,1,2,3,4").split(",")]:
         ctx.set_option("regex_debug", dbg)
         for _ in range(3):
             dc.regex_pages_async("special.*requests", False)
