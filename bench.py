@@ -49,7 +49,7 @@ for _p in (ROOT, PKG):
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel timers (HIP events on the decode stream, capi.hip Timed)
-KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "wide_chars", "pipe_count", "pipe_codes", "pipe_write", "pipe_fused",
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "wide_chars", "pipe_count", "pipe_codes", "pipe_write",
            "ba_fused", "ba_rows", "scan", "ba_gather", "plain_spec", "plain_ba", "fixed_plain", "fixed", "plain_opt")
 REGEX_KERNELS = ("regex_dict", "regex_codes", "regex_lanes", "regex_plain", "regex_pages")
 ROWS = 10_000_000
@@ -90,7 +90,7 @@ def parse():
                     help="gloo: rehearse N ranks on fewer GPUs (control path only; the data path has no collective)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     ap.add_argument("--opt", action="append", default=[],
-                    help="context option key=value set before any upload (repeatable), e.g. pipe_fused=1")
+                    help="context option key=value set before any upload (repeatable), e.g. write_waves=8")
     return ap.parse_args()
 
 
@@ -486,7 +486,7 @@ def api_read_all_leg(f: bytes, want):
         path, dump = os.path.join(td, "c2.parquet"), os.path.join(td, "c2.dump")
         with open(path, "wb") as fh:
             fh.write(f)
-        r = subprocess.run([tool, path, "time_read_all", "0", "0", "3", dump], stdout=subprocess.PIPE,
+        r = subprocess.run([tool, path, "time_read_all", "0", "0", "5", dump], stdout=subprocess.PIPE,
                            stderr=subprocess.PIPE, timeout=600)
         if r.returncode != 0:
             return {"error": r.stderr.decode(errors="replace")[-500:]}
@@ -497,6 +497,7 @@ def api_read_all_leg(f: bytes, want):
     return {"values_per_s": n / (js["read_all_ms"] * 1e-3), "read_all_ms": js["read_all_ms"],
             "read_columnar_ms": js["read_columnar_ms"], "to_values_ms": js["to_values_ms"],
             "to_values_per_s": n / (js["to_values_ms"] * 1e-3), "threads": js["threads"], "values": n,
+            "read_all_samples_ms": js.get("read_all_samples"), "to_values_samples_ms": js.get("to_values_samples"),
             "validated": (got == want) if want else None,
             "note": "ColumnReader::read_all from host file bytes to std::vector<Value>; compare cpu_baseline."
                     "chunk_parallel (the reference's read_all, one thread per chunk) and single_thread"}
@@ -1040,7 +1041,7 @@ def main():
     # algorithmic bytes of one launch of the dominant kernel:
     # pipe_write produces the decoded column (offsets, chars, validity); the
     # u16 codes it reads are this design's intermediate, not algorithmic bytes
-    dom_bytes = {"pipe_write": out_bytes, "pipe_codes": payload, "pipe_fused": b_alg,
+    dom_bytes = {"pipe_write": out_bytes, "pipe_codes": payload,
                  "ba_fused": b_alg}.get(dom, payload)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(args.pmc_json, dom)

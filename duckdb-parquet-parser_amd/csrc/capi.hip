@@ -111,7 +111,6 @@ struct pq_ctx {
     int opt_regex_index = 1;     // "regex_index": REQUIRED PLAIN chunks keep the string index of their first scan;
                                  // 2: every scan is a first scan (files the index again: the cold-scan timing)
     int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
-    int opt_regex_pre = 1;       // "regex_prefetch": the next window's bytes in registers (1), or not (0: four waves per SIMD)
     int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)
     bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
     bool opt_fixed_fused = false; // "fixed_fused": OPTIONAL ones scatter their values in the levels launch (slower: DESIGN §5)
@@ -123,14 +122,6 @@ struct pq_ctx {
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
     bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
-    bool opt_front = false;      // "pipe_front": windowed one-wave front (k_pipe_win) where the pages allow it
-    int opt_win_pages = 8;       // "win_pages": pages per k_pipe_win window (1..16), set before upload
-    int opt_win_bytes = 4096;    // "win_bytes": slot bytes per k_pipe_win window (1024..16384), set before upload
-    int opt_win_rc = 96;         // "win_rc": run records per stream in k_pipe_win (2..255)
-    bool opt_win_dict = false;
-    bool opt_write_self = false; // "write_self": k_pipe_write sums its tiles itself after every front (A/B; always after k_pipe_win)   // "win_dict": the dictionary decodes in k_pipe_win's leading workgroups (else side stream)
-    bool opt_pfused = false;     // "pipe_fused": codes + write in one pass (k_pipe_fused), planned at upload
-    int opt_fused_waves = 8;     // "pipe_fused_waves": k_pipe_fused waves per workgroup (1..16), set before upload
     int opt_write_bpc = 0;       // "write_bpc": cap on k_pipe_write workgroups per CU (0: as many as fit; set before upload)
     int opt_stage_bufs = 6;      // "stage_bufs" / "stage_piece_kb": pinned upload ring (stage.hpp)
 };
@@ -203,22 +194,13 @@ struct pq_chunk {
     bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
     uint32_t pipe_small_bytes = 0;      // the largest payload of those pages
     bool pipe_wide = false;             // 32-bit codes, dictionary in HBM (k_pipe_big<true> -> k_pipe_wwide)
-    bool pipe_fr = false;               // every page <= kTileRows rows, flat levels, every slot <= a window: k_pipe_win
-    std::vector<pqk::DevBatch> hfwins;  // its windows of consecutive pages
-    uint32_t win_bytes = 0, win_pages = 0;  // the largest window's slot bytes, pages per window (planned)
-    pqk::DevBatch* d_fwins = nullptr;
     int pipe_wpw = 10;                  // k_pipe_write writer waves per workgroup (planned)
     std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
     int32_t* d_bigp = nullptr;
     uint32_t big_max_bytes = 0;
     int32_t pipe_entry_base = 0;        // entry-table slot of the pipe dictionary's first entry
-    // k_pipe_fused, planned at upload when the context asks for it
-    bool fused_ok = false;
-    uint32_t fstage = 0, flds = 0;
-    int fgrid = 0, fwaves = 0;
-    int32_t nunits = 0;
-    size_t z_bsum = 0, z_fused = 0, z_flist = 0;  // offsets in a zero block: bsum, fused ticket + look-back words, flist
-    uint8_t* d_zero = nullptr;          // pipe chunks: two blocks of [flags][bsum][fused][flist], alternating per decode
+    size_t z_bsum = 0, z_flist = 0;  // offsets in a zero block: bsum, flist
+    uint8_t* d_zero = nullptr;          // pipe chunks: two blocks of [flags][bsum][flist], alternating per decode
     size_t zfull = 0;                   // bytes per block
     int zsel = 0;                       // block of the current decode
     bool next_zeroed = false;           // the other block is clear (the last k_pipe_write cleared it)
@@ -290,7 +272,6 @@ struct pq_chunk {
     uint32_t rwin_bytes = 0, rwin_for_dfa = 0;
     int rwin_grid = 0;
     int rwin_opt = 0;                   // regex_win the windows were planned with
-    int rwin_pre = -1;                  // and regex_prefetch
     uint32_t dfa_bytes = 0;
     bool dfa_full = false;               // the DFA image has full 256-column rows
     bool dfa_sink = false;               // full rows of an anchored pattern (k_regex_plain<.., true>)
@@ -467,7 +448,6 @@ void free_chunk_device(pq_chunk* c) {
     dfree(c->d_bsum);
     dfree(c->d_flist);
     dfree(c->d_bigp);
-    dfree(c->d_fwins);
     dfree(c->d_chunk_base);
     dfree(c->d_chunks);
     dfree(c->d_cand);
@@ -534,8 +514,6 @@ static void plan_pipe_wide(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages,
     c->pipe_ecap = static_cast<uint32_t>(std::min<int64_t>(d.nvals, d.size / 4 + 1));
     c->pipe_cus = ctx->cus;
     c->pipe_wpw = wpw;
-    c->fused_ok = false;
-    c->pipe_fr = false;
 }
 
 void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::vector<DevDict>& dicts) {
@@ -543,8 +521,6 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     c->pipe_wide = false;
     c->pipe_count = false;
     c->pipe_small = false;
-    c->pipe_fr = false;
-    c->hfwins.clear();
     c->hbig.clear();
     c->big_max_bytes = 0;
     if (c->type != PQ_BYTE_ARRAY || c->max_def > 254 || c->max_def < 0 || c->max_rep < 0 || pages.empty()) return;
@@ -597,53 +573,6 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     c->pipe_ecap = static_cast<uint32_t>(ecap);
     c->pipe_cus = cus;
     c->pipe_wpw = wpw;
-    c->fused_ok = false;
-    if (ctx->opt_pfused) {  // codes + write in one pass: the largest small page's slot as the stage
-        const uint32_t stage = std::min<uint32_t>(5120u, (small_bytes + 15) / 16 * 16 + 16);
-        const int fw = std::max(1, std::min(16, ctx->opt_fused_waves));
-        const pqk::PipePlan fp = pqk::plan_pipe_fused(dict_bytes, fw, stage);
-        if (fp.blocks_per_cu > 0) {
-            c->fused_ok = true;
-            c->fstage = stage;
-            c->flds = fp.lds;
-            c->fgrid = cus * fp.blocks_per_cu;
-            c->fwaves = fw;
-        }
-    }
-    // windows of consecutive pages for the whole front in one wavefront each
-    // (k_pipe_win): one-tile pages, flat levels (max_def <= 1, no rep levels)
-    c->hfwins.clear();
-    c->win_bytes = 0;
-    c->win_pages = static_cast<uint32_t>(std::max(1, std::min(16, ctx->opt_win_pages)));
-    const uint32_t wcap = static_cast<uint32_t>(ctx->opt_win_bytes);
-    c->pipe_fr = small && !multi && c->hbig.empty() && c->max_def <= 1 && c->max_rep == 0 &&
-                 pqk::pipe_win_slot(small_bytes) <= wcap;
-    if (c->pipe_fr) {
-        size_t p = 0;
-        while (p < pages.size()) {
-            pqk::DevBatch b{};
-            b.p0 = static_cast<int32_t>(p);
-            b.img_lo = pages[p].off;
-            uint64_t hi = b.img_lo;
-            size_t q = p;
-            while (q < pages.size() && q - p < c->win_pages && pages[q].off >= b.img_lo) {
-                const uint64_t e = pages[q].off + pqk::pipe_win_slot(static_cast<uint32_t>(std::max(pages[q].size, 0)));
-                if (e - b.img_lo > wcap || (q > p && pages[q].off != hi)) break;  // contiguous slots only
-                hi = e;
-                q++;
-            }
-            if (q == p) {  // (slots are contiguous and <= wcap: unreachable)
-                c->pipe_fr = false;
-                c->hfwins.clear();
-                break;
-            }
-            b.np = static_cast<int32_t>(q - p);
-            b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
-            c->win_bytes = std::max(c->win_bytes, b.img_bytes);
-            c->hfwins.push_back(b);
-            p = q;
-        }
-    }
 }
 
 // PLAIN BYTE_ARRAY chunks without levels go through plain_ba.hip: windows of
@@ -985,30 +914,6 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "plain_ba") == 0) { ctx->opt_plain = value != 0; return 0; }
     if (std::strcmp(key, "plain_fused") == 0) { ctx->opt_plain_fused = value != 0; return 0; }
     if (std::strcmp(key, "pipe_run_dict") == 0) { ctx->opt_run_dict = value != 0; return 0; }
-    if (std::strcmp(key, "pipe_front") == 0) { ctx->opt_front = value != 0; return 0; }
-    if (std::strcmp(key, "win_dict") == 0) { ctx->opt_win_dict = value != 0; return 0; }
-    if (std::strcmp(key, "write_self") == 0) { ctx->opt_write_self = value != 0; return 0; }
-    if (std::strcmp(key, "win_pages") == 0) {
-        if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "win_pages: 1..16");
-        ctx->opt_win_pages = static_cast<int>(value);
-        return 0;
-    }
-    if (std::strcmp(key, "win_bytes") == 0) {
-        if (value < 1024 || value > 16384 || value % 16) return set_err(ctx, PQ_ERR_ARG, "win_bytes: 1024..16384, a multiple of 16");
-        ctx->opt_win_bytes = static_cast<int>(value);
-        return 0;
-    }
-    if (std::strcmp(key, "win_rc") == 0) {
-        if (value < 2 || value > 255) return set_err(ctx, PQ_ERR_ARG, "win_rc: 2..255");
-        ctx->opt_win_rc = static_cast<int>(value);
-        return 0;
-    }
-    if (std::strcmp(key, "pipe_fused") == 0) { ctx->opt_pfused = value != 0; return 0; }
-    if (std::strcmp(key, "pipe_fused_waves") == 0) {
-        if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "pipe_fused_waves: 1..16");
-        ctx->opt_fused_waves = static_cast<int>(value);
-        return 0;
-    }
     if (std::strcmp(key, "write_bpc") == 0) {
         if (value < 0 || value > 4) return set_err(ctx, PQ_ERR_ARG, "write_bpc: 0..4");
         ctx->opt_write_bpc = static_cast<int>(value);
@@ -1034,10 +939,6 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "stage_piece_kb") == 0) {
         if (value < 64 || value > 65536) return set_err(ctx, PQ_ERR_ARG, "stage_piece_kb: 64..65536");
         ctx->stager.configure(ctx->opt_stage_bufs, static_cast<size_t>(value) << 10);
-        return 0;
-    }
-    if (std::strcmp(key, "regex_prefetch") == 0) {
-        ctx->opt_regex_pre = value ? 1 : 0;
         return 0;
     }
     if (std::strcmp(key, "regex_win") == 0) {
@@ -1517,16 +1418,11 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         rc |= dalloc(&c->d_dict_count, hdicts.size());
         rc |= dalloc(&c->d_page_err, hpages.size());
         rc |= dalloc(&c->d_dict_err, hdicts.size());
-        if (c->pipe) {  // flags | bsum | fused ticket + look-back words | flist, cleared together
-            // (bsum: pipe_grid workgroup sums, then the self-summing writer's ticket)
-            const size_t fb = 4 * sizeof(int32_t), bb = (static_cast<size_t>(c->pipe_grid) + 1) * sizeof(unsigned long long);
-            c->nunits = c->fused_ok ? (c->ntiles + pqk::pipe_fused_tiles() - 1) / pqk::pipe_fused_tiles() : 0;
+        if (c->pipe) {  // flags | bsum | flist, cleared together
+            // (bsum: pipe_grid k_pipe_write workgroup sums)
+            const size_t fb = 4 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long);
             c->z_bsum = fb;
-            c->z_fused = (fb + bb + 15) / 16 * 16;
-            // ticket, then per unit its look-back word, then per group of
-            // pipe_fused_super() units their (count, sum) word
-            const size_t nsb = c->fused_ok ? static_cast<size_t>((c->nunits + pqk::pipe_fused_super() - 1) / pqk::pipe_fused_super()) : 0;
-            c->z_flist = c->z_fused + (c->fused_ok ? 16 + (static_cast<size_t>(c->nunits) + nsb) * sizeof(unsigned long long) : 0);
+            c->z_flist = (fb + bb + 15) / 16 * 16;
             // cleared per decode (through flist[0]): a multiple of 16 bytes (an
             // odd size takes a second fill kernel for the tail)
             const size_t zb = (c->z_flist + sizeof(int32_t) + 15) / 16 * 16;
@@ -1593,7 +1489,6 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) * (c->pipe_wide ? 2 : 1) + 64);
             rc |= dalloc(&c->d_tile_nn, htiles.size());
             if (!c->hbig.empty()) rc |= dalloc(&c->d_bigp, c->hbig.size());
-            if (!c->hfwins.empty()) rc |= dalloc(&c->d_fwins, c->hfwins.size());
         }
         if (c->plain) {
             rc |= dalloc(&c->d_pwins, c->hpwins.size());
@@ -1851,7 +1746,6 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             if (!rc) (void)hipMemsetAsync(c->d_perr, 0, c->hchunks.size() * sizeof(DevErr), s);
         }
         if (c->d_bigp) put(c->d_bigp, c->hbig.data(), c->hbig.size() * sizeof(int32_t));
-        if (c->d_fwins) put(c->d_fwins, c->hfwins.data(), c->hfwins.size() * sizeof(pqk::DevBatch));
         if (c->d_pwins) put(c->d_pwins, c->hpwins.data(), c->hpwins.size() * sizeof(pqk::DevBatch));
         if (c->d_pwbase) put(c->d_pwbase, c->hpwbase.data(), c->hpwbase.size() * sizeof(int64_t));
         if (c->d_pwpage) put(c->d_pwpage, c->hpwpage.data(), c->hpwpage.size() * sizeof(int32_t));
@@ -2097,34 +1991,14 @@ static void launch_dicts(pq_chunk* c, hipStream_t s, int32_t* err_any) {
                              c->d_dict_err + b.di, err_any, reinterpret_cast<uint32_t*>(c->d_bigd + b.scr_off));
 }
 
-static bool front_path(pq_ctx* ctx, const pq_chunk* c) { return c->pipe_fr && c->d_fwins && ctx->opt_front; }
-
-static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs,
-                       bool fused = false) {
+static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs) {
     hipStream_t s = ctx->stream;
-    if (front_path(ctx, c)) {
-        // k_pipe_win reads no dictionary: it decodes in the leading workgroups
-        // (dict_in_runs), on the side stream (joined here, before the writer),
-        // or was decoded before (regex page filter)
-        {
-            Timed t(ctx, "pipe_front");
-            const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
-            pqk::launch_pipe_win(s, P, c->d_fwins, static_cast<int>(c->hfwins.size()), c->win_bytes, c->win_pages,
-                                 static_cast<uint32_t>(ctx->opt_win_rc), dict_in_runs ? &rd : nullptr, c->max_dict_bytes);
-        }
-        if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
-        if (!P.self_sum) {  // (k_pipe_write sums the tiles itself, else k_pipe_tail files them)
-            Timed t(ctx, "pipe_tail");
-            pqk::launch_pipe_exact(s, P);
-        }
-        return;
-    }
     {
         Timed t(ctx, "pipe_runs");
         const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
         pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, c->pipe_small ? c->npages : 0, c->max_def, c->max_rep,
                               c->d_runs, c->d_info, ctx->opt_run_pages, c->d_flist,  // flist[0], bsum: cleared with d_flags
-                              ctx->opt_debug, dict_in_runs ? &rd : nullptr, fused ? c->fstage - 16 : 0u,
+                              ctx->opt_debug, dict_in_runs ? &rd : nullptr, 0u,
                               (c->pipe_small_bytes + 15) / 16 * 16 + 16, c->max_dict_bytes, ctx->cus);
     }
     // the wide pipe's k_pipe_big writes raw indices and needs no dictionary:
@@ -2143,7 +2017,6 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
         Timed t(ctx, "pipe_count");
         pqk::launch_pipe_codes(s, P, true);
     }
-    if (fused) return;  // k_pipe_fused decodes the codes itself (and runs the exact decoder first)
     Timed t(ctx, "pipe_codes");
     pqk::launch_pipe_codes(s, P, false);
 }
@@ -2173,9 +2046,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     const bool plain_go = c->plain && ctx->opt_plain && !(c->plain_spec && c->spec_failed) &&
                           !(c->plain_opt && (c->popt_failed || !ctx->opt_plain_fused));
     const bool pipe_path = pipe && !plain_go;
-    // k_pipe_fused keeps the codes in registers: no codes for a later scan to reuse
-    const bool fused = pipe_path && ctx->opt_pfused && c->fused_ok && !front_path(ctx, c) && c->d_zero;
-    if (pipe_path && !fused) c->codes_pending = true;
+    if (pipe_path) c->codes_pending = true;
     if (c->ndicts && c->type == PQ_BYTE_ARRAY) c->entries_pending = true;
     if (pipe_path && c->d_zero && ctx->opt_zflip) {
         // flags, bsum and flist[0] of this decode: the other block, which the
@@ -2193,12 +2064,10 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (!(pipe_path && c->tiles_aligned32))
         (void)hipMemsetAsync(out->d_validity, 0, static_cast<size_t>(c->nrows / 32 + 4) * 4, s);
     // dictionary pages small enough for k_pipe_runs' workgroups decode there
-    const bool front = pipe && !plain_go && front_path(ctx, c);
-    // (k_pipe_win: only with "win_dict", else the dictionary decodes on the side stream beside it)
-    const bool dict_in_runs = pipe && !plain_go && ctx->opt_run_dict && (!front || ctx->opt_win_dict) && c->ndicts &&
+    const bool dict_in_runs = pipe && !plain_go && ctx->opt_run_dict && c->ndicts &&
                               c->type == PQ_BYTE_ARRAY && c->d_dflag && c->max_dict_bytes <= pqk::kRunDictMax;
     if (dict_in_runs) {
-        // k_pipe_runs / k_pipe_win decodes the dictionary
+        // k_pipe_runs decodes the dictionary
     } else if (c->ndicts && c->type == PQ_BYTE_ARRAY && pipe) {
         // the dictionary (one workgroup) decodes on the side stream while the
         // run-table pass runs; k_pipe_codes waits for both (ev_join).  The
@@ -2303,11 +2172,7 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         pqk::launch_plain_ba(s, P);
     } else if (pipe) {
         pqk::PipeLaunch P = pipe_launch(ctx, c, out);
-        // (A/B: the writer sums every tile's characters itself instead of
-        // k_pipe_codes3 / k_pipe_tail filing them)
-        P.self_sum = (front || ctx->opt_write_self) && !c->pipe_wide && c->hbig.empty() &&
-                     c->ntiles <= 64 * c->pipe_grid * c->pipe_wpw;
-        pipe_front(ctx, c, P, !dict_in_runs, dict_in_runs, fused);
+        pipe_front(ctx, c, P, !dict_in_runs, dict_in_runs);
         if (c->arm) {  // the page filter in the same pass: match bits per entry, then the writer tests them
             Timed t(ctx, "regex_dict");
             pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
@@ -2320,22 +2185,11 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
             (void)hipMemsetAsync(out->d_offsets, 0, sizeof(int64_t), s);
             (void)hipMemsetAsync(c->d_total, 0, sizeof(int64_t), s);
         }
-        if (c->d_zero) {  // k_pipe_write / k_pipe_fused clears the other block for the next decode
+        if (c->d_zero) {  // k_pipe_write clears the other block for the next decode
             P.znext = reinterpret_cast<uint32_t*>(c->d_zero + static_cast<size_t>(c->zsel ^ 1) * c->zfull);
             P.znext_words = static_cast<uint32_t>(c->zero_bytes / 4);
         }
-        if (fused) {
-            uint8_t* zb = reinterpret_cast<uint8_t*>(c->d_flags);  // this decode's zero block
-            P.fticket = reinterpret_cast<int32_t*>(zb + c->z_fused);
-            P.fstatus = reinterpret_cast<unsigned long long*>(zb + c->z_fused + 16);
-            P.nunits = c->nunits;
-            P.fstage = c->fstage;
-            P.flds = c->flds;
-            P.fgrid = c->fgrid;
-            P.fwaves = c->fwaves;
-            Timed t(ctx, "pipe_fused");
-            pqk::launch_pipe_fused(s, P);
-        } else {
+        {
             Timed t(ctx, "pipe_write");
             pqk::launch_pipe_write(s, P);
         }
@@ -2551,14 +2405,25 @@ int pq_column_copy_out(pq_ctx* ctx, const pq_column* col, uint32_t* validity, ui
     if (!ctx || !col) return PQ_ERR_ARG;
     DevGuard dg(ctx);
     hipStream_t s = ctx->stream;
-    int rc = 0;
-    if (validity && col->num_rows)
-        rc |= hip_check(ctx, hipMemcpyAsync(validity, col->d_validity, static_cast<size_t>((col->num_rows + 31) / 32) * 4, hipMemcpyDeviceToHost, s), "copy validity");
-    if (values && col->num_bytes)
-        rc |= hip_check(ctx, hipMemcpyAsync(values, col->d_values, static_cast<size_t>(col->num_bytes), hipMemcpyDeviceToHost, s), "copy values");
-    if (offsets && col->d_offsets)
-        rc |= hip_check(ctx, hipMemcpyAsync(offsets, col->d_offsets, static_cast<size_t>(col->num_rows + 1) * 8, hipMemcpyDeviceToHost, s), "copy offsets");
-    rc |= hip_check(ctx, hipStreamSynchronize(s), "copy sync");
+    int rc = hip_check(ctx, hipStreamSynchronize(s), "copy sync");  // (the decode that made the column)
+    // large arrays through the pinned ring (DMA of piece i + k while host
+    // threads copy piece i out: pageable destinations would take the
+    // runtime's bounce buffer at a fraction of PCIe bandwidth, one thread)
+    const int hw = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+    auto get = [&](void* dst, const void* src, size_t n, const char* what) {
+        if (!dst || !n || rc) return;
+        if (n < (4u << 20)) {
+            rc |= hip_check(ctx, hipMemcpy(dst, src, n, hipMemcpyDeviceToHost), what);
+            return;
+        }
+        uint8_t* d = static_cast<uint8_t*>(dst);
+        rc |= hip_check(ctx, ctx->stager.download(static_cast<const uint8_t*>(src), n, ctx->copy, hw,
+                                                  [&](const uint8_t* b, size_t a, size_t z) { std::memcpy(d + a, b, z - a); }),
+                        what);
+    };
+    if (col->num_rows) get(validity, col->d_validity, static_cast<size_t>((col->num_rows + 31) / 32) * 4, "copy validity");
+    if (col->num_bytes) get(values, col->d_values, static_cast<size_t>(col->num_bytes), "copy values");
+    if (col->d_offsets) get(offsets, col->d_offsets, static_cast<size_t>(col->num_rows + 1) * 8, "copy offsets");
     return rc ? PQ_ERR_HIP : 0;
 }
 
@@ -2644,17 +2509,14 @@ int pq_regex_compile_check(const char* pattern, char* err, size_t errlen) {
 // k_regex_plain): <= 64 pages and <= win bytes of image each.  False when a
 // page does not fit (the lane-per-page kernel runs then).
 bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
-    const bool pre = ctx->opt_regex_pre != 0;
-    if (c->d_rwins && c->rwin_for_dfa == c->dfa_bytes && c->rwin_opt == ctx->opt_regex_win &&
-        c->rwin_pre == ctx->opt_regex_pre)
-        return true;
+    if (c->d_rwins && c->rwin_for_dfa == c->dfa_bytes && c->rwin_opt == ctx->opt_regex_win) return true;
     const uint32_t maxslot = c->npages ? (c->max_page_bytes + 15) / 16 * 16 + 16 : 0u;
     const uint32_t win = std::max<uint32_t>(static_cast<uint32_t>(ctx->opt_regex_win), maxslot);
     // the kernel lists strings by u16 window offsets (and the string index
     // keeps them): pages whose slot leaves no room take k_regex_lanes
     if (win + 32 > 65535u) return false;
-    if (pqre::regex_plain_waves(c->dfa_bytes, win, pre) == 0) return false;
-    const uint32_t lds = pqre::regex_plain_lds(c->dfa_bytes, win, pre);
+    if (pqre::regex_plain_waves(c->dfa_bytes, win) == 0) return false;
+    const uint32_t lds = pqre::regex_plain_lds(c->dfa_bytes, win);
     if (lds > 160 * 1024) return false;
     c->hrwins.clear();
     // the PLAIN decode's windows are the same kind (<= 64 consecutive page
@@ -2696,8 +2558,7 @@ bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
     c->rwin_bytes = win;
     c->rwin_for_dfa = c->dfa_bytes;
     c->rwin_opt = ctx->opt_regex_win;
-    c->rwin_pre = ctx->opt_regex_pre;
-    const int scan = static_cast<int>(pqre::regex_plain_waves(c->dfa_bytes, win, pre));  // waves per workgroup
+    const int scan = static_cast<int>(pqre::regex_plain_waves(c->dfa_bytes, win));  // waves per workgroup
     c->rwin_grid = std::max(1, std::min<int>(per_cu * cus, static_cast<int>((c->hrwins.size() + scan - 1) / scan)));
     (void)cus;
     return true;
@@ -2808,8 +2669,7 @@ int pq_regex_pages_async(pq_ctx* ctx, pq_chunk* c, const char* pattern, int neg)
             pqre::launch_regex_plain(s, c->d_dfa, c->dfa_bytes, c->rwin_bytes, c->d_bytes, c->d_pages, c->d_rwins,
                                      static_cast<int>(c->hrwins.size()), c->d_rwin_ticket, c->rwin_grid, cp,
                                      (neg ? 1 : 0) | ((ctx->opt_regex_debug & 0xFF) << 8),
-                                     c->d_page_flags, c->d_page_err, c->d_flags, idx_in, idx_out, c->rwin_pre != 0,
-                                     c->dfa_sink);
+                                     c->d_page_flags, c->d_page_err, c->d_flags, idx_in, idx_out, c->dfa_sink);
         } else if (c->d_dfa) {
             Timed t(ctx, "regex_lanes");
             pqre::launch_regex_lanes(s, c->d_dfa, c->dfa_bytes, c->d_bytes, c->d_pages, c->npages, c->d_dicts,

@@ -2,6 +2,7 @@
 #include "pqgpu/reader.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <thread>
@@ -54,9 +55,10 @@ HostColumn decode_chunks(Device& dev, const uint8_t* file, size_t len, const std
     HostColumn h;
     h.type = static_cast<ParquetType>(out.type);
     h.num_rows = out.num_rows;
-    h.validity.assign(static_cast<size_t>((out.num_rows + 31) / 32) + 1, 0);
-    h.values.assign(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)), 0);
-    if (out.type == PQ_BYTE_ARRAY) h.offsets.assign(static_cast<size_t>(out.num_rows + 1), 0);
+    h.validity.resize(static_cast<size_t>((out.num_rows + 31) / 32) + 1);
+    h.validity.back() = 0;  // (the copy fills the others)
+    h.values.resize(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)));
+    if (out.type == PQ_BYTE_ARRAY) h.offsets.resize(static_cast<size_t>(out.num_rows + 1));
     rc = pq_column_copy_out(ctx, &out, h.validity.data(), h.values.data(),
                             h.offsets.empty() ? nullptr : h.offsets.data());
     h.values.resize(static_cast<size_t>(out.num_bytes));
@@ -90,9 +92,10 @@ HostColumn decode_range(Device& dev, const uint8_t* file, size_t len, const pq_c
     HostColumn h;
     h.type = static_cast<ParquetType>(desc.type);
     h.num_rows = out.num_rows;
-    h.validity.assign(static_cast<size_t>((out.num_rows + 31) / 32) + 1, 0);
-    h.values.assign(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)), 0);
-    if (desc.type == PQ_BYTE_ARRAY) h.offsets.assign(static_cast<size_t>(out.num_rows + 1), 0);
+    h.validity.resize(static_cast<size_t>((out.num_rows + 31) / 32) + 1);
+    h.validity.back() = 0;  // (the copy fills the others)
+    h.values.resize(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)));
+    if (desc.type == PQ_BYTE_ARRAY) h.offsets.resize(static_cast<size_t>(out.num_rows + 1));
     rc = pq_column_copy_out(ctx, &out, h.validity.data(), h.values.data(),
                             h.offsets.empty() ? nullptr : h.offsets.data());
     h.values.resize(static_cast<size_t>(out.num_bytes));
@@ -125,9 +128,10 @@ void scan_range(Device& dev, const uint8_t* file, size_t len, const pq_chunk_des
         if ((rc = pq_decode_check(ctx, ch))) fail(rc);
         col->type = static_cast<ParquetType>(desc.type);
         col->num_rows = out.num_rows;
-        col->validity.assign(static_cast<size_t>((out.num_rows + 31) / 32) + 1, 0);
-        col->values.assign(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)), 0);
-        if (desc.type == PQ_BYTE_ARRAY) col->offsets.assign(static_cast<size_t>(out.num_rows + 1), 0);
+        col->validity.resize(static_cast<size_t>((out.num_rows + 31) / 32) + 1);
+        col->validity.back() = 0;  // (the copy fills the others)
+        col->values.resize(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)));
+        if (desc.type == PQ_BYTE_ARRAY) col->offsets.resize(static_cast<size_t>(out.num_rows + 1));
         rc = pq_column_copy_out(ctx, &out, col->validity.data(), col->values.data(),
                                 col->offsets.empty() ? nullptr : col->offsets.data());
         col->values.resize(static_cast<size_t>(out.num_bytes));
@@ -197,10 +201,25 @@ std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned
     a = std::max<int64_t>(a, 0);
     b = std::min<int64_t>(b, h.num_rows);
     const int64_t n = std::max<int64_t>(b - a, 0);
-    std::vector<Value> out(static_cast<size_t>(n));
     unsigned t = threads ? threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // (below ~64k rows a thread costs more than it saves)
     t = static_cast<unsigned>(std::min<int64_t>(t, std::max<int64_t>(1, n / 65536)));
+    // the storage's pages are faulted in by the threads first: the vector's
+    // default construction then runs over mapped memory instead of taking
+    // every page fault on this thread
+    std::vector<Value> out;
+    out.reserve(static_cast<size_t>(n));
+    if (t > 1) {
+        volatile char* raw = reinterpret_cast<volatile char*>(out.data());
+        const size_t bytes = static_cast<size_t>(n) * sizeof(Value);
+        std::vector<std::thread> th;
+        for (unsigned k = 0; k < t; k++)
+            th.emplace_back([=] {
+                for (size_t o = bytes * k / t / 4096 * 4096; o < bytes * (k + 1) / t; o += 4096) raw[o] = 0;
+            });
+        for (auto& x : th) x.join();
+    }
+    out.resize(static_cast<size_t>(n));
     auto part = [&](unsigned k) {
         const int64_t r0 = n * k / t, r1 = n * (k + 1) / t;
         for (int64_t r = r0; r < r1; r++) out[static_cast<size_t>(r)] = h.value(a + r);
@@ -246,12 +265,25 @@ HostColumn ColumnReader::read_columnar() {
     if (meta_->dictionary_page_offset) start = std::min(start, *meta_->dictionary_page_offset);
     size_t cur = static_cast<size_t>(start), end = cur;
     int64_t values_read = 0;
+    // the chunk's extent per its metadata (+ one header window) in one read;
+    // header windows outside it (a chain longer than the metadata says) come
+    // from read_range_ as before, so the image holds the same bytes either way
+    std::vector<uint8_t> big;
+    if (meta_->total_compressed_size > 0)
+        big = read_range_(static_cast<size_t>(start), static_cast<size_t>(meta_->total_compressed_size) + 256);
+    std::vector<uint8_t> hdr;
     while (values_read < meta_->num_values) {
-        std::vector<uint8_t> hdr = read_range_(cur, 256);
-        hdr.resize(256, 0);
+        const uint8_t* win;
+        if (cur - static_cast<size_t>(start) + 256 <= big.size()) {
+            win = big.data() + (cur - static_cast<size_t>(start));
+        } else {
+            hdr = read_range_(cur, 256);
+            hdr.resize(256, 0);
+            win = hdr.data();
+        }
         pqfmt::PageHeader h;
         try {
-            h = pqfmt::read_page_header(hdr.data(), hdr.size(), 0);
+            h = pqfmt::read_page_header(win, 256, 0);
         } catch (const pqfmt::Error&) {
             end = std::max(end, cur + 256);
             break;  // the GPU-side walk reports it at the same place
@@ -264,7 +296,13 @@ HostColumn ColumnReader::read_columnar() {
         else if (h.type == 0 || (h.type == 2 && !h.has_dict)) break;
         cur += static_cast<size_t>(h.compressed);
     }
-    std::vector<uint8_t> image = read_range_(static_cast<size_t>(start), end - static_cast<size_t>(start));
+    std::vector<uint8_t> image;
+    if (end - static_cast<size_t>(start) <= big.size()) {
+        big.resize(end - static_cast<size_t>(start));
+        image = std::move(big);
+    } else {
+        image = read_range_(static_cast<size_t>(start), end - static_cast<size_t>(start));
+    }
     pq_chunk_desc d{};
     d.num_values = meta_->num_values;
     d.data_page_offset = meta_->data_page_offset - start;

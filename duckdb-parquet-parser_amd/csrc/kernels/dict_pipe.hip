@@ -275,10 +275,7 @@ __device__ void fail_page(const CodeArgs& a, const DevPage& pg, int32_t t0, uint
 // over the page in HBM, tile by tile; same error order as k_ba_fused.
 // (always inlined: a call would pass the LDS scratch as a generic pointer and
 // spill CodeArgs to scratch memory)
-// kRaw (k_pipe_win, before the dictionary is decoded): u16 codes hold the raw
-// index (0xFFFF for NULL and for indices that do not fit 16 bits), no tile
-// characters are filed (the self-summing k_pipe_write tests and sums them).
-template <bool kWide = false, bool kRaw = false>
+template <bool kWide = false>
 __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, int p, uint32_t dict_n, uint32_t ebase) {
     using CodeT = typename std::conditional<kWide, uint32_t, uint16_t>::type;
     constexpr CodeT kNullT = kWide ? static_cast<CodeT>(kNull32) : static_cast<CodeT>(kNull);
@@ -355,7 +352,6 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
     // dictionary, which may still be decoding while this runs)
     auto put_ix = [&](uint32_t k, uint32_t v) {
         if constexpr (kWide) ix[k] = v;
-        else if constexpr (kRaw) ix[k] = static_cast<CodeT>(v < 0xFFFFu ? v : static_cast<uint32_t>(kNullT));
         else ix[k] = static_cast<CodeT>(static_cast<int32_t>(v) >= 0 && v < dict_n ? v : static_cast<uint32_t>(kNullT));
     };
     for (uint32_t r0 = 0, ti = 0; r0 < n; r0 += kTileRows, ti++) {
@@ -388,14 +384,14 @@ __device__ __forceinline__ void exact_page_body(const CodeArgs& a, CodeLds& L, i
             CodeT code = kNullT;
             if (nnul) {
                 code = ix[k];
-                if (!kWide && !kRaw && code != kNullT) chars += static_cast<uint32_t>(a.entries[ebase + code] >> 32);
+                if (!kWide && code != kNullT) chars += static_cast<uint32_t>(a.entries[ebase + code] >> 32);
             }
             if (j < m) {
                 if (kWide) a.codes32[pg.first_row + r0 + j] = code;
                 else a.codes[pg.first_row + r0 + j] = static_cast<uint16_t>(code);
             }
         }
-        if (!kWide && !kRaw) {  // (kWide: k_wide_chars sums the tiles' characters)
+        if (!kWide) {  // (kWide: k_wide_chars sums the tiles' characters)
             chars = wave_sum(chars);
             tile_done(a, t0 + static_cast<int>(ti), chars);
         }
@@ -915,8 +911,8 @@ struct WriteArgs {
     const uint64_t* entries;
     const int32_t* dict_count;
     const uint16_t* codes;
-    int64_t* tile_chars;        // (written by the self-summing writer)
-    unsigned long long* bsum;
+    const int64_t* tile_chars;
+    const unsigned long long* bsum;
     int per;
     int64_t nrows_total;
     int64_t* total;
@@ -938,11 +934,6 @@ struct WriteArgs {
     uint8_t* page_flags;
     const uint32_t* codes32 = nullptr;  // wide chunks (k_pipe_wwide)
     const uint4* pad16 = nullptr;       // wide chunks: 16-byte entry slots (k_pipe_wwide<true>), or null
-    // self-summing (after k_pipe_win, which files no characters): every
-    // workgroup sums its own tiles' characters from their codes, publishes its
-    // total in bsum[its ticket] and adds up the totals before it; bsum[gridDim.x]
-    // holds the ticket counter (all zeroed with the decode's flags)
-    int self_sum = 0;
 };
 
 
@@ -1131,12 +1122,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     // descriptors of up to 64 tiles are loaded at once, one per lane, and the
     // next tile's codes are loaded before this tile's stores are issued
     const int per = a.per;
-    __shared__ unsigned long long red[kWriteMax], red2[kWriteMax];
-    __shared__ uint32_t ticket;
-    const bool self = a.self_sum != 0;
-    // (self-summing: the workgroup's place in the character prefix is its
-    // ticket, so every workgroup it waits on below had started before it)
-    if (self && threadIdx.x == 0) ticket = atomicAdd(reinterpret_cast<unsigned int*>(a.bsum + gridDim.x), 1u);
+    __shared__ unsigned long long red[kWriteMax];
     auto wave_sum64 = [](unsigned long long v) {
         for (int d = 1; d < kWave; d <<= 1) {
             const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
@@ -1149,11 +1135,12 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     // summed by k_pipe_codes), then this workgroup's earlier tiles.  Both
     // sums load together with the dictionary (one wait, one barrier).
     unsigned long long acc = 0, in = 0;
-    if (!self) {
-        const int ta0 = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
+    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
+    const int tb = min(a.ntiles, ta + per);
+    {
         for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) acc += a.bsum[b];
         const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
-        for (int q = tfirst + static_cast<int>(lane()); q < ta0; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
+        for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
     }
     {
         const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
@@ -1174,94 +1161,12 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
             });
         }
     }
-    if (!self) {
-        acc = wave_sum64(acc);
-        if (lane() == 0) red[wv] = acc;
-        in = wave_sum64(in);
-    }
+    acc = wave_sum64(acc);
+    if (lane() == 0) red[wv] = acc;
+    in = wave_sum64(in);
     __syncthreads();
-    const uint32_t bid = self ? ticket : blockIdx.x;
-    const int ta = min(a.ntiles, static_cast<int>(bid * a.wpw + wv) * per);
-    const int tb = min(a.ntiles, ta + per);
-    int64_t Grun = 0;
-    uint32_t self_chars = 0;
-    if (!self) {
-        Grun = static_cast<int64_t>(in);
-        for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
-    } else {
-        // 1. this wave's tiles (at most 64: the host plans the self-summing
-        //    writer only then): characters of their valid codes (indices past
-        //    the dictionary are NULL rows), kept in lane j for tile ta + j
-        const uint32_t l8 = lane() * kRowsPerLane;
-        const uint32_t lmask = armed ? 0x7FFFu : 0xFFFFu;
-        unsigned long long wsum = 0;
-        for (int c0 = ta; c0 < tb; c0 += kWave) {
-            const int cn = min(kWave, tb - c0);
-            int64_t myR0 = 0;
-            uint32_t mym = 0;
-            if (static_cast<int>(lane()) < cn) {
-                const DevTile T = a.tiles[c0 + lane()];
-                myR0 = a.pages[T.page].first_row + T.row0;
-                mym = static_cast<uint32_t>(T.nrows);
-            }
-            for (int i0 = 0; i0 < cn; i0 += kWBatch) {
-                uint4 cv[kWBatch];
-#pragma unroll
-                for (int u = 0; u < kWBatch; u++) {
-                    cv[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-                    const int i = i0 + u;
-                    if (i < cn) {
-                        const int64_t R = static_cast<int64_t>(
-                            (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(myR0) >> 32), i)) << 32) |
-                            __builtin_amdgcn_readlane(static_cast<uint32_t>(myR0), i));
-                        const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
-                        if (l8 < mm) {
-                            const U16B x = *reinterpret_cast<const U16B*>(a.codes + R + l8);
-                            cv[u] = make_uint4(x.x, x.y, x.z, x.w);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < kWBatch; u++) {
-                    const int i = i0 + u;
-                    if (i >= cn) break;
-                    const uint32_t ww[4] = {cv[u].x, cv[u].y, cv[u].z, cv[u].w};
-                    const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
-                    uint32_t sum = 0;
-#pragma unroll
-                    for (int k = 0; k < kRowsPerLane; k++) {
-                        const uint32_t c = (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                        const bool valid = l8 + k < mm && c < dict_n;
-                        sum += valid ? (dtab[valid ? c : 0u] >> 16) & lmask : 0u;
-                    }
-                    sum = wave_sum(sum);
-                    if (static_cast<int>(lane()) == c0 - ta + i) self_chars = sum;
-                    wsum += sum;
-                }
-            }
-        }
-        if (lane() == 0) red[wv] = wsum;
-        __syncthreads();
-        // 2. this workgroup's total, published with the ready bit; the
-        //    totals of every workgroup before it (by ticket)
-        constexpr unsigned long long kReady = 1ull << 63;
-        unsigned long long own = 0;
-        for (int w = 0; w < a.wpw; w++) own += red[w];
-        // (flag and value in one word, relaxed agent-scope atomics: no fence,
-        // which on gfx950 would write back the whole L2)
-        if (threadIdx.x == 0) __hip_atomic_store(&a.bsum[bid], own | kReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (uint32_t b = threadIdx.x; b < bid && !(a.debug & (1 << 24)); b += blockDim.x) {  // (bit 24: timing, no wait)
-            unsigned long long v;
-            while (!((v = __hip_atomic_load(&a.bsum[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & kReady))
-                __builtin_amdgcn_s_sleep(1);
-            acc += v & ~kReady;
-        }
-        acc = wave_sum64(acc);
-        if (lane() == 0) red2[wv] = acc;
-        __syncthreads();
-        Grun = 0;
-        for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red2[w]) + (w < static_cast<int>(wv) ? static_cast<int64_t>(red[w]) : 0);
-    }
+    int64_t Grun = static_cast<int64_t>(in);
+    for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
     if (a.debug & 8) return;
     for (int c0 = ta; c0 < tb; c0 += kWave) {
         const int cn = min(kWave, tb - c0);
@@ -1273,7 +1178,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
             myp = static_cast<uint32_t>(T.page);
             myR0 = a.pages[T.page].first_row + T.row0;
             mym = static_cast<uint32_t>(T.nrows);
-            myc = self ? self_chars : static_cast<uint32_t>(a.tile_chars[c0 + lane()]);
+            myc = static_cast<uint32_t>(a.tile_chars[c0 + lane()]);
         }
         {  // tile characters < 2^25 each: a 32-bit scan over <= 64 tiles
             const uint32_t inc = wave_incl_scan(myc);
@@ -2456,950 +2361,6 @@ __global__ void __launch_bounds__(kMatchWaves * 64) k_pipe_match_w(const DevTile
     }
 }
 
-// ── the whole front of windows of one-tile pages (k_pipe_win) ──────────────
-// Chunks whose data pages each hold <= kTileRows rows (the reference writer's
-// 1 KiB pages), max_def <= 1 and no repetition levels (flat OPTIONAL or
-// REQUIRED columns).  One wavefront per window of <= wp consecutive pages
-// whose payload slots form one contiguous image range (host-planned); nothing
-// but the codes leaves the wave's LDS:
-//   1. the window's slots -> LDS (each slot is followed by >= 16 zero bytes);
-//   2. lane 2k walks page k's def-level stream, lane 2k + 1 its dictionary-
-//      index stream (column_reader.cpp:146-182; rle_decoder.hpp:36-95), all
-//      streams of the window in lock step, one run header per step and one
-//      32-bit record per run in LDS: first value | literal << 10 | (RLE value,
-//      or the window bit offset of the literal run's values) << 11.  A stream
-//      that ends before its value count gets the zero run (rle_decoder.hpp:
-//      20-23);
-//   3. per page, all 64 lanes: each def run (one lane per run) ORs its rows'
-//      validity bits into a 512-bit LDS map (RLE runs of 1 as masks, literal
-//      runs as the stream's own bits: the level bit width is 1); non-null ranks
-//      by a wave scan; the index run of each rank by marking run starts and a
-//      max scan; rows 8l .. 8l + 7 per lane -> u16 codes: the raw index, or
-//      0xFFFF for NULL (k_pipe_write tests indices against the dictionary,
-//      column_reader.cpp:190-194, so no page here waits for the dictionary).
-// Pages outside that shape (a bad or zero-count header before the value
-// count, more than rc runs in a stream, a level above max_def, a bit width
-// > 16, a prologue error) are listed for k_pipe_exact, the reference state
-// machine.  The leading workgroups decode the chunk's dictionary page
-// (dict_index.hpp), as k_pipe_runs' do.
-constexpr int kWinWaves = kRunWaves;   // (the dictionary workgroups run dict_index_block<kRunWaves>)
-constexpr uint32_t kWinPagesMax = 16;  // pages per window: <= 32 walking lanes
-constexpr uint32_t kWinRecMax = 255;   // records per stream: u8 run ids in the rank marks
-
-// per-wave LDS: [stage: wbytes + 64][rank marks: kTileRows][validity map: 64]
-// [records: 2 x wp streams, win_stride(rc) u32 apart]
-// (an odd stride: the walking lanes' stores fall in distinct banks)
-__host__ __device__ constexpr uint32_t win_stride(uint32_t rc) { return (rc + 1) | 1u; }  // (+1: the zero run)
-// (at least one CodeLds: the listed pages' exact decode reuses the area)
-__host__ __device__ constexpr uint32_t win_wave_lds(uint32_t wbytes, uint32_t wp, uint32_t rc) {
-    return max(wbytes + 64 + kTileRows + 64 + (2 * wp * win_stride(rc) * 4 + 15) / 16 * 16,
-               static_cast<uint32_t>((sizeof(CodeLds) + 15) / 16 * 16));
-}
-
-// 32 bits of the staged window starting at bit b (b >= -31; bits before bit 0
-// read as 0); word indices past zw (the page slot's last, zero word) clamp
-__device__ __forceinline__ uint32_t win_bits32(const uint32_t* st, int32_t b, uint32_t zw) {
-    const uint32_t bp = static_cast<uint32_t>(max(b, 0));
-    const uint32_t wi = bp >> 5;
-    const uint32_t v = __builtin_amdgcn_alignbit(st[min(wi + 1, zw)], st[min(wi, zw)], bp & 31u);
-    return v << (bp - static_cast<uint32_t>(b));
-}
-
-template <bool kDict>
-__global__ void __launch_bounds__(kWinWaves * 64) k_pipe_win(CodeArgs ea, const DevBatch* __restrict__ wins, int nwins,
-                                                             uint32_t wbytes, uint32_t wp, uint32_t rc, uint32_t lds_total,
-                                                             RunDictArgs d) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t win_dyn[];
-    const uint8_t* __restrict__ bytes = ea.bytes;
-    const DevPage* __restrict__ pages = ea.pages;
-    uint16_t* __restrict__ codes = ea.codes;
-    const int32_t max_def = ea.max_def;
-    const int debug = ea.debug;
-    // (kDict: the leading workgroups decode the dictionary pages; its code
-    // costs the page waves registers and 12 KB of static LDS, so by default
-    // the dictionary decodes on the side stream instead)
-    if constexpr (kDict) {
-        if (static_cast<int>(blockIdx.x) < d.ndicts) {
-            dict_index_block<kRunWaves>(bytes, d.dicts, static_cast<int>(blockIdx.x), d.entries, d.dict_count, d.dict_err,
-                                        d.err_any, lds_total, win_dyn);
-            return;
-        }
-    }
-    const uint32_t wv = threadIdx.x / kWave;
-    const int w = (static_cast<int>(blockIdx.x) - d.ndicts) * kWinWaves + static_cast<int>(wv);
-    if (w >= nwins) return;
-    uint8_t* base = reinterpret_cast<uint8_t*>(win_dyn) + wv * win_wave_lds(wbytes, wp, rc);
-    uint32_t* stw = reinterpret_cast<uint32_t*>(base);
-    uint8_t* mk = base + wbytes + 64;
-    uint32_t* vmap = reinterpret_cast<uint32_t*>(mk + kTileRows);
-    uint32_t* recs = vmap + 16;
-    const DevBatch B = wins[w];
-    const uint32_t np = static_cast<uint32_t>(B.np);
-    const uint32_t md = static_cast<uint32_t>(max_def);
-    // 1. the window's slots, then 64 zero bytes
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(bytes + B.img_lo);
-        uint4* dst = reinterpret_cast<uint4*>(stw);
-        const uint32_t nb = B.img_bytes / 16;
-        copy_blocks(dst, src, nb, lane(), kWave);  // (eight loads in flight per lane before the stores)
-        if (lane() < 4) dst[nb + lane()] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    // one page per lane pair: descriptor and prologue (column_reader.cpp:146-182)
-    const uint32_t pk = min(lane() >> 1, np - 1);
-    const DevPage pg = pages[B.p0 + static_cast<int>(pk)];
-    const uint32_t size = static_cast<uint32_t>(max(pg.size, 0)), n = static_cast<uint32_t>(max(pg.nvals, 0));
-    const uint32_t s0 = static_cast<uint32_t>(pg.off - B.img_lo);
-    const uint32_t zw = (s0 + (size + 15) / 16 * 16 + 16) / 4 - 1;  // the slot's last word (zero)
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (debug & (1 << 20)) return;  // timing ablation: staging only (outputs invalid)
-    uint32_t fb = n > static_cast<uint32_t>(kTileRows) ? 1u : 0u;
-    uint32_t pos = 0, db = 0, dl = 0, bwi = 0;
-    if (md > 0) {
-        if (size < 4) fb = 1;
-        else {
-            dl = static_cast<uint32_t>(lds_u64(stw, s0));
-            pos = 4;
-            if (static_cast<uint64_t>(pos) + dl > size) fb = 1;
-            else { db = 4; pos += dl; }
-        }
-    }
-    if (!fb) {
-        if (pos + 1 > size) fb = 1;
-        else { bwi = static_cast<uint32_t>(lds_u64(stw, s0 + pos)) & 0xFFu; pos += 1; }
-    }
-    if (bwi > 16) fb = 1;
-    // 2. lock-step walk: lane 2k the def stream of page k, lane 2k + 1 its
-    //    index stream, to the stream's end (no value counts: the records are
-    //    formed per page below, one lane per run); each step lists one header
-    //    position.  Branch-free: flags are 0/1 words combined with & and |
-    //    (&& / || compile to exec-mask branches).  kOne: every live header is
-    //    one byte, what both writers emit for runs of < 64 values or groups.
-    const bool isi = (lane() & 1u) != 0;
-    const uint32_t bw = isi ? bwi : 1u, nbv = (bw + 7) / 8;
-    const uint32_t e = fb ? 0u : (isi ? s0 + size : s0 + db + dl);
-    uint32_t q = fb ? 0u : (isi ? s0 + pos : s0 + db);
-    uint32_t nr = 0;
-    uint32_t live = ((lane() >> 1) < np && !fb && (isi || md > 0) && n > 0 && q < e) ? 1u : 0u;
-    uint32_t* rec = recs + lane() * win_stride(rc);
-    auto step = [&](auto one, uint32_t x0, uint32_t x1) {
-        constexpr bool kOne = decltype(one)::value;
-        uint32_t hl, ind, hbad = 0;
-        if constexpr (kOne) {
-            hl = 1;
-            ind = x0 & 0x7Fu;
-        } else {
-            const uint32_t st0 = ~x0 & 0x80808080u;
-            const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;
-            hl = st0 ? hl4 : ((~x1 & 0x80u) ? 5u : 9u);
-            const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
-            const uint32_t x0m = x0 & lm;
-            const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
-            ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) | ((x0m >> 3) & 0xFE00000u) | top;
-            hbad = hl > 5 ? 1u : 0u;
-        }
-        const uint32_t g = ind >> 1, lit = ind & 1u, qh = q + hl;
-        const uint32_t litm = 0u - lit;
-        // literal: g groups of 8 values (the end clamps: the reference reads
-        // on past it); RLE: g copies of an nbv-byte value, which must fit
-        const uint32_t nql = min(__umul24(min(g, 0x10000u), bw) + qh, e);
-        const uint32_t nqr = qh + nbv;
-        const uint32_t over = (litm & qh) | (~litm & nqr);
-        const uint32_t ok = live & (nr < rc ? 1u : 0u) & ((hbad | (g == 0 ? 1u : 0u) | (over > e ? 1u : 0u)) ^ 1u);
-        if (ok) rec[nr] = q;
-        nr += ok;
-        q = (litm & nql) | (~litm & nqr);
-        live = ok & (q < e ? 1u : 0u);
-    };
-    while (__ballot(live)) {
-        const uint32_t qa = q >> 2, qs = q & 3u;
-        const uint32_t w0 = stw[qa], w1 = stw[qa + 1];
-        const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, qs);
-        if (__ballot(live & (x0 >> 7)) == 0) {
-            step(std::true_type{}, x0, 0u);
-        } else {
-            const uint32_t w2 = stw[qa + 2];
-            step(std::false_type{}, x0, __builtin_amdgcn_alignbyte(w2, w1, qs));
-        }
-    }
-    // a chain that stopped before its stream's end (a bad header or rc
-    // headers): an error only if its runs hold fewer values than needed
-    const uint32_t cut = (q < e && !fb) ? 1u : 0u;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (debug & (1 << 21)) return;  // timing ablation: + the walk
-    // The records of one listed stream, in place (one lane per run): header
-    // position -> first value (capped at 1023: past any page's rows) |
-    // literal << 10 | (RLE value, or the literal values' window bit offset)
-    // << 11; returns the values the runs hold (capped at 2^30).
-    auto form = [&](uint32_t* rr, uint32_t nrec, uint32_t bwv) -> uint32_t {
-        const uint32_t nbvv = (bwv + 7) / 8;
-        const uint32_t vmv = nbvv >= 2 ? 0xFFFFu : (nbvv ? 0xFFu : 0u);
-        uint32_t base = 0;
-        for (uint32_t r0 = 0; r0 < nrec; r0 += kWave) {
-            const uint32_t r = r0 + lane();
-            const uint32_t act = r < nrec ? 1u : 0u;
-            const uint32_t qq = rr[act ? r : 0u];
-            const uint32_t qa = qq >> 2, qs = qq & 3u;
-            const uint32_t w0 = stw[qa], w1 = stw[qa + 1], w2 = stw[qa + 2];
-            const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, qs), x1 = __builtin_amdgcn_alignbyte(w2, w1, qs);
-            const uint32_t st0 = ~x0 & 0x80808080u;
-            const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;
-            const uint32_t hl = st0 ? hl4 : 5u;  // (listed headers are <= 5 bytes)
-            const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
-            const uint32_t x0m = x0 & lm;
-            const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
-            const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) | ((x0m >> 3) & 0xFE00000u) | top;
-            const uint32_t vraw = hl < 4 ? __builtin_amdgcn_alignbyte(x1, x0, hl) : x1 >> (8 * ((hl - 4) & 3));
-            const uint32_t g = ind >> 1, lit = ind & 1u, litm = 0u - lit;
-            const uint32_t c = act * ((litm & (min(g, 1u << 17) << 3)) | (~litm & min(g, 1u << 20)));
-            const uint32_t incl = wave_incl_scan(c);
-            const uint32_t st = min(base + incl - c, 1023u);
-            const uint32_t pay = (litm & ((qq + hl) << 3)) | (~litm & vraw & vmv);
-            if (act) rr[r] = st | (lit << 10) | (pay << 11);
-            base = min(base + bcast_last(incl), 1u << 30);
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        return base;
-    };
-    // 3. per page (pages outside the fast shape: bits of `listed`)
-    const uint32_t l8 = lane() * 8;
-    uint32_t listed = 0;
-    for (uint32_t k = 0; k < np; k++) {
-        const uint32_t nk = __builtin_amdgcn_readlane(n, 2 * k);
-        const uint32_t zwk = __builtin_amdgcn_readlane(zw, 2 * k);
-        const uint32_t bwk = __builtin_amdgcn_readlane(bwi, 2 * k);
-        uint32_t nrd = __builtin_amdgcn_readlane(nr, 2 * k), nri = __builtin_amdgcn_readlane(nr, 2 * k + 1);
-        const uint32_t cutd = __builtin_amdgcn_readlane(cut, 2 * k), cuti = __builtin_amdgcn_readlane(cut, 2 * k + 1);
-        bool flk = __builtin_amdgcn_readlane(fb, 2 * k) != 0;
-        if (nk == 0 && !flk) continue;  // (no tile)
-        const int64_t R0 = static_cast<int64_t>(
-            (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(pg.first_row) >> 32), 2 * k)) << 32) |
-            __builtin_amdgcn_readlane(static_cast<uint32_t>(pg.first_row), 2 * k));
-        const uint32_t rowm = l8 >= nk ? 0u : (nk - l8 >= 8 ? 0xFFu : ((1u << (nk - l8)) - 1u));
-        uint32_t vb = rowm;
-        if (!flk && md > 0) {
-            uint32_t* rd = recs + 2 * k * win_stride(rc);
-            const uint32_t totd = form(rd, nrd, 1u);
-            if (totd < nk) {  // the stream ran out: the rest of the levels are 0 (rle_decoder.hpp:20-23)
-                if (cutd) flk = true;  // ... unless its chain stopped at a bad header
-                else {
-                    if (lane() == 0) rd[nrd] = totd;
-                    nrd++;
-                }
-            }
-            // def runs -> validity map (rows of level 1; literal runs: the stream's bits)
-            if (lane() < 16) vmap[lane()] = 0u;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            bool above = false;
-            for (uint32_t r = lane(); r < nrd && !flk; r += kWave) {
-                const uint32_t R = rd[r];
-                const uint32_t s = R & 0x3FFu, en = min(r + 1 < nrd ? (rd[r + 1] & 0x3FFu) : nk, nk);
-                if (s >= nk) continue;  // (runs past the rows)
-                const uint32_t lit = (R >> 10) & 1u, pay = R >> 11;
-                above |= !lit && pay > md;
-                if ((lit || pay == md) && en > s) {
-                    for (uint32_t wd = s >> 5; wd <= (en - 1) >> 5; wd++) {
-                        const uint32_t lo = max(s, wd * 32) - wd * 32, hi = min(en, wd * 32 + 32) - wd * 32;
-                        const uint32_t m = (hi >= 32 ? 0xFFFFFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-                        const uint32_t v = lit ? win_bits32(stw, static_cast<int32_t>(pay + wd * 32) - static_cast<int32_t>(s), zwk)
-                                               : 0xFFFFFFFFu;
-                        if (v & m) atomicOr(&vmap[wd], v & m);
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (__ballot(above)) flk = true;  // levels above max_def: the exact decoder's error
-            vb = static_cast<uint32_t>(reinterpret_cast<const uint8_t*>(vmap)[lane()]) & rowm;
-        }
-        if (flk) {
-            listed |= 1u << k;
-            continue;
-        }
-        if (debug & (1 << 22)) continue;  // timing ablation: + validity
-        const uint32_t nnl = __popc(vb);
-        const uint32_t nincl = wave_incl_scan(nnl);
-        const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
-        uint32_t pw[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-        uint32_t* ri = recs + (2 * k + 1) * win_stride(rc);
-        if (nn) {
-            const uint32_t toti = form(ri, nri, bwk);
-            if (toti < nn) {  // exhausted: the rest of the indices are 0
-                if (cuti) {
-                    listed |= 1u << k;
-                    continue;
-                }
-                if (lane() == 0) ri[nri] = toti;
-                nri++;
-            }
-        }
-        if (nn) {
-            *reinterpret_cast<uint2*>(mk + l8) = make_uint2(0u, 0u);
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (uint32_t r = lane(); r < nri; r += kWave) {
-                const uint32_t st = ri[r] & 0x3FFu;
-                if (r > 0 && st < nn) mk[st] = static_cast<uint8_t>(r);
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            {   // the record of ranks 8l .. 8l + 7 (max scan of the marks), back to mk
-                const uint2 mv = *reinterpret_cast<const uint2*>(mk + l8);
-                uint32_t rm[8], run = 0;
-#pragma unroll
-                for (int kk = 0; kk < 8; kk++) {
-                    run = max(run, ((kk < 4 ? mv.x : mv.y) >> (8 * (kk & 3))) & 0xFFu);
-                    rm[kk] = run;
-                }
-                const uint32_t ex = wave_shr1(wave_incl_max(run));
-                uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-                for (int kk = 0; kk < 8; kk++) {
-                    const uint32_t v = max(ex, rm[kk]);
-                    if (kk < 4) w0 |= v << (8 * kk);
-                    else w1 |= v << (8 * (kk - 4));
-                }
-                __builtin_amdgcn_wave_barrier();
-                *reinterpret_cast<uint2*>(mk + l8) = make_uint2(w0, w1);
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint32_t maski = (1u << bwk) - 1u;
-#pragma unroll
-            for (int kk = 0; kk < 8; kk++) {
-                const uint32_t rk = min(rbase + __popc(vb & ((1u << kk) - 1u)), static_cast<uint32_t>(kTileRows - 1));
-                const uint32_t R = ri[mk[rk]];
-                const uint32_t st = R & 0x3FFu, pay = R >> 11;
-                const uint32_t lb = sbits3(stw, pay + (rk - st) * bwk, zwk, maski);
-                const uint32_t v = ((R >> 10) & 1u) ? lb : pay;
-                const uint32_t code = ((vb >> kk) & 1u) ? v : static_cast<uint32_t>(kNull);
-                if (kk & 1) pw[kk >> 1] = (pw[kk >> 1] & 0xFFFFu) | (code << 16);
-                else pw[kk >> 1] = (pw[kk >> 1] & 0xFFFF0000u) | code;
-            }
-        }
-        if (debug & (1 << 23)) continue;  // timing ablation: no stores
-        store_packed8(codes, R0, l8, nk, pw);
-        __builtin_amdgcn_wave_barrier();
-    }
-    // the listed pages: the reference state machine, raw codes (the wave's
-    // LDS area is free now)
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t k = 0; k < np; k++) {
-        if (!((listed >> k) & 1u)) continue;
-        exact_page_body<false, true>(ea, *reinterpret_cast<CodeLds*>(base), B.p0 + static_cast<int>(k), 0u, 0u);
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// The pages k_pipe_win listed: the reference state machine, one wave per
-// page (a separate launch: its registers would cost the front its occupancy).
-__global__ void __launch_bounds__(64) k_pipe_exact(CodeArgs a, const int32_t* __restrict__ flist) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // one CodeLds: one wave per workgroup
-    CodeLds& L = *reinterpret_cast<CodeLds*>(smem);
-    const int nf = flist[0];
-    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
-    for (int i = static_cast<int>(blockIdx.x); i < nf; i += static_cast<int>(gridDim.x)) {
-        exact_page_body(a, L, flist[1 + i], dict_n, ebase);  // inlined: a call spills CodeArgs to scratch
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-
-// ── after k_pipe_win (k_pipe_tail) ─────────────────────────────────────────
-// Once the dictionary is decoded: the pages k_pipe_win listed, by the
-// reference state machine (their codes, tile characters and per-workgroup
-// sums), then the characters of every other tile from its raw codes (entry
-// lengths in LDS; indices at or past the dictionary's entry count are NULL
-// rows, column_reader.cpp:190-194), filed as k_pipe_codes3 files them for
-// k_pipe_write.  Each wave takes a contiguous tile range; the codes of four
-// tiles load at once.
-constexpr int kTailWaves = 4;
-__global__ void __launch_bounds__(kTailWaves * 64) k_pipe_tail(CodeArgs a, const int32_t* __restrict__ flist,
-                                                               uint32_t lt_n) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];  // [kTailWaves x CodeLds][lens]
-    CodeLds& L = reinterpret_cast<CodeLds*>(smem)[threadIdx.x / kWave];
-    uint16_t* lens = reinterpret_cast<uint16_t*>(smem + kTailWaves * sizeof(CodeLds));
-    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    const uint32_t ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
-    const uint32_t nl = min(dict_n, lt_n);
-    copy_map(lens, a.entries + ebase, nl, threadIdx.x, blockDim.x, [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
-    __syncthreads();
-    const int gw = static_cast<int>(blockIdx.x) * kTailWaves + static_cast<int>(threadIdx.x / kWave);
-    const int nw = static_cast<int>(gridDim.x) * kTailWaves;
-    const int nf = flist[0];
-    for (int i = gw; i < nf; i += nw) {
-        exact_page_body(a, L, flist[1 + i], dict_n, ebase);
-        __builtin_amdgcn_wave_barrier();
-    }
-    const uint32_t l8 = lane() * 8;
-    const int pw = (a.ntiles + nw - 1) / nw;
-    const int ta = min(a.ntiles, gw * pw), tb = min(a.ntiles, ta + pw);
-    for (int c0 = ta; c0 < tb; c0 += kWave) {
-        const int cn = min(kWave, tb - c0);
-        int64_t myR0 = 0;
-        uint32_t mym = 0, myskip = 1;
-        if (static_cast<int>(lane()) < cn) {
-            const DevTile T = a.tiles[c0 + lane()];
-            myR0 = a.pages[T.page].first_row + T.row0;
-            mym = static_cast<uint32_t>(T.nrows);
-            myskip = (a.info[T.page] & kFallback) ? 1u : 0u;  // (decoded above)
-        }
-        for (int i0 = 0; i0 < cn; i0 += 4) {
-            uint4 cv[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                cv[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-                const int i = i0 + u;
-                if (i < cn && !__builtin_amdgcn_readlane(myskip, i)) {
-                    const int64_t R = static_cast<int64_t>(
-                        (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(myR0) >> 32), i)) << 32) |
-                        __builtin_amdgcn_readlane(static_cast<uint32_t>(myR0), i));
-                    if (l8 < __builtin_amdgcn_readlane(mym, i)) {
-                        const U16B x = *reinterpret_cast<const U16B*>(a.codes + R + l8);
-                        cv[u] = make_uint4(x.x, x.y, x.z, x.w);
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int i = i0 + u;
-                if (i >= cn) break;
-                if (__builtin_amdgcn_readlane(myskip, i)) continue;
-                const uint32_t mm = __builtin_amdgcn_readlane(mym, i);
-                const uint32_t ww[4] = {cv[u].x, cv[u].y, cv[u].z, cv[u].w};
-                uint32_t sum = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t c = (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                    const bool ok = l8 + k < mm && c < nl;
-                    sum += ok ? lens[ok ? c : 0u] : 0u;
-                }
-                tile_done(a, c0 + i, wave_sum(sum));
-            }
-        }
-    }
-}
-
-// ── codes and write in one persistent pass (k_pipe_fused) ───────────────────
-// k_pipe_codes3's per-tile decode and k_pipe_write's per-tile write, fused so
-// that the u16 codes never go through HBM and the decode's VALU work of some
-// waves runs while other waves of the same CU wait on their stores (the two
-// kernels otherwise run back to back: the front, VALU/latency-bound, then the
-// writer, HBM-bound).  Work comes in units of kFuseTiles consecutive 512-row
-// tiles, claimed by ticket (an atomic counter: a unit's predecessors were all
-// claimed by running waves, so the look-back below always completes, whatever
-// else shares the GPU).  Per unit, one wave:
-//   1. decodes its tiles' codes into registers (rows 8l .. 8l + 7 per lane,
-//      packed two per dword, the writer's own code layout): run records from
-//      k_pipe_runs and the page payload staged in the wave's LDS scratch, as in
-//      k_pipe_codes3; tiles of pages k_pipe_big or the exact decoder
-//      (k_pipe_exact, launched before) already decoded are read from HBM;
-//   2. sums the unit's characters (entry lengths from the LDS dictionary
-//      table) and takes its first output byte by decoupled look-back over the
-//      units before it (status words: flag and value in one 8-byte word);
-//   3. writes offsets, validity and characters exactly as k_pipe_write does.
-constexpr int kFuseTiles = 4;  // = kWBatch: four tiles' codes in registers
-
-struct FuseDecLds {  // one wave's decode scratch (the stage follows); aliased by WriteLds when writing
-    uint2 recd[kPipeRunCap];
-    uint2 reci[kPipeRunCap];
-    uint8_t mark[kTileRows];
-    uint8_t mark2[kTileRows];
-};
-static_assert(sizeof(FuseDecLds) % 16 == 0, "stage alignment");
-
-struct FusedArgs {
-    const uint8_t* bytes;
-    const DevPage* pages;
-    const DevTile* tiles;
-    int ntiles;
-    const int32_t* page_tile0;
-    int32_t max_def;
-    const DevDict* dicts;
-    int32_t dict_id;
-    const uint64_t* entries;
-    const int32_t* dict_count;
-    const uint2* runs;
-    const uint32_t* info;
-    const int32_t* tile_nn;
-    const uint16_t* codes;  // rows of pages decoded before this pass (k_pipe_big, k_pipe_exact)
-    DevErr* page_err;
-    int32_t* err_any;
-    int64_t nrows_total;
-    int64_t* total;
-    int64_t capacity;
-    int32_t* overflow;
-    uint32_t* validity;
-    int64_t* offsets;
-    uint8_t* chars;
-    uint32_t dict_chars_bytes, dict_bytes;  // LDS: [kFront][dictionary payload][entry table], then per wave scratch
-    uint32_t wave_lds;                      // per-wave scratch: max(FuseDecLds + stage, WriteLds)
-    uint32_t stage_bytes;                   // payload stage (>= every k_pipe_runs page's slot)
-    int32_t nunits;
-    int32_t* ticket;                        // zeroed per decode
-    unsigned long long* status;             // nunits aggregate words, then the superblock words; zeroed per decode
-    uint32_t* znext;                        // the next decode's zero block (cleared here), or null
-    uint32_t znext_words;
-    const uint8_t* match;                   // armed page filter, as k_pipe_write
-    int match_neg;
-    uint8_t* page_flags;
-    int debug;
-};
-
-constexpr unsigned long long kFAgg = 1ull << 62;
-constexpr unsigned long long kFValMask = (1ull << 62) - 1;
-
-__device__ __forceinline__ unsigned long long fwave_sum64(unsigned long long v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t lo = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
-        const uint32_t hi = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v >> 32), d));
-        v = v + ((static_cast<unsigned long long>(hi) << 32) | lo) - 0;
-    }
-    return v;
-}
-
-// The exclusive prefix of unit u's characters, two-level: units in groups of
-// kFSuper (superblocks).  A unit publishes its aggregate in status[u] and adds
-// (1 << 48) | aggregate to its superblock's word sb[u / kFSuper]; its prefix
-// is the sums of the complete superblocks before its own (unit count reached)
-// plus the aggregates of its superblock's earlier units.  (A per-unit chained
-// look-back serialised here: every resident wave decodes its first unit at
-// once, so the inclusive prefixes propagated one 64-unit poll at a time, about
-// 50 us over C2's ~4,900 units.)  Units are claimed by ticket, so every unit
-// a poll waits for belongs to a running wave.
-constexpr int kFSuper = 64;
-constexpr unsigned long long kFSumMask = (1ull << 48) - 1;
-__device__ unsigned long long unit_prefix(unsigned long long* status, unsigned long long* sb, int32_t u,
-                                          unsigned long long total) {
-    const int32_t s = u / kFSuper, u0 = s * kFSuper;
-    if (lane() == 0) {
-        __hip_atomic_store(&status[u], kFAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&sb[s], (1ull << 48) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    unsigned long long prefix = 0;
-    // complete superblocks before s (all of them hold kFSuper units)
-    for (int32_t b0 = 0; b0 < s; b0 += kWave) {
-        const int32_t b = b0 + static_cast<int32_t>(lane());
-        uint32_t nap = 1;
-        for (;;) {
-            const unsigned long long v =
-                b < s ? __hip_atomic_load(&sb[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (static_cast<unsigned long long>(kFSuper) << 48);
-            if (__ballot((v >> 48) != static_cast<unsigned long long>(kFSuper)) == 0) {
-                prefix += fwave_sum64(b < s ? (v & kFSumMask) : 0ull);
-                break;
-            }
-            for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(4);
-            nap = nap < 8 ? 2 * nap : 8;
-        }
-    }
-    // this superblock's units before u
-    if (u > u0) {
-        const int32_t v = u0 + static_cast<int32_t>(lane());
-        uint32_t nap = 1;
-        for (;;) {
-            const unsigned long long x =
-                v < u ? __hip_atomic_load(&status[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFAgg;
-            if (__ballot((x >> 62) == 0) == 0) {
-                prefix += fwave_sum64(v < u ? (x & kFValMask) : 0ull);
-                break;
-            }
-            for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(4);
-            nap = nap < 8 ? 2 * nap : 8;
-        }
-    }
-    return prefix;
-}
-
-// One tile's codes (w[4]: rows 8l .. 8l + 7 of the lane, packed) and its
-// characters (wave-uniform).  k_pipe_codes3's decode, with the records and
-// payload loaded and staged here (no cross-tile prefetch).
-template <bool kArmed>
-__device__ __forceinline__ uint32_t fuse_codes(const FusedArgs& a, FuseDecLds& D, uint32_t* stage, const uint32_t* dtab,
-                                               uint32_t dict_n, int t, int p, uint32_t r0, uint32_t m, uint32_t inf,
-                                               uint32_t size, uint64_t off, int64_t R0, uint32_t tp, uint32_t w[4]) {
-    const uint32_t l8 = lane() * 8;
-    auto lenof = [&](uint32_t v, bool ok) -> uint32_t {
-        const uint32_t e = dtab[ok ? v : 0u];
-        return ok ? (kArmed ? ((e >> 16) & 0x7FFFu) : (e >> 16)) : 0u;
-    };
-    if (inf & kSkip) {  // decoded before this pass: the codes are in HBM
-        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        if (l8 < m) {
-            const U16B x = *reinterpret_cast<const U16B*>(a.codes + R0 + l8);
-            v = make_uint4(x.x, x.y, x.z, x.w);
-        }
-        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-        uint32_t chars = 0;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t c = l8 + k < m ? (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : kNull;
-            chars += lenof(c, c < dict_n);
-        }
-        return wave_sum(chars);
-    }
-    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
-    const uint32_t maskd = (1u << bwd) - 1u;
-    const uint32_t nd = inf & 0xFFu, ni = (inf >> 8) & 0xFFu, bwi = (inf >> 16) & 0xFFu;
-    // the page's run records (clamped indices: a page costs its records' lines)
-    const uint2* rd_ = a.runs + static_cast<size_t>(p) * 2 * kPipeRunCap;
-    const uint2 z = make_uint2(0u, 0u);
-    const uint32_t nd1 = nd ? nd - 1 : 0u, ni1 = ni ? ni - 1 : 0u;
-    const uint2 q0 = rd_[min(lane(), nd1)], q1 = rd_[min(lane() + kWave, nd1)];
-    const uint2 q2 = rd_[kPipeRunCap + min(lane(), ni1)], q3 = rd_[kPipeRunCap + min(lane() + kWave, ni1)];
-    const uint2 d0 = lane() < nd ? q0 : z, d1 = lane() + kWave < nd ? q1 : z;
-    const uint2 x0 = lane() < ni ? q2 : z, x1 = lane() + kWave < ni ? q3 : z;
-    // non-null rows of the page's earlier tiles (pages of <= 2048 rows: <= 3)
-    const uint32_t tn = static_cast<uint32_t>(a.tile_nn[min(tp + lane(), static_cast<uint32_t>(a.ntiles - 1))]);
-    const uint32_t k0n = (md > 0 && tp + lane() < static_cast<uint32_t>(t)) ? tn : 0u;
-    // payload -> stage (the slot's >= 16 zero bytes after the payload come along)
-    {
-        const uint32_t nb = (size + 15) / 16 + 1;
-        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + off);
-        uint4* st4 = reinterpret_cast<uint4*>(stage);
-        for (uint32_t b = lane(); b < nb; b += kWave) st4[b] = src[b];
-    }
-    D.recd[lane()] = d0;
-    D.recd[lane() + kWave] = d1;
-    D.reci[lane()] = x0;
-    D.reci[lane() + kWave] = x1;
-    *reinterpret_cast<uint2*>(D.mark + l8) = make_uint2(0u, 0u);
-    *reinterpret_cast<uint2*>(D.mark2 + l8) = make_uint2(0u, 0u);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t zw = ((size + 15) / 16 + 1) * 4 - 1;  // last word of the slot: zero
-    const uint32_t maski = (1u << bwi) - 1u;
-    uint32_t vb;
-    if (md > 0) {  // def levels of rows r0 + 8l .. r0 + 8l + 7
-        const uint32_t rd0 = run_at_reg(d0, d1, nd, r0);
-        {
-            const uint32_t k = lane(), st = rr_start(d0);
-            if (k < nd && k > rd0 && st < r0 + m) D.mark[st - r0] = static_cast<uint8_t>(k - rd0);
-            const uint32_t k1 = lane() + kWave, st1 = rr_start(d1);
-            if (k1 < nd && k1 > rd0 && st1 < r0 + m) D.mark[st1 - r0] = static_cast<uint8_t>(k1 - rd0);
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint2 mk = *reinterpret_cast<const uint2*>(D.mark + l8);
-        uint32_t rm[8], run = 0;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
-            rm[k] = run;
-        }
-        const uint32_t ex = wave_shr1(wave_incl_max(run));
-        vb = 0;
-        bool above = false;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t j = l8 + k;
-            const uint2 R = D.recd[(rd0 + max(ex, rm[k])) & (kPipeRunCap - 1)];
-            const uint32_t pay = rr_pay(R);
-            const uint32_t lb = sbits3(stage, pay + (r0 + j - rr_start(R)) * bwd, zw, maskd);
-            const uint32_t lvl = rr_lit(R) ? lb : pay;
-            const bool in = j < m;
-            vb |= (in && lvl == md ? 1u : 0u) << k;
-            above |= in && lvl > md;
-        }
-        if (__ballot(above)) {  // levels above max_def: outside the supported format
-            set_err(a.page_err + p, a.err_any, PQ_ERR_UNSUPPORTED, 0, 0, size);
-            w[0] = w[1] = w[2] = w[3] = 0xFFFFFFFFu;
-            __builtin_amdgcn_wave_barrier();
-            return 0;
-        }
-    } else {
-        vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
-    }
-    const uint32_t nnl = __popc(vb);
-    const uint32_t nincl = wave_incl_scan(nnl);
-    const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
-    const uint32_t k0 = md > 0 ? wave_sum(k0n) : r0;
-    const uint32_t ri0 = run_at_reg(x0, x1, ni, k0);
-    if (nn) {  // dictionary index runs over ranks [k0, k0 + nn): run of each rank -> mark2
-        {
-            const uint32_t k = lane(), st = rr_start(x0);
-            if (k < ni && k > ri0 && st < k0 + nn) D.mark2[st - k0] = static_cast<uint8_t>(k - ri0);
-            const uint32_t k1 = lane() + kWave, st1 = rr_start(x1);
-            if (k1 < ni && k1 > ri0 && st1 < k0 + nn) D.mark2[st1 - k0] = static_cast<uint8_t>(k1 - ri0);
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint2 mk = *reinterpret_cast<const uint2*>(D.mark2 + l8);
-        uint32_t rm[8], run = 0;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
-            rm[k] = run;
-        }
-        const uint32_t ex = wave_shr1(wave_incl_max(run));
-        uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t v = max(ex, rm[k]);
-            if (k < 4) w0 |= v << (8 * k);
-            else w1 |= v << (8 * (k - 4));
-        }
-        __builtin_amdgcn_wave_barrier();
-        *reinterpret_cast<uint2*>(D.mark2 + l8) = make_uint2(w0, w1);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    uint32_t chars = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const uint32_t rk = min(rbase + __popc(vb & ((1u << k) - 1u)), static_cast<uint32_t>(kTileRows - 1));
-        const uint2 R = D.reci[(ri0 + D.mark2[rk]) & (kPipeRunCap - 1)];
-        const uint32_t pay = rr_pay(R);
-        const uint32_t lb = sbits3(stage, pay + (k0 + rk - rr_start(R)) * bwi, zw, maski);
-        const uint32_t v = rr_lit(R) ? lb : pay;
-        const bool ok = ((vb >> k) & 1u) && v < dict_n;
-        chars += lenof(v, ok);
-        const uint32_t code = ok ? v : static_cast<uint32_t>(kNull);
-        if (k & 1) w[k >> 1] |= code << 16;
-        else w[k >> 1] = code;
-    }
-    __builtin_amdgcn_wave_barrier();  // the scratch is rewritten by the next tile / the writer
-    return wave_sum(chars);
-}
-
-template <bool kArmed>
-__global__ void __launch_bounds__(kWriteMax * 64) k_pipe_fused(FusedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if (a.znext)  // the other zero block, for the next decode (unused by this one)
-        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.znext_words; i += gridDim.x * blockDim.x) a.znext[i] = 0;
-    uint32_t* dwa = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* dw = reinterpret_cast<uint32_t*>(smem + kFront);
-    uint32_t* dtab = reinterpret_cast<uint32_t*>(smem + kFront + a.dict_chars_bytes);
-    const uint32_t wv = threadIdx.x / kWave;
-    uint8_t* scratch = smem + a.dict_bytes + static_cast<size_t>(wv) * a.wave_lds;
-    FuseDecLds& D = *reinterpret_cast<FuseDecLds*>(scratch);
-    uint32_t* stage = reinterpret_cast<uint32_t*>(scratch + sizeof(FuseDecLds));
-    WriteLds& S = *reinterpret_cast<WriteLds*>(scratch);
-    const DevDict d = a.dicts[a.dict_id];
-    const uint32_t dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-    {  // the dictionary into LDS (as k_pipe_write)
-        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + d.off);
-        copy_blocks(reinterpret_cast<uint4*>(dw), src, a.dict_chars_bytes / 16, threadIdx.x, blockDim.x);
-        if (kArmed) {
-            const uint64_t* es = a.entries + d.entry_base;
-            for (uint32_t k = threadIdx.x; k < dict_n; k += blockDim.x) {
-                const uint64_t e = es[k];
-                const uint32_t sat = (a.match[k] != 0) != (a.match_neg != 0) ? 1u : 0u;
-                dtab[k] = static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16) | (sat << 31);
-            }
-        } else {
-            copy_map(dtab, a.entries + d.entry_base, dict_n, threadIdx.x, blockDim.x, [](uint64_t e) {
-                return static_cast<uint32_t>(e & 0xFFFFu) | (static_cast<uint32_t>(e >> 32) << 16);
-            });
-        }
-    }
-    __syncthreads();
-    auto rl64 = [](int64_t v, int i) -> int64_t {
-        const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
-        const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32), i);
-        return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
-    };
-    const uint32_t l8 = lane() * kRowsPerLane;
-    for (;;) {
-        int32_t u = 0;
-        if (lane() == 0) u = atomicAdd(a.ticket, 1);
-        u = static_cast<int32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u)));
-        if (u >= a.nunits) break;
-        const int c0 = u * kFuseTiles;
-        const int cn = min(kFuseTiles, a.ntiles - c0);
-        int64_t myR0 = 0, myoff = 0;
-        uint32_t mym = 0, myp = 0, myr0 = 0, myinf = kFallback, mysize = 0, mytp = 0;
-        {  // (clamped index, selected after: see k_pipe_codes3)
-            const bool in = static_cast<int>(lane()) < cn;
-            const DevTile T = a.tiles[c0 + min(static_cast<int>(lane()), cn - 1)];
-            const DevPage pg = a.pages[T.page];
-            const uint32_t inf = a.info[T.page];
-            const uint32_t tp = static_cast<uint32_t>(a.page_tile0[T.page]);
-            myp = in ? static_cast<uint32_t>(T.page) : 0u;
-            myr0 = in ? static_cast<uint32_t>(T.row0) : 0u;
-            mym = in ? static_cast<uint32_t>(T.nrows) : 0u;
-            myR0 = in ? pg.first_row + T.row0 : 0;
-            myinf = in ? inf : kFallback;
-            mysize = in ? static_cast<uint32_t>(max(pg.size, 0)) : 0u;
-            myoff = in ? static_cast<int64_t>(pg.off) : 0;
-            mytp = in ? tp : 0u;
-        }
-        // 1. codes of the unit's tiles
-        uint4 cv0 = make_uint4(~0u, ~0u, ~0u, ~0u), cv1 = cv0, cv2 = cv0, cv3 = cv0;
-        uint32_t myc = 0;
-        static_assert(kFuseTiles == 4, "code registers");
-        for (int i = 0; i < cn; i++) {
-            uint32_t w[4];
-            const uint32_t ch = fuse_codes<kArmed>(
-                a, D, stage, dtab, dict_n, c0 + i, static_cast<int>(__builtin_amdgcn_readlane(myp, i)),
-                __builtin_amdgcn_readlane(myr0, i), __builtin_amdgcn_readlane(mym, i),
-                __builtin_amdgcn_readlane(myinf, i), __builtin_amdgcn_readlane(mysize, i),
-                static_cast<uint64_t>(rl64(myoff, i)), rl64(myR0, i), __builtin_amdgcn_readlane(mytp, i), w);
-            const uint4 v = make_uint4(w[0], w[1], w[2], w[3]);
-            if (i == 0) cv0 = v;
-            else if (i == 1) cv1 = v;
-            else if (i == 2) cv2 = v;
-            else cv3 = v;
-            myc = static_cast<int>(lane()) == i ? ch : myc;
-        }
-        // 2. the unit's first output byte
-        const uint32_t inc = wave_incl_scan(myc);
-        const unsigned long long prefix = unit_prefix(a.status, a.status + a.nunits, u, bcast_last(inc));
-        const int64_t myG0 = static_cast<int64_t>(prefix) + static_cast<int64_t>(inc - myc);
-        if (a.debug & 8) continue;
-        // 3. k_pipe_write's per-tile body
-        for (int i = 0; i < cn; i++) {
-            const int64_t R0 = rl64(myR0, i);
-            const int64_t G0 = rl64(myG0, i);
-            const uint32_t m = __builtin_amdgcn_readlane(mym, i);
-            uint32_t cur[kRowsPerLane];
-            {
-                const uint4 w = i == 0 ? cv0 : (i == 1 ? cv1 : (i == 2 ? cv2 : cv3));
-                const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++)
-                    cur[k] = l8 + k < m ? (ww[k >> 1] >> (16 * (k & 1))) & 0xFFFFu : kNull;
-            }
-            uint32_t len[kRowsPerLane], src[kRowsPerLane], vb = 0, acc = 0, sat = 0;
-#pragma unroll
-            for (int k = 0; k < kRowsPerLane; k++) {
-                const bool valid = cur[k] < dict_n;
-                const uint32_t e = valid ? dtab[cur[k]] : 0u;
-                len[k] = kArmed ? ((e >> 16) & 0x7FFFu) : (e >> 16);
-                if (kArmed) sat |= e;
-                src[k] = e & 0xFFFFu;
-                vb |= (valid ? 1u : 0u) << k;
-                acc += len[k];
-            }
-            if (kArmed && __ballot(sat >> 31) && lane() == 0)  // the page filter: a row whose entry satisfies it
-                a.page_flags[__builtin_amdgcn_readlane(myp, i)] = 0;
-            const uint32_t incl = wave_incl_scan(acc);
-            const uint32_t total = bcast_last(incl);
-            {
-                uint32_t o[kRowsPerLane];
-                o[0] = incl - acc;
-#pragma unroll
-                for (int k = 1; k < kRowsPerLane; k++) o[k] = o[k - 1] + len[k - 1];
-                uint4* po = reinterpret_cast<uint4*>(&S.off[lane() * kRowsPerLane]);
-                po[0] = make_uint4(o[0], o[1], o[2], o[3]);
-                po[1] = make_uint4(o[4], o[5], o[6], o[7]);
-                *reinterpret_cast<uint4*>(&S.src[lane() * kRowsPerLane]) =
-                    make_uint4(src[0] | (src[1] << 16), src[2] | (src[3] << 16), src[4] | (src[5] << 16),
-                               src[6] | (src[7] << 16));
-            }
-            S.vb[lane()] = static_cast<uint8_t>(vb);
-            if (lane() == 0) S.off[m] = total;
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            if ((R0 & 1) == 0) {  // offsets: rows 2j', 2j' + 1 per lane as one 16-byte store
-#pragma unroll
-                for (int k = 0; k < kRowsPerLane / 2; k++) {
-                    const uint32_t j = k * 2 * kWave + 2 * lane();
-                    if (j + 1 < m) {
-                        const uint2 o = *reinterpret_cast<const uint2*>(&S.off[j]);
-                        const int64_t v0 = G0 + o.x, v1 = G0 + o.y;
-                        *reinterpret_cast<uint4*>(a.offsets + R0 + j) =
-                            make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(static_cast<uint64_t>(v0) >> 32),
-                                       static_cast<uint32_t>(v1), static_cast<uint32_t>(static_cast<uint64_t>(v1) >> 32));
-                    } else if (j < m) {
-                        a.offsets[R0 + j] = G0 + S.off[j];
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < kRowsPerLane; k++) {
-                    const uint32_t j = k * kWave + lane();
-                    if (j < m) a.offsets[R0 + j] = G0 + S.off[j];
-                }
-            }
-            {  // validity words [R0 >> 5, (R0 + m - 1) >> 5]
-                const int64_t gfirst = R0 >> 5, glast = (R0 + m - 1) >> 5;
-                const uint32_t sh = static_cast<uint32_t>(R0 & 31);
-                const int64_t g = gfirst + lane();
-                if (g <= glast) {
-                    auto tw = [&](int tt) -> uint32_t {
-                        return (tt >= 0 && tt < kWave / 4) ? reinterpret_cast<const uint32_t*>(S.vb)[tt] : 0u;
-                    };
-                    const int tt = static_cast<int>(lane());
-                    const uint32_t val = (tw(tt) << sh) | (sh ? (tw(tt - 1) >> (32 - sh)) : 0u);
-                    const bool whole = g * 32 >= R0 && (g * 32 + 32 <= R0 + m || R0 + m == a.nrows_total);
-                    if (whole) a.validity[g] = val;
-                    else if (val) atomicOr(&a.validity[g], val);
-                }
-            }
-            if (R0 + m == a.nrows_total && lane() == 0) {
-                a.offsets[a.nrows_total] = G0 + total;
-                *a.total = G0 + total;
-            }
-            if (total == 0 || (a.debug & 2)) {
-                __builtin_amdgcn_wave_barrier();
-                continue;
-            }
-            if (G0 + total > a.capacity) {  // output too small: the host grows it and re-runs
-                if (lane() == 0) atomicOr(a.overflow, 1);
-                __builtin_amdgcn_wave_barrier();
-                continue;
-            }
-            for (uint32_t g0 = 0; g0 < m; g0 += kWave) {  // characters: row per lane from the LDS dictionary
-                const uint32_t r = g0 + lane();
-                uint32_t s0 = 0, ln = 0, sa = 0;
-                if (r < m) {
-                    s0 = S.off[r];
-                    ln = S.off[r + 1] - s0;
-                    sa = kFront + S.src[r];
-                }
-                const bool lng = ln > kLongRow;
-                if (!lng && ln) {
-                    uint8_t* dp = a.chars + G0 + s0;
-                    if (ln >= 16) {
-                        for (uint32_t x = 0; x + 16 < ln; x += 16) {
-                            const uint4 v = lds16(dwa, sa + x);
-                            *reinterpret_cast<U16B*>(dp + x) = U16B{v.x, v.y, v.z, v.w};
-                        }
-                        const uint4 v = lds16(dwa, sa + ln - 16);
-                        *reinterpret_cast<U16B*>(dp + ln - 16) = U16B{v.x, v.y, v.z, v.w};
-                    } else {
-                        const uint4 v = lds16(dwa, sa);
-                        const uint32_t tt = ln >= 8 ? ln - 8 : (ln >= 4 ? ln - 4 : (ln >= 2 ? ln - 2 : 0u));
-                        const uint4 uu = lds16(dwa, sa + tt);
-                        if (ln >= 8) {
-                            *reinterpret_cast<U8B*>(dp) = U8B{v.x, v.y};
-                            *reinterpret_cast<U8B*>(dp + tt) = U8B{uu.x, uu.y};
-                        } else if (ln >= 4) {
-                            *reinterpret_cast<U4B*>(dp) = U4B{v.x};
-                            *reinterpret_cast<U4B*>(dp + tt) = U4B{uu.x};
-                        } else if (ln >= 2) {
-                            *reinterpret_cast<U2B*>(dp) = U2B{static_cast<uint16_t>(v.x)};
-                            *reinterpret_cast<U2B*>(dp + tt) = U2B{static_cast<uint16_t>(uu.x)};
-                        } else {
-                            dp[0] = static_cast<uint8_t>(v.x);
-                        }
-                    }
-                }
-                uint64_t lm = __ballot(lng);
-                while (lm) {  // long rows: the whole wave, aligned destination blocks
-                    const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lm));
-                    lm &= lm - 1;
-                    const int64_t A0 = G0 + __builtin_amdgcn_readlane(s0, l);
-                    const int64_t A1 = A0 + __builtin_amdgcn_readlane(ln, l);
-                    const uint32_t src0 = __builtin_amdgcn_readlane(sa, l);
-                    const int64_t b0 = A0 & ~static_cast<int64_t>(15);
-                    for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < A1; blk += 16 * kWave) {
-                        const uint4 v = lds16(dwa, static_cast<uint32_t>(src0 + (blk - A0)));
-                        store_part(a.chars, blk, v, static_cast<uint32_t>(max(blk, A0) - blk),
-                                   static_cast<uint32_t>(min(blk + 16, A1) - blk));
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();  // S is rewritten by the next tile / the next unit's decode
-        }
-    }
-}
-
 }  // namespace
 
 // The launch's LDS: the largest layout any page up to max_page_bytes takes.
@@ -3479,7 +2440,7 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     write_shape(P, &wgrid, &per);
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.self_sum ? nullptr : P.bsum, per, P.debug, P.write_waves};
+               P.bsum, per, P.debug, P.write_waves};
     if (count_pass) {
         const dim3 grid((P.ntiles + kCodeWaves - 1) / kCodeWaves);
         hipLaunchKernelGGL(k_pipe_codes<true>, grid, dim3(kCodeWaves * kWave), 0, s, a);
@@ -3540,7 +2501,6 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
                 P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves, P.znext, P.znext_words,
                 P.match, P.match_neg, P.page_flags};
-    a.self_sum = P.self_sum ? 1 : 0;
     if (P.match)
         hipLaunchKernelGGL(k_pipe_write<true>, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
     else
@@ -3588,109 +2548,6 @@ void launch_wide_chars(hipStream_t s, const PipeLaunch& P) {
     }
     hipLaunchKernelGGL(k_wide_chars, dim3((P.ntiles + kWideCharWaves - 1) / kWideCharWaves), dim3(kWideCharWaves * kWave),
                        0, s, a);
-}
-
-uint32_t pipe_win_slot(uint32_t page_bytes) { return (page_bytes + 15) / 16 * 16 + 16; }
-
-uint32_t pipe_win_lds(uint32_t wbytes, uint32_t wp, uint32_t rc, uint32_t dict_max) {
-    uint32_t lds = static_cast<uint32_t>(kWinWaves) * win_wave_lds(wbytes, wp, rc);
-    if (dict_max) lds = max(lds, (dict_max + 32 + 15) / 16 * 16 + 16);  // dict_index_block: the page + 32 bytes
-    return lds;
-}
-
-bool pipe_win_shape_ok(uint32_t wp, uint32_t rc) { return wp >= 1 && wp <= kWinPagesMax && rc >= 2 && rc <= kWinRecMax; }
-
-void launch_pipe_win(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, int nwins, uint32_t wbytes, uint32_t wp,
-                     uint32_t rc, const RunDicts* dicts, uint32_t dict_max) {
-    const int nd = dicts ? dicts->ndicts : 0;
-    if (nwins <= 0 && nd <= 0) return;
-    const RunDictArgs d = dicts ? RunDictArgs{dicts->dicts, nd, dicts->entries, dicts->dict_count, dicts->dict_err,
-                                              dicts->err_any}
-                                : RunDictArgs{nullptr, 0, nullptr, nullptr, nullptr, nullptr};
-    const uint32_t lds = pipe_win_lds(wbytes, wp, rc, nd ? dict_max : 0u);
-    const void* fn = nd ? reinterpret_cast<const void*>(k_pipe_win<true>) : reinterpret_cast<const void*>(k_pipe_win<false>);
-    ensure_dyn_lds(fn, lds);
-    CodeArgs ea{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
-                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-                nullptr, 1, P.debug, P.write_waves};
-    if (nd)
-        hipLaunchKernelGGL(k_pipe_win<true>, dim3(nd + (max(nwins, 0) + kWinWaves - 1) / kWinWaves), dim3(kWinWaves * kWave),
-                           lds, s, ea, wins, nwins, wbytes, wp, rc, lds, d);
-    else
-        hipLaunchKernelGGL(k_pipe_win<false>, dim3((max(nwins, 0) + kWinWaves - 1) / kWinWaves), dim3(kWinWaves * kWave),
-                           lds, s, ea, wins, nwins, wbytes, wp, rc, lds, d);
-}
-
-void launch_pipe_exact(hipStream_t s, const PipeLaunch& P) {
-    int wgrid = 0, per = 0;
-    write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_write's workgroups
-    CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
-               P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.self_sum ? nullptr : P.bsum, per, P.debug, P.write_waves};
-    if (P.self_sum) {  // the self-summing writer sums every tile: the listed pages only
-        hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, P.npages))), dim3(kWave), sizeof(CodeLds), s, a, P.flist);
-        return;
-    }
-    if (P.ntiles <= 0) return;
-    const uint32_t lt_n = P.dict_entries_cap;
-    const uint32_t lds = kTailWaves * static_cast<uint32_t>(sizeof(CodeLds)) + (lt_n * 2 + 15) / 16 * 16;
-    const void* fn = reinterpret_cast<const void*>(k_pipe_tail);
-    ensure_dyn_lds(fn, lds);
-    const int bpc = max(1, resident_blocks(fn, kTailWaves * kWave, lds));
-    const int need = (P.ntiles + kTailWaves * 8 - 1) / (kTailWaves * 8);  // >= 8 tiles per wave
-    hipLaunchKernelGGL(k_pipe_tail, dim3(max(1, min(need, P.cus * bpc))), dim3(kTailWaves * kWave), lds, s, a, P.flist, lt_n);
-}
-
-int pipe_fused_tiles() { return kFuseTiles; }
-int pipe_fused_super() { return kFSuper; }
-
-static uint32_t fused_wave_lds(uint32_t stage) {
-    const uint32_t dec = static_cast<uint32_t>(sizeof(FuseDecLds)) + stage;
-    return (max(dec, static_cast<uint32_t>(sizeof(WriteLds))) + 15) / 16 * 16;
-}
-
-PipePlan plan_pipe_fused(uint32_t dict_bytes, int wpw, uint32_t stage) {
-    PipePlan pl{};
-    pl.lds = dict_bytes + static_cast<uint32_t>(wpw) * fused_wave_lds(stage);
-    pl.blocks_per_cu = pl.lds <= 160u * 1024 ? static_cast<int>((160u * 1024) / pl.lds) : 0;
-    if (pl.blocks_per_cu > 4) pl.blocks_per_cu = 4;
-    if (pl.blocks_per_cu > 0) {
-        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_fused<false>), pl.lds);
-        const int occ = resident_blocks(reinterpret_cast<const void*>(k_pipe_fused<false>), wpw * kWave, pl.lds);
-        pl.blocks_per_cu = min(pl.blocks_per_cu, occ);
-    }
-    return pl;
-}
-
-void launch_pipe_fused(hipStream_t s, const PipeLaunch& P) {
-    if (P.ntiles <= 0 || P.nunits <= 0) return;
-    int wgrid = 0, per = 0;
-    write_shape(P, &wgrid, &per);
-    if (P.has_small) {  // pages k_pipe_runs listed: the exact decoder writes their codes first
-        CodeArgs ca{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
-                    P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-                    P.bsum, per, P.debug, P.write_waves};
-        hipLaunchKernelGGL(k_pipe_exact, dim3(max(1, min(P.cus, P.npages))), dim3(kWave), sizeof(CodeLds), s, ca, P.flist);
-    }
-    FusedArgs a{};
-    a.bytes = P.bytes; a.pages = P.pages; a.tiles = P.tiles; a.ntiles = P.ntiles; a.page_tile0 = P.page_tile0;
-    a.max_def = P.max_def; a.dicts = P.dicts; a.dict_id = P.dict_id; a.entries = P.entries; a.dict_count = P.dict_count;
-    a.runs = P.runs; a.info = P.info; a.tile_nn = P.tile_nn; a.codes = P.codes; a.page_err = P.page_err;
-    a.err_any = P.err_any; a.nrows_total = P.nrows_total; a.total = P.total; a.capacity = P.capacity;
-    a.overflow = P.overflow; a.validity = P.validity; a.offsets = P.offsets; a.chars = P.chars;
-    a.dict_chars_bytes = P.dict_chars_bytes; a.dict_bytes = P.dict_bytes; a.wave_lds = fused_wave_lds(P.fstage);
-    a.stage_bytes = P.fstage; a.nunits = P.nunits; a.ticket = P.fticket; a.status = P.fstatus;
-    a.znext = P.znext; a.znext_words = P.znext_words; a.match = P.match; a.match_neg = P.match_neg;
-    a.page_flags = P.page_flags; a.debug = P.debug;
-    const int waves = max(1, P.fwaves);
-    const int grid = max(1, min(P.fgrid, (P.nunits + waves - 1) / waves));
-    if (P.match) {
-        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_fused<true>), P.flds);
-        hipLaunchKernelGGL(k_pipe_fused<true>, dim3(grid), dim3(waves * kWave), P.flds, s, a);
-    } else {
-        ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_fused<false>), P.flds);
-        hipLaunchKernelGGL(k_pipe_fused<false>, dim3(grid), dim3(waves * kWave), P.flds, s, a);
-    }
 }
 
 void launch_pipe_match(hipStream_t s, const PipeLaunch& P, const uint8_t* match, int neg, uint8_t* page_flags,

@@ -176,13 +176,6 @@ struct PipeLaunch {
     const uint8_t* match = nullptr;  // armed page filter (k_pipe_write), dictionary payloads < kArmDictBytes
     int match_neg = 0;
     uint8_t* page_flags = nullptr;
-    // k_pipe_fused (codes + write in one pass): zeroed ticket / look-back
-    // words of the decode, its units, payload stage, LDS, grid and waves
-    int32_t* fticket = nullptr;
-    unsigned long long* fstatus = nullptr;
-    int32_t nunits = 0;
-    uint32_t fstage = 0, flds = 0;
-    int fgrid = 0, fwaves = 0;
     // wide dictionaries (k_pipe_big<true> -> k_pipe_wwide): 32-bit codes
     // here (0xFFFFFFFF = NULL) instead of `codes`; P.lds / P.grid are then
     // plan_pipe_wide's
@@ -195,8 +188,6 @@ struct PipeLaunch {
     // the same dictionary as 16-byte slots (launch_dict_big's pad16), or
     // null: k_pipe_wwide then reads entry words and characters
     const uint4* pad16 = nullptr;
-    // k_pipe_write sums every tile's characters itself (k_pipe_win files none)
-    bool self_sum = false;
 };
 constexpr uint32_t kArmDictBytes = 32768;  // every entry length < 2^15: the match bit rides in the entry word
 struct PipePlan {
@@ -207,14 +198,6 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw);
 // k_pipe_wwide (dictionary in HBM): per-wave scratch only (pad: + the rows'
 // 16-byte entry slots, k_pipe_wwide<true>)
 PipePlan plan_pipe_wide(int wpw, bool pad);
-// k_pipe_fused: tiles per unit, and its LDS / resident workgroups per CU for
-// `wpw` waves per workgroup and a payload stage of `stage` bytes per wave
-int pipe_fused_tiles();
-int pipe_fused_super();  // units per superblock of k_pipe_fused's two-level prefix
-PipePlan plan_pipe_fused(uint32_t dict_bytes, int wpw, uint32_t stage);
-// codes and write in one pass (after k_pipe_runs / k_pipe_big / the count
-// pass; the exact decoder runs first, inside, over the pages k_pipe_runs listed)
-void launch_pipe_fused(hipStream_t s, const PipeLaunch& P);
 // Dictionary pages for k_pipe_runs' leading workgroups (4 waves each; pages
 // up to kRunDictMax bytes), so the dictionary decodes inside the run-table
 // launch instead of a k_dict_index launch on a side stream.
@@ -232,20 +215,7 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
                       const RunDicts* dicts = nullptr, uint32_t stage_max = 0,  // 0: k_pipe_codes3's stage
                       uint32_t slot_max = 0, uint32_t dict_max = 0, int cus = 256);  // pages_per_wave 0: auto
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
-// k_pipe_win: the whole front (run headers -> u16 codes, no characters) of
-// chunks whose pages hold <= kTileRows rows with max_def <= 1 and no rep
-// levels, one wavefront per window of <= wp consecutive pages whose slots
-// (pipe_win_slot bytes each) span <= wbytes; rc run records per stream.
-// k_pipe_exact then decodes the pages it listed; k_pipe_write must run with
-// self_sum.  The leading workgroups decode `dicts` (or null) as k_pipe_runs'.
-uint32_t pipe_win_slot(uint32_t page_bytes);
-uint32_t pipe_win_lds(uint32_t wbytes, uint32_t wp, uint32_t rc, uint32_t dict_max);
-bool pipe_win_shape_ok(uint32_t wp, uint32_t rc);
 struct DevBatch;
-void launch_pipe_win(hipStream_t s, const PipeLaunch& P, const DevBatch* wins, int nwins, uint32_t wbytes, uint32_t wp,
-                     uint32_t rc, const RunDicts* dicts, uint32_t dict_max);
-// the pages k_pipe_win listed, once the dictionary is decoded
-void launch_pipe_exact(hipStream_t s, const PipeLaunch& P);
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,
 // then codes and tile characters (one workgroup per listed page)

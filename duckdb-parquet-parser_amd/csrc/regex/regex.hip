@@ -480,11 +480,9 @@ __global__ void __launch_bounds__(256) k_regex_lanes(const uint8_t* __restrict__
 //             bare row offsets (the accept-at-end flag sits in column 256 of
 //             a row, read once per string), and the per-byte end-of-string
 //             selects are kept out of SGPR masks (C3: 0.119 ms, was 0.166).
-// waves per workgroup: as many as the LDS holds (host); with the next
-// window's bytes prefetched into registers (kPre) <= 3 per SIMD (VGPRs),
-// without <= 4
+// waves per workgroup: as many as the LDS holds (host), <= 3 per SIMD (the
+// next window's bytes ride in registers)
 constexpr uint32_t kPlainWavesMax = 12;
-constexpr uint32_t kPlainWavesMaxNp = 16;
 constexpr uint32_t kStrPerLane = 4;  // strings interleaved per lane (independent DFA chains)
 
 // The u32 at byte a of the staged window (>= 8 readable bytes past a).
@@ -498,8 +496,8 @@ __device__ __forceinline__ uint32_t st_u32(const uint32_t* st, uint32_t a) {
 // kSink (anchored patterns, full tables): a batch stops after its first block
 // once every longer string sits in an absorbing state (DEAD); a template
 // parameter, as the test costs unanchored patterns more than it saves
-template <bool kPre, bool kSink = false>
-__global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
+template <bool kSink>
+__global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8_t* __restrict__ dfa_img,
                                                                   uint32_t dfa_bytes, uint32_t win_bytes,
                                                                   const uint8_t* __restrict__ bytes,
                                                                   const DevPage* __restrict__ pages,
@@ -632,7 +630,7 @@ __global__ void __launch_bounds__((kPre ? kPlainWavesMax : kPlainWavesMaxNp) * 6
         if (wn < nwins) {
             if (lane() < static_cast<uint32_t>(Bn.np)) pgn = pages[Bn.p0 + static_cast<int32_t>(lane())];
             if (wn + nwt < nwins) Bnn = wins[wn + nwt];
-            held = kPre && Bn.img_bytes <= kPrefetchBlocks * kWave * 16;
+            held = Bn.img_bytes <= kPrefetchBlocks * kWave * 16;
             if (held) {  // (clamped indices: unconditional loads, no branch around them)
                 const uint4* src = reinterpret_cast<const uint4*>(bytes + Bn.img_lo);
                 const uint32_t nb = Bn.img_bytes / 16, b = lane();
@@ -1048,40 +1046,28 @@ void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, c
                        dicts, dict_count, dict_match, cp, neg, page_flags, page_err, err_any);
 }
 
-uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes, bool pre) {
+uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes) {
     const uint32_t per = regex_plain_wave_lds(win_bytes);
     if (dfa_bytes + per > 160u * 1024) return 0;
-    return std::min<uint32_t>(pre ? kPlainWavesMax : kPlainWavesMaxNp, (160u * 1024 - dfa_bytes) / per);
+    return std::min<uint32_t>(kPlainWavesMax, (160u * 1024 - dfa_bytes) / per);
 }
 
-uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes, bool pre) {
-    return dfa_bytes + regex_plain_waves(dfa_bytes, win_bytes, pre) * regex_plain_wave_lds(win_bytes);
+uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes) {
+    return dfa_bytes + regex_plain_waves(dfa_bytes, win_bytes) * regex_plain_wave_lds(win_bytes);
 }
 
 void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
                         const uint8_t* bytes, const DevPage* pages, const pqk::DevBatch* wins, int nwins,
                         int32_t* ticket, int grid, ColumnParams cp, int neg, uint8_t* page_flags,
-                        DevErr* page_err, int32_t* err_any, const uint16_t* index_in, uint16_t* index_out, bool pre,
-                        bool sink) {
+                        DevErr* page_err, int32_t* err_any, const uint16_t* index_in, uint16_t* index_out, bool sink) {
     if (nwins <= 0) return;
-    const void* k = pre ? (sink ? reinterpret_cast<const void*>(k_regex_plain<true, true>)
-                                : reinterpret_cast<const void*>(k_regex_plain<true>))
-                        : reinterpret_cast<const void*>(k_regex_plain<false>);
-    pqk::ensure_dyn_lds(k, 160 * 1024);
-    if (pre && sink) {
-        void (*fn)(const uint8_t*, uint32_t, uint32_t, const uint8_t*, const DevPage*, const pqk::DevBatch*, int, int32_t*,
-                   ColumnParams, int, uint8_t*, DevErr*, int32_t*, const uint16_t*, uint16_t*) = k_regex_plain<true, true>;
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes, true) * kWave),
-                           regex_plain_lds(dfa_bytes, win_bytes, true), s, dfa, dfa_bytes, win_bytes, bytes, pages, wins,
-                           nwins, ticket, cp, neg, page_flags, page_err, err_any, index_in, index_out);
-    } else if (pre)
-        hipLaunchKernelGGL(k_regex_plain<true>, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes, true) * kWave),
-                           regex_plain_lds(dfa_bytes, win_bytes, true), s, dfa, dfa_bytes, win_bytes, bytes, pages, wins,
-                           nwins, ticket, cp, neg, page_flags, page_err, err_any, index_in, index_out);
-    else
-        hipLaunchKernelGGL(k_regex_plain<false>, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes, false) * kWave),
-                           regex_plain_lds(dfa_bytes, win_bytes, false), s, dfa, dfa_bytes, win_bytes, bytes, pages, wins,
-                           nwins, ticket, cp, neg, page_flags, page_err, err_any, index_in, index_out);
+    void (*fn)(const uint8_t*, uint32_t, uint32_t, const uint8_t*, const DevPage*, const pqk::DevBatch*, int, int32_t*,
+               ColumnParams, int, uint8_t*, DevErr*, int32_t*, const uint16_t*, uint16_t*) =
+        sink ? k_regex_plain<true> : k_regex_plain<false>;
+    pqk::ensure_dyn_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(regex_plain_waves(dfa_bytes, win_bytes) * kWave),
+                       regex_plain_lds(dfa_bytes, win_bytes), s, dfa, dfa_bytes, win_bytes, bytes, pages, wins, nwins, ticket,
+                       cp, neg, page_flags, page_err, err_any, index_in, index_out);
 }
 
 // k_regex_plain reads its byte-state table through a constant LDS address
@@ -1091,8 +1077,7 @@ void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, u
 bool regex_plain_lds_ok() {
     static const bool ok = [] {
         hipFuncAttributes a{};
-        for (const void* k : {reinterpret_cast<const void*>(k_regex_plain<true>), reinterpret_cast<const void*>(k_regex_plain<false>),
-                              reinterpret_cast<const void*>(k_regex_plain<true, true>)})
+        for (const void* k : {reinterpret_cast<const void*>(k_regex_plain<true>), reinterpret_cast<const void*>(k_regex_plain<false>)})
             if (hipFuncGetAttributes(&a, k) != hipSuccess || a.sharedSizeBytes != 0) return false;
         return true;
     }();

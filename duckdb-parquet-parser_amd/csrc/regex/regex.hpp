@@ -82,16 +82,15 @@ bool build_dfa(const Program& p, std::vector<uint8_t>* image);
 // window (+32 zero bytes), a u16 offset per possible string, per-page counts,
 // list bases and kept counts, the hit mask.
 constexpr uint32_t regex_plain_wave_lds(uint32_t win_bytes) { return win_bytes + 32 + win_bytes / 2 + 3 * 64 * 4 + 16; }
-uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes, bool pre);
-uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes, bool pre);
+uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes);
+uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes);
 int regex_plain_occupancy(uint32_t lds);
 bool regex_plain_lds_ok();  // k_regex_plain's constant-address LDS table is valid (no static LDS)
 void launch_regex_plain(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, uint32_t win_bytes,
                         const uint8_t* bytes, const pqk::DevPage* pages, const pqk::DevBatch* wins, int nwins,
                         int32_t* ticket, int grid, pqk::ColumnParams cp, int neg, uint8_t* page_flags,
                         pqk::DevErr* page_err, int32_t* err_any,
-                        const uint16_t* index_in = nullptr, uint16_t* index_out = nullptr, bool pre = true,
-                        bool sink = false);
+                        const uint16_t* index_in = nullptr, uint16_t* index_out = nullptr, bool sink = false);
 
 void launch_regex_lanes(hipStream_t s, const uint8_t* dfa, uint32_t dfa_bytes, const uint8_t* bytes,
                         const pqk::DevPage* pages, int npages, const pqk::DevDict* dicts,

@@ -104,6 +104,60 @@ public:
         return e2;
     }
 
+    // The reverse direction: n bytes from HBM at d_src in pieces through the
+    // ring; sink(src, a, b) consumes bytes [a, b) from the pinned buffer src
+    // (b - a <= the piece) on one of `threads` host threads, and the thread
+    // that drained a buffer queues the next piece into it.  Returns when every
+    // piece is consumed.
+    template <class Sink>
+    hipError_t download(const uint8_t* d_src, size_t n, hipStream_t stream, int threads, Sink&& sink) {
+        if (n == 0) return hipSuccess;
+        hipError_t e = ensure();
+        if (e != hipSuccess) return e;
+        const size_t kPiece = piece_;
+        const size_t kBufs = static_cast<size_t>(bufs_);
+        const size_t npieces = (n + kPiece - 1) / kPiece;
+        std::mutex m;
+        std::condition_variable cv;
+        std::vector<char> queued(npieces, 0);
+        std::atomic<int> err{hipSuccess};
+        auto queue = [&](size_t i) {  // (under m)
+            const size_t a = i * kPiece, z = std::min(n, a + kPiece);
+            hipError_t r = hipMemcpyAsync(buf_[i % kBufs], d_src + a, z - a, hipMemcpyDeviceToHost, stream);
+            if (r == hipSuccess) r = hipEventRecord(ev_[i % kBufs], stream);
+            if (r != hipSuccess) err.store(r);
+            queued[i] = 1;
+        };
+        {
+            std::lock_guard<std::mutex> lk(m);
+            for (size_t i = 0; i < std::min(kBufs, npieces); i++) queue(i);
+        }
+        std::atomic<size_t> next{0};
+        auto worker = [&]() {
+            for (size_t i = next.fetch_add(1); i < npieces; i = next.fetch_add(1)) {
+                {
+                    std::unique_lock<std::mutex> lk(m);
+                    cv.wait(lk, [&] { return queued[i] != 0 || err.load() != hipSuccess; });
+                }
+                if (err.load() != hipSuccess) return;
+                const int b = static_cast<int>(i % kBufs);
+                hipError_t r = hipEventSynchronize(ev_[b]);
+                if (r != hipSuccess) { err.store(r); cv.notify_all(); return; }
+                const size_t a = i * kPiece, z = std::min(n, a + kPiece);
+                sink(buf_[b], a, z);
+                std::lock_guard<std::mutex> lk(m);
+                if (i + kBufs < npieces) queue(i + kBufs);
+                cv.notify_all();
+            }
+        };
+        threads = static_cast<int>(std::max<size_t>(1, std::min<size_t>(static_cast<size_t>(threads), npieces)));
+        std::vector<std::thread> th;
+        for (int t = 1; t < threads; t++) th.emplace_back(worker);
+        worker();
+        for (auto& x : th) x.join();
+        return static_cast<hipError_t>(err.load());
+    }
+
 private:
     hipError_t ensure() {
         for (int b = 0; b < bufs_; b++) {

@@ -58,6 +58,8 @@ struct ColumnMetaData {
     ParquetType type = ParquetType::INT32;
     CompressionCodec codec = CompressionCodec::UNCOMPRESSED;
     int64_t num_values = 0;
+    int64_t total_uncompressed_size = 0;
+    int64_t total_compressed_size = 0;  // 0: unknown (the chunk is read header by header)
     int64_t data_page_offset = 0;
     std::optional<int64_t> dictionary_page_offset;
 };
@@ -93,12 +95,25 @@ private:
 
 // Decoded column as device-independent host arrays (the columnar fast path:
 // no std::vector<Value> materialisation).
+// Host arrays whose resize leaves new elements uninitialised (the device
+// copy writes them; a zero fill first would touch every page on one thread).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInitAlloc<U>; };
+    NoInitAlloc() = default;
+    template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+template <class T>
+using HostVec = std::vector<T, NoInitAlloc<T>>;
+
 struct HostColumn {
     ParquetType type = ParquetType::INT32;
     int64_t num_rows = 0;
-    std::vector<uint32_t> validity;  // LSB-first bitmap
-    std::vector<uint8_t> values;     // fixed-width values or chars
-    std::vector<int64_t> offsets;    // BYTE_ARRAY: num_rows + 1
+    HostVec<uint32_t> validity;  // LSB-first bitmap
+    HostVec<uint8_t> values;     // fixed-width values or chars
+    HostVec<int64_t> offsets;    // BYTE_ARRAY: num_rows + 1
     bool valid(int64_t i) const { return (validity[i >> 5] >> (i & 31)) & 1u; }
     Value value(int64_t i) const;    // reference Value semantics (INT96 -> "INT96(hi:lo)")
 };

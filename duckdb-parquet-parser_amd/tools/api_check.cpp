@@ -130,6 +130,7 @@ int main(int argc, char** argv) {
             md.type = static_cast<pqgpu::ParquetType>(d.type);
             md.num_values = d.num_values;
             md.data_page_offset = d.data_page_offset;
+            md.total_compressed_size = d.total_compressed_size;
             if (d.has_dictionary_page_offset) md.dictionary_page_offset = d.dictionary_page_offset;
             cc.meta_data = md;
             pqgpu::ColumnReader cr([&](size_t off, size_t len) { return r.read_range(off, len); }, cc,
@@ -166,10 +167,17 @@ int main(int argc, char** argv) {
                 if (!fh) throw std::runtime_error("cannot write the dump");
                 std::fwrite(out.data(), 1, out.size(), fh);
                 std::fclose(fh);
+                auto list = [](const std::vector<double>& v) {
+                    std::string r = "[";
+                    for (size_t i = 0; i < v.size(); i++) r += (i ? ", " : "") + std::to_string(v[i]);
+                    return r + "]";
+                };
                 std::printf("{\"values\": %zu, \"read_all_ms\": %.4f, \"read_columnar_ms\": %.4f, "
-                            "\"to_values_ms\": %.4f, \"threads\": %u}\n",
+                            "\"to_values_ms\": %.4f, \"threads\": %u, \"read_all_samples\": %s, "
+                            "\"to_values_samples\": %s}\n",
                             vals.size(), med(ta), med(tc), med(tv),
-                            std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+                            std::max(1u, std::min(16u, std::thread::hardware_concurrency())), list(ta).c_str(),
+                            list(tv).c_str());
                 return 0;
             } else {
                 for (const auto& pr : cr.read_pages()) {

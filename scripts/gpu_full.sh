@@ -5,7 +5,7 @@
 # (pytest rc 1) still go on to the measurements; a crash, abort or time limit
 # of any step ends the call.
 set -o pipefail
-TAG=${1:-r4}
+TAG=${1:-r5}
 shift || true
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/$TAG

@@ -25,12 +25,11 @@ def ctx():
 
 
 # Kernel-path fixtures shared by the GPU parity tests.
-@pytest.fixture(params=["default", "pfused", "front", "big", "fused", "generic", "serial"])
+@pytest.fixture(params=["default", "big", "fused", "generic", "serial"])
 def path(request, ctx):
     """Every kernel path that ships: "default" = what a chunk takes with the
     default options (dictionary BYTE_ARRAY on dict_pipe.hip: the run-table
-    passes k_pipe_runs + k_pipe_codes3 + k_pipe_write; "front" puts chunks of
-    <= 512-row pages through the windowed k_pipe_front instead; two-pass
+    passes k_pipe_runs + k_pipe_codes3 + k_pipe_write; two-pass
     PLAIN BYTE_ARRAY, plain_ba.hip; tile-parallel PLAIN fixed width,
     fixed_fast.hip; the fused and generic kernels for chunks neither
     takes); "big" puts every page of a dictionary chunk through k_pipe_big
@@ -40,13 +39,11 @@ def path(request, ctx):
     per-page k_fixed (dictionary chunks: rows by k_wide_rows, a workgroup per
     page); "serial" is "generic" with the wave-per-page k_ba_rows, the byte-wise
     gather and k_fixed_levels2's large-LDS form.  PLAIN BYTE_ARRAY chunks take the one-pass kernel
-    (k_plain_fused) under "default" and the two passes under "big".  "pfused" is "default" with
-    the pipe's codes and write passes in one kernel (k_pipe_fused)."""
+    (k_plain_fused) under "default" and the two passes under "big"."""
     p = request.param
-    ctx.set_option("pipe_fused", int(p == "pfused"))
     ctx.set_option("big_all", int(p == "big"))
-    ctx.set_option("dict_pipe", int(p in ("default", "pfused", "front", "big")))
-    ctx.set_option("plain_ba", int(p in ("default", "pfused", "front", "big")))
+    ctx.set_option("dict_pipe", int(p in ("default", "big")))
+    ctx.set_option("plain_ba", int(p in ("default", "big")))
     ctx.set_option("fused_ba", int(p not in ("generic", "serial")))
     ctx.set_option("fixed_plain", int(p not in ("generic", "serial")))
     ctx.set_option("wide_rows", int(p != "serial"))
@@ -54,33 +51,27 @@ def path(request, ctx):
     ctx.set_option("levels_small", int(p != "serial"))
     ctx.set_option("plain_fused", int(p != "big"))
     ctx.set_option("fixed_fused", int(p == "big"))
-    ctx.set_option("pipe_front", int(p == "front"))
     yield p
-    ctx.set_option("pipe_fused", 0)
     for k in ("dict_pipe", "plain_ba", "fused_ba", "fixed_plain", "plain_fused"):
         ctx.set_option(k, 1)
     ctx.set_option("fixed_fused", 0)
-    ctx.set_option("pipe_front", 0)
     ctx.set_option("big_all", 0)
     ctx.set_option("wide_rows", 1)
     ctx.set_option("gather_rows", 1)
     ctx.set_option("levels_small", 1)
 
 
-@pytest.fixture(params=["window", "codes", "codes_front", "lanes", "nfa"])
+@pytest.fixture(params=["window", "codes", "lanes", "nfa"])
 def kernel(request, ctx):
     """Every page kernel: windowed DFA (default for chunks without dictionary
     pages), match bits over the pipe decode's codes (default for dictionary
-    chunks the pipe path takes; "codes" with the run-table passes' codes,
-    "codes_front" with k_pipe_front's where the pages allow it), lane-per-page
+    chunks the pipe path takes; "codes" with the run-table passes' codes), lane-per-page
     DFA (other dictionary chunks) and wave-per-page NFA (patterns whose DFA is
     over its size cap)."""
     ctx.set_option("regex_dfa", int(request.param != "nfa"))
     ctx.set_option("regex_plain", int(request.param == "window"))
-    ctx.set_option("regex_codes", int(request.param in ("window", "codes", "codes_front")))
-    ctx.set_option("pipe_front", int(request.param == "codes_front"))
+    ctx.set_option("regex_codes", int(request.param in ("window", "codes")))
     yield request.param
     ctx.set_option("regex_dfa", 1)
     ctx.set_option("regex_plain", 1)
     ctx.set_option("regex_codes", 1)
-    ctx.set_option("pipe_front", 0)

@@ -111,7 +111,7 @@ def test_regex_reuses_checked_decode_codes(ctx, layout, nrg):
     exp = {(p, n): golden_pages(f, chunks, p, n) for p in pats for n in (False, True)}
     dc.decode()
     ref = capi.canonical_dump(dc.to_host())
-    fronts = ("dict_index", "pipe_runs", "pipe_codes", "pipe_front", "pipe_big", "pipe_count")
+    fronts = ("dict_index", "pipe_runs", "pipe_codes", "pipe_big", "pipe_count")
     ctx.timing(True)
     ctx.timing_reset()
     dc.decode()
@@ -242,46 +242,6 @@ def test_string_index_reuse(ctx, layout, rpp):
     finally:
         ctx.set_option("regex_win", 8192)
         ctx.set_option("regex_index", 1)
-        dc.free()
-
-
-@pytest.mark.parametrize("name", ["c3_ref", "c3_arrow", "c3_optional"])
-def test_regex_prefetch_off(ctx, name):
-    """Option regex_prefetch 0: the windowed kernel's lighter build (no next
-    window in registers, four waves per SIMD where the LDS allows) gives the
-    oracle's page sets, cold and warm, and the same error text."""
-    _, cols, n, layout = next(c for c in CASES if c[0] == name)
-    f = gen.build(cols, n, 2, seed=7, layout=layout, rows_per_page=700)
-    chunks = file_chunks(f, 0)
-    pats = ["special.*requests", "e", "^(carefully|quickly) ", "[0-9]", "^$", "x*"]
-    dc = ctx.upload(f, chunks)
-    try:
-        ctx.set_option("regex_prefetch", 0)
-        for win in (8192, 5888):
-            ctx.set_option("regex_win", win)
-            for idx in (2, 1, 1):  # a cold scan that files the index, then warm ones
-                ctx.set_option("regex_index", idx)
-                for p in pats:
-                    for neg in (False, True):
-                        assert np.array_equal(dc.regex_pages(p, neg), golden_pages(f, chunks, p, neg)), (win, idx, p, neg)
-    finally:
-        ctx.set_option("regex_prefetch", 1)
-        ctx.set_option("regex_win", 8192)
-        ctx.set_option("regex_index", 1)
-        dc.free()
-    import struct
-    import pqbuild as B
-    pay = struct.pack("<I", 7) + b"special" + struct.pack("<I", 50) + b"xy"
-    f, ch = B.build_file([B.data_header(len(pay), 2, 0) + pay], gen.BYTE_ARRAY, False, 2)
-    rc_o, msg_o, _ = O.read_all(f, to_oracle_chunk(ch))
-    dc = ctx.upload(f, [to_desc(ch)])
-    try:
-        ctx.set_option("regex_prefetch", 0)
-        with pytest.raises(capi.PqError) as ei:
-            dc.regex_pages("special", False)
-        assert ei.value.code == rc_o and ei.value.msg == msg_o
-    finally:
-        ctx.set_option("regex_prefetch", 1)
         dc.free()
 
 
