@@ -986,6 +986,96 @@ int pq_build_page_table(const uint8_t* file, size_t file_len, const pq_chunk_des
     }
 }
 
+int pq_build_page_table_device(pq_ctx* ctx, const uint8_t* d_bytes, size_t len, int64_t base,
+                               const pq_chunk_desc* chunk, int64_t seg_bytes, int64_t rec_cap,
+                               pq_page_desc* pages, int64_t cap, int64_t* npages) {
+    if (!ctx || !chunk || !npages || (!d_bytes && len) || base < 0 || seg_bytes < 0 || rec_cap < 0 || cap < 0 ||
+        (cap && !pages))
+        return PQ_ERR_ARG;
+    *npages = 0;
+    if (chunk->codec != 0 || chunk->ext_flags != 0 || chunk->num_values <= 0) return PQ_ERR_UNSUPPORTED;
+    int64_t off = chunk->data_page_offset;
+    if (chunk->has_dictionary_page_offset) off = std::min(off, chunk->dictionary_page_offset);
+    if (off < base || off >= base + static_cast<int64_t>(len)) return PQ_ERR_UNSUPPORTED;
+    DevGuard dg(ctx);
+    const uint64_t seg = seg_bytes ? static_cast<uint64_t>(seg_bytes) : 8192u;
+    const uint32_t rc = static_cast<uint32_t>(rec_cap ? rec_cap : std::max<int64_t>(1, static_cast<int64_t>(seg) / 128));
+    const uint64_t start = static_cast<uint64_t>(off), end = static_cast<uint64_t>(base) + len;
+    const uint64_t nseg64 = (end - start + seg - 1) / seg;
+    if (nseg64 > (1u << 30) / rc) return PQ_ERR_UNSUPPORTED;
+    const uint32_t nseg = static_cast<uint32_t>(nseg64);
+    try {
+        pqk::WalkLaunch W{};
+        W.bytes = d_bytes; W.base = static_cast<uint64_t>(base); W.len = len;
+        W.start = start; W.end = end; W.seg = seg; W.nseg = nseg; W.cap = rc;
+        W.num_values = chunk->num_values;
+        const size_t nrec = static_cast<size_t>(nseg) * rc;
+        // one allocation: records, segments, links, bases, the page table
+        auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+        const size_t o_recs = 0, o_segs = o_recs + al(nrec * sizeof(pqk::WalkRec));
+        const size_t o_links = o_segs + al(nseg * pqk::walk_seg_bytes());
+        const size_t o_bases = o_links + al(nseg * pqk::walk_link_bytes());
+        const size_t o_out = o_bases + al(3 * static_cast<size_t>(nseg) * 8);
+        const size_t o_pages = o_out + 256, total = o_pages + al(nrec * sizeof(pq_page_desc));
+        uint8_t* mem = nullptr;
+        if (int rc2 = hip_check(ctx, hipMalloc(reinterpret_cast<void**>(&mem), total), "hipMalloc (device walk)")) return rc2;
+        W.recs = reinterpret_cast<pqk::WalkRec*>(mem + o_recs);
+        W.segs = mem + o_segs;
+        W.links = mem + o_links;
+        W.base_pg = reinterpret_cast<int64_t*>(mem + o_bases);
+        W.base_val = W.base_pg + nseg;
+        W.dict_in = W.base_val + nseg;
+        W.out = reinterpret_cast<int64_t*>(mem + o_out);
+        W.pages = reinterpret_cast<pq_page_desc*>(mem + o_pages);
+        {
+            Timed t(ctx, "walk");
+            pqk::launch_walk(ctx->stream, W);
+        }
+        int64_t res[8] = {-1, -1, 0, 0, 0, 0, 0, 0};
+        int rc2 = hip_check(ctx, hipGetLastError(), "walk launch");
+        if (!rc2) rc2 = hip_check(ctx, hipMemcpyAsync(res, W.out, sizeof res, hipMemcpyDeviceToHost, ctx->stream), "walk result");
+        if (!rc2) rc2 = hip_check(ctx, hipStreamSynchronize(ctx->stream), "walk sync");
+        if (std::getenv("PQ_WALK_DEBUG"))
+            std::fprintf(stderr, "walk: pages %lld cut %lld entry %lld n %lld exit %lld bad %lld prev_exit %lld first %lld (start %llu seg %llu)\n",
+                         (long long)res[0], (long long)res[1], (long long)res[2], (long long)res[3], (long long)res[4],
+                         (long long)res[5], (long long)res[6], (long long)res[7], (unsigned long long)start,
+                         (unsigned long long)seg);
+        if (!rc2 && res[0] >= 0) {
+            *npages = res[0];
+            const int64_t k = std::min(cap, res[0]);
+            if (k > 0)
+                rc2 = hip_check(ctx, hipMemcpy(pages, W.pages, static_cast<size_t>(k) * sizeof(pq_page_desc), hipMemcpyDeviceToHost),
+                                "walk copy");
+        }
+        (void)hipFree(mem);
+        if (rc2) return rc2;
+        return res[0] >= 0 ? 0 : PQ_ERR_UNSUPPORTED;
+    } catch (const std::exception& e) {
+        return set_err(ctx, PQ_ERR_ALLOC, e.what());
+    }
+}
+
+int pq_device_buffer(pq_ctx* ctx, const uint8_t* host, size_t n, void** d_out) {
+    if (!ctx || !d_out || (!host && n)) return PQ_ERR_ARG;
+    DevGuard dg(ctx);
+    uint8_t* d = nullptr;
+    if (int rc = hip_check(ctx, hipMalloc(reinterpret_cast<void**>(&d), n + 64), "hipMalloc (device buffer)")) return rc;
+    int rc = hip_check(ctx, hipMemset(d + n, 0, 64), "device buffer pad");
+    if (!rc && n) rc = hip_check(ctx, hipMemcpy(d, host, n, hipMemcpyHostToDevice), "device buffer copy");
+    if (rc) {
+        (void)hipFree(d);
+        return rc;
+    }
+    *d_out = d;
+    return 0;
+}
+
+void pq_device_buffer_free(pq_ctx* ctx, void* d) {
+    if (!ctx || !d) return;
+    DevGuard dg(ctx);
+    (void)hipFree(d);
+}
+
 // Raw path of an upload: the chunk's byte extents, exactly
 // as the file holds them, go to HBM (ctx->d_raw) through the pinned ring on a
 // host thread that starts before the page walk, so the H2D overlaps the walk

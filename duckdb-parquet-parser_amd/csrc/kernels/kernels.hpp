@@ -5,6 +5,8 @@
 
 #include <cstdint>
 
+#include "pq_gpu.h"
+
 namespace pqk {
 
 constexpr int kWave = 64;
@@ -217,6 +219,34 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
 struct DevBatch;
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
+// The page walk on the GPU (walk.hip): one header record per page a
+// segment's chain meets, the launch's buffers (nseg segments of `seg` bytes,
+// `cap` records each; segs / links: walk_seg_bytes() / walk_link_bytes() per
+// segment; base_pg / base_val / dict_in: nseg int64; out: 2 int64 (pages or
+// -1 = refused, cut segment); pages: the page table, <= nseg * cap entries).
+struct WalkRec {
+    uint64_t pos;
+    uint32_t hs;
+    int32_t comp, uncomp, type, nv, enc;
+    uint32_t flags;
+    uint32_t pad;
+};
+struct WalkLaunch {
+    const uint8_t* bytes;  // file bytes [base, base + len) in HBM
+    uint64_t base, len;
+    uint64_t start, end;   // the chain's first page and the extent's end (file offsets)
+    uint64_t seg;
+    uint32_t nseg, cap;
+    int64_t num_values;
+    WalkRec* recs;
+    void* segs;
+    void* links;
+    int64_t *base_pg, *base_val, *dict_in, *out;
+    pq_page_desc* pages;
+};
+size_t walk_seg_bytes();
+size_t walk_link_bytes();
+void launch_walk(hipStream_t s, const WalkLaunch& W);
 // pages of more than kPipeSmallRows rows: run tables by speculative parse,
 // then codes and tile characters (one workgroup per listed page)
 uint32_t pipe_big_lds(uint32_t max_page_bytes, uint32_t nlens);

@@ -1,0 +1,586 @@
+// walk.hip — the chunk's page walk on the GPU over bytes already in HBM
+// (the device page table; the host form is
+// csrc/host/format.cpp walk_chunk, whose page list this reproduces).
+//
+// The reference walks a column chunk's page chain serially: read the Thrift
+// PageHeader at the cursor, step over header and payload, until the data
+// pages' values reach ColumnMetaData.num_values
+// (src/reader/column_reader.cpp:18-71, src/reader/metadata.cpp:121-155).
+// Here the extent is cut into segments of `seg` bytes, one lane each:
+//   k_walk_seg    segment 0 starts at the chunk's first page; segment k > 0
+//                 at the first position of its range where a plausible header
+//                 begins a plausible three-page chain (format.cpp speculate's
+//                 rule); each lane records the headers its chain meets until
+//                 it leaves the segment (a 256-byte window per hop in LDS,
+//                 parsed with the host parser's exact acceptance rules);
+//   k_walk_link   segment k is entered where segment k - 1's chain left: the
+//                 record at that position (a false start converges or the
+//                 walk is refused), its chain records, data values and last
+//                 dictionary page;
+//   k_walk_scan   one workgroup: page and value prefixes over the segments,
+//                 the dictionary in force, the page where the values reach
+//                 num_values (the cut), every segment up to it linked;
+//   k_walk_emit   the pq_page_desc of every page up to the cut.
+// Anything the speculative chain cannot settle exactly (a page longer than a
+// segment, a header the parse refuses, an invalid header before the cut, a
+// chain that ends first, a segment over its record capacity) returns
+// "refused": the caller walks on the host, which also reports the
+// reference's errors.  Uncompressed V1 scope only (no PQ_EXT_* flags).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels/kernels.hpp"
+
+namespace pqk {
+namespace {
+
+constexpr uint32_t kWin = 256;          // header window (read_page_header's fixed window)
+constexpr uint32_t kWinStride = 65;     // dwords per lane window: 64 + 1 (LDS banks)
+constexpr int kWalkWaves = 1;           // one wave per workgroup (16.6 KiB of windows)
+constexpr uint32_t kScanLimit = 16384;  // bytes a segment scans for its first header (format.cpp kSpecScan)
+constexpr int kSkipDepth = 8;
+
+struct DHdr {
+    int32_t type, uncomp, comp, dnv, denc, dictnv;
+    uint32_t hs;
+    uint32_t flags;  // 1 has_data, 2 has_dict, 4 has_v2
+};
+
+// One lane's 256-byte window: bytes [0, avail) valid (zeros past the buffer).
+struct Win {
+    const uint8_t* w;
+    uint32_t p, e;
+    __device__ bool byte(uint32_t& v) {
+        if (p >= e) return false;
+        v = w[p++];
+        return true;
+    }
+    __device__ bool varint(uint64_t& r) {
+        r = 0;
+        for (int shift = 0;; shift += 7) {
+            if (shift > 63) return false;
+            uint32_t b;
+            if (!byte(b)) return false;
+            r |= static_cast<uint64_t>(b & 0x7Fu) << shift;
+            if ((b & 0x80u) == 0) return true;
+        }
+    }
+    __device__ bool i32(int32_t& v) {
+        uint64_t u;
+        if (!varint(u)) return false;
+        v = static_cast<int32_t>(static_cast<int64_t>((u >> 1) ^ (~(u & 1) + 1)));
+        return true;
+    }
+    // id = 0, type = 0 at STOP (a type nibble 0 ends the struct too: format.cpp FastHdr::field)
+    __device__ bool field(int32_t& last, int32_t& id, uint32_t& type) {
+        uint32_t b;
+        if (!byte(b)) return false;
+        if (b == 0) { id = 0; type = 0; return true; }
+        type = b & 0x0Fu;
+        const int32_t delta = static_cast<int32_t>((b >> 4) & 0x0Fu);
+        if (delta) {
+            id = static_cast<int16_t>(last + delta);
+        } else {
+            uint64_t u;
+            if (!varint(u)) return false;
+            id = static_cast<int16_t>(static_cast<int64_t>((u >> 1) ^ (~(u & 1) + 1)));
+        }
+        last = id;
+        if (type == 0) id = 0;
+        return true;
+    }
+    __device__ bool bytes(uint64_t n) {
+        if (n > static_cast<uint64_t>(e - p)) return false;
+        p += static_cast<uint32_t>(n);
+        return true;
+    }
+    // Thrift skip of a value of `type`, iterative (format.cpp FastHdr::skip;
+    // nesting past kSkipDepth refuses, which the walk treats as a parse failure)
+    __device__ bool skip(uint32_t type) {
+        // frame: kind 0 struct (last id), 1 list (remaining, elem type), 2 map (remaining pairs, kt, vt, half)
+        uint32_t kind[kSkipDepth], et[kSkipDepth], et2[kSkipDepth];
+        int64_t rem[kSkipDepth];
+        int32_t lastid[kSkipDepth];
+        int sp = 0;
+        uint32_t t = type;
+        for (;;) {
+            // a scalar or a container header for type t
+            bool pushed = false;
+            uint64_t u;
+            switch (t) {
+                case 1: case 2: break;
+                case 3: { uint32_t b; if (!byte(b)) return false; break; }
+                case 4: case 5: case 6: if (!varint(u)) return false; break;
+                case 7: if (!bytes(8)) return false; break;
+                case 8: if (!varint(u) || !bytes(static_cast<uint32_t>(u))) return false; break;
+                case 9: case 10: {
+                    uint32_t b;
+                    if (!byte(b)) return false;
+                    const uint32_t e1 = b & 0x0Fu;
+                    int64_t n = static_cast<int64_t>((b >> 4) & 0x0Fu);
+                    if (n == 0x0F) { if (!varint(u)) return false; n = static_cast<int32_t>(u); }
+                    if (e1 == 1 || e1 == 2 || n <= 0) break;  // bool elements take no bytes
+                    if (sp == kSkipDepth) return false;
+                    kind[sp] = 1; et[sp] = e1; rem[sp] = n; sp++;
+                    pushed = true;
+                    break;
+                }
+                case 11: {
+                    if (!varint(u)) return false;
+                    const int32_t n = static_cast<int32_t>(u);
+                    if (n <= 0) break;
+                    uint32_t kv;
+                    if (!byte(kv)) return false;
+                    const uint32_t kt = (kv >> 4) & 0x0Fu, vt = kv & 0x0Fu;
+                    if ((kt == 1 || kt == 2) && (vt == 1 || vt == 2)) break;
+                    if (sp == kSkipDepth) return false;
+                    kind[sp] = 2; et[sp] = kt; et2[sp] = vt; rem[sp] = 2 * static_cast<int64_t>(n); sp++;
+                    pushed = true;
+                    break;
+                }
+                case 12:
+                    if (sp == kSkipDepth) return false;
+                    kind[sp] = 0; lastid[sp] = 0; sp++;
+                    pushed = true;
+                    break;
+                default: return false;
+            }
+            (void)pushed;
+            // the next value to skip: from the innermost open container
+            for (;;) {
+                if (sp == 0) return true;
+                const int f = sp - 1;
+                if (kind[f] == 0) {
+                    int32_t id;
+                    uint32_t ft;
+                    if (!field(lastid[f], id, ft)) return false;
+                    if (ft == 0 && id == 0) { sp--; continue; }
+                    t = ft;
+                    break;
+                }
+                if (rem[f] == 0) { sp--; continue; }
+                rem[f]--;
+                t = kind[f] == 1 ? et[f] : ((rem[f] & 1) ? et[f] : et2[f]);  // map: key then value
+                break;
+            }
+        }
+    }
+};
+
+// format.cpp FastHdr::parse: true for every header read_page_header accepts
+// (identical fields), false where it would throw.
+__device__ bool dev_parse(const uint8_t* w, uint32_t avail, DHdr& h) {
+    Win c{w, 0, avail};
+    h = DHdr{0, 0, 0, 0, 0, 0, 0, 0};
+    int32_t last = 0;
+    for (;;) {
+        int32_t id;
+        uint32_t ty;
+        if (!c.field(last, id, ty)) return false;
+        if (ty == 0 && id == 0) break;
+        switch (id) {
+            case 1: if (!c.i32(h.type)) return false; break;
+            case 2: if (!c.i32(h.uncomp)) return false; break;
+            case 3: if (!c.i32(h.comp)) return false; break;
+            case 4: { int32_t x; if (!c.i32(x)) return false; break; }
+            case 5: {
+                h.flags |= 1u;
+                h.dnv = 0;
+                h.denc = 0;
+                int32_t l2 = 0;
+                for (;;) {
+                    int32_t i2;
+                    uint32_t t2;
+                    if (!c.field(l2, i2, t2)) return false;
+                    if (t2 == 0 && i2 == 0) break;
+                    int32_t x;
+                    if (i2 == 1) { if (!c.i32(h.dnv)) return false; }
+                    else if (i2 == 2) { if (!c.i32(h.denc)) return false; }
+                    else if (i2 == 3 || i2 == 4) { if (!c.i32(x)) return false; }
+                    else if (!c.skip(t2)) return false;
+                }
+                break;
+            }
+            case 8: {  // DataPageHeaderV2 (skipped by the reference: only its bytes)
+                if (ty != 12) {
+                    if (!c.skip(ty)) return false;
+                    break;
+                }
+                h.flags |= 4u;
+                int32_t l2 = 0;
+                for (;;) {
+                    int32_t i2;
+                    uint32_t t2;
+                    if (!c.field(l2, i2, t2)) return false;
+                    if (t2 == 0 && i2 == 0) break;
+                    int32_t x;
+                    if (t2 == 5 && (i2 == 1 || i2 == 4 || i2 == 5 || i2 == 6)) { if (!c.i32(x)) return false; }
+                    else if ((t2 == 1 || t2 == 2) && i2 == 7) { /* bool: no bytes */ }
+                    else if (!c.skip(t2)) return false;
+                }
+                break;
+            }
+            case 7: {
+                h.flags |= 2u;
+                h.dictnv = 0;
+                int32_t l2 = 0;
+                for (;;) {
+                    int32_t i2;
+                    uint32_t t2;
+                    if (!c.field(l2, i2, t2)) return false;
+                    if (t2 == 0 && i2 == 0) break;
+                    int32_t x;
+                    if (i2 == 1) { if (!c.i32(h.dictnv)) return false; }
+                    else if (i2 == 2) { if (!c.i32(x)) return false; }
+                    else if (i2 == 3) { /* read_bool: no bytes */ }
+                    else if (!c.skip(t2)) return false;
+                }
+                break;
+            }
+            default: if (!c.skip(ty)) return false;
+        }
+    }
+    h.hs = c.p;
+    return true;
+}
+
+// format.cpp plausible()
+__device__ bool dev_plausible(const DHdr& h, uint64_t pos, uint64_t end) {
+    if (h.type < 0 || h.type > 3 || h.comp < 0 || h.uncomp < 0 || h.hs < 2) return false;
+    if (h.type == PQ_DATA_PAGE && !(h.flags & 1u)) return false;
+    if (h.type == PQ_DICTIONARY_PAGE && !(h.flags & 2u)) return false;
+    return pos + h.hs + static_cast<uint64_t>(h.comp) <= end;
+}
+
+// The window at file offset pos: 260 bytes from the dword-aligned offset at
+// or below pos (zeros past the device buffer [base, base + len)); returns
+// pos's offset in it (0 .. 3), so 256 bytes from pos are in the window.
+__device__ uint32_t load_win(uint32_t* win, const uint8_t* __restrict__ d, uint64_t base, uint64_t len, uint64_t pos) {
+    const uint64_t rel = pos - base, a0 = rel & ~3ull;
+    if (a0 + kWinStride * 4 <= len) {  // (the buffer is 16-byte aligned)
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(d + a0);
+        for (uint32_t i = 0; i < kWinStride - 1; i += 16) {  // 16 dwords in flight at a time
+            uint32_t v[16];
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++) v[j] = s[i + j];
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++) win[i + j] = v[j];
+        }
+        win[kWinStride - 1] = s[kWinStride - 1];
+    } else {
+        for (uint32_t i = 0; i < kWinStride; i++) {
+            uint32_t w = 0;
+            for (uint32_t b = 0; b < 4; b++) {
+                const uint64_t q = a0 + 4 * i + b;
+                w |= static_cast<uint32_t>(q < len ? d[q] : 0u) << (8 * b);
+            }
+            win[i] = w;
+        }
+    }
+    return static_cast<uint32_t>(rel & 3u);
+}
+
+struct WalkSeg {
+    uint64_t exit;      // where the segment's chain left it (or stopped)
+    uint32_t n;         // records
+    uint32_t flags;     // 1: overflow, 2: the chain broke inside (parse failure / negative size)
+};
+
+__global__ void __launch_bounds__(kWalkWaves * 64) k_walk_seg(const uint8_t* __restrict__ d, uint64_t base, uint64_t len,
+                                                            uint64_t start, uint64_t end, uint64_t seg, uint32_t nseg,
+                                                            uint32_t cap, WalkRec* __restrict__ recs,
+                                                            WalkSeg* __restrict__ segs) {
+    __shared__ uint32_t wins[kWalkWaves * 64 * kWinStride];
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nseg) return;
+    uint32_t* win = wins + threadIdx.x * kWinStride;
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(win);
+    const uint64_t lo = start + seg * k, hi = min(end, lo + seg);
+    uint64_t pos = lo;
+    DHdr h;
+    if (k > 0) {
+        // the first plausible three-page chain start (format.cpp speculate)
+        const uint64_t lim = min(hi, lo + kScanLimit);
+        uint64_t wlo = ~0ull;  // file offset of the window's byte 0
+        for (; pos < lim; pos++) {
+            if (wlo == ~0ull || pos - wlo > kWinStride * 4 - 64) wlo = pos - load_win(win, d, base, len, pos);
+            const uint32_t o = static_cast<uint32_t>(pos - wlo);
+            // (a narrower opening than the host's: PageHeader field 1, an i32
+            // in short form, 0x15, as every writer emits it; a start it misses
+            // only leaves the segment unlinked, which refuses the walk.  The
+            // narrow test keeps the lanes' scans in step: a parse per passing
+            // byte diverges, and a wave runs its lanes' parses one by one)
+            const uint32_t b0 = wb[o];
+            if (b0 != 0x15u) continue;
+            const uint32_t avail = min(kWin, kWinStride * 4 - o);
+            bool ok = dev_parse(wb + o, avail, h);
+            if (!ok && avail < kWin) {  // the window's tail may have cut the header: a window at pos
+                wlo = pos - load_win(win, d, base, len, pos);
+                ok = dev_parse(wb + (pos - wlo), kWin, h);
+            }
+            if (!ok || !dev_plausible(h, pos, end)) continue;
+            uint64_t q = pos + h.hs + static_cast<uint64_t>(h.comp);
+            for (int hop = 0; hop < 2 && ok && q < end; hop++) {
+                const uint32_t oq = load_win(win, d, base, len, q);
+                wlo = ~0ull;
+                DHdr h2;
+                ok = dev_parse(wb + oq, kWin, h2) && dev_plausible(h2, q, end);
+                if (ok) q += h2.hs + static_cast<uint64_t>(h2.comp);
+            }
+            if (ok) break;
+        }
+        if (pos >= lim) pos = hi;
+    }
+    WalkRec* r = recs + static_cast<uint64_t>(k) * cap;
+    uint32_t n = 0, fl = 0;
+    while (pos < hi) {
+        const uint32_t o = load_win(win, d, base, len, pos);
+        if (!dev_parse(wb + o, kWin, h) || h.comp < 0) { fl |= 2u; break; }
+        if (n == cap) { fl |= 1u; break; }
+        WalkRec x;
+        x.pos = pos;
+        x.hs = h.hs;
+        x.comp = h.comp;
+        x.uncomp = h.uncomp;
+        x.type = h.type;
+        x.nv = h.type == PQ_DICTIONARY_PAGE ? h.dictnv : h.dnv;
+        x.enc = h.denc;
+        x.flags = h.flags;
+        r[n++] = x;
+        pos += h.hs + static_cast<uint64_t>(h.comp);
+    }
+    segs[k] = WalkSeg{pos, n, fl};
+}
+
+// Per segment on the chain: the record where the chain enters (found by the
+// previous segment's exit), and the chain's pages / data values / last
+// dictionary page (local index) / first invalid page from there.
+struct WalkLink {
+    int32_t entry;      // record index where the chain enters; -1: skipped (inside a page), -2: refused
+    int32_t pages;
+    int64_t values;
+    int32_t last_dict;  // local (from entry), -1 none
+    int32_t bad;        // local index of the first invalid page, -1 none
+};
+
+__device__ uint32_t rec_kind(const WalkRec& x, int64_t* v, bool* bad) {  // format.cpp linked_walk kind()
+    *v = 0;
+    *bad = false;
+    if (x.comp < 0) { *bad = true; return 0; }
+    if (x.type == PQ_DICTIONARY_PAGE) {
+        *bad = !(x.flags & 2u) || x.nv < 0;
+        return 1;
+    }
+    if (x.type == PQ_DATA_PAGE) {
+        *bad = !(x.flags & 1u) || x.nv < 0;
+        *v = x.nv;
+        return 2;
+    }
+    return 0;
+}
+
+constexpr uint32_t kMaxSkip = 64;  // segments a page may span (a longer page refuses)
+
+__global__ void k_walk_link(uint64_t start, uint64_t seg, uint32_t nseg, uint32_t cap, const WalkRec* __restrict__ recs,
+                            const WalkSeg* __restrict__ segs, WalkLink* __restrict__ links) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nseg) return;
+    const WalkSeg S = segs[k];
+    const WalkRec* r = recs + static_cast<uint64_t>(k) * cap;
+    WalkLink L{-2, 0, 0, -1, -1};
+    // the chain arrives where the nearest earlier segment with records left
+    // (segments inside a longer page find no header start: no records; one
+    // whose records lie inside a page is refused below)
+    uint64_t expect = start;
+    bool have = k == 0;
+    for (uint32_t j = k; j > 0 && k - j < kMaxSkip && !have; j--) {
+        const WalkSeg P = segs[j - 1];
+        if (P.n > 0 || j - 1 == 0) {
+            expect = P.n > 0 ? P.exit : start;
+            have = true;
+        }
+    }
+    const uint64_t lo = start + seg * k, hi = lo + seg;
+    if (have && expect >= hi) {  // inside a page that covers the segment
+        L.entry = S.n == 0 ? -1 : -2;
+    } else if (have && expect >= lo && !(S.flags & 1u)) {
+        uint32_t a = 0, b = S.n;  // lower_bound
+        while (a < b) {
+            const uint32_t m = (a + b) / 2;
+            if (r[m].pos < expect) a = m + 1;
+            else b = m;
+        }
+        if (a < S.n && r[a].pos == expect) {
+            L.entry = static_cast<int32_t>(a);
+            L.pages = static_cast<int32_t>(S.n - a);
+            for (uint32_t j = a; j < S.n; j++) {
+                int64_t v;
+                bool bad;
+                const uint32_t kd = rec_kind(r[j], &v, &bad);
+                if (bad) { L.bad = static_cast<int32_t>(j - a); break; }
+                L.values += v;
+                if (kd == 1) L.last_dict = static_cast<int32_t>(j - a);
+            }
+        }
+    }
+    links[k] = L;
+}
+
+// One workgroup: prefixes over the segments, the cut, the dictionary in force.
+// out[0] = pages (or -1: refused), the per-segment page base / value base /
+// dictionary-in base go to base_pg / base_val / dict_in.
+constexpr int kScanThreads = 1024;
+__global__ void __launch_bounds__(kScanThreads) k_walk_scan(int64_t num_values, uint32_t nseg, uint32_t cap,
+                                                          const WalkRec* __restrict__ recs,
+                                                          const WalkSeg* __restrict__ segs,
+                                                          const WalkLink* __restrict__ links,
+                                                          int64_t* __restrict__ base_pg, int64_t* __restrict__ base_val,
+                                                          int64_t* __restrict__ dict_in, int64_t* __restrict__ out) {
+    __shared__ int64_t sp[kScanThreads], sv[kScanThreads], sd[kScanThreads];
+    __shared__ int64_t carry_p, carry_v, carry_d;
+    __shared__ int32_t cut_seg, first;
+    if (threadIdx.x == 0) { carry_p = 0; carry_v = 0; carry_d = -1; cut_seg = -1; first = 0x7FFFFFFF; }
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < nseg; c0 += kScanThreads) {
+        const uint32_t k = c0 + threadIdx.x;
+        const WalkLink L = k < nseg ? links[k] : WalkLink{-1, 0, 0, -1, -1};
+        const bool on = L.entry >= 0;  // (-1: skipped inside a page, -2: refused)
+        // (segments past the cut are unused; an unlinked one before it refuses)
+        sp[threadIdx.x] = on ? L.pages : 0;
+        sv[threadIdx.x] = on ? L.values : 0;
+        __syncthreads();
+        // inclusive scans (Hillis-Steele) of pages and values
+        for (uint32_t o = 1; o < kScanThreads; o <<= 1) {
+            const int64_t a = threadIdx.x >= o ? sp[threadIdx.x - o] : 0;
+            const int64_t b = threadIdx.x >= o ? sv[threadIdx.x - o] : 0;
+            __syncthreads();
+            sp[threadIdx.x] += a;
+            sv[threadIdx.x] += b;
+            __syncthreads();
+        }
+        const int64_t pinc = sp[threadIdx.x], vinc = sv[threadIdx.x];
+        const int64_t pex = carry_p + pinc - (on ? L.pages : 0), vex = carry_v + vinc - (on ? L.values : 0);
+        // the last dictionary page at or before each segment's end (global index)
+        sd[threadIdx.x] = (on && L.last_dict >= 0) ? pex + L.last_dict : -1;
+        __syncthreads();
+        for (uint32_t o = 1; o < kScanThreads; o <<= 1) {
+            const int64_t a = threadIdx.x >= o ? sd[threadIdx.x - o] : -1;
+            __syncthreads();
+            sd[threadIdx.x] = max(sd[threadIdx.x], a);
+            __syncthreads();
+        }
+        const int64_t dex = threadIdx.x > 0 ? max(carry_d, sd[threadIdx.x - 1]) : carry_d;
+        if (k < nseg) {
+            base_pg[k] = pex;
+            base_val[k] = vex;
+            dict_in[k] = dex;
+        }
+        // the cut: the first segment whose values reach num_values (or whose
+        // chain holds an invalid page, or that is not linked: refused below)
+        const bool stop = k < nseg && (L.entry == -2 || L.bad >= 0 || (on && vex + L.values >= num_values));
+        if (stop) atomicMin(&first, static_cast<int32_t>(k));
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (first != 0x7FFFFFFF) cut_seg = first;
+            carry_p += sp[kScanThreads - 1];
+            carry_v += sv[kScanThreads - 1];
+            carry_d = max(carry_d, sd[kScanThreads - 1]);
+        }
+        __syncthreads();
+        if (cut_seg >= 0) break;
+    }
+    if (threadIdx.x != 0) return;
+    int64_t npages = -1;
+    const int32_t K = cut_seg;
+    if (K >= 0) {
+        const WalkLink L = links[K];
+        if (L.entry >= 0) {
+            // within segment K: the page at which the values reach num_values;
+            // an invalid page before it refuses (the host reports the error)
+            const WalkRec* r = recs + static_cast<uint64_t>(K) * cap;
+            int64_t a = base_val[K];
+            const uint32_t n = segs[K].n;
+            for (uint32_t j = static_cast<uint32_t>(L.entry); j < n; j++) {
+                int64_t v;
+                bool bad;
+                rec_kind(r[j], &v, &bad);
+                if (bad) break;
+                a += v;
+                if (a >= num_values) { npages = base_pg[K] + (j - L.entry) + 1; break; }
+            }
+        }
+    }
+    out[0] = npages;
+    out[1] = K;
+    if (K >= 0) {  // (diagnostics: the stopping segment's link state, records, exit)
+        out[2] = links[K].entry;
+        out[3] = segs[K].n;
+        out[4] = static_cast<int64_t>(segs[K].exit);
+        out[5] = links[K].bad;
+        out[6] = K > 0 ? static_cast<int64_t>(segs[K - 1].exit) : -1;
+        out[7] = segs[K].n ? static_cast<int64_t>(recs[static_cast<uint64_t>(K) * cap].pos) : -1;
+    }
+}
+
+__global__ void k_walk_emit(uint32_t cap, const WalkRec* __restrict__ recs, const WalkSeg* __restrict__ segs,
+                            const WalkLink* __restrict__ links, const int64_t* __restrict__ base_pg,
+                            const int64_t* __restrict__ base_val, const int64_t* __restrict__ dict_in,
+                            const int64_t* __restrict__ out, pq_page_desc* __restrict__ pages) {
+    const int64_t npages = out[0];
+    const int64_t K = out[1];
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (npages < 0 || static_cast<int64_t>(k) > K) return;
+    const WalkLink L = links[k];
+    if (L.entry < 0) return;
+    const WalkRec* r = recs + static_cast<uint64_t>(k) * cap;
+    const uint32_t n = segs[k].n;
+    int64_t idx = base_pg[k], row = base_val[k], d = dict_in[k];
+    for (uint32_t j = static_cast<uint32_t>(L.entry); j < n && idx < npages; j++, idx++) {
+        const WalkRec& x = r[j];
+        int64_t v;
+        bool bad;
+        const uint32_t kd = rec_kind(x, &v, &bad);
+        pq_page_desc p{};
+        p.header_offset = static_cast<int64_t>(x.pos);
+        p.payload_offset = static_cast<int64_t>(x.pos + x.hs);
+        p.payload_size = x.comp;
+        p.page_type = x.type;
+        p.first_row = row;
+        p.page_num = -1;
+        p.uncompressed_size = x.uncomp;
+        if (kd == 1) {
+            d = idx;
+            p.num_values = x.nv;
+            p.page_num = static_cast<int32_t>(idx);
+        } else if (kd == 2) {
+            p.num_values = x.nv;
+            p.encoding = x.enc;
+            p.page_num = static_cast<int32_t>(idx);
+        }
+        p.dict_page = static_cast<int32_t>(d);
+        row += v;
+        pages[idx] = p;
+    }
+}
+
+}  // namespace
+
+void launch_walk(hipStream_t s, const WalkLaunch& W) {
+    const uint32_t nseg = W.nseg;
+    hipLaunchKernelGGL(k_walk_seg, dim3((nseg + 63) / 64), dim3(kWalkWaves * 64), 0, s, W.bytes, W.base, W.len, W.start,
+                       W.end, W.seg, nseg, W.cap, W.recs, reinterpret_cast<WalkSeg*>(W.segs));
+    hipLaunchKernelGGL(k_walk_link, dim3((nseg + 255) / 256), dim3(256), 0, s, W.start, W.seg, nseg, W.cap, W.recs,
+                       reinterpret_cast<const WalkSeg*>(W.segs), reinterpret_cast<WalkLink*>(W.links));
+    hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kScanThreads), 0, s, W.num_values, nseg, W.cap, W.recs,
+                       reinterpret_cast<const WalkSeg*>(W.segs), reinterpret_cast<const WalkLink*>(W.links), W.base_pg,
+                       W.base_val, W.dict_in, W.out);
+    hipLaunchKernelGGL(k_walk_emit, dim3((nseg + 255) / 256), dim3(256), 0, s, W.cap, W.recs,
+                       reinterpret_cast<const WalkSeg*>(W.segs), reinterpret_cast<const WalkLink*>(W.links), W.base_pg,
+                       W.base_val, W.dict_in, W.out, W.pages);
+}
+
+size_t walk_seg_bytes() { return sizeof(WalkSeg); }
+size_t walk_link_bytes() { return sizeof(WalkLink); }
+
+}  // namespace pqk

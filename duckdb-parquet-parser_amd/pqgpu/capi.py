@@ -96,6 +96,11 @@ def lib():
             "pq_ctx_stream": ([vp], vp),
             "pq_ctx_sync": ([vp], C.c_int),
             "pq_ctx_set_option": ([vp, C.c_char_p, C.c_int64], C.c_int),
+            "pq_device_buffer": ([vp, u8p, C.c_size_t, C.POINTER(vp)], C.c_int),
+            "pq_device_buffer_free": ([vp, vp], None),
+            "pq_build_page_table_device": ([vp, vp, C.c_size_t, C.c_int64, C.POINTER(ChunkDesc), C.c_int64,
+                                            C.c_int64, C.POINTER(PageDesc), C.c_int64, C.POINTER(C.c_int64)],
+                                           C.c_int),
             "pq_build_page_table": ([u8p, C.c_size_t, C.POINTER(ChunkDesc), C.POINTER(PageDesc),
                                      C.c_int64, C.POINTER(C.c_int64), C.c_char_p, C.c_size_t], C.c_int),
             "pq_chunk_upload": ([vp, u8p, C.c_size_t, C.POINTER(ChunkDesc), C.c_int,
@@ -257,6 +262,22 @@ class HostColumn:
         return len(self.validity)
 
 
+class DeviceBuffer:
+    def __init__(self, ctx: "Context", h, n: int):
+        self.ctx, self.h, self.n = ctx, h, n
+
+    def data_ptr(self) -> int:
+        return self.h.value or 0
+
+    def free(self):
+        if self.h and self.ctx.h:
+            lib().pq_device_buffer_free(self.ctx.h, self.h)
+        self.h = None
+
+    def __del__(self):
+        self.free()
+
+
 class Context:
     def __init__(self, device: int = 0):
         self.h = lib().pq_ctx_create(device)
@@ -288,6 +309,29 @@ class Context:
         h = vp()
         self.check(lib().pq_chunk_upload(self.h, _buf(file), len(file), arr, len(chunks), C.byref(h)))
         return DeviceChunk(self, h)
+
+    def device_buffer(self, data: bytes) -> "DeviceBuffer":
+        """A device copy of `data` (pq_device_buffer), freed with the object."""
+        h = vp()
+        self.check(lib().pq_device_buffer(self.h, _buf(data), len(data), C.byref(h)))
+        return DeviceBuffer(self, h, len(data))
+
+    def build_page_table_device(self, d_ptr: int, length: int, base: int, chunk: ChunkDesc, seg_bytes: int = 0,
+                                rec_cap: int = 0, cap: int = 0):
+        """pq_build_page_table_device over file bytes [base, base + length)
+        already in device memory at d_ptr: (status, pages) with pages a
+        PageDesc array (status PQ_ERR_UNSUPPORTED = -8: walk on the host)."""
+        if cap <= 0:
+            cap = max(64, min(length // 16 + 64, 1 << 22))
+        pages = (PageDesc * cap)()
+        n = C.c_int64()
+        rc = lib().pq_build_page_table_device(self.h, C.c_void_p(d_ptr), length, base, C.byref(chunk), seg_bytes,
+                                              rec_cap, pages, cap, C.byref(n))
+        if rc == 0 and n.value > cap:
+            raise PqError(-20, "page table over its capacity")
+        exact = (PageDesc * n.value)()
+        C.memmove(exact, pages, C.sizeof(PageDesc) * n.value)
+        return rc, exact
 
     def upload_range(self, file: bytes, chunk: ChunkDesc, table, data_begin: int, data_end: int) -> "DeviceChunk":
         """Data pages [data_begin, data_end) of one chunk (+ their dictionary

@@ -206,6 +206,28 @@ int pq_build_page_table(const uint8_t* file, size_t file_len, const pq_chunk_des
                         pq_page_desc* pages, int64_t cap, int64_t* npages, char* err,
                         size_t errlen);
 
+/* The same walk on the GPU (the device page table): the
+ * chunk's bytes are already in HBM at d_bytes, holding file offsets
+ * [base, base + len) (16-byte aligned; zeros are read past its end).  The
+ * extent is cut into segments of seg_bytes (0: 8 KiB) walked speculatively,
+ * one lane each, linked where each segment's chain leaves it
+ * (csrc/kernels/walk.hip), with at most rec_cap pages per segment (0:
+ * seg_bytes / 128).  Returns 0 with the same pages pq_build_page_table
+ * lists (up to `cap` written to host `pages`, *npages = pages), or
+ * PQ_ERR_UNSUPPORTED when the speculative chain cannot settle the walk
+ * exactly (a page longer than a segment, an invalid header before the
+ * value count, codecs / V2 flags): walk on the host then, which also reports
+ * the reference's errors.  Replaces metadata.cpp:121-155's serial loop for
+ * chunks already in device memory. */
+int pq_build_page_table_device(pq_ctx* ctx, const uint8_t* d_bytes, size_t len, int64_t base,
+                               const pq_chunk_desc* chunk, int64_t seg_bytes, int64_t rec_cap,
+                               pq_page_desc* pages, int64_t cap, int64_t* npages);
+
+/* A device copy of host bytes for pq_build_page_table_device (callers
+ * without HIP headers): n bytes + 64 zero bytes, 256-byte aligned. */
+int pq_device_buffer(pq_ctx* ctx, const uint8_t* host, size_t n, void** d_out);
+void pq_device_buffer_free(pq_ctx* ctx, void* d);
+
 /* ── device chunks ───────────────────────────────────────────────────────── */
 /* Upload `nchunks` column chunks of ONE leaf column (e.g. every row group's
  * chunk of that column) from a host file image; the walk runs on the host,
