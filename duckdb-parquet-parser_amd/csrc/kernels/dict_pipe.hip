@@ -208,7 +208,23 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
     // (the run table's per-stream rows are kPipeRunCap * 8 = 1 KiB apart:
     // 16-byte aligned, records stored in pairs)
     static_assert((kPipeRunCap * sizeof(uint2)) % 16 == 0, "record rows 16-byte aligned");
-    if (staged) walk_runs<true, true>(W, stage, flag, nrec);
+    if (staged && (debug & (1 << 24))) {  // timing probe: position-only walk of 1-byte headers (outputs invalid)
+        uint32_t q = W.q, cnt = 0, nr = 0;
+        bool alive = W.alive && W.n > 0;
+        const uint32_t nbv = (W.bw + 7) / 8;
+        const uint8_t* st8 = reinterpret_cast<const uint8_t*>(stage);
+        while (__ballot(alive)) {
+            const uint32_t b = st8[W.sbase + min(q, W.end)];
+            const uint32_t lit = b & 1u, g = (b >> 1) & 0x3Fu;
+            cnt += lit ? g * 8u : g;
+            q += 1u + (lit ? g * W.bw : nbv);
+            nr++;
+            alive = alive && (b & 0x80u) == 0 && g != 0 && cnt < W.n && q < W.end && nr < W.cap;
+        }
+        if (nr == 0xFFFFFFu) info[0] = q;  // keeps the loop
+        return;
+    }
+    if (staged) walk_runs<true, true>(W, stage, flag, nrec, (debug & (1 << 25)) != 0);  // bit 25: no record stores (timing)
     else walk_runs<false, true>(W, stage, flag, nrec);
     const uint32_t oflag = static_cast<uint32_t>(__shfl_xor(static_cast<int>(flag), 1));
     const uint32_t orec = static_cast<uint32_t>(__shfl_xor(static_cast<int>(nrec), 1));
@@ -1168,6 +1184,8 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     int64_t Grun = static_cast<int64_t>(in);
     for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
     if (a.debug & 8) return;
+    uint4 cv0, cv1, cv2, cv3;
+    bool cv_loaded = false;
     for (int c0 = ta; c0 < tb; c0 += kWave) {
         const int cn = min(kWave, tb - c0);
         int64_t myR0 = 0, myG0 = 0;
@@ -1209,7 +1227,10 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
                 }
                 return v;
             };
-            const uint4 cv0 = ld(ib), cv1 = ld(ib + 1), cv2 = ld(ib + 2), cv3 = ld(ib + 3);
+            if (!(a.debug & (1 << 23)) || !cv_loaded) {  // bit 23 (timing only): the first batch's codes reused
+                cv0 = ld(ib); cv1 = ld(ib + 1); cv2 = ld(ib + 2); cv3 = ld(ib + 3);
+                cv_loaded = true;
+            }
         for (int i = ib; i < min(cn, ib + kWBatch); i++) {
             const int64_t R0 = rl64(myR0, i);
             const int64_t G0 = rl64(myG0, i);

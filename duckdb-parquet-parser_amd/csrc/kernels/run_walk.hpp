@@ -23,7 +23,8 @@ struct RunWalk {
 // aligned, nrec even on entry): half the store instructions, whole 16-byte
 // pieces of the record lines instead of 8-byte ones
 template <bool kStaged, bool kPair = false>
-__device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uint32_t& flag, uint32_t& nrec) {
+__device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uint32_t& flag, uint32_t& nrec,
+                                          bool nostore = false) {  // nostore: timing ablation only
     const uint32_t nbv = (W.bw + 7) / 8;
     const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
     const uint32_t litpay = W.bw ? 0x80000000u : 0u;
@@ -105,7 +106,7 @@ __device__ __forceinline__ void walk_runs(RunWalk& W, const uint32_t* stage, uin
         const uint32_t pl = (litm & (litpay | ((qh << 3) & litsh))) | (~litm & vraw & vmask);
         const uint32_t ry = exh ? 0u : pl;
         if constexpr (kPair) {
-            if (ok && (nr & 1u)) *reinterpret_cast<uint4*>(W.out + nr - 1) = make_uint4(held.x, held.y, rx, ry);
+            if (ok && (nr & 1u) && !nostore) *reinterpret_cast<uint4*>(W.out + nr - 1) = make_uint4(held.x, held.y, rx, ry);
             if (ok && !(nr & 1u)) held = make_uint2(rx, ry);
         } else {
             if (ok) W.out[nr] = make_uint2(rx, ry);

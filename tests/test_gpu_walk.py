@@ -15,6 +15,7 @@ import pytest
 from pqgpu import capi, gen
 from test_fuzz_host import _mutants
 from util import to_desc
+from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -107,6 +108,6 @@ def test_mutants_never_listed_wrong(ctx):
     pages or refuses; it never lists a chunk whose host walk fails."""
     settled = 0
     for name, f, c in _mutants(200, seed=29):
-        ch = to_desc(c)
+        ch = to_desc(O.Chunk(*c))  # _mutants yields the manifest's chunk list
         settled += check(ctx, bytes(f), ch, segs=(256, 4096)) > 0
     assert settled > 0
