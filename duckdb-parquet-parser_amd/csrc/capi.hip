@@ -71,6 +71,11 @@ struct pq_ctx {
     pqstage::Stager stager;
     uint8_t* d_raw = nullptr;              // raw chunk bytes of the current upload (relayout source)
     size_t raw_cap = 0;
+    bool opt_dev_walk = false;             // "device_walk": uploads walk pages on the GPU (walk.hip) over d_raw
+    uint8_t* d_walk = nullptr;             // the device walk's records, links and page table
+    size_t walk_cap = 0;
+    pq_page_desc* h_walk = nullptr;        // pinned: the page table back to the host
+    size_t h_walk_cap = 0;
     pqk::RelayoutEntry* d_relay = nullptr; // relayout entries of the current upload
     size_t relay_cap = 0;
     pqk::CodecEntry* d_codec = nullptr;    // compressed / V2 pages of the current upload (codec.hip)
@@ -862,6 +867,8 @@ void pq_ctx_destroy(pq_ctx* ctx) {
     (void)hipStreamDestroy(ctx->side);
     ctx->stager.release();
     if (ctx->d_raw) (void)hipFree(ctx->d_raw);
+    if (ctx->d_walk) (void)hipFree(ctx->d_walk);
+    if (ctx->h_walk) (void)hipHostFree(ctx->h_walk);
     if (ctx->d_relay) (void)hipFree(ctx->d_relay);
     if (ctx->d_codec) (void)hipFree(ctx->d_codec);
     if (ctx->d_codec_st) (void)hipFree(ctx->d_codec_st);
@@ -931,6 +938,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
         return 0;
     }
     if (std::strcmp(key, "raw_upload") == 0) { ctx->opt_raw = value != 0; return 0; }
+    if (std::strcmp(key, "device_walk") == 0) { ctx->opt_dev_walk = value != 0; return 0; }
     if (std::strcmp(key, "stage_streams") == 0) {
         if (value < 1 || value > 2) return set_err(ctx, PQ_ERR_ARG, "stage_streams: 1..2");
         ctx->opt_stage_streams = static_cast<int>(value);
@@ -986,6 +994,91 @@ int pq_build_page_table(const uint8_t* file, size_t file_len, const pq_chunk_des
     }
 }
 
+}  // extern "C" (a C++ helper)
+
+// The device walk (walk.hip) of one chunk over d_bytes = file bytes
+// [base, base + len): the page table to `host` (pinned staging, then `sink`)
+// and the page count.  PQ_ERR_UNSUPPORTED: refused (the host walk decides).
+template <class Sink>
+static int device_walk(pq_ctx* ctx, const uint8_t* d_bytes, size_t len, int64_t base, const pq_chunk_desc* chunk,
+                       int64_t seg_bytes, int64_t rec_cap, int64_t* npages, Sink&& sink) {
+    *npages = 0;
+    if (chunk->codec != 0 || chunk->ext_flags != 0 || chunk->num_values <= 0) return PQ_ERR_UNSUPPORTED;
+    int64_t off = chunk->data_page_offset;
+    if (chunk->has_dictionary_page_offset) off = std::min(off, chunk->dictionary_page_offset);
+    if (off < base || off >= base + static_cast<int64_t>(len)) return PQ_ERR_UNSUPPORTED;
+    const uint64_t seg = seg_bytes ? static_cast<uint64_t>(seg_bytes) : 8192u;
+    const uint32_t rc = static_cast<uint32_t>(rec_cap ? rec_cap : std::max<int64_t>(1, static_cast<int64_t>(seg) / 128));
+    const uint64_t start = static_cast<uint64_t>(off), end = static_cast<uint64_t>(base) + len;
+    const uint64_t nseg64 = (end - start + seg - 1) / seg;
+    if (nseg64 > (1u << 30) / rc) return PQ_ERR_UNSUPPORTED;
+    const uint32_t nseg = static_cast<uint32_t>(nseg64);
+    pqk::WalkLaunch W{};
+    W.bytes = d_bytes; W.base = static_cast<uint64_t>(base); W.len = len;
+    W.start = start; W.end = end; W.seg = seg; W.nseg = nseg; W.cap = rc;
+    W.num_values = chunk->num_values;
+    const size_t nrec = static_cast<size_t>(nseg) * rc;
+    // one device buffer, kept by the context: records, segments, links, bases, the page table
+    auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t o_recs = 0, o_segs = o_recs + al(nrec * sizeof(pqk::WalkRec));
+    const size_t o_links = o_segs + al(nseg * pqk::walk_seg_bytes());
+    const size_t o_bases = o_links + al(nseg * pqk::walk_link_bytes());
+    const size_t o_out = o_bases + al(3 * static_cast<size_t>(nseg) * 8);
+    const size_t o_pages = o_out + 256, total = o_pages + al(nrec * sizeof(pq_page_desc));
+    if (ctx->walk_cap < total) {
+        if (ctx->d_walk) (void)hipFree(ctx->d_walk);
+        ctx->d_walk = nullptr;
+        ctx->walk_cap = 0;
+        if (int e = hip_check(ctx, hipMalloc(reinterpret_cast<void**>(&ctx->d_walk), total), "hipMalloc (device walk)")) return e;
+        ctx->walk_cap = total;
+    }
+    uint8_t* mem = ctx->d_walk;
+    W.recs = reinterpret_cast<pqk::WalkRec*>(mem + o_recs);
+    W.segs = mem + o_segs;
+    W.links = mem + o_links;
+    W.base_pg = reinterpret_cast<int64_t*>(mem + o_bases);
+    W.base_val = W.base_pg + nseg;
+    W.dict_in = W.base_val + nseg;
+    W.out = reinterpret_cast<int64_t*>(mem + o_out);
+    W.pages = reinterpret_cast<pq_page_desc*>(mem + o_pages);
+    {
+        Timed t(ctx, "walk");
+        pqk::launch_walk(ctx->stream, W);
+    }
+    int64_t res[8] = {-1, -1, 0, 0, 0, 0, 0, 0};
+    int rc2 = hip_check(ctx, hipGetLastError(), "walk launch");
+    if (!rc2) rc2 = hip_check(ctx, hipMemcpyAsync(res, W.out, sizeof res, hipMemcpyDeviceToHost, ctx->stream), "walk result");
+    if (!rc2) rc2 = hip_check(ctx, hipStreamSynchronize(ctx->stream), "walk sync");
+    if (std::getenv("PQ_WALK_DEBUG"))
+        std::fprintf(stderr, "walk: pages %lld cut %lld entry %lld n %lld exit %lld bad %lld prev_exit %lld first %lld (start %llu seg %llu)\n",
+                     (long long)res[0], (long long)res[1], (long long)res[2], (long long)res[3], (long long)res[4],
+                     (long long)res[5], (long long)res[6], (long long)res[7], (unsigned long long)start,
+                     (unsigned long long)seg);
+    if (rc2) return rc2;
+    if (res[0] < 0) return PQ_ERR_UNSUPPORTED;
+    *npages = res[0];
+    const size_t k = static_cast<size_t>(res[0]);
+    if (k) {
+        if (ctx->h_walk_cap < k) {
+            if (ctx->h_walk) (void)hipHostFree(ctx->h_walk);
+            ctx->h_walk = nullptr;
+            ctx->h_walk_cap = 0;
+            if (int e = hip_check(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_walk), k * sizeof(pq_page_desc)),
+                                  "hipHostMalloc (device walk)"))
+                return e;
+            ctx->h_walk_cap = k;
+        }
+        if (int e = hip_check(ctx, hipMemcpyAsync(ctx->h_walk, W.pages, k * sizeof(pq_page_desc), hipMemcpyDeviceToHost,
+                                                  ctx->stream), "walk copy"))
+            return e;
+        if (int e = hip_check(ctx, hipStreamSynchronize(ctx->stream), "walk copy sync")) return e;
+    }
+    sink(ctx->h_walk, k);
+    return 0;
+}
+
+extern "C" {
+
 int pq_build_page_table_device(pq_ctx* ctx, const uint8_t* d_bytes, size_t len, int64_t base,
                                const pq_chunk_desc* chunk, int64_t seg_bytes, int64_t rec_cap,
                                pq_page_desc* pages, int64_t cap, int64_t* npages) {
@@ -993,63 +1086,12 @@ int pq_build_page_table_device(pq_ctx* ctx, const uint8_t* d_bytes, size_t len, 
         (cap && !pages))
         return PQ_ERR_ARG;
     *npages = 0;
-    if (chunk->codec != 0 || chunk->ext_flags != 0 || chunk->num_values <= 0) return PQ_ERR_UNSUPPORTED;
-    int64_t off = chunk->data_page_offset;
-    if (chunk->has_dictionary_page_offset) off = std::min(off, chunk->dictionary_page_offset);
-    if (off < base || off >= base + static_cast<int64_t>(len)) return PQ_ERR_UNSUPPORTED;
     DevGuard dg(ctx);
-    const uint64_t seg = seg_bytes ? static_cast<uint64_t>(seg_bytes) : 8192u;
-    const uint32_t rc = static_cast<uint32_t>(rec_cap ? rec_cap : std::max<int64_t>(1, static_cast<int64_t>(seg) / 128));
-    const uint64_t start = static_cast<uint64_t>(off), end = static_cast<uint64_t>(base) + len;
-    const uint64_t nseg64 = (end - start + seg - 1) / seg;
-    if (nseg64 > (1u << 30) / rc) return PQ_ERR_UNSUPPORTED;
-    const uint32_t nseg = static_cast<uint32_t>(nseg64);
     try {
-        pqk::WalkLaunch W{};
-        W.bytes = d_bytes; W.base = static_cast<uint64_t>(base); W.len = len;
-        W.start = start; W.end = end; W.seg = seg; W.nseg = nseg; W.cap = rc;
-        W.num_values = chunk->num_values;
-        const size_t nrec = static_cast<size_t>(nseg) * rc;
-        // one allocation: records, segments, links, bases, the page table
-        auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-        const size_t o_recs = 0, o_segs = o_recs + al(nrec * sizeof(pqk::WalkRec));
-        const size_t o_links = o_segs + al(nseg * pqk::walk_seg_bytes());
-        const size_t o_bases = o_links + al(nseg * pqk::walk_link_bytes());
-        const size_t o_out = o_bases + al(3 * static_cast<size_t>(nseg) * 8);
-        const size_t o_pages = o_out + 256, total = o_pages + al(nrec * sizeof(pq_page_desc));
-        uint8_t* mem = nullptr;
-        if (int rc2 = hip_check(ctx, hipMalloc(reinterpret_cast<void**>(&mem), total), "hipMalloc (device walk)")) return rc2;
-        W.recs = reinterpret_cast<pqk::WalkRec*>(mem + o_recs);
-        W.segs = mem + o_segs;
-        W.links = mem + o_links;
-        W.base_pg = reinterpret_cast<int64_t*>(mem + o_bases);
-        W.base_val = W.base_pg + nseg;
-        W.dict_in = W.base_val + nseg;
-        W.out = reinterpret_cast<int64_t*>(mem + o_out);
-        W.pages = reinterpret_cast<pq_page_desc*>(mem + o_pages);
-        {
-            Timed t(ctx, "walk");
-            pqk::launch_walk(ctx->stream, W);
-        }
-        int64_t res[8] = {-1, -1, 0, 0, 0, 0, 0, 0};
-        int rc2 = hip_check(ctx, hipGetLastError(), "walk launch");
-        if (!rc2) rc2 = hip_check(ctx, hipMemcpyAsync(res, W.out, sizeof res, hipMemcpyDeviceToHost, ctx->stream), "walk result");
-        if (!rc2) rc2 = hip_check(ctx, hipStreamSynchronize(ctx->stream), "walk sync");
-        if (std::getenv("PQ_WALK_DEBUG"))
-            std::fprintf(stderr, "walk: pages %lld cut %lld entry %lld n %lld exit %lld bad %lld prev_exit %lld first %lld (start %llu seg %llu)\n",
-                         (long long)res[0], (long long)res[1], (long long)res[2], (long long)res[3], (long long)res[4],
-                         (long long)res[5], (long long)res[6], (long long)res[7], (unsigned long long)start,
-                         (unsigned long long)seg);
-        if (!rc2 && res[0] >= 0) {
-            *npages = res[0];
-            const int64_t k = std::min(cap, res[0]);
-            if (k > 0)
-                rc2 = hip_check(ctx, hipMemcpy(pages, W.pages, static_cast<size_t>(k) * sizeof(pq_page_desc), hipMemcpyDeviceToHost),
-                                "walk copy");
-        }
-        (void)hipFree(mem);
-        if (rc2) return rc2;
-        return res[0] >= 0 ? 0 : PQ_ERR_UNSUPPORTED;
+        return device_walk(ctx, d_bytes, len, base, chunk, seg_bytes, rec_cap, npages,
+                           [&](const pq_page_desc* h, size_t k) {
+                               std::memcpy(pages, h, std::min<size_t>(k, static_cast<size_t>(cap)) * sizeof(pq_page_desc));
+                           });
     } catch (const std::exception& e) {
         return set_err(ctx, PQ_ERR_ALLOC, e.what());
     }
@@ -1108,6 +1150,8 @@ static void raw_start(pq_ctx* ctx, const uint8_t* file, size_t file_len, RawStag
     const size_t need = static_cast<size_t>(R.total) + 64;
     if (ctx->raw_cap < need) {
         if (ctx->d_raw) (void)hipFree(ctx->d_raw);
+    if (ctx->d_walk) (void)hipFree(ctx->d_walk);
+    if (ctx->h_walk) (void)hipHostFree(ctx->h_walk);
         ctx->d_raw = nullptr;
         ctx->raw_cap = 0;
         if (hipMalloc(reinterpret_cast<void**>(&ctx->d_raw), need) != hipSuccess) {
@@ -1904,7 +1948,28 @@ int pq_chunk_upload(pq_ctx* ctx, const uint8_t* file, size_t file_len, const pq_
         if (extents) raw_start(ctx, file, file_len, raw);
         {
             HostTimed ht(ctx, "up_walk");
-            parallel_for(nchunks, [&](int k) { walks[static_cast<size_t>(k)] = pqfmt::walk_chunk(file, file_len, chunks[k], per); });
+            // option device_walk: the page walk on the GPU over the raw bytes
+            // once they are in HBM (walk.hip); a chunk it refuses (or any
+            // chunk the raw upload does not cover) walks on the host, which
+            // also reports the reference's errors
+            std::vector<char> done(static_cast<size_t>(nchunks), 0);
+            if (ctx->opt_dev_walk && raw.active) {
+                raw.join();
+                if (raw.err == hipSuccess) {
+                    for (int k = 0; k < nchunks; k++) {
+                        int64_t np = 0;
+                        pqfmt::WalkResult& w = walks[static_cast<size_t>(k)];
+                        const int rc = device_walk(ctx, ctx->d_raw + raw.base[static_cast<size_t>(k)],
+                                                   static_cast<size_t>(raw.ext[static_cast<size_t>(k)].second),
+                                                   raw.ext[static_cast<size_t>(k)].first, &chunks[k], 0, 0, &np,
+                                                   [&](const pq_page_desc* h, size_t n) { w.pages.assign(h, h + n); });
+                        done[static_cast<size_t>(k)] = rc == 0;
+                    }
+                }
+            }
+            parallel_for(nchunks, [&](int k) {
+                if (!done[static_cast<size_t>(k)]) walks[static_cast<size_t>(k)] = pqfmt::walk_chunk(file, file_len, chunks[k], per);
+            });
         }
         return upload_walked(ctx, file, file_len, chunks[0], walks, 0, out, &raw);
     } catch (const std::exception& e) {

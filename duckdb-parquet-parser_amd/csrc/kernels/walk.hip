@@ -6,7 +6,7 @@
 // PageHeader at the cursor, step over header and payload, until the data
 // pages' values reach ColumnMetaData.num_values
 // (src/reader/column_reader.cpp:18-71, src/reader/metadata.cpp:121-155).
-// Here the extent is cut into segments of `seg` bytes, one lane each:
+// Here the extent is cut into segments of `seg` bytes, one wave each:
 //   k_walk_seg    segment 0 starts at the chunk's first page; segment k > 0
 //                 at the first position of its range where a plausible header
 //                 begins a plausible three-page chain (format.cpp speculate's
@@ -36,10 +36,14 @@ namespace pqk {
 namespace {
 
 constexpr uint32_t kWin = 256;          // header window (read_page_header's fixed window)
-constexpr uint32_t kWinStride = 65;     // dwords per lane window: 64 + 1 (LDS banks)
-constexpr int kWalkWaves = 1;           // one wave per workgroup (16.6 KiB of windows)
+constexpr uint32_t kWinStride = 65;     // dwords per window: 256 bytes from any byte of the first dword
 constexpr uint32_t kScanLimit = 16384;  // bytes a segment scans for its first header (format.cpp kSpecScan)
 constexpr int kSkipDepth = 8;
+
+// LDS pointers typed as such: a generic pointer compiles to flat loads, which
+// wait on both counters and take the longer path
+using lds8c = const __attribute__((address_space(3))) uint8_t;
+using lds32 = __attribute__((address_space(3))) uint32_t;
 
 struct DHdr {
     int32_t type, uncomp, comp, dnv, denc, dictnv;
@@ -49,14 +53,14 @@ struct DHdr {
 
 // One lane's 256-byte window: bytes [0, avail) valid (zeros past the buffer).
 struct Win {
-    const uint8_t* w;
+    lds8c* w;
     uint32_t p, e;
-    __device__ bool byte(uint32_t& v) {
+    __device__ __forceinline__ bool byte(uint32_t& v) {
         if (p >= e) return false;
         v = w[p++];
         return true;
     }
-    __device__ bool varint(uint64_t& r) {
+    __device__ __forceinline__ bool varint(uint64_t& r) {
         r = 0;
         for (int shift = 0;; shift += 7) {
             if (shift > 63) return false;
@@ -66,14 +70,14 @@ struct Win {
             if ((b & 0x80u) == 0) return true;
         }
     }
-    __device__ bool i32(int32_t& v) {
+    __device__ __forceinline__ bool i32(int32_t& v) {
         uint64_t u;
         if (!varint(u)) return false;
         v = static_cast<int32_t>(static_cast<int64_t>((u >> 1) ^ (~(u & 1) + 1)));
         return true;
     }
     // id = 0, type = 0 at STOP (a type nibble 0 ends the struct too: format.cpp FastHdr::field)
-    __device__ bool field(int32_t& last, int32_t& id, uint32_t& type) {
+    __device__ __forceinline__ bool field(int32_t& last, int32_t& id, uint32_t& type) {
         uint32_t b;
         if (!byte(b)) return false;
         if (b == 0) { id = 0; type = 0; return true; }
@@ -95,9 +99,12 @@ struct Win {
         p += static_cast<uint32_t>(n);
         return true;
     }
-    // Thrift skip of a value of `type`, iterative (format.cpp FastHdr::skip;
-    // nesting past kSkipDepth refuses, which the walk treats as a parse failure)
-    __device__ bool skip(uint32_t type) {
+    // Thrift skip of a value of `type` (skip_value below: out of line, by value,
+    // so this cursor stays in registers on the paths that never skip)
+    __device__ __forceinline__ bool skip(uint32_t type);
+    // iterative (format.cpp FastHdr::skip; nesting past kSkipDepth refuses,
+    // which the walk treats as a parse failure); its frame arrays live in scratch
+    __device__ __forceinline__ bool skip_impl(uint32_t type) {
         // frame: kind 0 struct (last id), 1 list (remaining, elem type), 2 map (remaining pairs, kt, vt, half)
         uint32_t kind[kSkipDepth], et[kSkipDepth], et2[kSkipDepth];
         int64_t rem[kSkipDepth];
@@ -168,9 +175,20 @@ struct Win {
     }
 };
 
+__device__ __noinline__ uint32_t skip_value(lds8c* w, uint32_t p, uint32_t e, uint32_t type) {
+    Win c{w, p, e};
+    return c.skip_impl(type) ? c.p : 0xFFFFFFFFu;
+}
+__device__ __forceinline__ bool Win::skip(uint32_t type) {
+    const uint32_t np = skip_value(w, p, e, type);
+    if (np == 0xFFFFFFFFu) return false;
+    p = np;
+    return true;
+}
+
 // format.cpp FastHdr::parse: true for every header read_page_header accepts
 // (identical fields), false where it would throw.
-__device__ bool dev_parse(const uint8_t* w, uint32_t avail, DHdr& h) {
+__device__ __forceinline__ bool dev_parse(lds8c* w, uint32_t avail, DHdr& h) {
     Win c{w, 0, avail};
     h = DHdr{0, 0, 0, 0, 0, 0, 0, 0};
     int32_t last = 0;
@@ -246,38 +264,35 @@ __device__ bool dev_parse(const uint8_t* w, uint32_t avail, DHdr& h) {
 }
 
 // format.cpp plausible()
-__device__ bool dev_plausible(const DHdr& h, uint64_t pos, uint64_t end) {
+__device__ __forceinline__ bool dev_plausible(const DHdr& h, uint64_t pos, uint64_t end) {
     if (h.type < 0 || h.type > 3 || h.comp < 0 || h.uncomp < 0 || h.hs < 2) return false;
     if (h.type == PQ_DATA_PAGE && !(h.flags & 1u)) return false;
     if (h.type == PQ_DICTIONARY_PAGE && !(h.flags & 2u)) return false;
     return pos + h.hs + static_cast<uint64_t>(h.comp) <= end;
 }
 
-// The window at file offset pos: 260 bytes from the dword-aligned offset at
-// or below pos (zeros past the device buffer [base, base + len)); returns
-// pos's offset in it (0 .. 3), so 256 bytes from pos are in the window.
-__device__ uint32_t load_win(uint32_t* win, const uint8_t* __restrict__ d, uint64_t base, uint64_t len, uint64_t pos) {
+// The window at file offset pos, loaded by the whole wave (one dword per lane,
+// lane 0 also the 65th): 260 bytes from the dword-aligned offset at or below
+// pos (zeros past the device buffer [base, base + len)); returns pos's offset
+// in it (0 .. 3), so 256 bytes from pos are in the window.
+__device__ __forceinline__ uint32_t load_win(lds32* win, const uint8_t* __restrict__ d, uint64_t base, uint64_t len,
+                                                 uint64_t pos) {
     const uint64_t rel = pos - base, a0 = rel & ~3ull;
-    if (a0 + kWinStride * 4 <= len) {  // (the buffer is 16-byte aligned)
-        const uint32_t* s = reinterpret_cast<const uint32_t*>(d + a0);
-        for (uint32_t i = 0; i < kWinStride - 1; i += 16) {  // 16 dwords in flight at a time
-            uint32_t v[16];
-#pragma unroll
-            for (uint32_t j = 0; j < 16; j++) v[j] = s[i + j];
-#pragma unroll
-            for (uint32_t j = 0; j < 16; j++) win[i + j] = v[j];
-        }
-        win[kWinStride - 1] = s[kWinStride - 1];
-    } else {
-        for (uint32_t i = 0; i < kWinStride; i++) {
-            uint32_t w = 0;
-            for (uint32_t b = 0; b < 4; b++) {
-                const uint64_t q = a0 + 4 * i + b;
-                w |= static_cast<uint32_t>(q < len ? d[q] : 0u) << (8 * b);
-            }
-            win[i] = w;
-        }
-    }
+    const uint32_t l = __lane_id();
+    auto dword = [&](uint32_t i) -> uint32_t {
+        const uint64_t q = a0 + 4ull * i;
+        if (q + 4 <= len) return *reinterpret_cast<const uint32_t*>(d + q);  // (the buffer is 16-byte aligned)
+        uint32_t w = 0;
+        for (uint32_t b = 0; b < 4; b++) w |= static_cast<uint32_t>(q + b < len ? d[q + b] : 0u) << (8 * b);
+        return w;
+    };
+    const uint32_t v = dword(l);
+    const uint32_t v2 = l == 0 ? dword(kWinStride - 1) : 0u;
+    __builtin_amdgcn_wave_barrier();  // every lane is done parsing the previous window
+    win[l] = v;
+    if (l == 0) win[kWinStride - 1] = v2;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     return static_cast<uint32_t>(rel & 3u);
 }
 
@@ -287,50 +302,56 @@ struct WalkSeg {
     uint32_t flags;     // 1: overflow, 2: the chain broke inside (parse failure / negative size)
 };
 
-__global__ void __launch_bounds__(kWalkWaves * 64) k_walk_seg(const uint8_t* __restrict__ d, uint64_t base, uint64_t len,
-                                                            uint64_t start, uint64_t end, uint64_t seg, uint32_t nseg,
-                                                            uint32_t cap, WalkRec* __restrict__ recs,
-                                                            WalkSeg* __restrict__ segs) {
-    __shared__ uint32_t wins[kWalkWaves * 64 * kWinStride];
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per segment.  Every lane parses the same header from the shared
+// window (the parse is serial; identical work keeps the lanes in step), and
+// the 64 lanes test 64 positions at once for a header opening while the
+// segment looks for its first chain start.
+__global__ void __launch_bounds__(kWave) k_walk_seg(const uint8_t* __restrict__ d, uint64_t base, uint64_t len,
+                                                    uint64_t start, uint64_t end, uint64_t seg, uint32_t nseg,
+                                                    uint32_t cap, WalkRec* __restrict__ recs,
+                                                    WalkSeg* __restrict__ segs) {
+    __shared__ uint32_t win_s[kWinStride + 3];
+    lds32* win = (lds32*)win_s;
+    const uint32_t k = blockIdx.x;
     if (k >= nseg) return;
-    uint32_t* win = wins + threadIdx.x * kWinStride;
-    const uint8_t* wb = reinterpret_cast<const uint8_t*>(win);
+    const uint32_t l = __lane_id();
+    lds8c* wb = (lds8c*)win_s;
     const uint64_t lo = start + seg * k, hi = min(end, lo + seg);
     uint64_t pos = lo;
     DHdr h;
     if (k > 0) {
-        // the first plausible three-page chain start (format.cpp speculate)
+        // the first plausible three-page chain start (format.cpp speculate):
+        // 64 positions per window; candidates in order
+        // (a narrower opening than the host's: PageHeader field 1, an i32 in
+        // short form, 0x15, as every writer emits it; a start it misses only
+        // leaves the segment unlinked, which refuses the walk)
         const uint64_t lim = min(hi, lo + kScanLimit);
-        uint64_t wlo = ~0ull;  // file offset of the window's byte 0
-        for (; pos < lim; pos++) {
-            if (wlo == ~0ull || pos - wlo > kWinStride * 4 - 64) wlo = pos - load_win(win, d, base, len, pos);
-            const uint32_t o = static_cast<uint32_t>(pos - wlo);
-            // (a narrower opening than the host's: PageHeader field 1, an i32
-            // in short form, 0x15, as every writer emits it; a start it misses
-            // only leaves the segment unlinked, which refuses the walk.  The
-            // narrow test keeps the lanes' scans in step: a parse per passing
-            // byte diverges, and a wave runs its lanes' parses one by one)
-            const uint32_t b0 = wb[o];
-            if (b0 != 0x15u) continue;
-            const uint32_t avail = min(kWin, kWinStride * 4 - o);
-            bool ok = dev_parse(wb + o, avail, h);
-            if (!ok && avail < kWin) {  // the window's tail may have cut the header: a window at pos
-                wlo = pos - load_win(win, d, base, len, pos);
-                ok = dev_parse(wb + (pos - wlo), kWin, h);
+        bool found = false;
+        for (uint64_t c = lo; c < lim && !found; c += kWave) {
+            uint32_t o = load_win(win, d, base, len, c);
+            uint64_t m = __ballot(c + l < lim && wb[o + l] == 0x15u);
+            while (m && !found) {
+                const uint32_t b = static_cast<uint32_t>(__builtin_ctzll(m));
+                m &= m - 1;
+                const uint64_t p = c + b;
+                uint32_t op = load_win(win, d, base, len, p);  // 256 bytes from p
+                bool ok = dev_parse(wb + op, kWin, h) && dev_plausible(h, p, end);
+                uint64_t q = p + h.hs + static_cast<uint64_t>(h.comp);
+                for (int hop = 0; hop < 2 && ok && q < end; hop++) {
+                    const uint32_t oq = load_win(win, d, base, len, q);
+                    DHdr h2;
+                    ok = dev_parse(wb + oq, kWin, h2) && dev_plausible(h2, q, end);
+                    if (ok) q += h2.hs + static_cast<uint64_t>(h2.comp);
+                }
+                if (ok) {
+                    found = true;
+                    pos = p;
+                } else if (m) {
+                    o = load_win(win, d, base, len, c);  // the chunk's window again for the next candidate
+                }
             }
-            if (!ok || !dev_plausible(h, pos, end)) continue;
-            uint64_t q = pos + h.hs + static_cast<uint64_t>(h.comp);
-            for (int hop = 0; hop < 2 && ok && q < end; hop++) {
-                const uint32_t oq = load_win(win, d, base, len, q);
-                wlo = ~0ull;
-                DHdr h2;
-                ok = dev_parse(wb + oq, kWin, h2) && dev_plausible(h2, q, end);
-                if (ok) q += h2.hs + static_cast<uint64_t>(h2.comp);
-            }
-            if (ok) break;
         }
-        if (pos >= lim) pos = hi;
+        if (!found) pos = hi;
     }
     WalkRec* r = recs + static_cast<uint64_t>(k) * cap;
     uint32_t n = 0, fl = 0;
@@ -338,19 +359,22 @@ __global__ void __launch_bounds__(kWalkWaves * 64) k_walk_seg(const uint8_t* __r
         const uint32_t o = load_win(win, d, base, len, pos);
         if (!dev_parse(wb + o, kWin, h) || h.comp < 0) { fl |= 2u; break; }
         if (n == cap) { fl |= 1u; break; }
-        WalkRec x;
-        x.pos = pos;
-        x.hs = h.hs;
-        x.comp = h.comp;
-        x.uncomp = h.uncomp;
-        x.type = h.type;
-        x.nv = h.type == PQ_DICTIONARY_PAGE ? h.dictnv : h.dnv;
-        x.enc = h.denc;
-        x.flags = h.flags;
-        r[n++] = x;
+        if (l == 0) {
+            WalkRec x;
+            x.pos = pos;
+            x.hs = h.hs;
+            x.comp = h.comp;
+            x.uncomp = h.uncomp;
+            x.type = h.type;
+            x.nv = h.type == PQ_DICTIONARY_PAGE ? h.dictnv : h.dnv;
+            x.enc = h.denc;
+            x.flags = h.flags;
+            r[n] = x;
+        }
+        n++;
         pos += h.hs + static_cast<uint64_t>(h.comp);
     }
-    segs[k] = WalkSeg{pos, n, fl};
+    if (l == 0) segs[k] = WalkSeg{pos, n, fl};
 }
 
 // Per segment on the chain: the record where the chain enters (found by the
@@ -568,7 +592,7 @@ __global__ void k_walk_emit(uint32_t cap, const WalkRec* __restrict__ recs, cons
 
 void launch_walk(hipStream_t s, const WalkLaunch& W) {
     const uint32_t nseg = W.nseg;
-    hipLaunchKernelGGL(k_walk_seg, dim3((nseg + 63) / 64), dim3(kWalkWaves * 64), 0, s, W.bytes, W.base, W.len, W.start,
+    hipLaunchKernelGGL(k_walk_seg, dim3(nseg), dim3(kWave), 0, s, W.bytes, W.base, W.len, W.start,
                        W.end, W.seg, nseg, W.cap, W.recs, reinterpret_cast<WalkSeg*>(W.segs));
     hipLaunchKernelGGL(k_walk_link, dim3((nseg + 255) / 256), dim3(256), 0, s, W.start, W.seg, nseg, W.cap, W.recs,
                        reinterpret_cast<const WalkSeg*>(W.segs), reinterpret_cast<WalkLink*>(W.links));

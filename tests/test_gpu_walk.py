@@ -111,3 +111,53 @@ def test_mutants_never_listed_wrong(ctx):
         ch = to_desc(O.Chunk(*c))  # _mutants yields the manifest's chunk list
         settled += check(ctx, bytes(f), ch, segs=(256, 4096)) > 0
     assert settled > 0
+
+
+def _decode_all(ctx, f, opt):
+    """Every chunk of `f` uploaded with device_walk = opt: (rc, canonical bytes)."""
+    ctx.set_option("device_walk", opt)
+    try:
+        try:
+            F = capi.File(f)
+        except capi.PqError as e:
+            return [("file", str(e))]
+        out = []
+        for rg in range(F.num_row_groups):
+            for col in range(F.num_columns):
+                try:
+                    ch = F.chunk(rg, col)
+                except capi.PqError as e:
+                    out.append(("chunk", str(e)))
+                    continue
+                try:
+                    dc = ctx.upload(f, [ch])
+                    dc.decode()
+                    h = dc.to_host()
+                    out.append((h.validity.tobytes(), h.data.tobytes(),
+                                None if h.offsets is None else h.offsets.tobytes()))
+                    dc.free()
+                except capi.PqError as e:
+                    out.append(("err", e.code, str(e)))
+        return out
+    finally:
+        ctx.set_option("device_walk", 0)
+
+
+@pytest.mark.parametrize("kind", ["golden", "generated", "mutants"])
+def test_upload_option_device_walk(ctx, kind):
+    """pq_chunk_upload with the device_walk option: the same decode (or the
+    same error) as the host-walked upload, on the golden fixtures, generated
+    ref/arrow files and mutated fixtures (refused chunks walk on the host)."""
+    files = []
+    if kind == "golden":
+        for path in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "*.parquet")))[:40]:
+            with open(path, "rb") as fh:
+                files.append(fh.read())
+    elif kind == "generated":
+        for cols, seed, layout in ((gen.c2_cols(), 2, gen.REF_LAYOUT), (gen.c3_cols(), 3, gen.REF_LAYOUT),
+                                   (gen.c2_cols(), 2, gen.ARROW_LAYOUT)):
+            files.append(gen.build(cols, 150_000, 2, seed=seed, layout=layout))
+    else:
+        files = [f for _, f, _ in _mutants(40, seed=31)]
+    for f in files:
+        assert _decode_all(ctx, f, 1) == _decode_all(ctx, f, 0)
