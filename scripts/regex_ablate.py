@@ -9,6 +9,8 @@ import os
 sys.path[:0] = ["/root/repo", os.environ.get("AB_PKG") or "/root/repo/duckdb-parquet-parser_amd"]
 from pqgpu import capi, gen  # noqa: E402
 ctx = capi.Context(0)
+# RX_INDEX=2: cold scans (every scan walks the length chains and files the index)
+ctx.set_option("regex_index", int(os.environ.get("RX_INDEX", "1")))
 f = gen.build(gen.c3_cols(), 10_000_000, 1, seed=gen.CONFIG_SEEDS["C3"])
 F = capi.File(f)
 for win in [int(a) for a in sys.argv[1:]] or [8192]:
@@ -26,6 +28,7 @@ for win in [int(a) for a in sys.argv[1:]] or [8192]:
         ctx.sync()
         ms, n = ctx.timing_get("regex_plain")
         ctx.timing(False)
-        print(json.dumps({"win": win, "dbg": dbg, "ms": round(ms / n, 4)}), flush=True)
+        print(json.dumps({"win": win, "dbg": dbg, "index": int(os.environ.get("RX_INDEX", "1")), "ms": round(ms / n, 4),
+                          "payload_frac_of_8TBs": round(dc.payload_bytes / (ms / n * 1e-3) / 8e12, 4)}), flush=True)
     ctx.set_option("regex_debug", 0)
     dc.free()
