@@ -177,14 +177,14 @@ int pq_ctx_sync(pq_ctx* ctx);
  *                 "stage_streams" DMA queues the pieces alternate over, 1..2 (2);
  *                 "raw_upload" 1 (default): chunks with a known byte extent go to
  *                 HBM as raw file bytes while the host walks, the slot image is
- *                 then built on the GPU (0: the host builds it)
+ *                 then built on the GPU (0: the host builds it);
+ *                 "device_walk" 0 (default) / 1: with the raw upload, the page
+ *                 walk runs on the GPU (pq_build_page_table_device) once the
+ *                 raw bytes are in HBM; a chunk it refuses walks on the host
  *   "regex_dfa", "regex_plain", "regex_codes" 1 (default): DFA kernels, the
  *                 windowed kernel for dictionary-free chunks, match bits over
  *                 the pipe's codes; "regex_win" window bytes (1024..32768,
- *                 multiple of 16; 8192); "regex_prefetch" 1 (default): the
- *                 windowed kernel holds the next window's bytes in registers
- *                 (0: a lighter build of it, four waves per SIMD where the
- *                 LDS allows); "regex_reuse" 1 (default): a scan
+ *                 multiple of 16; 8192); "regex_reuse" 1 (default): a scan
  *                 of a chunk whose earlier pipe decode was checked error-free
  *                 (pq_decode / pq_decode_check) reads that decode's codes
  *                 instead of recomputing them; "regex_index" 1 (default): a
@@ -210,7 +210,7 @@ int pq_build_page_table(const uint8_t* file, size_t file_len, const pq_chunk_des
  * chunk's bytes are already in HBM at d_bytes, holding file offsets
  * [base, base + len) (16-byte aligned; zeros are read past its end).  The
  * extent is cut into segments of seg_bytes (0: 8 KiB) walked speculatively,
- * one lane each, linked where each segment's chain leaves it
+ * one wavefront each, linked where each segment's chain leaves it
  * (csrc/kernels/walk.hip), with at most rec_cap pages per segment (0:
  * seg_bytes / 128).  Returns 0 with the same pages pq_build_page_table
  * lists (up to `cap` written to host `pages`, *npages = pages), or
