@@ -847,8 +847,8 @@ def wide_dict_leg(J, args):
 
 def ext_leg(J, args):
     """SURVEY §8f rank 4 (outside the reference's scope): the C3 and C2
-    columns as pyarrow writes them with SNAPPY (V1 pages) and LZ4_RAW
-    (DATA_PAGE_V2), 1 MiB pages; upload with PQ_EXT_CODECS | PQ_EXT_PAGE_V2
+    columns as pyarrow writes them with SNAPPY (V1 pages), LZ4_RAW
+    (DATA_PAGE_V2) and ZSTD (V1 pages, level 1), 1 MiB pages; upload with PQ_EXT_CODECS | PQ_EXT_PAGE_V2
     (the codec pass rebuilds every page on the GPU, codec.hip), then decode.
     Checked byte for byte against the uncompressed decode of the same column."""
     import io
@@ -862,7 +862,8 @@ def ext_leg(J, args):
     from pqgpu import capi, gen
     out = {}
     for name, cols, seed, use_dict, codec, ver in (("c3_snappy_v1", gen.c3_cols(), gen.CONFIG_SEEDS["C3"], False, "SNAPPY", "1.0"),
-                                                   ("c2_lz4raw_v2", gen.c2_cols(), gen.CONFIG_SEEDS["C2"], True, "LZ4", "2.0")):
+                                                   ("c2_lz4raw_v2", gen.c2_cols(), gen.CONFIG_SEEDS["C2"], True, "LZ4", "2.0"),
+                                                   ("c3_zstd_v1", gen.c3_cols(), gen.CONFIG_SEEDS["C3"], False, "ZSTD", "1.0")):
         rows = args.rows
         f = gen.build(cols, rows, 1, seed=seed, first_rg=J.rank)
         dc = J.ctx.upload(f, [capi.File(f).chunk(0, 0)])

@@ -1838,7 +1838,9 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                 if (gz && other) {
                     rc = set_err(ctx, PQ_ERR_CODEC, "GZIP pages mixed with other codecs in one upload");
                 } else {
-                    pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus, gz);
+                    const bool zstd = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec == 6; });
+                    pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus,
+                                      gz ? 1 : (zstd ? 2 : 0));
                     rc = hip_check(ctx, hipGetLastError(), "codec launch");
                 }
             }

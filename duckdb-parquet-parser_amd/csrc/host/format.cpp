@@ -880,9 +880,9 @@ WalkResult walk_chunk(const uint8_t* file, size_t len, const pq_chunk_desc& c, i
     try {
         const bool ext_codecs = (c.ext_flags & PQ_EXT_CODECS) != 0, ext_v2 = (c.ext_flags & PQ_EXT_PAGE_V2) != 0;
         if (c.codec != 0 && !ext_codecs) throw Error(PQ_ERR_CODEC, "Only uncompressed parquet files are supported");
-        if (c.codec != 0 && c.codec != 1 && c.codec != 2 && c.codec != 5 && c.codec != 7)
+        if (c.codec != 0 && c.codec != 1 && c.codec != 2 && c.codec != 5 && c.codec != 6 && c.codec != 7)
             throw Error(PQ_ERR_CODEC, "Unsupported compression codec " + std::to_string(c.codec) +
-                                          " (SNAPPY, GZIP, LZ4 and LZ4_RAW are decoded)");
+                                          " (SNAPPY, GZIP, LZ4, ZSTD and LZ4_RAW are decoded)");
         const int32_t cflag = c.codec != 0 ? (PQ_PAGE_COMPRESSED | (c.codec << 8)) : 0;
         int64_t off = c.data_page_offset;
         if (c.has_dictionary_page_offset) off = std::min(off, c.dictionary_page_offset);

@@ -29,11 +29,17 @@
 //                       canonical bit-serial walk
 //   LZ4      (codec 5): Hadoop framing ([u32 BE raw][u32 BE packed] blocks)
 //   LZ4_RAW  (codec 7): one LZ4 block
+//   ZSTD     (codec 6): RFC 8878 frames (zstd.hpp, the decoder the host tests
+//                       pin against pyarrow's zstd); Huffman literals go to
+//                       the slot's tail (at or past every byte still to be
+//                       written) and are copied out by the sequences; matches
+//                       farther back than the ring read the flushed output
 #include <algorithm>
 #include <cstddef>
 
 #include "kernels/device_common.hpp"
 #include "kernels/kernels.hpp"
+#include "kernels/zstd.hpp"
 #include "pq_gpu.h"
 
 namespace pqk {
@@ -58,6 +64,7 @@ struct CodecLds {
     uint8_t lens[320];        // code lengths: litlen [0, 288), dist [288, 320)
     uint16_t nxt[16], offs[16];  // build_code: next code / next symbol slot per length
     uint32_t scratch[4];
+    uint8_t zstage[64];       // ZSTD: literals on their way to the slot's tail
     uint32_t crc_tab[256];    // CRC-32 (gzip trailers): byte table
 };
 
@@ -695,13 +702,113 @@ __device__ __forceinline__ void gzip(CodecLds& L, In& I, Out<true>& O, uint32_t 
     }
 }
 
+// ── ZSTD adapters (zstd.hpp's source and output over In and the ring) ────
+struct ZSrc {
+    In* I;
+    uint32_t base, len;  // the zstd stream: input bytes [base, base + len)
+    __device__ __forceinline__ uint32_t byte(uint32_t q) const {
+        if (q >= len) return 0u;
+        const uint32_t p = base + q;
+        // the decoder reads forward (headers, raw blocks) and backward (bit
+        // streams): refill with p mid-window
+        if (p < I->wlo || p + 1 + I->sh > I->wlo + kInWin) I->refill(p > kInWin / 2 ? p - kInWin / 2 : 0u);
+        return I->byte(p);
+    }
+};
+
+template <class OutT>
+struct ZOut {
+    OutT* O;
+    In* I;
+    uint32_t base;         // input offset of the zstd stream (raw blocks)
+    lds8* stage;           // 64 literal bytes on their way to the slot
+    uint32_t litbase = 0;  // slot offset of the block's literals: its tail, past every byte still to be written
+    uint32_t nlit = 0, lp = 0, lk0 = 0, ln = 0;
+    __device__ __forceinline__ bool lit_begin(uint32_t n) {
+        if (O->st != ST_OK || n > O->cap - O->op) return false;
+        litbase = O->cap - n;
+        nlit = n;
+        lp = 0;
+        ln = 0;
+        return true;
+    }
+    __device__ __forceinline__ void lit_flush() {
+        wsync();
+        if (lane() < ln) O->dst[litbase + lk0 + lane()] = stage[lane()];
+        ln = 0;
+        wsync();
+    }
+    __device__ __forceinline__ void lit_at(uint32_t k, uint32_t b) {
+        if (ln && k != lk0 + ln) lit_flush();
+        if (ln == 0) lk0 = k;
+        if (lane() == 0) stage[ln] = static_cast<uint8_t>(b);
+        ln++;
+        if (ln == kWave) lit_flush();
+    }
+    __device__ __forceinline__ void visible() {  // this wave's global stores -> its later global loads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __device__ __forceinline__ void lit_done() {
+        if (ln) lit_flush();
+        visible();
+    }
+    __device__ __forceinline__ bool lits(uint32_t n) {
+        if (lp + n > nlit || !O->room(n)) return false;
+        for (uint32_t d = 0; d < n; d += kWave) {
+            const uint32_t m = min(static_cast<uint32_t>(kWave), n - d);
+            if (lane() < m) O->ring[(O->op + lane()) & kRingMask] = O->dst[litbase + lp + d + lane()];
+            O->op += m;
+            wsync();
+            if (O->op - O->fl >= kFlush) O->flush(false);
+        }
+        lp += n;
+        return O->st == ST_OK;
+    }
+    __device__ __forceinline__ bool raw(uint32_t p, uint32_t n) {
+        O->lit(*I, base + p, n);
+        return O->st == ST_OK;
+    }
+    __device__ __forceinline__ bool rle(uint32_t b, uint32_t n) {
+        if (!O->room(n)) return false;
+        for (uint32_t d = 0; d < n; d += kWave) {
+            const uint32_t m = min(static_cast<uint32_t>(kWave), n - d);
+            if (lane() < m) O->ring[(O->op + lane()) & kRingMask] = static_cast<uint8_t>(b);
+            O->op += m;
+            wsync();
+            if (O->op - O->fl >= kFlush) O->flush(false);
+        }
+        return true;
+    }
+    __device__ __forceinline__ uint32_t copy(uint32_t off, uint32_t n) {
+        if (off == 0 || off > O->op - O->vbase) return zs::ZS_CORRUPT;
+        if (off < kRing - 2 * kFlush) {  // from the ring
+            O->copy(off, n);
+            return O->st == ST_OK ? zs::ZS_OK : (O->st == ST_SIZE ? zs::ZS_SIZE : zs::ZS_CORRUPT);
+        }
+        // farther back than the ring: every source byte is flushed (the ring
+        // keeps < kFlush unflushed bytes), read from the slot
+        if (!O->room(n)) return zs::ZS_SIZE;
+        for (uint32_t d = 0; d < n; d += kWave) {
+            visible();
+            const uint32_t m = min(static_cast<uint32_t>(kWave), n - d);
+            if (lane() < m) O->ring[(O->op + lane()) & kRingMask] = O->dst[O->op + lane() - off];
+            O->op += m;
+            wsync();
+            if (O->op - O->fl >= kFlush) O->flush(false);
+        }
+        return zs::ZS_OK;
+    }
+};
+
 // kGzip: the GZIP instantiation (CRC-32 on, DEFLATE); the other one takes
 // every other codec and the V2 rebuild.  A chunk has one codec, so one
 // launch takes one instantiation (launch_codec).
-template <bool kGzip>
+template <int kKind>
 __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src, uint8_t* __restrict__ img,
                                                  const CodecEntry* __restrict__ ent, int32_t n,
                                                  uint32_t* __restrict__ status) {
+    constexpr bool kGzip = kKind == 1, kZstd = kKind == 2;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     CodecLds& L = *reinterpret_cast<CodecLds*>(smem);
     lds8* lring = (lds8*)(smem + offsetof(CodecLds, ring));
@@ -751,6 +858,19 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
                     case 1: snappy(I, O, p, end, expect); break;
                     case 5: lz4_hadoop(I, O, p, end); break;
                     case 7: lz4_block(I, O, p, end); break;
+                    case 6:
+                        if constexpr (kZstd) {
+                            // the tables after CodecLds (this instantiation's launch only)
+                            zs::ZTables& T = *reinterpret_cast<zs::ZTables*>(smem + sizeof(CodecLds));
+                            const ZSrc zsrc{&I, p, end - p};
+                            ZOut<Out<false>> zo{&O, &I, p, (lds8*)(smem + offsetof(CodecLds, zstage))};
+                            const uint32_t st = zs::decompress(zsrc, end - p, T, zo);
+                            if (O.st == ST_OK && st != zs::ZS_OK)
+                                O.st = st == zs::ZS_SIZE ? ST_SIZE : (st == zs::ZS_UNSUPPORTED ? ST_UNSUPPORTED : ST_CORRUPT);
+                            break;
+                        }
+                        O.st = ST_UNSUPPORTED;
+                        break;
                     default: O.st = ST_UNSUPPORTED;  // (GZIP: the other instantiation)
                 }
             }
@@ -767,15 +887,18 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
 size_t codec_lds_bytes() { return sizeof(CodecLds); }
 
 void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
-                  uint32_t* status, int cus, bool gzip) {
+                  uint32_t* status, int cus, int kind) {
     if (n <= 0) return;
-    const uint32_t lds = static_cast<uint32_t>(sizeof(CodecLds));
-    const void* k = gzip ? reinterpret_cast<const void*>(k_codec<true>) : reinterpret_cast<const void*>(k_codec<false>);
+    // kind 2 (ZSTD) carries its decode tables after CodecLds
+    const uint32_t lds = static_cast<uint32_t>(sizeof(CodecLds) + (kind == 2 ? sizeof(zs::ZTables) : 0));
+    const void* k = kind == 1 ? reinterpret_cast<const void*>(k_codec<1>)
+                              : (kind == 2 ? reinterpret_cast<const void*>(k_codec<2>) : reinterpret_cast<const void*>(k_codec<0>));
     ensure_dyn_lds(k, lds);
     const int per_cu = std::max(1, static_cast<int>((160u * 1024u) / lds));
     const int grid = std::min(n, std::max(1, cus) * per_cu);
-    if (gzip) hipLaunchKernelGGL(k_codec<true>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
-    else hipLaunchKernelGGL(k_codec<false>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
+    if (kind == 1) hipLaunchKernelGGL(k_codec<1>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
+    else if (kind == 2) hipLaunchKernelGGL(k_codec<2>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
+    else hipLaunchKernelGGL(k_codec<0>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
 }
 
 }  // namespace pqk

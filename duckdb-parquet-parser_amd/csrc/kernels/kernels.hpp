@@ -75,11 +75,12 @@ struct CodecEntry {
     uint32_t flags;    // kCodec*
 };
 size_t codec_lds_bytes();
-// status[i]: 0 ok, 1 corrupt input, 2 size mismatch, 3 unsupported.  gzip:
-// the entries include GZIP pages (the CRC-32 instantiation; it takes codec 0
-// and 2 only, the other one every codec but 2)
+// status[i]: 0 ok, 1 corrupt input, 2 size mismatch, 3 unsupported.  kind:
+// 1 the entries include GZIP pages (the CRC-32 instantiation; it takes codec
+// 0 and 2 only), 2 they include ZSTD pages (its decode tables in LDS; every
+// codec but 2), 0 neither
 void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
-                  uint32_t* status, int cus, bool gzip);
+                  uint32_t* status, int cus, int kind);
 
 // 4 KiB chunker (chunker.hip, src/main.cpp:17-32): device scratch bytes for
 // n rows, and the launch sequence (synchronises the stream; 0 = OK).

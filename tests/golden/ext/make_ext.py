@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Fixtures for the extended format scope: compressed
-pages (SNAPPY, GZIP, LZ4_RAW) and DATA_PAGE_V2 pages, written by pyarrow 25
+pages (SNAPPY, GZIP, LZ4_RAW, ZSTD) and DATA_PAGE_V2 pages, written by pyarrow 25
 (the oracle for this row: the reference rejects every codec,
 column_reader.cpp:13-15, and does not decode V2 pages, 56-67).
 
@@ -19,7 +19,7 @@ import pyarrow as pa
 import pyarrow.parquet as pq
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-CODECS = ["none", "snappy", "gzip", "lz4"]
+CODECS = ["none", "snappy", "gzip", "lz4", "zstd"]
 VERSIONS = ["1.0", "2.0"]
 ROWS = 3000
 RG_ROWS = 1500
@@ -85,12 +85,21 @@ def canonical_dump(col: pa.ChunkedArray) -> bytes:
 
 
 def main():
+    # --new: write only the files the manifest does not list yet (the others
+    # stay byte for byte as committed)
+    only_new = "--new" in sys.argv
     t = table(ROWS)
     man = {"rows": ROWS, "rg_rows": RG_ROWS, "pyarrow": pa.__version__, "files": {}}
+    mpath = os.path.join(HERE, "manifest.json")
+    if only_new and os.path.exists(mpath):
+        with open(mpath) as fh:
+            man = json.load(fh)
     for codec in CODECS:
         for v in VERSIONS:
             name = f"ext_{codec}_v{v[0]}.parquet"
             path = os.path.join(HERE, name)
+            if only_new and name in man["files"]:
+                continue
             write(t, path, codec, v)
             back = pq.read_table(path)
             cols = {}

@@ -10,7 +10,7 @@ from pqgpu import capi
 
 MAN = manifest()
 FILES = sorted(MAN["files"])
-CODEC_ID = {"none": 0, "snappy": 1, "gzip": 2, "lz4": 7}
+CODEC_ID = {"none": 0, "snappy": 1, "gzip": 2, "lz4": 7, "zstd": 6}
 
 
 def test_manifest_matches_pyarrow():
@@ -71,9 +71,9 @@ def test_reference_scope_rejects_codecs(name):
 def test_unknown_codec_rejected():
     f = load("ext_snappy_v1.parquet")
     d = ext_chunks(f, 0)[0]
-    d.codec = 6  # ZSTD: not decoded
+    d.codec = 4  # BROTLI: not decoded
     rc, msg, _ = capi.build_page_table(f, d)
-    assert rc == -1 and "Unsupported compression codec 6" in msg
+    assert rc == -1 and "Unsupported compression codec 4" in msg
 
 
 def test_v2_without_flag_is_not_counted():

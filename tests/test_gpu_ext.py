@@ -1,5 +1,5 @@
 """GPU parity for the extended format scope: compressed
-pages (SNAPPY, GZIP, LZ4_RAW; codec.hip) and DATA_PAGE_V2 pages, decoded
+pages (SNAPPY, GZIP, LZ4_RAW, ZSTD; codec.hip) and DATA_PAGE_V2 pages, decoded
 through the C ABI with PQ_EXT_* flags and compared bit for bit with pyarrow's
 reading of the same file (the oracle for this row; the reference decodes
 neither).  Expectations: tests/golden/ext/manifest.json (make_ext.py)."""
@@ -42,7 +42,7 @@ def test_ext_regex_same_across_codecs(ctx, version):
     uncompressed file (same table, same page boundaries)."""
     for pattern, neg in (("^[a-d][a-e]", False), ("q", True), ("x.*y", False)):
         base = None
-        for codec in ("none", "snappy", "gzip", "lz4"):
+        for codec in ("none", "snappy", "gzip", "lz4", "zstd"):
             f = load(f"ext_{codec}_v{version}.parquet")
             dc = ctx.upload(f, ext_chunks(f, 1))
             try:
@@ -58,7 +58,8 @@ def test_ext_regex_same_across_codecs(ctx, version):
 
 def test_ext_repeat_uploads(ctx):
     """The codec pass reuses its context buffers across uploads of different sizes."""
-    for name in ("ext_gzip_v1.parquet", "ext_snappy_v2.parquet", "ext_lz4_v1.parquet", "ext_gzip_v2.parquet"):
+    for name in ("ext_gzip_v1.parquet", "ext_snappy_v2.parquet", "ext_lz4_v1.parquet", "ext_gzip_v2.parquet",
+                 "ext_zstd_v1.parquet", "ext_zstd_v2.parquet"):
         f = load(name)
         got = capi.canonical_dump(decode(ctx, f, 0))
         assert sha(got) == MAN["files"][name]["columns"]["s_dict"]["sha256"]
@@ -78,7 +79,8 @@ def test_ext_host_fill_path(ctx):
         ctx.set_option("raw_upload", 1)
 
 
-@pytest.mark.parametrize("name", ["ext_snappy_v1.parquet", "ext_gzip_v1.parquet", "ext_lz4_v2.parquet"])
+@pytest.mark.parametrize("name", ["ext_snappy_v1.parquet", "ext_gzip_v1.parquet", "ext_lz4_v2.parquet",
+                                  "ext_zstd_v1.parquet"])
 def test_ext_corrupt_page_fails_cleanly(ctx, name):
     """Damaged compressed bytes end in an error (decompression or decode), never a fault."""
     f = bytearray(load(name))
@@ -111,7 +113,7 @@ except ImportError:  # pragma: no cover
 
 
 @pytest.mark.skipif(pa is None, reason="pyarrow not importable")
-@pytest.mark.parametrize("codec", ["snappy", "gzip", "lz4"])
+@pytest.mark.parametrize("codec", ["snappy", "gzip", "lz4", "zstd"])
 @pytest.mark.parametrize("version", ["1.0", "2.0"])
 def test_ext_large_pages_vs_pyarrow(ctx, tmp_path, codec, version):
     """1 MiB pages (pyarrow's default), 400k rows: dictionary and PLAIN
