@@ -8,9 +8,10 @@
 // computes the same scalar values, the output stage spreads copies over the
 // lanes) and in the host harness the tests use to pin it against pyarrow's
 // zstd (tools/zstd_check.cpp):
-//   src.byte(p)             input byte p (0 past the end)
-//   out.lit(n) / out.rle(b, n) / out.raw(p, n) / out.copy(off, n) / out.put_lits(...)
-//   tables: ZTables (FSE and Huffman decode tables, LDS on the device)
+//   src.byte(p)   input byte p (0 past the end)
+//   out           lit_begin(n) / lit_at(k, b) / lit_done(): the block's literals;
+//                 lits(n), raw(p, n), rle(b, n), copy(offset, n): the output
+//   ZTables       FSE and Huffman decode tables (LDS on the device)
 // Literals decoded by Huffman go to a literal buffer the output stage owns
 // (out.lit_at / out.lit_done); sequences then copy from it.
 // Not supported (status ZS_UNSUPPORTED): dictionaries (a frame naming a
@@ -48,6 +49,7 @@ struct ZTables {
     int16_t norm[64];            // normalized counts (build scratch)
     uint16_t next[64];           // symbolNext (build scratch)
     uint8_t weights[256];
+    uint32_t llc[36], mlc[53];   // code -> baseline | extra bits << 24 (filled by decompress)
     uint32_t ll_log, ml_log, of_log, huf_bits;
     uint32_t have_ll, have_ml, have_of, have_huf;  // repeat modes: a table from an earlier block
 };
@@ -76,7 +78,9 @@ template <class Src>
 struct BitB {
     const Src* src;
     uint32_t base, len;
-    int64_t pos;  // bits left above bit 0 (negative: read past the start)
+    int64_t pos;   // bits left above bit 0 (negative: read past the start)
+    uint64_t cont; // bits [clo, clo + 64) of the stream (0 outside it)
+    int64_t clo;
     ZS_HD bool init(const Src& s, uint32_t b, uint32_t l) {
         src = &s;
         base = b;
@@ -85,13 +89,32 @@ struct BitB {
         const uint32_t last = s.byte(b + l - 1);
         if (last == 0) return false;
         pos = static_cast<int64_t>(8 * (l - 1) + highbit(last));
+        fill(pos);
         return true;
+    }
+    // the 8 bytes that end with the byte holding bit e - 1 (a reader moving
+    // down the stream refills about once per 7 bytes)
+    ZS_HD void fill(int64_t e) {
+        const int64_t bend = (e + 7) >> 3;  // exclusive byte end
+        uint64_t v = 0;
+        for (int k = 0; k < 8; k++) {
+            const int64_t b = bend - 8 + k;
+            const uint32_t x = (b >= 0 && b < static_cast<int64_t>(len)) ? src->byte(base + static_cast<uint32_t>(b)) : 0u;
+            v |= static_cast<uint64_t>(x) << (8 * k);
+        }
+        cont = v;
+        clo = (bend - 8) * 8;
+    }
+    ZS_HD uint32_t get(int64_t lo, uint32_t n) {  // n <= 32
+        if (n == 0) return 0u;
+        if (lo < clo || lo + n > clo + 64) fill(lo + n);
+        return static_cast<uint32_t>((cont >> (lo - clo)) & ((n == 32) ? 0xFFFFFFFFull : ((1ull << n) - 1ull)));
     }
     ZS_HD uint32_t read(uint32_t n) {
         pos -= n;
-        return bits_at(*src, base, len, pos, n);
+        return get(pos, n);
     }
-    ZS_HD uint32_t peek(uint32_t n) const { return bits_at(*src, base, len, pos - n, n); }
+    ZS_HD uint32_t peek(uint32_t n) { return get(pos - n, n); }
 };
 
 // FSE table description (forward bit stream at src[p ..], at most `end`):
@@ -480,8 +503,9 @@ ZS_HD uint32_t block(const Src& src, uint32_t p, uint32_t bsize, ZTables& T, Out
         if (oc > 31 || mc > kMLMax || lc > kLLMax) return ZS_CORRUPT;
         uint32_t ofv = oc < 32 ? (1u << oc) : 0u;
         ofv += bs.read(oc);
-        const uint32_t mlv = ml_base(mc) + bs.read(ml_bits(mc));
-        const uint32_t llv = ll_base(lc) + bs.read(ll_bits(lc));
+        const uint32_t mlx = T.mlc[mc], llx = T.llc[lc];
+        const uint32_t mlv = (mlx & 0xFFFFFFu) + bs.read(mlx >> 24);
+        const uint32_t llv = (llx & 0xFFFFFFu) + bs.read(llx >> 24);
         if (i + 1 < nseq) {
             sll = el.base + bs.read(el.bits);
             sml = em.base + bs.read(em.bits);
@@ -521,6 +545,8 @@ template <class Src, class Out>
 ZS_HD uint32_t decompress(const Src& src, uint32_t len, ZTables& T, Out& out) {
     uint32_t p = 0;
     if (len == 0) return ZS_CORRUPT;
+    for (uint32_t c = 0; c < 36; c++) T.llc[c] = ll_base(c) | (ll_bits(c) << 24);
+    for (uint32_t c = 0; c < 53; c++) T.mlc[c] = ml_base(c) | (ml_bits(c) << 24);
     while (p < len) {
         if (p + 4 > len) return ZS_CORRUPT;
         const uint32_t magic = src.byte(p) | (src.byte(p + 1) << 8) | (src.byte(p + 2) << 16) | (src.byte(p + 3) << 24);
