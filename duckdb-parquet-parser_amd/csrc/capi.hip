@@ -1835,10 +1835,13 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                 Timed ct(ctx, "codec", s);
                 const bool gz = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec == 2; });
                 const bool other = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec != 2 && e.codec != 0; });
+                const bool zstd = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec == 6; });
+                const bool zother = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec != 6 && e.codec != 0; });
                 if (gz && other) {
                     rc = set_err(ctx, PQ_ERR_CODEC, "GZIP pages mixed with other codecs in one upload");
+                } else if (zstd && zother) {
+                    rc = set_err(ctx, PQ_ERR_CODEC, "ZSTD pages mixed with other codecs in one upload");
                 } else {
-                    const bool zstd = std::any_of(cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.codec == 6; });
                     pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus,
                                       gz ? 1 : (zstd ? 2 : 0));
                     rc = hip_check(ctx, hipGetLastError(), "codec launch");

@@ -64,7 +64,6 @@ struct CodecLds {
     uint8_t lens[320];        // code lengths: litlen [0, 288), dist [288, 320)
     uint16_t nxt[16], offs[16];  // build_code: next code / next symbol slot per length
     uint32_t scratch[4];
-    uint8_t zstage[64];       // ZSTD: literals on their way to the slot's tail
     uint32_t crc_tab[256];    // CRC-32 (gzip trailers): byte table
 };
 
@@ -198,8 +197,9 @@ __device__ __attribute__((noinline)) uint32_t crc_fold(const lds8* ring, const l
 // inlined, in every codec's hot loop (147 VGPRs and 64 B/lane of scratch
 // with it in round 3, against 111 VGPRs and none without): the non-GZIP
 // kernel compiles it out.
-template <bool kCrc>
+template <bool kCrc, uint32_t kRingB = kRing>
 struct Out {
+    static constexpr uint32_t kRingSize = kRingB, kMask = kRingB - 1;
     lds8* ring;
     uint8_t* dst;   // the page slot (16-byte aligned)
     uint32_t op;    // bytes produced
@@ -229,14 +229,14 @@ struct Out {
     static constexpr uint32_t kCrcSlack = 1024;
     __device__ __forceinline__ void crc_keep() {
         if constexpr (kCrc)
-            if (crc_on && op - crc_pos > kRing - kCrcSlack) crc_upto(op);
+            if (crc_on && op - crc_pos > kRingB - kCrcSlack) crc_upto(op);
     }
     __device__ __forceinline__ void flush(bool final) {
         while (op - fl >= kFlush || (final && fl < op)) {
             const uint32_t n = min(kFlush, op - fl);
             const uint32_t b = fl + 16u * lane();
             if (b < fl + n) {
-                uint4 v = lds_get16(ring, b & kRingMask);
+                uint4 v = lds_get16(ring, b & kMask);
                 if (b + 16 > op) {  // bytes past the payload stay zero (slot padding)
                     const int32_t keep = static_cast<int32_t>(op - b);
                     auto mk = [&](int j) -> uint32_t {
@@ -261,7 +261,7 @@ struct Out {
         for (uint32_t d = 0; d < n; d += kWave) {
             I.ensure(p + d, kWave);
             const uint32_t m = min(static_cast<uint32_t>(kWave), n - d);
-            if (lane() < m) ring[(op + lane()) & kRingMask] = static_cast<uint8_t>(I.byte(p + d + lane()));
+            if (lane() < m) ring[(op + lane()) & kMask] = static_cast<uint8_t>(I.byte(p + d + lane()));
             op += m;
             wsync();
             if (op - fl >= kFlush) flush(false);
@@ -270,14 +270,14 @@ struct Out {
     // copy of n bytes from distance d: 64 bytes per step, byte c0 + j of a
     // step from c0 - d + (j mod d) (d < 64) or c0 - d + j: before c0, final
     __device__ __forceinline__ void copy(uint32_t d, uint32_t n) {
-        if (d == 0 || d > op - vbase || d > kRing - 1) { st = ST_CORRUPT; return; }
+        if (d == 0 || d > op - vbase || d > kRingB - 1) { st = ST_CORRUPT; return; }
         if (!room(n)) return;
         const uint32_t r = d >= static_cast<uint32_t>(kWave) ? lane() : lane() % d;
         for (uint32_t k = 0; k < n; k += kWave) {
             const uint32_t m = min(static_cast<uint32_t>(kWave), n - k);
             if (lane() < m) {
-                const uint32_t v = ring[(op - d + r) & kRingMask];
-                ring[(op + lane()) & kRingMask] = static_cast<uint8_t>(v);
+                const uint32_t v = ring[(op - d + r) & kMask];
+                ring[(op + lane()) & kMask] = static_cast<uint8_t>(v);
             }
             op += m;
             wsync();
@@ -286,7 +286,7 @@ struct Out {
     }
     __device__ __forceinline__ void put1(uint32_t b) {
         if (!room(1)) return;
-        if (lane() == 0) ring[op & kRingMask] = static_cast<uint8_t>(b);
+        if (lane() == 0) ring[op & kMask] = static_cast<uint8_t>(b);
         op++;
         if (op - fl >= kFlush) {
             wsync();
@@ -295,7 +295,7 @@ struct Out {
     }
     __device__ __forceinline__ void put_u32(uint32_t v) {
         if (!room(4)) return;
-        if (lane() < 4) ring[(op + lane()) & kRingMask] = static_cast<uint8_t>(v >> (8 * lane()));
+        if (lane() < 4) ring[(op + lane()) & kMask] = static_cast<uint8_t>(v >> (8 * lane()));
         wsync();
         op += 4;
         flush(false);
@@ -702,6 +702,17 @@ __device__ __forceinline__ void gzip(CodecLds& L, In& I, Out<true>& O, uint32_t 
     }
 }
 
+// ZSTD's LDS (k_codec<2>): a 32 KiB ring (matches farther back read the
+// flushed slot), the staged input and the decode tables, 59 KiB in all, so
+// two pages share a CU (CodecLds with the tables: 91 KiB, one)
+constexpr uint32_t kZRing = 32768;
+struct ZCodecLds {
+    uint8_t ring[kZRing];
+    uint8_t in[kInWin + 32];
+    uint8_t zstage[64];
+    zs::ZTables T;
+};
+
 // ── ZSTD adapters (zstd.hpp's source and output over In and the ring) ────
 struct ZSrc {
     In* I;
@@ -757,7 +768,7 @@ struct ZOut {
         if (lp + n > nlit || !O->room(n)) return false;
         for (uint32_t d = 0; d < n; d += kWave) {
             const uint32_t m = min(static_cast<uint32_t>(kWave), n - d);
-            if (lane() < m) O->ring[(O->op + lane()) & kRingMask] = O->dst[litbase + lp + d + lane()];
+            if (lane() < m) O->ring[(O->op + lane()) & OutT::kMask] = O->dst[litbase + lp + d + lane()];
             O->op += m;
             wsync();
             if (O->op - O->fl >= kFlush) O->flush(false);
@@ -773,7 +784,7 @@ struct ZOut {
         if (!O->room(n)) return false;
         for (uint32_t d = 0; d < n; d += kWave) {
             const uint32_t m = min(static_cast<uint32_t>(kWave), n - d);
-            if (lane() < m) O->ring[(O->op + lane()) & kRingMask] = static_cast<uint8_t>(b);
+            if (lane() < m) O->ring[(O->op + lane()) & OutT::kMask] = static_cast<uint8_t>(b);
             O->op += m;
             wsync();
             if (O->op - O->fl >= kFlush) O->flush(false);
@@ -782,7 +793,7 @@ struct ZOut {
     }
     __device__ __forceinline__ uint32_t copy(uint32_t off, uint32_t n) {
         if (off == 0 || off > O->op - O->vbase) return zs::ZS_CORRUPT;
-        if (off < kRing - 2 * kFlush) {  // from the ring
+        if (off < OutT::kRingSize - 2 * kFlush) {  // from the ring
             O->copy(off, n);
             return O->st == ST_OK ? zs::ZS_OK : (O->st == ST_SIZE ? zs::ZS_SIZE : zs::ZS_CORRUPT);
         }
@@ -792,7 +803,7 @@ struct ZOut {
         for (uint32_t d = 0; d < n; d += kWave) {
             visible();
             const uint32_t m = min(static_cast<uint32_t>(kWave), n - d);
-            if (lane() < m) O->ring[(O->op + lane()) & kRingMask] = O->dst[O->op + lane() - off];
+            if (lane() < m) O->ring[(O->op + lane()) & OutT::kMask] = O->dst[O->op + lane() - off];
             O->op += m;
             wsync();
             if (O->op - O->fl >= kFlush) O->flush(false);
@@ -811,8 +822,9 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
     constexpr bool kGzip = kKind == 1, kZstd = kKind == 2;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     CodecLds& L = *reinterpret_cast<CodecLds*>(smem);
-    lds8* lring = (lds8*)(smem + offsetof(CodecLds, ring));
-    lds8* lin = (lds8*)(smem + offsetof(CodecLds, in));
+    lds8* lring = (lds8*)(smem + (kZstd ? offsetof(ZCodecLds, ring) : offsetof(CodecLds, ring)));
+    lds8* lin = (lds8*)(smem + (kZstd ? offsetof(ZCodecLds, in) : offsetof(CodecLds, in)));
+    using OutK = Out<kGzip, kZstd ? kZRing : kRing>;
     lds32* lcrc = (lds32*)(smem + offsetof(CodecLds, crc_tab));
     if constexpr (kGzip) {
         for (uint32_t b = lane(); b < 256; b += kWave) {  // CRC-32 byte table
@@ -826,7 +838,7 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
         const CodecEntry e = ent[i];
         In I{src + e.src, e.src_len, 0u, 0u, lin};
         I.refill(0);
-        Out<kGzip> O{lring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
+        OutK O{lring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
         O.crc_tab = lcrc;
         uint32_t p = 0;
         if (e.flags & kCodecV2) {  // level sections, as is, behind their V1 length prefixes
@@ -861,9 +873,9 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
                     case 6:
                         if constexpr (kZstd) {
                             // the tables after CodecLds (this instantiation's launch only)
-                            zs::ZTables& T = *reinterpret_cast<zs::ZTables*>(smem + sizeof(CodecLds));
+                            zs::ZTables& T = *reinterpret_cast<zs::ZTables*>(smem + offsetof(ZCodecLds, T));
                             const ZSrc zsrc{&I, p, end - p};
-                            ZOut<Out<false>> zo{&O, &I, p, (lds8*)(smem + offsetof(CodecLds, zstage))};
+                            ZOut<OutK> zo{&O, &I, p, (lds8*)(smem + offsetof(ZCodecLds, zstage))};
                             const uint32_t st = zs::decompress(zsrc, end - p, T, zo);
                             if (O.st == ST_OK && st != zs::ZS_OK)
                                 O.st = st == zs::ZS_SIZE ? ST_SIZE : (st == zs::ZS_UNSUPPORTED ? ST_UNSUPPORTED : ST_CORRUPT);
@@ -889,8 +901,8 @@ size_t codec_lds_bytes() { return sizeof(CodecLds); }
 void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
                   uint32_t* status, int cus, int kind) {
     if (n <= 0) return;
-    // kind 2 (ZSTD) carries its decode tables after CodecLds
-    const uint32_t lds = static_cast<uint32_t>(sizeof(CodecLds) + (kind == 2 ? sizeof(zs::ZTables) : 0));
+    // kind 2 (ZSTD): its own layout (a smaller ring and the decode tables)
+    const uint32_t lds = static_cast<uint32_t>(kind == 2 ? sizeof(ZCodecLds) : sizeof(CodecLds));
     const void* k = kind == 1 ? reinterpret_cast<const void*>(k_codec<1>)
                               : (kind == 2 ? reinterpret_cast<const void*>(k_codec<2>) : reinterpret_cast<const void*>(k_codec<0>));
     ensure_dyn_lds(k, lds);

@@ -77,8 +77,8 @@ struct CodecEntry {
 size_t codec_lds_bytes();
 // status[i]: 0 ok, 1 corrupt input, 2 size mismatch, 3 unsupported.  kind:
 // 1 the entries include GZIP pages (the CRC-32 instantiation; it takes codec
-// 0 and 2 only), 2 they include ZSTD pages (its decode tables in LDS; every
-// codec but 2), 0 neither
+// 0 and 2 only), 2 they include ZSTD pages (codecs 0 and 6 only: a 32 KiB
+// history ring and the decode tables in LDS), 0 neither
 void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
                   uint32_t* status, int cus, int kind);
 
