@@ -89,6 +89,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (control path only; the data path has no collective)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--full-json", default=os.path.join(ROOT, "gpurun_out", "bench_full.json"),
+                    help="every leg's full record goes here; stdout gets the compact headline line")
     ap.add_argument("--opt", action="append", default=[],
                     help="context option key=value set before any upload (repeatable), e.g. write_waves=8")
     return ap.parse_args()
@@ -1008,6 +1010,76 @@ def c5_leg(J, args, exp, layout="arrow"):
                                    **{k: v["ms_per_step"] for k, v in rkern.items()}}}
 
 
+HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                 "scaling", "vs_baseline", "dtype", "data", "config", "validated")
+
+
+def _r(x, nd=4):
+    return None if x is None else float(f"{x:.{nd}g}")
+
+
+def compact(res: dict, full_path: str) -> dict:
+    """The stdout line: headline keys, roofline, cpu_baseline and one small
+    summary per leg (value + roofline fraction).  Every leg's full record is
+    in `full_path` (round 5's 20 KB line was past what the driver parses)."""
+    out = {k: res[k] for k in HEADLINE_KEYS if k in res}
+    rf = res["roofline"]
+    out["roofline"] = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                              "kernel_ms", "algorithmic_bytes", "step_traffic",
+                                              "step_traffic_over_b_alg")}
+    pl = res["pipeline"]
+    out["pipeline"] = {"kernel_ms": {k: _r(v) for k, v in pl["kernel_ms"].items()},
+                       "b_alg_bytes": pl["b_alg_bytes"], "b_alg_frac_of_peak": _r(pl["b_alg_frac_of_peak"])}
+    if "cpu_baseline" in res:
+        cb = res["cpu_baseline"]
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cb}
+        for k in ("chunk_parallel", "page_parallel", "regex_native"):
+            if k in cb:
+                out["cpu_baseline"][k] = {"value": _r(cb[k]["value"]), "unit": cb[k]["unit"],
+                                          "cores": cb[k].get("cores")}
+    legs = {}
+    rx = res.get("regex")
+    if rx:
+        legs["c3_regex"] = {"pages_per_s": _r(rx["pages_per_s"]), "ms": _r(rx["ms_per_scan"]),
+                            "frac": _r(rx["roofline_frac"], 3), "pattern": rx["pattern"],
+                            "warm_ms": _r(rx["warm"]["ms_per_scan"]), "warm_frac": _r(rx["warm"]["roofline_frac"], 3),
+                            "validated": rx.get("all_validated", rx.get("validated"))}
+    cd = res.get("c3_decode")
+    if cd:
+        legs["c3_plain"] = {"values_per_s": _r(cd["values_per_s"]), "ms": _r(cd["ms_per_decode"]),
+                            "validated": cd["validated"]}
+    c4 = res.get("c4")
+    if c4:
+        legs["c4"] = {"values_per_s": _r(c4["values_per_s"]), "ms": _r(c4["ms_per_step"]),
+                      "frac": _r(c4["roofline"]["frac"], 3), "validated": c4["validated"]}
+    for k in ("c5", "c5_ref"):
+        c5 = res.get(k)
+        if c5:
+            legs[k] = {"values_per_s": _r(c5["decode_values_per_s"]), "ms": _r(c5["decode_ms"]),
+                       "step_values_per_s": _r(c5["step_values_per_s"]), "rows_per_gpu": c5["rows_per_gpu"],
+                       "validated": bool(c5["decode_validated"] and c5["regex_validated"])}
+    wd = res.get("wide_dict")
+    if wd:
+        legs["wide_dict"] = {"values_per_s": _r(wd["values_per_s"]), "ms": _r(wd["ms_per_decode"]),
+                             "frac": _r(wd["b_alg_frac_of_peak"], 3), "validated": wd["validated"]}
+    for k, v in (res.get("ext") or {}).items():
+        legs[k] = {"codec_GBs_out": _r(v["codec_GBs_out"]), "decode_ms": _r(v["decode_ms"]),
+                   "validated": v["validated"]}
+    for k, v in (res.get("end_to_end") or {}).items():
+        legs["e2e_" + k] = {"total_ms": _r(v["total_ms"])}
+        if "device_walk" in v and isinstance(v["device_walk"], dict) and "total_ms" in v["device_walk"]:
+            legs["e2e_" + k]["device_walk_total_ms"] = _r(v["device_walk"]["total_ms"])
+    if "api_read_all" in res:
+        a = res["api_read_all"]
+        legs["api_read_all"] = {"values_per_s": _r(a["values_per_s"]), "threads": a.get("threads")}
+    if "strong" in res:
+        legs["strong"] = {k: _r(v) if isinstance(v, float) else v for k, v in res["strong"].items()
+                          if not isinstance(v, (dict, list))}
+    out["legs"] = legs
+    out["full_record"] = os.path.relpath(full_path, ROOT)
+    return out
+
+
 def main():
     args = parse()
     maybe_spawn(args)
@@ -1125,7 +1197,13 @@ def main():
                                   **{k: v for k, v in cpu.items() if k != "single_thread"}}
     ctx.close()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        path = args.full_json
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as fh:
+            json.dump(result, fh, indent=1)
+        line = json.dumps(compact(result, path))
+        assert len(line) < 6000, f"headline line {len(line)} B: the driver reads ~8 KB of stdout"
+        print(line, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -1008,6 +1008,7 @@ static int device_walk(pq_ctx* ctx, const uint8_t* d_bytes, size_t len, int64_t 
     if (chunk->has_dictionary_page_offset) off = std::min(off, chunk->dictionary_page_offset);
     if (off < base || off >= base + static_cast<int64_t>(len)) return PQ_ERR_UNSUPPORTED;
     const uint64_t seg = seg_bytes ? static_cast<uint64_t>(seg_bytes) : 8192u;
+    if (seg > (1u << 30) || rec_cap < 0 || rec_cap > (int64_t{1} << 20)) return PQ_ERR_UNSUPPORTED;
     const uint32_t rc = static_cast<uint32_t>(rec_cap ? rec_cap : std::max<int64_t>(1, static_cast<int64_t>(seg) / 128));
     const uint64_t start = static_cast<uint64_t>(off), end = static_cast<uint64_t>(base) + len;
     const uint64_t nseg64 = (end - start + seg - 1) / seg;
@@ -1082,8 +1083,8 @@ extern "C" {
 int pq_build_page_table_device(pq_ctx* ctx, const uint8_t* d_bytes, size_t len, int64_t base,
                                const pq_chunk_desc* chunk, int64_t seg_bytes, int64_t rec_cap,
                                pq_page_desc* pages, int64_t cap, int64_t* npages) {
-    if (!ctx || !chunk || !npages || (!d_bytes && len) || base < 0 || seg_bytes < 0 || rec_cap < 0 || cap < 0 ||
-        (cap && !pages))
+    if (!ctx || !chunk || !npages || (!d_bytes && len) || base < 0 || seg_bytes < 0 || seg_bytes > (int64_t{1} << 30) ||
+        rec_cap < 0 || rec_cap > (int64_t{1} << 20) || cap < 0 || (cap && !pages))
         return PQ_ERR_ARG;
     *npages = 0;
     DevGuard dg(ctx);
@@ -1150,8 +1151,6 @@ static void raw_start(pq_ctx* ctx, const uint8_t* file, size_t file_len, RawStag
     const size_t need = static_cast<size_t>(R.total) + 64;
     if (ctx->raw_cap < need) {
         if (ctx->d_raw) (void)hipFree(ctx->d_raw);
-    if (ctx->d_walk) (void)hipFree(ctx->d_walk);
-    if (ctx->h_walk) (void)hipHostFree(ctx->h_walk);
         ctx->d_raw = nullptr;
         ctx->raw_cap = 0;
         if (hipMalloc(reinterpret_cast<void**>(&ctx->d_raw), need) != hipSuccess) {

@@ -357,7 +357,9 @@ __global__ void __launch_bounds__(kWave) k_walk_seg(const uint8_t* __restrict__ 
     uint32_t n = 0, fl = 0;
     while (pos < hi) {
         const uint32_t o = load_win(win, d, base, len, pos);
-        if (!dev_parse(wb + o, kWin, h) || h.comp < 0) { fl |= 2u; break; }
+        // a header reaching past the extent parsed zeros the host walk would
+        // read as file bytes: refuse rather than emit a different table
+        if (!dev_parse(wb + o, kWin, h) || h.comp < 0 || pos + h.hs > end) { fl |= 2u; break; }
         if (n == cap) { fl |= 1u; break; }
         if (l == 0) {
             WalkRec x;

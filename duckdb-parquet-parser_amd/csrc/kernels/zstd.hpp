@@ -128,6 +128,7 @@ ZS_HD uint32_t read_norm(const Src& src, uint32_t p, uint32_t end, int max_sym, 
     log = (bits_at(src, p, len, bp, 4)) + 5;
     bp += 4;
     if (log > max_log) return 0;
+    if (max_sym > 63) max_sym = 63;  // T.norm / T.next hold 64 symbols; no zstd alphabet is larger
     int32_t remaining = (1 << log) + 1;
     int32_t threshold = 1 << log;
     uint32_t nb = log + 1;
@@ -309,7 +310,7 @@ ZS_HD uint32_t read_huf(const Src& src, uint32_t p, uint32_t end, ZTables& T) {
         if (hb == 0 || p + 1 + hb > end) return 0;
         uint32_t lg = 0;
         int ns = 0;
-        const uint32_t d = read_norm(src, p + 1, p + 1 + hb, 255, 6, T, lg, ns);
+        const uint32_t d = read_norm(src, p + 1, p + 1 + hb, 12, 6, T, lg, ns);  // weights 0..12 (RFC 8878 4.2.1.2)
         if (d == 0 || d >= hb || !build_fse(T, T.wt, lg, ns)) return 0;
         BitB<Src> bs;
         if (!bs.init(src, p + 1 + d, hb - d)) return 0;

@@ -161,3 +161,28 @@ def test_upload_option_device_walk(ctx, kind):
         files = [f for _, f, _ in _mutants(40, seed=31)]
     for f in files:
         assert _decode_all(ctx, f, 1) == _decode_all(ctx, f, 0)
+
+
+def test_walk_buffers_survive_raw_regrowth():
+    """A device walk, then an upload whose raw extent is larger than any
+    before (the raw buffer regrows), then device walks again and the context
+    is destroyed: the walk's buffers stay the walk's own (round-5 advice: the
+    raw regrowth used to free them behind the walk's back)."""
+    ctx = capi.Context(0)
+    try:
+        ctx.set_option("device_walk", 1)
+        small = gen.build(gen.c2_cols(), 20_000, 1, seed=2)
+        big = gen.build(gen.c2_cols(), 600_000, 1, seed=2)
+        want = {}
+        for f in (small, big, small, big):
+            ch = capi.File(f).chunk(0, 0)
+            dc = ctx.upload(f, [ch])
+            dc.decode()
+            h = dc.to_host()
+            got = (h.validity.tobytes(), h.data.tobytes(), h.offsets.tobytes())
+            assert want.setdefault(len(f), got) == got
+            dc.free()
+            assert check(ctx, f, ch, segs=(0, 2048)) >= 1
+    finally:
+        ctx.set_option("device_walk", 0)
+        ctx.close()
