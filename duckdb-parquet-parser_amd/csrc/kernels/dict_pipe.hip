@@ -107,7 +107,8 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
                                                               uint2* __restrict__ runs,
                                                               uint32_t* __restrict__ info, int ppw,
                                                               int32_t* __restrict__ flist, uint32_t stage_max,
-                                                              RunDictArgs d, int debug, uint32_t wstage) {
+                                                              RunDictArgs d, int debug, uint32_t wstage,
+                                                              int page0) {
     // dynamic LDS: kRunWaves windows of wstage + 32 bytes each (wstage: the
     // group's pages fit when it is at least ppw page slots), or the leading
     // workgroups' dictionary page
@@ -121,7 +122,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
         return;
     }
     const uint32_t wv = threadIdx.x / kWave;
-    const int g0 = ((static_cast<int>(blockIdx.x) - d.ndicts) * kRunWaves + static_cast<int>(wv)) * ppw;
+    const int g0 = page0 + ((static_cast<int>(blockIdx.x) - d.ndicts) * kRunWaves + static_cast<int>(wv)) * ppw;
     if (g0 >= npages) return;
     const int g1 = min(npages, g0 + ppw);
     uint32_t* stage = stage_dyn + wv * wwords;
@@ -266,6 +267,10 @@ struct CodeArgs {
     int wpw;                   // k_pipe_write's writer waves per workgroup (bsum index)
     uint32_t* codes32 = nullptr;  // wide chunks: 32-bit codes here instead of `codes` (k_pipe_big<true>)
     const uint8_t* lens8 = nullptr;  // wide chunks: entry lengths as bytes (255: 255 or more), or null
+    // k_pipe_codes3 of one segment of a segmented decode (capi.hip
+    // pipe_segmented): tiles [t_lo, t_hi), and the marked pages [p_lo, p_hi)
+    // whose exact decode it owns; t_hi < 0: every tile and page
+    int t_lo = 0, t_hi = -1, p_lo = 0, p_hi = -1;
 };
 
 // Characters of tile t also go to the k_pipe_write workgroup that writes it.
@@ -625,9 +630,10 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
     const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
     const uint32_t maskd = (1u << bwd) - 1u;
     const int nw = static_cast<int>(gridDim.x) * kCodeWaves3;
-    const int per = (a.ntiles + nw - 1) / nw;
-    const int ta = min(a.ntiles, (static_cast<int>(blockIdx.x) * kCodeWaves3 + wv) * per);
-    const int tb = min(a.ntiles, ta + per);
+    const int t_lo = a.t_hi < 0 ? 0 : a.t_lo, t_hi = a.t_hi < 0 ? a.ntiles : a.t_hi;
+    const int per = (t_hi - t_lo + nw - 1) / nw;
+    const int ta = min(t_hi, t_lo + (static_cast<int>(blockIdx.x) * kCodeWaves3 + wv) * per);
+    const int tb = min(t_hi, ta + per);
     const uint32_t l8 = lane() * 8;
     auto rl64 = [](uint64_t v, int i) -> uint64_t {
         const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
@@ -847,9 +853,13 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
     }
     // pages k_pipe_runs / k_pipe_big marked (complete before this launch):
     // the exact serial decoder, one wave per page
+    // (a segment's launch: the marked pages of its own page range; the list
+    // also holds earlier segments' pages, decoded by their launches)
     const int nf = flist[0];
     for (int i = static_cast<int>(blockIdx.x) * kCodeWaves3 + wv; i < nf; i += nw) {
-        exact_page_body(a, LX, flist[1 + i], dict_n, ebase);
+        const int fp = flist[1 + i];
+        if (a.t_hi >= 0 && (fp < a.p_lo || fp >= a.p_hi)) continue;
+        exact_page_body(a, LX, fp, dict_n, ebase);
         __builtin_amdgcn_wave_barrier();
     }
     // a dictionary longer than the length table (not planned: lt_n covers
@@ -950,6 +960,7 @@ struct WriteArgs {
     uint8_t* page_flags;
     const uint32_t* codes32 = nullptr;  // wide chunks (k_pipe_wwide)
     const uint4* pad16 = nullptr;       // wide chunks: 16-byte entry slots (k_pipe_wwide<true>), or null
+    uint32_t wg0 = 0;                   // the launch's first workgroup of the decode's writer grid (segments)
 };
 
 
@@ -1151,11 +1162,12 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     // summed by k_pipe_codes), then this workgroup's earlier tiles.  Both
     // sums load together with the dictionary (one wait, one barrier).
     unsigned long long acc = 0, in = 0;
-    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
+    const uint32_t wg = a.wg0 + blockIdx.x;  // workgroup of the decode's writer grid
+    const int ta = min(a.ntiles, static_cast<int>(wg * a.wpw + wv) * per);
     const int tb = min(a.ntiles, ta + per);
     {
-        for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) acc += a.bsum[b];
-        const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
+        for (uint32_t b = threadIdx.x; b < wg; b += blockDim.x) acc += a.bsum[b];
+        const int tfirst = min(a.ntiles, static_cast<int>(wg * a.wpw) * per);
         for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
     }
     {
@@ -2415,13 +2427,15 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
                       int debug, const RunDicts* dicts, uint32_t stage_max, uint32_t slot_max, uint32_t dict_max,
-                      int cus) {
+                      int cus, int page0) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     const int nd = dicts ? dicts->ndicts : 0;
-    if (npages <= 0 && nd <= 0) return;
+    page0 = max(0, min(page0, npages));
+    if (npages - page0 <= 0 && nd <= 0) return;
+    const int np = npages - page0;  // pages of this launch
     int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
     if (pages_per_wave == 0) {  // auto: about two waves per SIMD over the chip, 4 .. 32 pages each
-        const int target = max(1, npages / max(1, cus * 4 * 2));
+        const int target = max(1, np / max(1, cus * 4 * 2));
         ppw = 4;
         while (ppw * 2 <= min(target, kRunPages)) ppw *= 2;
     }
@@ -2441,16 +2455,16 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
     }
     const uint32_t lds = kRunWaves * (wstage / 4 + 8) * 4;
     ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_runs), lds);
-    hipLaunchKernelGGL(k_pipe_runs, dim3(nd + (max(npages, 0) + per - 1) / per), dim3(kRunWaves * kWave), lds, s,
+    hipLaunchKernelGGL(k_pipe_runs, dim3(nd + (max(np, 0) + per - 1) / per), dim3(kRunWaves * kWave), lds, s,
                        bytes, pages, npages, max_def, max_rep, runs, info, ppw, flist,
-                       stage_max ? min(stage_max, kStage3 - 16) : kStage3 - 16, d, debug, wstage);
+                       stage_max ? min(stage_max, kStage3 - 16) : kStage3 - 16, d, debug, wstage, page0);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's
 // characters under the workgroup that will write it).
 static void write_shape(const PipeLaunch& P, int* grid, int* per) {
     const int need = (P.ntiles + P.write_waves - 1) / P.write_waves;
-    *grid = max(1, min(need, P.grid));
+    *grid = max(1, min(need, P.wg_total > 0 ? P.wg_total : P.grid));
     const int nw = *grid * P.write_waves;
     *per = max(1, (P.ntiles + nw - 1) / nw);
 }
@@ -2462,6 +2476,7 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
                P.bsum, per, P.debug, P.write_waves};
+    a.t_lo = P.t_lo; a.t_hi = P.t_hi; a.p_lo = P.p_lo; a.p_hi = P.p_hi;
     if (count_pass) {
         const dim3 grid((P.ntiles + kCodeWaves - 1) / kCodeWaves);
         hipLaunchKernelGGL(k_pipe_codes<true>, grid, dim3(kCodeWaves * kWave), 0, s, a);
@@ -2474,7 +2489,9 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     // resident workgroups per CU (LDS and registers), so the grid is one wave of blocks
     const int waves = kCodeWaves3;
     const int bpc = max(1, resident_blocks(fn, waves * kWave, lds));
-    const int need = (P.ntiles + waves - 1) / waves;
+    const int nt = P.t_hi >= 0 ? P.t_hi - P.t_lo : P.ntiles;
+    if (nt <= 0) return;
+    const int need = (nt + waves - 1) / waves;
     const int grid = max(1, min(need, P.cus * bpc));
     // also decodes the pages the run-table passes marked (flist)
     // (only k_pipe_big pages: nothing to do, k_pipe_big decoded its own
@@ -2522,6 +2539,11 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
                 P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves, P.znext, P.znext_words,
                 P.match, P.match_neg, P.page_flags};
+    if (P.wgn > 0) {  // one segment: workgroups [wg0, wg0 + wgn) of the grid
+        a.wg0 = static_cast<uint32_t>(P.wg0);
+        grid = min(P.wgn, grid - P.wg0);
+        if (grid <= 0) return;
+    }
     if (P.match)
         hipLaunchKernelGGL(k_pipe_write<true>, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
     else
