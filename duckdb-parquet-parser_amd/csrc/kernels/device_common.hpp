@@ -9,6 +9,16 @@
 namespace pqk {
 namespace dev {
 
+// Timing ablations and diagnostics (the `fused_debug` / `regex_debug` option
+// bits that scripts/ab_opts.py and scripts/regex_ablate.py set) exist only in
+// the probe build (`make PROBES=1 OBJDIR=... LIB=...`, loaded through AB_PKG):
+// in the shipped library kProbes is false and every such branch folds away.
+#ifndef PQ_PROBES
+#define PQ_PROBES 0
+#endif
+constexpr bool kProbes = PQ_PROBES != 0;
+__device__ __forceinline__ bool probe(int debug, int bits) { return kProbes && (debug & bits) != 0; }
+
 __device__ __forceinline__ uint32_t lane() { return __lane_id(); }
 
 // ── page byte source: LDS-staged words, or the HBM image (zero past end) ──

@@ -488,7 +488,7 @@ __device__ void produce(const FusedArgs& a, const PairLayout& L, uint8_t* pair, 
     int32_t tnext = 0, tend = 0;
     // debug bit 64 (with bit 1, no look-back): static page assignment, to
     // time the ticket atomics
-    const bool stat = (a.debug & 65) == 65;
+    const bool stat = kProbes && (a.debug & 65) == 65;
     const int32_t nprod = static_cast<int32_t>(gridDim.x * (blockDim.x / (2 * kWave)));
     int32_t sp = static_cast<int32_t>(blockIdx.x * (blockDim.x / (2 * kWave)) + threadIdx.x / kWave);
     for (;;) {
@@ -667,7 +667,7 @@ __device__ void produce(const FusedArgs& a, const PairLayout& L, uint8_t* pair, 
         __builtin_amdgcn_wave_barrier();
         P.mark(PH_ROWS);
         // 4. page start in the output
-        const int64_t G0 = (a.debug & 1) ? static_cast<int64_t>(t) * 24 * n
+        const int64_t G0 = probe(a.debug, 1) ? static_cast<int64_t>(t) * 24 * n
                                          : *a.base_in + static_cast<int64_t>(look_back(a.status, t, total));
         if (t == a.np - 1 && lane() == 0) {
             *a.base_out = G0 + static_cast<int64_t>(total);
@@ -758,7 +758,7 @@ __device__ void copy_chars(const FusedArgs& a, const Slot& S, uint32_t* ring, co
             const int64_t blk = b << 4;
             const uint32_t lo = blk < G0 ? static_cast<uint32_t>(G0 - blk) : 0u;
             const uint32_t hi = blk + 16 > G1 ? static_cast<uint32_t>(G1 - blk) : 16u;
-            if (!(a.debug & 16)) store_block(a.chars, blk, lo, hi, v);
+            if (!probe(a.debug, 16)) store_block(a.chars, blk, lo, hi, v);
         }
         __builtin_amdgcn_wave_barrier();
         fb = lb;
@@ -834,7 +834,7 @@ __device__ void write_pages(const FusedArgs& a, const PairLayout& L, uint8_t* pa
         const uint32_t total = __builtin_amdgcn_readfirstlane(S.meta->total);
         const bool dict = __builtin_amdgcn_readfirstlane(S.meta->dict) != 0;
         // offsets (two rows per lane and store)
-        if (!(a.debug & 4)) {
+        if (!probe(a.debug, 4)) {
             for (uint32_t j = 2 * lane(); j < n; j += 2 * kWave) {
                 const int64_t o0 = G0 + S.off[j];
                 if (j + 1 < n) {
@@ -874,11 +874,11 @@ __device__ void write_pages(const FusedArgs& a, const PairLayout& L, uint8_t* pa
         P.mark(PH_W_OFFSETS);
         const int64_t G1 = G0 + static_cast<int64_t>(total);
         const uint32_t* srcw = dict ? dwords : S.stage;
-        if (total && !(a.debug & 2) && G1 > a.capacity) {
+        if (total && !probe(a.debug, 2) && G1 > a.capacity) {
             if (lane() == 0) atomicOr(a.overflow, 1);
-        } else if (total && !(a.debug & 2) && __builtin_amdgcn_readfirstlane(S.meta->maxlen) <= kRingMaxRow) {
+        } else if (total && !probe(a.debug, 2) && __builtin_amdgcn_readfirstlane(S.meta->maxlen) <= kRingMaxRow) {
             copy_chars(a, S, ring, srcw, (dict ? a.dict_chars_bytes : a.stage_bytes) / 4 - 1, n, G0, G1);
-        } else if (total && !(a.debug & 2)) {
+        } else if (total && !probe(a.debug, 2)) {
             gather_chars(a, S, ring, srcw, n, G0, G1);
             for (uint32_t i = lane(); i < kRingBytes / 16; i += kWave)
                 reinterpret_cast<uint4*>(ring)[i] = make_uint4(0, 0, 0, 0);

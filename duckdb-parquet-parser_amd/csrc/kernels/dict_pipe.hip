@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (debug & (1 << 26)) return;  // timing ablation: staging only (outputs invalid)
+    if (probe(debug, 1 << 26)) return;  // timing ablation: staging only (outputs invalid)
 
     const uint32_t s = lane() & 1;
     const int p = g0 + static_cast<int>(lane() >> 1);
@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
     // (the run table's per-stream rows are kPipeRunCap * 8 = 1 KiB apart:
     // 16-byte aligned, records stored in pairs)
     static_assert((kPipeRunCap * sizeof(uint2)) % 16 == 0, "record rows 16-byte aligned");
-    if (staged && (debug & (1 << 24))) {  // timing probe: position-only walk of 1-byte headers (outputs invalid)
+    if (staged && probe(debug, 1 << 24)) {  // timing probe: position-only walk of 1-byte headers (outputs invalid)
         uint32_t q = W.q, cnt = 0, nr = 0;
         bool alive = W.alive && W.n > 0;
         const uint32_t nbv = (W.bw + 7) / 8;
@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
         if (nr == 0xFFFFFFu) info[0] = q;  // keeps the loop
         return;
     }
-    if (staged) walk_runs<true, true>(W, stage, flag, nrec, (debug & (1 << 25)) != 0);  // bit 25: no record stores (timing)
+    if (staged) walk_runs<true, true>(W, stage, flag, nrec, probe(debug, 1 << 25));  // bit 25: no record stores (timing)
     else walk_runs<false, true>(W, stage, flag, nrec);
     const uint32_t oflag = static_cast<uint32_t>(__shfl_xor(static_cast<int>(flag), 1));
     const uint32_t orec = static_cast<uint32_t>(__shfl_xor(static_cast<int>(nrec), 1));
@@ -1008,7 +1008,7 @@ __device__ __forceinline__ void write_tile(const WriteArgs& a, WriteLds& S, cons
     if (lane() == 0) S.off[m] = total;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (!(a.debug & 4)) {
+    if (!probe(a.debug, 4)) {
         // offsets: rows 2j', 2j' + 1 per lane as one 16-byte store when
         // the tile starts on an even row (coalesced), else row j = 64k + lane
         if ((R0 & 1) == 0) {
@@ -1052,7 +1052,7 @@ __device__ __forceinline__ void write_tile(const WriteArgs& a, WriteLds& S, cons
         a.offsets[a.nrows_total] = G0 + total;
         *a.total = G0 + total;
     }
-    if (total == 0 || (a.debug & 2)) return;
+    if (total == 0 || probe(a.debug, 2)) return;
     if (G0 + total > a.capacity) {  // output too small: the host grows it and re-runs
         if (lane() == 0) atomicOr(a.overflow, 1);
         return;
@@ -1067,7 +1067,7 @@ __device__ __forceinline__ void write_tile(const WriteArgs& a, WriteLds& S, cons
     // LDS first costs more than it saves: byte-unaligned LDS accesses
     // are slow; scripts/probe/unaligned_store.hip)
     const int64_t G1 = G0 + total;
-    if (a.debug & 128) {  // timing only: the tile's bytes as aligned 16-byte blocks of zeros
+    if (probe(a.debug, 128)) {  // timing only: the tile's bytes as aligned 16-byte blocks of zeros
         const int64_t b0 = G0 & ~static_cast<int64_t>(15);
         for (int64_t blk = b0 + 16 * static_cast<int64_t>(lane()); blk < G1; blk += 16 * kWave) {
             const uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -1195,7 +1195,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     __syncthreads();
     int64_t Grun = static_cast<int64_t>(in);
     for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
-    if (a.debug & 8) return;
+    if (probe(a.debug, 8)) return;
     uint4 cv0, cv1, cv2, cv3;
     bool cv_loaded = false;
     for (int c0 = ta; c0 < tb; c0 += kWave) {
@@ -1239,7 +1239,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
                 }
                 return v;
             };
-            if (!(a.debug & (1 << 23)) || !cv_loaded) {  // bit 23 (timing only): the first batch's codes reused
+            if (!probe(a.debug, 1 << 23) || !cv_loaded) {  // bit 23 (timing only): the first batch's codes reused
                 cv0 = ld(ib); cv1 = ld(ib + 1); cv2 = ld(ib + 2); cv3 = ld(ib + 3);
                 cv_loaded = true;
             }
@@ -1329,7 +1329,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
     __syncthreads();
     int64_t Grun = static_cast<int64_t>(in);
     for (int w = 0; w < a.wpw; w++) Grun += static_cast<int64_t>(red[w]);
-    if (a.debug & 8) return;
+    if (probe(a.debug, 8)) return;
     const uint32_t l8 = lane() * kRowsPerLane;
     auto rl64 = [](int64_t v, int i) -> int64_t {
         const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
@@ -1464,7 +1464,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                 if (lane() == 0) offp[m] = total;
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                if (!(a.debug & 4)) {  // offsets and validity words as k_pipe_write stores them
+                if (!probe(a.debug, 4)) {  // offsets and validity words as k_pipe_write stores them
                     if ((R0 & 1) == 0) {
 #pragma unroll
                         for (int k = 0; k < kRowsPerLane / 2; k++) {
@@ -1504,7 +1504,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_wwide(WriteArgs a) {
                     a.offsets[a.nrows_total] = G0 + total;
                     *a.total = G0 + total;
                 }
-                if (total == 0 || (a.debug & 2)) continue;
+                if (total == 0 || probe(a.debug, 2)) continue;
                 if (G0 + total > a.capacity) {
                     if (lane() == 0) atomicOr(a.overflow, 1);
                     continue;
@@ -1815,7 +1815,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     // of this workgroup (the page in HBM; LDS only for its small scratch),
     // so no further launch is needed after the big pages
     auto to_exact = [&](uint32_t why) {
-        if (a.debug & (1 << 27)) {  // diagnostics: which step sent the page to the exact decoder
+        if (probe(a.debug, 1 << 27)) {  // diagnostics: which step sent the page to the exact decoder
             if (tid == 0) set_err(a.page_err + p, a.err_any, PQ_ERR_BUFFER, why, static_cast<uint32_t>(p), size);
             return;
         }
@@ -1865,7 +1865,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     }
     const bool hasd = a.max_def > 0;
     const uint32_t dend = dbase + dlen, ibase = pos, iend = size;
-    if (a.debug & 0x10000) return;  // timing: staging only
+    if (probe(a.debug, 0x10000)) return;  // timing: staging only
     // 1. speculative headers at every byte, two bytes per thread and one
     //    dword store (bytes outside both streams get entries no chain reads:
     //    a next position is always inside its stream, else kBStop)
@@ -1896,7 +1896,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         for (uint32_t jp = tid; jp < npair; jp += kBigThreads)
             tab32[jp] = next_at(base + 2 * jp) | (next_at(base + 2 * jp + 1) << 16);
         __syncthreads();
-        if (a.debug & 0x20000) return false;  // timing: + header parse
+        if (probe(a.debug, 0x20000)) return false;  // timing: + header parse
         // 2. kBJump-run jumps by pointer doubling, two positions per thread
         //    (one dword of the table read and written)
         {
@@ -1933,7 +1933,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
                 __syncthreads();
             }
         }
-        if (a.debug & 4096) return false;  // timing: jump table only
+        if (probe(a.debug, 4096)) return false;  // timing: jump table only
         // 3. one lane per stream follows the jumps: every kBJump-th header
         //    (and the first header past a segment end)
         if (walker && !wdone) {
@@ -1962,7 +1962,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
     if (walker) sh[isd_w ? 1 : 2] = wk;
     __syncthreads();
     const uint32_t nld = sh[1], nli = sh[2];
-    if (a.debug & 8192) return;  // timing: + chain walk
+    if (probe(a.debug, 8192)) return;  // timing: + chain walk
     if (nld == ~0u || nli == ~0u) return to_exact(3);
     // 4. exact runs of each listed header: untruncated counts, bad-header step
     uint2* recd = reinterpret_cast<uint2*>(smem + Ly.tab);
@@ -2042,7 +2042,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         }
     }
     __syncthreads();
-    if (a.debug & 16384) return;  // timing: + exact records
+    if (probe(a.debug, 16384)) return;  // timing: + exact records
     const uint32_t nd = hasd ? sh[3] : 0u, ni = sh[4];
     if (sh[0] || (hasd && nd == 0) || ni == 0) return to_exact(4 | (sh[0] << 4) | ((nd == 0) << 5) | ((ni == 0) << 6));
     const int32_t t0 = a.page_tile0[p];
@@ -2079,7 +2079,7 @@ __global__ void __launch_bounds__(kBigThreads) k_pipe_big(CodeArgs a, const int3
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    if (a.debug & 32768) return;  // timing: + def levels
+    if (probe(a.debug, 32768)) return;  // timing: + def levels
     if (sh[0]) return to_exact(8);
     if (wv == 0) {  // first rank of each tile (ntp <= 64)
         const uint32_t v = lane() < ntp ? tnn[lane()] : 0u;

@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
     const bool empty_ok = D->empty_string != 0;
     const bool trivial = D->nonempty_trivial != 0;
     const uint32_t negv = neg & 1;  // bits 8..15: timing ablation (1: no DFA pass, 2: no chain walk,
-    const int dbg = (neg >> 8) & 0xFF;  // 4: exact walk for every page)
+    const int dbg = pqk::dev::kProbes ? (neg >> 8) & 0xFF : 0;  // 4: exact walk for every page; probe build only)
     const uint32_t wv = threadIdx.x / kWave;
     const uint32_t wpb = blockDim.x / kWave;
     const uint32_t md = static_cast<uint32_t>(cp.max_def);

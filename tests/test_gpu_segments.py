@@ -49,7 +49,7 @@ def _decode_n(ctx, f, chunks, times=3):
 def _mixed_pages_file(npages: int, seed: int, optional: bool):
     """`npages` dictionary-encoded pages of 200-512 rows: runs of repeated
     indices, some past the 300-entry dictionary (NULL rows), every 37th page
-    with a zero-count run (the exact decoder), every 41st with a 17-bit index
+    with a zero-count run after its first literal run (the exact decoder), every 41st with a 17-bit index
     width (the exact decoder), 10 % NULL when optional."""
     rng = np.random.default_rng(seed)
     dv = [b"e%d-" % i * (1 + i % 4) for i in range(300)]
@@ -67,7 +67,10 @@ def _mixed_pages_file(npages: int, seed: int, optional: bool):
             defs = [int(x) for x in rng.random(n) > 0.1]
             idx = [v for v, d in zip(idx, defs) if d]
         bw = 17 if k % 41 == 7 else 9
-        stream = bytes([bw]) + (B.rle(0, 1, bw) if k % 37 == 5 else b"") + _hybrid(idx, bw, rng, 20)
+        if k % 37 == 5:  # a zero-count run after a literal run
+            stream = bytes([bw]) + B.bitpack(idx[:8], bw) + B.rle(0, 1, bw) + _hybrid(idx[8:], bw, rng, 20)
+        else:
+            stream = bytes([bw]) + _hybrid(idx, bw, rng, 20)
         pay = (B.levels_section(_hybrid(defs, 1, rng)) if optional else b"") + stream
         pages.append(B.data_header(len(pay), n, 8) + pay)
         total += n
