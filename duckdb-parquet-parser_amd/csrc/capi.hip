@@ -131,7 +131,8 @@ struct pq_ctx {
     int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
-    int opt_pipe_segs = 4;       // "pipe_segs": tile segments of a pipe decode whose front overlaps the writer (1: off)
+    bool opt_pipe_page = true;   // "pipe_page": k_pipe_page (a wavefront per page) for the pipe's run tables and codes
+    int opt_pipe_segs = 1;       // "pipe_segs": tile segments of a pipe decode whose front overlaps the writer (1: off)
     int opt_seg_min_tiles = 1024;  // "pipe_seg_min_tiles": tiles per segment below which a decode is one pass
     bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
     int opt_write_bpc = 0;       // "write_bpc": cap on k_pipe_write workgroups per CU (0: as many as fit; set before upload)
@@ -178,6 +179,7 @@ struct pq_chunk {
     int64_t* d_tile_chars = nullptr;
     // three-pass dictionary BYTE_ARRAY decode (dict_pipe.hip)
     bool pipe = false, pipe_count = false;
+    bool pipe_page = false;             // k_pipe_page takes the run tables and codes (planned with opt_pipe_page)
     int32_t pipe_dict = -1;
     uint32_t pipe_dict_chars_bytes = 0, pipe_dict_bytes = 0, pipe_lds = 0, pipe_ecap = 0;
     int pipe_cus = 256;
@@ -540,6 +542,7 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     c->pipe = false;
     c->pipe_wide = false;
     c->pipe_count = false;
+    c->pipe_page = false;
     c->pipe_small = false;
     c->hbig.clear();
     c->big_max_bytes = 0;
@@ -581,6 +584,8 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     c->pipe_small = small;
     c->pipe_small_bytes = small_bytes;
     c->pipe_count = multi && c->max_def > 0;
+    c->pipe_page = ctx->opt_pipe_page && small && big.empty() && small_bytes <= pqk::pipe_page_stage();
+    if (c->pipe_page) c->pipe_count = false;  // k_pipe_page counts a page's earlier tiles itself
     c->hbig = std::move(big);
     c->big_max_bytes = big_bytes;
     c->pipe_dict = dict_id;
@@ -604,7 +609,7 @@ void plan_pipe_segs(pq_ctx* ctx, pq_chunk* c, const PVec<DevTile>& htiles, size_
     c->psegs.clear();
     c->pipe_wg_total = c->pipe_grid;
     const int K = ctx->opt_pipe_segs, nt = c->ntiles;
-    if (!c->pipe || c->pipe_wide || !c->hbig.empty() || c->pipe_count || !c->pipe_small || K < 2 ||
+    if (!c->pipe || c->pipe_wide || !c->hbig.empty() || (c->pipe_count && !c->pipe_page) || !c->pipe_small || K < 2 ||
         nt < K * ctx->opt_seg_min_tiles)
         return;
     const int wpw = c->pipe_wpw;
@@ -983,6 +988,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
         ctx->opt_write_bpc = static_cast<int>(value);
         return 0;
     }
+    if (std::strcmp(key, "pipe_page") == 0) { ctx->opt_pipe_page = value != 0; return 0; }
     if (std::strcmp(key, "pipe_segs") == 0) {
         if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "pipe_segs: 1..16");
         ctx->opt_pipe_segs = static_cast<int>(value);
@@ -1621,7 +1627,9 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         rc |= dalloc(&c->d_dict_err, hdicts.size());
         if (c->pipe) {  // flags | bsum | flist, cleared together
             // (bsum: pipe_grid k_pipe_write workgroup sums)
-            const size_t fb = 4 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_wg_total) * sizeof(unsigned long long);
+            // flags: [0] errors, [1] overflow, [2] fallback, [3] redo, [4] k_pipe_page's
+            // dictionary workgroups done, [5] its tickets
+            const size_t fb = 8 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_wg_total) * sizeof(unsigned long long);
             c->z_bsum = fb;
             c->z_flist = (fb + bb + 15) / 16 * 16;
             // cleared per decode (through flist[0]): a multiple of 16 bytes (an
@@ -1684,8 +1692,10 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         rc |= dalloc(&c->d_scan_scratch, std::max(htiles.size(), hpages.size()) / 8192 + 16);
         if (c->type == PQ_BYTE_ARRAY && !c->fused) rc |= dalloc(&c->d_row_codes, static_cast<size_t>(c->nrows));
         if (c->pipe) {
-            rc |= dalloc(&c->d_runs, hpages.size() * 2 * pqk::kPipeRunCap);
-            rc |= dalloc(&c->d_info, hpages.size());
+            if (!c->pipe_page) {  // k_pipe_page keeps its run tables in LDS
+                rc |= dalloc(&c->d_runs, hpages.size() * 2 * pqk::kPipeRunCap);
+                rc |= dalloc(&c->d_info, hpages.size());
+            }
             // u16 codes, or u32 on the wide pipe (d_codes then holds 2 per row)
             rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) * (c->pipe_wide ? 2 : 1) + 64);
             rc |= dalloc(&c->d_tile_nn, htiles.size());
@@ -2221,6 +2231,14 @@ static void launch_dicts(pq_chunk* c, hipStream_t s, int32_t* err_any) {
 
 static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs) {
     hipStream_t s = ctx->stream;
+    if (c->pipe_page) {  // a wavefront per page: run tables and codes in one launch
+        if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
+        const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
+        Timed t(ctx, "pipe_page");
+        pqk::launch_pipe_page(s, P, dict_in_runs ? &rd : nullptr, reinterpret_cast<uint32_t*>(c->d_flags + 4),
+                              c->max_dict_bytes);
+        return;
+    }
     {
         Timed t(ctx, "pipe_runs");
         const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
@@ -2285,17 +2303,22 @@ static void pipe_segmented(pq_ctx* ctx, pq_chunk* c, pq_column* out, bool dict_i
     if (c->d_zero) znext = reinterpret_cast<uint32_t*>(c->d_zero + static_cast<size_t>(c->zsel ^ 1) * c->zfull);
     for (int k = 0; k < K; k++) {
         const pq_chunk::PipeSeg& g = c->psegs[static_cast<size_t>(k)];
-        {
-            Timed t(ctx, "pipe_runs");
-            pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, g.p_hi, c->max_def, c->max_rep, c->d_runs, c->d_info,
-                                  ctx->opt_run_pages, c->d_flist, ctx->opt_debug,
-                                  k == 0 && dict_in_runs ? &rd : nullptr, 0u,
-                                  (c->pipe_small_bytes + 15) / 16 * 16 + 16, c->max_dict_bytes, ctx->cus, g.p_lo);
-        }
-        if (k == 0 && !dict_in_runs && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
         pqk::PipeLaunch Q = P;
         Q.t_lo = g.t_lo; Q.t_hi = g.t_hi; Q.p_lo = g.p_lo; Q.p_hi = g.p_hi;
-        {
+        if (c->pipe_page) {
+            if (k == 0 && !dict_in_runs && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
+            Timed t(ctx, "pipe_page");
+            pqk::launch_pipe_page(s, Q, k == 0 && dict_in_runs ? &rd : nullptr,
+                                  reinterpret_cast<uint32_t*>(c->d_flags + 4), c->max_dict_bytes);
+        } else {
+            {
+                Timed t(ctx, "pipe_runs");
+                pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, g.p_hi, c->max_def, c->max_rep, c->d_runs,
+                                      c->d_info, ctx->opt_run_pages, c->d_flist, ctx->opt_debug,
+                                      k == 0 && dict_in_runs ? &rd : nullptr, 0u,
+                                      (c->pipe_small_bytes + 15) / 16 * 16 + 16, c->max_dict_bytes, ctx->cus, g.p_lo);
+            }
+            if (k == 0 && !dict_in_runs && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
             Timed t(ctx, "pipe_codes");
             pqk::launch_pipe_codes(s, Q, false);
         }

@@ -226,6 +226,13 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
                       uint32_t slot_max = 0, uint32_t dict_max = 0, int cus = 256,  // pages_per_wave 0: auto
                       int page0 = 0);  // pages [page0, npages)
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
+// k_pipe_page: run tables and codes of pages of <= kPipeSmallRows rows and
+// <= pipe_page_stage() payload bytes, one wavefront per page (replaces
+// k_pipe_runs + k_pipe_codes3).  dicts: the chunk's dictionary pages decode
+// in the launch (ready: two zeroed words of the per-decode block; dict_max:
+// their largest payload), else null (decoded before the launch).
+uint32_t pipe_page_stage();
+void launch_pipe_page(hipStream_t s, const PipeLaunch& P, const RunDicts* dicts, uint32_t* ready, uint32_t dict_max);
 struct DevBatch;
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // The page walk on the GPU (walk.hip): one header record per page a

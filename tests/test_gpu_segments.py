@@ -29,7 +29,7 @@ SEGS = [1, 2, 3, 5, 16]
 def segs(request, ctx):
     ctx.set_option("pipe_seg_min_tiles", 1)
     yield
-    ctx.set_option("pipe_segs", 4)
+    ctx.set_option("pipe_segs", 1)
     ctx.set_option("pipe_seg_min_tiles", 1024)
     ctx.set_option("pipe_run_dict", 1)
 
