@@ -18,6 +18,12 @@
 //       Random patterns over the supported syntax and random bytes: compile,
 //       then for each pattern the DFA image (build_dfa) run on the host must
 //       agree with the NFA (match_host) on random strings.
+//   zstd   <seed> <iters> <file>...
+//       Each file: [u32 decompressed size][one or more zstd frames].  The
+//       codec pass's zstd decoder (csrc/kernels/zstd.hpp through
+//       tools/zstd_check.cpp's host harness) must decode the clean frame to
+//       exactly that size, then every mutant (1-4 flipped bytes, a cut tail,
+//       a short output buffer) must end in a status, never a fault.
 //   threads <seed> <iters> <file>...
 //       Speculative walks of several files from several host threads at
 //       once (the process-wide walk pool and its busy fallback; ThreadSanitizer
@@ -251,9 +257,56 @@ int fuzz_threads(uint64_t seed, int iters, int nfiles, char** files) {
 
 }  // namespace
 
+extern "C" int zs_decompress(const uint8_t* src, uint32_t len, uint8_t* dst, uint32_t cap, uint32_t* out_len);
+
+int fuzz_zstd(uint64_t seed, int iters, int nfiles, char** files) {
+    std::mt19937_64 rng(seed);
+    long mutants = 0, rejected = 0;
+    for (int fi = 0; fi < nfiles; fi++) {
+        std::ifstream in(files[fi], std::ios::binary);
+        std::vector<uint8_t> f((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+        if (f.size() < 4) return 3;
+        uint32_t want = 0;
+        std::memcpy(&want, f.data(), 4);
+        const std::vector<uint8_t> clean(f.begin() + 4, f.end());
+        std::vector<uint8_t> out(static_cast<size_t>(want) + 16);
+        uint32_t ol = 0;
+        // (exact-size heap buffers, so ASan sees any read or write past them)
+        {
+            std::vector<uint8_t> src(clean);
+            const int rc = zs_decompress(src.data(), static_cast<uint32_t>(src.size()), out.data(), want, &ol);
+            if (rc != 0 || ol != want) {
+                std::printf("clean frame %s: rc %d, %u of %u bytes\n", files[fi], rc, ol, want);
+                return 1;
+            }
+        }
+        for (int it = 0; it < iters; it++) {
+            std::vector<uint8_t> m(clean);
+            const int kind = static_cast<int>(rng() % 8);
+            if (kind == 0 && m.size() > 1) {
+                m.resize(1 + rng() % (m.size() - 1));  // a cut tail
+            } else {
+                const int flips = 1 + static_cast<int>(rng() % 4);
+                for (int k = 0; k < flips; k++) m[rng() % m.size()] = static_cast<uint8_t>(rng());
+            }
+            const uint32_t cap = kind == 1 ? static_cast<uint32_t>(rng() % (want + 1)) : want;
+            std::vector<uint8_t> dst(static_cast<size_t>(cap) + 1);
+            const int rc = zs_decompress(m.data(), static_cast<uint32_t>(m.size()), dst.data(), cap, &ol);
+            if (ol > cap) {
+                std::printf("mutant wrote %u bytes into %u\n", ol, cap);
+                return 1;
+            }
+            mutants++;
+            rejected += rc != 0;
+        }
+    }
+    std::printf("zstd: %ld mutants, %ld rejected, no fault\n", mutants, rejected);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: %s walk|regex|threads <seed> <iters> [file...]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s walk|regex|threads|zstd <seed> <iters> [file...]\n", argv[0]);
         return 2;
     }
     const std::string mode = argv[1];
@@ -262,5 +315,6 @@ int main(int argc, char** argv) {
     if (mode == "walk") return fuzz_walk(seed, iters, argc - 4, argv + 4);
     if (mode == "regex") return fuzz_regex(seed, iters);
     if (mode == "threads") return fuzz_threads(seed, iters, argc - 4, argv + 4);
+    if (mode == "zstd") return fuzz_zstd(seed, iters, argc - 4, argv + 4);
     return 2;
 }

@@ -191,3 +191,28 @@ def test_mutants_walk_matches_oracle(seed):
         assert rc_o != 0, (name, i, rc_w, msg_w)
         same += (rc_w, msg_w) == (rc_o, msg_o)
     assert failed >= 2 and same >= failed - 1, (failed, same)
+
+
+def test_asan_zstd_fuzz(tmp_path):
+    """The codec pass's zstd decoder (zstd.hpp) under ASan/UBSan: pyarrow
+    frames of several shapes decode clean, then 3,000 mutants each (flipped
+    bytes, cut tails, short output buffers) end in a status, never a fault."""
+    pa = pytest.importorskip("pyarrow")
+    if not pa.Codec.is_available("zstd"):
+        pytest.skip("pyarrow without zstd")
+    import numpy as np
+    rng = random.Random(3)
+    g = np.random.default_rng(4)
+    words = [b"carefully ", b"quickly ", b"special ", b"requests ", b"the ", b"deposits "]
+    datas = [b"".join(rng.choice(words) for _ in range(6000)),
+             g.integers(0, 1000, 30000).astype(np.int64).tobytes(),
+             bytes(rng.randrange(256) for _ in range(3000)),
+             b"ab" * 20000]
+    files = []
+    for i, d in enumerate(datas):
+        for level in (1, 19):
+            p = tmp_path / f"f{i}_{level}.zst"
+            p.write_bytes(len(d).to_bytes(4, "little") + pa.Codec("zstd", compression_level=level).compress(d, asbytes=True))
+            files.append(str(p))
+    out = _run([ASAN, "zstd", "11", "3000", *files])
+    assert "no fault" in out

@@ -85,3 +85,30 @@ def test_zstd_damaged_frames_end_in_a_status(zs):
     assert rc != 0
     rc, _ = dec(zs, clean, len(d) - 1)  # the slot one byte short
     assert rc == 2
+
+
+def _bits_le(fields):
+    """(value, nbits) fields packed LSB first."""
+    acc = n = 0
+    for v, nb in fields:
+        acc |= v << n
+        n += nb
+    return acc.to_bytes((n + 7) // 8, "little")
+
+
+def test_zstd_huffman_weights_zero_run_past_alphabet(zs):
+    """A compressed-literals block whose FSE-coded Huffman weight table
+    declares one symbol of probability 0 followed by a run of 66 more zeros:
+    past the 12 weight symbols zstd allows (RFC 8878 4.2.1.2), and past the
+    decoder's 64-entry count table.  Must end in a status (round-5 advice:
+    such a run used to write past the table)."""
+    hdesc = _bits_le([(0, 4), (1, 5)] + [(3, 2)] * 22 + [(0, 2)])
+    hb = len(hdesc) + 3
+    huf = bytes([hb]) + hdesc + b"\x00" * 3
+    regen, comp = 100, len(huf) + 8
+    lit_hdr = (2 | (0 << 2) | (regen << 4) | (comp << 14)).to_bytes(3, "little")
+    body = lit_hdr + huf + b"\x55" * 8 + b"\x00"  # then no sequences
+    block = (1 | (2 << 1) | (len(body) << 3)).to_bytes(3, "little") + body
+    frame = bytes([0x28, 0xB5, 0x2F, 0xFD, 0x20, regen]) + block
+    rc, _ = dec(zs, frame, regen)
+    assert rc != 0
