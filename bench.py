@@ -486,11 +486,18 @@ def c2_leg(J, args, exp):
     res["upload_s"] = upload_s
     if not args.no_e2e and J.rank == 0:
         res["api_read_all"] = api_read_all_leg(f, want)
+        # the same call on cpu_baseline's 1M-row chunk (like for like with its
+        # page_parallel / chunk_parallel rates)
+        from pqgpu import gen as _gen
+        layout = _gen.REF_LAYOUT if args.layout == "ref" else _gen.ARROW_LAYOUT
+        f1 = _gen.build(_gen.c2_cols(), 1_000_000, 1, seed=_gen.CONFIG_SEEDS["C2"], layout=layout)
+        want1 = sha(_gen.values_dump(_gen.c2_cols()[0], 0, 1_000_000, 0, _gen.CONFIG_SEEDS["C2"]))
+        res["api_read_all"]["chunk_1m"] = api_read_all_leg(f1, want1, reps=9)
     del f
     return res
 
 
-def api_read_all_leg(f: bytes, want):
+def api_read_all_leg(f: bytes, want, reps: int = 5):
     """What a drop-in caller of the reference API gets (the
     std::vector<Value> path): pqgpu::ColumnReader::read_all on the C2 chunk,
     host file bytes in, std::vector<Value> out (range read, upload, decode,
@@ -503,7 +510,7 @@ def api_read_all_leg(f: bytes, want):
         path, dump = os.path.join(td, "c2.parquet"), os.path.join(td, "c2.dump")
         with open(path, "wb") as fh:
             fh.write(f)
-        r = subprocess.run([tool, path, "time_read_all", "0", "0", "5", dump], stdout=subprocess.PIPE,
+        r = subprocess.run([tool, path, "time_read_all", "0", "0", str(reps), dump], stdout=subprocess.PIPE,
                            stderr=subprocess.PIPE, timeout=600)
         if r.returncode != 0:
             return {"error": r.stderr.decode(errors="replace")[-500:]}
@@ -515,6 +522,7 @@ def api_read_all_leg(f: bytes, want):
             "read_columnar_ms": js["read_columnar_ms"], "to_values_ms": js["to_values_ms"],
             "to_values_per_s": n / (js["to_values_ms"] * 1e-3), "threads": js["threads"], "values": n,
             "read_all_samples_ms": js.get("read_all_samples"), "to_values_samples_ms": js.get("to_values_samples"),
+            "phases_ms": js.get("phases_ms"),
             "validated": (got == want) if want else None,
             "note": "ColumnReader::read_all from host file bytes to std::vector<Value>; compare cpu_baseline."
                     "chunk_parallel (the reference's read_all, one thread per chunk) and single_thread"}
@@ -1072,6 +1080,8 @@ def compact(res: dict, full_path: str) -> dict:
     if "api_read_all" in res:
         a = res["api_read_all"]
         legs["api_read_all"] = {"values_per_s": _r(a["values_per_s"]), "threads": a.get("threads")}
+        if isinstance(a.get("chunk_1m"), dict) and "values_per_s" in a["chunk_1m"]:
+            legs["api_read_all"]["chunk_1m_values_per_s"] = _r(a["chunk_1m"]["values_per_s"])
     if "strong" in res:
         legs["strong"] = {k: _r(v) if isinstance(v, float) else v for k, v in res["strong"].items()
                           if not isinstance(v, (dict, list))}

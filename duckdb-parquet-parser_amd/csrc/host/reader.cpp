@@ -2,6 +2,7 @@
 #include "pqgpu/reader.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -197,7 +198,22 @@ Value HostColumn::value(int64_t i) const {
     }
 }
 
+namespace {
+thread_local ToValuesPhases g_tv_phases;
+double ms_since(std::chrono::steady_clock::time_point& t) {
+    const auto n = std::chrono::steady_clock::now();
+    const double r = std::chrono::duration<double, std::milli>(n - t).count();
+    t = n;
+    return r;
+}
+}  // namespace
+
+ToValuesPhases last_to_values_phases() { return g_tv_phases; }
+
 std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned threads) {
+    ToValuesPhases& P = g_tv_phases;
+    P = ToValuesPhases{};
+    auto tp = std::chrono::steady_clock::now();
     a = std::max<int64_t>(a, 0);
     b = std::min<int64_t>(b, h.num_rows);
     const int64_t n = std::max<int64_t>(b - a, 0);
@@ -207,8 +223,10 @@ std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned
     // the storage's pages are faulted in by the threads first: the vector's
     // default construction then runs over mapped memory instead of taking
     // every page fault on this thread
+    P.threads = t;
     std::vector<Value> out;
     out.reserve(static_cast<size_t>(n));
+    P.reserve_ms = ms_since(tp);
     if (t > 1) {
         volatile char* raw = reinterpret_cast<volatile char*>(out.data());
         const size_t bytes = static_cast<size_t>(n) * sizeof(Value);
@@ -219,13 +237,16 @@ std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned
             });
         for (auto& x : th) x.join();
     }
+    P.fault_ms = ms_since(tp);
     out.resize(static_cast<size_t>(n));
+    P.resize_ms = ms_since(tp);
     auto part = [&](unsigned k) {
         const int64_t r0 = n * k / t, r1 = n * (k + 1) / t;
         for (int64_t r = r0; r < r1; r++) out[static_cast<size_t>(r)] = h.value(a + r);
     };
     if (t <= 1) {
         part(0);
+        P.fill_ms = ms_since(tp);
         return out;
     }
     std::vector<std::thread> th;
@@ -233,6 +254,7 @@ std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned
     for (unsigned k = 1; k < t; k++) th.emplace_back(part, k);
     part(0);
     for (auto& x : th) x.join();
+    P.fill_ms = ms_since(tp);
     return out;
 }
 

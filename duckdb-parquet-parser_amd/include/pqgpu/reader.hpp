@@ -123,6 +123,14 @@ struct HostColumn {
 // `threads` host threads (0: hardware_concurrency, at most 16), each
 // constructing its rows' Values in place.
 std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned threads = 0);
+// Wall ms of the calling thread's last to_values, by phase (bench / api_check
+// accounting): the storage reserve, its pages faulted in by the workers, the
+// default construction (resize), the parallel fill (strings allocated here).
+struct ToValuesPhases {
+    double reserve_ms = 0, fault_ms = 0, resize_ms = 0, fill_ms = 0;
+    unsigned threads = 0;
+};
+ToValuesPhases last_to_values_phases();
 inline std::vector<Value> to_values(const HostColumn& h, unsigned threads = 0) { return to_values(h, 0, h.num_rows, threads); }
 
 class ColumnReader {

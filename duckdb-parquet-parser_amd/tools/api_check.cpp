@@ -146,21 +146,31 @@ int main(int argc, char** argv) {
                     std::sort(v.begin(), v.end());
                     return v[v.size() / 2];
                 };
-                std::vector<double> ta, tc, tv;
+                std::vector<double> ta, tc, tv, td, tr, tf, tz, tl, tdh;
                 std::vector<pqgpu::Value> vals = cr.read_all();  // warm-up (device buffers, first-touch pages)
                 for (int i = 0; i < reps; i++) {
-                    vals.clear();
+                    const auto tq = now();
+                    vals.clear();  // the previous result's destruction (10M strings freed)
                     vals.shrink_to_fit();
                     const auto t0 = now();
                     vals = cr.read_all();
                     const auto t1 = now();
+                    const pqgpu::ToValuesPhases P = pqgpu::last_to_values_phases();
                     pqgpu::HostColumn h = cr.read_columnar();
                     const auto t2 = now();
                     std::vector<pqgpu::Value> v2 = pqgpu::to_values(h);
                     const auto t3 = now();
+                    { std::vector<pqgpu::Value> drop(std::move(v2)); }
+                    const auto t4 = now();
+                    td.push_back(ms(tq, t0));
                     ta.push_back(ms(t0, t1));
                     tc.push_back(ms(t1, t2));
                     tv.push_back(ms(t2, t3));
+                    tdh.push_back(ms(t3, t4));
+                    tr.push_back(P.reserve_ms);
+                    tf.push_back(P.fault_ms);
+                    tz.push_back(P.resize_ms);
+                    tl.push_back(P.fill_ms);
                 }
                 for (const auto& v : vals) dump(v, out);
                 FILE* fh = std::fopen(argv[6], "wb");
@@ -172,12 +182,16 @@ int main(int argc, char** argv) {
                     for (size_t i = 0; i < v.size(); i++) r += (i ? ", " : "") + std::to_string(v[i]);
                     return r + "]";
                 };
+                // read_all's phases: columnar read (read_all_ms - the to_values
+                // phases), then to_values' reserve / fault / resize / fill; the
+                // destruction of a result before the next read is timed apart
                 std::printf("{\"values\": %zu, \"read_all_ms\": %.4f, \"read_columnar_ms\": %.4f, "
                             "\"to_values_ms\": %.4f, \"threads\": %u, \"read_all_samples\": %s, "
-                            "\"to_values_samples\": %s}\n",
+                            "\"to_values_samples\": %s, \"phases_ms\": {\"reserve\": %.4f, \"fault\": %.4f, "
+                            "\"resize\": %.4f, \"fill\": %.4f, \"destroy_before\": %.4f, \"destroy_v2\": %.4f}}\n",
                             vals.size(), med(ta), med(tc), med(tv),
                             std::max(1u, std::min(16u, std::thread::hardware_concurrency())), list(ta).c_str(),
-                            list(tv).c_str());
+                            list(tv).c_str(), med(tr), med(tf), med(tz), med(tl), med(td), med(tdh));
                 return 0;
             } else {
                 for (const auto& pr : cr.read_pages()) {
