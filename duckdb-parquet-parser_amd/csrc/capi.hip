@@ -1921,8 +1921,10 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                 } else if (zstd && zother) {
                     rc = set_err(ctx, PQ_ERR_CODEC, "ZSTD pages mixed with other codecs in one upload");
                 } else {
+                    const int32_t nsmall = static_cast<int32_t>(std::count_if(
+                        cents.begin(), cents.end(), [](const pqk::CodecEntry& e) { return e.out_len < pqk::codec_small_bytes(); }));
                     pqk::launch_codec(s, csrc, c->d_bytes, ctx->d_codec, static_cast<int32_t>(n), ctx->d_codec_st, ctx->cus,
-                                      gz ? 1 : (zstd ? 2 : 0));
+                                      gz ? 1 : (zstd ? 2 : 0), nsmall);
                     rc = hip_check(ctx, hipGetLastError(), "codec launch");
                 }
             }

@@ -93,7 +93,10 @@ __device__ __forceinline__ void wsync() {
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ── staged input ───────────────────────────────────────────────────────────
-struct In {
+// kWin: staged input bytes (kInWin; kSWin in the small-page instantiations)
+template <uint32_t kWin>
+struct InT {
+    static constexpr uint32_t kWindow = kWin;
     const uint8_t* g;  // page input in HBM
     uint32_t len;      // input bytes
     uint32_t wlo;      // input byte held at in[sh]
@@ -106,7 +109,8 @@ struct In {
         // (derived from g, so the loads stay global: a pointer made from an
         // integer would compile to flat loads)
         const uint4* src = reinterpret_cast<const uint4*>(g + p - sh);  // (g + p) - sh: never below g's buffer
-        constexpr uint32_t nb = kInWin / 16;
+        constexpr uint32_t nb = kWin / 16;
+        static_assert(nb % kWave == 0, "one block per lane per step");
         const uint32_t nvalid = (sh + len > p ? (sh + len - p + 15) / 16 : 0u);  // blocks holding input bytes
         uint4 v[nb / kWave];
 #pragma unroll
@@ -122,9 +126,9 @@ struct In {
     }
     // bytes [p, p + k) staged (k <= 16)
     __device__ __forceinline__ void ensure(uint32_t p, uint32_t k) {
-        if (p < wlo || p + k + sh > wlo + kInWin) refill(p);
+        if (p < wlo || p + k + sh > wlo + kWin) refill(p);
     }
-    __device__ __forceinline__ uint32_t at(uint32_t p) const { return min(p - wlo + sh, kInWin + 16u); }
+    __device__ __forceinline__ uint32_t at(uint32_t p) const { return min(p - wlo + sh, kWin + 16u); }
     __device__ __forceinline__ uint32_t byte(uint32_t p) const { return w[at(p)]; }
     __device__ __forceinline__ uint32_t u16le(uint32_t p) const { return byte(p) | (byte(p + 1) << 8); }
     __device__ __forceinline__ uint32_t u32le(uint32_t p) const {
@@ -134,6 +138,15 @@ struct In {
         return (byte(p) << 24) | (byte(p + 1) << 16) | (byte(p + 2) << 8) | byte(p + 3);
     }
 };
+
+using In = InT<kInWin>;
+// Pages whose payload is under kSRing bytes decode in the small-page
+// instantiations: an 8 KiB history that holds the whole page and a 1 KiB
+// input window, ~9 KiB of LDS per wavefront instead of 72, so a CU holds as
+// many decoding pages as its registers allow (16) instead of two
+constexpr uint32_t kSRing = 8192;
+constexpr uint32_t kSWin = 1024;
+using InS = InT<kSWin>;
 
 enum : uint32_t { ST_OK = 0, ST_CORRUPT = 1, ST_SIZE = 2, ST_UNSUPPORTED = 3 };
 
@@ -256,7 +269,8 @@ struct Out {
         return true;
     }
     // literal bytes [p, p + n) of the input
-    __device__ __forceinline__ void lit(In& I, uint32_t p, uint32_t n) {
+    template <class InX>
+    __device__ __forceinline__ void lit(InX& I, uint32_t p, uint32_t n) {
         if (!room(n)) return;
         for (uint32_t d = 0; d < n; d += kWave) {
             I.ensure(p + d, kWave);
@@ -303,8 +317,8 @@ struct Out {
 };
 
 // ── SNAPPY ─────────────────────────────────────────────────────────────────
-template <class OutT>
-__device__ __forceinline__ void snappy(In& I, OutT& O, uint32_t p, uint32_t end, uint32_t expect) {
+template <class InX, class OutT>
+__device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end, uint32_t expect) {
     uint32_t ulen = 0;
     I.ensure(p, 8);
     for (uint32_t k = 0;; k++) {
@@ -354,8 +368,8 @@ __device__ __forceinline__ void snappy(In& I, OutT& O, uint32_t p, uint32_t end,
 }
 
 // ── LZ4 block ──────────────────────────────────────────────────────────────
-template <class OutT>
-__device__ __forceinline__ void lz4_block(In& I, OutT& O, uint32_t p, uint32_t end) {
+template <class InX, class OutT>
+__device__ __forceinline__ void lz4_block(InX& I, OutT& O, uint32_t p, uint32_t end) {
     for (;;) {
         if (p >= end) { O.st = ST_CORRUPT; return; }
         I.ensure(p, 1);
@@ -395,8 +409,8 @@ __device__ __forceinline__ void lz4_block(In& I, OutT& O, uint32_t p, uint32_t e
 }
 
 // Hadoop framing (codec LZ4): blocks of [u32 BE raw bytes][u32 BE packed bytes][LZ4 block].
-template <class OutT>
-__device__ __forceinline__ void lz4_hadoop(In& I, OutT& O, uint32_t p, uint32_t end) {
+template <class InX, class OutT>
+__device__ __forceinline__ void lz4_hadoop(InX& I, OutT& O, uint32_t p, uint32_t end) {
     while (p < end && O.st == ST_OK) {
         if (end - p < 8) { O.st = ST_CORRUPT; return; }
         I.ensure(p, 8);
@@ -706,31 +720,41 @@ __device__ __forceinline__ void gzip(CodecLds& L, In& I, Out<true>& O, uint32_t 
 // flushed slot), the staged input and the decode tables, 59 KiB in all, so
 // two pages share a CU (CodecLds with the tables: 91 KiB, one)
 constexpr uint32_t kZRing = 32768;
-struct ZCodecLds {
-    uint8_t ring[kZRing];
-    uint8_t in[kInWin + 32];
+template <uint32_t kRingB, uint32_t kWin>
+struct ZCodecLdsT {
+    uint8_t ring[kRingB];
+    uint8_t in[kWin + 32];
     uint8_t zstage[64];
     zs::ZTables T;
 };
+using ZCodecLds = ZCodecLdsT<kZRing, kInWin>;
+// the small-page layouts (pages under kSRing bytes)
+struct SCodecLds {
+    uint8_t ring[kSRing];
+    uint8_t in[kSWin + 32];
+};
+using ZSCodecLds = ZCodecLdsT<kSRing, kSWin>;
 
 // ── ZSTD adapters (zstd.hpp's source and output over In and the ring) ────
+template <class InX>
 struct ZSrc {
-    In* I;
+    InX* I;
     uint32_t base, len;  // the zstd stream: input bytes [base, base + len)
     __device__ __forceinline__ uint32_t byte(uint32_t q) const {
         if (q >= len) return 0u;
         const uint32_t p = base + q;
         // the decoder reads forward (headers, raw blocks) and backward (bit
         // streams): refill with p mid-window
-        if (p < I->wlo || p + 1 + I->sh > I->wlo + kInWin) I->refill(p > kInWin / 2 ? p - kInWin / 2 : 0u);
+        constexpr uint32_t w = InX::kWindow;
+        if (p < I->wlo || p + 1 + I->sh > I->wlo + w) I->refill(p > w / 2 ? p - w / 2 : 0u);
         return I->byte(p);
     }
 };
 
-template <class OutT>
+template <class OutT, class InX>
 struct ZOut {
     OutT* O;
-    In* I;
+    InX* I;
     uint32_t base;         // input offset of the zstd stream (raw blocks)
     lds8* stage;           // 64 literal bytes on their way to the slot
     uint32_t litbase = 0;  // slot offset of the block's literals: its tail, past every byte still to be written
@@ -814,17 +838,25 @@ struct ZOut {
 
 // kGzip: the GZIP instantiation (CRC-32 on, DEFLATE); the other one takes
 // every other codec and the V2 rebuild.  A chunk has one codec, so one
-// launch takes one instantiation (launch_codec).
-template <int kKind>
+// launch takes one instantiation (launch_codec).  kSmall: the small-page
+// layout (SCodecLds / ZSCodecLds), over the entries whose payload is under
+// kSRing bytes; the full layout takes the rest (each launch skips the others).
+template <int kKind, bool kSmall>
 __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src, uint8_t* __restrict__ img,
                                                  const CodecEntry* __restrict__ ent, int32_t n,
                                                  uint32_t* __restrict__ status) {
     constexpr bool kGzip = kKind == 1, kZstd = kKind == 2;
+    static_assert(!(kGzip && kSmall), "GZIP keeps the full layout (its Huffman tables)");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     CodecLds& L = *reinterpret_cast<CodecLds*>(smem);
-    lds8* lring = (lds8*)(smem + (kZstd ? offsetof(ZCodecLds, ring) : offsetof(CodecLds, ring)));
-    lds8* lin = (lds8*)(smem + (kZstd ? offsetof(ZCodecLds, in) : offsetof(CodecLds, in)));
-    using OutK = Out<kGzip, kZstd ? kZRing : kRing>;
+    constexpr size_t kRingOff = kSmall ? (kZstd ? offsetof(ZSCodecLds, ring) : offsetof(SCodecLds, ring))
+                                       : (kZstd ? offsetof(ZCodecLds, ring) : offsetof(CodecLds, ring));
+    constexpr size_t kInOff = kSmall ? (kZstd ? offsetof(ZSCodecLds, in) : offsetof(SCodecLds, in))
+                                     : (kZstd ? offsetof(ZCodecLds, in) : offsetof(CodecLds, in));
+    lds8* lring = (lds8*)(smem + kRingOff);
+    lds8* lin = (lds8*)(smem + kInOff);
+    using OutK = Out<kGzip, kSmall ? kSRing : (kZstd ? kZRing : kRing)>;
+    using InK = typename std::conditional<kSmall, InS, In>::type;
     lds32* lcrc = (lds32*)(smem + offsetof(CodecLds, crc_tab));
     if constexpr (kGzip) {
         for (uint32_t b = lane(); b < 256; b += kWave) {  // CRC-32 byte table
@@ -836,7 +868,8 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
     }
     for (int32_t i = static_cast<int32_t>(blockIdx.x); i < n; i += static_cast<int32_t>(gridDim.x)) {
         const CodecEntry e = ent[i];
-        In I{src + e.src, e.src_len, 0u, 0u, lin};
+        if (!kGzip && (e.out_len < kSRing) != kSmall) continue;  // the other layout's page
+        InK I{src + e.src, e.src_len, 0u, 0u, lin};
         I.refill(0);
         OutK O{lring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
         O.crc_tab = lcrc;
@@ -872,10 +905,11 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
                     case 7: lz4_block(I, O, p, end); break;
                     case 6:
                         if constexpr (kZstd) {
-                            // the tables after CodecLds (this instantiation's launch only)
-                            zs::ZTables& T = *reinterpret_cast<zs::ZTables*>(smem + offsetof(ZCodecLds, T));
-                            const ZSrc zsrc{&I, p, end - p};
-                            ZOut<OutK> zo{&O, &I, p, (lds8*)(smem + offsetof(ZCodecLds, zstage))};
+                            // the tables after the ring and the window (this instantiation's launch only)
+                            using ZL = typename std::conditional<kSmall, ZSCodecLds, ZCodecLds>::type;
+                            zs::ZTables& T = *reinterpret_cast<zs::ZTables*>(smem + offsetof(ZL, T));
+                            const ZSrc<InK> zsrc{&I, p, end - p};
+                            ZOut<OutK, InK> zo{&O, &I, p, (lds8*)(smem + offsetof(ZL, zstage))};
                             const uint32_t st = zs::decompress(zsrc, end - p, T, zo);
                             if (O.st == ST_OK && st != zs::ZS_OK)
                                 O.st = st == zs::ZS_SIZE ? ST_SIZE : (st == zs::ZS_UNSUPPORTED ? ST_UNSUPPORTED : ST_CORRUPT);
@@ -898,19 +932,34 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
 
 size_t codec_lds_bytes() { return sizeof(CodecLds); }
 
-void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
-                  uint32_t* status, int cus, int kind) {
-    if (n <= 0) return;
-    // kind 2 (ZSTD): its own layout (a smaller ring and the decode tables)
-    const uint32_t lds = static_cast<uint32_t>(kind == 2 ? sizeof(ZCodecLds) : sizeof(CodecLds));
-    const void* k = kind == 1 ? reinterpret_cast<const void*>(k_codec<1>)
-                              : (kind == 2 ? reinterpret_cast<const void*>(k_codec<2>) : reinterpret_cast<const void*>(k_codec<0>));
+template <int kKind, bool kSmall>
+static void codec_launch(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
+                         uint32_t* status, int cus, uint32_t lds, int32_t pages) {
+    const void* k = reinterpret_cast<const void*>(k_codec<kKind, kSmall>);
     ensure_dyn_lds(k, lds);
-    const int per_cu = std::max(1, static_cast<int>((160u * 1024u) / lds));
-    const int grid = std::min(n, std::max(1, cus) * per_cu);
-    if (kind == 1) hipLaunchKernelGGL(k_codec<1>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
-    else if (kind == 2) hipLaunchKernelGGL(k_codec<2>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
-    else hipLaunchKernelGGL(k_codec<0>, dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
+    const int per_cu = std::max(1, resident_blocks(k, kWave, lds));
+    const int grid = std::min(std::max(pages, 1), std::max(1, cus) * per_cu);
+    hipLaunchKernelGGL((k_codec<kKind, kSmall>), dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
 }
+
+void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
+                  uint32_t* status, int cus, int kind, int32_t nsmall) {
+    if (n <= 0) return;
+    // kind 2 (ZSTD): its own layout (a smaller ring and the decode tables);
+    // nsmall: entries whose payload is under kSRing (the small-page layout)
+    const int32_t nbig = kind == 1 ? n : n - nsmall;
+    if (kind == 1) codec_launch<1, false>(s, src, img, ent, n, status, cus, sizeof(CodecLds), n);
+    if (kind == 2) {
+        if (nsmall > 0) codec_launch<2, true>(s, src, img, ent, n, status, cus, sizeof(ZSCodecLds), nsmall);
+        if (nbig > 0) codec_launch<2, false>(s, src, img, ent, n, status, cus, sizeof(ZCodecLds), nbig);
+    }
+    if (kind == 0) {
+        if (nsmall > 0) codec_launch<0, true>(s, src, img, ent, n, status, cus, sizeof(SCodecLds), nsmall);
+        // (the full layout without the DEFLATE tables and the CRC table)
+        if (nbig > 0) codec_launch<0, false>(s, src, img, ent, n, status, cus, offsetof(CodecLds, lt), nbig);
+    }
+}
+
+uint32_t codec_small_bytes() { return kSRing; }
 
 }  // namespace pqk

@@ -80,7 +80,9 @@ size_t codec_lds_bytes();
 // 0 and 2 only), 2 they include ZSTD pages (codecs 0 and 6 only: a 32 KiB
 // history ring and the decode tables in LDS), 0 neither
 void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
-                  uint32_t* status, int cus, int kind);
+                  uint32_t* status, int cus, int kind, int32_t nsmall);
+// entries with out_len under this take the small-page layout (nsmall counts them)
+uint32_t codec_small_bytes();
 
 // 4 KiB chunker (chunker.hip, src/main.cpp:17-32): device scratch bytes for
 // n rows, and the launch sequence (synchronises the stream; 0 = OK).

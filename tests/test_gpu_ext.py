@@ -129,3 +129,29 @@ def test_ext_large_pages_vs_pyarrow(ctx, tmp_path, codec, version):
     for ci, c in enumerate(back.column_names):
         got = capi.canonical_dump(decode(ctx, f, ci))
         assert sha(got) == sha(canonical_dump(back.column(c))), c
+
+
+@pytest.mark.skipif(pa is None, reason="pyarrow not importable")
+@pytest.mark.parametrize("codec", ["snappy", "lz4", "zstd"])
+@pytest.mark.parametrize("version", ["1.0", "2.0"])
+@pytest.mark.parametrize("page", [5000, 8100])
+def test_ext_pages_both_layouts(ctx, tmp_path, codec, version, page):
+    """Pages on both sides of the small-page layout's 8 KiB history (codec.hip
+    kSRing) in one chunk: the small-page and the full-layout launches each take
+    their own pages of the same upload, equal to pyarrow."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden", "ext"))
+    from make_ext import canonical_dump, table
+    t = table(60_000, seed=13).select(["s_dict", "s_plain", "i64", "f64"])
+    path = tmp_path / f"mix_{codec}_{version}_{page}.parquet"
+    pq.write_table(t, path, compression=codec.upper() if codec != "lz4" else "LZ4", data_page_version=version,
+                   use_dictionary=["s_dict"], row_group_size=60_000, data_page_size=page)
+    f = path.read_bytes()
+    back = pq.read_table(path)
+    sizes = set()
+    for ci, c in enumerate(back.column_names):
+        rc, _, tab = capi.build_page_table(f, ext_chunks(f, ci)[0])
+        assert rc == 0
+        sizes |= {p.uncompressed_size >= 8192 for p in tab if p.page_type in (0, 3)}
+        got = capi.canonical_dump(decode(ctx, f, ci))
+        assert sha(got) == sha(canonical_dump(back.column(c))), c
+    assert sizes == {False, True}  # both layouts ran
