@@ -132,7 +132,6 @@ struct pq_ctx {
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
     bool opt_pipe_page = false;  // "pipe_page": k_pipe_page (a wavefront per page) for the pipe's run tables and codes
-    bool opt_write_ilv = false;  // "write_ilv": k_pipe_write's waves take their workgroup's tiles in turn
     int opt_pipe_segs = 1;       // "pipe_segs": tile segments of a pipe decode whose front overlaps the writer (1: off)
     int opt_seg_min_tiles = 1024;  // "pipe_seg_min_tiles": tiles per segment below which a decode is one pass
     bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
@@ -989,7 +988,6 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
         ctx->opt_write_bpc = static_cast<int>(value);
         return 0;
     }
-    if (std::strcmp(key, "write_ilv") == 0) { ctx->opt_write_ilv = value != 0; return 0; }
     if (std::strcmp(key, "pipe_page") == 0) { ctx->opt_pipe_page = value != 0; return 0; }
     if (std::strcmp(key, "pipe_segs") == 0) {
         if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "pipe_segs: 1..16");
@@ -2206,7 +2204,6 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     P.dict_chars_bytes = c->pipe_dict_chars_bytes; P.dict_bytes = c->pipe_dict_bytes; P.lds = c->pipe_lds;
     P.grid = c->pipe_grid;
     P.wg_total = c->psegs.empty() ? 0 : c->pipe_wg_total;
-    P.write_ilv = ctx->opt_write_ilv ? 1 : 0;
     P.debug = ctx->opt_debug;
     P.dict_entries_cap = c->pipe_ecap;
     P.cus = c->pipe_cus;

@@ -1418,7 +1418,6 @@ struct WriteArgs {
     const uint32_t* codes32 = nullptr;  // wide chunks (k_pipe_wwide)
     const uint4* pad16 = nullptr;       // wide chunks: 16-byte entry slots (k_pipe_wwide<true>), or null
     uint32_t wg0 = 0;                   // the launch's first workgroup of the decode's writer grid (segments)
-    int ilv = 0;                        // k_pipe_write: a workgroup's waves take its tiles in turn (one write front per workgroup)
 };
 
 
@@ -1619,15 +1618,11 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     // first output byte of the range: the workgroups before this one (bsum,
     // summed by k_pipe_codes), then this workgroup's earlier tiles.  Both
     // sums load together with the dictionary (one wait, one barrier).
-    // (a.ilv: the workgroup's whole range, its waves taking tiles in turn:
-    // the workgroup writes one advancing front of offsets and characters
-    // instead of one per wave)
     unsigned long long acc = 0, in = 0;
     const uint32_t wg = a.wg0 + blockIdx.x;  // workgroup of the decode's writer grid
     const int tfirst = min(a.ntiles, static_cast<int>(wg * a.wpw) * per);
-    const int ta = a.ilv ? tfirst : min(a.ntiles, static_cast<int>(wg * a.wpw + wv) * per);
-    const int tb = a.ilv ? min(a.ntiles, tfirst + a.wpw * per) : min(a.ntiles, ta + per);
-    const int tstride = a.ilv ? a.wpw : 1;
+    const int ta = min(a.ntiles, static_cast<int>(wg * a.wpw + wv) * per);
+    const int tb = min(a.ntiles, ta + per);
     {
         for (uint32_t b = threadIdx.x; b < wg; b += blockDim.x) acc += a.bsum[b];
         for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
@@ -1686,9 +1681,7 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
         // the tile loop, so one wait (which also drains this wave's earlier
         // stores: loads and stores share vmcnt) per batch, not per tile
         const uint32_t l8 = lane() * kRowsPerLane;
-        // this wave's tiles of the batch: i0, i0 + tstride, ...
-        const int i0 = a.ilv ? ((static_cast<int>(wv) - (c0 - ta)) % tstride + tstride) % tstride : 0;
-        for (int ib = i0; ib < cn; ib += kWBatch * tstride) {
+        for (int ib = 0; ib < cn; ib += kWBatch) {
             // four named registers (an indexed array would go to scratch)
             static_assert(kWBatch == 4, "batch registers");
             auto ld = [&](int i) -> uint4 {
@@ -1704,16 +1697,16 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
                 return v;
             };
             if (!probe(a.debug, 1 << 23) || !cv_loaded) {  // bit 23 (timing only): the first batch's codes reused
-                cv0 = ld(ib); cv1 = ld(ib + tstride); cv2 = ld(ib + 2 * tstride); cv3 = ld(ib + 3 * tstride);
+                cv0 = ld(ib); cv1 = ld(ib + 1); cv2 = ld(ib + 2); cv3 = ld(ib + 3);
                 cv_loaded = true;
             }
-        for (int i = ib; i < min(cn, ib + kWBatch * tstride); i += tstride) {
+        for (int i = ib; i < min(cn, ib + kWBatch); i++) {
             const int64_t R0 = rl64(myR0, i);
             const int64_t G0 = rl64(myG0, i);
             const uint32_t m = __builtin_amdgcn_readlane(mym, i);
             uint32_t cur[kRowsPerLane];
             {
-                const int u = (i - ib) / tstride;  // register select (no dynamic indexing into cv)
+                const int u = i - ib;  // register select (no dynamic indexing into cv)
                 const uint4 w = u == 0 ? cv0 : (u == 1 ? cv1 : (u == 2 ? cv2 : cv3));
                 const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -3033,7 +3026,6 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
                 P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves, P.znext, P.znext_words,
                 P.match, P.match_neg, P.page_flags};
-    a.ilv = P.write_ilv;
     if (P.wgn > 0) {  // one segment: workgroups [wg0, wg0 + wgn) of the grid
         a.wg0 = static_cast<uint32_t>(P.wg0);
         grid = min(P.wgn, grid - P.wg0);

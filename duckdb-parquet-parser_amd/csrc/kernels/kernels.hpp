@@ -199,7 +199,6 @@ struct PipeLaunch {
     // k_pipe_codes3 tiles [t_lo, t_hi) and the marked pages [p_lo, p_hi)
     // (t_hi < 0: all)
     int wg_total = 0, wg0 = 0, wgn = 0;
-    int write_ilv = 0;  // k_pipe_write: a workgroup's waves take its tiles in turn
     int t_lo = 0, t_hi = -1, p_lo = 0, p_hi = -1;
 };
 constexpr uint32_t kArmDictBytes = 32768;  // every entry length < 2^15: the match bit rides in the entry word
