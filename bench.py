@@ -49,7 +49,7 @@ for _p in (ROOT, PKG):
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 # kernel timers (HIP events on the decode stream, capi.hip Timed)
-KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_page", "pipe_big", "wide_chars", "pipe_count", "pipe_codes", "pipe_write",
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "wide_chars", "pipe_count", "pipe_codes", "pipe_write",
            "ba_fused", "ba_rows", "scan", "ba_gather", "plain_spec", "plain_ba", "fixed_plain", "fixed", "plain_opt")
 REGEX_KERNELS = ("regex_dict", "regex_codes", "regex_lanes", "regex_plain", "regex_pages")
 ROWS = 10_000_000

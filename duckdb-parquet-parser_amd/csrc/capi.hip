@@ -87,11 +87,6 @@ struct pq_ctx {
     size_t chunker_cap = 0;
     bool opt_raw = true;                   // "raw_upload": DMA raw chunk bytes during the walk, relayout on the GPU
     hipStream_t side = nullptr;            // dictionary decode beside the run-table pass
-    // segmented pipe decode (pipe_segmented): the writer's stream, one event
-    // per segment (its codes are complete) and the join back to `stream`
-    hipStream_t wstream = nullptr;
-    std::vector<hipEvent_t> ev_seg;
-    hipEvent_t ev_wend = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     bool timing = false;
@@ -131,9 +126,6 @@ struct pq_ctx {
     int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
     int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
-    bool opt_pipe_page = false;  // "pipe_page": k_pipe_page (a wavefront per page) for the pipe's run tables and codes
-    int opt_pipe_segs = 1;       // "pipe_segs": tile segments of a pipe decode whose front overlaps the writer (1: off)
-    int opt_seg_min_tiles = 1024;  // "pipe_seg_min_tiles": tiles per segment below which a decode is one pass
     bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
     int opt_write_bpc = 0;       // "write_bpc": cap on k_pipe_write workgroups per CU (0: as many as fit; set before upload)
     int opt_stage_bufs = 6;      // "stage_bufs" / "stage_piece_kb": pinned upload ring (stage.hpp)
@@ -179,7 +171,6 @@ struct pq_chunk {
     int64_t* d_tile_chars = nullptr;
     // three-pass dictionary BYTE_ARRAY decode (dict_pipe.hip)
     bool pipe = false, pipe_count = false;
-    bool pipe_page = false;             // k_pipe_page takes the run tables and codes (planned with opt_pipe_page)
     int32_t pipe_dict = -1;
     uint32_t pipe_dict_chars_bytes = 0, pipe_dict_bytes = 0, pipe_lds = 0, pipe_ecap = 0;
     int pipe_cus = 256;
@@ -209,14 +200,6 @@ struct pq_chunk {
     uint32_t pipe_small_bytes = 0;      // the largest payload of those pages
     bool pipe_wide = false;             // 32-bit codes, dictionary in HBM (k_pipe_big<true> -> k_pipe_wwide)
     int pipe_wpw = 10;                  // k_pipe_write writer waves per workgroup (planned)
-    // segments of a segmented decode (pipe_segmented; empty: one pass):
-    // writer workgroups [wg0, wg0 + wgn) of pipe_wg_total, their tiles
-    // [t_lo, t_hi), the pages [p_lo, p_hi) whose first tile is among them
-    struct PipeSeg {
-        int wg0, wgn, t_lo, t_hi, p_lo, p_hi;
-    };
-    std::vector<PipeSeg> psegs;
-    int pipe_wg_total = 0;              // writer workgroups of the decode (bsum entries)
     std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
     int32_t* d_bigp = nullptr;
     uint32_t big_max_bytes = 0;
@@ -542,7 +525,6 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     c->pipe = false;
     c->pipe_wide = false;
     c->pipe_count = false;
-    c->pipe_page = false;
     c->pipe_small = false;
     c->hbig.clear();
     c->big_max_bytes = 0;
@@ -584,8 +566,6 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     c->pipe_small = small;
     c->pipe_small_bytes = small_bytes;
     c->pipe_count = multi && c->max_def > 0;
-    c->pipe_page = ctx->opt_pipe_page && small && big.empty() && small_bytes <= pqk::pipe_page_stage();
-    if (c->pipe_page) c->pipe_count = false;  // k_pipe_page counts a page's earlier tiles itself
     c->hbig = std::move(big);
     c->big_max_bytes = big_bytes;
     c->pipe_dict = dict_id;
@@ -598,42 +578,6 @@ void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::
     c->pipe_ecap = static_cast<uint32_t>(ecap);
     c->pipe_cus = cus;
     c->pipe_wpw = wpw;
-}
-
-// A pipe decode in segments (pipe_segmented): the writer grid of the decode
-// (pipe_grid workgroups per launch, opt_pipe_segs launches) cut into
-// opt_pipe_segs ranges of workgroups; a segment's tiles are its workgroups'
-// tiles, its pages those whose first tile is among them.  Chunks whose pages
-// all take k_pipe_runs / k_pipe_codes3 with no count pass (the C2 shape).
-void plan_pipe_segs(pq_ctx* ctx, pq_chunk* c, const PVec<DevTile>& htiles, size_t npages) {
-    c->psegs.clear();
-    c->pipe_wg_total = c->pipe_grid;
-    const int K = ctx->opt_pipe_segs, nt = c->ntiles;
-    if (!c->pipe || c->pipe_wide || !c->hbig.empty() || (c->pipe_count && !c->pipe_page) || !c->pipe_small || K < 2 ||
-        nt < K * ctx->opt_seg_min_tiles)
-        return;
-    const int wpw = c->pipe_wpw;
-    const int64_t need = (static_cast<int64_t>(nt) + wpw - 1) / wpw;
-    const int gt = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(need, static_cast<int64_t>(c->pipe_grid) * K)));
-    const int64_t per = std::max<int64_t>(1, (nt + static_cast<int64_t>(gt) * wpw - 1) / (static_cast<int64_t>(gt) * wpw));
-    if (gt < K) return;
-    const int NP = static_cast<int>(npages);
-    auto first_page = [&](int64_t t) {  // the first page whose first tile is at or after t
-        if (t >= nt) return NP;
-        const DevTile& T = htiles[static_cast<size_t>(t)];
-        return T.page + (T.row0 != 0 ? 1 : 0);
-    };
-    for (int k = 0; k < K; k++) {
-        pq_chunk::PipeSeg g{};
-        g.wg0 = static_cast<int>(static_cast<int64_t>(k) * gt / K);
-        g.wgn = static_cast<int>(static_cast<int64_t>(k + 1) * gt / K) - g.wg0;
-        g.t_lo = static_cast<int>(std::min<int64_t>(nt, static_cast<int64_t>(g.wg0) * wpw * per));
-        g.t_hi = static_cast<int>(std::min<int64_t>(nt, static_cast<int64_t>(g.wg0 + g.wgn) * wpw * per));
-        g.p_lo = first_page(g.t_lo);
-        g.p_hi = first_page(g.t_hi);
-        c->psegs.push_back(g);
-    }
-    c->pipe_wg_total = gt;
 }
 
 // PLAIN BYTE_ARRAY chunks without levels go through plain_ba.hip: windows of
@@ -921,12 +865,6 @@ void pq_ctx_destroy(pq_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_fork);
     (void)hipEventDestroy(ctx->ev_join);
     (void)hipStreamDestroy(ctx->side);
-    if (ctx->wstream) {
-        (void)hipStreamSynchronize(ctx->wstream);
-        (void)hipStreamDestroy(ctx->wstream);
-    }
-    for (hipEvent_t e : ctx->ev_seg) (void)hipEventDestroy(e);
-    if (ctx->ev_wend) (void)hipEventDestroy(ctx->ev_wend);
     ctx->stager.release();
     if (ctx->d_raw) (void)hipFree(ctx->d_raw);
     if (ctx->d_walk) (void)hipFree(ctx->d_walk);
@@ -986,17 +924,6 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
     if (std::strcmp(key, "write_bpc") == 0) {
         if (value < 0 || value > 4) return set_err(ctx, PQ_ERR_ARG, "write_bpc: 0..4");
         ctx->opt_write_bpc = static_cast<int>(value);
-        return 0;
-    }
-    if (std::strcmp(key, "pipe_page") == 0) { ctx->opt_pipe_page = value != 0; return 0; }
-    if (std::strcmp(key, "pipe_segs") == 0) {
-        if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "pipe_segs: 1..16");
-        ctx->opt_pipe_segs = static_cast<int>(value);
-        return 0;
-    }
-    if (std::strcmp(key, "pipe_seg_min_tiles") == 0) {
-        if (value < 1 || value > (1 << 24)) return set_err(ctx, PQ_ERR_ARG, "pipe_seg_min_tiles: 1..2^24");
-        ctx->opt_seg_min_tiles = static_cast<int>(value);
         return 0;
     }
     if (std::strcmp(key, "pipe_run_pages") == 0) {
@@ -1609,7 +1536,6 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
                 c->fixed_plain &= P.plain;
             }
         }
-        plan_pipe_segs(ctx, c.get(), htiles, hpages.size());
 
         sub_timer.reset();
         plan_timer.reset();
@@ -1627,9 +1553,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         rc |= dalloc(&c->d_dict_err, hdicts.size());
         if (c->pipe) {  // flags | bsum | flist, cleared together
             // (bsum: pipe_grid k_pipe_write workgroup sums)
-            // flags: [0] errors, [1] overflow, [2] fallback, [3] redo, [4] k_pipe_page's
-            // dictionary workgroups done, [5] its tickets
-            const size_t fb = 8 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_wg_total) * sizeof(unsigned long long);
+            const size_t fb = 4 * sizeof(int32_t), bb = static_cast<size_t>(c->pipe_grid) * sizeof(unsigned long long);
             c->z_bsum = fb;
             c->z_flist = (fb + bb + 15) / 16 * 16;
             // cleared per decode (through flist[0]): a multiple of 16 bytes (an
@@ -1692,10 +1616,8 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
         rc |= dalloc(&c->d_scan_scratch, std::max(htiles.size(), hpages.size()) / 8192 + 16);
         if (c->type == PQ_BYTE_ARRAY && !c->fused) rc |= dalloc(&c->d_row_codes, static_cast<size_t>(c->nrows));
         if (c->pipe) {
-            if (!c->pipe_page) {  // k_pipe_page keeps its run tables in LDS
-                rc |= dalloc(&c->d_runs, hpages.size() * 2 * pqk::kPipeRunCap);
-                rc |= dalloc(&c->d_info, hpages.size());
-            }
+            rc |= dalloc(&c->d_runs, hpages.size() * 2 * pqk::kPipeRunCap);
+            rc |= dalloc(&c->d_info, hpages.size());
             // u16 codes, or u32 on the wide pipe (d_codes then holds 2 per row)
             rc |= dalloc(&c->d_codes, static_cast<size_t>(c->nrows) * (c->pipe_wide ? 2 : 1) + 64);
             rc |= dalloc(&c->d_tile_nn, htiles.size());
@@ -2203,7 +2125,6 @@ static pqk::PipeLaunch pipe_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     P.page_err = c->d_page_err; P.err_any = c->d_flags;
     P.dict_chars_bytes = c->pipe_dict_chars_bytes; P.dict_bytes = c->pipe_dict_bytes; P.lds = c->pipe_lds;
     P.grid = c->pipe_grid;
-    P.wg_total = c->psegs.empty() ? 0 : c->pipe_wg_total;
     P.debug = ctx->opt_debug;
     P.dict_entries_cap = c->pipe_ecap;
     P.cus = c->pipe_cus;
@@ -2233,14 +2154,6 @@ static void launch_dicts(pq_chunk* c, hipStream_t s, int32_t* err_any) {
 
 static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool dict_on_side, bool dict_in_runs) {
     hipStream_t s = ctx->stream;
-    if (c->pipe_page) {  // a wavefront per page: run tables and codes in one launch
-        if (dict_on_side && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
-        const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
-        Timed t(ctx, "pipe_page");
-        pqk::launch_pipe_page(s, P, dict_in_runs ? &rd : nullptr, reinterpret_cast<uint32_t*>(c->d_flags + 4),
-                              c->max_dict_bytes);
-        return;
-    }
     {
         Timed t(ctx, "pipe_runs");
         const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
@@ -2270,83 +2183,6 @@ static void pipe_front(pq_ctx* ctx, pq_chunk* c, const pqk::PipeLaunch& P, bool 
 }
 
 static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out);
-
-// The writer's stream and events of a segmented decode (created on first use).
-static bool ensure_seg_streams(pq_ctx* ctx, size_t k) {
-    if (!ctx->wstream && hipStreamCreateWithFlags(&ctx->wstream, hipStreamNonBlocking) != hipSuccess) {
-        ctx->wstream = nullptr;
-        return false;
-    }
-    if (!ctx->ev_wend && hipEventCreateWithFlags(&ctx->ev_wend, hipEventDisableTiming) != hipSuccess) {
-        ctx->ev_wend = nullptr;
-        return false;
-    }
-    while (ctx->ev_seg.size() < k) {
-        hipEvent_t e = nullptr;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
-        ctx->ev_seg.push_back(e);
-    }
-    return true;
-}
-
-// A pipe decode in segments (plan_pipe_segs): segment k's run tables and
-// codes go to `stream` ahead of segment k - 1's writer on `wstream`, so the
-// latency-bound front of one segment runs beside the HBM-bound writer of the
-// previous one.  Writer k waits for its segment's codes (ev_seg[k]); the
-// decode ends with `stream` waiting for the last writer (ev_wend), so
-// everything after it (collect, the next decode, a regex scan over the
-// codes) is ordered after every writer.
-static void pipe_segmented(pq_ctx* ctx, pq_chunk* c, pq_column* out, bool dict_in_runs) {
-    hipStream_t s = ctx->stream, w = ctx->wstream;
-    pqk::PipeLaunch P = pipe_launch(ctx, c, out);
-    const pqk::RunDicts rd{c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count, c->d_dict_err, c->d_dflag};
-    const int K = static_cast<int>(c->psegs.size());
-    uint32_t* znext = nullptr;
-    if (c->d_zero) znext = reinterpret_cast<uint32_t*>(c->d_zero + static_cast<size_t>(c->zsel ^ 1) * c->zfull);
-    for (int k = 0; k < K; k++) {
-        const pq_chunk::PipeSeg& g = c->psegs[static_cast<size_t>(k)];
-        pqk::PipeLaunch Q = P;
-        Q.t_lo = g.t_lo; Q.t_hi = g.t_hi; Q.p_lo = g.p_lo; Q.p_hi = g.p_hi;
-        if (c->pipe_page) {
-            if (k == 0 && !dict_in_runs && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
-            Timed t(ctx, "pipe_page");
-            pqk::launch_pipe_page(s, Q, k == 0 && dict_in_runs ? &rd : nullptr,
-                                  reinterpret_cast<uint32_t*>(c->d_flags + 4), c->max_dict_bytes);
-        } else {
-            {
-                Timed t(ctx, "pipe_runs");
-                pqk::launch_pipe_runs(s, c->d_bytes, c->d_pages, g.p_hi, c->max_def, c->max_rep, c->d_runs,
-                                      c->d_info, ctx->opt_run_pages, c->d_flist, ctx->opt_debug,
-                                      k == 0 && dict_in_runs ? &rd : nullptr, 0u,
-                                      (c->pipe_small_bytes + 15) / 16 * 16 + 16, c->max_dict_bytes, ctx->cus, g.p_lo);
-            }
-            if (k == 0 && !dict_in_runs && c->ndicts) (void)hipStreamWaitEvent(s, ctx->ev_join, 0);
-            Timed t(ctx, "pipe_codes");
-            pqk::launch_pipe_codes(s, Q, false);
-        }
-        if (k == 0 && c->arm) {  // the page filter's match bits per entry, before the first writer
-            Timed t(ctx, "regex_dict");
-            pqre::launch_regex_dict(s, c->d_prog, c->d_bytes, c->d_dicts, c->ndicts, c->d_entries, c->d_dict_count,
-                                    c->d_dict_match, c->d_page_flags, c->npages);
-            P.match = c->d_dict_match + c->pipe_entry_base;
-            P.match_neg = c->arm_neg;
-            P.page_flags = c->d_page_flags;
-        }
-        (void)hipEventRecord(ctx->ev_seg[static_cast<size_t>(k)], s);
-        (void)hipStreamWaitEvent(w, ctx->ev_seg[static_cast<size_t>(k)], 0);
-        Q = P;
-        Q.wg0 = g.wg0; Q.wgn = g.wgn;
-        if (k == K - 1 && znext) {  // the last writer clears the other block for the next decode
-            Q.znext = znext;
-            Q.znext_words = static_cast<uint32_t>(c->zero_bytes / 4);
-        }
-        Timed t(ctx, "pipe_write", w);
-        pqk::launch_pipe_write(w, Q);
-    }
-    (void)hipEventRecord(ctx->ev_wend, w);
-    (void)hipStreamWaitEvent(s, ctx->ev_wend, 0);
-    if (c->d_zero) c->next_zeroed = true;
-}
 
 int pq_decode_async(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
     if (!ctx || !c || !out) return PQ_ERR_ARG;
@@ -2495,8 +2331,6 @@ static int decode_launch(pq_ctx* ctx, pq_chunk* c, pq_column* out) {
         }
         Timed t(ctx, "plain_ba");
         pqk::launch_plain_ba(s, P);
-    } else if (pipe && !c->psegs.empty() && ensure_seg_streams(ctx, c->psegs.size())) {
-        pipe_segmented(ctx, c, out, dict_in_runs);
     } else if (pipe) {
         pqk::PipeLaunch P = pipe_launch(ctx, c, out);
         pipe_front(ctx, c, P, !dict_in_runs, dict_in_runs);

@@ -107,8 +107,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
                                                               uint2* __restrict__ runs,
                                                               uint32_t* __restrict__ info, int ppw,
                                                               int32_t* __restrict__ flist, uint32_t stage_max,
-                                                              RunDictArgs d, int debug, uint32_t wstage,
-                                                              int page0) {
+                                                              RunDictArgs d, int debug, uint32_t wstage) {
     // dynamic LDS: kRunWaves windows of wstage + 32 bytes each (wstage: the
     // group's pages fit when it is at least ppw page slots), or the leading
     // workgroups' dictionary page
@@ -122,7 +121,7 @@ __global__ void __launch_bounds__(kRunWaves * 64) k_pipe_runs(const uint8_t* __r
         return;
     }
     const uint32_t wv = threadIdx.x / kWave;
-    const int g0 = page0 + ((static_cast<int>(blockIdx.x) - d.ndicts) * kRunWaves + static_cast<int>(wv)) * ppw;
+    const int g0 = ((static_cast<int>(blockIdx.x) - d.ndicts) * kRunWaves + static_cast<int>(wv)) * ppw;
     if (g0 >= npages) return;
     const int g1 = min(npages, g0 + ppw);
     uint32_t* stage = stage_dyn + wv * wwords;
@@ -267,10 +266,6 @@ struct CodeArgs {
     int wpw;                   // k_pipe_write's writer waves per workgroup (bsum index)
     uint32_t* codes32 = nullptr;  // wide chunks: 32-bit codes here instead of `codes` (k_pipe_big<true>)
     const uint8_t* lens8 = nullptr;  // wide chunks: entry lengths as bytes (255: 255 or more), or null
-    // k_pipe_codes3 of one segment of a segmented decode (capi.hip
-    // pipe_segmented): tiles [t_lo, t_hi), and the marked pages [p_lo, p_hi)
-    // whose exact decode it owns; t_hi < 0: every tile and page
-    int t_lo = 0, t_hi = -1, p_lo = 0, p_hi = -1;
 };
 
 // Characters of tile t also go to the k_pipe_write workgroup that writes it.
@@ -630,10 +625,9 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
     const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
     const uint32_t maskd = (1u << bwd) - 1u;
     const int nw = static_cast<int>(gridDim.x) * kCodeWaves3;
-    const int t_lo = a.t_hi < 0 ? 0 : a.t_lo, t_hi = a.t_hi < 0 ? a.ntiles : a.t_hi;
-    const int per = (t_hi - t_lo + nw - 1) / nw;
-    const int ta = min(t_hi, t_lo + (static_cast<int>(blockIdx.x) * kCodeWaves3 + wv) * per);
-    const int tb = min(t_hi, ta + per);
+    const int per = (a.ntiles + nw - 1) / nw;
+    const int ta = min(a.ntiles, (static_cast<int>(blockIdx.x) * kCodeWaves3 + wv) * per);
+    const int tb = min(a.ntiles, ta + per);
     const uint32_t l8 = lane() * 8;
     auto rl64 = [](uint64_t v, int i) -> uint64_t {
         const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), i);
@@ -853,13 +847,9 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
     }
     // pages k_pipe_runs / k_pipe_big marked (complete before this launch):
     // the exact serial decoder, one wave per page
-    // (a segment's launch: the marked pages of its own page range; the list
-    // also holds earlier segments' pages, decoded by their launches)
     const int nf = flist[0];
     for (int i = static_cast<int>(blockIdx.x) * kCodeWaves3 + wv; i < nf; i += nw) {
-        const int fp = flist[1 + i];
-        if (a.t_hi >= 0 && (fp < a.p_lo || fp >= a.p_hi)) continue;
-        exact_page_body(a, LX, fp, dict_n, ebase);
+        exact_page_body(a, LX, flist[1 + i], dict_n, ebase);
         __builtin_amdgcn_wave_barrier();
     }
     // a dictionary longer than the length table (not planned: lt_n covers
@@ -870,463 +860,6 @@ __global__ void __launch_bounds__(kCodeWaves3 * 64) k_pipe_codes3(CodeArgs a, ui
             if (T.row0 == 0 && !(a.info[T.page] & kSkip)) exact_page_body(a, LX, T.page, dict_n, ebase);
             __builtin_amdgcn_wave_barrier();
         }
-    }
-}
-
-// ── one wavefront per page: run tables by speculative parse, then codes ───
-// k_pipe_page replaces k_pipe_runs + k_pipe_codes3 (+ the count pass) for
-// chunks whose data pages all hold <= kPipeSmallRows rows and <= kPgStage
-// payload bytes (the C2 shape).  Per page, one wavefront:
-//  1. stages the payload into its LDS (one 16-byte block per lane);
-//  2. parses a run header (rle_decoder.hpp:36-95) at EVERY byte position of
-//     the def-level and index streams at once (positions lane, lane + 64, ...):
-//     t1[p] = the next header's position (kPgTerm: the stream ends there) |
-//     the run's values (saturating) | header length | literal bit; a position
-//     where no valid header starts reads kPgBad;
-//  3. four pointer-doubling rounds over a copy give tk[p] = the position 16
-//     headers on and the values those 16 runs hold;
-//  4. one lane per stream follows the 16-run jumps from the stream start (at
-//     most 8 hops: kPipeRunCap = 128 records); one lane per 16-run group then
-//     walks its group through t1 and emits exactly the records walk_runs
-//     emits (run_walk.hpp: counts clamped at the values left, the record of
-//     an exhausted stream, the same fallback conditions);
-//  5. decodes the page's tiles from the records in LDS as k_pipe_codes3 does
-//     (the non-null count of the earlier tiles rides in a register).
-// The serial chain per stream is ~4 + 8 + 17 dependent LDS reads instead of
-// one header parse per run, and every wave has its own page, so the chip
-// holds 4 waves per SIMD of independent chains (k_pipe_runs: 0.6 per SIMD).
-// Pages outside the shape (payload past the stage, prologue errors, zero-count
-// runs, bit widths > 16, more than kPipeRunCap runs) take exact_page_body in
-// the same wavefront.  Dictionary pages decode in the leading workgroups
-// (dict_index_block); page workgroups wait for them (counter `ready`, in the
-// zeroed per-decode block) after their first pages' run tables, before any
-// codes.  Persistent: wave g takes pages p_lo + g, p_lo + g + nw, ...
-constexpr int kPageWaves = 4;
-constexpr uint32_t kPgStage = 1024;                 // largest payload a wave stages (bytes)
-constexpr uint32_t kPgTerm = 0x1FFFu, kPgBad = 0x1FFEu;
-constexpr uint32_t kPgJ = 0x1FFFu;                  // next-position field (13 bits)
-constexpr uint32_t kPgSat1 = 0x7FFFu;               // t1 values field (15 bits)
-constexpr uint32_t kPgSatK = 0x7FFFFu;              // tk values field (19 bits)
-constexpr int kPgPos = static_cast<int>(kPgStage) / kWave;  // byte positions per lane
-static_assert(kPgStage < kPgBad && kPipeSmallRows < static_cast<int32_t>(kPgSat1), "field widths");
-
-struct __attribute__((aligned(16))) PageLds {
-    union {
-        uint32_t tk[kPgStage];  // doubling table: next position (13 bits) | values (19 bits)
-        CodeLds code;           // then: the run records and marks (also exact_page_body's scratch)
-    } u;
-    uint32_t t1[kPgStage];      // per position: next | values << 13 | header length << 28 | literal << 31
-    uint32_t stage[kPgStage / 4 + 8 + 16];  // the payload's slot (<= kPgStage + 16 bytes), then 2 x 8 group heads
-};
-static_assert(sizeof(CodeLds) <= sizeof(uint32_t) * kPgStage, "records and marks in tk");
-
-struct PageArgs {
-    RunDictArgs d;      // dictionary pages decoded by the first d.ndicts workgroups to take a ticket
-    uint32_t* ready;    // [0]: dictionary workgroups done, [1]: tickets (both zeroed per decode)
-    uint32_t lens_bytes;
-    uint32_t lt_n;
-    uint32_t dyn_bytes;
-};
-
-// The u32 at stage byte a (>= 8 readable bytes past a).
-__device__ __forceinline__ uint32_t pg_u32(const uint32_t* st, uint32_t a) {
-    const uint32_t i = a >> 2, sh = a & 3u;
-    return __builtin_amdgcn_alignbyte(st[i + 1], st[i], sh);
-}
-
-// Run header at stage byte p of a stream ending at e (bit width bw): t1 word.
-__device__ __forceinline__ uint32_t pg_parse(const uint32_t* st, uint32_t p, uint32_t e, uint32_t bw) {
-    const uint32_t x0 = pg_u32(st, p), x1 = pg_u32(st, p + 4);
-    const uint32_t nbv = (bw + 7) / 8;
-    // varint header (rle_decoder.hpp:76-86), as walk_runs parses it
-    const uint32_t st0 = ~x0 & 0x80808080u;
-    const uint32_t hl4 = (__builtin_ctz(st0 | 0x80000000u) >> 3) + 1;
-    const uint32_t hl = st0 ? hl4 : ((~x1 & 0x80u) ? 5u : 9u);
-    const uint32_t lm = (hl >= 4) ? 0xFFFFFFFFu : ((1u << (8 * (hl & 3))) - 1u);
-    const uint32_t x0m = x0 & lm;
-    const uint32_t top = (hl >= 5) ? (x1 << 28) : 0u;
-    const uint32_t ind = (x0m & 0x7Fu) | ((x0m >> 1) & 0x3F80u) | ((x0m >> 2) & 0x1FC000u) | ((x0m >> 3) & 0xFE00000u) | top;
-    const uint32_t g = ind >> 1, lit = ind & 1u;
-    const uint32_t qh = p + hl;
-    const bool bad = hl > 5 || qh > e || g == 0 || (!lit && qh + nbv > e);
-    const uint32_t nq = lit ? min(__umul24(min(g, 0x10000u), bw) + qh, e) : qh + nbv;
-    const uint32_t c = lit ? min(g, kPgSat1 / 8) * 8 : min(g, kPgSat1);
-    const uint32_t J = nq >= e ? kPgTerm : nq;
-    return bad ? (kPgBad | (kPgSat1 << 13)) : (J | (c << 13) | (hl << 28) | (lit << 31));
-}
-
-// What phase A (stage, run tables) hands phase B (codes) for one page.
-struct PgState {
-    bool ex;             // exact decoder
-    uint32_t size, n, nd, ni, bwi;
-    int64_t first_row;
-};
-
-// Phase A: the page's payload to LDS and its run records (walk_runs' records
-// for the def-level and index streams) into L.u.code.recd / reci.
-__device__ __forceinline__ PgState page_runs(const CodeArgs& a, PageLds& L, int p) {
-    PgState S{};
-    const DevPage pg = a.pages[p];
-    S.size = static_cast<uint32_t>(max(pg.size, 0));
-    S.n = static_cast<uint32_t>(max(pg.nvals, 0));
-    S.first_row = pg.first_row;
-    const uint32_t size = S.size, n = S.n;
-    bool ex = size > kPgStage || n > static_cast<uint32_t>(kPipeSmallRows) || n > 65535u;
-    if (ex) {
-        S.ex = true;
-        return S;
-    }
-    {  // the slot's blocks (payload + >= 16 zero bytes): one per lane
-        const uint4* src = reinterpret_cast<const uint4*>(a.bytes + pg.off);
-        uint4* dst = reinterpret_cast<uint4*>(L.stage);
-        const uint32_t nb = (size + 15) / 16 + 1;
-        for (uint32_t b = lane(); b < nb; b += kWave) dst[b] = src[b];
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (probe(a.debug, 1 << 20)) { S.ex = true; return S; }  // timing: staging only
-    const uint32_t* st = L.stage;
-    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
-    // prologue (column_reader.cpp:146-182); any error -> exact decoder
-    uint32_t pos = 0, b0 = 0, e0 = 0, bwi = 0;
-    if (md > 0) {
-        if (size < 4) ex = true;
-        else {
-            const uint32_t dlen = pg_u32(st, 0);
-            pos = 4;
-            if (static_cast<uint64_t>(pos) + dlen > size) ex = true;
-            else { b0 = 4; e0 = 4 + dlen; pos = e0; }
-        }
-    }
-    if (!ex && a.max_rep > 0) {
-        if (pos + 4 > size) ex = true;
-        else {
-            const uint32_t rl = pg_u32(st, pos);
-            pos += 4;
-            if (static_cast<uint64_t>(pos) + rl > size) ex = true;
-            else pos += rl;
-        }
-    }
-    if (!ex) {
-        if (pos + 1 > size) ex = true;
-        else { bwi = pg_u32(st, pos) & 0xFFu; pos += 1; }
-    }
-    if (!ex && bwi > 16) ex = true;
-    S.bwi = bwi;
-    if (ex) {
-        S.ex = true;
-        return S;
-    }
-    const uint32_t b1 = pos, e1 = size;
-    uint32_t* t1 = L.t1;
-    uint32_t* tk = L.u.tk;
-    // 2. a header parse at every position of both streams
-    constexpr uint32_t kBadW = kPgBad | (kPgSat1 << 13);
-    for (uint32_t q = lane(); q < size; q += kWave) {
-        const bool ind = md > 0 && q >= b0 && q < e0, inx = q >= b1;
-        const uint32_t w = (ind || inx) ? pg_parse(st, q, ind ? e0 : e1, ind ? bwd : bwi) : kBadW;
-        t1[q] = w;
-        tk[q] = (w & kPgJ) | (((w >> 13) & kPgSat1) << 13);
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if (probe(a.debug, 1 << 21)) { S.ex = true; return S; }  // timing: + header parse
-    // 3. jumps of 2, 4, 8, 16 runs (the new words held in registers until
-    // every lane has read the old ones)
-    for (int rnd = 0; rnd < 4; rnd++) {
-        uint32_t nv[kPgPos];
-#pragma unroll
-        for (int i = 0; i < kPgPos; i++) {
-            const uint32_t q = lane() + static_cast<uint32_t>(i) * kWave;
-            uint32_t v = 0;
-            if (static_cast<uint32_t>(i) * kWave < size && q < size) {
-                v = tk[q];
-                const uint32_t J = v & kPgJ;
-                if (J < kPgBad) {
-                    const uint32_t w = tk[J];
-                    v = (w & kPgJ) | (min((v >> 13) + (w >> 13), kPgSatK) << 13);
-                }
-            }
-            nv[i] = v;
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int i = 0; i < kPgPos; i++) {
-            const uint32_t q = lane() + static_cast<uint32_t>(i) * kWave;
-            if (static_cast<uint32_t>(i) * kWave < size && q < size) tk[q] = nv[i];
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    }
-    if (probe(a.debug, 1 << 22)) { S.ex = true; return S; }  // timing: + doubling
-    // 4a. group heads: lane s follows stream s's 16-run jumps
-    uint32_t* heads = L.stage + kPgStage / 4 + 8;  // 2 x 8: position | values before << 16
-    uint32_t G = 0, ovf = 0;
-    if (lane() < 2) {
-        const uint32_t s = lane();
-        const uint32_t b = s ? b1 : b0, e = s ? e1 : e0;
-        if ((s == 1 || md > 0) && n > 0) {  // walk_runs: a stream with values to read
-            uint32_t q = b, cum = 0;
-            heads[s * 8] = q;
-            G = 1;
-            while (q < e) {
-                const uint32_t v = tk[q];
-                const uint32_t J = v & kPgJ, C = v >> 13;
-                if (J >= kPgBad || cum + C >= n) break;
-                if (G == kPipeRunCap / 16) { ovf = 1; break; }
-                q = J;
-                cum += C;
-                heads[s * 8 + G] = q | (cum << 16);
-                G++;
-            }
-        }
-    }
-    const uint32_t G0 = __builtin_amdgcn_readlane(G, 0), G1 = __builtin_amdgcn_readlane(G, 1);
-    const bool over = __ballot(ovf != 0) != 0;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // 4b. one lane per group walks its runs through t1 (the records overlay tk)
-    CodeLds& R = L.u.code;
-    const uint32_t s = lane() >> 3, j = lane() & 7;
-    const uint32_t Gs = s ? G1 : G0;
-    uint32_t r = 0, fl = 0;
-    if (lane() < 16 && j < Gs) {
-        const uint32_t h = heads[s * 8 + j];
-        uint32_t q = h & 0xFFFFu, cnt = h >> 16;
-        const bool last = j + 1 == Gs;
-        const uint32_t e = s ? e1 : e0, bw = s ? bwi : bwd;
-        const uint32_t nbv = (bw + 7) / 8;
-        const uint32_t vmask = nbv >= 2 ? 0xFFFFu : (nbv ? 0xFFu : 0u);
-        uint2* rec = s ? R.reci : R.recd;
-        r = 16 * j;
-        const uint32_t lim = r + (last ? 17u : 16u);
-        while (r < lim) {
-            if (r >= kPipeRunCap) { fl = 1; break; }
-            if (q >= e) {  // exhausted (rle_decoder.hpp:20-23): the values left read as 0
-                rec[r++] = make_uint2(cnt | ((n - cnt) << 16), 0u);
-                break;
-            }
-            const uint32_t w = t1[q];
-            const uint32_t J = w & kPgJ;
-            if (J == kPgBad) { fl = 1; break; }
-            const uint32_t hl = (w >> 28) & 7u, lit = w >> 31, c = min((w >> 13) & kPgSat1, n - cnt);
-            const uint32_t qh = q + hl;
-            const uint32_t pl = lit ? (bw ? (0x80000000u | (qh << 3)) : 0u) : (pg_u32(st, qh) & vmask);
-            rec[r++] = make_uint2(cnt | (c << 16), pl);
-            cnt += c;
-            q = J == kPgTerm ? e : J;
-            if (cnt >= n) break;
-        }
-    }
-    S.nd = G0 ? __builtin_amdgcn_readlane(r, G0 - 1) : 0u;
-    S.ni = G1 ? __builtin_amdgcn_readlane(r, 8 + G1 - 1) : 0u;
-    S.ex = over || __ballot(fl != 0) != 0;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    return S;
-}
-
-// Phase B: the page's tiles from its records (k_pipe_codes3's tile body over
-// LDS records; the earlier tiles' non-null count in a register).
-__device__ __forceinline__ void page_codes(const CodeArgs& a, PageLds& L, const uint16_t* lens, int p, const PgState& S,
-                                           uint32_t dict_n) {
-    CodeLds& R = L.u.code;
-    const uint32_t md = static_cast<uint32_t>(a.max_def), bwd = level_bw(a.max_def);
-    const uint32_t maskd = (1u << bwd) - 1u;
-    const uint32_t size = S.size, n = S.n, nd = S.nd, ni = S.ni, bwi = S.bwi;
-    const uint32_t maski = (1u << bwi) - 1u;
-    const uint32_t zw = ((size + 15) / 16 + 1) * 4 - 1;  // last word of the slot: zero
-    const uint32_t l8 = lane() * 8;
-    const int32_t t0 = a.page_tile0[p];
-    const uint2 z = make_uint2(0u, 0u);
-    const uint2 d0 = lane() < nd ? R.recd[lane()] : z, d1 = lane() + kWave < nd ? R.recd[lane() + kWave] : z;
-    const uint2 x0 = lane() < ni ? R.reci[lane()] : z, x1 = lane() + kWave < ni ? R.reci[lane() + kWave] : z;
-    uint32_t kacc = 0;  // non-null values of the page's earlier tiles
-    for (uint32_t r0 = 0, ti = 0; r0 < n; r0 += kTileRows, ti++) {
-        const uint32_t m = min(n - r0, static_cast<uint32_t>(kTileRows));
-        const int t = t0 + static_cast<int>(ti);
-        __builtin_amdgcn_wave_barrier();
-        *reinterpret_cast<uint2*>(R.mark + l8) = z;
-        *reinterpret_cast<uint2*>(R.mark2 + l8) = z;
-        // def levels of rows r0 + 8l .. r0 + 8l + 7
-        uint32_t vb;
-        if (md > 0) {
-            const uint32_t rd0 = run_at_reg(d0, d1, nd, r0);
-            __builtin_amdgcn_wave_barrier();
-            {
-                const uint32_t k = lane(), st = rr_start(d0);
-                if (k < nd && k > rd0 && st < r0 + m) R.mark[st - r0] = static_cast<uint8_t>(k - rd0);
-                const uint32_t k1 = lane() + kWave, st1 = rr_start(d1);
-                if (k1 < nd && k1 > rd0 && st1 < r0 + m) R.mark[st1 - r0] = static_cast<uint8_t>(k1 - rd0);
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint2 mk = *reinterpret_cast<const uint2*>(R.mark + l8);
-            uint32_t rm[8], run = 0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
-                rm[k] = run;
-            }
-            const uint32_t ex = wave_shr1(wave_incl_max(run));
-            vb = 0;
-            bool above = false;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t j = l8 + k;
-                const uint2 Rr = R.recd[(rd0 + max(ex, rm[k])) & (kPipeRunCap - 1)];
-                const uint32_t pay = rr_pay(Rr);
-                const uint32_t lb = sbits3(L.stage, pay + (r0 + j - rr_start(Rr)) * bwd, zw, maskd);
-                const uint32_t lvl = rr_lit(Rr) ? lb : pay;
-                const bool in = j < m;
-                vb |= (in && lvl == md ? 1u : 0u) << k;
-                above |= in && lvl > md;
-            }
-            if (__ballot(above)) {  // levels above max_def: outside the supported format
-                set_err(a.page_err + p, a.err_any, PQ_ERR_UNSUPPORTED, 0, 0, size);
-                for (uint32_t j = lane(); j < m; j += kWave) a.codes[S.first_row + r0 + j] = kNull;
-                if (lane() == 0) a.tile_chars[t] = 0;
-                continue;
-            }
-        } else {
-            vb = l8 >= m ? 0u : (m - l8 >= 8 ? 0xFFu : ((1u << (m - l8)) - 1u));
-        }
-        const uint32_t nnl = __popc(vb);
-        const uint32_t nincl = wave_incl_scan(nnl);
-        const uint32_t rbase = nincl - nnl, nn = bcast_last(nincl);
-        const uint32_t k0 = md > 0 ? kacc : r0;
-        kacc += nn;
-        // dictionary index runs over ranks [k0, k0 + nn): run of each rank -> mark2
-        const uint32_t ri0 = run_at_reg(x0, x1, ni, k0);
-        if (nn) {
-            __builtin_amdgcn_wave_barrier();
-            {
-                const uint32_t k = lane(), st = rr_start(x0);
-                if (k < ni && k > ri0 && st < k0 + nn) R.mark2[st - k0] = static_cast<uint8_t>(k - ri0);
-                const uint32_t k1 = lane() + kWave, st1 = rr_start(x1);
-                if (k1 < ni && k1 > ri0 && st1 < k0 + nn) R.mark2[st1 - k0] = static_cast<uint8_t>(k1 - ri0);
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint2 mk = *reinterpret_cast<const uint2*>(R.mark2 + l8);
-            uint32_t rm[8], run = 0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                run = max(run, ((k < 4 ? mk.x : mk.y) >> (8 * (k & 3))) & 0xFFu);
-                rm[k] = run;
-            }
-            const uint32_t ex = wave_shr1(wave_incl_max(run));
-            uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t v = max(ex, rm[k]);
-                if (k < 4) w0 |= v << (8 * k);
-                else w1 |= v << (8 * (k - 4));
-            }
-            __builtin_amdgcn_wave_barrier();
-            *reinterpret_cast<uint2*>(R.mark2 + l8) = make_uint2(w0, w1);
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        uint32_t chars = 0, pw[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t rk = min(rbase + __popc(vb & ((1u << k) - 1u)), static_cast<uint32_t>(kTileRows - 1));
-            const uint2 Rr = R.reci[(ri0 + R.mark2[rk]) & (kPipeRunCap - 1)];
-            const uint32_t pay = rr_pay(Rr);
-            const uint32_t lb = sbits3(L.stage, pay + (k0 + rk - rr_start(Rr)) * bwi, zw, maski);
-            const uint32_t v = rr_lit(Rr) ? lb : pay;
-            const bool ok = ((vb >> k) & 1u) && v < dict_n;
-            const uint32_t len = lens[ok ? v : 0u];
-            chars += ok ? len : 0u;
-            const uint32_t code = ok ? v : static_cast<uint32_t>(kNull);
-            if (k & 1) pw[k >> 1] |= code << 16;
-            else pw[k >> 1] = code;
-        }
-        // (the empty asm keeps the packed words opaque: ROCm 7.2's instruction
-        // selection crashes on this kernel when it folds them into the store)
-        asm volatile("" : "+v"(pw[0]), "+v"(pw[1]), "+v"(pw[2]), "+v"(pw[3]));
-        store_packed8(a.codes, S.first_row + r0, l8, m, pw);
-        tile_done(a, t, wave_sum(chars));
-    }
-}
-
-__global__ void __launch_bounds__(kPageWaves * 64) k_pipe_page(CodeArgs a, PageArgs pa) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-    __shared__ int role_s;
-    const int nd = pa.d.ndicts;
-    // roles by ticket, not blockIdx: the dictionary workgroups are the first
-    // to run whatever the dispatch order, so a page workgroup only waits for
-    // workgroups already resident (no deadlock when fewer fit)
-    int role = static_cast<int>(blockIdx.x);
-    if (nd > 0) {
-        if (threadIdx.x == 0)
-            role_s = static_cast<int>(__hip_atomic_fetch_add(pa.ready + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        __syncthreads();
-        role = role_s;
-    }
-    if (role < nd) {
-        dict_index_block<kPageWaves>(a.bytes, pa.d.dicts, role, pa.d.entries, pa.d.dict_count, pa.d.dict_err,
-                                     pa.d.err_any, pa.dyn_bytes, dyn);
-        // publish (MI355X_MICROARCH.md, cross-workgroup hand-off): every
-        // storing wave's vmcnt(0), a workgroup barrier, one lane's agent
-        // release, its vmcnt(0), then the counter
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(pa.ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
-    uint16_t* lens = reinterpret_cast<uint16_t*>(dyn);
-    const int wv = static_cast<int>(threadIdx.x / kWave);
-    PageLds& L = reinterpret_cast<PageLds*>(reinterpret_cast<uint8_t*>(dyn) + pa.lens_bytes)[wv];
-    const int p_lo = a.p_lo, p_hi = a.p_hi;
-    const int nw = (static_cast<int>(gridDim.x) - nd) * kPageWaves;
-    int p = p_lo + (role - nd) * kPageWaves + wv;
-    uint32_t dict_n = 0, ebase = 0;
-    bool lean = false, first = true;
-    for (;;) {
-        const bool mine = p < p_hi;
-        PgState S{};
-        if (mine) S = page_runs(a, L, p);
-        if (first) {
-            // the dictionary: wait for its workgroups (one relaxed poll loop,
-            // one agent acquire, a barrier), then its entry lengths -> LDS
-            first = false;
-            if (nd > 0 && wv == 0) {
-                // (bounded: ~4 s, then the decode fails instead of hanging the GPU)
-                uint32_t it = 0;
-                while (__hip_atomic_load(pa.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < static_cast<uint32_t>(nd) &&
-                       it < (1u << 23)) {
-                    __builtin_amdgcn_s_sleep(8);
-                    it++;
-                }
-                if (it == (1u << 23) && lane() == 0) atomicOr(a.err_any, 1);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-            dict_n = static_cast<uint32_t>(a.dict_count[a.dict_id]);
-            ebase = static_cast<uint32_t>(a.dicts[a.dict_id].entry_base);
-            lean = dict_n <= pa.lt_n;
-            copy_map(lens, a.entries + ebase, min(dict_n, pa.lt_n), threadIdx.x, blockDim.x,
-                     [](uint64_t e) { return static_cast<uint16_t>(e >> 32); });
-            __syncthreads();
-        }
-        if (!mine) break;
-        if (probe(a.debug, 0xF << 19)) {  // timing: phase A (bit 19) or a part of it only (no characters filed)
-            for (uint32_t r0 = 0, ti = 0; r0 < S.n; r0 += kTileRows, ti++)
-                if (lane() == 0) a.tile_chars[a.page_tile0[p] + static_cast<int>(ti)] = 0;
-            p += nw;
-            continue;
-        }
-        if (S.ex || !lean) exact_page_body(a, L.u.code, p, dict_n, ebase);
-        else page_codes(a, L, lens, p, S, dict_n);
-        __builtin_amdgcn_wave_barrier();
-        p += nw;
     }
 }
 
@@ -1417,7 +950,6 @@ struct WriteArgs {
     uint8_t* page_flags;
     const uint32_t* codes32 = nullptr;  // wide chunks (k_pipe_wwide)
     const uint4* pad16 = nullptr;       // wide chunks: 16-byte entry slots (k_pipe_wwide<true>), or null
-    uint32_t wg0 = 0;                   // the launch's first workgroup of the decode's writer grid (segments)
 };
 
 
@@ -1619,12 +1151,11 @@ __global__ void __launch_bounds__(kWriteMax * 64) k_pipe_write(WriteArgs a) {
     // summed by k_pipe_codes), then this workgroup's earlier tiles.  Both
     // sums load together with the dictionary (one wait, one barrier).
     unsigned long long acc = 0, in = 0;
-    const uint32_t wg = a.wg0 + blockIdx.x;  // workgroup of the decode's writer grid
-    const int tfirst = min(a.ntiles, static_cast<int>(wg * a.wpw) * per);
-    const int ta = min(a.ntiles, static_cast<int>(wg * a.wpw + wv) * per);
+    const int ta = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw + wv) * per);
     const int tb = min(a.ntiles, ta + per);
     {
-        for (uint32_t b = threadIdx.x; b < wg; b += blockDim.x) acc += a.bsum[b];
+        for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) acc += a.bsum[b];
+        const int tfirst = min(a.ntiles, static_cast<int>(blockIdx.x * a.wpw) * per);
         for (int q = tfirst + static_cast<int>(lane()); q < ta; q += kWave) in += static_cast<unsigned long long>(a.tile_chars[q]);
     }
     {
@@ -2884,15 +2415,13 @@ PipePlan plan_pipe_lds(uint32_t dict_bytes, int wpw) {
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist,
                       int debug, const RunDicts* dicts, uint32_t stage_max, uint32_t slot_max, uint32_t dict_max,
-                      int cus, int page0) {
+                      int cus) {
     (void)flist;  // flist[0] is cleared by the caller (capi.hip: one memset of flags, bsum, flist[0])
     const int nd = dicts ? dicts->ndicts : 0;
-    page0 = max(0, min(page0, npages));
-    if (npages - page0 <= 0 && nd <= 0) return;
-    const int np = npages - page0;  // pages of this launch
+    if (npages <= 0 && nd <= 0) return;
     int ppw = pages_per_wave > 0 && pages_per_wave <= kRunPages ? pages_per_wave : kRunPages;
     if (pages_per_wave == 0) {  // auto: about two waves per SIMD over the chip, 4 .. 32 pages each
-        const int target = max(1, np / max(1, cus * 4 * 2));
+        const int target = max(1, npages / max(1, cus * 4 * 2));
         ppw = 4;
         while (ppw * 2 <= min(target, kRunPages)) ppw *= 2;
     }
@@ -2912,16 +2441,16 @@ void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages,
     }
     const uint32_t lds = kRunWaves * (wstage / 4 + 8) * 4;
     ensure_dyn_lds(reinterpret_cast<const void*>(k_pipe_runs), lds);
-    hipLaunchKernelGGL(k_pipe_runs, dim3(nd + (max(np, 0) + per - 1) / per), dim3(kRunWaves * kWave), lds, s,
+    hipLaunchKernelGGL(k_pipe_runs, dim3(nd + (max(npages, 0) + per - 1) / per), dim3(kRunWaves * kWave), lds, s,
                        bytes, pages, npages, max_def, max_rep, runs, info, ppw, flist,
-                       stage_max ? min(stage_max, kStage3 - 16) : kStage3 - 16, d, debug, wstage, page0);
+                       stage_max ? min(stage_max, kStage3 - 16) : kStage3 - 16, d, debug, wstage);
 }
 
 // k_pipe_write's grid and tiles per wavefront (k_pipe_codes files each tile's
 // characters under the workgroup that will write it).
 static void write_shape(const PipeLaunch& P, int* grid, int* per) {
     const int need = (P.ntiles + P.write_waves - 1) / P.write_waves;
-    *grid = max(1, min(need, P.wg_total > 0 ? P.wg_total : P.grid));
+    *grid = max(1, min(need, P.grid));
     const int nw = *grid * P.write_waves;
     *per = max(1, (P.ntiles + nw - 1) / nw);
 }
@@ -2933,7 +2462,6 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
                P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
                P.bsum, per, P.debug, P.write_waves};
-    a.t_lo = P.t_lo; a.t_hi = P.t_hi; a.p_lo = P.p_lo; a.p_hi = P.p_hi;
     if (count_pass) {
         const dim3 grid((P.ntiles + kCodeWaves - 1) / kCodeWaves);
         hipLaunchKernelGGL(k_pipe_codes<true>, grid, dim3(kCodeWaves * kWave), 0, s, a);
@@ -2946,44 +2474,12 @@ void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass) {
     // resident workgroups per CU (LDS and registers), so the grid is one wave of blocks
     const int waves = kCodeWaves3;
     const int bpc = max(1, resident_blocks(fn, waves * kWave, lds));
-    const int nt = P.t_hi >= 0 ? P.t_hi - P.t_lo : P.ntiles;
-    if (nt <= 0) return;
-    const int need = (nt + waves - 1) / waves;
+    const int need = (P.ntiles + waves - 1) / waves;
     const int grid = max(1, min(need, P.cus * bpc));
     // also decodes the pages the run-table passes marked (flist)
     // (only k_pipe_big pages: nothing to do, k_pipe_big decoded its own
     // fallback pages exactly)
     if (P.has_small) hipLaunchKernelGGL(k_pipe_codes3, dim3(grid), dim3(kCodeWaves3 * kWave), lds, s, a, lt_n, P.flist);
-}
-
-uint32_t pipe_page_stage() { return kPgStage; }
-
-void launch_pipe_page(hipStream_t s, const PipeLaunch& P, const RunDicts* dicts, uint32_t* ready, uint32_t dict_max) {
-    const int nd = dicts ? dicts->ndicts : 0;
-    const int p_lo = P.p_hi >= 0 ? P.p_lo : 0, p_hi = P.p_hi >= 0 ? P.p_hi : P.npages;
-    const int np = max(0, p_hi - p_lo);
-    if (np == 0 && nd == 0) return;
-    int wgrid = 0, per = 0;
-    write_shape(P, &wgrid, &per);  // tile characters are filed under k_pipe_write's workgroups
-    CodeArgs a{P.bytes, P.pages, P.tiles, P.ntiles, P.page_tile0, P.max_def, P.max_rep, P.dicts, P.dict_id,
-               P.entries, P.dict_count, P.runs, P.info, P.tile_nn, P.codes, P.tile_chars, P.page_err, P.err_any,
-               P.bsum, per, P.debug, P.write_waves};
-    a.p_lo = p_lo;
-    a.p_hi = p_hi;
-    const uint32_t lt_n = P.dict_entries_cap;
-    const uint32_t lens_bytes = (lt_n * 2 + 15) / 16 * 16;
-    uint32_t dyn = lens_bytes + static_cast<uint32_t>(kPageWaves * sizeof(PageLds));
-    if (nd) dyn = max(dyn, (dict_max + 32 + 15) / 16 * 16);  // dict_index_block stages its page there
-    const void* fn = reinterpret_cast<const void*>(k_pipe_page);
-    ensure_dyn_lds(fn, dyn);
-    const int bpc = max(1, resident_blocks(fn, kPageWaves * kWave, dyn));
-    const int need = (np + kPageWaves - 1) / kPageWaves;
-    const int pages_wg = np ? max(1, min(need, P.cus * bpc - nd)) : 0;
-    const PageArgs pa{dicts ? RunDictArgs{dicts->dicts, nd, dicts->entries, dicts->dict_count, dicts->dict_err,
-                                          dicts->err_any}
-                            : RunDictArgs{nullptr, 0, nullptr, nullptr, nullptr, nullptr},
-                      ready, lens_bytes, lt_n, dyn};
-    hipLaunchKernelGGL(k_pipe_page, dim3(nd + pages_wg), dim3(kPageWaves * kWave), dyn, s, a, pa);
 }
 
 PipePlan plan_pipe_wide(int wpw, bool pad) {
@@ -3026,11 +2522,6 @@ void launch_pipe_write(hipStream_t s, const PipeLaunch& P) {
                 P.tile_chars, P.bsum, per, P.nrows_total, P.total, P.capacity, P.overflow, P.validity, P.offsets,
                 P.chars, P.dict_chars_bytes, P.dict_bytes, P.debug, P.write_waves, P.znext, P.znext_words,
                 P.match, P.match_neg, P.page_flags};
-    if (P.wgn > 0) {  // one segment: workgroups [wg0, wg0 + wgn) of the grid
-        a.wg0 = static_cast<uint32_t>(P.wg0);
-        grid = min(P.wgn, grid - P.wg0);
-        if (grid <= 0) return;
-    }
     if (P.match)
         hipLaunchKernelGGL(k_pipe_write<true>, dim3(grid), dim3(P.write_waves * kWave), P.lds, s, a);
     else

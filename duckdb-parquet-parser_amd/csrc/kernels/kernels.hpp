@@ -193,13 +193,6 @@ struct PipeLaunch {
     // the same dictionary as 16-byte slots (launch_dict_big's pad16), or
     // null: k_pipe_wwide then reads entry words and characters
     const uint4* pad16 = nullptr;
-    // segmented decode (capi.hip pipe_segmented): the writer grid of the whole
-    // decode has wg_total workgroups (0: planned from grid); this launch's
-    // k_pipe_write runs workgroups [wg0, wg0 + wgn) (wgn 0: all), its
-    // k_pipe_codes3 tiles [t_lo, t_hi) and the marked pages [p_lo, p_hi)
-    // (t_hi < 0: all)
-    int wg_total = 0, wg0 = 0, wgn = 0;
-    int t_lo = 0, t_hi = -1, p_lo = 0, p_hi = -1;
 };
 constexpr uint32_t kArmDictBytes = 32768;  // every entry length < 2^15: the match bit rides in the entry word
 struct PipePlan {
@@ -225,16 +218,8 @@ constexpr uint32_t kRunDictMax = 60 * 1024;
 void launch_pipe_runs(hipStream_t s, const uint8_t* bytes, const DevPage* pages, int npages, int32_t max_def,
                       int32_t max_rep, uint2* runs, uint32_t* info, int pages_per_wave, int32_t* flist, int debug,
                       const RunDicts* dicts = nullptr, uint32_t stage_max = 0,  // 0: k_pipe_codes3's stage
-                      uint32_t slot_max = 0, uint32_t dict_max = 0, int cus = 256,  // pages_per_wave 0: auto
-                      int page0 = 0);  // pages [page0, npages)
+                      uint32_t slot_max = 0, uint32_t dict_max = 0, int cus = 256);  // pages_per_wave 0: auto
 void launch_pipe_codes(hipStream_t s, const PipeLaunch& P, bool count_pass);
-// k_pipe_page: run tables and codes of pages of <= kPipeSmallRows rows and
-// <= pipe_page_stage() payload bytes, one wavefront per page (replaces
-// k_pipe_runs + k_pipe_codes3).  dicts: the chunk's dictionary pages decode
-// in the launch (ready: two zeroed words of the per-decode block; dict_max:
-// their largest payload), else null (decoded before the launch).
-uint32_t pipe_page_stage();
-void launch_pipe_page(hipStream_t s, const PipeLaunch& P, const RunDicts* dicts, uint32_t* ready, uint32_t dict_max);
 struct DevBatch;
 void launch_pipe_write(hipStream_t s, const PipeLaunch& P);
 // The page walk on the GPU (walk.hip): one header record per page a

@@ -150,10 +150,6 @@ int pq_ctx_sync(pq_ctx* ctx);
  *   "big_all"     1: every page of a pipe chunk takes the large-page kernel
  *                 (k_pipe_big; coverage of that kernel on small pages), 0 (default)
  *   "pipe_run_pages" pages per wavefront of the run-table pass, 1..32 (32)
- *   "pipe_segs"   pipe decodes of small-page chunks in this many tile segments,
- *                 each segment's run/code passes overlapping the previous
- *                 segment's write pass on a second stream, 1..16 (4; 1: one pass)
- *   "pipe_seg_min_tiles" fewest tiles per segment (1024)
  *   "pipe_run_dict" 1 (default): dictionary pages up to 60 KiB decode in the
  *                 run-table launch (its leading workgroups), else in their own
  *                 launch on a side stream

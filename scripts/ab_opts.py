@@ -24,9 +24,8 @@ CONFIGS = {"C2": (gen.c2_cols, gen.REF_LAYOUT, 2), "C2a": (gen.c2_cols, gen.ARRO
 # library defaults of the options the variants may set (restored after each)
 DEFAULTS = {"pipe_run_pages": 32, "pipe_run_dict": 1, "regex_index": 1, "zflip": 1, "write_waves": 10, "dict_pipe": 1, "plain_ba": 1,
             "fused_ba": 1, "fixed_plain": 1, "fixed_fused": 0, "big_all": 0, "fused_debug": 0, "plain_fused": 1, "regex_win": 8192,
-            "raw_upload": 1, "write_bpc": 0, "wide_rows": 1, "gather_rows": 1, "levels_small": 1, "pipe_wide": 1,
-            "pipe_segs": 1, "pipe_seg_min_tiles": 1024, "pipe_page": 0}
-KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_page", "pipe_big", "wide_chars", "plain_spec", "pipe_count", "pipe_codes",
+            "raw_upload": 1, "write_bpc": 0, "wide_rows": 1, "gather_rows": 1, "levels_small": 1, "pipe_wide": 1}
+KERNELS = ("dict_index", "dict_entries", "pipe_runs", "pipe_big", "wide_chars", "plain_spec", "pipe_count", "pipe_codes",
            "pipe_write", "ba_fused", "ba_rows", "scan", "ba_gather", "fixed", "fixed_plain", "plain_ba", "plain_opt")
 
 cfg, _, colname = sys.argv[1].partition(":")

@@ -25,16 +25,14 @@ def ctx():
 
 
 # Kernel-path fixtures shared by the GPU parity tests.
-@pytest.fixture(params=["default", "page", "big", "fused", "generic", "serial"])
+@pytest.fixture(params=["default", "big", "fused", "generic", "serial"])
 def path(request, ctx):
     """Every kernel path that ships: "default" = what a chunk takes with the
     default options (dictionary BYTE_ARRAY on dict_pipe.hip: the run-table
     passes k_pipe_runs + k_pipe_codes3 + k_pipe_write; two-pass
     PLAIN BYTE_ARRAY, plain_ba.hip; tile-parallel PLAIN fixed width,
     fixed_fast.hip; the fused and generic kernels for chunks neither
-    takes); "page" is "default" with a wavefront per page (k_pipe_page:
-    speculative run-header parse and pointer jumps) instead of k_pipe_runs +
-    k_pipe_codes3 (option pipe_page); "big" puts every page of a dictionary chunk through k_pipe_big
+    takes); "big" puts every page of a dictionary chunk through k_pipe_big
     (the large-page kernel) so it also meets small pages; "fused" forces the
     per-page fused BYTE_ARRAY kernel (dict_fused.hip) onto every BYTE_ARRAY
     chunk it can take; "generic" forces decode.hip's rows/scan/gather and
@@ -44,9 +42,8 @@ def path(request, ctx):
     (k_plain_fused) under "default" and the two passes under "big"."""
     p = request.param
     ctx.set_option("big_all", int(p == "big"))
-    ctx.set_option("dict_pipe", int(p in ("default", "page", "big")))
-    ctx.set_option("pipe_page", int(p == "page"))
-    ctx.set_option("plain_ba", int(p in ("default", "page", "big")))
+    ctx.set_option("dict_pipe", int(p in ("default", "big")))
+    ctx.set_option("plain_ba", int(p in ("default", "big")))
     ctx.set_option("fused_ba", int(p not in ("generic", "serial")))
     ctx.set_option("fixed_plain", int(p not in ("generic", "serial")))
     ctx.set_option("wide_rows", int(p != "serial"))
@@ -57,7 +54,6 @@ def path(request, ctx):
     yield p
     for k in ("dict_pipe", "plain_ba", "fused_ba", "fixed_plain", "plain_fused"):
         ctx.set_option(k, 1)
-    ctx.set_option("pipe_page", 0)
     ctx.set_option("fixed_fused", 0)
     ctx.set_option("big_all", 0)
     ctx.set_option("wide_rows", 1)
