@@ -122,6 +122,7 @@ struct pq_ctx {
     bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
     bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
     bool opt_plain_fused = true; // "plain_fused": their one-pass form when the pages' character counts are known
+    bool opt_codec_batch = true; // "codec_batch": SNAPPY / LZ4 short commands executed in batches (codec.hip lz_run)
     bool opt_zflip = true;       // "zflip": per-decode flags from the block the previous k_pipe_write cleared (else a fill)
     int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
     bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
@@ -909,6 +910,7 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
         return 0;
     }
     if (std::strcmp(key, "zflip") == 0) { ctx->opt_zflip = value != 0; return 0; }
+    if (std::strcmp(key, "codec_batch") == 0) { ctx->opt_codec_batch = value != 0; return 0; }
     if (std::strcmp(key, "write_waves") == 0) {
         if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "write_waves: 1..16");
         ctx->opt_write_waves = static_cast<int>(value);
@@ -1376,6 +1378,7 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             e.flags = v2 ? (pqk::kCodecV2 | (desc.max_def_level > 0 ? pqk::kCodecDefPrefix : 0u) |
                             (desc.max_rep_level > 0 ? pqk::kCodecRepPrefix : 0u))
                          : 0u;
+            if (!ctx->opt_codec_batch) e.flags |= pqk::kCodecSerial;
             cents.push_back(e);
             cent_file.push_back(p.payload_offset);
             *out_len = static_cast<int32_t>(n);

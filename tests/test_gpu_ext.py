@@ -155,3 +155,44 @@ def test_ext_pages_both_layouts(ctx, tmp_path, codec, version, page):
         got = capi.canonical_dump(decode(ctx, f, ci))
         assert sha(got) == sha(canonical_dump(back.column(c))), c
     assert sizes == {False, True}  # both layouts ran
+
+
+@pytest.mark.skipif(pa is None, reason="pyarrow not importable")
+@pytest.mark.parametrize("codec", ["snappy", "lz4"])
+@pytest.mark.parametrize("batch", [1, 0], ids=["batched", "serial"])
+@pytest.mark.parametrize("page", [3000, 1 << 20])
+def test_ext_lz_command_shapes(ctx, tmp_path, codec, batch, page):
+    """Streams whose commands stress the batched executor (codec.hip lz_run):
+    distance-1 and distance-3 runs (references inside one batch, resolved by
+    pointer jumping), incompressible bytes (long literals), text (short
+    commands that fill batches), runs of exactly 64 and 65 bytes; both the
+    batched and the one-command-per-step execution equal pyarrow."""
+    rng = np.random.default_rng(17)
+    vals = []
+    for i in range(6000):
+        k = i % 6
+        if k == 0:
+            vals.append("a" * int(rng.integers(1, 300)))
+        elif k == 1:
+            vals.append("xyz" * int(rng.integers(1, 100)))
+        elif k == 2:
+            vals.append(bytes(rng.integers(32, 127, int(rng.integers(1, 500)), dtype=np.uint8)).decode())
+        elif k == 3:
+            vals.append("the quick brown fox " * int(rng.integers(1, 6)))
+        elif k == 4:
+            vals.append("b" * (64 if i % 12 == 4 else 65))
+        else:
+            vals.append(str(int(rng.integers(0, 10**9))))
+    t = pa.table({"s": pa.array(vals, pa.string())})
+    path = tmp_path / f"lz_{codec}_{page}.parquet"
+    pq.write_table(t, path, compression=codec.upper() if codec != "lz4" else "LZ4", use_dictionary=False,
+                   data_page_size=page)
+    f = path.read_bytes()
+    ctx.set_option("codec_batch", batch)
+    try:
+        got = capi.canonical_dump(decode(ctx, f, 0))
+    finally:
+        ctx.set_option("codec_batch", 1)
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden", "ext"))
+    from make_ext import canonical_dump
+    assert sha(got) == sha(canonical_dump(pq.read_table(path).column("s")))
