@@ -190,16 +190,32 @@ class Job:
 
 
 def kernel_source_hash() -> str:
-    """sha256 over the HIP sources (what a PMC summary must have been taken on
-    for its traffic figure to apply to this run)."""
+    """sha256 over the sources of the C2 pipe kernels a PMC summary measures
+    (dict_pipe.hip and every header it includes, recursively): the summary's
+    traffic figure applies to a run only when these are unchanged."""
+    import re
     h = hashlib.sha256()
     base = os.path.join(PKG, "csrc")
-    for d, _, fs in sorted(os.walk(base)):
-        for f in sorted(fs):
-            if f.endswith((".hip", ".hpp", ".cpp")):
-                with open(os.path.join(d, f), "rb") as fh:
-                    h.update(f.encode())
+    seen, todo = set(), ["kernels/dict_pipe.hip"]
+    while todo:
+        rel = todo.pop()
+        if rel in seen:
+            continue
+        seen.add(rel)
+        path = os.path.join(base, rel) if os.path.exists(os.path.join(base, rel)) else os.path.join(ROOT, "include", rel)
+        if not os.path.exists(path):
+            continue
+        with open(path, "rb") as fh:
+            src = fh.read()
+        for inc in re.findall(rb'#include "([^"]+)"', src):
+            todo.append(inc.decode())
+    for rel in sorted(seen):
+        for path in (os.path.join(base, rel), os.path.join(ROOT, "include", rel)):
+            if os.path.exists(path):
+                with open(path, "rb") as fh:
+                    h.update(rel.encode())
                     h.update(fh.read())
+                break
     return h.hexdigest()[:16]
 
 

@@ -17,6 +17,7 @@ rc=$?; tail -15 "$OUT/pytest_gpu.log"
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "PYTEST rc=$rc"; exit $rc; }
 timeout -k 10 600 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; tail -c 400 "$OUT/bench.json"; [ $rc -eq 0 ] || { echo "BENCH rc=$rc"; tail -20 "$OUT/bench.err"; exit $rc; }
+cp gpurun_out/bench_full.json "$OUT/bench_full.json"  # (the profiled runs below overwrite it)
 HEAD_ARGS="--no-cpu --no-c4 --no-c5 --no-ext --no-wide"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/prof_kt" -o kt --output-format csv -- \
     python3 bench.py --steps 10 --warmup 2 $HEAD_ARGS "$@" > "$OUT/prof_kt.log" 2>&1
