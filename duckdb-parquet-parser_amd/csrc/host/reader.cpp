@@ -210,21 +210,19 @@ double ms_since(std::chrono::steady_clock::time_point& t) {
 
 ToValuesPhases last_to_values_phases() { return g_tv_phases; }
 
-std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned threads) {
-    ToValuesPhases& P = g_tv_phases;
-    P = ToValuesPhases{};
-    auto tp = std::chrono::steady_clock::now();
-    a = std::max<int64_t>(a, 0);
-    b = std::min<int64_t>(b, h.num_rows);
-    const int64_t n = std::max<int64_t>(b - a, 0);
+namespace {
+unsigned value_threads(unsigned threads, int64_t n) {
     unsigned t = threads ? threads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     // (below ~64k rows a thread costs more than it saves)
-    t = static_cast<unsigned>(std::min<int64_t>(t, std::max<int64_t>(1, n / 65536)));
-    // the storage's pages are faulted in by the threads first: the vector's
-    // default construction then runs over mapped memory instead of taking
-    // every page fault on this thread
-    P.threads = t;
-    std::vector<Value> out;
+    return static_cast<unsigned>(std::min<int64_t>(t, std::max<int64_t>(1, n / 65536)));
+}
+
+// `out` sized to n rows: the storage reserved, its pages faulted in by the
+// workers (the default construction then runs over mapped memory instead of
+// taking every page fault on this thread), then default-constructed.
+void prepare_values(std::vector<Value>& out, int64_t n, unsigned t, ToValuesPhases& P) {
+    auto tp = std::chrono::steady_clock::now();
+    out.clear();
     out.reserve(static_cast<size_t>(n));
     P.reserve_ms = ms_since(tp);
     if (t > 1) {
@@ -240,21 +238,54 @@ std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned
     P.fault_ms = ms_since(tp);
     out.resize(static_cast<size_t>(n));
     P.resize_ms = ms_since(tp);
+}
+
+// Rows [a, a + out.size()) of h into the default-constructed `out`, each
+// Value built in place (the string constructed inside the variant: no
+// temporary, no moves), on t threads over contiguous ranges.
+void fill_values(const HostColumn& h, int64_t a, std::vector<Value>& out, unsigned t, ToValuesPhases& P) {
+    auto tp = std::chrono::steady_clock::now();
+    const int64_t n = static_cast<int64_t>(out.size());
+    const bool ba = h.type == ParquetType::BYTE_ARRAY;
     auto part = [&](unsigned k) {
         const int64_t r0 = n * k / t, r1 = n * (k + 1) / t;
-        for (int64_t r = r0; r < r1; r++) out[static_cast<size_t>(r)] = h.value(a + r);
+        if (ba) {
+            const char* chars = reinterpret_cast<const char*>(h.values.data());
+            for (int64_t r = r0; r < r1; r++) {
+                const int64_t i = a + r;
+                Value& v = out[static_cast<size_t>(r)];
+                if (!h.valid(i)) continue;  // (default: NULL)
+                v.is_null = false;
+                v.data.template emplace<std::string>(chars + h.offsets[i], static_cast<size_t>(h.offsets[i + 1] - h.offsets[i]));
+            }
+        } else {
+            for (int64_t r = r0; r < r1; r++) out[static_cast<size_t>(r)] = h.value(a + r);
+        }
     };
     if (t <= 1) {
         part(0);
-        P.fill_ms = ms_since(tp);
-        return out;
+    } else {
+        std::vector<std::thread> th;
+        th.reserve(t - 1);
+        for (unsigned k = 1; k < t; k++) th.emplace_back(part, k);
+        part(0);
+        for (auto& x : th) x.join();
     }
-    std::vector<std::thread> th;
-    th.reserve(t - 1);
-    for (unsigned k = 1; k < t; k++) th.emplace_back(part, k);
-    part(0);
-    for (auto& x : th) x.join();
     P.fill_ms = ms_since(tp);
+}
+}  // namespace
+
+std::vector<Value> to_values(const HostColumn& h, int64_t a, int64_t b, unsigned threads) {
+    ToValuesPhases& P = g_tv_phases;
+    P = ToValuesPhases{};
+    a = std::max<int64_t>(a, 0);
+    b = std::min<int64_t>(b, h.num_rows);
+    const int64_t n = std::max<int64_t>(b - a, 0);
+    const unsigned t = value_threads(threads, n);
+    P.threads = t;
+    std::vector<Value> out;
+    prepare_values(out, n, t, P);
+    fill_values(h, a, out, t, P);
     return out;
 }
 
@@ -337,7 +368,33 @@ HostColumn ColumnReader::read_columnar() {
     return decode_chunks(dev_, image.data(), image.size(), {d}, nullptr);
 }
 
-std::vector<Value> ColumnReader::read_all() { return to_values(read_columnar()); }
+// The Value vector is sized (allocated, faulted in, default-constructed) on a
+// host thread while the chunk uploads and decodes on the GPU; the decoded
+// column then fills it in place (to_values' phases, overlapped).
+std::vector<Value> ColumnReader::read_all() {
+    ToValuesPhases& P = g_tv_phases;
+    P = ToValuesPhases{};
+    const int64_t guess = std::max<int64_t>(meta_->num_values, 0);  // a flat column's rows
+    const unsigned t = value_threads(0, guess);
+    std::vector<Value> out;
+    ToValuesPhases prep{};
+    std::thread pre([&] { prepare_values(out, guess, t, prep); });
+    HostColumn h;
+    try {
+        h = read_columnar();
+    } catch (...) {
+        pre.join();
+        throw;
+    }
+    pre.join();
+    P.reserve_ms = prep.reserve_ms;
+    P.fault_ms = prep.fault_ms;
+    P.resize_ms = prep.resize_ms;
+    P.threads = value_threads(0, h.num_rows);
+    if (static_cast<int64_t>(out.size()) != h.num_rows) out.resize(static_cast<size_t>(std::max<int64_t>(h.num_rows, 0)));
+    fill_values(h, 0, out, P.threads, P);
+    return out;
+}
 
 std::vector<PageResult> ColumnReader::read_pages() {
     int64_t start = meta_->data_page_offset;
