@@ -421,11 +421,38 @@ __device__ __forceinline__ void lz_batch(InX& I, OutT& O, lds8* bx, uint32_t K, 
     if (O.op - O.fl >= kFlush) O.flush(false);
 }
 
+// The command parser's input bytes in registers: 256 bytes from `base`, 4
+// per lane, read with v_readlane (a few cycles) instead of an LDS round trip
+// per header byte; bytes past its reach fall back to the staged window.
+template <class InX>
+struct RegWin {
+    InX* I;
+    uint32_t base = 0, lim = 0, w = 0;
+    __device__ __forceinline__ void load(uint32_t p) {
+        base = p & ~3u;
+        const uint32_t q = base + 4 * lane();
+        w = I->byte(q) | (I->byte(q + 1) << 8) | (I->byte(q + 2) << 16) | (I->byte(q + 3) << 24);
+        // valid up to the staged window's end
+        lim = min(base + 4 * static_cast<uint32_t>(kWave), I->wlo + InX::kWindow - I->sh);
+    }
+    __device__ __forceinline__ bool covers(uint32_t p, uint32_t k) const { return p >= base && p + k <= lim; }
+    __device__ __forceinline__ uint32_t byte(uint32_t q) const {
+        if (!covers(q, 1)) return I->byte(q);
+        const uint32_t o = q - base;
+        return (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w), static_cast<int>(o >> 2))) >>
+                (8 * (o & 3u))) & 0xFFu;
+    }
+    __device__ __forceinline__ uint32_t u16le(uint32_t q) const { return byte(q) | (byte(q + 1) << 8); }
+    __device__ __forceinline__ uint32_t u32le(uint32_t q) const {
+        return byte(q) | (byte(q + 1) << 8) | (byte(q + 2) << 16) | (byte(q + 3) << 24);
+    }
+};
+
 // next(p, cmd): parses the command at input position p (the window holds
 // [p, p + 80) when next is called) and advances p: 1 a command, 0 the end of
 // the stream or an error (O.st set), 2 the window must move first (p kept).
 template <class InX, class OutT, class Next>
-__device__ __forceinline__ void lz_run(InX& I, OutT& O, lds8* bx, uint32_t& p, uint32_t end, Next&& next) {
+__device__ __forceinline__ void lz_run(InX& I, OutT& O, lds8* bx, uint32_t& p, uint32_t end, RegWin<InX>& R, Next&& next) {
     LzCmd cmd{};
     bool have = false, done = false, slide = false;
     while (O.st == ST_OK) {
@@ -437,7 +464,9 @@ __device__ __forceinline__ void lz_run(InX& I, OutT& O, lds8* bx, uint32_t& p, u
                     if (K) break;  // the batch's literals must stay in the window
                     I.refill(p);
                     slide = false;
+                    R.load(p);
                 }
+                if (!R.covers(p, 16)) R.load(p);
                 const int r = next(p, cmd);
                 if (r == 2) {
                     slide = true;
@@ -538,15 +567,17 @@ __device__ __forceinline__ void snappy_b(InX& I, OutT& O, lds8* bx, uint32_t p, 
         if (!(b & 0x80u)) break;
     }
     if (ulen != expect) { O.st = ST_SIZE; return; }
-    lz_run(I, O, bx, p, end, [&](uint32_t& q, LzCmd& c) -> int {
-        const uint32_t t = uni(I.byte(q));
+    RegWin<InX> R{&I};
+    R.load(p);
+    lz_run(I, O, bx, p, end, R, [&](uint32_t& q, LzCmd& c) -> int {
+        const uint32_t t = uni(R.byte(q));
         const uint32_t ty = t & 3u;
         if (ty == 0) {
             uint32_t n = (t >> 2) + 1;
             q += 1;
             if (n > 60) {
                 const uint32_t nb = n - 60;
-                const uint32_t x = I.u32le(q);
+                const uint32_t x = R.u32le(q);
                 n = (nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u))) + 1;
                 q += nb;
             }
@@ -559,15 +590,15 @@ __device__ __forceinline__ void snappy_b(InX& I, OutT& O, lds8* bx, uint32_t p, 
         uint32_t n, d;
         if (ty == 1) {
             n = 4 + ((t >> 2) & 7u);
-            d = ((t >> 5) << 8) | I.byte(q + 1);
+            d = ((t >> 5) << 8) | R.byte(q + 1);
             q += 2;
         } else if (ty == 2) {
             n = (t >> 2) + 1;
-            d = I.u16le(q + 1);
+            d = R.u16le(q + 1);
             q += 3;
         } else {
             n = (t >> 2) + 1;
-            d = I.u32le(q + 1);
+            d = R.u32le(q + 1);
             q += 5;
         }
         if (q > end) { O.st = ST_CORRUPT; return 0; }
@@ -585,11 +616,14 @@ template <class InX, class OutT>
 __device__ __forceinline__ void lz4_block_b(InX& I, OutT& O, lds8* bx, uint32_t p, uint32_t end) {
     bool in_match = false, ended = false;
     uint32_t tok = 0;
+    if (!I.has(p, 80)) I.refill(p);
+    RegWin<InX> R{&I};
+    R.load(p);
     auto match = [&](uint32_t& q, LzCmd& c) -> int {
         if (q == end) { in_match = false; ended = true; return 0; }  // the last sequence holds literals only
         if (end - q < 2) { O.st = ST_CORRUPT; return 0; }
         const uint32_t qm = q;
-        const uint32_t d = uni(I.u16le(q));
+        const uint32_t d = uni(R.u16le(q));
         q += 2;
         uint32_t m = tok & 15u;
         if (m == 15) {
@@ -600,7 +634,7 @@ __device__ __forceinline__ void lz4_block_b(InX& I, OutT& O, lds8* bx, uint32_t 
                     q = qm;
                     return 2;
                 }
-                b = uni(I.byte(q++));
+                b = uni(R.byte(q++));
                 m += b;
             } while (b == 255);
         }
@@ -608,10 +642,10 @@ __device__ __forceinline__ void lz4_block_b(InX& I, OutT& O, lds8* bx, uint32_t 
         c = LzCmd{1u, m + 4, d};
         return 1;
     };
-    lz_run(I, O, bx, p, end, [&](uint32_t& q, LzCmd& c) -> int {
+    lz_run(I, O, bx, p, end, R, [&](uint32_t& q, LzCmd& c) -> int {
         if (in_match) return match(q, c);
         const uint32_t q0 = q;
-        tok = uni(I.byte(q++));
+        tok = uni(R.byte(q++));
         uint32_t n = tok >> 4;
         if (n == 15) {
             uint32_t b;
@@ -621,7 +655,7 @@ __device__ __forceinline__ void lz4_block_b(InX& I, OutT& O, lds8* bx, uint32_t 
                     q = q0;
                     return 2;
                 }
-                b = uni(I.byte(q++));
+                b = uni(R.byte(q++));
                 n += b;
             } while (b == 255);
         }
