@@ -5,286 +5,9 @@
 // bytes are uploaded to HBM once per chunk, and the decode is a short,
 // allocation-free sequence of launches on the context's stream.  No C++
 // exception crosses an extern "C" function.
-#include <hip/hip_runtime.h>
+#include "host/capi_state.hpp"
 
-#include <algorithm>
-#include <atomic>
-#include <chrono>
-#include <cstring>
-#include <thread>
-#include <map>
-#include <memory>
-#include <string>
-#include <vector>
-
-#include "host/format.hpp"
-#include "kernels/kernels.hpp"
-#include "pq_gpu.h"
-#include "regex/regex.hpp"
-#include "stage.hpp"
-
-using pqk::DevDict;
-using pqk::DevErr;
-using pqk::DevPage;
-using pqk::DevTile;
-
-// host tables filled by index from several threads: no zero fill on resize
-template <class T>
-using HVec = std::vector<T, pqfmt::NoInitAlloc<T>>;
-
-// ... and in pinned memory: the page and tile tables go to HBM by DMA
-// straight from where the plan wrote them (no staging copy)
-template <class T>
-struct PinnedAlloc : pqfmt::NoInitAlloc<T> {
-    using value_type = T;
-    template <class U>
-    struct rebind { using other = PinnedAlloc<U>; };
-    PinnedAlloc() = default;
-    template <class U>
-    PinnedAlloc(const PinnedAlloc<U>&) noexcept {}
-    T* allocate(size_t n) {
-        void* p = nullptr;
-        if (hipHostMalloc(&p, std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault) != hipSuccess) throw std::bad_alloc();
-        return static_cast<T*>(p);
-    }
-    void deallocate(T* p, size_t) noexcept { (void)hipHostFree(p); }
-};
-template <class A, class B>
-bool operator==(const PinnedAlloc<A>&, const PinnedAlloc<B>&) { return true; }
-template <class A, class B>
-bool operator!=(const PinnedAlloc<A>&, const PinnedAlloc<B>&) { return false; }
-template <class T>
-using PVec = std::vector<T, PinnedAlloc<T>>;
-
-struct PendingTimer {
-    std::string name;
-    hipEvent_t a, b;
-};
-
-struct pq_ctx {
-    int device = 0;
-    int cus = 256;                         // compute units (queried once: the property call costs ms)
-    hipStream_t stream = nullptr;
-    hipStream_t copy = nullptr;            // uploads (pinned staging), beside the decode stream
-    hipStream_t copy2 = nullptr;           // second DMA queue of the upload ring (option "stage_streams")
-    int opt_stage_streams = 2;
-    pqstage::Stager stager;
-    uint8_t* d_raw = nullptr;              // raw chunk bytes of the current upload (relayout source)
-    size_t raw_cap = 0;
-    bool opt_dev_walk = false;             // "device_walk": uploads walk pages on the GPU (walk.hip) over d_raw
-    uint8_t* d_walk = nullptr;             // the device walk's records, links and page table
-    size_t walk_cap = 0;
-    pq_page_desc* h_walk = nullptr;        // pinned: the page table back to the host
-    size_t h_walk_cap = 0;
-    pqk::RelayoutEntry* d_relay = nullptr; // relayout entries of the current upload
-    size_t relay_cap = 0;
-    pqk::CodecEntry* d_codec = nullptr;    // compressed / V2 pages of the current upload (codec.hip)
-    size_t codec_cap = 0;
-    uint32_t* d_codec_st = nullptr;        // their status words
-    uint8_t* d_zsrc = nullptr;             // their payloads, when not in d_raw
-    size_t zsrc_cap = 0;
-    uint8_t* d_chunker = nullptr;          // pq_chunk_assign scratch and (no caller buffer) output
-    size_t chunker_cap = 0;
-    bool opt_raw = true;                   // "raw_upload": DMA raw chunk bytes during the walk, relayout on the GPU
-    hipStream_t side = nullptr;            // dictionary decode beside the run-table pass
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    std::string err;
-    bool timing = false;
-    std::vector<PendingTimer> pending;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events;
-    std::map<std::string, std::pair<double, int64_t>> timers;
-    // upload scratch (upload_walked): per-page host tables, reused
-    PVec<pqk::DevPage> s_hpages;
-    HVec<std::pair<int64_t, int64_t>> s_copies;
-    HVec<int32_t> s_copy_size;
-    PVec<int32_t> s_tile0;
-    PVec<pqk::DevTile> s_htiles;
-    PVec<pqk::RelayoutEntry> s_ents;
-    bool opt_fused = true;  // pq_ctx_set_option("fused_ba", 0) forces the generic path
-    bool opt_pipe_wide = true;   // "pipe_wide": dictionaries beyond the writer's LDS / 65,535 entries on the pipe (k_pipe_wwide)
-    bool opt_wide_rows = true;  // "wide_rows": generic BYTE_ARRAY rows by a workgroup per page (k_wide_rows)
-    bool opt_levels_small = true;  // "levels_small": k_fixed_levels2 in its 35 KB LDS form (4 workgroups per CU)
-    bool opt_gather_rows = true;  // "gather_rows": k_ba_gather copies characters row per lane (0: byte-wise blocks)
-    int opt_debug = 0;      // "fused_debug": ablation switches for timing studies
-    int opt_waves = 0;      // "fused_waves": waves per workgroup override (0 = auto)
-    uint64_t* d_prof = nullptr;  // "fused_prof": per-phase cycle sums of k_ba_fused
-    int opt_claim = 1;           // "fused_claim": pages claimed per ticket by k_ba_fused producers (>1 serialises the look-back; diagnostics)
-    bool opt_regex_dfa = true;   // "regex_dfa": DFA kernels (else the NFA kernel)
-    bool opt_regex_plain = true; // "regex_plain": windowed kernel for chunks without dictionary pages
-    bool opt_regex_codes = true; // "regex_codes": dictionary chunks on the pipe path: match bits over the decode's codes
-    bool opt_regex_reuse = true; // "regex_reuse": ... reusing the codes of an earlier checked decode of the chunk
-    int opt_regex_index = 1;     // "regex_index": REQUIRED PLAIN chunks keep the string index of their first scan;
-                                 // 2: every scan is a first scan (files the index again: the cold-scan timing)
-    int opt_regex_win = 8192;    // "regex_win": window bytes of the windowed kernel
-    int opt_regex_debug = 0;     // "regex_debug": timing ablation of the windowed kernel (output invalid)
-    bool opt_fixed_plain = true; // "fixed_plain": tile-parallel PLAIN fixed-width kernels (fixed_fast.hip)
-    bool opt_fixed_fused = false; // "fixed_fused": OPTIONAL ones scatter their values in the levels launch (slower: DESIGN §5)
-    bool opt_pipe = true;        // "dict_pipe": three-pass dictionary BYTE_ARRAY kernels (dict_pipe.hip)
-    bool opt_plain = true;       // "plain_ba": two-pass PLAIN BYTE_ARRAY kernels for REQUIRED chunks (plain_ba.hip)
-    bool opt_plain_fused = true; // "plain_fused": their one-pass form when the pages' character counts are known
-    bool opt_codec_batch = true; // "codec_batch": SNAPPY / LZ4 short commands executed in batches (codec.hip lz_run)
-    bool opt_zflip = true;       // "zflip": per-decode flags from the block the previous k_pipe_write cleared (else a fill)
-    int opt_write_waves = 10;    // "write_waves": k_pipe_write writer waves per workgroup (1..16), set before upload
-    bool opt_big_all = false;    // "big_all": every page of a pipe chunk takes k_pipe_big (set before upload)
-    int opt_run_pages = 32;      // "pipe_run_pages": pages per wavefront of the run-table pass (1..32)
-    bool opt_run_dict = true;    // "pipe_run_dict": the dictionary decodes in k_pipe_runs' leading workgroups
-    int opt_write_bpc = 0;       // "write_bpc": cap on k_pipe_write workgroups per CU (0: as many as fit; set before upload)
-    int opt_stage_bufs = 6;      // "stage_bufs" / "stage_piece_kb": pinned upload ring (stage.hpp)
-};
-
-struct pq_chunk {
-    int32_t type = 0;
-    int16_t max_def = 0, max_rep = 0;
-    int32_t width = 0, plain_width = 0;
-    int64_t nrows = 0;
-    int64_t row_offset = 0;             // page-range uploads: global row of the first data page
-    int64_t payload_bytes = 0;
-    pqfmt::PageList walked;             // every walked page, all chunks, global rows
-    HVec<int64_t> page_seq;             // walk sequence of each device data page
-    std::vector<int64_t> dict_seq;      // walk sequence of each device dict page
-    int walk_error = 0;
-    std::string walk_message;
-    int64_t walk_error_seq = 0;
-    int first_error = 0;                // error detected at upload time
-    // device
-    uint8_t* d_bytes = nullptr;
-    size_t nbytes = 0;
-    DevPage* d_pages = nullptr;
-    int npages = 0;
-    DevDict* d_dicts = nullptr;
-    int ndicts = 0;
-    DevTile* d_tiles = nullptr;
-    int ntiles = 0;
-    int32_t* d_page_tile0 = nullptr;
-    uint64_t* d_entries = nullptr;
-    int64_t nentries = 0;
-    uint32_t max_dict_bytes = 0;        // largest dictionary payload
-    // dictionary pages too large for k_dict_index's LDS (launch_dict_big)
-    struct BigDict { int di; pqk::DevDict d; size_t scr_off, lens_off, pad_off; };
-    std::vector<BigDict> hbigd;
-    uint8_t* d_bigd = nullptr;          // their scratch
-    uint32_t max_page_bytes = 0;        // largest data-page payload
-    int32_t* d_dict_count = nullptr;
-    DevErr* d_page_err = nullptr;
-    DevErr* d_dict_err = nullptr;
-    int32_t* d_flags = nullptr;  // [0] err_any, [1] overflow
-    uint64_t* d_row_codes = nullptr;
-    int64_t* d_tile_chars = nullptr;
-    // three-pass dictionary BYTE_ARRAY decode (dict_pipe.hip)
-    bool pipe = false, pipe_count = false;
-    int32_t pipe_dict = -1;
-    uint32_t pipe_dict_chars_bytes = 0, pipe_dict_bytes = 0, pipe_lds = 0, pipe_ecap = 0;
-    int pipe_cus = 256;
-    int pipe_grid = 0;
-    uint2* d_runs = nullptr;
-    uint32_t* d_info = nullptr;
-    uint16_t* d_codes = nullptr;
-    // the per-row codes (and dictionary entry table) depend only on the
-    // chunk's bytes: once a pipe pass that wrote them was checked error-free
-    // (collect), regex scans read them instead of recomputing
-    bool codes_pending = false, codes_ok = false;
-    bool entries_pending = false, entries_ok = false;  // the same for the dictionary entry table
-    // pq_decode_regex_async: the decode about to launch also runs the page
-    // filter (k_regex_dict before k_pipe_write, match bits in the writer)
-    bool arm = false;
-    int arm_neg = 0;
-    // string index of a REQUIRED PLAIN chunk (u16 window offset per row),
-    // filed by the first error-free windowed scan, read by the later ones
-    uint16_t* d_rx_index = nullptr;
-    bool rx_index_ok = false, rx_index_pending = false;
-    uint32_t rx_index_win = 0;
-    uint32_t pipe_dict_payload = ~0u;  // payload bytes of the pipe's dictionary (arming bound)
-    int32_t* d_tile_nn = nullptr;
-    unsigned long long* d_bsum = nullptr;
-    int32_t* d_flist = nullptr;
-    bool pipe_small = false;            // some pages take k_pipe_runs (<= kPipeSmallRows rows)
-    uint32_t pipe_small_bytes = 0;      // the largest payload of those pages
-    bool pipe_wide = false;             // 32-bit codes, dictionary in HBM (k_pipe_big<true> -> k_pipe_wwide)
-    int pipe_wpw = 10;                  // k_pipe_write writer waves per workgroup (planned)
-    std::vector<int32_t> hbig;          // pages of more than kPipeSmallRows rows (k_pipe_big)
-    int32_t* d_bigp = nullptr;
-    uint32_t big_max_bytes = 0;
-    int32_t pipe_entry_base = 0;        // entry-table slot of the pipe dictionary's first entry
-    size_t z_bsum = 0, z_flist = 0;  // offsets in a zero block: bsum, flist
-    uint8_t* d_zero = nullptr;          // pipe chunks: two blocks of [flags][bsum][flist], alternating per decode
-    size_t zfull = 0;                   // bytes per block
-    int zsel = 0;                       // block of the current decode
-    bool next_zeroed = false;           // the other block is clear (the last k_pipe_write cleared it)
-    int32_t* d_dflag = nullptr;         // the side-stream dictionary decode's error flag (sticky, cleared at upload)
-    size_t zero_bytes = 4 * sizeof(int32_t);  // bytes of d_flags cleared per decode (flags, bsum, flist[0])
-    bool tiles_aligned32 = false;       // every tile starts on a 32-row boundary: k_pipe_write owns whole validity words
-    // PLAIN BYTE_ARRAY, REQUIRED (plain_ba.hip)
-    bool plain = false;
-    std::vector<pqk::DevBatch> hpwins;
-    pqk::DevBatch* d_pwins = nullptr;
-    std::vector<int64_t> hpwbase;      // k_plain_fused: first output byte per window (+ total), or empty
-    int64_t* d_pwbase = nullptr;
-    uint32_t* d_rowinfo = nullptr;
-    int64_t* d_wchars = nullptr;
-    unsigned long long* d_pbsum = nullptr;
-    int plain_grid = 0;
-    // pages larger than a window: speculative chunk chains (plain_ba.hip k_plain_spec)
-    bool plain_spec = false, spec_failed = false;
-    bool pfused_failed = false;          // k_plain_fused gave up on this chunk: two passes from now on
-    // OPTIONAL chunks on the PLAIN kernels (plain_ba.hip OptLaunch): levels,
-    // value-section pages, dense offsets spread over the rows
-    bool plain_opt = false, popt_failed = false;
-    bool opt_lane_levels = false;       // every page <= kOptLaneRows rows: lane-per-page levels
-    int32_t* d_page_nn = nullptr;
-    int64_t* d_onnv = nullptr;          // per page: non-null values | characters
-    int64_t* d_ochv = nullptr;
-    int64_t* d_opdense = nullptr;       // their exclusive scans
-    int64_t* d_opbase = nullptr;
-    int64_t* d_otot = nullptr;          // [0] non-null values, [1] characters
-    DevPage* d_vpages = nullptr;
-    int64_t* d_doffs = nullptr;         // dense offsets (nrows + 1)
-    DevErr* d_operr = nullptr;          // level / chain errors of this path (not reported: the general path re-runs)
-    std::vector<int32_t> hpwpage;       // spec windows: their real page
-    int32_t* d_pwpage = nullptr;
-    std::vector<int32_t> hchunk_base;
-    std::vector<uint2> hchunks;
-    int32_t* d_chunk_base = nullptr;
-    uint2* d_chunks = nullptr;
-    uint4* d_cand = nullptr;
-    DevPage* d_ppages = nullptr;
-    DevErr* d_perr = nullptr;
-    pq_column* last_out = nullptr;      // output of the last pq_decode_async (collect re-runs into it)
-    // tile-parallel PLAIN fixed-width decode (fixed_fast.hip)
-    bool fixed_plain = false;
-    int32_t* d_tile_rank = nullptr;
-    int32_t* d_page_pos = nullptr;
-    int64_t* d_tile_base = nullptr;
-    int64_t* d_total = nullptr;
-    int64_t* d_scan_scratch = nullptr;
-    int64_t char_estimate = 0;
-    // fused BYTE_ARRAY path (dict_fused.hip): one launch per input chunk
-    struct Range {
-        int32_t p0 = 0, np = 0, dict_id = -1;
-        uint32_t rows_cap = 0, stage_bytes = 0, wave_bytes = 0, dict_bytes = 0, dict_chars_bytes = 0;
-        int waves = 0, grid = 0;
-    };
-    std::vector<Range> ranges;
-    bool fused = false;
-    uint64_t* d_status = nullptr;
-    int32_t* d_tickets = nullptr;
-    int64_t* d_bases = nullptr;
-    // regex
-    uint8_t* d_page_flags = nullptr;
-    uint8_t* d_dict_match = nullptr;
-    uint8_t* d_dfa = nullptr;           // regex DFA image (regex.hpp DevDfa)
-    std::vector<pqk::DevBatch> hrwins;  // windowed PLAIN regex scan: page windows
-    pqk::DevBatch* d_rwins = nullptr;
-    int32_t* d_rwin_ticket = nullptr;
-    uint32_t rwin_bytes = 0, rwin_for_dfa = 0;
-    int rwin_grid = 0;
-    int rwin_opt = 0;                   // regex_win the windows were planned with
-    uint32_t dfa_bytes = 0;
-    bool dfa_full = false;               // the DFA image has full 256-column rows
-    bool dfa_sink = false;               // full rows of an anchored pattern (k_regex_plain<.., true>)
-    std::string prog_pattern;           // pattern of d_prog / d_dfa
-    int64_t dict_match_cap = 0;
-    pqre::DeviceProgram* d_prog = nullptr;
-};
+using namespace pqcapi;
 
 namespace {
 
@@ -303,18 +26,6 @@ void parallel_for(int n, Fn&& fn) {
             for (int i = next.fetch_add(1); i < n; i = next.fetch_add(1)) fn(i);
         });
     for (auto& x : th) x.join();
-}
-
-template <class T>
-int dalloc(T** p, size_t n) {
-    *p = nullptr;
-    if (n == 0) n = 1;
-    return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)) == hipSuccess ? 0 : PQ_ERR_HIP;
-}
-template <class T>
-void dfree(T*& p) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
 }
 
 int set_err(pq_ctx* ctx, int code, const std::string& m) {
@@ -475,302 +186,6 @@ void free_chunk_device(pq_chunk* c) {
     if (c->d_prog) { pqre::free_device_program(c->d_prog); c->d_prog = nullptr; }
 }
 
-// The three-pass dictionary path (dict_pipe.hip) takes a BYTE_ARRAY chunk
-// whose data pages all use one dictionary page that fits in LDS.
-// Dictionaries the writer's LDS cannot hold (or of more than 65,535 entries):
-// every page through k_pipe_big<true> (32-bit codes, index bit widths up to
-// 24, entry lengths from HBM), then k_pipe_wwide, which reads the entry words
-// and characters from HBM/L2.  Called by plan_pipe after its page checks
-// (dictionary-encoded pages of one dictionary).
-static void plan_pipe_wide(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const DevDict& d, int32_t dict_id) {
-    if (!ctx->opt_pipe_wide) return;
-    std::vector<int32_t> big;
-    uint32_t big_bytes = 0;
-    big.reserve(pages.size());
-    for (size_t i = 0; i < pages.size(); i++) {
-        const DevPage& pg = pages[i];
-        if (pg.nvals > pqk::kBigTiles * pqk::kTileRows || static_cast<uint32_t>(pg.size) > pqk::kBigMaxBytes) return;
-        big.push_back(static_cast<int32_t>(i));
-        big_bytes = std::max(big_bytes, static_cast<uint32_t>(pg.size));
-    }
-    if (pqk::pipe_big_lds(big_bytes, 0) > 160u * 1024) return;
-    // a dictionary page past k_dict_index's LDS decodes in launch_dict_big,
-    // which also files its 16-byte entry slots: the writer keeps one per row
-    // of its tile in LDS (10 KiB per wave: four waves per workgroup, three
-    // workgroups per CU; five per workgroup measured 82 vs 58 µs, r4e)
-    const bool pad = static_cast<uint64_t>(std::max(d.size, 0)) + 32 > pqk::kDictLdsCap;
-    const int wpw = std::max(1, std::min(pad ? 4 : 16, ctx->opt_write_waves));
-    pqk::PipePlan pl = pqk::plan_pipe_wide(wpw, pad);
-    if (pl.blocks_per_cu == 0) return;
-    if (ctx->opt_write_bpc > 0) pl.blocks_per_cu = std::min(pl.blocks_per_cu, ctx->opt_write_bpc);
-    c->pipe = true;
-    c->pipe_wide = true;
-    c->pipe_small = false;
-    c->pipe_small_bytes = 0;
-    c->pipe_count = false;
-    c->hbig = std::move(big);
-    c->big_max_bytes = big_bytes;
-    c->pipe_dict = dict_id;
-    c->pipe_dict_payload = static_cast<uint32_t>(d.size);
-    c->pipe_entry_base = d.entry_base;
-    c->pipe_dict_chars_bytes = 0;
-    c->pipe_dict_bytes = 0;
-    c->pipe_lds = pl.lds;
-    c->pipe_grid = ctx->cus * pl.blocks_per_cu;
-    c->pipe_ecap = static_cast<uint32_t>(std::min<int64_t>(d.nvals, d.size / 4 + 1));
-    c->pipe_cus = ctx->cus;
-    c->pipe_wpw = wpw;
-}
-
-void plan_pipe(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages, const std::vector<DevDict>& dicts) {
-    c->pipe = false;
-    c->pipe_wide = false;
-    c->pipe_count = false;
-    c->pipe_small = false;
-    c->hbig.clear();
-    c->big_max_bytes = 0;
-    if (c->type != PQ_BYTE_ARRAY || c->max_def > 254 || c->max_def < 0 || c->max_rep < 0 || pages.empty()) return;
-    int32_t dict_id = -1;
-    bool multi = false, small = false;
-    std::vector<int32_t> big;
-    uint32_t big_bytes = 0, small_bytes = 0;
-    for (size_t i = 0; i < pages.size(); i++) {
-        const DevPage& pg = pages[i];
-        if (pg.mode != pqk::MODE_DICT || pg.size > (1 << 27) || pg.size < 0) return;
-        if (pg.nvals > pqk::kPipeSmallRows || ctx->opt_big_all) {
-            // k_pipe_big: the page's jump table and up to kBigTiles tiles in one workgroup
-            if (pg.nvals > pqk::kBigTiles * pqk::kTileRows || static_cast<uint32_t>(pg.size) > pqk::kBigMaxBytes) return;
-            big.push_back(static_cast<int32_t>(i));
-            big_bytes = std::max(big_bytes, static_cast<uint32_t>(pg.size));
-        } else {
-            small = true;
-            multi |= pg.nvals > pqk::kTileRows;
-            small_bytes = std::max(small_bytes, static_cast<uint32_t>(pg.size));
-        }
-        if (dict_id >= 0 && pg.dict != dict_id) return;
-        dict_id = pg.dict;
-    }
-    const DevDict& d = dicts[dict_id];
-    if (d.size < 0 || d.nvals < 0) return;
-    if (d.size > 65536 - 64 || d.nvals > 65535) return plan_pipe_wide(ctx, c, pages, d, dict_id);
-    const int64_t ecap = std::min<int64_t>(d.nvals, d.size / 4 + 1);
-    if (!big.empty() && pqk::pipe_big_lds(big_bytes, std::min<uint32_t>(static_cast<uint32_t>(ecap), pqk::kBigLens)) > 160u * 1024)
-        return;
-    const uint32_t chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
-    const uint32_t dict_bytes = 16 + chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
-    const int wpw = std::max(1, std::min(16, ctx->opt_write_waves));
-    pqk::PipePlan pl = pqk::plan_pipe_lds(dict_bytes, wpw);
-    if (pl.blocks_per_cu == 0) return plan_pipe_wide(ctx, c, pages, d, dict_id);
-    if (ctx->opt_write_bpc > 0) pl.blocks_per_cu = std::min(pl.blocks_per_cu, ctx->opt_write_bpc);
-    const int cus = ctx->cus;
-    c->pipe = true;
-    c->pipe_small = small;
-    c->pipe_small_bytes = small_bytes;
-    c->pipe_count = multi && c->max_def > 0;
-    c->hbig = std::move(big);
-    c->big_max_bytes = big_bytes;
-    c->pipe_dict = dict_id;
-    c->pipe_dict_payload = static_cast<uint32_t>(d.size);
-    c->pipe_entry_base = d.entry_base;
-    c->pipe_dict_chars_bytes = chars_bytes;
-    c->pipe_dict_bytes = dict_bytes;
-    c->pipe_lds = pl.lds;
-    c->pipe_grid = cus * pl.blocks_per_cu;
-    c->pipe_ecap = static_cast<uint32_t>(ecap);
-    c->pipe_cus = cus;
-    c->pipe_wpw = wpw;
-}
-
-// PLAIN BYTE_ARRAY chunks without levels go through plain_ba.hip: windows of
-// consecutive page slots of at most kPWin bytes.
-void plan_plain(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages) {
-    c->plain = false;
-    c->plain_spec = false;
-    c->plain_opt = false;
-    c->hpwins.clear();
-    c->hpwbase.clear();
-    c->hpwpage.clear();
-    c->hchunk_base.clear();
-    c->hchunks.clear();
-    if (c->type != PQ_BYTE_ARRAY || c->max_def < 0 || c->max_rep != 0 || pages.empty()) return;
-    // OPTIONAL: the value sections (after the levels) are decoded as
-    // REQUIRED-shaped pages of their non-null values; the windows and chunks
-    // below cover the whole slots, which hold them
-    const bool opt = c->max_def > 0;
-    auto slot = [](const DevPage& p) {
-        return (static_cast<uint64_t>(std::max(p.size, 0)) + 15) / 16 * 16 + 16;
-    };
-    bool big = false;
-    for (const auto& pg : pages) {
-        if (pg.mode != pqk::MODE_PLAIN || pg.nvals < 0) return;
-        big |= slot(pg) > pqk::kPWin;
-    }
-    if (big) {
-        // every page in kPChunk-byte chunks, windows of kPChunkGroup chunks
-        // (the pseudo pages k_plain_link writes, one per chunk)
-        if (pages.size() > (1u << 24)) return;
-        int64_t nch = 0;
-        for (size_t p = 0; p < pages.size(); p++) {
-            const uint32_t size = static_cast<uint32_t>(std::max(pages[p].size, 0));
-            const uint32_t k = std::max<uint32_t>(1, (size + pqk::kPChunk - 1) / pqk::kPChunk);
-            c->hchunk_base.push_back(static_cast<int32_t>(nch));
-            for (uint32_t i = 0; i < k; i++) {
-                c->hchunks.push_back(make_uint2(static_cast<uint32_t>(p), i));
-            }
-            const uint64_t se = pages[p].off + slot(pages[p]);
-            for (uint32_t g = 0; g < k; g += pqk::kPChunkGroup) {
-                pqk::DevBatch b{};
-                b.p0 = static_cast<int32_t>(nch + g);
-                b.np = static_cast<int32_t>(std::min(pqk::kPChunkGroup, k - g));
-                b.img_lo = pages[p].off + static_cast<uint64_t>(g) * pqk::kPChunk;
-                b.img_bytes = static_cast<uint32_t>(std::min<uint64_t>(pqk::kPWin, se - b.img_lo));
-                c->hpwins.push_back(b);
-            }
-            nch += k;
-            if (nch > (1ll << 30)) return;
-        }
-        c->hchunk_base.push_back(static_cast<int32_t>(nch));
-        c->plain_spec = true;
-        for (const auto& b : c->hpwins) c->hpwpage.push_back(static_cast<int32_t>(c->hchunks[static_cast<size_t>(b.p0)].x));
-        // one-pass form over the pseudo pages (k_plain_fused, kWinPseudo): per
-        // window, its page's first output byte (pages whose strings fill them
-        // exactly: size - 4 * num_values each, verified on the device) minus
-        // the page's image offset plus 4 x its first row
-        bool known = true;
-        std::vector<int64_t> pbase(pages.size());
-        int64_t acc = 0;
-        for (size_t p = 0; p < pages.size(); p++) {
-            pbase[p] = acc;
-            const int64_t x = static_cast<int64_t>(pages[p].size) - 4 * static_cast<int64_t>(pages[p].nvals);
-            known &= x >= 0;
-            acc += x;
-        }
-        if (known && !opt) {
-            c->hpwbase.reserve(c->hpwins.size());
-            for (const auto& b : c->hpwins) {
-                const uint2 ch = c->hchunks[static_cast<size_t>(b.p0)];
-                const DevPage& pg = pages[ch.x];
-                c->hpwbase.push_back(pbase[ch.x] - static_cast<int64_t>(pg.off) + 4 * pg.first_row);
-            }
-        }
-    } else {
-        // greedy windows from the start of each page range (one range per
-        // host thread; a range start also starts a window), with each
-        // window's characters for the one-pass form (k_plain_fused): a page's
-        // strings fill it exactly, so its characters are size - 4 *
-        // num_values; verified on the device
-        const size_t NP = pages.size();
-        const int T = static_cast<int>(std::min<size_t>(16, std::max<size_t>(1, NP / 16384)));
-        const size_t per = (NP + static_cast<size_t>(T) - 1) / static_cast<size_t>(T);
-        std::vector<std::vector<pqk::DevBatch>> wparts(static_cast<size_t>(T));
-        std::vector<std::vector<int64_t>> cparts(static_cast<size_t>(T));
-        std::vector<char> kparts(static_cast<size_t>(T), 1);
-        pqfmt::parallel_run(T, T, [&](int t) {
-            auto& W = wparts[static_cast<size_t>(t)];
-            auto& C = cparts[static_cast<size_t>(t)];
-            const size_t end = std::min(NP, (static_cast<size_t>(t) + 1) * per);
-            W.reserve((end - std::min(end, static_cast<size_t>(t) * per)) / 4 + 1);
-            C.reserve(W.capacity());
-            bool known = true;
-            size_t p = static_cast<size_t>(t) * per;
-            while (p < end) {
-                pqk::DevBatch b{};
-                b.p0 = static_cast<int32_t>(p);
-                b.img_lo = pages[p].off;
-                uint64_t hi = b.img_lo;
-                size_t q = p;
-                int64_t ch = 0;
-                while (q < end && q - p < 64 && pages[q].off >= b.img_lo) {
-                    const uint64_t e = pages[q].off + slot(pages[q]);
-                    if (e - b.img_lo > pqk::kPWin) break;
-                    hi = e;
-                    const int64_t x = static_cast<int64_t>(pages[q].size) - 4 * static_cast<int64_t>(pages[q].nvals);
-                    known &= x >= 0;
-                    ch += x;
-                    b.nrows += static_cast<uint32_t>(std::max(pages[q].nvals, 0));
-                    q++;
-                }
-                b.row0 = pages[p].first_row;
-                b.np = static_cast<int32_t>(q - p);
-                b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
-                W.push_back(b);
-                C.push_back(ch);
-                p = q;
-            }
-            kparts[static_cast<size_t>(t)] = known;
-        });
-        bool known = true;
-        size_t nw = 0;
-        for (int t = 0; t < T; t++) {
-            nw += wparts[static_cast<size_t>(t)].size();
-            known &= kparts[static_cast<size_t>(t)] != 0;
-        }
-        c->hpwins.reserve(nw);
-        for (const auto& W : wparts) c->hpwins.insert(c->hpwins.end(), W.begin(), W.end());
-        if (known && !opt) {
-            c->hpwbase.reserve(nw + 1);
-            c->hpwbase.push_back(0);
-            for (const auto& C : cparts)
-                for (int64_t ch : C) c->hpwbase.push_back(c->hpwbase.back() + ch);
-        }
-    }
-    c->plain_opt = opt;
-    c->opt_lane_levels = true;
-    for (const auto& pg : pages) c->opt_lane_levels &= pg.nvals <= pqk::kOptLaneRows;
-    const int cus = ctx->cus;
-    c->plain_grid = cus * pqk::plain_write_blocks_per_cu();
-    c->plain = true;
-}
-
-// Decide whether every chunk of the column can take the fused BYTE_ARRAY
-// path (dict_fused.hip) and size its LDS carve-up; otherwise the generic
-// rows -> scan -> gather path runs.
-void plan_fused(pq_ctx* ctx, pq_chunk* c, const PVec<DevPage>& pages,
-                const std::vector<DevDict>& dicts) {
-    c->fused = false;
-    if (!ctx->opt_fused || c->type != PQ_BYTE_ARRAY || c->max_def > 255 || c->max_def < 0 || c->ranges.empty()) return;
-    const int cus = ctx->cus;
-    const uint32_t kLds = 160 * 1024;
-    for (auto& r : c->ranges) {
-        int32_t dict_id = -1;
-        uint32_t maxn = 0, maxs = 0;
-        for (int p = r.p0; p < r.p0 + r.np; p++) {
-            const DevPage& pg = pages[p];
-            if (pg.mode == pqk::MODE_DICT) {
-                if (dict_id >= 0 && pg.dict != dict_id) return;  // several dictionaries in force
-                dict_id = pg.dict;
-            }
-            maxn = std::max(maxn, static_cast<uint32_t>(std::max(pg.nvals, 0)));
-            maxs = std::max(maxs, static_cast<uint32_t>(std::max(pg.size, 0)));
-        }
-        if (maxn > 4096 || maxs > 16384) return;
-        r.dict_id = dict_id;
-        r.rows_cap = (std::max(maxn, 64u) + 63) / 64 * 64;
-        r.stage_bytes = (maxs + 15) / 16 * 16 + 16;
-        r.wave_bytes = pqk::fused_wave_bytes(r.rows_cap, r.stage_bytes);
-        r.dict_chars_bytes = r.dict_bytes = 0;
-        if (dict_id >= 0) {
-            const DevDict& d = dicts[dict_id];
-            if (d.size > 65536 - 64 || d.nvals < 0 || d.nvals > 65535) return;
-            int64_t ecap = std::min<int64_t>(d.nvals, d.size / 4 + 1);
-            r.dict_chars_bytes = (static_cast<uint32_t>(d.size) + 15) / 16 * 16 + 16;
-            r.dict_bytes = r.dict_chars_bytes + static_cast<uint32_t>((4 * ecap + 15) / 16 * 16);
-        }
-        if (r.dict_bytes + r.wave_bytes > kLds) return;
-        // producer/writer pairs per workgroup (dict_fused.hip)
-        int pairs = static_cast<int>(std::min<uint32_t>(8, (kLds - r.dict_bytes) / r.wave_bytes));
-        if (ctx->opt_waves > 0) pairs = std::max(1, std::min(pairs, ctx->opt_waves / 2));
-        const int W = 2 * pairs;
-        r.waves = W;
-        uint32_t lds = r.dict_bytes + static_cast<uint32_t>(pairs) * r.wave_bytes;
-        int per_cu = pqk::fused_occupancy_waves(lds, W);
-        if (per_cu < 1) per_cu = 1;
-        int need = (r.np + pairs - 1) / pairs;
-        r.grid = std::max(1, std::min(per_cu * cus, need));
-    }
-    c->fused = true;
-}
-
 }  // namespace
 
 extern "C" {
@@ -910,7 +325,6 @@ int pq_ctx_set_option(pq_ctx* ctx, const char* key, int64_t value) {
         return 0;
     }
     if (std::strcmp(key, "zflip") == 0) { ctx->opt_zflip = value != 0; return 0; }
-    if (std::strcmp(key, "codec_batch") == 0) { ctx->opt_codec_batch = value != 0; return 0; }
     if (std::strcmp(key, "write_waves") == 0) {
         if (value < 1 || value > 16) return set_err(ctx, PQ_ERR_ARG, "write_waves: 1..16");
         ctx->opt_write_waves = static_cast<int>(value);
@@ -1194,128 +608,6 @@ static void raw_start(pq_ctx* ctx, const uint8_t* file, size_t file_len, RawStag
     });
 }
 
-// The host page tables of one walk (dictionary and data pages, their image
-// slots and copy list) on host threads: per-range counts, then every page
-// written at its index.  Same tables as upload_walked's page loop, which
-// runs instead when a page goes through the codec pass (returns false).
-static bool plan_pages_parallel(pq_chunk* c, const pq_chunk_desc& desc, const pqfmt::WalkResult& w, bool keep_walk,
-                                int hw, int64_t seq, int64_t& row_base, int64_t& img, PVec<DevPage>& hpages,
-                                std::vector<DevDict>& hdicts, HVec<std::pair<int64_t, int64_t>>& copies,
-                                HVec<int32_t>& copy_size) {
-    const size_t N = w.pages.size();
-    const int T = static_cast<int>(std::min<size_t>(static_cast<size_t>(hw), std::max<size_t>(1, N / 16384)));
-    const size_t per = (N + static_cast<size_t>(T) - 1) / static_cast<size_t>(T);
-    struct Part {
-        int64_t nslot = 0, ndata = 0, bytes = 0, rows = 0, payload = 0;
-        bool codec = false;
-        std::vector<size_t> dicts;
-    };
-    std::vector<Part> parts(static_cast<size_t>(T));
-    auto slot_bytes = [](int32_t size) { return (static_cast<int64_t>(size) + 15) / 16 * 16 + 16; };
-    pqfmt::parallel_run(T, T, [&](int t) {
-        Part& P = parts[static_cast<size_t>(t)];
-        const size_t a = static_cast<size_t>(t) * per, b = std::min(N, a + per);
-        for (size_t i = a; i < b; i++) {
-            const pq_page_desc& p = w.pages[i];
-            const bool dict = p.page_type == PQ_DICTIONARY_PAGE, data = p.page_type == PQ_DATA_PAGE;
-            if (!dict && !data) continue;
-            P.codec |= (p.flags & (PQ_PAGE_COMPRESSED | PQ_PAGE_V2)) != 0;
-            P.nslot++;
-            P.bytes += slot_bytes(p.payload_size);
-            P.payload += p.payload_size;
-            if (dict) P.dicts.push_back(i);
-            else {
-                P.ndata++;
-                P.rows += p.num_values;
-            }
-        }
-    });
-    for (const auto& P : parts)
-        if (P.codec) return false;
-    // dictionary pages (few) in walk order: device index, entry base
-    std::vector<size_t> dpos;  // walk index of each, ascending
-    const int32_t d0 = static_cast<int32_t>(hdicts.size());
-    for (const auto& P : parts)
-        for (size_t i : P.dicts) {
-            const pq_page_desc& p = w.pages[i];
-            DevDict d{};
-            d.size = p.payload_size;
-            d.nvals = p.num_values;
-            d.entry_base = static_cast<int32_t>(c->nentries);
-            c->max_dict_bytes = std::max<uint32_t>(c->max_dict_bytes, static_cast<uint32_t>(std::max(p.payload_size, 0)));
-            const int64_t cap = c->type == PQ_BYTE_ARRAY ? std::min<int64_t>(p.num_values, p.payload_size / 4 + 1) : 0;
-            c->nentries += std::max<int64_t>(cap, 0);
-            hdicts.push_back(d);
-            c->dict_seq.push_back(seq + static_cast<int64_t>(i));
-            dpos.push_back(i);
-        }
-    auto dict_dev = [&](int64_t walk_idx) -> int32_t {
-        auto it = std::lower_bound(dpos.begin(), dpos.end(), static_cast<size_t>(walk_idx));
-        return (walk_idx >= 0 && it != dpos.end() && *it == static_cast<size_t>(walk_idx))
-                   ? d0 + static_cast<int32_t>(it - dpos.begin())
-                   : -1;
-    };
-    // bases of each range
-    std::vector<int64_t> img0(static_cast<size_t>(T)), slot0(static_cast<size_t>(T)), data0(static_cast<size_t>(T));
-    int64_t ti = 0, ts = 0, td = 0, rows = 0;
-    for (int t = 0; t < T; t++) {
-        const Part& P = parts[static_cast<size_t>(t)];
-        img0[static_cast<size_t>(t)] = ti;
-        slot0[static_cast<size_t>(t)] = ts;
-        data0[static_cast<size_t>(t)] = td;
-        ti += P.bytes;
-        ts += P.nslot;
-        td += P.ndata;
-        rows += P.rows;
-        c->payload_bytes += P.payload;
-    }
-    const size_t cp0 = copies.size(), hp0 = hpages.size(), ps0 = c->page_seq.size(), wk0 = c->walked.size();
-    copies.resize(cp0 + static_cast<size_t>(ts));
-    copy_size.resize(cp0 + static_cast<size_t>(ts));
-    hpages.resize(hp0 + static_cast<size_t>(td));
-    c->page_seq.resize(ps0 + static_cast<size_t>(td));
-    if (keep_walk) c->walked.resize(wk0 + N);
-    const int64_t img_base = img, rb = row_base;
-    pqfmt::parallel_run(T, T, [&](int t) {
-        const size_t a = static_cast<size_t>(t) * per, b = std::min(N, a + per);
-        int64_t at = img_base + img0[static_cast<size_t>(t)];
-        size_t si = cp0 + static_cast<size_t>(slot0[static_cast<size_t>(t)]);
-        size_t di = hp0 + static_cast<size_t>(data0[static_cast<size_t>(t)]);
-        for (size_t i = a; i < b; i++) {
-            pq_page_desc p = w.pages[i];
-            if (p.page_type == PQ_DICTIONARY_PAGE || p.page_type == PQ_DATA_PAGE) {
-                copies[si] = {p.payload_offset, at};
-                copy_size[si] = p.payload_size;
-                si++;
-                if (p.page_type == PQ_DICTIONARY_PAGE) {
-                    hdicts[static_cast<size_t>(dict_dev(static_cast<int64_t>(i)))].off = static_cast<uint64_t>(at);
-                } else {
-                    DevPage d{};
-                    d.off = static_cast<uint64_t>(at);
-                    d.size = p.payload_size;
-                    d.nvals = p.num_values;
-                    d.first_row = rb + p.first_row;
-                    const int32_t dd = p.dict_page >= 0 ? dict_dev(p.dict_page) : -1;
-                    const bool enc_dict = p.encoding == 2 || p.encoding == 8;
-                    d.mode = (enc_dict && dd >= 0) ? pqk::MODE_DICT
-                             : (c->type == PQ_BOOLEAN ? ((desc.ext_flags && p.encoding == 3) ? pqk::MODE_BOOL_RLE : pqk::MODE_BOOL)
-                                                      : pqk::MODE_PLAIN);
-                    d.dict = d.mode == pqk::MODE_DICT ? dd : -1;
-                    c->page_seq[ps0 + (di - hp0)] = seq + static_cast<int64_t>(i);
-                    hpages[di++] = d;
-                }
-                at += slot_bytes(p.payload_size);
-            }
-            if (keep_walk) {
-                p.first_row += rb;
-                c->walked[wk0 + i] = p;
-            }
-        }
-    });
-    img += ti;
-    row_base += rows;
-    return true;
-}
 
 // Builds the device chunk from page walks already made on the host: one walk
 // per input chunk (pq_chunk_upload) or one page-range walk (pq_chunk_upload_range).
@@ -1378,7 +670,6 @@ static int upload_walked(pq_ctx* ctx, const uint8_t* file, size_t file_len, cons
             e.flags = v2 ? (pqk::kCodecV2 | (desc.max_def_level > 0 ? pqk::kCodecDefPrefix : 0u) |
                             (desc.max_rep_level > 0 ? pqk::kCodecRepPrefix : 0u))
                          : 0u;
-            if (!ctx->opt_codec_batch) e.flags |= pqk::kCodecSerial;
             cents.push_back(e);
             cent_file.push_back(p.payload_offset);
             *out_len = static_cast<int32_t>(n);
@@ -2670,65 +1961,6 @@ int pq_regex_compile_check(const char* pattern, char* err, size_t errlen) {
         err[errlen - 1] = 0;
     }
     return rc;
-}
-
-// Windows of consecutive pages for the windowed PLAIN regex kernel (regex.hip
-// k_regex_plain): <= 64 pages and <= win bytes of image each.  False when a
-// page does not fit (the lane-per-page kernel runs then).
-bool plan_regex_windows(pq_ctx* ctx, pq_chunk* c) {
-    if (c->d_rwins && c->rwin_for_dfa == c->dfa_bytes && c->rwin_opt == ctx->opt_regex_win) return true;
-    const uint32_t maxslot = c->npages ? (c->max_page_bytes + 15) / 16 * 16 + 16 : 0u;
-    const uint32_t win = std::max<uint32_t>(static_cast<uint32_t>(ctx->opt_regex_win), maxslot);
-    // the kernel lists strings by u16 window offsets (and the string index
-    // keeps them): pages whose slot leaves no room take k_regex_lanes
-    if (win + 32 > 65535u) return false;
-    if (pqre::regex_plain_waves(c->dfa_bytes, win) == 0) return false;
-    const uint32_t lds = pqre::regex_plain_lds(c->dfa_bytes, win);
-    if (lds > 160 * 1024) return false;
-    c->hrwins.clear();
-    // the PLAIN decode's windows are the same kind (<= 64 consecutive page
-    // slots, <= kPWin bytes; planned on host threads at upload): no page
-    // table read back
-    const bool same = c->plain && !c->plain_spec && win == pqk::kPWin && !c->hpwins.empty();
-    std::vector<DevPage> hp(same ? 0 : static_cast<size_t>(c->npages));
-    if (same) c->hrwins = c->hpwins;
-    else if (c->npages && hipMemcpy(hp.data(), c->d_pages, hp.size() * sizeof(DevPage), hipMemcpyDeviceToHost) != hipSuccess)
-        return false;
-    size_t p = 0;
-    while (p < hp.size()) {
-        pqk::DevBatch b{};
-        b.p0 = static_cast<int32_t>(p);
-        b.img_lo = hp[p].off;
-        uint64_t hi = b.img_lo;
-        size_t q = p;
-        while (q < hp.size() && q - p < 64) {
-            const uint64_t e = hp[q].off + (static_cast<uint64_t>(std::max(hp[q].size, 0)) + 15) / 16 * 16 + 16;
-            if (e - b.img_lo > win) break;
-            hi = e;
-            b.nrows += static_cast<uint32_t>(std::max(hp[q].nvals, 0));
-            q++;
-        }
-        b.row0 = hp[p].first_row;
-        b.np = static_cast<int32_t>(q - p);
-        b.img_bytes = static_cast<uint32_t>(hi - b.img_lo);
-        c->hrwins.push_back(b);
-        p = q;
-    }
-    dfree(c->d_rwins);
-    if (!c->d_rwin_ticket && dalloc(&c->d_rwin_ticket, 1)) return false;
-    if (dalloc(&c->d_rwins, std::max<size_t>(c->hrwins.size(), 1))) return false;
-    if (!c->hrwins.empty() &&
-        hipMemcpy(c->d_rwins, c->hrwins.data(), c->hrwins.size() * sizeof(pqk::DevBatch), hipMemcpyHostToDevice) != hipSuccess)
-        return false;
-    const int cus = ctx->cus;
-    const int per_cu = std::max(1, pqre::regex_plain_occupancy(lds));
-    c->rwin_bytes = win;
-    c->rwin_for_dfa = c->dfa_bytes;
-    c->rwin_opt = ctx->opt_regex_win;
-    const int scan = static_cast<int>(pqre::regex_plain_waves(c->dfa_bytes, win));  // waves per workgroup
-    c->rwin_grid = std::max(1, std::min<int>(per_cu * cus, static_cast<int>((c->hrwins.size() + scan - 1) / scan)));
-    (void)cus;
-    return true;
 }
 
 // The compiled pattern (cached per chunk), page flags and the per-entry

@@ -53,16 +53,9 @@ constexpr uint32_t kInWin = 8192;  // staged input bytes (+16 slack)
 constexpr uint32_t kFlush = 1024;  // output bytes per flush step (16 per lane)
 constexpr uint32_t kFast = 10;     // Huffman lookup bits
 
-constexpr uint32_t kBatch = 256;  // output bytes per batch of short commands (4 per lane)
-struct BatchLds {                 // lz_run's per-batch scratch
-    uint8_t mark[kBatch];         // command index at its first byte
-    uint8_t val[kBatch];          // each byte's value once resolved
-    uint16_t ref[kBatch];         // or the batch byte it copies (kNoRef: resolved)
-};
 struct CodecLds {
     uint8_t ring[kRing];
     uint8_t in[kInWin + 32];
-    BatchLds bx;
     uint16_t lt[1 << kFast];  // litlen: sym << 4 | len (0 = longer code)
     uint16_t dt[1 << kFast];  // distance
     uint16_t sym[320];        // symbols in canonical order: litlen [0, 288), dist [288, 320)
@@ -136,8 +129,6 @@ struct InT {
         if (p < wlo || p + k + sh > wlo + kWin) refill(p);
     }
     __device__ __forceinline__ uint32_t at(uint32_t p) const { return min(p - wlo + sh, kWin + 16u); }
-    // bytes [p, p + k) in the window now (no refill)
-    __device__ __forceinline__ bool has(uint32_t p, uint32_t k) const { return p >= wlo && p + k + sh <= wlo + kWin; }
     __device__ __forceinline__ uint32_t byte(uint32_t p) const { return w[at(p)]; }
     __device__ __forceinline__ uint32_t u16le(uint32_t p) const { return byte(p) | (byte(p + 1) << 8); }
     __device__ __forceinline__ uint32_t u32le(uint32_t p) const {
@@ -325,185 +316,6 @@ struct Out {
     }
 };
 
-// ── short LZ77 commands in batches ─────────────────────────────────────────
-// SNAPPY and LZ4 streams are mostly short commands (C3's text: ~10 output
-// bytes each), and a command executed by the wave on its own costs a wave
-// step of 64 lanes plus its synchronisation.  lz_run gathers consecutive
-// commands of <= 64 bytes (one per lane, at most kBatch output bytes, every
-// literal byte inside the staged input window) and executes the batch at once:
-//  * lane k holds command k (kind, length, input position or distance) and
-//    marks its first output byte; a max-scan over the marks gives every byte
-//    its command (4 bytes per lane);
-//  * a literal byte comes from the window, a copied byte from the ring when
-//    its source precedes the batch (final bytes), else it refers to an earlier
-//    byte of the batch;
-//  * pointer jumping resolves the references (<= 8 rounds for 256 bytes:
-//    chains such as a distance-1 run halve each round); then the bytes go to
-//    the ring.
-// Longer commands run as before (O.lit / O.copy, 64 bytes per step).
-struct LzCmd {
-    uint32_t kind;  // 0 literal (val: input position), 1 copy (val: distance)
-    uint32_t n, val;
-};
-constexpr uint16_t kNoRef = 0xFFFFu;
-
-template <class InX, class OutT>
-__device__ __forceinline__ void lz_batch(InX& I, OutT& O, lds8* bx, uint32_t K, uint32_t T, uint32_t my_kind,
-                                         uint32_t my_val, uint32_t my_start) {
-    using lds16b = __attribute__((address_space(3))) uint16_t;
-    lds8* mark = bx + offsetof(BatchLds, mark);
-    lds8* val = bx + offsetof(BatchLds, val);
-    lds16b* ref = reinterpret_cast<lds16b*>(bx + offsetof(BatchLds, ref));
-    const uint32_t l4 = lane() * 4;
-    reinterpret_cast<lds32*>(mark)[lane()] = 0u;
-    wsync();
-    if (lane() < K) mark[my_start] = static_cast<uint8_t>(lane());
-    wsync();
-    const uint32_t mk = reinterpret_cast<lds32*>(mark)[lane()];
-    uint32_t cm[4], run = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        run = max(run, (mk >> (8 * i)) & 0xFFu);
-        cm[i] = run;
-    }
-    const uint32_t ex = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(dev::wave_incl_max(run)),
-                                                                          0x138, 0xf, 0xf, true));  // lane - 1's max
-    uint32_t v[4], r[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t j = l4 + static_cast<uint32_t>(i);
-        const uint32_t c = max(ex, cm[i]);
-        const uint32_t kd = static_cast<uint32_t>(__shfl(static_cast<int>(my_kind), static_cast<int>(c)));
-        const uint32_t vl = static_cast<uint32_t>(__shfl(static_cast<int>(my_val), static_cast<int>(c)));
-        const uint32_t st = static_cast<uint32_t>(__shfl(static_cast<int>(my_start), static_cast<int>(c)));
-        v[i] = 0u;
-        r[i] = kNoRef;
-        if (j < T) {
-            if (kd == 0) {
-                v[i] = I.byte(vl + (j - st));
-            } else if (j < vl) {  // the source precedes the batch: final bytes in the ring
-                v[i] = O.ring[(O.op + j - vl) & OutT::kMask];
-            } else {
-                r[i] = j - vl;
-            }
-        }
-    }
-    // resolve in-batch references: jump while any byte still refers
-    bool open = r[0] != kNoRef || r[1] != kNoRef || r[2] != kNoRef || r[3] != kNoRef;
-    while (__ballot(open)) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            val[l4 + i] = static_cast<uint8_t>(v[i]);
-            ref[l4 + i] = static_cast<uint16_t>(r[i]);
-        }
-        wsync();
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            if (r[i] != kNoRef) {
-                const uint32_t q = r[i];
-                const uint32_t rq = ref[q];
-                if (rq == kNoRef) {
-                    v[i] = val[q];
-                    r[i] = kNoRef;
-                } else {
-                    r[i] = rq;
-                }
-            }
-        }
-        open = r[0] != kNoRef || r[1] != kNoRef || r[2] != kNoRef || r[3] != kNoRef;
-        wsync();
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-        if (l4 + i < T) O.ring[(O.op + l4 + i) & OutT::kMask] = static_cast<uint8_t>(v[i]);
-    O.op += T;
-    wsync();
-    if (O.op - O.fl >= kFlush) O.flush(false);
-}
-
-// The command parser's input bytes in registers: 256 bytes from `base`, 4
-// per lane, read with v_readlane (a few cycles) instead of an LDS round trip
-// per header byte; bytes past its reach fall back to the staged window.
-template <class InX>
-struct RegWin {
-    InX* I;
-    uint32_t base = 0, lim = 0, w = 0;
-    __device__ __forceinline__ void load(uint32_t p) {
-        base = p & ~3u;
-        const uint32_t q = base + 4 * lane();
-        w = I->byte(q) | (I->byte(q + 1) << 8) | (I->byte(q + 2) << 16) | (I->byte(q + 3) << 24);
-        // valid up to the staged window's end
-        lim = min(base + 4 * static_cast<uint32_t>(kWave), I->wlo + InX::kWindow - I->sh);
-    }
-    __device__ __forceinline__ bool covers(uint32_t p, uint32_t k) const { return p >= base && p + k <= lim; }
-    __device__ __forceinline__ uint32_t byte(uint32_t q) const {
-        if (!covers(q, 1)) return I->byte(q);
-        const uint32_t o = q - base;
-        return (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w), static_cast<int>(o >> 2))) >>
-                (8 * (o & 3u))) & 0xFFu;
-    }
-    __device__ __forceinline__ uint32_t u16le(uint32_t q) const { return byte(q) | (byte(q + 1) << 8); }
-    __device__ __forceinline__ uint32_t u32le(uint32_t q) const {
-        return byte(q) | (byte(q + 1) << 8) | (byte(q + 2) << 16) | (byte(q + 3) << 24);
-    }
-};
-
-// next(p, cmd): parses the command at input position p (the window holds
-// [p, p + 80) when next is called) and advances p: 1 a command, 0 the end of
-// the stream or an error (O.st set), 2 the window must move first (p kept).
-template <class InX, class OutT, class Next>
-__device__ __forceinline__ void lz_run(InX& I, OutT& O, lds8* bx, uint32_t& p, uint32_t end, RegWin<InX>& R, Next&& next) {
-    LzCmd cmd{};
-    bool have = false, done = false, slide = false;
-    while (O.st == ST_OK) {
-        uint32_t K = 0, T = 0, my_kind = 0, my_val = 0, my_start = 0;
-        for (;;) {
-            if (!have) {
-                if (p >= end) { done = true; break; }
-                if (!I.has(p, 80) || slide) {
-                    if (K) break;  // the batch's literals must stay in the window
-                    I.refill(p);
-                    slide = false;
-                    R.load(p);
-                }
-                if (!R.covers(p, 16)) R.load(p);
-                const int r = next(p, cmd);
-                if (r == 2) {
-                    slide = true;
-                    if (K) break;
-                    continue;
-                }
-                if (r == 0) { done = true; break; }
-                have = true;
-            }
-            if (cmd.n > static_cast<uint32_t>(kWave) || T + cmd.n > kBatch || K == static_cast<uint32_t>(kWave)) break;
-            if (cmd.kind == 1 && (cmd.val == 0 || cmd.val > O.op + T - O.vbase || cmd.val > OutT::kRingSize - 1)) {
-                O.st = ST_CORRUPT;
-                return;
-            }
-            if (lane() == K) {
-                my_kind = cmd.kind;
-                my_val = cmd.val;
-                my_start = T;
-            }
-            K++;
-            T += cmd.n;
-            have = false;
-        }
-        if (O.st != ST_OK) return;
-        if (K) {
-            if (!O.room(T)) return;
-            lz_batch(I, O, bx, K, T, my_kind, my_val, my_start);
-        }
-        if (have && cmd.n > static_cast<uint32_t>(kWave)) {  // a long command on its own
-            if (cmd.kind == 0) O.lit(I, cmd.val, cmd.n);
-            else O.copy(cmd.val, cmd.n);
-            have = false;
-        }
-        if (done && !have) return;
-    }
-}
-
 // ── SNAPPY ─────────────────────────────────────────────────────────────────
 template <class InX, class OutT>
 __device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end, uint32_t expect) {
@@ -555,123 +367,6 @@ __device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end
     if (O.st == ST_OK && O.op - O.vbase != expect) O.st = ST_SIZE;
 }
 
-// SNAPPY through lz_run (the same stream checks as snappy()).
-template <class InX, class OutT>
-__device__ __forceinline__ void snappy_b(InX& I, OutT& O, lds8* bx, uint32_t p, uint32_t end, uint32_t expect) {
-    uint32_t ulen = 0;
-    I.ensure(p, 8);
-    for (uint32_t k = 0;; k++) {
-        if (k == 5 || p >= end) { O.st = ST_CORRUPT; return; }
-        const uint32_t b = I.byte(p++);
-        ulen |= (b & 0x7Fu) << (7 * k);
-        if (!(b & 0x80u)) break;
-    }
-    if (ulen != expect) { O.st = ST_SIZE; return; }
-    RegWin<InX> R{&I};
-    R.load(p);
-    lz_run(I, O, bx, p, end, R, [&](uint32_t& q, LzCmd& c) -> int {
-        const uint32_t t = uni(R.byte(q));
-        const uint32_t ty = t & 3u;
-        if (ty == 0) {
-            uint32_t n = (t >> 2) + 1;
-            q += 1;
-            if (n > 60) {
-                const uint32_t nb = n - 60;
-                const uint32_t x = R.u32le(q);
-                n = (nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u))) + 1;
-                q += nb;
-            }
-            n = uni(n);
-            if (q > end || n > end - q || n == 0) { O.st = ST_CORRUPT; return 0; }
-            c = LzCmd{0u, n, q};
-            q += n;
-            return 1;
-        }
-        uint32_t n, d;
-        if (ty == 1) {
-            n = 4 + ((t >> 2) & 7u);
-            d = ((t >> 5) << 8) | R.byte(q + 1);
-            q += 2;
-        } else if (ty == 2) {
-            n = (t >> 2) + 1;
-            d = R.u16le(q + 1);
-            q += 3;
-        } else {
-            n = (t >> 2) + 1;
-            d = R.u32le(q + 1);
-            q += 5;
-        }
-        if (q > end) { O.st = ST_CORRUPT; return 0; }
-        c = LzCmd{1u, uni(n), uni(d)};
-        return 1;
-    });
-    if (O.st == ST_OK && O.op - O.vbase != expect) O.st = ST_SIZE;
-}
-
-// One LZ4 block through lz_run (the same sequence checks as lz4_block()):
-// a sequence's literals and its match are two commands; the match is parsed
-// by the call after the literals' (they may have moved the position past the
-// window).
-template <class InX, class OutT>
-__device__ __forceinline__ void lz4_block_b(InX& I, OutT& O, lds8* bx, uint32_t p, uint32_t end) {
-    bool in_match = false, ended = false;
-    uint32_t tok = 0;
-    if (!I.has(p, 80)) I.refill(p);
-    RegWin<InX> R{&I};
-    R.load(p);
-    auto match = [&](uint32_t& q, LzCmd& c) -> int {
-        if (q == end) { in_match = false; ended = true; return 0; }  // the last sequence holds literals only
-        if (end - q < 2) { O.st = ST_CORRUPT; return 0; }
-        const uint32_t qm = q;
-        const uint32_t d = uni(R.u16le(q));
-        q += 2;
-        uint32_t m = tok & 15u;
-        if (m == 15) {
-            uint32_t b;
-            do {
-                if (q >= end) { O.st = ST_CORRUPT; return 0; }
-                if (!I.has(q, 1)) {  // a long run of length bytes: parse the match again from a moved window
-                    q = qm;
-                    return 2;
-                }
-                b = uni(R.byte(q++));
-                m += b;
-            } while (b == 255);
-        }
-        in_match = false;
-        c = LzCmd{1u, m + 4, d};
-        return 1;
-    };
-    lz_run(I, O, bx, p, end, R, [&](uint32_t& q, LzCmd& c) -> int {
-        if (in_match) return match(q, c);
-        const uint32_t q0 = q;
-        tok = uni(R.byte(q++));
-        uint32_t n = tok >> 4;
-        if (n == 15) {
-            uint32_t b;
-            do {
-                if (q >= end) { O.st = ST_CORRUPT; return 0; }
-                if (!I.has(q, 1)) {  // a long run of length bytes: parse it again from a moved window
-                    q = q0;
-                    return 2;
-                }
-                b = uni(R.byte(q++));
-                n += b;
-            } while (b == 255);
-        }
-        if (n > end - q) { O.st = ST_CORRUPT; return 0; }
-        in_match = true;
-        if (n) {
-            c = LzCmd{0u, n, q};
-            q += n;
-            return 1;
-        }
-        return match(q, c);
-    });
-    // the stream ends right after a sequence's literals, and nowhere else
-    if (O.st == ST_OK && !(ended || (in_match && p == end))) O.st = ST_CORRUPT;
-}
-
 // ── LZ4 block ──────────────────────────────────────────────────────────────
 template <class InX, class OutT>
 __device__ __forceinline__ void lz4_block(InX& I, OutT& O, uint32_t p, uint32_t end) {
@@ -713,10 +408,9 @@ __device__ __forceinline__ void lz4_block(InX& I, OutT& O, uint32_t p, uint32_t 
     }
 }
 
-// Hadoop framing (codec LZ4): blocks of [u32 BE raw bytes][u32 BE packed bytes][LZ4 block]
-// (bx: blocks through lz4_block_b, else lz4_block).
+// Hadoop framing (codec LZ4): blocks of [u32 BE raw bytes][u32 BE packed bytes][LZ4 block].
 template <class InX, class OutT>
-__device__ __forceinline__ void lz4_hadoop(InX& I, OutT& O, uint32_t p, uint32_t end, lds8* bx = nullptr) {
+__device__ __forceinline__ void lz4_hadoop(InX& I, OutT& O, uint32_t p, uint32_t end) {
     while (p < end && O.st == ST_OK) {
         if (end - p < 8) { O.st = ST_CORRUPT; return; }
         I.ensure(p, 8);
@@ -724,8 +418,7 @@ __device__ __forceinline__ void lz4_hadoop(InX& I, OutT& O, uint32_t p, uint32_t
         p += 8;
         if (packed > end - p) { O.st = ST_CORRUPT; return; }
         const uint32_t o0 = O.op;
-        if (bx) lz4_block_b(I, O, bx, p, p + packed);
-        else lz4_block(I, O, p, p + packed);
+        lz4_block(I, O, p, p + packed);
         if (O.st == ST_OK && O.op - o0 != raw) O.st = ST_SIZE;
         p += packed;
     }
@@ -1039,7 +732,6 @@ using ZCodecLds = ZCodecLdsT<kZRing, kInWin>;
 struct SCodecLds {
     uint8_t ring[kSRing];
     uint8_t in[kSWin + 32];
-    BatchLds bx;
 };
 using ZSCodecLds = ZCodecLdsT<kSRing, kSWin>;
 
@@ -1163,10 +855,6 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
                                      : (kZstd ? offsetof(ZCodecLds, in) : offsetof(CodecLds, in));
     lds8* lring = (lds8*)(smem + kRingOff);
     lds8* lin = (lds8*)(smem + kInOff);
-    // the batch executor's scratch (lz_run; not in the ZSTD layouts, whose
-    // streams never take it)
-    constexpr size_t kBxOff = kZstd ? 0 : (kSmall ? offsetof(SCodecLds, bx) : offsetof(CodecLds, bx));
-    lds8* lbx = (lds8*)(smem + kBxOff);
     using OutK = Out<kGzip, kSmall ? kSRing : (kZstd ? kZRing : kRing)>;
     using InK = typename std::conditional<kSmall, InS, In>::type;
     lds32* lcrc = (lds32*)(smem + offsetof(CodecLds, crc_tab));
@@ -1212,22 +900,9 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
             } else {
                 switch (e.codec) {
                     case 0: O.lit(I, p, end - p); break;
-                    case 1:
-                    case 5:
-                    case 7:
-                        if constexpr (kZstd) {  // (a ZSTD chunk holds no other codec: the host checks)
-                            O.st = ST_UNSUPPORTED;
-                        } else if (e.codec == 1) {
-                            if (e.flags & kCodecSerial) snappy(I, O, p, end, expect);
-                            else snappy_b(I, O, lbx, p, end, expect);
-                        } else if (e.codec == 5) {
-                            if (e.flags & kCodecSerial) lz4_hadoop(I, O, p, end);
-                            else lz4_hadoop(I, O, p, end, lbx);
-                        } else {
-                            if (e.flags & kCodecSerial) lz4_block(I, O, p, end);
-                            else lz4_block_b(I, O, lbx, p, end);
-                        }
-                        break;
+                    case 1: snappy(I, O, p, end, expect); break;
+                    case 5: lz4_hadoop(I, O, p, end); break;
+                    case 7: lz4_block(I, O, p, end); break;
                     case 6:
                         if constexpr (kZstd) {
                             // the tables after the ring and the window (this instantiation's launch only)

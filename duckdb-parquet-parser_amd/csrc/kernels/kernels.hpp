@@ -63,7 +63,7 @@ struct RelayoutEntry {
 void launch_relayout(hipStream_t s, const uint8_t* raw, uint8_t* img, const RelayoutEntry* ent, int32_t n);
 
 // One compressed or DATA_PAGE_V2 payload → its slot (codec.hip).
-enum : uint32_t { kCodecV2 = 1, kCodecDefPrefix = 2, kCodecRepPrefix = 4, kCodecSerial = 8 };  // 8: one command per wave step (option codec_batch 0)
+enum : uint32_t { kCodecV2 = 1, kCodecDefPrefix = 2, kCodecRepPrefix = 4 };
 struct CodecEntry {
     uint64_t src;      // payload offset in the source buffer (raw chunk bytes)
     uint64_t dst;      // slot offset in the image (16-byte aligned)

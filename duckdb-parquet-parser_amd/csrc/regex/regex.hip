@@ -566,7 +566,6 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
     uint32_t* lbase = pref + 64;
     uint32_t* pcnt = lbase + 64;
     uint32_t* hit = pcnt + 64;  // [0..1]: satisfied-page mask of the window
-    uint16_t* surv = reinterpret_cast<uint16_t*>(hit + 4);  // prefilter survivors of a batch (kStrPerLane x 64)
     int32_t w = static_cast<int32_t>(blockIdx.x * K + c);
     if (w >= nwins) return;
     // descriptors two windows ahead: the batch of window i + 2 and the
@@ -887,69 +886,22 @@ __global__ void __launch_bounds__(kPlainWavesMax * 64) k_regex_plain(const uint8
         const uint32_t wtotal = bcast_last(pinc);
         __builtin_amdgcn_wave_barrier();
         const uint64_t sinks = kSink && full ? (static_cast<uint64_t>(D->sink_hi) << 32) | D->sink_lo : 0ull;
-        // string g of the window: its page lane and its window offset
-        auto locate = [&](uint32_t g, bool ok, uint32_t& gl, uint32_t& ent) {
-            uint32_t lo2 = 0;  // first page lane whose inclusive count exceeds g
-#pragma unroll
-            for (uint32_t stp = 32; stp >= 1; stp >>= 1)
-                if (pref[lo2 + stp - 1] <= g) lo2 += stp;
-            gl = ok ? lo2 : 0u;
-            const uint32_t bef = gl ? pref[gl - 1] : 0u;
-            ent = ok ? list[lbase[gl] + (g - bef)] : 4u;
-        };
-        // Prefilter (D->req: a byte every match contains, regex_host.cpp
-        // build_dfa): a batch takes only the strings holding that byte, found
-        // 4 bytes per step by a zero-byte test; the others cannot match (their
-        // pages are satisfied only under NOT LIKE).  Survivors of up to
-        // kStrPerLane x 64 strings go to `surv`, then run the DFA as a batch.
-        const bool pre = (D->req >> 8) & 1u;
-        const uint32_t rbyte = (D->req & 0xFFu) * 0x01010101u;
-        uint32_t gnext = 0;
-        for (;;) {
-            uint32_t ns = 0;
-            if (pre) {
-                while (ns + kWave <= kStrPerLane * kWave && gnext < ((dbg & 1) ? 0u : wtotal)) {
-                    const uint32_t g = gnext + lane();
-                    const bool ok = g < wtotal;
-                    uint32_t gl, ent;
-                    locate(g, ok, gl, ent);
-                    if (idx_w && ok) idx_w[fr0 + g] = static_cast<uint16_t>(ent);
-                    const uint32_t len = ok ? st_u32(stage, ent - 4) : 0u;
-                    bool has = false;
-                    for (uint32_t o = 0; o < len && !has; o += 4) {
-                        const uint32_t x = st_u32(stage, ent + o) ^ rbyte;
-                        const uint32_t keep = len - o >= 4 ? 0u : (0xFFFFFFFFu << (8 * (len - o)));  // bytes past the string: nonzero
-                        const uint32_t y = x | keep;
-                        has = ((y - 0x01010101u) & ~y & 0x80808080u) != 0;
-                    }
-                    const uint64_t sb = __ballot(ok && has);
-                    if (ok && has) surv[ns + popc_below(sb)] = static_cast<uint16_t>(g);
-                    // without the byte: no match; satisfied under NOT LIKE
-                    if (ok && !has && negv) atomicOr(&hit[gl >> 5], 1u << (gl & 31));
-                    ns += static_cast<uint32_t>(__popcll(sb));
-                    gnext += kWave;
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (ns == 0) {
-                    if (gnext >= wtotal || (dbg & 1)) break;
-                    continue;
-                }
-            } else {
-                if (gnext >= ((dbg & 1) ? 0u : wtotal)) break;
-            }
-            const uint32_t g0 = gnext;  // (no prefilter: strings g0 .. g0 + 255)
-            if (!pre) gnext += kStrPerLane * kWave;
+        for (uint32_t g0 = 0; g0 < ((dbg & 1) ? 0u : wtotal); g0 += kStrPerLane * kWave) {
             uint32_t e2[kStrPerLane], off2[kStrPerLane], len2[kStrPerLane], pg2[kStrPerLane];
             bool ok2[kStrPerLane];
 #pragma unroll
             for (uint32_t h = 0; h < kStrPerLane; h++) {
-                const uint32_t k = h * kWave + lane();
-                const uint32_t g = pre ? (k < ns ? static_cast<uint32_t>(surv[k]) : 0u) : g0 + k;
-                ok2[h] = pre ? k < ns : g < wtotal;
-                uint32_t gl, ent;
-                locate(g, ok2[h], gl, ent);
-                if (!pre && idx_w && ok2[h]) idx_w[fr0 + g] = static_cast<uint16_t>(ent);
+                const uint32_t g = g0 + h * kWave + lane();
+                ok2[h] = g < wtotal;
+                // first page lane whose inclusive count exceeds g
+                uint32_t lo2 = 0;
+#pragma unroll
+                for (uint32_t stp = 32; stp >= 1; stp >>= 1)
+                    if (pref[lo2 + stp - 1] <= g) lo2 += stp;
+                const uint32_t gl = ok2[h] ? lo2 : 0u;
+                const uint32_t bef = gl ? pref[gl - 1] : 0u;
+                const uint32_t ent = ok2[h] ? list[lbase[gl] + (g - bef)] : 4u;
+                if (idx_w && ok2[h]) idx_w[fr0 + g] = static_cast<uint16_t>(ent);
                 off2[h] = ent;
                 len2[h] = ok2[h] ? st_u32(stage, ent - 4) : 0u;
                 pg2[h] = gl;

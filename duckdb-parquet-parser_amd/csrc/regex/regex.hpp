@@ -80,11 +80,8 @@ bool build_dfa(const Program& p, std::vector<uint8_t>* image);
 
 // Windowed PLAIN scan (chunks without dictionary pages).  Per wave: the
 // window (+32 zero bytes), a u16 offset per possible string, per-page counts,
-// list bases and kept counts, the hit mask, the prefilter's survivors of a
-// batch (4 x 64 u16).
-constexpr uint32_t regex_plain_wave_lds(uint32_t win_bytes) {
-    return win_bytes + 32 + win_bytes / 2 + 3 * 64 * 4 + 16 + 4 * 64 * 2;
-}
+// list bases and kept counts, the hit mask.
+constexpr uint32_t regex_plain_wave_lds(uint32_t win_bytes) { return win_bytes + 32 + win_bytes / 2 + 3 * 64 * 4 + 16; }
 uint32_t regex_plain_waves(uint32_t dfa_bytes, uint32_t win_bytes);
 uint32_t regex_plain_lds(uint32_t dfa_bytes, uint32_t win_bytes);
 int regex_plain_occupancy(uint32_t lds);

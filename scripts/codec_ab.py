@@ -3,7 +3,8 @@
 (SNAPPY / LZ4 / LZ4_RAW / ZSTD; 1 MiB pages and 8 KiB pages): the codec
 kernel's time (HIP events) per option set, every variant's decode checked
 against the uncompressed decode.
-usage: codec_ab.py [rows] [opt=val,...]..."""
+usage: codec_ab.py [rows] [opt=val[:reset],...]...  (reset: the value restored
+after the variant, default 0)"""
 import hashlib
 import io
 import json
@@ -43,9 +44,9 @@ for codec, ver, page in (("SNAPPY", "1.0", 1 << 20), ("SNAPPY", "1.0", 8192), ("
     d = capi.File(cf).chunk(0, 0)
     d.ext_flags = capi.EXT_CODECS | capi.EXT_PAGE_V2
     for v in variants:
-        opts = {} if v == "-" else {k: int(x) for k, x in (kv.split("=") for kv in v.split(","))}
-        for k, x in opts.items():
-            ctx.set_option(k, x)
+        opts = {} if v == "-" else {k: (x + ":0").split(":")[:2] for k, x in (kv.split("=") for kv in v.split(","))}
+        for k, (x, _) in opts.items():
+            ctx.set_option(k, int(x))
         ms = []
         for _ in range(3):
             ctx.timing(True)
@@ -60,8 +61,8 @@ for codec, ver, page in (("SNAPPY", "1.0", 1 << 20), ("SNAPPY", "1.0", 8192), ("
         ok = hashlib.sha256(capi.canonical_dump(x.to_host())).hexdigest() == ref
         ub = x.payload_bytes
         x.free()
-        for k in opts:
-            ctx.set_option(k, 1 if k == "codec_batch" else 0)
+        for k, (_, r) in opts.items():
+            ctx.set_option(k, int(r))
         m = statistics.median(ms)
         print(json.dumps({"codec": codec, "version": ver, "page": page, "variant": v, "codec_ms": round(m, 3),
                           "GBs_out": round(ub / (m * 1e-3) / 1e9, 2), "validated": ok}), flush=True)

@@ -3,5 +3,5 @@ set -o pipefail
 OUT=gpurun_out/${1:-r6i}; mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest tests/test_gpu_ext.py -x -q --timeout 200 --timeout-method thread > "$OUT/pytest.log" 2>&1
 rc=$?; tail -4 "$OUT/pytest.log"; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python scripts/codec_ab.py 10000000 - codec_batch=0 > "$OUT/codec_ab.txt" 2>&1
+timeout -k 10 600 python scripts/codec_ab.py 10000000 - > "$OUT/codec_ab.txt" 2>&1
 rc=$?; cat "$OUT/codec_ab.txt"; exit $rc
