@@ -316,6 +316,40 @@ struct Out {
     }
 };
 
+// ── command headers from registers ─────────────────────────────────────────
+// The SNAPPY / LZ4 command stream is parsed wave-uniformly, one command after
+// the other.  Reading each header byte from the staged input costs an LDS
+// round trip on that serial chain; instead 256 input bytes sit in one VGPR
+// (4 per lane) and a header byte is a v_readlane, so a command's only LDS
+// round trip is its own execution (the ring read before the ring write).
+template <class InX>
+struct TagWin {
+    InX* I;
+    uint32_t base = 1u, lim = 0u, w = 0u;  // bytes [base, lim) held (empty at first)
+    __device__ __forceinline__ void load(uint32_t p) {
+        I->ensure(p, 16);
+        base = p & ~3u;
+        const uint32_t q = base + 4 * lane();
+        w = I->byte(q) | (I->byte(q + 1) << 8) | (I->byte(q + 2) << 16) | (I->byte(q + 3) << 24);
+        // the staged window's bytes only (past it the LDS holds others)
+        lim = uni(min(base + 4 * static_cast<uint32_t>(kWave), I->wlo + InX::kWindow - I->sh));
+        base = uni(base);
+    }
+    // bytes [p, p + k) held, loading them when they are not (k <= 16)
+    __device__ __forceinline__ void need(uint32_t p, uint32_t k) {
+        if (p < base || p + k > lim) load(p);
+    }
+    __device__ __forceinline__ uint32_t byte(uint32_t q) const {
+        const uint32_t o = q - base;
+        return (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w), static_cast<int>(o >> 2))) >>
+                (8 * (o & 3u))) & 0xFFu;
+    }
+    __device__ __forceinline__ uint32_t u16le(uint32_t q) const { return byte(q) | (byte(q + 1) << 8); }
+    __device__ __forceinline__ uint32_t u32le(uint32_t q) const {
+        return byte(q) | (byte(q + 1) << 8) | (byte(q + 2) << 16) | (byte(q + 3) << 24);
+    }
+};
+
 // ── SNAPPY ─────────────────────────────────────────────────────────────────
 template <class InX, class OutT>
 __device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end, uint32_t expect) {
@@ -328,16 +362,17 @@ __device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end
         if (!(b & 0x80u)) break;
     }
     if (ulen != expect) { O.st = ST_SIZE; return; }
+    TagWin<InX> T{&I};
     while (p < end && O.st == ST_OK) {
-        I.ensure(p, 8);
-        const uint32_t t = uni(I.byte(p));
+        T.need(p, 5);  // the longest header: a tag and four bytes
+        const uint32_t t = T.byte(p);
         const uint32_t ty = t & 3u;
         if (ty == 0) {
             uint32_t n = (t >> 2) + 1;
             p += 1;
             if (n > 60) {
                 const uint32_t nb = n - 60;
-                const uint32_t x = I.u32le(p);
+                const uint32_t x = T.u32le(p);
                 n = (nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u))) + 1;
                 p += nb;
             }
@@ -349,15 +384,15 @@ __device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end
             uint32_t n, d;
             if (ty == 1) {
                 n = 4 + ((t >> 2) & 7u);
-                d = ((t >> 5) << 8) | I.byte(p + 1);
+                d = ((t >> 5) << 8) | T.byte(p + 1);
                 p += 2;
             } else if (ty == 2) {
                 n = (t >> 2) + 1;
-                d = I.u16le(p + 1);
+                d = T.u16le(p + 1);
                 p += 3;
             } else {
                 n = (t >> 2) + 1;
-                d = I.u32le(p + 1);
+                d = T.u32le(p + 1);
                 p += 5;
             }
             if (p > end) { O.st = ST_CORRUPT; return; }
@@ -370,39 +405,42 @@ __device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end
 // ── LZ4 block ──────────────────────────────────────────────────────────────
 template <class InX, class OutT>
 __device__ __forceinline__ void lz4_block(InX& I, OutT& O, uint32_t p, uint32_t end) {
+    TagWin<InX> T{&I};
     for (;;) {
         if (p >= end) { O.st = ST_CORRUPT; return; }
-        I.ensure(p, 1);
-        const uint32_t tok = uni(I.byte(p++));
+        T.need(p, 1);
+        const uint32_t tok = T.byte(p++);
         uint32_t n = tok >> 4;
         if (n == 15) {
             uint32_t b;
             do {
                 if (p >= end) { O.st = ST_CORRUPT; return; }
-                I.ensure(p, 1);
-                b = uni(I.byte(p++));
+                T.need(p, 1);
+                b = T.byte(p++);
                 n += b;
             } while (b == 255);
         }
+        n = uni(n);
         if (n > end - p) { O.st = ST_CORRUPT; return; }
         if (n) O.lit(I, p, n);
         if (O.st != ST_OK) return;
         p += n;
         if (p == end) return;  // the last sequence holds literals only
         if (end - p < 2) { O.st = ST_CORRUPT; return; }
-        I.ensure(p, 2);
-        const uint32_t d = uni(I.u16le(p));
+        T.need(p, 2);
+        const uint32_t d = T.u16le(p);
         p += 2;
         uint32_t m = tok & 15u;
         if (m == 15) {
             uint32_t b;
             do {
                 if (p >= end) { O.st = ST_CORRUPT; return; }
-                I.ensure(p, 1);
-                b = uni(I.byte(p++));
+                T.need(p, 1);
+                b = T.byte(p++);
                 m += b;
             } while (b == 255);
         }
+        m = uni(m);
         O.copy(d, m + 4);
         if (O.st != ST_OK) return;
     }
