@@ -42,6 +42,10 @@
 #include "kernels/zstd.hpp"
 #include "pq_gpu.h"
 
+#ifndef PQ_CODEC_PARSE_ONLY
+#define PQ_CODEC_PARSE_ONLY 0
+#endif
+
 namespace pqk {
 namespace {
 
@@ -378,7 +382,11 @@ __device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end
             }
             n = uni(n);
             if (p > end || n > end - p || n == 0) { O.st = ST_CORRUPT; return; }
+#if PQ_CODEC_PARSE_ONLY  // timing probe: the command stream parsed, nothing executed
+            O.op += n;
+#else
             O.lit(I, p, n);
+#endif
             p += n;
         } else {
             uint32_t n, d;
@@ -396,7 +404,11 @@ __device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end
                 p += 5;
             }
             if (p > end) { O.st = ST_CORRUPT; return; }
+#if PQ_CODEC_PARSE_ONLY
+            O.op += uni(n);
+#else
             O.copy(uni(d), uni(n));
+#endif
         }
     }
     if (O.st == ST_OK && O.op - O.vbase != expect) O.st = ST_SIZE;

@@ -13,7 +13,8 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "duckdb-parquet-parser_amd")]
+# AB_PKG: a directory holding another build's pqgpu package (probe builds)
+sys.path[:0] = [ROOT, os.environ.get("AB_PKG") or os.path.join(ROOT, "duckdb-parquet-parser_amd")]
 import numpy as np  # noqa: E402
 import pyarrow as pa  # noqa: E402
 import pyarrow.parquet as pq  # noqa: E402
@@ -57,8 +58,11 @@ for codec, ver, page in (("SNAPPY", "1.0", 1 << 20), ("SNAPPY", "1.0", 8192), ("
             ctx.timing(False)
             x.free()
         x = ctx.upload(cf, [d])
-        x.decode()
-        ok = hashlib.sha256(capi.canonical_dump(x.to_host())).hexdigest() == ref
+        try:
+            x.decode()
+            ok = hashlib.sha256(capi.canonical_dump(x.to_host())).hexdigest() == ref
+        except capi.PqError:  # timing probes leave invalid pages
+            ok = False
         ub = x.payload_bytes
         x.free()
         for k, (_, r) in opts.items():
