@@ -45,6 +45,9 @@
 #ifndef PQ_CODEC_PARSE_ONLY
 #define PQ_CODEC_PARSE_ONLY 0
 #endif
+#ifndef PQ_CODEC_EXEC_SKIP  // timing probe: the executor drains the command queue without running it
+#define PQ_CODEC_EXEC_SKIP 0
+#endif
 
 namespace pqk {
 namespace {
@@ -276,6 +279,14 @@ struct Out {
     template <class InX>
     __device__ __forceinline__ void lit(InX& I, uint32_t p, uint32_t n) {
         if (!room(n)) return;
+        if (n <= static_cast<uint32_t>(kWave)) {  // one step (most literals): no loop
+            I.ensure(p, n);
+            if (lane() < n) ring[(op + lane()) & kMask] = static_cast<uint8_t>(I.byte(p + lane()));
+            op += n;
+            wsync();
+            if (op - fl >= kFlush) flush(false);
+            return;
+        }
         for (uint32_t d = 0; d < n; d += kWave) {
             I.ensure(p + d, kWave);
             const uint32_t m = min(static_cast<uint32_t>(kWave), n - d);
@@ -290,6 +301,13 @@ struct Out {
     __device__ __forceinline__ void copy(uint32_t d, uint32_t n) {
         if (d == 0 || d > op - vbase || d > kRingB - 1) { st = ST_CORRUPT; return; }
         if (!room(n)) return;
+        if (n <= static_cast<uint32_t>(kWave) && d >= n) {  // one step, no overlap (most copies): no loop, no lane % d
+            if (lane() < n) ring[(op + lane()) & kMask] = ring[(op - d + lane()) & kMask];
+            op += n;
+            wsync();
+            if (op - fl >= kFlush) flush(false);
+            return;
+        }
         const uint32_t r = d >= static_cast<uint32_t>(kWave) ? lane() : lane() % d;
         for (uint32_t k = 0; k < n; k += kWave) {
             const uint32_t m = min(static_cast<uint32_t>(kWave), n - k);
@@ -472,6 +490,150 @@ __device__ __forceinline__ void lz4_hadoop(InX& I, OutT& O, uint32_t p, uint32_t
         if (O.st == ST_OK && O.op - o0 != raw) O.st = ST_SIZE;
         p += packed;
     }
+}
+
+// ── SNAPPY / LZ4: parse and execute on two waves ───────────────────────────
+// One wave alone is issue-bound on a page (one instruction per four clocks
+// and per wave, about half of them the serial parse: PQ_CODEC_PARSE_ONLY),
+// and a chunk of 1 MiB pages has a few hundred pages for 1,024 SIMDs.  So
+// the kind-0 kernel runs two waves per page: wave 0 parses the command
+// stream (snappy / lz4_block with a QSink as their output: the same checks
+// as Out's, on its own copy of the input) into a queue of command groups in
+// LDS, wave 1 executes them on the ring (Out::lit / Out::copy) as they come.
+constexpr uint32_t kQGroups = 4;              // groups of kWave commands in the queue
+constexpr uint32_t kSpinCap = 1u << 22;       // polls before a wave gives up (ST_CORRUPT): no hang
+enum : uint32_t { Q_PUB = 0, Q_DONE = 1, Q_END = 2, Q_ST = 3, Q_STOP = 4, Q_CTL = 8 };
+// record word 0: bytes | kCmdCopy | kCmdSlow; word 1: input position (literal) / distance (copy)
+constexpr uint32_t kCmdCopy = 1u << 31;
+constexpr uint32_t kCmdSlow = 1u << 30;       // longer than a wave step, or a copy overlapping itself
+constexpr uint32_t kCmdBytes = kCmdSlow - 1u;
+
+__device__ __forceinline__ uint32_t vload(const lds32* a) { return *reinterpret_cast<const volatile lds32*>(a); }
+__device__ __forceinline__ void vstore(lds32* a, uint32_t v) { *reinterpret_cast<volatile lds32*>(a) = v; }
+__device__ __forceinline__ void wg_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+__device__ __forceinline__ void wg_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
+
+// The parser's output: Out's interface (st, op, vbase, lit, copy) with
+// Out's checks, each command appended to the open group (lane k holds
+// command k), a full group published to the queue.
+struct QSink {
+    lds32* rec;       // kQGroups * kWave records of two words
+    lds32* ctl;
+    uint32_t ring;    // the executor's ring bytes (copies reach at most ring - 1 back)
+    uint32_t st = ST_OK;
+    uint32_t op, vbase, cap;
+    uint32_t k = 0, g = 0;  // commands in the open group; groups published
+    uint32_t rn = 0, rs = 0;
+    __device__ __forceinline__ bool publish() {
+        for (uint32_t spins = 0; g - vload(ctl + Q_DONE) >= kQGroups;) {
+            if (vload(ctl + Q_STOP) || ++spins > kSpinCap) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        wg_acquire();
+        const uint32_t slot = (g % kQGroups) * kWave + lane();
+        rec[2 * slot] = lane() < k ? rn : 0u;  // 0: no command (the group's end)
+        rec[2 * slot + 1] = rs;
+        wg_release();
+        g++;
+        if (lane() == 0) vstore(ctl + Q_PUB, g);
+        k = 0;
+        return true;
+    }
+    __device__ __forceinline__ void push(uint32_t w0, uint32_t w1) {
+        // (selects, not a branch on the lane: no exec-mask round trip through the scalar unit)
+        const bool mine = lane() == k;
+        rn = mine ? w0 : rn;
+        rs = mine ? w1 : rs;
+        if (++k == kWave && !publish()) st = ST_CORRUPT;
+    }
+    // (op <= cap holds throughout, so each check is one compare)
+    template <class InX>
+    __device__ __forceinline__ void lit(InX&, uint32_t p, uint32_t n) {
+        if (n > cap - op) { st = ST_SIZE; return; }
+        push(n | (n > static_cast<uint32_t>(kWave) ? kCmdSlow : 0u), p);
+        op += n;
+    }
+    __device__ __forceinline__ void copy(uint32_t d, uint32_t n) {
+        if (d - 1u >= min(op - vbase, ring - 1)) { st = ST_CORRUPT; return; }  // d in [1, min(history, ring - 1)]
+        if (n > cap - op) { st = ST_SIZE; return; }
+        if (n == 0) return;
+        push(n | kCmdCopy | (n > static_cast<uint32_t>(kWave) || d < n ? kCmdSlow : 0u), d);
+        op += n;
+    }
+    // the last group and the parse's status; Q_END after them
+    __device__ __forceinline__ void finish() {
+        if (k && !publish() && st == ST_OK) st = ST_CORRUPT;
+        if (lane() == 0) {
+            vstore(ctl + Q_ST, st);
+            wg_release();
+            vstore(ctl + Q_END, 1u);
+        }
+    }
+};
+
+// The executor: every published group, in order, until Q_END.
+template <class InX, class OutT>
+__device__ __forceinline__ void lz_execute(InX& I, OutT& O, const lds32* rec, lds32* ctl) {
+    uint32_t g = 0, spins = 0;
+    for (;;) {
+        const uint32_t pub = vload(ctl + Q_PUB);
+        if (g == pub) {
+            if (vload(ctl + Q_END)) {
+                wg_acquire();
+                if (vload(ctl + Q_PUB) == g) break;
+                continue;
+            }
+            if (++spins > kSpinCap) {
+                O.st = ST_CORRUPT;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        spins = 0;
+        wg_acquire();
+        const uint32_t slot = (g % kQGroups) * kWave + lane();
+        const uint32_t rn = rec[2 * slot], rs = rec[2 * slot + 1];
+        // The parser has checked every command against the same counts (QSink
+        // keeps Out's op), so a short command runs without checks and without
+        // a branch on its kind: one source address per lane (ring or staged
+        // input), one LDS read, one LDS write.
+        const uint32_t ring0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(O.ring));
+        const uint32_t in0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(I.w));
+#if PQ_CODEC_EXEC_SKIP
+        for (uint32_t j = 0; j < static_cast<uint32_t>(kWave); j++)  // the bytes only, so the size check passes
+            O.op += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rn), static_cast<int>(j))) & kCmdBytes;
+#endif
+        for (uint32_t j = 0; j < (PQ_CODEC_EXEC_SKIP ? 0u : static_cast<uint32_t>(kWave)) && O.st == ST_OK; j++) {
+            const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rn), static_cast<int>(j)));
+            if (w == 0) break;
+            const uint32_t a = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rs), static_cast<int>(j)));
+            const uint32_t n = w & kCmdBytes;
+            if (w & kCmdSlow) {
+                if (w & kCmdCopy) O.copy(a, n);
+                else O.lit(I, a, n);
+                continue;
+            }
+            const bool cp = (w & kCmdCopy) != 0;
+            if (!cp) I.ensure(a, n);
+            const uint32_t src = cp ? ring0 + ((O.op - a + lane()) & OutT::kMask) : in0 + (a + lane() - I.wlo + I.sh);
+            if (lane() < n) O.ring[(O.op + lane()) & OutT::kMask] = *reinterpret_cast<const lds8*>(static_cast<uintptr_t>(src));
+            O.op += n;
+            if (O.op - O.fl >= kFlush) {
+                wsync();
+                O.flush(false);
+            }
+        }
+        wsync();
+        g++;
+        if (lane() == 0) {
+            if (O.st != ST_OK) vstore(ctl + Q_STOP, 1u);
+            vstore(ctl + Q_DONE, g);
+        }
+    }
+    if (lane() == 0) vstore(ctl + Q_STOP, 1u);  // (a parser still waiting for room stops)
+    const uint32_t ps = vload(ctl + Q_ST);
+    if (O.st == ST_OK && vload(ctl + Q_END) && ps != ST_OK) O.st = ps;
 }
 
 // ── DEFLATE ────────────────────────────────────────────────────────────────
@@ -891,11 +1053,34 @@ struct ZOut {
 // launch takes one instantiation (launch_codec).  kSmall: the small-page
 // layout (SCodecLds / ZSCodecLds), over the entries whose payload is under
 // kSRing bytes; the full layout takes the rest (each launch skips the others).
+// The kind-0 layouts: the executor's ring and window where CodecLds /
+// SCodecLds have them, then the parser's window and the command queue.
+template <uint32_t kRingB, uint32_t kWinB, uint32_t kPWinB>
+struct LzLdsT {
+    uint8_t ring[kRingB];
+    uint8_t in[kWinB + 32];
+    uint8_t pin[kPWinB + 32];
+    uint32_t rec[2 * kQGroups * kWave];
+    uint32_t ctl[Q_CTL];
+};
+constexpr uint32_t kPWin = 2048;  // the parser's staged input (full layout): headers only
+using LzLds = LzLdsT<kRing, kInWin, kPWin>;
+using LzSLds = LzLdsT<kSRing, kSWin, kSWin>;
+static_assert(offsetof(LzLds, in) == offsetof(CodecLds, in) && offsetof(LzSLds, in) == offsetof(SCodecLds, in),
+              "kind 0 keeps the ring and window offsets");
+static_assert(offsetof(LzLds, rec) % 8 == 0 && offsetof(LzSLds, rec) % 8 == 0, "record alignment");
+static_assert(offsetof(LzLds, rec) - offsetof(LzLds, pin) == kPWin + 32 &&
+              offsetof(LzSLds, rec) - offsetof(LzSLds, pin) == kSWin + 32, "the parser's window and its staging size");
+
+template <int kKind>
+constexpr int codec_threads() { return kKind == 0 ? 2 * kWave : kWave; }
+
 template <int kKind, bool kSmall>
-__global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src, uint8_t* __restrict__ img,
+__global__ void __launch_bounds__(codec_threads<kKind>()) k_codec(const uint8_t* __restrict__ src, uint8_t* __restrict__ img,
                                                  const CodecEntry* __restrict__ ent, int32_t n,
                                                  uint32_t* __restrict__ status) {
     constexpr bool kGzip = kKind == 1, kZstd = kKind == 2;
+    constexpr bool kPipe = kKind == 0;  // SNAPPY / LZ4 on two waves (parser 0, executor 1)
     static_assert(!(kGzip && kSmall), "GZIP keeps the full layout (its Huffman tables)");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     CodecLds& L = *reinterpret_cast<CodecLds*>(smem);
@@ -916,9 +1101,44 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
         }
         wsync();
     }
+    using LL = typename std::conditional<kSmall, LzSLds, LzLds>::type;
+    lds32* qrec = (lds32*)(smem + offsetof(LL, rec));
+    lds32* qctl = (lds32*)(smem + offsetof(LL, ctl));
+    const uint32_t wv = kPipe ? threadIdx.x / kWave : 1u;
     for (int32_t i = static_cast<int32_t>(blockIdx.x); i < n; i += static_cast<int32_t>(gridDim.x)) {
         const CodecEntry e = ent[i];
         if (!kGzip && (e.out_len < kSRing) != kSmall) continue;  // the other layout's page
+        const bool lz = kPipe && (e.codec == 1 || e.codec == 5 || e.codec == 7);
+        if constexpr (kPipe) {
+            __syncthreads();  // both waves are done with the previous entry's queue
+            if (threadIdx.x == kWave)
+                for (uint32_t c = 0; c < Q_CTL; c++) vstore(qctl + c, 0u);
+            __syncthreads();
+            if (wv == 0) {  // the parser
+                if (lz) {
+                    using InP = InT<kSmall ? kSWin : kPWin>;  // (the size of LL::pin)
+                    InP Ip{src + e.src, e.src_len, 0u, 0u, (lds8*)(smem + offsetof(LL, pin))};
+                    Ip.refill(0);
+                    QSink Q{qrec, qctl, OutK::kRingSize};
+                    uint32_t p = 0, vb = 0;
+                    if (e.flags & kCodecV2) {  // (the executor writes the level sections)
+                        p = e.def_len + e.rep_len;
+                        vb = ((e.flags & kCodecDefPrefix) ? 4 + e.def_len : 0u) + ((e.flags & kCodecRepPrefix) ? 4 + e.rep_len : 0u);
+                        if (p > e.src_len) Q.st = ST_CORRUPT;
+                    }
+                    Q.op = vb;
+                    Q.vbase = vb;
+                    Q.cap = e.out_len;
+                    if (Q.st == ST_OK) {
+                        if (e.codec == 1) snappy(Ip, Q, p, e.src_len, e.out_len - vb);
+                        else if (e.codec == 5) lz4_hadoop(Ip, Q, p, e.src_len);
+                        else lz4_block(Ip, Q, p, e.src_len);
+                    }
+                    Q.finish();
+                }
+                continue;
+            }
+        }
         InK I{src + e.src, e.src_len, 0u, 0u, lin};
         I.refill(0);
         OutK O{lring, img + e.dst, 0u, 0u, e.out_len, 0u, ST_OK};
@@ -950,9 +1170,16 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
             } else {
                 switch (e.codec) {
                     case 0: O.lit(I, p, end - p); break;
-                    case 1: snappy(I, O, p, end, expect); break;
-                    case 5: lz4_hadoop(I, O, p, end); break;
-                    case 7: lz4_block(I, O, p, end); break;
+                    case 1: case 5: case 7:
+                        if constexpr (kPipe) {
+                            lz_execute(I, O, qrec, qctl);
+                            break;
+                        } else {
+                            if (e.codec == 1) snappy(I, O, p, end, expect);
+                            else if (e.codec == 5) lz4_hadoop(I, O, p, end);
+                            else lz4_block(I, O, p, end);
+                            break;
+                        }
                     case 6:
                         if constexpr (kZstd) {
                             // the tables after the ring and the window (this instantiation's launch only)
@@ -971,6 +1198,8 @@ __global__ void __launch_bounds__(kWave) k_codec(const uint8_t* __restrict__ src
                 }
             }
         }
+        if constexpr (kPipe)  // (a parser still waiting for room stops: e.g. a bad V2 prologue)
+            if (lz && lane() == 0) vstore(qctl + Q_STOP, 1u);
         if (O.st == ST_OK && O.op != e.out_len) O.st = ST_SIZE;
         if (O.st == ST_OK) O.flush(true);
         if (lane() == 0) status[i] = O.st;
@@ -987,9 +1216,9 @@ static void codec_launch(hipStream_t s, const uint8_t* src, uint8_t* img, const 
                          uint32_t* status, int cus, uint32_t lds, int32_t pages) {
     const void* k = reinterpret_cast<const void*>(k_codec<kKind, kSmall>);
     ensure_dyn_lds(k, lds);
-    const int per_cu = std::max(1, resident_blocks(k, kWave, lds));
+    const int per_cu = std::max(1, resident_blocks(k, codec_threads<kKind>(), lds));
     const int grid = std::min(std::max(pages, 1), std::max(1, cus) * per_cu);
-    hipLaunchKernelGGL((k_codec<kKind, kSmall>), dim3(grid), dim3(kWave), lds, s, src, img, ent, n, status);
+    hipLaunchKernelGGL((k_codec<kKind, kSmall>), dim3(grid), dim3(codec_threads<kKind>()), lds, s, src, img, ent, n, status);
 }
 
 void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEntry* ent, int32_t n,
@@ -1004,9 +1233,8 @@ void launch_codec(hipStream_t s, const uint8_t* src, uint8_t* img, const CodecEn
         if (nbig > 0) codec_launch<2, false>(s, src, img, ent, n, status, cus, sizeof(ZCodecLds), nbig);
     }
     if (kind == 0) {
-        if (nsmall > 0) codec_launch<0, true>(s, src, img, ent, n, status, cus, sizeof(SCodecLds), nsmall);
-        // (the full layout without the DEFLATE tables and the CRC table)
-        if (nbig > 0) codec_launch<0, false>(s, src, img, ent, n, status, cus, offsetof(CodecLds, lt), nbig);
+        if (nsmall > 0) codec_launch<0, true>(s, src, img, ent, n, status, cus, sizeof(LzSLds), nsmall);
+        if (nbig > 0) codec_launch<0, false>(s, src, img, ent, n, status, cus, sizeof(LzLds), nbig);
     }
 }
 
