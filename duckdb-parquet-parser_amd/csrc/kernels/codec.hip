@@ -48,6 +48,12 @@
 #ifndef PQ_CODEC_EXEC_SKIP  // timing probe: the executor drains the command queue without running it
 #define PQ_CODEC_EXEC_SKIP 0
 #endif
+#ifndef PQ_CODEC_PUSH_SKIP
+#define PQ_CODEC_PUSH_SKIP 0
+#endif
+#ifndef PQ_CODEC_CHECK_SKIP
+#define PQ_CODEC_CHECK_SKIP 0
+#endif
 
 namespace pqk {
 namespace {
@@ -540,7 +546,11 @@ struct QSink {
         return true;
     }
     __device__ __forceinline__ void push(uint32_t w0, uint32_t w1) {
-        // (selects, not a branch on the lane: no exec-mask round trip through the scalar unit)
+#if PQ_CODEC_PUSH_SKIP  // timing probe: commands checked, not queued
+        return;
+#endif
+        // (selects, not a branch on the lane: no exec-mask round trip through
+        // the scalar unit; v_writelane through M0 measured the same, r6t)
         const bool mine = lane() == k;
         rn = mine ? w0 : rn;
         rs = mine ? w1 : rs;
@@ -549,11 +559,19 @@ struct QSink {
     // (op <= cap holds throughout, so each check is one compare)
     template <class InX>
     __device__ __forceinline__ void lit(InX&, uint32_t p, uint32_t n) {
+#if PQ_CODEC_CHECK_SKIP  // timing probe: commands counted only
+        op += n;
+        return;
+#endif
         if (n > cap - op) { st = ST_SIZE; return; }
         push(n | (n > static_cast<uint32_t>(kWave) ? kCmdSlow : 0u), p);
         op += n;
     }
     __device__ __forceinline__ void copy(uint32_t d, uint32_t n) {
+#if PQ_CODEC_CHECK_SKIP
+        op += n;
+        return;
+#endif
         if (d - 1u >= min(op - vbase, ring - 1)) { st = ST_CORRUPT; return; }  // d in [1, min(history, ring - 1)]
         if (n > cap - op) { st = ST_SIZE; return; }
         if (n == 0) return;
@@ -600,10 +618,6 @@ __device__ __forceinline__ void lz_execute(InX& I, OutT& O, const lds32* rec, ld
         // input), one LDS read, one LDS write.
         const uint32_t ring0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(O.ring));
         const uint32_t in0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(I.w));
-#if PQ_CODEC_EXEC_SKIP
-        for (uint32_t j = 0; j < static_cast<uint32_t>(kWave); j++)  // the bytes only, so the size check passes
-            O.op += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rn), static_cast<int>(j))) & kCmdBytes;
-#endif
         for (uint32_t j = 0; j < (PQ_CODEC_EXEC_SKIP ? 0u : static_cast<uint32_t>(kWave)) && O.st == ST_OK; j++) {
             const uint32_t w = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rn), static_cast<int>(j)));
             if (w == 0) break;
@@ -631,6 +645,9 @@ __device__ __forceinline__ void lz_execute(InX& I, OutT& O, const lds32* rec, ld
             vstore(ctl + Q_DONE, g);
         }
     }
+#if PQ_CODEC_EXEC_SKIP
+    O.op = O.cap;  // (the size check passes; the output is not written)
+#endif
     if (lane() == 0) vstore(ctl + Q_STOP, 1u);  // (a parser still waiting for room stops)
     const uint32_t ps = vload(ctl + Q_ST);
     if (O.st == ST_OK && vload(ctl + Q_END) && ps != ST_OK) O.st = ps;
