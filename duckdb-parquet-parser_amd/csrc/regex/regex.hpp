@@ -67,7 +67,7 @@ struct DevDfa {
                                 // the state accepts at the string end
     uint32_t pad[2];
     uint32_t sink_lo, sink_hi;  // full tables: absorbing states (every byte stays), bit = state
-    uint32_t req;               // a byte every match contains (bits 0..7), bit 8: set (prefilter)
+    uint32_t pad2;
     uint32_t anchored;          // matches start at byte 0 only (the DFA dies early on most strings)
     uint8_t cls_of[256];        // byte -> class
 };

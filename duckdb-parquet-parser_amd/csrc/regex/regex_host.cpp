@@ -562,46 +562,6 @@ bool build_dfa(const Program& p, std::vector<uint8_t>* image) {
     if (overflow) return false;
     trans.resize(sets.size() * nc);
     for (auto& t : trans) t = entry(t & 0x7FFFu);
-    // a byte every match consumes (a prefilter: a string without it cannot
-    // match): a byte alone in its class whose transitions, removed, leave no
-    // accepting state reachable from START.  Kept only when it is rare in text
-    // (English letter frequency) and the pattern is not anchored at the start
-    // (an anchored DFA dies within a few bytes anyway)
-    uint32_t req = 0;
-    if (!p.empty_string && !p.nonempty_trivial && p.first_mid != 0) {
-        auto accepting = [&](size_t s) {
-            return s == DFA_ACCEPT || (s >= 3 && (sets[s] & p.accept_end) != 0);
-        };
-        static const char kFreq[] = " etaoinsrhldcumfpgwybvkxjqz";  // common -> rare
-        auto rarity = [&](int b) {
-            for (int i = 0; kFreq[i]; i++)
-                if (kFreq[i] == b) return i;
-            return (b >= 'A' && b <= 'Z') ? 18 : 20;  // capitals, digits, punctuation: rare in text
-        };
-        int best = -1, best_r = 15;  // 'p' (16) and rarer
-        std::vector<int> members(nc, 0);
-        for (int b = 0; b < 256; b++) members[cls_of[b]]++;
-        for (int b = 0; b < 256; b++) {
-            const uint32_t c = cls_of[b];
-            if (members[c] != 1 || rarity(b) <= best_r) continue;
-            std::vector<char> seen(sets.size(), 0);
-            std::vector<size_t> st = {DFA_START};
-            seen[DFA_START] = 1;
-            bool reach = false;
-            while (!st.empty() && !reach) {
-                const size_t s = st.back();
-                st.pop_back();
-                if (accepting(s)) { reach = true; break; }
-                for (uint32_t k = 0; k < nc; k++) {
-                    if (k == c) continue;
-                    const size_t t = trans[s * nc + k] & 0x7FFFu;
-                    if (!seen[t]) { seen[t] = 1; st.push_back(t); }
-                }
-            }
-            if (!reach) { best = b; best_r = rarity(b); }
-        }
-        if (best >= 0) req = static_cast<uint32_t>(best) | 0x100u;
-    }
     bool is_full = false;
     // few states: expand to one column per byte value (no class lookup on
     // the device's dependent chain)
@@ -632,7 +592,6 @@ bool build_dfa(const Program& p, std::vector<uint8_t>* image) {
         is_full = true;
     }
     DevDfa h{};
-    h.req = req;
     h.anchored = p.first_mid == 0 ? 1u : 0u;
     if (is_full) {  // absorbing states (the device stops a batch once every string sits in one)
         for (size_t st = 0; st < sets.size() && st < 64; st++) {
@@ -703,10 +662,10 @@ extern "C" int pq_regex_dfa_info(const char* pattern, int* nstates, int* nclasse
     return 0;
 }
 
-// The DFA's prefilter byte (test hook): 0x100 | byte when the scan skips the
-// DFA for strings without that byte, 0 when it runs every string; also the
-// absorbing-state masks.  PQ_ERR_REGEX / PQ_ERR_UNSUPPORTED as above.
-extern "C" int pq_regex_dfa_prefilter(const char* pattern, uint32_t* req, uint32_t* sink_lo, uint32_t* sink_hi) {
+// The DFA's absorbing-state masks (test hook; k_regex_plain<true> stops a
+// batch once every string sits in one).  PQ_ERR_REGEX / PQ_ERR_UNSUPPORTED
+// as above.
+extern "C" int pq_regex_dfa_sinks(const char* pattern, uint32_t* sink_lo, uint32_t* sink_hi) {
     pqre::Program p;
     std::string msg;
     if (pqre::compile(pattern ? pattern : "", &p, &msg)) return PQ_ERR_REGEX;
@@ -714,7 +673,6 @@ extern "C" int pq_regex_dfa_prefilter(const char* pattern, uint32_t* req, uint32
     if (!pqre::build_dfa(p, &img)) return PQ_ERR_UNSUPPORTED;
     pqre::DevDfa h;
     std::memcpy(&h, img.data(), sizeof h);
-    if (req) *req = h.req;
     if (sink_lo) *sink_lo = h.sink_lo;
     if (sink_hi) *sink_hi = h.sink_hi;
     return 0;

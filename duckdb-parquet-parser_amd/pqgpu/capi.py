@@ -126,8 +126,7 @@ def lib():
             "pq_regex_pages_result": ([vp, vp, vp], C.c_int),
             "pq_regex_match_host": ([C.c_char_p, u8p, C.c_size_t], C.c_int),
             "pq_regex_match_host_dfa": ([C.c_char_p, u8p, C.c_size_t], C.c_int),
-            "pq_regex_dfa_prefilter": ([C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
-                                        C.POINTER(C.c_uint32)], C.c_int),
+            "pq_regex_dfa_sinks": ([C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], C.c_int),
             "pq_timing_enable": ([vp, C.c_int], None),
             "pq_timing_reset": ([vp], None),
             "pq_timing_get": ([vp, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)], C.c_int),
@@ -474,11 +473,11 @@ def regex_match_host(pattern: str, s: bytes) -> int:
     return lib().pq_regex_match_host(pattern.encode(), _buf(s), len(s))
 
 
-def regex_dfa_prefilter(pattern: str):
-    """(rc, prefilter byte or None, absorbing-state mask) of the pattern's DFA."""
-    req, lo, hi = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
-    rc = lib().pq_regex_dfa_prefilter(pattern.encode(), C.byref(req), C.byref(lo), C.byref(hi))
-    return rc, (req.value & 0xFF) if req.value & 0x100 else None, (hi.value << 32) | lo.value
+def regex_dfa_sinks(pattern: str):
+    """(rc, absorbing-state mask) of the pattern's DFA."""
+    lo, hi = C.c_uint32(0), C.c_uint32(0)
+    rc = lib().pq_regex_dfa_sinks(pattern.encode(), C.byref(lo), C.byref(hi))
+    return rc, (hi.value << 32) | lo.value
 
 
 def regex_match_host_dfa(pattern: str, s: bytes) -> int:

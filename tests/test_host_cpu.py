@@ -85,31 +85,14 @@ def test_regex_dfa_matches_python_re(pattern):
 
 
 @pytest.mark.parametrize("pattern", PATTERNS + ["zebra|quartz", "x[0-9]q", "(?:jq|qj)k", "^q", "Q.*Z"])
-def test_regex_prefilter_byte_is_required(pattern):
-    """The windowed scan skips the DFA for strings without the DFA's
-    prefilter byte (a rare byte every match consumes): no string without it
-    may match, and the absorbing states the scan stops on are absorbing."""
-    rc, req, sinks = capi.regex_dfa_prefilter(pattern)
+def test_regex_dfa_sinks_absorb(pattern):
+    """The absorbing-state mask k_regex_plain<true> stops a batch on holds
+    DEAD and ACCEPT."""
+    rc, sinks = capi.regex_dfa_sinks(pattern)
     if rc == -8:
         pytest.skip("DFA over its size cap")
     assert rc == 0
     assert sinks & 0b11 == 0b11  # DEAD and ACCEPT
-    rx = re.compile(pattern, re.ASCII)
-    rng = random.Random(zlib.crc32(pattern.encode()))
-    alphabet = ALPHABET + "qQzZjk"
-    for _ in range(3000):
-        s = "".join(rng.choice(alphabet) for _ in range(rng.randrange(0, 14)))
-        if req is not None and req not in s.encode():  # (bytes: "é" is two)
-            assert rx.search(s) is None, (pattern, s)
-    if req is not None:  # only bytes rare in text ('p' and rarer; not lowercase, not the space)
-        assert chr(req) in "pgwybvkxjqz" or (not chr(req).islower() and req != 0x20)
-
-
-@pytest.mark.parametrize("pattern,req", [("special.*requests", "q"), ("q.u", "q"), ("e", None), ("[0-9]", None),
-                                         ("^(carefully|quickly) ", None), ("a|b", None), ("zebra|quartz", "z")])
-def test_regex_prefilter_choice(pattern, req):
-    rc, got, _ = capi.regex_dfa_prefilter(pattern)
-    assert rc == 0 and (None if got is None else chr(got)) == req
 
 
 @pytest.mark.parametrize("pattern,why", [
