@@ -1,4 +1,5 @@
 // reader.cpp — the C++ reader API (include/pqgpu/reader.hpp) over the C ABI.
+#include <sys/mman.h>
 #include "pqgpu/reader.hpp"
 
 #include <algorithm>
@@ -224,6 +225,16 @@ void prepare_values(std::vector<Value>& out, int64_t n, unsigned t, ToValuesPhas
     auto tp = std::chrono::steady_clock::now();
     out.clear();
     out.reserve(static_cast<size_t>(n));
+    // transparent huge pages for the storage (hundreds of MB for 10M values):
+    // a 2 MiB fault instead of 512 4 KiB ones, and a faster unmap when the
+    // caller frees the vector (no-op where THP is off)
+    {
+        const uintptr_t b = reinterpret_cast<uintptr_t>(out.data());
+        const uintptr_t e = b + static_cast<size_t>(n) * sizeof(Value);
+        constexpr uintptr_t kHuge = uintptr_t{2} << 20;
+        const uintptr_t hb = (b + kHuge - 1) & ~(kHuge - 1), he = e & ~(kHuge - 1);
+        if (he > hb) (void)madvise(reinterpret_cast<void*>(hb), he - hb, MADV_HUGEPAGE);
+    }
     P.reserve_ms = ms_since(tp);
     if (t > 1) {
         volatile char* raw = reinterpret_cast<volatile char*>(out.data());
