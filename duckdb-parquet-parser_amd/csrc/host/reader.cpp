@@ -38,6 +38,22 @@ const char* type_name(ParquetType t) {  // common.hpp:205-217
     }
 }
 
+// Storage of large host vectors on transparent huge pages: a 2 MiB fault
+// instead of 512 4 KiB ones (and a faster unmap when freed); a no-op where
+// THP is off or the range holds no whole huge page.
+static void advise_huge(const void* p, size_t bytes) {
+    constexpr uintptr_t kHuge = uintptr_t{2} << 20;
+    const uintptr_t b = reinterpret_cast<uintptr_t>(p), e = b + bytes;
+    const uintptr_t hb = (b + kHuge - 1) & ~(kHuge - 1), he = e & ~(kHuge - 1);
+    if (he > hb) (void)madvise(reinterpret_cast<void*>(hb), he - hb, MADV_HUGEPAGE);
+}
+template <class V>
+static void resize_huge(V& v, size_t n) {
+    v.reserve(n);
+    advise_huge(v.data(), n * sizeof(typename V::value_type));
+    v.resize(n);
+}
+
 // Decode `descs` (chunks of one column) on `dev`; returns host arrays and
 // optionally the walked page list.
 HostColumn decode_chunks(Device& dev, const uint8_t* file, size_t len, const std::vector<pq_chunk_desc>& descs,
@@ -59,8 +75,8 @@ HostColumn decode_chunks(Device& dev, const uint8_t* file, size_t len, const std
     h.num_rows = out.num_rows;
     h.validity.resize(static_cast<size_t>((out.num_rows + 31) / 32) + 1);
     h.validity.back() = 0;  // (the copy fills the others)
-    h.values.resize(static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)));
-    if (out.type == PQ_BYTE_ARRAY) h.offsets.resize(static_cast<size_t>(out.num_rows + 1));
+    resize_huge(h.values, static_cast<size_t>(std::max<int64_t>(out.num_bytes, 1)));
+    if (out.type == PQ_BYTE_ARRAY) resize_huge(h.offsets, static_cast<size_t>(out.num_rows + 1));
     rc = pq_column_copy_out(ctx, &out, h.validity.data(), h.values.data(),
                             h.offsets.empty() ? nullptr : h.offsets.data());
     h.values.resize(static_cast<size_t>(out.num_bytes));
@@ -225,16 +241,7 @@ void prepare_values(std::vector<Value>& out, int64_t n, unsigned t, ToValuesPhas
     auto tp = std::chrono::steady_clock::now();
     out.clear();
     out.reserve(static_cast<size_t>(n));
-    // transparent huge pages for the storage (hundreds of MB for 10M values):
-    // a 2 MiB fault instead of 512 4 KiB ones, and a faster unmap when the
-    // caller frees the vector (no-op where THP is off)
-    {
-        const uintptr_t b = reinterpret_cast<uintptr_t>(out.data());
-        const uintptr_t e = b + static_cast<size_t>(n) * sizeof(Value);
-        constexpr uintptr_t kHuge = uintptr_t{2} << 20;
-        const uintptr_t hb = (b + kHuge - 1) & ~(kHuge - 1), he = e & ~(kHuge - 1);
-        if (he > hb) (void)madvise(reinterpret_cast<void*>(hb), he - hb, MADV_HUGEPAGE);
-    }
+    advise_huge(out.data(), static_cast<size_t>(n) * sizeof(Value));  // (hundreds of MB for 10M values)
     P.reserve_ms = ms_since(tp);
     if (t > 1) {
         volatile char* raw = reinterpret_cast<volatile char*>(out.data());
