@@ -193,3 +193,56 @@ def test_ext_lz_command_shapes(ctx, tmp_path, codec, page):
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden", "ext"))
     from make_ext import canonical_dump
     assert sha(got) == sha(canonical_dump(pq.read_table(path).column("s")))
+
+
+@pytest.mark.skipif(pa is None, reason="pyarrow not importable")
+@pytest.mark.parametrize("codec", ["snappy", "lz4"])
+@pytest.mark.parametrize("page", [3000, 1 << 20])
+def test_ext_lz_mutants_vs_pyarrow(ctx, tmp_path, codec, page):
+    """Seeded damage to SNAPPY / LZ4 page payloads (byte flips, bursts of
+    one value, and a few bytes set to the 255 that extends LZ4 lengths),
+    through the two-wave parse/execute pass (codec.hip QSink / lz_execute):
+    every mutant ends in a clean error or a decode, never a fault or a hang;
+    where pyarrow also decodes the mutant, the values are equal (the formats
+    carry no checksum, so a damaged stream can be a valid one)."""
+    rng = np.random.default_rng(29)
+    words = ["special", "requests", "carefully", "quickly", "pending", "deposits", "the", "of", " "]
+    vals = [" ".join(rng.choice(words, int(rng.integers(1, 12)))) for _ in range(20000)]
+    path = tmp_path / f"mut_{codec}_{page}.parquet"
+    pq.write_table(pa.table({"s": pa.array(vals, pa.string())}), path, compression=codec.upper(),
+                   use_dictionary=False, data_page_size=page, write_statistics=False)
+    base = path.read_bytes()
+    rc, _, table = capi.build_page_table(base, ext_chunks(base, 0)[0])
+    assert rc == 0
+    pages = [q for q in table if q.page_type == 0 and q.payload_size > 64]
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden", "ext"))
+    from make_ext import canonical_dump
+    import io
+    both = errors = 0
+    for m in range(30):
+        f = bytearray(base)
+        p = pages[m % len(pages)]
+        kind = m % 3
+        for _ in range(1 + m % 4):
+            o = p.payload_offset + int(rng.integers(0, p.payload_size))
+            if kind == 0:
+                f[o] ^= int(rng.integers(1, 256))
+            elif kind == 1:
+                n = int(rng.integers(2, 40))
+                f[o:o + n] = bytes([int(rng.integers(0, 256))]) * len(f[o:o + n])
+            else:
+                f[o] = 0xFF
+        f = bytes(f)
+        try:
+            got = capi.canonical_dump(decode(ctx, f, 0))
+        except capi.PqError as e:
+            assert e.code in (-9, -2, -8), e
+            errors += 1
+            continue
+        try:
+            exp = canonical_dump(pq.read_table(io.BytesIO(f)).column("s"))
+        except Exception:  # pyarrow refuses it; ours decoded (no checksum to tell)
+            continue
+        both += 1
+        assert sha(got) == sha(exp), (codec, page, m)
+    assert errors > 0  # the damage reached the parsers
