@@ -76,23 +76,32 @@ struct Win {
         v = static_cast<int32_t>(static_cast<int64_t>((u >> 1) ^ (~(u & 1) + 1)));
         return true;
     }
-    // id = 0, type = 0 at STOP (a type nibble 0 ends the struct too: format.cpp FastHdr::field)
-    __device__ __forceinline__ bool field(int32_t& last, int32_t& id, uint32_t& type) {
+    // id = 0, type = 0 at STOP (a type nibble 0 ends the struct too: format.cpp FastHdr::field).
+    // Results by value: out-parameters of the callers' loop locals were kept
+    // in scratch (a global store and load per field, ~8 us per header hop)
+    struct Fld {
+        int32_t id, last;
+        uint32_t type;
+        bool ok;
+    };
+    __device__ __forceinline__ Fld field(int32_t last) {
+        Fld f{0, last, 0u, false};
         uint32_t b;
-        if (!byte(b)) return false;
-        if (b == 0) { id = 0; type = 0; return true; }
-        type = b & 0x0Fu;
+        if (!byte(b)) return f;
+        f.ok = true;
+        if (b == 0) return f;
+        f.type = b & 0x0Fu;
         const int32_t delta = static_cast<int32_t>((b >> 4) & 0x0Fu);
         if (delta) {
-            id = static_cast<int16_t>(last + delta);
+            f.id = static_cast<int16_t>(last + delta);
         } else {
             uint64_t u;
-            if (!varint(u)) return false;
-            id = static_cast<int16_t>(static_cast<int64_t>((u >> 1) ^ (~(u & 1) + 1)));
+            if (!varint(u)) { f.ok = false; return f; }
+            f.id = static_cast<int16_t>(static_cast<int64_t>((u >> 1) ^ (~(u & 1) + 1)));
         }
-        last = id;
-        if (type == 0) id = 0;
-        return true;
+        f.last = f.id;
+        if (f.type == 0) f.id = 0;
+        return f;
     }
     __device__ bool bytes(uint64_t n) {
         if (n > static_cast<uint64_t>(e - p)) return false;
@@ -159,11 +168,11 @@ struct Win {
                 if (sp == 0) return true;
                 const int f = sp - 1;
                 if (kind[f] == 0) {
-                    int32_t id;
-                    uint32_t ft;
-                    if (!field(lastid[f], id, ft)) return false;
-                    if (ft == 0 && id == 0) { sp--; continue; }
-                    t = ft;
+                    const Fld fd = field(lastid[f]);
+                    if (!fd.ok) return false;
+                    lastid[f] = fd.last;
+                    if (fd.type == 0 && fd.id == 0) { sp--; continue; }
+                    t = fd.type;
                     break;
                 }
                 if (rem[f] == 0) { sp--; continue; }
@@ -193,9 +202,11 @@ __device__ __forceinline__ bool dev_parse(lds8c* w, uint32_t avail, DHdr& h) {
     h = DHdr{0, 0, 0, 0, 0, 0, 0, 0};
     int32_t last = 0;
     for (;;) {
-        int32_t id;
-        uint32_t ty;
-        if (!c.field(last, id, ty)) return false;
+        const Win::Fld fd = c.field(last);
+        if (!fd.ok) return false;
+        last = fd.last;
+        const int32_t id = fd.id;
+        const uint32_t ty = fd.type;
         if (ty == 0 && id == 0) break;
         switch (id) {
             case 1: if (!c.i32(h.type)) return false; break;
@@ -208,9 +219,11 @@ __device__ __forceinline__ bool dev_parse(lds8c* w, uint32_t avail, DHdr& h) {
                 h.denc = 0;
                 int32_t l2 = 0;
                 for (;;) {
-                    int32_t i2;
-                    uint32_t t2;
-                    if (!c.field(l2, i2, t2)) return false;
+                    const Win::Fld f2 = c.field(l2);
+                    if (!f2.ok) return false;
+                    l2 = f2.last;
+                    const int32_t i2 = f2.id;
+                    const uint32_t t2 = f2.type;
                     if (t2 == 0 && i2 == 0) break;
                     int32_t x;
                     if (i2 == 1) { if (!c.i32(h.dnv)) return false; }
@@ -228,9 +241,11 @@ __device__ __forceinline__ bool dev_parse(lds8c* w, uint32_t avail, DHdr& h) {
                 h.flags |= 4u;
                 int32_t l2 = 0;
                 for (;;) {
-                    int32_t i2;
-                    uint32_t t2;
-                    if (!c.field(l2, i2, t2)) return false;
+                    const Win::Fld f2 = c.field(l2);
+                    if (!f2.ok) return false;
+                    l2 = f2.last;
+                    const int32_t i2 = f2.id;
+                    const uint32_t t2 = f2.type;
                     if (t2 == 0 && i2 == 0) break;
                     int32_t x;
                     if (t2 == 5 && (i2 == 1 || i2 == 4 || i2 == 5 || i2 == 6)) { if (!c.i32(x)) return false; }
@@ -244,9 +259,11 @@ __device__ __forceinline__ bool dev_parse(lds8c* w, uint32_t avail, DHdr& h) {
                 h.dictnv = 0;
                 int32_t l2 = 0;
                 for (;;) {
-                    int32_t i2;
-                    uint32_t t2;
-                    if (!c.field(l2, i2, t2)) return false;
+                    const Win::Fld f2 = c.field(l2);
+                    if (!f2.ok) return false;
+                    l2 = f2.last;
+                    const int32_t i2 = f2.id;
+                    const uint32_t t2 = f2.type;
                     if (t2 == 0 && i2 == 0) break;
                     int32_t x;
                     if (i2 == 1) { if (!c.i32(h.dictnv)) return false; }
@@ -309,14 +326,56 @@ struct WalkSeg {
 __global__ void __launch_bounds__(kWave) k_walk_seg(const uint8_t* __restrict__ d, uint64_t base, uint64_t len,
                                                     uint64_t start, uint64_t end, uint64_t seg, uint32_t nseg,
                                                     uint32_t cap, WalkRec* __restrict__ recs,
-                                                    WalkSeg* __restrict__ segs) {
+                                                    WalkSeg* __restrict__ segs, uint32_t stage_cap) {
     __shared__ uint32_t win_s[kWinStride + 3];
+    extern __shared__ __attribute__((aligned(16))) uint32_t seg_dyn[];
     lds32* win = (lds32*)win_s;
     const uint32_t k = blockIdx.x;
     if (k >= nseg) return;
     const uint32_t l = __lane_id();
     lds8c* wb = (lds8c*)win_s;
     const uint64_t lo = start + seg * k, hi = min(end, lo + seg);
+    // The segment and one header window past it, staged in LDS once (16-byte
+    // loads, zeros past the buffer): every hop inside it parses from LDS
+    // instead of waiting for a 260-byte load from HBM per header (a hop was
+    // ~10 us, almost all of it that load).  Positions outside (the start
+    // search past the segment, the three-page check) load their window.
+    const uint64_t rlo = (lo - base) & ~15ull;
+    uint32_t sbytes = 0;
+    if (stage_cap) {
+        sbytes = static_cast<uint32_t>(min<uint64_t>((hi - base) + kWin + 16 - rlo, stage_cap)) & ~15u;
+        lds32* sd = (lds32*)seg_dyn;
+        for (uint32_t b = l; b < sbytes / 16; b += kWave) {
+            const uint64_t q = rlo + 16ull * b;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (q + 16 <= len) {
+                v = *reinterpret_cast<const uint4*>(d + q);  // (the buffer is 16-byte aligned)
+            } else if (q < len) {  // the buffer's last bytes, zeros past them
+                uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+                for (uint32_t j = 0; j < 16 && q + j < len; j++) {
+                    const uint32_t x = static_cast<uint32_t>(d[q + j]) << (8 * (j & 3));
+                    if (j < 4) w0 |= x;
+                    else if (j < 8) w1 |= x;
+                    else if (j < 12) w2 |= x;
+                    else w3 |= x;
+                }
+                v = make_uint4(w0, w1, w2, w3);
+            }
+            sd[4 * b] = v.x;
+            sd[4 * b + 1] = v.y;
+            sd[4 * b + 2] = v.z;
+            sd[4 * b + 3] = v.w;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    // 256 bytes from pos: in the staged segment, else loaded into the window
+    lds8c* segb = (lds8c*)seg_dyn;
+    auto at = [&](uint64_t pos) -> lds8c* {
+        const uint64_t rel = pos - base;
+        if (rel >= rlo && rel + kWin <= rlo + sbytes) return segb + (rel - rlo);
+        return wb + load_win(win, d, base, len, pos);
+    };
     uint64_t pos = lo;
     DHdr h;
     if (k > 0) {
@@ -328,26 +387,27 @@ __global__ void __launch_bounds__(kWave) k_walk_seg(const uint8_t* __restrict__ 
         const uint64_t lim = min(hi, lo + kScanLimit);
         bool found = false;
         for (uint64_t c = lo; c < lim && !found; c += kWave) {
-            uint32_t o = load_win(win, d, base, len, c);
-            uint64_t m = __ballot(c + l < lim && wb[o + l] == 0x15u);
+            // a PageHeader opens with field 1 (an i32 in short form, 0x15),
+            // the page type's zigzag byte (0, 2, 4 or 6: types 0..3, as the
+            // plausibility rule requires) and field 2 (0x15): the three bytes
+            // reject almost every payload position before a parse is tried
+            // (a parse from a random 0x15 could run through hundreds of bytes)
+            lds8c* cw = at(c);
+            uint64_t m = __ballot(c + l < lim && cw[l] == 0x15u && (cw[l + 1] & 0xF9u) == 0u && cw[l + 2] == 0x15u);
             while (m && !found) {
                 const uint32_t b = static_cast<uint32_t>(__builtin_ctzll(m));
                 m &= m - 1;
                 const uint64_t p = c + b;
-                uint32_t op = load_win(win, d, base, len, p);  // 256 bytes from p
-                bool ok = dev_parse(wb + op, kWin, h) && dev_plausible(h, p, end);
+                bool ok = dev_parse(at(p), kWin, h) && dev_plausible(h, p, end);  // 256 bytes from p
                 uint64_t q = p + h.hs + static_cast<uint64_t>(h.comp);
                 for (int hop = 0; hop < 2 && ok && q < end; hop++) {
-                    const uint32_t oq = load_win(win, d, base, len, q);
                     DHdr h2;
-                    ok = dev_parse(wb + oq, kWin, h2) && dev_plausible(h2, q, end);
+                    ok = dev_parse(at(q), kWin, h2) && dev_plausible(h2, q, end);
                     if (ok) q += h2.hs + static_cast<uint64_t>(h2.comp);
                 }
                 if (ok) {
                     found = true;
                     pos = p;
-                } else if (m) {
-                    o = load_win(win, d, base, len, c);  // the chunk's window again for the next candidate
                 }
             }
         }
@@ -356,10 +416,9 @@ __global__ void __launch_bounds__(kWave) k_walk_seg(const uint8_t* __restrict__ 
     WalkRec* r = recs + static_cast<uint64_t>(k) * cap;
     uint32_t n = 0, fl = 0;
     while (pos < hi) {
-        const uint32_t o = load_win(win, d, base, len, pos);
         // a header reaching past the extent parsed zeros the host walk would
         // read as file bytes: refuse rather than emit a different table
-        if (!dev_parse(wb + o, kWin, h) || h.comp < 0 || pos + h.hs > end) { fl |= 2u; break; }
+        if (!dev_parse(at(pos), kWin, h) || h.comp < 0 || pos + h.hs > end) { fl |= 2u; break; }
         if (n == cap) { fl |= 1u; break; }
         if (l == 0) {
             WalkRec x;
@@ -594,8 +653,11 @@ __global__ void k_walk_emit(uint32_t cap, const WalkRec* __restrict__ recs, cons
 
 void launch_walk(hipStream_t s, const WalkLaunch& W) {
     const uint32_t nseg = W.nseg;
-    hipLaunchKernelGGL(k_walk_seg, dim3(nseg), dim3(kWave), 0, s, W.bytes, W.base, W.len, W.start,
-                       W.end, W.seg, nseg, W.cap, W.recs, reinterpret_cast<WalkSeg*>(W.segs));
+    // the segment staged in LDS when it is at most 32 KiB (+ one header window)
+    const uint32_t stage = W.seg <= 32768u ? static_cast<uint32_t>(W.seg) + kWin + 32 : 0u;
+    if (stage) ensure_dyn_lds(reinterpret_cast<const void*>(k_walk_seg), stage);
+    hipLaunchKernelGGL(k_walk_seg, dim3(nseg), dim3(kWave), stage, s, W.bytes, W.base, W.len, W.start,
+                       W.end, W.seg, nseg, W.cap, W.recs, reinterpret_cast<WalkSeg*>(W.segs), stage);
     hipLaunchKernelGGL(k_walk_link, dim3((nseg + 255) / 256), dim3(256), 0, s, W.start, W.seg, nseg, W.cap, W.recs,
                        reinterpret_cast<const WalkSeg*>(W.segs), reinterpret_cast<WalkLink*>(W.links));
     hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kScanThreads), 0, s, W.num_values, nseg, W.cap, W.recs,
