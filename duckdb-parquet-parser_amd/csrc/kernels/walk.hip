@@ -415,24 +415,89 @@ __global__ void __launch_bounds__(kWave) k_walk_seg(const uint8_t* __restrict__ 
     }
     WalkRec* r = recs + static_cast<uint64_t>(k) * cap;
     uint32_t n = 0, fl = 0;
-    while (pos < hi) {
+    auto emit = [&](uint64_t at_pos, const DHdr& x0) {
+        if (l == 0) {
+            WalkRec x;
+            x.pos = at_pos;
+            x.hs = x0.hs;
+            x.comp = x0.comp;
+            x.uncomp = x0.uncomp;
+            x.type = x0.type;
+            x.nv = x0.type == PQ_DICTIONARY_PAGE ? x0.dictnv : x0.dnv;
+            x.enc = x0.denc;
+            x.flags = x0.flags;
+            r[n] = x;
+        }
+        n++;
+    };
+    // Headers parsed 64 at a time, a lane each: every position of the staged
+    // segment that opens like a PageHeader (the three bytes of the start
+    // search) from the chain's position on is a candidate; the lanes parse
+    // their candidates at once and the chain then steps through them by
+    // position (one header parse per hop on the whole wave was ~5-7 us of
+    // serial latency).  A chain position that is not a candidate takes the
+    // one-wave parse below, which also reports a refused header.
+    __shared__ uint64_t cand[kWave];
+    auto rl64 = [](uint64_t v, uint32_t i) -> uint64_t {
+        return (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v >> 32), static_cast<int>(i)))) << 32) |
+               static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v)), static_cast<int>(i)));
+    };
+    auto rl32 = [](int32_t v, uint32_t i) -> int32_t { return __builtin_amdgcn_readlane(v, static_cast<int>(i)); };
+    while (pos < hi && !fl) {
+        const uint64_t rel0 = pos - base;
+        if (sbytes && rel0 >= rlo && hi - base + kWin <= rlo + sbytes) {
+            // up to 64 candidates from pos on (in position order)
+            const uint64_t pos_before = pos;
+            uint32_t got = 0;
+            for (uint64_t c0 = pos; c0 < hi && got < static_cast<uint32_t>(kWave); c0 += kWave) {
+                const uint64_t c = c0 + l;
+                lds8c* q = segb + (c - base - rlo);
+                const bool sig = c < hi && q[0] == 0x15u && (q[1] & 0xF9u) == 0u && q[2] == 0x15u;
+                const uint64_t m = __ballot(sig);
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+                if (sig && got + rank < static_cast<uint32_t>(kWave)) cand[got + rank] = c;
+                got += static_cast<uint32_t>(__builtin_popcountll(m));
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            const uint32_t nc = min(got, static_cast<uint32_t>(kWave));
+            const uint64_t mc = l < nc ? cand[l] : ~0ull;
+            DHdr hc{};
+            bool okc = false;
+            if (l < nc) okc = dev_parse(segb + (mc - base - rlo), kWin, hc) && hc.comp >= 0 && mc + hc.hs <= end;
+            // the chain through this batch
+            uint32_t j = 0;
+            bool miss = false;
+            while (pos < hi) {
+                while (j < nc && rl64(mc, j) < pos) j++;
+                if (j >= nc) break;             // past the batch: the next one from pos
+                if (rl64(mc, j) != pos) { miss = true; break; }
+                if (!__builtin_amdgcn_readlane(static_cast<int>(okc), static_cast<int>(j))) { fl |= 2u; break; }
+                if (n == cap) { fl |= 1u; break; }
+                DHdr x;
+                x.type = rl32(hc.type, j);
+                x.uncomp = rl32(hc.uncomp, j);
+                x.comp = rl32(hc.comp, j);
+                x.dnv = rl32(hc.dnv, j);
+                x.denc = rl32(hc.denc, j);
+                x.dictnv = rl32(hc.dictnv, j);
+                x.hs = static_cast<uint32_t>(rl32(static_cast<int32_t>(hc.hs), j));
+                x.flags = static_cast<uint32_t>(rl32(static_cast<int32_t>(hc.flags), j));
+                emit(pos, x);
+                pos += x.hs + static_cast<uint64_t>(x.comp);
+                j++;
+            }
+            if (fl || (!miss && pos != pos_before)) continue;
+            // (no candidate at or past pos, or pos is not one: one step below)
+        }
+        // one header on the whole wave (positions outside the staged segment
+        // or not opening like a candidate)
         // a header reaching past the extent parsed zeros the host walk would
         // read as file bytes: refuse rather than emit a different table
         if (!dev_parse(at(pos), kWin, h) || h.comp < 0 || pos + h.hs > end) { fl |= 2u; break; }
         if (n == cap) { fl |= 1u; break; }
-        if (l == 0) {
-            WalkRec x;
-            x.pos = pos;
-            x.hs = h.hs;
-            x.comp = h.comp;
-            x.uncomp = h.uncomp;
-            x.type = h.type;
-            x.nv = h.type == PQ_DICTIONARY_PAGE ? h.dictnv : h.dnv;
-            x.enc = h.denc;
-            x.flags = h.flags;
-            r[n] = x;
-        }
-        n++;
+        emit(pos, h);
         pos += h.hs + static_cast<uint64_t>(h.comp);
     }
     if (l == 0) segs[k] = WalkSeg{pos, n, fl};
