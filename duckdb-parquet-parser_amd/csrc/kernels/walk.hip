@@ -673,44 +673,69 @@ __global__ void __launch_bounds__(kScanThreads) k_walk_scan(int64_t num_values, 
     }
 }
 
-__global__ void k_walk_emit(uint32_t cap, const WalkRec* __restrict__ recs, const WalkSeg* __restrict__ segs,
+// A wave per segment, a lane per record: the page's first row is an
+// exclusive scan of the records' values, the dictionary in force an
+// inclusive max-scan of the dictionary pages' indices (one thread walking a
+// segment's records paid a dependent global load per record).
+constexpr int kEmitWaves = 4;
+__global__ void __launch_bounds__(kEmitWaves * kWave) k_walk_emit(uint32_t cap, const WalkRec* __restrict__ recs, const WalkSeg* __restrict__ segs,
                             const WalkLink* __restrict__ links, const int64_t* __restrict__ base_pg,
                             const int64_t* __restrict__ base_val, const int64_t* __restrict__ dict_in,
                             const int64_t* __restrict__ out, pq_page_desc* __restrict__ pages) {
     const int64_t npages = out[0];
     const int64_t K = out[1];
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t k = blockIdx.x * kEmitWaves + threadIdx.x / kWave;
+    const uint32_t ln = __lane_id();
     if (npages < 0 || static_cast<int64_t>(k) > K) return;
     const WalkLink L = links[k];
     if (L.entry < 0) return;
     const WalkRec* r = recs + static_cast<uint64_t>(k) * cap;
     const uint32_t n = segs[k].n;
-    int64_t idx = base_pg[k], row = base_val[k], d = dict_in[k];
-    for (uint32_t j = static_cast<uint32_t>(L.entry); j < n && idx < npages; j++, idx++) {
-        const WalkRec& x = r[j];
-        int64_t v;
-        bool bad;
-        const uint32_t kd = rec_kind(x, &v, &bad);
-        pq_page_desc p{};
-        p.header_offset = static_cast<int64_t>(x.pos);
-        p.payload_offset = static_cast<int64_t>(x.pos + x.hs);
-        p.payload_size = x.comp;
-        p.page_type = x.type;
-        p.first_row = row;
-        p.page_num = -1;
-        p.uncompressed_size = x.uncomp;
-        if (kd == 1) {
-            d = idx;
-            p.num_values = x.nv;
-            p.page_num = static_cast<int32_t>(idx);
-        } else if (kd == 2) {
-            p.num_values = x.nv;
-            p.encoding = x.enc;
-            p.page_num = static_cast<int32_t>(idx);
+    int64_t idx0 = base_pg[k], row = base_val[k], d = dict_in[k];
+    for (uint32_t j0 = static_cast<uint32_t>(L.entry); j0 < n && idx0 < npages; j0 += kWave, idx0 += kWave) {
+        const uint32_t j = j0 + ln;
+        const int64_t idx = idx0 + ln;
+        const bool act = j < n && idx < npages;
+        WalkRec x{};
+        int64_t v = 0;
+        uint32_t kd = 0;
+        if (act) {
+            x = r[j];
+            bool bad;
+            kd = rec_kind(x, &v, &bad);
         }
-        p.dict_page = static_cast<int32_t>(d);
-        row += v;
-        pages[idx] = p;
+        int64_t inc = v, dm = (act && kd == 1) ? idx : -1;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const int64_t a = __shfl_up(inc, static_cast<unsigned>(o));
+            const int64_t b = __shfl_up(dm, static_cast<unsigned>(o));
+            if (ln >= static_cast<uint32_t>(o)) {
+                inc += a;
+                dm = max(dm, b);
+            }
+        }
+        if (act) {
+            pq_page_desc p{};
+            p.header_offset = static_cast<int64_t>(x.pos);
+            p.payload_offset = static_cast<int64_t>(x.pos + x.hs);
+            p.payload_size = x.comp;
+            p.page_type = x.type;
+            p.first_row = row + inc - v;
+            p.page_num = -1;
+            p.uncompressed_size = x.uncomp;
+            if (kd == 1) {
+                p.num_values = x.nv;
+                p.page_num = static_cast<int32_t>(idx);
+            } else if (kd == 2) {
+                p.num_values = x.nv;
+                p.encoding = x.enc;
+                p.page_num = static_cast<int32_t>(idx);
+            }
+            p.dict_page = static_cast<int32_t>(max(d, dm));
+            pages[idx] = p;
+        }
+        row += __shfl(inc, kWave - 1);
+        d = max(d, __shfl(dm, kWave - 1));
     }
 }
 
@@ -728,7 +753,7 @@ void launch_walk(hipStream_t s, const WalkLaunch& W) {
     hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kScanThreads), 0, s, W.num_values, nseg, W.cap, W.recs,
                        reinterpret_cast<const WalkSeg*>(W.segs), reinterpret_cast<const WalkLink*>(W.links), W.base_pg,
                        W.base_val, W.dict_in, W.out);
-    hipLaunchKernelGGL(k_walk_emit, dim3((nseg + 255) / 256), dim3(256), 0, s, W.cap, W.recs,
+    hipLaunchKernelGGL(k_walk_emit, dim3((nseg + kEmitWaves - 1) / kEmitWaves), dim3(kEmitWaves * kWave), 0, s, W.cap, W.recs,
                        reinterpret_cast<const WalkSeg*>(W.segs), reinterpret_cast<const WalkLink*>(W.links), W.base_pg,
                        W.base_val, W.dict_in, W.out, W.pages);
 }
