@@ -532,9 +532,11 @@ __device__ uint32_t rec_kind(const WalkRec& x, int64_t* v, bool* bad) {  // form
 
 constexpr uint32_t kMaxSkip = 64;  // segments a page may span (a longer page refuses)
 
-__global__ void k_walk_link(uint64_t start, uint64_t seg, uint32_t nseg, uint32_t cap, const WalkRec* __restrict__ recs,
+constexpr int kLinkWaves = 4;  // a wave per segment
+__global__ void __launch_bounds__(kLinkWaves * kWave) k_walk_link(uint64_t start, uint64_t seg, uint32_t nseg, uint32_t cap, const WalkRec* __restrict__ recs,
                             const WalkSeg* __restrict__ segs, WalkLink* __restrict__ links) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t k = blockIdx.x * kLinkWaves + threadIdx.x / kWave;
+    const uint32_t ln = __lane_id();
     if (k >= nseg) return;
     const WalkSeg S = segs[k];
     const WalkRec* r = recs + static_cast<uint64_t>(k) * cap;
@@ -555,26 +557,49 @@ __global__ void k_walk_link(uint64_t start, uint64_t seg, uint32_t nseg, uint32_
     if (have && expect >= hi) {  // inside a page that covers the segment
         L.entry = S.n == 0 ? -1 : -2;
     } else if (have && expect >= lo && !(S.flags & 1u)) {
-        uint32_t a = 0, b = S.n;  // lower_bound
-        while (a < b) {
-            const uint32_t m = (a + b) / 2;
-            if (r[m].pos < expect) a = m + 1;
-            else b = m;
+        // the record at `expect` (records are in position order), then the
+        // chain's values, its first invalid page and last dictionary page from
+        // there, a lane per record
+        int32_t entry = -1;
+        for (uint32_t a0 = 0; a0 < S.n; a0 += kWave) {
+            const uint32_t a = a0 + ln;
+            const uint64_t p = a < S.n ? r[a].pos : ~0ull;
+            const uint64_t m = __ballot(p >= expect);
+            if (m) {
+                const uint32_t f = static_cast<uint32_t>(__builtin_ctzll(m));
+                const uint64_t pf = (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(p >> 32), static_cast<int>(f)))) << 32) |
+                                    static_cast<uint32_t>(__shfl(static_cast<int>(static_cast<uint32_t>(p)), static_cast<int>(f)));
+                if (pf == expect) entry = static_cast<int32_t>(a0 + f);
+                break;
+            }
         }
-        if (a < S.n && r[a].pos == expect) {
-            L.entry = static_cast<int32_t>(a);
-            L.pages = static_cast<int32_t>(S.n - a);
-            for (uint32_t j = a; j < S.n; j++) {
-                int64_t v;
-                bool bad;
-                const uint32_t kd = rec_kind(r[j], &v, &bad);
-                if (bad) { L.bad = static_cast<int32_t>(j - a); break; }
-                L.values += v;
-                if (kd == 1) L.last_dict = static_cast<int32_t>(j - a);
+        if (entry >= 0) {
+            L.entry = entry;
+            L.pages = static_cast<int32_t>(S.n - static_cast<uint32_t>(entry));
+            for (uint32_t j0 = static_cast<uint32_t>(entry); j0 < S.n; j0 += kWave) {
+                const uint32_t j = j0 + ln;
+                const bool act = j < S.n;
+                int64_t v = 0;
+                bool bad = false;
+                uint32_t kd = 0;
+                if (act) kd = rec_kind(r[j], &v, &bad);
+                const uint64_t mb = __ballot(act && bad);
+                const uint32_t lim = mb ? static_cast<uint32_t>(__builtin_ctzll(mb)) : static_cast<uint32_t>(kWave);
+                const bool take = act && ln < lim;
+                int64_t sv = take ? v : 0;
+#pragma unroll
+                for (int o = 1; o < kWave; o <<= 1) sv += __shfl_xor(sv, o);
+                L.values += sv;
+                const uint64_t md = __ballot(take && kd == 1);
+                if (md) L.last_dict = static_cast<int32_t>(j0 + 63u - static_cast<uint32_t>(__builtin_clzll(md)) - static_cast<uint32_t>(entry));
+                if (mb) {
+                    L.bad = static_cast<int32_t>(j0 + lim - static_cast<uint32_t>(entry));
+                    break;
+                }
             }
         }
     }
-    links[k] = L;
+    if (ln == 0) links[k] = L;
 }
 
 // One workgroup: prefixes over the segments, the cut, the dictionary in force.
@@ -748,7 +773,7 @@ void launch_walk(hipStream_t s, const WalkLaunch& W) {
     if (stage) ensure_dyn_lds(reinterpret_cast<const void*>(k_walk_seg), stage);
     hipLaunchKernelGGL(k_walk_seg, dim3(nseg), dim3(kWave), stage, s, W.bytes, W.base, W.len, W.start,
                        W.end, W.seg, nseg, W.cap, W.recs, reinterpret_cast<WalkSeg*>(W.segs), stage);
-    hipLaunchKernelGGL(k_walk_link, dim3((nseg + 255) / 256), dim3(256), 0, s, W.start, W.seg, nseg, W.cap, W.recs,
+    hipLaunchKernelGGL(k_walk_link, dim3((nseg + kLinkWaves - 1) / kLinkWaves), dim3(kLinkWaves * kWave), 0, s, W.start, W.seg, nseg, W.cap, W.recs,
                        reinterpret_cast<const WalkSeg*>(W.segs), reinterpret_cast<WalkLink*>(W.links));
     hipLaunchKernelGGL(k_walk_scan, dim3(1), dim3(kScanThreads), 0, s, W.num_values, nseg, W.cap, W.recs,
                        reinterpret_cast<const WalkSeg*>(W.segs), reinterpret_cast<const WalkLink*>(W.links), W.base_pg,
