@@ -39,12 +39,10 @@
 
 #include "kernels/device_common.hpp"
 #include "kernels/kernels.hpp"
+#include "kernels/lz.hpp"
 #include "kernels/zstd.hpp"
 #include "pq_gpu.h"
 
-#ifndef PQ_CODEC_PARSE_ONLY
-#define PQ_CODEC_PARSE_ONLY 0
-#endif
 #ifndef PQ_CODEC_EXEC_SKIP  // timing probe: the executor drains the command queue without running it
 #define PQ_CODEC_EXEC_SKIP 0
 #endif
@@ -376,126 +374,22 @@ struct TagWin {
     __device__ __forceinline__ uint32_t u32le(uint32_t q) const {
         return byte(q) | (byte(q + 1) << 8) | (byte(q + 2) << 16) | (byte(q + 3) << 24);
     }
+    static __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 };
 
-// ── SNAPPY ─────────────────────────────────────────────────────────────────
+// ── SNAPPY / LZ4 parsers (lz.hpp), headers through TagWin ─────────────────
+static_assert(pqlz::ST_OK == ST_OK && pqlz::ST_CORRUPT == ST_CORRUPT && pqlz::ST_SIZE == ST_SIZE, "status codes");
 template <class InX, class OutT>
 __device__ __forceinline__ void snappy(InX& I, OutT& O, uint32_t p, uint32_t end, uint32_t expect) {
-    uint32_t ulen = 0;
-    I.ensure(p, 8);
-    for (uint32_t k = 0;; k++) {
-        if (k == 5 || p >= end) { O.st = ST_CORRUPT; return; }
-        const uint32_t b = I.byte(p++);
-        ulen |= (b & 0x7Fu) << (7 * k);
-        if (!(b & 0x80u)) break;
-    }
-    if (ulen != expect) { O.st = ST_SIZE; return; }
-    TagWin<InX> T{&I};
-    while (p < end && O.st == ST_OK) {
-        T.need(p, 5);  // the longest header: a tag and four bytes
-        const uint32_t t = T.byte(p);
-        const uint32_t ty = t & 3u;
-        if (ty == 0) {
-            uint32_t n = (t >> 2) + 1;
-            p += 1;
-            if (n > 60) {
-                const uint32_t nb = n - 60;
-                const uint32_t x = T.u32le(p);
-                n = (nb == 4 ? x : (x & ((1u << (8 * nb)) - 1u))) + 1;
-                p += nb;
-            }
-            n = uni(n);
-            if (p > end || n > end - p || n == 0) { O.st = ST_CORRUPT; return; }
-#if PQ_CODEC_PARSE_ONLY  // timing probe: the command stream parsed, nothing executed
-            O.op += n;
-#else
-            O.lit(I, p, n);
-#endif
-            p += n;
-        } else {
-            uint32_t n, d;
-            if (ty == 1) {
-                n = 4 + ((t >> 2) & 7u);
-                d = ((t >> 5) << 8) | T.byte(p + 1);
-                p += 2;
-            } else if (ty == 2) {
-                n = (t >> 2) + 1;
-                d = T.u16le(p + 1);
-                p += 3;
-            } else {
-                n = (t >> 2) + 1;
-                d = T.u32le(p + 1);
-                p += 5;
-            }
-            if (p > end) { O.st = ST_CORRUPT; return; }
-#if PQ_CODEC_PARSE_ONLY
-            O.op += uni(n);
-#else
-            O.copy(uni(d), uni(n));
-#endif
-        }
-    }
-    if (O.st == ST_OK && O.op - O.vbase != expect) O.st = ST_SIZE;
+    pqlz::snappy<TagWin<InX>>(I, O, p, end, expect);
 }
-
-// ── LZ4 block ──────────────────────────────────────────────────────────────
 template <class InX, class OutT>
 __device__ __forceinline__ void lz4_block(InX& I, OutT& O, uint32_t p, uint32_t end) {
-    TagWin<InX> T{&I};
-    for (;;) {
-        if (p >= end) { O.st = ST_CORRUPT; return; }
-        T.need(p, 1);
-        const uint32_t tok = T.byte(p++);
-        uint32_t n = tok >> 4;
-        if (n == 15) {
-            uint32_t b;
-            do {
-                if (p >= end) { O.st = ST_CORRUPT; return; }
-                T.need(p, 1);
-                b = T.byte(p++);
-                n += b;
-            } while (b == 255);
-        }
-        n = uni(n);
-        if (n > end - p) { O.st = ST_CORRUPT; return; }
-        if (n) O.lit(I, p, n);
-        if (O.st != ST_OK) return;
-        p += n;
-        if (p == end) return;  // the last sequence holds literals only
-        if (end - p < 2) { O.st = ST_CORRUPT; return; }
-        T.need(p, 2);
-        const uint32_t d = T.u16le(p);
-        p += 2;
-        uint32_t m = tok & 15u;
-        if (m == 15) {
-            uint32_t b;
-            do {
-                if (p >= end) { O.st = ST_CORRUPT; return; }
-                T.need(p, 1);
-                b = T.byte(p++);
-                m += b;
-            } while (b == 255);
-        }
-        m = uni(m);
-        O.copy(d, m + 4);
-        if (O.st != ST_OK) return;
-    }
+    pqlz::lz4_block<TagWin<InX>>(I, O, p, end);
 }
-
-// Hadoop framing (codec LZ4): blocks of [u32 BE raw bytes][u32 BE packed bytes][LZ4 block].
 template <class InX, class OutT>
 __device__ __forceinline__ void lz4_hadoop(InX& I, OutT& O, uint32_t p, uint32_t end) {
-    while (p < end && O.st == ST_OK) {
-        if (end - p < 8) { O.st = ST_CORRUPT; return; }
-        I.ensure(p, 8);
-        const uint32_t raw = uni(I.u32be(p)), packed = uni(I.u32be(p + 4));
-        p += 8;
-        if (packed > end - p) { O.st = ST_CORRUPT; return; }
-        const uint32_t o0 = O.op;
-        lz4_block(I, O, p, p + packed);
-        if (O.st == ST_OK && O.op - o0 != raw) O.st = ST_SIZE;
-        p += packed;
-    }
+    pqlz::lz4_hadoop<TagWin<InX>>(I, O, p, end);
 }
 
 // ── SNAPPY / LZ4: parse and execute on two waves ───────────────────────────

@@ -24,6 +24,11 @@
 //       tools/zstd_check.cpp's host harness) must decode the clean frame to
 //       exactly that size, then every mutant (1-4 flipped bytes, a cut tail,
 //       a short output buffer) must end in a status, never a fault.
+//   lz     <seed> <iters> <file>...
+//       Each file: [u32 codec][u32 decompressed size][payload], codec 1
+//       SNAPPY, 5 LZ4 (Hadoop framing) or 7 LZ4_RAW: the codec pass's parsers
+//       (csrc/kernels/lz.hpp through tools/lz_check.cpp, with k_codec's queue
+//       checks), the same clean-then-mutants rule as zstd.
 //   threads <seed> <iters> <file>...
 //       Speculative walks of several files from several host threads at
 //       once (the process-wide walk pool and its busy fallback; ThreadSanitizer
@@ -258,25 +263,34 @@ int fuzz_threads(uint64_t seed, int iters, int nfiles, char** files) {
 }  // namespace
 
 extern "C" int zs_decompress(const uint8_t* src, uint32_t len, uint8_t* dst, uint32_t cap, uint32_t* out_len);
+extern "C" int lz_decompress(int codec, const uint8_t* src, uint32_t len, uint8_t* dst, uint32_t cap, uint32_t ring,
+                             uint32_t* out_len);
 
-int fuzz_zstd(uint64_t seed, int iters, int nfiles, char** files) {
+// The clean payload of each file must decode to exactly its size, then every
+// mutant (1-4 flipped bytes, a cut tail, a short output buffer) must end in a
+// status with no more bytes written than the output holds.  `hdr`: the file's
+// u32 header words ([size] for zstd, [codec][size] for lz); dec(hdr, src, len,
+// dst, cap, out_len) decodes one payload.
+template <class Dec>
+int fuzz_payloads(const char* name, uint64_t seed, int iters, int nfiles, char** files, int hdr, Dec&& dec) {
     std::mt19937_64 rng(seed);
     long mutants = 0, rejected = 0;
     for (int fi = 0; fi < nfiles; fi++) {
         std::ifstream in(files[fi], std::ios::binary);
         std::vector<uint8_t> f((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
-        if (f.size() < 4) return 3;
-        uint32_t want = 0;
-        std::memcpy(&want, f.data(), 4);
-        const std::vector<uint8_t> clean(f.begin() + 4, f.end());
+        if (f.size() < static_cast<size_t>(4 * hdr)) return 3;
+        uint32_t h[2] = {0, 0};
+        std::memcpy(h, f.data(), 4 * static_cast<size_t>(hdr));
+        const uint32_t want = h[hdr - 1];
+        const std::vector<uint8_t> clean(f.begin() + 4 * hdr, f.end());
         std::vector<uint8_t> out(static_cast<size_t>(want) + 16);
         uint32_t ol = 0;
         // (exact-size heap buffers, so ASan sees any read or write past them)
         {
             std::vector<uint8_t> src(clean);
-            const int rc = zs_decompress(src.data(), static_cast<uint32_t>(src.size()), out.data(), want, &ol);
+            const int rc = dec(h, src.data(), static_cast<uint32_t>(src.size()), out.data(), want, &ol);
             if (rc != 0 || ol != want) {
-                std::printf("clean frame %s: rc %d, %u of %u bytes\n", files[fi], rc, ol, want);
+                std::printf("clean payload %s: rc %d, %u of %u bytes\n", files[fi], rc, ol, want);
                 return 1;
             }
         }
@@ -285,13 +299,14 @@ int fuzz_zstd(uint64_t seed, int iters, int nfiles, char** files) {
             const int kind = static_cast<int>(rng() % 8);
             if (kind == 0 && m.size() > 1) {
                 m.resize(1 + rng() % (m.size() - 1));  // a cut tail
-            } else {
+            } else if (!m.empty()) {
                 const int flips = 1 + static_cast<int>(rng() % 4);
                 for (int k = 0; k < flips; k++) m[rng() % m.size()] = static_cast<uint8_t>(rng());
             }
             const uint32_t cap = kind == 1 ? static_cast<uint32_t>(rng() % (want + 1)) : want;
             std::vector<uint8_t> dst(static_cast<size_t>(cap) + 1);
-            const int rc = zs_decompress(m.data(), static_cast<uint32_t>(m.size()), dst.data(), cap, &ol);
+            ol = 0;
+            const int rc = dec(h, m.data(), static_cast<uint32_t>(m.size()), dst.data(), cap, &ol);
             if (ol > cap) {
                 std::printf("mutant wrote %u bytes into %u\n", ol, cap);
                 return 1;
@@ -300,13 +315,29 @@ int fuzz_zstd(uint64_t seed, int iters, int nfiles, char** files) {
             rejected += rc != 0;
         }
     }
-    std::printf("zstd: %ld mutants, %ld rejected, no fault\n", mutants, rejected);
+    std::printf("%s: %ld mutants, %ld rejected, no fault\n", name, mutants, rejected);
     return 0;
+}
+
+int fuzz_zstd(uint64_t seed, int iters, int nfiles, char** files) {
+    return fuzz_payloads("zstd", seed, iters, nfiles, files, 1,
+                         [](const uint32_t*, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap, uint32_t* ol) {
+                             return zs_decompress(s, n, d, cap, ol);
+                         });
+}
+
+// both of k_codec's history sizes: the 64 KiB ring and the small-page 8 KiB one
+int fuzz_lz(uint64_t seed, int iters, int nfiles, char** files) {
+    return fuzz_payloads("lz", seed, iters, nfiles, files, 2,
+                         [](const uint32_t* h, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap, uint32_t* ol) {
+                             const uint32_t ring = cap < 8192 ? 8192u : 65536u;
+                             return lz_decompress(static_cast<int>(h[0]), s, n, d, cap, ring, ol);
+                         });
 }
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: %s walk|regex|threads|zstd <seed> <iters> [file...]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s walk|regex|threads|zstd|lz <seed> <iters> [file...]\n", argv[0]);
         return 2;
     }
     const std::string mode = argv[1];
@@ -316,5 +347,6 @@ int main(int argc, char** argv) {
     if (mode == "regex") return fuzz_regex(seed, iters);
     if (mode == "threads") return fuzz_threads(seed, iters, argc - 4, argv + 4);
     if (mode == "zstd") return fuzz_zstd(seed, iters, argc - 4, argv + 4);
+    if (mode == "lz") return fuzz_lz(seed, iters, argc - 4, argv + 4);
     return 2;
 }
