@@ -29,6 +29,10 @@
 //       SNAPPY, 5 LZ4 (Hadoop framing) or 7 LZ4_RAW: the codec pass's parsers
 //       (csrc/kernels/lz.hpp through tools/lz_check.cpp, with k_codec's queue
 //       checks), the same clean-then-mutants rule as zstd.
+//   gzip   <seed> <iters> <file>...
+//       Each file: [u32 decompressed size][GZIP members or a zlib stream]:
+//       the codec pass's DEFLATE decoder (csrc/kernels/deflate.hpp through
+//       tools/gzip_check.cpp), the same rule as zstd.
 //   threads <seed> <iters> <file>...
 //       Speculative walks of several files from several host threads at
 //       once (the process-wide walk pool and its busy fallback; ThreadSanitizer
@@ -263,6 +267,7 @@ int fuzz_threads(uint64_t seed, int iters, int nfiles, char** files) {
 }  // namespace
 
 extern "C" int zs_decompress(const uint8_t* src, uint32_t len, uint8_t* dst, uint32_t cap, uint32_t* out_len);
+extern "C" int gz_decompress(const uint8_t* src, uint32_t len, uint8_t* dst, uint32_t cap, uint32_t* out_len);
 extern "C" int lz_decompress(int codec, const uint8_t* src, uint32_t len, uint8_t* dst, uint32_t cap, uint32_t ring,
                              uint32_t* out_len);
 
@@ -326,6 +331,13 @@ int fuzz_zstd(uint64_t seed, int iters, int nfiles, char** files) {
                          });
 }
 
+int fuzz_gzip(uint64_t seed, int iters, int nfiles, char** files) {
+    return fuzz_payloads("gzip", seed, iters, nfiles, files, 1,
+                         [](const uint32_t*, const uint8_t* s, uint32_t n, uint8_t* d, uint32_t cap, uint32_t* ol) {
+                             return gz_decompress(s, n, d, cap, ol);
+                         });
+}
+
 // both of k_codec's history sizes: the 64 KiB ring and the small-page 8 KiB one
 int fuzz_lz(uint64_t seed, int iters, int nfiles, char** files) {
     return fuzz_payloads("lz", seed, iters, nfiles, files, 2,
@@ -337,7 +349,7 @@ int fuzz_lz(uint64_t seed, int iters, int nfiles, char** files) {
 
 int main(int argc, char** argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: %s walk|regex|threads|zstd|lz <seed> <iters> [file...]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s walk|regex|threads|zstd|lz|gzip <seed> <iters> [file...]\n", argv[0]);
         return 2;
     }
     const std::string mode = argv[1];
@@ -348,5 +360,6 @@ int main(int argc, char** argv) {
     if (mode == "threads") return fuzz_threads(seed, iters, argc - 4, argv + 4);
     if (mode == "zstd") return fuzz_zstd(seed, iters, argc - 4, argv + 4);
     if (mode == "lz") return fuzz_lz(seed, iters, argc - 4, argv + 4);
+    if (mode == "gzip") return fuzz_gzip(seed, iters, argc - 4, argv + 4);
     return 2;
 }
